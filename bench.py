@@ -1,0 +1,243 @@
+#!/usr/bin/env python3
+"""bench.py — scans/sec of the FAST-LIO scan-matching hot path on MI355X.
+
+Metric (BASELINE.json): "scans/sec (100k-pt scan vs N-pt map) + ms/IESKF-iteration, 1 GPU".
+One step = one complete iterated-ESKF update (lio_ieskf_update: up to
+max_iteration+1 = 4 h_share_model evaluations, kNN on the iterations where
+ekfom_data.converge is true, host 23-dim algebra) of one synthetic scan whose
+points are already resident in HBM (a ring of pre-uploaded scans).
+
+Default workload = BASELINE.json configs[1] ("C2"): 65,536-pt Ouster-64 scan vs
+a 1M-pt static map, max_iteration = 3.  Multi-GPU: the front end does not shard
+(replicas only) — each rank runs its own replica on its own scans
+(weak scaling); the loop-closure ICP (C4: 500k vs 500k) is sharded across the
+ranks with the record all-gather (lio_gpu.dist) and reported in "loop_icp".
+
+    python bench.py --gpus N --steps K --warmup W
+    torchrun --nproc-per-node N bench.py --gpus N ...
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "fast-lio-sam_gps_amd"))
+
+HBM_PEAK_GBS = 8000.0        # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+BYTES_PER_PT_KNN = 112       # h-evaluation with kNN
+BYTES_PER_PT_REUSE = 32      # h-evaluation reusing kNN
+BYTES_PER_PT_ICP = 24        # per ICP iteration and source point
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="C2", choices=["C1", "C2", "C3", "C5"])
+    ap.add_argument("--scans", type=int, default=8, help="distinct resident scans cycled through")
+    ap.add_argument("--cell", type=float, default=1.0)
+    ap.add_argument("--no-icp", action="store_true")
+    ap.add_argument("--icp-reps", type=int, default=5)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"),
+                    help="per-launch HBM traffic measured with rocprofv3 --pmc (profiles/)")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import numpy as np
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+
+    from lio_gpu import frontend as F
+    from lio_gpu import loop_closure as LC
+    from lio_gpu import synth
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    # ---------------------------------------------------------------- inputs
+    t0 = time.time()
+    mp, L, sp, kind = synth.CONFIGS[args.config]
+    scene = synth.make_scene(L, 1234)
+    mappts = synth.sample_surface(scene, mp, 1234)
+    scans = []
+    for k in range(args.scans):
+        x = -0.15 * L + (k + rank * args.scans) * 3.7
+        scans.append(synth.make_scan(scene, sp, kind, pos_gt=[x, 0.6 * np.sin(0.7 * k), 0.0],
+                                     yaw_gt=0.05 * np.sin(0.3 * k), seed=99 + k + 1000 * rank))
+    gen_s = time.time() - t0
+    d_map = torch.from_numpy(mappts).to(dev)
+    d_scans = [torch.from_numpy(s.body).to(dev) for s in scans]
+    torch.cuda.synchronize()
+    tree = F.IkdTreeGPU(cell_size=args.cell, device=local)
+    tb = time.time()
+    tree.Build_device(d_map.data_ptr(), len(mappts))
+    build_ms = (time.time() - tb) * 1e3
+    hm = F.HShareModelGPU(tree)
+    kf = F.EsekfGPU(hm, laser_point_cov=0.001, max_iteration=3, epsi=0.001)
+    P0 = synth.initial_cov()
+    states = [synth.initial_state(s.pos_init, s.rot_init) for s in scans]
+
+    def step(k):
+        j = k % len(scans)
+        hm.set_scan_device(d_scans[j].data_ptr(), len(scans[j].body))
+        return kf.update_iterated_dyn_share_modified(states[j], P0)
+
+    for k in range(args.warmup):
+        step(k)
+    barrier()
+    hm.reset_timing()
+    hm.set_timing(True)
+    h_evals = knn_calls = 0
+    pos_err = []
+    barrier()
+    t_start = time.perf_counter()
+    for k in range(args.steps):
+        x, P, st = step(k)
+        h_evals += st["h_evals"]
+        knn_calls += st["knn_calls"]
+        if k < len(scans):
+            pos_err.append(float(np.linalg.norm(x["pos"] - scans[k % len(scans)].pos_gt)))
+    barrier()
+    elapsed = time.perf_counter() - t_start
+    hm.set_timing(False)
+    tm = hm.timing()
+    if dist is not None:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    total_scans = args.steps * world
+    value = total_scans / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    ms_per_iter = elapsed / max(h_evals, 1) * 1e3
+
+    n_pts = sp
+    knn_avg_ms = tm["knn_ms"] / max(tm["knn_launches"], 1)
+    reuse_avg_ms = tm["reuse_ms"] / max(tm["reuse_launches"], 1)
+    achieved = BYTES_PER_PT_KNN * n_pts / (knn_avg_ms * 1e-3) / 1e9 if tm["knn_launches"] else None
+    traffic = None
+    if os.path.exists(args.pmc):
+        try:
+            pmc = json.load(open(args.pmc))
+            if pmc.get("config") == args.config:
+                traffic = pmc.get("knn_hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    roofline = {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
+                "traffic": traffic, "kernel": "h_model_kernel<REDO_KNN=true>",
+                "bytes_per_launch": BYTES_PER_PT_KNN * n_pts, "avg_launch_ms": round(knn_avg_ms, 5),
+                "reuse_kernel_avg_ms": round(reuse_avg_ms, 5),
+                "reuse_achieved_gbs": round(BYTES_PER_PT_REUSE * n_pts / (reuse_avg_ms * 1e-3) / 1e9, 2)
+                if tm["reuse_launches"] else None}
+
+    # ------------------------------------------------------------- loop ICP (sharded)
+    loop_icp = None
+    if not args.no_icp:
+        src, dst, Tgt = synth.make_icp_pair(n_points=500_000, seed=4321)
+        lc = LC.LoopClosure(LC.LoopClosureConfig(), device=local)
+        cb = None
+        if world > 1:
+            from lio_gpu import dist as ldist
+
+            cb = ldist.make_allgather(device=dev)
+            lc.set_shard(rank, world, cb)
+        lc.setInputSource(src)
+        lc.setInputTarget(dst)
+        lc.align(keep_aligned=False)
+        lc.set_timing(True)
+        barrier()
+        ti = time.perf_counter()
+        iters = 0
+        for _ in range(args.icp_reps):
+            r = lc.align(keep_aligned=False)
+            iters += r.iterations
+        barrier()
+        icp_s = time.perf_counter() - ti
+        if dist is not None:
+            t = torch.tensor([icp_s], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            icp_s = float(t.item())
+        itm = lc.timing()
+        passes = itm["icp_launches"]
+        shard_n = len(src) // world
+        icp_kernel_ms = itm["icp_ms"] / max(passes, 1)
+        loop_icp = {"config": "C4: 500k vs 500k, voxel 0.3 m, PCL ICP semantics", "n_gpus": world,
+                    "ms_per_alignment": round(icp_s / args.icp_reps * 1e3, 3),
+                    "iterations": r.iterations, "ms_per_iteration": round(icp_s / max(iters, 1) * 1e3, 3),
+                    "score": r.score, "converged": bool(r.is_converged), "scaling": "strong",
+                    "kernel_ms_per_pass": round(icp_kernel_ms, 4),
+                    "kernel_gbs": round(BYTES_PER_PT_ICP * shard_n / (icp_kernel_ms * 1e-3) / 1e9, 2)
+                    if passes else None}
+
+    # ------------------------------------------------------------- CPU baseline
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import oracle_py as O
+
+        threads = min(os.cpu_count() or 1, 16)
+        om = O.OracleMap(mappts)
+        done = 0
+        cpu_iters = 0
+        tc = time.perf_counter()
+        while True:
+            s = scans[done % len(scans)]
+            _, _, so, _ = O.ieskf_update(om, s.body, states[done % len(scans)], P0, threads=threads)
+            done += 1
+            cpu_iters += int(so[0])
+            if time.perf_counter() - tc > args.cpu_seconds and done >= 3:
+                break
+        cpu_s = time.perf_counter() - tc
+        cpu = {"value": round(done / cpu_s, 3), "unit": "scans/s", "cores": threads, "kind": "port",
+               "sample": f"{done} full IESKF updates of {args.config} scans ({sp} pts vs {mp} pts map), "
+                         f"oracle/lio_oracle.cpp kd-tree + OpenMP, {cpu_s:.1f} s",
+               "ms_per_iteration": round(cpu_s / max(cpu_iters, 1) * 1e3, 3)}
+
+    if rank == 0:
+        line = {
+            "metric": "scans/sec (100k-pt scan vs N-pt map) + ms/IESKF-iteration, 1 GPU",
+            "value": round(value, 3), "unit": "scans/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32/f64",
+            "data": "synthetic (seeded urban-canyon scene, ray-cast scans; no datasets offline)",
+            "config": {"workload": f"{args.config}: {sp}-pt {kind} scan vs {mp}-pt static map, "
+                                   "max_iteration=3 (<=4 h-evals/scan)",
+                       "scan_points": sp, "map_points": mp, "resident_scans": len(scans),
+                       "parallelism": f"replicas x{world} (front end does not shard)"},
+            "ms_per_ieskf_iteration": round(ms_per_iter, 4),
+            "h_evals_per_scan": round(h_evals / args.steps, 3), "knn_evals_per_scan": round(knn_calls / args.steps, 3),
+            "pos_err_m": round(float(np.mean(pos_err)), 5) if pos_err else None,
+            "map_build_ms": round(build_ms, 2), "input_gen_s": round(gen_s, 1),
+            "roofline": roofline, "cpu_baseline": cpu, "loop_icp": loop_icp,
+        }
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

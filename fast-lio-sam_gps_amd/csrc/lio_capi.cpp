@@ -1,0 +1,518 @@
+// lio_capi.cpp — the C-ABI (include/lio_gpu.h): handles, streams, device
+// buffers, and the host drivers (IESKF update, PCL-semantics ICP loop).
+// There is deliberately no CPU compute path: every compute entry point runs
+// the gfx950 kernels or fails with LIO_ERR_NODEV / LIO_ERR_HIP.
+#include "../../include/lio_gpu.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "ieskf.hpp"
+#include "lio_error.hpp"
+#include "lio_kernels.hpp"
+
+namespace {
+
+int fail(int code, const std::string& msg) {
+    lio::last_error() = msg;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                           \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess) return fail(LIO_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+int check_device(int dev) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return fail(LIO_ERR_NODEV, "no HIP device visible (this library has no CPU path)");
+    if (dev < 0 || dev >= n) return fail(LIO_ERR_ARG, "device ordinal out of range");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return fail(LIO_ERR_HIP, "hipGetDeviceProperties failed");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(LIO_ERR_NODEV, std::string("built for gfx950, device is ") + prop.gcnArchName);
+    return LIO_OK;
+}
+
+template <class T>
+int grow(T** p, int64_t& cap, int64_t need, size_t elems_per = 1) {
+    if (need <= cap && *p) return LIO_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    int64_t c = std::max<int64_t>(need, cap + cap / 2);
+    if (hipMalloc(p, (size_t)c * elems_per * sizeof(T)) != hipSuccess) {
+        cap = 0;
+        return fail(LIO_ERR_NOMEM, "hipMalloc failed");
+    }
+    cap = c;
+    return LIO_OK;
+}
+
+struct EventPair {
+    hipEvent_t a = nullptr, b = nullptr;
+};
+
+}  // namespace
+
+// =============================================================================
+// map
+// =============================================================================
+struct lio_map {
+    int dev = 0;
+    hipStream_t st = nullptr;
+    lio_map_params p{};
+    lio::GridBuf grid;
+    float* d_xyz = nullptr;
+    int64_t xyz_cap = 0;
+    int64_t n = 0;
+};
+
+struct lio_ctx {
+    lio_map* map = nullptr;
+    lio_match_params p{};
+    int64_t n = 0, cap = 0;
+    float* d_body = nullptr;
+    int32_t* d_nn = nullptr;
+    float4* d_planes = nullptr;
+    uint8_t* d_sel = nullptr;
+    double* d_partials = nullptr;
+    int64_t part_cap = 0;
+    double* d_sums = nullptr;
+    double* h_sums = nullptr;  // pinned
+    double* d_rows = nullptr;
+    int64_t rows_cap = 0;
+    int64_t* d_nrows = nullptr;
+    lio_pose last_pose{};
+    bool have_eval = false;
+    bool knn_valid = false;
+    // timing
+    bool timing = false;
+    lio_kernel_timing tm{};
+    EventPair ev_main, ev_fin;
+};
+
+extern "C" {
+
+int lio_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+const char* lio_last_error(void) { return lio::last_error().c_str(); }
+
+const char* lio_build_info(void) {
+    return "lio_gpu: gfx950 HIP kernels (grid kNN + esti_plane + H^T H reduction, ICP); -ffp-contract=off";
+}
+
+int lio_map_create(const lio_map_params* p, lio_map** out) {
+    if (!out) return fail(LIO_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    lio_map_params pp{};
+    if (p) pp = *p;
+    if (!(pp.cell_size > 0.f)) pp.cell_size = 1.0f;
+    if (!(pp.downsample_size > 0.f)) pp.downsample_size = 0.5f;
+    int rc = check_device(pp.device);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(pp.device));
+    auto* m = new lio_map();
+    m->dev = pp.device;
+    m->p = pp;
+    if (hipStreamCreateWithFlags(&m->st, hipStreamNonBlocking) != hipSuccess) {
+        delete m;
+        return fail(LIO_ERR_HIP, "hipStreamCreate failed");
+    }
+    *out = m;
+    return LIO_OK;
+}
+
+int lio_map_destroy(lio_map* m) {
+    if (!m) return LIO_OK;
+    (void)hipSetDevice(m->dev);
+    (void)hipStreamSynchronize(m->st);
+    lio::grid_free(m->grid);
+    if (m->d_xyz) (void)hipFree(m->d_xyz);
+    (void)hipStreamDestroy(m->st);
+    delete m;
+    return LIO_OK;
+}
+
+static int map_build_impl(lio_map* m, const float* d_xyz, int64_t n) {
+    int rc = lio::grid_build(m->grid, d_xyz, n, m->p.cell_size, m->st);
+    if (rc == -5) return fail(LIO_ERR_NOMEM, "grid build: out of device memory");
+    if (rc == -1) return fail(LIO_ERR_ARG, "grid build: invalid points (empty, too many, or non-finite)");
+    if (rc != 0) return fail(LIO_ERR_HIP, "grid build failed");
+    HIP_TRY(hipStreamSynchronize(m->st));
+    m->n = n;
+    return LIO_OK;
+}
+
+int lio_map_build(lio_map* m, const float* xyz, int64_t n) {
+    if (!m || (!xyz && n > 0) || n <= 0) return fail(LIO_ERR_ARG, "lio_map_build: bad arguments");
+    HIP_TRY(hipSetDevice(m->dev));
+    int rc = grow(&m->d_xyz, m->xyz_cap, n, 3);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(m->d_xyz, xyz, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice, m->st));
+    return map_build_impl(m, m->d_xyz, n);
+}
+
+int lio_map_build_device(lio_map* m, const float* d_xyz, int64_t n) {
+    if (!m || !d_xyz || n <= 0) return fail(LIO_ERR_ARG, "lio_map_build_device: bad arguments");
+    HIP_TRY(hipSetDevice(m->dev));
+    return map_build_impl(m, d_xyz, n);
+}
+
+int64_t lio_map_size(const lio_map* m) { return m ? m->n : 0; }
+
+int lio_map_get_points(lio_map* m, float* xyz_out) {
+    if (!m || !xyz_out) return fail(LIO_ERR_ARG, "bad arguments");
+    if (m->n == 0) return LIO_OK;
+    HIP_TRY(hipSetDevice(m->dev));
+    std::vector<float4> tmp(m->n);
+    HIP_TRY(hipMemcpyAsync(tmp.data(), m->grid.by_id, m->n * sizeof(float4), hipMemcpyDeviceToHost, m->st));
+    HIP_TRY(hipStreamSynchronize(m->st));
+    for (int64_t i = 0; i < m->n; ++i) {
+        xyz_out[3 * i] = tmp[i].x;
+        xyz_out[3 * i + 1] = tmp[i].y;
+        xyz_out[3 * i + 2] = tmp[i].z;
+    }
+    return LIO_OK;
+}
+
+int lio_map_get_grid(lio_map* m, double* out7) {
+    if (!m || !out7) return fail(LIO_ERR_ARG, "bad arguments");
+    const lio::GridGeom& g = m->grid.geom;
+    out7[0] = g.ox;
+    out7[1] = g.oy;
+    out7[2] = g.oz;
+    out7[3] = g.cell;
+    out7[4] = g.nx;
+    out7[5] = g.ny;
+    out7[6] = g.nz;
+    return LIO_OK;
+}
+
+// =============================================================================
+// h_share_model context
+// =============================================================================
+int lio_ctx_create(lio_map* m, const lio_match_params* p, lio_ctx** out) {
+    if (!m || !out) return fail(LIO_ERR_ARG, "bad arguments");
+    HIP_TRY(hipSetDevice(m->dev));
+    auto* c = new lio_ctx();
+    c->map = m;
+    if (p)
+        c->p = *p;
+    else
+        c->p = lio_match_params{5.0f, 0.1f, 0.9, 0.9};
+    if (hipMalloc(&c->d_sums, 32 * sizeof(double)) != hipSuccess ||
+        hipHostMalloc(&c->h_sums, 32 * sizeof(double)) != hipSuccess ||
+        hipMalloc(&c->d_nrows, sizeof(int64_t)) != hipSuccess) {
+        delete c;
+        return fail(LIO_ERR_NOMEM, "context allocation failed");
+    }
+    for (EventPair* e : {&c->ev_main, &c->ev_fin}) {
+        (void)hipEventCreate(&e->a);
+        (void)hipEventCreate(&e->b);
+    }
+    *out = c;
+    return LIO_OK;
+}
+
+int lio_ctx_destroy(lio_ctx* c) {
+    if (!c) return LIO_OK;
+    (void)hipSetDevice(c->map->dev);
+    (void)hipStreamSynchronize(c->map->st);
+    void* ptrs[] = {c->d_body, c->d_nn, c->d_planes, c->d_sel, c->d_partials, c->d_sums, c->d_rows, c->d_nrows};
+    for (void* q : ptrs)
+        if (q) (void)hipFree(q);
+    if (c->h_sums) (void)hipHostFree(c->h_sums);
+    for (EventPair* e : {&c->ev_main, &c->ev_fin}) {
+        if (e->a) (void)hipEventDestroy(e->a);
+        if (e->b) (void)hipEventDestroy(e->b);
+    }
+    delete c;
+    return LIO_OK;
+}
+
+static int ctx_reserve(lio_ctx* c, int64_t n) {
+    if (n > c->cap || !c->d_body) {
+        int64_t cap = std::max<int64_t>(n, c->cap + c->cap / 2);
+        void* ptrs[] = {c->d_body, c->d_nn, c->d_planes, c->d_sel};
+        for (void* q : ptrs)
+            if (q) (void)hipFree(q);
+        c->d_body = nullptr;
+        c->d_nn = nullptr;
+        c->d_planes = nullptr;
+        c->d_sel = nullptr;
+        if (hipMalloc(&c->d_body, cap * 3 * sizeof(float)) != hipSuccess ||
+            hipMalloc(&c->d_nn, cap * 5 * sizeof(int32_t)) != hipSuccess ||
+            hipMalloc(&c->d_planes, cap * sizeof(float4)) != hipSuccess ||
+            hipMalloc(&c->d_sel, cap + 64) != hipSuccess)
+            return fail(LIO_ERR_NOMEM, "scan buffers: hipMalloc failed");
+        c->cap = cap;
+    }
+    int rc = grow(&c->d_partials, c->part_cap, (int64_t)lio::match_blocks((int)n) * 32 + 32);
+    if (rc) return rc;
+    c->n = n;
+    c->have_eval = false;
+    c->knn_valid = false;
+    return LIO_OK;
+}
+
+int lio_scan_set(lio_ctx* c, const float* body, int64_t n) {
+    if (!c || n < 0 || (n > 0 && !body) || n >= (int64_t)1 << 30) return fail(LIO_ERR_ARG, "lio_scan_set: bad arguments");
+    HIP_TRY(hipSetDevice(c->map->dev));
+    int rc = ctx_reserve(c, n);
+    if (rc) return rc;
+    if (n) HIP_TRY(hipMemcpyAsync(c->d_body, body, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice, c->map->st));
+    HIP_TRY(hipMemsetAsync(c->d_sel, 0, (size_t)std::max<int64_t>(n, 1), c->map->st));
+    return LIO_OK;
+}
+
+int lio_scan_set_device(lio_ctx* c, const float* d_body, int64_t n) {
+    if (!c || n < 0 || (n > 0 && !d_body) || n >= (int64_t)1 << 30) return fail(LIO_ERR_ARG, "lio_scan_set_device: bad arguments");
+    HIP_TRY(hipSetDevice(c->map->dev));
+    int rc = ctx_reserve(c, n);
+    if (rc) return rc;
+    if (n)
+        HIP_TRY(hipMemcpyAsync(c->d_body, d_body, (size_t)n * 3 * sizeof(float), hipMemcpyDeviceToDevice, c->map->st));
+    HIP_TRY(hipMemsetAsync(c->d_sel, 0, (size_t)std::max<int64_t>(n, 1), c->map->st));
+    return LIO_OK;
+}
+
+static lio::MatchArgs make_args(lio_ctx* c, const lio_pose& pose) {
+    lio::MatchArgs a{};
+    std::memcpy(&a.pose, &pose, sizeof(lio::PoseArg));
+    a.grid = lio::grid_view(c->map->grid);
+    a.body = c->d_body;
+    a.map_by_id = c->map->grid.by_id;
+    a.nn_idx = c->d_nn;
+    a.planes = c->d_planes;
+    a.sel = c->d_sel;
+    a.partials = c->d_partials;
+    a.n = (int)c->n;
+    // every point with d2 <= range lies within ceil(sqrt(range)/cell)+1 shells
+    a.max_shell = (int)std::ceil(std::sqrt((double)c->p.knn_range_sq) / a.grid.cell) + 1;
+    a.range_sq = c->p.knn_range_sq;
+    a.plane_thr = c->p.plane_thr;
+    a.s_coef = c->p.s_coef;
+    a.s_gate = c->p.s_gate;
+    return a;
+}
+
+static void accum_event(EventPair& e, int64_t& launches, double& ms) {
+    float t = 0.f;
+    if (hipEventElapsedTime(&t, e.a, e.b) == hipSuccess) {
+        ms += t;
+        ++launches;
+    }
+}
+
+int lio_match(lio_ctx* c, const lio_pose* pose, int redo_knn, double* sums) {
+    if (!c || !pose || !sums) return fail(LIO_ERR_ARG, "lio_match: bad arguments");
+    if (c->map->n == 0) return fail(LIO_ERR_STATE, "lio_match: map is empty (call lio_map_build)");
+    if (!redo_knn && !c->knn_valid) return fail(LIO_ERR_STATE, "lio_match: redo_knn=0 before any kNN evaluation");
+    HIP_TRY(hipSetDevice(c->map->dev));
+    hipStream_t st = c->map->st;
+    lio::MatchArgs a = make_args(c, *pose);
+    if (c->n == 0) {
+        std::memset(sums, 0, LIO_SUMS_LEN * sizeof(double));
+        c->last_pose = *pose;
+        c->have_eval = true;
+        c->knn_valid = true;
+        return LIO_OK;
+    }
+    if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.a, st));
+    const int nb = lio::launch_h_model(a, redo_knn != 0, st);
+    if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.b, st));
+    lio::launch_finalize(c->d_partials, nb, c->d_sums, st);
+    if (c->timing) HIP_TRY(hipEventRecord(c->ev_fin.b, st));
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(c->h_sums, c->d_sums, 32 * sizeof(double), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    std::memcpy(sums, c->h_sums, LIO_SUMS_LEN * sizeof(double));
+    if (c->timing) {
+        if (redo_knn)
+            accum_event(c->ev_main, c->tm.knn_launches, c->tm.knn_ms);
+        else
+            accum_event(c->ev_main, c->tm.reuse_launches, c->tm.reuse_ms);
+        EventPair f{c->ev_main.b, c->ev_fin.b};
+        accum_event(f, c->tm.final_launches, c->tm.final_ms);
+    }
+    c->last_pose = *pose;
+    c->have_eval = true;
+    if (redo_knn) c->knn_valid = true;
+    return LIO_OK;
+}
+
+int lio_get_knn(lio_ctx* c, int32_t* idx, float* d2) {
+    if (!c || !c->have_eval) return fail(LIO_ERR_STATE, "lio_get_knn: no evaluation yet");
+    HIP_TRY(hipSetDevice(c->map->dev));
+    hipStream_t st = c->map->st;
+    if (c->n == 0) return LIO_OK;
+    if (idx) HIP_TRY(hipMemcpyAsync(idx, c->d_nn, c->n * 5 * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    if (d2) {
+        float* tmp = nullptr;
+        HIP_TRY(hipMalloc(&tmp, c->n * 5 * sizeof(float)));
+        lio::launch_debug(make_args(c, c->last_pose), nullptr, tmp, nullptr, st);
+        hipError_t e = hipMemcpyAsync(d2, tmp, c->n * 5 * sizeof(float), hipMemcpyDeviceToHost, st);
+        (void)hipStreamSynchronize(st);
+        (void)hipFree(tmp);
+        if (e != hipSuccess) return fail(LIO_ERR_HIP, "lio_get_knn copy failed");
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    return LIO_OK;
+}
+
+int lio_get_planes(lio_ctx* c, float* abcd_pd2, uint8_t* sel) {
+    if (!c || !c->have_eval) return fail(LIO_ERR_STATE, "lio_get_planes: no evaluation yet");
+    HIP_TRY(hipSetDevice(c->map->dev));
+    hipStream_t st = c->map->st;
+    if (c->n == 0) return LIO_OK;
+    if (sel) HIP_TRY(hipMemcpyAsync(sel, c->d_sel, c->n, hipMemcpyDeviceToHost, st));
+    if (abcd_pd2) {
+        float* tmp = nullptr;
+        HIP_TRY(hipMalloc(&tmp, c->n * 4 * sizeof(float)));
+        lio::launch_debug(make_args(c, c->last_pose), nullptr, nullptr, tmp, st);
+        hipError_t e = hipMemcpyAsync(abcd_pd2, tmp, c->n * 4 * sizeof(float), hipMemcpyDeviceToHost, st);
+        (void)hipStreamSynchronize(st);
+        (void)hipFree(tmp);
+        if (e != hipSuccess) return fail(LIO_ERR_HIP, "lio_get_planes copy failed");
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    return LIO_OK;
+}
+
+int lio_get_world(lio_ctx* c, float* world) {
+    if (!c || !world || !c->have_eval) return fail(LIO_ERR_STATE, "lio_get_world: no evaluation yet");
+    HIP_TRY(hipSetDevice(c->map->dev));
+    hipStream_t st = c->map->st;
+    if (c->n == 0) return LIO_OK;
+    float* tmp = nullptr;
+    HIP_TRY(hipMalloc(&tmp, c->n * 3 * sizeof(float)));
+    lio::launch_debug(make_args(c, c->last_pose), tmp, nullptr, nullptr, st);
+    hipError_t e = hipMemcpyAsync(world, tmp, c->n * 3 * sizeof(float), hipMemcpyDeviceToHost, st);
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(tmp);
+    if (e != hipSuccess) return fail(LIO_ERR_HIP, "lio_get_world copy failed");
+    return LIO_OK;
+}
+
+int lio_get_h_rows(lio_ctx* c, double* rows, int64_t max_rows, int64_t* n_rows) {
+    if (!c || !n_rows || (max_rows > 0 && !rows)) return fail(LIO_ERR_ARG, "lio_get_h_rows: bad arguments");
+    if (!c->have_eval) return fail(LIO_ERR_STATE, "lio_get_h_rows: no evaluation yet");
+    HIP_TRY(hipSetDevice(c->map->dev));
+    hipStream_t st = c->map->st;
+    int rc = grow(&c->d_rows, c->rows_cap, std::max<int64_t>(max_rows, 1) * 7);
+    if (rc) return rc;
+    lio::launch_h_rows(make_args(c, c->last_pose), c->d_rows, max_rows, c->d_nrows, st);
+    int64_t nr = 0;
+    HIP_TRY(hipMemcpyAsync(&nr, c->d_nrows, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const int64_t ncopy = std::min(nr, max_rows);
+    if (ncopy > 0) {
+        HIP_TRY(hipMemcpyAsync(rows, c->d_rows, ncopy * 7 * sizeof(double), hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    *n_rows = nr;
+    return LIO_OK;
+}
+
+// =============================================================================
+// IESKF
+// =============================================================================
+static lio::host::State to_host(const lio_state& s) {
+    lio::host::State x;
+    std::memcpy(x.pos, s.pos, sizeof(x.pos));
+    x.rot = {s.rot[0], s.rot[1], s.rot[2], s.rot[3]};
+    x.offR = {s.offset_R_L_I[0], s.offset_R_L_I[1], s.offset_R_L_I[2], s.offset_R_L_I[3]};
+    std::memcpy(x.offT, s.offset_T_L_I, sizeof(x.offT));
+    std::memcpy(x.vel, s.vel, sizeof(x.vel));
+    std::memcpy(x.bg, s.bg, sizeof(x.bg));
+    std::memcpy(x.ba, s.ba, sizeof(x.ba));
+    std::memcpy(x.grav, s.grav, sizeof(x.grav));
+    return x;
+}
+static void from_host(const lio::host::State& x, lio_state& s) {
+    std::memcpy(s.pos, x.pos, sizeof(x.pos));
+    s.rot[0] = x.rot.w; s.rot[1] = x.rot.x; s.rot[2] = x.rot.y; s.rot[3] = x.rot.z;
+    s.offset_R_L_I[0] = x.offR.w; s.offset_R_L_I[1] = x.offR.x; s.offset_R_L_I[2] = x.offR.y; s.offset_R_L_I[3] = x.offR.z;
+    std::memcpy(s.offset_T_L_I, x.offT, sizeof(x.offT));
+    std::memcpy(s.vel, x.vel, sizeof(x.vel));
+    std::memcpy(s.bg, x.bg, sizeof(x.bg));
+    std::memcpy(s.ba, x.ba, sizeof(x.ba));
+    std::memcpy(s.grav, x.grav, sizeof(x.grav));
+}
+
+int lio_ieskf_update(lio_ctx* c, lio_state* xs, double* P, const lio_ieskf_params* p, lio_ieskf_stats* st) {
+    if (!c || !xs || !P) return fail(LIO_ERR_ARG, "lio_ieskf_update: bad arguments");
+    lio_ieskf_params pp = p ? *p : lio_ieskf_params{0.001, 3, 0.001};
+    lio::host::State x = to_host(*xs);
+    lio::host::Mat Pm(P, P + LIO_STATE_DIM * LIO_STATE_DIM);
+    int err = LIO_OK;
+    auto hfn = [&](const lio::host::State& s, bool redo, bool want_rows, lio::host::HModel& hm) -> int {
+        if (want_rows) {
+            const int64_t want = (int64_t)hm.sums[LIO_SUMS_NEFF];
+            hm.rows.assign((size_t)std::max<int64_t>(want, 1) * 7, 0.0);
+            int64_t nr = 0;
+            int rc = lio_get_h_rows(c, hm.rows.data(), want, &nr);
+            if (rc) return err = rc;
+            hm.rows.resize((size_t)std::min(nr, want) * 7);
+            return 0;
+        }
+        lio_pose pose;
+        lio::host::quat_to_mat(s.rot, pose.R);
+        lio::host::quat_to_mat(s.offR, pose.R_LI);
+        std::memcpy(pose.t, s.pos, sizeof(pose.t));
+        std::memcpy(pose.t_LI, s.offT, sizeof(pose.t_LI));
+        hm.rows.clear();
+        int rc = lio_match(c, &pose, redo ? 1 : 0, hm.sums);
+        if (rc) return err = rc;
+        return 0;
+    };
+    lio::host::IeskfResult r;
+    int rc = lio::host::update_iterated(x, Pm, pp.laser_point_cov, pp.max_iteration, pp.epsi, hfn, r);
+    if (rc) return err ? err : fail(LIO_ERR_STATE, "IESKF: singular matrix");
+    from_host(x, *xs);
+    std::memcpy(P, Pm.data(), sizeof(double) * LIO_STATE_DIM * LIO_STATE_DIM);
+    if (st) {
+        st->h_evals = r.h_evals;
+        st->knn_calls = r.knn_calls;
+        st->converged = r.converged;
+        st->n_eff = r.n_eff;
+        st->res_mean = r.res_mean;
+        st->solve_ms = r.solve_ms;
+    }
+    return LIO_OK;
+}
+
+// =============================================================================
+// timing
+// =============================================================================
+int lio_ctx_set_timing(lio_ctx* c, int enable) {
+    if (!c) return fail(LIO_ERR_ARG, "NULL ctx");
+    c->timing = enable != 0;
+    return LIO_OK;
+}
+int lio_ctx_get_timing(lio_ctx* c, lio_kernel_timing* out) {
+    if (!c || !out) return fail(LIO_ERR_ARG, "bad arguments");
+    *out = c->tm;
+    return LIO_OK;
+}
+int lio_ctx_reset_timing(lio_ctx* c) {
+    if (!c) return fail(LIO_ERR_ARG, "NULL ctx");
+    c->tm = lio_kernel_timing{};
+    return LIO_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,493 @@
+// lio_icp_host.cpp — LoopClosure::icpAlignment replacement (C-ABI lio_icp_*).
+//
+// Host loop = pcl::IterativeClosestPoint::computeTransformation as configured at
+// /root/reference/fast_lio_sam/src/loop_closure.cpp:3-14 (PCL 1.10 semantics [U]):
+//   repeat { correspondences (1-NN, d2 <= max_corr_dist^2) on the incrementally
+//            transformed source; < 3 => not converged, stop;
+//            T_inc = Umeyama(src_corr, tgt_corr) (TransformationEstimationSVD);
+//            transform source by T_inc; final = T_inc * final; ++iter;
+//            DefaultConvergenceCriteria }
+//   score = getFitnessScore() (unbounded 1-NN of src*final), is_valid =
+//   converged && score < icp_score_threshold (loop_closure.cpp:85-90).
+// Per iteration the GPU returns Umeyama sufficient statistics per 4096-point
+// record; ranks all-gather the records and every rank sums them in record
+// order, so the result is bit-identical for any number of ranks.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <cstring>
+#include <limits>
+#include <string>
+#include <vector>
+
+#include "../../include/lio_gpu.h"
+#include "lio_error.hpp"
+#include "lio_kernels.hpp"
+
+namespace {
+int ifail(int code, const std::string& m) {
+    lio::last_error() = m;
+    return code;
+}
+#define IHIP(expr)                                                                                  \
+    do {                                                                                            \
+        hipError_t e_ = (expr);                                                                     \
+        if (e_ != hipSuccess) return ifail(LIO_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+// ---- 3x3 SVD by one-sided Jacobi (Hestenes) on the columns of A: A = U S V^T
+void svd3(const double A[9], double U[9], double S[3], double V[9]) {
+    double W[9];
+    std::memcpy(W, A, sizeof(W));
+    for (int i = 0; i < 9; ++i) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
+    for (int sweep = 0; sweep < 60; ++sweep) {
+        double off = 0.0;
+        for (int p = 0; p < 2; ++p)
+            for (int q = p + 1; q < 3; ++q) {
+                double al = 0, be = 0, ga = 0;
+                for (int r = 0; r < 3; ++r) {
+                    al += W[3 * r + p] * W[3 * r + p];
+                    be += W[3 * r + q] * W[3 * r + q];
+                    ga += W[3 * r + p] * W[3 * r + q];
+                }
+                if (ga == 0.0) continue;
+                off = std::max(off, std::fabs(ga) / std::sqrt(al * be + 1e-300));
+                const double zeta = (be - al) / (2.0 * ga);
+                const double t = (zeta >= 0 ? 1.0 : -1.0) / (std::fabs(zeta) + std::sqrt(1.0 + zeta * zeta));
+                const double c = 1.0 / std::sqrt(1.0 + t * t), s = c * t;
+                for (int r = 0; r < 3; ++r) {
+                    const double wp = W[3 * r + p], wq = W[3 * r + q];
+                    W[3 * r + p] = c * wp - s * wq;
+                    W[3 * r + q] = s * wp + c * wq;
+                    const double vp = V[3 * r + p], vq = V[3 * r + q];
+                    V[3 * r + p] = c * vp - s * vq;
+                    V[3 * r + q] = s * vp + c * vq;
+                }
+            }
+        if (off < 1e-15) break;
+    }
+    double sv[3];
+    for (int c = 0; c < 3; ++c) sv[c] = std::sqrt(W[c] * W[c] + W[3 + c] * W[3 + c] + W[6 + c] * W[6 + c]);
+    int ord[3] = {0, 1, 2};
+    std::sort(ord, ord + 3, [&](int a, int b) { return sv[a] > sv[b]; });
+    double Vs[9], Us[9];
+    for (int k = 0; k < 3; ++k) {
+        const int c = ord[k];
+        S[k] = sv[c];
+        for (int r = 0; r < 3; ++r) {
+            Vs[3 * r + k] = V[3 * r + c];
+            Us[3 * r + k] = sv[c] > 0 ? W[3 * r + c] / sv[c] : 0.0;
+        }
+    }
+    // complete U to an orthonormal basis where sigma vanished
+    if (!(S[2] > 1e-300 * S[0])) {
+        Us[2] = Us[3] * Us[7] - Us[6] * Us[4];
+        Us[5] = Us[6] * Us[1] - Us[0] * Us[7];
+        Us[8] = Us[0] * Us[4] - Us[3] * Us[1];
+    }
+    std::memcpy(U, Us, sizeof(Us));
+    std::memcpy(V, Vs, sizeof(Vs));
+}
+double det3(const double* M) {
+    return M[0] * (M[4] * M[8] - M[5] * M[7]) - M[1] * (M[3] * M[8] - M[5] * M[6]) + M[2] * (M[3] * M[7] - M[4] * M[6]);
+}
+
+// Umeyama without scaling (Eigen::umeyama(src, dst, false)) from statistics:
+// st[0]=n, st[1..3]=sum p, st[4..6]=sum q, st[7..15]=sum q p^T, all about c0.
+void umeyama(const double* st, const double c0[3], float Ti[16]) {
+    const double inv_n = 1.0 / st[0];
+    double pm[3], qm[3], Sg[9];
+    for (int d = 0; d < 3; ++d) {
+        pm[d] = st[1 + d] * inv_n;
+        qm[d] = st[4 + d] * inv_n;
+    }
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) Sg[3 * r + c] = st[7 + 3 * r + c] * inv_n - qm[r] * pm[c];
+    double U[9], S[3], V[9];
+    svd3(Sg, U, S, V);
+    const double D = (det3(U) * det3(V) < 0) ? -1.0 : 1.0;
+    double R[9];
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) R[3 * r + c] = U[3 * r] * V[3 * c] + U[3 * r + 1] * V[3 * c + 1] + D * U[3 * r + 2] * V[3 * c + 2];
+    std::memset(Ti, 0, 16 * sizeof(float));
+    for (int r = 0; r < 3; ++r) {
+        const double t = (qm[r] + c0[r]) -
+                         (R[3 * r] * (pm[0] + c0[0]) + R[3 * r + 1] * (pm[1] + c0[1]) + R[3 * r + 2] * (pm[2] + c0[2]));
+        for (int c = 0; c < 3; ++c) Ti[4 * r + c] = (float)R[3 * r + c];
+        Ti[4 * r + 3] = (float)t;
+    }
+    Ti[15] = 1.f;
+}
+
+struct EvPair {
+    hipEvent_t a = nullptr, b = nullptr;
+};
+
+}  // namespace
+
+struct lio_icp {
+    int dev = 0;
+    hipStream_t st = nullptr;
+    lio_icp_params p{};
+    lio::GridBuf tgt;
+    float* d_tgt = nullptr;
+    int64_t nt = 0;
+    double c0[3] = {0, 0, 0};
+    std::vector<float> src;  // full source (host copy)
+    int64_t ns = 0;
+    int rank = 0, world = 1;
+    lio_allgather_fn fn = nullptr;
+    void* user = nullptr;
+    // shard buffers
+    int64_t sh_begin = 0, sh_n = 0, cap = 0;
+    float* d_src = nullptr;
+    float* d_cur = nullptr;
+    float* d_fd2 = nullptr;
+    int* d_fid = nullptr;
+    int* d_far = nullptr;
+    int* d_far_count = nullptr;
+    double* d_part = nullptr;
+    double* d_super = nullptr;
+    double* h_super = nullptr;  // pinned
+    int64_t super_cap = 0;
+    bool src_dirty = true;
+    bool timing = false;
+    lio_kernel_timing tm{};
+    EvPair ev;
+};
+
+static int icp_check_dev(int dev) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ifail(LIO_ERR_NODEV, "no HIP device (no CPU path)");
+    if (dev < 0 || dev >= n) return ifail(LIO_ERR_ARG, "device ordinal out of range");
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return ifail(LIO_ERR_HIP, "hipGetDeviceProperties");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return ifail(LIO_ERR_NODEV, "device is not gfx950");
+    return LIO_OK;
+}
+
+static void shard_range(int64_t ns, int rank, int world, int64_t& b, int64_t& n) {
+    const int64_t nsup = (ns + lio::kIcpSuper - 1) / lio::kIcpSuper;
+    const int64_t s0 = nsup * rank / world, s1 = nsup * (rank + 1) / world;
+    b = std::min<int64_t>(s0 * lio::kIcpSuper, ns);
+    n = std::min<int64_t>(s1 * lio::kIcpSuper, ns) - b;
+}
+
+extern "C" {
+
+int lio_icp_create(const lio_icp_params* p, lio_icp** out) {
+    if (!p || !out) return ifail(LIO_ERR_ARG, "bad arguments");
+    *out = nullptr;
+    int rc = icp_check_dev(p->device);
+    if (rc) return rc;
+    IHIP(hipSetDevice(p->device));
+    auto* h = new lio_icp();
+    h->dev = p->device;
+    h->p = *p;
+    if (!(h->p.cell_size > 0.f)) h->p.cell_size = 1.0f;
+    if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&h->d_far_count, 64) != hipSuccess) {
+        delete h;
+        return ifail(LIO_ERR_HIP, "icp stream/alloc failed");
+    }
+    (void)hipEventCreate(&h->ev.a);
+    (void)hipEventCreate(&h->ev.b);
+    *out = h;
+    return LIO_OK;
+}
+
+int lio_icp_destroy(lio_icp* h) {
+    if (!h) return LIO_OK;
+    (void)hipSetDevice(h->dev);
+    (void)hipStreamSynchronize(h->st);
+    lio::grid_free(h->tgt);
+    void* ptrs[] = {h->d_tgt, h->d_src, h->d_cur, h->d_fd2, h->d_fid, h->d_far, h->d_far_count, h->d_part, h->d_super};
+    for (void* q : ptrs)
+        if (q) (void)hipFree(q);
+    if (h->h_super) (void)hipHostFree(h->h_super);
+    if (h->ev.a) (void)hipEventDestroy(h->ev.a);
+    if (h->ev.b) (void)hipEventDestroy(h->ev.b);
+    (void)hipStreamDestroy(h->st);
+    delete h;
+    return LIO_OK;
+}
+
+int lio_icp_set_target(lio_icp* h, const float* xyz, int64_t n) {
+    if (!h || n <= 0 || !xyz) return ifail(LIO_ERR_ARG, "lio_icp_set_target: bad arguments");
+    IHIP(hipSetDevice(h->dev));
+    if (h->d_tgt) IHIP(hipFree(h->d_tgt));
+    h->d_tgt = nullptr;
+    IHIP(hipMalloc(&h->d_tgt, (size_t)n * 3 * sizeof(float)));
+    IHIP(hipMemcpyAsync(h->d_tgt, xyz, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice, h->st));
+    int rc = lio::grid_build(h->tgt, h->d_tgt, n, h->p.cell_size, h->st);
+    if (rc) return ifail(rc == -5 ? LIO_ERR_NOMEM : LIO_ERR_HIP, "target grid build failed");
+    IHIP(hipStreamSynchronize(h->st));
+    h->nt = n;
+    // fixed accumulation centre: target bounding-box centre (float)
+    const float* bb = h->tgt.aabb_host;
+    for (int d = 0; d < 3; ++d) h->c0[d] = (double)(0.5f * (bb[d] + bb[3 + d]));
+    return LIO_OK;
+}
+
+int lio_icp_set_source(lio_icp* h, const float* xyz, int64_t n) {
+    if (!h || n < 0 || (n > 0 && !xyz) || n >= (int64_t)1 << 30) return ifail(LIO_ERR_ARG, "lio_icp_set_source: bad arguments");
+    h->src.assign(xyz, xyz + 3 * n);
+    h->ns = n;
+    h->src_dirty = true;
+    return LIO_OK;
+}
+
+int lio_icp_set_shard(lio_icp* h, int rank, int world, lio_allgather_fn fn, void* user) {
+    if (!h || world < 1 || rank < 0 || rank >= world || (world > 1 && !fn))
+        return ifail(LIO_ERR_ARG, "lio_icp_set_shard: bad arguments");
+    h->rank = rank;
+    h->world = world;
+    h->fn = fn;
+    h->user = user;
+    h->src_dirty = true;
+    return LIO_OK;
+}
+
+static int icp_prepare(lio_icp* h) {
+    if (!h->src_dirty) return LIO_OK;
+    shard_range(h->ns, h->rank, h->world, h->sh_begin, h->sh_n);
+    const int64_t n = std::max<int64_t>(h->sh_n, 1);
+    if (n > h->cap) {
+        void* ptrs[] = {h->d_src, h->d_cur, h->d_fd2, h->d_fid, h->d_far, h->d_part};
+        for (void* q : ptrs)
+            if (q) IHIP(hipFree(q));
+        const int64_t nch = (n + lio::kIcpChunk - 1) / lio::kIcpChunk;
+        IHIP(hipMalloc(&h->d_src, n * 3 * sizeof(float)));
+        IHIP(hipMalloc(&h->d_cur, n * 3 * sizeof(float)));
+        IHIP(hipMalloc(&h->d_fd2, n * sizeof(float)));
+        IHIP(hipMalloc(&h->d_fid, n * sizeof(int)));
+        IHIP(hipMalloc(&h->d_far, n * sizeof(int)));
+        IHIP(hipMalloc(&h->d_part, nch * lio::kIcpStride * sizeof(double)));
+        h->cap = n;
+    }
+    const int64_t nsup_all = (h->ns + lio::kIcpSuper - 1) / lio::kIcpSuper + 1;
+    if (nsup_all > h->super_cap) {
+        if (h->d_super) IHIP(hipFree(h->d_super));
+        if (h->h_super) IHIP(hipHostFree(h->h_super));
+        IHIP(hipMalloc(&h->d_super, nsup_all * lio::kIcpStride * sizeof(double)));
+        IHIP(hipHostMalloc(&h->h_super, nsup_all * lio::kIcpStride * sizeof(double)));
+        h->super_cap = nsup_all;
+    }
+    if (h->sh_n > 0)
+        IHIP(hipMemcpyAsync(h->d_src, h->src.data() + 3 * h->sh_begin, h->sh_n * 3 * sizeof(float),
+                            hipMemcpyHostToDevice, h->st));
+    h->src_dirty = false;
+    return LIO_OK;
+}
+
+// One correspondence (or fitness) pass: GPU kernels + exchange + ordered sum.
+static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, double max_d2, double out17[17]) {
+    lio::IcpArgs a{};
+    a.grid = lio::grid_view(h->tgt);
+    a.tgt_by_id = h->tgt.by_id;
+    a.cur = h->d_cur;
+    a.src = h->d_src;
+    a.n = (int)h->sh_n;
+    a.apply_T = apply_T ? 1 : 0;
+    std::memcpy(a.T, T, sizeof(a.T));
+    std::memcpy(a.c0, h->c0, sizeof(a.c0));
+    a.max_d2 = max_d2;
+    a.fitness = fitness ? 1 : 0;
+    a.max_shell_near = 2;
+    a.partials = h->d_part;
+    a.far_list = h->d_far;
+    a.far_count = h->d_far_count;
+    a.far_d2 = h->d_fd2;
+    a.far_id = h->d_fid;
+    const int nch = (int)((h->sh_n + lio::kIcpChunk - 1) / lio::kIcpChunk);
+    const int nsup_loc = (int)((h->sh_n + lio::kIcpSuper - 1) / lio::kIcpSuper);
+    if (h->sh_n > 0) {
+        IHIP(hipMemsetAsync(h->d_far_count, 0, 64, h->st));
+        if (h->timing) IHIP(hipEventRecord(h->ev.a, h->st));
+        lio::launch_icp_near(a, h->st);
+        lio::launch_icp_far(a, 512, h->st);
+        lio::launch_icp_stats(a, h->st);
+        if (h->timing) IHIP(hipEventRecord(h->ev.b, h->st));
+        lio::launch_icp_reduce(h->d_part, nch, h->d_super, h->st);
+        IHIP(hipGetLastError());
+        IHIP(hipMemcpyAsync(h->h_super, h->d_super, (size_t)nsup_loc * lio::kIcpStride * sizeof(double),
+                            hipMemcpyDeviceToHost, h->st));
+    }
+    IHIP(hipStreamSynchronize(h->st));
+    if (h->timing && h->sh_n > 0) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, h->ev.a, h->ev.b) == hipSuccess) {
+            h->tm.icp_ms += ms;
+            ++h->tm.icp_launches;
+        }
+    }
+    for (int k = 0; k < 17; ++k) out17[k] = 0.0;
+    if (h->world == 1) {
+        for (int s = 0; s < nsup_loc; ++s)
+            for (int k = 0; k < 17; ++k) out17[k] += h->h_super[(size_t)s * lio::kIcpStride + k];
+        return LIO_OK;
+    }
+    // sharded: all-gather fixed-size slots (max records per rank), sum in global record order
+    const int64_t nsup = (h->ns + lio::kIcpSuper - 1) / lio::kIcpSuper;
+    const int64_t slot = (nsup + h->world - 1) / h->world;
+    std::vector<double> send((size_t)slot * lio::kIcpStride, 0.0), recv((size_t)slot * lio::kIcpStride * h->world);
+    std::memcpy(send.data(), h->h_super, (size_t)nsup_loc * lio::kIcpStride * sizeof(double));
+    if (h->fn(send.data(), (int64_t)send.size(), recv.data(), h->user) != 0)
+        return ifail(LIO_ERR_STATE, "allgather callback failed");
+    return lio_icp_combine(recv.data(), h->ns, h->world, out17);
+}
+
+extern "C" int lio_icp_shard_range(int64_t ns, int rank, int world, int64_t* begin, int64_t* count) {
+    if (ns < 0 || world < 1 || rank < 0 || rank >= world || !begin || !count)
+        return ifail(LIO_ERR_ARG, "lio_icp_shard_range: bad arguments");
+    shard_range(ns, rank, world, *begin, *count);
+    return LIO_OK;
+}
+
+extern "C" int lio_icp_combine(const double* recv, int64_t ns, int world, double* out17) {
+    if (!recv || !out17 || world < 1 || ns < 0) return ifail(LIO_ERR_ARG, "lio_icp_combine: bad arguments");
+    const int64_t nsup = (ns + lio::kIcpSuper - 1) / lio::kIcpSuper;
+    const int64_t slot = (nsup + world - 1) / world;
+    for (int k = 0; k < 17; ++k) out17[k] = 0.0;
+    for (int r = 0; r < world; ++r) {
+        const int64_t s0 = nsup * r / world, s1 = nsup * (r + 1) / world;
+        for (int64_t s = s0; s < s1; ++s) {
+            const double* rec = &recv[((size_t)r * slot + (size_t)(s - s0)) * lio::kIcpStride];
+            for (int k = 0; k < 17; ++k) out17[k] += rec[k];
+        }
+    }
+    return LIO_OK;
+}
+
+int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* aligned) {
+    if (!h || !out) return ifail(LIO_ERR_ARG, "lio_icp_align: bad arguments");
+    if (h->nt == 0) return ifail(LIO_ERR_STATE, "lio_icp_align: no target");
+    IHIP(hipSetDevice(h->dev));
+    int rc = icp_prepare(h);
+    if (rc) return rc;
+    float fin[16], G[16];
+    bool ident = true;
+    for (int i = 0; i < 16; ++i) {
+        G[i] = guess16 ? guess16[i] : ((i % 5 == 0) ? 1.f : 0.f);
+        fin[i] = G[i];
+        if (G[i] != ((i % 5 == 0) ? 1.f : 0.f)) ident = false;
+    }
+    if (h->sh_n > 0)
+        IHIP(hipMemcpyAsync(h->d_cur, h->d_src, h->sh_n * 3 * sizeof(float), hipMemcpyDeviceToDevice, h->st));
+    const double max_d2 = h->p.max_corr_dist * h->p.max_corr_dist;
+    const double rot_thr = h->p.rot_eps > 0 ? h->p.rot_eps : 1.0 - h->p.trans_eps;
+    double prev_mse = std::numeric_limits<double>::max();
+    int iters = 0, similar = 0;
+    bool apply = !ident;
+    float Tapply[16];
+    std::memcpy(Tapply, G, sizeof(G));
+    std::memset(out, 0, sizeof(*out));
+    out->state = 0;
+    out->is_converged = 0;
+    for (;;) {
+        double st[17];
+        rc = icp_pass(h, false, apply, Tapply, max_d2, st);
+        if (rc) return rc;
+        out->last_corr = (int64_t)st[0];
+        if (st[0] < 3) {
+            out->is_converged = 0;
+            out->state = 5;
+            break;
+        }
+        float Ti[16];
+        umeyama(st, h->c0, Ti);
+        float nf[16];
+        for (int r = 0; r < 4; ++r)
+            for (int c = 0; c < 4; ++c) {
+                float s = Ti[4 * r] * fin[c];
+                s += Ti[4 * r + 1] * fin[4 + c];
+                s += Ti[4 * r + 2] * fin[8 + c];
+                s += Ti[4 * r + 3] * fin[12 + c];
+                nf[4 * r + c] = s;
+            }
+        std::memcpy(fin, nf, sizeof(fin));
+        ++iters;
+        const double mse = st[16] / st[0];
+        out->last_mse = mse;
+        // DefaultConvergenceCriteria (max_iterations_similar_transforms_ = 0)
+        bool done = false, is_similar = false;
+        if (iters >= h->p.max_iter) {
+            out->state = 1;
+            done = true;
+        } else {
+            const double cosang = 0.5 * ((double)Ti[0] + (double)Ti[5] + (double)Ti[10] - 1);
+            const double tsq = (double)Ti[3] * Ti[3] + (double)Ti[7] * Ti[7] + (double)Ti[11] * Ti[11];
+            if (cosang >= rot_thr && tsq <= h->p.trans_eps) {
+                out->state = 2;
+                done = true;
+                is_similar = true;
+            }
+            if (!done && std::fabs(mse - prev_mse) < 1e-12) {
+                out->state = 3;
+                done = true;
+            }
+            if (!done && std::fabs(mse - prev_mse) / prev_mse < h->p.fitness_eps) {
+                out->state = 4;
+                done = true;
+            }
+            if (!done) {
+                similar = is_similar ? similar + 1 : 0;
+                prev_mse = mse;
+            }
+        }
+        std::memcpy(Tapply, Ti, sizeof(Ti));
+        apply = true;
+        if (done) {
+            out->is_converged = 1;
+            break;
+        }
+    }
+    (void)similar;
+    out->iterations = iters;
+    std::memcpy(out->T, fin, sizeof(fin));
+    // getFitnessScore(): original source * final, unbounded 1-NN
+    double fs[17];
+    rc = icp_pass(h, true, true, fin, std::numeric_limits<double>::infinity(), fs);
+    if (rc) return rc;
+    out->score = fs[0] > 0 ? fs[16] / fs[0] : std::numeric_limits<double>::max();
+    out->is_valid = (out->is_converged && out->score < h->p.score_threshold) ? 1 : 0;
+    if (aligned && h->sh_n > 0) {
+        IHIP(hipMemcpyAsync(aligned, h->d_cur, h->sh_n * 3 * sizeof(float), hipMemcpyDeviceToHost, h->st));
+        IHIP(hipStreamSynchronize(h->st));
+    }
+    return LIO_OK;
+}
+
+int icp_align(const float* src, int64_t ns, const float* dst, int64_t nd, const lio_icp_params* p, float* T_out,
+              double* fitness, int* converged, int* iters, float* aligned) {
+    lio_icp* h = nullptr;
+    int rc = lio_icp_create(p, &h);
+    if (rc) return rc;
+    rc = lio_icp_set_target(h, dst, nd);
+    if (!rc) rc = lio_icp_set_source(h, src, ns);
+    lio_icp_result r{};
+    if (!rc) rc = lio_icp_align(h, nullptr, &r, aligned);
+    if (!rc) {
+        if (T_out) std::memcpy(T_out, r.T, sizeof(r.T));
+        if (fitness) *fitness = r.score;
+        if (converged) *converged = r.is_converged;
+        if (iters) *iters = r.iterations;
+    }
+    lio_icp_destroy(h);
+    return rc;
+}
+
+int lio_icp_set_timing(lio_icp* h, int enable) {
+    if (!h) return ifail(LIO_ERR_ARG, "NULL handle");
+    h->timing = enable != 0;
+    return LIO_OK;
+}
+int lio_icp_get_timing(lio_icp* h, lio_kernel_timing* out) {
+    if (!h || !out) return ifail(LIO_ERR_ARG, "bad arguments");
+    *out = h->tm;
+    return LIO_OK;
+}
+
+}  // extern "C"

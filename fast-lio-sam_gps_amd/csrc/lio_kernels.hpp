@@ -1,0 +1,94 @@
+// lio_kernels.hpp — kernel argument blocks and launcher declarations.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lio_dev.hpp"
+
+namespace lio {
+
+struct MatchArgs {
+    PoseArg pose;
+    GridDev grid;
+    const float* body;        // n*3 feats_down_body
+    const float4* map_by_id;  // map points in id order (neighbour coordinates)
+    int32_t* nn_idx;          // n*5 Nearest_Points ids
+    float4* planes;           // n plane (a,b,c,d) cache
+    uint8_t* sel;             // n point_selected_surf
+    double* partials;         // nblocks*32
+    int n;
+    int max_shell;
+    float range_sq;
+    float plane_thr;
+    double s_coef;
+    double s_gate;
+};
+
+int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st);
+void launch_finalize(const double* partials, int nblocks, double* out, hipStream_t st);
+void launch_debug(const MatchArgs& a, float* world, float* d2, float* abcd_pd2, hipStream_t st);
+void launch_h_rows(const MatchArgs& a, double* rows, int64_t max_rows, int64_t* n_rows, hipStream_t st);
+int match_blocks(int n);
+
+// --------------------------------------------------------------- grid build
+struct GridGeom {
+    float ox, oy, oz, cell;
+    int nx, ny, nz;
+    uint32_t ncells;
+};
+
+// Device buffers owned by a grid (map or ICP target).
+struct GridBuf {
+    float4* pts = nullptr;      // sorted by cell
+    float4* by_id = nullptr;    // id order
+    uint32_t* start = nullptr;  // ncells + 1
+    int64_t n = 0, cap = 0;
+    uint32_t cells_cap = 0;
+    GridGeom geom{};
+    // temporaries
+    uint32_t* keys = nullptr;
+    uint32_t* keys_alt = nullptr;
+    uint32_t* vals = nullptr;
+    uint32_t* vals_alt = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    float* aabb = nullptr;       // device 6 floats
+    float* aabb_host = nullptr;  // pinned 6 floats
+    float* xyz = nullptr;        // staging for host input, cap*3
+};
+
+// Build grid from device xyz (n*3).  Synchronises the stream once (AABB).
+int grid_build(GridBuf& g, const float* d_xyz, int64_t n, float cell, hipStream_t st);
+void grid_free(GridBuf& g);
+GridDev grid_view(const GridBuf& g);
+
+// ---------------------------------------------------------------------- ICP
+struct IcpArgs {
+    GridDev grid;
+    const float4* tgt_by_id;
+    float* cur;          // n*3 incrementally transformed source (this rank's shard)
+    const float* src;    // n*3 original source (fitness pass)
+    int n;               // points in this shard
+    int apply_T;         // apply T (float 4x4 row-major) to cur before the NN (incremental transform)
+    float T[16];
+    double c0[3];        // accumulation centre
+    double max_d2;       // correspondence rejection (d2 > max_d2 => skip)
+    int fitness;         // 1: fitness pass (src with T, unbounded, sum d2 only)
+    int max_shell_near;  // shells searched in the first pass
+    double* partials;    // per 256-point chunk: 17 doubles padded to 20
+    int* far_list;       // queries left unresolved by the first pass
+    int* far_count;
+    float* far_d2;       // best-so-far per point (n)
+    int* far_id;
+};
+
+constexpr int kIcpChunk = 256;     // points per partial
+constexpr int kIcpSuper = 4096;    // points per exchanged partial (shard granule)
+constexpr int kIcpStride = 20;     // doubles per partial record
+
+void launch_icp_near(const IcpArgs& a, hipStream_t st);
+void launch_icp_far(const IcpArgs& a, int max_far_blocks, hipStream_t st);
+void launch_icp_stats(const IcpArgs& a, hipStream_t st);
+void launch_icp_reduce(const double* partials, int nchunks, double* super, hipStream_t st);
+
+}  // namespace lio

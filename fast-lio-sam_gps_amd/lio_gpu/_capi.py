@@ -1,0 +1,161 @@
+"""ctypes declarations of include/lio_gpu.h and the loader for liblio_gpu.so.
+
+The shared library is built in-tree (``make -C fast-lio-sam_gps_amd``) into
+``lio_gpu/_lib/liblio_gpu.so``.  There is no fallback: if the library is
+missing, :func:`lib` raises, and every compute entry point of the library
+itself fails with ``LIO_ERR_NODEV`` when no gfx950 device is visible.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "_lib", "liblio_gpu.so")
+
+LIO_OK = 0
+LIO_ERR_ARG = -1
+LIO_ERR_HIP = -2
+LIO_ERR_NODEV = -3
+LIO_ERR_STATE = -4
+LIO_ERR_NOMEM = -5
+LIO_SUMS_LEN = 32
+SUMS_HTH, SUMS_HTh, SUMS_NEFF, SUMS_RES, SUMS_HH = 0, 21, 27, 28, 29
+
+# Every symbol include/lio_gpu.h declares (checked by tests/test_capi_symbols.py).
+EXPORTS = [
+    "lio_device_count", "lio_last_error", "lio_build_info",
+    "lio_map_create", "lio_map_destroy", "lio_map_build", "lio_map_build_device", "lio_map_size",
+    "lio_map_get_points", "lio_map_get_grid",
+    "lio_ctx_create", "lio_ctx_destroy", "lio_scan_set", "lio_scan_set_device", "lio_match",
+    "lio_get_knn", "lio_get_planes", "lio_get_world", "lio_get_h_rows",
+    "lio_ieskf_update",
+    "lio_icp_create", "lio_icp_destroy", "lio_icp_set_target", "lio_icp_set_source", "lio_icp_set_shard",
+    "lio_icp_align", "icp_align", "lio_icp_shard_range", "lio_icp_combine",
+    "lio_ctx_set_timing", "lio_ctx_get_timing", "lio_ctx_reset_timing", "lio_icp_set_timing", "lio_icp_get_timing",
+]
+
+
+class LioError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"lio_gpu error {code}: {msg}")
+        self.code = code
+
+
+class MapParams(C.Structure):
+    _fields_ = [("cell_size", C.c_float), ("downsample_size", C.c_float), ("device", C.c_int),
+                ("reserved", C.c_int)]
+
+
+class MatchParams(C.Structure):
+    _fields_ = [("knn_range_sq", C.c_float), ("plane_thr", C.c_float), ("s_coef", C.c_double),
+                ("s_gate", C.c_double)]
+
+
+class Pose(C.Structure):
+    _fields_ = [("R", C.c_double * 9), ("t", C.c_double * 3), ("R_LI", C.c_double * 9), ("t_LI", C.c_double * 3)]
+
+
+class State(C.Structure):
+    _fields_ = [("pos", C.c_double * 3), ("rot", C.c_double * 4), ("offset_R_L_I", C.c_double * 4),
+                ("offset_T_L_I", C.c_double * 3), ("vel", C.c_double * 3), ("bg", C.c_double * 3),
+                ("ba", C.c_double * 3), ("grav", C.c_double * 3)]
+
+
+class IeskfParams(C.Structure):
+    _fields_ = [("laser_point_cov", C.c_double), ("max_iteration", C.c_int), ("epsi", C.c_double)]
+
+
+class IeskfStats(C.Structure):
+    _fields_ = [("h_evals", C.c_int), ("knn_calls", C.c_int), ("converged", C.c_int), ("n_eff", C.c_int),
+                ("res_mean", C.c_double), ("solve_ms", C.c_double)]
+
+
+class IcpParams(C.Structure):
+    _fields_ = [("max_corr_dist", C.c_double), ("trans_eps", C.c_double), ("fitness_eps", C.c_double),
+                ("max_iter", C.c_int), ("rot_eps", C.c_double), ("score_threshold", C.c_double),
+                ("cell_size", C.c_float), ("device", C.c_int)]
+
+
+class IcpResult(C.Structure):
+    _fields_ = [("is_valid", C.c_int), ("is_converged", C.c_int), ("score", C.c_double), ("T", C.c_float * 16),
+                ("iterations", C.c_int), ("state", C.c_int), ("last_mse", C.c_double), ("last_corr", C.c_int64)]
+
+
+class KernelTiming(C.Structure):
+    _fields_ = [("knn_launches", C.c_int64), ("knn_ms", C.c_double), ("reuse_launches", C.c_int64),
+                ("reuse_ms", C.c_double), ("final_launches", C.c_int64), ("final_ms", C.c_double),
+                ("icp_launches", C.c_int64), ("icp_ms", C.c_double)]
+
+
+ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double), C.c_void_p)
+
+_lib = None
+
+fp = C.POINTER(C.c_float)
+dp = C.POINTER(C.c_double)
+vp = C.c_void_p
+
+
+def _declare(L):
+    sig = {
+        "lio_device_count": (C.c_int, []),
+        "lio_last_error": (C.c_char_p, []),
+        "lio_build_info": (C.c_char_p, []),
+        "lio_map_create": (C.c_int, [C.POINTER(MapParams), C.POINTER(vp)]),
+        "lio_map_destroy": (C.c_int, [vp]),
+        "lio_map_build": (C.c_int, [vp, fp, C.c_int64]),
+        "lio_map_build_device": (C.c_int, [vp, vp, C.c_int64]),
+        "lio_map_size": (C.c_int64, [vp]),
+        "lio_map_get_points": (C.c_int, [vp, fp]),
+        "lio_map_get_grid": (C.c_int, [vp, dp]),
+        "lio_ctx_create": (C.c_int, [vp, C.POINTER(MatchParams), C.POINTER(vp)]),
+        "lio_ctx_destroy": (C.c_int, [vp]),
+        "lio_scan_set": (C.c_int, [vp, fp, C.c_int64]),
+        "lio_scan_set_device": (C.c_int, [vp, vp, C.c_int64]),
+        "lio_match": (C.c_int, [vp, C.POINTER(Pose), C.c_int, dp]),
+        "lio_get_knn": (C.c_int, [vp, C.POINTER(C.c_int32), fp]),
+        "lio_get_planes": (C.c_int, [vp, fp, C.POINTER(C.c_uint8)]),
+        "lio_get_world": (C.c_int, [vp, fp]),
+        "lio_get_h_rows": (C.c_int, [vp, dp, C.c_int64, C.POINTER(C.c_int64)]),
+        "lio_ieskf_update": (C.c_int, [vp, C.POINTER(State), dp, C.POINTER(IeskfParams), C.POINTER(IeskfStats)]),
+        "lio_icp_create": (C.c_int, [C.POINTER(IcpParams), C.POINTER(vp)]),
+        "lio_icp_destroy": (C.c_int, [vp]),
+        "lio_icp_set_target": (C.c_int, [vp, fp, C.c_int64]),
+        "lio_icp_set_source": (C.c_int, [vp, fp, C.c_int64]),
+        "lio_icp_set_shard": (C.c_int, [vp, C.c_int, C.c_int, ALLGATHER_FN, vp]),
+        "lio_icp_align": (C.c_int, [vp, fp, C.POINTER(IcpResult), fp]),
+        "icp_align": (C.c_int, [fp, C.c_int64, fp, C.c_int64, C.POINTER(IcpParams), fp, dp,
+                                C.POINTER(C.c_int), C.POINTER(C.c_int), fp]),
+        "lio_icp_shard_range": (C.c_int, [C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
+        "lio_icp_combine": (C.c_int, [dp, C.c_int64, C.c_int, dp]),
+        "lio_ctx_set_timing": (C.c_int, [vp, C.c_int]),
+        "lio_ctx_get_timing": (C.c_int, [vp, C.POINTER(KernelTiming)]),
+        "lio_ctx_reset_timing": (C.c_int, [vp]),
+        "lio_icp_set_timing": (C.c_int, [vp, C.c_int]),
+        "lio_icp_get_timing": (C.c_int, [vp, C.POINTER(KernelTiming)]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+
+
+def lib():
+    """Load liblio_gpu.so (raises if it was not built — there is no fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run `make -C fast-lio-sam_gps_amd` "
+                              "(or __graft_entry__.build()); lio_gpu has no CPU path")
+        L = C.CDLL(LIB_PATH)
+        _declare(L)
+        _lib = L
+    return _lib
+
+
+def check(rc):
+    if rc != LIO_OK:
+        msg = lib().lio_last_error()
+        raise LioError(rc, msg.decode() if msg else "")
+    return rc

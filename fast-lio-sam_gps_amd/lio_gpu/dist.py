@@ -1,0 +1,69 @@
+"""Multi-GPU plumbing for the sharded loop ICP (one process per GPU).
+
+The ICP correspondence search shards the SOURCE cloud over ranks in whole
+4096-point records (``lio_icp_shard_range``); per iteration every rank
+all-gathers the per-record Umeyama statistics (20 doubles/record) and sums
+them in record order (``lio_icp_combine``), so every rank — and every world
+size — computes the bit-identical transform.  The exchange goes through
+``torch.distributed`` (backend "nccl" = RCCL over xGMI on the GPU box, "gloo"
+in the CPU tests): torch is plumbing here, the statistics are produced by the
+HIP kernels behind the C-ABI.  SURVEY.md §8e.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _capi
+from ._capi import check, lib
+
+
+def shard_range(n_source: int, rank: int, world: int):
+    b, n = C.c_int64(), C.c_int64()
+    check(lib().lio_icp_shard_range(n_source, rank, world, C.byref(b), C.byref(n)))
+    return b.value, n.value
+
+
+def combine(recv: np.ndarray, n_source: int, world: int) -> np.ndarray:
+    recv = np.ascontiguousarray(recv, dtype=np.float64)
+    out = np.zeros(17)
+    check(lib().lio_icp_combine(recv.ctypes.data_as(C.POINTER(C.c_double)), n_source, world,
+                                out.ctypes.data_as(C.POINTER(C.c_double))))
+    return out
+
+
+def allgather_numpy(send: np.ndarray, group=None, device=None) -> np.ndarray:
+    """All-gather one float64 vector per rank (rank order) through torch.distributed."""
+    import torch
+    import torch.distributed as dist
+
+    world = dist.get_world_size(group)
+    t = torch.from_numpy(np.ascontiguousarray(send, dtype=np.float64))
+    if device is not None:
+        t = t.to(device)
+    out = torch.empty(world * t.numel(), dtype=t.dtype, device=t.device)
+    dist.all_gather_into_tensor(out, t, group=group)
+    return out.cpu().numpy()
+
+
+def make_allgather(group=None, device=None):
+    """ctypes ``lio_allgather_fn`` doing the exchange with torch.distributed.
+
+    Keep the returned object alive while the ICP handle uses it.
+    """
+
+    def _cb(send_p, n, recv_p, user):
+        try:
+            send = np.ctypeslib.as_array(send_p, shape=(n,)).copy()
+            res = allgather_numpy(send, group=group, device=device)
+            recv = np.ctypeslib.as_array(recv_p, shape=(res.size,))
+            recv[:] = res
+            return 0
+        except Exception:  # the C side turns a non-zero status into LIO_ERR_STATE
+            import traceback
+
+            traceback.print_exc()
+            return -1
+
+    return _capi.ALLGATHER_FN(_cb)

@@ -1,0 +1,205 @@
+"""Host mirror of the FAST-LIO front-end hot path over the C-ABI.
+
+Names follow the reference's interfaces so callers read like FAST-LIO
+(upstream hku-mars src/laserMapping.cpp, include/ikd-Tree, IKFoM esekfom.hpp;
+the Kodifly fork is an empty submodule in the reference, .gitmodules:1-3):
+
+* :class:`IkdTreeGPU` — ``KD_TREE<PointType> ikdtree`` (``Build``, ``size``)
+* :class:`HShareModelGPU` — ``h_share_model(state_ikfom&, dyn_share_datastruct&)``
+  with its globals (``Nearest_Points``, ``point_selected_surf``, ``normvec``,
+  ``feats_down_world``) exposed as getters
+* :class:`EsekfGPU` — ``kf.update_iterated_dyn_share_modified(LASER_POINT_COV, solve_H_time)``
+
+All compute runs in liblio_gpu.so on a gfx950 device; errors raise
+:class:`lio_gpu._capi.LioError` (no CPU fallback).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _capi
+from ._capi import check, lib
+
+_STATE_KEYS = ("pos", "rot", "offset_R_L_I", "offset_T_L_I", "vel", "bg", "ba", "grav")
+
+
+def _fp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _dp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_double))
+
+
+def default_match_params(**kw) -> _capi.MatchParams:
+    """h_share_model constants [U]: gate sqdist[4] > 5, esti_plane 0.1f, s = 1 - 0.9|pd2|/sqrt(|p|) > 0.9."""
+    p = _capi.MatchParams(5.0, 0.1, 0.9, 0.9)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def pose_from_arrays(R, t, R_LI=np.eye(3), t_LI=np.zeros(3)) -> _capi.Pose:
+    p = _capi.Pose()
+    for i, v in enumerate(np.asarray(R, float).ravel()):
+        p.R[i] = v
+    for i, v in enumerate(np.asarray(t, float).ravel()):
+        p.t[i] = v
+    for i, v in enumerate(np.asarray(R_LI, float).ravel()):
+        p.R_LI[i] = v
+    for i, v in enumerate(np.asarray(t_LI, float).ravel()):
+        p.t_LI[i] = v
+    return p
+
+
+def pose_from_pose24(p24) -> _capi.Pose:
+    p24 = np.asarray(p24, float)
+    return pose_from_arrays(p24[0:9], p24[9:12], p24[12:21], p24[21:24])
+
+
+def state_to_c(st: dict) -> _capi.State:
+    s = _capi.State()
+    for k in _STATE_KEYS:
+        arr = getattr(s, k)
+        for i, v in enumerate(np.asarray(st[k], float)):
+            arr[i] = float(v)
+    return s
+
+
+def state_from_c(s: _capi.State) -> dict:
+    return {k: np.array(list(getattr(s, k))) for k in _STATE_KEYS}
+
+
+class IkdTreeGPU:
+    """Dense-grid map in HBM standing in for the ikd-Tree (exact kNN)."""
+
+    def __init__(self, cell_size: float = 1.0, downsample_size: float = 0.5, device: int = 0):
+        self._h = C.c_void_p()
+        check(lib().lio_map_create(C.byref(_capi.MapParams(cell_size, downsample_size, device, 0)),
+                                   C.byref(self._h)))
+
+    def Build(self, points: np.ndarray):
+        pts = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 3)
+        check(lib().lio_map_build(self._h, _fp(pts), len(pts)))
+
+    def Build_device(self, ptr: int, n: int):
+        """Build from an xyz float32 buffer already in device memory (e.g. a torch tensor's data_ptr())."""
+        check(lib().lio_map_build_device(self._h, C.c_void_p(ptr), n))
+
+    def size(self) -> int:
+        return int(lib().lio_map_size(self._h))
+
+    def points(self) -> np.ndarray:
+        out = np.empty((self.size(), 3), np.float32)
+        check(lib().lio_map_get_points(self._h, _fp(out)))
+        return out
+
+    def grid(self):
+        g = np.zeros(7)
+        check(lib().lio_map_get_grid(self._h, _dp(g)))
+        return dict(origin=g[0:3], cell=g[3], dims=g[4:7].astype(int))
+
+    def close(self):
+        if self._h:
+            lib().lio_map_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class HShareModelGPU:
+    """``h_share_model`` on the GPU for one ``feats_down_body`` scan."""
+
+    def __init__(self, tree: IkdTreeGPU, params: _capi.MatchParams | None = None):
+        self.tree = tree
+        self._h = C.c_void_p()
+        self.params = params or default_match_params()
+        check(lib().lio_ctx_create(tree._h, C.byref(self.params), C.byref(self._h)))
+        self.n = 0
+
+    def set_scan(self, body: np.ndarray):
+        b = np.ascontiguousarray(body, dtype=np.float32).reshape(-1, 3)
+        check(lib().lio_scan_set(self._h, _fp(b), len(b)))
+        self.n = len(b)
+
+    def set_scan_device(self, ptr: int, n: int):
+        check(lib().lio_scan_set_device(self._h, C.c_void_p(ptr), n))
+        self.n = n
+
+    def __call__(self, pose, converge: bool = True) -> np.ndarray:
+        """One evaluation; ``pose`` is a lio Pose or a pose24 array. Returns sums[32]."""
+        if not isinstance(pose, _capi.Pose):
+            pose = pose_from_pose24(pose)
+        sums = np.zeros(_capi.LIO_SUMS_LEN)
+        check(lib().lio_match(self._h, C.byref(pose), 1 if converge else 0, _dp(sums)))
+        return sums
+
+    # ---- globals of the reference's h_share_model, for inspection / parity
+    def nearest_points(self):
+        idx = np.empty((self.n, 5), np.int32)
+        d2 = np.empty((self.n, 5), np.float32)
+        check(lib().lio_get_knn(self._h, idx.ctypes.data_as(C.POINTER(C.c_int32)), _fp(d2)))
+        return idx, d2
+
+    def normvec(self):
+        abcd = np.empty((self.n, 4), np.float32)
+        sel = np.empty(self.n, np.uint8)
+        check(lib().lio_get_planes(self._h, _fp(abcd), sel.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return abcd, sel
+
+    def world(self):
+        w = np.empty((self.n, 3), np.float32)
+        check(lib().lio_get_world(self._h, _fp(w)))
+        return w
+
+    def h_rows(self, max_rows: int):
+        rows = np.empty((max(max_rows, 1), 7), np.float64)
+        nr = C.c_int64(0)
+        check(lib().lio_get_h_rows(self._h, _dp(rows), max_rows, C.byref(nr)))
+        return rows[: min(nr.value, max_rows)], nr.value
+
+    # ---- timing (HIP events on the context's stream)
+    def set_timing(self, on: bool):
+        check(lib().lio_ctx_set_timing(self._h, 1 if on else 0))
+
+    def timing(self) -> dict:
+        t = _capi.KernelTiming()
+        check(lib().lio_ctx_get_timing(self._h, C.byref(t)))
+        return {k: getattr(t, k) for k, _ in _capi.KernelTiming._fields_}
+
+    def reset_timing(self):
+        check(lib().lio_ctx_reset_timing(self._h))
+
+    def close(self):
+        if self._h:
+            lib().lio_ctx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class EsekfGPU:
+    """``esekfom::esekf::update_iterated_dyn_share_modified`` with the GPU h-model."""
+
+    def __init__(self, model: HShareModelGPU, laser_point_cov: float = 0.001, max_iteration: int = 3,
+                 epsi: float = 0.001):
+        self.model = model
+        self.params = _capi.IeskfParams(laser_point_cov, max_iteration, epsi)
+
+    def update_iterated_dyn_share_modified(self, state: dict, P: np.ndarray):
+        s = state_to_c(state)
+        Pc = np.ascontiguousarray(P, dtype=np.float64).copy()
+        st = _capi.IeskfStats()
+        check(lib().lio_ieskf_update(self.model._h, C.byref(s), _dp(Pc), C.byref(self.params), C.byref(st)))
+        stats = {k: getattr(st, k) for k, _ in _capi.IeskfStats._fields_}
+        return state_from_c(s), Pc, stats

@@ -1,0 +1,126 @@
+"""Host mirror of ``LoopClosure`` (/root/reference/fast_lio_sam/include/loop_closure.h:21-72).
+
+Only the ★ hot-path member ``icpAlignment`` (loop_closure.cpp:69-92) is backed
+by the GPU; it keeps the class surface: configuration as in the constructor
+(loop_closure.cpp:3-14), ``RegistrationOutput`` as returned value, the aligned
+cloud kept for ``getFinalAlignedCloud`` (loop_closure.cpp:73,81,139-142).
+Sharding over ranks (one process per GPU) plugs in through
+:func:`lio_gpu.dist.make_allgather` — see include/lio_gpu.h lio_icp_set_shard.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import dataclasses
+
+import numpy as np
+
+from . import _capi
+from ._capi import check, lib
+
+
+@dataclasses.dataclass
+class LoopClosureConfig:  # loop_closure.h:21-29, values from fast_lio_sam.cpp:64-80 + config.yaml
+    num_submap_keyframes_: int = 5
+    voxel_res_: float = 0.3
+    loop_detection_radius_: float = 35.0
+    loop_detection_timediff_threshold_: float = 30.0
+    icp_score_threshold_: float = 1.5
+    icp_max_corr_dist_: float = 52.5  # 1.5 * loop_detection_radius_ (fast_lio_sam.cpp:73)
+
+
+@dataclasses.dataclass
+class RegistrationOutput:  # loop_closure.h:31-37
+    is_valid_: bool = False
+    is_converged_: bool = False
+    score_: float = float(np.finfo(np.float64).max)
+    pose_between_eig_: np.ndarray = dataclasses.field(default_factory=lambda: np.eye(4))
+    iterations: int = 0
+    state: int = 0
+
+
+def icp_params(config: LoopClosureConfig, cell_size: float = 1.0, device: int = 0) -> _capi.IcpParams:
+    # setTransformationEpsilon(0.01), setEuclideanFitnessEpsilon(0.01), setMaximumIterations(50)
+    return _capi.IcpParams(config.icp_max_corr_dist_, 0.01, 0.01, 50, 0.0, config.icp_score_threshold_,
+                           cell_size, device)
+
+
+class LoopClosure:
+    def __init__(self, config: LoopClosureConfig, cell_size: float = 1.0, device: int = 0):
+        self.config_ = config
+        self._p = icp_params(config, cell_size, device)
+        self._h = C.c_void_p()
+        check(lib().lio_icp_create(C.byref(self._p), C.byref(self._h)))
+        self.aligned_ = np.zeros((0, 3), np.float32)
+        self._shard = (0, 1)
+        self._cb = None
+
+    def set_shard(self, rank: int, world: int, allgather=None):
+        """Shard the source over ``world`` ranks; ``allgather`` from lio_gpu.dist.make_allgather."""
+        self._cb = allgather
+        fn = allgather if allgather is not None else _capi.ALLGATHER_FN()
+        check(lib().lio_icp_set_shard(self._h, rank, world, fn, None))
+        self._shard = (rank, world)
+
+    def set_timing(self, on: bool):
+        check(lib().lio_icp_set_timing(self._h, 1 if on else 0))
+
+    def timing(self) -> dict:
+        t = _capi.KernelTiming()
+        check(lib().lio_icp_get_timing(self._h, C.byref(t)))
+        return {k: getattr(t, k) for k, _ in _capi.KernelTiming._fields_}
+
+    def setInputTarget(self, dst: np.ndarray):
+        d = np.ascontiguousarray(dst, dtype=np.float32).reshape(-1, 3)
+        check(lib().lio_icp_set_target(self._h, d.ctypes.data_as(C.POINTER(C.c_float)), len(d)))
+
+    def setInputSource(self, src: np.ndarray):
+        s = np.ascontiguousarray(src, dtype=np.float32).reshape(-1, 3)
+        check(lib().lio_icp_set_source(self._h, s.ctypes.data_as(C.POINTER(C.c_float)), len(s)))
+        self._ns = len(s)
+
+    def align(self, guess: np.ndarray | None = None, keep_aligned: bool = True):
+        res = _capi.IcpResult()
+        g = None if guess is None else np.ascontiguousarray(guess, dtype=np.float32).reshape(16)
+        out = None
+        if keep_aligned:
+            rank, world = self._shard
+            nsup = (self._ns + 4095) // 4096
+            b = min(nsup * rank // world * 4096, self._ns)
+            e = min(nsup * (rank + 1) // world * 4096, self._ns)
+            out = np.empty((max(e - b, 0), 3), np.float32)
+        check(lib().lio_icp_align(self._h, None if g is None else g.ctypes.data_as(C.POINTER(C.c_float)),
+                                  C.byref(res), None if out is None else out.ctypes.data_as(C.POINTER(C.c_float))))
+        if out is not None:
+            self.aligned_ = out
+        return res
+
+    def icpAlignment(self, src: np.ndarray, dst: np.ndarray) -> RegistrationOutput:
+        """loop_closure.cpp:69-92: align src to dst; valid iff converged and score < threshold."""
+        out = RegistrationOutput()
+        self.aligned_ = np.zeros((0, 3), np.float32)
+        self.setInputSource(src)
+        self.setInputTarget(dst)
+        res = self.align()
+        out.score_ = res.score
+        out.iterations = res.iterations
+        out.state = res.state
+        if res.is_converged and res.score < self.config_.icp_score_threshold_:
+            out.is_valid_ = True
+            out.is_converged_ = True
+            out.pose_between_eig_ = np.array(list(res.T), dtype=np.float32).reshape(4, 4).astype(np.float64)
+        self.last_result = res
+        return out
+
+    def getFinalAlignedCloud(self) -> np.ndarray:
+        return self.aligned_
+
+    def close(self):
+        if self._h:
+            lib().lio_icp_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,222 @@
+/*
+ * lio_gpu.h — C-ABI of the MI355X (gfx950) scan-matching hot path.
+ *
+ * Drop-in boundary for the reference's hot path:
+ *
+ *  B-front: FAST-LIO's measurement model `void h_share_model(state_ikfom&,
+ *    esekfom::dyn_share_datastruct<double>&)` plus the ikd-Tree it queries
+ *    (upstream hku-mars FAST_LIO src/laserMapping.cpp + include/ikd-Tree; the
+ *    Kodifly fork is an empty submodule in the reference: .gitmodules:1-3,
+ *    launched by fast_lio_sam/launch/run.launch:20-46).  The host IESKF keeps
+ *    its 23-dim state; one lio_match() per h-evaluation replaces the per-point
+ *    OpenMP loop, and lio_ieskf_update() is the complete
+ *    `kf.update_iterated_dyn_share_modified(LASER_POINT_COV, solve_H_time)`.
+ *  B-loop: `RegistrationOutput LoopClosure::icpAlignment(src, dst)`
+ *    (/root/reference/fast_lio_sam/src/loop_closure.cpp:69-92, declared at
+ *    include/loop_closure.h:59-60) — replaced whole by lio_icp_align().
+ *
+ * Conventions: every call returns int status (LIO_OK = 0, < 0 on error;
+ * lio_last_error() gives text).  Host buffers are caller-owned and copied in;
+ * handles own device memory; one HIP stream per handle; a handle is not
+ * thread-safe, distinct handles may be used concurrently.  No torch types.
+ * There is no CPU fallback: without a gfx950 device every compute entry point
+ * fails with LIO_ERR_NODEV.
+ */
+#ifndef LIO_GPU_H
+#define LIO_GPU_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LIO_OK 0
+#define LIO_ERR_ARG (-1)
+#define LIO_ERR_HIP (-2)
+#define LIO_ERR_NODEV (-3)
+#define LIO_ERR_STATE (-4)
+#define LIO_ERR_NOMEM (-5)
+
+#define LIO_NUM_MATCH_POINTS 5 /* NUM_MATCH_POINTS [U: FAST-LIO common_lib.h] */
+#define LIO_STATE_DIM 23       /* state_ikfom DOF [U: FAST-LIO use-ikfom.hpp] */
+
+/* Layout of the per-h-evaluation reduction returned by lio_match() (doubles):
+ * H^T H upper triangle of the 6 non-zero columns (extrinsic_est_en = false,
+ * kitti.yaml:22) row-major i<=j, H^T h, effct_feat_num, total_residual, h^T h. */
+#define LIO_SUMS_HTH 0
+#define LIO_SUMS_HTh 21
+#define LIO_SUMS_NEFF 27
+#define LIO_SUMS_RES 28
+#define LIO_SUMS_HH 29
+#define LIO_SUMS_LEN 32
+
+/* ------------------------------------------------------------------ device */
+int lio_device_count(void);
+const char* lio_last_error(void);
+const char* lio_build_info(void);
+
+/* -------------------------------------------------------------------- map
+ * Replaces `KD_TREE<PointType> ikdtree` [U: ikd-Tree ikd_Tree.h]: a dense
+ * uniform grid in HBM (points float4 sorted by cell, u32 cell offsets).
+ * kNN results are exact; point ids are insertion order (0..size-1).       */
+typedef struct lio_map lio_map;
+
+typedef struct lio_map_params {
+    float cell_size;        /* grid cell edge [m]; 0 => 1.0                          */
+    float downsample_size;  /* filter_size_map (kitti.launch:10) for lio_map_add    */
+    int device;             /* HIP device ordinal                                   */
+    int reserved;
+} lio_map_params;
+
+int lio_map_create(const lio_map_params* p, lio_map** out);
+int lio_map_destroy(lio_map* m);
+/* ikdtree.Build(points) [U]: replaces the content. xyz: n*3 float, host.   */
+int lio_map_build(lio_map* m, const float* xyz, int64_t n);
+/* same, xyz already resident in device memory (e.g. a torch tensor).       */
+int lio_map_build_device(lio_map* m, const float* d_xyz, int64_t n);
+/* ikdtree.size() [U]                                                       */
+int64_t lio_map_size(const lio_map* m);
+/* copies the map points (id order) to host, n*3 float                      */
+int lio_map_get_points(lio_map* m, float* xyz_out);
+/* grid geometry: origin[3], cell, dims[3] (as doubles)                     */
+int lio_map_get_grid(lio_map* m, double* out7);
+
+/* ------------------------------------------------------------ h-model ctx */
+typedef struct lio_ctx lio_ctx;
+
+typedef struct lio_match_params {
+    float knn_range_sq; /* 5.0: gate `sqdist[4] > 5` rejects; bounded-search radius^2 */
+    float plane_thr;    /* 0.1f: esti_plane(pabcd, points_near, 0.1f)                  */
+    double s_coef;      /* 0.9: s = 1 - 0.9*|pd2|/sqrt(|p_body|)                        */
+    double s_gate;      /* 0.9: keep if s > 0.9                                         */
+} lio_match_params;
+
+/* The parts of state_ikfom the measurement model reads, as row-major double
+ * rotation matrices: p_world = R*(R_LI*p_body + t_LI) + t.                 */
+typedef struct lio_pose {
+    double R[9];
+    double t[3];
+    double R_LI[9];
+    double t_LI[3];
+} lio_pose;
+
+int lio_ctx_create(lio_map* m, const lio_match_params* p, lio_ctx** out);
+int lio_ctx_destroy(lio_ctx* c);
+/* feats_down_body (n*3 float, LiDAR frame), host / device pointer.         */
+int lio_scan_set(lio_ctx* c, const float* body_xyz, int64_t n);
+int lio_scan_set_device(lio_ctx* c, const float* d_body_xyz, int64_t n);
+/* One h_share_model evaluation [U]. redo_knn = ekfom_data.converge.
+ * sums: LIO_SUMS_LEN doubles (see layout above).                           */
+int lio_match(lio_ctx* c, const lio_pose* pose, int redo_knn, double* sums);
+/* Debug getters (not on the timed path):
+ *   Nearest_Points ids + sq-distances (n*5, -1 / +inf where fewer than 5),
+ *   normvec (a,b,c,pd2 for selected points) + point_selected_surf,
+ *   feats_down_world for the pose of the last lio_match.                    */
+int lio_get_knn(lio_ctx* c, int32_t* idx, float* d2);
+int lio_get_planes(lio_ctx* c, float* abcd_pd2, uint8_t* sel);
+int lio_get_world(lio_ctx* c, float* world);
+/* ekfom_data.h_x rows (6 non-zero columns) + h of the selected points, in
+ * point order, for the dof < 23 branch of the IESKF: rows = 7 doubles each. */
+int lio_get_h_rows(lio_ctx* c, double* rows, int64_t max_rows, int64_t* n_rows);
+
+/* ------------------------------------------------------------------ IESKF */
+typedef struct lio_state { /* state_ikfom [U], quaternions are (w, x, y, z) */
+    double pos[3];
+    double rot[4];
+    double offset_R_L_I[4];
+    double offset_T_L_I[3];
+    double vel[3];
+    double bg[3];
+    double ba[3];
+    double grav[3];
+} lio_state;
+
+typedef struct lio_ieskf_params {
+    double laser_point_cov; /* LASER_POINT_COV = 0.001 [U]                  */
+    int max_iteration;      /* NUM_MAX_ITERATIONS = max_iteration = 3 (kitti.launch:8) */
+    double epsi;            /* convergence limit per state dim = 0.001 [U]  */
+} lio_ieskf_params;
+
+typedef struct lio_ieskf_stats {
+    int h_evals;    /* h_share_model calls                               */
+    int knn_calls;  /* of which redid the kNN (ekfom_data.converge)      */
+    int converged;  /* exited through t > 1 (1) or the iteration cap (0) */
+    int n_eff;      /* effct_feat_num of the last evaluation             */
+    double res_mean;/* res_mean_last                                     */
+    double solve_ms;/* host time in the 23-dim algebra                   */
+} lio_ieskf_stats;
+
+/* esekf::update_iterated_dyn_share_modified(R, solve_time) [U IKFoM];
+ * x and P (23x23 row-major) are updated in place.                          */
+int lio_ieskf_update(lio_ctx* c, lio_state* x, double* P, const lio_ieskf_params* p, lio_ieskf_stats* st);
+
+/* ---------------------------------------------------------------- loop ICP */
+typedef struct lio_icp lio_icp;
+
+typedef struct lio_icp_params {
+    double max_corr_dist;   /* icp_max_corr_dist_ = 1.5 * loop_detection_radius (fast_lio_sam.cpp:73) */
+    double trans_eps;       /* setTransformationEpsilon(0.01)   loop_closure.cpp:8  */
+    double fitness_eps;     /* setEuclideanFitnessEpsilon(0.01) loop_closure.cpp:9  */
+    int max_iter;           /* setMaximumIterations(50)         loop_closure.cpp:10 */
+    double rot_eps;         /* 0 => PCL default 1 - trans_eps                        */
+    double score_threshold; /* icp_score_threshold (config.yaml:16)                   */
+    float cell_size;        /* target grid cell [m]; 0 => 1.0                        */
+    int device;
+} lio_icp_params;
+
+typedef struct lio_icp_result {  /* RegistrationOutput (loop_closure.h:21-27) + diagnostics */
+    int is_valid;
+    int is_converged;
+    double score;          /* getFitnessScore()                         */
+    float T[16];           /* getFinalTransformation(), row-major        */
+    int iterations;
+    int state;             /* convergence state: 0 none, 1 iter, 2 transform, 3 abs mse, 4 rel mse, 5 no corr */
+    double last_mse;
+    int64_t last_corr;
+} lio_icp_result;
+
+/* Exchange hook for sharded ICP (one process per GPU): all-gather `n` doubles
+ * from every rank into recv (world*n, rank order).  NULL => single rank.   */
+typedef int (*lio_allgather_fn)(const double* send, int64_t n, double* recv, void* user);
+
+int lio_icp_create(const lio_icp_params* p, lio_icp** out);
+int lio_icp_destroy(lio_icp* h);
+int lio_icp_set_target(lio_icp* h, const float* xyz, int64_t n);         /* setInputTarget */
+int lio_icp_set_source(lio_icp* h, const float* xyz, int64_t n);         /* setInputSource */
+/* Shard the source's fixed 4096-point blocks over `world` ranks.          */
+int lio_icp_set_shard(lio_icp* h, int rank, int world, lio_allgather_fn fn, void* user);
+/* Host-only helpers of the sharded path (no device needed): the contiguous
+ * source range a rank owns (whole 4096-point records), and the rank-order
+ * combination of all-gathered records into the 17 Umeyama statistics
+ * [n, sum p(3), sum q(3), sum q p^T(9), sum d2].  recv = world slots of
+ * ceil(records/world)*20 doubles, as lio_allgather_fn delivers them.       */
+int lio_icp_shard_range(int64_t n_source, int rank, int world, int64_t* begin, int64_t* count);
+int lio_icp_combine(const double* recv, int64_t n_source, int world, double* out17);
+/* align(guess) + getFitnessScore() + is_valid decision (loop_closure.cpp:81-90).
+ * aligned_opt (n*3, this rank's shard only when sharded) may be NULL.      */
+int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* aligned_opt);
+/* One-shot form of the above (SURVEY §8b signature).                       */
+int icp_align(const float* src_xyz, int64_t ns, const float* dst_xyz, int64_t nd, const lio_icp_params* p,
+              float* T_out, double* fitness, int* converged, int* iters, float* aligned_xyz_opt);
+
+/* ----------------------------------------------------------------- timing */
+typedef struct lio_kernel_timing {
+    int64_t knn_launches;   double knn_ms;     /* fused kNN + plane + H + reduce kernel */
+    int64_t reuse_launches; double reuse_ms;   /* converge=false re-evaluation kernel   */
+    int64_t final_launches; double final_ms;   /* block-partial finalize kernel          */
+    int64_t icp_launches;   double icp_ms;     /* ICP correspondence + statistics kernel */
+} lio_kernel_timing;
+
+/* When enabled, HIP events bracket every hot-kernel launch on the handle's
+ * stream and their elapsed times accumulate here.                          */
+int lio_ctx_set_timing(lio_ctx* c, int enable);
+int lio_ctx_get_timing(lio_ctx* c, lio_kernel_timing* out);
+int lio_ctx_reset_timing(lio_ctx* c);
+int lio_icp_set_timing(lio_icp* h, int enable);
+int lio_icp_get_timing(lio_icp* h, lio_kernel_timing* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LIO_GPU_H */

@@ -1,0 +1,178 @@
+"""ctypes binding of the CPU oracle (oracle/lio_oracle.cpp).
+
+Test infrastructure only: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg as the CHECKER / timed CPU baseline — never by the
+product package.  Parity against the real reference is unpinned (see the
+oracle header and DESIGN.md §Oracle).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB_PATH = os.path.join(ORACLE_DIR, "build", "liblio_oracle.so")
+
+_lib = None
+
+
+class MatchParams(C.Structure):
+    _fields_ = [("knn_range_sq", C.c_float), ("plane_thr", C.c_float),
+                ("s_coef", C.c_double), ("s_gate", C.c_double)]
+
+
+class State(C.Structure):
+    _fields_ = [("pos", C.c_double * 3), ("rot", C.c_double * 4), ("offset_R_L_I", C.c_double * 4),
+                ("offset_T_L_I", C.c_double * 3), ("vel", C.c_double * 3), ("bg", C.c_double * 3),
+                ("ba", C.c_double * 3), ("grav", C.c_double * 3)]
+
+
+class IcpParams(C.Structure):
+    _fields_ = [("max_corr_dist", C.c_double), ("trans_eps", C.c_double), ("fitness_eps", C.c_double),
+                ("max_iter", C.c_int), ("rot_eps", C.c_double), ("score_threshold", C.c_double)]
+
+
+def default_match_params():
+    return MatchParams(5.0, 0.1, 0.9, 0.9)
+
+
+def default_icp_params():
+    # loop_closure.cpp:7-10, fast_lio_sam.cpp:73 (1.5 * 35 m), config.yaml:16
+    return IcpParams(52.5, 0.01, 0.01, 50, 0.0, 1.5)
+
+
+def _p(a, t):
+    return a.ctypes.data_as(C.POINTER(t))
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = C.CDLL(LIB_PATH)
+        L.orc_map_build.restype = C.c_void_p
+        L.orc_map_build.argtypes = [C.POINTER(C.c_float), C.c_int64]
+        L.orc_map_free.argtypes = [C.c_void_p]
+        L.orc_map_knn.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.c_int64, C.c_int, C.c_float,
+                                  C.POINTER(C.c_int32), C.POINTER(C.c_float), C.c_int]
+        L.orc_esti_plane.argtypes = [C.POINTER(C.c_float), C.c_float, C.POINTER(C.c_float)]
+        L.orc_body_to_world.argtypes = [C.POINTER(C.c_double), C.POINTER(C.c_float), C.c_int64,
+                                        C.POINTER(C.c_float)]
+        L.orc_h_share_model.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.c_int64, C.POINTER(C.c_double),
+                                        C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_uint8),
+                                        C.POINTER(C.c_float), C.POINTER(MatchParams), C.POINTER(C.c_double),
+                                        C.c_int]
+        L.orc_ieskf_update.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.c_int64, C.POINTER(State),
+                                       C.POINTER(C.c_double), C.POINTER(MatchParams), C.c_double, C.c_int,
+                                       C.c_double, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+        L.orc_icp_align.argtypes = [C.POINTER(C.c_float), C.c_int64, C.POINTER(C.c_float), C.c_int64,
+                                    C.POINTER(IcpParams), C.POINTER(C.c_float), C.POINTER(C.c_float),
+                                    C.POINTER(C.c_double), C.POINTER(C.c_float), C.POINTER(C.c_double),
+                                    C.c_int, C.c_int]
+        _lib = L
+    return _lib
+
+
+class OracleMap:
+    """Static kd-tree with ikd-Tree Nearest_Search result semantics."""
+
+    def __init__(self, xyz: np.ndarray):
+        self.xyz = np.ascontiguousarray(xyz, dtype=np.float32)
+        self.h = lib().orc_map_build(_p(self.xyz, C.c_float), len(self.xyz))
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.orc_map_free(self.h)
+            self.h = None
+
+    def knn(self, q, k=5, range_sq=5.0, threads=8):
+        q = np.ascontiguousarray(q, dtype=np.float32)
+        idx = np.empty((len(q), k), np.int32)
+        d2 = np.empty((len(q), k), np.float32)
+        rc = lib().orc_map_knn(self.h, _p(q, C.c_float), len(q), k, C.c_float(range_sq), _p(idx, C.c_int32),
+                               _p(d2, C.c_float), threads)
+        assert rc == 0
+        return idx, d2
+
+
+def esti_plane(pts5x3, thr=0.1):
+    p = np.ascontiguousarray(pts5x3, dtype=np.float32).reshape(15)
+    out = np.empty(4, np.float32)
+    ok = lib().orc_esti_plane(_p(p, C.c_float), C.c_float(thr), _p(out, C.c_float))
+    return bool(ok), out
+
+
+def body_to_world(pose24, body):
+    pose24 = np.ascontiguousarray(pose24, dtype=np.float64)
+    body = np.ascontiguousarray(body, dtype=np.float32)
+    out = np.empty_like(body)
+    lib().orc_body_to_world(_p(pose24, C.c_double), _p(body, C.c_float), len(body), _p(out, C.c_float))
+    return out
+
+
+def h_share_model(omap: OracleMap, body, pose24, redo_knn, nn_idx, sel, planes, mp=None, threads=8):
+    """One h-evaluation; nn_idx/sel/planes are updated in place. Returns sums[32]."""
+    mp = mp or default_match_params()
+    body = np.ascontiguousarray(body, dtype=np.float32)
+    pose24 = np.ascontiguousarray(pose24, dtype=np.float64)
+    sums = np.zeros(32, np.float64)
+    rc = lib().orc_h_share_model(omap.h, _p(body, C.c_float), len(body), _p(pose24, C.c_double), int(redo_knn),
+                                 _p(nn_idx, C.c_int32), _p(sel, C.c_uint8), _p(planes, C.c_float),
+                                 C.byref(mp), _p(sums, C.c_double), threads)
+    assert rc == 0
+    return sums
+
+
+def state_to_c(st: dict) -> State:
+    s = State()
+    for k in ("pos", "rot", "offset_R_L_I", "offset_T_L_I", "vel", "bg", "ba", "grav"):
+        arr = getattr(s, k)
+        for i, v in enumerate(st[k]):
+            arr[i] = float(v)
+    return s
+
+
+def state_from_c(s: State) -> dict:
+    return {k: np.array(list(getattr(s, k))) for k, _ in State._fields_}
+
+
+def ieskf_update(omap: OracleMap, body, state: dict, P, mp=None, R=0.001, max_iter=3, limit=0.001, threads=8):
+    mp = mp or default_match_params()
+    body = np.ascontiguousarray(body, dtype=np.float32)
+    s = state_to_c(state)
+    Pc = np.ascontiguousarray(P, dtype=np.float64).copy()
+    stats = np.zeros(8)
+    trace = np.zeros(8 * 8)
+    rc = lib().orc_ieskf_update(omap.h, _p(body, C.c_float), len(body), C.byref(s), _p(Pc, C.c_double),
+                                C.byref(mp), R, max_iter, limit, threads, _p(stats, C.c_double),
+                                _p(trace, C.c_double))
+    assert rc == 0
+    return state_from_c(s), Pc, stats, trace.reshape(8, 8)
+
+
+def icp_align(src, dst, params=None, guess=None, threads=8, max_trace=64, want_aligned=False):
+    params = params or default_icp_params()
+    src = np.ascontiguousarray(src, dtype=np.float32)
+    dst = np.ascontiguousarray(dst, dtype=np.float32)
+    g = np.ascontiguousarray(np.eye(4, dtype=np.float32) if guess is None else guess, dtype=np.float32)
+    T = np.zeros(16, np.float32)
+    out = np.zeros(8)
+    trace = np.zeros(20 * max_trace)
+    aligned = np.empty_like(src) if want_aligned else None
+    rc = lib().orc_icp_align(_p(src, C.c_float), len(src), _p(dst, C.c_float), len(dst), C.byref(params),
+                             _p(g, C.c_float), _p(T, C.c_float), _p(out, C.c_double),
+                             _p(aligned, C.c_float) if want_aligned else None, _p(trace, C.c_double),
+                             max_trace, threads)
+    assert rc == 0
+    it = int(out[2])
+    return dict(T=T.reshape(4, 4), fitness=out[0], converged=bool(out[1]), iterations=it, state=int(out[3]),
+                is_valid=bool(out[4]), trace=trace.reshape(max_trace, 20)[:it], aligned=aligned)
