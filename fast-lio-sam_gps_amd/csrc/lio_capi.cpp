@@ -10,6 +10,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <string>
@@ -93,6 +94,7 @@ struct lio_ctx {
     int64_t rows_cap = 0;
     int64_t* d_nrows = nullptr;
     lio_pose last_pose{};
+    int knn_mode = 0;  // LIO_KNN_MODE=group selects the 8-lane kernel (A/B diagnostics)
     bool have_eval = false;
     bool knn_valid = false;
     // timing
@@ -210,6 +212,7 @@ int lio_ctx_create(lio_map* m, const lio_match_params* p, lio_ctx** out) {
     HIP_TRY(hipSetDevice(m->dev));
     auto* c = new lio_ctx();
     c->map = m;
+    if (const char* e = std::getenv("LIO_KNN_MODE")) c->knn_mode = std::strcmp(e, "group") == 0 ? 1 : 0;
     if (p)
         c->p = *p;
     else
@@ -303,6 +306,8 @@ static lio::MatchArgs make_args(lio_ctx* c, const lio_pose& pose) {
     a.n = (int)c->n;
     // every point with d2 <= range lies within ceil(sqrt(range)/cell)+1 shells
     a.max_shell = (int)std::ceil(std::sqrt((double)c->p.knn_range_sq) / a.grid.cell) + 1;
+    a.dbg = nullptr;
+    a.knn_mode = c->knn_mode;
     a.range_sq = c->p.knn_range_sq;
     a.plane_thr = c->p.plane_thr;
     a.s_coef = c->p.s_coef;
@@ -352,6 +357,30 @@ int lio_match(lio_ctx* c, const lio_pose* pose, int redo_knn, double* sums) {
     c->last_pose = *pose;
     c->have_eval = true;
     if (redo_knn) c->knn_valid = true;
+    return LIO_OK;
+}
+
+int lio_ctx_knn_stats(lio_ctx* c, const lio_pose* pose, double* sums, int32_t* stats3) {
+    if (!c || !pose || !sums || !stats3) return fail(LIO_ERR_ARG, "lio_ctx_knn_stats: bad arguments");
+    if (c->map->n == 0) return fail(LIO_ERR_STATE, "lio_ctx_knn_stats: map is empty");
+    HIP_TRY(hipSetDevice(c->map->dev));
+    hipStream_t st = c->map->st;
+    if (c->n == 0) return LIO_OK;
+    int* d_dbg = nullptr;
+    HIP_TRY(hipMalloc(&d_dbg, c->n * 3 * sizeof(int)));
+    lio::MatchArgs a = make_args(c, *pose);
+    a.dbg = d_dbg;
+    const int nb = lio::launch_h_model(a, true, st);
+    lio::launch_finalize(c->d_partials, nb, c->d_sums, st);
+    hipError_t e1 = hipMemcpyAsync(c->h_sums, c->d_sums, 32 * sizeof(double), hipMemcpyDeviceToHost, st);
+    hipError_t e2 = hipMemcpyAsync(stats3, d_dbg, c->n * 3 * sizeof(int), hipMemcpyDeviceToHost, st);
+    hipError_t e3 = hipStreamSynchronize(st);
+    (void)hipFree(d_dbg);
+    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) return fail(LIO_ERR_HIP, "lio_ctx_knn_stats failed");
+    std::memcpy(sums, c->h_sums, LIO_SUMS_LEN * sizeof(double));
+    c->last_pose = *pose;
+    c->have_eval = true;
+    c->knn_valid = true;
     return LIO_OK;
 }
 

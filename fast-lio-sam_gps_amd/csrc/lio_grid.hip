@@ -43,12 +43,36 @@ __global__ void aabb_partial_kernel(const float* __restrict__ xyz, int64_t n, fl
     if (threadIdx.x < 6) part[blockIdx.x * 6 + threadIdx.x] = s[threadIdx.x][0];
 }
 
-__global__ void aabb_final_kernel(const float* __restrict__ part, int nb, float* __restrict__ out) {
-    if (threadIdx.x >= 6) return;
-    const int d = threadIdx.x;
-    float v = d < 3 ? INFINITY : -INFINITY;
-    for (int b = 0; b < nb; ++b) v = d < 3 ? fminf(v, part[b * 6 + d]) : fmaxf(v, part[b * 6 + d]);
-    out[d] = v;
+// min/max over the block partials: 256 threads stride the partials, then an
+// LDS tree (min/max are order-independent, so this is exact)
+__global__ void __launch_bounds__(256) aabb_final_kernel(const float* __restrict__ part, int nb,
+                                                         float* __restrict__ out) {
+    __shared__ float s[6][256];
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int b = threadIdx.x; b < nb; b += 256) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            lo[d] = fminf(lo[d], part[b * 6 + d]);
+            hi[d] = fmaxf(hi[d], part[b * 6 + 3 + d]);
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        s[d][threadIdx.x] = lo[d];
+        s[3 + d][threadIdx.x] = hi[d];
+    }
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                s[d][threadIdx.x] = fminf(s[d][threadIdx.x], s[d][threadIdx.x + w]);
+                s[3 + d][threadIdx.x] = fmaxf(s[3 + d][threadIdx.x], s[3 + d][threadIdx.x + w]);
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 6) out[threadIdx.x] = s[threadIdx.x][0];
 }
 
 __global__ void cell_key_kernel(const float* __restrict__ xyz, int64_t n, GridGeom g, uint32_t* __restrict__ keys,
@@ -146,7 +170,7 @@ int grid_build(GridBuf& g, const float* d_xyz, int64_t n, float cell, hipStream_
     const int nbA = (int)std::min<int64_t>(1024, (n + 255) / 256);
     float* part = g.aabb + 8;
     aabb_partial_kernel<<<nbA, 256, 0, st>>>(d_xyz, n, part);
-    aabb_final_kernel<<<1, 64, 0, st>>>(part, nbA, g.aabb);
+    aabb_final_kernel<<<1, 256, 0, st>>>(part, nbA, g.aabb);
     HIPCHK(hipMemcpyAsync(g.aabb_host, g.aabb, 6 * sizeof(float), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
     const float* bb = g.aabb_host;

@@ -27,15 +27,16 @@ __device__ __forceinline__ void xform_pcl(const float* T, float x, float y, floa
     oz = T[8] * x + (T[9] * y + (T[10] * z + T[11]));
 }
 
+constexpr int kIcpGroup = 8;  // lanes cooperating on one query's 1-NN
+
+// 256 threads = 32 source points, 8 lanes per point.
 __global__ void __launch_bounds__(256) icp_near_kernel(IcpArgs a) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= a.n) return;
+    const int i = xcd_block(blockIdx.x, gridDim.x) * (256 / kIcpGroup) + threadIdx.x / kIcpGroup;
+    const int sub = threadIdx.x % kIcpGroup;
+    if (i >= a.n) return;  // whole groups leave together
     float x, y, z;
     if (a.fitness) {  // getFitnessScore: original source * final; kept in cur for `aligned_`
         xform_pcl(a.T, a.src[3 * i], a.src[3 * i + 1], a.src[3 * i + 2], x, y, z);
-        a.cur[3 * i] = x;
-        a.cur[3 * i + 1] = y;
-        a.cur[3 * i + 2] = z;
     } else {
         x = a.cur[3 * i];
         y = a.cur[3 * i + 1];
@@ -46,41 +47,45 @@ __global__ void __launch_bounds__(256) icp_near_kernel(IcpArgs a) {
             x = ox;
             y = oy;
             z = oz;
-            a.cur[3 * i] = x;
-            a.cur[3 * i + 1] = y;
-            a.cur[3 * i + 2] = z;
         }
     }
     TopK<1> tk;
     tk.init(INFINITY);
-    const bool done = grid_knn_exact<1>(a.grid, x, y, z, a.max_shell_near, tk);
-    a.far_d2[i] = tk.d[0];
-    a.far_id[i] = tk.id[0];
-    if (!done) {
-        const int slot = atomicAdd(a.far_count, 1);
-        a.far_list[slot] = i;
+    const bool done = group_knn_split<1, kIcpGroup>(a.grid, x, y, z, a.max_shell_near, sub, tk);
+    if (sub == 0) {
+        if (a.fitness || a.apply_T) {
+            a.cur[3 * i] = x;
+            a.cur[3 * i + 1] = y;
+            a.cur[3 * i + 2] = z;
+        }
+        a.far_d2[i] = tk.d[0];
+        a.far_id[i] = tk.id[0];
+        if (!done) {
+            const int slot = atomicAdd(a.far_count, 1);
+            a.far_list[slot] = i;
+        }
     }
 }
 
+// Unresolved points: unbounded shell walk seeded with the near result.
 __global__ void __launch_bounds__(256) icp_far_kernel(IcpArgs a) {
     const int cnt = *a.far_count;
-    for (int k = blockIdx.x * 256 + threadIdx.x; k < cnt; k += gridDim.x * 256) {
+    const int sub = threadIdx.x % kIcpGroup;
+    const int gpb = 256 / kIcpGroup;
+    for (int k = blockIdx.x * gpb + threadIdx.x / kIcpGroup; k < cnt; k += gridDim.x * gpb) {
         const int i = a.far_list[k];
-        float x, y, z;
-        if (a.fitness) {
-            xform_pcl(a.T, a.src[3 * i], a.src[3 * i + 1], a.src[3 * i + 2], x, y, z);
-        } else {
-            x = a.cur[3 * i];
-            y = a.cur[3 * i + 1];
-            z = a.cur[3 * i + 2];
-        }
+        const float x = a.cur[3 * i], y = a.cur[3 * i + 1], z = a.cur[3 * i + 2];
         TopK<1> tk;
         tk.init(INFINITY);
-        tk.d[0] = a.far_d2[i];
-        tk.id[0] = a.far_id[i];
-        grid_knn_exact<1>(a.grid, x, y, z, 0x3fffffff, tk);
-        a.far_d2[i] = tk.d[0];
-        a.far_id[i] = tk.id[0];
+        if (sub == 0) {  // the near pass's best is a valid starting bound (only lane 0 holds it)
+            tk.d[0] = a.far_d2[i];
+            tk.id[0] = a.far_id[i];
+        }
+        group_knn_exact<1, kIcpGroup>(a.grid, x, y, z, 0x3fffffff, sub, tk);
+        if (sub == 0) {
+            a.far_d2[i] = tk.d[0];
+            a.far_id[i] = tk.id[0];
+        }
     }
 }
 
@@ -147,7 +152,8 @@ __global__ void icp_reduce_kernel(const double* __restrict__ partials, int nchun
 
 void launch_icp_near(const IcpArgs& a, hipStream_t st) {
     if (a.n == 0) return;
-    icp_near_kernel<<<(a.n + 255) / 256, 256, 0, st>>>(a);
+    const int ppb = 256 / kIcpGroup;
+    icp_near_kernel<<<(a.n + ppb - 1) / ppb, 256, 0, st>>>(a);
 }
 void launch_icp_far(const IcpArgs& a, int max_far_blocks, hipStream_t st) {
     if (a.n == 0) return;

@@ -16,6 +16,8 @@ struct MatchArgs {
     float4* planes;           // n plane (a,b,c,d) cache
     uint8_t* sel;             // n point_selected_surf
     double* partials;         // nblocks*32
+    int* dbg;                 // optional n*3 search statistics (diagnostics only)
+    int knn_mode;             // 0: lane per point (default), 1: 8-lane groups
     int n;
     int max_shell;
     float range_sq;

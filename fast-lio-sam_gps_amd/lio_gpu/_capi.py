@@ -28,7 +28,7 @@ EXPORTS = [
     "lio_map_create", "lio_map_destroy", "lio_map_build", "lio_map_build_device", "lio_map_size",
     "lio_map_get_points", "lio_map_get_grid",
     "lio_ctx_create", "lio_ctx_destroy", "lio_scan_set", "lio_scan_set_device", "lio_match",
-    "lio_get_knn", "lio_get_planes", "lio_get_world", "lio_get_h_rows",
+    "lio_get_knn", "lio_get_planes", "lio_get_world", "lio_get_h_rows", "lio_ctx_knn_stats",
     "lio_ieskf_update",
     "lio_icp_create", "lio_icp_destroy", "lio_icp_set_target", "lio_icp_set_source", "lio_icp_set_shard",
     "lio_icp_align", "icp_align", "lio_icp_shard_range", "lio_icp_combine",
@@ -118,6 +118,7 @@ def _declare(L):
         "lio_get_planes": (C.c_int, [vp, fp, C.POINTER(C.c_uint8)]),
         "lio_get_world": (C.c_int, [vp, fp]),
         "lio_get_h_rows": (C.c_int, [vp, dp, C.c_int64, C.POINTER(C.c_int64)]),
+        "lio_ctx_knn_stats": (C.c_int, [vp, C.POINTER(Pose), dp, C.POINTER(C.c_int32)]),
         "lio_ieskf_update": (C.c_int, [vp, C.POINTER(State), dp, C.POINTER(IeskfParams), C.POINTER(IeskfStats)]),
         "lio_icp_create": (C.c_int, [C.POINTER(IcpParams), C.POINTER(vp)]),
         "lio_icp_destroy": (C.c_int, [vp]),

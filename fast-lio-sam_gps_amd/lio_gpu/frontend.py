@@ -164,6 +164,15 @@ class HShareModelGPU:
         check(lib().lio_get_h_rows(self._h, _dp(rows), max_rows, C.byref(nr)))
         return rows[: min(nr.value, max_rows)], nr.value
 
+    def knn_stats(self, pose):
+        """Diagnostics: a kNN evaluation returning per-point (cells, points, last shell)."""
+        if not isinstance(pose, _capi.Pose):
+            pose = pose_from_pose24(pose)
+        sums = np.zeros(_capi.LIO_SUMS_LEN)
+        st = np.zeros((self.n, 3), np.int32)
+        check(lib().lio_ctx_knn_stats(self._h, C.byref(pose), _dp(sums), st.ctypes.data_as(C.POINTER(C.c_int32))))
+        return sums, st
+
     # ---- timing (HIP events on the context's stream)
     def set_timing(self, on: bool):
         check(lib().lio_ctx_set_timing(self._h, 1 if on else 0))

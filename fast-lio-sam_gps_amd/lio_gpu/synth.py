@@ -363,9 +363,12 @@ def make_icp_pair(n_points: int = 500_000, seed: int = 4321, voxel: float = 0.3,
     rng = np.random.default_rng(seed)
     scene = make_scene(length, 1234)
 
+    # street window long enough to hold n_points occupied 0.3 m voxels (~2.1k per metre)
+    half = float(np.clip(0.5 * n_points / 1900.0 + 5.0, 10.0, 0.5 * length - 1.0))
+
     def submap(xc, s):
-        # dense surface sample in a 120 m window, PCL-VoxelGrid-style centroids
-        raw = sample_surface(scene, int(n_points * 3.2), seed=s, x_window=(xc - 60, xc + 60))
+        # dense surface sample in the window, PCL-VoxelGrid-style centroids
+        raw = sample_surface(scene, int(n_points * 3.2), seed=s, x_window=(xc - half, xc + half))
         ijk = np.floor(raw.astype(np.float64) / voxel).astype(np.int64)
         ijk -= ijk.min(axis=0)
         dims = ijk.max(axis=0) + 1
@@ -379,7 +382,8 @@ def make_icp_pair(n_points: int = 500_000, seed: int = 4321, voxel: float = 0.3,
             cen = cen[keep]
         return np.ascontiguousarray(cen)
 
-    src = submap(-10.0, seed)
+    # same 120 m stretch of street, independent surface samples / voxelizations
+    src = submap(0.0, seed)
     tgt = submap(0.0, seed + 1)
     ang = np.deg2rad(disp[1])
     axis = rng.normal(size=3)

@@ -119,6 +119,10 @@ int lio_get_world(lio_ctx* c, float* world);
 /* ekfom_data.h_x rows (6 non-zero columns) + h of the selected points, in
  * point order, for the dof < 23 branch of the IESKF: rows = 7 doubles each. */
 int lio_get_h_rows(lio_ctx* c, double* rows, int64_t max_rows, int64_t* n_rows);
+/* Diagnostics: one kNN evaluation (same results as lio_match(redo_knn=1))
+ * that also reports, per point, {cells scanned, map points scanned, last
+ * shell visited} (stats3: n*3 int32).                                     */
+int lio_ctx_knn_stats(lio_ctx* c, const lio_pose* pose, double* sums, int32_t* stats3);
 
 /* ------------------------------------------------------------------ IESKF */
 typedef struct lio_state { /* state_ikfom [U], quaternions are (w, x, y, z) */

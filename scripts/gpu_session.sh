@@ -1,0 +1,43 @@
+#!/bin/bash
+# GPU-box session: parity tests, smoke, bench, rocprof.  Each GPU step has its
+# own time limit; any fault / abort / timeout (exit status other than 0 or 1)
+# ends the session immediately — nothing else touches the GPU after it.
+# usage: scripts/gpu_session.sh <tag> [steps...]   steps: test smoke bench prof pmc
+set -u
+TAG=${1:-r01}; shift || true
+STEPS=${*:-"test smoke bench prof"}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+echo "host: $(nproc) cpus; $(grep -m1 'model name' /proc/cpuinfo)" | tee "$OUT/host.txt"
+
+run() {  # run <name> <seconds> <cmd...>
+    local name=$1 secs=$2; shift 2
+    echo "== $name ($(date +%T))"
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "== $name rc=$rc"
+    tail -n 25 "$OUT/$name.log"
+    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then
+        echo "!! $name ended with rc=$rc: stopping the session (no further GPU work)"
+        exit $rc
+    fi
+    return 0
+}
+
+for s in $STEPS; do
+    case $s in
+    test)  run pytest_gpu 900 python -m pytest tests -q -m gpu -p no:cacheprovider ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) run bench 600 python bench.py --steps 200 --warmup 20 ;;
+    quick) run bench_quick 400 python bench.py --steps 60 --warmup 5 --icp-reps 2 --cpu-seconds 5 ;;
+    prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
+               -- python bench.py --steps 100 --warmup 10 --no-cpu --icp-reps 3 ;;
+    pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv \
+               -- python bench.py --steps 30 --warmup 3 --no-cpu --no-icp &&
+           run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv \
+               -- python bench.py --steps 30 --warmup 3 --no-cpu --no-icp ;;
+    *) echo "unknown step $s" ;;
+    esac
+done
+echo "session done"
