@@ -1,0 +1,88 @@
+"""Generate the committed golden fixtures in tests/golden/*.npz.
+
+The reference ships no golden vectors for this path, so
+these are produced by the CPU restatement (oracle/lio_oracle.cpp) on small
+seeded synthetic inputs, and stored with their inputs so the tests do not
+depend on the generator's stability.  They pin the oracle against
+regressions (tests/test_golden.py) and give the GPU tests fixed vectors.
+Parity with the real reference remains unpinned.
+
+    python tests/golden/make_golden.py
+"""
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "fast-lio-sam_gps_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import numpy as np  # noqa: E402
+
+import oracle_py as O  # noqa: E402
+from lio_gpu import synth  # noqa: E402
+
+
+def main():
+    rng = np.random.default_rng(20251226)
+    # ---- front end: small C1-like scene
+    scene, m, scans = synth.make_config("C1", n_scans=1, map_points=20_000, scan_points=2048)
+    sc = scans[0]
+    st = synth.initial_state(sc.pos_init, sc.rot_init)
+    p24 = synth.pose24(st)
+    om = O.OracleMap(m)
+    world = O.body_to_world(p24, sc.body)
+    idx, d2 = om.knn(world, 5, 5.0, threads=1)
+    n = len(sc.body)
+    nn = np.full((n, 5), -1, np.int32)
+    sel = np.zeros(n, np.uint8)
+    planes = np.zeros((n, 4), np.float32)
+    sums1 = O.h_share_model(om, sc.body, p24, True, nn, sel, planes, threads=1)
+    sel1, planes1, nn1 = sel.copy(), planes.copy(), nn.copy()
+    st2 = dict(st)
+    st2["pos"] = st["pos"] + np.array([0.02, -0.01, 0.005])
+    st2["rot"] = synth.quat_mul(st["rot"], synth.rotvec_to_quat([0.001, -0.002, 0.003]))
+    p24b = synth.pose24(st2)
+    sums2 = O.h_share_model(om, sc.body, p24b, False, nn, sel, planes, threads=1)
+    P0 = synth.initial_cov()
+    x, P, stats, trace = O.ieskf_update(om, sc.body, st, P0, threads=1)
+    np.savez_compressed(
+        os.path.join(HERE, "frontend_small.npz"),
+        map=m, body=sc.body, pose24=p24, pose24_b=p24b, world=world, knn_idx=idx, knn_d2=d2,
+        nn_idx=nn1, sel=sel1, planes=planes1, sums=sums1, sel_b=sel, planes_b=planes, sums_b=sums2,
+        x0=np.concatenate([np.asarray(st[k], float) for k, _ in O.State._fields_]),
+        P0=P0, x1=np.concatenate([np.asarray(x[k], float) for k, _ in O.State._fields_]), P1=P,
+        ieskf_stats=stats[:5])
+    # ---- esti_plane: random near-planar and non-planar 5-point sets
+    sets = []
+    for t in range(256):
+        nrm = rng.normal(size=3)
+        nrm /= np.linalg.norm(nrm)
+        base = rng.uniform(-40, 40, 3)
+        u = np.cross(nrm, [1, 0, 0] if abs(nrm[0]) < 0.9 else [0, 1, 0])
+        u /= np.linalg.norm(u)
+        v = np.cross(nrm, u)
+        P5 = base + rng.uniform(-0.6, 0.6, (5, 1)) * u + rng.uniform(-0.6, 0.6, (5, 1)) * v
+        P5 += rng.normal(0, 0.01 if t % 4 else 0.2, (5, 1)) * nrm
+        sets.append(P5.astype(np.float32))
+    sets = np.stack(sets)
+    outs = np.zeros((len(sets), 4), np.float32)
+    oks = np.zeros(len(sets), np.uint8)
+    for i, P5 in enumerate(sets):
+        ok, o = O.esti_plane(P5, 0.1)
+        outs[i] = o
+        oks[i] = ok
+    np.savez_compressed(os.path.join(HERE, "esti_plane.npz"), pts=sets, out=outs, ok=oks)
+    # ---- loop ICP: small pair
+    src, dst, T = synth.make_icp_pair(n_points=6000, seed=77)
+    r = O.icp_align(src, dst, threads=1, want_aligned=True)
+    np.savez_compressed(os.path.join(HERE, "icp_small.npz"), src=src, dst=dst, T_disp=T, T=r["T"],
+                        fitness=r["fitness"], iterations=r["iterations"], state=r["state"],
+                        converged=r["converged"], trace=r["trace"], aligned=r["aligned"])
+    for f in sorted(os.listdir(HERE)):
+        if f.endswith(".npz"):
+            print(f, os.path.getsize(os.path.join(HERE, f)), "bytes")
+
+
+if __name__ == "__main__":
+    main()
