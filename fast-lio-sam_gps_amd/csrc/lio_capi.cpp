@@ -94,7 +94,10 @@ struct lio_ctx {
     int64_t rows_cap = 0;
     int64_t* d_nrows = nullptr;
     lio_pose last_pose{};
-    int knn_mode = 0;  // LIO_KNN_MODE=group selects the 8-lane kernel (A/B diagnostics)
+    int* d_far_list = nullptr;  // far-pass queue (cap), its length, and queued lists (cap*5)
+    int* d_far_count = nullptr;
+    float* d_far_d = nullptr;
+    int* d_far_id = nullptr;
     bool have_eval = false;
     bool knn_valid = false;
     // timing
@@ -212,14 +215,15 @@ int lio_ctx_create(lio_map* m, const lio_match_params* p, lio_ctx** out) {
     HIP_TRY(hipSetDevice(m->dev));
     auto* c = new lio_ctx();
     c->map = m;
-    if (const char* e = std::getenv("LIO_KNN_MODE")) c->knn_mode = std::strcmp(e, "group") == 0 ? 1 : 0;
     if (p)
         c->p = *p;
     else
         c->p = lio_match_params{5.0f, 0.1f, 0.9, 0.9};
     if (hipMalloc(&c->d_sums, 32 * sizeof(double)) != hipSuccess ||
         hipHostMalloc(&c->h_sums, 32 * sizeof(double)) != hipSuccess ||
-        hipMalloc(&c->d_nrows, sizeof(int64_t)) != hipSuccess) {
+        hipMalloc(&c->d_nrows, sizeof(int64_t)) != hipSuccess ||
+        hipMalloc(&c->d_far_count, sizeof(int)) != hipSuccess ||
+        hipMemset(c->d_far_count, 0, sizeof(int)) != hipSuccess) {
         delete c;
         return fail(LIO_ERR_NOMEM, "context allocation failed");
     }
@@ -235,7 +239,8 @@ int lio_ctx_destroy(lio_ctx* c) {
     if (!c) return LIO_OK;
     (void)hipSetDevice(c->map->dev);
     (void)hipStreamSynchronize(c->map->st);
-    void* ptrs[] = {c->d_body, c->d_nn, c->d_planes, c->d_sel, c->d_partials, c->d_sums, c->d_rows, c->d_nrows};
+    void* ptrs[] = {c->d_body,  c->d_nn,    c->d_planes,   c->d_sel,       c->d_partials, c->d_sums,
+                    c->d_rows,  c->d_nrows, c->d_far_list, c->d_far_count, c->d_far_d,    c->d_far_id};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (c->h_sums) (void)hipHostFree(c->h_sums);
@@ -250,17 +255,23 @@ int lio_ctx_destroy(lio_ctx* c) {
 static int ctx_reserve(lio_ctx* c, int64_t n) {
     if (n > c->cap || !c->d_body) {
         int64_t cap = std::max<int64_t>(n, c->cap + c->cap / 2);
-        void* ptrs[] = {c->d_body, c->d_nn, c->d_planes, c->d_sel};
+        void* ptrs[] = {c->d_body, c->d_nn, c->d_planes, c->d_sel, c->d_far_list, c->d_far_d, c->d_far_id};
         for (void* q : ptrs)
             if (q) (void)hipFree(q);
         c->d_body = nullptr;
         c->d_nn = nullptr;
         c->d_planes = nullptr;
         c->d_sel = nullptr;
+        c->d_far_list = nullptr;
+        c->d_far_d = nullptr;
+        c->d_far_id = nullptr;
         if (hipMalloc(&c->d_body, cap * 3 * sizeof(float)) != hipSuccess ||
             hipMalloc(&c->d_nn, cap * 5 * sizeof(int32_t)) != hipSuccess ||
             hipMalloc(&c->d_planes, cap * sizeof(float4)) != hipSuccess ||
-            hipMalloc(&c->d_sel, cap + 64) != hipSuccess)
+            hipMalloc(&c->d_sel, cap + 64) != hipSuccess ||
+            hipMalloc(&c->d_far_list, cap * sizeof(int)) != hipSuccess ||
+            hipMalloc(&c->d_far_d, cap * 5 * sizeof(float)) != hipSuccess ||
+            hipMalloc(&c->d_far_id, cap * 5 * sizeof(int)) != hipSuccess)
             return fail(LIO_ERR_NOMEM, "scan buffers: hipMalloc failed");
         c->cap = cap;
     }
@@ -307,7 +318,10 @@ static lio::MatchArgs make_args(lio_ctx* c, const lio_pose& pose) {
     // every point with d2 <= range lies within ceil(sqrt(range)/cell)+1 shells
     a.max_shell = (int)std::ceil(std::sqrt((double)c->p.knn_range_sq) / a.grid.cell) + 1;
     a.dbg = nullptr;
-    a.knn_mode = c->knn_mode;
+    a.far_list = c->d_far_list;
+    a.far_count = c->d_far_count;
+    a.far_d = c->d_far_d;
+    a.far_id = c->d_far_id;
     a.range_sq = c->p.knn_range_sq;
     a.plane_thr = c->p.plane_thr;
     a.s_coef = c->p.s_coef;

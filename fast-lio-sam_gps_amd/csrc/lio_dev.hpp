@@ -4,12 +4,15 @@
 //       pts[]   float4 (x, y, z, id-bits) sorted by linear cell index, id order
 //               inside a cell (16-B aligned: one global_load_dwordx4 per point)
 //       start[] u32 cell offsets, ncells+1 (count = start[c+1]-start[c])
-//   * grid_knn<K>: exact K nearest neighbours under the total order (d2, id),
+//   * exact K nearest neighbours under the total order (d2, id),
 //     d2 = float ((dx*dx + dy*dy) + dz*dz) (ikd-Tree calc_dist [U]), restricted
 //     to d2 <= bound.  Cells are visited shell by shell (Chebyshev rings around
-//     the query's cell), each cell/row pruned by its box distance against the
+//     the query's cell), each cell pruned by its box distance against the
 //     current K-th best, and the walk stops once the K-th best lies inside the
-//     radius the finished shells guarantee.
+//     radius the finished shells guarantee:
+//       group_knn_near  8 lanes per query, shells 0-1 (the common case)
+//       wave_knn_from   64 lanes per query, shells >= 2 (the sparse tail)
+//       group_knn_exact 8 lanes per query, any number of shells
 //   * esti_plane_dev: FAST-LIO esti_plane<float> [U] — Eigen ColPivHouseholderQR
 //     restated in registers, same float operation order as the oracle.
 //
@@ -62,36 +65,46 @@ __device__ __forceinline__ void body_to_world(const PoseArg& ps, float bx, float
     wz = (float)(((ps.R[6] * p0 + ps.R[7] * p1) + ps.R[8] * p2) + ps.t[2]);
 }
 
-// Sorted top-K list in registers.  Unfilled slots hold (bound, kNone) so the
-// acceptance test `lexless(d, id, d[K-1], id[K-1])` is exactly "d2 <= bound".
+// Sorted top-K list in registers.  Each entry is one 64-bit key
+// (float bits of d2) << 32 | id: d2 >= +0, so the float bits order like the
+// values and ONE unsigned compare is the (d2, id) total order of the
+// reference's tie-free kNN.  Unfilled slots hold (bound, kNone), so the
+// acceptance test `key < k[K-1]` is exactly "d2 <= bound".
+__device__ __forceinline__ uint64_t knn_key(float d, int id) {
+    return ((uint64_t)__float_as_uint(d) << 32) | (uint32_t)id;
+}
+
 template <int K>
 struct TopK {
-    float d[K];
-    int id[K];
+    uint64_t k[K];
     __device__ __forceinline__ void init(float bound) {
 #pragma unroll
-        for (int j = 0; j < K; ++j) {
-            d[j] = bound;
-            id[j] = kNone;
-        }
+        for (int j = 0; j < K; ++j) k[j] = knn_key(bound, kNone);
     }
+    __device__ __forceinline__ float d(int j) const { return __uint_as_float((uint32_t)(k[j] >> 32)); }
+    __device__ __forceinline__ int id(int j) const { return (int)(uint32_t)k[j]; }
+    __device__ __forceinline__ float worst() const { return d(K - 1); }
+    // insertion: entry j takes k[j-1] if x sorts before it, else x if x sorts
+    // before k[j] (old values throughout), one compare per slot
     __device__ __forceinline__ void push(float dc, int ic) {
-        if (!lexless(dc, ic, d[K - 1], id[K - 1])) return;
-        d[K - 1] = dc;
-        id[K - 1] = ic;
+        const uint64_t x = knn_key(dc, ic);
+        if (!(x < k[K - 1])) return;
+        bool c[K];
 #pragma unroll
-        for (int j = K - 1; j > 0; --j) {
-            if (lexless(d[j], id[j], d[j - 1], id[j - 1])) {
-                float td = d[j];
-                d[j] = d[j - 1];
-                d[j - 1] = td;
-                int ti = id[j];
-                id[j] = id[j - 1];
-                id[j - 1] = ti;
-            }
-        }
+        for (int j = 0; j < K - 1; ++j) c[j] = x < k[j];
+#pragma unroll
+        for (int j = K - 1; j > 0; --j) k[j] = c[j - 1] ? k[j - 1] : ((j == K - 1 || c[j]) ? x : k[j]);
+        if (K == 1 || c[0]) k[0] = x;
     }
-    __device__ __forceinline__ float worst() const { return d[K - 1]; }
+    // every slot := the K-th entry (a filler that is never re-inserted)
+    __device__ __forceinline__ void fill_with_worst() {
+#pragma unroll
+        for (int j = 0; j < K - 1; ++j) k[j] = k[K - 1];
+    }
+};
+
+struct SearchStats {  // diagnostics (lio_ctx_knn_stats), per lane
+    int cells, points, shell;
 };
 
 __device__ __forceinline__ int cell_coord(float v, float o, float inv) {
@@ -104,91 +117,6 @@ __device__ __forceinline__ int cell_coord(float v, float o, float inv) {
 __device__ __forceinline__ float axis_gap(float q, float lo, float hi) {
     float g = fmaxf(fmaxf(lo - q, q - hi), 0.f);
     return g * g;
-}
-
-// Scan the points of one cell into the top-K list.
-template <int K>
-__device__ __forceinline__ void scan_cell(const GridDev& g, uint32_t c, float qx, float qy, float qz,
-                                          TopK<K>& tk) {
-    uint32_t b = g.start[c];
-    uint32_t e = g.start[c + 1];
-    for (uint32_t j = b; j < e; ++j) {
-        float4 p = g.pts[j];
-        float d = sqdist3(qx, qy, qz, p.x, p.y, p.z);
-        tk.push(d, __float_as_int(p.w));
-    }
-}
-
-// Exact bounded K-NN.  Shells 0..max_shell around the query's cell (clipped to
-// the grid).  Returns true when the list is provably final: the K-th best lies
-// inside the radius the visited shells guarantee, or the whole grid was
-// visited.  false => cells beyond max_shell could still hold a better point.
-// Shell walk from shell s_first on (own = distance from q to its own cell's
-// faces, shrunk by the margin).
-template <int K>
-__device__ bool grid_knn_from(const GridDev& g, float qx, float qy, float qz, int cx, int cy, int cz, float own,
-                              int s_first, int max_shell, TopK<K>& tk) {
-    // first shell that can touch the grid at all
-    int s0 = s_first;
-    s0 = max(s0, max(-cx, cx - (g.nx - 1)));
-    s0 = max(s0, max(-cy, cy - (g.ny - 1)));
-    s0 = max(s0, max(-cz, cz - (g.nz - 1)));
-    int smax_grid = max(max(max(cx, g.nx - 1 - cx), max(cy, g.ny - 1 - cy)), max(cz, g.nz - 1 - cz));
-    const int smax = min(max_shell, smax_grid);
-    const float cs = g.cell, m = g.margin;
-    int s = s0;
-    for (; s <= smax; ++s) {
-        const int z0 = max(cz - s, 0), z1 = min(cz + s, g.nz - 1);
-        const int y0 = max(cy - s, 0), y1 = min(cy + s, g.ny - 1);
-        const int x0 = max(cx - s, 0), x1 = min(cx + s, g.nx - 1);
-        for (int z = z0; z <= z1; ++z) {
-            const float zl = g.oz + (float)z * cs - m;
-            const float gz = axis_gap(qz, zl, zl + cs + 2.f * m);
-            if (gz * 0.999999f > tk.worst()) continue;
-            const bool zb = (z == cz - s) || (z == cz + s);
-            for (int y = y0; y <= y1; ++y) {
-                const float yl = g.oy + (float)y * cs - m;
-                const float gyz = gz + axis_gap(qy, yl, yl + cs + 2.f * m);
-                if (gyz * 0.999999f > tk.worst()) continue;
-                const bool full = zb || (y == cy - s) || (y == cy + s);
-                const uint32_t rowbase = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx;
-                if (full) {
-                    for (int x = x0; x <= x1; ++x) {
-                        const float xl = g.ox + (float)x * cs - m;
-                        const float bd = gyz + axis_gap(qx, xl, xl + cs + 2.f * m);
-                        if (bd * 0.999999f > tk.worst()) continue;
-                        scan_cell<K>(g, rowbase + (uint32_t)x, qx, qy, qz, tk);
-                    }
-                } else {
-#pragma unroll
-                    for (int side = 0; side < 2; ++side) {
-                        const int x = side ? cx + s : cx - s;
-                        if (x < x0 || x > x1) continue;
-                        const float xl = g.ox + (float)x * cs - m;
-                        const float bd = gyz + axis_gap(qx, xl, xl + cs + 2.f * m);
-                        if (bd * 0.999999f > tk.worst()) continue;
-                        scan_cell<K>(g, rowbase + (uint32_t)x, qx, qy, qz, tk);
-                    }
-                }
-            }
-        }
-        // every unvisited cell is farther than the radius the shells <= s guarantee
-        const float gr = own + (float)s * cs;
-        if (gr > 0.f && tk.worst() < gr * gr * 0.999999f) return true;
-    }
-    return smax == smax_grid;
-}
-
-template <int K>
-__device__ bool grid_knn_exact(const GridDev& g, float qx, float qy, float qz, int max_shell, TopK<K>& tk) {
-    const int cx = cell_coord(qx, g.ox, g.inv_cell);
-    const int cy = cell_coord(qy, g.oy, g.inv_cell);
-    const int cz = cell_coord(qz, g.oz, g.inv_cell);
-    // distance from q to the faces of its own cell (shrunk by the margin)
-    const float lox = g.ox + (float)cx * g.cell, loy = g.oy + (float)cy * g.cell, loz = g.oz + (float)cz * g.cell;
-    float own = fminf(fminf(qx - lox, lox + g.cell - qx), fminf(qy - loy, loy + g.cell - qy));
-    own = fminf(own, fminf(qz - loz, loz + g.cell - qz)) - g.margin;
-    return grid_knn_from<K>(g, qx, qy, qz, cx, cy, cz, own, 0, max_shell, tk);
 }
 
 // ----------------------------------------------------------------------------
@@ -206,19 +134,44 @@ __device__ __forceinline__ float group_min(float v) {
     return v;
 }
 
+// Sort a bitonic (non-decreasing, then non-increasing) list in place.
+template <int K>
+__device__ __forceinline__ void cmpx(uint64_t (&v)[K], int i, int j) {
+    const uint64_t a = v[i], b = v[j];
+    const bool sw = b < a;
+    v[i] = sw ? b : a;
+    v[j] = sw ? a : b;
+}
+template <int K>
+__device__ __forceinline__ void sort_bitonic(uint64_t (&v)[K]) {
+    static_assert(K == 1 || K == 5, "sort_bitonic: K = 1 or 5");
+    if constexpr (K == 5) {  // 5 comparators suffice for bitonic inputs (0-1 principle)
+        cmpx(v, 0, 4);
+        cmpx(v, 1, 3);
+        cmpx(v, 1, 4);
+        cmpx(v, 2, 4);
+        cmpx(v, 3, 4);
+    }
+}
+
+// Butterfly merge over the G lanes of a group: per round the K smallest of
+// the two (disjoint) sorted lists are min(a[j], b[K-1-j]) — a bitonic
+// sequence — then sorted.  Afterwards every lane holds the group's top-K.
 template <int K, int G>
 __device__ __forceinline__ void group_merge(TopK<K>& tk) {
 #pragma unroll
     for (int off = 1; off < G; off <<= 1) {
-        float od[K];
-        int oi[K];
+        uint64_t c[K];
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            od[j] = __shfl_xor(tk.d[j], off, 64);
-            oi[j] = __shfl_xor(tk.id[j], off, 64);
+            const uint32_t lo = __shfl_xor((uint32_t)tk.k[K - 1 - j], off, 64);
+            const uint32_t hi = __shfl_xor((uint32_t)(tk.k[K - 1 - j] >> 32), off, 64);
+            const uint64_t b = ((uint64_t)hi << 32) | lo;
+            c[j] = b < tk.k[j] ? b : tk.k[j];
         }
+        sort_bitonic<K>(c);
 #pragma unroll
-        for (int j = 0; j < K; ++j) tk.push(od[j], oi[j]);
+        for (int j = 0; j < K; ++j) tk.k[j] = c[j];
     }
 }
 
@@ -233,17 +186,22 @@ __device__ __forceinline__ void scan_cell_group(const GridDev& g, uint32_t c, fl
     }
 }
 
-// Returns true when the merged list is provably final (see grid_knn_exact).
+// Returns true when the merged list is provably final: the K-th best lies
+// inside the radius the visited shells guarantee, or the whole grid was
+// visited; false => cells beyond max_shell could still hold a better point.
+// s_first > 0 resumes the walk (lists may already be merged across the group:
+// re-seeding is then needed before the first shell too, and is a no-op on
+// lists that are identical fillers).
 template <int K, int G>
-__device__ bool group_knn_exact(const GridDev& g, float qx, float qy, float qz, int max_shell, int sub,
-                                TopK<K>& tk) {
+__device__ bool group_knn_exact_from(const GridDev& g, float qx, float qy, float qz, int s_first, int max_shell,
+                                     int sub, TopK<K>& tk) {
     const int cx = cell_coord(qx, g.ox, g.inv_cell);
     const int cy = cell_coord(qy, g.oy, g.inv_cell);
     const int cz = cell_coord(qz, g.oz, g.inv_cell);
     const float lox = g.ox + (float)cx * g.cell, loy = g.oy + (float)cy * g.cell, loz = g.oz + (float)cz * g.cell;
     float own = fminf(fminf(qx - lox, lox + g.cell - qx), fminf(qy - loy, loy + g.cell - qy));
     own = fminf(own, fminf(qz - loz, loz + g.cell - qz)) - g.margin;
-    int s0 = 0;
+    int s0 = s_first;
     s0 = max(s0, max(-cx, cx - (g.nx - 1)));
     s0 = max(s0, max(-cy, cy - (g.ny - 1)));
     s0 = max(s0, max(-cz, cz - (g.nz - 1)));
@@ -253,16 +211,13 @@ __device__ bool group_knn_exact(const GridDev& g, float qx, float qy, float qz, 
     float bound = group_min<G>(tk.worst());  // group-uniform pruning bound
     bool done = false;
     for (int s = s0; s <= smax && !done; ++s) {
-        if (s > s0 && sub != 0) {
+        if (sub != 0) {
             // after the merge every lane holds the group list; keep it in lane 0
-            // only and re-seed the others with its K-th entry as filler: fillers
-            // are never re-inserted (push rejects equal keys), so the next merge
-            // sees each candidate once, and every lane prunes with the tight bound
-#pragma unroll
-            for (int j = 0; j < K - 1; ++j) {
-                tk.d[j] = tk.d[K - 1];
-                tk.id[j] = tk.id[K - 1];
-            }
+            // only and re-seed the others with its K-th entry f as filler: push
+            // accepts only keys < f, so every real candidate lives in exactly one
+            // lane, copies of f can only fill the tail of a merged list (lane 0
+            // holds K entries <= f), and every lane prunes with the tight bound
+                tk.fill_with_worst();
         }
         const int z0 = max(cz - s, 0), z1 = min(cz + s, g.nz - 1);
         const int y0 = max(cy - s, 0), y1 = min(cy + s, g.ny - 1);
@@ -297,6 +252,12 @@ __device__ bool group_knn_exact(const GridDev& g, float qx, float qy, float qz, 
     return done || smax == smax_grid;
 }
 
+template <int K, int G>
+__device__ bool group_knn_exact(const GridDev& g, float qx, float qy, float qz, int max_shell, int sub,
+                                TopK<K>& tk) {
+    return group_knn_exact_from<K, G>(g, qx, qy, qz, 0, max_shell, sub, tk);
+}
+
 // Scan one cell sequentially, four independent point loads in flight.
 template <int K>
 __device__ __forceinline__ void scan_cell_seq(const GridDev& g, uint32_t c, float qx, float qy, float qz,
@@ -314,55 +275,6 @@ __device__ __forceinline__ void scan_cell_seq(const GridDev& g, uint32_t c, floa
     for (; j < e; ++j) {
         const float4 p = g.pts[j];
         tk.push(sqdist3(qx, qy, qz, p.x, p.y, p.z), __float_as_int(p.w));
-    }
-}
-
-// Scan up to 4 cells (cl[u] == 0xffffffff: unused) as ONE concatenated range:
-// the 8 start[] loads issue together, then 8 point loads at a time, so a lane
-// pays ~2 dependent memory round trips instead of 2 per cell plus 1 per point.
-template <int K>
-__device__ __forceinline__ void scan_cells_flat4(const GridDev& g, const uint32_t cl[4], float qx, float qy, float qz,
-                                                 TopK<K>& tk) {
-    uint32_t b[4], n[4];
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-        const bool ok = cl[u] != 0xffffffffu;
-        const uint32_t c = ok ? cl[u] : 0u;
-        const uint32_t s0 = g.start[c], s1 = g.start[c + 1];
-        b[u] = s0;
-        n[u] = ok ? s1 - s0 : 0u;
-    }
-    const uint32_t p1 = n[0], p2 = p1 + n[1], p3 = p2 + n[2], tot = p3 + n[3];
-    for (uint32_t t = 0; t < tot; t += 8) {
-        float4 pp[8];
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const uint32_t tt = t + (uint32_t)u;
-            const uint32_t addr = tt < p1 ? b[0] + tt : (tt < p2 ? b[1] + (tt - p1) : (tt < p3 ? b[2] + (tt - p2) : b[3] + (tt - p3)));
-            pp[u] = tt < tot ? g.pts[addr] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (t + (uint32_t)u < tot) tk.push(sqdist3(qx, qy, qz, pp[u].x, pp[u].y, pp[u].z), __float_as_int(pp[u].w));
-    }
-}
-
-// Lane-strided scan of one cell by the whole group, 4 loads per lane in flight.
-template <int K, int G>
-__device__ __forceinline__ void scan_cell_group4(const GridDev& g, uint32_t c, float qx, float qy, float qz, int sub,
-                                                 TopK<K>& tk) {
-    const uint32_t b = g.start[c];
-    const uint32_t e = g.start[c + 1];
-    for (uint32_t j = b + (uint32_t)sub; j < e; j += 4 * G) {
-        float4 pp[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const uint32_t jj = j + (uint32_t)(u * G);
-            pp[u] = jj < e ? g.pts[jj] : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (j + (uint32_t)(u * G) < e) tk.push(sqdist3(qx, qy, qz, pp[u].x, pp[u].y, pp[u].z), __float_as_int(pp[u].w));
     }
 }
 
@@ -396,216 +308,155 @@ __device__ __forceinline__ void shell_offset(int s, int k, int& dx, int& dy, int
     }
 }
 
-// Split variant for short searches (front-end kNN, ICP near pass): shell 0
-// (the query's own cell) is scanned lane-strided by the whole group; for every
-// later shell the G lanes take disjoint subsets of the shell's cells, each
-// lane pruning and scanning its own cells (so the per-query cell enumeration
-// is not replicated G times).  Lists are merged after every shell, which keeps
-// the pruning bound exact and group-uniform.  Same result contract as
-// grid_knn_exact.
-struct SearchStats {  // diagnostics (lio_ctx_knn_stats), per lane
-    int cells, points, shell;
-};
-
+// Lean group walk for dense maps (front-end kNN, ICP near pass), written for
+// occupancy (no per-lane arrays): the own cell lane-strided by the whole group,
+// merge; then lane `sub` takes the shell-1 cells k = sub, sub+G, ... of the
+// 3x3x3 block, pruned against its own (tightening) K-th best and scanned
+// sequentially; merge.  Shells >= 2 (sparse neighbourhoods) continue with the
+// generic walk.  Same result contract as group_knn_exact_from.
 template <int K, int G>
-__device__ bool group_knn_split(const GridDev& g, float qx, float qy, float qz, int max_shell, int sub,
-                                TopK<K>& tk, SearchStats* dbg = nullptr) {
+__device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, int max_shell, int sub, TopK<K>& tk,
+                               SearchStats* dbg = nullptr) {
     const int cx = cell_coord(qx, g.ox, g.inv_cell);
     const int cy = cell_coord(qy, g.oy, g.inv_cell);
     const int cz = cell_coord(qz, g.oz, g.inv_cell);
-    const float lox = g.ox + (float)cx * g.cell, loy = g.oy + (float)cy * g.cell, loz = g.oz + (float)cz * g.cell;
-    float own = fminf(fminf(qx - lox, lox + g.cell - qx), fminf(qy - loy, loy + g.cell - qy));
-    own = fminf(own, fminf(qz - loz, loz + g.cell - qz)) - g.margin;
-    int s0 = 0;
+    const bool inside = (unsigned)cx < (unsigned)g.nx && (unsigned)cy < (unsigned)g.ny && (unsigned)cz < (unsigned)g.nz;
+    if (!inside || max_shell < 1) return group_knn_exact_from<K, G>(g, qx, qy, qz, 0, max_shell, sub, tk);
+    const float cs = g.cell, m = g.margin;
+    const float lox = g.ox + (float)cx * cs, loy = g.oy + (float)cy * cs, loz = g.oz + (float)cz * cs;
+    float own = fminf(fminf(qx - lox, lox + cs - qx), fminf(qy - loy, loy + cs - qy));
+    own = fminf(own, fminf(qz - loz, loz + cs - qz)) - m;
+    const uint32_t nx = (uint32_t)g.nx, nxy = (uint32_t)g.nx * (uint32_t)g.ny;
+    const uint32_t c0 = (uint32_t)cz * nxy + (uint32_t)cy * nx + (uint32_t)cx;
+    scan_cell_group<K, G>(g, c0, qx, qy, qz, sub, tk);
+    group_merge<K, G>(tk);
+    if (dbg) dbg->shell = 0;
+    if (own > 0.f && tk.worst() < own * own * 0.999999f) return true;
+    if (sub != 0) {  // re-seed non-leader lanes (see group_knn_exact_from)
+        tk.fill_with_worst();
+    }
+    for (int k = sub; k < 27; k += G) {
+        if (k == 13) continue;  // own cell
+        const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
+        const int x = cx + dx, y = cy + dy, z = cz + dz;
+        if ((unsigned)x >= nx || (unsigned)y >= (unsigned)g.ny || (unsigned)z >= (unsigned)g.nz) continue;
+        const float xl = lox + (float)dx * cs - m, yl = loy + (float)dy * cs - m, zl = loz + (float)dz * cs - m;
+        const float w = cs + 2.f * m;
+        const float bd = (axis_gap(qx, xl, xl + w) + axis_gap(qy, yl, yl + w)) + axis_gap(qz, zl, zl + w);
+        if (bd * 0.999999f > tk.worst()) continue;
+        const uint32_t c = (uint32_t)((int)c0 + dz * (int)nxy + dy * (int)nx + dx);
+        if (dbg) dbg->cells += 1;
+        scan_cell_seq<K>(g, c, qx, qy, qz, tk);
+    }
+    group_merge<K, G>(tk);
+    if (dbg) dbg->shell = 1;
+    const float gr = own + cs;
+    if (gr > 0.f && tk.worst() < gr * gr * 0.999999f) return true;
+    if (max_shell < 2) return false;
+    if (dbg) dbg->shell = 2;
+    return group_knn_exact_from<K, G>(g, qx, qy, qz, 2, max_shell, sub, tk);
+}
+
+// Far pass: one wave (64 lanes) per query resumes the walk at shell s_first
+// from the list an earlier pass left (identical in every lane, or held by
+// lane 0 with fillers elsewhere).  Lane l takes cells l, l+64, ... of each
+// shell (shell_offset order), prunes them against its own K-th best and scans
+// them sequentially; the wave merges after every shell.  Result in every lane;
+// same contract as group_knn_exact_from.
+template <int K>
+__device__ bool wave_knn_from(const GridDev& g, float qx, float qy, float qz, int s_first, int max_shell, int lane,
+                              TopK<K>& tk) {
+    const int cx = cell_coord(qx, g.ox, g.inv_cell);
+    const int cy = cell_coord(qy, g.oy, g.inv_cell);
+    const int cz = cell_coord(qz, g.oz, g.inv_cell);
+    const float cs = g.cell, m = g.margin, w = cs + 2.f * m;
+    const float lox = g.ox + (float)cx * cs, loy = g.oy + (float)cy * cs, loz = g.oz + (float)cz * cs;
+    float own = fminf(fminf(qx - lox, lox + cs - qx), fminf(qy - loy, loy + cs - qy));
+    own = fminf(own, fminf(qz - loz, loz + cs - qz)) - m;
+    int s0 = s_first;
     s0 = max(s0, max(-cx, cx - (g.nx - 1)));
     s0 = max(s0, max(-cy, cy - (g.ny - 1)));
     s0 = max(s0, max(-cz, cz - (g.nz - 1)));
     const int smax_grid = max(max(max(cx, g.nx - 1 - cx), max(cy, g.ny - 1 - cy)), max(cz, g.nz - 1 - cz));
     const int smax = min(max_shell, smax_grid);
-    const float cs = g.cell, m = g.margin;
-    float bound = group_min<G>(tk.worst());
     bool done = false;
     for (int s = s0; s <= smax && !done; ++s) {
-        if (s > s0 && sub != 0) {  // re-seed non-leader lanes (see group_knn_exact)
-#pragma unroll
-            for (int j = 0; j < K - 1; ++j) {
-                tk.d[j] = tk.d[K - 1];
-                tk.id[j] = tk.id[K - 1];
-            }
+        if (lane != 0) {  // keep the list in lane 0 only (see group_knn_exact_from)
+            tk.fill_with_worst();
         }
-        if (dbg) dbg->shell = s;
-        if (s == 0) {
-            const uint32_t c0 = ((uint32_t)cz * (uint32_t)g.ny + (uint32_t)cy) * (uint32_t)g.nx + (uint32_t)cx;
-            if (dbg && sub == 0) {
-                dbg->cells += 1;
-                dbg->points += (int)(g.start[c0 + 1] - g.start[c0]);
-            }
-            scan_cell_group4<K, G>(g, c0, qx, qy, qz, sub, tk);
-        } else {
-            const int ncell = 24 * s * s + 2;
-            for (int k0 = sub; k0 < ncell; k0 += 4 * G) {  // chunks of 4 cells per lane
-                uint32_t cl[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    cl[u] = 0xffffffffu;
-                    const int k = k0 + u * G;
-                    if (k >= ncell) continue;
-                    int dx, dy, dz;
-                    shell_offset(s, k, dx, dy, dz);
-                    const int x = cx + dx, y = cy + dy, z = cz + dz;
-                    if ((unsigned)x >= (unsigned)g.nx || (unsigned)y >= (unsigned)g.ny || (unsigned)z >= (unsigned)g.nz)
-                        continue;
-                    const float xl = g.ox + (float)x * cs - m, yl = g.oy + (float)y * cs - m,
-                                zl = g.oz + (float)z * cs - m;
-                    const float bd = axis_gap(qx, xl, xl + cs + 2.f * m) + axis_gap(qy, yl, yl + cs + 2.f * m) +
-                                     axis_gap(qz, zl, zl + cs + 2.f * m);
-                    if (bd * 0.999999f > fminf(bound, tk.worst())) continue;
-                    cl[u] = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
-                    if (dbg) {
-                        dbg->cells += 1;
-                        dbg->points += (int)(g.start[cl[u] + 1] - g.start[cl[u]]);
-                    }
-                }
-                scan_cells_flat4<K>(g, cl, qx, qy, qz, tk);
-            }
+        const int ncell = s == 0 ? 1 : 24 * s * s + 2;
+        for (int k = lane; k < ncell; k += 64) {
+            int dx = 0, dy = 0, dz = 0;
+            if (s > 0) shell_offset(s, k, dx, dy, dz);
+            const int x = cx + dx, y = cy + dy, z = cz + dz;
+            if ((unsigned)x >= (unsigned)g.nx || (unsigned)y >= (unsigned)g.ny || (unsigned)z >= (unsigned)g.nz)
+                continue;
+            const float xl = lox + (float)dx * cs - m, yl = loy + (float)dy * cs - m, zl = loz + (float)dz * cs - m;
+            const float bd = (axis_gap(qx, xl, xl + w) + axis_gap(qy, yl, yl + w)) + axis_gap(qz, zl, zl + w);
+            if (bd * 0.999999f > tk.worst()) continue;
+            scan_cell_seq<K>(g, ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x, qx, qy,
+                             qz, tk);
         }
-        group_merge<K, G>(tk);
-        bound = tk.worst();
+        group_merge<K, 64>(tk);
         const float gr = own + (float)s * cs;
-        if (gr > 0.f && bound < gr * gr * 0.999999f) done = true;
+        if (gr > 0.f && tk.worst() < gr * gr * 0.999999f) done = true;
     }
     return done || smax == smax_grid;
 }
 
-// ----------------------------------------------------------------------------
-// One lane = one query, built for memory-level parallelism rather than for
-// lanes cooperating on a query:
-//   1. own cell: one start[] pair, then its points 8 loads at a time;
-//   2. the 26 neighbours as 9 x-rows (dy, dz in {-1,0,1}): rows and their end
-//      cells are pruned against the own-cell bound WITHOUT memory access, the
-//      start[] values of all surviving rows are loaded in one batch, and the
-//      surviving row ranges (each contiguous in the cell-sorted point array;
-//      the centre row splits around the own cell => <= 10 ranges) are scanned
-//      as ONE flat stream, software pipelined: batch t+1's 8 loads are in
-//      flight while batch t is pushed;
-//   3. only if the radius guaranteed by shells 0-1 does not cover the K-th
-//      best (sparse maps) the generic shell walk continues from shell 2.
-// Exactness contract identical to grid_knn_exact.
-// ----------------------------------------------------------------------------
-constexpr int kFlatRanges = 10;
-
+// Far pass of the front-end kNN: one wave (64 lanes) per query.  The near
+// pass left the exact top-K over the 3x3x3 block around the query's cell
+// (merged: the same list in every lane); what remains are the cells of the
+// axis box [q - r, q + r], r = sqrt(K-th best) (+ margins), outside that
+// block.  Lane l takes box cells l, l+64, ..., prunes each against its own
+// K-th best and scans it sequentially; one wave merge.  Exact: every point
+// with d2 <= K-th best lies in the box, because the cell assignment of the
+// grid build (cell_coord, clamped) is monotone in each coordinate.
 template <int K>
-__device__ __forceinline__ void flat_stream_scan(const GridDev& g, const uint32_t (&b)[kFlatRanges],
-                                                 const uint32_t (&n)[kFlatRanges], float qx, float qy, float qz,
-                                                 TopK<K>& tk) {
-    uint32_t P[kFlatRanges];  // exclusive prefix of range lengths
-    uint32_t tot = 0;
-#pragma unroll
-    for (int k = 0; k < kFlatRanges; ++k) {
-        P[k] = tot;
-        tot += n[k];
-    }
-    auto addr_of = [&](uint32_t tt) {
-        uint32_t a = b[0] + tt;
-#pragma unroll
-        for (int k = 1; k < kFlatRanges; ++k)
-            if (n[k] != 0u && tt >= P[k]) a = b[k] + (tt - P[k]);
-        return a;
-    };
-    float4 cur[8], nxt[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) cur[u] = (uint32_t)u < tot ? g.pts[addr_of((uint32_t)u)] : make_float4(0, 0, 0, 0);
-    for (uint32_t t = 0; t < tot; t += 8) {
-#pragma unroll
-        for (int u = 0; u < 8; ++u) {
-            const uint32_t tt = t + 8u + (uint32_t)u;
-            nxt[u] = tt < tot ? g.pts[addr_of(tt)] : make_float4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int u = 0; u < 8; ++u)
-            if (t + (uint32_t)u < tot) tk.push(sqdist3(qx, qy, qz, cur[u].x, cur[u].y, cur[u].z), __float_as_int(cur[u].w));
-#pragma unroll
-        for (int u = 0; u < 8; ++u) cur[u] = nxt[u];
-    }
-}
-
-template <int K>
-__device__ bool lane_knn_exact(const GridDev& g, float qx, float qy, float qz, int max_shell, TopK<K>& tk) {
+__device__ void wave_knn_box(const GridDev& g, float qx, float qy, float qz, int lane, TopK<K>& tk) {
     const int cx = cell_coord(qx, g.ox, g.inv_cell);
     const int cy = cell_coord(qy, g.oy, g.inv_cell);
     const int cz = cell_coord(qz, g.oz, g.inv_cell);
-    const bool inside = (unsigned)cx < (unsigned)g.nx && (unsigned)cy < (unsigned)g.ny && (unsigned)cz < (unsigned)g.nz;
-    if (!inside || max_shell < 1) return grid_knn_exact<K>(g, qx, qy, qz, max_shell, tk);
-    const float cs = g.cell, m = g.margin;
-    const float lox = g.ox + (float)cx * cs, loy = g.oy + (float)cy * cs, loz = g.oz + (float)cz * cs;
-    float own = fminf(fminf(qx - lox, lox + cs - qx), fminf(qy - loy, loy + cs - qy));
-    own = fminf(own, fminf(qz - loz, loz + cs - qz)) - m;
-    const uint32_t nx = (uint32_t)g.nx, ny = (uint32_t)g.ny;
-    // ---- shell 0
-    {
-        uint32_t b[kFlatRanges], n[kFlatRanges];
-        const uint32_t c0 = ((uint32_t)cz * ny + (uint32_t)cy) * nx + (uint32_t)cx;
-        b[0] = g.start[c0];
-        n[0] = g.start[c0 + 1] - b[0];
-#pragma unroll
-        for (int k = 1; k < kFlatRanges; ++k) b[k] = n[k] = 0u;
-        flat_stream_scan<K>(g, b, n, qx, qy, qz, tk);
+    const float r = sqrtf(tk.worst()) + 2.f * g.margin;
+    const int x0 = max(cell_coord(qx - r, g.ox, g.inv_cell), 0), x1 = min(cell_coord(qx + r, g.ox, g.inv_cell), g.nx - 1);
+    const int y0 = max(cell_coord(qy - r, g.oy, g.inv_cell), 0), y1 = min(cell_coord(qy + r, g.oy, g.inv_cell), g.ny - 1);
+    const int z0 = max(cell_coord(qz - r, g.oz, g.inv_cell), 0), z1 = min(cell_coord(qz + r, g.oz, g.inv_cell), g.nz - 1);
+    if (x0 > x1 || y0 > y1 || z0 > z1) return;
+    if (lane != 0) {  // keep the list in lane 0 only (see group_knn_exact_from)
+        tk.fill_with_worst();
     }
-    if (own > 0.f && tk.worst() < own * own * 0.999999f) return true;
-    // ---- shell 1 as 9 x-rows; per-axis gaps of the neighbour slabs
-    const float gxl = axis_gap(qx, lox - cs - m, lox + m), gxh = axis_gap(qx, lox + cs - m, lox + 2.f * cs + m);
-    float gyv[3], gzv[3];
-    gyv[0] = axis_gap(qy, loy - cs - m, loy + m);
-    gyv[1] = 0.f;
-    gyv[2] = axis_gap(qy, loy + cs - m, loy + 2.f * cs + m);
-    gzv[0] = axis_gap(qz, loz - cs - m, loz + m);
-    gzv[1] = 0.f;
-    gzv[2] = axis_gap(qz, loz + cs - m, loz + 2.f * cs + m);
-    const float w = tk.worst();
-    const bool xl_ok = cx > 0, xh_ok = cx + 1 < g.nx;
-    uint32_t lo_i[kFlatRanges], hi_i[kFlatRanges];  // cell index ranges [lo, hi) to load
-    int r = 0;
-#pragma unroll
-    for (int dz = 0; dz < 3; ++dz) {
-#pragma unroll
-        for (int dy = 0; dy < 3; ++dy) {
-            const int z = cz + dz - 1, y = cy + dy - 1;
-            const float gyz = gzv[dz] + gyv[dy];
-            const bool row_ok = (unsigned)z < (unsigned)g.nz && (unsigned)y < (unsigned)g.ny && gyz * 0.999999f <= w;
-            const uint32_t rb = ((uint32_t)max(z, 0) * ny + (uint32_t)max(y, 0)) * nx;
-            const bool use_l = row_ok && xl_ok && (gyz + gxl) * 0.999999f <= w;
-            const bool use_h = row_ok && xh_ok && (gyz + gxh) * 0.999999f <= w;
-            if (dz == 1 && dy == 1) {  // centre row: the two side cells only
-                lo_i[r] = rb + (uint32_t)cx - 1u;
-                hi_i[r] = use_l ? rb + (uint32_t)cx : lo_i[r];
-                ++r;
-                lo_i[r] = rb + (uint32_t)cx + 1u;
-                hi_i[r] = use_h ? rb + (uint32_t)cx + 2u : lo_i[r];
-                ++r;
-            } else {
-                const bool use_c = row_ok;
-                const uint32_t a = rb + (uint32_t)cx - (use_l ? 1u : 0u);
-                const uint32_t e = rb + (uint32_t)cx + 1u + (use_h ? 1u : 0u);
-                lo_i[r] = use_c ? a : 0u;
-                hi_i[r] = use_c ? e : 0u;
-                ++r;
-            }
-        }
+    const float cs = g.cell, m = g.margin, w = cs + 2.f * m;
+    const int wx = x1 - x0 + 1, wxy = wx * (y1 - y0 + 1), nbox = wxy * (z1 - z0 + 1);
+    for (int k = lane; k < nbox; k += 64) {
+        const int z = z0 + k / wxy, kk = k % wxy;
+        const int y = y0 + kk / wx, x = x0 + kk % wx;
+        if (abs(x - cx) <= 1 && abs(y - cy) <= 1 && abs(z - cz) <= 1) continue;  // scanned by the near pass
+        const float xl = g.ox + (float)x * cs - m, yl = g.oy + (float)y * cs - m, zl = g.oz + (float)z * cs - m;
+        const float bd = (axis_gap(qx, xl, xl + w) + axis_gap(qy, yl, yl + w)) + axis_gap(qz, zl, zl + w);
+        if (bd * 0.999999f > tk.worst()) continue;
+        scan_cell_seq<K>(g, ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x, qx, qy, qz,
+                         tk);
     }
-    uint32_t b[kFlatRanges], n[kFlatRanges];
-#pragma unroll
-    for (int k = 0; k < kFlatRanges; ++k) {
-        const bool nz = hi_i[k] > lo_i[k];
-        const uint32_t s0 = nz ? g.start[lo_i[k]] : 0u;
-        const uint32_t s1 = nz ? g.start[hi_i[k]] : 0u;
-        b[k] = s0;
-        n[k] = s1 - s0;
-    }
-    flat_stream_scan<K>(g, b, n, qx, qy, qz, tk);
-    const float gr = own + cs;
-    if (gr > 0.f && tk.worst() < gr * gr * 0.999999f) return true;
-    if (max_shell < 2) return false;
-    return grid_knn_from<K>(g, qx, qy, qz, cx, cy, cz, own, 2, max_shell, tk);
+    group_merge<K, 64>(tk);
+}
+
+// Wave64 sum of a double with DPP row operations (no LDS round trips):
+// quad swaps, row_shr 4/8, row_bcast 15/31 leave the total in lane 63.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ double dpp_d(double v) {
+    const int lo = __double2loint(v), hi = __double2hiint(v);
+    const int rlo = __builtin_amdgcn_update_dpp(0, lo, CTRL, ROWMASK, 0xf, false);
+    const int rhi = __builtin_amdgcn_update_dpp(0, hi, CTRL, ROWMASK, 0xf, false);
+    return __hiloint2double(rhi, rlo);
+}
+__device__ __forceinline__ double wave_sum_to_lane63(double v) {
+    v += dpp_d<0xb1, 0xf>(v);   // quad_perm [1,0,3,2]
+    v += dpp_d<0x4e, 0xf>(v);   // quad_perm [2,3,0,1]
+    v += dpp_d<0x114, 0xf>(v);  // row_shr:4
+    v += dpp_d<0x118, 0xf>(v);  // row_shr:8
+    v += dpp_d<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+    v += dpp_d<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
+    return v;                   // lane 63 holds the wave total
 }
 
 // XCD-aware block order: the hardware deals blocks round-robin over the 8 XCDs

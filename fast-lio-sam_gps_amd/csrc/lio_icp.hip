@@ -51,15 +51,15 @@ __global__ void __launch_bounds__(256) icp_near_kernel(IcpArgs a) {
     }
     TopK<1> tk;
     tk.init(INFINITY);
-    const bool done = group_knn_split<1, kIcpGroup>(a.grid, x, y, z, a.max_shell_near, sub, tk);
+    const bool done = group_knn_near<1, kIcpGroup>(a.grid, x, y, z, a.max_shell_near, sub, tk);
     if (sub == 0) {
         if (a.fitness || a.apply_T) {
             a.cur[3 * i] = x;
             a.cur[3 * i + 1] = y;
             a.cur[3 * i + 2] = z;
         }
-        a.far_d2[i] = tk.d[0];
-        a.far_id[i] = tk.id[0];
+        a.far_d2[i] = tk.d(0);
+        a.far_id[i] = tk.id(0);
         if (!done) {
             const int slot = atomicAdd(a.far_count, 1);
             a.far_list[slot] = i;
@@ -78,13 +78,12 @@ __global__ void __launch_bounds__(256) icp_far_kernel(IcpArgs a) {
         TopK<1> tk;
         tk.init(INFINITY);
         if (sub == 0) {  // the near pass's best is a valid starting bound (only lane 0 holds it)
-            tk.d[0] = a.far_d2[i];
-            tk.id[0] = a.far_id[i];
+            tk.k[0] = knn_key(a.far_d2[i], a.far_id[i]);
         }
         group_knn_exact<1, kIcpGroup>(a.grid, x, y, z, 0x3fffffff, sub, tk);
         if (sub == 0) {
-            a.far_d2[i] = tk.d[0];
-            a.far_id[i] = tk.id[0];
+            a.far_d2[i] = tk.d(0);
+            a.far_id[i] = tk.id(0);
         }
     }
 }

@@ -17,7 +17,10 @@ struct MatchArgs {
     uint8_t* sel;             // n point_selected_surf
     double* partials;         // nblocks*32
     int* dbg;                 // optional n*3 search statistics (diagnostics only)
-    int knn_mode;             // 0: lane per point (default), 1: 8-lane groups
+    int* far_list;            // n: points queued for the far pass
+    int* far_count;           // queue length (reset to 0 by plane_kernel)
+    float* far_d;             // n*5 their near-pass lists
+    int* far_id;
     int n;
     int max_shell;
     float range_sq;

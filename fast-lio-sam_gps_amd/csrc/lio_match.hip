@@ -1,16 +1,18 @@
 // lio_match.hip — FAST-LIO h_share_model on gfx950.
 //
-// Two fused kernels per h-evaluation:
+// Per h-evaluation:
 //
-//   h_model_knn_kernel  (ekfom_data.converge == true), 512 threads = 64 points
-//     phase 1 (8 lanes per point): body->world (double, stored float) -> exact
-//       grid 5-NN, cell points scanned lane-strided (coalesced), private
-//       top-5 lists merged by a shuffle butterfly
-//     phase 2 (wave 0, lane = point): gate (found == 5 && d2[4] <= 5) ->
+//   ekfom_data.converge == true (redo the kNN):
+//     knn_near_kernel  512 threads = 64 points, 8 lanes per point:
+//       body->world (double, stored float) -> exact grid 5-NN over shells 0-1,
+//       cell points scanned lane-strided (coalesced), private top-5 lists
+//       merged by a shuffle butterfly; unresolved points -> far queue
+//     knn_far_kernel   one wave per queued point, the rest of its search box
+//     plane_kernel     lane = point: gate (found == 5 && d2[4] <= 5) ->
 //       esti_plane (QR, registers) -> pd2, s-gate -> H row (double) ->
-//       30-value wave reduction -> block partial
+//       30-value DPP wave reduction -> block partial
 //     writes: nn_idx[5] (20 B), plane abcd (16 B), sel (1 B)
-//   h_model_reuse_kernel (converge == false: reuse Nearest_Points), lane = point
+//   ekfom_data.converge == false: h_model_reuse_kernel, lane = point
 //     body->world -> cached plane -> pd2, s-gate -> H row -> block partial
 //   finalize_kernel: sums the block partials in a fixed order (deterministic)
 //
@@ -20,13 +22,16 @@
 #include "lio_kernels.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace lio {
 
 constexpr int kBlock = 256;
-constexpr int kNSum = 30;  // 21 HTH + 6 HTh + neff + res + hh (reduced in wave_reduce_store)
+
 constexpr int kGroup = 8;   // lanes cooperating on one query's kNN
 constexpr int kKnnBlock = 512;
+constexpr int kFarBlock = 256;
+constexpr int kFarBlocks = 256;  // 1024 waves stride the far queue
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -39,13 +44,13 @@ __device__ __forceinline__ double wave_sum(double v) {
 // Products are formed and reduced a few at a time so the 30 sums never need
 // 60 live VGPRs (the kernel's occupancy is set by its peak register count).
 __device__ __forceinline__ void wave_reduce_store(const double J[6], double h, double res, double cnt, double* dst) {
-    const bool l0 = (threadIdx.x & 63) == 0;
+    const bool l0 = (threadIdx.x & 63) == 63;  // DPP sums land in lane 63
     int q = 0;
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
 #pragma unroll
         for (int c = r; c < 6; ++c) {
-            const double v = wave_sum(J[r] * J[c]);
+            const double v = wave_sum_to_lane63(J[r] * J[c]);
             if (l0) dst[q] = v;
             ++q;
         }
@@ -53,11 +58,11 @@ __device__ __forceinline__ void wave_reduce_store(const double J[6], double h, d
     }
 #pragma unroll
     for (int r = 0; r < 6; ++r) {
-        const double v = wave_sum(J[r] * h);
+        const double v = wave_sum_to_lane63(J[r] * h);
         if (l0) dst[21 + r] = v;
     }
     __builtin_amdgcn_sched_barrier(0);
-    const double s0 = wave_sum(cnt), s1 = wave_sum(res), s2 = wave_sum(h * h);
+    const double s0 = wave_sum_to_lane63(cnt), s1 = wave_sum_to_lane63(res), s2 = wave_sum_to_lane63(h * h);
     if (l0) {
         dst[27] = s0;
         dst[28] = s1;
@@ -81,112 +86,105 @@ __device__ __forceinline__ bool residual_row(const MatchArgs& a, float bx, float
     return true;
 }
 
-// ekfom_data.converge == true: kNN + plane + H.  512 threads = 64 queries.
-//   phase 1: 8 lanes per query run the exact grid 5-NN cooperatively
-//   phase 2: wave 0, one lane per query: gate, esti_plane, s-gate, H row,
-//            wave reduction -> block partial
+// ekfom_data.converge == true, pass 1: 512 threads = 64 queries, 8 lanes per
+// query run the exact 5-NN over shells 0-1 cooperatively (group_knn_near).
+// Queries whose 5th neighbour is not yet provably final (sparse
+// neighbourhoods, ~0.4% of a dense scan) are queued, with their list, for
+// the wave-per-query far pass instead of holding their wave: a kernel runs as
+// long as its slowest wave.  Written for 8 waves/SIMD (<= 64 VGPRs).
 template <bool DBG>
-__global__ void __launch_bounds__(kKnnBlock) h_model_knn_kernel(MatchArgs a) {
+__global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) knn_near_kernel(MatchArgs a) {
     constexpr int QPB = kKnnBlock / kGroup;  // 64 queries per block
-    __shared__ int s_id[QPB][5];
-    __shared__ float s_w[QPB][3];
     const int blk = xcd_block(blockIdx.x, gridDim.x);
-    const int qloc = threadIdx.x / kGroup;
     const int sub = threadIdx.x % kGroup;
-    const int i = blk * QPB + qloc;
-    if (i < a.n) {
-        const float bx = a.body[3 * i], by = a.body[3 * i + 1], bz = a.body[3 * i + 2];
-        float wx, wy, wz;
-        body_to_world(a.pose, bx, by, bz, wx, wy, wz);
-        TopK<5> tk;
-        tk.init(a.range_sq);
-        SearchStats st{0, 0, 0};
-        group_knn_split<5, kGroup>(a.grid, wx, wy, wz, a.max_shell, sub, tk, DBG ? &st : nullptr);
-        if constexpr (DBG) {
+    const int i = blk * QPB + threadIdx.x / kGroup;
+    if (i >= a.n) return;
+    const float bx = a.body[3 * i], by = a.body[3 * i + 1], bz = a.body[3 * i + 2];
+    float wx, wy, wz;
+    body_to_world(a.pose, bx, by, bz, wx, wy, wz);
+    TopK<5> tk;
+    tk.init(a.range_sq);
+    SearchStats st{0, 0, 0};
+    const bool done = group_knn_near<5, kGroup>(a.grid, wx, wy, wz, min(a.max_shell, 1), sub, tk, DBG ? &st : nullptr);
+    const bool far = !done && a.max_shell > 1;
+    if constexpr (DBG) {
 #pragma unroll
-            for (int off = 1; off < kGroup; off <<= 1) {
-                st.cells += __shfl_xor(st.cells, off, 64);
-                st.points += __shfl_xor(st.points, off, 64);
-            }
-            if (sub == 0) {
-                a.dbg[3 * (size_t)i] = st.cells;
-                a.dbg[3 * (size_t)i + 1] = st.points;
-                a.dbg[3 * (size_t)i + 2] = st.shell;
-            }
-        }
-        if (sub < 5) {
-            int v = tk.id[0];
-#pragma unroll
-            for (int j = 1; j < 5; ++j)
-                if (sub == j) v = tk.id[j];
-            s_id[qloc][sub] = v;
-            a.nn_idx[5 * (size_t)i + sub] = v == kNone ? -1 : v;
+        for (int off = 1; off < kGroup; off <<= 1) {
+            st.cells += __shfl_xor(st.cells, off, 64);
+            st.points += __shfl_xor(st.points, off, 64);
         }
         if (sub == 0) {
-            s_w[qloc][0] = wx;
-            s_w[qloc][1] = wy;
-            s_w[qloc][2] = wz;
+            a.dbg[3 * (size_t)i] = st.cells;
+            a.dbg[3 * (size_t)i + 1] = st.points;
+            a.dbg[3 * (size_t)i + 2] = far ? 2 : st.shell;
         }
     }
-    __syncthreads();
-    if (threadIdx.x >= 64) return;
-    // ---- phase 2: lane = query
-    const int lane = threadIdx.x;
-    const int ip = blk * QPB + lane;
-    double J[6] = {0, 0, 0, 0, 0, 0};
-    double h = 0.0, res = 0.0, cnt = 0.0;
-    if (ip < a.n) {
-        // point_selected_surf = found == 5 && !(sqdist[4] > 5)   (d <= range by construction)
-        bool sel = s_id[lane][4] != kNone;
-        if (sel) {
-            float P[5][3];
+    if (far) {
+        if (sub == 0) {
+            const int slot = atomicAdd(a.far_count, 1);
+            a.far_list[slot] = i;
 #pragma unroll
             for (int j = 0; j < 5; ++j) {
-                const float4 q = a.map_by_id[s_id[lane][j]];
-                P[j][0] = q.x;
-                P[j][1] = q.y;
-                P[j][2] = q.z;
-            }
-            float abcd[4];
-            sel = esti_plane_dev(P, a.plane_thr, abcd);
-            const float4 pl = make_float4(abcd[0], abcd[1], abcd[2], abcd[3]);
-            a.planes[ip] = pl;
-            if (sel) {
-                sel = residual_row(a, a.body[3 * ip], a.body[3 * ip + 1], a.body[3 * ip + 2], s_w[lane][0],
-                                   s_w[lane][1], s_w[lane][2], pl, J, h, res);
-                cnt = sel ? 1.0 : 0.0;
+                a.far_d[5 * (size_t)slot + j] = tk.d(j);
+                a.far_id[5 * (size_t)slot + j] = tk.id(j);
             }
         }
-        a.sel[ip] = sel ? 1 : 0;
+        return;
     }
-    wave_reduce_store(J, h, res, cnt, a.partials + (size_t)blk * 32);
+    if (sub < 5) {
+        int v = tk.id(0);
+#pragma unroll
+        for (int j = 1; j < 5; ++j)
+            if (sub == j) v = tk.id(j);
+        a.nn_idx[5 * (size_t)i + sub] = v == kNone ? -1 : v;
+    }
 }
 
-// ekfom_data.converge == true, one lane per point (kNN with deep memory-level
-// parallelism, see lane_knn_exact), plane + H in the same lane, 4 wave
-// partials combined in LDS.  256 threads = 256 points.
-__global__ void __launch_bounds__(kBlock) h_model_knn_lane_kernel(MatchArgs a) {
+// Pass 2: the queued queries, one wave each (wave_knn_box).
+// Fixed grid; every wave strides the queue and exits once past its end.
+__global__ void __launch_bounds__(kFarBlock) knn_far_kernel(MatchArgs a) {
+    const int lane = threadIdx.x & 63;
+    const int nw = gridDim.x * (kFarBlock / 64);
+    const int cnt = *a.far_count;
+    for (int f = blockIdx.x * (kFarBlock / 64) + (threadIdx.x >> 6); f < cnt; f += nw) {
+        const int i = a.far_list[f];
+        float wx, wy, wz;
+        body_to_world(a.pose, a.body[3 * i], a.body[3 * i + 1], a.body[3 * i + 2], wx, wy, wz);
+        TopK<5> tk;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            tk.k[j] = knn_key(a.far_d[5 * (size_t)f + j], a.far_id[5 * (size_t)f + j]);
+        }
+        wave_knn_box<5>(a.grid, wx, wy, wz, lane, tk);
+        if (lane < 5) {
+            int v = tk.id(0);
+#pragma unroll
+            for (int j = 1; j < 5; ++j)
+                if (lane == j) v = tk.id(j);
+            a.nn_idx[5 * (size_t)i + lane] = v == kNone ? -1 : v;
+        }
+    }
+}
+
+// Pass 3, lane = point: gate (found == 5 && d2[4] <= 5), esti_plane, pd2,
+// s-gate, H row, 4 wave partials combined in LDS -> block partial.  Resets
+// the far queue for the next kNN evaluation.
+__global__ void __launch_bounds__(kBlock) plane_kernel(MatchArgs a) {
     __shared__ double red[kBlock / 64][32];
-    const int blk = xcd_block(blockIdx.x, gridDim.x);
-    const int i = blk * kBlock + threadIdx.x;
+    const int i = blockIdx.x * kBlock + threadIdx.x;
     double J[6] = {0, 0, 0, 0, 0, 0};
     double h = 0.0, res = 0.0, cnt = 0.0;
     if (i < a.n) {
-        const float bx = a.body[3 * i], by = a.body[3 * i + 1], bz = a.body[3 * i + 2];
-        float wx, wy, wz;
-        body_to_world(a.pose, bx, by, bz, wx, wy, wz);
-        TopK<5> tk;
-        tk.init(a.range_sq);
-        lane_knn_exact<5>(a.grid, wx, wy, wz, a.max_shell, tk);
-        int32_t* o = a.nn_idx + 5 * (size_t)i;
+        const int32_t* nn = a.nn_idx + 5 * (size_t)i;
+        int id[5];
 #pragma unroll
-        for (int j = 0; j < 5; ++j) o[j] = tk.id[j] == kNone ? -1 : tk.id[j];
-        bool sel = tk.id[4] != kNone;  // found == 5 && d2[4] <= range (by construction)
+        for (int j = 0; j < 5; ++j) id[j] = nn[j];
+        bool sel = id[4] >= 0;  // sorted list: the 5th exists => all exist, d2 <= range by construction
         if (sel) {
             float P[5][3];
 #pragma unroll
             for (int j = 0; j < 5; ++j) {
-                const float4 q = a.map_by_id[tk.id[j]];
+                const float4 q = a.map_by_id[id[j]];
                 P[j][0] = q.x;
                 P[j][1] = q.y;
                 P[j][2] = q.z;
@@ -196,6 +194,9 @@ __global__ void __launch_bounds__(kBlock) h_model_knn_lane_kernel(MatchArgs a) {
             const float4 pl = make_float4(abcd[0], abcd[1], abcd[2], abcd[3]);
             a.planes[i] = pl;
             if (sel) {
+                const float bx = a.body[3 * i], by = a.body[3 * i + 1], bz = a.body[3 * i + 2];
+                float wx, wy, wz;
+                body_to_world(a.pose, bx, by, bz, wx, wy, wz);
                 sel = residual_row(a, bx, by, bz, wx, wy, wz, pl, J, h, res);
                 cnt = sel ? 1.0 : 0.0;
             }
@@ -209,8 +210,9 @@ __global__ void __launch_bounds__(kBlock) h_model_knn_lane_kernel(MatchArgs a) {
         double s = 0.0;
 #pragma unroll
         for (int w = 0; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
-        a.partials[(size_t)blk * 32 + threadIdx.x] = s;
+        a.partials[(size_t)blockIdx.x * 32 + threadIdx.x] = s;
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.far_count = 0;
 }
 
 // ekfom_data.converge == false: reuse Nearest_Points / planes.  256 threads,
@@ -354,21 +356,23 @@ __global__ void __launch_bounds__(1024) h_rows_kernel(MatchArgs a, double* __res
 // ---------------------------------------------------------------- launchers
 int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st) {
     if (a.n == 0) return 0;
+    const int nb = (a.n + kBlock - 1) / kBlock;
     if (redo) {
-        if (a.knn_mode == 0 && !a.dbg) {  // lane per point (default)
-            const int nb = (a.n + kBlock - 1) / kBlock;
-            h_model_knn_lane_kernel<<<nb, kBlock, 0, st>>>(a);
-            return nb;
-        }
-        const int qpb = kKnnBlock / kGroup;  // 8 lanes per point (diagnostics / A-B)
-        const int nb = (a.n + qpb - 1) / qpb;
+        const int qpb = kKnnBlock / kGroup;
+        const int nq = (a.n + qpb - 1) / qpb;
         if (a.dbg)
-            h_model_knn_kernel<true><<<nb, kKnnBlock, 0, st>>>(a);
+            knn_near_kernel<true><<<nq, kKnnBlock, 0, st>>>(a);
         else
-            h_model_knn_kernel<false><<<nb, kKnnBlock, 0, st>>>(a);
+            knn_near_kernel<false><<<nq, kKnnBlock, 0, st>>>(a);
+        static const int far_blocks = [] {  // LIO_FAR_BLOCKS: diagnostics override of the far-pass grid
+            const char* e = std::getenv("LIO_FAR_BLOCKS");
+            const int v = e ? std::atoi(e) : 0;
+            return v > 0 ? std::min(v, 4096) : kFarBlocks;
+        }();
+        if (a.max_shell > 1) knn_far_kernel<<<far_blocks, kFarBlock, 0, st>>>(a);
+        plane_kernel<<<nb, kBlock, 0, st>>>(a);
         return nb;
     }
-    const int nb = (a.n + kBlock - 1) / kBlock;
     h_model_reuse_kernel<<<nb, kBlock, 0, st>>>(a);
     return nb;
 }
@@ -386,9 +390,8 @@ void launch_h_rows(const MatchArgs& a, double* rows, int64_t max_rows, int64_t* 
     h_rows_kernel<<<1, 1024, 0, st>>>(a, rows, max_rows, n_rows);
 }
 
-int match_blocks(int n) {  // partial slots needed by either kernel
-    const int qpb = kKnnBlock / kGroup;
-    return std::max((n + kBlock - 1) / kBlock, (n + qpb - 1) / qpb);
+int match_blocks(int n) {  // partial slots (plane / reuse kernels)
+    return (n + kBlock - 1) / kBlock;
 }
 
 }  // namespace lio

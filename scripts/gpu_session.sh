@@ -30,6 +30,9 @@ for s in $STEPS; do
     test)  run pytest_gpu 900 python -m pytest tests -q -m gpu -p no:cacheprovider ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 200 --warmup 20 ;;
+    knn)   run knn_timing 300 python scripts/knn_timing.py C2 &&
+           LIO_FAR_BLOCKS=8 run knn_timing_fb8 300 python scripts/knn_timing.py C2 &&
+           run knn_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/knnprof" -o run --output-format csv -- python scripts/knn_timing.py C2 ;;
     quick) run bench_quick 400 python bench.py --steps 60 --warmup 5 --icp-reps 2 --cpu-seconds 5 ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
                -- python bench.py --steps 100 --warmup 10 --no-cpu --icp-reps 3 ;;
