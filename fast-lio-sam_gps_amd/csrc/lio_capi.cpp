@@ -19,6 +19,7 @@
 #include "ieskf.hpp"
 #include "lio_error.hpp"
 #include "lio_kernels.hpp"
+#include "lio_mapupd.hpp"
 
 namespace {
 
@@ -73,10 +74,15 @@ struct lio_map {
     hipStream_t st = nullptr;
     lio_map_params p{};
     lio::GridBuf grid;
+    lio::MapUpdBuf upd;
     float* d_xyz = nullptr;
     int64_t xyz_cap = 0;
-    int64_t n = 0;
+    int64_t n = 0;  // alive points (== grid.n)
 };
+
+// geometry slack when an insert leaves the grid: the rebuild reserves room
+// around the map (half a local-map cube of travel at the usual 1 m cells)
+static float map_slack(const lio_map* m) { return 64.f * m->grid.geom.cell; }
 
 struct lio_ctx {
     lio_map* map = nullptr;
@@ -94,6 +100,7 @@ struct lio_ctx {
     int64_t rows_cap = 0;
     int64_t* d_nrows = nullptr;
     lio_pose last_pose{};
+    lio_pose knn_pose{};  // pose of the last kNN evaluation (Nearest_Points)
     int* d_far_list = nullptr;  // far-pass queue (cap), its length, and queued lists (cap*5)
     int* d_far_count = nullptr;
     float* d_far_d = nullptr;
@@ -146,6 +153,7 @@ int lio_map_destroy(lio_map* m) {
     (void)hipSetDevice(m->dev);
     (void)hipStreamSynchronize(m->st);
     lio::grid_free(m->grid);
+    lio::mapupd_free(m->upd);
     if (m->d_xyz) (void)hipFree(m->d_xyz);
     (void)hipStreamDestroy(m->st);
     delete m;
@@ -158,7 +166,7 @@ static int map_build_impl(lio_map* m, const float* d_xyz, int64_t n) {
     if (rc == -1) return fail(LIO_ERR_ARG, "grid build: invalid points (empty, too many, or non-finite)");
     if (rc != 0) return fail(LIO_ERR_HIP, "grid build failed");
     HIP_TRY(hipStreamSynchronize(m->st));
-    m->n = n;
+    m->n = m->grid.n;
     return LIO_OK;
 }
 
@@ -178,19 +186,152 @@ int lio_map_build_device(lio_map* m, const float* d_xyz, int64_t n) {
 }
 
 int64_t lio_map_size(const lio_map* m) { return m ? m->n : 0; }
+int64_t lio_map_num_ids(const lio_map* m) { return m ? m->grid.n_ids : 0; }
+
+static int map_by_id_host(lio_map* m, std::vector<float4>& tmp) {
+    tmp.resize(m->grid.n_ids);
+    if (m->grid.n_ids == 0) return LIO_OK;
+    HIP_TRY(hipSetDevice(m->dev));
+    HIP_TRY(hipMemcpyAsync(tmp.data(), m->grid.by_id, m->grid.n_ids * sizeof(float4), hipMemcpyDeviceToHost, m->st));
+    HIP_TRY(hipStreamSynchronize(m->st));
+    return LIO_OK;
+}
 
 int lio_map_get_points(lio_map* m, float* xyz_out) {
     if (!m || !xyz_out) return fail(LIO_ERR_ARG, "bad arguments");
-    if (m->n == 0) return LIO_OK;
-    HIP_TRY(hipSetDevice(m->dev));
-    std::vector<float4> tmp(m->n);
-    HIP_TRY(hipMemcpyAsync(tmp.data(), m->grid.by_id, m->n * sizeof(float4), hipMemcpyDeviceToHost, m->st));
-    HIP_TRY(hipStreamSynchronize(m->st));
-    for (int64_t i = 0; i < m->n; ++i) {
-        xyz_out[3 * i] = tmp[i].x;
-        xyz_out[3 * i + 1] = tmp[i].y;
-        xyz_out[3 * i + 2] = tmp[i].z;
+    std::vector<float4> tmp;
+    int rc = map_by_id_host(m, tmp);
+    if (rc) return rc;
+    int64_t k = 0;
+    for (const float4& p : tmp) {
+        if (p.w == 0.f) continue;
+        xyz_out[3 * k] = p.x;
+        xyz_out[3 * k + 1] = p.y;
+        xyz_out[3 * k + 2] = p.z;
+        ++k;
     }
+    return LIO_OK;
+}
+
+int lio_map_get_by_id(lio_map* m, float* xyz_out, uint8_t* alive_out) {
+    if (!m) return fail(LIO_ERR_ARG, "bad arguments");
+    std::vector<float4> tmp;
+    int rc = map_by_id_host(m, tmp);
+    if (rc) return rc;
+    for (size_t i = 0; i < tmp.size(); ++i) {
+        if (xyz_out) {
+            xyz_out[3 * i] = tmp[i].x;
+            xyz_out[3 * i + 1] = tmp[i].y;
+            xyz_out[3 * i + 2] = tmp[i].z;
+        }
+        if (alive_out) alive_out[i] = tmp[i].w != 0.f;
+    }
+    return LIO_OK;
+}
+
+static int map_status(int rc, const char* what) {
+    if (rc == 0) return LIO_OK;
+    if (rc == -5) return fail(LIO_ERR_NOMEM, std::string(what) + ": out of device memory");
+    if (rc == -1) return fail(LIO_ERR_ARG, std::string(what) + ": invalid points");
+    return fail(LIO_ERR_HIP, std::string(what) + " failed");
+}
+
+int lio_map_add_device(lio_map* m, const float* d_xyz, int64_t n, int downsample, int64_t* n_added) {
+    if (!m || n < 0 || (n > 0 && !d_xyz)) return fail(LIO_ERR_ARG, "lio_map_add: bad arguments");
+    HIP_TRY(hipSetDevice(m->dev));
+    int64_t out[2] = {0, 0};
+    if (m->grid.n_ids == 0 && !downsample && n > 0) {  // empty map: a plain add is a build
+        int rc = lio_map_build_device(m, d_xyz, n);
+        if (n_added) *n_added = n;
+        return rc;
+    }
+    int rc = lio::map_add_device(m->grid, m->upd, d_xyz, n, downsample != 0, m->p.downsample_size, map_slack(m), out,
+                                 m->st);
+    HIP_TRY(hipStreamSynchronize(m->st));
+    m->n = m->grid.n;
+    if (n_added) *n_added = out[0];
+    return map_status(rc, "lio_map_add");
+}
+
+int lio_map_add(lio_map* m, const float* xyz, int64_t n, int downsample, int64_t* n_added) {
+    if (!m || n < 0 || (n > 0 && !xyz)) return fail(LIO_ERR_ARG, "lio_map_add: bad arguments");
+    if (n == 0) {
+        if (n_added) *n_added = 0;
+        return LIO_OK;
+    }
+    HIP_TRY(hipSetDevice(m->dev));
+    int rc = grow(&m->d_xyz, m->xyz_cap, n, 3);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(m->d_xyz, xyz, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice, m->st));
+    return lio_map_add_device(m, m->d_xyz, n, downsample, n_added);
+}
+
+int lio_map_delete_boxes(lio_map* m, const float* boxes, int nb, int64_t* n_deleted) {
+    if (!m || nb < 0 || (nb > 0 && !boxes)) return fail(LIO_ERR_ARG, "lio_map_delete_boxes: bad arguments");
+    HIP_TRY(hipSetDevice(m->dev));
+    int64_t nd = 0;
+    int rc = lio::map_delete_boxes(m->grid, m->upd, boxes, nb, map_slack(m), &nd, m->st);
+    HIP_TRY(hipStreamSynchronize(m->st));
+    m->n = m->grid.n;
+    if (n_deleted) *n_deleted = nd;
+    return map_status(rc, "lio_map_delete_boxes");
+}
+
+// lasermap_fov_segment() [U]: float box vertices, MOV_THRESHOLD * DET_RANGE
+// trigger distance, mov_dist = max((cube_len - 2*MOV_THRESHOLD*DET_RANGE)*0.5*0.9,
+// DET_RANGE*(MOV_THRESHOLD-1)) (double, stored float).
+int lio_localmap_update(lio_localmap* lm, const double pos_lid[3], double cube_len, float det_range,
+                        float mov_threshold, float boxes_out[18], int* n_boxes) {
+    if (!lm || !pos_lid || !boxes_out || !n_boxes) return fail(LIO_ERR_ARG, "lio_localmap_update: bad arguments");
+    *n_boxes = 0;
+    if (!lm->initialized) {
+        for (int i = 0; i < 3; ++i) {
+            lm->vertex_min[i] = (float)(pos_lid[i] - cube_len / 2.0);
+            lm->vertex_max[i] = (float)(pos_lid[i] + cube_len / 2.0);
+        }
+        lm->initialized = 1;
+        return LIO_OK;
+    }
+    float dist_to_edge[3][2];
+    bool need_move = false;
+    for (int i = 0; i < 3; ++i) {
+        dist_to_edge[i][0] = (float)std::fabs(pos_lid[i] - lm->vertex_min[i]);
+        dist_to_edge[i][1] = (float)std::fabs(pos_lid[i] - lm->vertex_max[i]);
+        if (dist_to_edge[i][0] <= mov_threshold * det_range || dist_to_edge[i][1] <= mov_threshold * det_range)
+            need_move = true;
+    }
+    if (!need_move) return LIO_OK;
+    lio_localmap nw = *lm;
+    const float mov_dist = (float)std::max((cube_len - 2.0 * mov_threshold * det_range) * 0.5 * 0.9,
+                                           (double)(det_range * (mov_threshold - 1)));
+    for (int i = 0; i < 3; ++i) {
+        float bmin[3], bmax[3];
+        for (int d = 0; d < 3; ++d) {
+            bmin[d] = lm->vertex_min[d];
+            bmax[d] = lm->vertex_max[d];
+        }
+        bool add = false;
+        if (dist_to_edge[i][0] <= mov_threshold * det_range) {
+            nw.vertex_max[i] -= mov_dist;
+            nw.vertex_min[i] -= mov_dist;
+            bmin[i] = lm->vertex_max[i] - mov_dist;
+            add = true;
+        } else if (dist_to_edge[i][1] <= mov_threshold * det_range) {
+            nw.vertex_max[i] += mov_dist;
+            nw.vertex_min[i] += mov_dist;
+            bmax[i] = lm->vertex_min[i] + mov_dist;
+            add = true;
+        }
+        if (add) {
+            float* b = boxes_out + 6 * (*n_boxes);
+            for (int d = 0; d < 3; ++d) {
+                b[d] = bmin[d];
+                b[3 + d] = bmax[d];
+            }
+            ++*n_boxes;
+        }
+    }
+    *lm = nw;
     return LIO_OK;
 }
 
@@ -370,7 +511,10 @@ int lio_match(lio_ctx* c, const lio_pose* pose, int redo_knn, double* sums) {
     }
     c->last_pose = *pose;
     c->have_eval = true;
-    if (redo_knn) c->knn_valid = true;
+    if (redo_knn) {
+        c->knn_valid = true;
+        c->knn_pose = *pose;
+    }
     return LIO_OK;
 }
 
@@ -393,9 +537,49 @@ int lio_ctx_knn_stats(lio_ctx* c, const lio_pose* pose, double* sums, int32_t* s
     if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) return fail(LIO_ERR_HIP, "lio_ctx_knn_stats failed");
     std::memcpy(sums, c->h_sums, LIO_SUMS_LEN * sizeof(double));
     c->last_pose = *pose;
+    c->knn_pose = *pose;
     c->have_eval = true;
     c->knn_valid = true;
     return LIO_OK;
+}
+
+int lio_ctx_get_knn_pose(lio_ctx* c, lio_pose* out) {
+    if (!c || !out) return fail(LIO_ERR_ARG, "bad arguments");
+    if (!c->knn_valid) return fail(LIO_ERR_STATE, "lio_ctx_get_knn_pose: no kNN evaluation");
+    *out = c->knn_pose;
+    return LIO_OK;
+}
+
+int lio_map_incremental(lio_ctx* c, const lio_pose* pose, double filter_size_map, lio_incremental_stats* st) {
+    if (!c || !pose || !(filter_size_map > 0.0)) return fail(LIO_ERR_ARG, "lio_map_incremental: bad arguments");
+    if (c->n > 0 && !c->knn_valid && c->map->n > 0)
+        return fail(LIO_ERR_STATE, "lio_map_incremental: no kNN evaluation for this scan (Nearest_Points)");
+    lio_map* m = c->map;
+    HIP_TRY(hipSetDevice(m->dev));
+    lio::IncrArgs a{};
+    std::memcpy(&a.pose, pose, sizeof(lio::PoseArg));
+    std::memcpy(&a.pose_knn, &c->knn_pose, sizeof(lio::PoseArg));
+    a.body = c->d_body;
+    a.nn_idx = c->d_nn;
+    a.n = (int)c->n;
+    a.fs = filter_size_map;
+    a.range_sq = c->p.knn_range_sq;
+    int64_t out[4] = {0, 0, 0, 0};
+    int rc = 0;
+    if (m->grid.n_ids == 0) {  // ikdtree.Build on the first scan is the caller's job (lio_map_build)
+        return fail(LIO_ERR_STATE, "lio_map_incremental: map is empty (build it from the first scan)");
+    }
+    rc = lio::map_incremental(m->grid, m->upd, a, m->p.downsample_size, map_slack(m), out, m->st);
+    HIP_TRY(hipStreamSynchronize(m->st));
+    m->n = m->grid.n;
+    c->knn_valid = false;  // ids/grid changed
+    if (st) {
+        st->n_to_add = out[0];
+        st->n_no_downsample = out[1];
+        st->n_skipped = out[2];
+        st->n_added_downsample = out[3];
+    }
+    return map_status(rc, "lio_map_incremental");
 }
 
 int lio_get_knn(lio_ctx* c, int32_t* idx, float* d2) {

@@ -43,13 +43,23 @@ struct GridGeom {
 };
 
 // Device buffers owned by a grid (map or ICP target).
+//   by_id[id]   (x, y, z, alive 1/0) for every id ever inserted (ids are
+//               insertion order; deleted ids stay as tombstones)
+//   pts[j]      alive points sorted by (cell, id), w = id bits; ckeys[j] = cell
+//   start[c]    CSR offsets into pts, ncells + 1
 struct GridBuf {
     float4* pts = nullptr;      // sorted by cell
+    uint32_t* ckeys = nullptr;  // cell of pts[j]
     float4* by_id = nullptr;    // id order
-    uint32_t* start = nullptr;  // ncells + 1
-    int64_t n = 0, cap = 0;
+    uint32_t* start = nullptr;  // ncells + 1 (+ histogram scratch)
+    int64_t n = 0, cap = 0;     // alive entries / entry capacity
+    int64_t n_ids = 0, id_cap = 0;
     uint32_t cells_cap = 0;
     GridGeom geom{};
+    float4* pts_alt = nullptr;  // merge targets
+    uint32_t* ckeys_alt = nullptr;
+    uint32_t* flag = nullptr;
+    uint32_t* pos = nullptr;
     // temporaries
     uint32_t* keys = nullptr;
     uint32_t* keys_alt = nullptr;
@@ -62,8 +72,14 @@ struct GridBuf {
     float* xyz = nullptr;        // staging for host input, cap*3
 };
 
-// Build grid from device xyz (n*3).  Synchronises the stream once (AABB).
+// Build grid from device xyz (n*3), ids 0..n-1.  Synchronises the stream once (AABB).
 int grid_build(GridBuf& g, const float* d_xyz, int64_t n, float cell, hipStream_t st);
+// Full rebuild over the alive ids of by_id; geometry = AABB + slack (+1-cell pad).
+int grid_rebuild(GridBuf& g, float cell, float slack, hipStream_t st);
+// Merge update after appending ids [id0, n_ids) and/or marking ids dead.
+int grid_update(GridBuf& g, int64_t id0, bool deleted, float slack, hipStream_t st);
+// Grow by_id to hold n_ids ids (contents kept).
+int grid_reserve_ids(GridBuf& g, int64_t n_ids, hipStream_t st);
 void grid_free(GridBuf& g);
 GridDev grid_view(const GridBuf& g);
 

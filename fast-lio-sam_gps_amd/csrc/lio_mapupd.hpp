@@ -1,0 +1,60 @@
+// lio_mapupd.hpp — incremental map maintenance (lio_mapupd.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lio_kernels.hpp"
+
+namespace lio {
+
+// Scratch owned by a map handle.
+struct MapUpdBuf {
+    uint64_t* keys = nullptr;  // voxel keys
+    uint64_t* keys_alt = nullptr;
+    uint32_t* vals = nullptr;
+    uint32_t* vals_alt = nullptr;
+    uint32_t* flag = nullptr;
+    uint32_t* pos = nullptr;
+    uint32_t* flag2 = nullptr;
+    uint32_t* pos2 = nullptr;
+    uint8_t* cls = nullptr;  // per point class / survivor flag
+    float* world = nullptr;  // n*3 world points (map_incremental)
+    float* xyz_a = nullptr;  // PointToAdd
+    float* xyz_b = nullptr;  // PointNoNeedDownsample
+    int* pending = nullptr;
+    int64_t cap = 0;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    int* d_small = nullptr;  // counters
+    int* h_small = nullptr;  // pinned
+    float* boxes = nullptr;
+    int boxes_cap = 0;
+};
+
+// map_incremental inputs (per scan)
+struct IncrArgs {
+    PoseArg pose;      // final state (pointBodyToWorld)
+    PoseArg pose_knn;  // pose of the last kNN evaluation (Nearest_Points)
+    const float* body;
+    const int32_t* nn_idx;  // n*5, -1 = none within range
+    int n;
+    double fs;        // filter_size_map_min (double, laserMapping)
+    float range_sq;   // kNN range of the lists
+    // filled by map_incremental()
+    GridDev grid;
+    const float4* map_by_id;
+    int64_t map_alive;
+    float* world;
+    uint8_t* cls;
+    int* pending;
+    int* pending_count;
+};
+
+void mapupd_free(MapUpdBuf& u);
+int map_add_device(GridBuf& g, MapUpdBuf& u, const float* d_xyz, int64_t n, bool downsample, float ds, float slack,
+                   int64_t out[2], hipStream_t st);
+int map_delete_boxes(GridBuf& g, MapUpdBuf& u, const float* boxes, int nb, float slack, int64_t* n_deleted,
+                     hipStream_t st);
+int map_incremental(GridBuf& g, MapUpdBuf& u, IncrArgs a, float ds, float slack, int64_t out[4], hipStream_t st);
+
+}  // namespace lio

@@ -26,7 +26,9 @@ SUMS_HTH, SUMS_HTh, SUMS_NEFF, SUMS_RES, SUMS_HH = 0, 21, 27, 28, 29
 EXPORTS = [
     "lio_device_count", "lio_last_error", "lio_build_info",
     "lio_map_create", "lio_map_destroy", "lio_map_build", "lio_map_build_device", "lio_map_size",
-    "lio_map_get_points", "lio_map_get_grid",
+    "lio_map_get_points", "lio_map_get_grid", "lio_map_num_ids", "lio_map_get_by_id", "lio_map_add",
+    "lio_map_add_device", "lio_map_delete_boxes", "lio_localmap_update", "lio_map_incremental",
+    "lio_ctx_get_knn_pose",
     "lio_ctx_create", "lio_ctx_destroy", "lio_scan_set", "lio_scan_set_device", "lio_match",
     "lio_get_knn", "lio_get_planes", "lio_get_world", "lio_get_h_rows", "lio_ctx_knn_stats",
     "lio_ieskf_update",
@@ -82,6 +84,15 @@ class IcpResult(C.Structure):
                 ("iterations", C.c_int), ("state", C.c_int), ("last_mse", C.c_double), ("last_corr", C.c_int64)]
 
 
+class LocalMap(C.Structure):
+    _fields_ = [("vertex_min", C.c_float * 3), ("vertex_max", C.c_float * 3), ("initialized", C.c_int)]
+
+
+class IncrementalStats(C.Structure):
+    _fields_ = [("n_to_add", C.c_int64), ("n_no_downsample", C.c_int64), ("n_skipped", C.c_int64),
+                ("n_added_downsample", C.c_int64)]
+
+
 class KernelTiming(C.Structure):
     _fields_ = [("knn_launches", C.c_int64), ("knn_ms", C.c_double), ("reuse_launches", C.c_int64),
                 ("reuse_ms", C.c_double), ("final_launches", C.c_int64), ("final_ms", C.c_double),
@@ -109,6 +120,15 @@ def _declare(L):
         "lio_map_size": (C.c_int64, [vp]),
         "lio_map_get_points": (C.c_int, [vp, fp]),
         "lio_map_get_grid": (C.c_int, [vp, dp]),
+        "lio_map_num_ids": (C.c_int64, [vp]),
+        "lio_map_get_by_id": (C.c_int, [vp, fp, C.POINTER(C.c_uint8)]),
+        "lio_map_add": (C.c_int, [vp, fp, C.c_int64, C.c_int, C.POINTER(C.c_int64)]),
+        "lio_map_add_device": (C.c_int, [vp, vp, C.c_int64, C.c_int, C.POINTER(C.c_int64)]),
+        "lio_map_delete_boxes": (C.c_int, [vp, fp, C.c_int, C.POINTER(C.c_int64)]),
+        "lio_localmap_update": (C.c_int, [C.POINTER(LocalMap), dp, C.c_double, C.c_float, C.c_float, fp,
+                                          C.POINTER(C.c_int)]),
+        "lio_map_incremental": (C.c_int, [vp, C.POINTER(Pose), C.c_double, C.POINTER(IncrementalStats)]),
+        "lio_ctx_get_knn_pose": (C.c_int, [vp, C.POINTER(Pose)]),
         "lio_ctx_create": (C.c_int, [vp, C.POINTER(MatchParams), C.POINTER(vp)]),
         "lio_ctx_destroy": (C.c_int, [vp]),
         "lio_scan_set": (C.c_int, [vp, fp, C.c_int64]),

@@ -4,7 +4,9 @@ Names follow the reference's interfaces so callers read like FAST-LIO
 (upstream hku-mars src/laserMapping.cpp, include/ikd-Tree, IKFoM esekfom.hpp;
 the Kodifly fork is an empty submodule in the reference, .gitmodules:1-3):
 
-* :class:`IkdTreeGPU` — ``KD_TREE<PointType> ikdtree`` (``Build``, ``size``)
+* :class:`IkdTreeGPU` — ``KD_TREE<PointType> ikdtree`` (``Build``, ``Add_Points``,
+  ``Delete_Point_Boxes``, ``size``)
+* :class:`LocalMap` — ``lasermap_fov_segment()``'s local-map cube
 * :class:`HShareModelGPU` — ``h_share_model(state_ikfom&, dyn_share_datastruct&)``
   with its globals (``Nearest_Points``, ``point_selected_surf``, ``normvec``,
   ``feats_down_world``) exposed as getters
@@ -91,6 +93,37 @@ class IkdTreeGPU:
     def size(self) -> int:
         return int(lib().lio_map_size(self._h))
 
+    def num_ids(self) -> int:
+        """Ids ever inserted (alive + deleted); kNN ids index this space."""
+        return int(lib().lio_map_num_ids(self._h))
+
+    def by_id(self):
+        """(xyz[num_ids,3], alive[num_ids]) for every id."""
+        n = self.num_ids()
+        xyz = np.empty((n, 3), np.float32)
+        alive = np.empty(n, np.uint8)
+        check(lib().lio_map_get_by_id(self._h, _fp(xyz), alive.ctypes.data_as(C.POINTER(C.c_uint8))))
+        return xyz, alive.astype(bool)
+
+    def Add_Points(self, points: np.ndarray, downsample_on: bool) -> int:
+        """ikdtree.Add_Points(PointToAdd, downsample_on) [U]; returns the reference's count."""
+        pts = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 3)
+        n = C.c_int64(0)
+        check(lib().lio_map_add(self._h, _fp(pts), len(pts), 1 if downsample_on else 0, C.byref(n)))
+        return int(n.value)
+
+    def Add_Points_device(self, ptr: int, n: int, downsample_on: bool) -> int:
+        out = C.c_int64(0)
+        check(lib().lio_map_add_device(self._h, C.c_void_p(ptr), n, 1 if downsample_on else 0, C.byref(out)))
+        return int(out.value)
+
+    def Delete_Point_Boxes(self, boxes) -> int:
+        """ikdtree.Delete_Point_Boxes(cub_needrm) [U]; boxes: (nb, 6) min xyz, max xyz."""
+        b = np.ascontiguousarray(boxes, dtype=np.float32).reshape(-1, 6)
+        n = C.c_int64(0)
+        check(lib().lio_map_delete_boxes(self._h, _fp(b), len(b), C.byref(n)))
+        return int(n.value)
+
     def points(self) -> np.ndarray:
         out = np.empty((self.size(), 3), np.float32)
         check(lib().lio_map_get_points(self._h, _fp(out)))
@@ -111,6 +144,31 @@ class IkdTreeGPU:
             self.close()
         except Exception:
             pass
+
+
+class LocalMap:
+    """``lasermap_fov_segment()`` [U]: the local-map cube around the LiDAR.
+
+    ``update(pos_lid)`` returns the boxes to delete (``cub_needrm``), to be
+    passed to :meth:`IkdTreeGPU.Delete_Point_Boxes`.  Defaults: cube_side_length
+    1000 (kitti.launch:11), det_range 100 (kitti.yaml), MOV_THRESHOLD 1.5 [U].
+    """
+
+    def __init__(self, cube_len: float = 1000.0, det_range: float = 100.0, mov_threshold: float = 1.5):
+        self.c = _capi.LocalMap()
+        self.cube_len, self.det_range, self.mov_threshold = cube_len, det_range, mov_threshold
+
+    def update(self, pos_lid) -> np.ndarray:
+        pos = np.ascontiguousarray(pos_lid, dtype=np.float64).reshape(3)
+        boxes = np.zeros((3, 6), np.float32)
+        nb = C.c_int(0)
+        check(lib().lio_localmap_update(C.byref(self.c), _dp(pos), self.cube_len, self.det_range,
+                                        self.mov_threshold, _fp(boxes), C.byref(nb)))
+        return boxes[: nb.value].copy()
+
+    @property
+    def box(self):
+        return np.array(list(self.c.vertex_min)), np.array(list(self.c.vertex_max))
 
 
 class HShareModelGPU:
@@ -172,6 +230,23 @@ class HShareModelGPU:
         st = np.zeros((self.n, 3), np.int32)
         check(lib().lio_ctx_knn_stats(self._h, C.byref(pose), _dp(sums), st.ctypes.data_as(C.POINTER(C.c_int32))))
         return sums, st
+
+    def last_knn_pose24(self) -> np.ndarray:
+        """pose24 of the last kNN evaluation (the pose Nearest_Points belong to)."""
+        p = _capi.Pose()
+        check(lib().lio_ctx_get_knn_pose(self._h, C.byref(p)))
+        return np.concatenate([list(p.R), list(p.t), list(p.R_LI), list(p.t_LI)]).astype(np.float64)
+
+    def map_incremental(self, pose, filter_size_map: float = 0.5) -> dict:
+        """FAST-LIO ``map_incremental()`` [U]: add this scan to the map with the final pose.
+
+        Uses Nearest_Points from the last kNN evaluation of this scan.
+        """
+        if not isinstance(pose, _capi.Pose):
+            pose = pose_from_pose24(pose)
+        st = _capi.IncrementalStats()
+        check(lib().lio_map_incremental(self._h, C.byref(pose), float(filter_size_map), C.byref(st)))
+        return {k: int(getattr(st, k)) for k, _ in _capi.IncrementalStats._fields_}
 
     # ---- timing (HIP events on the context's stream)
     def set_timing(self, on: bool):

@@ -75,10 +75,36 @@ int lio_map_destroy(lio_map* m);
 int lio_map_build(lio_map* m, const float* xyz, int64_t n);
 /* same, xyz already resident in device memory (e.g. a torch tensor).       */
 int lio_map_build_device(lio_map* m, const float* d_xyz, int64_t n);
-/* ikdtree.size() [U]                                                       */
+/* ikdtree.size() [U]: alive points                                        */
 int64_t lio_map_size(const lio_map* m);
-/* copies the map points (id order) to host, n*3 float                      */
+/* ids ever inserted (alive + deleted); kNN ids index this space            */
+int64_t lio_map_num_ids(const lio_map* m);
+/* copies the alive map points (id order) to host, lio_map_size()*3 float   */
 int lio_map_get_points(lio_map* m, float* xyz_out);
+/* every id: xyz (num_ids*3, may be NULL) and alive flags (num_ids, may be NULL) */
+int lio_map_get_by_id(lio_map* m, float* xyz_out, uint8_t* alive_out);
+
+/* ---- incremental maintenance ----
+ * ikdtree.Add_Points(PointToAdd, downsample_on) [U]: with downsample, per
+ * point (in order) the filter_size_map voxel [floor(p/ds)*ds, +ds) keeps only
+ * the point nearest its centre (Search_by_range + Delete_by_range +
+ * Add_by_point).  n_added (may be NULL): the reference's return value (the
+ * number of Add_by_point calls; n for downsample = 0).                      */
+int lio_map_add(lio_map* m, const float* xyz, int64_t n, int downsample, int64_t* n_added);
+int lio_map_add_device(lio_map* m, const float* d_xyz, int64_t n, int downsample, int64_t* n_added);
+/* ikdtree.Delete_Point_Boxes(cub_needrm) [U]: boxes nb x 6 floats
+ * (min x y z, max x y z), a point is inside when min <= p < max.           */
+int lio_map_delete_boxes(lio_map* m, const float* boxes, int nb, int64_t* n_deleted);
+
+/* lasermap_fov_segment() [U] (FAST-LIO laserMapping.cpp): host helper that
+ * keeps the local map cube around the LiDAR and returns the boxes to delete
+ * (pass them to lio_map_delete_boxes).  pos_lid = pos + rot * offset_T_L_I.  */
+typedef struct lio_localmap {
+    float vertex_min[3], vertex_max[3];
+    int initialized;
+} lio_localmap;
+int lio_localmap_update(lio_localmap* lm, const double pos_lid[3], double cube_len, float det_range,
+                        float mov_threshold, float boxes_out[18], int* n_boxes);
 /* grid geometry: origin[3], cell, dims[3] (as doubles)                     */
 int lio_map_get_grid(lio_map* m, double* out7);
 
@@ -203,6 +229,22 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
 /* One-shot form of the above (SURVEY §8b signature).                       */
 int icp_align(const float* src_xyz, int64_t ns, const float* dst_xyz, int64_t nd, const lio_icp_params* p,
               float* T_out, double* fitness, int* converged, int* iters, float* aligned_xyz_opt);
+
+/* FAST-LIO map_incremental() [U] for the ctx's current scan: world points
+ * with the final pose, Nearest_Points from the ctx's last kNN evaluation
+ * (lio_match / lio_ieskf_update with redo), PointToAdd / PointNoNeedDownsample
+ * classification on filter_size_map (double, as laserMapping), then
+ * Add_Points(PointToAdd, true) and Add_Points(PointNoNeedDownsample, false)
+ * on the ctx's map.  Invalidates the ctx's kNN lists.                      */
+typedef struct lio_incremental_stats {
+    int64_t n_to_add;           /* PointToAdd.size()                          */
+    int64_t n_no_downsample;    /* PointNoNeedDownsample.size()               */
+    int64_t n_skipped;          /* points not added                           */
+    int64_t n_added_downsample; /* Add_Points(PointToAdd, true) return value  */
+} lio_incremental_stats;
+int lio_map_incremental(lio_ctx* c, const lio_pose* pose, double filter_size_map, lio_incremental_stats* st);
+/* pose of the ctx's last kNN evaluation (the pose Nearest_Points belong to) */
+int lio_ctx_get_knn_pose(lio_ctx* c, lio_pose* out);
 
 /* ----------------------------------------------------------------- timing */
 typedef struct lio_kernel_timing {

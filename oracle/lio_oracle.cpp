@@ -33,6 +33,7 @@
 #include <cstring>
 #include <limits>
 #include <numeric>
+#include <unordered_map>
 #include <vector>
 #ifdef _OPENMP
 #include <omp.h>
@@ -114,9 +115,15 @@ struct KdTree {
     }
 
     void build(const float* p, int64_t n) {
-        xyz.assign(p, p + 3 * n);
-        perm.resize(n);
-        std::iota(perm.begin(), perm.end(), 0);
+        std::vector<int32_t> ids(n);
+        std::iota(ids.begin(), ids.end(), 0);
+        build_ids(p, n, ids);
+    }
+    // tree over the subset `ids` of the n_all points p (ids are reported)
+    void build_ids(const float* p, int64_t n_all, const std::vector<int32_t>& ids) {
+        xyz.assign(p, p + 3 * n_all);
+        perm = ids;
+        const int64_t n = (int64_t)perm.size();
         nodes.clear();
         nodes.reserve(2 * (n / LEAF + 1) + 8);
         if (n > 0) build_rec(0, (int)n);
@@ -1138,6 +1145,216 @@ int icp_align(const float* src, int64_t ns, const float* dst, int64_t nd, const 
     return 0;
 }
 
+
+// ---------------------------------------------------------------------------
+// Incremental map maintenance.
+//
+// DynMap: every point ever inserted keeps its id (insertion order); deleted
+// points stay as tombstones.  The kNN tree is rebuilt over the alive ids.
+//
+// add_points   = ikd-Tree KD_TREE::Add_Points(PointToAdd, downsample_on) [U]:
+//   for each point p (in order), with downsample:
+//     box  = [floor(p/ds)*ds, +ds) per axis (float), half-open like
+//            Search_by_range's `min <= x < max` [U]
+//     mid  = box_min + (box_max - box_min)/2.0 (double, stored float)
+//     S    = alive points in the box; winner = p, then any s in S with
+//            calc_dist(s, mid) < calc_dist(winner, mid) (strict, first wins)
+//     if |S| > 1 || same_point(p, winner): delete the box, add the winner
+//   without downsample: plain add.
+//   Ids: the survivor of a box keeps its id when it was already in the map;
+//   new survivors get ids appended in input order when the call ends (a new
+//   point superseded later in the same call never receives an id).  The
+//   ikd-Tree re-inserts a surviving point as a new node; ids are internal to
+//   this restatement and the GPU path, so the point set is what matches.
+// delete_boxes = KD_TREE::Delete_Point_Boxes [U]: alive points with
+//   min <= x < max on all axes are deleted.
+// map_incremental = FAST-LIO laserMapping.cpp map_incremental() [U]: see
+//   classify() below.
+// ---------------------------------------------------------------------------
+static inline float calc_dist3(const float* a, const float* b) { return sqdist(a, b); }
+static inline bool same_point3(const float* a, const float* b) {
+    return std::fabs(a[0] - b[0]) < 1e-6f && std::fabs(a[1] - b[1]) < 1e-6f && std::fabs(a[2] - b[2]) < 1e-6f;
+}
+
+struct DynMap {
+    std::vector<float> xyz;      // all ids
+    std::vector<uint8_t> alive;  // per id
+    KdTree tree;
+    bool dirty = true;
+
+    int64_t n_ids() const { return (int64_t)alive.size(); }
+    void refresh() {
+        if (!dirty) return;
+        std::vector<int32_t> ids;
+        for (int64_t i = 0; i < n_ids(); ++i)
+            if (alive[i]) ids.push_back((int32_t)i);
+        tree.build_ids(xyz.data(), n_ids(), ids);
+        dirty = false;
+    }
+    int64_t alive_count() const {
+        int64_t c = 0;
+        for (uint8_t a : alive) c += a;
+        return c;
+    }
+
+    int64_t add_points(const float* p, int64_t n, bool downsample, float ds) {
+        if (!downsample) {
+            for (int64_t i = 0; i < 3 * n; ++i) xyz.push_back(p[i]);
+            alive.insert(alive.end(), (size_t)n, 1);
+            dirty = true;
+            return n;
+        }
+        // pending new points (index into p), alive until superseded.  Candidate
+        // lookup through integer voxel buckets (the exact float box test below
+        // decides; the 27 neighbouring buckets cover any rounding at the faces).
+        std::vector<uint8_t> pend(n, 0);
+        int64_t counter = 0;
+        auto bkey = [ds](const float* a) {
+            const int64_t kx = (int64_t)std::floor(a[0] / ds), ky = (int64_t)std::floor(a[1] / ds),
+                          kz = (int64_t)std::floor(a[2] / ds);
+            return ((kx + (1 << 20)) << 42) | ((ky + (1 << 20)) << 21) | (kz + (1 << 20));
+        };
+        std::unordered_map<int64_t, std::vector<int64_t>> bmap, bnew;
+        for (int64_t id = 0; id < n_ids(); ++id)
+            if (alive[id]) bmap[bkey(&xyz[3 * id])].push_back(id);
+        auto gather = [&](std::unordered_map<int64_t, std::vector<int64_t>>& bm, int64_t k0, std::vector<int64_t>& out) {
+            for (int dx = -1; dx <= 1; ++dx)
+                for (int dy = -1; dy <= 1; ++dy)
+                    for (int dz = -1; dz <= 1; ++dz) {
+                        auto it = bm.find(k0 + ((int64_t)dx << 42) + ((int64_t)dy << 21) + dz);
+                        if (it != bm.end()) out.insert(out.end(), it->second.begin(), it->second.end());
+                    }
+            std::sort(out.begin(), out.end());
+        };
+        for (int64_t i = 0; i < n; ++i) {
+            const float* q = p + 3 * i;
+            float vmin[3], vmax[3], mid[3];
+            for (int d = 0; d < 3; ++d) {
+                vmin[d] = std::floor(q[d] / ds) * ds;
+                vmax[d] = vmin[d] + ds;
+                mid[d] = (float)((double)vmin[d] + (double)(vmax[d] - vmin[d]) / 2.0);
+            }
+            auto inbox = [&](const float* a) {
+                return vmin[0] <= a[0] && vmax[0] > a[0] && vmin[1] <= a[1] && vmax[1] > a[1] && vmin[2] <= a[2] &&
+                       vmax[2] > a[2];
+            };
+            // storage: alive map points in id order, then pending new points in input order
+            std::vector<int64_t> cand_map, cand_new, st_map, st_new;
+            const int64_t k0 = bkey(q);
+            gather(bmap, k0, cand_map);
+            gather(bnew, k0, cand_new);
+            for (int64_t id : cand_map)
+                if (alive[id] && inbox(&xyz[3 * id])) st_map.push_back(id);
+            for (int64_t j : cand_new)
+                if (pend[j] && inbox(p + 3 * j)) st_new.push_back(j);
+        const size_t ns = st_map.size() + st_new.size();
+            float md = calc_dist3(q, mid);
+            const float* win = q;
+            int64_t win_map = -1, win_new = i;
+            for (int64_t id : st_map) {
+                const float t = calc_dist3(&xyz[3 * id], mid);
+                if (t < md) { md = t; win = &xyz[3 * id]; win_map = id; win_new = -1; }
+            }
+            for (int64_t j : st_new) {
+                const float t = calc_dist3(p + 3 * j, mid);
+                if (t < md) { md = t; win = p + 3 * j; win_map = -1; win_new = j; }
+            }
+            if (ns > 1 || same_point3(q, win)) {
+                for (int64_t id : st_map)
+                    if (id != win_map) alive[id] = 0;
+                for (int64_t j : st_new)
+                    if (j != win_new) pend[j] = 0;
+                if (win_new == i) {
+                    pend[i] = 1;
+                    bnew[k0].push_back(i);
+                }
+                ++counter;
+            }
+        }
+        for (int64_t i = 0; i < n; ++i)
+            if (pend[i]) {
+                xyz.insert(xyz.end(), p + 3 * i, p + 3 * i + 3);
+                alive.push_back(1);
+            }
+        dirty = true;
+        return counter;
+    }
+
+    int64_t delete_boxes(const float* boxes, int nb) {
+        int64_t cnt = 0;
+        for (int64_t id = 0; id < n_ids(); ++id) {
+            if (!alive[id]) continue;
+            const float* a = &xyz[3 * id];
+            for (int b = 0; b < nb; ++b) {
+                const float* bx = boxes + 6 * b;
+                if (bx[0] <= a[0] && bx[3] > a[0] && bx[1] <= a[1] && bx[4] > a[1] && bx[2] <= a[2] && bx[5] > a[2]) {
+                    alive[id] = 0;
+                    ++cnt;
+                    break;
+                }
+            }
+        }
+        dirty = true;
+        return cnt;
+    }
+};
+
+// map_incremental() [U]: Nearest_Points come from the last kNN evaluation
+// (unbounded 5-NN at pose_knn: ikd-Tree Nearest_Search with max_dist = INF);
+// the world points use the final state.  Per point:
+//   mid  = floor(w/fs)*fs + 0.5*fs (double, stored float); dist = calc_dist(w, mid)
+//   |near0 - mid| > 0.5*fs on all three axes          -> PointNoNeedDownsample
+//   else need_add unless some near_j (j < 5, only when 5 exist) has
+//        calc_dist(near_j, mid) < dist                 -> PointToAdd / skip
+//   then Add_Points(PointToAdd, true); Add_Points(PointNoNeedDownsample, false).
+// stats: [to_add, no_need, skipped, added_by_downsample_call]
+static void map_incremental(DynMap& dm, const float* body, int64_t n, const Pose& pk, const Pose& pf, double fs,
+                            float ds, int64_t* stats) {
+    dm.refresh();
+    std::vector<float> to_add, no_need;
+    int64_t skipped = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        float wk[3], w[3];
+        body_to_world(pk, body + 3 * i, wk);
+        body_to_world(pf, body + 3 * i, w);
+        int32_t nn[5];
+        float d2[5];
+        const int found = dm.tree.knn(wk, 5, INFINITY, nn, d2);
+        if (found == 0) {
+            to_add.insert(to_add.end(), w, w + 3);
+            continue;
+        }
+        float mid[3];
+        for (int d = 0; d < 3; ++d) mid[d] = (float)(std::floor((double)w[d] / fs) * fs + 0.5 * fs);
+        const float dist = calc_dist3(w, mid);
+        const float* n0 = &dm.xyz[3 * (size_t)nn[0]];
+        if (std::fabs(n0[0] - mid[0]) > 0.5 * fs && std::fabs(n0[1] - mid[1]) > 0.5 * fs &&
+            std::fabs(n0[2] - mid[2]) > 0.5 * fs) {
+            no_need.insert(no_need.end(), w, w + 3);
+            continue;
+        }
+        bool need_add = true;
+        for (int j = 0; j < 5; ++j) {
+            if (found < 5) break;
+            if (calc_dist3(&dm.xyz[3 * (size_t)nn[j]], mid) < dist) {
+                need_add = false;
+                break;
+            }
+        }
+        if (need_add)
+            to_add.insert(to_add.end(), w, w + 3);
+        else
+            ++skipped;
+    }
+    const int64_t na = (int64_t)to_add.size() / 3, nn_ = (int64_t)no_need.size() / 3;
+    const int64_t c = dm.add_points(to_add.data(), na, true, ds);
+    dm.add_points(no_need.data(), nn_, false, ds);
+    stats[0] = na;
+    stats[1] = nn_;
+    stats[2] = skipped;
+    stats[3] = c;
+}
+
 }  // namespace orc
 
 // =============================================================================
@@ -1152,7 +1369,46 @@ struct orc_state {
 };
 struct orc_icp_params { double max_corr_dist, trans_eps, fitness_eps; int max_iter; double rot_eps, score_threshold; };
 
-int orc_version(void) { return 1; }
+int orc_version(void) { return 2; }
+
+// ---- incremental map (DynMap) ----
+void* orc_dmap_create(const float* xyz, int64_t n) {
+    auto* d = new orc::DynMap();
+    d->xyz.assign(xyz, xyz + 3 * n);
+    d->alive.assign((size_t)n, 1);
+    return d;
+}
+void orc_dmap_free(void* m) { delete (orc::DynMap*)m; }
+int64_t orc_dmap_num_ids(void* m) { return ((orc::DynMap*)m)->n_ids(); }
+int64_t orc_dmap_alive_count(void* m) { return ((orc::DynMap*)m)->alive_count(); }
+int orc_dmap_get(void* m, float* xyz, uint8_t* alive) {
+    auto* d = (orc::DynMap*)m;
+    if (xyz) std::memcpy(xyz, d->xyz.data(), d->xyz.size() * sizeof(float));
+    if (alive) std::memcpy(alive, d->alive.data(), d->alive.size());
+    return 0;
+}
+int64_t orc_dmap_add(void* m, const float* xyz, int64_t n, int downsample, float ds) {
+    return ((orc::DynMap*)m)->add_points(xyz, n, downsample != 0, ds);
+}
+int64_t orc_dmap_delete_boxes(void* m, const float* boxes, int nb) {
+    return ((orc::DynMap*)m)->delete_boxes(boxes, nb);
+}
+int orc_dmap_knn(void* m, const float* q, int64_t nq, int k, float range_sq, int32_t* idx, float* d2) {
+    if (k < 1 || k > 8) return -1;
+    auto* d = (orc::DynMap*)m;
+    d->refresh();
+    for (int64_t i = 0; i < nq; ++i) d->tree.knn(q + 3 * i, k, range_sq, idx + (size_t)k * i, d2 + (size_t)k * i);
+    return 0;
+}
+int orc_map_incremental(void* m, const float* body, int64_t n, const double* pose_knn24, const double* pose24,
+                        double fs, float ds, int64_t* stats4) {
+    orc::Pose pk, pf;
+    std::memcpy(&pk, pose_knn24, sizeof(pk));
+    std::memcpy(&pf, pose24, sizeof(pf));
+    orc::map_incremental(*(orc::DynMap*)m, body, n, pk, pf, fs, ds, stats4);
+    return 0;
+}
+
 
 void* orc_map_build(const float* xyz, int64_t n) {
     auto* t = new orc::KdTree();

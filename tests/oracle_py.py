@@ -78,6 +78,23 @@ def lib():
                                     C.POINTER(IcpParams), C.POINTER(C.c_float), C.POINTER(C.c_float),
                                     C.POINTER(C.c_double), C.POINTER(C.c_float), C.POINTER(C.c_double),
                                     C.c_int, C.c_int]
+        vp, i64 = C.c_void_p, C.c_int64
+        L.orc_dmap_create.restype = vp
+        L.orc_dmap_create.argtypes = [C.POINTER(C.c_float), i64]
+        L.orc_dmap_free.argtypes = [vp]
+        L.orc_dmap_num_ids.restype = i64
+        L.orc_dmap_num_ids.argtypes = [vp]
+        L.orc_dmap_alive_count.restype = i64
+        L.orc_dmap_alive_count.argtypes = [vp]
+        L.orc_dmap_get.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(C.c_uint8)]
+        L.orc_dmap_add.restype = i64
+        L.orc_dmap_add.argtypes = [vp, C.POINTER(C.c_float), i64, C.c_int, C.c_float]
+        L.orc_dmap_delete_boxes.restype = i64
+        L.orc_dmap_delete_boxes.argtypes = [vp, C.POINTER(C.c_float), C.c_int]
+        L.orc_dmap_knn.argtypes = [vp, C.POINTER(C.c_float), i64, C.c_int, C.c_float, C.POINTER(C.c_int32),
+                                   C.POINTER(C.c_float)]
+        L.orc_map_incremental.argtypes = [vp, C.POINTER(C.c_float), i64, C.POINTER(C.c_double),
+                                          C.POINTER(C.c_double), C.c_double, C.c_float, C.POINTER(C.c_int64)]
         _lib = L
     return _lib
 
@@ -176,3 +193,56 @@ def icp_align(src, dst, params=None, guess=None, threads=8, max_trace=64, want_a
     it = int(out[2])
     return dict(T=T.reshape(4, 4), fitness=out[0], converged=bool(out[1]), iterations=it, state=int(out[3]),
                 is_valid=bool(out[4]), trace=trace.reshape(max_trace, 20)[:it], aligned=aligned)
+
+
+class OracleDynMap:
+    """Incremental map restatement: ikd-Tree Add_Points / Delete_Point_Boxes and
+    FAST-LIO map_incremental() semantics (oracle/lio_oracle.cpp DynMap)."""
+
+    def __init__(self, xyz: np.ndarray):
+        xyz = np.ascontiguousarray(xyz, dtype=np.float32).reshape(-1, 3)
+        self.h = lib().orc_dmap_create(_p(xyz, C.c_float), len(xyz))
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.orc_dmap_free(self.h)
+            self.h = None
+
+    def num_ids(self):
+        return int(lib().orc_dmap_num_ids(self.h))
+
+    def size(self):
+        return int(lib().orc_dmap_alive_count(self.h))
+
+    def by_id(self):
+        n = self.num_ids()
+        xyz = np.empty((n, 3), np.float32)
+        alive = np.empty(n, np.uint8)
+        lib().orc_dmap_get(self.h, _p(xyz, C.c_float), _p(alive, C.c_uint8))
+        return xyz, alive.astype(bool)
+
+    def add(self, xyz, downsample, ds=0.5):
+        xyz = np.ascontiguousarray(xyz, dtype=np.float32).reshape(-1, 3)
+        return int(lib().orc_dmap_add(self.h, _p(xyz, C.c_float), len(xyz), int(downsample), C.c_float(ds)))
+
+    def delete_boxes(self, boxes):
+        b = np.ascontiguousarray(boxes, dtype=np.float32).reshape(-1, 6)
+        return int(lib().orc_dmap_delete_boxes(self.h, _p(b, C.c_float), len(b)))
+
+    def knn(self, q, k=5, range_sq=5.0):
+        q = np.ascontiguousarray(q, dtype=np.float32).reshape(-1, 3)
+        idx = np.empty((len(q), k), np.int32)
+        d2 = np.empty((len(q), k), np.float32)
+        assert lib().orc_dmap_knn(self.h, _p(q, C.c_float), len(q), k, C.c_float(range_sq), _p(idx, C.c_int32),
+                                  _p(d2, C.c_float)) == 0
+        return idx, d2
+
+    def map_incremental(self, body, pose_knn24, pose24, fs=0.5, ds=0.5):
+        body = np.ascontiguousarray(body, dtype=np.float32).reshape(-1, 3)
+        pk = np.ascontiguousarray(pose_knn24, dtype=np.float64)
+        pf = np.ascontiguousarray(pose24, dtype=np.float64)
+        st = np.zeros(4, np.int64)
+        lib().orc_map_incremental(self.h, _p(body, C.c_float), len(body), _p(pk, C.c_double), _p(pf, C.c_double),
+                                  float(fs), C.c_float(ds), _p(st, C.c_int64))
+        return dict(n_to_add=int(st[0]), n_no_downsample=int(st[1]), n_skipped=int(st[2]),
+                    n_added_downsample=int(st[3]))

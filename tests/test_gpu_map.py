@@ -1,0 +1,119 @@
+"""GPU parity of the incremental map against the oracle.
+
+Bars: the map content (every id's xyz + alive flag) bit-exact after each
+Add_Points / Delete_Point_Boxes / map_incremental; the reference's counters
+equal; kNN over the updated map bit-exact (ids + sq-distances).
+"""
+import numpy as np
+import pytest
+
+from lio_gpu import frontend as F
+from lio_gpu import synth
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def scene_scans():
+    scene, m, scans = synth.make_config("C1", n_scans=4)
+    return scene, m, scans
+
+
+def _same_map(tree, om):
+    gx, ga = tree.by_id()
+    ox, oa = om.by_id()
+    assert gx.shape == ox.shape
+    np.testing.assert_array_equal(ga, oa)
+    np.testing.assert_array_equal(gx, ox)
+    assert tree.size() == om.size()
+
+
+def _knn_parity(tree, om, q):
+    hm = F.HShareModelGPU(tree)
+    hm.set_scan(q)  # identity pose: world = body
+    p24 = np.zeros(24)
+    p24[0:9] = np.eye(3).ravel()
+    p24[12:21] = np.eye(3).ravel()
+    hm(p24, True)
+    gi, gd = hm.nearest_points()
+    oi, od = om.knn(q, 5, 5.0)
+    np.testing.assert_array_equal(gi, oi)
+    np.testing.assert_array_equal(gd, od)
+    hm.close()
+
+
+def test_add_points_downsample_parity(oracle, scene_scans):
+    _, m, scans = scene_scans
+    base = m[:60000]
+    tree = F.IkdTreeGPU(cell_size=1.0, downsample_size=0.5)
+    tree.Build(base)
+    om = oracle.OracleDynMap(base)
+    for k, sc in enumerate(scans[:3]):
+        w = oracle.body_to_world(synth.pose24(synth.initial_state(sc.pos_gt, sc.rot_gt)), sc.body)
+        c_gpu = tree.Add_Points(w, True)
+        c_orc = om.add(w, True, 0.5)
+        assert c_gpu == c_orc
+        _same_map(tree, om)
+    assert om.num_ids() > om.size()  # replaced points became tombstones
+    _knn_parity(tree, om, scans[3].body + np.float32([3.0, 1.0, 0.0]))
+
+
+def test_add_points_plain_and_delete_boxes(oracle, scene_scans):
+    _, m, scans = scene_scans
+    base = m[:40000]
+    tree = F.IkdTreeGPU(cell_size=1.0)
+    tree.Build(base)
+    om = oracle.OracleDynMap(base)
+    extra = m[40000:52000]
+    assert tree.Add_Points(extra, False) == len(extra)
+    om.add(extra, False)
+    _same_map(tree, om)
+    lo, hi = base.min(0), base.max(0)
+    mid = (lo + hi) / 2
+    boxes = np.array([[lo[0] - 1, lo[1] - 1, lo[2] - 1, mid[0], mid[1], hi[2] + 1],
+                      [mid[0] + 5, lo[1] - 1, lo[2] - 1, mid[0] + 20, hi[1] + 1, mid[2]]], np.float32)
+    n_gpu = tree.Delete_Point_Boxes(boxes)
+    n_orc = om.delete_boxes(boxes)
+    assert n_gpu == n_orc > 0
+    _same_map(tree, om)
+    q = base[::97] + np.float32([0.05, -0.03, 0.02])
+    _knn_parity(tree, om, q)
+
+
+def test_add_outside_grid_rebuilds(oracle, scene_scans):
+    _, m, _ = scene_scans
+    base = m[:20000]
+    tree = F.IkdTreeGPU(cell_size=1.0)
+    tree.Build(base)
+    om = oracle.OracleDynMap(base)
+    far = base[:3000] + np.float32([500.0, -300.0, 40.0])  # leaves the grid: full rebuild path
+    assert tree.Add_Points(far, True) == om.add(far, True, 0.5)
+    _same_map(tree, om)
+    _knn_parity(tree, om, far[::7] + np.float32([0.1, 0.1, 0.0]))
+
+
+def test_map_incremental_parity(oracle, scene_scans):
+    """Scan-to-map sequence: build from the first scan, then per scan an IESKF
+    update on the GPU followed by map_incremental; the oracle replays
+    map_incremental with the same kNN pose / final pose."""
+    _, _, scans = scene_scans
+    sc0 = scans[0]
+    p0 = synth.pose24(synth.initial_state(sc0.pos_gt, sc0.rot_gt))
+    first = oracle.body_to_world(p0, sc0.body)
+    tree = F.IkdTreeGPU(cell_size=1.0, downsample_size=0.5)
+    tree.Build(first)
+    om = oracle.OracleDynMap(first)
+    for sc in scans[1:]:
+        hm = F.HShareModelGPU(tree)
+        hm.set_scan(sc.body)
+        kf = F.EsekfGPU(hm, laser_point_cov=0.001, max_iteration=3, epsi=0.001)
+        x, P, st = kf.update_iterated_dyn_share_modified(synth.initial_state(sc.pos_init, sc.rot_init),
+                                                         synth.initial_cov())
+        p_knn = hm.last_knn_pose24()
+        p_fin = synth.pose24(x)
+        s_gpu = hm.map_incremental(p_fin, 0.5)
+        s_orc = om.map_incremental(sc.body, p_knn, p_fin, 0.5, 0.5)
+        assert s_gpu == s_orc
+        _same_map(tree, om)
+        hm.close()
+    assert s_orc["n_to_add"] > 0
