@@ -33,6 +33,16 @@ BYTES_PER_PT_REUSE = 32      # h-evaluation reusing kNN
 BYTES_PER_PT_ICP = 24        # per ICP iteration and source point
 
 
+def _cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -44,7 +54,10 @@ def parse():
     ap.add_argument("--no-icp", action="store_true")
     ap.add_argument("--icp-reps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline sample at all cores "
+                    "(plus half of it at 1 and at 3 threads)")
+    ap.add_argument("--grow-scans", type=int, default=20,
+                    help="C3/C5: scans appended through map_incremental before timing (SURVEY §8d)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"),
                     help="per-launch HBM traffic measured with rocprofv3 --pmc (profiles/)")
     return ap.parse_args()
@@ -105,11 +118,32 @@ def main():
         hm.set_scan_device(d_scans[j].data_ptr(), len(scans[j].body))
         return kf.update_iterated_dyn_share_modified(states[j], P0)
 
+    # C3/C5: the map is grown through the insert path (FAST-LIO map_incremental
+    # after each update, filter_size_map = 0.5, kitti.launch:10) before timing
+    incr = None
+    if args.config in ("C3", "C5") and args.grow_scans > 0:
+        grow = []
+        for k in range(args.grow_scans):
+            x = -0.15 * L + 1.85 + (k + rank * args.grow_scans) * 3.7
+            grow.append(synth.make_scan(scene, sp, kind, pos_gt=[x, 0.6 * np.sin(0.7 * k + 0.3), 0.0],
+                                        yaw_gt=0.05 * np.sin(0.3 * k + 0.2), seed=5099 + k + 1000 * rank))
+        d_grow = [torch.from_numpy(s.body).to(dev) for s in grow]
+        torch.cuda.synchronize()
+        t_incr = 0.0
+        added = 0
+        for k, s in enumerate(grow):
+            hm.set_scan_device(d_grow[k].data_ptr(), len(s.body))
+            xg, _, _ = kf.update_iterated_dyn_share_modified(synth.initial_state(s.pos_init, s.rot_init), P0)
+            ti = time.perf_counter()
+            st_i = hm.map_incremental(synth.pose24(xg), 0.5)
+            t_incr += time.perf_counter() - ti
+            added += st_i["n_to_add"] + st_i["n_no_downsample"]
+        incr = {"scans": len(grow), "ms_per_scan": round(t_incr / len(grow) * 1e3, 3),
+                "points_offered_per_scan": round(added / len(grow), 1), "map_size_after": tree.size(),
+                "map_ids_after": tree.num_ids()}
+
     for k in range(args.warmup):
         step(k)
-    barrier()
-    hm.reset_timing()
-    hm.set_timing(True)
     h_evals = knn_calls = 0
     pos_err = []
     barrier()
@@ -122,6 +156,12 @@ def main():
             pos_err.append(float(np.linalg.norm(x["pos"] - scans[k % len(scans)].pos_gt)))
     barrier()
     elapsed = time.perf_counter() - t_start
+    # kernel durations for the roofline: a separate pass with HIP events on the
+    # ctx stream (events cost host time, so they stay out of the timed region)
+    hm.reset_timing()
+    hm.set_timing(True)
+    for k in range(min(args.steps, 50)):
+        step(k)
     hm.set_timing(False)
     tm = hm.timing()
     if dist is not None:
@@ -135,6 +175,8 @@ def main():
 
     n_pts = sp
     knn_avg_ms = tm["knn_ms"] / max(tm["knn_launches"], 1)
+    near_avg_ms = tm["near_ms"] / max(tm["near_launches"], 1)
+    far_avg_ms = tm["far_ms"] / max(tm["far_launches"], 1)
     reuse_avg_ms = tm["reuse_ms"] / max(tm["reuse_launches"], 1)
     achieved = BYTES_PER_PT_KNN * n_pts / (knn_avg_ms * 1e-3) / 1e9 if tm["knn_launches"] else None
     traffic = None
@@ -145,10 +187,17 @@ def main():
                 traffic = pmc.get("knn_hbm_bytes_per_launch")
         except Exception:
             traffic = None
+    # unit of work = one kNN h-evaluation (112 B/pt), which runs as
+    # knn_near_kernel + knn_far_kernel + plane_kernel back to back on the ctx
+    # stream; achieved = algorithmic bytes / the bracketed duration (HIP events
+    # on that stream, a separate pass after the timed loop)
     roofline = {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
-                "traffic": traffic, "kernel": "h_model_kernel<REDO_KNN=true>",
+                "traffic": traffic,
+                "kernel": "kNN h-evaluation = knn_near_kernel + knn_far_kernel + plane_kernel",
                 "bytes_per_launch": BYTES_PER_PT_KNN * n_pts, "avg_launch_ms": round(knn_avg_ms, 5),
+                "near_kernel_avg_ms": round(near_avg_ms, 5), "far_kernel_avg_ms": round(far_avg_ms, 5),
+                "plane_kernel_avg_ms": round(knn_avg_ms - near_avg_ms - far_avg_ms, 5),
                 "reuse_kernel_avg_ms": round(reuse_avg_ms, 5),
                 "reuse_achieved_gbs": round(BYTES_PER_PT_REUSE * n_pts / (reuse_avg_ms * 1e-3) / 1e9, 2)
                 if tm["reuse_launches"] else None}
@@ -199,22 +248,31 @@ def main():
         import oracle_py as O
 
         threads = min(os.cpu_count() or 1, 16)
-        om = O.OracleMap(mappts)
-        done = 0
-        cpu_iters = 0
-        tc = time.perf_counter()
-        while True:
-            s = scans[done % len(scans)]
-            _, _, so, _ = O.ieskf_update(om, s.body, states[done % len(scans)], P0, threads=threads)
-            done += 1
-            cpu_iters += int(so[0])
-            if time.perf_counter() - tc > args.cpu_seconds and done >= 3:
-                break
-        cpu_s = time.perf_counter() - tc
+        om = O.OracleMap(tree.points() if incr else mappts)  # the same map content as the GPU's
+
+        def cpu_rate(nthr, seconds):
+            done = iters = 0
+            tc = time.perf_counter()
+            while True:
+                s = scans[done % len(scans)]
+                _, _, so, _ = O.ieskf_update(om, s.body, states[done % len(scans)], P0, threads=nthr)
+                done += 1
+                iters += int(so[0])
+                if time.perf_counter() - tc > seconds and done >= 3:
+                    break
+            el = time.perf_counter() - tc
+            return done, iters, el
+
+        done, cpu_iters, cpu_s = cpu_rate(threads, args.cpu_seconds)
+        by_thr = {}
+        for nthr in (1, 3):  # 1 thread and FAST-LIO's MP_PROC_NUM = 3
+            d1, _, e1 = cpu_rate(nthr, args.cpu_seconds / 2)
+            by_thr[str(nthr)] = round(d1 / e1, 3)
         cpu = {"value": round(done / cpu_s, 3), "unit": "scans/s", "cores": threads, "kind": "port",
                "sample": f"{done} full IESKF updates of {args.config} scans ({sp} pts vs {mp} pts map), "
                          f"oracle/lio_oracle.cpp kd-tree + OpenMP, {cpu_s:.1f} s",
-               "ms_per_iteration": round(cpu_s / max(cpu_iters, 1) * 1e3, 3)}
+               "ms_per_iteration": round(cpu_s / max(cpu_iters, 1) * 1e3, 3),
+               "scans_per_s_by_threads": by_thr, "host_cpus": os.cpu_count(), "cpu_model": _cpu_model()}
 
     if rank == 0:
         line = {
@@ -223,7 +281,9 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32/f64",
             "data": "synthetic (seeded urban-canyon scene, ray-cast scans; no datasets offline)",
-            "config": {"workload": f"{args.config}: {sp}-pt {kind} scan vs {mp}-pt static map, "
+            "config": {"workload": f"{args.config}: {sp}-pt {kind} scan vs {mp}-pt "
+                                   + (f"map grown by {incr['scans']} scans (map_incremental)" if incr else "static map")
+                                   + ", "
                                    "max_iteration=3 (<=4 h-evals/scan)",
                        "scan_points": sp, "map_points": mp, "resident_scans": len(scans),
                        "parallelism": f"replicas x{world} (front end does not shard)"},
@@ -231,7 +291,7 @@ def main():
             "h_evals_per_scan": round(h_evals / args.steps, 3), "knn_evals_per_scan": round(knn_calls / args.steps, 3),
             "pos_err_m": round(float(np.mean(pos_err)), 5) if pos_err else None,
             "map_build_ms": round(build_ms, 2), "input_gen_s": round(gen_s, 1),
-            "roofline": roofline, "cpu_baseline": cpu, "loop_icp": loop_icp,
+            "roofline": roofline, "cpu_baseline": cpu, "loop_icp": loop_icp, "map_incremental": incr,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:

@@ -370,22 +370,35 @@ int update_iterated(State& x, Mat& P, double R, int max_iter, double epsi, const
                 for (int c = 0; c < 6; ++c) K_x[(size_t)r * N + c] = kx[c];
             }
         } else {
-            Mat Pt((size_t)N * N);
-            for (size_t q = 0; q < Pt.size(); ++q) Pt[q] = P[q] / R;
-            if (!lu_inverse(Pt, N)) return -4;
+            // Reference: P_temp = (P/R)^-1; P_temp[:6,:6] += HTH; P_inv = P_temp^-1;
+            // K_h = P_inv[:, :6] HTh; K_x[:, :6] = P_inv[:, :6] HTH.  Only P_inv's
+            // first 6 columns are used, and with A = P/R, E = [I6; 0]:
+            //   (A^-1 + E HTH E^T)^-1 E = A E (I6 + HTH A11)^-1   (Woodbury + push-through)
+            // so one 6x6 inverse replaces the two 23x23 inverses (equal in exact
+            // arithmetic; the IESKF parity bar is a tolerance).
             double HTH[36];
             unpack_hth(hm.sums, HTH);
+            Mat Mm(36);
             for (int a = 0; a < 6; ++a)
-                for (int b = 0; b < 6; ++b) Pt[(size_t)a * N + b] += HTH[6 * a + b];
-            if (!lu_inverse(Pt, N)) return -4;  // P_inv
+                for (int b = 0; b < 6; ++b) {
+                    double s = 0;
+                    for (int m = 0; m < 6; ++m) s += HTH[6 * a + m] * (P[(size_t)m * N + b] / R);
+                    Mm[(size_t)a * 6 + b] = s + (a == b ? 1.0 : 0.0);
+                }
+            if (!lu_inverse(Mm, 6)) return -4;
             for (int r = 0; r < N; ++r) {
-                const double* pr = &Pt[(size_t)r * N];
+                double q[6];
+                for (int c = 0; c < 6; ++c) {
+                    double s = 0;
+                    for (int m = 0; m < 6; ++m) s += (P[(size_t)r * N + m] / R) * Mm[(size_t)m * 6 + c];
+                    q[c] = s;
+                }
                 double kh = 0;
-                for (int c = 0; c < 6; ++c) kh += pr[c] * hm.sums[21 + c];
+                for (int c = 0; c < 6; ++c) kh += q[c] * hm.sums[21 + c];
                 K_h[r] = kh;
                 for (int c = 0; c < 6; ++c) {
                     double s = 0;
-                    for (int m = 0; m < 6; ++m) s += pr[m] * HTH[6 * m + c];
+                    for (int m = 0; m < 6; ++m) s += q[m] * HTH[6 * m + c];
                     K_x[(size_t)r * N + c] = s;
                 }
             }

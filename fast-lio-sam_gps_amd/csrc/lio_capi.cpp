@@ -111,6 +111,7 @@ struct lio_ctx {
     bool timing = false;
     lio_kernel_timing tm{};
     EventPair ev_main, ev_fin;
+    hipEvent_t ev_marks[2] = {nullptr, nullptr};  // after near / after far (redo)
 };
 
 extern "C" {
@@ -372,6 +373,7 @@ int lio_ctx_create(lio_map* m, const lio_match_params* p, lio_ctx** out) {
         (void)hipEventCreate(&e->a);
         (void)hipEventCreate(&e->b);
     }
+    for (hipEvent_t& e : c->ev_marks) (void)hipEventCreate(&e);
     *out = c;
     return LIO_OK;
 }
@@ -389,6 +391,8 @@ int lio_ctx_destroy(lio_ctx* c) {
         if (e->a) (void)hipEventDestroy(e->a);
         if (e->b) (void)hipEventDestroy(e->b);
     }
+    for (hipEvent_t e : c->ev_marks)
+        if (e) (void)hipEventDestroy(e);
     delete c;
     return LIO_OK;
 }
@@ -493,7 +497,7 @@ int lio_match(lio_ctx* c, const lio_pose* pose, int redo_knn, double* sums) {
         return LIO_OK;
     }
     if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.a, st));
-    const int nb = lio::launch_h_model(a, redo_knn != 0, st);
+    const int nb = lio::launch_h_model(a, redo_knn != 0, st, c->timing && redo_knn ? c->ev_marks : nullptr);
     if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.b, st));
     lio::launch_finalize(c->d_partials, nb, c->d_sums, st);
     if (c->timing) HIP_TRY(hipEventRecord(c->ev_fin.b, st));
@@ -502,8 +506,12 @@ int lio_match(lio_ctx* c, const lio_pose* pose, int redo_knn, double* sums) {
     HIP_TRY(hipStreamSynchronize(st));
     std::memcpy(sums, c->h_sums, LIO_SUMS_LEN * sizeof(double));
     if (c->timing) {
-        if (redo_knn)
+        if (redo_knn) {
             accum_event(c->ev_main, c->tm.knn_launches, c->tm.knn_ms);
+            EventPair n{c->ev_main.a, c->ev_marks[0]}, f{c->ev_marks[0], c->ev_marks[1]};
+            accum_event(n, c->tm.near_launches, c->tm.near_ms);
+            accum_event(f, c->tm.far_launches, c->tm.far_ms);
+        }
         else
             accum_event(c->ev_main, c->tm.reuse_launches, c->tm.reuse_ms);
         EventPair f{c->ev_main.b, c->ev_fin.b};

@@ -29,7 +29,8 @@ struct MatchArgs {
     double s_gate;
 };
 
-int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st);
+// marks (optional, redo only): events recorded after the near and the far kernel
+int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* marks = nullptr);
 void launch_finalize(const double* partials, int nblocks, double* out, hipStream_t st);
 void launch_debug(const MatchArgs& a, float* world, float* d2, float* abcd_pd2, hipStream_t st);
 void launch_h_rows(const MatchArgs& a, double* rows, int64_t max_rows, int64_t* n_rows, hipStream_t st);

@@ -354,7 +354,7 @@ __global__ void __launch_bounds__(1024) h_rows_kernel(MatchArgs a, double* __res
 }
 
 // ---------------------------------------------------------------- launchers
-int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st) {
+int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* marks) {
     if (a.n == 0) return 0;
     const int nb = (a.n + kBlock - 1) / kBlock;
     if (redo) {
@@ -364,12 +364,14 @@ int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st) {
             knn_near_kernel<true><<<nq, kKnnBlock, 0, st>>>(a);
         else
             knn_near_kernel<false><<<nq, kKnnBlock, 0, st>>>(a);
+        if (marks) (void)hipEventRecord(marks[0], st);
         static const int far_blocks = [] {  // LIO_FAR_BLOCKS: diagnostics override of the far-pass grid
             const char* e = std::getenv("LIO_FAR_BLOCKS");
             const int v = e ? std::atoi(e) : 0;
             return v > 0 ? std::min(v, 4096) : kFarBlocks;
         }();
         if (a.max_shell > 1) knn_far_kernel<<<far_blocks, kFarBlock, 0, st>>>(a);
+        if (marks) (void)hipEventRecord(marks[1], st);
         plane_kernel<<<nb, kBlock, 0, st>>>(a);
         return nb;
     }

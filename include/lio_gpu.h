@@ -248,10 +248,12 @@ int lio_ctx_get_knn_pose(lio_ctx* c, lio_pose* out);
 
 /* ----------------------------------------------------------------- timing */
 typedef struct lio_kernel_timing {
-    int64_t knn_launches;   double knn_ms;     /* fused kNN + plane + H + reduce kernel */
+    int64_t knn_launches;   double knn_ms;     /* kNN h-evaluation: near + far + plane/H  */
     int64_t reuse_launches; double reuse_ms;   /* converge=false re-evaluation kernel   */
     int64_t final_launches; double final_ms;   /* block-partial finalize kernel          */
     int64_t icp_launches;   double icp_ms;     /* ICP correspondence + statistics kernel */
+    int64_t near_launches;  double near_ms;    /* kNN near pass (inside knn_ms)          */
+    int64_t far_launches;   double far_ms;     /* kNN far pass (inside knn_ms)           */
 } lio_kernel_timing;
 
 /* When enabled, HIP events bracket every hot-kernel launch on the handle's
