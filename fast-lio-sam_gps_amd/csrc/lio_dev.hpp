@@ -10,9 +10,10 @@
 //     the query's cell), each cell pruned by its box distance against the
 //     current K-th best, and the walk stops once the K-th best lies inside the
 //     radius the finished shells guarantee:
-//       group_knn_near  8 lanes per query, shells 0-1 (the common case)
-//       wave_knn_from   64 lanes per query, shells >= 2 (the sparse tail)
-//       group_knn_exact 8 lanes per query, any number of shells
+//       group_knn_near      8 lanes per query, shells 0-1 (the common case)
+//       block_knn_box_flat  a block per query, the rest of its search box
+//                           (the sparse tail, ~0.4% of a dense scan)
+//       group_knn_exact     8 lanes per query, any number of shells
 //   * esti_plane_dev: FAST-LIO esti_plane<float> [U] — Eigen ColPivHouseholderQR
 //     restated in registers, same float operation order as the oracle.
 //
@@ -308,6 +309,89 @@ __device__ __forceinline__ void shell_offset(int s, int k, int& dx, int& dy, int
     }
 }
 
+// Shell 1 of the 3x3x3 block, load-balanced over an aligned group of G = 8
+// lanes.  Lane `sub` judges cells 4*sub .. 4*sub+3 of the block against the
+// (merged, group-uniform) K-th best without memory access, loads the kept
+// cells' [start, end) ranges (8 independent loads), a group prefix sum
+// concatenates the ranges into a slot table in LDS (lds[0..32) range starts,
+// lds[32..65) offsets), and the G lanes then stride the concatenated points,
+// two loads in flight per lane.  The work per group is ceil(points / G)
+// steps whatever the cells' sizes, instead of the largest cell of each lane.
+template <int K, int G>
+__device__ __forceinline__ void scan_shell1_flat(const GridDev& g, float qx, float qy, float qz, int cx, int cy,
+                                                 int cz, float lox, float loy, float loz, int sub, uint32_t* lds,
+                                                 TopK<K>& tk, SearchStats* dbg) {
+    static_assert(G == 8, "scan_shell1_flat: 8-lane groups (4 cells per lane cover the 27-cell block)");
+    const float cs = g.cell, m = g.margin, w = cs + 2.f * m;
+    const float bound = tk.worst();
+    uint32_t b4[4], n4[4];
+    uint32_t lane_total = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int k = 4 * sub + j;
+        const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
+        const int x = cx + dx, y = cy + dy, z = cz + dz;
+        bool keep = k < 27 && k != 13 && (unsigned)x < (unsigned)g.nx && (unsigned)y < (unsigned)g.ny &&
+                    (unsigned)z < (unsigned)g.nz;
+        if (keep) {
+            const float xl = lox + (float)dx * cs - m, yl = loy + (float)dy * cs - m, zl = loz + (float)dz * cs - m;
+            const float bd = (axis_gap(qx, xl, xl + w) + axis_gap(qy, yl, yl + w)) + axis_gap(qz, zl, zl + w);
+            keep = !(bd * 0.999999f > bound);
+        }
+        uint32_t b = 0, e = 0;
+        if (keep) {
+            const uint32_t c = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
+            b = g.start[c];
+            e = g.start[c + 1];
+            if (dbg) dbg->cells += 1;
+        }
+        b4[j] = b;
+        n4[j] = e - b;
+        lane_total += e - b;
+    }
+    uint32_t incl = lane_total;
+#pragma unroll
+    for (int off = 1; off < G; off <<= 1) {
+        const uint32_t v = __shfl_up(incl, off, G);
+        if (sub >= off) incl += v;
+    }
+    const uint32_t T = __shfl(incl, G - 1, G);
+    uint32_t o = incl - lane_total;
+    uint32_t* s_b = lds;
+    uint32_t* s_off = lds + 4 * G;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        s_b[4 * sub + j] = b4[j];
+        s_off[4 * sub + j] = o;
+        o += n4[j];
+    }
+    if (sub == G - 1) s_off[4 * G] = T;
+    if (dbg && sub == 0) dbg->points += (int)T;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    int sl = 0;
+    uint32_t lo = 0, hi = s_off[1];
+    for (uint32_t t = (uint32_t)sub; t < T; t += 2 * G) {
+        while (t >= hi) {
+            lo = hi;
+            hi = s_off[++sl + 1];
+        }
+        const float4 p0 = g.pts[s_b[sl] + (t - lo)];
+        const uint32_t t2 = t + G;
+        float4 p1 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (t2 < T) {
+            while (t2 >= hi) {
+                lo = hi;
+                hi = s_off[++sl + 1];
+            }
+            p1 = g.pts[s_b[sl] + (t2 - lo)];
+        }
+        tk.push(sqdist3(qx, qy, qz, p0.x, p0.y, p0.z), __float_as_int(p0.w));
+        if (t2 < T) tk.push(sqdist3(qx, qy, qz, p1.x, p1.y, p1.z), __float_as_int(p1.w));
+    }
+}
+
 // Lean group walk for dense maps (front-end kNN, ICP near pass), written for
 // occupancy (no per-lane arrays): the own cell lane-strided by the whole group,
 // merge; then lane `sub` takes the shell-1 cells k = sub, sub+G, ... of the
@@ -316,7 +400,7 @@ __device__ __forceinline__ void shell_offset(int s, int k, int& dx, int& dy, int
 // generic walk.  Same result contract as group_knn_exact_from.
 template <int K, int G>
 __device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, int max_shell, int sub, TopK<K>& tk,
-                               SearchStats* dbg = nullptr) {
+                               SearchStats* dbg = nullptr, uint32_t* lds = nullptr) {
     const int cx = cell_coord(qx, g.ox, g.inv_cell);
     const int cy = cell_coord(qy, g.oy, g.inv_cell);
     const int cz = cell_coord(qz, g.oz, g.inv_cell);
@@ -335,18 +419,22 @@ __device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, i
     if (sub != 0) {  // re-seed non-leader lanes (see group_knn_exact_from)
         tk.fill_with_worst();
     }
-    for (int k = sub; k < 27; k += G) {
-        if (k == 13) continue;  // own cell
-        const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
-        const int x = cx + dx, y = cy + dy, z = cz + dz;
-        if ((unsigned)x >= nx || (unsigned)y >= (unsigned)g.ny || (unsigned)z >= (unsigned)g.nz) continue;
-        const float xl = lox + (float)dx * cs - m, yl = loy + (float)dy * cs - m, zl = loz + (float)dz * cs - m;
-        const float w = cs + 2.f * m;
-        const float bd = (axis_gap(qx, xl, xl + w) + axis_gap(qy, yl, yl + w)) + axis_gap(qz, zl, zl + w);
-        if (bd * 0.999999f > tk.worst()) continue;
-        const uint32_t c = (uint32_t)((int)c0 + dz * (int)nxy + dy * (int)nx + dx);
-        if (dbg) dbg->cells += 1;
-        scan_cell_seq<K>(g, c, qx, qy, qz, tk);
+    if (lds) {
+        scan_shell1_flat<K, G>(g, qx, qy, qz, cx, cy, cz, lox, loy, loz, sub, lds, tk, dbg);
+    } else {
+        for (int k = sub; k < 27; k += G) {
+            if (k == 13) continue;  // own cell
+            const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
+            const int x = cx + dx, y = cy + dy, z = cz + dz;
+            if ((unsigned)x >= nx || (unsigned)y >= (unsigned)g.ny || (unsigned)z >= (unsigned)g.nz) continue;
+            const float xl = lox + (float)dx * cs - m, yl = loy + (float)dy * cs - m, zl = loz + (float)dz * cs - m;
+            const float w = cs + 2.f * m;
+            const float bd = (axis_gap(qx, xl, xl + w) + axis_gap(qy, yl, yl + w)) + axis_gap(qz, zl, zl + w);
+            if (bd * 0.999999f > tk.worst()) continue;
+            const uint32_t c = (uint32_t)((int)c0 + dz * (int)nxy + dy * (int)nx + dx);
+            if (dbg) dbg->cells += 1;
+            scan_cell_seq<K>(g, c, qx, qy, qz, tk);
+        }
     }
     group_merge<K, G>(tk);
     if (dbg) dbg->shell = 1;
@@ -357,63 +445,22 @@ __device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, i
     return group_knn_exact_from<K, G>(g, qx, qy, qz, 2, max_shell, sub, tk);
 }
 
-// Far pass: one wave (64 lanes) per query resumes the walk at shell s_first
-// from the list an earlier pass left (identical in every lane, or held by
-// lane 0 with fillers elsewhere).  Lane l takes cells l, l+64, ... of each
-// shell (shell_offset order), prunes them against its own K-th best and scans
-// them sequentially; the wave merges after every shell.  Result in every lane;
-// same contract as group_knn_exact_from.
-template <int K>
-__device__ bool wave_knn_from(const GridDev& g, float qx, float qy, float qz, int s_first, int max_shell, int lane,
-                              TopK<K>& tk) {
-    const int cx = cell_coord(qx, g.ox, g.inv_cell);
-    const int cy = cell_coord(qy, g.oy, g.inv_cell);
-    const int cz = cell_coord(qz, g.oz, g.inv_cell);
-    const float cs = g.cell, m = g.margin, w = cs + 2.f * m;
-    const float lox = g.ox + (float)cx * cs, loy = g.oy + (float)cy * cs, loz = g.oz + (float)cz * cs;
-    float own = fminf(fminf(qx - lox, lox + cs - qx), fminf(qy - loy, loy + cs - qy));
-    own = fminf(own, fminf(qz - loz, loz + cs - qz)) - m;
-    int s0 = s_first;
-    s0 = max(s0, max(-cx, cx - (g.nx - 1)));
-    s0 = max(s0, max(-cy, cy - (g.ny - 1)));
-    s0 = max(s0, max(-cz, cz - (g.nz - 1)));
-    const int smax_grid = max(max(max(cx, g.nx - 1 - cx), max(cy, g.ny - 1 - cy)), max(cz, g.nz - 1 - cz));
-    const int smax = min(max_shell, smax_grid);
-    bool done = false;
-    for (int s = s0; s <= smax && !done; ++s) {
-        if (lane != 0) {  // keep the list in lane 0 only (see group_knn_exact_from)
-            tk.fill_with_worst();
-        }
-        const int ncell = s == 0 ? 1 : 24 * s * s + 2;
-        for (int k = lane; k < ncell; k += 64) {
-            int dx = 0, dy = 0, dz = 0;
-            if (s > 0) shell_offset(s, k, dx, dy, dz);
-            const int x = cx + dx, y = cy + dy, z = cz + dz;
-            if ((unsigned)x >= (unsigned)g.nx || (unsigned)y >= (unsigned)g.ny || (unsigned)z >= (unsigned)g.nz)
-                continue;
-            const float xl = lox + (float)dx * cs - m, yl = loy + (float)dy * cs - m, zl = loz + (float)dz * cs - m;
-            const float bd = (axis_gap(qx, xl, xl + w) + axis_gap(qy, yl, yl + w)) + axis_gap(qz, zl, zl + w);
-            if (bd * 0.999999f > tk.worst()) continue;
-            scan_cell_seq<K>(g, ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x, qx, qy,
-                             qz, tk);
-        }
-        group_merge<K, 64>(tk);
-        const float gr = own + (float)s * cs;
-        if (gr > 0.f && tk.worst() < gr * gr * 0.999999f) done = true;
-    }
-    return done || smax == smax_grid;
-}
-
-// Far pass of the front-end kNN: one wave (64 lanes) per query.  The near
-// pass left the exact top-K over the 3x3x3 block around the query's cell
-// (merged: the same list in every lane); what remains are the cells of the
-// axis box [q - r, q + r], r = sqrt(K-th best) (+ margins), outside that
-// block.  Lane l takes box cells l, l+64, ..., prunes each against its own
-// K-th best and scans it sequentially; one wave merge.  Exact: every point
-// with d2 <= K-th best lies in the box, because the cell assignment of the
-// grid build (cell_coord, clamped) is monotone in each coordinate.
-template <int K>
-__device__ void wave_knn_box(const GridDev& g, float qx, float qy, float qz, int lane, TopK<K>& tk) {
+// Far pass with a whole block (NT lanes) per query: the box cells outside
+// the 3x3x3 block are judged one per lane per round of NT, the kept cells'
+// ranges concatenated by a block prefix sum (slot table in LDS: s_b[NT],
+// s_off[NT+1]), every lane takes a contiguous chunk of the concatenation
+// (one binary search, then sequential, four loads in flight), and the lists
+// are merged per wave (butterfly) and across waves (thread 0).  The result is
+// in thread 0.  Exact: every point with d2 <= K-th best lies in
+// the box, because the grid build's cell assignment (cell_coord, clamped) is
+// monotone in each coordinate.  Must be called
+// by all NT threads of the block (it synchronises the block).
+template <int K, int NT>
+__device__ void block_knn_box_flat(const GridDev& g, float qx, float qy, float qz, uint32_t* s_b, uint32_t* s_off,
+                                   uint32_t* s_w, uint64_t* s_lists, TopK<K>& tk) {
+    static_assert(NT % 64 == 0 && NT <= 1024, "block_knn_box_flat: NT = multiple of 64");
+    constexpr int NW = NT / 64;
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int cx = cell_coord(qx, g.ox, g.inv_cell);
     const int cy = cell_coord(qy, g.oy, g.inv_cell);
     const int cz = cell_coord(qz, g.oz, g.inv_cell);
@@ -421,23 +468,94 @@ __device__ void wave_knn_box(const GridDev& g, float qx, float qy, float qz, int
     const int x0 = max(cell_coord(qx - r, g.ox, g.inv_cell), 0), x1 = min(cell_coord(qx + r, g.ox, g.inv_cell), g.nx - 1);
     const int y0 = max(cell_coord(qy - r, g.oy, g.inv_cell), 0), y1 = min(cell_coord(qy + r, g.oy, g.inv_cell), g.ny - 1);
     const int z0 = max(cell_coord(qz - r, g.oz, g.inv_cell), 0), z1 = min(cell_coord(qz + r, g.oz, g.inv_cell), g.nz - 1);
-    if (x0 > x1 || y0 > y1 || z0 > z1) return;
-    if (lane != 0) {  // keep the list in lane 0 only (see group_knn_exact_from)
-        tk.fill_with_worst();
-    }
+    if (x0 > x1 || y0 > y1 || z0 > z1) return;  // block-uniform
+    if (tid != 0) tk.fill_with_worst();
     const float cs = g.cell, m = g.margin, w = cs + 2.f * m;
+    const float bound = tk.worst();
     const int wx = x1 - x0 + 1, wxy = wx * (y1 - y0 + 1), nbox = wxy * (z1 - z0 + 1);
-    for (int k = lane; k < nbox; k += 64) {
-        const int z = z0 + k / wxy, kk = k % wxy;
-        const int y = y0 + kk / wx, x = x0 + kk % wx;
-        if (abs(x - cx) <= 1 && abs(y - cy) <= 1 && abs(z - cz) <= 1) continue;  // scanned by the near pass
-        const float xl = g.ox + (float)x * cs - m, yl = g.oy + (float)y * cs - m, zl = g.oz + (float)z * cs - m;
-        const float bd = (axis_gap(qx, xl, xl + w) + axis_gap(qy, yl, yl + w)) + axis_gap(qz, zl, zl + w);
-        if (bd * 0.999999f > tk.worst()) continue;
-        scan_cell_seq<K>(g, ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x, qx, qy, qz,
-                         tk);
+    for (int base = 0; base < nbox; base += NT) {
+        const int k = base + tid;
+        uint32_t b = 0, n = 0;
+        if (k < nbox) {
+            const int z = z0 + k / wxy, kk = k % wxy;
+            const int y = y0 + kk / wx, x = x0 + kk % wx;
+            if (!(abs(x - cx) <= 1 && abs(y - cy) <= 1 && abs(z - cz) <= 1)) {  // block: near pass
+                const float xl = g.ox + (float)x * cs - m, yl = g.oy + (float)y * cs - m, zl = g.oz + (float)z * cs - m;
+                const float bd = (axis_gap(qx, xl, xl + w) + axis_gap(qy, yl, yl + w)) + axis_gap(qz, zl, zl + w);
+                if (!(bd * 0.999999f > bound)) {
+                    const uint32_t c = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
+                    b = g.start[c];
+                    n = g.start[c + 1] - b;
+                }
+            }
+        }
+        uint32_t incl = n;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const uint32_t v = __shfl_up(incl, off, 64);
+            if (lane >= off) incl += v;
+        }
+        if (lane == 63) s_w[wid] = incl;
+        __syncthreads();  // also: the previous round's readers are done
+        uint32_t wbase = 0, T = 0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) {
+            const uint32_t v = s_w[q];
+            wbase += q < wid ? v : 0u;
+            T += v;
+        }
+        s_b[tid] = b;
+        s_off[tid] = wbase + incl - n;
+        if (tid == 0) s_off[NT] = T;
+        __syncthreads();
+        if (T == 0) continue;  // block-uniform
+        // contiguous chunk [c0, c1) of the concatenation per lane
+        const uint32_t chunk = (T + NT - 1) / NT;
+        const uint32_t c0 = min((uint32_t)tid * chunk, T), c1 = min(c0 + chunk, T);
+        if (c0 < c1) {
+            int lo = 0, hi = NT;  // last slot with s_off[slot] <= c0
+            while (hi - lo > 1) {
+                const int mid = (lo + hi) >> 1;
+                if (s_off[mid] <= c0) lo = mid;
+                else hi = mid;
+            }
+            int sl = lo;
+            uint32_t so = s_off[sl], se = s_off[sl + 1], sb = s_b[sl];
+            for (uint32_t t = c0; t < c1; t += 4) {
+                float4 pp[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t tt = t + (uint32_t)u;
+                    pp[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                    if (tt < c1) {
+                        while (tt >= se) {
+                            ++sl;
+                            so = se;
+                            se = s_off[sl + 1];
+                            sb = s_b[sl];
+                        }
+                        pp[u] = g.pts[sb + (tt - so)];
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                    if (t + (uint32_t)u < c1) tk.push(sqdist3(qx, qy, qz, pp[u].x, pp[u].y, pp[u].z), __float_as_int(pp[u].w));
+            }
+        }
     }
     group_merge<K, 64>(tk);
+    if (lane == 0)
+#pragma unroll
+        for (int j = 0; j < K; ++j) s_lists[wid * K + j] = tk.k[j];
+    __syncthreads();
+    if (tid == 0)
+        for (int q = 1; q < NW; ++q)
+#pragma unroll
+            for (int j = 0; j < K; ++j) {
+                const uint64_t v = s_lists[q * K + j];
+                tk.push(__uint_as_float((uint32_t)(v >> 32)), (int)(uint32_t)v);
+            }
+    __syncthreads();  // s_lists / slot tables free for the caller's next query
 }
 
 // Wave64 sum of a double with DPP row operations (no LDS round trips):

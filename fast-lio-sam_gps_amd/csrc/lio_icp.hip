@@ -31,6 +31,7 @@ constexpr int kIcpGroup = 8;  // lanes cooperating on one query's 1-NN
 
 // 256 threads = 32 source points, 8 lanes per point.
 __global__ void __launch_bounds__(256) icp_near_kernel(IcpArgs a) {
+    __shared__ uint32_t s_tab[256 / kIcpGroup][72];  // per-group shell-1 slot table
     const int i = xcd_block(blockIdx.x, gridDim.x) * (256 / kIcpGroup) + threadIdx.x / kIcpGroup;
     const int sub = threadIdx.x % kIcpGroup;
     if (i >= a.n) return;  // whole groups leave together
@@ -51,7 +52,8 @@ __global__ void __launch_bounds__(256) icp_near_kernel(IcpArgs a) {
     }
     TopK<1> tk;
     tk.init(INFINITY);
-    const bool done = group_knn_near<1, kIcpGroup>(a.grid, x, y, z, a.max_shell_near, sub, tk);
+    const bool done =
+        group_knn_near<1, kIcpGroup>(a.grid, x, y, z, a.max_shell_near, sub, tk, nullptr, s_tab[threadIdx.x / kIcpGroup]);
     if (sub == 0) {
         if (a.fitness || a.apply_T) {
             a.cur[3 * i] = x;

@@ -7,7 +7,7 @@
 //       body->world (double, stored float) -> exact grid 5-NN over shells 0-1,
 //       cell points scanned lane-strided (coalesced), private top-5 lists
 //       merged by a shuffle butterfly; unresolved points -> far queue
-//     knn_far_kernel   one wave per queued point, the rest of its search box
+//     knn_far_kernel   one block per queued point, the rest of its search box
 //     plane_kernel     lane = point: gate (found == 5 && d2[4] <= 5) ->
 //       esti_plane (QR, registers) -> pd2, s-gate -> H row (double) ->
 //       30-value DPP wave reduction -> block partial
@@ -31,7 +31,7 @@ constexpr int kBlock = 256;
 constexpr int kGroup = 8;   // lanes cooperating on one query's kNN
 constexpr int kKnnBlock = 512;
 constexpr int kFarBlock = 256;
-constexpr int kFarBlocks = 256;  // 1024 waves stride the far queue
+constexpr int kFarBlocks = 1024;  // blocks striding the far queue (one query per block)
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -95,6 +95,7 @@ __device__ __forceinline__ bool residual_row(const MatchArgs& a, float bx, float
 template <bool DBG>
 __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) knn_near_kernel(MatchArgs a) {
     constexpr int QPB = kKnnBlock / kGroup;  // 64 queries per block
+    __shared__ uint32_t s_tab[QPB][72];      // per-group shell-1 slot table
     const int blk = xcd_block(blockIdx.x, gridDim.x);
     const int sub = threadIdx.x % kGroup;
     const int i = blk * QPB + threadIdx.x / kGroup;
@@ -105,7 +106,8 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
     TopK<5> tk;
     tk.init(a.range_sq);
     SearchStats st{0, 0, 0};
-    const bool done = group_knn_near<5, kGroup>(a.grid, wx, wy, wz, min(a.max_shell, 1), sub, tk, DBG ? &st : nullptr);
+    const bool done = group_knn_near<5, kGroup>(a.grid, wx, wy, wz, min(a.max_shell, 1), sub, tk, DBG ? &st : nullptr,
+                                                s_tab[threadIdx.x / kGroup]);
     const bool far = !done && a.max_shell > 1;
     if constexpr (DBG) {
 #pragma unroll
@@ -140,29 +142,24 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
     }
 }
 
-// Pass 2: the queued queries, one wave each (wave_knn_box).
-// Fixed grid; every wave strides the queue and exits once past its end.
+// Pass 2: the queued queries, one block each (block_knn_box_flat over the
+// rest of the query's search box).  Fixed grid; every block strides the queue
+// and exits once past its end.
 __global__ void __launch_bounds__(kFarBlock) knn_far_kernel(MatchArgs a) {
-    const int lane = threadIdx.x & 63;
-    const int nw = gridDim.x * (kFarBlock / 64);
+    __shared__ uint32_t s_b[kFarBlock], s_off[kFarBlock + 1], s_w[kFarBlock / 64];
+    __shared__ uint64_t s_lists[(kFarBlock / 64) * 5];
     const int cnt = *a.far_count;
-    for (int f = blockIdx.x * (kFarBlock / 64) + (threadIdx.x >> 6); f < cnt; f += nw) {
+    for (int f = blockIdx.x; f < cnt; f += gridDim.x) {
         const int i = a.far_list[f];
         float wx, wy, wz;
         body_to_world(a.pose, a.body[3 * i], a.body[3 * i + 1], a.body[3 * i + 2], wx, wy, wz);
         TopK<5> tk;
 #pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            tk.k[j] = knn_key(a.far_d[5 * (size_t)f + j], a.far_id[5 * (size_t)f + j]);
-        }
-        wave_knn_box<5>(a.grid, wx, wy, wz, lane, tk);
-        if (lane < 5) {
-            int v = tk.id(0);
+        for (int j = 0; j < 5; ++j) tk.k[j] = knn_key(a.far_d[5 * (size_t)f + j], a.far_id[5 * (size_t)f + j]);
+        block_knn_box_flat<5, kFarBlock>(a.grid, wx, wy, wz, s_b, s_off, s_w, s_lists, tk);
+        if (threadIdx.x == 0)
 #pragma unroll
-            for (int j = 1; j < 5; ++j)
-                if (lane == j) v = tk.id(j);
-            a.nn_idx[5 * (size_t)i + lane] = v == kNone ? -1 : v;
-        }
+            for (int j = 0; j < 5; ++j) a.nn_idx[5 * (size_t)i + j] = tk.id(j) == kNone ? -1 : tk.id(j);
     }
 }
 
