@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -95,7 +96,9 @@ struct lio_ctx {
     double* d_partials = nullptr;
     int64_t part_cap = 0;
     double* d_sums = nullptr;
-    double* h_sums = nullptr;  // pinned
+    double* h_sums = nullptr;    // pinned, host-mapped: [0,32) sums, [32] sequence number
+    double* h_sums_dev = nullptr;  // device view of h_sums
+    unsigned long long seq = 0;
     double* d_rows = nullptr;
     int64_t rows_cap = 0;
     int64_t* d_nrows = nullptr;
@@ -362,7 +365,8 @@ int lio_ctx_create(lio_map* m, const lio_match_params* p, lio_ctx** out) {
     else
         c->p = lio_match_params{5.0f, 0.1f, 0.9, 0.9};
     if (hipMalloc(&c->d_sums, 32 * sizeof(double)) != hipSuccess ||
-        hipHostMalloc(&c->h_sums, 32 * sizeof(double)) != hipSuccess ||
+        hipHostMalloc(&c->h_sums, 40 * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+        hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_sums_dev), c->h_sums, 0) != hipSuccess ||
         hipMalloc(&c->d_nrows, sizeof(int64_t)) != hipSuccess ||
         hipMalloc(&c->d_far_count, sizeof(int)) != hipSuccess ||
         hipMemset(c->d_far_count, 0, sizeof(int)) != hipSuccess) {
@@ -463,6 +467,9 @@ static lio::MatchArgs make_args(lio_ctx* c, const lio_pose& pose) {
     // every point with d2 <= range lies within ceil(sqrt(range)/cell)+1 shells
     a.max_shell = (int)std::ceil(std::sqrt((double)c->p.knn_range_sq) / a.grid.cell) + 1;
     a.dbg = nullptr;
+    a.sums_out = c->h_sums_dev;
+    a.seq_out = reinterpret_cast<unsigned long long*>(c->h_sums_dev + 32);
+    a.seq = 0;
     a.far_list = c->d_far_list;
     a.far_count = c->d_far_count;
     a.far_d = c->d_far_d;
@@ -482,6 +489,25 @@ static void accum_event(EventPair& e, int64_t& launches, double& ms) {
     }
 }
 
+// Wait until the evaluation's last block has published sequence number `seq`
+// (zero-copy result, no copy / stream-sync round trip); a stream error or an
+// idle stream without the result ends the wait with an error.
+static int wait_result(lio_ctx* c, unsigned long long seq, double* sums) {
+    volatile unsigned long long* flag = reinterpret_cast<volatile unsigned long long*>(c->h_sums + 32);
+    for (uint64_t it = 0;; ++it) {
+        if (*flag == seq) break;
+        if ((it & 255) == 255) {
+            const hipError_t e = hipStreamQuery(c->map->st);
+            if (e != hipSuccess && e != hipErrorNotReady)
+                return fail(LIO_ERR_HIP, std::string("lio_match: ") + hipGetErrorString(e));
+            if (e == hipSuccess && *flag != seq) return fail(LIO_ERR_HIP, "lio_match: evaluation produced no result");
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    std::memcpy(sums, c->h_sums, LIO_SUMS_LEN * sizeof(double));
+    return LIO_OK;
+}
+
 int lio_match(lio_ctx* c, const lio_pose* pose, int redo_knn, double* sums) {
     if (!c || !pose || !sums) return fail(LIO_ERR_ARG, "lio_match: bad arguments");
     if (c->map->n == 0) return fail(LIO_ERR_STATE, "lio_match: map is empty (call lio_map_build)");
@@ -496,16 +522,19 @@ int lio_match(lio_ctx* c, const lio_pose* pose, int redo_knn, double* sums) {
         c->knn_valid = true;
         return LIO_OK;
     }
+    a.seq = ++c->seq;
     if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.a, st));
     const int nb = lio::launch_h_model(a, redo_knn != 0, st, c->timing && redo_knn ? c->ev_marks : nullptr);
     if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.b, st));
-    lio::launch_finalize(c->d_partials, nb, c->d_sums, st);
+    lio::launch_finalize(a, nb, st);
     if (c->timing) HIP_TRY(hipEventRecord(c->ev_fin.b, st));
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipMemcpyAsync(c->h_sums, c->d_sums, 32 * sizeof(double), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-    std::memcpy(sums, c->h_sums, LIO_SUMS_LEN * sizeof(double));
+    int rc = wait_result(c, a.seq, sums);
+    if (rc) return rc;
     if (c->timing) {
+        HIP_TRY(hipEventSynchronize(c->ev_fin.b));
+        EventPair f{c->ev_main.b, c->ev_fin.b};
+        accum_event(f, c->tm.final_launches, c->tm.final_ms);
         if (redo_knn) {
             accum_event(c->ev_main, c->tm.knn_launches, c->tm.knn_ms);
             EventPair n{c->ev_main.a, c->ev_marks[0]}, f{c->ev_marks[0], c->ev_marks[1]};
@@ -514,8 +543,6 @@ int lio_match(lio_ctx* c, const lio_pose* pose, int redo_knn, double* sums) {
         }
         else
             accum_event(c->ev_main, c->tm.reuse_launches, c->tm.reuse_ms);
-        EventPair f{c->ev_main.b, c->ev_fin.b};
-        accum_event(f, c->tm.final_launches, c->tm.final_ms);
     }
     c->last_pose = *pose;
     c->have_eval = true;
@@ -536,14 +563,15 @@ int lio_ctx_knn_stats(lio_ctx* c, const lio_pose* pose, double* sums, int32_t* s
     HIP_TRY(hipMalloc(&d_dbg, c->n * 3 * sizeof(int)));
     lio::MatchArgs a = make_args(c, *pose);
     a.dbg = d_dbg;
+    a.seq = ++c->seq;
     const int nb = lio::launch_h_model(a, true, st);
-    lio::launch_finalize(c->d_partials, nb, c->d_sums, st);
-    hipError_t e1 = hipMemcpyAsync(c->h_sums, c->d_sums, 32 * sizeof(double), hipMemcpyDeviceToHost, st);
+    lio::launch_finalize(a, nb, st);
     hipError_t e2 = hipMemcpyAsync(stats3, d_dbg, c->n * 3 * sizeof(int), hipMemcpyDeviceToHost, st);
     hipError_t e3 = hipStreamSynchronize(st);
     (void)hipFree(d_dbg);
-    if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess) return fail(LIO_ERR_HIP, "lio_ctx_knn_stats failed");
-    std::memcpy(sums, c->h_sums, LIO_SUMS_LEN * sizeof(double));
+    if (e2 != hipSuccess || e3 != hipSuccess) return fail(LIO_ERR_HIP, "lio_ctx_knn_stats failed");
+    int rc = wait_result(c, a.seq, sums);
+    if (rc) return rc;
     c->last_pose = *pose;
     c->knn_pose = *pose;
     c->have_eval = true;

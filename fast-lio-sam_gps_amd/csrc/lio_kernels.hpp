@@ -16,6 +16,9 @@ struct MatchArgs {
     float4* planes;           // n plane (a,b,c,d) cache
     uint8_t* sel;             // n point_selected_surf
     double* partials;         // nblocks*32
+    double* sums_out;         // 32 sums (host-mapped)
+    unsigned long long* seq_out;  // written with `seq` after sums_out (host-mapped)
+    unsigned long long seq;
     int* dbg;                 // optional n*3 search statistics (diagnostics only)
     int* far_list;            // n: points queued for the far pass
     int* far_count;           // queue length (reset to 0 by plane_kernel)
@@ -31,9 +34,9 @@ struct MatchArgs {
 
 // marks (optional, redo only): events recorded after the near and the far kernel
 int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* marks = nullptr);
-void launch_finalize(const double* partials, int nblocks, double* out, hipStream_t st);
 void launch_debug(const MatchArgs& a, float* world, float* d2, float* abcd_pd2, hipStream_t st);
 void launch_h_rows(const MatchArgs& a, double* rows, int64_t max_rows, int64_t* n_rows, hipStream_t st);
+void launch_finalize(const MatchArgs& a, int nblocks, hipStream_t st);  // -> sums_out, seq_out
 int match_blocks(int n);
 
 // --------------------------------------------------------------- grid build

@@ -15,6 +15,7 @@
 //   ekfom_data.converge == false: h_model_reuse_kernel, lane = point
 //     body->world -> cached plane -> pd2, s-gate -> H row -> block partial
 //   finalize_kernel: sums the block partials in a fixed order (deterministic)
+//     into host-mapped memory + a sequence number (zero-copy result)
 //
 // The per-point dense H (effct x 12 doubles) of the reference is never
 // materialised: the IESKF only consumes H^T H and H^T h.
@@ -241,12 +242,15 @@ __global__ void __launch_bounds__(kBlock) h_model_reuse_kernel(MatchArgs a) {
     }
 }
 
-// Fixed-order sum of nblocks x 32 partials -> out[32] (one block of 1024).
-// 32 row groups x 32 columns; each thread issues its rows' loads 8 at a time
-// (independent, so the latency overlaps) and adds them in row order; the 32
-// group sums are then added in group order: deterministic for a given nblocks.
+// Fixed-order sum of nblocks x 32 partials -> 32 sums (one block of 1024):
+// 32 row groups x 32 columns, each thread issues its rows' loads 8 at a time
+// and adds them in row order, then the 32 group sums in group order
+// (deterministic for a given nblocks).  The sums go straight to the ctx's
+// host-mapped result (zero-copy), followed by the sequence number the host
+// waits on (no copy launch, no stream-sync round trip).
 __global__ void __launch_bounds__(1024) finalize_kernel(const double* __restrict__ partials, int nblocks,
-                                                       double* __restrict__ out) {
+                                                       double* __restrict__ out, unsigned long long* seq_out,
+                                                       unsigned long long seq) {
     __shared__ double sg[32][33];
     const int col = threadIdx.x & 31, grp = threadIdx.x >> 5;
     const int per = (nblocks + 31) / 32;
@@ -268,6 +272,11 @@ __global__ void __launch_bounds__(1024) finalize_kernel(const double* __restrict
 #pragma unroll
         for (int g = 0; g < 32; ++g) t += sg[g][threadIdx.x];
         out[threadIdx.x] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __threadfence_system();
+        *reinterpret_cast<volatile unsigned long long*>(seq_out) = seq;
     }
 }
 
@@ -376,10 +385,6 @@ int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* ma
     return nb;
 }
 
-void launch_finalize(const double* partials, int nblocks, double* out, hipStream_t st) {
-    finalize_kernel<<<1, 1024, 0, st>>>(partials, nblocks, out);
-}
-
 void launch_debug(const MatchArgs& a, float* world, float* d2, float* abcd_pd2, hipStream_t st) {
     if (a.n == 0) return;
     debug_kernel<<<(a.n + 255) / 256, 256, 0, st>>>(a, world, d2, abcd_pd2);
@@ -387,6 +392,10 @@ void launch_debug(const MatchArgs& a, float* world, float* d2, float* abcd_pd2, 
 
 void launch_h_rows(const MatchArgs& a, double* rows, int64_t max_rows, int64_t* n_rows, hipStream_t st) {
     h_rows_kernel<<<1, 1024, 0, st>>>(a, rows, max_rows, n_rows);
+}
+
+void launch_finalize(const MatchArgs& a, int nblocks, hipStream_t st) {
+    finalize_kernel<<<1, 1024, 0, st>>>(a.partials, nblocks, a.sums_out, a.seq_out, a.seq);
 }
 
 int match_blocks(int n) {  // partial slots (plane / reuse kernels)
