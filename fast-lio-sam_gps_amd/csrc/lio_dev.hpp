@@ -187,6 +187,21 @@ __device__ __forceinline__ void scan_cell_group(const GridDev& g, uint32_t c, fl
     }
 }
 
+// Lane-strided scan of one cell by the group, two loads in flight per lane.
+template <int K, int G>
+__device__ __forceinline__ void scan_cell_group2(const GridDev& g, uint32_t c, float qx, float qy, float qz, int sub,
+                                                 TopK<K>& tk) {
+    const uint32_t b = g.start[c];
+    const uint32_t e = g.start[c + 1];
+    for (uint32_t j = b + (uint32_t)sub; j < e; j += 2 * G) {
+        const float4 p0 = g.pts[j];
+        float4 p1 = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (j + G < e) p1 = g.pts[j + G];
+        tk.push(sqdist3(qx, qy, qz, p0.x, p0.y, p0.z), __float_as_int(p0.w));
+        if (j + G < e) tk.push(sqdist3(qx, qy, qz, p1.x, p1.y, p1.z), __float_as_int(p1.w));
+    }
+}
+
 // Returns true when the merged list is provably final: the K-th best lies
 // inside the radius the visited shells guarantee, or the whole grid was
 // visited; false => cells beyond max_shell could still hold a better point.
@@ -310,44 +325,53 @@ __device__ __forceinline__ void shell_offset(int s, int k, int& dx, int& dy, int
 }
 
 // Shell 1 of the 3x3x3 block, load-balanced over an aligned group of G = 8
-// lanes.  Lane `sub` judges cells 4*sub .. 4*sub+3 of the block against the
-// (merged, group-uniform) K-th best without memory access, loads the kept
-// cells' [start, end) ranges (8 independent loads), a group prefix sum
+// lanes.  Lane `sub` owns cells 4*sub .. 4*sub+3 of the block (their ranges
+// preloaded by shell1_ranges), drops those the (merged, group-uniform) K-th
+// best rules out by box distance, a group prefix sum
 // concatenates the ranges into a slot table in LDS (lds[0..32) range starts,
 // lds[32..65) offsets), and the G lanes then stride the concatenated points,
 // two loads in flight per lane.  The work per group is ceil(points / G)
 // steps whatever the cells' sizes, instead of the largest cell of each lane.
-template <int K, int G>
-__device__ __forceinline__ void scan_shell1_flat(const GridDev& g, float qx, float qy, float qz, int cx, int cy,
-                                                 int cz, float lox, float loy, float loz, int sub, uint32_t* lds,
-                                                 TopK<K>& tk, SearchStats* dbg) {
-    static_assert(G == 8, "scan_shell1_flat: 8-lane groups (4 cells per lane cover the 27-cell block)");
-    const float cs = g.cell, m = g.margin, w = cs + 2.f * m;
-    const float bound = tk.worst();
-    uint32_t b4[4], n4[4];
-    uint32_t lane_total = 0;
+// Shell-1 ranges of lane `sub` (cells 4*sub .. 4*sub+3 of the 3x3x3 block),
+// loaded before the own cell is scanned so their latency overlaps it.
+template <int G>
+__device__ __forceinline__ void shell1_ranges(const GridDev& g, int cx, int cy, int cz, int sub, uint32_t b4[4],
+                                              uint32_t n4[4]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int k = 4 * sub + j;
         const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
         const int x = cx + dx, y = cy + dy, z = cz + dz;
-        bool keep = k < 27 && k != 13 && (unsigned)x < (unsigned)g.nx && (unsigned)y < (unsigned)g.ny &&
-                    (unsigned)z < (unsigned)g.nz;
-        if (keep) {
-            const float xl = lox + (float)dx * cs - m, yl = loy + (float)dy * cs - m, zl = loz + (float)dz * cs - m;
-            const float bd = (axis_gap(qx, xl, xl + w) + axis_gap(qy, yl, yl + w)) + axis_gap(qz, zl, zl + w);
-            keep = !(bd * 0.999999f > bound);
-        }
+        const bool ok = k < 27 && k != 13 && (unsigned)x < (unsigned)g.nx && (unsigned)y < (unsigned)g.ny &&
+                        (unsigned)z < (unsigned)g.nz;
         uint32_t b = 0, e = 0;
-        if (keep) {
+        if (ok) {
             const uint32_t c = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
             b = g.start[c];
             e = g.start[c + 1];
-            if (dbg) dbg->cells += 1;
         }
         b4[j] = b;
         n4[j] = e - b;
-        lane_total += e - b;
+    }
+}
+
+template <int K, int G>
+__device__ __forceinline__ void scan_shell1_flat(const GridDev& g, float qx, float qy, float qz, int cx, int cy,
+                                                 int cz, float lox, float loy, float loz, int sub, uint32_t* lds,
+                                                 uint32_t b4[4], uint32_t n4[4], TopK<K>& tk, SearchStats* dbg) {
+    static_assert(G == 8, "scan_shell1_flat: 8-lane groups (4 cells per lane cover the 27-cell block)");
+    const float cs = g.cell, m = g.margin, w = cs + 2.f * m;
+    const float bound = tk.worst();
+    uint32_t lane_total = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {  // prune the preloaded ranges against the own-cell bound
+        const int k = 4 * sub + j;
+        const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
+        const float xl = lox + (float)dx * cs - m, yl = loy + (float)dy * cs - m, zl = loz + (float)dz * cs - m;
+        const float bd = (axis_gap(qx, xl, xl + w) + axis_gap(qy, yl, yl + w)) + axis_gap(qz, zl, zl + w);
+        if (bd * 0.999999f > bound) n4[j] = 0;
+        if (dbg && n4[j]) dbg->cells += 1;
+        lane_total += n4[j];
     }
     uint32_t incl = lane_total;
 #pragma unroll
@@ -412,7 +436,9 @@ __device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, i
     own = fminf(own, fminf(qz - loz, loz + cs - qz)) - m;
     const uint32_t nx = (uint32_t)g.nx, nxy = (uint32_t)g.nx * (uint32_t)g.ny;
     const uint32_t c0 = (uint32_t)cz * nxy + (uint32_t)cy * nx + (uint32_t)cx;
-    scan_cell_group<K, G>(g, c0, qx, qy, qz, sub, tk);
+    uint32_t b4[4], n4[4];
+    if (lds) shell1_ranges<G>(g, cx, cy, cz, sub, b4, n4);  // in flight during the own-cell scan
+    scan_cell_group2<K, G>(g, c0, qx, qy, qz, sub, tk);
     group_merge<K, G>(tk);
     if (dbg) dbg->shell = 0;
     if (own > 0.f && tk.worst() < own * own * 0.999999f) return true;
@@ -420,7 +446,7 @@ __device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, i
         tk.fill_with_worst();
     }
     if (lds) {
-        scan_shell1_flat<K, G>(g, qx, qy, qz, cx, cy, cz, lox, loy, loz, sub, lds, tk, dbg);
+        scan_shell1_flat<K, G>(g, qx, qy, qz, cx, cy, cz, lox, loy, loz, sub, lds, b4, n4, tk, dbg);
     } else {
         for (int k = sub; k < 27; k += G) {
             if (k == 13) continue;  // own cell

@@ -186,7 +186,7 @@ int lio_icp_create(const lio_icp_params* p, lio_icp** out) {
     auto* h = new lio_icp();
     h->dev = p->device;
     h->p = *p;
-    if (!(h->p.cell_size > 0.f)) h->p.cell_size = 1.0f;
+    if (!(h->p.cell_size > 0.f)) h->p.cell_size = 2.0f;  // 0.3 m voxelised submaps: 2 m cells (scripts/icp_cells.py)
     if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&h->d_far_count, 64) != hipSuccess) {
         delete h;

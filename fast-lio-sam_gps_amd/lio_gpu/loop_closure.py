@@ -38,14 +38,14 @@ class RegistrationOutput:  # loop_closure.h:31-37
     state: int = 0
 
 
-def icp_params(config: LoopClosureConfig, cell_size: float = 1.0, device: int = 0) -> _capi.IcpParams:
+def icp_params(config: LoopClosureConfig, cell_size: float = 2.0, device: int = 0) -> _capi.IcpParams:
     # setTransformationEpsilon(0.01), setEuclideanFitnessEpsilon(0.01), setMaximumIterations(50)
     return _capi.IcpParams(config.icp_max_corr_dist_, 0.01, 0.01, 50, 0.0, config.icp_score_threshold_,
                            cell_size, device)
 
 
 class LoopClosure:
-    def __init__(self, config: LoopClosureConfig, cell_size: float = 1.0, device: int = 0):
+    def __init__(self, config: LoopClosureConfig, cell_size: float = 2.0, device: int = 0):
         self.config_ = config
         self._p = icp_params(config, cell_size, device)
         self._h = C.c_void_p()

@@ -191,7 +191,7 @@ typedef struct lio_icp_params {
     int max_iter;           /* setMaximumIterations(50)         loop_closure.cpp:10 */
     double rot_eps;         /* 0 => PCL default 1 - trans_eps                        */
     double score_threshold; /* icp_score_threshold (config.yaml:16)                   */
-    float cell_size;        /* target grid cell [m]; 0 => 1.0                        */
+    float cell_size;        /* target grid cell [m]; 0 => 2.0                        */
     int device;
 } lio_icp_params;
 
