@@ -20,6 +20,7 @@
 #include "ieskf.hpp"
 #include "lio_error.hpp"
 #include "lio_kernels.hpp"
+#include "lio_filter.hpp"
 #include "lio_mapupd.hpp"
 
 namespace {
@@ -115,6 +116,13 @@ struct lio_ctx {
     lio_kernel_timing tm{};
     EventPair ev_main, ev_fin;
     hipEvent_t ev_marks[2] = {nullptr, nullptr};  // after near / after far (redo)
+    lio::FilterBuf filt;                          // scan preprocessing
+    float* d_raw = nullptr;                       // raw records / preprocessed records
+    int64_t raw_cap = 0;
+    float* d_rec = nullptr;
+    int64_t rec_cap = 0;
+    lio::ImuPose* d_poses = nullptr;
+    int64_t poses_cap = 0;
 };
 
 extern "C" {
@@ -397,6 +405,9 @@ int lio_ctx_destroy(lio_ctx* c) {
     }
     for (hipEvent_t e : c->ev_marks)
         if (e) (void)hipEventDestroy(e);
+    lio::filter_free(c->filt);
+    for (void* q : {(void*)c->d_raw, (void*)c->d_rec, (void*)c->d_poses})
+        if (q) (void)hipFree(q);
     delete c;
     return LIO_OK;
 }
@@ -756,6 +767,193 @@ int lio_ieskf_update(lio_ctx* c, lio_state* xs, double* P, const lio_ieskf_param
         st->res_mean = r.res_mean;
         st->solve_ms = r.solve_ms;
     }
+    return LIO_OK;
+}
+
+// =============================================================================
+// filters
+// =============================================================================
+struct lio_filter {
+    int dev = 0;
+    hipStream_t st = nullptr;
+    lio::FilterBuf b;
+    float* d_in = nullptr;
+    int64_t in_cap = 0;
+    float* d_out = nullptr;
+    int64_t out_cap = 0;
+    int64_t* d_seg = nullptr;
+    int64_t seg_cap = 0;
+    double* d_T = nullptr;
+    int64_t T_cap = 0;
+    lio::ImuPose* d_poses = nullptr;
+    int64_t poses_cap = 0;
+};
+
+static int filter_status(int rc, const char* what) {
+    if (rc == 0) return LIO_OK;
+    if (rc == -5) return fail(LIO_ERR_NOMEM, std::string(what) + ": out of device memory");
+    if (rc == -1) return fail(LIO_ERR_ARG, std::string(what) + ": bad arguments");
+    return fail(LIO_ERR_HIP, std::string(what) + " failed");
+}
+
+static lio::UndistortEnd undistort_end(const lio_pose* e) {
+    lio::UndistortEnd u{};
+    if (!e) {
+        for (int k = 0; k < 9; ++k) u.R[k] = u.R_LI[k] = (k % 4 == 0) ? 1.0 : 0.0;
+        return u;
+    }
+    std::memcpy(u.pos, e->t, sizeof(u.pos));
+    std::memcpy(u.R, e->R, sizeof(u.R));
+    std::memcpy(u.R_LI, e->R_LI, sizeof(u.R_LI));
+    std::memcpy(u.t_LI, e->t_LI, sizeof(u.t_LI));
+    return u;
+}
+
+static_assert(sizeof(lio_imu_pose) == sizeof(lio::ImuPose), "lio_imu_pose layout");
+
+int lio_filter_create(int device, lio_filter** out) {
+    if (!out) return fail(LIO_ERR_ARG, "out is NULL");
+    *out = nullptr;
+    int rc = check_device(device);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(device));
+    auto* f = new lio_filter();
+    f->dev = device;
+    if (hipStreamCreateWithFlags(&f->st, hipStreamNonBlocking) != hipSuccess) {
+        delete f;
+        return fail(LIO_ERR_HIP, "hipStreamCreate failed");
+    }
+    *out = f;
+    return LIO_OK;
+}
+
+int lio_filter_destroy(lio_filter* f) {
+    if (!f) return LIO_OK;
+    (void)hipSetDevice(f->dev);
+    (void)hipStreamSynchronize(f->st);
+    lio::filter_free(f->b);
+    for (void* q : {(void*)f->d_in, (void*)f->d_out, (void*)f->d_seg, (void*)f->d_T, (void*)f->d_poses})
+        if (q) (void)hipFree(q);
+    (void)hipStreamDestroy(f->st);
+    delete f;
+    return LIO_OK;
+}
+
+int lio_voxel_grid(lio_filter* f, const float* pts, int64_t n, int stride, const float leaf[3], float* out,
+                   int64_t* n_out) {
+    if (!f || !leaf || !n_out || n < 0 || (n > 0 && (!pts || !out)) || stride < 3 || stride > lio::kMaxFields ||
+        !(leaf[0] > 0.f && leaf[1] > 0.f && leaf[2] > 0.f))
+        return fail(LIO_ERR_ARG, "lio_voxel_grid: bad arguments");
+    *n_out = 0;
+    if (n == 0) return LIO_OK;
+    HIP_TRY(hipSetDevice(f->dev));
+    int rc = grow(&f->d_in, f->in_cap, n * stride);
+    if (!rc) rc = grow(&f->d_out, f->out_cap, n * stride);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(f->d_in, pts, (size_t)n * stride * sizeof(float), hipMemcpyHostToDevice, f->st));
+    int64_t m = 0;
+    rc = lio::voxel_grid(f->b, f->d_in, n, stride, leaf, f->d_out, &m, f->st);
+    if (rc) return filter_status(rc, "lio_voxel_grid");
+    if (m) HIP_TRY(hipMemcpyAsync(out, f->d_out, (size_t)m * stride * sizeof(float), hipMemcpyDeviceToHost, f->st));
+    HIP_TRY(hipStreamSynchronize(f->st));
+    *n_out = m;
+    return LIO_OK;
+}
+
+int lio_submap_voxelize(lio_filter* f, const float* pts, const int64_t* seg_off, int nk, int stride,
+                        const double* poses16, float voxel_res, float* out, int64_t* n_out) {
+    if (!f || !seg_off || !n_out || nk < 0 || stride < 3 || stride > lio::kMaxFields || !(voxel_res > 0.f) ||
+        (nk > 0 && !poses16))
+        return fail(LIO_ERR_ARG, "lio_submap_voxelize: bad arguments");
+    *n_out = 0;
+    const int64_t n = nk > 0 ? seg_off[nk] : 0;
+    for (int k = 0; k < nk; ++k)
+        if (seg_off[k] < 0 || seg_off[k + 1] < seg_off[k]) return fail(LIO_ERR_ARG, "lio_submap_voxelize: bad segments");
+    if (seg_off[0] != 0) return fail(LIO_ERR_ARG, "lio_submap_voxelize: seg_off[0] must be 0");
+    if (n == 0) return LIO_OK;
+    if (!pts || !out) return fail(LIO_ERR_ARG, "lio_submap_voxelize: bad arguments");
+    HIP_TRY(hipSetDevice(f->dev));
+    int rc = grow(&f->d_in, f->in_cap, n * stride);
+    if (!rc) rc = grow(&f->d_out, f->out_cap, 2 * n * stride);
+    if (!rc) rc = grow(&f->d_seg, f->seg_cap, nk + 1);
+    if (!rc) rc = grow(&f->d_T, f->T_cap, 16 * (int64_t)nk);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(f->d_in, pts, (size_t)n * stride * sizeof(float), hipMemcpyHostToDevice, f->st));
+    HIP_TRY(hipMemcpyAsync(f->d_seg, seg_off, (size_t)(nk + 1) * sizeof(int64_t), hipMemcpyHostToDevice, f->st));
+    HIP_TRY(hipMemcpyAsync(f->d_T, poses16, (size_t)nk * 16 * sizeof(double), hipMemcpyHostToDevice, f->st));
+    float* d_tf = f->d_out + (size_t)n * stride;  // transformed, concatenated cloud
+    rc = lio::transform_segments(f->d_in, n, stride, f->d_seg, nk, f->d_T, d_tf, f->st);
+    if (rc) return filter_status(rc, "lio_submap_voxelize");
+    const float leaf[3] = {voxel_res, voxel_res, voxel_res};
+    int64_t m = 0;
+    rc = lio::voxel_grid(f->b, d_tf, n, stride, leaf, f->d_out, &m, f->st);
+    if (rc) return filter_status(rc, "lio_submap_voxelize");
+    if (m) HIP_TRY(hipMemcpyAsync(out, f->d_out, (size_t)m * stride * sizeof(float), hipMemcpyDeviceToHost, f->st));
+    HIP_TRY(hipStreamSynchronize(f->st));
+    *n_out = m;
+    return LIO_OK;
+}
+
+static int prep_args_ok(const float* raw, int64_t n, int stride, const lio_scan_prep_params* p,
+                        const lio_imu_pose* poses, int n_poses) {
+    if (!p || n < 0 || (n > 0 && !raw) || stride < 4 || stride > lio::kMaxFields || p->time_field < 3 ||
+        p->time_field >= stride || n_poses < 0 || (n_poses > 0 && !poses) || n >= (int64_t)1 << 30)
+        return fail(LIO_ERR_ARG, "scan preprocessing: bad arguments");
+    return LIO_OK;
+}
+
+int lio_preprocess(lio_filter* f, const float* raw, int64_t n, int stride, const lio_scan_prep_params* p,
+                   const lio_imu_pose* poses, int n_poses, const lio_pose* end, float* out, int64_t* n_out) {
+    if (!f || !n_out || (n > 0 && !out)) return fail(LIO_ERR_ARG, "lio_preprocess: bad arguments");
+    int rc = prep_args_ok(raw, n, stride, p, poses, n_poses);
+    if (rc) return rc;
+    *n_out = 0;
+    if (n == 0) return LIO_OK;
+    HIP_TRY(hipSetDevice(f->dev));
+    rc = grow(&f->d_in, f->in_cap, n * stride);
+    if (!rc) rc = grow(&f->d_out, f->out_cap, n * stride);
+    if (!rc && n_poses) rc = grow(&f->d_poses, f->poses_cap, n_poses);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(f->d_in, raw, (size_t)n * stride * sizeof(float), hipMemcpyHostToDevice, f->st));
+    if (n_poses)
+        HIP_TRY(hipMemcpyAsync(f->d_poses, poses, (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, f->st));
+    const lio::ScanPrepParams sp{p->point_filter_num, p->blind, p->filter_size_surf, p->time_field};
+    int64_t m = 0;
+    rc = lio::scan_preprocess(f->b, f->d_in, n, stride, sp, f->d_poses, n_poses, undistort_end(end), f->d_out, &m,
+                              f->st);
+    if (rc) return filter_status(rc, "lio_preprocess");
+    if (m) HIP_TRY(hipMemcpyAsync(out, f->d_out, (size_t)m * stride * sizeof(float), hipMemcpyDeviceToHost, f->st));
+    HIP_TRY(hipStreamSynchronize(f->st));
+    *n_out = m;
+    return LIO_OK;
+}
+
+int lio_scan_preprocess(lio_ctx* c, const float* raw, int64_t n, int stride, const lio_scan_prep_params* p,
+                        const lio_imu_pose* poses, int n_poses, const lio_pose* end, int64_t* n_down) {
+    if (!c) return fail(LIO_ERR_ARG, "lio_scan_preprocess: NULL ctx");
+    int rc = prep_args_ok(raw, n, stride, p, poses, n_poses);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->map->dev));
+    hipStream_t st = c->map->st;
+    rc = grow(&c->d_raw, c->raw_cap, std::max<int64_t>(n, 1) * stride);
+    if (!rc) rc = grow(&c->d_rec, c->rec_cap, std::max<int64_t>(n, 1) * stride);
+    if (!rc && n_poses) rc = grow(&c->d_poses, c->poses_cap, n_poses);
+    if (rc) return rc;
+    if (n) HIP_TRY(hipMemcpyAsync(c->d_raw, raw, (size_t)n * stride * sizeof(float), hipMemcpyHostToDevice, st));
+    if (n_poses)
+        HIP_TRY(hipMemcpyAsync(c->d_poses, poses, (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
+    const lio::ScanPrepParams sp{p->point_filter_num, p->blind, p->filter_size_surf, p->time_field};
+    int64_t m = 0;
+    rc = lio::scan_preprocess(c->filt, c->d_raw, n, stride, sp, c->d_poses, n_poses, undistort_end(end), c->d_rec, &m,
+                              st);
+    if (rc) return filter_status(rc, "lio_scan_preprocess");
+    rc = ctx_reserve(c, m);
+    if (rc) return rc;
+    rc = lio::records_to_xyz(c->d_rec, m, stride, c->d_body, st);
+    if (rc) return filter_status(rc, "lio_scan_preprocess");
+    HIP_TRY(hipMemsetAsync(c->d_sel, 0, (size_t)std::max<int64_t>(m, 1), st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (n_down) *n_down = m;
     return LIO_OK;
 }
 

@@ -1,0 +1,480 @@
+// lio_filter.hip — point-cloud filters on either side of the hot path
+// (SURVEY §8(f) rows 2 and 3), on gfx950:
+//
+//   voxel_grid      pcl::VoxelGrid<PointT>::filter (PCL 1.10 applyFilter) [U]:
+//                   FAST-LIO's downSizeFilterSurf (filter_size_surf) and the
+//                   loop closure's voxelizePcd (utilities.hpp:161-183)
+//   transform_segs  pcl::transformPointCloud(cloud, out, Matrix4d) [U] per
+//                   keyframe segment (transformPcd, utilities.hpp:132-143)
+//   undistort       FAST-LIO ImuProcess::UndistortPcl backward propagation [U]
+//   scan_select     FAST-LIO Preprocess point_filter_num / blind selection [U]
+//
+// VoxelGrid on the GPU: AABB -> (min_b, divb_mul) on the device -> one int
+// voxel index per point -> stable radix sort (index, input position) -> run
+// heads -> one lane per voxel sums its points' fields in input order and
+// divides by the count (the PCL centroid; PCL sorts with std::sort, whose
+// order inside a voxel is unspecified — the stable order makes the float sums
+// reproducible).  Output in voxel-index order, as PCL.
+#include <hipcub/hipcub.hpp>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "lio_filter.hpp"
+
+namespace lio {
+
+namespace {
+
+constexpr uint32_t kInvalid = 0xffffffffu;
+
+__global__ void minmax_partial_kernel(const float* __restrict__ p, int64_t n, int stride, float* __restrict__ part) {
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float* q = p + (size_t)i * stride;
+        const float x = q[0], y = q[1], z = q[2];
+        if (!(isfinite(x) && isfinite(y) && isfinite(z))) continue;
+        lo[0] = fminf(lo[0], x);
+        lo[1] = fminf(lo[1], y);
+        lo[2] = fminf(lo[2], z);
+        hi[0] = fmaxf(hi[0], x);
+        hi[1] = fmaxf(hi[1], y);
+        hi[2] = fmaxf(hi[2], z);
+    }
+    __shared__ float s[6][256];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        s[d][threadIdx.x] = lo[d];
+        s[3 + d][threadIdx.x] = hi[d];
+    }
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                s[d][threadIdx.x] = fminf(s[d][threadIdx.x], s[d][threadIdx.x + w]);
+                s[3 + d][threadIdx.x] = fmaxf(s[3 + d][threadIdx.x], s[3 + d][threadIdx.x + w]);
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 6) part[blockIdx.x * 6 + threadIdx.x] = s[threadIdx.x][0];
+}
+
+// min/max of the partials, then PCL's voxel geometry:
+//   inverse_leaf = 1 / leaf;  min_b = floor(min_p * inv), max_b = floor(max_p * inv)
+//   div_b = max_b - min_b + 1; divb_mul = (1, div_b.x, div_b.x * div_b.y)
+//   overflow when div_b.x * div_b.y * div_b.z > INT_MAX (PCL then returns the input)
+__global__ void __launch_bounds__(256) voxel_geom_kernel(const float* __restrict__ part, int nb, float lx, float ly,
+                                                         float lz, VoxelGeom* __restrict__ out) {
+    __shared__ float s[6][256];
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int b = threadIdx.x; b < nb; b += 256) {
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            lo[d] = fminf(lo[d], part[b * 6 + d]);
+            hi[d] = fmaxf(hi[d], part[b * 6 + 3 + d]);
+        }
+    }
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        s[d][threadIdx.x] = lo[d];
+        s[3 + d][threadIdx.x] = hi[d];
+    }
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                s[d][threadIdx.x] = fminf(s[d][threadIdx.x], s[d][threadIdx.x + w]);
+                s[3 + d][threadIdx.x] = fmaxf(s[3 + d][threadIdx.x], s[3 + d][threadIdx.x + w]);
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    VoxelGeom g;
+    const float inv[3] = {1.0f / lx, 1.0f / ly, 1.0f / lz};
+    int64_t div[3];
+    g.empty = !(s[0][0] <= s[3][0]);
+    for (int d = 0; d < 3; ++d) {
+        g.inv[d] = inv[d];
+        g.min_b[d] = g.empty ? 0 : (int)floorf(s[d][0] * inv[d]);
+        const int max_b = g.empty ? 0 : (int)floorf(s[3 + d][0] * inv[d]);
+        div[d] = (int64_t)max_b - g.min_b[d] + 1;
+    }
+    g.overflow = div[0] * div[1] * div[2] > (int64_t)0x7fffffff;
+    g.mul[0] = 1;
+    g.mul[1] = (int)div[0];
+    g.mul[2] = (int)(div[0] * div[1]);
+    *out = g;
+}
+
+// PCL: ijk = (int)(floor(p * inv) - (float)min_b); idx = ijk . divb_mul; non-finite points skipped
+__global__ void voxel_key_kernel(const float* __restrict__ p, int64_t n, int stride, const VoxelGeom* __restrict__ gp,
+                                 uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const VoxelGeom g = *gp;
+    const float* q = p + (size_t)i * stride;
+    uint32_t k = kInvalid;
+    if (isfinite(q[0]) && isfinite(q[1]) && isfinite(q[2]) && !g.overflow) {
+        const int i0 = (int)(floorf(q[0] * g.inv[0]) - (float)g.min_b[0]);
+        const int i1 = (int)(floorf(q[1] * g.inv[1]) - (float)g.min_b[1]);
+        const int i2 = (int)(floorf(q[2] * g.inv[2]) - (float)g.min_b[2]);
+        k = (uint32_t)(i0 * g.mul[0] + i1 * g.mul[1] + i2 * g.mul[2]);
+    }
+    keys[i] = k;
+    vals[i] = (uint32_t)i;
+}
+
+__global__ void run_head_kernel(const uint32_t* __restrict__ keys, int64_t n, uint32_t* __restrict__ head) {
+    const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (j > n) return;
+    head[j] = (j < n && keys[j] != kInvalid && (j == 0 || keys[j - 1] != keys[j])) ? 1u : 0u;
+}
+
+// one lane per voxel: fields summed in input order, divided by the count (float)
+__global__ void voxel_centroid_kernel(const float* __restrict__ p, int stride, const uint32_t* __restrict__ keys,
+                                      const uint32_t* __restrict__ vals, int64_t n, const uint32_t* __restrict__ head,
+                                      const uint32_t* __restrict__ vid, float* __restrict__ out) {
+    const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (j >= n || !head[j]) return;
+    float acc[kMaxFields];
+#pragma unroll
+    for (int f = 0; f < kMaxFields; ++f) acc[f] = 0.f;
+    const uint32_t key = keys[j];
+    int64_t k = j;
+    for (; k < n && keys[k] == key; ++k) {
+        const float* q = p + (size_t)vals[k] * stride;
+#pragma unroll
+        for (int f = 0; f < kMaxFields; ++f)
+            if (f < stride) acc[f] += q[f];
+    }
+    const float cnt = (float)(k - j);
+    float* o = out + (size_t)vid[j] * stride;
+#pragma unroll
+    for (int f = 0; f < kMaxFields; ++f)
+        if (f < stride) o[f] = acc[f] / cnt;
+}
+
+__global__ void copy_strided_kernel(const float* __restrict__ a, int64_t nf, float* __restrict__ b) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i < nf) b[i] = a[i];
+}
+
+// transformPcd: double 4x4 per segment, ((m0 x + m1 y) + m2 z) + m3 in double, stored float;
+// non-finite points copied unchanged (PCL's !is_dense branch); other fields copied
+__global__ void transform_segs_kernel(const float* __restrict__ in, int64_t n, int stride,
+                                      const int64_t* __restrict__ seg_off, int nseg, const double* __restrict__ T16,
+                                      float* __restrict__ out) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    int lo = 0, hi = nseg;  // segment s: [seg_off[s], seg_off[s+1])
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (seg_off[mid] <= i) lo = mid;
+        else hi = mid;
+    }
+    const double* m = T16 + 16 * lo;
+    const float* q = in + (size_t)i * stride;
+    float* o = out + (size_t)i * stride;
+    for (int f = 3; f < stride; ++f) o[f] = q[f];
+    if (!(isfinite(q[0]) && isfinite(q[1]) && isfinite(q[2]))) {
+        o[0] = q[0];
+        o[1] = q[1];
+        o[2] = q[2];
+        return;
+    }
+    const double x = q[0], y = q[1], z = q[2];
+    o[0] = (float)(((m[0] * x + m[1] * y) + m[2] * z) + m[3]);
+    o[1] = (float)(((m[4] * x + m[5] * y) + m[6] * z) + m[7]);
+    o[2] = (float)(((m[8] * x + m[9] * y) + m[10] * z) + m[11]);
+}
+
+// ---- scan preprocessing --------------------------------------------------------
+// Preprocess (point_filter_num, blind) [U]: keep input i when i % every == 0 and
+// x*x + y*y + z*z > blind^2 (float); stable compaction.
+__global__ void scan_select_flags_kernel(const float* __restrict__ p, int64_t n, int stride, int every, float blind2,
+                                         uint32_t* __restrict__ flag) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i > n) return;
+    uint32_t f = 0;
+    if (i < n && i % every == 0) {
+        const float* q = p + (size_t)i * stride;
+        f = (q[0] * q[0] + q[1] * q[1] + q[2] * q[2]) > blind2 ? 1u : 0u;
+    }
+    flag[i] = f;
+}
+
+__global__ void compact_kernel(const float* __restrict__ p, int64_t n, int stride, const uint32_t* __restrict__ flag,
+                               const uint32_t* __restrict__ pos, float* __restrict__ out) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n || !flag[i]) return;
+    for (int f = 0; f < stride; ++f) out[(size_t)pos[i] * stride + f] = p[(size_t)i * stride + f];
+}
+
+// sort key of the point time (curvature, ms): float bits of a non-negative
+// float order like the values; negative times map below every positive one
+__global__ void time_key_kernel(const float* __restrict__ p, int64_t n, int stride, int tfield,
+                                uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t b = __float_as_uint(p[(size_t)i * stride + tfield]);
+    keys[i] = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    vals[i] = (uint32_t)i;
+}
+
+__global__ void gather_rows_kernel(const float* __restrict__ p, int64_t n, int stride,
+                                   const uint32_t* __restrict__ order, float* __restrict__ out) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* q = p + (size_t)order[i] * stride;
+    for (int f = 0; f < stride; ++f) out[(size_t)i * stride + f] = q[f];
+}
+
+// FAST-LIO so3_math Exp(ang_vel, dt): I + sin(a) K + (1 - cos(a)) K K
+__device__ __forceinline__ void so3_exp(const double w[3], double dt, double E[9]) {
+    const double nrm = sqrt((w[0] * w[0] + w[1] * w[1]) + w[2] * w[2]);
+    for (int k = 0; k < 9; ++k) E[k] = (k % 4 == 0) ? 1.0 : 0.0;
+    if (!(nrm > 0.0000001)) return;
+    const double r[3] = {w[0] / nrm, w[1] / nrm, w[2] / nrm};
+    const double K[9] = {0.0, -r[2], r[1], r[2], 0.0, -r[0], -r[1], r[0], 0.0};
+    const double a = nrm * dt, s = sin(a), c1 = 1.0 - cos(a);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            const double kk = ((c1 * K[3 * i + 0]) * K[0 + j] + (c1 * K[3 * i + 1]) * K[3 + j]) + (c1 * K[3 * i + 2]) * K[6 + j];
+            E[3 * i + j] = (E[3 * i + j] + s * K[3 * i + j]) + kk;
+        }
+}
+
+__device__ __forceinline__ void mv3(const double* M, const double* v, double* o) {
+    for (int r = 0; r < 3; ++r) o[r] = (M[3 * r] * v[0] + M[3 * r + 1] * v[1]) + M[3 * r + 2] * v[2];
+}
+__device__ __forceinline__ void mtv3(const double* M, const double* v, double* o) {  // M^T v
+    for (int r = 0; r < 3; ++r) o[r] = (M[r] * v[0] + M[3 + r] * v[1]) + M[6 + r] * v[2];
+}
+
+__device__ __forceinline__ void compensate(float* q, int tfield, const ImuPose& hd, const ImuPose& tl,
+                                           const UndistortEnd& end) {
+    const double dt = (double)q[tfield] / double(1000) - hd.offset_time;
+    double E[9], Ri[9];
+    so3_exp(tl.gyr, dt, E);
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c)
+            Ri[3 * r + c] = (hd.rot[3 * r] * E[c] + hd.rot[3 * r + 1] * E[3 + c]) + hd.rot[3 * r + 2] * E[6 + c];
+    double Tei[3];
+    for (int k = 0; k < 3; ++k) Tei[k] = ((hd.pos[k] + hd.vel[k] * dt) + ((0.5 * tl.acc[k]) * dt) * dt) - end.pos[k];
+    const double Pi[3] = {q[0], q[1], q[2]};
+    double a[3], b[3], c[3];
+    mv3(end.R_LI, Pi, a);
+    for (int k = 0; k < 3; ++k) a[k] += end.t_LI[k];
+    mv3(Ri, a, b);
+    for (int k = 0; k < 3; ++k) b[k] += Tei[k];
+    mtv3(end.R, b, c);
+    for (int k = 0; k < 3; ++k) c[k] -= end.t_LI[k];
+    mtv3(end.R_LI, c, a);
+    q[0] = (float)a[0];
+    q[1] = (float)a[1];
+    q[2] = (float)a[2];
+}
+
+// UndistortPcl backward propagation, one lane per (time-sorted) point: head =
+// the last IMU pose whose offset_time is < t (tail = head + 1 gives acc/gyr);
+// points at or before the first pose are left unchanged, as the reference's
+// loop never reaches them.  The reference's loop `break`s at the first point
+// without stepping past it, so that point is compensated again by every older
+// segment (head h-1, ..., 0) — reproduced for point 0.
+__global__ void undistort_kernel(float* __restrict__ p, int64_t n, int stride, int tfield,
+                                 const ImuPose* __restrict__ poses, int np, UndistortEnd end) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float* q = p + (size_t)i * stride;
+    const double t = (double)q[tfield] / double(1000);
+    int h = -1;
+    for (int k = np - 2; k >= 0; --k)
+        if (t > poses[k].offset_time) {
+            h = k;
+            break;
+        }
+    if (h < 0) return;
+    compensate(q, tfield, poses[h], poses[h + 1], end);
+    if (i == 0)
+        for (int k = h - 1; k >= 0; --k)
+            if ((double)q[tfield] / double(1000) > poses[k].offset_time) compensate(q, tfield, poses[k], poses[k + 1], end);
+}
+
+#define FCHK(x)                           \
+    do {                                  \
+        if ((x) != hipSuccess) return -2; \
+    } while (0)
+
+template <class T>
+int fgrow(T** p, int64_t& cap, int64_t need) {
+    if (need <= cap && *p) return 0;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    const int64_t c = std::max<int64_t>(need, cap + cap / 2);
+    if (hipMalloc(p, (size_t)c * sizeof(T)) != hipSuccess) {
+        cap = 0;
+        return -5;
+    }
+    cap = c;
+    return 0;
+}
+
+int ftmp(FilterBuf& b, size_t need) {
+    if (need <= b.tmp_bytes && b.tmp) return 0;
+    if (b.tmp) (void)hipFree(b.tmp);
+    b.tmp = nullptr;
+    if (hipMalloc(&b.tmp, need) != hipSuccess) {
+        b.tmp_bytes = 0;
+        return -5;
+    }
+    b.tmp_bytes = need;
+    return 0;
+}
+
+int reserve(FilterBuf& b, int64_t n) {
+    if (n <= b.cap && b.keys) return 0;
+    const int64_t c = std::max<int64_t>(n, b.cap + b.cap / 2);
+    void* bufs[] = {b.keys, b.keys_alt, b.vals, b.vals_alt, b.head, b.vid};
+    for (void* p : bufs)
+        if (p) (void)hipFree(p);
+    FCHK(hipMalloc(&b.keys, c * sizeof(uint32_t)));
+    FCHK(hipMalloc(&b.keys_alt, c * sizeof(uint32_t)));
+    FCHK(hipMalloc(&b.vals, c * sizeof(uint32_t)));
+    FCHK(hipMalloc(&b.vals_alt, c * sizeof(uint32_t)));
+    FCHK(hipMalloc(&b.head, (c + 1) * sizeof(uint32_t)));
+    FCHK(hipMalloc(&b.vid, (c + 1) * sizeof(uint32_t)));
+    b.cap = c;
+    if (!b.part) FCHK(hipMalloc(&b.part, 6 * 1024 * sizeof(float)));
+    if (!b.geom) FCHK(hipMalloc(&b.geom, sizeof(VoxelGeom)));
+    if (!b.h_small) FCHK(hipHostMalloc(&b.h_small, 256));
+    return 0;
+}
+
+int exscan(FilterBuf& b, const uint32_t* in, uint32_t* out, int64_t n1, hipStream_t st) {
+    size_t bytes = 0;
+    FCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, (int)n1, st));
+    if (ftmp(b, bytes)) return -5;
+    bytes = b.tmp_bytes;
+    FCHK(hipcub::DeviceScan::ExclusiveSum(b.tmp, bytes, in, out, (int)n1, st));
+    return 0;
+}
+
+int sort_pairs(FilterBuf& b, int64_t n, hipStream_t st) {
+    size_t bytes = 0;
+    FCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, b.keys, b.keys_alt, b.vals, b.vals_alt, (int)n, 0, 32, st));
+    if (ftmp(b, bytes)) return -5;
+    bytes = b.tmp_bytes;
+    FCHK(hipcub::DeviceRadixSort::SortPairs(b.tmp, bytes, b.keys, b.keys_alt, b.vals, b.vals_alt, (int)n, 0, 32, st));
+    return 0;
+}
+
+inline int nblk(int64_t n) { return (int)std::max<int64_t>(1, (n + 255) / 256); }
+
+__global__ void records_xyz_kernel(const float* __restrict__ rec, int64_t n, int stride, float* __restrict__ xyz) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    xyz[3 * i] = rec[(size_t)i * stride];
+    xyz[3 * i + 1] = rec[(size_t)i * stride + 1];
+    xyz[3 * i + 2] = rec[(size_t)i * stride + 2];
+}
+
+}  // namespace
+
+int records_to_xyz(const float* d_rec, int64_t n, int stride, float* d_xyz, hipStream_t st) {
+    if (n <= 0) return 0;
+    records_xyz_kernel<<<nblk(n), 256, 0, st>>>(d_rec, n, stride, d_xyz);
+    FCHK(hipGetLastError());
+    return 0;
+}
+
+void filter_free(FilterBuf& b) {
+    void* bufs[] = {b.keys, b.keys_alt, b.vals, b.vals_alt, b.head, b.vid, b.part, b.geom, b.tmp, b.a, b.c, b.aux};
+    for (void* p : bufs)
+        if (p) (void)hipFree(p);
+    if (b.h_small) (void)hipHostFree(b.h_small);
+    b = FilterBuf{};
+}
+
+int voxel_grid(FilterBuf& b, const float* d_in, int64_t n, int stride, const float leaf[3], float* d_out,
+               int64_t* n_out, hipStream_t st) {
+    *n_out = 0;
+    if (n <= 0) return 0;
+    if (stride < 3 || stride > kMaxFields || n >= (int64_t)0x7fffffff) return -1;
+    if (reserve(b, n)) return -5;
+    const int nbA = (int)std::min<int64_t>(1024, (n + 255) / 256);
+    minmax_partial_kernel<<<nbA, 256, 0, st>>>(d_in, n, stride, b.part);
+    voxel_geom_kernel<<<1, 256, 0, st>>>(b.part, nbA, leaf[0], leaf[1], leaf[2], b.geom);
+    voxel_key_kernel<<<nblk(n), 256, 0, st>>>(d_in, n, stride, b.geom, b.keys, b.vals);
+    int rc = sort_pairs(b, n, st);
+    if (rc) return rc;
+    run_head_kernel<<<nblk(n + 1), 256, 0, st>>>(b.keys_alt, n, b.head);
+    rc = exscan(b, b.head, b.vid, n + 1, st);
+    if (rc) return rc;
+    voxel_centroid_kernel<<<nblk(n), 256, 0, st>>>(d_in, stride, b.keys_alt, b.vals_alt, n, b.head, b.vid, d_out);
+    FCHK(hipMemcpyAsync(b.h_small, b.vid + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    FCHK(hipMemcpyAsync(b.h_small + 1, b.geom, sizeof(VoxelGeom), hipMemcpyDeviceToHost, st));
+    FCHK(hipStreamSynchronize(st));
+    VoxelGeom g;
+    std::memcpy(&g, b.h_small + 1, sizeof(VoxelGeom));
+    if (g.overflow) {  // PCL: "Leaf size is too small ... Integer indices would overflow" -> output = input
+        copy_strided_kernel<<<nblk(n * stride), 256, 0, st>>>(d_in, n * stride, d_out);
+        FCHK(hipStreamSynchronize(st));
+        *n_out = n;
+        return 0;
+    }
+    *n_out = b.h_small[0];
+    return 0;
+}
+
+int transform_segments(const float* d_in, int64_t n, int stride, const int64_t* d_seg_off, int nseg,
+                       const double* d_T16, float* d_out, hipStream_t st) {
+    if (n <= 0) return 0;
+    if (stride < 3) return -1;
+    transform_segs_kernel<<<nblk(n), 256, 0, st>>>(d_in, n, stride, d_seg_off, nseg, d_T16, d_out);
+    FCHK(hipGetLastError());
+    return 0;
+}
+
+int scan_preprocess(FilterBuf& b, const float* d_raw, int64_t n, int stride, const ScanPrepParams& p,
+                    const ImuPose* d_poses, int np, const UndistortEnd& end, float* d_out, int64_t* n_out,
+                    hipStream_t st) {
+    *n_out = 0;
+    if (n <= 0) return 0;
+    if (stride < 4 || stride > kMaxFields || p.time_field < 3 || p.time_field >= stride) return -1;
+    if (reserve(b, n)) return -5;
+    int rc = fgrow(&b.a, b.a_cap, n * stride);
+    if (!rc) rc = fgrow(&b.c, b.c_cap, n * stride);
+    if (rc) return rc;
+    // 1. Preprocess selection (stable)
+    const int every = p.point_filter_num > 0 ? p.point_filter_num : 1;
+    scan_select_flags_kernel<<<nblk(n + 1), 256, 0, st>>>(d_raw, n, stride, every, p.blind * p.blind, b.head);
+    rc = exscan(b, b.head, b.vid, n + 1, st);
+    if (rc) return rc;
+    compact_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, b.head, b.vid, b.a);
+    FCHK(hipMemcpyAsync(b.h_small, b.vid + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    FCHK(hipStreamSynchronize(st));
+    const int64_t m = (uint32_t)b.h_small[0];
+    if (m == 0) return 0;
+    // 2. sort by time (stable), 3. undistort
+    time_key_kernel<<<nblk(m), 256, 0, st>>>(b.a, m, stride, p.time_field, b.keys, b.vals);
+    rc = sort_pairs(b, m, st);
+    if (rc) return rc;
+    gather_rows_kernel<<<nblk(m), 256, 0, st>>>(b.a, m, stride, b.vals_alt, b.c);
+    if (np >= 2) undistort_kernel<<<nblk(m), 256, 0, st>>>(b.c, m, stride, p.time_field, d_poses, np, end);
+    // 4. downSizeFilterSurf
+    if (p.leaf > 0.f) {
+        const float leaf[3] = {p.leaf, p.leaf, p.leaf};
+        return voxel_grid(b, b.c, m, stride, leaf, d_out, n_out, st);
+    }
+    FCHK(hipMemcpyAsync(d_out, b.c, (size_t)m * stride * sizeof(float), hipMemcpyDeviceToDevice, st));
+    FCHK(hipStreamSynchronize(st));
+    *n_out = m;
+    return 0;
+}
+
+}  // namespace lio

@@ -1,0 +1,73 @@
+// lio_filter.hpp — point-cloud filters (lio_filter.hip): PCL VoxelGrid,
+// transformPcd, FAST-LIO scan preprocessing / undistortion.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lio {
+
+constexpr int kMaxFields = 8;  // floats per point record (x, y, z, + up to 5 attributes)
+
+struct VoxelGeom {
+    float inv[3];
+    int min_b[3];
+    int mul[3];
+    int overflow;
+    int empty;
+};
+
+// One IMUpose entry (FAST-LIO set_pose6d [U]): offset_time [s] from the scan
+// start, acc (world, gravity added), gyr (bias removed), vel, pos, rot (row-major).
+struct ImuPose {
+    double offset_time;
+    double acc[3], gyr[3], vel[3], pos[3], rot[9];
+};
+
+// State at the scan end (after the last predict): rot/pos of the IMU and the
+// LiDAR-IMU extrinsic, row-major rotation matrices.
+struct UndistortEnd {
+    double pos[3];
+    double R[9];
+    double R_LI[9];
+    double t_LI[3];
+};
+
+struct ScanPrepParams {
+    int point_filter_num;  // keep every n-th input point (Preprocess, kitti.launch:6)
+    float blind;           // drop points with |p| <= blind (kitti.yaml:13)
+    float leaf;            // filter_size_surf (kitti.launch:9); 0 = no downsample
+    int time_field;        // index of the per-point time offset [ms] (FAST-LIO's curvature)
+};
+
+struct FilterBuf {
+    uint32_t *keys = nullptr, *keys_alt = nullptr, *vals = nullptr, *vals_alt = nullptr;
+    uint32_t *head = nullptr, *vid = nullptr;
+    int64_t cap = 0;
+    float* part = nullptr;
+    VoxelGeom* geom = nullptr;
+    void* tmp = nullptr;
+    size_t tmp_bytes = 0;
+    int* h_small = nullptr;  // pinned
+    float* a = nullptr;      // staging records
+    int64_t a_cap = 0;
+    float* c = nullptr;
+    int64_t c_cap = 0;
+    void* aux = nullptr;     // caller-side scratch (host API uploads)
+    size_t aux_bytes = 0;
+};
+
+void filter_free(FilterBuf& b);
+// d_out capacity: n * stride floats.  Synchronises the stream (output count).
+int voxel_grid(FilterBuf& b, const float* d_in, int64_t n, int stride, const float leaf[3], float* d_out,
+               int64_t* n_out, hipStream_t st);
+// points of segment s ([seg_off[s], seg_off[s+1]), nseg segments, seg_off[nseg] = n) through T16[s]
+int transform_segments(const float* d_in, int64_t n, int stride, const int64_t* d_seg_off, int nseg,
+                       const double* d_T16, float* d_out, hipStream_t st);
+// selection -> stable sort by time -> undistortion (np >= 2 poses) -> voxel grid
+int scan_preprocess(FilterBuf& b, const float* d_raw, int64_t n, int stride, const ScanPrepParams& p,
+                    const ImuPose* d_poses, int np, const UndistortEnd& end, float* d_out, int64_t* n_out,
+                    hipStream_t st);
+
+int records_to_xyz(const float* d_rec, int64_t n, int stride, float* d_xyz, hipStream_t st);
+
+}  // namespace lio

@@ -28,7 +28,8 @@ EXPORTS = [
     "lio_map_create", "lio_map_destroy", "lio_map_build", "lio_map_build_device", "lio_map_size",
     "lio_map_get_points", "lio_map_get_grid", "lio_map_num_ids", "lio_map_get_by_id", "lio_map_add",
     "lio_map_add_device", "lio_map_delete_boxes", "lio_localmap_update", "lio_map_incremental",
-    "lio_ctx_get_knn_pose",
+    "lio_ctx_get_knn_pose", "lio_filter_create", "lio_filter_destroy", "lio_voxel_grid", "lio_submap_voxelize",
+    "lio_preprocess", "lio_scan_preprocess",
     "lio_ctx_create", "lio_ctx_destroy", "lio_scan_set", "lio_scan_set_device", "lio_match",
     "lio_get_knn", "lio_get_planes", "lio_get_world", "lio_get_h_rows", "lio_ctx_knn_stats",
     "lio_ieskf_update",
@@ -93,6 +94,16 @@ class IncrementalStats(C.Structure):
                 ("n_added_downsample", C.c_int64)]
 
 
+class ImuPose(C.Structure):
+    _fields_ = [("offset_time", C.c_double), ("acc", C.c_double * 3), ("gyr", C.c_double * 3), ("vel", C.c_double * 3),
+                ("pos", C.c_double * 3), ("rot", C.c_double * 9)]
+
+
+class ScanPrepParams(C.Structure):
+    _fields_ = [("point_filter_num", C.c_int), ("blind", C.c_float), ("filter_size_surf", C.c_float),
+                ("time_field", C.c_int)]
+
+
 class KernelTiming(C.Structure):
     _fields_ = [("knn_launches", C.c_int64), ("knn_ms", C.c_double), ("reuse_launches", C.c_int64),
                 ("reuse_ms", C.c_double), ("final_launches", C.c_int64), ("final_ms", C.c_double),
@@ -130,6 +141,15 @@ def _declare(L):
                                           C.POINTER(C.c_int)]),
         "lio_map_incremental": (C.c_int, [vp, C.POINTER(Pose), C.c_double, C.POINTER(IncrementalStats)]),
         "lio_ctx_get_knn_pose": (C.c_int, [vp, C.POINTER(Pose)]),
+        "lio_filter_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
+        "lio_filter_destroy": (C.c_int, [vp]),
+        "lio_voxel_grid": (C.c_int, [vp, fp, C.c_int64, C.c_int, fp, fp, C.POINTER(C.c_int64)]),
+        "lio_submap_voxelize": (C.c_int, [vp, fp, C.POINTER(C.c_int64), C.c_int, C.c_int, dp, C.c_float, fp,
+                                          C.POINTER(C.c_int64)]),
+        "lio_preprocess": (C.c_int, [vp, fp, C.c_int64, C.c_int, C.POINTER(ScanPrepParams), C.POINTER(ImuPose), C.c_int,
+                                     C.POINTER(Pose), fp, C.POINTER(C.c_int64)]),
+        "lio_scan_preprocess": (C.c_int, [vp, fp, C.c_int64, C.c_int, C.POINTER(ScanPrepParams), C.POINTER(ImuPose),
+                                          C.c_int, C.POINTER(Pose), C.POINTER(C.c_int64)]),
         "lio_ctx_create": (C.c_int, [vp, C.POINTER(MatchParams), C.POINTER(vp)]),
         "lio_ctx_destroy": (C.c_int, [vp]),
         "lio_scan_set": (C.c_int, [vp, fp, C.c_int64]),

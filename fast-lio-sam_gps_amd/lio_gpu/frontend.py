@@ -231,6 +231,20 @@ class HShareModelGPU:
         check(lib().lio_ctx_knn_stats(self._h, C.byref(pose), _dp(sums), st.ctypes.data_as(C.POINTER(C.c_int32))))
         return sums, st
 
+    def preprocess_scan(self, raw: np.ndarray, imu_poses, end_pose, point_filter_num=4, blind=2.0,
+                        filter_size_surf=0.5, time_field=4) -> int:
+        """Raw scan -> Preprocess + UndistortPcl + downSizeFilterSurf straight into this scan
+        (feats_down_body) on the device; returns feats_down_size."""
+        from .filters import imu_poses_to_c
+
+        raw = np.ascontiguousarray(raw, dtype=np.float32)
+        prm = _capi.ScanPrepParams(point_filter_num, blind, filter_size_surf, time_field)
+        n = C.c_int64(0)
+        check(lib().lio_scan_preprocess(self._h, _fp(raw), len(raw), raw.shape[1], C.byref(prm),
+                                        imu_poses_to_c(imu_poses), len(imu_poses), C.byref(end_pose), C.byref(n)))
+        self.n = int(n.value)
+        return self.n
+
     def last_knn_pose24(self) -> np.ndarray:
         """pose24 of the last kNN evaluation (the pose Nearest_Points belong to)."""
         p = _capi.Pose()

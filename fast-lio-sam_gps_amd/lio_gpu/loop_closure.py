@@ -29,6 +29,15 @@ class LoopClosureConfig:  # loop_closure.h:21-29, values from fast_lio_sam.cpp:6
 
 
 @dataclasses.dataclass
+class PosePcd:  # pose_pcd.hpp:7-19 (the fields setSrcAndDstCloud reads)
+    pcd_: np.ndarray  # PointXYZI rows (x, y, z, intensity), float32
+    pose_corrected_eig_: np.ndarray = dataclasses.field(default_factory=lambda: np.eye(4))
+    pose_eig_: np.ndarray = dataclasses.field(default_factory=lambda: np.eye(4))
+    timestamp_: float = 0.0
+    idx_: int = 0
+
+
+@dataclasses.dataclass
 class RegistrationOutput:  # loop_closure.h:31-37
     is_valid_: bool = False
     is_converged_: bool = False
@@ -36,6 +45,12 @@ class RegistrationOutput:  # loop_closure.h:31-37
     pose_between_eig_: np.ndarray = dataclasses.field(default_factory=lambda: np.eye(4))
     iterations: int = 0
     state: int = 0
+
+
+def _xyz(cloud) -> np.ndarray:
+    """xyz columns of a cloud given as (n, 3) or PointXYZI-like (n, >= 3) rows."""
+    a = np.asarray(cloud, dtype=np.float32)
+    return a.reshape(-1, 3) if a.ndim == 1 else a[:, :3]
 
 
 def icp_params(config: LoopClosureConfig, cell_size: float = 2.0, device: int = 0) -> _capi.IcpParams:
@@ -70,11 +85,11 @@ class LoopClosure:
         return {k: getattr(t, k) for k, _ in _capi.KernelTiming._fields_}
 
     def setInputTarget(self, dst: np.ndarray):
-        d = np.ascontiguousarray(dst, dtype=np.float32).reshape(-1, 3)
+        d = np.ascontiguousarray(_xyz(dst), dtype=np.float32)
         check(lib().lio_icp_set_target(self._h, d.ctypes.data_as(C.POINTER(C.c_float)), len(d)))
 
     def setInputSource(self, src: np.ndarray):
-        s = np.ascontiguousarray(src, dtype=np.float32).reshape(-1, 3)
+        s = np.ascontiguousarray(_xyz(src), dtype=np.float32)
         check(lib().lio_icp_set_source(self._h, s.ctypes.data_as(C.POINTER(C.c_float)), len(s)))
         self._ns = len(s)
 
@@ -93,6 +108,27 @@ class LoopClosure:
         if out is not None:
             self.aligned_ = out
         return res
+
+    def setSrcAndDstCloud(self, keyframes, src_idx: int, dst_idx: int, submap_range: int, voxel_res: float):
+        """loop_closure.cpp:42-67 on the GPU: per side, transformPcd of keyframes
+        [idx - range, idx + range] (skipping i >= keyframes.size() - 1: the newest keyframe
+        never enters a submap, :54/:62), concatenated, voxelizePcd(voxel_res)."""
+        from .filters import VoxelGrid, voxelize_submap
+
+        if getattr(self, "_vg", None) is None:
+            self._vg = VoxelGrid(voxel_res, device=self._p.device)
+
+        def side(center):
+            clouds, poses = [], []
+            for i in range(center - submap_range, center + submap_range + 1):
+                if 0 <= i < len(keyframes) - 1:
+                    clouds.append(np.asarray(keyframes[i].pcd_, np.float32).reshape(-1, 4))
+                    poses.append(keyframes[i].pose_corrected_eig_)
+            if not clouds:
+                return np.zeros((0, 4), np.float32)
+            return voxelize_submap(clouds, poses, voxel_res, self._vg)
+
+        return side(src_idx), side(dst_idx)
 
     def icpAlignment(self, src: np.ndarray, dst: np.ndarray) -> RegistrationOutput:
         """loop_closure.cpp:69-92: align src to dst; valid iff converged and score < threshold."""

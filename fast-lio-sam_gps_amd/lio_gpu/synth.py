@@ -397,3 +397,44 @@ def make_icp_pair(n_points: int = 500_000, seed: int = 4321, voxel: float = 0.3,
     T[:3, 3] = t
     dst = (tgt.astype(np.float64) @ R.T + t).astype(np.float32)
     return src, np.ascontiguousarray(dst), T
+
+
+# ----------------------------------------------------------------------------
+# Raw scans for the preprocessing path
+# ----------------------------------------------------------------------------
+def rotz(a):
+    c, s = math.cos(a), math.sin(a)
+    return np.array([[c, -s, 0.0], [s, c, 0.0], [0.0, 0.0, 1.0]])
+
+
+def make_raw_scan(scene: Scene, n: int = 120_000, kind: str = "kitti64", seed: int = 7, speed: float = 8.0,
+                  yaw_rate: float = 0.3, duration: float = 0.1, imu_hz: float = 100.0):
+    """A raw LiDAR sweep with per-point time offsets and the IMU poses of that sweep.
+
+    Returns (raw, imu_poses, end24): raw rows (x, y, z, intensity, time_ms) in the LiDAR frame,
+    in firing (azimuth) order with time = azimuth fraction * duration; imu_poses as FAST-LIO's
+    IMUpose list (set_pose6d: offset_time, acc, gyr, vel, pos, rot) for constant forward speed
+    and yaw rate; end24 = pose24 of the state at the sweep end (lio_pose layout).
+    """
+    sc = make_scan(scene, n, kind, pos_gt=[0.0, 0.0, 0.0], yaw_gt=0.0, seed=seed)
+    rng = np.random.default_rng(seed)
+    b = sc.body.astype(np.float32)
+    az = np.arctan2(b[:, 1], b[:, 0])
+    t_ms = ((az + np.pi) / (2 * np.pi) * duration * 1000.0).astype(np.float32)
+    inten = rng.uniform(0, 255, len(b)).astype(np.float32)
+    raw = np.concatenate([b, inten[:, None], t_ms[:, None]], axis=1).astype(np.float32)
+    raw = raw[np.argsort(az, kind="stable")]
+    poses = []
+    k = int(round(duration * imu_hz))
+    for j in range(k + 1):
+        t = j / imu_hz
+        yaw = yaw_rate * t
+        R = rotz(yaw)
+        vel = R @ np.array([speed, 0.0, 0.0])
+        poses.append(dict(offset_time=t, acc=np.array([0.0, speed * yaw_rate, 0.0]) + rng.normal(0, 0.01, 3),
+                          gyr=np.array([0.0, 0.0, yaw_rate]) + rng.normal(0, 0.001, 3), vel=vel,
+                          pos=np.array([speed * t, 0.5 * speed * yaw_rate * t * t, 0.0]), rot=R))
+    e = poses[-1]
+    end24 = np.concatenate([e["rot"].ravel(), e["pos"] + rng.normal(0, 0.002, 3), np.eye(3).ravel(),
+                            T_LI]).astype(np.float64)
+    return raw, poses, end24

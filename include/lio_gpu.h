@@ -246,6 +246,48 @@ int lio_map_incremental(lio_ctx* c, const lio_pose* pose, double filter_size_map
 /* pose of the ctx's last kNN evaluation (the pose Nearest_Points belong to) */
 int lio_ctx_get_knn_pose(lio_ctx* c, lio_pose* out);
 
+/* ------------------------------------------ filters */
+typedef struct lio_filter lio_filter;
+int lio_filter_create(int device, lio_filter** out);
+int lio_filter_destroy(lio_filter* f);
+
+/* pcl::VoxelGrid<PointT>::filter, PCL 1.10 applyFilter [U] (FAST-LIO downSizeFilterSurf,
+ * voxelizePcd utilities.hpp:161-183): pts is n x stride floats (x, y, z first; stride 3..8);
+ * every field is averaged per voxel (downsample_all_data_ = true), summed in input order inside
+ * a voxel (PCL's std::sort order there is unspecified); output in voxel-index order (out capacity
+ * n x stride); non-finite points are dropped; index overflow returns the input unchanged (as PCL). */
+int lio_voxel_grid(lio_filter* f, const float* pts, int64_t n, int stride, const float leaf[3], float* out,
+                   int64_t* n_out);
+
+/* One side of LoopClosure::setSrcAndDstCloud (loop_closure.cpp:42-67): the nk keyframe clouds
+ * (segments [seg_off[k], seg_off[k+1]) of pts) each through transformPcd(cloud, pose_k)
+ * (utilities.hpp:132-143: pcl::transformPointCloud with a double 4x4, row-major poses16[16k..]),
+ * concatenated in order, then voxelizePcd(voxel_res). */
+int lio_submap_voxelize(lio_filter* f, const float* pts, const int64_t* seg_off, int nk, int stride,
+                        const double* poses16, float voxel_res, float* out, int64_t* n_out);
+
+/* FAST-LIO front-end preprocessing of one raw scan [U]: Preprocess selection (every
+ * point_filter_num-th point with |p| > blind), ImuProcess::UndistortPcl (sort by the per-point
+ * time offset in ms, field time_field; backward propagation through the IMU poses of the scan
+ * to the scan-end state `end`), then downSizeFilterSurf (VoxelGrid, filter_size_surf; 0 = off). */
+typedef struct lio_imu_pose {  /* set_pose6d: offset from scan start [s], acc, gyr, vel, pos, rot */
+    double offset_time;
+    double acc[3], gyr[3], vel[3], pos[3];
+    double rot[9];
+} lio_imu_pose;
+typedef struct lio_scan_prep_params {
+    int point_filter_num;   /* kitti.launch:6 = 4 */
+    float blind;            /* kitti.yaml:13 = 2 */
+    float filter_size_surf; /* kitti.launch:9 = 0.5 */
+    int time_field;         /* index of the time offset [ms] in a record (FAST-LIO's curvature) */
+} lio_scan_prep_params;
+/* to host memory: out capacity n x stride, *n_out records (x, y, z, ... averaged)            */
+int lio_preprocess(lio_filter* f, const float* raw, int64_t n, int stride, const lio_scan_prep_params* p,
+                   const lio_imu_pose* poses, int n_poses, const lio_pose* end, float* out, int64_t* n_out);
+/* straight into the ctx's scan (feats_down_body) without a host round trip; *n_down points */
+int lio_scan_preprocess(lio_ctx* c, const float* raw, int64_t n, int stride, const lio_scan_prep_params* p,
+                        const lio_imu_pose* poses, int n_poses, const lio_pose* end, int64_t* n_down);
+
 /* ----------------------------------------------------------------- timing */
 typedef struct lio_kernel_timing {
     int64_t knn_launches;   double knn_ms;     /* kNN h-evaluation: near + far + plane/H  */

@@ -1355,6 +1355,183 @@ static void map_incremental(DynMap& dm, const float* body, int64_t n, const Pose
     stats[3] = c;
 }
 
+
+// ---------------------------------------------------------------------------
+// Point-cloud filters.
+//
+// voxel_grid = pcl::VoxelGrid<PointT>::applyFilter, PCL 1.10 [U], with
+//   downsample_all_data_ = true and min_points_per_voxel_ = 0:
+//   getMinMax3D over finite points; inverse_leaf = 1/leaf (float);
+//   min_b = (int)floor(min_p * inv), max_b = (int)floor(max_p * inv);
+//   div_b = max_b - min_b + 1, divb_mul = (1, div_b.x, div_b.x*div_b.y);
+//   overflow (div_b product > INT_MAX) -> output = input;
+//   idx = (int)(floor(p*inv) - (float)min_b) . divb_mul; sort by idx (PCL's
+//   std::sort leaves the order inside a voxel unspecified: here input order);
+//   centroid = fields summed in that order, / (float)count; output by idx.
+// transform_segments = pcl::transformPointCloud(in, out, Matrix4d) [U]:
+//   Transformer<double>::se3, ((m0 x + m1 y) + m2 z) + m3 in double -> float;
+//   non-finite points kept unchanged (the !is_dense branch).
+// preprocess = FAST-LIO Preprocess selection (i % point_filter_num == 0 and
+//   x*x+y*y+z*z > blind^2) + ImuProcess::UndistortPcl (sort by time — stable
+//   here, std::sort in the reference — and backward propagation, rotations as
+//   matrices) + downSizeFilterSurf (voxel_grid) [U].
+// ---------------------------------------------------------------------------
+static int64_t voxel_grid(const float* p, int64_t n, int stride, const float leaf[3], float* out) {
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int64_t i = 0; i < n; ++i) {
+        const float* q = p + (size_t)i * stride;
+        if (!(std::isfinite(q[0]) && std::isfinite(q[1]) && std::isfinite(q[2]))) continue;
+        for (int d = 0; d < 3; ++d) {
+            lo[d] = std::min(lo[d], q[d]);
+            hi[d] = std::max(hi[d], q[d]);
+        }
+    }
+    if (!(lo[0] <= hi[0])) return 0;
+    float inv[3];
+    int min_b[3];
+    int64_t div[3];
+    for (int d = 0; d < 3; ++d) {
+        inv[d] = 1.0f / leaf[d];
+        min_b[d] = (int)std::floor(lo[d] * inv[d]);
+        const int max_b = (int)std::floor(hi[d] * inv[d]);
+        div[d] = (int64_t)max_b - min_b[d] + 1;
+    }
+    if (div[0] * div[1] * div[2] > (int64_t)std::numeric_limits<int32_t>::max()) {
+        std::memcpy(out, p, (size_t)n * stride * sizeof(float));
+        return n;
+    }
+    const int mul[3] = {1, (int)div[0], (int)(div[0] * div[1])};
+    std::vector<std::pair<int, int64_t>> idx;
+    idx.reserve(n);
+    for (int64_t i = 0; i < n; ++i) {
+        const float* q = p + (size_t)i * stride;
+        if (!(std::isfinite(q[0]) && std::isfinite(q[1]) && std::isfinite(q[2]))) continue;
+        int k = 0;
+        for (int d = 0; d < 3; ++d) k += (int)(std::floor(q[d] * inv[d]) - (float)min_b[d]) * mul[d];
+        idx.emplace_back(k, i);
+    }
+    std::stable_sort(idx.begin(), idx.end(), [](const std::pair<int, int64_t>& a, const std::pair<int, int64_t>& b) {
+        return a.first < b.first;
+    });
+    int64_t m = 0;
+    for (size_t j = 0; j < idx.size();) {
+        size_t e = j;
+        float acc[16] = {0};
+        while (e < idx.size() && idx[e].first == idx[j].first) {
+            const float* q = p + (size_t)idx[e].second * stride;
+            for (int f = 0; f < stride; ++f) acc[f] += q[f];
+            ++e;
+        }
+        for (int f = 0; f < stride; ++f) out[(size_t)m * stride + f] = acc[f] / (float)(e - j);
+        ++m;
+        j = e;
+    }
+    return m;
+}
+
+static void transform_segments(const float* in, int64_t n, int stride, const int64_t* seg, int nseg,
+                               const double* T16, float* out) {
+    for (int s = 0; s < nseg; ++s) {
+        const double* m = T16 + 16 * s;
+        for (int64_t i = seg[s]; i < seg[s + 1] && i < n; ++i) {
+            const float* q = in + (size_t)i * stride;
+            float* o = out + (size_t)i * stride;
+            std::memcpy(o, q, stride * sizeof(float));
+            if (!(std::isfinite(q[0]) && std::isfinite(q[1]) && std::isfinite(q[2]))) continue;
+            const double x = q[0], y = q[1], z = q[2];
+            o[0] = (float)(((m[0] * x + m[1] * y) + m[2] * z) + m[3]);
+            o[1] = (float)(((m[4] * x + m[5] * y) + m[6] * z) + m[7]);
+            o[2] = (float)(((m[8] * x + m[9] * y) + m[10] * z) + m[11]);
+        }
+    }
+}
+
+struct ImuPoseO {
+    double offset_time;
+    double acc[3], gyr[3], vel[3], pos[3], rot[9];
+};
+
+// FAST-LIO so3_math.h Exp(ang_vel, dt) [U]
+static void so3_exp(const double w[3], double dt, double E[9]) {
+    const double nrm = std::sqrt((w[0] * w[0] + w[1] * w[1]) + w[2] * w[2]);
+    for (int k = 0; k < 9; ++k) E[k] = (k % 4 == 0) ? 1.0 : 0.0;
+    if (!(nrm > 0.0000001)) return;
+    const double r[3] = {w[0] / nrm, w[1] / nrm, w[2] / nrm};
+    const double K[9] = {0.0, -r[2], r[1], r[2], 0.0, -r[0], -r[1], r[0], 0.0};
+    const double a = nrm * dt, sn = std::sin(a), c1 = 1.0 - std::cos(a);
+    for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+            const double kk = ((c1 * K[3 * i + 0]) * K[0 + j] + (c1 * K[3 * i + 1]) * K[3 + j]) + (c1 * K[3 * i + 2]) * K[6 + j];
+            E[3 * i + j] = (E[3 * i + j] + sn * K[3 * i + j]) + kk;
+        }
+}
+
+// UndistortPcl's backward loop over a time-sorted cloud [U], literally: the
+// point iterator walks back through the IMU segments; at the first point the
+// inner loop `break`s without stepping, so every later (earlier-in-time)
+// segment whose head is older than that point compensates it again — a quirk
+// of the reference kept here (it only bites when the earliest point lies past
+// the first IMU sample).
+static void compensate(float* q, int tf, const ImuPoseO& hd, const ImuPoseO& tl, const Pose& end) {
+    const double dt = (double)q[tf] / double(1000) - hd.offset_time;
+    double E[9], Ri[9];
+    so3_exp(tl.gyr, dt, E);
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c)
+            Ri[3 * r + c] = (hd.rot[3 * r] * E[c] + hd.rot[3 * r + 1] * E[3 + c]) + hd.rot[3 * r + 2] * E[6 + c];
+    double Tei[3];
+    for (int k = 0; k < 3; ++k) Tei[k] = ((hd.pos[k] + hd.vel[k] * dt) + ((0.5 * tl.acc[k]) * dt) * dt) - end.t[k];
+    const double Pi[3] = {q[0], q[1], q[2]};
+    double a[3], b[3], c[3];
+    for (int r = 0; r < 3; ++r) a[r] = ((end.RLI[3 * r] * Pi[0] + end.RLI[3 * r + 1] * Pi[1]) + end.RLI[3 * r + 2] * Pi[2]) + end.tLI[r];
+    for (int r = 0; r < 3; ++r) b[r] = ((Ri[3 * r] * a[0] + Ri[3 * r + 1] * a[1]) + Ri[3 * r + 2] * a[2]) + Tei[r];
+    for (int r = 0; r < 3; ++r) c[r] = ((end.R[r] * b[0] + end.R[3 + r] * b[1]) + end.R[6 + r] * b[2]) - end.tLI[r];
+    for (int r = 0; r < 3; ++r) a[r] = (end.RLI[r] * c[0] + end.RLI[3 + r] * c[1]) + end.RLI[6 + r] * c[2];
+    q[0] = (float)a[0];
+    q[1] = (float)a[1];
+    q[2] = (float)a[2];
+}
+
+static void undistort(float* p, int64_t n, int stride, int tf, const ImuPoseO* poses, int np, const Pose& end) {
+    if (np < 2 || n == 0) return;
+    int64_t it = n - 1;
+    for (int kp = np - 1; kp >= 1; --kp) {
+        const ImuPoseO& hd = poses[kp - 1];
+        const ImuPoseO& tl = poses[kp];
+        for (; (double)p[(size_t)it * stride + tf] / double(1000) > hd.offset_time; --it) {
+            compensate(p + (size_t)it * stride, tf, hd, tl, end);
+            if (it == 0) break;
+        }
+    }
+}
+
+static int64_t preprocess(const float* raw, int64_t n, int stride, int every, float blind, float leaf, int tf,
+                          const ImuPoseO* poses, int np, const Pose& end, float* out) {
+    std::vector<float> sel;
+    sel.reserve((size_t)n * stride);
+    if (every < 1) every = 1;
+    for (int64_t i = 0; i < n; ++i) {
+        const float* q = raw + (size_t)i * stride;
+        if (i % every == 0 && (q[0] * q[0] + q[1] * q[1] + q[2] * q[2]) > blind * blind) sel.insert(sel.end(), q, q + stride);
+    }
+    const int64_t m = (int64_t)sel.size() / stride;
+    std::vector<int64_t> order(m);
+    std::iota(order.begin(), order.end(), 0);
+    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) {
+        return sel[(size_t)a * stride + tf] < sel[(size_t)b * stride + tf];
+    });
+    std::vector<float> srt((size_t)m * stride);
+    for (int64_t i = 0; i < m; ++i)
+        std::memcpy(&srt[(size_t)i * stride], &sel[(size_t)order[i] * stride], stride * sizeof(float));
+    undistort(srt.data(), m, stride, tf, poses, np, end);
+    if (leaf > 0.f) {
+        const float lf[3] = {leaf, leaf, leaf};
+        return voxel_grid(srt.data(), m, stride, lf, out);
+    }
+    std::memcpy(out, srt.data(), srt.size() * sizeof(float));
+    return m;
+}
+
 }  // namespace orc
 
 // =============================================================================
@@ -1369,7 +1546,29 @@ struct orc_state {
 };
 struct orc_icp_params { double max_corr_dist, trans_eps, fitness_eps; int max_iter; double rot_eps, score_threshold; };
 
-int orc_version(void) { return 2; }
+int orc_version(void) { return 3; }
+
+// ---- filters ----
+int64_t orc_voxel_grid(const float* p, int64_t n, int stride, const float* leaf3, float* out) {
+    if (stride < 3 || stride > 16) return -1;
+    return orc::voxel_grid(p, n, stride, leaf3, out);
+}
+int64_t orc_submap_voxelize(const float* p, const int64_t* seg, int nseg, int stride, const double* T16,
+                            float voxel_res, float* out) {
+    if (stride < 3 || stride > 16) return -1;
+    const int64_t n = nseg > 0 ? seg[nseg] : 0;
+    std::vector<float> tf((size_t)n * stride);
+    orc::transform_segments(p, n, stride, seg, nseg, T16, tf.data());
+    const float leaf[3] = {voxel_res, voxel_res, voxel_res};
+    return orc::voxel_grid(tf.data(), n, stride, leaf, out);
+}
+int64_t orc_preprocess(const float* raw, int64_t n, int stride, int every, float blind, float leaf, int tf,
+                       const double* poses, int np, const double* end24, float* out) {
+    orc::Pose e;
+    std::memcpy(&e, end24, sizeof(e));
+    return orc::preprocess(raw, n, stride, every, blind, leaf, tf, (const orc::ImuPoseO*)poses, np, e, out);
+}
+
 
 // ---- incremental map (DynMap) ----
 void* orc_dmap_create(const float* xyz, int64_t n) {

@@ -95,6 +95,14 @@ def lib():
                                    C.POINTER(C.c_float)]
         L.orc_map_incremental.argtypes = [vp, C.POINTER(C.c_float), i64, C.POINTER(C.c_double),
                                           C.POINTER(C.c_double), C.c_double, C.c_float, C.POINTER(C.c_int64)]
+        L.orc_voxel_grid.restype = i64
+        L.orc_voxel_grid.argtypes = [C.POINTER(C.c_float), i64, C.c_int, C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.orc_submap_voxelize.restype = i64
+        L.orc_submap_voxelize.argtypes = [C.POINTER(C.c_float), C.POINTER(C.c_int64), C.c_int, C.c_int,
+                                          C.POINTER(C.c_double), C.c_float, C.POINTER(C.c_float)]
+        L.orc_preprocess.restype = i64
+        L.orc_preprocess.argtypes = [C.POINTER(C.c_float), i64, C.c_int, C.c_int, C.c_float, C.c_float, C.c_int,
+                                     C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_float)]
         _lib = L
     return _lib
 
@@ -246,3 +254,41 @@ class OracleDynMap:
                                   float(fs), C.c_float(ds), _p(st, C.c_int64))
         return dict(n_to_add=int(st[0]), n_no_downsample=int(st[1]), n_skipped=int(st[2]),
                     n_added_downsample=int(st[3]))
+
+
+def voxel_grid(pts, leaf):
+    """pcl::VoxelGrid (PCL 1.10) restatement; pts (n, stride) float32."""
+    pts = np.ascontiguousarray(pts, dtype=np.float32)
+    leaf3 = np.ascontiguousarray(np.broadcast_to(np.asarray(leaf, np.float32), 3))
+    out = np.empty_like(pts)
+    m = lib().orc_voxel_grid(_p(pts, C.c_float), len(pts), pts.shape[1], _p(leaf3, C.c_float), _p(out, C.c_float))
+    assert m >= 0
+    return out[:m].copy()
+
+
+def submap_voxelize(clouds, poses, voxel_res):
+    clouds = [np.ascontiguousarray(c, dtype=np.float32) for c in clouds]
+    seg = np.zeros(len(clouds) + 1, np.int64)
+    for k, c in enumerate(clouds):
+        seg[k + 1] = seg[k] + len(c)
+    pts = np.ascontiguousarray(np.concatenate(clouds))
+    T = np.ascontiguousarray(np.stack([np.asarray(p, np.float64).reshape(4, 4) for p in poses]))
+    out = np.empty_like(pts)
+    m = lib().orc_submap_voxelize(_p(pts, C.c_float), _p(seg, C.c_int64), len(clouds), pts.shape[1],
+                                  _p(T, C.c_double), C.c_float(voxel_res), _p(out, C.c_float))
+    return out[:m].copy()
+
+
+def preprocess(raw, imu_poses, end24, point_filter_num=4, blind=2.0, leaf=0.5, time_field=4):
+    """Preprocess + UndistortPcl + downSizeFilterSurf restatement.  imu_poses: list of dicts."""
+    raw = np.ascontiguousarray(raw, dtype=np.float32)
+    P = np.zeros((max(len(imu_poses), 1), 22), np.float64)
+    for k, p in enumerate(imu_poses):
+        P[k] = np.concatenate([[p["offset_time"]], p["acc"], p["gyr"], p["vel"], p["pos"],
+                               np.asarray(p["rot"], float).ravel()])
+    e = np.ascontiguousarray(end24, dtype=np.float64)
+    out = np.empty_like(raw)
+    m = lib().orc_preprocess(_p(raw, C.c_float), len(raw), raw.shape[1], point_filter_num, C.c_float(blind),
+                             C.c_float(leaf), time_field, _p(P, C.c_double), len(imu_poses), _p(e, C.c_double),
+                             _p(out, C.c_float))
+    return out[:m].copy()

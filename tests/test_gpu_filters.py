@@ -1,0 +1,101 @@
+"""GPU parity of the point-cloud filters against the oracle.
+
+Bars: VoxelGrid and transformPcd + voxelizePcd bit-exact (same float op order,
+input order inside a voxel); scan preprocessing (Preprocess + UndistortPcl +
+downSizeFilterSurf) within one float ulp (the undistortion's sin/cos come from
+the device and host math libraries) and the same number of points.
+"""
+import math
+
+import numpy as np
+import pytest
+
+from lio_gpu import filters as FL
+from lio_gpu import frontend as F
+from lio_gpu import loop_closure as LC
+from lio_gpu import synth
+
+pytestmark = pytest.mark.gpu
+f32 = np.float32
+
+
+def test_voxel_grid_bit_exact(oracle):
+    rng = np.random.default_rng(21)
+    vg = FL.VoxelGrid(0.5)
+    for stride in (3, 4, 5, 8):
+        pts = rng.uniform(-30, 30, (200_000, stride)).astype(f32)
+        pts[:, 2] *= 0.1
+        pts[::1013, 0] = np.nan
+        for leaf in (0.3, 0.5, 2.0):
+            vg.setLeafSize(leaf, leaf, leaf)
+            np.testing.assert_array_equal(vg.filter(pts), oracle.voxel_grid(pts, leaf))
+    # clustered (many points per voxel), anisotropic leaf
+    c = (rng.normal(0, 0.05, (50_000, 4)) + np.repeat(rng.uniform(-5, 5, (500, 4)), 100, axis=0)).astype(f32)
+    vg.setLeafSize(0.2, 0.4, 0.3)
+    np.testing.assert_array_equal(vg.filter(c), oracle.voxel_grid(c, [0.2, 0.4, 0.3]))
+    # index overflow: PCL returns the input
+    big = np.array([[0, 0, 0], [1e6, 1e6, 1e6], [5, 5, 5]], f32)
+    vg.setLeafSize(1e-3, 1e-3, 1e-3)
+    np.testing.assert_array_equal(vg.filter(big), big)
+
+
+def test_submap_voxelize_bit_exact(oracle):
+    scene, m, scans = synth.make_config("C1", n_scans=6)
+    rng = np.random.default_rng(5)
+    kfs = []
+    for k, sc in enumerate(scans):
+        pcd = np.concatenate([sc.body, rng.uniform(0, 255, (len(sc.body), 1))], axis=1).astype(f32)
+        T = np.eye(4)
+        T[:3, :3] = synth.quat_to_mat(sc.rot_gt)
+        T[:3, 3] = sc.pos_gt
+        kfs.append(LC.PosePcd(pcd_=pcd, pose_corrected_eig_=T))
+    lc = LC.LoopClosure(LC.LoopClosureConfig())
+    src, dst = lc.setSrcAndDstCloud(kfs, src_idx=4, dst_idx=1, submap_range=2, voxel_res=0.3)
+    # reference loop: i in [idx - range, idx + range], 0 <= i < keyframes.size() - 1 (newest excluded)
+    def ref(center):
+        ids = [i for i in range(center - 2, center + 3) if 0 <= i < len(kfs) - 1]
+        return oracle.submap_voxelize([kfs[i].pcd_ for i in ids], [kfs[i].pose_corrected_eig_ for i in ids], 0.3)
+    np.testing.assert_array_equal(src, ref(4))
+    np.testing.assert_array_equal(dst, ref(1))
+    # the voxelized submaps feed icpAlignment (xyz of PointXYZI rows)
+    out = lc.icpAlignment(src, dst)
+    assert np.isfinite(out.score_)
+
+
+def _close(a, b):
+    assert a.shape == b.shape
+    np.testing.assert_allclose(a, b, rtol=2e-7, atol=2e-6)
+
+
+def test_preprocess_matches_oracle(oracle):
+    scene = synth.make_scene(400.0, 1234)
+    raw, poses, end24 = synth.make_raw_scan(scene, 120_000, seed=3)
+    end = F.pose_from_pose24(end24)
+    for leaf in (0.0, 0.5):
+        pp = FL.ScanPreprocessor(point_filter_num=4, blind=2.0, filter_size_surf=leaf, time_field=4)
+        g = pp.process(raw, poses, end)
+        o = oracle.preprocess(raw, poses, end24, point_filter_num=4, blind=2.0, leaf=leaf)
+        _close(g, o)
+    # earliest point past the first IMU sample: the reference's repeated compensation of the first point
+    raw2 = raw[raw[:, 4] > 35.0]
+    pp = FL.ScanPreprocessor(point_filter_num=1, blind=2.0, filter_size_surf=0.0, time_field=4)
+    _close(pp.process(raw2, poses, end), oracle.preprocess(raw2, poses, end24, point_filter_num=1, leaf=0.0))
+
+
+def test_scan_preprocess_into_ctx(oracle):
+    """Raw scan -> feats_down_body on the device -> h_share_model, without a host round trip."""
+    scene = synth.make_scene(400.0, 1234)
+    raw, poses, end24 = synth.make_raw_scan(scene, 120_000, seed=4)
+    m = synth.sample_surface(scene, 200_000, 1234)
+    tree = F.IkdTreeGPU(cell_size=1.0)
+    tree.Build(m)
+    hm = F.HShareModelGPU(tree)
+    n = hm.preprocess_scan(raw, poses, F.pose_from_pose24(end24), point_filter_num=4, blind=2.0,
+                           filter_size_surf=0.5, time_field=4)
+    o = oracle.preprocess(raw, poses, end24, point_filter_num=4, blind=2.0, leaf=0.5)
+    assert n == len(o) > 0
+    p24 = np.zeros(24)
+    p24[0:9] = np.eye(3).ravel()
+    p24[12:21] = np.eye(3).ravel()
+    hm(p24, True)
+    np.testing.assert_allclose(hm.world(), o[:, :3], rtol=2e-7, atol=2e-6)
