@@ -958,6 +958,263 @@ int lio_scan_preprocess(lio_ctx* c, const float* raw, int64_t n, int stride, con
 }
 
 // =============================================================================
+// wire / disk formats
+// =============================================================================
+static_assert(sizeof(lio_cloud_field) == sizeof(lio::CloudField), "lio_cloud_field layout");
+
+int lio_cloud2_decode(lio_filter* f, const uint8_t* data, int64_t n_points, int32_t point_step, int is_bigendian,
+                      const lio_cloud_field* fields, int n_fields, float* out) {
+    if (!f || n_points < 0 || (n_points > 0 && (!data || !out)) || point_step <= 0 || !fields || n_fields < 1 ||
+        n_fields > lio::kMaxFields)
+        return fail(LIO_ERR_ARG, "lio_cloud2_decode: bad arguments");
+    for (int k = 0; k < n_fields; ++k) {
+        const int dt = fields[k].datatype;
+        const int size = dt <= 2 ? 1 : dt <= 4 ? 2 : dt <= 7 ? 4 : 8;
+        if (dt < 0 || dt > 8 || (dt && (fields[k].offset < 0 || fields[k].offset + size > point_step)))
+            return fail(LIO_ERR_ARG, "lio_cloud2_decode: field outside the record");
+    }
+    if (n_points == 0) return LIO_OK;
+    HIP_TRY(hipSetDevice(f->dev));
+    const int64_t bytes = n_points * point_step;
+    int rc = grow(&f->d_in, f->in_cap, (bytes + 3) / 4);
+    if (!rc) rc = grow(&f->d_out, f->out_cap, n_points * n_fields);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(f->d_in, data, (size_t)bytes, hipMemcpyHostToDevice, f->st));
+    rc = lio::cloud_decode(reinterpret_cast<const uint8_t*>(f->d_in), n_points, point_step, is_bigendian != 0,
+                           reinterpret_cast<const lio::CloudField*>(fields), n_fields, f->d_out, f->st);
+    if (rc) return filter_status(rc, "lio_cloud2_decode");
+    HIP_TRY(hipMemcpyAsync(out, f->d_out, (size_t)n_points * n_fields * sizeof(float), hipMemcpyDeviceToHost, f->st));
+    HIP_TRY(hipStreamSynchronize(f->st));
+    return LIO_OK;
+}
+
+int lio_cloud2_encode(lio_filter* f, const float* rec, int64_t n, int stride, const lio_cloud_field* fields,
+                      int n_fields, int32_t point_step, uint8_t* data) {
+    if (!f || n < 0 || (n > 0 && (!rec || !data)) || stride < 1 || !fields || n_fields < 1 ||
+        n_fields > lio::kMaxFields || point_step <= 0)
+        return fail(LIO_ERR_ARG, "lio_cloud2_encode: bad arguments");
+    for (int k = 0; k < n_fields; ++k)
+        if (fields[k].datatype == 7 && (fields[k].offset < 0 || fields[k].offset + 4 > point_step))
+            return fail(LIO_ERR_ARG, "lio_cloud2_encode: field outside the record");
+    if (n == 0) return LIO_OK;
+    HIP_TRY(hipSetDevice(f->dev));
+    const int64_t bytes = n * point_step;
+    int rc = grow(&f->d_in, f->in_cap, n * stride);
+    if (!rc) rc = grow(&f->d_out, f->out_cap, (bytes + 3) / 4);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(f->d_in, rec, (size_t)n * stride * sizeof(float), hipMemcpyHostToDevice, f->st));
+    rc = lio::cloud_encode(f->d_in, n, stride, point_step, reinterpret_cast<const lio::CloudField*>(fields), n_fields,
+                           reinterpret_cast<uint8_t*>(f->d_out), f->st);
+    if (rc) return filter_status(rc, "lio_cloud2_encode");
+    HIP_TRY(hipMemcpyAsync(data, f->d_out, (size_t)bytes, hipMemcpyDeviceToHost, f->st));
+    HIP_TRY(hipStreamSynchronize(f->st));
+    return LIO_OK;
+}
+
+int lio_scan_preprocess_cloud2(lio_ctx* c, const uint8_t* data, int64_t n_points, int32_t point_step,
+                               int is_bigendian, const lio_cloud_field fields[5], const lio_scan_prep_params* p,
+                               const lio_imu_pose* poses, int n_poses, const lio_pose* end, int64_t* n_down) {
+    if (!c || !fields || point_step <= 0 || n_points < 0 || (n_points > 0 && !data))
+        return fail(LIO_ERR_ARG, "lio_scan_preprocess_cloud2: bad arguments");
+    lio_scan_prep_params pp = p ? *p : lio_scan_prep_params{1, 0.f, 0.f, 4};
+    pp.time_field = 4;
+    int rc = prep_args_ok(nullptr, 0, 5, &pp, poses, n_poses);
+    if (rc) return rc;
+    HIP_TRY(hipSetDevice(c->map->dev));
+    hipStream_t st = c->map->st;
+    const int64_t bytes = n_points * point_step;
+    rc = grow(&c->d_rec, c->rec_cap, std::max<int64_t>((bytes + 3) / 4, n_points * 5 + 1));  // staging for the bytes
+    if (!rc) rc = grow(&c->d_raw, c->raw_cap, std::max<int64_t>(n_points, 1) * 5);
+    if (!rc && n_poses) rc = grow(&c->d_poses, c->poses_cap, n_poses);
+    if (rc) return rc;
+    if (n_points) HIP_TRY(hipMemcpyAsync(c->d_rec, data, (size_t)bytes, hipMemcpyHostToDevice, st));
+    if (n_poses)
+        HIP_TRY(hipMemcpyAsync(c->d_poses, poses, (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
+    rc = lio::cloud_decode(reinterpret_cast<const uint8_t*>(c->d_rec), n_points, point_step, is_bigendian != 0,
+                           reinterpret_cast<const lio::CloudField*>(fields), 5, c->d_raw, st);
+    if (rc) return filter_status(rc, "lio_scan_preprocess_cloud2");
+    const lio::ScanPrepParams sp{pp.point_filter_num, pp.blind, pp.filter_size_surf, 4};
+    int64_t m = 0;
+    rc = lio::scan_preprocess(c->filt, c->d_raw, n_points, 5, sp, c->d_poses, n_poses, undistort_end(end), c->d_rec, &m,
+                              st);
+    if (rc) return filter_status(rc, "lio_scan_preprocess_cloud2");
+    rc = ctx_reserve(c, m);
+    if (rc) return rc;
+    rc = lio::records_to_xyz(c->d_rec, m, 5, c->d_body, st);
+    if (rc) return filter_status(rc, "lio_scan_preprocess_cloud2");
+    HIP_TRY(hipMemsetAsync(c->d_sel, 0, (size_t)std::max<int64_t>(m, 1), st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (n_down) *n_down = m;
+    return LIO_OK;
+}
+
+int lio_pcd_write_binary(const char* path, const float* rec, int64_t n, int stride, const char* const* names) {
+    if (!path || n < 0 || (n > 0 && !rec) || stride < 1 || stride > 16 || !names)
+        return fail(LIO_ERR_ARG, "lio_pcd_write_binary: bad arguments");
+    FILE* fp = std::fopen(path, "wb");
+    if (!fp) return fail(LIO_ERR_ARG, std::string("lio_pcd_write_binary: cannot open ") + path);
+    std::string h = "# .PCD v0.7 - Point Cloud Data file format\nVERSION 0.7\nFIELDS";
+    for (int k = 0; k < stride; ++k) h += std::string(" ") + names[k];
+    h += "\nSIZE";
+    for (int k = 0; k < stride; ++k) h += " 4";
+    h += "\nTYPE";
+    for (int k = 0; k < stride; ++k) h += " F";
+    h += "\nCOUNT";
+    for (int k = 0; k < stride; ++k) h += " 1";
+    h += "\nWIDTH " + std::to_string(n) + "\nHEIGHT 1\nVIEWPOINT 0 0 0 1 0 0 0\nPOINTS " + std::to_string(n) +
+         "\nDATA binary\n";
+    bool ok = std::fwrite(h.data(), 1, h.size(), fp) == h.size();
+    if (ok && n) ok = std::fwrite(rec, sizeof(float) * stride, (size_t)n, fp) == (size_t)n;
+    ok = (std::fclose(fp) == 0) && ok;
+    return ok ? LIO_OK : fail(LIO_ERR_ARG, "lio_pcd_write_binary: write failed");
+}
+
+namespace {
+struct PcdHeader {
+    std::vector<std::string> names;
+    std::vector<int> sizes, counts;
+    std::vector<char> types;
+    int64_t points = 0;
+    std::string data;
+    long data_pos = 0;
+};
+
+int pcd_parse(FILE* fp, PcdHeader& h) {
+    char line[4096];
+    while (std::fgets(line, sizeof(line), fp)) {
+        std::string l(line);
+        while (!l.empty() && (l.back() == '\n' || l.back() == '\r')) l.pop_back();
+        if (l.empty() || l[0] == '#') continue;
+        std::vector<std::string> tok;
+        size_t a = 0;
+        while (a < l.size()) {
+            size_t b = l.find_first_of(" \t", a);
+            if (b == std::string::npos) b = l.size();
+            if (b > a) tok.push_back(l.substr(a, b - a));
+            a = b + 1;
+        }
+        if (tok.empty()) continue;
+        const std::string& k = tok[0];
+        if (k == "FIELDS") h.names.assign(tok.begin() + 1, tok.end());
+        else if (k == "SIZE") for (size_t i = 1; i < tok.size(); ++i) h.sizes.push_back(std::atoi(tok[i].c_str()));
+        else if (k == "TYPE") for (size_t i = 1; i < tok.size(); ++i) h.types.push_back(tok[i][0]);
+        else if (k == "COUNT") for (size_t i = 1; i < tok.size(); ++i) h.counts.push_back(std::atoi(tok[i].c_str()));
+        else if (k == "POINTS" && tok.size() > 1) h.points = std::atoll(tok[1].c_str());
+        else if (k == "DATA" && tok.size() > 1) {
+            h.data = tok[1];
+            h.data_pos = std::ftell(fp);
+            break;
+        }
+    }
+    if (h.counts.empty()) h.counts.assign(h.names.size(), 1);
+    if (h.data.empty() || h.names.size() != h.sizes.size() || h.names.size() != h.types.size() ||
+        h.names.size() != h.counts.size())
+        return -1;
+    return 0;
+}
+
+int pcd_datatype(char t, int size) {
+    if (t == 'F') return size == 4 ? 7 : size == 8 ? 8 : 0;
+    if (t == 'I') return size == 1 ? 1 : size == 2 ? 3 : size == 4 ? 5 : 0;
+    if (t == 'U') return size == 1 ? 2 : size == 2 ? 4 : size == 4 ? 6 : 0;
+    return 0;
+}
+}  // namespace
+
+int lio_pcd_read(lio_filter* f, const char* path, const char* const* want, int n_want, float* out, int64_t cap,
+                 int64_t* n_points) {
+    if (!path || !n_points || (out && (!f || !want || n_want < 1 || n_want > lio::kMaxFields)))
+        return fail(LIO_ERR_ARG, "lio_pcd_read: bad arguments");
+    FILE* fp = std::fopen(path, "rb");
+    if (!fp) return fail(LIO_ERR_ARG, std::string("lio_pcd_read: cannot open ") + path);
+    PcdHeader h;
+    if (pcd_parse(fp, h)) {
+        std::fclose(fp);
+        return fail(LIO_ERR_ARG, "lio_pcd_read: malformed header");
+    }
+    *n_points = h.points;
+    if (!out) {
+        std::fclose(fp);
+        return LIO_OK;
+    }
+    if (h.points > cap) {
+        std::fclose(fp);
+        return fail(LIO_ERR_ARG, "lio_pcd_read: out too small");
+    }
+    // column layout of one record
+    std::vector<int> off(h.names.size());
+    int step = 0;
+    for (size_t k = 0; k < h.names.size(); ++k) {
+        off[k] = step;
+        step += h.sizes[k] * h.counts[k];
+    }
+    std::vector<lio::CloudField> fl(n_want, lio::CloudField{0, 0, 1.f});
+    std::vector<int> col(n_want, -1);
+    for (int w = 0; w < n_want; ++w)
+        for (size_t k = 0; k < h.names.size(); ++k)
+            if (h.names[k] == want[w]) {
+                fl[w] = lio::CloudField{off[k], pcd_datatype(h.types[k], h.sizes[k]), 1.f};
+                col[w] = (int)k;
+            }
+    int rc = LIO_OK;
+    if (h.data == "binary") {
+        std::vector<uint8_t> buf((size_t)h.points * step);
+        const bool ok = h.points == 0 || std::fread(buf.data(), (size_t)step, (size_t)h.points, fp) == (size_t)h.points;
+        std::fclose(fp);
+        if (!ok) return fail(LIO_ERR_ARG, "lio_pcd_read: truncated data");
+        rc = lio_cloud2_decode(f, buf.data(), h.points, step, 0, reinterpret_cast<const lio_cloud_field*>(fl.data()),
+                               n_want, out);
+    } else if (h.data == "ascii") {
+        // one record per line, COUNT values per field, parsed as float (strtof)
+        std::vector<int> first(h.names.size());
+        int nv = 0;
+        for (size_t k = 0; k < h.names.size(); ++k) {
+            first[k] = nv;
+            nv += h.counts[k];
+        }
+        char line[1 << 16];
+        int64_t i = 0;
+        while (i < h.points && std::fgets(line, sizeof(line), fp)) {
+            std::vector<float> v;
+            char* p = line;
+            char* e = nullptr;
+            for (int t = 0; t < nv; ++t) {
+                const float x = std::strtof(p, &e);
+                if (e == p) break;
+                v.push_back(x);
+                p = e;
+            }
+            if ((int)v.size() < nv) continue;
+            for (int w = 0; w < n_want; ++w) out[i * n_want + w] = col[w] >= 0 ? v[first[col[w]]] : 0.f;
+            ++i;
+        }
+        std::fclose(fp);
+        if (i != h.points) return fail(LIO_ERR_ARG, "lio_pcd_read: truncated ascii data");
+    } else {
+        std::fclose(fp);
+        return fail(LIO_ERR_ARG, "lio_pcd_read: DATA " + h.data + " unsupported (ascii | binary)");
+    }
+    return rc;
+}
+
+int lio_map_build_pcd(lio_map* m, const char* path) {
+    if (!m || !path) return fail(LIO_ERR_ARG, "lio_map_build_pcd: bad arguments");
+    int64_t n = 0;
+    int rc = lio_pcd_read(nullptr, path, nullptr, 0, nullptr, 0, &n);
+    if (rc) return rc;
+    if (n <= 0) return fail(LIO_ERR_ARG, "lio_map_build_pcd: empty cloud");
+    lio_filter* f = nullptr;
+    rc = lio_filter_create(m->dev, &f);
+    if (rc) return rc;
+    std::vector<float> xyz((size_t)n * 3);
+    const char* want[3] = {"x", "y", "z"};
+    rc = lio_pcd_read(f, path, want, 3, xyz.data(), n, &n);
+    lio_filter_destroy(f);
+    if (rc) return rc;
+    return lio_map_build(m, xyz.data(), n);
+}
+
+// =============================================================================
 // timing
 // =============================================================================
 int lio_ctx_set_timing(lio_ctx* c, int enable) {

@@ -383,7 +383,91 @@ __global__ void records_xyz_kernel(const float* __restrict__ rec, int64_t n, int
     xyz[3 * i + 2] = rec[(size_t)i * stride + 2];
 }
 
+// sensor_msgs/PointField datatypes: INT8 1, UINT8 2, INT16 3, UINT16 4, INT32 5,
+// UINT32 6, FLOAT32 7, FLOAT64 8 (unaligned reads byte by byte)
+__device__ __forceinline__ float read_field(const uint8_t* p, int dt, bool be) {
+    uint8_t b[8];
+    const int sz = (dt <= 2) ? 1 : (dt <= 4) ? 2 : (dt <= 7) ? 4 : 8;
+    for (int k = 0; k < sz; ++k) b[k] = be ? p[sz - 1 - k] : p[k];
+    switch (dt) {
+        case 1: return (float)(int8_t)b[0];
+        case 2: return (float)b[0];
+        case 3: return (float)(int16_t)(b[0] | (b[1] << 8));
+        case 4: return (float)(uint16_t)(b[0] | (b[1] << 8));
+        case 5: return (float)(int32_t)(b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24));
+        case 6: return (float)(uint32_t)(b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24));
+        case 7: return __uint_as_float(b[0] | (b[1] << 8) | (b[2] << 16) | ((uint32_t)b[3] << 24));
+        case 8: {
+            uint64_t v = 0;
+            for (int k = 7; k >= 0; --k) v = (v << 8) | b[k];
+            return (float)__longlong_as_double((long long)v);
+        }
+        default: return 0.f;
+    }
+}
+
+// one thread per point: record field f = value(offset_f, datatype_f) * scale_f (scale 1 => exact copy)
+__global__ void cloud_decode_kernel(const uint8_t* __restrict__ data, int64_t n, int point_step, int be,
+                                    CloudField fl0, CloudField fl1, CloudField fl2, CloudField fl3, CloudField fl4,
+                                    CloudField fl5, CloudField fl6, CloudField fl7, int nf, float* __restrict__ out) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const CloudField fl[kMaxFields] = {fl0, fl1, fl2, fl3, fl4, fl5, fl6, fl7};
+    const uint8_t* rec = data + (size_t)i * point_step;
+#pragma unroll
+    for (int f = 0; f < kMaxFields; ++f) {
+        if (f >= nf) break;
+        float v = fl[f].datatype ? read_field(rec + fl[f].offset, fl[f].datatype, be != 0) : 0.f;
+        if (fl[f].scale != 1.f) v *= fl[f].scale;
+        out[(size_t)i * nf + f] = v;
+    }
+}
+
+// float records -> little-endian FLOAT32 fields at the given offsets (other bytes zero)
+__global__ void cloud_encode_kernel(const float* __restrict__ rec, int64_t n, int stride, int point_step,
+                                    CloudField fl0, CloudField fl1, CloudField fl2, CloudField fl3, CloudField fl4,
+                                    CloudField fl5, CloudField fl6, CloudField fl7, int nf, uint8_t* __restrict__ data) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const CloudField fl[kMaxFields] = {fl0, fl1, fl2, fl3, fl4, fl5, fl6, fl7};
+    uint8_t* o = data + (size_t)i * point_step;
+    for (int k = 0; k < point_step; ++k) o[k] = 0;
+    for (int f = 0; f < nf && f < stride; ++f) {
+        if (fl[f].datatype != 7) continue;
+        const uint32_t b = __float_as_uint(rec[(size_t)i * stride + f]);
+        uint8_t* d = o + fl[f].offset;
+        d[0] = (uint8_t)b;
+        d[1] = (uint8_t)(b >> 8);
+        d[2] = (uint8_t)(b >> 16);
+        d[3] = (uint8_t)(b >> 24);
+    }
+}
+
 }  // namespace
+
+int cloud_decode(const uint8_t* d_data, int64_t n, int point_step, bool big_endian, const CloudField* fields, int nf,
+                 float* d_out, hipStream_t st) {
+    if (n <= 0) return 0;
+    if (nf < 1 || nf > kMaxFields || point_step <= 0) return -1;
+    CloudField f[kMaxFields] = {};
+    for (int k = 0; k < nf; ++k) f[k] = fields[k];
+    cloud_decode_kernel<<<nblk(n), 256, 0, st>>>(d_data, n, point_step, big_endian ? 1 : 0, f[0], f[1], f[2], f[3],
+                                                 f[4], f[5], f[6], f[7], nf, d_out);
+    FCHK(hipGetLastError());
+    return 0;
+}
+
+int cloud_encode(const float* d_rec, int64_t n, int stride, int point_step, const CloudField* fields, int nf,
+                 uint8_t* d_data, hipStream_t st) {
+    if (n <= 0) return 0;
+    if (nf < 1 || nf > kMaxFields || point_step <= 0) return -1;
+    CloudField f[kMaxFields] = {};
+    for (int k = 0; k < nf; ++k) f[k] = fields[k];
+    cloud_encode_kernel<<<nblk(n), 256, 0, st>>>(d_rec, n, stride, point_step, f[0], f[1], f[2], f[3], f[4], f[5],
+                                                 f[6], f[7], nf, d_data);
+    FCHK(hipGetLastError());
+    return 0;
+}
 
 int records_to_xyz(const float* d_rec, int64_t n, int stride, float* d_xyz, hipStream_t st) {
     if (n <= 0) return 0;

@@ -70,4 +70,16 @@ int scan_preprocess(FilterBuf& b, const float* d_raw, int64_t n, int stride, con
 
 int records_to_xyz(const float* d_rec, int64_t n, int stride, float* d_xyz, hipStream_t st);
 
+// One output column of a packed point record (sensor_msgs/PointField or a PCD field):
+// byte offset, PointField datatype (1..8, 0 = absent -> 0), scale (e.g. time unit -> ms).
+struct CloudField {
+    int32_t offset;
+    int32_t datatype;
+    float scale;
+};
+int cloud_decode(const uint8_t* d_data, int64_t n, int point_step, bool big_endian, const CloudField* fields, int nf,
+                 float* d_out, hipStream_t st);
+int cloud_encode(const float* d_rec, int64_t n, int stride, int point_step, const CloudField* fields, int nf,
+                 uint8_t* d_data, hipStream_t st);
+
 }  // namespace lio

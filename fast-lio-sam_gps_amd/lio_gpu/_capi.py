@@ -29,7 +29,8 @@ EXPORTS = [
     "lio_map_get_points", "lio_map_get_grid", "lio_map_num_ids", "lio_map_get_by_id", "lio_map_add",
     "lio_map_add_device", "lio_map_delete_boxes", "lio_localmap_update", "lio_map_incremental",
     "lio_ctx_get_knn_pose", "lio_filter_create", "lio_filter_destroy", "lio_voxel_grid", "lio_submap_voxelize",
-    "lio_preprocess", "lio_scan_preprocess",
+    "lio_preprocess", "lio_scan_preprocess", "lio_cloud2_decode", "lio_cloud2_encode", "lio_scan_preprocess_cloud2",
+    "lio_pcd_write_binary", "lio_pcd_read", "lio_map_build_pcd",
     "lio_ctx_create", "lio_ctx_destroy", "lio_scan_set", "lio_scan_set_device", "lio_match",
     "lio_get_knn", "lio_get_planes", "lio_get_world", "lio_get_h_rows", "lio_ctx_knn_stats",
     "lio_ieskf_update",
@@ -104,6 +105,10 @@ class ScanPrepParams(C.Structure):
                 ("time_field", C.c_int)]
 
 
+class CloudField(C.Structure):
+    _fields_ = [("offset", C.c_int32), ("datatype", C.c_int32), ("scale", C.c_float)]
+
+
 class KernelTiming(C.Structure):
     _fields_ = [("knn_launches", C.c_int64), ("knn_ms", C.c_double), ("reuse_launches", C.c_int64),
                 ("reuse_ms", C.c_double), ("final_launches", C.c_int64), ("final_ms", C.c_double),
@@ -141,6 +146,15 @@ def _declare(L):
                                           C.POINTER(C.c_int)]),
         "lio_map_incremental": (C.c_int, [vp, C.POINTER(Pose), C.c_double, C.POINTER(IncrementalStats)]),
         "lio_ctx_get_knn_pose": (C.c_int, [vp, C.POINTER(Pose)]),
+        "lio_cloud2_decode": (C.c_int, [vp, vp, C.c_int64, C.c_int32, C.c_int, C.POINTER(CloudField), C.c_int, fp]),
+        "lio_cloud2_encode": (C.c_int, [vp, fp, C.c_int64, C.c_int, C.POINTER(CloudField), C.c_int, C.c_int32, vp]),
+        "lio_scan_preprocess_cloud2": (C.c_int, [vp, vp, C.c_int64, C.c_int32, C.c_int, C.POINTER(CloudField),
+                                                 C.POINTER(ScanPrepParams), C.POINTER(ImuPose), C.c_int,
+                                                 C.POINTER(Pose), C.POINTER(C.c_int64)]),
+        "lio_pcd_write_binary": (C.c_int, [C.c_char_p, fp, C.c_int64, C.c_int, C.POINTER(C.c_char_p)]),
+        "lio_pcd_read": (C.c_int, [vp, C.c_char_p, C.POINTER(C.c_char_p), C.c_int, fp, C.c_int64,
+                                   C.POINTER(C.c_int64)]),
+        "lio_map_build_pcd": (C.c_int, [vp, C.c_char_p]),
         "lio_filter_create": (C.c_int, [C.c_int, C.POINTER(vp)]),
         "lio_filter_destroy": (C.c_int, [vp]),
         "lio_voxel_grid": (C.c_int, [vp, fp, C.c_int64, C.c_int, fp, fp, C.POINTER(C.c_int64)]),

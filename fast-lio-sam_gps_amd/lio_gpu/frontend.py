@@ -90,6 +90,10 @@ class IkdTreeGPU:
         """Build from an xyz float32 buffer already in device memory (e.g. a torch tensor's data_ptr())."""
         check(lib().lio_map_build_device(self._h, C.c_void_p(ptr), n))
 
+    def Build_pcd(self, path: str):
+        """Build from the x y z columns of a saved PCD map."""
+        check(lib().lio_map_build_pcd(self._h, path.encode()))
+
     def size(self) -> int:
         return int(lib().lio_map_size(self._h))
 
@@ -242,6 +246,23 @@ class HShareModelGPU:
         n = C.c_int64(0)
         check(lib().lio_scan_preprocess(self._h, _fp(raw), len(raw), raw.shape[1], C.byref(prm),
                                         imu_poses_to_c(imu_poses), len(imu_poses), C.byref(end_pose), C.byref(n)))
+        self.n = int(n.value)
+        return self.n
+
+    def preprocess_cloud2(self, data, n_points: int, point_step: int, fields, imu_poses, end_pose, big_endian=False,
+                          point_filter_num=4, blind=2.0, filter_size_surf=0.5) -> int:
+        """preprocess_scan from sensor_msgs/PointCloud2 bytes; fields = 5 (offset, datatype[, scale]) for
+        x, y, z, intensity, time (scaled to ms)."""
+        from .filters import imu_poses_to_c
+        from .formats import fields_to_c
+
+        buf = np.frombuffer(bytes(data), np.uint8)
+        prm = _capi.ScanPrepParams(point_filter_num, blind, filter_size_surf, 4)
+        n = C.c_int64(0)
+        check(lib().lio_scan_preprocess_cloud2(self._h, buf.ctypes.data_as(C.c_void_p), n_points, point_step,
+                                               1 if big_endian else 0, fields_to_c(fields), C.byref(prm),
+                                               imu_poses_to_c(imu_poses), len(imu_poses), C.byref(end_pose),
+                                               C.byref(n)))
         self.n = int(n.value)
         return self.n
 

@@ -288,6 +288,37 @@ int lio_preprocess(lio_filter* f, const float* raw, int64_t n, int stride, const
 int lio_scan_preprocess(lio_ctx* c, const float* raw, int64_t n, int stride, const lio_scan_prep_params* p,
                         const lio_imu_pose* poses, int n_poses, const lio_pose* end, int64_t* n_down);
 
+/* ------------------------------------------- wire / disk formats (§8(f) row 4) */
+/* One output column of a packed point record: byte offset, sensor_msgs/PointField datatype
+ * (INT8 1, UINT8 2, INT16 3, UINT16 4, INT32 5, UINT32 6, FLOAT32 7, FLOAT64 8; 0 = absent -> 0)
+ * and a scale (1 = exact; e.g. a time unit -> ms as FAST-LIO's time_unit_scale).                 */
+typedef struct lio_cloud_field {
+    int32_t offset;
+    int32_t datatype;
+    float scale;
+} lio_cloud_field;
+/* sensor_msgs/PointCloud2 data (n_points records of point_step bytes) -> float records with one
+ * column per field (pcl::fromROSMsg's field copy; other datatypes are converted to float).     */
+int lio_cloud2_decode(lio_filter* f, const uint8_t* data, int64_t n_points, int32_t point_step, int is_bigendian,
+                      const lio_cloud_field* fields, int n_fields, float* out);
+/* float records -> little-endian FLOAT32 fields at the given offsets, other bytes zero
+ * (pcl::toROSMsg of PointXYZI: x 0, y 4, z 8, intensity 16, point_step 32).                   */
+int lio_cloud2_encode(lio_filter* f, const float* rec, int64_t n, int stride, const lio_cloud_field* fields,
+                      int n_fields, int32_t point_step, uint8_t* data);
+/* lio_scan_preprocess straight from the PointCloud2 bytes of a raw scan; fields[5] = x, y, z,
+ * intensity, time (scaled to ms): one upload, decode + preprocessing on the device.            */
+int lio_scan_preprocess_cloud2(lio_ctx* c, const uint8_t* data, int64_t n_points, int32_t point_step,
+                               int is_bigendian, const lio_cloud_field fields[5], const lio_scan_prep_params* p,
+                               const lio_imu_pose* poses, int n_poses, const lio_pose* end, int64_t* n_down);
+/* pcl::io::savePCDFileBinary (fast_lio_sam.cpp:925-932): header + packed float32 fields.       */
+int lio_pcd_write_binary(const char* path, const float* rec, int64_t n, int stride, const char* const* names);
+/* PCD v0.7 reader (DATA ascii | binary): POINTS and the float columns named in `want`
+ * (absent fields read 0).  out == NULL returns the point count only.                           */
+int lio_pcd_read(lio_filter* f, const char* path, const char* const* want, int n_want, float* out, int64_t cap,
+                 int64_t* n_points);
+/* a saved map (x y z of a PCD file) straight into the GPU grid (ikdtree.Build)                   */
+int lio_map_build_pcd(lio_map* m, const char* path);
+
 /* ----------------------------------------------------------------- timing */
 typedef struct lio_kernel_timing {
     int64_t knn_launches;   double knn_ms;     /* kNN h-evaluation: near + far + plane/H  */
