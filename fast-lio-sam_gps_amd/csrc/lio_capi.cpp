@@ -91,6 +91,7 @@ struct lio_ctx {
     lio_match_params p{};
     int64_t n = 0, cap = 0;
     float* d_body = nullptr;
+    const float* body_ext = nullptr;  // lio_scan_bind_device: caller-owned scan (no copy)
     int32_t* d_nn = nullptr;
     float4* d_planes = nullptr;
     uint8_t* d_sel = nullptr;
@@ -438,6 +439,7 @@ static int ctx_reserve(lio_ctx* c, int64_t n) {
     int rc = grow(&c->d_partials, c->part_cap, (int64_t)lio::match_blocks((int)n) * 32 + 32);
     if (rc) return rc;
     c->n = n;
+    c->body_ext = nullptr;
     c->have_eval = false;
     c->knn_valid = false;
     return LIO_OK;
@@ -449,7 +451,6 @@ int lio_scan_set(lio_ctx* c, const float* body, int64_t n) {
     int rc = ctx_reserve(c, n);
     if (rc) return rc;
     if (n) HIP_TRY(hipMemcpyAsync(c->d_body, body, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice, c->map->st));
-    HIP_TRY(hipMemsetAsync(c->d_sel, 0, (size_t)std::max<int64_t>(n, 1), c->map->st));
     return LIO_OK;
 }
 
@@ -460,15 +461,25 @@ int lio_scan_set_device(lio_ctx* c, const float* d_body, int64_t n) {
     if (rc) return rc;
     if (n)
         HIP_TRY(hipMemcpyAsync(c->d_body, d_body, (size_t)n * 3 * sizeof(float), hipMemcpyDeviceToDevice, c->map->st));
-    HIP_TRY(hipMemsetAsync(c->d_sel, 0, (size_t)std::max<int64_t>(n, 1), c->map->st));
     return LIO_OK;
 }
+
+int lio_scan_bind_device(lio_ctx* c, const float* d_body, int64_t n) {
+    if (!c || n < 0 || (n > 0 && !d_body) || n >= (int64_t)1 << 30) return fail(LIO_ERR_ARG, "lio_scan_bind_device: bad arguments");
+    HIP_TRY(hipSetDevice(c->map->dev));
+    int rc = ctx_reserve(c, n);
+    if (rc) return rc;
+    c->body_ext = n ? d_body : nullptr;
+    return LIO_OK;
+}
+
+static const float* body_ptr(const lio_ctx* c) { return c->body_ext ? c->body_ext : c->d_body; }
 
 static lio::MatchArgs make_args(lio_ctx* c, const lio_pose& pose) {
     lio::MatchArgs a{};
     std::memcpy(&a.pose, &pose, sizeof(lio::PoseArg));
     a.grid = lio::grid_view(c->map->grid);
-    a.body = c->d_body;
+    a.body = body_ptr(c);
     a.map_by_id = c->map->grid.by_id;
     a.nn_idx = c->d_nn;
     a.planes = c->d_planes;
@@ -606,7 +617,7 @@ int lio_map_incremental(lio_ctx* c, const lio_pose* pose, double filter_size_map
     lio::IncrArgs a{};
     std::memcpy(&a.pose, pose, sizeof(lio::PoseArg));
     std::memcpy(&a.pose_knn, &c->knn_pose, sizeof(lio::PoseArg));
-    a.body = c->d_body;
+    a.body = body_ptr(c);
     a.nn_idx = c->d_nn;
     a.n = (int)c->n;
     a.fs = filter_size_map;
@@ -730,6 +741,7 @@ static void from_host(const lio::host::State& x, lio_state& s) {
 
 int lio_ieskf_update(lio_ctx* c, lio_state* xs, double* P, const lio_ieskf_params* p, lio_ieskf_stats* st) {
     if (!c || !xs || !P) return fail(LIO_ERR_ARG, "lio_ieskf_update: bad arguments");
+    const auto t_call = std::chrono::steady_clock::now();
     lio_ieskf_params pp = p ? *p : lio_ieskf_params{0.001, 3, 0.001};
     lio::host::State x = to_host(*xs);
     lio::host::Mat Pm(P, P + LIO_STATE_DIM * LIO_STATE_DIM);
@@ -766,6 +778,7 @@ int lio_ieskf_update(lio_ctx* c, lio_state* xs, double* P, const lio_ieskf_param
         st->n_eff = r.n_eff;
         st->res_mean = r.res_mean;
         st->solve_ms = r.solve_ms;
+        st->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call).count();
     }
     return LIO_OK;
 }

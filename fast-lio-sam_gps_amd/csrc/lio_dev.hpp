@@ -332,14 +332,20 @@ __device__ __forceinline__ void shell_offset(int s, int k, int& dx, int& dy, int
 // lds[32..65) offsets), and the G lanes then stride the concatenated points,
 // two loads in flight per lane.  The work per group is ceil(points / G)
 // steps whatever the cells' sizes, instead of the largest cell of each lane.
-// Shell-1 ranges of lane `sub` (cells 4*sub .. 4*sub+3 of the 3x3x3 block),
+// Shell-1 ranges of lane `sub` (cells CPL*sub .. CPL*sub+CPL-1 of the 3x3x3 block),
 // loaded before the own cell is scanned so their latency overlaps it.
 template <int G>
-__device__ __forceinline__ void shell1_ranges(const GridDev& g, int cx, int cy, int cz, int sub, uint32_t b4[4],
-                                              uint32_t n4[4]) {
+constexpr int shell1_cpl() {  // cells of the 3x3x3 block per lane
+    return (27 + G - 1) / G;
+}
+
+template <int G>
+__device__ __forceinline__ void shell1_ranges(const GridDev& g, int cx, int cy, int cz, int sub,
+                                              uint32_t* b4, uint32_t* n4) {
+    constexpr int CPL = shell1_cpl<G>();
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int k = 4 * sub + j;
+    for (int j = 0; j < CPL; ++j) {
+        const int k = CPL * sub + j;
         const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
         const int x = cx + dx, y = cy + dy, z = cz + dz;
         const bool ok = k < 27 && k != 13 && (unsigned)x < (unsigned)g.nx && (unsigned)y < (unsigned)g.ny &&
@@ -358,14 +364,15 @@ __device__ __forceinline__ void shell1_ranges(const GridDev& g, int cx, int cy, 
 template <int K, int G>
 __device__ __forceinline__ void scan_shell1_flat(const GridDev& g, float qx, float qy, float qz, int cx, int cy,
                                                  int cz, float lox, float loy, float loz, int sub, uint32_t* lds,
-                                                 uint32_t b4[4], uint32_t n4[4], TopK<K>& tk, SearchStats* dbg) {
-    static_assert(G == 8, "scan_shell1_flat: 8-lane groups (4 cells per lane cover the 27-cell block)");
+                                                 uint32_t* b4, uint32_t* n4, TopK<K>& tk, SearchStats* dbg) {
+    constexpr int CPL = shell1_cpl<G>();
+    static_assert(CPL * G <= 32, "scan_shell1_flat: slot table holds 32 ranges");
     const float cs = g.cell, m = g.margin, w = cs + 2.f * m;
     const float bound = tk.worst();
     uint32_t lane_total = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {  // prune the preloaded ranges against the own-cell bound
-        const int k = 4 * sub + j;
+    for (int j = 0; j < CPL; ++j) {  // prune the preloaded ranges against the own-cell bound
+        const int k = CPL * sub + j;
         const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
         const float xl = lox + (float)dx * cs - m, yl = loy + (float)dy * cs - m, zl = loz + (float)dz * cs - m;
         const float bd = (axis_gap(qx, xl, xl + w) + axis_gap(qy, yl, yl + w)) + axis_gap(qz, zl, zl + w);
@@ -382,14 +389,14 @@ __device__ __forceinline__ void scan_shell1_flat(const GridDev& g, float qx, flo
     const uint32_t T = __shfl(incl, G - 1, G);
     uint32_t o = incl - lane_total;
     uint32_t* s_b = lds;
-    uint32_t* s_off = lds + 4 * G;
+    uint32_t* s_off = lds + CPL * G;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        s_b[4 * sub + j] = b4[j];
-        s_off[4 * sub + j] = o;
+    for (int j = 0; j < CPL; ++j) {
+        s_b[CPL * sub + j] = b4[j];
+        s_off[CPL * sub + j] = o;
         o += n4[j];
     }
-    if (sub == G - 1) s_off[4 * G] = T;
+    if (sub == G - 1) s_off[CPL * G] = T;
     if (dbg && sub == 0) dbg->points += (int)T;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -436,7 +443,7 @@ __device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, i
     own = fminf(own, fminf(qz - loz, loz + cs - qz)) - m;
     const uint32_t nx = (uint32_t)g.nx, nxy = (uint32_t)g.nx * (uint32_t)g.ny;
     const uint32_t c0 = (uint32_t)cz * nxy + (uint32_t)cy * nx + (uint32_t)cx;
-    uint32_t b4[4], n4[4];
+    uint32_t b4[shell1_cpl<G>()], n4[shell1_cpl<G>()];
     if (lds) shell1_ranges<G>(g, cx, cy, cz, sub, b4, n4);  // in flight during the own-cell scan
     scan_cell_group2<K, G>(g, c0, qx, qy, qz, sub, tk);
     group_merge<K, G>(tk);

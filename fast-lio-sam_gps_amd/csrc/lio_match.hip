@@ -93,13 +93,13 @@ __device__ __forceinline__ bool residual_row(const MatchArgs& a, float bx, float
 // neighbourhoods, ~0.4% of a dense scan) are queued, with their list, for
 // the wave-per-query far pass instead of holding their wave: a kernel runs as
 // long as its slowest wave.  Written for 8 waves/SIMD (<= 64 VGPRs).
-template <bool DBG>
+template <bool DBG, int G = kGroup>
 __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) knn_near_kernel(MatchArgs a) {
-    constexpr int QPB = kKnnBlock / kGroup;  // 64 queries per block
+    constexpr int QPB = kKnnBlock / G;  // 64 queries per block at G = 8
     __shared__ uint32_t s_tab[QPB][72];      // per-group shell-1 slot table
     const int blk = xcd_block(blockIdx.x, gridDim.x);
-    const int sub = threadIdx.x % kGroup;
-    const int i = blk * QPB + threadIdx.x / kGroup;
+    const int sub = threadIdx.x % G;
+    const int i = blk * QPB + threadIdx.x / G;
     if (i >= a.n) return;
     const float bx = a.body[3 * i], by = a.body[3 * i + 1], bz = a.body[3 * i + 2];
     float wx, wy, wz;
@@ -107,12 +107,12 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
     TopK<5> tk;
     tk.init(a.range_sq);
     SearchStats st{0, 0, 0};
-    const bool done = group_knn_near<5, kGroup>(a.grid, wx, wy, wz, min(a.max_shell, 1), sub, tk, DBG ? &st : nullptr,
-                                                s_tab[threadIdx.x / kGroup]);
+    const bool done = group_knn_near<5, G>(a.grid, wx, wy, wz, min(a.max_shell, 1), sub, tk, DBG ? &st : nullptr,
+                                                s_tab[threadIdx.x / G]);
     const bool far = !done && a.max_shell > 1;
     if constexpr (DBG) {
 #pragma unroll
-        for (int off = 1; off < kGroup; off <<= 1) {
+        for (int off = 1; off < G; off <<= 1) {
             st.cells += __shfl_xor(st.cells, off, 64);
             st.points += __shfl_xor(st.points, off, 64);
         }
@@ -134,12 +134,16 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
         }
         return;
     }
-    if (sub < 5) {
-        int v = tk.id(0);
 #pragma unroll
-        for (int j = 1; j < 5; ++j)
-            if (sub == j) v = tk.id(j);
-        a.nn_idx[5 * (size_t)i + sub] = v == kNone ? -1 : v;
+    for (int js = 0; js < 5; js += G) {
+        const int jj = js + sub;
+        if (jj < 5) {
+            int v = tk.id(0);
+#pragma unroll
+            for (int j = 1; j < 5; ++j)
+                if (jj == j) v = tk.id(j);
+            a.nn_idx[5 * (size_t)i + jj] = v == kNone ? -1 : v;
+        }
     }
 }
 
@@ -364,10 +368,19 @@ int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* ma
     if (a.n == 0) return 0;
     const int nb = (a.n + kBlock - 1) / kBlock;
     if (redo) {
-        const int qpb = kKnnBlock / kGroup;
+        static const int group = [] {  // LIO_KNN_GROUP: diagnostics override of the lanes per query
+            const char* e = std::getenv("LIO_KNN_GROUP");
+            const int v = e ? std::atoi(e) : kGroup;
+            return (v == 4 || v == 16) ? v : kGroup;
+        }();
+        const int qpb = kKnnBlock / group;
         const int nq = (a.n + qpb - 1) / qpb;
         if (a.dbg)
-            knn_near_kernel<true><<<nq, kKnnBlock, 0, st>>>(a);
+            knn_near_kernel<true><<<(a.n + kKnnBlock / kGroup - 1) / (kKnnBlock / kGroup), kKnnBlock, 0, st>>>(a);
+        else if (group == 4)
+            knn_near_kernel<false, 4><<<nq, kKnnBlock, 0, st>>>(a);
+        else if (group == 16)
+            knn_near_kernel<false, 16><<<nq, kKnnBlock, 0, st>>>(a);
         else
             knn_near_kernel<false><<<nq, kKnnBlock, 0, st>>>(a);
         if (marks) (void)hipEventRecord(marks[0], st);

@@ -31,7 +31,7 @@ EXPORTS = [
     "lio_ctx_get_knn_pose", "lio_filter_create", "lio_filter_destroy", "lio_voxel_grid", "lio_submap_voxelize",
     "lio_preprocess", "lio_scan_preprocess", "lio_cloud2_decode", "lio_cloud2_encode", "lio_scan_preprocess_cloud2",
     "lio_pcd_write_binary", "lio_pcd_read", "lio_map_build_pcd",
-    "lio_ctx_create", "lio_ctx_destroy", "lio_scan_set", "lio_scan_set_device", "lio_match",
+    "lio_ctx_create", "lio_ctx_destroy", "lio_scan_set", "lio_scan_set_device", "lio_scan_bind_device", "lio_match",
     "lio_get_knn", "lio_get_planes", "lio_get_world", "lio_get_h_rows", "lio_ctx_knn_stats",
     "lio_ieskf_update",
     "lio_icp_create", "lio_icp_destroy", "lio_icp_set_target", "lio_icp_set_source", "lio_icp_set_shard",
@@ -72,7 +72,7 @@ class IeskfParams(C.Structure):
 
 class IeskfStats(C.Structure):
     _fields_ = [("h_evals", C.c_int), ("knn_calls", C.c_int), ("converged", C.c_int), ("n_eff", C.c_int),
-                ("res_mean", C.c_double), ("solve_ms", C.c_double)]
+                ("res_mean", C.c_double), ("solve_ms", C.c_double), ("wall_ms", C.c_double)]
 
 
 class IcpParams(C.Structure):
@@ -168,6 +168,7 @@ def _declare(L):
         "lio_ctx_destroy": (C.c_int, [vp]),
         "lio_scan_set": (C.c_int, [vp, fp, C.c_int64]),
         "lio_scan_set_device": (C.c_int, [vp, vp, C.c_int64]),
+        "lio_scan_bind_device": (C.c_int, [vp, vp, C.c_int64]),
         "lio_match": (C.c_int, [vp, C.POINTER(Pose), C.c_int, dp]),
         "lio_get_knn": (C.c_int, [vp, C.POINTER(C.c_int32), fp]),
         "lio_get_planes": (C.c_int, [vp, fp, C.POINTER(C.c_uint8)]),

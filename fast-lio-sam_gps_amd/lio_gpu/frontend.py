@@ -194,6 +194,11 @@ class HShareModelGPU:
         check(lib().lio_scan_set_device(self._h, C.c_void_p(ptr), n))
         self.n = n
 
+    def bind_scan_device(self, ptr: int, n: int):
+        """Use a caller-owned device scan in place (kept alive and unchanged by the caller)."""
+        check(lib().lio_scan_bind_device(self._h, C.c_void_p(ptr), n))
+        self.n = n
+
     def __call__(self, pose, converge: bool = True) -> np.ndarray:
         """One evaluation; ``pose`` is a lio Pose or a pose24 array. Returns sums[32]."""
         if not isinstance(pose, _capi.Pose):
@@ -322,3 +327,9 @@ class EsekfGPU:
         check(lib().lio_ieskf_update(self.model._h, C.byref(s), _dp(Pc), C.byref(self.params), C.byref(st)))
         stats = {k: getattr(st, k) for k, _ in _capi.IeskfStats._fields_}
         return state_from_c(s), Pc, stats
+
+    def update_raw(self, s: _capi.State, P: np.ndarray, st: _capi.IeskfStats):
+        """Same call on caller-owned ctypes state / float64 23x23 P / stats (updated in place):
+        no per-call conversions (the shape a C++ caller of lio_ieskf_update has)."""
+        check(lib().lio_ieskf_update(self.model._h, C.byref(s), P.ctypes.data_as(C.POINTER(C.c_double)),
+                                     C.byref(self.params), C.byref(st)))

@@ -132,6 +132,9 @@ int lio_ctx_destroy(lio_ctx* c);
 /* feats_down_body (n*3 float, LiDAR frame), host / device pointer.         */
 int lio_scan_set(lio_ctx* c, const float* body_xyz, int64_t n);
 int lio_scan_set_device(lio_ctx* c, const float* d_body_xyz, int64_t n);
+/* same without a copy: the ctx reads the caller's device buffer, which must stay valid and
+ * unchanged until the next lio_scan_* call on this ctx.                                       */
+int lio_scan_bind_device(lio_ctx* c, const float* d_body, int64_t n);
 /* One h_share_model evaluation [U]. redo_knn = ekfom_data.converge.
  * sums: LIO_SUMS_LEN doubles (see layout above).                           */
 int lio_match(lio_ctx* c, const lio_pose* pose, int redo_knn, double* sums);
@@ -175,6 +178,7 @@ typedef struct lio_ieskf_stats {
     int n_eff;      /* effct_feat_num of the last evaluation             */
     double res_mean;/* res_mean_last                                     */
     double solve_ms;/* host time in the 23-dim algebra                   */
+    double wall_ms; /* host wall time of the whole call                  */
 } lio_ieskf_stats;
 
 /* esekf::update_iterated_dyn_share_modified(R, solve_time) [U IKFoM];

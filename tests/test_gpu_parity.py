@@ -279,3 +279,25 @@ def test_icp_c4_full_size_matches_oracle(oracle):
     # size-independent property: the accepted step brought the clouds together
     assert r.score < r.last_mse
     assert out.score_ < 1.5 and out.is_valid_
+
+
+def test_bind_scan_device_matches_copy(c1):
+    """lio_scan_bind_device (caller-owned device scan, no copy) == lio_scan_set."""
+    import torch
+
+    _, m, scans = c1
+    sc = scans[0]
+    tree = F.IkdTreeGPU()
+    tree.Build(m)
+    p24 = synth.pose24(synth.initial_state(sc.pos_init, sc.rot_init))
+    h1 = F.HShareModelGPU(tree)
+    h1.set_scan(sc.body)
+    s1 = h1(p24, True)
+    d = torch.from_numpy(sc.body).to("cuda:0")
+    torch.cuda.synchronize()
+    h2 = F.HShareModelGPU(tree)
+    h2.bind_scan_device(d.data_ptr(), len(sc.body))
+    s2 = h2(p24, True)
+    np.testing.assert_array_equal(s1, s2)
+    np.testing.assert_array_equal(h1.nearest_points()[0], h2.nearest_points()[0])
+    np.testing.assert_array_equal(h1(p24, False), h2(p24, False))
