@@ -193,9 +193,16 @@ __global__ void merge_new_kernel(const float4* __restrict__ by_id, const uint32_
     ckeys_out[o] = c;
 }
 
-__global__ void count_keys_kernel(const uint32_t* __restrict__ ckeys, int64_t n, uint32_t* __restrict__ counts) {
+// cell counts of the (cell-sorted) entries without atomics: the head of each
+// run of equal keys walks to the run's end and writes the length once
+__global__ void run_count_kernel(const uint32_t* __restrict__ ckeys, int64_t n, uint32_t* __restrict__ counts) {
     const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (j < n) atomicAdd(&counts[ckeys[j]], 1u);
+    if (j >= n) return;
+    const uint32_t k = ckeys[j];
+    if (j > 0 && ckeys[j - 1] == k) return;
+    int64_t e = j + 1;
+    while (e < n && ckeys[e] == k) ++e;
+    counts[k] = (uint32_t)(e - j);
 }
 
 #define HIPCHK(x)                                                               \
@@ -394,9 +401,12 @@ int grid_rebuild(GridBuf& g, float cell, float slack, hipStream_t st) {
 // the new ones are merged in cell order (no full sort), start[] recounted.
 // Falls back to grid_rebuild (geometry + slack) when a new point lies outside
 // the grid.  Synchronises the stream once.
+int grid_reserve_entries(GridBuf& g, int64_t n, hipStream_t st) { return reserve_entries(g, std::max<int64_t>(n, 1), st); }
+
 int grid_update(GridBuf& g, int64_t id0, bool deleted, float slack, hipStream_t st) {
     const int64_t n_new = g.n_ids - id0, n_old = g.n;
     if (n_new < 0) return -1;
+    if (g.flags_ready && g.cap < g.n_ids) return -1;  // the caller reserved the entries first
     int rc = reserve_entries(g, std::max<int64_t>(g.n_ids, 1), st);
     if (rc) return rc;
     int* d_out = reinterpret_cast<int*>(g.aabb + 7);  // outside flag
@@ -415,7 +425,8 @@ int grid_update(GridBuf& g, int64_t id0, bool deleted, float slack, hipStream_t 
     }
     uint32_t* pos = nullptr;
     if (deleted && n_old > 0) {
-        alive_flag_kernel<<<(int)((n_old + 1 + 255) / 256), 256, 0, st>>>(g.pts, g.by_id, n_old, g.flag);
+        if (!g.flags_ready)  // survivor flags from the alive bits (else set by the caller's kernels)
+            alive_flag_kernel<<<(int)((n_old + 1 + 255) / 256), 256, 0, st>>>(g.pts, g.by_id, n_old, g.flag);
         size_t scan_bytes = 0;
         HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, g.flag, g.pos, (int)(n_old + 1), st));
         if (ensure(&g.tmp, g.tmp_bytes, scan_bytes) != 0) return -5;
@@ -428,6 +439,7 @@ int grid_update(GridBuf& g, int64_t id0, bool deleted, float slack, hipStream_t 
     HIPCHK(hipStreamSynchronize(st));
     int outside = 0;
     std::memcpy(&outside, g.aabb_host + 7, sizeof(int));
+    g.flags_ready = false;
     if (outside || g.n == 0) return grid_rebuild(g, g.geom.cell, slack, st);
     uint32_t kept = (uint32_t)n_old;
     if (pos) std::memcpy(&kept, g.aabb_host + 8, sizeof(uint32_t));
@@ -443,7 +455,7 @@ int grid_update(GridBuf& g, int64_t id0, bool deleted, float slack, hipStream_t 
     const uint32_t nc1 = g.geom.ncells + 1;
     uint32_t* counts = g.start + g.cells_cap;
     HIPCHK(hipMemsetAsync(counts, 0, (size_t)nc1 * sizeof(uint32_t), st));
-    if (g.n > 0) count_keys_kernel<<<(int)((g.n + 255) / 256), 256, 0, st>>>(g.ckeys, g.n, counts);
+    if (g.n > 0) run_count_kernel<<<(int)((g.n + 255) / 256), 256, 0, st>>>(g.ckeys, g.n, counts);
     size_t scan_bytes = 0;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, counts, g.start, (int)nc1, st));
     if (ensure(&g.tmp, g.tmp_bytes, scan_bytes) != 0) return -5;

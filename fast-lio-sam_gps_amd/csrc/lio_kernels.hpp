@@ -62,8 +62,9 @@ struct GridBuf {
     GridGeom geom{};
     float4* pts_alt = nullptr;  // merge targets
     uint32_t* ckeys_alt = nullptr;
-    uint32_t* flag = nullptr;
+    uint32_t* flag = nullptr;  // per-entry survivor flags (+ slot n = 0)
     uint32_t* pos = nullptr;
+    bool flags_ready = false;  // flag[] already set by the caller (grid_update skips the by_id gather)
     // temporaries
     uint32_t* keys = nullptr;
     uint32_t* keys_alt = nullptr;
@@ -82,6 +83,8 @@ int grid_build(GridBuf& g, const float* d_xyz, int64_t n, float cell, hipStream_
 int grid_rebuild(GridBuf& g, float cell, float slack, hipStream_t st);
 // Merge update after appending ids [id0, n_ids) and/or marking ids dead.
 int grid_update(GridBuf& g, int64_t id0, bool deleted, float slack, hipStream_t st);
+// Entry buffers for n entries (the live cell-sorted entries are kept).
+int grid_reserve_entries(GridBuf& g, int64_t n, hipStream_t st);
 // Grow by_id to hold n_ids ids (contents kept).
 int grid_reserve_ids(GridBuf& g, int64_t n_ids, hipStream_t st);
 void grid_free(GridBuf& g);

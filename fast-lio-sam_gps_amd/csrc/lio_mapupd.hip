@@ -78,23 +78,25 @@ __global__ void voxel_key_kernel(const float* __restrict__ xyz, int n, float ds,
 // for the new point that survives (at most one per voxel).
 __global__ void voxel_resolve_kernel(const uint64_t* __restrict__ skeys, const uint32_t* __restrict__ svals, int n,
                                      const float* __restrict__ xyz, float ds, GridDev g, int grid_n,
-                                     float4* __restrict__ by_id, uint8_t* __restrict__ add_flag,
-                                     int* __restrict__ counters) {
+                                     float4* __restrict__ by_id, uint32_t* __restrict__ entry_alive,
+                                     uint8_t* __restrict__ add_flag, int* __restrict__ counters) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n) return;
     const uint64_t key = skeys[j];
     if (j > 0 && skeys[j - 1] == key) return;
     const int i0 = (int)svals[j];
     const VoxBox b = vox_box(xyz[3 * i0], xyz[3 * i0 + 1], xyz[3 * i0 + 2], ds);
-    // ---- map points in the box (cells overlapping the box, widened by the margin)
+    // ---- map points in the box: a point p with lo <= p < hi has its (clamped) cell
+    // between the cells of lo and of the largest float below hi — the build's
+    // cell assignment is monotone in each coordinate — so no margin is needed
     int x0 = 0, x1 = -1, y0 = 0, y1 = -1, z0 = 0, z1 = -1;
     if (grid_n > 0) {
-        x0 = max(cell_coord(b.lo[0] - g.margin, g.ox, g.inv_cell), 0);
-        x1 = min(cell_coord(b.hi[0] + g.margin, g.ox, g.inv_cell), g.nx - 1);
-        y0 = max(cell_coord(b.lo[1] - g.margin, g.oy, g.inv_cell), 0);
-        y1 = min(cell_coord(b.hi[1] + g.margin, g.oy, g.inv_cell), g.ny - 1);
-        z0 = max(cell_coord(b.lo[2] - g.margin, g.oz, g.inv_cell), 0);
-        z1 = min(cell_coord(b.hi[2] + g.margin, g.oz, g.inv_cell), g.nz - 1);
+        x0 = min(max(cell_coord(b.lo[0], g.ox, g.inv_cell), 0), g.nx - 1);
+        x1 = min(max(cell_coord(nextafterf(b.hi[0], -INFINITY), g.ox, g.inv_cell), 0), g.nx - 1);
+        y0 = min(max(cell_coord(b.lo[1], g.oy, g.inv_cell), 0), g.ny - 1);
+        y1 = min(max(cell_coord(nextafterf(b.hi[1], -INFINITY), g.oy, g.inv_cell), 0), g.ny - 1);
+        z0 = min(max(cell_coord(b.lo[2], g.oz, g.inv_cell), 0), g.nz - 1);
+        z1 = min(max(cell_coord(nextafterf(b.hi[2], -INFINITY), g.oz, g.inv_cell), 0), g.nz - 1);
     }
     int cnt_e = 0, best_id = -1;
     float best_d = INFINITY, bx = 0.f, by = 0.f, bz = 0.f;
@@ -152,6 +154,7 @@ __global__ void voxel_resolve_kernel(const uint64_t* __restrict__ skeys, const u
                         const int id = __float_as_int(p.w);
                         if (surv_new < 0 && id == best_id) continue;
                         by_id[id].w = 0.f;
+                        entry_alive[k] = 0u;
                         ++dead;
                     }
                 }
@@ -394,7 +397,8 @@ int exclusive_scan(MapUpdBuf& u, const uint32_t* in, uint32_t* out, int n1, hipS
 // Downsampled add of n device points (xyz): voxel sort + resolve; survivors'
 // flags in u.cls[0..n) (as u8), their count -> *n_surv (host), triggers /
 // tombstones -> counters.  Does not touch by_id beyond the tombstones.
-int resolve_downsample(GridBuf& g, MapUpdBuf& u, const float* xyz, int n, float ds, hipStream_t st) {
+int resolve_downsample(GridBuf& g, MapUpdBuf& u, const float* xyz, int n, float ds, int64_t extra_ids,
+                       hipStream_t st) {
     const int nb = (n + 255) / 256;
     voxel_key_kernel<<<nb, 256, 0, st>>>(xyz, n, ds, u.keys, u.vals);
     size_t bytes = 0;
@@ -405,8 +409,15 @@ int resolve_downsample(GridBuf& g, MapUpdBuf& u, const float* xyz, int n, float 
     UPD_CHK(hipcub::DeviceRadixSort::SortPairs(u.tmp, bytes, u.keys, u.keys_alt, u.vals, u.vals_alt, n, 0,
                                                3 * kVoxBits, st));
     UPD_CHK(hipMemsetAsync(u.cls, 0, n, st));
+    // survivor flags of the cell-sorted entries, cleared by the resolve kernel for the
+    // entries it replaces (grid_update then skips its by_id gather)
+    int rc = grid_reserve_entries(g, g.n_ids + n + extra_ids, st);  // no re-allocation before grid_update
+    if (rc) return rc;
+    UPD_CHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(g.flag), 1, (size_t)g.n, st));
+    UPD_CHK(hipMemsetAsync(g.flag + g.n, 0, sizeof(uint32_t), st));
+    g.flags_ready = true;
     voxel_resolve_kernel<<<nb, 256, 0, st>>>(u.keys_alt, u.vals_alt, n, xyz, ds, grid_view(g), (int)g.n, g.by_id,
-                                            u.cls, u.d_small);
+                                            g.flag, u.cls, u.d_small);
     return 0;
 }
 
@@ -439,7 +450,7 @@ int map_add_device(GridBuf& g, MapUpdBuf& u, const float* d_xyz, int64_t n64, bo
         return grid_update(g, id0, false, slack, st);
     }
     UPD_CHK(hipMemsetAsync(u.d_small, 0, 4 * sizeof(int), st));
-    int rc = resolve_downsample(g, u, d_xyz, n, ds, st);
+    int rc = resolve_downsample(g, u, d_xyz, n, ds, 0, st);
     if (rc) return rc;
     u8_to_u32_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(u.cls, n, u.flag);
     rc = exclusive_scan(u, u.flag, u.pos, n + 1, st);
@@ -460,6 +471,7 @@ int map_add_device(GridBuf& g, MapUpdBuf& u, const float* d_xyz, int64_t n64, bo
 int map_delete_boxes(GridBuf& g, MapUpdBuf& u, const float* boxes, int nb, float slack, int64_t* n_deleted,
                      hipStream_t st) {
     *n_deleted = 0;
+    g.flags_ready = false;  // tombstones come from the alive bits here
     if (nb <= 0 || g.n_ids == 0) return 0;
     if (ensure_small(u)) return -5;
     if (!u.boxes || nb > u.boxes_cap) {
@@ -512,7 +524,7 @@ int map_incremental(GridBuf& g, MapUpdBuf& u, IncrArgs a, float ds, float slack,
     const int64_t id0 = g.n_ids;
     int64_t n_surv = 0, dead = 0;
     if (n_add > 0) {
-        rc = resolve_downsample(g, u, u.xyz_a, n_add, ds, st);  // cls reused as survivor flags
+        rc = resolve_downsample(g, u, u.xyz_a, n_add, ds, n_nn, st);  // cls reused as survivor flags
         if (rc) return rc;
         u8_to_u32_kernel<<<(n_add + 1 + 255) / 256, 256, 0, st>>>(u.cls, n_add, u.flag);
         rc = exclusive_scan(u, u.flag, u.pos, n_add + 1, st);
