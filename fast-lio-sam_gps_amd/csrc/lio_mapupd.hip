@@ -69,21 +69,45 @@ __global__ void voxel_key_kernel(const float* __restrict__ xyz, int n, float ds,
     vals[i] = (uint32_t)i;
 }
 
-// One lane per voxel run of the sorted keys: replay Add_Points' sequence for
+// One wave per voxel run of the sorted keys: replay Add_Points' sequence for
 // the run's points against the alive map points in the voxel.
 //   S := map points in the box; for each new point q (input order):
 //     winner = q unless some s in S has calc_dist(s, mid) < calc_dist(q, mid)
 //     if |S| > 1 or same_point(q, winner): S := {winner}, counter++
-// Writes tombstones (by_id[id].w = 0) for replaced map points and add_flag[i]
-// for the new point that survives (at most one per voxel).
-__global__ void voxel_resolve_kernel(const uint64_t* __restrict__ skeys, const uint32_t* __restrict__ svals, int n,
-                                     const float* __restrict__ xyz, float ds, GridDev g, int grid_n,
-                                     float4* __restrict__ by_id, uint32_t* __restrict__ entry_alive,
-                                     uint8_t* __restrict__ add_flag, int* __restrict__ counters) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+// The 64 lanes stride the box's cells (count + first nearest-to-centre point
+// in visit order = a min over (d, visit index)), lane 0 replays the run's few
+// new points, and the lanes stride again to write the tombstones
+// (by_id[id].w = 0 and the entry's survivor flag) of replaced map points.
+// add_flag[i] marks the new point that survives (at most one per voxel).
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(v, off, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+__device__ __forceinline__ int wave_sum_i32(int v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+__global__ void __launch_bounds__(256) voxel_resolve_kernel(const uint64_t* __restrict__ skeys,
+                                                           const uint32_t* __restrict__ svals, int n,
+                                                           const float* __restrict__ xyz, float ds, GridDev g,
+                                                           int grid_n, float4* __restrict__ by_id,
+                                                           uint32_t* __restrict__ entry_alive,
+                                                           uint8_t* __restrict__ add_flag, int* __restrict__ trig_out,
+                                                           int* __restrict__ dead_out) {
+    const int lane = threadIdx.x & 63;
+    const int j = blockIdx.x * 4 + (threadIdx.x >> 6);  // one sorted position per wave
     if (j >= n) return;
     const uint64_t key = skeys[j];
-    if (j > 0 && skeys[j - 1] == key) return;
+    if (j > 0 && skeys[j - 1] == key) {  // not a run head (wave-uniform)
+        if (lane == 0) trig_out[j] = dead_out[j] = 0;
+        return;
+    }
     const int i0 = (int)svals[j];
     const VoxBox b = vox_box(xyz[3 * i0], xyz[3 * i0 + 1], xyz[3 * i0 + 2], ds);
     // ---- map points in the box: a point p with lo <= p < hi has its (clamped) cell
@@ -98,28 +122,50 @@ __global__ void voxel_resolve_kernel(const uint64_t* __restrict__ skeys, const u
         z0 = min(max(cell_coord(b.lo[2], g.oz, g.inv_cell), 0), g.nz - 1);
         z1 = min(max(cell_coord(nextafterf(b.hi[2], -INFINITY), g.oz, g.inv_cell), 0), g.nz - 1);
     }
-    int cnt_e = 0, best_id = -1;
-    float best_d = INFINITY, bx = 0.f, by = 0.f, bz = 0.f;
+    int cnt_e = 0;
+    unsigned long long best = ~0ull;  // (float bits of d, visit index): first strict minimum
+    uint32_t visit = 0;
     for (int z = z0; z <= z1; ++z)
         for (int y = y0; y <= y1; ++y)
             for (int x = x0; x <= x1; ++x) {
                 const uint32_t c = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
-                for (uint32_t k = g.start[c]; k < g.start[c + 1]; ++k) {
+                const uint32_t cb = g.start[c], ce = g.start[c + 1];
+                for (uint32_t k = cb + (uint32_t)lane; k < ce; k += 64) {
                     const float4 p = g.pts[k];
                     if (!in_box(b, p.x, p.y, p.z)) continue;
                     ++cnt_e;
                     const float t = calc_dist(p.x, p.y, p.z, b.mid[0], b.mid[1], b.mid[2]);
-                    if (t < best_d) {
-                        best_d = t;
+                    const unsigned long long kk = ((unsigned long long)__float_as_uint(t) << 32) | (visit + (k - cb));
+                    best = kk < best ? kk : best;
+                }
+                visit += ce - cb;
+            }
+    cnt_e = wave_sum_i32(cnt_e);
+    best = wave_min_u64(best);
+    // best's entry: re-locate by visit index (wave-uniform)
+    int best_id = -1;
+    float bx = 0.f, by = 0.f, bz = 0.f, best_d = INFINITY;
+    if (cnt_e > 0) {
+        uint32_t v = (uint32_t)best;
+        best_d = __uint_as_float((uint32_t)(best >> 32));
+        for (int z = z0; z <= z1; ++z)
+            for (int y = y0; y <= y1; ++y)
+                for (int x = x0; x <= x1; ++x) {
+                    const uint32_t c = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
+                    const uint32_t cb = g.start[c], ce = g.start[c + 1];
+                    if (best_id < 0 && v < ce - cb) {
+                        const float4 p = g.pts[cb + v];
                         best_id = __float_as_int(p.w);
                         bx = p.x;
                         by = p.y;
                         bz = p.z;
+                    } else if (best_id < 0) {
+                        v -= ce - cb;
                     }
                 }
-            }
-    // ---- replay the run
-    int surv_new = -1;  // survivor is a new point (its input index), else the map point best_id (if any)
+    }
+    // ---- replay the run (lane 0's result broadcast through the uniform loop)
+    int surv_new = -1;
     float sx = bx, sy = by, sz = bz, sd = best_d;
     int triggers = 0;
     bool first = true;
@@ -142,13 +188,13 @@ __global__ void voxel_resolve_kernel(const uint64_t* __restrict__ skeys, const u
         first = false;
     }
     // ---- tombstones: every map point of the box except a surviving map point
+    int dead = 0;
     if (cnt_e > 0 && (surv_new >= 0 || cnt_e > 1)) {
-        int dead = 0;
         for (int z = z0; z <= z1; ++z)
             for (int y = y0; y <= y1; ++y)
                 for (int x = x0; x <= x1; ++x) {
                     const uint32_t c = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
-                    for (uint32_t k = g.start[c]; k < g.start[c + 1]; ++k) {
+                    for (uint32_t k = g.start[c] + (uint32_t)lane; k < g.start[c + 1]; k += 64) {
                         const float4 p = g.pts[k];
                         if (!in_box(b, p.x, p.y, p.z)) continue;
                         const int id = __float_as_int(p.w);
@@ -158,10 +204,13 @@ __global__ void voxel_resolve_kernel(const uint64_t* __restrict__ skeys, const u
                         ++dead;
                     }
                 }
-        atomicAdd(&counters[1], dead);
+        dead = wave_sum_i32(dead);
     }
-    if (surv_new >= 0) add_flag[surv_new] = 1;
-    atomicAdd(&counters[0], triggers);
+    if (lane == 0) {  // per-run counts, summed by a reduction (no contended atomics)
+        if (surv_new >= 0) add_flag[surv_new] = 1;
+        trig_out[j] = triggers;
+        dead_out[j] = dead;
+    }
 }
 
 // append the flagged points (pos = exclusive scan of the flags) as ids id0 + pos
@@ -202,9 +251,12 @@ __global__ void delete_boxes_kernel(float4* __restrict__ by_id, int64_t n, const
             }
         }
     }
-    // one atomic per wave
+    // per-block count (summed by a reduction: no contended atomics)
+    __shared__ int s_cnt[4];
     const unsigned long long m = __ballot(hit);
-    if ((threadIdx.x & 63) == 0 && m) atomicAdd(counter, __popcll(m));
+    if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = __popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) counter[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
 }
 
 // ---- map_incremental ---------------------------------------------------------
@@ -416,8 +468,17 @@ int resolve_downsample(GridBuf& g, MapUpdBuf& u, const float* xyz, int n, float 
     UPD_CHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(g.flag), 1, (size_t)g.n, st));
     UPD_CHK(hipMemsetAsync(g.flag + g.n, 0, sizeof(uint32_t), st));
     g.flags_ready = true;
-    voxel_resolve_kernel<<<nb, 256, 0, st>>>(u.keys_alt, u.vals_alt, n, xyz, ds, grid_view(g), (int)g.n, g.by_id,
-                                            g.flag, u.cls, u.d_small);
+    int* trig = reinterpret_cast<int*>(u.pos2);  // n + n ints of scratch (pos2 / flag2 free here)
+    int* dead = reinterpret_cast<int*>(u.flag2);
+    voxel_resolve_kernel<<<(n + 3) / 4, 256, 0, st>>>(u.keys_alt, u.vals_alt, n, xyz, ds, grid_view(g), (int)g.n,
+                                                     g.by_id, g.flag, u.cls, trig, dead);
+    size_t rbytes = 0;
+    UPD_CHK(hipcub::DeviceReduce::Sum(nullptr, rbytes, trig, u.d_small, n, st));
+    if (ensure_tmp(u, rbytes)) return -5;
+    rbytes = u.tmp_bytes;
+    UPD_CHK(hipcub::DeviceReduce::Sum(u.tmp, rbytes, trig, u.d_small, n, st));
+    rbytes = u.tmp_bytes;
+    UPD_CHK(hipcub::DeviceReduce::Sum(u.tmp, rbytes, dead, u.d_small + 1, n, st));
     return 0;
 }
 
@@ -480,8 +541,15 @@ int map_delete_boxes(GridBuf& g, MapUpdBuf& u, const float* boxes, int nb, float
         u.boxes_cap = nb;
     }
     UPD_CHK(hipMemcpyAsync(u.boxes, boxes, (size_t)nb * 6 * sizeof(float), hipMemcpyHostToDevice, st));
-    UPD_CHK(hipMemsetAsync(u.d_small, 0, sizeof(int), st));
-    delete_boxes_kernel<<<(int)((g.n_ids + 255) / 256), 256, 0, st>>>(g.by_id, g.n_ids, u.boxes, nb, u.d_small);
+    const int nblk = (int)((g.n_ids + 255) / 256);
+    if (ensure_pts(u, nblk)) return -5;
+    int* cnt = reinterpret_cast<int*>(u.flag2);
+    delete_boxes_kernel<<<nblk, 256, 0, st>>>(g.by_id, g.n_ids, u.boxes, nb, cnt);
+    size_t bytes = 0;
+    UPD_CHK(hipcub::DeviceReduce::Sum(nullptr, bytes, cnt, u.d_small, nblk, st));
+    if (ensure_tmp(u, bytes)) return -5;
+    bytes = u.tmp_bytes;
+    UPD_CHK(hipcub::DeviceReduce::Sum(u.tmp, bytes, cnt, u.d_small, nblk, st));
     UPD_CHK(hipMemcpyAsync(u.h_small, u.d_small, sizeof(int), hipMemcpyDeviceToHost, st));
     UPD_CHK(hipStreamSynchronize(st));
     *n_deleted = u.h_small[0];
