@@ -408,33 +408,61 @@ def rotz(a):
 
 
 def make_raw_scan(scene: Scene, n: int = 120_000, kind: str = "kitti64", seed: int = 7, speed: float = 8.0,
-                  yaw_rate: float = 0.3, duration: float = 0.1, imu_hz: float = 100.0):
-    """A raw LiDAR sweep with per-point time offsets and the IMU poses of that sweep.
+                  yaw_rate: float = 0.3, duration: float = 0.1, imu_hz: float = 100.0, origin=(0.0, 0.0, 0.0),
+                  yaw0: float = 0.0):
+    """A raw, motion-distorted LiDAR sweep with per-point time offsets and the IMU poses of that sweep.
 
-    Returns (raw, imu_poses, end24): raw rows (x, y, z, intensity, time_ms) in the LiDAR frame,
-    in firing (azimuth) order with time = azimuth fraction * duration; imu_poses as FAST-LIO's
-    IMUpose list (set_pose6d: offset_time, acc, gyr, vel, pos, rot) for constant forward speed
-    and yaw rate; end24 = pose24 of the state at the sweep end (lio_pose layout).
+    The IMU moves from `origin` (heading yaw0) at constant speed and yaw rate; the sweep is
+    ray-cast at the end pose and every point is re-expressed in the LiDAR frame of its own
+    firing time (time = azimuth fraction * duration), so FAST-LIO's UndistortPcl maps it back.
+    Returns (raw, imu_poses, end24): raw rows (x, y, z, intensity, time_ms) in firing order;
+    imu_poses as the IMUpose list (set_pose6d: offset_time, acc, gyr, vel, pos, rot); end24 =
+    pose24 of the IMU state at the sweep end (lio_pose layout).
     """
-    sc = make_scan(scene, n, kind, pos_gt=[0.0, 0.0, 0.0], yaw_gt=0.0, seed=seed)
+    o = np.asarray(origin, dtype=np.float64)
+
+    def traj(t):
+        yaw = yaw0 + yaw_rate * t
+        if abs(yaw_rate) > 1e-12:
+            dx = speed / yaw_rate * (math.sin(yaw) - math.sin(yaw0))
+            dy = speed / yaw_rate * (math.cos(yaw0) - math.cos(yaw))
+        else:
+            dx, dy = speed * t * math.cos(yaw0), speed * t * math.sin(yaw0)
+        return rotz(yaw), o + np.array([dx, dy, 0.0]), yaw
+
+    R_e, p_e, yaw_e = traj(duration)
+    sc = make_scan(scene, n, kind, pos_gt=p_e, yaw_gt=yaw_e, seed=seed)
     rng = np.random.default_rng(seed)
-    b = sc.body.astype(np.float32)
-    az = np.arctan2(b[:, 1], b[:, 0])
+    pe = sc.body.astype(np.float64)  # LiDAR frame at the sweep end
+    az = np.arctan2(pe[:, 1], pe[:, 0])
+    order = np.argsort(az, kind="stable")
+    pe, az = pe[order], az[order]
     t_ms = ((az + np.pi) / (2 * np.pi) * duration * 1000.0).astype(np.float32)
-    inten = rng.uniform(0, 255, len(b)).astype(np.float32)
-    raw = np.concatenate([b, inten[:, None], t_ms[:, None]], axis=1).astype(np.float32)
-    raw = raw[np.argsort(az, kind="stable")]
+    w = (pe @ R_LI.T + T_LI) @ R_e.T + p_e  # world points
+    raw = np.empty((len(pe), 5), np.float32)
+    for i0 in range(0, len(pe), 4096):  # re-express at each firing time
+        sl = slice(i0, i0 + 4096)
+        t = t_ms[sl].astype(np.float64) / 1000.0
+        yaw = yaw0 + yaw_rate * t
+        c, s_ = np.cos(yaw), np.sin(yaw)
+        if abs(yaw_rate) > 1e-12:
+            px = o[0] + speed / yaw_rate * (s_ - math.sin(yaw0))
+            py = o[1] + speed / yaw_rate * (math.cos(yaw0) - c)
+        else:
+            px = o[0] + speed * t * math.cos(yaw0)
+            py = o[1] + speed * t * math.sin(yaw0)
+        d = w[sl] - np.stack([px, py, np.full_like(px, o[2])], axis=1)
+        imu = np.stack([c * d[:, 0] + s_ * d[:, 1], -s_ * d[:, 0] + c * d[:, 1], d[:, 2]], axis=1)  # R_t^T d
+        raw[sl, :3] = ((imu - T_LI) @ R_LI).astype(np.float32)
+    raw[:, 3] = rng.uniform(0, 255, len(pe)).astype(np.float32)
+    raw[:, 4] = t_ms
     poses = []
     k = int(round(duration * imu_hz))
     for j in range(k + 1):
         t = j / imu_hz
-        yaw = yaw_rate * t
-        R = rotz(yaw)
-        vel = R @ np.array([speed, 0.0, 0.0])
-        poses.append(dict(offset_time=t, acc=np.array([0.0, speed * yaw_rate, 0.0]) + rng.normal(0, 0.01, 3),
-                          gyr=np.array([0.0, 0.0, yaw_rate]) + rng.normal(0, 0.001, 3), vel=vel,
-                          pos=np.array([speed * t, 0.5 * speed * yaw_rate * t * t, 0.0]), rot=R))
-    e = poses[-1]
-    end24 = np.concatenate([e["rot"].ravel(), e["pos"] + rng.normal(0, 0.002, 3), np.eye(3).ravel(),
-                            T_LI]).astype(np.float64)
+        R, p, yaw = traj(t)
+        vel = speed * np.array([math.cos(yaw), math.sin(yaw), 0.0])
+        acc = speed * yaw_rate * np.array([-math.sin(yaw), math.cos(yaw), 0.0])
+        poses.append(dict(offset_time=t, acc=acc, gyr=np.array([0.0, 0.0, yaw_rate]), vel=vel, pos=p, rot=R))
+    end24 = np.concatenate([R_e.ravel(), p_e, R_LI.ravel(), T_LI]).astype(np.float64)
     return raw, poses, end24
