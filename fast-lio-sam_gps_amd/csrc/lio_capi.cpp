@@ -532,16 +532,24 @@ static int wait_result(lio_ctx* c, unsigned long long seq, double* sums) {
 
 int lio_match(lio_ctx* c, const lio_pose* pose, int redo_knn, double* sums) {
     if (!c || !pose || !sums) return fail(LIO_ERR_ARG, "lio_match: bad arguments");
-    if (c->map->n == 0) return fail(LIO_ERR_STATE, "lio_match: map is empty (call lio_map_build)");
+    if (c->map->grid.n_ids == 0) return fail(LIO_ERR_STATE, "lio_match: map is empty (call lio_map_build)");
     if (!redo_knn && !c->knn_valid) return fail(LIO_ERR_STATE, "lio_match: redo_knn=0 before any kNN evaluation");
     HIP_TRY(hipSetDevice(c->map->dev));
     hipStream_t st = c->map->st;
     lio::MatchArgs a = make_args(c, *pose);
-    if (c->n == 0) {
+    if (c->map->n == 0 && c->n > 0) {
+        // every map point deleted (Delete_Point_Boxes): Nearest_Search finds
+        // nothing, no point is effective ("No Effective Points!")
+        HIP_TRY(hipMemsetAsync(c->d_nn, 0xff, c->n * 5 * sizeof(int32_t), st));
+        HIP_TRY(hipMemsetAsync(c->d_sel, 0, c->n, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    if (c->n == 0 || c->map->n == 0) {
         std::memset(sums, 0, LIO_SUMS_LEN * sizeof(double));
         c->last_pose = *pose;
         c->have_eval = true;
         c->knn_valid = true;
+        c->knn_pose = *pose;
         return LIO_OK;
     }
     a.seq = ++c->seq;

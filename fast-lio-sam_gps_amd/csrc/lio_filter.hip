@@ -135,28 +135,125 @@ __global__ void run_head_kernel(const uint32_t* __restrict__ keys, int64_t n, ui
     head[j] = (j < n && keys[j] != kInvalid && (j == 0 || keys[j - 1] != keys[j])) ? 1u : 0u;
 }
 
-// one lane per voxel: fields summed in input order, divided by the count (float)
-__global__ void voxel_centroid_kernel(const float* __restrict__ p, int stride, const uint32_t* __restrict__ keys,
-                                      const uint32_t* __restrict__ vals, int64_t n, const uint32_t* __restrict__ head,
-                                      const uint32_t* __restrict__ vid, float* __restrict__ out) {
+// Voxel runs of the sorted keys: run r = [starts[r], ends[r]).  The run index
+// of element j is (inclusive head count) - 1 = vid[j] + head[j] - 1.
+__global__ void voxel_bounds_kernel(const uint32_t* __restrict__ keys, int64_t n, const uint32_t* __restrict__ head,
+                                    const uint32_t* __restrict__ vid, uint32_t* __restrict__ starts,
+                                    uint32_t* __restrict__ ends) {
     const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (j >= n || !head[j]) return;
+    if (j >= n) return;
+    const uint32_t key = keys[j];
+    if (key == kInvalid) return;
+    const uint32_t h = head[j];
+    const uint32_t r = vid[j] + h - 1;
+    if (h) starts[r] = (uint32_t)j;
+    if (j + 1 == n || keys[j + 1] != key) ends[r] = (uint32_t)(j + 1);
+}
+
+constexpr int kLaneRun = 16;  // runs up to this length: one lane; longer: one wave
+
+template <int NF>
+__device__ __forceinline__ void write_centroid(float* __restrict__ o, const float* acc, int stride, uint32_t cnt) {
+    const float c = (float)cnt;
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+        if (f < stride) o[f] = acc[f] / c;
+}
+
+// PCL VoxelGrid centroid: the voxel's fields summed one point at a time in
+// input order (float), divided by the count.  The chain of adds is serial, the
+// loads are not: short runs are summed by one lane with its loads issued four
+// points ahead; long runs (the dense ground next to the sensor) go to a wave.
+__global__ void voxel_centroid_kernel(const float* __restrict__ p, int stride, const uint32_t* __restrict__ vals,
+                                      const uint32_t* __restrict__ starts, const uint32_t* __restrict__ ends,
+                                      const uint32_t* __restrict__ n_vox, uint32_t* __restrict__ big,
+                                      uint32_t* __restrict__ n_big, float* __restrict__ out) {
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= *n_vox) return;
+    const uint32_t s = starts[v], e = ends[v];
+    if (e - s > (uint32_t)kLaneRun) {
+        big[atomicAdd(n_big, 1u)] = v;
+        return;
+    }
     float acc[kMaxFields];
 #pragma unroll
     for (int f = 0; f < kMaxFields; ++f) acc[f] = 0.f;
-    const uint32_t key = keys[j];
-    int64_t k = j;
-    for (; k < n && keys[k] == key; ++k) {
-        const float* q = p + (size_t)vals[k] * stride;
+    for (uint32_t k = s; k < e; k += 4) {
+        float q[4][kMaxFields];
 #pragma unroll
-        for (int f = 0; f < kMaxFields; ++f)
-            if (f < stride) acc[f] += q[f];
+        for (int u = 0; u < 4; ++u) {
+            const float* r = p + (size_t)vals[k + u < e ? k + u : s] * stride;
+#pragma unroll
+            for (int f = 0; f < kMaxFields; ++f) q[u][f] = f < stride ? r[f] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (k + u < e) {
+#pragma unroll
+                for (int f = 0; f < kMaxFields; ++f) acc[f] += q[u][f];
+            }
     }
-    const float cnt = (float)(k - j);
-    float* o = out + (size_t)vid[j] * stride;
+    write_centroid<kMaxFields>(out + (size_t)v * stride, acc, stride, e - s);
+}
+
+// long runs, one wave (= block) each: the lanes load 64 points at a time into
+// LDS (the next chunk's loads in flight while this one is summed); lane f
+// then adds field f of the 64 points in order — one LDS read + one add per
+// point, the fields in parallel
+__global__ void __launch_bounds__(64) voxel_centroid_big_kernel(const float* __restrict__ p, int stride,
+                                                                 const uint32_t* __restrict__ vals,
+                                                                 const uint32_t* __restrict__ starts,
+                                                                 const uint32_t* __restrict__ ends,
+                                                                 const uint32_t* __restrict__ big,
+                                                                 const uint32_t* __restrict__ n_big,
+                                                                 float* __restrict__ out) {
+    __shared__ float s_q[2][64 * kMaxFields];
+    const int lane = threadIdx.x;
+    const uint32_t nb = *n_big;
+    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const uint32_t v = big[b];
+        const uint32_t s = starts[v], e = ends[v];
+        float q[kMaxFields];
+        auto load = [&](uint32_t k) {
+            const float* r = p + (size_t)vals[k + lane < e ? k + lane : s] * stride;
 #pragma unroll
-    for (int f = 0; f < kMaxFields; ++f)
-        if (f < stride) o[f] = acc[f] / cnt;
+            for (int f = 0; f < kMaxFields; ++f) q[f] = f < stride ? r[f] : 0.f;
+        };
+        auto stash = [&](int buf) {
+#pragma unroll
+            for (int f = 0; f < kMaxFields; ++f)
+                if (f < stride) s_q[buf][lane * stride + f] = q[f];
+        };
+        float acc = 0.f;
+        load(s);
+        stash(0);
+        __syncthreads();
+        int buf = 0;
+        for (uint32_t k = s; k < e; k += 64) {
+            const bool more = k + 64 < e;
+            if (more) load(k + 64);
+            const uint32_t m = min(64u, e - k);
+            if (lane < stride) {
+                const float* col = s_q[buf] + lane;
+                uint32_t l = 0;
+                for (; l + 4 <= m; l += 4) {
+                    const float a0 = col[(l + 0) * stride], a1 = col[(l + 1) * stride];
+                    const float a2 = col[(l + 2) * stride], a3 = col[(l + 3) * stride];
+                    acc += a0;
+                    acc += a1;
+                    acc += a2;
+                    acc += a3;
+                }
+                for (; l < m; ++l) acc += col[l * stride];
+            }
+            if (more) {
+                stash(buf ^ 1);
+                buf ^= 1;
+            }
+            __syncthreads();
+        }
+        if (lane < stride) out[(size_t)v * stride + lane] = acc / (float)(e - s);
+    }
 }
 
 __global__ void copy_strided_kernel(const float* __restrict__ a, int64_t nf, float* __restrict__ b) {
@@ -339,7 +436,7 @@ int ftmp(FilterBuf& b, size_t need) {
 int reserve(FilterBuf& b, int64_t n) {
     if (n <= b.cap && b.keys) return 0;
     const int64_t c = std::max<int64_t>(n, b.cap + b.cap / 2);
-    void* bufs[] = {b.keys, b.keys_alt, b.vals, b.vals_alt, b.head, b.vid};
+    void* bufs[] = {b.keys, b.keys_alt, b.vals, b.vals_alt, b.head, b.vid, b.big};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     FCHK(hipMalloc(&b.keys, c * sizeof(uint32_t)));
@@ -348,6 +445,7 @@ int reserve(FilterBuf& b, int64_t n) {
     FCHK(hipMalloc(&b.vals_alt, c * sizeof(uint32_t)));
     FCHK(hipMalloc(&b.head, (c + 1) * sizeof(uint32_t)));
     FCHK(hipMalloc(&b.vid, (c + 1) * sizeof(uint32_t)));
+    FCHK(hipMalloc(&b.big, (c + 1) * sizeof(uint32_t)));  // long-run list + its count at [c]
     b.cap = c;
     if (!b.part) FCHK(hipMalloc(&b.part, 6 * 1024 * sizeof(float)));
     if (!b.geom) FCHK(hipMalloc(&b.geom, sizeof(VoxelGeom)));
@@ -477,7 +575,8 @@ int records_to_xyz(const float* d_rec, int64_t n, int stride, float* d_xyz, hipS
 }
 
 void filter_free(FilterBuf& b) {
-    void* bufs[] = {b.keys, b.keys_alt, b.vals, b.vals_alt, b.head, b.vid, b.part, b.geom, b.tmp, b.a, b.c, b.aux};
+    void* bufs[] = {b.keys, b.keys_alt, b.vals,  b.vals_alt, b.head, b.vid, b.big,
+                    b.part, b.geom,     b.tmp,  b.a,         b.c,    b.aux};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (b.h_small) (void)hipHostFree(b.h_small);
@@ -499,7 +598,13 @@ int voxel_grid(FilterBuf& b, const float* d_in, int64_t n, int stride, const flo
     run_head_kernel<<<nblk(n + 1), 256, 0, st>>>(b.keys_alt, n, b.head);
     rc = exscan(b, b.head, b.vid, n + 1, st);
     if (rc) return rc;
-    voxel_centroid_kernel<<<nblk(n), 256, 0, st>>>(d_in, stride, b.keys_alt, b.vals_alt, n, b.head, b.vid, d_out);
+    // runs -> [start, end) per voxel (b.keys / b.vals are free after the sort)
+    voxel_bounds_kernel<<<nblk(n), 256, 0, st>>>(b.keys_alt, n, b.head, b.vid, b.keys, b.vals);
+    FCHK(hipMemsetAsync(b.big + b.cap, 0, sizeof(uint32_t), st));
+    voxel_centroid_kernel<<<nblk(n), 256, 0, st>>>(d_in, stride, b.vals_alt, b.keys, b.vals, b.vid + n, b.big,
+                                                   b.big + b.cap, d_out);
+    voxel_centroid_big_kernel<<<1024, 64, 0, st>>>(d_in, stride, b.vals_alt, b.keys, b.vals, b.big, b.big + b.cap,
+                                                   d_out);
     FCHK(hipMemcpyAsync(b.h_small, b.vid + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     FCHK(hipMemcpyAsync(b.h_small + 1, b.geom, sizeof(VoxelGeom), hipMemcpyDeviceToHost, st));
     FCHK(hipStreamSynchronize(st));

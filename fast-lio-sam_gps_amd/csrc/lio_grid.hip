@@ -193,16 +193,18 @@ __global__ void merge_new_kernel(const float4* __restrict__ by_id, const uint32_
     ckeys_out[o] = c;
 }
 
-// cell counts of the (cell-sorted) entries without atomics: the head of each
-// run of equal keys walks to the run's end and writes the length once
+// cell counts of the (cell-sorted) entries: a run's head subtracts its index
+// and its tail adds its end (two uncontended atomics per cell, mod 2^32), so no
+// lane walks a run — dense cells hold thousands of entries
 __global__ void run_count_kernel(const uint32_t* __restrict__ ckeys, int64_t n, uint32_t* __restrict__ counts) {
     const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (j >= n) return;
     const uint32_t k = ckeys[j];
-    if (j > 0 && ckeys[j - 1] == k) return;
-    int64_t e = j + 1;
-    while (e < n && ckeys[e] == k) ++e;
-    counts[k] = (uint32_t)(e - j);
+    const bool head = j == 0 || ckeys[j - 1] != k;
+    const bool tail = j + 1 == n || ckeys[j + 1] != k;
+    if (head && tail) counts[k] = 1u;
+    else if (head) atomicSub(&counts[k], (uint32_t)j);
+    else if (tail) atomicAdd(&counts[k], (uint32_t)(j + 1));
 }
 
 #define HIPCHK(x)                                                               \

@@ -164,28 +164,46 @@ __global__ void __launch_bounds__(256) voxel_resolve_kernel(const uint64_t* __re
                     }
                 }
     }
-    // ---- replay the run (lane 0's result broadcast through the uniform loop)
+    // ---- replay the run: the lanes load 64 of its points at a time (the run is
+    // a prefix of the chunk: keys are sorted), every lane replays them in order
+    // from the broadcast values (wave-uniform state)
     int surv_new = -1;
     float sx = bx, sy = by, sz = bz, sd = best_d;
     int triggers = 0;
     bool first = true;
-    for (int k = j; k < n && skeys[k] == key; ++k) {
-        const int i = (int)svals[k];
-        const float qx = xyz[3 * i], qy = xyz[3 * i + 1], qz = xyz[3 * i + 2];
-        const float qd = calc_dist(qx, qy, qz, b.mid[0], b.mid[1], b.mid[2]);
-        const int size_s = first ? cnt_e : 1;
-        const bool q_wins = size_s == 0 || !(sd < qd);
-        if (size_s > 1 || q_wins || same_point(qx, qy, qz, sx, sy, sz)) {
-            ++triggers;
-            if (q_wins) {
-                surv_new = i;
-                sx = qx;
-                sy = qy;
-                sz = qz;
-                sd = qd;
-            }
+    for (int k = j;; k += 64) {
+        const int kk = k + lane;
+        const bool in = kk < n && skeys[kk] == key;
+        const int m = __popcll(__ballot(in));
+        int il = 0;
+        float lx = 0.f, ly = 0.f, lz = 0.f;
+        if (in) {
+            il = (int)svals[kk];
+            lx = xyz[3 * il];
+            ly = xyz[3 * il + 1];
+            lz = xyz[3 * il + 2];
         }
-        first = false;
+        for (int l = 0; l < m; ++l) {
+            const int i = __builtin_amdgcn_readlane(il, l);
+            const float qx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lx), l));
+            const float qy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ly), l));
+            const float qz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lz), l));
+            const float qd = calc_dist(qx, qy, qz, b.mid[0], b.mid[1], b.mid[2]);
+            const int size_s = first ? cnt_e : 1;
+            const bool q_wins = size_s == 0 || !(sd < qd);
+            if (size_s > 1 || q_wins || same_point(qx, qy, qz, sx, sy, sz)) {
+                ++triggers;
+                if (q_wins) {
+                    surv_new = i;
+                    sx = qx;
+                    sy = qy;
+                    sz = qz;
+                    sd = qd;
+                }
+            }
+            first = false;
+        }
+        if (m < 64) break;
     }
     // ---- tombstones: every map point of the box except a surviving map point
     int dead = 0;

@@ -35,6 +35,8 @@ for s in $STEPS; do
            run knn_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/knnprof" -o run --output-format csv -- python scripts/knn_timing.py C2 ;;
     quick) run bench_quick 400 python bench.py --steps 60 --warmup 5 --icp-reps 2 --cpu-seconds 4 ;;
     c3)    run bench_c3 600 python bench.py --config C3 --steps 60 --warmup 5 --no-icp --cpu-seconds 4 --pipeline 12 ;;
+    ppprof) run rocprof_pipeline 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/ppprof" -o run \
+               --output-format csv -- python bench.py --config C3 --steps 5 --warmup 2 --no-icp --no-cpu --pipeline 12 ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
                -- python bench.py --steps 100 --warmup 10 --no-cpu --icp-reps 3 ;;
     pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv \

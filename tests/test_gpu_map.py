@@ -117,3 +117,32 @@ def test_map_incremental_parity(oracle, scene_scans):
         _same_map(tree, om)
         hm.close()
     assert s_orc["n_to_add"] > 0
+
+
+def test_everything_deleted_then_regrown(oracle, scene_scans):
+    """Delete_Point_Boxes over the whole map: Nearest_Search finds nothing (no
+    effective points, sums zero, empty lists); map_incremental then re-adds the
+    scan through the downsampled Add_Points, as the oracle does."""
+    _, m, scans = scene_scans
+    base = m[:30000]
+    tree = F.IkdTreeGPU(cell_size=1.0, downsample_size=0.5)
+    tree.Build(base)
+    om = oracle.OracleDynMap(base)
+    lo, hi = base.min(0) - 1, base.max(0) + 1
+    box = np.array([[lo[0], lo[1], lo[2], hi[0], hi[1], hi[2]]], np.float32)
+    assert tree.Delete_Point_Boxes(box) == om.delete_boxes(box) == len(base)
+    assert tree.size() == 0
+    sc = scans[1]
+    hm = F.HShareModelGPU(tree)
+    hm.set_scan(sc.body)
+    p24 = synth.pose24(synth.initial_state(sc.pos_gt, sc.rot_gt))
+    sums = hm(p24, True)
+    assert not np.any(sums)
+    gi, _ = hm.nearest_points()
+    assert np.all(gi == -1)
+    s_gpu = hm.map_incremental(p24, 0.5)
+    s_orc = om.map_incremental(sc.body, p24, p24, 0.5, 0.5)
+    assert s_gpu == s_orc and s_gpu["n_to_add"] == len(sc.body)
+    _same_map(tree, om)
+    hm.close()
+    _knn_parity(tree, om, scans[2].body)
