@@ -80,6 +80,10 @@ struct lio_map {
     float* d_xyz = nullptr;
     int64_t xyz_cap = 0;
     int64_t n = 0;  // alive points (== grid.n)
+    int32_t* d_qidx = nullptr;  // lio_map_nearest_search results
+    int64_t qidx_cap = 0;
+    float* d_qd2 = nullptr;
+    int64_t qd2_cap = 0;
 };
 
 // geometry slack when an insert leaves the grid: the rebuild reserves room
@@ -168,6 +172,8 @@ int lio_map_destroy(lio_map* m) {
     lio::grid_free(m->grid);
     lio::mapupd_free(m->upd);
     if (m->d_xyz) (void)hipFree(m->d_xyz);
+    if (m->d_qidx) (void)hipFree(m->d_qidx);
+    if (m->d_qd2) (void)hipFree(m->d_qd2);
     (void)hipStreamDestroy(m->st);
     delete m;
     return LIO_OK;
@@ -239,6 +245,44 @@ int lio_map_get_by_id(lio_map* m, float* xyz_out, uint8_t* alive_out) {
         }
         if (alive_out) alive_out[i] = tmp[i].w != 0.f;
     }
+    return LIO_OK;
+}
+
+int lio_map_nearest_search(lio_map* m, const float* q, int64_t n, int k, float max_dist, int32_t* idx, float* d2) {
+    if (!m || n < 0 || k < 1 || k > 5 || (n > 0 && (!q || !idx)) || n >= (int64_t)1 << 30 || std::isnan(max_dist))
+        return fail(LIO_ERR_ARG, "lio_map_nearest_search: bad arguments (k must be 1..5)");
+    if (m->grid.n_ids == 0) return fail(LIO_ERR_STATE, "lio_map_nearest_search: map is empty (call lio_map_build)");
+    if (n == 0) return LIO_OK;
+    HIP_TRY(hipSetDevice(m->dev));
+    int rc = grow(&m->d_xyz, m->xyz_cap, n, 3);
+    if (!rc) rc = grow(&m->d_qidx, m->qidx_cap, n * k);
+    if (!rc && d2) rc = grow(&m->d_qd2, m->qd2_cap, n * k);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(m->d_xyz, q, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice, m->st));
+    const lio::GridDev g = lio::grid_view(m->grid);
+    const bool unbounded = !(max_dist > 0.f) || std::isinf(max_dist);
+    const float bound = unbounded ? INFINITY : max_dist * max_dist;
+    const int max_shell = unbounded ? 0x3fffffff : (int)std::ceil(max_dist / g.cell) + 1;
+    lio::launch_map_knn(g, m->d_xyz, (int)n, bound, max_shell, k, m->d_qidx, d2 ? m->d_qd2 : nullptr, m->st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(idx, m->d_qidx, (size_t)n * k * sizeof(int32_t), hipMemcpyDeviceToHost, m->st));
+    if (d2) HIP_TRY(hipMemcpyAsync(d2, m->d_qd2, (size_t)n * k * sizeof(float), hipMemcpyDeviceToHost, m->st));
+    HIP_TRY(hipStreamSynchronize(m->st));
+    return LIO_OK;
+}
+
+int lio_map_gather(lio_map* m, const int32_t* ids, int64_t n, float* xyz_out) {
+    if (!m || n < 0 || (n > 0 && (!ids || !xyz_out))) return fail(LIO_ERR_ARG, "lio_map_gather: bad arguments");
+    if (n == 0) return LIO_OK;
+    HIP_TRY(hipSetDevice(m->dev));
+    int rc = grow(&m->d_qidx, m->qidx_cap, n);
+    if (!rc) rc = grow(&m->d_xyz, m->xyz_cap, n, 3);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(m->d_qidx, ids, (size_t)n * sizeof(int32_t), hipMemcpyHostToDevice, m->st));
+    lio::map_gather_ids(m->grid, m->d_qidx, n, m->d_xyz, m->st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(xyz_out, m->d_xyz, (size_t)n * 3 * sizeof(float), hipMemcpyDeviceToHost, m->st));
+    HIP_TRY(hipStreamSynchronize(m->st));
     return LIO_OK;
 }
 

@@ -38,6 +38,9 @@ void launch_debug(const MatchArgs& a, float* world, float* d2, float* abcd_pd2, 
 void launch_h_rows(const MatchArgs& a, double* rows, int64_t max_rows, int64_t* n_rows, hipStream_t st);
 void launch_finalize(const MatchArgs& a, int nblocks, hipStream_t st);  // -> sums_out, seq_out
 int match_blocks(int n);
+// batch Nearest_Search: k <= 5 neighbours per query within d2 <= bound (INFINITY: unbounded)
+void launch_map_knn(const GridDev& g, const float* q, int n, float bound, int max_shell, int k, int32_t* idx,
+                    float* d2, hipStream_t st);
 
 // --------------------------------------------------------------- grid build
 struct GridGeom {

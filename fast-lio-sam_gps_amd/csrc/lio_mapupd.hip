@@ -630,4 +630,23 @@ int map_incremental(GridBuf& g, MapUpdBuf& u, IncrArgs a, float ds, float slack,
     return grid_update(g, id0, dead > 0, slack, st);
 }
 
+namespace {
+__global__ void gather_ids_kernel(const float4* __restrict__ by_id, int64_t n_ids, const int32_t* __restrict__ ids,
+                                  int64_t n, float* __restrict__ xyz) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const int32_t id = ids[i];
+    float4 p = make_float4(NAN, NAN, NAN, 0.f);
+    if (id >= 0 && id < n_ids) p = by_id[id];
+    xyz[3 * i] = p.x;
+    xyz[3 * i + 1] = p.y;
+    xyz[3 * i + 2] = p.z;
+}
+}  // namespace
+
+void map_gather_ids(const GridBuf& g, const int32_t* d_ids, int64_t n, float* d_xyz, hipStream_t st) {
+    if (n <= 0) return;
+    gather_ids_kernel<<<(int)((n + 255) / 256), 256, 0, st>>>(g.by_id, g.n_ids, d_ids, n, d_xyz);
+}
+
 }  // namespace lio

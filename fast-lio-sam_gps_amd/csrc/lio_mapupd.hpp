@@ -56,5 +56,7 @@ int map_add_device(GridBuf& g, MapUpdBuf& u, const float* d_xyz, int64_t n, bool
 int map_delete_boxes(GridBuf& g, MapUpdBuf& u, const float* boxes, int nb, float slack, int64_t* n_deleted,
                      hipStream_t st);
 int map_incremental(GridBuf& g, MapUpdBuf& u, IncrArgs a, float ds, float slack, int64_t out[4], hipStream_t st);
+// xyz of map ids (Nearest_Points from ids): ids < 0 or >= n_ids -> NaN
+void map_gather_ids(const GridBuf& g, const int32_t* d_ids, int64_t n, float* d_xyz, hipStream_t st);
 
 }  // namespace lio

@@ -284,6 +284,35 @@ __global__ void __launch_bounds__(1024) finalize_kernel(const double* __restrict
     }
 }
 
+// ikd-Tree Nearest_Search(point, k, Nearest_Points, Point_Distance, max_dist)
+// over a batch of query points: 8 lanes per query, exact (d2, id)-ordered
+// 5-NN within d2 <= bound (bound = INFINITY: unbounded, any number of shells),
+// the first k kept.  Missing neighbours: id -1, d2 = INFINITY.
+__global__ void __launch_bounds__(256) map_knn_kernel(GridDev g, const float* __restrict__ q, int n, float bound,
+                                                      int max_shell, int k, int32_t* __restrict__ idx,
+                                                      float* __restrict__ d2) {
+    constexpr int G = kGroup;
+    const int sub = threadIdx.x % G;
+    const int i = blockIdx.x * (256 / G) + threadIdx.x / G;
+    if (i >= n) return;
+    TopK<5> tk;
+    tk.init(bound);
+    group_knn_exact<5, G>(g, q[3 * (size_t)i], q[3 * (size_t)i + 1], q[3 * (size_t)i + 2], max_shell, sub, tk);
+    if (sub < k) {
+        int v = tk.id(0);
+        float d = tk.d(0);
+#pragma unroll
+        for (int j = 1; j < 5; ++j)
+            if (sub == j) {
+                v = tk.id(j);
+                d = tk.d(j);
+            }
+        const bool ok = v != kNone;
+        idx[(size_t)i * k + sub] = ok ? v : -1;
+        if (d2) d2[(size_t)i * k + sub] = ok ? d : INFINITY;
+    }
+}
+
 // Debug: world points, d2 of the stored neighbours, pd2 of selected points.
 __global__ void debug_kernel(MatchArgs a, float* __restrict__ world, float* __restrict__ d2,
                              float* __restrict__ abcd_pd2) {
@@ -409,6 +438,12 @@ void launch_h_rows(const MatchArgs& a, double* rows, int64_t max_rows, int64_t* 
 
 void launch_finalize(const MatchArgs& a, int nblocks, hipStream_t st) {
     finalize_kernel<<<1, 1024, 0, st>>>(a.partials, nblocks, a.sums_out, a.seq_out, a.seq);
+}
+
+void launch_map_knn(const GridDev& g, const float* q, int n, float bound, int max_shell, int k, int32_t* idx,
+                    float* d2, hipStream_t st) {
+    if (n <= 0) return;
+    map_knn_kernel<<<(n + 256 / kGroup - 1) / (256 / kGroup), 256, 0, st>>>(g, q, n, bound, max_shell, k, idx, d2);
 }
 
 int match_blocks(int n) {  // partial slots (plane / reuse kernels)

@@ -109,6 +109,16 @@ class IkdTreeGPU:
         check(lib().lio_map_get_by_id(self._h, _fp(xyz), alive.ctypes.data_as(C.POINTER(C.c_uint8))))
         return xyz, alive.astype(bool)
 
+    def Nearest_Search(self, points: np.ndarray, k_nearest: int = 5, max_dist: float = float("inf")):
+        """ikdtree.Nearest_Search(point, k, Nearest_Points, Point_Distance, max_dist) [U] for a batch:
+        (ids[n,k] into by_id (-1 where missing), sq-distances[n,k] (inf where missing))."""
+        q = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 3)
+        idx = np.empty((len(q), k_nearest), np.int32)
+        d2 = np.empty((len(q), k_nearest), np.float32)
+        check(lib().lio_map_nearest_search(self._h, _fp(q), len(q), k_nearest, max_dist,
+                                           idx.ctypes.data_as(C.POINTER(C.c_int32)), _fp(d2)))
+        return idx, d2
+
     def Add_Points(self, points: np.ndarray, downsample_on: bool) -> int:
         """ikdtree.Add_Points(PointToAdd, downsample_on) [U]; returns the reference's count."""
         pts = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 3)

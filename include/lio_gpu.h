@@ -83,6 +83,17 @@ int64_t lio_map_num_ids(const lio_map* m);
 int lio_map_get_points(lio_map* m, float* xyz_out);
 /* every id: xyz (num_ids*3, may be NULL) and alive flags (num_ids, may be NULL) */
 int lio_map_get_by_id(lio_map* m, float* xyz_out, uint8_t* alive_out);
+/* ikd-Tree Nearest_Search(point, k, Nearest_Points, Point_Distance, max_dist)
+ * [U: ikd-Tree ikd_Tree.h; FAST-LIO laserMapping.cpp h_share_model calls it
+ * with k = NUM_MATCH_POINTS = 5, max_dist = INFINITY] for a batch of n query
+ * points q (n*3 float): the k <= 5 nearest alive map points in ascending
+ * (sq-distance, id) order with sq-distance <= max_dist^2 (max_dist <= 0 or
+ * INFINITY: unbounded).  idx (n*k, map ids = insertion order, -1 where fewer
+ * exist), d2 (n*k, optional, INFINITY where missing).                      */
+int lio_map_nearest_search(lio_map* m, const float* q, int64_t n, int k, float max_dist, int32_t* idx, float* d2);
+/* Coordinates of map ids (Nearest_Points from lio_map_nearest_search /
+ * lio_get_knn ids): xyz_out n*3; ids < 0 or unknown give NaN.             */
+int lio_map_gather(lio_map* m, const int32_t* ids, int64_t n, float* xyz_out);
 
 /* ---- incremental maintenance ----
  * ikdtree.Add_Points(PointToAdd, downsample_on) [U]: with downsample, per

@@ -1,0 +1,328 @@
+// lio_gpu.hpp — C++ host-side mirror of the reference interfaces over the
+// C-ABI in lio_gpu.h (header-only; link liblio_gpu.so).
+//
+// What a FAST-LIO-SAM maintainer swaps in, under the reference's own names:
+//   * KdTreeGPU<PointType>   ~ ikd-Tree `KD_TREE<PointType>` [U: ikd_Tree.h]:
+//       Build, Nearest_Search (single point and batch), Add_Points,
+//       Delete_Point_Boxes, size, validnum, flatten, set_downsample_param
+//   * ScanMatcherGPU          ~ laserMapping.cpp h_share_model +
+//       kf.update_iterated_dyn_share_modified(LASER_POINT_COV, solve_time)
+//       + map_incremental() + lasermap_fov_segment() [U]
+//   * LoopClosureICP          ~ LoopClosure::icpAlignment
+//       (fast_lio_sam/src/loop_closure.cpp:69-92, loop_closure.h:31-37)
+// PointType is any struct with float members x, y, z (pcl::PointXYZI,
+// pcl::PointXYZINormal, ...).  Errors throw lio_gpu::Error carrying
+// lio_last_error(); there is no CPU fallback behind any call.
+#pragma once
+#include <cmath>
+#include <cstdint>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "lio_gpu.h"
+
+namespace lio_gpu {
+
+struct Error : std::runtime_error {
+    int code;
+    Error(int rc, const std::string& what) : std::runtime_error(what), code(rc) {}
+};
+
+inline void check(int rc, const char* where) {
+    if (rc != LIO_OK) throw Error(rc, std::string(where) + ": " + lio_last_error());
+}
+
+// ikd-Tree's BoxPointType (vertex_min / vertex_max), min <= p < max
+struct BoxPointType {
+    float vertex_min[3];
+    float vertex_max[3];
+};
+
+template <typename P>
+std::vector<float> packed_xyz(const std::vector<P>& pts) {
+    std::vector<float> xyz(pts.size() * 3);
+    for (size_t i = 0; i < pts.size(); ++i) {
+        xyz[3 * i] = pts[i].x;
+        xyz[3 * i + 1] = pts[i].y;
+        xyz[3 * i + 2] = pts[i].z;
+    }
+    return xyz;
+}
+
+// Eigen::Quaterniond::toRotationMatrix for (w, x, y, z), row-major
+inline void quat_to_rot(const double q[4], double R[9]) {
+    const double w = q[0], x = q[1], y = q[2], z = q[3];
+    const double tx = 2 * x, ty = 2 * y, tz = 2 * z;
+    const double twx = tx * w, twy = ty * w, twz = tz * w, txx = tx * x, txy = ty * x, txz = tz * x;
+    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    R[0] = 1 - (tyy + tzz), R[1] = txy - twz, R[2] = txz + twy;
+    R[3] = txy + twz, R[4] = 1 - (txx + tzz), R[5] = tyz - twx;
+    R[6] = txz - twy, R[7] = tyz + twx, R[8] = 1 - (txx + tyy);
+}
+
+// the parts of state_ikfom the measurement model reads
+inline lio_pose pose_of(const lio_state& x) {
+    lio_pose p{};
+    quat_to_rot(x.rot, p.R);
+    quat_to_rot(x.offset_R_L_I, p.R_LI);
+    for (int k = 0; k < 3; ++k) {
+        p.t[k] = x.pos[k];
+        p.t_LI[k] = x.offset_T_L_I[k];
+    }
+    return p;
+}
+
+// ---------------------------------------------------------------------------
+// KD_TREE<PointType> surface used by laserMapping.cpp, on the device grid.
+// Ids are insertion order; deleted points stay as tombstoned ids.
+template <typename PointType>
+class KdTreeGPU {
+public:
+    using PointVector = std::vector<PointType>;
+
+    explicit KdTreeGPU(float cell_size = 1.0f, float downsample_size = 0.5f, int device = 0)
+        : cell_(cell_size), dev_(device) {
+        lio_map_params p{cell_size, downsample_size, device, 0};
+        check(lio_map_create(&p, &m_), "lio_map_create");
+    }
+    ~KdTreeGPU() { lio_map_destroy(m_); }
+    KdTreeGPU(const KdTreeGPU&) = delete;
+    KdTreeGPU& operator=(const KdTreeGPU&) = delete;
+
+    // ikdtree.set_downsample_param(filter_size_map_min): recreates the map
+    // parameters; call before Build, as laserMapping does
+    void set_downsample_param(float ds) {
+        if (lio_map_num_ids(m_) > 0) throw Error(LIO_ERR_STATE, "set_downsample_param: call before Build");
+        lio_map_params p{cell_, ds, dev_, 0};
+        lio_map_destroy(m_);
+        m_ = nullptr;
+        check(lio_map_create(&p, &m_), "lio_map_create");
+    }
+
+    void Build(const PointVector& pts) {
+        const std::vector<float> xyz = packed_xyz(pts);
+        check(lio_map_build(m_, xyz.data(), (int64_t)pts.size()), "Build");
+    }
+
+    // single query, as h_share_model calls it (k = 5, max_dist = INFINITY);
+    // prefer the batch form or ScanMatcherGPU on hot loops
+    void Nearest_Search(const PointType& point, int k_nearest, PointVector& Nearest_Points,
+                        std::vector<float>& Point_Distance, double max_dist = INFINITY) {
+        std::vector<int32_t> ids;
+        Nearest_Search_Batch(PointVector{point}, k_nearest, ids, Point_Distance, max_dist);
+        resolve(ids, Nearest_Points);
+        size_t found = 0;
+        while (found < ids.size() && ids[found] >= 0) ++found;
+        Point_Distance.resize(found);
+    }
+
+    // batch: ids (n*k, -1 where fewer exist) and sq-distances (n*k, +inf where missing)
+    void Nearest_Search_Batch(const PointVector& q, int k_nearest, std::vector<int32_t>& ids,
+                              std::vector<float>& sq_dist, double max_dist = INFINITY) {
+        const std::vector<float> xyz = packed_xyz(q);
+        ids.resize(q.size() * k_nearest);
+        sq_dist.resize(q.size() * k_nearest);
+        check(lio_map_nearest_search(m_, xyz.data(), (int64_t)q.size(), k_nearest, (float)max_dist, ids.data(),
+                                     sq_dist.data()),
+              "Nearest_Search");
+    }
+
+    // ikdtree.Add_Points(PointToAdd, downsample_on): the reference's return value
+    int Add_Points(const PointVector& pts, bool downsample_on) {
+        const std::vector<float> xyz = packed_xyz(pts);
+        int64_t n = 0;
+        check(lio_map_add(m_, xyz.data(), (int64_t)pts.size(), downsample_on ? 1 : 0, &n), "Add_Points");
+        return (int)n;
+    }
+
+    int Delete_Point_Boxes(const std::vector<BoxPointType>& boxes) {
+        std::vector<float> b(boxes.size() * 6);
+        for (size_t i = 0; i < boxes.size(); ++i)
+            for (int d = 0; d < 3; ++d) {
+                b[6 * i + d] = boxes[i].vertex_min[d];
+                b[6 * i + 3 + d] = boxes[i].vertex_max[d];
+            }
+        int64_t n = 0;
+        check(lio_map_delete_boxes(m_, b.data(), (int)boxes.size(), &n), "Delete_Point_Boxes");
+        return (int)n;
+    }
+
+    int size() const { return (int)lio_map_num_ids(m_); }   // ikd-Tree size(): nodes incl. deleted
+    int validnum() const { return (int)lio_map_size(m_); }  // alive points
+
+    // ikdtree.flatten(Root_Node, PCL_Storage, NOT_RECORD): the alive points (id order)
+    void flatten(PointVector& storage) {
+        std::vector<float> xyz;
+        std::vector<uint8_t> alive;
+        by_id(xyz, alive);
+        storage.clear();
+        for (size_t i = 0; i < alive.size(); ++i)
+            if (alive[i]) storage.push_back(make_point(&xyz[3 * i]));
+    }
+
+    // every id's coordinates + alive flag (kNN ids index this)
+    void by_id(std::vector<float>& xyz, std::vector<uint8_t>& alive) {
+        const int64_t n = lio_map_num_ids(m_);
+        xyz.resize((size_t)n * 3);
+        alive.resize((size_t)n);
+        check(lio_map_get_by_id(m_, xyz.data(), alive.data()), "by_id");
+    }
+
+    // ids -> points (Nearest_Points), skipping -1
+    void resolve(const std::vector<int32_t>& ids, PointVector& out) {
+        std::vector<int32_t> valid;
+        for (int32_t id : ids)
+            if (id >= 0) valid.push_back(id);
+        std::vector<float> xyz(valid.size() * 3);
+        check(lio_map_gather(m_, valid.data(), (int64_t)valid.size(), xyz.data()), "resolve");
+        out.clear();
+        for (size_t i = 0; i < valid.size(); ++i) out.push_back(make_point(&xyz[3 * i]));
+    }
+
+    lio_map* handle() { return m_; }
+
+private:
+    static PointType make_point(const float* p) {
+        PointType q{};
+        q.x = p[0];
+        q.y = p[1];
+        q.z = p[2];
+        return q;
+    }
+    lio_map* m_ = nullptr;
+    float cell_ = 1.0f;
+    int dev_ = 0;
+};
+
+// ---------------------------------------------------------------------------
+// h_share_model + IESKF update + map maintenance for one map.
+class ScanMatcherGPU {
+public:
+    template <typename P>
+    explicit ScanMatcherGPU(KdTreeGPU<P>& tree, const lio_match_params& p = defaults()) {
+        check(lio_ctx_create(tree.handle(), &p, &c_), "lio_ctx_create");
+    }
+    ~ScanMatcherGPU() { lio_ctx_destroy(c_); }
+    ScanMatcherGPU(const ScanMatcherGPU&) = delete;
+    ScanMatcherGPU& operator=(const ScanMatcherGPU&) = delete;
+
+    static lio_match_params defaults() { return lio_match_params{5.0f, 0.1f, 0.9, 0.9}; }
+
+    // feats_down_body
+    template <typename P>
+    void set_scan(const std::vector<P>& feats_down_body) {
+        const std::vector<float> xyz = packed_xyz(feats_down_body);
+        check(lio_scan_set(c_, xyz.data(), (int64_t)feats_down_body.size()), "set_scan");
+    }
+
+    // kf.update_iterated_dyn_share_modified(LASER_POINT_COV, solve_H_time): x, P (23x23 row-major) in place
+    lio_ieskf_stats update_iterated_dyn_share_modified(lio_state& x, double* P, double laser_point_cov = 0.001,
+                                                       int max_iteration = 3, double epsi = 0.001) {
+        lio_ieskf_params ip{laser_point_cov, max_iteration, epsi};
+        lio_ieskf_stats st{};
+        check(lio_ieskf_update(c_, &x, P, &ip, &st), "update_iterated_dyn_share_modified");
+        return st;
+    }
+
+    // one h_share_model evaluation: sums[LIO_SUMS_LEN] (H^T H, H^T h, effct_feat_num, ...)
+    void h_share_model(const lio_state& x, bool converge, double* sums) {
+        const lio_pose p = pose_of(x);
+        check(lio_match(c_, &p, converge ? 1 : 0, sums), "h_share_model");
+    }
+
+    // map_incremental() after the update, with the final state
+    lio_incremental_stats map_incremental(const lio_state& x, double filter_size_map) {
+        const lio_pose p = pose_of(x);
+        lio_incremental_stats st{};
+        check(lio_map_incremental(c_, &p, filter_size_map, &st), "map_incremental");
+        return st;
+    }
+
+    // Nearest_Points ids + sq-distances of the last kNN evaluation (n*5)
+    void nearest_points(std::vector<int32_t>& ids, std::vector<float>& sq_dist, int64_t n) {
+        ids.resize((size_t)n * 5);
+        sq_dist.resize((size_t)n * 5);
+        check(lio_get_knn(c_, ids.data(), sq_dist.data()), "nearest_points");
+    }
+
+    lio_ctx* handle() { return c_; }
+
+private:
+    lio_ctx* c_ = nullptr;
+};
+
+// lasermap_fov_segment(): boxes to pass to Delete_Point_Boxes
+class LocalMap {
+public:
+    std::vector<BoxPointType> segment(const double pos_lid[3], double cube_len = 1000.0, float det_range = 300.f,
+                                      float mov_threshold = 1.5f) {
+        float b[18];
+        int nb = 0;
+        check(lio_localmap_update(&lm_, pos_lid, cube_len, det_range, mov_threshold, b, &nb), "lasermap_fov_segment");
+        std::vector<BoxPointType> out((size_t)nb);
+        for (int i = 0; i < nb; ++i)
+            for (int d = 0; d < 3; ++d) {
+                out[i].vertex_min[d] = b[6 * i + d];
+                out[i].vertex_max[d] = b[6 * i + 3 + d];
+            }
+        return out;
+    }
+    const lio_localmap& state() const { return lm_; }
+
+private:
+    lio_localmap lm_{};
+};
+
+// ---------------------------------------------------------------------------
+// LoopClosure::icpAlignment (loop_closure.cpp:69-92) with the reference's ICP
+// settings (loop_closure.cpp:6-11) and LoopClosureConfig fields.
+struct LoopClosureConfig {  // loop_closure.h:21-29, values from fast_lio_sam.cpp:64-80
+    double icp_max_corr_dist_ = 52.5;
+    double icp_score_threshold_ = 1.5;
+};
+
+struct RegistrationOutput {  // loop_closure.h:31-37
+    bool is_valid_ = false;
+    bool is_converged_ = false;
+    double score_ = 1.7976931348623157e308;
+    double pose_between_eig_[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};  // row-major
+};
+
+class LoopClosureICP {
+public:
+    explicit LoopClosureICP(const LoopClosureConfig& cfg = {}, int device = 0, float cell_size = 2.0f) {
+        lio_icp_params p{cfg.icp_max_corr_dist_, 0.01, 0.01, 50, 0.0, cfg.icp_score_threshold_, cell_size, device};
+        check(lio_icp_create(&p, &h_), "lio_icp_create");
+    }
+    ~LoopClosureICP() { lio_icp_destroy(h_); }
+    LoopClosureICP(const LoopClosureICP&) = delete;
+    LoopClosureICP& operator=(const LoopClosureICP&) = delete;
+
+    template <typename P>
+    RegistrationOutput icpAlignment(const std::vector<P>& src, const std::vector<P>& dst,
+                                    std::vector<float>* aligned_xyz = nullptr) {
+        const std::vector<float> s = packed_xyz(src), d = packed_xyz(dst);
+        check(lio_icp_set_source(h_, s.data(), (int64_t)src.size()), "setInputSource");
+        check(lio_icp_set_target(h_, d.data(), (int64_t)dst.size()), "setInputTarget");
+        if (aligned_xyz) aligned_xyz->resize(s.size());
+        lio_icp_result r{};
+        check(lio_icp_align(h_, nullptr, &r, aligned_xyz ? aligned_xyz->data() : nullptr), "align");
+        RegistrationOutput out;
+        out.score_ = r.score;
+        if (r.is_valid) {
+            out.is_valid_ = out.is_converged_ = true;
+            for (int k = 0; k < 16; ++k) out.pose_between_eig_[k] = r.T[k];
+        }
+        last_ = r;
+        return out;
+    }
+    const lio_icp_result& last() const { return last_; }
+    lio_icp* handle() { return h_; }
+
+private:
+    lio_icp* h_ = nullptr;
+    lio_icp_result last_{};
+};
+
+}  // namespace lio_gpu

@@ -1,0 +1,214 @@
+// C++ drop-in surface (include/lio_gpu.hpp) exercised the way laserMapping.cpp
+// and LoopClosure use the reference classes.  Checks, on one GPU:
+//   * KdTreeGPU::Nearest_Search (batch and single point) against a brute-force
+//     (sq-distance, id) scan — bit-exact ids and distances — before and after
+//     Add_Points / Delete_Point_Boxes;
+//   * ScanMatcherGPU::update_iterated_dyn_share_modified recovers a known pose
+//     offset of a scan of a planar scene; map_incremental grows the map;
+//   * LoopClosureICP::icpAlignment converges on a displaced copy.
+// Built by tests/test_cpp_api.py with g++ -ffp-contract=off (same float
+// operation order as the device distances).  Prints "ALL OK" on success.
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <vector>
+
+#include "lio_gpu.hpp"
+
+struct PointXYZI {  // pcl::PointXYZI's fields
+    float x, y, z, intensity;
+};
+using PointVector = std::vector<PointXYZI>;
+
+static int g_fail = 0;
+#define EXPECT(cond, ...)                          \
+    do {                                           \
+        if (!(cond)) {                             \
+            std::printf("FAIL %s:%d: ", __FILE__, __LINE__); \
+            std::printf(__VA_ARGS__);              \
+            std::printf("\n");                     \
+            ++g_fail;                              \
+        }                                          \
+    } while (0)
+
+static float sqdist(const PointXYZI& a, const float* b) {
+    const float dx = a.x - b[0], dy = a.y - b[1], dz = a.z - b[2];
+    return (dx * dx + dy * dy) + dz * dz;
+}
+
+// k nearest alive points in (d2, id) order within d2 <= bound
+static void brute_knn(const std::vector<float>& xyz, const std::vector<uint8_t>& alive, const PointXYZI& q, int k,
+                      float bound, std::vector<int32_t>& ids, std::vector<float>& d2) {
+    std::vector<std::pair<float, int32_t>> c;
+    for (size_t i = 0; i < alive.size(); ++i) {
+        if (!alive[i]) continue;
+        const float d = sqdist(q, &xyz[3 * i]);
+        if (d <= bound) c.emplace_back(d, (int32_t)i);
+    }
+    const size_t m = std::min<size_t>((size_t)k, c.size());
+    std::partial_sort(c.begin(), c.begin() + m, c.end());
+    ids.assign((size_t)k, -1);
+    d2.assign((size_t)k, INFINITY);
+    for (size_t j = 0; j < m; ++j) {
+        ids[j] = c[j].second;
+        d2[j] = c[j].first;
+    }
+}
+
+// walls of a street canyon + ground + a few boxes: enough planes to constrain 6 DoF
+static PointVector make_scene(int n, std::mt19937& rng) {
+    std::uniform_real_distribution<float> u(-1.f, 1.f);
+    PointVector pts;
+    pts.reserve(n);
+    for (int i = 0; i < n; ++i) {
+        PointXYZI p{0, 0, 0, 1};
+        const int s = i % 6;
+        const float a = 20.f * u(rng), b = 4.f * u(rng) + 4.f;
+        if (s == 0) p = {a, 6.f, b, 1};                                   // left wall
+        else if (s == 1) p = {a, -6.f, b, 1};                             // right wall
+        else if (s == 2) p = {a, 6.f * u(rng), 0.f, 1};                   // ground
+        else if (s == 3) p = {8.f, 2.f * u(rng) + 3.f, 1.5f * u(rng) + 1.5f, 1};  // box face x
+        else if (s == 4) p = {2.f * u(rng) - 5.f, -3.f, 1.5f * u(rng) + 1.5f, 1}; // box face y
+        else p = {2.f * u(rng) - 5.f, 1.f * u(rng) - 2.f, 3.f, 1};       // box top
+        pts.push_back(p);
+    }
+    return pts;
+}
+
+static void check_knn(lio_gpu::KdTreeGPU<PointXYZI>& tree, const PointVector& q, int k, double max_dist) {
+    std::vector<int32_t> ids;
+    std::vector<float> d2;
+    tree.Nearest_Search_Batch(q, k, ids, d2, max_dist);
+    std::vector<float> xyz;
+    std::vector<uint8_t> alive;
+    tree.by_id(xyz, alive);
+    const float bound = std::isinf(max_dist) ? INFINITY : (float)(max_dist * max_dist);
+    int bad = 0;
+    for (size_t i = 0; i < q.size(); ++i) {
+        std::vector<int32_t> bi;
+        std::vector<float> bd;
+        brute_knn(xyz, alive, q[i], k, bound, bi, bd);
+        for (int j = 0; j < k; ++j)
+            if (bi[j] != ids[i * k + j] || !(bd[j] == d2[i * k + j] || (std::isinf(bd[j]) && std::isinf(d2[i * k + j]))))
+                ++bad;
+    }
+    EXPECT(bad == 0, "Nearest_Search k=%d max_dist=%g: %d mismatches", k, max_dist, bad);
+}
+
+int main() {
+    if (lio_device_count() < 1) {
+        std::printf("no GPU\n");
+        return 2;
+    }
+    std::mt19937 rng(7);
+    const PointVector map_pts = make_scene(60000, rng);
+
+    // ---------------------------------------------------------------- ikd-Tree surface
+    lio_gpu::KdTreeGPU<PointXYZI> tree(1.0f, 0.5f);
+    tree.set_downsample_param(0.5f);
+    tree.Build(map_pts);
+    EXPECT(tree.size() == (int)map_pts.size() && tree.validnum() == (int)map_pts.size(), "Build size");
+    std::uniform_real_distribution<float> uq(-25.f, 25.f);
+    PointVector q(800);
+    for (auto& p : q) p = {uq(rng), 0.3f * uq(rng), 0.2f * uq(rng) + 3.f, 0};
+    for (int k : {1, 5}) {
+        check_knn(tree, q, k, INFINITY);
+        check_knn(tree, q, k, std::sqrt(5.0));
+    }
+    // single point, as h_share_model calls it
+    {
+        PointVector near;
+        std::vector<float> dist;
+        tree.Nearest_Search(q[0], 5, near, dist);
+        std::vector<float> xyz;
+        std::vector<uint8_t> alive;
+        tree.by_id(xyz, alive);
+        std::vector<int32_t> bi;
+        std::vector<float> bd;
+        brute_knn(xyz, alive, q[0], 5, INFINITY, bi, bd);
+        bool same = near.size() == 5 && dist.size() == 5;
+        for (size_t j = 0; same && j < 5; ++j)
+            same = near[j].x == xyz[3 * bi[j]] && near[j].y == xyz[3 * bi[j] + 1] && near[j].z == xyz[3 * bi[j] + 2] &&
+                   dist[j] == bd[j];
+        EXPECT(same, "single-point Nearest_Search");
+    }
+    // Add_Points (no downsample) + Delete_Point_Boxes, then kNN again
+    {
+        PointVector extra = make_scene(5000, rng);
+        for (auto& p : extra) p.x += 0.05f;
+        EXPECT(tree.Add_Points(extra, false) == (int)extra.size(), "Add_Points count");
+        std::vector<lio_gpu::BoxPointType> boxes(1);
+        boxes[0] = {{-30.f, -10.f, -1.f}, {0.f, 0.f, 10.f}};
+        const int del = tree.Delete_Point_Boxes(boxes);
+        EXPECT(del > 0 && tree.validnum() == tree.size() - del, "Delete_Point_Boxes");
+        check_knn(tree, q, 5, INFINITY);
+        PointVector flat;
+        tree.flatten(flat);
+        EXPECT((int)flat.size() == tree.validnum(), "flatten");
+    }
+
+    // ------------------------------------------------------------- scan matching
+    {
+        lio_gpu::KdTreeGPU<PointXYZI> map(1.0f, 0.5f);
+        map.Build(map_pts);
+        lio_gpu::ScanMatcherGPU matcher(map);
+        // body-frame scan: a subset of the scene seen from the true pose (yaw 2 deg, t = (0.3, -0.2, 0.05))
+        const double yaw = 2.0 * M_PI / 180.0, c = std::cos(yaw), s = std::sin(yaw);
+        const double t[3] = {0.3, -0.2, 0.05};
+        std::mt19937 r2(11);
+        PointVector world = make_scene(8000, r2), body;
+        for (const auto& w : world) {
+            const double dx = w.x - t[0], dy = w.y - t[1], dz = w.z - t[2];  // R^T (w - t)
+            body.push_back({(float)(c * dx + s * dy), (float)(-s * dx + c * dy), (float)dz, w.intensity});
+        }
+        matcher.set_scan(body);
+        lio_state x{};
+        x.rot[0] = 1.0;
+        x.offset_R_L_I[0] = 1.0;
+        x.grav[2] = -9.809;
+        std::vector<double> P(23 * 23, 0.0);
+        for (int i = 0; i < 23; ++i) P[i * 23 + i] = i < 6 ? 1e-2 : 1e-4;
+        double err = 1e9;
+        for (int it = 0; it < 4 && err > 0.01; ++it) {  // successive scans from the same place
+            const lio_ieskf_stats st = matcher.update_iterated_dyn_share_modified(x, P.data(), 0.001, 3, 0.001);
+            EXPECT(st.n_eff > 1000, "n_eff %d", st.n_eff);
+            err = std::sqrt((x.pos[0] - t[0]) * (x.pos[0] - t[0]) + (x.pos[1] - t[1]) * (x.pos[1] - t[1]) +
+                            (x.pos[2] - t[2]) * (x.pos[2] - t[2]));
+        }
+        const double yaw_est = 2.0 * std::atan2(x.rot[3], x.rot[0]);
+        EXPECT(err < 0.01 && std::fabs(yaw_est - yaw) < 1e-3, "IESKF pose error %.4f m, yaw %.5f vs %.5f", err, yaw_est,
+               yaw);
+        const int before = map.size();
+        const lio_incremental_stats inc = matcher.map_incremental(x, 0.5);
+        EXPECT(map.size() > before, "map_incremental grew the map: %d -> %d", before, map.size());
+        EXPECT(inc.n_to_add + inc.n_no_downsample + inc.n_skipped == (int64_t)body.size(), "map_incremental classes");
+        lio_gpu::LocalMap lm;
+        const double pos_lid[3] = {x.pos[0], x.pos[1], x.pos[2]};
+        const auto boxes = lm.segment(pos_lid, 1000.0, 300.f, 1.5f);
+        EXPECT(boxes.empty() && lm.state().initialized, "lasermap_fov_segment first call");
+    }
+
+    // ---------------------------------------------------------------- loop ICP
+    {
+        std::mt19937 r3(5);
+        const PointVector src = make_scene(40000, r3);
+        PointVector dst;
+        const double a = 1.0 * M_PI / 180.0, c = std::cos(a), s = std::sin(a);
+        for (const auto& p : src)
+            dst.push_back({(float)(c * p.x - s * p.y + 0.05), (float)(s * p.x + c * p.y - 0.03), p.z + 0.02f, p.intensity});
+        lio_gpu::LoopClosureICP icp(lio_gpu::LoopClosureConfig{}, 0);
+        const lio_gpu::RegistrationOutput r = icp.icpAlignment(src, dst);
+        EXPECT(r.is_converged_ && r.is_valid_ && r.score_ < 0.05, "icpAlignment converged=%d score=%g", (int)r.is_converged_,
+               r.score_);
+        EXPECT(std::fabs(r.pose_between_eig_[3]) < 0.2 && std::fabs(r.pose_between_eig_[7]) < 0.2, "icp translation");
+    }
+
+    if (g_fail) {
+        std::printf("%d FAILURES\n", g_fail);
+        return 1;
+    }
+    std::printf("ALL OK\n");
+    return 0;
+}

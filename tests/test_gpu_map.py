@@ -146,3 +146,29 @@ def test_everything_deleted_then_regrown(oracle, scene_scans):
     _same_map(tree, om)
     hm.close()
     _knn_parity(tree, om, scans[2].body)
+
+
+def test_nearest_search_batch(oracle, scene_scans):
+    """ikd-Tree Nearest_Search over a batch (lio_map_nearest_search): k = 1..5,
+    bounded and unbounded, after deletions (tombstoned ids) — ids and
+    sq-distances bit-exact against the oracle, including far-away queries."""
+    _, m, scans = scene_scans
+    base = m[:50000]
+    tree = F.IkdTreeGPU(cell_size=1.0)
+    tree.Build(base)
+    om = oracle.OracleDynMap(base)
+    lo, hi = base.min(0), base.max(0)
+    mid = (lo + hi) / 2
+    box = np.array([[lo[0] - 1, lo[1] - 1, lo[2] - 1, mid[0], mid[1], hi[2] + 1]], np.float32)
+    assert tree.Delete_Point_Boxes(box) == om.delete_boxes(box) > 0
+    rng = np.random.default_rng(3)
+    q = np.concatenate([scans[1].body[::5],
+                        rng.uniform(lo - 20, hi + 20, (3000, 3)).astype(np.float32)]).astype(np.float32)
+    for k in (1, 3, 5):
+        for max_dist in (float("inf"), 2.0, 0.3):
+            gi, gd = tree.Nearest_Search(q, k, max_dist)
+            oi, od = om.knn(q, k, max_dist * max_dist)
+            np.testing.assert_array_equal(gi, oi)
+            np.testing.assert_array_equal(gd, od)
+    gi, _ = tree.Nearest_Search(q, 5)
+    assert np.all(gi[:, 4] >= 0)  # unbounded: always 5 over a 25k-point map
