@@ -163,10 +163,13 @@ def main():
     pos_err = []
     barrier()
     t_start = time.perf_counter()
-    capi_ms = 0.0
+    capi_ms = launch_ms = wait_ms = solve_ms = 0.0
     for k in range(args.steps):
         st = step(k)
         capi_ms += st.wall_ms
+        launch_ms += st.launch_ms
+        wait_ms += st.wait_ms
+        solve_ms += st.solve_ms
         h_evals += st.h_evals
         knn_calls += st.knn_calls
         if k < len(scans):
@@ -349,6 +352,8 @@ def main():
                        "parallelism": f"replicas x{world} (front end does not shard)"},
             "ms_per_ieskf_iteration": round(ms_per_iter, 4),
             "capi_ms_per_scan": round(capi_ms / args.steps, 4),
+            "host_ms_per_scan": {"launch": round(launch_ms / args.steps, 4), "wait": round(wait_ms / args.steps, 4),
+                                 "ieskf_algebra": round(solve_ms / args.steps, 4)},
             "h_evals_per_scan": round(h_evals / args.steps, 3), "knn_evals_per_scan": round(knn_calls / args.steps, 3),
             "pos_err_m": round(float(np.mean(pos_err)), 5) if pos_err else None,
             "map_build_ms": round(build_ms, 2), "input_gen_s": round(gen_s, 1),

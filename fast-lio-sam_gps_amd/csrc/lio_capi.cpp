@@ -92,6 +92,7 @@ static float map_slack(const lio_map* m) { return 64.f * m->grid.geom.cell; }
 
 struct lio_ctx {
     lio_map* map = nullptr;
+    double last_launch_ms = 0.0, last_wait_ms = 0.0;  // host side of the last lio_match
     lio_match_params p{};
     int64_t n = 0, cap = 0;
     float* d_body = nullptr;
@@ -597,14 +598,19 @@ int lio_match(lio_ctx* c, const lio_pose* pose, int redo_knn, double* sums) {
         return LIO_OK;
     }
     a.seq = ++c->seq;
+    const auto t0 = std::chrono::steady_clock::now();
     if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.a, st));
     const int nb = lio::launch_h_model(a, redo_knn != 0, st, c->timing && redo_knn ? c->ev_marks : nullptr);
     if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.b, st));
     lio::launch_finalize(a, nb, st);
     if (c->timing) HIP_TRY(hipEventRecord(c->ev_fin.b, st));
     HIP_TRY(hipGetLastError());
+    const auto t1 = std::chrono::steady_clock::now();
     int rc = wait_result(c, a.seq, sums);
     if (rc) return rc;
+    const auto t2 = std::chrono::steady_clock::now();
+    c->last_launch_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    c->last_wait_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
     if (c->timing) {
         HIP_TRY(hipEventSynchronize(c->ev_fin.b));
         EventPair f{c->ev_main.b, c->ev_fin.b};
@@ -798,6 +804,7 @@ int lio_ieskf_update(lio_ctx* c, lio_state* xs, double* P, const lio_ieskf_param
     lio::host::State x = to_host(*xs);
     lio::host::Mat Pm(P, P + LIO_STATE_DIM * LIO_STATE_DIM);
     int err = LIO_OK;
+    double launch_ms = 0.0, wait_ms = 0.0;
     auto hfn = [&](const lio::host::State& s, bool redo, bool want_rows, lio::host::HModel& hm) -> int {
         if (want_rows) {
             const int64_t want = (int64_t)hm.sums[LIO_SUMS_NEFF];
@@ -814,8 +821,11 @@ int lio_ieskf_update(lio_ctx* c, lio_state* xs, double* P, const lio_ieskf_param
         std::memcpy(pose.t, s.pos, sizeof(pose.t));
         std::memcpy(pose.t_LI, s.offT, sizeof(pose.t_LI));
         hm.rows.clear();
+        c->last_launch_ms = c->last_wait_ms = 0.0;
         int rc = lio_match(c, &pose, redo ? 1 : 0, hm.sums);
         if (rc) return err = rc;
+        launch_ms += c->last_launch_ms;
+        wait_ms += c->last_wait_ms;
         return 0;
     };
     lio::host::IeskfResult r;
@@ -831,6 +841,8 @@ int lio_ieskf_update(lio_ctx* c, lio_state* xs, double* P, const lio_ieskf_param
         st->res_mean = r.res_mean;
         st->solve_ms = r.solve_ms;
         st->wall_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_call).count();
+        st->launch_ms = launch_ms;
+        st->wait_ms = wait_ms;
     }
     return LIO_OK;
 }

@@ -72,7 +72,8 @@ class IeskfParams(C.Structure):
 
 class IeskfStats(C.Structure):
     _fields_ = [("h_evals", C.c_int), ("knn_calls", C.c_int), ("converged", C.c_int), ("n_eff", C.c_int),
-                ("res_mean", C.c_double), ("solve_ms", C.c_double), ("wall_ms", C.c_double)]
+                ("res_mean", C.c_double), ("solve_ms", C.c_double), ("wall_ms", C.c_double),
+                ("launch_ms", C.c_double), ("wait_ms", C.c_double)]
 
 
 class IcpParams(C.Structure):

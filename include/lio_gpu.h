@@ -190,6 +190,8 @@ typedef struct lio_ieskf_stats {
     double res_mean;/* res_mean_last                                     */
     double solve_ms;/* host time in the 23-dim algebra                   */
     double wall_ms; /* host wall time of the whole call                  */
+    double launch_ms;/* host time enqueueing the evaluations' kernels     */
+    double wait_ms; /* host time waiting for the evaluations' results    */
 } lio_ieskf_stats;
 
 /* esekf::update_iterated_dyn_share_modified(R, solve_time) [U IKFoM];
