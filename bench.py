@@ -75,15 +75,24 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # LIO_BENCH_REHEARSE=1: every rank on device 0 with gloo collectives (CPU tensors), to rehearse
+    # the multi-rank path on a one-GPU box; the driver's N-GPU runs use one device per rank over RCCL
+    rehearse = os.environ.get("LIO_BENCH_REHEARSE") == "1"
+    if rehearse:
+        local = 0
     dist = None
     if world > 1:
         import torch.distributed as dist
 
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    coll_dev = torch.device("cpu") if rehearse else dev  # tensors handed to collectives
 
     from lio_gpu import frontend as F
     from lio_gpu import loop_closure as LC
@@ -185,7 +194,7 @@ def main():
     hm.set_timing(False)
     tm = hm.timing()
     if dist is not None:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     total_scans = args.steps * world
@@ -274,7 +283,7 @@ def main():
         if world > 1:
             from lio_gpu import dist as ldist
 
-            cb = ldist.make_allgather(device=dev)
+            cb = ldist.make_allgather(device=coll_dev)
             lc.set_shard(rank, world, cb)
         lc.setInputSource(src)
         lc.setInputTarget(dst)
@@ -289,7 +298,7 @@ def main():
         barrier()
         icp_s = time.perf_counter() - ti
         if dist is not None:
-            t = torch.tensor([icp_s], dtype=torch.float64, device=dev)
+            t = torch.tensor([icp_s], dtype=torch.float64, device=coll_dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             icp_s = float(t.item())
         itm = lc.timing()

@@ -37,6 +37,8 @@ for s in $STEPS; do
     c3)    run bench_c3 600 python bench.py --config C3 --steps 60 --warmup 5 --no-icp --cpu-seconds 4 --pipeline 12 ;;
     ppprof) run rocprof_pipeline 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/ppprof" -o run \
                --output-format csv -- python bench.py --config C3 --steps 5 --warmup 2 --no-icp --no-cpu --pipeline 12 ;;
+    rehearse) LIO_BENCH_REHEARSE=1 run rehearse2 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+               --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 100 --warmup 10 --icp-reps 2 ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
                -- python bench.py --steps 100 --warmup 10 --no-cpu --icp-reps 3 ;;
     pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv \
