@@ -123,6 +123,29 @@ def test_ieskf_update_matches_oracle(oracle, c1):
         assert np.linalg.norm(xg["pos"] - sc.pos_gt) < 0.2 * np.linalg.norm(sc.pos_init - sc.pos_gt)
 
 
+@pytest.mark.parametrize("cfg", ["C2", "C3"])
+def test_ieskf_update_full_size(oracle, cfg):
+    """Whole update_iterated_dyn_share_modified at BASELINE sizes: same evaluation / kNN counts and
+    effective points as the oracle, state and covariance within the north_star tolerance."""
+    _, m, scans = synth.make_config(cfg, n_scans=2)
+    om = oracle.OracleMap(m)
+    tree = F.IkdTreeGPU()
+    tree.Build(m)
+    hm = F.HShareModelGPU(tree)
+    kf = F.EsekfGPU(hm)
+    for sc in scans:
+        hm.set_scan(sc.body)
+        st = synth.initial_state(sc.pos_init, sc.rot_init)
+        P0 = synth.initial_cov()
+        xg, Pg, sg = kf.update_iterated_dyn_share_modified(st, P0)
+        xo, Po, so, _ = oracle.ieskf_update(om, sc.body, st, P0)
+        assert sg["h_evals"] == int(so[0]) and sg["knn_calls"] == int(so[1])
+        assert sg["n_eff"] == int(so[3])
+        np.testing.assert_allclose(xg["pos"], xo["pos"], atol=1e-5)
+        np.testing.assert_allclose(xg["rot"], xo["rot"], atol=1e-5)
+        np.testing.assert_allclose(Pg, Po, rtol=1e-5, atol=1e-10)
+
+
 def test_edge_cases(oracle):
     rng = np.random.default_rng(5)
     # tiny map with duplicates (ties broken by id) and sparse areas (< 5 neighbours)
@@ -178,8 +201,10 @@ def test_no_effective_points_and_small_dof_branch(oracle):
         np.testing.assert_allclose(Pg, Po, rtol=1e-6, atol=1e-12)
 
 
-@pytest.mark.parametrize("cfg", ["C2"])
-def test_knn_full_size_c2(oracle, cfg):
+@pytest.mark.parametrize("cfg", ["C2", "C3", "C5"])
+def test_knn_full_size(oracle, cfg):
+    """BASELINE.json's full sizes (C2 65k/1M, C3 131k/5M, C5 120k/10M): Nearest_Points ids and
+    point_selected_surf bit-exact, H^T H / H^T h sums within the double-order tolerance."""
     scene, m, scans = synth.make_config(cfg, n_scans=1)
     sc = scans[0]
     tree = F.IkdTreeGPU()
