@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--no-icp", action="store_true")
     ap.add_argument("--icp-reps", type=int, default=5)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--streams", default="2,8",
+                    help="secondary figure: S independent scan streams (own map + ctx + HIP stream each) "
+                         "driven by S host threads in this process; '' to skip (reported under 'multi_stream')")
     ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline sample at all cores "
                     "(plus half of it at 1 and at 3 threads)")
     ap.add_argument("--pipeline", type=int, default=0, metavar="N",
@@ -274,6 +277,49 @@ def main():
                     "pos_err_m": round(float(np.mean(errs)), 4) if errs else None,
                     "note": "raw float records uploaded from host per scan (PCIe included)"}
 
+    # ------------------------------------------------- several scan streams on one GPU (secondary)
+    # One stream is latency-bound (host round trip per h-evaluation); independent sensors / robots
+    # can share the card. Each stream: its own map replica, ctx and HIP stream, one host thread.
+    multi = None
+    if args.streams and rank == 0:
+        import threading
+
+        multi = []
+        for S in [int(v) for v in args.streams.split(",") if v.strip()]:
+            sess = []
+            for _ in range(S):
+                t_s = F.IkdTreeGPU(cell_size=args.cell, device=local)
+                t_s.Build_device(d_map.data_ptr(), len(mappts))
+                h_s = F.HShareModelGPU(t_s)
+                k_s = F.EsekfGPU(h_s, laser_point_cov=0.001, max_iteration=3, epsi=0.001)
+                sess.append((t_s, h_s, k_s, type(init_c[0])(), np.empty((23, 23)), type(F._capi.IeskfStats())()))
+
+            def run(si, n):
+                _, h_s, k_s, x_s, p_s, st_s = sess[si]
+                for k in range(n):
+                    j = (k + si) % len(scans)
+                    h_s.bind_scan_device(*ptrs[j])
+                    ctypes.pointer(x_s)[0] = init_c[j]
+                    np.copyto(p_s, P0)
+                    k_s.update_raw(x_s, p_s, st_s)
+
+            n_per = max(args.steps, 50)
+            for si in range(S):
+                run(si, 5)  # warm-up
+            torch.cuda.synchronize()
+            th = [threading.Thread(target=run, args=(si, n_per)) for si in range(S)]
+            tm0 = time.perf_counter()
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            torch.cuda.synchronize()
+            dt = time.perf_counter() - tm0
+            multi.append({"streams": S, "scans_per_s": round(S * n_per / dt, 1), "scans_per_stream": n_per})
+            for t_s, h_s, k_s, *_ in sess:
+                h_s.close()
+            del sess
+
     # ------------------------------------------------------------- loop ICP (sharded)
     loop_icp = None
     if not args.no_icp:
@@ -366,7 +412,7 @@ def main():
             "h_evals_per_scan": round(h_evals / args.steps, 3), "knn_evals_per_scan": round(knn_calls / args.steps, 3),
             "pos_err_m": round(float(np.mean(pos_err)), 5) if pos_err else None,
             "map_build_ms": round(build_ms, 2), "input_gen_s": round(gen_s, 1),
-            "roofline": roofline, "cpu_baseline": cpu, "loop_icp": loop_icp, "map_incremental": incr, "pipeline": pipeline,
+            "roofline": roofline, "cpu_baseline": cpu, "loop_icp": loop_icp, "multi_stream": multi, "map_incremental": incr, "pipeline": pipeline,
         }
         print(json.dumps(line), flush=True)
     if dist is not None:
