@@ -10,6 +10,9 @@
 //       + map_incremental() + lasermap_fov_segment() [U]
 //   * LoopClosureICP          ~ LoopClosure::icpAlignment
 //       (fast_lio_sam/src/loop_closure.cpp:69-92, loop_closure.h:31-37)
+//   * VoxelGrid<PointT>, submap_voxelize, preprocess_scan, savePCDFileBinary,
+//     loadPCDFile ~ pcl::VoxelGrid, setSrcAndDstCloud's transformPcd +
+//     voxelizePcd, Preprocess + UndistortPcl, pcl::io PCD I/O
 // PointType is any struct with float members x, y, z (pcl::PointXYZI,
 // pcl::PointXYZINormal, ...).  Errors throw lio_gpu::Error carrying
 // lio_last_error(); there is no CPU fallback behind any call.
@@ -48,6 +51,15 @@ std::vector<float> packed_xyz(const std::vector<P>& pts) {
         xyz[3 * i + 2] = pts[i].z;
     }
     return xyz;
+}
+
+// floats per record of a POD point type: 3..8 floats, x, y, z first
+template <typename PointT>
+constexpr int float_stride() {
+    static_assert(sizeof(PointT) % sizeof(float) == 0 && sizeof(PointT) >= 3 * sizeof(float) &&
+                      sizeof(PointT) <= 8 * sizeof(float),
+                  "PointT must be 3..8 floats (x, y, z first)");
+    return (int)(sizeof(PointT) / sizeof(float));
 }
 
 // Eigen::Quaterniond::toRotationMatrix for (w, x, y, z), row-major
@@ -216,6 +228,18 @@ public:
         check(lio_scan_set(c_, xyz.data(), (int64_t)feats_down_body.size()), "set_scan");
     }
 
+    // raw scan -> Preprocess + UndistortPcl + downSizeFilterSurf -> feats_down_body on the device
+    template <typename PointT>
+    int64_t set_scan_raw(const std::vector<PointT>& raw, const lio_scan_prep_params& params,
+                         const std::vector<lio_imu_pose>& imu_poses, const lio_state& end_state) {
+        const lio_pose end = pose_of(end_state);
+        int64_t n = 0;
+        check(lio_scan_preprocess(c_, reinterpret_cast<const float*>(raw.data()), (int64_t)raw.size(),
+                                  float_stride<PointT>(), &params, imu_poses.data(), (int)imu_poses.size(), &end, &n),
+              "set_scan_raw");
+        return n;
+    }
+
     // kf.update_iterated_dyn_share_modified(LASER_POINT_COV, solve_H_time): x, P (23x23 row-major) in place
     lio_ieskf_stats update_iterated_dyn_share_modified(lio_state& x, double* P, double laser_point_cov = 0.001,
                                                        int max_iteration = 3, double epsi = 0.001) {
@@ -273,6 +297,110 @@ public:
 private:
     lio_localmap lm_{};
 };
+
+// ---------------------------------------------------------------------------
+// Filters and formats.  PointT: a POD of 3..8 floats starting with x, y, z
+// (every float field is averaged / carried, as PCL does with downsample_all_data_).
+class FilterGPU {  // device + scratch shared by the filters below
+public:
+    explicit FilterGPU(int device = 0) { check(lio_filter_create(device, &f_), "lio_filter_create"); }
+    ~FilterGPU() { lio_filter_destroy(f_); }
+    FilterGPU(const FilterGPU&) = delete;
+    FilterGPU& operator=(const FilterGPU&) = delete;
+    lio_filter* handle() { return f_; }
+
+private:
+    lio_filter* f_ = nullptr;
+};
+
+// pcl::VoxelGrid<PointT>: setLeafSize / setInputCloud / filter (FAST-LIO downSizeFilterSurf,
+// utilities.hpp voxelizePcd)
+template <typename PointT>
+class VoxelGrid {
+public:
+    explicit VoxelGrid(FilterGPU& f) : f_(f) {}
+    void setLeafSize(float lx, float ly, float lz) { leaf_[0] = lx, leaf_[1] = ly, leaf_[2] = lz; }
+    void setInputCloud(const std::vector<PointT>* cloud) { in_ = cloud; }
+    void filter(std::vector<PointT>& out) {
+        if (!in_) throw Error(LIO_ERR_ARG, "VoxelGrid: no input cloud");
+        out.resize(in_->size());
+        int64_t n = 0;
+        check(lio_voxel_grid(f_.handle(), reinterpret_cast<const float*>(in_->data()), (int64_t)in_->size(),
+                             float_stride<PointT>(), leaf_, reinterpret_cast<float*>(out.data()), &n),
+              "VoxelGrid::filter");
+        out.resize((size_t)n);
+    }
+
+private:
+    FilterGPU& f_;
+    const std::vector<PointT>* in_ = nullptr;
+    float leaf_[3] = {0.5f, 0.5f, 0.5f};
+};
+
+// one side of LoopClosure::setSrcAndDstCloud (loop_closure.cpp:42-67): transformPcd of each
+// keyframe cloud by its corrected pose (row-major double 4x4), concatenated, voxelizePcd
+template <typename PointT>
+std::vector<PointT> submap_voxelize(FilterGPU& f, const std::vector<const std::vector<PointT>*>& clouds,
+                                    const std::vector<const double*>& poses16, float voxel_res) {
+    if (clouds.size() != poses16.size()) throw Error(LIO_ERR_ARG, "submap_voxelize: clouds / poses mismatch");
+    std::vector<PointT> all;
+    std::vector<int64_t> off{0};
+    std::vector<double> T;
+    for (size_t k = 0; k < clouds.size(); ++k) {
+        all.insert(all.end(), clouds[k]->begin(), clouds[k]->end());
+        off.push_back((int64_t)all.size());
+        T.insert(T.end(), poses16[k], poses16[k] + 16);
+    }
+    std::vector<PointT> out(all.size());
+    int64_t n = 0;
+    check(lio_submap_voxelize(f.handle(), reinterpret_cast<const float*>(all.data()), off.data(), (int)clouds.size(),
+                              float_stride<PointT>(), T.data(), voxel_res, reinterpret_cast<float*>(out.data()), &n),
+          "submap_voxelize");
+    out.resize((size_t)n);
+    return out;
+}
+
+// Preprocess + UndistortPcl + downSizeFilterSurf of one raw scan; the record's time offset [ms]
+// sits at float index params.time_field (FAST-LIO keeps it in `curvature`)
+template <typename PointT>
+std::vector<PointT> preprocess_scan(FilterGPU& f, const std::vector<PointT>& raw, const lio_scan_prep_params& params,
+                                    const std::vector<lio_imu_pose>& imu_poses, const lio_state& end_state) {
+    const lio_pose end = pose_of(end_state);
+    std::vector<PointT> out(raw.size());
+    int64_t n = 0;
+    check(lio_preprocess(f.handle(), reinterpret_cast<const float*>(raw.data()), (int64_t)raw.size(),
+                         float_stride<PointT>(), &params, imu_poses.data(), (int)imu_poses.size(), &end,
+                         reinterpret_cast<float*>(out.data()), &n),
+          "preprocess_scan");
+    out.resize((size_t)n);
+    return out;
+}
+
+// pcl::io::savePCDFileBinary of the float fields `names` (one per float of PointT)
+template <typename PointT>
+void savePCDFileBinary(const std::string& path, const std::vector<PointT>& cloud, const std::vector<std::string>& names) {
+    if ((int)names.size() != float_stride<PointT>()) throw Error(LIO_ERR_ARG, "savePCDFileBinary: one name per field");
+    std::vector<const char*> nm;
+    for (const auto& s : names) nm.push_back(s.c_str());
+    check(lio_pcd_write_binary(path.c_str(), reinterpret_cast<const float*>(cloud.data()), (int64_t)cloud.size(),
+                               float_stride<PointT>(), nm.data()),
+          "savePCDFileBinary");
+}
+
+// PCD reader (ascii / binary): the fields `names`, in order, into PointT (absent fields read 0)
+template <typename PointT>
+std::vector<PointT> loadPCDFile(FilterGPU& f, const std::string& path, const std::vector<std::string>& names) {
+    if ((int)names.size() != float_stride<PointT>()) throw Error(LIO_ERR_ARG, "loadPCDFile: one name per field");
+    std::vector<const char*> nm;
+    for (const auto& s : names) nm.push_back(s.c_str());
+    int64_t n = 0;
+    check(lio_pcd_read(f.handle(), path.c_str(), nm.data(), (int)nm.size(), nullptr, 0, &n), "loadPCDFile");
+    std::vector<PointT> out((size_t)n);
+    check(lio_pcd_read(f.handle(), path.c_str(), nm.data(), (int)nm.size(), reinterpret_cast<float*>(out.data()), n,
+                       &n),
+          "loadPCDFile");
+    return out;
+}
 
 // ---------------------------------------------------------------------------
 // LoopClosure::icpAlignment (loop_closure.cpp:69-92) with the reference's ICP

@@ -97,6 +97,51 @@ static void check_knn(lio_gpu::KdTreeGPU<PointXYZI>& tree, const PointVector& q,
     EXPECT(bad == 0, "Nearest_Search k=%d max_dist=%g: %d mismatches", k, max_dist, bad);
 }
 
+// pcl::VoxelGrid (PCL 1.10 applyFilter) restated on the host: voxel index from floor(p / leaf)
+// relative to the min voxel, stable order inside a voxel, fields summed in input order (float)
+static PointVector brute_voxel(const PointVector& in, float leaf) {
+    const float inv = 1.0f / leaf;
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (const auto& p : in) {
+        const float v[3] = {p.x, p.y, p.z};
+        for (int d = 0; d < 3; ++d) lo[d] = std::min(lo[d], v[d]), hi[d] = std::max(hi[d], v[d]);
+    }
+    long long mn[3], dv[3];
+    for (int d = 0; d < 3; ++d) {
+        mn[d] = (long long)std::floor(lo[d] * inv);
+        dv[d] = (long long)std::floor(hi[d] * inv) - mn[d] + 1;
+    }
+    std::vector<std::pair<long long, size_t>> key;
+    for (size_t i = 0; i < in.size(); ++i) {
+        const float v[3] = {in[i].x, in[i].y, in[i].z};
+        long long ijk[3];
+        for (int d = 0; d < 3; ++d) ijk[d] = (long long)(std::floor(v[d] * inv) - (float)mn[d]);
+        key.emplace_back(ijk[0] + ijk[1] * dv[0] + ijk[2] * dv[0] * dv[1], i);
+    }
+    std::stable_sort(key.begin(), key.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    PointVector out;
+    for (size_t j = 0; j < key.size();) {
+        size_t e = j;
+        PointXYZI acc{0, 0, 0, 0};
+        while (e < key.size() && key[e].first == key[j].first) {
+            const PointXYZI& q = in[key[e].second];
+            acc.x += q.x, acc.y += q.y, acc.z += q.z, acc.intensity += q.intensity;
+            ++e;
+        }
+        const float c = (float)(e - j);
+        out.push_back({acc.x / c, acc.y / c, acc.z / c, acc.intensity / c});
+        j = e;
+    }
+    return out;
+}
+
+static bool same_cloud(const PointVector& a, const PointVector& b) {
+    if (a.size() != b.size()) return false;
+    for (size_t i = 0; i < a.size(); ++i)
+        if (a[i].x != b[i].x || a[i].y != b[i].y || a[i].z != b[i].z || a[i].intensity != b[i].intensity) return false;
+    return true;
+}
+
 int main() {
     if (lio_device_count() < 1) {
         std::printf("no GPU\n");
@@ -188,6 +233,41 @@ int main() {
         const double pos_lid[3] = {x.pos[0], x.pos[1], x.pos[2]};
         const auto boxes = lm.segment(pos_lid, 1000.0, 300.f, 1.5f);
         EXPECT(boxes.empty() && lm.state().initialized, "lasermap_fov_segment first call");
+    }
+
+    // ---------------------------------------------------------------- filters / formats
+    {
+        lio_gpu::FilterGPU filt;
+        std::mt19937 r4(3);
+        PointVector cloud = make_scene(30000, r4);
+        std::uniform_real_distribution<float> ui(0.f, 255.f);
+        for (auto& p : cloud) p.intensity = ui(r4);
+        lio_gpu::VoxelGrid<PointXYZI> vg(filt);
+        vg.setLeafSize(0.5f, 0.5f, 0.5f);
+        vg.setInputCloud(&cloud);
+        PointVector down;
+        vg.filter(down);
+        EXPECT(same_cloud(down, brute_voxel(cloud, 0.5f)), "VoxelGrid bit-exact (%zu points)", down.size());
+        // setSrcAndDstCloud side: two keyframes through transformPcd (double 4x4) + voxelizePcd
+        const double T0[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+        const double c = std::cos(0.3), s = std::sin(0.3);
+        const double T1[16] = {c, -s, 0, 2.5, s, c, 0, -1.0, 0, 0, 1, 0.2, 0, 0, 0, 1};
+        PointVector half(cloud.begin(), cloud.begin() + 15000), rest(cloud.begin() + 15000, cloud.end());
+        const PointVector sub = lio_gpu::submap_voxelize<PointXYZI>(filt, {&half, &rest}, {T0, T1}, 0.3f);
+        PointVector tf = half;
+        for (const auto& p : rest) {
+            const double x = p.x, y = p.y, z = p.z;
+            tf.push_back({(float)(((T1[0] * x + T1[1] * y) + T1[2] * z) + T1[3]),
+                          (float)(((T1[4] * x + T1[5] * y) + T1[6] * z) + T1[7]),
+                          (float)(((T1[8] * x + T1[9] * y) + T1[10] * z) + T1[11]), p.intensity});
+        }
+        EXPECT(same_cloud(sub, brute_voxel(tf, 0.3f)), "submap_voxelize bit-exact");
+        // PCD round trip
+        const std::string path = "/tmp/lio_cpp_api_test.pcd";
+        lio_gpu::savePCDFileBinary(path, down, {"x", "y", "z", "intensity"});
+        const PointVector back = lio_gpu::loadPCDFile<PointXYZI>(filt, path, {"x", "y", "z", "intensity"});
+        EXPECT(same_cloud(back, down), "PCD binary round trip");
+        std::remove(path.c_str());
     }
 
     // ---------------------------------------------------------------- loop ICP
