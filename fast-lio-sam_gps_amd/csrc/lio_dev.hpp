@@ -425,18 +425,25 @@ __device__ __forceinline__ void scan_shell1_flat(const GridDev& g, float qx, flo
 
 // Lean group walk for dense maps (front-end kNN, ICP near pass), written for
 // occupancy (no per-lane arrays): the own cell lane-strided by the whole group,
-// merge; then lane `sub` takes the shell-1 cells k = sub, sub+G, ... of the
-// 3x3x3 block, pruned against its own (tightening) K-th best and scanned
-// sequentially; merge.  Shells >= 2 (sparse neighbourhoods) continue with the
-// generic walk.  Same result contract as group_knn_exact_from.
-template <int K, int G>
+// merge; then the shell-1 cells of the 3x3x3 block (ranges loaded during the
+// own-cell scan) pruned against the merged K-th best, concatenated through the
+// group's LDS slot table and strided by the lanes (scan_shell1_flat); merge.
+// Shells >= 2 (sparse neighbourhoods) continue with the generic walk, or are
+// left to the far pass when max_shell < 2.  Same result contract as
+// group_knn_exact_from.  TAIL = false (front-end near pass): no generic walk
+// at all — queries outside the grid or unresolved after shell 1 return false
+// with their partial list and go to the far pass.
+template <int K, int G, bool TAIL = true>
 __device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, int max_shell, int sub, TopK<K>& tk,
-                               SearchStats* dbg = nullptr, uint32_t* lds = nullptr) {
+                               SearchStats* dbg, uint32_t* lds) {
     const int cx = cell_coord(qx, g.ox, g.inv_cell);
     const int cy = cell_coord(qy, g.oy, g.inv_cell);
     const int cz = cell_coord(qz, g.oz, g.inv_cell);
     const bool inside = (unsigned)cx < (unsigned)g.nx && (unsigned)cy < (unsigned)g.ny && (unsigned)cz < (unsigned)g.nz;
-    if (!inside || max_shell < 1) return group_knn_exact_from<K, G>(g, qx, qy, qz, 0, max_shell, sub, tk);
+    if (!inside || max_shell < 1) {
+        if constexpr (TAIL) return group_knn_exact_from<K, G>(g, qx, qy, qz, 0, max_shell, sub, tk);
+        return false;
+    }
     const float cs = g.cell, m = g.margin;
     const float lox = g.ox + (float)cx * cs, loy = g.oy + (float)cy * cs, loz = g.oz + (float)cz * cs;
     float own = fminf(fminf(qx - lox, lox + cs - qx), fminf(qy - loy, loy + cs - qy));
@@ -444,7 +451,7 @@ __device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, i
     const uint32_t nx = (uint32_t)g.nx, nxy = (uint32_t)g.nx * (uint32_t)g.ny;
     const uint32_t c0 = (uint32_t)cz * nxy + (uint32_t)cy * nx + (uint32_t)cx;
     uint32_t b4[shell1_cpl<G>()], n4[shell1_cpl<G>()];
-    if (lds) shell1_ranges<G>(g, cx, cy, cz, sub, b4, n4);  // in flight during the own-cell scan
+    shell1_ranges<G>(g, cx, cy, cz, sub, b4, n4);  // in flight during the own-cell scan
     scan_cell_group2<K, G>(g, c0, qx, qy, qz, sub, tk);
     group_merge<K, G>(tk);
     if (dbg) dbg->shell = 0;
@@ -452,28 +459,12 @@ __device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, i
     if (sub != 0) {  // re-seed non-leader lanes (see group_knn_exact_from)
         tk.fill_with_worst();
     }
-    if (lds) {
-        scan_shell1_flat<K, G>(g, qx, qy, qz, cx, cy, cz, lox, loy, loz, sub, lds, b4, n4, tk, dbg);
-    } else {
-        for (int k = sub; k < 27; k += G) {
-            if (k == 13) continue;  // own cell
-            const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
-            const int x = cx + dx, y = cy + dy, z = cz + dz;
-            if ((unsigned)x >= nx || (unsigned)y >= (unsigned)g.ny || (unsigned)z >= (unsigned)g.nz) continue;
-            const float xl = lox + (float)dx * cs - m, yl = loy + (float)dy * cs - m, zl = loz + (float)dz * cs - m;
-            const float w = cs + 2.f * m;
-            const float bd = (axis_gap(qx, xl, xl + w) + axis_gap(qy, yl, yl + w)) + axis_gap(qz, zl, zl + w);
-            if (bd * 0.999999f > tk.worst()) continue;
-            const uint32_t c = (uint32_t)((int)c0 + dz * (int)nxy + dy * (int)nx + dx);
-            if (dbg) dbg->cells += 1;
-            scan_cell_seq<K>(g, c, qx, qy, qz, tk);
-        }
-    }
+    scan_shell1_flat<K, G>(g, qx, qy, qz, cx, cy, cz, lox, loy, loz, sub, lds, b4, n4, tk, dbg);
     group_merge<K, G>(tk);
     if (dbg) dbg->shell = 1;
     const float gr = own + cs;
     if (gr > 0.f && tk.worst() < gr * gr * 0.999999f) return true;
-    if (max_shell < 2) return false;
+    if (!TAIL || max_shell < 2) return false;
     if (dbg) dbg->shell = 2;
     return group_knn_exact_from<K, G>(g, qx, qy, qz, 2, max_shell, sub, tk);
 }
@@ -497,6 +488,8 @@ __device__ void block_knn_box_flat(const GridDev& g, float qx, float qy, float q
     const int cx = cell_coord(qx, g.ox, g.inv_cell);
     const int cy = cell_coord(qy, g.oy, g.inv_cell);
     const int cz = cell_coord(qz, g.oz, g.inv_cell);
+    // the near pass covered the 3x3x3 block only for queries whose cell lies in the grid
+    const bool near_done = (unsigned)cx < (unsigned)g.nx && (unsigned)cy < (unsigned)g.ny && (unsigned)cz < (unsigned)g.nz;
     const float r = sqrtf(tk.worst()) + 2.f * g.margin;
     const int x0 = max(cell_coord(qx - r, g.ox, g.inv_cell), 0), x1 = min(cell_coord(qx + r, g.ox, g.inv_cell), g.nx - 1);
     const int y0 = max(cell_coord(qy - r, g.oy, g.inv_cell), 0), y1 = min(cell_coord(qy + r, g.oy, g.inv_cell), g.ny - 1);
@@ -512,7 +505,7 @@ __device__ void block_knn_box_flat(const GridDev& g, float qx, float qy, float q
         if (k < nbox) {
             const int z = z0 + k / wxy, kk = k % wxy;
             const int y = y0 + kk / wx, x = x0 + kk % wx;
-            if (!(abs(x - cx) <= 1 && abs(y - cy) <= 1 && abs(z - cz) <= 1)) {  // block: near pass
+            if (!(near_done && abs(x - cx) <= 1 && abs(y - cy) <= 1 && abs(z - cz) <= 1)) {  // block: near pass
                 const float xl = g.ox + (float)x * cs - m, yl = g.oy + (float)y * cs - m, zl = g.oz + (float)z * cs - m;
                 const float bd = (axis_gap(qx, xl, xl + w) + axis_gap(qy, yl, yl + w)) + axis_gap(qz, zl, zl + w);
                 if (!(bd * 0.999999f > bound)) {

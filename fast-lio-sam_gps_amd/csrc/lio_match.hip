@@ -107,7 +107,7 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
     TopK<5> tk;
     tk.init(a.range_sq);
     SearchStats st{0, 0, 0};
-    const bool done = group_knn_near<5, G>(a.grid, wx, wy, wz, min(a.max_shell, 1), sub, tk, DBG ? &st : nullptr,
+    const bool done = group_knn_near<5, G, false>(a.grid, wx, wy, wz, 1, sub, tk, DBG ? &st : nullptr,
                                                 s_tab[threadIdx.x / G]);
     const bool far = !done && a.max_shell > 1;
     if constexpr (DBG) {

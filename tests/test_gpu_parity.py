@@ -146,6 +146,36 @@ def test_ieskf_update_full_size(oracle, cfg):
         np.testing.assert_allclose(Pg, Po, rtol=1e-5, atol=1e-10)
 
 
+def test_queries_just_outside_the_grid(oracle):
+    """Scan points whose cell lies outside the map grid but within the kNN range of its faces:
+    the near pass hands them to the far pass, which must search the whole box (the near pass
+    scanned nothing for them). Nearest_Points bit-exact against the oracle."""
+    rng = np.random.default_rng(8)
+    m = rng.uniform(0.0, 10.0, (60000, 3)).astype(np.float32)
+    tree = F.IkdTreeGPU(cell_size=1.0)
+    tree.Build(m)
+    om = oracle.OracleMap(m)
+    q = rng.uniform(0.0, 10.0, (6000, 3))
+    axis = rng.integers(0, 3, len(q))
+    side = rng.integers(0, 2, len(q))
+    off = rng.uniform(0.05, 2.5, len(q))
+    q[np.arange(len(q)), axis] = np.where(side == 1, 10.0 + off, -off)
+    body = (q - synth.T_LI).astype(np.float32)  # identity pose: world = body + t_LI
+    hm = F.HShareModelGPU(tree)
+    hm.set_scan(body)
+    p24 = np.zeros(24)
+    p24[0:9] = np.eye(3).ravel()
+    p24[12:21] = np.eye(3).ravel()
+    p24[21:24] = synth.T_LI
+    g = hm(p24, True)
+    o, nn, sel, _ = _oracle_eval(oracle, om, body, p24)
+    gi, _ = hm.nearest_points()
+    np.testing.assert_array_equal(gi, nn)
+    np.testing.assert_array_equal(hm.normvec()[1], sel)
+    _check_sums(g, o)
+    assert (gi[:, 4] >= 0).sum() > len(q) // 2 and (gi[:, 0] < 0).sum() > 0  # both kinds present
+
+
 def test_edge_cases(oracle):
     rng = np.random.default_rng(5)
     # tiny map with duplicates (ties broken by id) and sparse areas (< 5 neighbours)
