@@ -93,9 +93,10 @@ __device__ __forceinline__ bool residual_row(const MatchArgs& a, float bx, float
 // neighbourhoods, ~0.4% of a dense scan) are queued, with their list, for
 // the wave-per-query far pass instead of holding their wave: a kernel runs as
 // long as its slowest wave.  Written for 8 waves/SIMD (<= 64 VGPRs).
-template <bool DBG, int G = kGroup>
+template <bool DBG>
 __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) knn_near_kernel(MatchArgs a) {
-    constexpr int QPB = kKnnBlock / G;  // 64 queries per block at G = 8
+    constexpr int G = kGroup;
+    constexpr int QPB = kKnnBlock / G;  // 64 queries per block
     __shared__ uint32_t s_tab[QPB][72];      // per-group shell-1 slot table
     const int blk = xcd_block(blockIdx.x, gridDim.x);
     const int sub = threadIdx.x % G;
@@ -397,19 +398,9 @@ int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* ma
     if (a.n == 0) return 0;
     const int nb = (a.n + kBlock - 1) / kBlock;
     if (redo) {
-        static const int group = [] {  // LIO_KNN_GROUP: diagnostics override of the lanes per query
-            const char* e = std::getenv("LIO_KNN_GROUP");
-            const int v = e ? std::atoi(e) : kGroup;
-            return (v == 4 || v == 16) ? v : kGroup;
-        }();
-        const int qpb = kKnnBlock / group;
-        const int nq = (a.n + qpb - 1) / qpb;
+        const int nq = (a.n + kKnnBlock / kGroup - 1) / (kKnnBlock / kGroup);
         if (a.dbg)
-            knn_near_kernel<true><<<(a.n + kKnnBlock / kGroup - 1) / (kKnnBlock / kGroup), kKnnBlock, 0, st>>>(a);
-        else if (group == 4)
-            knn_near_kernel<false, 4><<<nq, kKnnBlock, 0, st>>>(a);
-        else if (group == 16)
-            knn_near_kernel<false, 16><<<nq, kKnnBlock, 0, st>>>(a);
+            knn_near_kernel<true><<<nq, kKnnBlock, 0, st>>>(a);
         else
             knn_near_kernel<false><<<nq, kKnnBlock, 0, st>>>(a);
         if (marks) (void)hipEventRecord(marks[0], st);
