@@ -1,19 +1,23 @@
 // lio_icp.hip — loop-closure ICP (PCL IterativeClosestPoint as configured at
 // /root/reference/fast_lio_sam/src/loop_closure.cpp:3-14, aligned at :81) on gfx950.
 //
-// Per ICP iteration (one lane = one source point of this rank's shard):
-//   icp_near_kernel  apply the previous T_inc to the incrementally transformed
-//                    cloud (PCL transformCloud, float SSE order [U]), exact 1-NN
-//                    in the target grid over shells 0..2; lanes whose answer is
-//                    not yet certain go to a far list
-//   icp_far_kernel   finishes those lanes with an unbounded shell walk
-//   icp_stats_kernel per 256-point chunk: Umeyama sufficient statistics of the
-//                    accepted correspondences (d2 <= 52.5^2) in double about a
-//                    fixed centre c0: count, sum p, sum q, sum q p^T, sum d2
+// Per ICP iteration (this rank's shard of the source):
+//   icp_tile_kernel  one wave per tile of <= 64 spatially compact source
+//                    points (binned once per setInputSource): apply the
+//                    previous T_inc to the incrementally transformed cloud
+//                    (PCL transformCloud, float SSE order [U]), exact
+//                    unbounded 1-NN in the target grid with the candidate
+//                    points staged through LDS once per tile
+//   icp_stats_kernel per 256-point chunk (index order): Umeyama sufficient
+//                    statistics of the accepted correspondences
+//                    (d2 <= 52.5^2) in double about a fixed centre c0:
+//                    count, sum p, sum q, sum q p^T, sum d2
 //   icp_reduce_kernel 16 chunks -> one 4096-point record, fixed order
 // The 4096-point records are what ranks all-gather (deterministic, identical
 // for any number of ranks).  The fitness pass is the same pipeline on the
-// ORIGINAL source transformed by the final T, unbounded.
+// ORIGINAL source transformed by the final T.
+#include <hipcub/hipcub.hpp>
+
 #include "lio_dev.hpp"
 #include "lio_kernels.hpp"
 
@@ -27,66 +31,296 @@ __device__ __forceinline__ void xform_pcl(const float* T, float x, float y, floa
     oz = T[8] * x + (T[9] * y + (T[10] * z + T[11]));
 }
 
-constexpr int kIcpGroup = 8;  // lanes cooperating on one query's 1-NN
+// ----------------------------------------------------------------------------
+// Exact 1-NN of a tile of source points (one wave, lane = query).
+//
+// The source is binned once per setInputSource into a grid of tile cells
+// (icp_build_tiles): a tile is <= 64 source points of one cell, so its
+// bounding box Q is compact.  The target grid is x-fastest, so a row of cells
+// (fixed y, z) is ONE contiguous range of points: the wave works on rows,
+// one lane per row, and every range goes through the same staging step
+// (scan_ranges: wave prefix sum -> LDS chunks -> every lane tests every
+// staged point against its own query, LDS broadcast reads), so the candidate
+// points are loaded once per tile instead of once per query.
+//   1. bound: a lane starts from its previous correspondence when the pass
+//      has one (an exact candidate: its distance bounds the answer), else
+//      the rows of Q's own cells are scanned; while some lane has found
+//      nothing, the box grows geometrically (empty surroundings).
+//   2. final: B = the largest best over the lanes; every target point within
+//      sqrt(B) of some query lies in a row whose (y, z) gap to Q is <= sqrt(B),
+//      inside that row's x-range [Q.x0 - r, Q.x1 + r], r = sqrt(B - gap^2):
+//      those rows (minus what step 1 scanned) are scanned once, and every
+//      lane's best is then exact.
+// Total order (d2, id), d2 = float ((dx*dx + dy*dy) + dz*dz): the result
+// does not depend on the tiling.
+// ----------------------------------------------------------------------------
+constexpr int kTileCh = 256;  // candidates staged per LDS round
+constexpr int kTileWaves = 4; // waves per tile: the tile's candidate stream is split over them
 
-// 256 threads = 32 source points, 8 lanes per point.
-__global__ void __launch_bounds__(256) icp_near_kernel(IcpArgs a) {
-    __shared__ uint32_t s_tab[256 / kIcpGroup][72];  // per-group shell-1 slot table
-    const int i = xcd_block(blockIdx.x, gridDim.x) * (256 / kIcpGroup) + threadIdx.x / kIcpGroup;
-    const int sub = threadIdx.x % kIcpGroup;
-    if (i >= a.n) return;  // whole groups leave together
-    float x, y, z;
-    if (a.fitness) {  // getFitnessScore: original source * final; kept in cur for `aligned_`
-        xform_pcl(a.T, a.src[3 * i], a.src[3 * i + 1], a.src[3 * i + 2], x, y, z);
-    } else {
-        x = a.cur[3 * i];
-        y = a.cur[3 * i + 1];
-        z = a.cur[3 * i + 2];
-        if (a.apply_T) {
-            float ox, oy, oz;
-            xform_pcl(a.T, x, y, z, ox, oy, oz);
-            x = ox;
-            y = oy;
-            z = oz;
+// LDS handoff between the lanes of ONE wave (each wave owns its staging area)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+struct TileLds {
+    float4 pts[kTileCh];
+    uint32_t b[kIcpTileQ];
+    uint32_t off[kIcpTileQ + 1];
+};
+
+__device__ __forceinline__ float wave_min_f(float v) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) v = fminf(v, __shfl_xor(v, off, 64));
+    return v;
+}
+__device__ __forceinline__ float wave_max_f(float v) {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+    return v;
+}
+// wave-uniform values to SGPRs (the compiler cannot see that a butterfly
+// result is uniform; keeping the box arithmetic scalar frees VGPRs)
+__device__ __forceinline__ float uni_f(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
+__device__ __forceinline__ uint32_t uni_u(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+// squared gap between the closed intervals [lo, hi] and [a, b]
+__device__ __forceinline__ float interval_gap(float lo, float hi, float a, float b) {
+    const float gap = fmaxf(fmaxf(lo - b, a - hi), 0.f);
+    return gap * gap;
+}
+
+// Every lane contributes one point range [b, b+n); the concatenation is
+// streamed through LDS in kTileCh chunks, wave w of the tile's kTileWaves
+// taking chunks w, w + kTileWaves, ...; every active lane keeps the minimum
+// (d2, id) key over the chunks its wave saw (merged across waves by the caller).
+__device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32_t b, uint32_t n, bool act, float x,
+                                            float y, float z, uint64_t& best, unsigned long long& cand) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t incl = n;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t v = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += v;
+    }
+    const uint32_t T = uni_u(__shfl(incl, 63, 64));
+    if (T == 0) return;  // wave-uniform
+    if (w == 0) cand += T;
+    wave_sync();  // previous readers of the slot table are done
+    L.b[lane] = b;
+    L.off[lane] = incl - n;
+    if (lane == 63) L.off[kIcpTileQ] = T;
+    wave_sync();
+    int sl = 0;
+    uint32_t lo = 0, hi = L.off[1], sb = L.b[0];
+#pragma unroll 1
+    for (uint32_t base = (uint32_t)w * kTileCh; base < T; base += kTileWaves * kTileCh) {
+        constexpr int U = kTileCh / kIcpTileQ;
+        uint32_t src[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {  // slot walk first, so the U loads are in flight together
+            const uint32_t t = base + (uint32_t)(u * kIcpTileQ + lane);
+            src[u] = 0xffffffffu;
+            if (t < T) {
+                while (t >= hi) {
+                    ++sl;
+                    lo = hi;
+                    hi = L.off[sl + 1];
+                    sb = L.b[sl];
+                }
+                src[u] = sb + (t - lo);
+            }
+        }
+        float4 v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (src[u] != 0xffffffffu) v[u] = g.pts[src[u]];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (src[u] != 0xffffffffu) L.pts[u * kIcpTileQ + lane] = v[u];
+        wave_sync();
+        const int cnt = (int)min((uint32_t)kTileCh, T - base);
+        if (act) {
+            int j = 0;
+#pragma unroll 1
+            for (; j + 4 <= cnt; j += 4) {
+                const float4 p0 = L.pts[j], p1 = L.pts[j + 1], p2 = L.pts[j + 2], p3 = L.pts[j + 3];
+                const uint64_t k0 = knn_key(sqdist3(x, y, z, p0.x, p0.y, p0.z), __float_as_int(p0.w));
+                const uint64_t k1 = knn_key(sqdist3(x, y, z, p1.x, p1.y, p1.z), __float_as_int(p1.w));
+                const uint64_t k2 = knn_key(sqdist3(x, y, z, p2.x, p2.y, p2.z), __float_as_int(p2.w));
+                const uint64_t k3 = knn_key(sqdist3(x, y, z, p3.x, p3.y, p3.z), __float_as_int(p3.w));
+                const uint64_t m01 = k0 < k1 ? k0 : k1, m23 = k2 < k3 ? k2 : k3;
+                const uint64_t mm = m01 < m23 ? m01 : m23;
+                best = mm < best ? mm : best;
+            }
+            for (; j < cnt; ++j) {
+                const float4 p = L.pts[j];
+                const uint64_t kk = knn_key(sqdist3(x, y, z, p.x, p.y, p.z), __float_as_int(p.w));
+                best = kk < best ? kk : best;
+            }
+        }
+        wave_sync();  // chunk consumed before it is overwritten
+    }
+}
+
+struct CellBox {
+    int x0, x1, y0, y1, z0, z1;  // empty when x0 > x1
+};
+
+// Scan the rows (y, z) of box N, minus the cells of box S (already scanned;
+// S inside N or empty).  With a finite bound B, rows whose (y, z) gap to the
+// tile box exceeds sqrt(B) are skipped and each row's x-range is trimmed to
+// [qx0 - r, qx1 + r], r = sqrt(B - gap^2) (conservatively rounded).
+__device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const CellBox& S, float B, float qx0, float qx1,
+                          float qy0, float qy1, float qz0, float qz1, bool act, float x, float y, float z,
+                          uint64_t& best, unsigned long long& cand) {
+    const int lane = threadIdx.x & 63;
+    const float cs = g.cell, m = g.margin;
+    const int ny = N.y1 - N.y0 + 1, nrows = ny * (N.z1 - N.z0 + 1);
+    const bool sempty = S.x0 > S.x1;
+    const uint32_t gnx = (uint32_t)g.nx, gnxy = (uint32_t)g.nx * (uint32_t)g.ny;
+#pragma unroll 1
+    for (int rb = 0; rb < nrows; rb += kIcpTileQ) {
+        const int r = rb + lane;
+        uint32_t b0 = 0, n0 = 0, b1 = 0, n1 = 0;
+        if (r < nrows) {
+            const int rz = N.z0 + r / ny, ry = N.y0 + r % ny;
+            int x0 = N.x0, x1 = N.x1;
+            bool keep = true;
+            if (B < INFINITY) {
+                const float yl = g.oy + (float)ry * cs - m, zl = g.oz + (float)rz * cs - m;
+                const float g2 = interval_gap(yl, yl + cs + 2.f * m, qy0, qy1) + interval_gap(zl, zl + cs + 2.f * m, qz0, qz1);
+                if (g2 * 0.999999f > B) {
+                    keep = false;
+                } else {
+                    const float rx = sqrtf(fmaxf(B - g2 * 0.999999f, 0.f)) * 1.00001f + m;
+                    x0 = max(x0, cell_coord(qx0 - rx, g.ox, g.inv_cell));
+                    x1 = min(x1, cell_coord(qx1 + rx, g.ox, g.inv_cell));
+                }
+            }
+            if (keep && x0 <= x1) {
+                const uint32_t rowc = (uint32_t)rz * gnxy + (uint32_t)ry * gnx;
+                const bool inS = !sempty && ry >= S.y0 && ry <= S.y1 && rz >= S.z0 && rz <= S.z1;
+                // piece left of S (or the whole row), piece right of S
+                const int lx1 = inS ? min(x1, S.x0 - 1) : x1;
+                if (x0 <= lx1) {
+                    b0 = g.start[rowc + (uint32_t)x0];
+                    n0 = g.start[rowc + (uint32_t)lx1 + 1] - b0;
+                }
+                const int rx0 = max(x0, S.x1 + 1);
+                if (inS && rx0 <= x1) {
+                    b1 = g.start[rowc + (uint32_t)rx0];
+                    n1 = g.start[rowc + (uint32_t)x1 + 1] - b1;
+                }
+            }
+        }
+        scan_ranges(g, L, b0, n0, act, x, y, z, best, cand);
+        scan_ranges(g, L, b1, n1, act, x, y, z, best, cand);
+    }
+}
+
+// min over the tile's waves of every lane's key (all waves end with the same best)
+__device__ __forceinline__ uint64_t tile_min(uint64_t best, uint64_t (*s_best)[kIcpTileQ]) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    __syncthreads();
+    s_best[w][lane] = best;
+    __syncthreads();
+#pragma unroll
+    for (int v = 0; v < kTileWaves; ++v) {
+        const uint64_t o = s_best[v][lane];
+        best = o < best ? o : best;
+    }
+    return best;
+}
+
+__global__ void __launch_bounds__(kIcpTileQ * kTileWaves) icp_tile_kernel(IcpArgs a) {
+    __shared__ TileLds Ls[kTileWaves];
+    __shared__ uint64_t s_best[kTileWaves][kIcpTileQ];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    TileLds& L = Ls[wv];
+    const uint2 tl = a.tiles[xcd_block(blockIdx.x, gridDim.x)];
+    const bool act = lane < (int)tl.y;
+    const int i = act ? __float_as_int(a.qpts[tl.x + lane].w) : 0;
+    float x = 0.f, y = 0.f, z = 0.f;
+    int prior = -1;
+    if (act) {
+        if (a.prior) prior = a.nn_id[i];
+        if (a.fitness) {  // getFitnessScore: original source * final; kept in cur for `aligned_`
+            xform_pcl(a.T, a.src[3 * i], a.src[3 * i + 1], a.src[3 * i + 2], x, y, z);
+        } else {
+            x = a.cur[3 * i];
+            y = a.cur[3 * i + 1];
+            z = a.cur[3 * i + 2];
+            if (a.apply_T) {
+                float ox, oy, oz;
+                xform_pcl(a.T, x, y, z, ox, oy, oz);
+                x = ox;
+                y = oy;
+                z = oz;
+            }
         }
     }
-    TopK<1> tk;
-    tk.init(INFINITY);
-    const bool done =
-        group_knn_near<1, kIcpGroup>(a.grid, x, y, z, a.max_shell_near, sub, tk, nullptr, s_tab[threadIdx.x / kIcpGroup]);
-    if (sub == 0) {
+    const GridDev& g = a.grid;
+    uint64_t best = knn_key(INFINITY, kNone);
+    if (prior >= 0 && prior != kNone) {  // the previous correspondence: an exact candidate
+        const float4 p = a.tgt_by_id[prior];
+        best = knn_key(sqdist3(x, y, z, p.x, p.y, p.z), prior);
+    }
+    // tile bounding box (active lanes)
+    const float qx0 = uni_f(wave_min_f(act ? x : INFINITY)), qx1 = uni_f(wave_max_f(act ? x : -INFINITY));
+    const float qy0 = uni_f(wave_min_f(act ? y : INFINITY)), qy1 = uni_f(wave_max_f(act ? y : -INFINITY));
+    const float qz0 = uni_f(wave_min_f(act ? z : INFINITY)), qz1 = uni_f(wave_max_f(act ? z : -INFINITY));
+    const CellBox Q{min(max(cell_coord(qx0, g.ox, g.inv_cell), 0), g.nx - 1),
+                    min(max(cell_coord(qx1, g.ox, g.inv_cell), 0), g.nx - 1),
+                    min(max(cell_coord(qy0, g.oy, g.inv_cell), 0), g.ny - 1),
+                    min(max(cell_coord(qy1, g.oy, g.inv_cell), 0), g.ny - 1),
+                    min(max(cell_coord(qz0, g.oz, g.inv_cell), 0), g.nz - 1),
+                    min(max(cell_coord(qz1, g.oz, g.inv_cell), 0), g.nz - 1)};
+    unsigned long long cand = 0;
+    int rounds = 0;
+    // 1. bound: grow a box around Q until every lane holds a candidate
+    CellBox S{1, 0, 1, 0, 1, 0};  // scanned so far (empty)
+    int r = 0;
+    while (__any(act && (uint32_t)best == (uint32_t)kNone)) {
+        const CellBox N{max(Q.x0 - r, 0), min(Q.x1 + r, g.nx - 1), max(Q.y0 - r, 0), min(Q.y1 + r, g.ny - 1),
+                        max(Q.z0 - r, 0), min(Q.z1 + r, g.nz - 1)};
+        scan_rows(g, L, N, S, INFINITY, qx0, qx1, qy0, qy1, qz0, qz1, act, x, y, z, best, cand);
+        best = tile_min(best, s_best);
+        ++rounds;
+        S = N;
+        if (N.x0 == 0 && N.y0 == 0 && N.z0 == 0 && N.x1 == g.nx - 1 && N.y1 == g.ny - 1 && N.z1 == g.nz - 1) break;
+        r = 2 * r + 1;
+    }
+    // 2. final: everything within sqrt(B) of the tile box, minus S
+    const float B = uni_f(wave_max_f(act ? __uint_as_float((uint32_t)(best >> 32)) : 0.f));
+    if (B < INFINITY) {
+        const float R = sqrtf(B) * 1.00001f + g.margin;
+        const CellBox N{max(cell_coord(qx0 - R, g.ox, g.inv_cell), 0), min(cell_coord(qx1 + R, g.ox, g.inv_cell), g.nx - 1),
+                        max(cell_coord(qy0 - R, g.oy, g.inv_cell), 0), min(cell_coord(qy1 + R, g.oy, g.inv_cell), g.ny - 1),
+                        max(cell_coord(qz0 - R, g.oz, g.inv_cell), 0), min(cell_coord(qz1 + R, g.oz, g.inv_cell), g.nz - 1)};
+        // S may stick out of N (a grown box): clip it, the part outside N is not needed
+        CellBox Sc{max(S.x0, N.x0), min(S.x1, N.x1), max(S.y0, N.y0), min(S.y1, N.y1), max(S.z0, N.z0), min(S.z1, N.z1)};
+        if (Sc.y0 > Sc.y1 || Sc.z0 > Sc.z1) Sc.x0 = 1, Sc.x1 = 0;
+        scan_rows(g, L, N, Sc, B, qx0, qx1, qy0, qy1, qz0, qz1, act, x, y, z, best, cand);
+        best = tile_min(best, s_best);
+        ++rounds;
+    }
+    if (a.dbg && threadIdx.x == 0) {
+        atomicAdd(a.dbg, cand);
+        atomicAdd(a.dbg + 1, (unsigned long long)rounds);
+        atomicAdd(a.dbg + 2, 1ull);
+        atomicAdd(a.dbg + 3, (unsigned long long)tl.y);
+    }
+    __syncthreads();       // every wave has read cur[i] before it is overwritten
+    if (act && wv == 0) {
         if (a.fitness || a.apply_T) {
             a.cur[3 * i] = x;
             a.cur[3 * i + 1] = y;
             a.cur[3 * i + 2] = z;
         }
-        a.far_d2[i] = tk.d(0);
-        a.far_id[i] = tk.id(0);
-        if (!done) {
-            const int slot = atomicAdd(a.far_count, 1);
-            a.far_list[slot] = i;
-        }
-    }
-}
-
-// Unresolved points: unbounded shell walk seeded with the near result.
-__global__ void __launch_bounds__(256) icp_far_kernel(IcpArgs a) {
-    const int cnt = *a.far_count;
-    const int sub = threadIdx.x % kIcpGroup;
-    const int gpb = 256 / kIcpGroup;
-    for (int k = blockIdx.x * gpb + threadIdx.x / kIcpGroup; k < cnt; k += gridDim.x * gpb) {
-        const int i = a.far_list[k];
-        const float x = a.cur[3 * i], y = a.cur[3 * i + 1], z = a.cur[3 * i + 2];
-        TopK<1> tk;
-        tk.init(INFINITY);
-        if (sub == 0) {  // the near pass's best is a valid starting bound (only lane 0 holds it)
-            tk.k[0] = knn_key(a.far_d2[i], a.far_id[i]);
-        }
-        group_knn_exact<1, kIcpGroup>(a.grid, x, y, z, 0x3fffffff, sub, tk);
-        if (sub == 0) {
-            a.far_d2[i] = tk.d(0);
-            a.far_id[i] = tk.id(0);
-        }
+        a.nn_d2[i] = __uint_as_float((uint32_t)(best >> 32));
+        a.nn_id[i] = (int)(uint32_t)best;
     }
 }
 
@@ -104,8 +338,8 @@ __global__ void __launch_bounds__(256) icp_stats_kernel(IcpArgs a) {
 #pragma unroll
     for (int k = 0; k < 17; ++k) v[k] = 0.0;
     if (i < a.n) {
-        const int id = a.far_id[i];
-        const float d2 = a.far_d2[i];
+        const int id = a.nn_id[i];
+        const float d2 = a.nn_d2[i];
         if (a.fitness) {
             if (id >= 0 && id != kNone) {
                 v[0] = 1.0;
@@ -151,15 +385,53 @@ __global__ void icp_reduce_kernel(const double* __restrict__ partials, int nchun
     super[(size_t)sidx * kIcpStride + k] = s;
 }
 
-void launch_icp_near(const IcpArgs& a, hipStream_t st) {
-    if (a.n == 0) return;
-    const int ppb = 256 / kIcpGroup;
-    icp_near_kernel<<<(a.n + ppb - 1) / ppb, 256, 0, st>>>(a);
+void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st) {
+    if (a.n == 0 || ntiles == 0) return;
+    icp_tile_kernel<<<ntiles, kIcpTileQ * kTileWaves, 0, st>>>(a);
 }
-void launch_icp_far(const IcpArgs& a, int max_far_blocks, hipStream_t st) {
-    if (a.n == 0) return;
-    icp_far_kernel<<<max_far_blocks, 256, 0, st>>>(a);
+
+// per cell: number of tiles (ceil(count / 64)); slot ncells = 0 for the scan's total
+__global__ void tile_count_kernel(const uint32_t* __restrict__ start, uint32_t ncells, uint32_t* __restrict__ tcount) {
+    const uint32_t c = blockIdx.x * 256u + threadIdx.x;
+    if (c > ncells) return;
+    tcount[c] = c < ncells ? (start[c + 1] - start[c] + kIcpTileQ - 1) / kIcpTileQ : 0u;
 }
+__global__ void tile_write_kernel(const uint32_t* __restrict__ start, uint32_t ncells, const uint32_t* __restrict__ toff,
+                                  uint2* __restrict__ tiles) {
+    const uint32_t c = blockIdx.x * 256u + threadIdx.x;
+    if (c >= ncells) return;
+    const uint32_t b = start[c], n = start[c + 1] - b, nt = toff[c + 1] - toff[c];
+    for (uint32_t t = 0; t < nt; ++t) {  // balanced split of the cell's points
+        const uint32_t s0 = (uint32_t)((uint64_t)n * t / nt), s1 = (uint32_t)((uint64_t)n * (t + 1) / nt);
+        tiles[toff[c] + t] = make_uint2(b + s0, s1 - s0);
+    }
+}
+
+int icp_build_tiles(const GridBuf& q, uint2* tiles, uint32_t* scratch, void*& tmp, size_t& tmp_bytes, hipStream_t st) {
+    const uint32_t nc = q.geom.ncells;
+    uint32_t* tcount = scratch;          // nc + 1
+    uint32_t* toff = scratch + nc + 1;   // nc + 1
+    const int nb = (int)((nc + 1 + 255) / 256);
+    tile_count_kernel<<<nb, 256, 0, st>>>(q.start, nc, tcount);
+    size_t need = 0;
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, need, tcount, toff, (int)(nc + 1), st) != hipSuccess) return -1;
+    if (need > tmp_bytes) {
+        if (tmp) (void)hipFree(tmp);
+        tmp = nullptr;
+        tmp_bytes = 0;
+        if (hipMalloc(&tmp, need) != hipSuccess) return -5;
+        tmp_bytes = need;
+    }
+    size_t tb = tmp_bytes;
+    if (hipcub::DeviceScan::ExclusiveSum(tmp, tb, tcount, toff, (int)(nc + 1), st) != hipSuccess) return -1;
+    tile_write_kernel<<<nb, 256, 0, st>>>(q.start, nc, toff, tiles);
+    uint32_t total = 0;
+    if (hipMemcpyAsync(&total, toff + nc, sizeof(uint32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess || hipGetLastError() != hipSuccess)
+        return -1;
+    return (int)total;
+}
+
 void launch_icp_stats(const IcpArgs& a, hipStream_t st) {
     if (a.n == 0) return;
     icp_stats_kernel<<<(a.n + 255) / 256, 256, 0, st>>>(a);

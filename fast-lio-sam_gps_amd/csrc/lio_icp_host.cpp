@@ -17,6 +17,8 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <string>
@@ -146,8 +148,16 @@ struct lio_icp {
     float* d_cur = nullptr;
     float* d_fd2 = nullptr;
     int* d_fid = nullptr;
-    int* d_far = nullptr;
-    int* d_far_count = nullptr;
+    lio::GridBuf qgrid;      // the shard's source binned by tile cell (icp_build_tiles)
+    uint2* d_tiles = nullptr;
+    uint32_t* d_tscratch = nullptr;
+    void* d_ttmp = nullptr;
+    size_t ttmp_bytes = 0;
+    int64_t tiles_cap = 0, tscratch_cap = 0;
+    int ntiles = 0;
+    float tile_cell = 2.0f;
+    bool have_prior = false;  // nn ids of this alignment's previous pass are in d_fid
+    unsigned long long* d_dbg = nullptr;  // LIO_ICP_DEBUG counters
     double* d_part = nullptr;
     double* d_super = nullptr;
     double* h_super = nullptr;  // pinned
@@ -186,9 +196,12 @@ int lio_icp_create(const lio_icp_params* p, lio_icp** out) {
     auto* h = new lio_icp();
     h->dev = p->device;
     h->p = *p;
-    if (!(h->p.cell_size > 0.f)) h->p.cell_size = 2.0f;  // 0.3 m voxelised submaps: 2 m cells (scripts/icp_cells.py)
-    if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess ||
-        hipMalloc(&h->d_far_count, 64) != hipSuccess) {
+    if (!(h->p.cell_size > 0.f)) h->p.cell_size = 1.0f;  // 0.3 m voxelised submaps: 1 m target cells (scripts/icp_cells.py)
+    if (const char* e = std::getenv("LIO_ICP_TILE_CELL")) {  // diagnostics override (scripts/icp_cells.py)
+        const float v = (float)std::atof(e);
+        if (v > 0.f) h->tile_cell = v;
+    }
+    if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess) {
         delete h;
         return ifail(LIO_ERR_HIP, "icp stream/alloc failed");
     }
@@ -203,7 +216,8 @@ int lio_icp_destroy(lio_icp* h) {
     (void)hipSetDevice(h->dev);
     (void)hipStreamSynchronize(h->st);
     lio::grid_free(h->tgt);
-    void* ptrs[] = {h->d_tgt, h->d_src, h->d_cur, h->d_fd2, h->d_fid, h->d_far, h->d_far_count, h->d_part, h->d_super};
+    lio::grid_free(h->qgrid);
+    void* ptrs[] = {h->d_tgt, h->d_src, h->d_cur, h->d_fd2, h->d_fid, h->d_tiles, h->d_tscratch, h->d_ttmp, h->d_dbg, h->d_part, h->d_super};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (h->h_super) (void)hipHostFree(h->h_super);
@@ -255,7 +269,7 @@ static int icp_prepare(lio_icp* h) {
     shard_range(h->ns, h->rank, h->world, h->sh_begin, h->sh_n);
     const int64_t n = std::max<int64_t>(h->sh_n, 1);
     if (n > h->cap) {
-        void* ptrs[] = {h->d_src, h->d_cur, h->d_fd2, h->d_fid, h->d_far, h->d_part};
+        void* ptrs[] = {h->d_src, h->d_cur, h->d_fd2, h->d_fid, h->d_tiles, h->d_part};
         for (void* q : ptrs)
             if (q) IHIP(hipFree(q));
         const int64_t nch = (n + lio::kIcpChunk - 1) / lio::kIcpChunk;
@@ -263,7 +277,7 @@ static int icp_prepare(lio_icp* h) {
         IHIP(hipMalloc(&h->d_cur, n * 3 * sizeof(float)));
         IHIP(hipMalloc(&h->d_fd2, n * sizeof(float)));
         IHIP(hipMalloc(&h->d_fid, n * sizeof(int)));
-        IHIP(hipMalloc(&h->d_far, n * sizeof(int)));
+        IHIP(hipMalloc(&h->d_tiles, (n + n / lio::kIcpTileQ + 1) * sizeof(uint2)));
         IHIP(hipMalloc(&h->d_part, nch * lio::kIcpStride * sizeof(double)));
         h->cap = n;
     }
@@ -275,9 +289,25 @@ static int icp_prepare(lio_icp* h) {
         IHIP(hipHostMalloc(&h->h_super, nsup_all * lio::kIcpStride * sizeof(double)));
         h->super_cap = nsup_all;
     }
-    if (h->sh_n > 0)
+    h->ntiles = 0;
+    if (h->sh_n > 0) {
         IHIP(hipMemcpyAsync(h->d_src, h->src.data() + 3 * h->sh_begin, h->sh_n * 3 * sizeof(float),
                             hipMemcpyHostToDevice, h->st));
+        // bin the shard by tile cell: tiles of <= 64 spatially compact queries (perf only: every
+        // query's 1-NN is exact whatever tile it is in)
+        int rc = lio::grid_build(h->qgrid, h->d_src, h->sh_n, h->tile_cell, h->st);
+        if (rc) return ifail(rc == -5 ? LIO_ERR_NOMEM : LIO_ERR_HIP, "source binning failed");
+        const int64_t need = 2 * ((int64_t)h->qgrid.geom.ncells + 1);
+        if (need > h->tscratch_cap) {
+            if (h->d_tscratch) IHIP(hipFree(h->d_tscratch));
+            h->d_tscratch = nullptr;
+            IHIP(hipMalloc(&h->d_tscratch, need * sizeof(uint32_t)));
+            h->tscratch_cap = need;
+        }
+        const int nt = lio::icp_build_tiles(h->qgrid, h->d_tiles, h->d_tscratch, h->d_ttmp, h->ttmp_bytes, h->st);
+        if (nt < 0) return ifail(nt == -5 ? LIO_ERR_NOMEM : LIO_ERR_HIP, "tile list failed");
+        h->ntiles = nt;
+    }
     h->src_dirty = false;
     return LIO_OK;
 }
@@ -295,19 +325,23 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     std::memcpy(a.c0, h->c0, sizeof(a.c0));
     a.max_d2 = max_d2;
     a.fitness = fitness ? 1 : 0;
-    a.max_shell_near = 2;
+    a.prior = h->have_prior ? 1 : 0;
     a.partials = h->d_part;
-    a.far_list = h->d_far;
-    a.far_count = h->d_far_count;
-    a.far_d2 = h->d_fd2;
-    a.far_id = h->d_fid;
+    a.nn_d2 = h->d_fd2;
+    a.nn_id = h->d_fid;
+    a.qpts = h->qgrid.pts;
+    a.tiles = h->d_tiles;
+    static const bool dbg_on = std::getenv("LIO_ICP_DEBUG") != nullptr;  // search statistics on stderr
+    if (dbg_on) {
+        if (!h->d_dbg) IHIP(hipMalloc(&h->d_dbg, 64));
+        IHIP(hipMemsetAsync(h->d_dbg, 0, 64, h->st));
+        a.dbg = h->d_dbg;
+    }
     const int nch = (int)((h->sh_n + lio::kIcpChunk - 1) / lio::kIcpChunk);
     const int nsup_loc = (int)((h->sh_n + lio::kIcpSuper - 1) / lio::kIcpSuper);
     if (h->sh_n > 0) {
-        IHIP(hipMemsetAsync(h->d_far_count, 0, 64, h->st));
         if (h->timing) IHIP(hipEventRecord(h->ev.a, h->st));
-        lio::launch_icp_near(a, h->st);
-        lio::launch_icp_far(a, 512, h->st);
+        lio::launch_icp_tiles(a, h->ntiles, h->st);
         lio::launch_icp_stats(a, h->st);
         if (h->timing) IHIP(hipEventRecord(h->ev.b, h->st));
         lio::launch_icp_reduce(h->d_part, nch, h->d_super, h->st);
@@ -316,6 +350,13 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
                             hipMemcpyDeviceToHost, h->st));
     }
     IHIP(hipStreamSynchronize(h->st));
+    h->have_prior = true;
+    if (dbg_on) {
+        unsigned long long c[4];
+        IHIP(hipMemcpy(c, h->d_dbg, sizeof(c), hipMemcpyDeviceToHost));
+        std::fprintf(stderr, "icp dbg: tiles %llu lanes %llu cand/tile %.1f rounds/tile %.2f cand/lane %.1f\n", c[2], c[3],
+                     (double)c[0] / c[2], (double)c[1] / c[2], (double)c[0] / c[3]);
+    }
     if (h->timing && h->sh_n > 0) {
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, h->ev.a, h->ev.b) == hipSuccess) {
@@ -376,6 +417,7 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
     }
     if (h->sh_n > 0)
         IHIP(hipMemcpyAsync(h->d_cur, h->d_src, h->sh_n * 3 * sizeof(float), hipMemcpyDeviceToDevice, h->st));
+    h->have_prior = false;
     const double max_d2 = h->p.max_corr_dist * h->p.max_corr_dist;
     const double rot_thr = h->p.rot_eps > 0 ? h->p.rot_eps : 1.0 - h->p.trans_eps;
     double prev_mse = std::numeric_limits<double>::max();
@@ -477,6 +519,18 @@ int icp_align(const float* src, int64_t ns, const float* dst, int64_t nd, const 
     }
     lio_icp_destroy(h);
     return rc;
+}
+
+int lio_icp_get_correspondences(lio_icp* h, int32_t* ids, float* d2) {
+    if (!h || !ids || !d2) return ifail(LIO_ERR_ARG, "bad arguments");
+    if (!h->have_prior) return ifail(LIO_ERR_STATE, "lio_icp_get_correspondences: no pass run yet");
+    IHIP(hipSetDevice(h->dev));
+    if (h->sh_n > 0) {
+        IHIP(hipMemcpyAsync(ids, h->d_fid, h->sh_n * sizeof(int32_t), hipMemcpyDeviceToHost, h->st));
+        IHIP(hipMemcpyAsync(d2, h->d_fd2, h->sh_n * sizeof(float), hipMemcpyDeviceToHost, h->st));
+        IHIP(hipStreamSynchronize(h->st));
+    }
+    return LIO_OK;
 }
 
 int lio_icp_set_timing(lio_icp* h, int enable) {

@@ -105,20 +105,26 @@ struct IcpArgs {
     double c0[3];        // accumulation centre
     double max_d2;       // correspondence rejection (d2 > max_d2 => skip)
     int fitness;         // 1: fitness pass (src with T, unbounded, sum d2 only)
-    int max_shell_near;  // shells searched in the first pass
+    int prior;           // 1: nn_id holds this alignment's previous correspondences (a starting bound)
     double* partials;    // per 256-point chunk: 17 doubles padded to 20
-    int* far_list;       // queries left unresolved by the first pass
-    int* far_count;
-    float* far_d2;       // best-so-far per point (n)
-    int* far_id;
+    float* nn_d2;        // per point: 1-NN squared distance (n)
+    int* nn_id;          //            1-NN target id
+    const float4* qpts;  // source binned by tile cell: (x, y, z, local index bits), cell order
+    const uint2* tiles;  // (first entry in qpts, query count <= kIcpTileQ) per tile
+    unsigned long long* dbg;  // optional counters (diagnostics): candidates, rings, tiles, lanes
 };
 
 constexpr int kIcpChunk = 256;     // points per partial
 constexpr int kIcpSuper = 4096;    // points per exchanged partial (shard granule)
 constexpr int kIcpStride = 20;     // doubles per partial record
 
-void launch_icp_near(const IcpArgs& a, hipStream_t st);
-void launch_icp_far(const IcpArgs& a, int max_far_blocks, hipStream_t st);
+constexpr int kIcpTileQ = 64;     // queries per tile (one wave)
+
+// tiles of <= kIcpTileQ queries per non-empty cell of the source grid `q`
+// (ceil(count / 64) tiles per cell, sizes balanced), in cell order.  Returns
+// the tile count (synchronises the stream once).  tiles: capacity n + n / 64 + 1.
+int icp_build_tiles(const GridBuf& q, uint2* tiles, uint32_t* scratch, void*& tmp, size_t& tmp_bytes, hipStream_t st);
+void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st);
 void launch_icp_stats(const IcpArgs& a, hipStream_t st);
 void launch_icp_reduce(const double* partials, int nchunks, double* super, hipStream_t st);
 

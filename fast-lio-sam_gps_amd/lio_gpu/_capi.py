@@ -35,7 +35,7 @@ EXPORTS = [
     "lio_get_knn", "lio_get_planes", "lio_get_world", "lio_get_h_rows", "lio_ctx_knn_stats",
     "lio_ieskf_update",
     "lio_icp_create", "lio_icp_destroy", "lio_icp_set_target", "lio_icp_set_source", "lio_icp_set_shard",
-    "lio_icp_align", "icp_align", "lio_icp_shard_range", "lio_icp_combine",
+    "lio_icp_align", "icp_align", "lio_icp_shard_range", "lio_icp_combine", "lio_icp_get_correspondences",
     "lio_ctx_set_timing", "lio_ctx_get_timing", "lio_ctx_reset_timing", "lio_icp_set_timing", "lio_icp_get_timing",
 ]
 
@@ -185,6 +185,7 @@ def _declare(L):
         "lio_icp_set_source": (C.c_int, [vp, fp, C.c_int64]),
         "lio_icp_set_shard": (C.c_int, [vp, C.c_int, C.c_int, ALLGATHER_FN, vp]),
         "lio_icp_align": (C.c_int, [vp, fp, C.POINTER(IcpResult), fp]),
+        "lio_icp_get_correspondences": (C.c_int, [vp, C.POINTER(C.c_int32), fp]),
         "icp_align": (C.c_int, [fp, C.c_int64, fp, C.c_int64, C.POINTER(IcpParams), fp, dp,
                                 C.POINTER(C.c_int), C.POINTER(C.c_int), fp]),
         "lio_icp_shard_range": (C.c_int, [C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
@@ -201,6 +202,29 @@ def _declare(L):
         f.argtypes = args
 
 
+def _share_torch_hip_runtime():
+    """One HIP runtime per process.
+
+    PyTorch-ROCm bundles its own libamdhip64.so.7 (+ HSA runtime) under
+    torch/lib; ours links /opt/rocm's under the same soname, so whichever loads
+    first serves both, and torch cannot see the GPU through the other one
+    ("No HIP GPUs are available").  When torch is installed, load its runtime
+    first (without importing torch) so that device pointers from torch tensors
+    (lio_scan_bind_device) and our kernels share one runtime.  A process
+    without torch (the C++ host) uses /opt/rocm's.
+    """
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return
+    for d in spec.submodule_search_locations:
+        hip = os.path.join(d, "lib", "libamdhip64.so")
+        if os.path.exists(hip):
+            C.CDLL(hip, mode=C.RTLD_GLOBAL)
+            return
+
+
 def lib():
     """Load liblio_gpu.so (raises if it was not built — there is no fallback)."""
     global _lib
@@ -208,6 +232,7 @@ def lib():
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} not built: run `make -C fast-lio-sam_gps_amd` "
                               "(or __graft_entry__.build()); lio_gpu has no CPU path")
+        _share_torch_hip_runtime()
         L = C.CDLL(LIB_PATH)
         _declare(L)
         _lib = L

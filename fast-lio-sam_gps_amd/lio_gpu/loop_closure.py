@@ -53,14 +53,14 @@ def _xyz(cloud) -> np.ndarray:
     return a.reshape(-1, 3) if a.ndim == 1 else a[:, :3]
 
 
-def icp_params(config: LoopClosureConfig, cell_size: float = 2.0, device: int = 0) -> _capi.IcpParams:
+def icp_params(config: LoopClosureConfig, cell_size: float = 1.0, device: int = 0) -> _capi.IcpParams:
     # setTransformationEpsilon(0.01), setEuclideanFitnessEpsilon(0.01), setMaximumIterations(50)
     return _capi.IcpParams(config.icp_max_corr_dist_, 0.01, 0.01, 50, 0.0, config.icp_score_threshold_,
                            cell_size, device)
 
 
 class LoopClosure:
-    def __init__(self, config: LoopClosureConfig, cell_size: float = 2.0, device: int = 0):
+    def __init__(self, config: LoopClosureConfig, cell_size: float = 1.0, device: int = 0):
         self.config_ = config
         self._p = icp_params(config, cell_size, device)
         self._h = C.c_void_p()
@@ -108,6 +108,19 @@ class LoopClosure:
         if out is not None:
             self.aligned_ = out
         return res
+
+    def correspondences(self):
+        """1-NN (target index, float d2) of every source point of this rank's shard in the
+        last pass (after align(): the getFitnessScore pass over the aligned cloud)."""
+        rank, world = self._shard
+        nsup = (self._ns + 4095) // 4096
+        b = min(nsup * rank // world * 4096, self._ns)
+        e = min(nsup * (rank + 1) // world * 4096, self._ns)
+        ids = np.empty(max(e - b, 0), np.int32)
+        d2 = np.empty(max(e - b, 0), np.float32)
+        check(lib().lio_icp_get_correspondences(self._h, ids.ctypes.data_as(C.POINTER(C.c_int32)),
+                                                d2.ctypes.data_as(C.POINTER(C.c_float))))
+        return ids, d2
 
     def setSrcAndDstCloud(self, keyframes, src_idx: int, dst_idx: int, submap_range: int, voxel_res: float):
         """loop_closure.cpp:42-67 on the GPU: per side, transformPcd of keyframes

@@ -208,7 +208,7 @@ typedef struct lio_icp_params {
     int max_iter;           /* setMaximumIterations(50)         loop_closure.cpp:10 */
     double rot_eps;         /* 0 => PCL default 1 - trans_eps                        */
     double score_threshold; /* icp_score_threshold (config.yaml:16)                   */
-    float cell_size;        /* target grid cell [m]; 0 => 2.0                        */
+    float cell_size;        /* target grid cell [m]; 0 => 1.0                        */
     int device;
 } lio_icp_params;
 
@@ -243,6 +243,10 @@ int lio_icp_combine(const double* recv, int64_t n_source, int world, double* out
 /* align(guess) + getFitnessScore() + is_valid decision (loop_closure.cpp:81-90).
  * aligned_opt (n*3, this rank's shard only when sharded) may be NULL.      */
 int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* aligned_opt);
+/* Diagnostics: the 1-NN of the last pass (after lio_icp_align: the
+ * getFitnessScore pass) per source point of this rank's shard: target index
+ * (input order of lio_icp_set_target) and float squared distance.          */
+int lio_icp_get_correspondences(lio_icp* h, int32_t* ids, float* d2);
 /* One-shot form of the above (SURVEY §8b signature).                       */
 int icp_align(const float* src_xyz, int64_t ns, const float* dst_xyz, int64_t nd, const lio_icp_params* p,
               float* T_out, double* fitness, int* converged, int* iters, float* aligned_xyz_opt);

@@ -419,7 +419,7 @@ struct RegistrationOutput {  // loop_closure.h:31-37
 
 class LoopClosureICP {
 public:
-    explicit LoopClosureICP(const LoopClosureConfig& cfg = {}, int device = 0, float cell_size = 2.0f) {
+    explicit LoopClosureICP(const LoopClosureConfig& cfg = {}, int device = 0, float cell_size = 1.0f) {
         lio_icp_params p{cfg.icp_max_corr_dist_, 0.01, 0.01, 50, 0.0, cfg.icp_score_threshold_, cell_size, device};
         check(lio_icp_create(&p, &h_), "lio_icp_create");
     }
