@@ -18,6 +18,8 @@
 // ORIGINAL source transformed by the final T.
 #include <hipcub/hipcub.hpp>
 
+#include <cstdlib>
+
 #include "lio_dev.hpp"
 #include "lio_kernels.hpp"
 
@@ -55,7 +57,6 @@ __device__ __forceinline__ void xform_pcl(const float* T, float x, float y, floa
 // does not depend on the tiling.
 // ----------------------------------------------------------------------------
 constexpr int kTileCh = 256;  // candidates staged per LDS round
-constexpr int kTileWaves = 4; // waves per tile: the tile's candidate stream is split over them
 
 // LDS handoff between the lanes of ONE wave (each wave owns its staging area)
 __device__ __forceinline__ void wave_sync() {
@@ -66,8 +67,8 @@ __device__ __forceinline__ void wave_sync() {
 
 struct TileLds {
     float4 pts[kTileCh];
-    uint32_t b[kIcpTileQ];
-    uint32_t off[kIcpTileQ + 1];
+    uint32_t b[2 * kIcpTileQ];
+    uint32_t off[2 * kIcpTileQ + 1];
 };
 
 __device__ __forceinline__ float wave_min_f(float v) {
@@ -91,13 +92,16 @@ __device__ __forceinline__ float interval_gap(float lo, float hi, float a, float
     return gap * gap;
 }
 
-// Every lane contributes one point range [b, b+n); the concatenation is
-// streamed through LDS in kTileCh chunks, wave w of the tile's kTileWaves
-// taking chunks w, w + kTileWaves, ...; every active lane keeps the minimum
+// Every lane contributes two point ranges [b0, b0+n0), [b1, b1+n1); the concatenation is
+// streamed through LDS in kTileCh chunks, wave w of the tile's NW
+// taking chunks w, w + NW, ...; every active lane keeps the minimum
 // (d2, id) key over the chunks its wave saw (merged across waves by the caller).
-__device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32_t b, uint32_t n, bool act, float x,
-                                            float y, float z, uint64_t& best, unsigned long long& cand) {
+template <int NW>  // waves per tile: the tile's candidate stream is split over them
+__device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32_t b0, uint32_t n0, uint32_t b1,
+                                            uint32_t n1, bool act, float x, float y, float z, uint64_t& best,
+                                            unsigned long long& cand) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint32_t n = n0 + n1;
     uint32_t incl = n;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -108,50 +112,42 @@ __device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32
     if (T == 0) return;  // wave-uniform
     if (w == 0) cand += T;
     wave_sync();  // previous readers of the slot table are done
-    L.b[lane] = b;
-    L.off[lane] = incl - n;
-    if (lane == 63) L.off[kIcpTileQ] = T;
+    L.b[2 * lane] = b0;
+    L.b[2 * lane + 1] = b1;
+    L.off[2 * lane] = incl - n;
+    L.off[2 * lane + 1] = incl - n1;
+    if (lane == 63) L.off[2 * kIcpTileQ] = T;
     wave_sync();
     int sl = 0;
     uint32_t lo = 0, hi = L.off[1], sb = L.b[0];
 #pragma unroll 1
-    for (uint32_t base = (uint32_t)w * kTileCh; base < T; base += kTileWaves * kTileCh) {
+    for (uint32_t base = (uint32_t)w * kTileCh; base < T; base += NW * kTileCh) {
         constexpr int U = kTileCh / kIcpTileQ;
-        uint32_t src[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {  // slot walk first, so the U loads are in flight together
-            const uint32_t t = base + (uint32_t)(u * kIcpTileQ + lane);
-            src[u] = 0xffffffffu;
-            if (t < T) {
-                while (t >= hi) {
-                    ++sl;
-                    lo = hi;
-                    hi = L.off[sl + 1];
-                    sb = L.b[sl];
-                }
-                src[u] = sb + (t - lo);
-            }
-        }
         float4 v[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (src[u] != 0xffffffffu) v[u] = g.pts[src[u]];
+        for (int u = 0; u < U; ++u) {  // slot walk first (clamped to the last point), U loads in flight
+            const uint32_t t = min(base + (uint32_t)(u * kIcpTileQ + lane), T - 1);
+            while (t >= hi) {
+                ++sl;
+                lo = hi;
+                hi = L.off[sl + 1];
+                sb = L.b[sl];
+            }
+            v[u] = g.pts[sb + (t - lo)];
+        }
 #pragma unroll
         for (int u = 0; u < U; ++u)
-            if (src[u] != 0xffffffffu) L.pts[u * kIcpTileQ + lane] = v[u];
+            if (base + (uint32_t)(u * kIcpTileQ + lane) < T) L.pts[u * kIcpTileQ + lane] = v[u];
         wave_sync();
         const int cnt = (int)min((uint32_t)kTileCh, T - base);
         if (act) {
             int j = 0;
 #pragma unroll 1
-            for (; j + 4 <= cnt; j += 4) {
-                const float4 p0 = L.pts[j], p1 = L.pts[j + 1], p2 = L.pts[j + 2], p3 = L.pts[j + 3];
+            for (; j + 2 <= cnt; j += 2) {
+                const float4 p0 = L.pts[j], p1 = L.pts[j + 1];
                 const uint64_t k0 = knn_key(sqdist3(x, y, z, p0.x, p0.y, p0.z), __float_as_int(p0.w));
                 const uint64_t k1 = knn_key(sqdist3(x, y, z, p1.x, p1.y, p1.z), __float_as_int(p1.w));
-                const uint64_t k2 = knn_key(sqdist3(x, y, z, p2.x, p2.y, p2.z), __float_as_int(p2.w));
-                const uint64_t k3 = knn_key(sqdist3(x, y, z, p3.x, p3.y, p3.z), __float_as_int(p3.w));
-                const uint64_t m01 = k0 < k1 ? k0 : k1, m23 = k2 < k3 ? k2 : k3;
-                const uint64_t mm = m01 < m23 ? m01 : m23;
+                const uint64_t mm = k0 < k1 ? k0 : k1;
                 best = mm < best ? mm : best;
             }
             for (; j < cnt; ++j) {
@@ -172,6 +168,7 @@ struct CellBox {
 // S inside N or empty).  With a finite bound B, rows whose (y, z) gap to the
 // tile box exceeds sqrt(B) are skipped and each row's x-range is trimmed to
 // [qx0 - r, qx1 + r], r = sqrt(B - gap^2) (conservatively rounded).
+template <int NW>
 __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const CellBox& S, float B, float qx0, float qx1,
                           float qy0, float qy1, float qz0, float qz1, bool act, float x, float y, float z,
                           uint64_t& best, unsigned long long& cand) {
@@ -215,28 +212,29 @@ __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const 
                 }
             }
         }
-        scan_ranges(g, L, b0, n0, act, x, y, z, best, cand);
-        scan_ranges(g, L, b1, n1, act, x, y, z, best, cand);
+        scan_ranges<NW>(g, L, b0, n0, b1, n1, act, x, y, z, best, cand);
     }
 }
 
 // min over the tile's waves of every lane's key (all waves end with the same best)
+template <int NW>
 __device__ __forceinline__ uint64_t tile_min(uint64_t best, uint64_t (*s_best)[kIcpTileQ]) {
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     __syncthreads();
     s_best[w][lane] = best;
     __syncthreads();
 #pragma unroll
-    for (int v = 0; v < kTileWaves; ++v) {
+    for (int v = 0; v < NW; ++v) {
         const uint64_t o = s_best[v][lane];
         best = o < best ? o : best;
     }
     return best;
 }
 
-__global__ void __launch_bounds__(kIcpTileQ * kTileWaves) icp_tile_kernel(IcpArgs a) {
-    __shared__ TileLds Ls[kTileWaves];
-    __shared__ uint64_t s_best[kTileWaves][kIcpTileQ];
+template <int NW>
+__global__ void __launch_bounds__(kIcpTileQ * NW) icp_tile_kernel(IcpArgs a) {
+    __shared__ TileLds Ls[NW];
+    __shared__ uint64_t s_best[NW][kIcpTileQ];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     TileLds& L = Ls[wv];
     const uint2 tl = a.tiles[xcd_block(blockIdx.x, gridDim.x)];
@@ -279,32 +277,34 @@ __global__ void __launch_bounds__(kIcpTileQ * kTileWaves) icp_tile_kernel(IcpArg
                     min(max(cell_coord(qz1, g.oz, g.inv_cell), 0), g.nz - 1)};
     unsigned long long cand = 0;
     int rounds = 0;
-    // 1. bound: grow a box around Q until every lane holds a candidate
+    // 1. bound: grow a box around Q until every lane holds a candidate;
+    // 2. final: everything within sqrt(B) of the tile box, minus what was scanned
     CellBox S{1, 0, 1, 0, 1, 0};  // scanned so far (empty)
     int r = 0;
-    while (__any(act && (uint32_t)best == (uint32_t)kNone)) {
-        const CellBox N{max(Q.x0 - r, 0), min(Q.x1 + r, g.nx - 1), max(Q.y0 - r, 0), min(Q.y1 + r, g.ny - 1),
+    for (;;) {
+        const bool grow = __any(act && (uint32_t)best == (uint32_t)kNone);  // block-uniform (lists merged)
+        CellBox N;
+        float B = INFINITY;
+        if (grow) {
+            N = CellBox{max(Q.x0 - r, 0), min(Q.x1 + r, g.nx - 1), max(Q.y0 - r, 0), min(Q.y1 + r, g.ny - 1),
                         max(Q.z0 - r, 0), min(Q.z1 + r, g.nz - 1)};
-        scan_rows(g, L, N, S, INFINITY, qx0, qx1, qy0, qy1, qz0, qz1, act, x, y, z, best, cand);
-        best = tile_min(best, s_best);
-        ++rounds;
-        S = N;
-        if (N.x0 == 0 && N.y0 == 0 && N.z0 == 0 && N.x1 == g.nx - 1 && N.y1 == g.ny - 1 && N.z1 == g.nz - 1) break;
-        r = 2 * r + 1;
-    }
-    // 2. final: everything within sqrt(B) of the tile box, minus S
-    const float B = uni_f(wave_max_f(act ? __uint_as_float((uint32_t)(best >> 32)) : 0.f));
-    if (B < INFINITY) {
-        const float R = sqrtf(B) * 1.00001f + g.margin;
-        const CellBox N{max(cell_coord(qx0 - R, g.ox, g.inv_cell), 0), min(cell_coord(qx1 + R, g.ox, g.inv_cell), g.nx - 1),
+        } else {
+            B = uni_f(wave_max_f(act ? __uint_as_float((uint32_t)(best >> 32)) : 0.f));
+            const float R = sqrtf(B) * 1.00001f + g.margin;
+            N = CellBox{max(cell_coord(qx0 - R, g.ox, g.inv_cell), 0), min(cell_coord(qx1 + R, g.ox, g.inv_cell), g.nx - 1),
                         max(cell_coord(qy0 - R, g.oy, g.inv_cell), 0), min(cell_coord(qy1 + R, g.oy, g.inv_cell), g.ny - 1),
                         max(cell_coord(qz0 - R, g.oz, g.inv_cell), 0), min(cell_coord(qz1 + R, g.oz, g.inv_cell), g.nz - 1)};
-        // S may stick out of N (a grown box): clip it, the part outside N is not needed
+        }
+        // the scanned box may stick out of N (a grown box): clip it, the part outside N is not needed
         CellBox Sc{max(S.x0, N.x0), min(S.x1, N.x1), max(S.y0, N.y0), min(S.y1, N.y1), max(S.z0, N.z0), min(S.z1, N.z1)};
         if (Sc.y0 > Sc.y1 || Sc.z0 > Sc.z1) Sc.x0 = 1, Sc.x1 = 0;
-        scan_rows(g, L, N, Sc, B, qx0, qx1, qy0, qy1, qz0, qz1, act, x, y, z, best, cand);
-        best = tile_min(best, s_best);
+        scan_rows<NW>(g, L, N, Sc, B, qx0, qx1, qy0, qy1, qz0, qz1, act, x, y, z, best, cand);
+        best = tile_min<NW>(best, s_best);
         ++rounds;
+        const bool full = N.x0 == 0 && N.y0 == 0 && N.z0 == 0 && N.x1 == g.nx - 1 && N.y1 == g.ny - 1 && N.z1 == g.nz - 1;
+        if (!grow || full) break;  // final pass done, or the whole grid scanned
+        S = N;
+        r = 2 * r + 1;
     }
     if (a.dbg && threadIdx.x == 0) {
         atomicAdd(a.dbg, cand);
@@ -324,11 +324,6 @@ __global__ void __launch_bounds__(kIcpTileQ * kTileWaves) icp_tile_kernel(IcpArg
     }
 }
 
-__device__ __forceinline__ double wsum(double v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
 
 // one block = one 256-point chunk -> partials[chunk][kIcpStride]
 __global__ void __launch_bounds__(256) icp_stats_kernel(IcpArgs a) {
@@ -359,12 +354,12 @@ __global__ void __launch_bounds__(256) icp_stats_kernel(IcpArgs a) {
             v[16] = (double)d2;
         }
     }
-#pragma unroll
-    for (int k = 0; k < 17; ++k) v[k] = wsum(v[k]);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    if (lane == 0)
 #pragma unroll
-        for (int k = 0; k < 17; ++k) red[wid][k] = v[k];
+    for (int k = 0; k < 17; ++k) {  // DPP row reductions: the wave total lands in lane 63
+        const double t = wave_sum_to_lane63(v[k]);
+        if (lane == 63) red[wid][k] = t;
+    }
     __syncthreads();
     if (threadIdx.x < kIcpStride) {
         double s = 0.0;
@@ -387,7 +382,16 @@ __global__ void icp_reduce_kernel(const double* __restrict__ partials, int nchun
 
 void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st) {
     if (a.n == 0 || ntiles == 0) return;
-    icp_tile_kernel<<<ntiles, kIcpTileQ * kTileWaves, 0, st>>>(a);
+    static const int nw = [] {  // LIO_ICP_TILE_WAVES: diagnostics override (1, 2, 4)
+        const char* e = std::getenv("LIO_ICP_TILE_WAVES");
+        return e ? std::atoi(e) : 2;
+    }();
+    if (nw == 1)
+        icp_tile_kernel<1><<<ntiles, kIcpTileQ, 0, st>>>(a);
+    else if (nw == 4)
+        icp_tile_kernel<4><<<ntiles, kIcpTileQ * 4, 0, st>>>(a);
+    else  // 2 waves per tile: measured best (scripts/icp_exp.sh)
+        icp_tile_kernel<2><<<ntiles, kIcpTileQ * 2, 0, st>>>(a);
 }
 
 // per cell: number of tiles (ceil(count / 64)); slot ncells = 0 for the scan's total

@@ -1,13 +1,10 @@
 #!/bin/bash
-# ICP (C4) tile-kernel sweep: target cell x tile cell, with ICP parity tests first.
+# ICP (C4) tile-kernel check: exactness tests, then timing vs target cell size (tile cell via LIO_ICP_TILE_CELL).
 set -u
 export TMPDIR=/tmp
-OUT=gpurun_out/icpexp2; mkdir -p $OUT
-timeout -k 10 300 python -u -m pytest tests -q -m gpu -k "icp or ICP or loop" -p no:cacheprovider > $OUT/parity.log 2>&1
-rc=$?; tail -5 $OUT/parity.log; [ $rc -ne 0 ] && exit $rc
-for tc in 2.0 3.0 1.5; do
-  LIO_ICP_TILE_CELL=$tc timeout -k 10 200 python scripts/icp_cells.py 0.5,0.75,1.0,1.5,2.0 > $OUT/t$tc.log 2>&1 || exit $?
-  echo "tile=$tc"; cat $OUT/t$tc.log
-done
+OUT=gpurun_out/icpexp; mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest tests/test_gpu_icp.py tests/test_gpu_parity.py -q -m gpu -k "icp or ICP" -p no:cacheprovider --timeout 120 --timeout-method thread > $OUT/tests.log 2>&1; rc=$?; tail -3 $OUT/tests.log; [ $rc -ne 0 ] && exit $rc
+for tc in ${TILES:-2.0}; do echo tile=$tc; LIO_ICP_TILE_CELL=$tc timeout -k 10 120 python scripts/icp_cells.py ${CELLS:-0.75,1.0} 2>&1 | grep -E 'cell='; done
+LIO_ICP_DEBUG=1 timeout -k 10 120 python scripts/icp_cells.py 1.0 2>&1 | grep -E 'dbg' | sort | uniq -c | head -3
 timeout -k 10 200 rocprofv3 --kernel-trace --stats -d $OUT/prof -o run --output-format csv -- python scripts/icp_cells.py 1.0 > $OUT/prof.log 2>&1 || exit $?
-grep -h icp_ $(find $OUT/prof -name '*kernel_stats.csv') | cut -d, -f1-4
+grep -h -E 'icp_|tile_' $(find $OUT/prof -name '*kernel_stats.csv') | cut -d, -f1-4
