@@ -113,6 +113,7 @@ struct lio_ctx {
     lio_pose knn_pose{};  // pose of the last kNN evaluation (Nearest_Points)
     int* d_far_list = nullptr;  // far-pass queue (cap), its length, and queued lists (cap*5)
     int* d_far_count = nullptr;
+    unsigned* d_done = nullptr;  // plane/reuse block counter (last block publishes)
     float* d_far_d = nullptr;
     int* d_far_id = nullptr;
     bool have_eval = false;
@@ -423,7 +424,8 @@ int lio_ctx_create(lio_map* m, const lio_match_params* p, lio_ctx** out) {
         hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_sums_dev), c->h_sums, 0) != hipSuccess ||
         hipMalloc(&c->d_nrows, sizeof(int64_t)) != hipSuccess ||
         hipMalloc(&c->d_far_count, sizeof(int)) != hipSuccess ||
-        hipMemset(c->d_far_count, 0, sizeof(int)) != hipSuccess) {
+        hipMemset(c->d_far_count, 0, sizeof(int)) != hipSuccess || hipMalloc(&c->d_done, 64) != hipSuccess ||
+        hipMemset(c->d_done, 0, 64) != hipSuccess) {
         delete c;
         return fail(LIO_ERR_NOMEM, "context allocation failed");
     }
@@ -441,7 +443,7 @@ int lio_ctx_destroy(lio_ctx* c) {
     (void)hipSetDevice(c->map->dev);
     (void)hipStreamSynchronize(c->map->st);
     void* ptrs[] = {c->d_body,  c->d_nn,    c->d_planes,   c->d_sel,       c->d_partials, c->d_sums,
-                    c->d_rows,  c->d_nrows, c->d_far_list, c->d_far_count, c->d_far_d,    c->d_far_id};
+                    c->d_rows,  c->d_nrows, c->d_far_list, c->d_far_count, c->d_far_d,    c->d_far_id, c->d_done};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (c->h_sums) (void)hipHostFree(c->h_sums);
@@ -539,6 +541,12 @@ static lio::MatchArgs make_args(lio_ctx* c, const lio_pose& pose) {
     a.seq = 0;
     a.far_list = c->d_far_list;
     a.far_count = c->d_far_count;
+    a.done_count = c->d_done;
+    static const int fused = [] {  // LIO_FUSED_FINAL=0: separate finalize launch (A/B diagnostics)
+        const char* e = std::getenv("LIO_FUSED_FINAL");
+        return e ? std::atoi(e) : 1;
+    }();
+    a.fused_final = fused;
     a.far_d = c->d_far_d;
     a.far_id = c->d_far_id;
     a.range_sq = c->p.knn_range_sq;
@@ -602,7 +610,7 @@ int lio_match(lio_ctx* c, const lio_pose* pose, int redo_knn, double* sums) {
     if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.a, st));
     const int nb = lio::launch_h_model(a, redo_knn != 0, st, c->timing && redo_knn ? c->ev_marks : nullptr);
     if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.b, st));
-    lio::launch_finalize(a, nb, st);
+    lio::launch_finalize(a, nb, st);  // no-op: the last plane/reuse block publishes the sums
     if (c->timing) HIP_TRY(hipEventRecord(c->ev_fin.b, st));
     HIP_TRY(hipGetLastError());
     const auto t1 = std::chrono::steady_clock::now();
@@ -644,8 +652,7 @@ int lio_ctx_knn_stats(lio_ctx* c, const lio_pose* pose, double* sums, int32_t* s
     lio::MatchArgs a = make_args(c, *pose);
     a.dbg = d_dbg;
     a.seq = ++c->seq;
-    const int nb = lio::launch_h_model(a, true, st);
-    lio::launch_finalize(a, nb, st);
+    lio::launch_finalize(a, lio::launch_h_model(a, true, st), st);
     hipError_t e2 = hipMemcpyAsync(stats3, d_dbg, c->n * 3 * sizeof(int), hipMemcpyDeviceToHost, st);
     hipError_t e3 = hipStreamSynchronize(st);
     (void)hipFree(d_dbg);

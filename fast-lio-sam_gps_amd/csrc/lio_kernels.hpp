@@ -22,6 +22,8 @@ struct MatchArgs {
     int* dbg;                 // optional n*3 search statistics (diagnostics only)
     int* far_list;            // n: points queued for the far pass
     int* far_count;           // queue length (reset to 0 by plane_kernel)
+    unsigned* done_count;     // blocks of plane/reuse finished (0 between launches; the last block resets it)
+    int fused_final;          // 1: the last plane/reuse block publishes the sums; 0: launch_finalize does
     float* far_d;             // n*5 their near-pass lists
     int* far_id;
     int n;
@@ -36,7 +38,7 @@ struct MatchArgs {
 int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* marks = nullptr);
 void launch_debug(const MatchArgs& a, float* world, float* d2, float* abcd_pd2, hipStream_t st);
 void launch_h_rows(const MatchArgs& a, double* rows, int64_t max_rows, int64_t* n_rows, hipStream_t st);
-void launch_finalize(const MatchArgs& a, int nblocks, hipStream_t st);  // -> sums_out, seq_out
+void launch_finalize(const MatchArgs& a, int nblocks, hipStream_t st);  // no-op when fused_final
 int match_blocks(int n);
 // batch Nearest_Search: k <= 5 neighbours per query within d2 <= bound (INFINITY: unbounded)
 void launch_map_knn(const GridDev& g, const float* q, int n, float bound, int max_shell, int k, int32_t* idx,

@@ -14,8 +14,9 @@
 //     writes: nn_idx[5] (20 B), plane abcd (16 B), sel (1 B)
 //   ekfom_data.converge == false: h_model_reuse_kernel, lane = point
 //     body->world -> cached plane -> pd2, s-gate -> H row -> block partial
-//   finalize_kernel: sums the block partials in a fixed order (deterministic)
-//     into host-mapped memory + a sequence number (zero-copy result)
+//   the last block of plane/reuse to finish (agent-scope counter) sums the
+//     block partials in a fixed order (deterministic) into host-mapped memory
+//     + a sequence number (zero-copy result, no finalize launch)
 //
 // The per-point dense H (effct x 12 doubles) of the reference is never
 // materialised: the IESKF only consumes H^T H and H^T h.
@@ -169,6 +170,81 @@ __global__ void __launch_bounds__(kFarBlock) knn_far_kernel(MatchArgs a) {
     }
 }
 
+// Block partial -> global, and the LAST block to finish sums all partials
+// (fixed order: deterministic) into the host-mapped result + sequence number,
+// so no separate finalize launch.  Hand-off per MI355X_MICROARCH.md
+// § visibility, row "one lane of each storing workgroup ... agent-scope atomic
+// add / the workgroup whose add came last": the partial is stored
+// write-through (sc1: agent-scope relaxed atomic store), the storing wave
+// drains (vmcnt(0)), a barrier, ONE lane adds to the counter; the block
+// whose add returns nblocks-1 reads every partial with sc1 loads
+// (agent-scope relaxed atomic loads) after a barrier.  No release fence (an
+// agent release per block writes back the XCD's L2: 8 -> 35 us measured).
+typedef __attribute__((address_space(1))) double gdouble;
+typedef __attribute__((address_space(1))) unsigned int guint;
+
+__device__ __forceinline__ void publish_and_finalize(const MatchArgs& a, double (*red)[32]) {
+    __shared__ int s_last;
+    const int nb = (int)gridDim.x;
+    if (!a.fused_final) {  // separate finalize_kernel launch (A/B switch LIO_FUSED_FINAL=0)
+        if (threadIdx.x < 32) {
+            double s = 0.0;
+#pragma unroll
+            for (int w = 0; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
+            a.partials[(size_t)blockIdx.x * 32 + threadIdx.x] = s;
+        }
+        return;
+    }
+    if (threadIdx.x < 32) {
+        double s = 0.0;
+#pragma unroll
+        for (int w = 0; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
+        __hip_atomic_store((gdouble*)(a.partials + (size_t)blockIdx.x * 32 + threadIdx.x), s, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing wave drains
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned old = __hip_atomic_fetch_add((guint*)a.done_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = old == (unsigned)(nb - 1);
+    }
+    __syncthreads();
+    if (!s_last) return;  // block-uniform
+    // fixed-order sum: 8 row groups x 32 columns, then the groups in order
+    const int col = threadIdx.x & 31, grp = threadIdx.x >> 5;
+    constexpr int NG = kBlock / 32;
+    const int per = (nb + NG - 1) / NG;
+    const int b0 = grp * per, b1 = min(nb, b0 + per);
+    double acc = 0.0;
+    int b = b0;
+    for (; b + 16 <= b1; b += 16) {  // 16 sc1 loads in flight per thread (cross-XCD: each batch is an L2 miss)
+        double v[16];
+#pragma unroll
+        for (int k = 0; k < 16; ++k)
+            v[k] = __hip_atomic_load((gdouble*)(a.partials + (size_t)(b + k) * 32 + col), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc += v[k];
+    }
+    for (; b < b1; ++b)
+        acc += __hip_atomic_load((gdouble*)(a.partials + (size_t)b * 32 + col), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __shared__ double sg[NG][33];
+    sg[grp][col] = acc;
+    __syncthreads();
+    if (threadIdx.x < 32) {
+        double t = 0.0;
+#pragma unroll
+        for (int g = 0; g < NG; ++g) t += sg[g][threadIdx.x];
+        a.sums_out[threadIdx.x] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        __hip_atomic_store((guint*)a.done_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+        __threadfence_system();
+        *reinterpret_cast<volatile unsigned long long*>(a.seq_out) = a.seq;
+    }
+}
+
 // Pass 3, lane = point: gate (found == 5 && d2[4] <= 5), esti_plane, pd2,
 // s-gate, H row, 4 wave partials combined in LDS -> block partial.  Resets
 // the far queue for the next kNN evaluation.
@@ -209,12 +285,7 @@ __global__ void __launch_bounds__(kBlock) plane_kernel(MatchArgs a) {
     const int wid = threadIdx.x >> 6;
     wave_reduce_store(J, h, res, cnt, red[wid]);
     __syncthreads();
-    if (threadIdx.x < 32) {
-        double s = 0.0;
-#pragma unroll
-        for (int w = 0; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
-        a.partials[(size_t)blockIdx.x * 32 + threadIdx.x] = s;
-    }
+    publish_and_finalize(a, red);
     if (blockIdx.x == 0 && threadIdx.x == 0) *a.far_count = 0;
 }
 
@@ -239,12 +310,7 @@ __global__ void __launch_bounds__(kBlock) h_model_reuse_kernel(MatchArgs a) {
     const int wid = threadIdx.x >> 6;
     wave_reduce_store(J, h, res, cnt, red[wid]);
     __syncthreads();
-    if (threadIdx.x < 32) {
-        double s = 0.0;
-#pragma unroll
-        for (int w = 0; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
-        a.partials[(size_t)blockIdx.x * 32 + threadIdx.x] = s;
-    }
+    publish_and_finalize(a, red);
 }
 
 // Fixed-order sum of nblocks x 32 partials -> 32 sums (one block of 1024):
@@ -427,8 +493,9 @@ void launch_h_rows(const MatchArgs& a, double* rows, int64_t max_rows, int64_t* 
     h_rows_kernel<<<1, 1024, 0, st>>>(a, rows, max_rows, n_rows);
 }
 
+
 void launch_finalize(const MatchArgs& a, int nblocks, hipStream_t st) {
-    finalize_kernel<<<1, 1024, 0, st>>>(a.partials, nblocks, a.sums_out, a.seq_out, a.seq);
+    if (!a.fused_final) finalize_kernel<<<1, 1024, 0, st>>>(a.partials, nblocks, a.sums_out, a.seq_out, a.seq);
 }
 
 void launch_map_knn(const GridDev& g, const float* q, int n, float bound, int max_shell, int k, int32_t* idx,
