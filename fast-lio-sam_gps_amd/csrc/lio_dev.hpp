@@ -128,11 +128,32 @@ __device__ __forceinline__ float axis_gap(float q, float lo, float hi) {
 // private K-th bests (>= the group's true K-th best, so pruning stays exact),
 // and a butterfly merge leaves the exact group top-K in every lane.
 // ----------------------------------------------------------------------------
-template <int G>
+// Exchange with the partner lane of butterfly round `off` inside aligned
+// groups of 8: DPP lane permutations on the VALU (no LDS round trip).  Round
+// 1 and 2 are xor 1 / xor 2 (quad_perm); round 4 pairs lane i with 7 - i
+// (row_half_mirror) — a different matching than xor 4, equally valid for
+// butterfly min / merge since after rounds 1-2 all lanes of a quad agree.
+// Other offsets (groups wider than 8) fall back to ds_bpermute.
+template <int OFF>
+__device__ __forceinline__ uint32_t partner_u32(uint32_t v) {
+    if constexpr (OFF == 1) return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xb1, 0xf, 0xf, false);
+    else if constexpr (OFF == 2) return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4e, 0xf, 0xf, false);
+    else if constexpr (OFF == 4) return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x141, 0xf, 0xf, false);
+    else return (uint32_t)__shfl_xor((int)v, OFF, 64);
+}
+template <int OFF>
+__device__ __forceinline__ float partner_f(float v) {
+    return __uint_as_float(partner_u32<OFF>(__float_as_uint(v)));
+}
+
+template <int G, int OFF = 1>
 __device__ __forceinline__ float group_min(float v) {
-#pragma unroll
-    for (int off = 1; off < G; off <<= 1) v = fminf(v, __shfl_xor(v, off, 64));
-    return v;
+    if constexpr (OFF >= G) {
+        return v;
+    } else {
+        v = fminf(v, partner_f<OFF>(v));
+        return group_min<G, 2 * OFF>(v);
+    }
 }
 
 // Sort a bitonic (non-decreasing, then non-increasing) list in place.
@@ -158,21 +179,21 @@ __device__ __forceinline__ void sort_bitonic(uint64_t (&v)[K]) {
 // Butterfly merge over the G lanes of a group: per round the K smallest of
 // the two (disjoint) sorted lists are min(a[j], b[K-1-j]) — a bitonic
 // sequence — then sorted.  Afterwards every lane holds the group's top-K.
-template <int K, int G>
+template <int K, int G, int OFF = 1>
 __device__ __forceinline__ void group_merge(TopK<K>& tk) {
-#pragma unroll
-    for (int off = 1; off < G; off <<= 1) {
+    if constexpr (OFF < G) {
         uint64_t c[K];
 #pragma unroll
         for (int j = 0; j < K; ++j) {
-            const uint32_t lo = __shfl_xor((uint32_t)tk.k[K - 1 - j], off, 64);
-            const uint32_t hi = __shfl_xor((uint32_t)(tk.k[K - 1 - j] >> 32), off, 64);
+            const uint32_t lo = partner_u32<OFF>((uint32_t)tk.k[K - 1 - j]);
+            const uint32_t hi = partner_u32<OFF>((uint32_t)(tk.k[K - 1 - j] >> 32));
             const uint64_t b = ((uint64_t)hi << 32) | lo;
             c[j] = b < tk.k[j] ? b : tk.k[j];
         }
         sort_bitonic<K>(c);
 #pragma unroll
         for (int j = 0; j < K; ++j) tk.k[j] = c[j];
+        group_merge<K, G, 2 * OFF>(tk);
     }
 }
 
@@ -380,13 +401,27 @@ __device__ __forceinline__ void scan_shell1_flat(const GridDev& g, float qx, flo
         if (dbg && n4[j]) dbg->cells += 1;
         lane_total += n4[j];
     }
-    uint32_t incl = lane_total;
+    uint32_t incl = lane_total, T;
+    if constexpr (G == 8) {  // DPP row shifts (lanes from the neighbouring group are masked by sub >= off)
+        uint32_t v = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x111, 0xf, 0xf, false);  // row_shr:1
+        if (sub >= 1) incl += v;
+        v = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x112, 0xf, 0xf, false);  // row_shr:2
+        if (sub >= 2) incl += v;
+        v = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x114, 0xf, 0xf, false);  // row_shr:4
+        if (sub >= 4) incl += v;
+        uint32_t t = lane_total;  // group total by butterfly (integer: order-free)
+        t += partner_u32<1>(t);
+        t += partner_u32<2>(t);
+        t += partner_u32<4>(t);
+        T = t;
+    } else {
 #pragma unroll
-    for (int off = 1; off < G; off <<= 1) {
-        const uint32_t v = __shfl_up(incl, off, G);
-        if (sub >= off) incl += v;
+        for (int off = 1; off < G; off <<= 1) {
+            const uint32_t v = __shfl_up(incl, off, G);
+            if (sub >= off) incl += v;
+        }
+        T = __shfl(incl, G - 1, G);
     }
-    const uint32_t T = __shfl(incl, G - 1, G);
     uint32_t o = incl - lane_total;
     uint32_t* s_b = lds;
     uint32_t* s_off = lds + CPL * G;
