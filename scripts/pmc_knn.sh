@@ -19,10 +19,10 @@ while read -r ctrs; do
 done <<'EOF'
 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY
 SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_BUSY_CYCLES SQ_INSTS_BRANCH SQ_INSTS_SMEM SQ_INSTS_VMEM_WR
-
-
-
-
+SQC_ICACHE_MISSES SQC_ICACHE_HITS SQ_IFETCH SQC_DCACHE_MISSES
+TCP_UTCL1_TRANSLATION_MISS TCP_UTCL1_TRANSLATION_HIT TCC_HIT TCC_MISS
+FETCH_SIZE
+WRITE_SIZE
 EOF
 python - "$OUT" <<'PY'
 import csv, glob, os, sys, collections
