@@ -606,6 +606,14 @@ int lio_match(lio_ctx* c, const lio_pose* pose, int redo_knn, double* sums) {
         return LIO_OK;
     }
     a.seq = ++c->seq;
+    static const char* tdir = std::getenv("LIO_KNN_TDBG");  // diagnostics: per-wave near-pass timestamps
+    unsigned long long* d_t = nullptr;
+    const size_t nwaves = (size_t)((c->n + 63) / 64) * 8;
+    if (tdir && redo_knn) {
+        HIP_TRY(hipMalloc(&d_t, nwaves * 16));
+        HIP_TRY(hipMemsetAsync(d_t, 0, nwaves * 16, st));
+        a.tdbg = d_t;
+    }
     const auto t0 = std::chrono::steady_clock::now();
     if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.a, st));
     const int nb = lio::launch_h_model(a, redo_knn != 0, st, c->timing && redo_knn ? c->ev_marks : nullptr);
@@ -617,6 +625,18 @@ int lio_match(lio_ctx* c, const lio_pose* pose, int redo_knn, double* sums) {
     int rc = wait_result(c, a.seq, sums);
     if (rc) return rc;
     const auto t2 = std::chrono::steady_clock::now();
+    if (d_t) {
+        std::vector<unsigned long long> h(nwaves * 2);
+        HIP_TRY(hipMemcpy(h.data(), d_t, nwaves * 16, hipMemcpyDeviceToHost));
+        (void)hipFree(d_t);
+        static int k = 0;
+        char fn[512];
+        std::snprintf(fn, sizeof(fn), "%s/near_%d.bin", tdir, k++);
+        if (FILE* f = std::fopen(fn, "wb")) {
+            std::fwrite(h.data(), 8, h.size(), f);
+            std::fclose(f);
+        }
+    }
     c->last_launch_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     c->last_wait_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
     if (c->timing) {

@@ -382,14 +382,16 @@ __device__ __forceinline__ void shell1_ranges(const GridDev& g, int cx, int cy, 
     }
 }
 
+// The pruned shell-1 ranges of a group's query, concatenated into the
+// group's LDS slot table (lds[0..32) range starts, lds[32..65) offsets);
+// returns the total point count T (group-uniform).
 template <int K, int G>
-__device__ __forceinline__ void scan_shell1_flat(const GridDev& g, float qx, float qy, float qz, int cx, int cy,
-                                                 int cz, float lox, float loy, float loz, int sub, uint32_t* lds,
-                                                 uint32_t* b4, uint32_t* n4, TopK<K>& tk, SearchStats* dbg) {
+__device__ __forceinline__ uint32_t shell1_table(const GridDev& g, float qx, float qy, float qz, float lox, float loy,
+                                                 float loz, int sub, uint32_t* lds, uint32_t* b4, uint32_t* n4,
+                                                 float bound, SearchStats* dbg) {
     constexpr int CPL = shell1_cpl<G>();
-    static_assert(CPL * G <= 32, "scan_shell1_flat: slot table holds 32 ranges");
+    static_assert(CPL * G == 32, "shell1_table: slot table = 32 range starts + 33 offsets");
     const float cs = g.cell, m = g.margin, w = cs + 2.f * m;
-    const float bound = tk.worst();
     uint32_t lane_total = 0;
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {  // prune the preloaded ranges against the own-cell bound
@@ -433,18 +435,25 @@ __device__ __forceinline__ void scan_shell1_flat(const GridDev& g, float qx, flo
     }
     if (sub == G - 1) s_off[CPL * G] = T;
     if (dbg && sub == 0) dbg->points += (int)T;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return T;
+}
+
+// Lane `r` of `L` lanes strides the concatenated table [0, T) (two loads in
+// flight per lane) and pushes every point into its private list.
+template <int K>
+__device__ __forceinline__ void scan_table_strided(const GridDev& g, float qx, float qy, float qz, const uint32_t* lds,
+                                                   uint32_t T, uint32_t r, uint32_t L, TopK<K>& tk) {
+    const uint32_t* s_b = lds;
+    const uint32_t* s_off = lds + 32;
     int sl = 0;
     uint32_t lo = 0, hi = s_off[1];
-    for (uint32_t t = (uint32_t)sub; t < T; t += 2 * G) {
+    for (uint32_t t = r; t < T; t += 2 * L) {
         while (t >= hi) {
             lo = hi;
             hi = s_off[++sl + 1];
         }
         const float4 p0 = g.pts[s_b[sl] + (t - lo)];
-        const uint32_t t2 = t + G;
+        const uint32_t t2 = t + L;
         float4 p1 = make_float4(0.f, 0.f, 0.f, 0.f);
         if (t2 < T) {
             while (t2 >= hi) {
@@ -456,6 +465,18 @@ __device__ __forceinline__ void scan_shell1_flat(const GridDev& g, float qx, flo
         tk.push(sqdist3(qx, qy, qz, p0.x, p0.y, p0.z), __float_as_int(p0.w));
         if (t2 < T) tk.push(sqdist3(qx, qy, qz, p1.x, p1.y, p1.z), __float_as_int(p1.w));
     }
+}
+
+template <int K, int G>
+__device__ __forceinline__ void scan_shell1_flat(const GridDev& g, float qx, float qy, float qz, int cx, int cy,
+                                                 int cz, float lox, float loy, float loz, int sub, uint32_t* lds,
+                                                 uint32_t* b4, uint32_t* n4, TopK<K>& tk, SearchStats* dbg) {
+    (void)cx, (void)cy, (void)cz;
+    const uint32_t T = shell1_table<K, G>(g, qx, qy, qz, lox, loy, loz, sub, lds, b4, n4, tk.worst(), dbg);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    scan_table_strided<K>(g, qx, qy, qz, lds, T, (uint32_t)sub, (uint32_t)G, tk);
 }
 
 // Lean group walk for dense maps (front-end kNN, ICP near pass), written for

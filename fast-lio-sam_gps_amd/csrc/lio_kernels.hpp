@@ -20,6 +20,7 @@ struct MatchArgs {
     unsigned long long* seq_out;  // written with `seq` after sums_out (host-mapped)
     unsigned long long seq;
     int* dbg;                 // optional n*3 search statistics (diagnostics only)
+    unsigned long long* tdbg; // optional per-wave (start, end) wall clock of the near pass (diagnostics only)
     int* far_list;            // n: points queued for the far pass
     int* far_count;           // queue length (reset to 0 by plane_kernel)
     unsigned* done_count;     // blocks of plane/reuse finished (0 between launches; the last block resets it)

@@ -102,6 +102,7 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
     const int blk = xcd_block(blockIdx.x, gridDim.x);
     const int sub = threadIdx.x % G;
     const int i = blk * QPB + threadIdx.x / G;
+    const unsigned long long t_beg = a.tdbg ? wall_clock64() : 0ull;
     if (i >= a.n) return;
     const float bx = a.body[3 * i], by = a.body[3 * i + 1], bz = a.body[3 * i + 2];
     float wx, wy, wz;
@@ -134,6 +135,11 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
                 a.far_id[5 * (size_t)slot + j] = tk.id(j);
             }
         }
+        if (a.tdbg && (threadIdx.x & 63) == 0) {
+            const size_t wv = (size_t)blockIdx.x * (kKnnBlock / 64) + (threadIdx.x >> 6);
+            a.tdbg[2 * wv] = t_beg;
+            a.tdbg[2 * wv + 1] = wall_clock64();
+        }
         return;
     }
 #pragma unroll
@@ -146,6 +152,11 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
                 if (jj == j) v = tk.id(j);
             a.nn_idx[5 * (size_t)i + jj] = v == kNone ? -1 : v;
         }
+    }
+    if (a.tdbg && (threadIdx.x & 63) == 0) {
+        const size_t wv = (size_t)blockIdx.x * (kKnnBlock / 64) + (threadIdx.x >> 6);
+        a.tdbg[2 * wv] = t_beg;
+        a.tdbg[2 * wv + 1] = wall_clock64();
     }
 }
 
