@@ -116,6 +116,12 @@ def main():
         x = -0.15 * L + (k + rank * args.scans) * 3.7
         scans.append(synth.make_scan(scene, sp, kind, pos_gt=[x, 0.6 * np.sin(0.7 * k), 0.0],
                                      yaw_gt=0.05 * np.sin(0.3 * k), seed=99 + k + 1000 * rank))
+    if os.environ.get("LIO_BENCH_PERMUTE") == "tiles":  # diagnostics: spatially tiled query order
+        for sc in scans:
+            b = sc.body.astype(np.float64)
+            t = np.floor(b[:, :2] / float(os.environ.get("LIO_BENCH_TILE", "8"))).astype(np.int64)
+            t -= t.min(axis=0)
+            sc.body = np.ascontiguousarray(sc.body[np.lexsort((b[:, 2], t[:, 0], t[:, 1]))])
     gen_s = time.time() - t0
     d_map = torch.from_numpy(mappts).to(dev)
     d_scans = [torch.from_numpy(s.body).to(dev) for s in scans]

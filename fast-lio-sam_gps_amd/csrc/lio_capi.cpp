@@ -72,6 +72,7 @@ struct EventPair {
 // map
 // =============================================================================
 struct lio_map {
+    uint64_t version = 0;  // bumped by every change of the point set (seeded kNN validity)
     int dev = 0;
     hipStream_t st = nullptr;
     lio_map_params p{};
@@ -118,6 +119,7 @@ struct lio_ctx {
     int* d_far_id = nullptr;
     bool have_eval = false;
     bool knn_valid = false;
+    uint64_t knn_map_version = 0;  // map version of the last kNN evaluation
     // timing
     bool timing = false;
     lio_kernel_timing tm{};
@@ -188,6 +190,7 @@ static int map_build_impl(lio_map* m, const float* d_xyz, int64_t n) {
     if (rc != 0) return fail(LIO_ERR_HIP, "grid build failed");
     HIP_TRY(hipStreamSynchronize(m->st));
     m->n = m->grid.n;
+    ++m->version;
     return LIO_OK;
 }
 
@@ -308,6 +311,7 @@ int lio_map_add_device(lio_map* m, const float* d_xyz, int64_t n, int downsample
                                  m->st);
     HIP_TRY(hipStreamSynchronize(m->st));
     m->n = m->grid.n;
+    ++m->version;
     if (n_added) *n_added = out[0];
     return map_status(rc, "lio_map_add");
 }
@@ -332,6 +336,7 @@ int lio_map_delete_boxes(lio_map* m, const float* boxes, int nb, int64_t* n_dele
     int rc = lio::map_delete_boxes(m->grid, m->upd, boxes, nb, map_slack(m), &nd, m->st);
     HIP_TRY(hipStreamSynchronize(m->st));
     m->n = m->grid.n;
+    ++m->version;
     if (n_deleted) *n_deleted = nd;
     return map_status(rc, "lio_map_delete_boxes");
 }
@@ -602,10 +607,17 @@ int lio_match(lio_ctx* c, const lio_pose* pose, int redo_knn, double* sums) {
         c->last_pose = *pose;
         c->have_eval = true;
         c->knn_valid = true;
+        c->knn_map_version = c->map->version;
         c->knn_pose = *pose;
         return LIO_OK;
     }
     a.seq = ++c->seq;
+    // later kNN evaluations of the same scan against the same map start from the previous lists
+    static const bool seed_ok = [] {  // LIO_KNN_SEED=0: always the unseeded near pass (A/B diagnostics)
+        const char* e = std::getenv("LIO_KNN_SEED");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    a.prior = (seed_ok && redo_knn && c->knn_valid && c->knn_map_version == c->map->version) ? 1 : 0;
     static const char* tdir = std::getenv("LIO_KNN_TDBG");  // diagnostics: per-wave near-pass timestamps
     unsigned long long* d_t = nullptr;
     const size_t nwaves = (size_t)((c->n + 63) / 64) * 8;
@@ -656,6 +668,7 @@ int lio_match(lio_ctx* c, const lio_pose* pose, int redo_knn, double* sums) {
     c->have_eval = true;
     if (redo_knn) {
         c->knn_valid = true;
+        c->knn_map_version = c->map->version;
         c->knn_pose = *pose;
     }
     return LIO_OK;
@@ -683,6 +696,7 @@ int lio_ctx_knn_stats(lio_ctx* c, const lio_pose* pose, double* sums, int32_t* s
     c->knn_pose = *pose;
     c->have_eval = true;
     c->knn_valid = true;
+    c->knn_map_version = c->map->version;
     return LIO_OK;
 }
 
@@ -715,6 +729,7 @@ int lio_map_incremental(lio_ctx* c, const lio_pose* pose, double filter_size_map
     rc = lio::map_incremental(m->grid, m->upd, a, m->p.downsample_size, map_slack(m), out, m->st);
     HIP_TRY(hipStreamSynchronize(m->st));
     m->n = m->grid.n;
+    ++m->version;
     c->knn_valid = false;  // ids/grid changed
     if (st) {
         st->n_to_add = out[0];

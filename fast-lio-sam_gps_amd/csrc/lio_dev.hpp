@@ -208,18 +208,21 @@ __device__ __forceinline__ void scan_cell_group(const GridDev& g, uint32_t c, fl
     }
 }
 
-// Lane-strided scan of one cell by the group, two loads in flight per lane.
+// Lane-strided scan of one cell by the group, four loads in flight per lane
+// (the addresses clamped to the cell's last point; only real ones pushed).
 template <int K, int G>
 __device__ __forceinline__ void scan_cell_group2(const GridDev& g, uint32_t c, float qx, float qy, float qz, int sub,
                                                  TopK<K>& tk) {
+    constexpr int U = 4;
     const uint32_t b = g.start[c];
     const uint32_t e = g.start[c + 1];
-    for (uint32_t j = b + (uint32_t)sub; j < e; j += 2 * G) {
-        const float4 p0 = g.pts[j];
-        float4 p1 = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (j + G < e) p1 = g.pts[j + G];
-        tk.push(sqdist3(qx, qy, qz, p0.x, p0.y, p0.z), __float_as_int(p0.w));
-        if (j + G < e) tk.push(sqdist3(qx, qy, qz, p1.x, p1.y, p1.z), __float_as_int(p1.w));
+    for (uint32_t j = b + (uint32_t)sub; j < e; j += U * G) {
+        float4 p[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) p[u] = g.pts[min(j + (uint32_t)(u * G), e - 1)];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (j + (uint32_t)(u * G) < e) tk.push(sqdist3(qx, qy, qz, p[u].x, p[u].y, p[u].z), __float_as_int(p[u].w));
     }
 }
 
@@ -360,7 +363,7 @@ constexpr int shell1_cpl() {  // cells of the 3x3x3 block per lane
     return (27 + G - 1) / G;
 }
 
-template <int G>
+template <int G, bool OWN = false>  // OWN: the own cell (k = 13) is a range too
 __device__ __forceinline__ void shell1_ranges(const GridDev& g, int cx, int cy, int cz, int sub,
                                               uint32_t* b4, uint32_t* n4) {
     constexpr int CPL = shell1_cpl<G>();
@@ -369,7 +372,7 @@ __device__ __forceinline__ void shell1_ranges(const GridDev& g, int cx, int cy, 
         const int k = CPL * sub + j;
         const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
         const int x = cx + dx, y = cy + dy, z = cz + dz;
-        const bool ok = k < 27 && k != 13 && (unsigned)x < (unsigned)g.nx && (unsigned)y < (unsigned)g.ny &&
+        const bool ok = k < 27 && (OWN || k != 13) && (unsigned)x < (unsigned)g.nx && (unsigned)y < (unsigned)g.ny &&
                         (unsigned)z < (unsigned)g.nz;
         uint32_t b = 0, e = 0;
         if (ok) {
@@ -392,18 +395,20 @@ __device__ __forceinline__ uint32_t shell1_table(const GridDev& g, float qx, flo
     constexpr int CPL = shell1_cpl<G>();
     static_assert(CPL * G == 32, "shell1_table: slot table = 32 range starts + 33 offsets");
     const float cs = g.cell, m = g.margin, w = cs + 2.f * m;
-    uint32_t lane_total = 0;
+    // prune the preloaded ranges against the bound; count points and non-empty ranges in one
+    // packed word (ranges << 24 | points) so one group prefix sum gives both
+    uint32_t packed = 0;
 #pragma unroll
-    for (int j = 0; j < CPL; ++j) {  // prune the preloaded ranges against the own-cell bound
+    for (int j = 0; j < CPL; ++j) {
         const int k = CPL * sub + j;
         const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
         const float xl = lox + (float)dx * cs - m, yl = loy + (float)dy * cs - m, zl = loz + (float)dz * cs - m;
         const float bd = (axis_gap(qx, xl, xl + w) + axis_gap(qy, yl, yl + w)) + axis_gap(qz, zl, zl + w);
         if (bd * 0.999999f > bound) n4[j] = 0;
         if (dbg && n4[j]) dbg->cells += 1;
-        lane_total += n4[j];
+        packed += n4[j] + (n4[j] ? (1u << 24) : 0u);
     }
-    uint32_t incl = lane_total, T;
+    uint32_t incl = packed, tot;
     if constexpr (G == 8) {  // DPP row shifts (lanes from the neighbouring group are masked by sub >= off)
         uint32_t v = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x111, 0xf, 0xf, false);  // row_shr:1
         if (sub >= 1) incl += v;
@@ -411,59 +416,68 @@ __device__ __forceinline__ uint32_t shell1_table(const GridDev& g, float qx, flo
         if (sub >= 2) incl += v;
         v = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)incl, 0x114, 0xf, 0xf, false);  // row_shr:4
         if (sub >= 4) incl += v;
-        uint32_t t = lane_total;  // group total by butterfly (integer: order-free)
+        uint32_t t = packed;  // group total by butterfly (integer: order-free)
         t += partner_u32<1>(t);
         t += partner_u32<2>(t);
         t += partner_u32<4>(t);
-        T = t;
+        tot = t;
     } else {
 #pragma unroll
         for (int off = 1; off < G; off <<= 1) {
             const uint32_t v = __shfl_up(incl, off, G);
             if (sub >= off) incl += v;
         }
-        T = __shfl(incl, G - 1, G);
+        tot = __shfl(incl, G - 1, G);
     }
-    uint32_t o = incl - lane_total;
+    const uint32_t T = tot & 0xffffffu, NR = tot >> 24;
+    // compacted slot table: only the non-empty ranges, so the lanes' slot walks never step
+    // through pruned or empty cells (each step is a dependent LDS read)
+    const uint32_t excl = incl - packed;
+    uint32_t o = excl & 0xffffffu, slot = excl >> 24;
     uint32_t* s_b = lds;
     uint32_t* s_off = lds + CPL * G;
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {
-        s_b[CPL * sub + j] = b4[j];
-        s_off[CPL * sub + j] = o;
+        if (n4[j]) {
+            s_b[slot] = b4[j];
+            s_off[slot] = o;
+            ++slot;
+        }
         o += n4[j];
     }
-    if (sub == G - 1) s_off[CPL * G] = T;
+    if (sub == G - 1) s_off[NR] = T;
     if (dbg && sub == 0) dbg->points += (int)T;
     return T;
 }
 
-// Lane `r` of `L` lanes strides the concatenated table [0, T) (two loads in
-// flight per lane) and pushes every point into its private list.
-template <int K>
+// Lane `r` of `L` lanes strides the concatenated table [0, T) (U loads in
+// flight per lane: the slot walk first, then the loads, then the pushes) and
+// pushes every point into its private list.
+template <int K, int U = 4>
 __device__ __forceinline__ void scan_table_strided(const GridDev& g, float qx, float qy, float qz, const uint32_t* lds,
                                                    uint32_t T, uint32_t r, uint32_t L, TopK<K>& tk) {
     const uint32_t* s_b = lds;
     const uint32_t* s_off = lds + 32;
     int sl = 0;
-    uint32_t lo = 0, hi = s_off[1];
-    for (uint32_t t = r; t < T; t += 2 * L) {
-        while (t >= hi) {
-            lo = hi;
-            hi = s_off[++sl + 1];
-        }
-        const float4 p0 = g.pts[s_b[sl] + (t - lo)];
-        const uint32_t t2 = t + L;
-        float4 p1 = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (t2 < T) {
-            while (t2 >= hi) {
+    uint32_t lo = 0, hi = s_off[1], sb = s_b[0];
+    for (uint32_t t = r; t < T; t += U * L) {
+        uint32_t src[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const uint32_t tu = min(t + (uint32_t)u * L, T - 1);  // clamped: a valid address, pushed only if < T
+            while (tu >= hi) {
                 lo = hi;
                 hi = s_off[++sl + 1];
+                sb = s_b[sl];
             }
-            p1 = g.pts[s_b[sl] + (t2 - lo)];
+            src[u] = sb + (tu - lo);
         }
-        tk.push(sqdist3(qx, qy, qz, p0.x, p0.y, p0.z), __float_as_int(p0.w));
-        if (t2 < T) tk.push(sqdist3(qx, qy, qz, p1.x, p1.y, p1.z), __float_as_int(p1.w));
+        float4 p[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) p[u] = g.pts[src[u]];
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+            if (t + (uint32_t)u * L < T) tk.push(sqdist3(qx, qy, qz, p[u].x, p[u].y, p[u].z), __float_as_int(p[u].w));
     }
 }
 
@@ -523,6 +537,55 @@ __device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, i
     if (!TAIL || max_shell < 2) return false;
     if (dbg) dbg->shell = 2;
     return group_knn_exact_from<K, G>(g, qx, qy, qz, 2, max_shell, sub, tk);
+}
+
+// Near pass seeded by the query's previous neighbours (the second and later
+// kNN evaluations of a scan, map unchanged since): their keys recomputed at
+// the new position bound the answer — f = the largest of the five (capped at
+// the gate) — so every lane starts with f as filler (push keeps only keys
+// < f; a previous neighbour met again with key f is represented by the filler
+// itself, the others are found again), the 27 cells of the 3x3x3 block are
+// pruned against f and scanned in ONE flat pass, and one merge gives the
+// list.  Result contract as group_knn_near (TAIL = false): true when final.
+template <int K, int G>
+__device__ bool group_knn_seeded(const GridDev& g, const float4* __restrict__ by_id, const int32_t* prev, float qx,
+                                 float qy, float qz, float range_sq, int sub, TopK<K>& tk, uint32_t* lds) {
+    static_assert(K == 5, "group_knn_seeded: K = 5");
+    uint64_t f = knn_key(range_sq, kNone);
+    int32_t id[5];
+#pragma unroll
+    for (int j = 0; j < 5; ++j) id[j] = prev[j];
+    if (id[4] >= 0) {  // a full previous list (sorted: the 5th exists => all exist)
+        uint64_t m = 0;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) {
+            const float4 p = by_id[id[j]];
+            const uint64_t k = knn_key(sqdist3(qx, qy, qz, p.x, p.y, p.z), id[j]);
+            m = k > m ? k : m;
+        }
+        f = m < f ? m : f;
+    }
+#pragma unroll
+    for (int j = 0; j < K; ++j) tk.k[j] = f;
+    const int cx = cell_coord(qx, g.ox, g.inv_cell);
+    const int cy = cell_coord(qy, g.oy, g.inv_cell);
+    const int cz = cell_coord(qz, g.oz, g.inv_cell);
+    const bool inside = (unsigned)cx < (unsigned)g.nx && (unsigned)cy < (unsigned)g.ny && (unsigned)cz < (unsigned)g.nz;
+    if (!inside) return false;  // the far pass scans the whole box from the filler list
+    const float cs = g.cell, m = g.margin;
+    const float lox = g.ox + (float)cx * cs, loy = g.oy + (float)cy * cs, loz = g.oz + (float)cz * cs;
+    float own = fminf(fminf(qx - lox, lox + cs - qx), fminf(qy - loy, loy + cs - qy));
+    own = fminf(own, fminf(qz - loz, loz + cs - qz)) - m;
+    uint32_t b4[shell1_cpl<G>()], n4[shell1_cpl<G>()];
+    shell1_ranges<G, true>(g, cx, cy, cz, sub, b4, n4);
+    const uint32_t T = shell1_table<K, G>(g, qx, qy, qz, lox, loy, loz, sub, lds, b4, n4, tk.worst(), nullptr);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    scan_table_strided<K>(g, qx, qy, qz, lds, T, (uint32_t)sub, (uint32_t)G, tk);
+    group_merge<K, G>(tk);
+    const float gr = own + cs;
+    return gr > 0.f && tk.worst() < gr * gr * 0.999999f;
 }
 
 // Far pass with a whole block (NT lanes) per query: the box cells outside

@@ -29,6 +29,7 @@ struct MatchArgs {
     int* far_id;
     int n;
     int max_shell;
+    int prior;                // 1: nn_idx holds this scan's previous lists against the unchanged map (seeded near pass)
     float range_sq;
     float plane_thr;
     double s_coef;

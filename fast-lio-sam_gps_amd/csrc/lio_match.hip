@@ -94,7 +94,7 @@ __device__ __forceinline__ bool residual_row(const MatchArgs& a, float bx, float
 // neighbourhoods, ~0.4% of a dense scan) are queued, with their list, for
 // the wave-per-query far pass instead of holding their wave: a kernel runs as
 // long as its slowest wave.  Written for 8 waves/SIMD (<= 64 VGPRs).
-template <bool DBG>
+template <bool DBG, bool SEEDED>
 __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) knn_near_kernel(MatchArgs a) {
     constexpr int G = kGroup;
     constexpr int QPB = kKnnBlock / G;  // 64 queries per block
@@ -110,8 +110,12 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
     TopK<5> tk;
     tk.init(a.range_sq);
     SearchStats st{0, 0, 0};
-    const bool done = group_knn_near<5, G, false>(a.grid, wx, wy, wz, 1, sub, tk, DBG ? &st : nullptr,
-                                                s_tab[threadIdx.x / G]);
+    bool done;
+    if constexpr (SEEDED)  // nn_idx holds this scan's previous lists against the same map
+        done = group_knn_seeded<5, G>(a.grid, a.map_by_id, a.nn_idx + 5 * (size_t)i, wx, wy, wz, a.range_sq, sub, tk,
+                                      s_tab[threadIdx.x / G]);
+    else
+        done = group_knn_near<5, G, false>(a.grid, wx, wy, wz, 1, sub, tk, DBG ? &st : nullptr, s_tab[threadIdx.x / G]);
     const bool far = !done && a.max_shell > 1;
     if constexpr (DBG) {
 #pragma unroll
@@ -477,9 +481,11 @@ int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* ma
     if (redo) {
         const int nq = (a.n + kKnnBlock / kGroup - 1) / (kKnnBlock / kGroup);
         if (a.dbg)
-            knn_near_kernel<true><<<nq, kKnnBlock, 0, st>>>(a);
+            knn_near_kernel<true, false><<<nq, kKnnBlock, 0, st>>>(a);
+        else if (a.prior)
+            knn_near_kernel<false, true><<<nq, kKnnBlock, 0, st>>>(a);
         else
-            knn_near_kernel<false><<<nq, kKnnBlock, 0, st>>>(a);
+            knn_near_kernel<false, false><<<nq, kKnnBlock, 0, st>>>(a);
         if (marks) (void)hipEventRecord(marks[0], st);
         static const int far_blocks = [] {  // LIO_FAR_BLOCKS: diagnostics override of the far-pass grid
             const char* e = std::getenv("LIO_FAR_BLOCKS");

@@ -356,3 +356,29 @@ def test_bind_scan_device_matches_copy(c1):
     np.testing.assert_array_equal(s1, s2)
     np.testing.assert_array_equal(h1.nearest_points()[0], h2.nearest_points()[0])
     np.testing.assert_array_equal(h1(p24, False), h2(p24, False))
+
+
+@pytest.mark.parametrize("shift", [0.02, 0.3, 3.0])
+def test_seeded_second_knn_bit_exact(oracle, c1, shift):
+    """A later kNN evaluation of the same scan (map unchanged) starts from the previous
+    neighbours' recomputed 5th key (group_knn_seeded): still the oracle's lists, bit-exact,
+    for a small, a medium and a large pose change between the evaluations."""
+    _, m, scans = c1
+    sc = scans[0]
+    tree = F.IkdTreeGPU()
+    tree.Build(m)
+    hm = F.HShareModelGPU(tree)
+    hm.set_scan(sc.body)
+    st = synth.initial_state(sc.pos_init, sc.rot_init)
+    hm(synth.pose24(st), converge=True)  # first evaluation: unseeded
+    st2 = dict(st)
+    st2["pos"] = np.asarray(st["pos"]) + np.array([shift, -0.5 * shift, 0.25 * shift])
+    p24 = synth.pose24(st2)
+    g = hm(p24, converge=True)  # seeded by the first evaluation's lists
+    om = oracle.OracleMap(m)
+    o, nn, sel, planes = _oracle_eval(oracle, om, sc.body, p24)
+    gi, gd = hm.nearest_points()
+    np.testing.assert_array_equal(gi, nn)
+    oi, od = om.knn(oracle.body_to_world(p24, sc.body), 5, 5.0)
+    np.testing.assert_array_equal(gd, od)
+    _check_sums(g, o)
