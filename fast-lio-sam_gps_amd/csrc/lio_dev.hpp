@@ -481,7 +481,7 @@ __device__ __forceinline__ void scan_table_strided(const GridDev& g, float qx, f
     }
 }
 
-template <int K, int G>
+template <int K, int G, int U = 4>
 __device__ __forceinline__ void scan_shell1_flat(const GridDev& g, float qx, float qy, float qz, int cx, int cy,
                                                  int cz, float lox, float loy, float loz, int sub, uint32_t* lds,
                                                  uint32_t* b4, uint32_t* n4, TopK<K>& tk, SearchStats* dbg) {
@@ -490,7 +490,7 @@ __device__ __forceinline__ void scan_shell1_flat(const GridDev& g, float qx, flo
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    scan_table_strided<K>(g, qx, qy, qz, lds, T, (uint32_t)sub, (uint32_t)G, tk);
+    scan_table_strided<K, U>(g, qx, qy, qz, lds, T, (uint32_t)sub, (uint32_t)G, tk);
 }
 
 // Lean group walk for dense maps (front-end kNN, ICP near pass), written for
@@ -503,7 +503,7 @@ __device__ __forceinline__ void scan_shell1_flat(const GridDev& g, float qx, flo
 // group_knn_exact_from.  TAIL = false (front-end near pass): no generic walk
 // at all — queries outside the grid or unresolved after shell 1 return false
 // with their partial list and go to the far pass.
-template <int K, int G, bool TAIL = true>
+template <int K, int G, bool TAIL = true, int U = 4>
 __device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, int max_shell, int sub, TopK<K>& tk,
                                SearchStats* dbg, uint32_t* lds) {
     const int cx = cell_coord(qx, g.ox, g.inv_cell);
@@ -529,7 +529,7 @@ __device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, i
     if (sub != 0) {  // re-seed non-leader lanes (see group_knn_exact_from)
         tk.fill_with_worst();
     }
-    scan_shell1_flat<K, G>(g, qx, qy, qz, cx, cy, cz, lox, loy, loz, sub, lds, b4, n4, tk, dbg);
+    scan_shell1_flat<K, G, U>(g, qx, qy, qz, cx, cy, cz, lox, loy, loz, sub, lds, b4, n4, tk, dbg);
     group_merge<K, G>(tk);
     if (dbg) dbg->shell = 1;
     const float gr = own + cs;
@@ -547,42 +547,42 @@ __device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, i
 // itself, the others are found again), the 27 cells of the 3x3x3 block are
 // pruned against f and scanned in ONE flat pass, and one merge gives the
 // list.  Result contract as group_knn_near (TAIL = false): true when final.
-template <int K, int G>
+template <int K, int G, int U = 4>
 __device__ bool group_knn_seeded(const GridDev& g, const float4* __restrict__ by_id, const int32_t* prev, float qx,
                                  float qy, float qz, float range_sq, int sub, TopK<K>& tk, uint32_t* lds) {
     static_assert(K == 5, "group_knn_seeded: K = 5");
+    const int cx = cell_coord(qx, g.ox, g.inv_cell);
+    const int cy = cell_coord(qy, g.oy, g.inv_cell);
+    const int cz = cell_coord(qz, g.oz, g.inv_cell);
+    const bool inside = (unsigned)cx < (unsigned)g.nx && (unsigned)cy < (unsigned)g.ny && (unsigned)cz < (unsigned)g.nz;
+    uint32_t b4[shell1_cpl<G>()], n4[shell1_cpl<G>()];
+    if (inside) shell1_ranges<G, true>(g, cx, cy, cz, sub, b4, n4);  // in flight with the previous neighbours
     uint64_t f = knn_key(range_sq, kNone);
     int32_t id[5];
 #pragma unroll
     for (int j = 0; j < 5; ++j) id[j] = prev[j];
     if (id[4] >= 0) {  // a full previous list (sorted: the 5th exists => all exist)
-        uint64_t m = 0;
+        uint64_t mx = 0;
 #pragma unroll
         for (int j = 0; j < 5; ++j) {
             const float4 p = by_id[id[j]];
             const uint64_t k = knn_key(sqdist3(qx, qy, qz, p.x, p.y, p.z), id[j]);
-            m = k > m ? k : m;
+            mx = k > mx ? k : mx;
         }
-        f = m < f ? m : f;
+        f = mx < f ? mx : f;
     }
 #pragma unroll
     for (int j = 0; j < K; ++j) tk.k[j] = f;
-    const int cx = cell_coord(qx, g.ox, g.inv_cell);
-    const int cy = cell_coord(qy, g.oy, g.inv_cell);
-    const int cz = cell_coord(qz, g.oz, g.inv_cell);
-    const bool inside = (unsigned)cx < (unsigned)g.nx && (unsigned)cy < (unsigned)g.ny && (unsigned)cz < (unsigned)g.nz;
     if (!inside) return false;  // the far pass scans the whole box from the filler list
     const float cs = g.cell, m = g.margin;
     const float lox = g.ox + (float)cx * cs, loy = g.oy + (float)cy * cs, loz = g.oz + (float)cz * cs;
     float own = fminf(fminf(qx - lox, lox + cs - qx), fminf(qy - loy, loy + cs - qy));
     own = fminf(own, fminf(qz - loz, loz + cs - qz)) - m;
-    uint32_t b4[shell1_cpl<G>()], n4[shell1_cpl<G>()];
-    shell1_ranges<G, true>(g, cx, cy, cz, sub, b4, n4);
     const uint32_t T = shell1_table<K, G>(g, qx, qy, qz, lox, loy, loz, sub, lds, b4, n4, tk.worst(), nullptr);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    scan_table_strided<K>(g, qx, qy, qz, lds, T, (uint32_t)sub, (uint32_t)G, tk);
+    scan_table_strided<K, U>(g, qx, qy, qz, lds, T, (uint32_t)sub, (uint32_t)G, tk);
     group_merge<K, G>(tk);
     const float gr = own + cs;
     return gr > 0.f && tk.worst() < gr * gr * 0.999999f;

@@ -94,7 +94,7 @@ __device__ __forceinline__ bool residual_row(const MatchArgs& a, float bx, float
 // neighbourhoods, ~0.4% of a dense scan) are queued, with their list, for
 // the wave-per-query far pass instead of holding their wave: a kernel runs as
 // long as its slowest wave.  Written for 8 waves/SIMD (<= 64 VGPRs).
-template <bool DBG, bool SEEDED>
+template <bool DBG, bool SEEDED, int U = 4>
 __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) knn_near_kernel(MatchArgs a) {
     constexpr int G = kGroup;
     constexpr int QPB = kKnnBlock / G;  // 64 queries per block
@@ -112,10 +112,10 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
     SearchStats st{0, 0, 0};
     bool done;
     if constexpr (SEEDED)  // nn_idx holds this scan's previous lists against the same map
-        done = group_knn_seeded<5, G>(a.grid, a.map_by_id, a.nn_idx + 5 * (size_t)i, wx, wy, wz, a.range_sq, sub, tk,
+        done = group_knn_seeded<5, G, U>(a.grid, a.map_by_id, a.nn_idx + 5 * (size_t)i, wx, wy, wz, a.range_sq, sub, tk,
                                       s_tab[threadIdx.x / G]);
     else
-        done = group_knn_near<5, G, false>(a.grid, wx, wy, wz, 1, sub, tk, DBG ? &st : nullptr, s_tab[threadIdx.x / G]);
+        done = group_knn_near<5, G, false, U>(a.grid, wx, wy, wz, 1, sub, tk, DBG ? &st : nullptr, s_tab[threadIdx.x / G]);
     const bool far = !done && a.max_shell > 1;
     if constexpr (DBG) {
 #pragma unroll
