@@ -270,6 +270,9 @@ __global__ void __launch_bounds__(kBlock) plane_kernel(MatchArgs a) {
     double h = 0.0, res = 0.0, cnt = 0.0;
     if (i < a.n) {
         const int32_t* nn = a.nn_idx + 5 * (size_t)i;
+        // the body point is needed only for selected points, but loading it here keeps
+        // its latency off the chain nn_idx -> neighbours -> esti_plane
+        const float bx = a.body[3 * i], by = a.body[3 * i + 1], bz = a.body[3 * i + 2];
         int id[5];
 #pragma unroll
         for (int j = 0; j < 5; ++j) id[j] = nn[j];
@@ -288,7 +291,6 @@ __global__ void __launch_bounds__(kBlock) plane_kernel(MatchArgs a) {
             const float4 pl = make_float4(abcd[0], abcd[1], abcd[2], abcd[3]);
             a.planes[i] = pl;
             if (sel) {
-                const float bx = a.body[3 * i], by = a.body[3 * i + 1], bz = a.body[3 * i + 2];
                 float wx, wy, wz;
                 body_to_world(a.pose, bx, by, bz, wx, wy, wz);
                 sel = residual_row(a, bx, by, bz, wx, wy, wz, pl, J, h, res);
@@ -312,12 +314,14 @@ __global__ void __launch_bounds__(kBlock) h_model_reuse_kernel(MatchArgs a) {
     double J[6] = {0, 0, 0, 0, 0, 0};
     double h = 0.0, res = 0.0, cnt = 0.0;
     if (i < a.n) {
+        // all three loads issued together (one round trip instead of sel -> body/plane)
         bool sel = a.sel[i] != 0;
+        const float bx = a.body[3 * i], by = a.body[3 * i + 1], bz = a.body[3 * i + 2];
+        const float4 pl = a.planes[i];
         if (sel) {
-            const float bx = a.body[3 * i], by = a.body[3 * i + 1], bz = a.body[3 * i + 2];
             float wx, wy, wz;
             body_to_world(a.pose, bx, by, bz, wx, wy, wz);
-            sel = residual_row(a, bx, by, bz, wx, wy, wz, a.planes[i], J, h, res);
+            sel = residual_row(a, bx, by, bz, wx, wy, wz, pl, J, h, res);
             cnt = sel ? 1.0 : 0.0;
             a.sel[i] = sel ? 1 : 0;
         }
