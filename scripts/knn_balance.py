@@ -25,3 +25,7 @@ wm = w.max(1)
 print("per-wave max points pct 50/90/99/max:", np.percentile(wm, [50, 90, 99]).round(1), wm.max())
 print("per-wave sum points pct 50/90/99/max:", np.percentile(w.sum(1), [50, 90, 99]).round(1), w.sum(1).max())
 # own-cell sizes of the map grid
+far = (s[:, 2] == 2).astype(np.int64)
+fb = far[: len(far) // 64 * 64].reshape(-1, 64).sum(1)
+print("far queries:", int(far.sum()), "per 64-query block: max", int(fb.max()), "blocks with >0:", int((fb > 0).sum()),
+      "hist", np.bincount(fb)[:12].tolist())
