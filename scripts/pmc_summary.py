@@ -35,7 +35,11 @@ def bytes_of(k):
 
 
 near = [k for k in kern if k.startswith("knn_near_kernel")]
-total = sum(bytes_of(k) for k in near + ["knn_far_kernel", "plane_kernel"])
+# one near pass per kNN evaluation: its instantiations (first / seeded later evaluations) are
+# averaged, weighted by their dispatch counts
+nd = sum(kern[k]["dispatches"] for k in near)
+near_bytes = sum(bytes_of(k) * kern[k]["dispatches"] for k in near) / max(nd, 1)
+total = near_bytes + sum(bytes_of(k) for k in ["knn_far_kernel", "plane_kernel"])
 res = {"config": cfg, "knn_hbm_bytes_per_launch": round(total),
        "reuse_hbm_bytes_per_launch": round(bytes_of("h_model_reuse_kernel")),
        "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, --kernel-trace only); "
