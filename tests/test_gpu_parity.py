@@ -382,3 +382,37 @@ def test_seeded_second_knn_bit_exact(oracle, c1, shift):
     oi, od = om.knn(oracle.body_to_world(p24, sc.body), 5, 5.0)
     np.testing.assert_array_equal(gd, od)
     _check_sums(g, o)
+
+
+@pytest.mark.parametrize("env", [{"LIO_FUSED_FINAL": "0"}, {"LIO_KNN_SEED": "0"}])
+def test_ieskf_alternative_paths(env):
+    """The A/B switches keep parity: the separate finalize launch (LIO_FUSED_FINAL=0) and the
+    unseeded later kNN evaluations (LIO_KNN_SEED=0), through a whole IESKF update against the
+    oracle.  Child process: the switches are read once per process."""
+    import os
+    import subprocess
+    import sys
+
+    code = r'''
+import sys, numpy as np
+sys.path[:0] = [r"%s", r"%s"]
+import oracle_py as O
+from lio_gpu import frontend as F, synth
+scene, m, scans = synth.make_config("C1", n_scans=2)
+om = O.OracleMap(m)
+tree = F.IkdTreeGPU(); tree.Build(m)
+hm = F.HShareModelGPU(tree); kf = F.EsekfGPU(hm)
+for sc in scans:
+    hm.set_scan(sc.body)
+    st = synth.initial_state(sc.pos_init, sc.rot_init)
+    P0 = synth.initial_cov()
+    xg, Pg, sg = kf.update_iterated_dyn_share_modified(st, P0)
+    xo, Po, so, _ = O.ieskf_update(om, sc.body, st, P0)
+    assert sg["h_evals"] == int(so[0]) and sg["knn_calls"] == int(so[1]) and sg["n_eff"] == int(so[3])
+    assert np.allclose(xg["pos"], xo["pos"], atol=1e-5) and np.allclose(xg["rot"], xo["rot"], atol=1e-5)
+    assert np.allclose(Pg, Po, rtol=1e-5, atol=1e-10)
+print("ok")
+''' % (os.path.join(os.path.dirname(__file__), "..", "fast-lio-sam_gps_amd"), os.path.dirname(__file__))
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
