@@ -237,7 +237,8 @@ __global__ void __launch_bounds__(kIcpTileQ * NW) icp_tile_kernel(IcpArgs a) {
     __shared__ uint64_t s_best[NW][kIcpTileQ];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     TileLds& L = Ls[wv];
-    const uint2 tl = a.tiles[xcd_block(blockIdx.x, gridDim.x)];
+    const int tix = a.order ? (int)a.order[blockIdx.x] : xcd_block(blockIdx.x, gridDim.x);
+    const uint2 tl = a.tiles[tix];
     const bool act = lane < (int)tl.y;
     const int i = act ? __float_as_int(a.qpts[tl.x + lane].w) : 0;
     float x = 0.f, y = 0.f, z = 0.f;
@@ -306,6 +307,7 @@ __global__ void __launch_bounds__(kIcpTileQ * NW) icp_tile_kernel(IcpArgs a) {
         S = N;
         r = 2 * r + 1;
     }
+    if (a.tile_cost && threadIdx.x == 0) a.tile_cost[tix] = (uint32_t)min(cand, 0xffffffffull);
     if (a.dbg && threadIdx.x == 0) {
         atomicAdd(a.dbg, cand);
         atomicAdd(a.dbg + 1, (unsigned long long)rounds);
@@ -392,6 +394,37 @@ void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st) {
         icp_tile_kernel<4><<<ntiles, kIcpTileQ * 4, 0, st>>>(a);
     else  // 2 waves per tile: measured best (scripts/icp_exp.sh)
         icp_tile_kernel<2><<<ntiles, kIcpTileQ * 2, 0, st>>>(a);
+}
+
+// Longest-first tile order from the previous pass's candidate counts: tiles
+// bucketed by floor(log2(cost)), buckets in descending order (counting sort in
+// one block; order inside a bucket is arbitrary: it affects speed only).  The
+// heavy tiles (misaligned regions) start first instead of forming the tail.
+__global__ void __launch_bounds__(1024) icp_order_kernel(const uint32_t* __restrict__ cost, int n,
+                                                         uint32_t* __restrict__ order) {
+    __shared__ uint32_t hist[33], base[33];
+    if (threadIdx.x < 33) hist[threadIdx.x] = 0;
+    __syncthreads();
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+        const uint32_t c = cost[t];
+        atomicAdd(&hist[c ? 32 - __clz(c) : 0], 1u);
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int b = 32; b >= 0; --b) {
+            base[b] = acc;
+            acc += hist[b];
+        }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < n; t += blockDim.x) {
+        const uint32_t c = cost[t];
+        order[atomicAdd(&base[c ? 32 - __clz(c) : 0], 1u)] = (uint32_t)t;
+    }
+}
+void launch_icp_order(const uint32_t* tile_cost, int ntiles, uint32_t* order, hipStream_t st) {
+    if (ntiles > 0) icp_order_kernel<<<1, 1024, 0, st>>>(tile_cost, ntiles, order);
 }
 
 // per cell: number of tiles (ceil(count / 64)); slot ncells = 0 for the scan's total

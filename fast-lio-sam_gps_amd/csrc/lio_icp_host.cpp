@@ -157,6 +157,9 @@ struct lio_icp {
     int ntiles = 0;
     float tile_cell = 2.0f;
     bool have_prior = false;  // nn ids of this alignment's previous pass are in d_fid
+    uint32_t* d_tcost = nullptr;  // per tile: candidates of the last pass
+    uint32_t* d_order = nullptr;  // longest-first tile order (valid when have_order)
+    bool have_order = false;
     unsigned long long* d_dbg = nullptr;  // LIO_ICP_DEBUG counters
     double* d_part = nullptr;
     double* d_super = nullptr;
@@ -217,7 +220,7 @@ int lio_icp_destroy(lio_icp* h) {
     (void)hipStreamSynchronize(h->st);
     lio::grid_free(h->tgt);
     lio::grid_free(h->qgrid);
-    void* ptrs[] = {h->d_tgt, h->d_src, h->d_cur, h->d_fd2, h->d_fid, h->d_tiles, h->d_tscratch, h->d_ttmp, h->d_dbg, h->d_part, h->d_super};
+    void* ptrs[] = {h->d_tgt, h->d_src, h->d_cur, h->d_fd2, h->d_fid, h->d_tiles, h->d_tscratch, h->d_ttmp, h->d_dbg, h->d_tcost, h->d_order, h->d_part, h->d_super};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (h->h_super) (void)hipHostFree(h->h_super);
@@ -269,7 +272,7 @@ static int icp_prepare(lio_icp* h) {
     shard_range(h->ns, h->rank, h->world, h->sh_begin, h->sh_n);
     const int64_t n = std::max<int64_t>(h->sh_n, 1);
     if (n > h->cap) {
-        void* ptrs[] = {h->d_src, h->d_cur, h->d_fd2, h->d_fid, h->d_tiles, h->d_part};
+        void* ptrs[] = {h->d_src, h->d_cur, h->d_fd2, h->d_fid, h->d_tiles, h->d_tcost, h->d_order, h->d_part};
         for (void* q : ptrs)
             if (q) IHIP(hipFree(q));
         const int64_t nch = (n + lio::kIcpChunk - 1) / lio::kIcpChunk;
@@ -278,6 +281,8 @@ static int icp_prepare(lio_icp* h) {
         IHIP(hipMalloc(&h->d_fd2, n * sizeof(float)));
         IHIP(hipMalloc(&h->d_fid, n * sizeof(int)));
         IHIP(hipMalloc(&h->d_tiles, (n + n / lio::kIcpTileQ + 1) * sizeof(uint2)));
+        IHIP(hipMalloc(&h->d_tcost, (n + n / lio::kIcpTileQ + 1) * sizeof(uint32_t)));
+        IHIP(hipMalloc(&h->d_order, (n + n / lio::kIcpTileQ + 1) * sizeof(uint32_t)));
         IHIP(hipMalloc(&h->d_part, nch * lio::kIcpStride * sizeof(double)));
         h->cap = n;
     }
@@ -290,6 +295,7 @@ static int icp_prepare(lio_icp* h) {
         h->super_cap = nsup_all;
     }
     h->ntiles = 0;
+    h->have_order = false;  // new tiles: cell order until a pass has measured them
     if (h->sh_n > 0) {
         IHIP(hipMemcpyAsync(h->d_src, h->src.data() + 3 * h->sh_begin, h->sh_n * 3 * sizeof(float),
                             hipMemcpyHostToDevice, h->st));
@@ -312,6 +318,15 @@ static int icp_prepare(lio_icp* h) {
     return LIO_OK;
 }
 
+// LIO_ICP_ORDER=0 keeps every pass in cell order (A/B switch for the longest-first tile order).
+static bool icp_order_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("LIO_ICP_ORDER");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    return on;
+}
+
 // One correspondence (or fitness) pass: GPU kernels + exchange + ordered sum.
 static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, double max_d2, double out17[17]) {
     lio::IcpArgs a{};
@@ -331,6 +346,8 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     a.nn_id = h->d_fid;
     a.qpts = h->qgrid.pts;
     a.tiles = h->d_tiles;
+    a.tile_cost = h->d_tcost;
+    a.order = h->have_order ? h->d_order : nullptr;
     static const bool dbg_on = std::getenv("LIO_ICP_DEBUG") != nullptr;  // search statistics on stderr
     if (dbg_on) {
         if (!h->d_dbg) IHIP(hipMalloc(&h->d_dbg, 64));
@@ -343,6 +360,8 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
         if (h->timing) IHIP(hipEventRecord(h->ev.a, h->st));
         lio::launch_icp_tiles(a, h->ntiles, h->st);
         lio::launch_icp_stats(a, h->st);
+        if (!fitness && icp_order_on())  // longest-first order for the next pass of this alignment
+            lio::launch_icp_order(h->d_tcost, h->ntiles, h->d_order, h->st);
         if (h->timing) IHIP(hipEventRecord(h->ev.b, h->st));
         lio::launch_icp_reduce(h->d_part, nch, h->d_super, h->st);
         IHIP(hipGetLastError());
@@ -351,6 +370,7 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     }
     IHIP(hipStreamSynchronize(h->st));
     h->have_prior = true;
+    if (!fitness && h->sh_n > 0 && icp_order_on()) h->have_order = true;
     if (dbg_on) {
         unsigned long long c[4];
         IHIP(hipMemcpy(c, h->d_dbg, sizeof(c), hipMemcpyDeviceToHost));
@@ -418,6 +438,7 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
     if (h->sh_n > 0)
         IHIP(hipMemcpyAsync(h->d_cur, h->d_src, h->sh_n * 3 * sizeof(float), hipMemcpyDeviceToDevice, h->st));
     h->have_prior = false;
+    h->have_order = false;  // every alignment starts in cell order (its first pass measures the tiles)
     const double max_d2 = h->p.max_corr_dist * h->p.max_corr_dist;
     const double rot_thr = h->p.rot_eps > 0 ? h->p.rot_eps : 1.0 - h->p.trans_eps;
     double prev_mse = std::numeric_limits<double>::max();

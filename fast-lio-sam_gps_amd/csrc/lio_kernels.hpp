@@ -115,6 +115,8 @@ struct IcpArgs {
     int* nn_id;          //            1-NN target id
     const float4* qpts;  // source binned by tile cell: (x, y, z, local index bits), cell order
     const uint2* tiles;  // (first entry in qpts, query count <= kIcpTileQ) per tile
+    const uint32_t* order;  // optional tile visit order (heaviest first, from the previous pass's costs)
+    uint32_t* tile_cost;    // per tile: candidates scanned in this pass
     unsigned long long* dbg;  // optional counters (diagnostics): candidates, rings, tiles, lanes
 };
 
@@ -129,6 +131,8 @@ constexpr int kIcpTileQ = 64;     // queries per tile (one wave)
 // the tile count (synchronises the stream once).  tiles: capacity n + n / 64 + 1.
 int icp_build_tiles(const GridBuf& q, uint2* tiles, uint32_t* scratch, void*& tmp, size_t& tmp_bytes, hipStream_t st);
 void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st);
+// tile order for the next pass: descending log2(cost) buckets (one block)
+void launch_icp_order(const uint32_t* tile_cost, int ntiles, uint32_t* order, hipStream_t st);
 void launch_icp_stats(const IcpArgs& a, hipStream_t st);
 void launch_icp_reduce(const double* partials, int nchunks, double* super, hipStream_t st);
 
