@@ -1221,7 +1221,7 @@ struct DynMap {
             for (int dx = -1; dx <= 1; ++dx)
                 for (int dy = -1; dy <= 1; ++dy)
                     for (int dz = -1; dz <= 1; ++dz) {
-                        auto it = bm.find(k0 + ((int64_t)dx << 42) + ((int64_t)dy << 21) + dz);
+                        auto it = bm.find(k0 + (int64_t)dx * (int64_t(1) << 42) + (int64_t)dy * (int64_t(1) << 21) + dz);
                         if (it != bm.end()) out.insert(out.end(), it->second.begin(), it->second.end());
                     }
             std::sort(out.begin(), out.end());
@@ -1697,7 +1697,9 @@ int orc_icp_align(const float* src, int64_t ns, const float* dst, int64_t nd, co
     orc::IcpParams ip{ipp->max_corr_dist, ipp->trans_eps, ipp->fitness_eps, ipp->max_iter, ipp->rot_eps,
                       ipp->score_threshold};
     orc::IcpResult r{};
-    int rc = orc::icp_align(src, ns, dst, nd, ip, guess16, &r, aligned, trace, max_trace, threads);
+    static const float kIdentity[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    int rc = orc::icp_align(src, ns, dst, nd, ip, guess16 ? guess16 : kIdentity, &r, aligned, trace, max_trace,
+                            threads);  // no guess = identity, as pcl::Registration::align(output)
     std::memcpy(T16, r.T, sizeof(r.T));
     out8[0] = r.fitness;
     out8[1] = r.converged;

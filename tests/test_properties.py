@@ -1,0 +1,198 @@
+"""Property tests (hypothesis) for the path's size-independent invariants.
+
+CPU part: the oracle restatement (oracle/lio_oracle.cpp) against numpy on
+generated inputs — lattice clouds with exact distance ties and duplicates, k
+and range at their edges, single-point maps:
+  * kNN = brute force under the (d2, id) total order, rows ascending, ids unique,
+    -1 / inf padding only at the tail;
+  * ICP from the true transform stays there (exact correspondences, fitness 0);
+  * VoxelGrid emits one centroid per occupied voxel, each inside its voxel;
+  * esti_plane recovers a plane the points lie on.
+GPU part (-m gpu), through the C-ABI on the same generated inputs, so
+hypothesis's shrinking names the smallest failing case: Nearest_Search
+bit-exact against the oracle, VoxelGrid bit-exact against the oracle, and the
+ICP fixed point (transform and fitness equal to the oracle's within 1e-5).
+"""
+import numpy as np
+import pytest
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+SETTINGS = dict(max_examples=40, deadline=None, derandomize=True,
+                suppress_health_check=[HealthCheck.too_slow, HealthCheck.function_scoped_fixture])
+
+
+def bf_knn(m, q, k, r2):
+    """Brute force in the reference's float op order ((dx*dx + dy*dy) + dz*dz), total order (d2, id)."""
+    out_i = np.full((len(q), k), -1, np.int32)
+    out_d = np.full((len(q), k), np.inf, np.float32)
+    for j, p in enumerate(q):
+        if len(m) == 0:
+            continue
+        dx = (p[0] - m[:, 0]).astype(np.float32)
+        dy = (p[1] - m[:, 1]).astype(np.float32)
+        dz = (p[2] - m[:, 2]).astype(np.float32)
+        d = (dx * dx + dy * dy) + dz * dz
+        ok = np.nonzero(d <= np.float32(r2))[0]
+        o = ok[np.lexsort((ok, d[ok]))][:k]
+        out_i[j, :len(o)] = o
+        out_d[j, :len(o)] = d[o]
+    return out_i, out_d
+
+
+@st.composite
+def lattice_cloud(draw, max_n=300):
+    """Points on a 0.25 m lattice (many exact distance ties), with duplicated points."""
+    n = draw(st.integers(1, max_n))
+    seed = draw(st.integers(0, 2**31 - 1))
+    span = draw(st.integers(1, 16))
+    rng = np.random.default_rng(seed)
+    m = (rng.integers(-span, span + 1, (n, 3)) * 0.25).astype(np.float32)
+    dup = draw(st.integers(0, min(n, 20)))
+    if dup:
+        m = np.concatenate([m, m[:dup]])
+    nq = draw(st.integers(1, 64))
+    q = (rng.integers(-span - 4, span + 5, (nq, 3)) * 0.25).astype(np.float32)
+    q[: nq // 3] += rng.uniform(-0.2, 0.2, (nq // 3, 3)).astype(np.float32)  # off-lattice queries too
+    return m, q
+
+
+def _check_knn_shape(idx, d2):
+    for i_row, d_row in zip(idx, d2):
+        valid = i_row >= 0
+        nv = int(valid.sum())
+        assert np.all(valid[:nv]) and not np.any(valid[nv:])  # padding only at the tail
+        assert np.all(np.isinf(d_row[nv:]))
+        assert np.all(np.diff(d_row[:nv]) >= 0)
+        assert len(set(i_row[:nv].tolist())) == nv
+
+
+@settings(**SETTINGS)
+@given(cloud=lattice_cloud(), k=st.integers(1, 5), r2=st.sampled_from([0.0, 0.0625, 0.5, 5.0, np.inf]))
+def test_oracle_knn_matches_bruteforce(oracle, cloud, k, r2):
+    m, q = cloud
+    om = oracle.OracleMap(m)
+    idx, d2 = om.knn(q, k=k, range_sq=r2, threads=1)
+    bi, bd = bf_knn(m, q, k, r2)
+    np.testing.assert_array_equal(idx, bi)
+    np.testing.assert_array_equal(d2, bd)
+    _check_knn_shape(idx, d2)
+
+
+def _rot(ax, ang):
+    ax = np.asarray(ax, float)
+    ax = ax / np.linalg.norm(ax)
+    K = np.array([[0, -ax[2], ax[1]], [ax[2], 0, -ax[0]], [-ax[1], ax[0], 0]])
+    return np.eye(3) + np.sin(ang) * K + (1 - np.cos(ang)) * K @ K
+
+
+@settings(**dict(SETTINGS, max_examples=15))
+@given(seed=st.integers(0, 2**31 - 1), ang=st.floats(-0.5, 0.5), tr=st.floats(-3.0, 3.0))
+def test_oracle_icp_fixed_point_at_true_transform(oracle, seed, ang, tr):
+    """dst = T src: an alignment started at T finds every source point's exact
+    twin (d2 = 0 up to float rounding), so PCL's loop stops at once with
+    fitness ~0 and keeps T."""
+    rng = np.random.default_rng(seed)
+    src = rng.uniform(-10, 10, (400, 3)).astype(np.float32)
+    T = np.eye(4)
+    T[:3, :3] = _rot(rng.normal(size=3), ang)
+    T[:3, 3] = [tr, -0.5 * tr, 0.25 * tr]
+    dst = (src.astype(np.float64) @ T[:3, :3].T + T[:3, 3]).astype(np.float32)
+    r = oracle.icp_align(src, dst, guess=T.astype(np.float32))
+    assert r["converged"]
+    assert r["fitness"] < 1e-8
+    np.testing.assert_allclose(r["T"], T, atol=1e-4)
+
+
+@settings(**SETTINGS)
+@given(seed=st.integers(0, 2**31 - 1), n=st.integers(1, 2000),
+       leaf=st.sampled_from([0.1, 0.25, 0.5, 1.0, 2.0]), span=st.floats(0.5, 40.0))
+def test_oracle_voxel_grid_one_centroid_per_voxel(oracle, seed, n, leaf, span):
+    rng = np.random.default_rng(seed)
+    pts = rng.uniform(-span, span, (n, 4)).astype(np.float32)
+    out = oracle.voxel_grid(pts, leaf)
+    inv = np.float32(1.0 / np.float32(leaf))
+    keys = np.floor(pts[:, :3] * inv).astype(np.int64)  # pcl::VoxelGrid's floor(p * inverse_leaf)
+    n_vox = len(np.unique(keys, axis=0))
+    assert len(out) == n_vox
+    # every centroid sits in an occupied voxel (its own: a mean of points in a box stays in the box)
+    okeys = np.floor(out[:, :3] * inv).astype(np.int64)
+    occupied = {tuple(r) for r in keys.tolist()}
+    inside = np.mean([tuple(r) in occupied for r in okeys.tolist()])
+    assert inside > 0.99  # float rounding can push a centroid of boundary points one voxel over
+    lo, hi = pts[:, :3].min(0), pts[:, :3].max(0)
+    assert np.all(out[:, :3] >= lo - 1e-4) and np.all(out[:, :3] <= hi + 1e-4)
+
+
+@settings(**SETTINGS)
+@given(seed=st.integers(0, 2**31 - 1), spread=st.floats(0.05, 1.0))
+def test_oracle_esti_plane_recovers_plane(oracle, seed, spread):
+    rng = np.random.default_rng(seed)
+    nrm = rng.normal(size=3)
+    nrm /= np.linalg.norm(nrm)
+    u = np.cross(nrm, [1.0, 0, 0] if abs(nrm[0]) < 0.9 else [0, 1.0, 0])
+    u /= np.linalg.norm(u)
+    v = np.cross(nrm, u)
+    c = rng.uniform(-20, 20, 3)
+    ab = rng.uniform(-spread, spread, (5, 2))
+    pts = c + ab[:, :1] * u + ab[:, 1:] * v
+    ok, pabcd = oracle.esti_plane(pts.astype(np.float32))
+    if not ok:  # degenerate draws (collinear points) may be rejected, never accepted wrongly
+        return
+    n_est = pabcd[:3].astype(float)
+    assert abs(abs(n_est @ nrm) - 1.0) < 2e-3
+    res = pts.astype(np.float32) @ pabcd[:3] + pabcd[3]
+    assert np.all(np.abs(res) <= 0.1)  # the reference's plane_thr gate
+
+
+@pytest.mark.gpu
+@settings(**dict(SETTINGS, max_examples=25))
+@given(cloud=lattice_cloud(max_n=2000), k=st.integers(1, 5), max_dist=st.sampled_from([0.25, 0.7, 2.0, np.inf]))
+def test_gpu_nearest_search_matches_oracle(oracle, cloud, k, max_dist):
+    from lio_gpu.frontend import IkdTreeGPU
+
+    m, q = cloud
+    tree = IkdTreeGPU(cell_size=1.0)
+    tree.Build(m)
+    gi, gd = tree.Nearest_Search(q, k, max_dist)
+    oi, od = oracle.OracleMap(m).knn(q, k, max_dist * max_dist, threads=1)
+    np.testing.assert_array_equal(gi, oi)
+    np.testing.assert_array_equal(gd, od)
+    tree.close()
+
+
+@pytest.mark.gpu
+@settings(**dict(SETTINGS, max_examples=25))
+@given(seed=st.integers(0, 2**31 - 1), n=st.integers(1, 5000),
+       leaf=st.sampled_from([0.1, 0.25, 0.5, 1.0, 2.0]), span=st.floats(0.5, 40.0))
+def test_gpu_voxel_grid_matches_oracle(oracle, seed, n, leaf, span):
+    from lio_gpu.filters import VoxelGrid
+
+    rng = np.random.default_rng(seed)
+    pts = rng.uniform(-span, span, (n, 4)).astype(np.float32)
+    vg = VoxelGrid(leaf)
+    np.testing.assert_array_equal(vg.filter(pts), oracle.voxel_grid(pts, leaf))
+    vg.close()
+
+
+@pytest.mark.gpu
+@settings(**dict(SETTINGS, max_examples=10))
+@given(seed=st.integers(0, 2**31 - 1), ang=st.floats(-0.5, 0.5), tr=st.floats(-3.0, 3.0))
+def test_gpu_icp_fixed_point_matches_oracle(oracle, seed, ang, tr):
+    from lio_gpu import loop_closure as LC
+
+    rng = np.random.default_rng(seed)
+    src = rng.uniform(-10, 10, (3000, 3)).astype(np.float32)
+    T = np.eye(4)
+    T[:3, :3] = _rot(rng.normal(size=3), ang)
+    T[:3, 3] = [tr, -0.5 * tr, 0.25 * tr]
+    dst = (src.astype(np.float64) @ T[:3, :3].T + T[:3, 3]).astype(np.float32)
+    lc = LC.LoopClosure(LC.LoopClosureConfig())
+    lc.setInputSource(src)
+    lc.setInputTarget(dst)
+    r = lc.align(guess=T.astype(np.float32))
+    o = oracle.icp_align(src, dst, guess=T.astype(np.float32))
+    assert bool(r.is_converged) == o["converged"] and r.iterations == o["iterations"]
+    np.testing.assert_allclose(np.array(r.T).reshape(4, 4), o["T"], atol=1e-5)
+    assert abs(r.score - o["fitness"]) <= 1e-5
+    lc.close()
