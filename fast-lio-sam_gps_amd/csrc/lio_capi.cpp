@@ -104,7 +104,7 @@ struct lio_ctx {
     double* d_partials = nullptr;
     int64_t part_cap = 0;
     double* d_sums = nullptr;
-    double* h_sums = nullptr;    // pinned, host-mapped: [0,32) sums, [32] sequence number
+    double* h_sums = nullptr;    // pinned, host-mapped: [0,32) sums, [32] sequence number, [33] checksum
     double* h_sums_dev = nullptr;  // device view of h_sums
     unsigned long long seq = 0;
     double* d_rows = nullptr;
@@ -570,22 +570,42 @@ static void accum_event(EventPair& e, int64_t& launches, double& ms) {
 }
 
 // Wait until the evaluation's last block has published sequence number `seq`
-// (zero-copy result, no copy / stream-sync round trip); a stream error or an
-// idle stream without the result ends the wait with an error.
+// (zero-copy result, no copy / stream-sync round trip).  The GPU stores the
+// sums, the number and a checksum of both unordered (lio_match.hip
+// publish_host), so a result counts only when the number matches AND the
+// sums read after it hash to the checksum; once the stream is idle every word
+// has landed, so a stream error, or an idle stream whose words still do not
+// match, ends the wait with an error.
+static uint64_t mix64(uint64_t z) {  // splitmix64 finaliser, as publish_host
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+static bool read_result(const lio_ctx* c, unsigned long long seq, double* sums) {
+    const volatile uint64_t* w = reinterpret_cast<const volatile uint64_t*>(c->h_sums);
+    if (w[32] != seq) return false;
+    uint64_t h = 0, bits[LIO_SUMS_LEN];
+    for (int l = 0; l < LIO_SUMS_LEN; ++l) {
+        bits[l] = w[l];
+        h ^= mix64(bits[l] ^ ((uint64_t)l * 0x9e3779b97f4a7c15ull));
+    }
+    if ((h ^ mix64(seq)) != w[33]) return false;
+    std::memcpy(sums, bits, sizeof(bits));
+    return true;
+}
+
 static int wait_result(lio_ctx* c, unsigned long long seq, double* sums) {
-    volatile unsigned long long* flag = reinterpret_cast<volatile unsigned long long*>(c->h_sums + 32);
     for (uint64_t it = 0;; ++it) {
-        if (*flag == seq) break;
+        if (read_result(c, seq, sums)) return LIO_OK;
         if ((it & 255) == 255) {
             const hipError_t e = hipStreamQuery(c->map->st);
             if (e != hipSuccess && e != hipErrorNotReady)
                 return fail(LIO_ERR_HIP, std::string("lio_match: ") + hipGetErrorString(e));
-            if (e == hipSuccess && *flag != seq) return fail(LIO_ERR_HIP, "lio_match: evaluation produced no result");
+            if (e == hipSuccess && !read_result(c, seq, sums))
+                return fail(LIO_ERR_HIP, "lio_match: evaluation produced no result");
         }
     }
-    std::atomic_thread_fence(std::memory_order_acquire);
-    std::memcpy(sums, c->h_sums, LIO_SUMS_LEN * sizeof(double));
-    return LIO_OK;
 }
 
 int lio_match(lio_ctx* c, const lio_pose* pose, int redo_knn, double* sums) {

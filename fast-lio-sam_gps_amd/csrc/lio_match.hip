@@ -28,7 +28,10 @@
 
 namespace lio {
 
-constexpr int kBlock = 256;
+#ifndef LIO_HBLOCK
+#define LIO_HBLOCK 256
+#endif
+constexpr int kBlock = LIO_HBLOCK;
 
 constexpr int kGroup = 8;   // lanes cooperating on one query's kNN
 constexpr int kKnnBlock = 512;
@@ -41,36 +44,57 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-// Block reduction of one lane's contribution [HTH(21), HTh(6), cnt, res, hh]
-// over the wave, lane 0 stores the wave's 30 partial sums to `dst`.
-// Products are formed and reduced a few at a time so the 30 sums never need
-// 60 live VGPRs (the kernel's occupancy is set by its peak register count).
+// Wave reduction of one lane's contribution [HTH(21), HTh(6), cnt, res, hh]
+// by recursive halving: at each step a lane keeps half of its remaining
+// values and adds the partner's copy of that half (the partner keeps the
+// other half), so 32 values take 16+8+4+2+1 exchanges and adds instead of
+// 32 x 6.  Partners: row_mirror (lane bit 3 decides the half), row_half_mirror
+// (bit 2), quad_perm xor 2 (bit 1), xor 1 (bit 0), xor 16 (bit 4; a mirror
+// partner flips the lower bits too, so the mirrors go first, while every
+// partner pair still holds the same index set), then xor 32.  Lane l < 32 ends
+// with the wave total of value 16*b3 + 8*b2 + 4*b1 + 2*b0 + b4 (bits of l) and
+// stores it: a fixed order for a given lane assignment (deterministic).
+template <int CTRL, int BIT, int H>
+__device__ __forceinline__ void halve_step(double (&v)[32], int lane) {
+    const bool up = (lane >> BIT) & 1;
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        const double send = up ? v[j] : v[j + H];
+        const double keep = up ? v[j + H] : v[j];
+        v[j] = keep + dpp_d<CTRL, 0xf>(send);
+    }
+}
+
 __device__ __forceinline__ void wave_reduce_store(const double J[6], double h, double res, double cnt, double* dst) {
-    const bool l0 = (threadIdx.x & 63) == 63;  // DPP sums land in lane 63
+    const int lane = threadIdx.x & 63;
+    double v[32];
     int q = 0;
 #pragma unroll
-    for (int r = 0; r < 6; ++r) {
+    for (int r = 0; r < 6; ++r)
 #pragma unroll
-        for (int c = r; c < 6; ++c) {
-            const double v = wave_sum_to_lane63(J[r] * J[c]);
-            if (l0) dst[q] = v;
-            ++q;
-        }
-        __builtin_amdgcn_sched_barrier(0);
-    }
+        for (int c = r; c < 6; ++c) v[q++] = J[r] * J[c];
 #pragma unroll
-    for (int r = 0; r < 6; ++r) {
-        const double v = wave_sum_to_lane63(J[r] * h);
-        if (l0) dst[21 + r] = v;
+    for (int r = 0; r < 6; ++r) v[21 + r] = J[r] * h;
+    v[27] = cnt;
+    v[28] = res;
+    v[29] = h * h;
+    v[30] = 0.0;
+    v[31] = 0.0;
+    halve_step<0x140, 3, 16>(v, lane);  // row_mirror
+    halve_step<0x141, 2, 8>(v, lane);   // row_half_mirror
+    halve_step<0x4e, 1, 4>(v, lane);    // quad_perm [2,3,0,1]
+    halve_step<0xb1, 0, 2>(v, lane);    // quad_perm [1,0,3,2]
+    {
+        const bool up = (lane >> 4) & 1;
+        const double send = up ? v[0] : v[1];
+        const double keep = up ? v[1] : v[0];
+        v[0] = keep + __shfl_xor(send, 16, 64);
     }
-    __builtin_amdgcn_sched_barrier(0);
-    const double s0 = wave_sum_to_lane63(cnt), s1 = wave_sum_to_lane63(res), s2 = wave_sum_to_lane63(h * h);
-    if (l0) {
-        dst[27] = s0;
-        dst[28] = s1;
-        dst[29] = s2;
-        dst[30] = 0.0;
-        dst[31] = 0.0;
+    const double tot = v[0] + __shfl_xor(v[0], 32, 64);
+    if (lane < 32) {
+        const int idx = ((lane >> 3) & 1) * 16 + ((lane >> 2) & 1) * 8 + ((lane >> 1) & 1) * 4 + (lane & 1) * 2 +
+                        ((lane >> 4) & 1);
+        dst[idx] = tot;
     }
 }
 
@@ -197,6 +221,35 @@ __global__ void __launch_bounds__(kFarBlock) knn_far_kernel(MatchArgs a) {
 // agent release per block writes back the XCD's L2: 8 -> 35 us measured).
 typedef __attribute__((address_space(1))) double gdouble;
 typedef __attribute__((address_space(1))) unsigned int guint;
+typedef __attribute__((address_space(1))) unsigned long long gull;
+
+// Host hand-off in ONE round trip: wave lanes 0-31 store the 32 sums, lane 32
+// the sequence number, lane 33 a checksum of (sums, seq), all write-through at
+// system scope (sc0 sc1) and unordered.  The host (lio_capi.cpp wait_result)
+// accepts a result once it reads the expected sequence number AND sums whose
+// checksum matches: a word still in flight (or the previous evaluation's)
+// fails the check and the host polls again; once the kernel has completed,
+// every word has landed.  No system release (its write-back and the wait for
+// the sums' completion before the flag cost 1.7-2 us per evaluation).
+// Called by all 64 lanes of one wave; lane l < 32 passes sum l.
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {  // splitmix64 finaliser
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ void publish_host(double t, double* out, unsigned long long* seq_out, unsigned long long seq) {
+    const int lane = threadIdx.x & 63;
+    unsigned long long h =
+        lane < 32 ? mix64((unsigned long long)__double_as_longlong(t) ^ ((unsigned long long)lane * 0x9e3779b97f4a7c15ull))
+                  : 0ull;
+#pragma unroll
+    for (int off = 1; off < 32; off <<= 1) h ^= __shfl_xor(h, off, 64);
+    h = __shfl(h, 0, 64);
+    if (lane < 32) __hip_atomic_store((gdouble*)(out + lane), t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else if (lane == 32) __hip_atomic_store((gull*)seq_out, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else if (lane == 33) __hip_atomic_store((gull*)(seq_out + 1), h ^ mix64(seq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 __device__ __forceinline__ void publish_and_finalize(const MatchArgs& a, double (*red)[32]) {
     __shared__ int s_last;
@@ -232,31 +285,28 @@ __device__ __forceinline__ void publish_and_finalize(const MatchArgs& a, double 
     const int b0 = grp * per, b1 = min(nb, b0 + per);
     double acc = 0.0;
     int b = b0;
-    for (; b + 16 <= b1; b += 16) {  // 16 sc1 loads in flight per thread (cross-XCD: each batch is an L2 miss)
-        double v[16];
+    for (; b + 32 <= b1; b += 32) {  // 32 sc1 loads in flight per thread (cross-XCD: each batch is an L2 miss)
+        double v[32];
 #pragma unroll
-        for (int k = 0; k < 16; ++k)
+        for (int k = 0; k < 32; ++k)
             v[k] = __hip_atomic_load((gdouble*)(a.partials + (size_t)(b + k) * 32 + col), __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
-        for (int k = 0; k < 16; ++k) acc += v[k];
+        for (int k = 0; k < 32; ++k) acc += v[k];
     }
     for (; b < b1; ++b)
         acc += __hip_atomic_load((gdouble*)(a.partials + (size_t)b * 32 + col), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __shared__ double sg[NG][33];
     sg[grp][col] = acc;
     __syncthreads();
-    if (threadIdx.x < 32) {
+    if (threadIdx.x < 64) {
         double t = 0.0;
+        if (threadIdx.x < 32)
 #pragma unroll
-        for (int g = 0; g < NG; ++g) t += sg[g][threadIdx.x];
-        a.sums_out[threadIdx.x] = t;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __hip_atomic_store((guint*)a.done_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-        __threadfence_system();
-        *reinterpret_cast<volatile unsigned long long*>(a.seq_out) = a.seq;
+            for (int g = 0; g < NG; ++g) t += sg[g][threadIdx.x];
+        if (threadIdx.x == 0)
+            __hip_atomic_store((guint*)a.done_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+        publish_host(t, a.sums_out, a.seq_out, a.seq);
     }
 }
 
@@ -357,16 +407,12 @@ __global__ void __launch_bounds__(1024) finalize_kernel(const double* __restrict
     for (; b < b1; ++b) s += partials[(size_t)b * 32 + col];
     sg[grp][col] = s;
     __syncthreads();
-    if (threadIdx.x < 32) {
+    if (threadIdx.x < 64) {
         double t = 0.0;
+        if (threadIdx.x < 32)
 #pragma unroll
-        for (int g = 0; g < 32; ++g) t += sg[g][threadIdx.x];
-        out[threadIdx.x] = t;
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        __threadfence_system();
-        *reinterpret_cast<volatile unsigned long long*>(seq_out) = seq;
+            for (int g = 0; g < 32; ++g) t += sg[g][threadIdx.x];
+        publish_host(t, out, seq_out, seq);
     }
 }
 

@@ -11,7 +11,8 @@ import ctypes as C
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "_lib", "liblio_gpu.so")
+# LIO_GPU_LIB: load another build of the library (A/B diagnostics between builds)
+LIB_PATH = os.environ.get("LIO_GPU_LIB") or os.path.join(HERE, "_lib", "liblio_gpu.so")
 
 LIO_OK = 0
 LIO_ERR_ARG = -1

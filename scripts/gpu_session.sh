@@ -27,7 +27,7 @@ run() {  # run <name> <seconds> <cmd...>
 
 for s in $STEPS; do
     case $s in
-    test)  run pytest_gpu 900 python -m pytest tests -q -m gpu -p no:cacheprovider ;;
+    test)  run pytest_gpu 900 python -u -m pytest tests -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 200 --warmup 20 ;;
     knn)   run knn_timing 300 python scripts/knn_timing.py C2 &&

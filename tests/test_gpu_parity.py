@@ -416,3 +416,51 @@ print("ok")
     r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_sums_handoff_under_load(c1):
+    """The result hand-off (last block -> host-mapped sums + sequence number,
+    write-through stores, no system release) checked word for word under
+    uneven load: 300 rounds of redo/reuse evaluations at two alternating poses
+    while another map + ctx on its own stream keeps the GPU busy from a second
+    host thread.  Every returned sums vector must equal, bit for bit, the one
+    the same evaluation gave on an idle GPU; a stale word (the previous
+    evaluation's) would differ."""
+    _, m, scans = c1
+    sc = scans[0]
+    tree = F.IkdTreeGPU(cell_size=1.0)
+    tree.Build(m)
+    hm = F.HShareModelGPU(tree)
+    hm.set_scan(sc.body)
+    pa = synth.pose24(synth.initial_state(sc.pos_init, sc.rot_init))
+    pb = pa.copy()
+    pb[9:12] += np.array([0.05, -0.03, 0.02])  # translation
+
+    def round_trip():
+        return [hm(pa, True), hm(pa, False), hm(pb, True), hm(pb, False)]
+
+    want = round_trip()
+    assert not np.array_equal(want[0], want[2])  # the poses give different sums
+
+    busy_tree = F.IkdTreeGPU(cell_size=1.0)
+    busy_tree.Build(m)
+    busy = F.HShareModelGPU(busy_tree)
+    busy.set_scan(scans[1].body)
+    stop = threading.Event()
+
+    def load():
+        k = 0
+        while not stop.is_set():
+            busy(pa, k % 3 == 0)
+            k += 1
+
+    th = threading.Thread(target=load)
+    th.start()
+    try:
+        for it in range(300):
+            got = round_trip()
+            for g, w in zip(got, want):
+                assert np.array_equal(g, w), f"round {it}: stale or torn sums"
+    finally:
+        stop.set()
+        th.join()
