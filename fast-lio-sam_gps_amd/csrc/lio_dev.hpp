@@ -722,6 +722,42 @@ __device__ __forceinline__ double wave_sum_to_lane63(double v) {
     return v;                   // lane 63 holds the wave total
 }
 
+// Wave sum of 32 per-lane doubles by recursive halving: at each step a lane
+// keeps half of its remaining values and adds the partner's copy of that half
+// (the partner keeps the other half), so 32 values take 16+8+4+2+1 exchanges
+// and adds instead of 32 x 6 (wave_sum_to_lane63 per value).  Partners:
+// row_mirror (lane bit 3 decides the half), row_half_mirror (bit 2), quad_perm
+// xor 2 (bit 1), xor 1 (bit 0), xor 16 (bit 4; a mirror partner flips the
+// lower bits too, so the mirrors go first, while every partner pair still
+// holds the same index set), then xor 32.  Returns, in lane l < 32, the wave
+// total of value wave_sum32_index(l) (a fixed order: deterministic).
+template <int CTRL, int BIT, int H>
+__device__ __forceinline__ void halve_step(double (&v)[32], int lane) {
+    const bool up = (lane >> BIT) & 1;
+#pragma unroll
+    for (int j = 0; j < H; ++j) {
+        const double send = up ? v[j] : v[j + H];
+        const double keep = up ? v[j + H] : v[j];
+        v[j] = keep + dpp_d<CTRL, 0xf>(send);
+    }
+}
+
+__device__ __forceinline__ int wave_sum32_index(int lane) {
+    return ((lane >> 3) & 1) * 16 + ((lane >> 2) & 1) * 8 + ((lane >> 1) & 1) * 4 + (lane & 1) * 2 + ((lane >> 4) & 1);
+}
+
+__device__ __forceinline__ double wave_sum32(double (&v)[32], int lane) {
+    halve_step<0x140, 3, 16>(v, lane);  // row_mirror
+    halve_step<0x141, 2, 8>(v, lane);   // row_half_mirror
+    halve_step<0x4e, 1, 4>(v, lane);    // quad_perm [2,3,0,1]
+    halve_step<0xb1, 0, 2>(v, lane);    // quad_perm [1,0,3,2]
+    const bool up = (lane >> 4) & 1;
+    const double send = up ? v[0] : v[1];
+    const double keep = up ? v[1] : v[0];
+    const double t = keep + __shfl_xor(send, 16, 64);
+    return t + __shfl_xor(t, 32, 64);
+}
+
 // XCD-aware block order: the hardware deals blocks round-robin over the 8 XCDs
 // (block b -> XCD b % 8, MI355X_MICROARCH.md); remap so every XCD works on one
 // contiguous range of logical blocks — spatially coherent queries share that

@@ -331,9 +331,9 @@ __global__ void __launch_bounds__(kIcpTileQ * NW) icp_tile_kernel(IcpArgs a) {
 __global__ void __launch_bounds__(256) icp_stats_kernel(IcpArgs a) {
     __shared__ double red[4][kIcpStride];
     const int i = blockIdx.x * 256 + threadIdx.x;
-    double v[17];
+    double v[32];
 #pragma unroll
-    for (int k = 0; k < 17; ++k) v[k] = 0.0;
+    for (int k = 0; k < 32; ++k) v[k] = 0.0;
     if (i < a.n) {
         const int id = a.nn_id[i];
         const float d2 = a.nn_d2[i];
@@ -357,10 +357,10 @@ __global__ void __launch_bounds__(256) icp_stats_kernel(IcpArgs a) {
         }
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-#pragma unroll
-    for (int k = 0; k < 17; ++k) {  // DPP row reductions: the wave total lands in lane 63
-        const double t = wave_sum_to_lane63(v[k]);
-        if (lane == 63) red[wid][k] = t;
+    const double t = wave_sum32(v, lane);  // recursive halving (lio_dev.hpp)
+    if (lane < 32) {
+        const int k = wave_sum32_index(lane);
+        if (k < 17) red[wid][k] = t;
     }
     __syncthreads();
     if (threadIdx.x < kIcpStride) {

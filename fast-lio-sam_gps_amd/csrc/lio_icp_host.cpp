@@ -125,6 +125,7 @@ void umeyama(const double* st, const double c0[3], float Ti[16]) {
 
 struct EvPair {
     hipEvent_t a = nullptr, b = nullptr;
+    hipEvent_t done = nullptr;  // a pass's statistics have reached the host
 };
 
 }  // namespace
@@ -210,6 +211,7 @@ int lio_icp_create(const lio_icp_params* p, lio_icp** out) {
     }
     (void)hipEventCreate(&h->ev.a);
     (void)hipEventCreate(&h->ev.b);
+    (void)hipEventCreateWithFlags(&h->ev.done, hipEventDisableTiming);
     *out = h;
     return LIO_OK;
 }
@@ -226,6 +228,7 @@ int lio_icp_destroy(lio_icp* h) {
     if (h->h_super) (void)hipHostFree(h->h_super);
     if (h->ev.a) (void)hipEventDestroy(h->ev.a);
     if (h->ev.b) (void)hipEventDestroy(h->ev.b);
+    if (h->ev.done) (void)hipEventDestroy(h->ev.done);
     (void)hipStreamDestroy(h->st);
     delete h;
     return LIO_OK;
@@ -360,15 +363,20 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
         if (h->timing) IHIP(hipEventRecord(h->ev.a, h->st));
         lio::launch_icp_tiles(a, h->ntiles, h->st);
         lio::launch_icp_stats(a, h->st);
-        if (!fitness && icp_order_on())  // longest-first order for the next pass of this alignment
-            lio::launch_icp_order(h->d_tcost, h->ntiles, h->d_order, h->st);
         if (h->timing) IHIP(hipEventRecord(h->ev.b, h->st));
         lio::launch_icp_reduce(h->d_part, nch, h->d_super, h->st);
         IHIP(hipGetLastError());
         IHIP(hipMemcpyAsync(h->h_super, h->d_super, (size_t)nsup_loc * lio::kIcpStride * sizeof(double),
                             hipMemcpyDeviceToHost, h->st));
+        IHIP(hipEventRecord(h->ev.done, h->st));
+        // longest-first order for the next pass of this alignment: behind the copy, so it runs
+        // while the host does the SVD / convergence test
+        if (!fitness && icp_order_on()) lio::launch_icp_order(h->d_tcost, h->ntiles, h->d_order, h->st);
+        IHIP(hipGetLastError());
+        IHIP(hipEventSynchronize(h->ev.done));
+    } else {
+        IHIP(hipStreamSynchronize(h->st));
     }
-    IHIP(hipStreamSynchronize(h->st));
     h->have_prior = true;
     if (!fitness && h->sh_n > 0 && icp_order_on()) h->have_order = true;
     if (dbg_on) {

@@ -45,26 +45,8 @@ __device__ __forceinline__ double wave_sum(double v) {
 }
 
 // Wave reduction of one lane's contribution [HTH(21), HTh(6), cnt, res, hh]
-// by recursive halving: at each step a lane keeps half of its remaining
-// values and adds the partner's copy of that half (the partner keeps the
-// other half), so 32 values take 16+8+4+2+1 exchanges and adds instead of
-// 32 x 6.  Partners: row_mirror (lane bit 3 decides the half), row_half_mirror
-// (bit 2), quad_perm xor 2 (bit 1), xor 1 (bit 0), xor 16 (bit 4; a mirror
-// partner flips the lower bits too, so the mirrors go first, while every
-// partner pair still holds the same index set), then xor 32.  Lane l < 32 ends
-// with the wave total of value 16*b3 + 8*b2 + 4*b1 + 2*b0 + b4 (bits of l) and
-// stores it: a fixed order for a given lane assignment (deterministic).
-template <int CTRL, int BIT, int H>
-__device__ __forceinline__ void halve_step(double (&v)[32], int lane) {
-    const bool up = (lane >> BIT) & 1;
-#pragma unroll
-    for (int j = 0; j < H; ++j) {
-        const double send = up ? v[j] : v[j + H];
-        const double keep = up ? v[j + H] : v[j];
-        v[j] = keep + dpp_d<CTRL, 0xf>(send);
-    }
-}
-
+// (wave_sum32, lio_dev.hpp: recursive halving); lane l < 32 stores value
+// wave_sum32_index(l): a fixed order, deterministic.
 __device__ __forceinline__ void wave_reduce_store(const double J[6], double h, double res, double cnt, double* dst) {
     const int lane = threadIdx.x & 63;
     double v[32];
@@ -80,22 +62,8 @@ __device__ __forceinline__ void wave_reduce_store(const double J[6], double h, d
     v[29] = h * h;
     v[30] = 0.0;
     v[31] = 0.0;
-    halve_step<0x140, 3, 16>(v, lane);  // row_mirror
-    halve_step<0x141, 2, 8>(v, lane);   // row_half_mirror
-    halve_step<0x4e, 1, 4>(v, lane);    // quad_perm [2,3,0,1]
-    halve_step<0xb1, 0, 2>(v, lane);    // quad_perm [1,0,3,2]
-    {
-        const bool up = (lane >> 4) & 1;
-        const double send = up ? v[0] : v[1];
-        const double keep = up ? v[1] : v[0];
-        v[0] = keep + __shfl_xor(send, 16, 64);
-    }
-    const double tot = v[0] + __shfl_xor(v[0], 32, 64);
-    if (lane < 32) {
-        const int idx = ((lane >> 3) & 1) * 16 + ((lane >> 2) & 1) * 8 + ((lane >> 1) & 1) * 4 + (lane & 1) * 2 +
-                        ((lane >> 4) & 1);
-        dst[idx] = tot;
-    }
+    const double tot = wave_sum32(v, lane);
+    if (lane < 32) dst[wave_sum32_index(lane)] = tot;
 }
 
 // pd2 / s-gate / H row of one selected point (h_share_model [U])
