@@ -28,10 +28,7 @@
 
 namespace lio {
 
-#ifndef LIO_HBLOCK
-#define LIO_HBLOCK 256
-#endif
-constexpr int kBlock = LIO_HBLOCK;
+constexpr int kBlock = 256;  // plane / reuse: 1 point per lane (1024-thread blocks measured slower)
 
 constexpr int kGroup = 8;   // lanes cooperating on one query's kNN
 constexpr int kKnnBlock = 512;
