@@ -1,4 +1,4 @@
-"""world_size-2 gloo test of the sharded loop-ICP exchange (CPU).
+"""world_size 2, 3 and 4 gloo tests of the sharded loop-ICP exchange (CPU).
 
 Each rank owns a contiguous range of 4096-point records (lio_icp_shard_range),
 all-gathers its record statistics through lio_gpu.dist (the same code path the
@@ -65,7 +65,7 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_sharded_icp_exchange_gloo(world):
     import sys
 
