@@ -250,17 +250,19 @@ __device__ __forceinline__ void publish_and_finalize(const MatchArgs& a, double 
     const int b0 = grp * per, b1 = min(nb, b0 + per);
     double acc = 0.0;
     int b = b0;
-    for (; b + 32 <= b1; b += 32) {  // 32 sc1 loads in flight per thread (cross-XCD: each batch is an L2 miss)
+    // batches of 32 sc1 loads in flight per thread (cross-XCD: each batch is an L2 miss), the
+    // last batch masked rather than finished one load at a time (a serial tail of 27 loads
+    // doubled the kernel at C5's 469 blocks)
+    for (; b < b1; b += 32) {
         double v[32];
 #pragma unroll
         for (int k = 0; k < 32; ++k)
-            v[k] = __hip_atomic_load((gdouble*)(a.partials + (size_t)(b + k) * 32 + col), __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT);
+            v[k] = b + k < b1 ? __hip_atomic_load((gdouble*)(a.partials + (size_t)(b + k) * 32 + col), __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT)
+                              : 0.0;
 #pragma unroll
         for (int k = 0; k < 32; ++k) acc += v[k];
     }
-    for (; b < b1; ++b)
-        acc += __hip_atomic_load((gdouble*)(a.partials + (size_t)b * 32 + col), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __shared__ double sg[NG][33];
     sg[grp][col] = acc;
     __syncthreads();

@@ -2,7 +2,7 @@
 # GPU-box session: parity tests, smoke, bench, rocprof.  Each GPU step has its
 # own time limit; any fault / abort / timeout (exit status other than 0 or 1)
 # ends the session immediately — nothing else touches the GPU after it.
-# usage: scripts/gpu_session.sh <tag> [steps...]   steps: test smoke bench prof pmc
+# usage: scripts/gpu_session.sh <tag> [steps...]   steps: test smoke bench prof pmc c3 c5 ppprof quick knn rehearse
 set -u
 TAG=${1:-r01}; shift || true
 STEPS=${*:-"test smoke bench prof"}
@@ -35,6 +35,7 @@ for s in $STEPS; do
            run knn_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/knnprof" -o run --output-format csv -- python scripts/knn_timing.py C2 ;;
     quick) run bench_quick 400 python bench.py --steps 60 --warmup 5 --icp-reps 2 --cpu-seconds 4 ;;
     c3)    run bench_c3 600 python bench.py --config C3 --steps 60 --warmup 5 --no-icp --cpu-seconds 4 --pipeline 12 ;;
+    c5)    run bench_c5 600 python bench.py --config C5 --steps 60 --warmup 5 --no-icp --cpu-seconds 4 --pipeline 12 ;;
     ppprof) run rocprof_pipeline 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/ppprof" -o run \
                --output-format csv -- python bench.py --config C3 --steps 5 --warmup 2 --no-icp --no-cpu --pipeline 12 ;;
     rehearse) LIO_BENCH_REHEARSE=1 run rehearse2 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
