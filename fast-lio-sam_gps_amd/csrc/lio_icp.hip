@@ -8,11 +8,10 @@
 //                    (PCL transformCloud, float SSE order [U]), exact
 //                    unbounded 1-NN in the target grid with the candidate
 //                    points staged through LDS once per tile
-//   icp_stats_kernel per 256-point chunk (index order): Umeyama sufficient
-//                    statistics of the accepted correspondences
+//   icp_stats_kernel one 1024-thread block per 4096-point record: Umeyama
+//                    sufficient statistics of the accepted correspondences
 //                    (d2 <= 52.5^2) in double about a fixed centre c0:
-//                    count, sum p, sum q, sum q p^T, sum d2
-//   icp_reduce_kernel 16 chunks -> one 4096-point record, fixed order
+//                    count, sum p, sum q, sum q p^T, sum d2 (fixed order)
 // The 4096-point records are what ranks all-gather (deterministic, identical
 // for any number of ranks).  The fitness pass is the same pipeline on the
 // ORIGINAL source transformed by the final T.
@@ -327,33 +326,47 @@ __global__ void __launch_bounds__(kIcpTileQ * NW) icp_tile_kernel(IcpArgs a) {
 }
 
 
-// one block = one 256-point chunk -> partials[chunk][kIcpStride]
-__global__ void __launch_bounds__(256) icp_stats_kernel(IcpArgs a) {
-    __shared__ double red[4][kIcpStride];
-    const int i = blockIdx.x * 256 + threadIdx.x;
+// One block = one 4096-point record -> super[record][kIcpStride]: each lane
+// accumulates its 4 points (record-relative index lane + 1024 k, k ascending),
+// each wave sums its lanes (wave_sum32, recursive halving), and the 16 wave
+// sums are added in wave order.  A fixed order for a given record, so the
+// records (what ranks all-gather) are bit-identical for any number of ranks.
+constexpr int kIcpStatsThreads = 1024;
+__global__ void __launch_bounds__(kIcpStatsThreads) icp_stats_kernel(IcpArgs a, double* __restrict__ super) {
+    constexpr int NW = kIcpStatsThreads / 64, PER = kIcpSuper / kIcpStatsThreads;
+    __shared__ double red[NW][kIcpStride];
     double v[32];
 #pragma unroll
     for (int k = 0; k < 32; ++k) v[k] = 0.0;
-    if (i < a.n) {
-        const int id = a.nn_id[i];
-        const float d2 = a.nn_d2[i];
+    int ids[PER];
+    float d2s[PER];
+    const int base = blockIdx.x * kIcpSuper + threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {  // all correspondence loads first: one round trip
+        const int i = base + k * kIcpStatsThreads;
+        ids[k] = i < a.n ? a.nn_id[i] : -1;
+        d2s[k] = i < a.n ? a.nn_d2[i] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        const int i = base + k * kIcpStatsThreads, id = ids[k];
+        const float d2 = d2s[k];
+        if (id < 0 || id == kNone) continue;
         if (a.fitness) {
-            if (id >= 0 && id != kNone) {
-                v[0] = 1.0;
-                v[16] = (double)d2;
-            }
-        } else if (id >= 0 && id != kNone && !((double)d2 > a.max_d2)) {
+            v[0] += 1.0;
+            v[16] += (double)d2;
+        } else if (!((double)d2 > a.max_d2)) {
             const float4 q = a.tgt_by_id[id];
             const double p0 = (double)a.cur[3 * i] - a.c0[0], p1 = (double)a.cur[3 * i + 1] - a.c0[1],
                          p2 = (double)a.cur[3 * i + 2] - a.c0[2];
             const double q0 = (double)q.x - a.c0[0], q1 = (double)q.y - a.c0[1], q2 = (double)q.z - a.c0[2];
-            v[0] = 1.0;
-            v[1] = p0; v[2] = p1; v[3] = p2;
-            v[4] = q0; v[5] = q1; v[6] = q2;
-            v[7] = q0 * p0; v[8] = q0 * p1; v[9] = q0 * p2;
-            v[10] = q1 * p0; v[11] = q1 * p1; v[12] = q1 * p2;
-            v[13] = q2 * p0; v[14] = q2 * p1; v[15] = q2 * p2;
-            v[16] = (double)d2;
+            v[0] += 1.0;
+            v[1] += p0; v[2] += p1; v[3] += p2;
+            v[4] += q0; v[5] += q1; v[6] += q2;
+            v[7] += q0 * p0; v[8] += q0 * p1; v[9] += q0 * p2;
+            v[10] += q1 * p0; v[11] += q1 * p1; v[12] += q1 * p2;
+            v[13] += q2 * p0; v[14] += q2 * p1; v[15] += q2 * p2;
+            v[16] += (double)d2;
         }
     }
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -366,20 +379,10 @@ __global__ void __launch_bounds__(256) icp_stats_kernel(IcpArgs a) {
     if (threadIdx.x < kIcpStride) {
         double s = 0.0;
         if (threadIdx.x < 17)
-            for (int w = 0; w < 4; ++w) s += red[w][threadIdx.x];
-        a.partials[(size_t)blockIdx.x * kIcpStride + threadIdx.x] = s;
+#pragma unroll
+            for (int w = 0; w < NW; ++w) s += red[w][threadIdx.x];
+        super[(size_t)blockIdx.x * kIcpStride + threadIdx.x] = s;
     }
-}
-
-// 16 consecutive chunk records -> one 4096-point record, ascending order
-__global__ void icp_reduce_kernel(const double* __restrict__ partials, int nchunks, double* __restrict__ super) {
-    const int sidx = blockIdx.x;
-    const int k = threadIdx.x;
-    if (k >= kIcpStride) return;
-    constexpr int per = kIcpSuper / kIcpChunk;
-    double s = 0.0;
-    for (int c = sidx * per; c < min(nchunks, (sidx + 1) * per); ++c) s += partials[(size_t)c * kIcpStride + k];
-    super[(size_t)sidx * kIcpStride + k] = s;
 }
 
 void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st) {
@@ -469,14 +472,9 @@ int icp_build_tiles(const GridBuf& q, uint2* tiles, uint32_t* scratch, void*& tm
     return (int)total;
 }
 
-void launch_icp_stats(const IcpArgs& a, hipStream_t st) {
+void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st) {
     if (a.n == 0) return;
-    icp_stats_kernel<<<(a.n + 255) / 256, 256, 0, st>>>(a);
-}
-void launch_icp_reduce(const double* partials, int nchunks, double* super, hipStream_t st) {
-    const int ns = (nchunks + (kIcpSuper / kIcpChunk) - 1) / (kIcpSuper / kIcpChunk);
-    if (ns == 0) return;
-    icp_reduce_kernel<<<ns, 64, 0, st>>>(partials, nchunks, super);
+    icp_stats_kernel<<<(a.n + kIcpSuper - 1) / kIcpSuper, kIcpStatsThreads, 0, st>>>(a, super);
 }
 
 }  // namespace lio

@@ -162,7 +162,6 @@ struct lio_icp {
     uint32_t* d_order = nullptr;  // longest-first tile order (valid when have_order)
     bool have_order = false;
     unsigned long long* d_dbg = nullptr;  // LIO_ICP_DEBUG counters
-    double* d_part = nullptr;
     double* d_super = nullptr;
     double* h_super = nullptr;  // pinned
     int64_t super_cap = 0;
@@ -222,7 +221,7 @@ int lio_icp_destroy(lio_icp* h) {
     (void)hipStreamSynchronize(h->st);
     lio::grid_free(h->tgt);
     lio::grid_free(h->qgrid);
-    void* ptrs[] = {h->d_tgt, h->d_src, h->d_cur, h->d_fd2, h->d_fid, h->d_tiles, h->d_tscratch, h->d_ttmp, h->d_dbg, h->d_tcost, h->d_order, h->d_part, h->d_super};
+    void* ptrs[] = {h->d_tgt, h->d_src, h->d_cur, h->d_fd2, h->d_fid, h->d_tiles, h->d_tscratch, h->d_ttmp, h->d_dbg, h->d_tcost, h->d_order, h->d_super};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (h->h_super) (void)hipHostFree(h->h_super);
@@ -275,10 +274,9 @@ static int icp_prepare(lio_icp* h) {
     shard_range(h->ns, h->rank, h->world, h->sh_begin, h->sh_n);
     const int64_t n = std::max<int64_t>(h->sh_n, 1);
     if (n > h->cap) {
-        void* ptrs[] = {h->d_src, h->d_cur, h->d_fd2, h->d_fid, h->d_tiles, h->d_tcost, h->d_order, h->d_part};
+        void* ptrs[] = {h->d_src, h->d_cur, h->d_fd2, h->d_fid, h->d_tiles, h->d_tcost, h->d_order};
         for (void* q : ptrs)
             if (q) IHIP(hipFree(q));
-        const int64_t nch = (n + lio::kIcpChunk - 1) / lio::kIcpChunk;
         IHIP(hipMalloc(&h->d_src, n * 3 * sizeof(float)));
         IHIP(hipMalloc(&h->d_cur, n * 3 * sizeof(float)));
         IHIP(hipMalloc(&h->d_fd2, n * sizeof(float)));
@@ -286,7 +284,6 @@ static int icp_prepare(lio_icp* h) {
         IHIP(hipMalloc(&h->d_tiles, (n + n / lio::kIcpTileQ + 1) * sizeof(uint2)));
         IHIP(hipMalloc(&h->d_tcost, (n + n / lio::kIcpTileQ + 1) * sizeof(uint32_t)));
         IHIP(hipMalloc(&h->d_order, (n + n / lio::kIcpTileQ + 1) * sizeof(uint32_t)));
-        IHIP(hipMalloc(&h->d_part, nch * lio::kIcpStride * sizeof(double)));
         h->cap = n;
     }
     const int64_t nsup_all = (h->ns + lio::kIcpSuper - 1) / lio::kIcpSuper + 1;
@@ -344,7 +341,6 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     a.max_d2 = max_d2;
     a.fitness = fitness ? 1 : 0;
     a.prior = h->have_prior ? 1 : 0;
-    a.partials = h->d_part;
     a.nn_d2 = h->d_fd2;
     a.nn_id = h->d_fid;
     a.qpts = h->qgrid.pts;
@@ -357,14 +353,12 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
         IHIP(hipMemsetAsync(h->d_dbg, 0, 64, h->st));
         a.dbg = h->d_dbg;
     }
-    const int nch = (int)((h->sh_n + lio::kIcpChunk - 1) / lio::kIcpChunk);
     const int nsup_loc = (int)((h->sh_n + lio::kIcpSuper - 1) / lio::kIcpSuper);
     if (h->sh_n > 0) {
         if (h->timing) IHIP(hipEventRecord(h->ev.a, h->st));
         lio::launch_icp_tiles(a, h->ntiles, h->st);
-        lio::launch_icp_stats(a, h->st);
+        lio::launch_icp_stats(a, h->d_super, h->st);
         if (h->timing) IHIP(hipEventRecord(h->ev.b, h->st));
-        lio::launch_icp_reduce(h->d_part, nch, h->d_super, h->st);
         IHIP(hipGetLastError());
         IHIP(hipMemcpyAsync(h->h_super, h->d_super, (size_t)nsup_loc * lio::kIcpStride * sizeof(double),
                             hipMemcpyDeviceToHost, h->st));

@@ -110,7 +110,6 @@ struct IcpArgs {
     double max_d2;       // correspondence rejection (d2 > max_d2 => skip)
     int fitness;         // 1: fitness pass (src with T, unbounded, sum d2 only)
     int prior;           // 1: nn_id holds this alignment's previous correspondences (a starting bound)
-    double* partials;    // per 256-point chunk: 17 doubles padded to 20
     float* nn_d2;        // per point: 1-NN squared distance (n)
     int* nn_id;          //            1-NN target id
     const float4* qpts;  // source binned by tile cell: (x, y, z, local index bits), cell order
@@ -120,9 +119,8 @@ struct IcpArgs {
     unsigned long long* dbg;  // optional counters (diagnostics): candidates, rings, tiles, lanes
 };
 
-constexpr int kIcpChunk = 256;     // points per partial
 constexpr int kIcpSuper = 4096;    // points per exchanged partial (shard granule)
-constexpr int kIcpStride = 20;     // doubles per partial record
+constexpr int kIcpStride = 20;     // doubles per record (17 statistics, padded)
 
 constexpr int kIcpTileQ = 64;     // queries per tile (one wave)
 
@@ -133,7 +131,6 @@ int icp_build_tiles(const GridBuf& q, uint2* tiles, uint32_t* scratch, void*& tm
 void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st);
 // tile order for the next pass: descending log2(cost) buckets (one block)
 void launch_icp_order(const uint32_t* tile_cost, int ntiles, uint32_t* order, hipStream_t st);
-void launch_icp_stats(const IcpArgs& a, hipStream_t st);
-void launch_icp_reduce(const double* partials, int nchunks, double* super, hipStream_t st);
+void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st);  // one record per 4096 points
 
 }  // namespace lio
