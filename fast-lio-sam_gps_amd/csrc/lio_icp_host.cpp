@@ -162,8 +162,8 @@ struct lio_icp {
     uint32_t* d_order = nullptr;  // longest-first tile order (valid when have_order)
     bool have_order = false;
     unsigned long long* d_dbg = nullptr;  // LIO_ICP_DEBUG counters
-    double* d_super = nullptr;
-    double* h_super = nullptr;  // pinned
+    double* h_super = nullptr;      // pinned, host-mapped: the pass's 4096-point records
+    double* h_super_dev = nullptr;  // device view of h_super (the statistics kernel writes it, zero-copy)
     int64_t super_cap = 0;
     bool src_dirty = true;
     bool timing = false;
@@ -221,7 +221,7 @@ int lio_icp_destroy(lio_icp* h) {
     (void)hipStreamSynchronize(h->st);
     lio::grid_free(h->tgt);
     lio::grid_free(h->qgrid);
-    void* ptrs[] = {h->d_tgt, h->d_src, h->d_cur, h->d_fd2, h->d_fid, h->d_tiles, h->d_tscratch, h->d_ttmp, h->d_dbg, h->d_tcost, h->d_order, h->d_super};
+    void* ptrs[] = {h->d_tgt, h->d_src, h->d_cur, h->d_fd2, h->d_fid, h->d_tiles, h->d_tscratch, h->d_ttmp, h->d_dbg, h->d_tcost, h->d_order};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (h->h_super) (void)hipHostFree(h->h_super);
@@ -288,10 +288,9 @@ static int icp_prepare(lio_icp* h) {
     }
     const int64_t nsup_all = (h->ns + lio::kIcpSuper - 1) / lio::kIcpSuper + 1;
     if (nsup_all > h->super_cap) {
-        if (h->d_super) IHIP(hipFree(h->d_super));
         if (h->h_super) IHIP(hipHostFree(h->h_super));
-        IHIP(hipMalloc(&h->d_super, nsup_all * lio::kIcpStride * sizeof(double)));
-        IHIP(hipHostMalloc(&h->h_super, nsup_all * lio::kIcpStride * sizeof(double)));
+        IHIP(hipHostMalloc(&h->h_super, nsup_all * lio::kIcpStride * sizeof(double), hipHostMallocMapped));
+        IHIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->h_super_dev), h->h_super, 0));
         h->super_cap = nsup_all;
     }
     h->ntiles = 0;
@@ -357,13 +356,11 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     if (h->sh_n > 0) {
         if (h->timing) IHIP(hipEventRecord(h->ev.a, h->st));
         lio::launch_icp_tiles(a, h->ntiles, h->st);
-        lio::launch_icp_stats(a, h->d_super, h->st);
+        lio::launch_icp_stats(a, h->h_super_dev, h->st);  // records straight to host memory
         if (h->timing) IHIP(hipEventRecord(h->ev.b, h->st));
         IHIP(hipGetLastError());
-        IHIP(hipMemcpyAsync(h->h_super, h->d_super, (size_t)nsup_loc * lio::kIcpStride * sizeof(double),
-                            hipMemcpyDeviceToHost, h->st));
         IHIP(hipEventRecord(h->ev.done, h->st));
-        // longest-first order for the next pass of this alignment: behind the copy, so it runs
+        // longest-first order for the next pass of this alignment: behind the records, so it runs
         // while the host does the SVD / convergence test
         if (!fitness && icp_order_on()) lio::launch_icp_order(h->d_tcost, h->ntiles, h->d_order, h->st);
         IHIP(hipGetLastError());
