@@ -280,7 +280,7 @@ __global__ void __launch_bounds__(kIcpTileQ * NW) icp_tile_kernel(IcpArgs a) {
     // 1. bound: grow a box around Q until every lane holds a candidate;
     // 2. final: everything within sqrt(B) of the tile box, minus what was scanned
     CellBox S{1, 0, 1, 0, 1, 0};  // scanned so far (empty)
-    int r = 0;
+    int r = a.r0;
     for (;;) {
         const bool grow = __any(act && (uint32_t)best == (uint32_t)kNone);  // block-uniform (lists merged)
         CellBox N;

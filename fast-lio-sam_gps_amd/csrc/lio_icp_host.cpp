@@ -340,6 +340,11 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     a.max_d2 = max_d2;
     a.fitness = fitness ? 1 : 0;
     a.prior = h->have_prior ? 1 : 0;
+    static const int r0 = [] {  // LIO_ICP_R0: first bound box growth (1: rounds/tile 2.73 -> 2.19 at C4)
+        const char* e = std::getenv("LIO_ICP_R0");
+        return e ? std::max(0, std::atoi(e)) : 1;
+    }();
+    a.r0 = r0;
     a.nn_d2 = h->d_fd2;
     a.nn_id = h->d_fid;
     a.qpts = h->qgrid.pts;

@@ -110,6 +110,7 @@ struct IcpArgs {
     double max_d2;       // correspondence rejection (d2 > max_d2 => skip)
     int fitness;         // 1: fitness pass (src with T, unbounded, sum d2 only)
     int prior;           // 1: nn_id holds this alignment's previous correspondences (a starting bound)
+    int r0;              // first bound box: the tile's cells grown by r0 target cells
     float* nn_d2;        // per point: 1-NN squared distance (n)
     int* nn_id;          //            1-NN target id
     const float4* qpts;  // source binned by tile cell: (x, y, z, local index bits), cell order
