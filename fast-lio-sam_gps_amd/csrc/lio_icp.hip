@@ -2,12 +2,14 @@
 // /root/reference/fast_lio_sam/src/loop_closure.cpp:3-14, aligned at :81) on gfx950.
 //
 // Per ICP iteration (this rank's shard of the source):
-//   icp_tile_kernel  one wave per tile of <= 64 spatially compact source
-//                    points (binned once per setInputSource): apply the
-//                    previous T_inc to the incrementally transformed cloud
-//                    (PCL transformCloud, float SSE order [U]), exact
-//                    unbounded 1-NN in the target grid with the candidate
-//                    points staged through LDS once per tile
+//   icp_tile_kernel  one block (2 waves splitting the candidate stream) per
+//                    tile of <= 64 spatially compact source points (binned
+//                    once per setInputSource): apply the previous T_inc to
+//                    the incrementally transformed cloud (PCL transformCloud,
+//                    float SSE order [U]), exact unbounded 1-NN in the target
+//                    grid with the candidate points staged through LDS once
+//                    per tile; tiles visited longest-first in the pass after
+//                    the first (icp_order_kernel, from this pass's counts)
 //   icp_stats_kernel one 1024-thread block per 4096-point record: Umeyama
 //                    sufficient statistics of the accepted correspondences
 //                    (d2 <= 52.5^2) in double about a fixed centre c0:
