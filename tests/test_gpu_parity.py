@@ -464,3 +464,26 @@ def test_sums_handoff_under_load(c1):
     finally:
         stop.set()
         th.join()
+
+
+@pytest.mark.parametrize("n_pts", [120_001, 200_000])
+def test_h_model_many_blocks_matches_oracle(oracle, n_pts):
+    """Scan sizes whose plane / reuse grids (469, 782 blocks) leave the last block's partial
+    gather a multi-batch masked tail: sums of a redo and a reuse evaluation against the
+    oracle (C2 map, the C2 scan repeated with a small offset to reach n_pts)."""
+    _, m, scans = synth.make_config("C2", n_scans=1)
+    sc = scans[0]
+    reps = -(-n_pts // len(sc.body))
+    body = np.concatenate([sc.body + np.float32(0.013 * k) for k in range(reps)])[:n_pts].astype(np.float32)
+    tree = F.IkdTreeGPU(cell_size=1.0)
+    tree.Build(m)
+    hm = F.HShareModelGPU(tree)
+    hm.set_scan(body)
+    p24 = synth.pose24(synth.initial_state(sc.pos_init, sc.rot_init))
+    om = oracle.OracleMap(m)
+    o_redo, nn, sel, planes = _oracle_eval(oracle, om, body, p24)
+    _check_sums(hm(p24, True), o_redo)
+    p2 = p24.copy()
+    p2[9:12] += np.array([0.02, -0.01, 0.005])
+    o_reuse, _, _, _ = _oracle_eval(oracle, om, body, p2, nn, sel, planes, redo=False)
+    _check_sums(hm(p2, False), o_reuse)
