@@ -58,7 +58,7 @@ def parse():
     ap.add_argument("--streams", default="2,8",
                     help="secondary figure: S independent scan streams (own map + ctx + HIP stream each) "
                          "driven by S host threads in this process; '' to skip (reported under 'multi_stream')")
-    ap.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline sample at all cores "
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample at all cores "
                     "(plus half of it at 1 and at 3 threads)")
     ap.add_argument("--pipeline", type=int, default=0, metavar="N",
                     help="also time N raw scans through the whole front end: Preprocess + UndistortPcl + "
