@@ -9,7 +9,7 @@ STEPS=${*:-"test smoke bench prof"}
 OUT=gpurun_out/$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
-echo "host: $(nproc) cpus; $(grep -m1 'model name' /proc/cpuinfo)" | tee "$OUT/host.txt"
+echo "host: $(nproc) cpus; $(grep -m1 'model name' /proc/cpuinfo); cpu.max: $(cat /sys/fs/cgroup/cpu.max 2>/dev/null); affinity: $(python3 -c 'import os;print(len(os.sched_getaffinity(0)))')" | tee "$OUT/host.txt"
 
 run() {  # run <name> <seconds> <cmd...>
     local name=$1 secs=$2; shift 2
@@ -33,9 +33,9 @@ for s in $STEPS; do
     knn)   run knn_timing 300 python scripts/knn_timing.py C2 &&
            LIO_FAR_BLOCKS=8 run knn_timing_fb8 300 python scripts/knn_timing.py C2 &&
            run knn_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/knnprof" -o run --output-format csv -- python scripts/knn_timing.py C2 ;;
-    quick) run bench_quick 400 python bench.py --steps 60 --warmup 5 --icp-reps 2 --cpu-seconds 4 ;;
-    c3)    run bench_c3 600 python bench.py --config C3 --steps 60 --warmup 5 --no-icp --cpu-seconds 4 --pipeline 12 ;;
-    c5)    run bench_c5 600 python bench.py --config C5 --steps 60 --warmup 5 --no-icp --cpu-seconds 4 --pipeline 12 ;;
+    quick) run bench_quick 400 python bench.py --steps 60 --warmup 5 --icp-reps 2 --cpu-scans 10 --cpu-warmup 2 ;;
+    c3)    run bench_c3 600 python bench.py --config C3 --steps 60 --warmup 5 --no-icp --cpu-scans 10 --cpu-warmup 2 --pipeline 12 ;;
+    c5)    run bench_c5 600 python bench.py --config C5 --steps 60 --warmup 5 --no-icp --cpu-scans 10 --cpu-warmup 2 --pipeline 12 ;;
     ppprof) run rocprof_pipeline 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/ppprof" -o run \
                --output-format csv -- python bench.py --config C3 --steps 5 --warmup 2 --no-icp --no-cpu --pipeline 12 ;;
     rehearse) LIO_BENCH_REHEARSE=1 run rehearse2 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
