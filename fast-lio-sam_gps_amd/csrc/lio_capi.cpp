@@ -66,6 +66,44 @@ struct EventPair {
     hipEvent_t a = nullptr, b = nullptr;
 };
 
+// Eigen 3.3 quaternionbase_assign_impl<Other,3,3>::run (Geometry/Quaternion.h): rotation matrix ->
+// quaternion (w, x, y, z), trace = m00 + (m11 + m22).  Only for callers that hand over matrices
+// without the state quaternion (lio_pose.q all zero); the oracle derives it the same way.
+void mat_to_quat(const double* m, double* q) {
+    auto M = [&](int r, int c) { return m[3 * r + c]; };
+    double t = M(0, 0) + (M(1, 1) + M(2, 2));
+    double c[4];  // x, y, z, w
+    if (t > 0.0) {
+        t = std::sqrt(t + 1.0);
+        c[3] = 0.5 * t;
+        t = 0.5 / t;
+        c[0] = (M(2, 1) - M(1, 2)) * t;
+        c[1] = (M(0, 2) - M(2, 0)) * t;
+        c[2] = (M(1, 0) - M(0, 1)) * t;
+    } else {
+        int i = 0;
+        if (M(1, 1) > M(0, 0)) i = 1;
+        if (M(2, 2) > M(i, i)) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = std::sqrt(M(i, i) - M(j, j) - M(k, k) + 1.0);
+        c[i] = 0.5 * t;
+        t = 0.5 / t;
+        c[3] = (M(k, j) - M(j, k)) * t;
+        c[j] = (M(j, i) + M(i, j)) * t;
+        c[k] = (M(k, i) + M(i, k)) * t;
+    }
+    q[0] = c[3], q[1] = c[0], q[2] = c[1], q[3] = c[2];
+}
+
+bool quat_zero(const double* q) { return q[0] == 0.0 && q[1] == 0.0 && q[2] == 0.0 && q[3] == 0.0; }
+
+lio_pose filled(const lio_pose& p) {
+    lio_pose o = p;
+    if (quat_zero(o.q)) mat_to_quat(o.R, o.q);
+    if (quat_zero(o.q_LI)) mat_to_quat(o.R_LI, o.q_LI);
+    return o;
+}
+
 }  // namespace
 
 // =============================================================================
@@ -73,6 +111,7 @@ struct EventPair {
 // =============================================================================
 struct lio_map {
     uint64_t version = 0;  // bumped by every change of the point set (seeded kNN validity)
+    std::atomic<int> n_ctx{0};  // live lio_ctx handles on this map (destroy refuses while > 0)
     int dev = 0;
     hipStream_t st = nullptr;
     lio_map_params p{};
@@ -171,6 +210,8 @@ int lio_map_create(const lio_map_params* p, lio_map** out) {
 
 int lio_map_destroy(lio_map* m) {
     if (!m) return LIO_OK;
+    if (m->n_ctx.load() > 0)
+        return fail(LIO_ERR_STATE, "lio_map_destroy: h_share_model contexts still use this map (lio_ctx_destroy them first)");
     (void)hipSetDevice(m->dev);
     (void)hipStreamSynchronize(m->st);
     lio::grid_free(m->grid);
@@ -180,6 +221,15 @@ int lio_map_destroy(lio_map* m) {
     if (m->d_qd2) (void)hipFree(m->d_qd2);
     (void)hipStreamDestroy(m->st);
     delete m;
+    return LIO_OK;
+}
+
+int lio_map_set_params(lio_map* m, const lio_map_params* p) {
+    if (!m || !p) return fail(LIO_ERR_ARG, "lio_map_set_params: bad arguments");
+    if (m->grid.n_ids > 0) return fail(LIO_ERR_STATE, "lio_map_set_params: map already holds points (call before Build)");
+    if (p->device != m->dev) return fail(LIO_ERR_ARG, "lio_map_set_params: device cannot change");
+    if (p->cell_size > 0.f) m->p.cell_size = p->cell_size;
+    if (p->downsample_size > 0.f) m->p.downsample_size = p->downsample_size;
     return LIO_OK;
 }
 
@@ -420,6 +470,7 @@ int lio_ctx_create(lio_map* m, const lio_match_params* p, lio_ctx** out) {
     HIP_TRY(hipSetDevice(m->dev));
     auto* c = new lio_ctx();
     c->map = m;
+    ++m->n_ctx;
     if (p)
         c->p = *p;
     else
@@ -431,6 +482,7 @@ int lio_ctx_create(lio_map* m, const lio_match_params* p, lio_ctx** out) {
         hipMalloc(&c->d_far_count, sizeof(int)) != hipSuccess ||
         hipMemset(c->d_far_count, 0, sizeof(int)) != hipSuccess || hipMalloc(&c->d_done, 64) != hipSuccess ||
         hipMemset(c->d_done, 0, 64) != hipSuccess) {
+        --m->n_ctx;
         delete c;
         return fail(LIO_ERR_NOMEM, "context allocation failed");
     }
@@ -461,13 +513,16 @@ int lio_ctx_destroy(lio_ctx* c) {
     lio::filter_free(c->filt);
     for (void* q : {(void*)c->d_raw, (void*)c->d_rec, (void*)c->d_poses})
         if (q) (void)hipFree(q);
+    --c->map->n_ctx;
     delete c;
     return LIO_OK;
 }
 
 static int ctx_reserve(lio_ctx* c, int64_t n) {
-    if (n > c->cap || !c->d_body) {
+    if (n > c->cap || !c->d_body || !c->d_nn || !c->d_planes || !c->d_sel || !c->d_far_list || !c->d_far_d ||
+        !c->d_far_id) {
         int64_t cap = std::max<int64_t>(n, c->cap + c->cap / 2);
+        c->cap = 0;  // a failed reallocation below leaves no buffer that looks usable
         void* ptrs[] = {c->d_body, c->d_nn, c->d_planes, c->d_sel, c->d_far_list, c->d_far_d, c->d_far_id};
         for (void* q : ptrs)
             if (q) (void)hipFree(q);
@@ -527,8 +582,11 @@ int lio_scan_bind_device(lio_ctx* c, const float* d_body, int64_t n) {
 
 static const float* body_ptr(const lio_ctx* c) { return c->body_ext ? c->body_ext : c->d_body; }
 
-static lio::MatchArgs make_args(lio_ctx* c, const lio_pose& pose) {
+static_assert(sizeof(lio_pose) == sizeof(lio::PoseArg), "lio_pose / PoseArg layout");
+
+static lio::MatchArgs make_args(lio_ctx* c, const lio_pose& pose_in) {
     lio::MatchArgs a{};
+    const lio_pose pose = filled(pose_in);
     std::memcpy(&a.pose, &pose, sizeof(lio::PoseArg));
     a.grid = lio::grid_view(c->map->grid);
     a.body = body_ptr(c);
@@ -608,10 +666,14 @@ static int wait_result(lio_ctx* c, unsigned long long seq, double* sums) {
     }
 }
 
-int lio_match(lio_ctx* c, const lio_pose* pose, int redo_knn, double* sums) {
-    if (!c || !pose || !sums) return fail(LIO_ERR_ARG, "lio_match: bad arguments");
+int lio_match(lio_ctx* c, const lio_pose* pose_in, int redo_knn, double* sums) {
+    if (!c || !pose_in || !sums) return fail(LIO_ERR_ARG, "lio_match: bad arguments");
+    const lio_pose pose_f = filled(*pose_in);
+    const lio_pose* pose = &pose_f;
     if (c->map->grid.n_ids == 0) return fail(LIO_ERR_STATE, "lio_match: map is empty (call lio_map_build)");
     if (!redo_knn && !c->knn_valid) return fail(LIO_ERR_STATE, "lio_match: redo_knn=0 before any kNN evaluation");
+    if (!redo_knn && c->knn_map_version != c->map->version)
+        return fail(LIO_ERR_STATE, "lio_match: redo_knn=0 but the map changed since this scan's kNN evaluation");
     HIP_TRY(hipSetDevice(c->map->dev));
     hipStream_t st = c->map->st;
     lio::MatchArgs a = make_args(c, *pose);
@@ -731,11 +793,15 @@ int lio_map_incremental(lio_ctx* c, const lio_pose* pose, double filter_size_map
     if (!c || !pose || !(filter_size_map > 0.0)) return fail(LIO_ERR_ARG, "lio_map_incremental: bad arguments");
     if (c->n > 0 && !c->knn_valid && c->map->n > 0)
         return fail(LIO_ERR_STATE, "lio_map_incremental: no kNN evaluation for this scan (Nearest_Points)");
+    if (c->n > 0 && c->map->n > 0 && c->knn_map_version != c->map->version)
+        return fail(LIO_ERR_STATE, "lio_map_incremental: the map changed since this scan's kNN evaluation");
     lio_map* m = c->map;
     HIP_TRY(hipSetDevice(m->dev));
     lio::IncrArgs a{};
-    std::memcpy(&a.pose, pose, sizeof(lio::PoseArg));
-    std::memcpy(&a.pose_knn, &c->knn_pose, sizeof(lio::PoseArg));
+    const lio_pose pf = filled(*pose);
+    std::memcpy(&a.pose, &pf, sizeof(lio::PoseArg));
+    const lio_pose pk = filled(c->knn_pose);
+    std::memcpy(&a.pose_knn, &pk, sizeof(lio::PoseArg));
     a.body = body_ptr(c);
     a.nn_idx = c->d_nn;
     a.n = (int)c->n;
@@ -880,6 +946,8 @@ int lio_ieskf_update(lio_ctx* c, lio_state* xs, double* P, const lio_ieskf_param
         lio_pose pose;
         lio::host::quat_to_mat(s.rot, pose.R);
         lio::host::quat_to_mat(s.offR, pose.R_LI);
+        pose.q[0] = s.rot.w, pose.q[1] = s.rot.x, pose.q[2] = s.rot.y, pose.q[3] = s.rot.z;
+        pose.q_LI[0] = s.offR.w, pose.q_LI[1] = s.offR.x, pose.q_LI[2] = s.offR.y, pose.q_LI[3] = s.offR.z;
         std::memcpy(pose.t, s.pos, sizeof(pose.t));
         std::memcpy(pose.t_LI, s.offT, sizeof(pose.t_LI));
         hm.rows.clear();
@@ -939,12 +1007,16 @@ static lio::UndistortEnd undistort_end(const lio_pose* e) {
     lio::UndistortEnd u{};
     if (!e) {
         for (int k = 0; k < 9; ++k) u.R[k] = u.R_LI[k] = (k % 4 == 0) ? 1.0 : 0.0;
+        u.q[0] = u.q_LI[0] = 1.0;
         return u;
     }
-    std::memcpy(u.pos, e->t, sizeof(u.pos));
-    std::memcpy(u.R, e->R, sizeof(u.R));
-    std::memcpy(u.R_LI, e->R_LI, sizeof(u.R_LI));
-    std::memcpy(u.t_LI, e->t_LI, sizeof(u.t_LI));
+    const lio_pose f = filled(*e);
+    std::memcpy(u.pos, f.t, sizeof(u.pos));
+    std::memcpy(u.R, f.R, sizeof(u.R));
+    std::memcpy(u.R_LI, f.R_LI, sizeof(u.R_LI));
+    std::memcpy(u.t_LI, f.t_LI, sizeof(u.t_LI));
+    std::memcpy(u.q, f.q, sizeof(u.q));
+    std::memcpy(u.q_LI, f.q_LI, sizeof(u.q_LI));
     return u;
 }
 

@@ -41,7 +41,31 @@ struct PoseArg {  // lio_pose
     double t[3];
     double RLI[9];
     double tLI[3];
+    double q[4];    // state rot as MTK::SO3 = Eigen::Quaternion<double>, (w, x, y, z)
+    double qLI[4];  // offset_R_L_I
 };
+
+// `Eigen::Quaternion<double> * Vector3d` as Eigen 3.3 evaluates it
+// (QuaternionBase::_transformVector, Geometry/Quaternion.h):
+//   uv = q.vec().cross(v); uv += uv; return v + q.w() * uv + q.vec().cross(uv);
+// conj: by q.conjugate() (vec negated).  Same operation order as the oracle's quat_rotate.
+__device__ __forceinline__ void quat_rotate(const double* q, bool conj, double v0, double v1, double v2,
+                                            double& o0, double& o1, double& o2) {
+    const double w = q[0];
+    const double x = conj ? -q[1] : q[1], y = conj ? -q[2] : q[2], z = conj ? -q[3] : q[3];
+    double u0 = y * v2 - z * v1;
+    double u1 = z * v0 - x * v2;
+    double u2 = x * v1 - y * v0;
+    u0 += u0;
+    u1 += u1;
+    u2 += u2;
+    const double c0 = y * u2 - z * u1;
+    const double c1 = z * u0 - x * u2;
+    const double c2 = x * u1 - y * u0;
+    o0 = (v0 + w * u0) + c0;
+    o1 = (v1 + w * u1) + c1;
+    o2 = (v2 + w * u2) + c2;
+}
 
 __device__ __forceinline__ float sqdist3(float ax, float ay, float az, float bx, float by, float bz) {
     float dx = ax - bx;
@@ -54,16 +78,16 @@ __device__ __forceinline__ bool lexless(float da, int ia, float db, int ib) {
     return da < db || (da == db && ia < ib);
 }
 
-// world = R*(R_LI*p + t_LI) + t in double, stored as float  (h_share_model [U])
+// pointBodyToWorld / h_share_model [U]: p_global = s.rot * (s.offset_R_L_I * p_body + s.offset_T_L_I)
+// + s.pos in double (both SO3 products through quat_rotate), stored as float
 __device__ __forceinline__ void body_to_world(const PoseArg& ps, float bx, float by, float bz, float& wx,
                                               float& wy, float& wz) {
-    double b0 = bx, b1 = by, b2 = bz;
-    double p0 = ((ps.RLI[0] * b0 + ps.RLI[1] * b1) + ps.RLI[2] * b2) + ps.tLI[0];
-    double p1 = ((ps.RLI[3] * b0 + ps.RLI[4] * b1) + ps.RLI[5] * b2) + ps.tLI[1];
-    double p2 = ((ps.RLI[6] * b0 + ps.RLI[7] * b1) + ps.RLI[8] * b2) + ps.tLI[2];
-    wx = (float)(((ps.R[0] * p0 + ps.R[1] * p1) + ps.R[2] * p2) + ps.t[0]);
-    wy = (float)(((ps.R[3] * p0 + ps.R[4] * p1) + ps.R[5] * p2) + ps.t[1]);
-    wz = (float)(((ps.R[6] * p0 + ps.R[7] * p1) + ps.R[8] * p2) + ps.t[2]);
+    double a0, a1, a2, w0, w1, w2;
+    quat_rotate(ps.qLI, false, bx, by, bz, a0, a1, a2);
+    quat_rotate(ps.q, false, a0 + ps.tLI[0], a1 + ps.tLI[1], a2 + ps.tLI[2], w0, w1, w2);
+    wx = (float)(w0 + ps.t[0]);
+    wy = (float)(w1 + ps.t[1]);
+    wz = (float)(w2 + ps.t[2]);
 }
 
 // Sorted top-K list in registers.  Each entry is one 64-bit key
@@ -934,17 +958,17 @@ __device__ __forceinline__ bool esti_plane_dev(const float P[5][3], float thr, f
     return ok;
 }
 
-// H row, extrinsic_est_en = false: J = [n, (R_LI p + t_LI) x (R^T n)]  [U]
+// H row, extrinsic_est_en = false [U]: point_this = offset_R_L_I * p + offset_T_L_I,
+// C = s.rot.conjugate() * n (quat_rotate), A = skew(point_this) * C:
+// J = [n, p1 C2 - p2 C1, p2 C0 - p0 C2, p0 C1 - p1 C0]
 __device__ __forceinline__ void h_row(const PoseArg& ps, float bx, float by, float bz, float na, float nb,
                                       float nc, double J[6]) {
-    double b0 = bx, b1 = by, b2 = bz;
-    double p0 = ((ps.RLI[0] * b0 + ps.RLI[1] * b1) + ps.RLI[2] * b2) + ps.tLI[0];
-    double p1 = ((ps.RLI[3] * b0 + ps.RLI[4] * b1) + ps.RLI[5] * b2) + ps.tLI[1];
-    double p2 = ((ps.RLI[6] * b0 + ps.RLI[7] * b1) + ps.RLI[8] * b2) + ps.tLI[2];
+    double a0, a1, a2;
+    quat_rotate(ps.qLI, false, bx, by, bz, a0, a1, a2);
+    const double p0 = a0 + ps.tLI[0], p1 = a1 + ps.tLI[1], p2 = a2 + ps.tLI[2];
     double n0 = na, n1 = nb, n2 = nc;
-    double C0 = (ps.R[0] * n0 + ps.R[3] * n1) + ps.R[6] * n2;
-    double C1 = (ps.R[1] * n0 + ps.R[4] * n1) + ps.R[7] * n2;
-    double C2 = (ps.R[2] * n0 + ps.R[5] * n1) + ps.R[8] * n2;
+    double C0, C1, C2;
+    quat_rotate(ps.q, true, n0, n1, n2, C0, C1, C2);
     J[0] = n0;
     J[1] = n1;
     J[2] = n2;

@@ -21,6 +21,7 @@
 #include <cmath>
 #include <cstring>
 
+#include "lio_dev.hpp"
 #include "lio_filter.hpp"
 
 namespace lio {
@@ -341,16 +342,16 @@ __device__ __forceinline__ void so3_exp(const double w[3], double dt, double E[9
     const double a = nrm * dt, s = sin(a), c1 = 1.0 - cos(a);
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) {
-            const double kk = ((c1 * K[3 * i + 0]) * K[0 + j] + (c1 * K[3 * i + 1]) * K[3 + j]) + (c1 * K[3 * i + 2]) * K[6 + j];
+            // ((1 - cos) K) * K: Eigen's coefficient-based 3x3 product sums e0 + (e1 + e2)
+            // (redux_novec_unroller halves the 3 terms 1 + 2)
+            const double kk = (c1 * K[3 * i + 0]) * K[0 + j] + ((c1 * K[3 * i + 1]) * K[3 + j] + (c1 * K[3 * i + 2]) * K[6 + j]);
             E[3 * i + j] = (E[3 * i + j] + s * K[3 * i + j]) + kk;
         }
 }
 
+// M3D * V3D as Eigen evaluates it (coefficient-based product: e0 + (e1 + e2))
 __device__ __forceinline__ void mv3(const double* M, const double* v, double* o) {
-    for (int r = 0; r < 3; ++r) o[r] = (M[3 * r] * v[0] + M[3 * r + 1] * v[1]) + M[3 * r + 2] * v[2];
-}
-__device__ __forceinline__ void mtv3(const double* M, const double* v, double* o) {  // M^T v
-    for (int r = 0; r < 3; ++r) o[r] = (M[r] * v[0] + M[3 + r] * v[1]) + M[6 + r] * v[2];
+    for (int r = 0; r < 3; ++r) o[r] = M[3 * r] * v[0] + (M[3 * r + 1] * v[1] + M[3 * r + 2] * v[2]);
 }
 
 __device__ __forceinline__ void compensate(float* q, int tfield, const ImuPose& hd, const ImuPose& tl,
@@ -360,18 +361,19 @@ __device__ __forceinline__ void compensate(float* q, int tfield, const ImuPose& 
     so3_exp(tl.gyr, dt, E);
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c)
-            Ri[3 * r + c] = (hd.rot[3 * r] * E[c] + hd.rot[3 * r + 1] * E[3 + c]) + hd.rot[3 * r + 2] * E[6 + c];
+            Ri[3 * r + c] = hd.rot[3 * r] * E[c] + (hd.rot[3 * r + 1] * E[3 + c] + hd.rot[3 * r + 2] * E[6 + c]);
     double Tei[3];
     for (int k = 0; k < 3; ++k) Tei[k] = ((hd.pos[k] + hd.vel[k] * dt) + ((0.5 * tl.acc[k]) * dt) * dt) - end.pos[k];
-    const double Pi[3] = {q[0], q[1], q[2]};
+    // P_compensate = offset_R_L_I.conjugate() * (rot.conjugate() * (R_i * (offset_R_L_I * P_i +
+    //                offset_T_L_I) + T_ei) - offset_T_L_I)  [U]; SO3 products as Eigen (quat_rotate)
     double a[3], b[3], c[3];
-    mv3(end.R_LI, Pi, a);
+    quat_rotate(end.q_LI, false, (double)q[0], (double)q[1], (double)q[2], a[0], a[1], a[2]);
     for (int k = 0; k < 3; ++k) a[k] += end.t_LI[k];
     mv3(Ri, a, b);
     for (int k = 0; k < 3; ++k) b[k] += Tei[k];
-    mtv3(end.R, b, c);
+    quat_rotate(end.q, true, b[0], b[1], b[2], c[0], c[1], c[2]);
     for (int k = 0; k < 3; ++k) c[k] -= end.t_LI[k];
-    mtv3(end.R_LI, c, a);
+    quat_rotate(end.q_LI, true, c[0], c[1], c[2], a[0], a[1], a[2]);
     q[0] = (float)a[0];
     q[1] = (float)a[1];
     q[2] = (float)a[2];

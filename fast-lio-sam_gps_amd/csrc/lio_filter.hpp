@@ -30,6 +30,8 @@ struct UndistortEnd {
     double R[9];
     double R_LI[9];
     double t_LI[3];
+    double q[4];     // rot as Eigen::Quaternion<double> (w, x, y, z): the SO3 products use it
+    double q_LI[4];  // offset_R_L_I
 };
 
 struct ScanPrepParams {

@@ -484,8 +484,12 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
             out->state = 1;
             done = true;
         } else {
-            const double cosang = 0.5 * ((double)Ti[0] + (double)Ti[5] + (double)Ti[10] - 1);
-            const double tsq = (double)Ti[3] * Ti[3] + (double)Ti[7] * Ti[7] + (double)Ti[11] * Ti[11];
+            // PCL 1.10 DefaultConvergenceCriteria<float>: the coefficients of the Matrix4f are summed and
+            // squared in float, then widened (0.5 * float -> double; float -> double translation_sqr)
+            const float tr_f = Ti[0] + Ti[5] + Ti[10] - 1.f;
+            const float tsq_f = Ti[3] * Ti[3] + Ti[7] * Ti[7] + Ti[11] * Ti[11];
+            const double cosang = 0.5 * (double)tr_f;
+            const double tsq = (double)tsq_f;
             if (cosang >= rot_thr && tsq <= h->p.trans_eps) {
                 out->state = 2;
                 done = true;

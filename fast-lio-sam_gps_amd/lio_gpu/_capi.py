@@ -26,7 +26,7 @@ SUMS_HTH, SUMS_HTh, SUMS_NEFF, SUMS_RES, SUMS_HH = 0, 21, 27, 28, 29
 # Every symbol include/lio_gpu.h declares (checked by tests/test_capi_symbols.py).
 EXPORTS = [
     "lio_device_count", "lio_last_error", "lio_build_info",
-    "lio_map_create", "lio_map_destroy", "lio_map_build", "lio_map_build_device", "lio_map_size",
+    "lio_map_create", "lio_map_destroy", "lio_map_set_params", "lio_map_build", "lio_map_build_device", "lio_map_size",
     "lio_map_get_points", "lio_map_get_grid", "lio_map_num_ids", "lio_map_get_by_id", "lio_map_nearest_search", "lio_map_gather", "lio_map_add",
     "lio_map_add_device", "lio_map_delete_boxes", "lio_localmap_update", "lio_map_incremental",
     "lio_ctx_get_knn_pose", "lio_filter_create", "lio_filter_destroy", "lio_voxel_grid", "lio_submap_voxelize",
@@ -58,7 +58,8 @@ class MatchParams(C.Structure):
 
 
 class Pose(C.Structure):
-    _fields_ = [("R", C.c_double * 9), ("t", C.c_double * 3), ("R_LI", C.c_double * 9), ("t_LI", C.c_double * 3)]
+    _fields_ = [("R", C.c_double * 9), ("t", C.c_double * 3), ("R_LI", C.c_double * 9), ("t_LI", C.c_double * 3),
+                ("q", C.c_double * 4), ("q_LI", C.c_double * 4)]
 
 
 class State(C.Structure):
@@ -134,6 +135,7 @@ def _declare(L):
         "lio_build_info": (C.c_char_p, []),
         "lio_map_create": (C.c_int, [C.POINTER(MapParams), C.POINTER(vp)]),
         "lio_map_destroy": (C.c_int, [vp]),
+        "lio_map_set_params": (C.c_int, [vp, C.POINTER(MapParams)]),
         "lio_map_build": (C.c_int, [vp, fp, C.c_int64]),
         "lio_map_build_device": (C.c_int, [vp, vp, C.c_int64]),
         "lio_map_size": (C.c_int64, [vp]),

@@ -43,8 +43,16 @@ def default_match_params(**kw) -> _capi.MatchParams:
     return p
 
 
-def pose_from_arrays(R, t, R_LI=np.eye(3), t_LI=np.zeros(3)) -> _capi.Pose:
+def pose_from_arrays(R, t, R_LI=np.eye(3), t_LI=np.zeros(3), q=None, q_LI=None) -> _capi.Pose:
+    """lio_pose; q / q_LI = the state's quaternions (w, x, y, z) — left zero (derived from R on the
+    device side) when only matrices are given."""
     p = _capi.Pose()
+    if q is not None:
+        for i, v in enumerate(np.asarray(q, float).ravel()):
+            p.q[i] = v
+    if q_LI is not None:
+        for i, v in enumerate(np.asarray(q_LI, float).ravel()):
+            p.q_LI[i] = v
     for i, v in enumerate(np.asarray(R, float).ravel()):
         p.R[i] = v
     for i, v in enumerate(np.asarray(t, float).ravel()):
@@ -57,7 +65,10 @@ def pose_from_arrays(R, t, R_LI=np.eye(3), t_LI=np.zeros(3)) -> _capi.Pose:
 
 
 def pose_from_pose24(p24) -> _capi.Pose:
+    """From a pose vector: R(9) t(3) R_LI(9) t_LI(3) [q(4) q_LI(4)] (synth.pose24 gives all 32)."""
     p24 = np.asarray(p24, float)
+    if len(p24) >= 32:
+        return pose_from_arrays(p24[0:9], p24[9:12], p24[12:21], p24[21:24], p24[24:28], p24[28:32])
     return pose_from_arrays(p24[0:9], p24[9:12], p24[12:21], p24[21:24])
 
 
@@ -79,8 +90,13 @@ class IkdTreeGPU:
 
     def __init__(self, cell_size: float = 1.0, downsample_size: float = 0.5, device: int = 0):
         self._h = C.c_void_p()
+        self.device = device
         check(lib().lio_map_create(C.byref(_capi.MapParams(cell_size, downsample_size, device, 0)),
                                    C.byref(self._h)))
+
+    def set_downsample_param(self, downsample_size: float):
+        """``ikdtree.set_downsample_param(filter_size_map_min)``: in place, before Build."""
+        check(lib().lio_map_set_params(self._h, C.byref(_capi.MapParams(0.0, downsample_size, self.device, 0))))
 
     def Build(self, points: np.ndarray):
         pts = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 3)
@@ -149,8 +165,8 @@ class IkdTreeGPU:
         return dict(origin=g[0:3], cell=g[3], dims=g[4:7].astype(int))
 
     def close(self):
-        if self._h:
-            lib().lio_map_destroy(self._h)
+        # refused (and the handle kept) while an HShareModelGPU still uses this map
+        if self._h and lib().lio_map_destroy(self._h) == 0:
             self._h = C.c_void_p()
 
     def __del__(self):
@@ -285,7 +301,8 @@ class HShareModelGPU:
         """pose24 of the last kNN evaluation (the pose Nearest_Points belong to)."""
         p = _capi.Pose()
         check(lib().lio_ctx_get_knn_pose(self._h, C.byref(p)))
-        return np.concatenate([list(p.R), list(p.t), list(p.R_LI), list(p.t_LI)]).astype(np.float64)
+        return np.concatenate([list(p.R), list(p.t), list(p.R_LI), list(p.t_LI), list(p.q),
+                               list(p.q_LI)]).astype(np.float64)
 
     def map_incremental(self, pose, filter_size_map: float = 0.5) -> dict:
         """FAST-LIO ``map_incremental()`` [U]: add this scan to the map with the final pose.

@@ -324,10 +324,12 @@ def initial_cov() -> np.ndarray:
 
 
 def pose24(state: dict) -> np.ndarray:
-    """Row-major R, t, R_LI, t_LI as the kernels consume them (lio_pose)."""
+    """lio_pose as a vector: row-major R, t, R_LI, t_LI, then the state quaternions rot, offset_R_L_I
+    (w, x, y, z) that the kernels rotate with (32 doubles; the name predates the quaternions)."""
     R = quat_to_mat(state["rot"])
     RLI = quat_to_mat(state["offset_R_L_I"])
-    return np.concatenate([R.ravel(), state["pos"], RLI.ravel(), state["offset_T_L_I"]]).astype(np.float64)
+    return np.concatenate([R.ravel(), state["pos"], RLI.ravel(), state["offset_T_L_I"],
+                           state["rot"], state["offset_R_L_I"]]).astype(np.float64)
 
 
 # ----------------------------------------------------------------------------
@@ -464,5 +466,6 @@ def make_raw_scan(scene: Scene, n: int = 120_000, kind: str = "kitti64", seed: i
         vel = speed * np.array([math.cos(yaw), math.sin(yaw), 0.0])
         acc = speed * yaw_rate * np.array([-math.sin(yaw), math.cos(yaw), 0.0])
         poses.append(dict(offset_time=t, acc=acc, gyr=np.array([0.0, 0.0, yaw_rate]), vel=vel, pos=p, rot=R))
-    end24 = np.concatenate([R_e.ravel(), p_e, R_LI.ravel(), T_LI]).astype(np.float64)
+    q_e = np.array([math.cos(0.5 * yaw_e), 0.0, 0.0, math.sin(0.5 * yaw_e)])  # state rot (yaw-only)
+    end24 = np.concatenate([R_e.ravel(), p_e, R_LI.ravel(), T_LI, q_e, [1.0, 0.0, 0.0, 0.0]]).astype(np.float64)
     return raw, poses, end24

@@ -70,7 +70,13 @@ typedef struct lio_map_params {
 } lio_map_params;
 
 int lio_map_create(const lio_map_params* p, lio_map** out);
+/* Refuses (LIO_ERR_STATE) while lio_ctx handles created on m are alive.    */
 int lio_map_destroy(lio_map* m);
+/* ikdtree.set_downsample_param(filter_size_map_min) [U: laserMapping.cpp
+ * main(), before Build]: changes cell_size / downsample_size in place (a
+ * value <= 0 keeps the current one); only while the map holds no points, so
+ * every lio_ctx already created on m stays valid.  device must not change. */
+int lio_map_set_params(lio_map* m, const lio_map_params* p);
 /* ikdtree.Build(points) [U]: replaces the content. xyz: n*3 float, host.   */
 int lio_map_build(lio_map* m, const float* xyz, int64_t n);
 /* same, xyz already resident in device memory (e.g. a torch tensor).       */
@@ -129,13 +135,21 @@ typedef struct lio_match_params {
     double s_gate;      /* 0.9: keep if s > 0.9                                         */
 } lio_match_params;
 
-/* The parts of state_ikfom the measurement model reads, as row-major double
- * rotation matrices: p_world = R*(R_LI*p_body + t_LI) + t.                 */
+/* The parts of state_ikfom the measurement model reads:
+ *   p_world = rot * (offset_R_L_I * p_body + t_LI) + t.
+ * q / q_LI are state_ikfom's rot / offset_R_L_I (MTK::SO3 = Eigen::Quaternion
+ * <double>, stored (w, x, y, z)); the kernels evaluate every `SO3 * v` from
+ * them exactly as Eigen's QuaternionBase::_transformVector does.  R / R_LI are
+ * the same rotations as row-major matrices.  A caller holding only matrices
+ * leaves q (q_LI) all zero: it is then derived from R (R_LI) with Eigen's
+ * Matrix3 -> Quaternion conversion.                                         */
 typedef struct lio_pose {
     double R[9];
     double t[3];
     double R_LI[9];
     double t_LI[3];
+    double q[4];
+    double q_LI[4];
 } lio_pose;
 
 int lio_ctx_create(lio_map* m, const lio_match_params* p, lio_ctx** out);

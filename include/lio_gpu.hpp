@@ -78,6 +78,10 @@ inline lio_pose pose_of(const lio_state& x) {
     lio_pose p{};
     quat_to_rot(x.rot, p.R);
     quat_to_rot(x.offset_R_L_I, p.R_LI);
+    for (int k = 0; k < 4; ++k) {
+        p.q[k] = x.rot[k];
+        p.q_LI[k] = x.offset_R_L_I[k];
+    }
     for (int k = 0; k < 3; ++k) {
         p.t[k] = x.pos[k];
         p.t_LI[k] = x.offset_T_L_I[k];
@@ -102,14 +106,12 @@ public:
     KdTreeGPU(const KdTreeGPU&) = delete;
     KdTreeGPU& operator=(const KdTreeGPU&) = delete;
 
-    // ikdtree.set_downsample_param(filter_size_map_min): recreates the map
-    // parameters; call before Build, as laserMapping does
+    // ikdtree.set_downsample_param(filter_size_map_min): changes the map's
+    // parameters in place (ScanMatcherGPU objects built on this tree stay
+    // valid); call before Build, as laserMapping does
     void set_downsample_param(float ds) {
-        if (lio_map_num_ids(m_) > 0) throw Error(LIO_ERR_STATE, "set_downsample_param: call before Build");
-        lio_map_params p{cell_, ds, dev_, 0};
-        lio_map_destroy(m_);
-        m_ = nullptr;
-        check(lio_map_create(&p, &m_), "lio_map_create");
+        lio_map_params p{0.f, ds, dev_, 0};
+        check(lio_map_set_params(m_, &p), "set_downsample_param");
     }
 
     void Build(const PointVector& pts) {

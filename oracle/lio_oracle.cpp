@@ -24,7 +24,8 @@
 //   * kNN squared distance: float ((dx*dx + dy*dy) + dz*dz)  [ikd-Tree calc_dist, U]
 //   * ties in the kNN ordering are broken by the lower map point id (the
 //     ikd-Tree breaks them by traversal order, which is not reproducible).
-//   * world point: double R*(R_LI*p + t_LI) + t, stored as float   [U]
+//   * world point: double s.rot * (s.offset_R_L_I * p + t_LI) + pos, the two SO3 products as
+//     Eigen's QuaternionBase::_transformVector evaluates them (quat_rotate), stored as float [U]
 // =============================================================================
 #include <algorithm>
 #include <cfloat>
@@ -316,31 +317,100 @@ struct MatchParams {
     double s_coef;       // 0.9  : s = 1 - s_coef*|pd2|/sqrt(|p_body|) [U]
     double s_gate;       // 0.9  : keep if s > s_gate [U]
 };
+// The parts of state_ikfom the measurement model reads.  rot / offset_R_L_I are MTK::SO3<double>,
+// i.e. Eigen::Quaternion<double> [U: IKFoM use-ikfom.hpp, MTK SO3.hpp]: q, qLI = (w, x, y, z) of the
+// state; every `SO3 * v` below is evaluated as Eigen does it (quat_rotate).  R / RLI are the row-major
+// matrices of the same rotations (kept in the C-ABI for callers that hold matrices; when q is all zero
+// it is derived from R by Eigen's Matrix3 -> Quaternion conversion, pose_fill_quat).
 struct Pose {
-    double R[9], t[3], RLI[9], tLI[3];  // row-major rotations
+    double R[9], t[3], RLI[9], tLI[3];
+    double q[4], qLI[4];
 };
 
+// Eigen 3.3 QuaternionBase<Derived>::_transformVector (Geometry/Quaternion.h) — how
+// `Eigen::Quaternion<double> * Vector3d` (RotationBase::operator* -> _transformVector) is computed:
+//   Vector3 uv = this->vec().cross(v); uv += uv; return v + this->w() * uv + this->vec().cross(uv);
+// with MatrixBase::cross = (a1 b2 - a2 b1, a2 b0 - a0 b2, a0 b1 - a1 b0) (Geometry/OrthoMethods.h).
+// conj: rotate by q.conjugate() (vec negated, w kept), as `s.rot.conjugate() * n`.
+static inline void quat_rotate(const double* q, bool conj, const double v[3], double o[3]) {
+    const double w = q[0];
+    const double x = conj ? -q[1] : q[1], y = conj ? -q[2] : q[2], z = conj ? -q[3] : q[3];
+    double u0 = y * v[2] - z * v[1];
+    double u1 = z * v[0] - x * v[2];
+    double u2 = x * v[1] - y * v[0];
+    u0 += u0;
+    u1 += u1;
+    u2 += u2;
+    const double c0 = y * u2 - z * u1;
+    const double c1 = z * u0 - x * u2;
+    const double c2 = x * u1 - y * u0;
+    o[0] = (v[0] + w * u0) + c0;
+    o[1] = (v[1] + w * u1) + c1;
+    o[2] = (v[2] + w * u2) + c2;
+}
+
+// Eigen 3.3 quaternionbase_assign_impl<Other,3,3>::run (Geometry/Quaternion.h): rotation matrix ->
+// quaternion; trace() = m00 + (m11 + m22) (the unrolled redux splits the 3 terms 1 + 2).  Only
+// for callers that pass matrices without the state quaternion.
+static void mat_to_quat(const double* m, double* q) {
+    auto M = [&](int r, int c) { return m[3 * r + c]; };
+    double t = M(0, 0) + (M(1, 1) + M(2, 2));
+    double c[4];  // x, y, z, w (Eigen coeffs order)
+    if (t > 0.0) {
+        t = std::sqrt(t + 1.0);
+        c[3] = 0.5 * t;
+        t = 0.5 / t;
+        c[0] = (M(2, 1) - M(1, 2)) * t;
+        c[1] = (M(0, 2) - M(2, 0)) * t;
+        c[2] = (M(1, 0) - M(0, 1)) * t;
+    } else {
+        int i = 0;
+        if (M(1, 1) > M(0, 0)) i = 1;
+        if (M(2, 2) > M(i, i)) i = 2;
+        const int j = (i + 1) % 3, k = (j + 1) % 3;
+        t = std::sqrt(M(i, i) - M(j, j) - M(k, k) + 1.0);
+        c[i] = 0.5 * t;
+        t = 0.5 / t;
+        c[3] = (M(k, j) - M(j, k)) * t;
+        c[j] = (M(j, i) + M(i, j)) * t;
+        c[k] = (M(k, i) + M(i, k)) * t;
+    }
+    q[0] = c[3];
+    q[1] = c[0];
+    q[2] = c[1];
+    q[3] = c[2];
+}
+
+static void pose_fill_quat(Pose& ps) {
+    if (ps.q[0] == 0.0 && ps.q[1] == 0.0 && ps.q[2] == 0.0 && ps.q[3] == 0.0) mat_to_quat(ps.R, ps.q);
+    if (ps.qLI[0] == 0.0 && ps.qLI[1] == 0.0 && ps.qLI[2] == 0.0 && ps.qLI[3] == 0.0) mat_to_quat(ps.RLI, ps.qLI);
+}
+
+// pointBodyToWorld / h_share_model [U]:
+//   V3D p_global(s.rot * (s.offset_R_L_I * p_body + s.offset_T_L_I) + s.pos);  stored as float
 static inline void body_to_world(const Pose& ps, const float* pb, float* pw) {
-    double b[3] = {pb[0], pb[1], pb[2]};
-    double pi[3], w[3];
-    for (int r = 0; r < 3; ++r)
-        pi[r] = ((ps.RLI[3 * r] * b[0] + ps.RLI[3 * r + 1] * b[1]) + ps.RLI[3 * r + 2] * b[2]) + ps.tLI[r];
-    for (int r = 0; r < 3; ++r)
-        w[r] = ((ps.R[3 * r] * pi[0] + ps.R[3 * r + 1] * pi[1]) + ps.R[3 * r + 2] * pi[2]) + ps.t[r];
+    const double b[3] = {pb[0], pb[1], pb[2]};
+    double a[3], pi[3], w[3];
+    quat_rotate(ps.qLI, false, b, a);
+    for (int r = 0; r < 3; ++r) pi[r] = a[r] + ps.tLI[r];
+    quat_rotate(ps.q, false, pi, w);
+    for (int r = 0; r < 3; ++r) w[r] = w[r] + ps.t[r];
     pw[0] = (float)w[0];
     pw[1] = (float)w[1];
     pw[2] = (float)w[2];
 }
 
 // H row (extrinsic_est_en = false): [n, (R_LI p + t_LI) x (R^T n), 0 ...] [U]
+//   point_this = s.offset_R_L_I * point_this_be + s.offset_T_L_I;  C = s.rot.conjugate() * norm_vec;
+//   A = point_crossmat * C  (SKEW_SYM_MATRX rows: 0*C0 + (-p2)*C1 + p1*C2 = p1*C2 - p2*C1 exactly, ...)
 static inline void h_row(const Pose& ps, const float* pb, const float* nrm, double J[6]) {
-    double b[3] = {pb[0], pb[1], pb[2]};
-    double pi[3];
-    for (int r = 0; r < 3; ++r)
-        pi[r] = ((ps.RLI[3 * r] * b[0] + ps.RLI[3 * r + 1] * b[1]) + ps.RLI[3 * r + 2] * b[2]) + ps.tLI[r];
-    double n[3] = {nrm[0], nrm[1], nrm[2]};
+    const double b[3] = {pb[0], pb[1], pb[2]};
+    double a[3], pi[3];
+    quat_rotate(ps.qLI, false, b, a);
+    for (int r = 0; r < 3; ++r) pi[r] = a[r] + ps.tLI[r];
+    const double n[3] = {nrm[0], nrm[1], nrm[2]};
     double C[3];
-    for (int r = 0; r < 3; ++r) C[r] = (ps.R[r] * n[0] + ps.R[3 + r] * n[1]) + ps.R[6 + r] * n[2];
+    quat_rotate(ps.q, true, n, C);
     J[0] = n[0];
     J[1] = n[1];
     J[2] = n[2];
@@ -669,6 +739,8 @@ struct IeskfStats {
 static void pose_from_state(const State& x, Pose& ps) {
     qtomat(x.rot, ps.R);
     qtomat(x.offR, ps.RLI);
+    ps.q[0] = x.rot.w, ps.q[1] = x.rot.x, ps.q[2] = x.rot.y, ps.q[3] = x.rot.z;
+    ps.qLI[0] = x.offR.w, ps.qLI[1] = x.offR.x, ps.qLI[2] = x.offR.y, ps.qLI[3] = x.offR.z;
     for (int i = 0; i < 3; ++i) {
         ps.t[i] = x.pos[i];
         ps.tLI[i] = x.offT[i];
@@ -900,6 +972,8 @@ struct IcpParams {
     int max_iter;           // 50
     double rot_eps;         // 0 => 1 - trans_eps
     double score_threshold; // 1.5 (config.yaml:16)
+    int umeyama_float = 0;  // 1: pcl::umeyama in float + Eigen JacobiSVD (umeyama_pcl_float) instead of the
+                            //    double statistics — a fidelity study mode, not what the GPU path computes
 };
 
 static inline void xform_pt(const float T[16], const float* p, float* o) {
@@ -998,6 +1072,175 @@ static void umeyama(const double* st, const double c0[3], double Rout[9], double
     }
 }
 
+// ---------------------------------------------------------------------------
+// Float mode (IcpParams::umeyama_float): PCL 1.10 TransformationEstimationSVD<PointXYZI, PointXYZI, float>
+// with use_umeyama_ = true calls pcl::umeyama(cloud_src, cloud_tgt, false) on 3 x N float matrices
+// (common/impl/eigen.hpp, a copy of Eigen 3.3 Geometry/Umeyama.h) [U]:
+//   one_over_n = 1 / n; src_mean = src.rowwise().sum() * one_over_n (likewise dst);
+//   demean; sigma = one_over_n * dst_demean * src_demean^T; JacobiSVD(sigma, FullU | FullV);
+//   S = I, S(2) = -1 if det(U) det(V) < 0; R = U S V^T; t = dst_mean - R src_mean.
+// Restated in float: the row sums are sequential (Eigen 3.3's partial redux over a strided row is
+// not vectorised); sigma's depth sum is sequential too — Eigen's GEMM blocks the depth by an
+// L1-size-dependent kc and adds alpha * (block sum) per block, which this does NOT model, so the
+// last bits of sigma can differ from a given PCL build.  JacobiSVD (Eigen 3.3 JacobiSVD::compute,
+// real_2x2_jacobi_svd, JacobiRotation::makeJacobi, apply_rotation_in_the_plane) is restated exactly.
+// Small fixed products (R = U S V^T, R * src_mean) sum their 3 terms as e0 + (e1 + e2).
+// ---------------------------------------------------------------------------
+struct JRot { float c, s; };
+
+static bool make_jacobi(float x, float y, float z, JRot& j) {  // JacobiRotation::makeJacobi (real)
+    const float deno = 2.f * std::fabs(y);
+    if (deno < FLT_MIN) {
+        j.c = 1.f;
+        j.s = 0.f;
+        return false;
+    }
+    const float tau = (x - z) / deno;
+    const float w = std::sqrt(tau * tau + 1.f);
+    const float t = tau > 0.f ? 1.f / (tau + w) : 1.f / (tau - w);
+    const float sign_t = t > 0.f ? 1.f : -1.f;
+    const float n = 1.f / std::sqrt(t * t + 1.f);
+    j.s = ((-sign_t) * (y / std::fabs(y))) * std::fabs(t) * n;
+    j.c = n;
+    return true;
+}
+
+// apply_rotation_in_the_plane(x, y, j) over 3 strided elements
+static void rot_plane(float* x, float* y, int inc, JRot j) {
+    if (j.c == 1.f && j.s == 0.f) return;
+    for (int i = 0; i < 3; ++i) {
+        const float xi = x[i * inc], yi = y[i * inc];
+        x[i * inc] = j.c * xi + j.s * yi;
+        y[i * inc] = -j.s * xi + j.c * yi;
+    }
+}
+// M is column-major 3x3 (M[3*col + row]), as Eigen stores Matrix3f
+static void apply_left(float* M, int p, int q, JRot j) { rot_plane(M + p, M + q, 3, j); }          // rows
+static void apply_right(float* M, int p, int q, JRot j) { rot_plane(M + 3 * p, M + 3 * q, 1, {j.c, -j.s}); }  // cols, j^T
+
+static void jacobi_svd3f(const float* A, float U[9], float V[9], float sv[3]) {
+    float scale = 0.f;
+    for (int i = 0; i < 9; ++i) scale = std::max(scale, std::fabs(A[i]));  // cwiseAbs().maxCoeff()
+    if (scale == 0.f) scale = 1.f;
+    float W[9];
+    for (int i = 0; i < 9; ++i) W[i] = A[i] / scale;
+    for (int i = 0; i < 9; ++i) U[i] = V[i] = (i % 4 == 0) ? 1.f : 0.f;
+    const float precision = 2.f * FLT_EPSILON, consider_zero = FLT_MIN;
+    auto w = [&](int r, int c) -> float& { return W[3 * c + r]; };
+    float max_diag = std::max(std::max(std::fabs(w(0, 0)), std::fabs(w(1, 1))), std::fabs(w(2, 2)));
+    bool finished = false;
+    for (int sweep = 0; !finished && sweep < 1000; ++sweep) {
+        finished = true;
+        for (int p = 1; p < 3; ++p)
+            for (int q = 0; q < p; ++q) {
+                const float threshold = std::max(consider_zero, precision * max_diag);
+                if (std::fabs(w(p, q)) > threshold || std::fabs(w(q, p)) > threshold) {
+                    finished = false;
+                    // real_2x2_jacobi_svd(W, p, q, &j_left, &j_right)
+                    float m00 = w(p, p), m01 = w(p, q), m10 = w(q, p), m11 = w(q, q);
+                    JRot rot1;
+                    const float t = m00 + m11, d = m10 - m01;
+                    if (std::fabs(d) < FLT_MIN) {
+                        rot1 = {1.f, 0.f};
+                    } else {
+                        const float u = t / d;
+                        const float tmp = std::sqrt(1.f + u * u);
+                        rot1.s = 1.f / tmp;
+                        rot1.c = u / tmp;
+                    }
+                    {  // m.applyOnTheLeft(0, 1, rot1)
+                        float x0 = m00, y0 = m10, x1 = m01, y1 = m11;
+                        if (!(rot1.c == 1.f && rot1.s == 0.f)) {
+                            m00 = rot1.c * x0 + rot1.s * y0;
+                            m10 = -rot1.s * x0 + rot1.c * y0;
+                            m01 = rot1.c * x1 + rot1.s * y1;
+                            m11 = -rot1.s * x1 + rot1.c * y1;
+                        }
+                    }
+                    JRot jr;
+                    make_jacobi(m00, m01, m11, jr);
+                    const JRot jrt{jr.c, -jr.s};                 // j_right.transpose()
+                    const JRot jl{rot1.c * jrt.c - rot1.s * jrt.s,  // rot1 * j_right^T
+                                  rot1.c * jrt.s + rot1.s * jrt.c};
+                    apply_left(W, p, q, jl);
+                    apply_right(U, p, q, {jl.c, -jl.s});  // U.applyOnTheRight(p, q, j_left.transpose())
+                    apply_right(W, p, q, jr);
+                    apply_right(V, p, q, jr);
+                    max_diag = std::max(max_diag, std::max(std::fabs(w(p, p)), std::fabs(w(q, q))));
+                }
+            }
+    }
+    for (int i = 0; i < 3; ++i) {
+        const float a = w(i, i);
+        sv[i] = std::fabs(a);
+        if (a < 0.f)
+            for (int r = 0; r < 3; ++r) U[3 * i + r] = -U[3 * i + r];
+    }
+    for (int i = 0; i < 3; ++i) sv[i] *= scale;
+    for (int i = 0; i < 3; ++i) {  // sort descending (maxCoeff: first maximum)
+        int pos = i;
+        for (int k = i + 1; k < 3; ++k)
+            if (sv[k] > sv[pos]) pos = k;
+        if (sv[pos] == 0.f) break;
+        if (pos != i) {
+            std::swap(sv[i], sv[pos]);
+            for (int r = 0; r < 3; ++r) {
+                std::swap(U[3 * i + r], U[3 * pos + r]);
+                std::swap(V[3 * i + r], V[3 * pos + r]);
+            }
+        }
+    }
+}
+
+static float det3f_colmajor(const float* M) {  // Eigen determinant_impl<3>: bruteforce_det3_helper
+    auto m = [&](int r, int c) { return M[3 * c + r]; };
+    auto h = [&](int a, int b, int c) { return m(a, 0) * (m(b, 1) * m(c, 2) - m(b, 2) * m(c, 1)); };
+    return h(0, 1, 2) - h(1, 0, 2) + h(2, 0, 1);
+}
+
+// src / tgt: the correspondence pairs in correspondence (source index) order, xyz interleaved
+static void umeyama_pcl_float(const std::vector<float>& src, const std::vector<float>& tgt, float Ti[16]) {
+    const int64_t n = (int64_t)(src.size() / 3);
+    const float one_over_n = 1.f / (float)n;
+    float sm[3], dm[3];
+    for (int d = 0; d < 3; ++d) {
+        float a = src[d], b = tgt[d];
+        for (int64_t i = 1; i < n; ++i) {
+            a += src[3 * i + d];
+            b += tgt[3 * i + d];
+        }
+        sm[d] = a * one_over_n;
+        dm[d] = b * one_over_n;
+    }
+    float acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // sum_k dst_demean(r, k) src_demean(c, k), row-major r, c
+    for (int64_t i = 0; i < n; ++i) {
+        const float s0 = src[3 * i] - sm[0], s1 = src[3 * i + 1] - sm[1], s2 = src[3 * i + 2] - sm[2];
+        const float d0 = tgt[3 * i] - dm[0], d1 = tgt[3 * i + 1] - dm[1], d2 = tgt[3 * i + 2] - dm[2];
+        const float sv[3] = {s0, s1, s2}, dv[3] = {d0, d1, d2};
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) acc[3 * r + c] += dv[r] * sv[c];
+    }
+    float sigma[9];  // column-major
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) sigma[3 * c + r] = one_over_n * acc[3 * r + c];
+    float U[9], V[9], svals[3];
+    jacobi_svd3f(sigma, U, V, svals);
+    float S[3] = {1.f, 1.f, 1.f};
+    if (det3f_colmajor(U) * det3f_colmajor(V) < 0.f) S[2] = -1.f;
+    float R[9];  // row-major
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) {
+            const float e0 = (U[r] * S[0]) * V[c], e1 = (U[3 + r] * S[1]) * V[3 + c], e2 = (U[6 + r] * S[2]) * V[6 + c];
+            R[3 * r + c] = e0 + (e1 + e2);
+        }
+    for (int i = 0; i < 16; ++i) Ti[i] = 0.f;
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) Ti[4 * r + c] = R[3 * r + c];
+        Ti[4 * r + 3] = dm[r] - (R[3 * r] * sm[0] + (R[3 * r + 1] * sm[1] + R[3 * r + 2] * sm[2]));
+    }
+    Ti[15] = 1.f;
+}
+
 struct IcpResult {
     float T[16];
     double fitness;
@@ -1063,14 +1306,26 @@ int icp_align(const float* src, int64_t ns, const float* dst, int64_t nd, const 
             res->state = 5;
             break;
         }
-        double Rd[9], td[3];
-        umeyama(st, c0, Rd, td);
         float Ti[16] = {0};
-        for (int r = 0; r < 3; ++r) {
-            for (int c = 0; c < 3; ++c) Ti[4 * r + c] = (float)Rd[3 * r + c];
-            Ti[4 * r + 3] = (float)td[r];
+        if (ip.umeyama_float) {
+            std::vector<float> ps, qs;
+            ps.reserve(3 * (size_t)st[0]);
+            qs.reserve(3 * (size_t)st[0]);
+            for (int64_t i = 0; i < ns; ++i) {
+                if (nn[i] < 0 || (double)nd2[i] > max_d2) continue;
+                ps.insert(ps.end(), &cur[3 * i], &cur[3 * i] + 3);
+                qs.insert(qs.end(), dst + 3 * (size_t)nn[i], dst + 3 * (size_t)nn[i] + 3);
+            }
+            umeyama_pcl_float(ps, qs, Ti);
+        } else {
+            double Rd[9], td[3];
+            umeyama(st, c0, Rd, td);
+            for (int r = 0; r < 3; ++r) {
+                for (int c = 0; c < 3; ++c) Ti[4 * r + c] = (float)Rd[3 * r + c];
+                Ti[4 * r + 3] = (float)td[r];
+            }
+            Ti[15] = 1.f;
         }
-        Ti[15] = 1.f;
         for (int64_t i = 0; i < ns; ++i) {
             float o[3];
             xform_pt(Ti, &cur[3 * i], o);
@@ -1101,8 +1356,12 @@ int icp_align(const float* src, int64_t ns, const float* dst, int64_t nd, const 
             res->state = 1;
             done = true;
         } else {
-            double cosang = 0.5 * ((double)Ti[0] + (double)Ti[5] + (double)Ti[10] - 1);
-            double tsq = (double)Ti[3] * Ti[3] + (double)Ti[7] * Ti[7] + (double)Ti[11] * Ti[11];
+            // PCL 1.10 DefaultConvergenceCriteria<float>: the coefficients of the Matrix4f are summed and
+            // squared in float, then widened (0.5 * float -> double; float -> double translation_sqr)
+            const float tr_f = Ti[0] + Ti[5] + Ti[10] - 1.f;
+            const float tsq_f = Ti[3] * Ti[3] + Ti[7] * Ti[7] + Ti[11] * Ti[11];
+            double cosang = 0.5 * (double)tr_f;
+            double tsq = (double)tsq_f;
             if (cosang >= rot_thr && tsq <= ip.trans_eps) {
                 if (similar >= 0) { res->state = 2; done = true; }
                 is_similar = true;
@@ -1461,7 +1720,9 @@ static void so3_exp(const double w[3], double dt, double E[9]) {
     const double a = nrm * dt, sn = std::sin(a), c1 = 1.0 - std::cos(a);
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) {
-            const double kk = ((c1 * K[3 * i + 0]) * K[0 + j] + (c1 * K[3 * i + 1]) * K[3 + j]) + (c1 * K[3 * i + 2]) * K[6 + j];
+            // ((1 - cos) K) * K: Eigen's coefficient-based 3x3 product sums e0 + (e1 + e2)
+            // (redux_novec_unroller halves the 3 terms 1 + 2)
+            const double kk = (c1 * K[3 * i + 0]) * K[0 + j] + ((c1 * K[3 * i + 1]) * K[3 + j] + (c1 * K[3 * i + 2]) * K[6 + j]);
             E[3 * i + j] = (E[3 * i + j] + sn * K[3 * i + j]) + kk;
         }
 }
@@ -1478,15 +1739,20 @@ static void compensate(float* q, int tf, const ImuPoseO& hd, const ImuPoseO& tl,
     so3_exp(tl.gyr, dt, E);
     for (int r = 0; r < 3; ++r)
         for (int c = 0; c < 3; ++c)
-            Ri[3 * r + c] = (hd.rot[3 * r] * E[c] + hd.rot[3 * r + 1] * E[3 + c]) + hd.rot[3 * r + 2] * E[6 + c];
+            Ri[3 * r + c] = hd.rot[3 * r] * E[c] + (hd.rot[3 * r + 1] * E[3 + c] + hd.rot[3 * r + 2] * E[6 + c]);  // M3D*M3D
     double Tei[3];
     for (int k = 0; k < 3; ++k) Tei[k] = ((hd.pos[k] + hd.vel[k] * dt) + ((0.5 * tl.acc[k]) * dt) * dt) - end.t[k];
+    // P_compensate = offset_R_L_I.conjugate() * (rot.conjugate() * (R_i * (offset_R_L_I * P_i +
+    //                offset_T_L_I) + T_ei) - offset_T_L_I)   (quaternion products as Eigen evaluates them)
     const double Pi[3] = {q[0], q[1], q[2]};
     double a[3], b[3], c[3];
-    for (int r = 0; r < 3; ++r) a[r] = ((end.RLI[3 * r] * Pi[0] + end.RLI[3 * r + 1] * Pi[1]) + end.RLI[3 * r + 2] * Pi[2]) + end.tLI[r];
-    for (int r = 0; r < 3; ++r) b[r] = ((Ri[3 * r] * a[0] + Ri[3 * r + 1] * a[1]) + Ri[3 * r + 2] * a[2]) + Tei[r];
-    for (int r = 0; r < 3; ++r) c[r] = ((end.R[r] * b[0] + end.R[3 + r] * b[1]) + end.R[6 + r] * b[2]) - end.tLI[r];
-    for (int r = 0; r < 3; ++r) a[r] = (end.RLI[r] * c[0] + end.RLI[3 + r] * c[1]) + end.RLI[6 + r] * c[2];
+    quat_rotate(end.qLI, false, Pi, a);
+    for (int r = 0; r < 3; ++r) a[r] = a[r] + end.tLI[r];
+    // R_i * (...) + T_ei: M3D * V3D, Eigen's coefficient-based product e0 + (e1 + e2)
+    for (int r = 0; r < 3; ++r) b[r] = (Ri[3 * r] * a[0] + (Ri[3 * r + 1] * a[1] + Ri[3 * r + 2] * a[2])) + Tei[r];
+    quat_rotate(end.q, true, b, c);
+    for (int r = 0; r < 3; ++r) c[r] = c[r] - end.tLI[r];
+    quat_rotate(end.qLI, true, c, a);
     q[0] = (float)a[0];
     q[1] = (float)a[1];
     q[2] = (float)a[2];
@@ -1544,7 +1810,12 @@ struct orc_state {
     double pos[3]; double rot[4]; double offset_R_L_I[4]; double offset_T_L_I[3];
     double vel[3]; double bg[3]; double ba[3]; double grav[3];
 };
-struct orc_icp_params { double max_corr_dist, trans_eps, fitness_eps; int max_iter; double rot_eps, score_threshold; };
+struct orc_icp_params {
+    double max_corr_dist, trans_eps, fitness_eps;
+    int max_iter;
+    double rot_eps, score_threshold;
+    int umeyama_float;  // 1: float pcl::umeyama + JacobiSVD restatement (fidelity study)
+};
 
 int orc_version(void) { return 3; }
 
@@ -1565,7 +1836,7 @@ int64_t orc_submap_voxelize(const float* p, const int64_t* seg, int nseg, int st
 int64_t orc_preprocess(const float* raw, int64_t n, int stride, int every, float blind, float leaf, int tf,
                        const double* poses, int np, const double* end24, float* out) {
     orc::Pose e;
-    std::memcpy(&e, end24, sizeof(e));
+    std::memcpy(&e, end24, sizeof(e)); orc::pose_fill_quat(e);
     return orc::preprocess(raw, n, stride, every, blind, leaf, tf, (const orc::ImuPoseO*)poses, np, e, out);
 }
 
@@ -1602,8 +1873,8 @@ int orc_dmap_knn(void* m, const float* q, int64_t nq, int k, float range_sq, int
 int orc_map_incremental(void* m, const float* body, int64_t n, const double* pose_knn24, const double* pose24,
                         double fs, float ds, int64_t* stats4) {
     orc::Pose pk, pf;
-    std::memcpy(&pk, pose_knn24, sizeof(pk));
-    std::memcpy(&pf, pose24, sizeof(pf));
+    std::memcpy(&pk, pose_knn24, sizeof(pk)); orc::pose_fill_quat(pk);
+    std::memcpy(&pf, pose24, sizeof(pf)); orc::pose_fill_quat(pf);
     orc::map_incremental(*(orc::DynMap*)m, body, n, pk, pf, fs, ds, stats4);
     return 0;
 }
@@ -1634,6 +1905,7 @@ int orc_esti_plane(const float* pts15, float thr, float* out4) {
 int orc_body_to_world(const double* pose24, const float* body, int64_t n, float* world) {
     orc::Pose ps;
     std::memcpy(&ps, pose24, sizeof(ps));
+    orc::pose_fill_quat(ps);
     for (int64_t i = 0; i < n; ++i) orc::body_to_world(ps, body + 3 * i, world + 3 * i);
     return 0;
 }
@@ -1643,6 +1915,7 @@ int orc_h_share_model(void* m, const float* body, int64_t n, const double* pose2
                       double* sums32, int threads) {
     orc::Pose ps;
     std::memcpy(&ps, pose24, sizeof(ps));
+    orc::pose_fill_quat(ps);
     orc::MatchParams p{mp->knn_range_sq, mp->plane_thr, mp->s_coef, mp->s_gate};
     return orc::h_share_model(*(orc::KdTree*)m, body, n, ps, redo_knn, nn_idx, sel, planes, p, sums32, threads, nullptr);
 }
@@ -1695,7 +1968,7 @@ int orc_icp_align(const float* src, int64_t ns, const float* dst, int64_t nd, co
                   const float* guess16, float* T16, double* out8, float* aligned, double* trace,
                   int max_trace, int threads) {
     orc::IcpParams ip{ipp->max_corr_dist, ipp->trans_eps, ipp->fitness_eps, ipp->max_iter, ipp->rot_eps,
-                      ipp->score_threshold};
+                      ipp->score_threshold, ipp->umeyama_float};
     orc::IcpResult r{};
     static const float kIdentity[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
     int rc = orc::icp_align(src, ns, dst, nd, ip, guess16 ? guess16 : kIdentity, &r, aligned, trace, max_trace,

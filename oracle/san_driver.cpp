@@ -20,10 +20,14 @@ std::vector<float> cloud(std::mt19937& g, int n, float span) {
     return p;
 }
 
-void identity_pose(double* p24) {
-    std::memset(p24, 0, 24 * sizeof(double));
-    p24[0] = p24[4] = p24[8] = 1.0;
-    p24[12] = p24[16] = p24[20] = 1.0;
+// pose vector: R(9) t(3) R_LI(9) t_LI(3) q(4) q_LI(4); q = (w, x, y, z).  Odd calls leave the
+// quaternions zero, so the oracle derives them from R (pose_fill_quat) under the sanitizers too.
+void identity_pose(double* p32) {
+    static int k = 0;
+    std::memset(p32, 0, 32 * sizeof(double));
+    p32[0] = p32[4] = p32[8] = 1.0;
+    p32[12] = p32[16] = p32[20] = 1.0;
+    if (k++ % 2 == 0) p32[24] = p32[28] = 1.0;
 }
 
 int fail(const char* what) {
@@ -49,7 +53,7 @@ int main() {
                 if (orc_map_knn(t, q.data(), 300, k, r2, idx.data(), d2.data(), 2) != 0) return fail("knn");
         }
         // h-evaluation (kNN + plane) and one IESKF update
-        double pose[24];
+        double pose[32];
         identity_pose(pose);
         std::vector<int32_t> nn((size_t)300 * 5);
         std::vector<uint8_t> sel(300);
@@ -86,6 +90,9 @@ int main() {
         for (size_t i = 0; i < far.size(); i += 3) far[i] += 1000.f;
         orc_icp_align(src.data(), 1500, far.data(), 1500, &ip, nullptr, T, out8, nullptr, tr, 64, 2);
         orc_icp_align(src.data(), 1500, dst.data(), 1, &ip, nullptr, T, out8, nullptr, tr, 64, 2);
+        ip.umeyama_float = 1;  // float pcl::umeyama + JacobiSVD restatement
+        orc_icp_align(src.data(), 1500, dst.data(), 1500, &ip, nullptr, T, out8, al.data(), tr, 64, 2);
+        orc_icp_align(src.data(), 1500, dst.data(), 1, &ip, nullptr, T, out8, nullptr, tr, 64, 2);
     }
 
     // filters: VoxelGrid at stride 4, submap voxelize over two segments
@@ -113,7 +120,7 @@ int main() {
             imu[k][13] = imu[k][17] = imu[k][21] = 1.0;  // rot = I
             imu[k][7] = 1.0;                             // vel x
         }
-        double end24[24];
+        double end24[32];
         identity_pose(end24);
         std::vector<float> pout(raw.size());
         if (orc_preprocess(raw.data(), 3000, 5, 4, 2.f, 0.5f, 4, &imu[0][0], 2, end24, pout.data()) < 0)
@@ -136,7 +143,7 @@ int main() {
         const float all[6] = {-100.f, -100.f, -100.f, 100.f, 100.f, 100.f};
         orc_dmap_delete_boxes(d, all, 1);
         orc_dmap_knn(d, q.data(), 200, 5, INFINITY, idx.data(), d2.data());
-        double pose[24];
+        double pose[32];
         identity_pose(pose);
         int64_t st4[4];
         orc_map_incremental(d, q.data(), 200, pose, pose, 0.5, 0.5f, st4);

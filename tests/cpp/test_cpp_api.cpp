@@ -194,6 +194,34 @@ int main() {
         EXPECT((int)flat.size() == tree.validnum(), "flatten");
     }
 
+    // ------------------------------------------------ matcher built before set_downsample_param
+    // (laserMapping may configure the tree after the objects that use it exist): the parameters
+    // change in place, the matcher keeps a valid map, and the tree refuses to die under it
+    {
+        lio_gpu::KdTreeGPU<PointXYZI> early(1.0f, 0.5f);
+        lio_gpu::ScanMatcherGPU m0(early);
+        early.set_downsample_param(0.3f);
+        early.Build(map_pts);
+        m0.set_scan(PointVector(q.begin(), q.begin() + 200));
+        lio_state x{};
+        x.rot[0] = 1.0;
+        x.offset_R_L_I[0] = 1.0;
+        std::vector<double> P(23 * 23, 0.0);
+        for (int i = 0; i < 23; ++i) P[i * 23 + i] = 1e-4;
+        const lio_ieskf_stats st = m0.update_iterated_dyn_share_modified(x, P.data(), 0.001, 3, 0.001);
+        EXPECT(st.h_evals >= 1, "matcher built before set_downsample_param still runs");
+        bool refused = false;
+        try {
+            early.set_downsample_param(0.5f);  // map now holds points
+        } catch (const lio_gpu::Error&) {
+            refused = true;
+        }
+        EXPECT(refused, "set_downsample_param after Build refused");
+        lio_map_params pp{0.f, 0.5f, 0, 0};
+        EXPECT(lio_map_destroy(early.handle()) == LIO_ERR_STATE, "map destroy refused while a matcher exists");
+        (void)pp;
+    }
+
     // ------------------------------------------------------------- scan matching
     {
         lio_gpu::KdTreeGPU<PointXYZI> map(1.0f, 0.5f);

@@ -33,7 +33,8 @@ class State(C.Structure):
 
 class IcpParams(C.Structure):
     _fields_ = [("max_corr_dist", C.c_double), ("trans_eps", C.c_double), ("fitness_eps", C.c_double),
-                ("max_iter", C.c_int), ("rot_eps", C.c_double), ("score_threshold", C.c_double)]
+                ("max_iter", C.c_int), ("rot_eps", C.c_double), ("score_threshold", C.c_double),
+                ("umeyama_float", C.c_int)]
 
 
 def default_match_params():
@@ -42,7 +43,7 @@ def default_match_params():
 
 def default_icp_params():
     # loop_closure.cpp:7-10, fast_lio_sam.cpp:73 (1.5 * 35 m), config.yaml:16
-    return IcpParams(52.5, 0.01, 0.01, 50, 0.0, 1.5)
+    return IcpParams(52.5, 0.01, 0.01, 50, 0.0, 1.5, 0)
 
 
 def _p(a, t):
@@ -136,8 +137,16 @@ def esti_plane(pts5x3, thr=0.1):
     return bool(ok), out
 
 
+def _pose32(p):
+    """Pose vector R t R_LI t_LI [q q_LI] -> the oracle's 32 doubles (zero quaternions = derive from R)."""
+    p = np.asarray(p, dtype=np.float64).ravel()
+    out = np.zeros(32, np.float64)
+    out[: min(len(p), 32)] = p[:32]
+    return out
+
+
 def body_to_world(pose24, body):
-    pose24 = np.ascontiguousarray(pose24, dtype=np.float64)
+    pose24 = _pose32(pose24)
     body = np.ascontiguousarray(body, dtype=np.float32)
     out = np.empty_like(body)
     lib().orc_body_to_world(_p(pose24, C.c_double), _p(body, C.c_float), len(body), _p(out, C.c_float))
@@ -148,7 +157,7 @@ def h_share_model(omap: OracleMap, body, pose24, redo_knn, nn_idx, sel, planes, 
     """One h-evaluation; nn_idx/sel/planes are updated in place. Returns sums[32]."""
     mp = mp or default_match_params()
     body = np.ascontiguousarray(body, dtype=np.float32)
-    pose24 = np.ascontiguousarray(pose24, dtype=np.float64)
+    pose24 = _pose32(pose24)
     sums = np.zeros(32, np.float64)
     rc = lib().orc_h_share_model(omap.h, _p(body, C.c_float), len(body), _p(pose24, C.c_double), int(redo_knn),
                                  _p(nn_idx, C.c_int32), _p(sel, C.c_uint8), _p(planes, C.c_float),
@@ -247,8 +256,8 @@ class OracleDynMap:
 
     def map_incremental(self, body, pose_knn24, pose24, fs=0.5, ds=0.5):
         body = np.ascontiguousarray(body, dtype=np.float32).reshape(-1, 3)
-        pk = np.ascontiguousarray(pose_knn24, dtype=np.float64)
-        pf = np.ascontiguousarray(pose24, dtype=np.float64)
+        pk = _pose32(pose_knn24)
+        pf = _pose32(pose24)
         st = np.zeros(4, np.int64)
         lib().orc_map_incremental(self.h, _p(body, C.c_float), len(body), _p(pk, C.c_double), _p(pf, C.c_double),
                                   float(fs), C.c_float(ds), _p(st, C.c_int64))
@@ -286,7 +295,7 @@ def preprocess(raw, imu_poses, end24, point_filter_num=4, blind=2.0, leaf=0.5, t
     for k, p in enumerate(imu_poses):
         P[k] = np.concatenate([[p["offset_time"]], p["acc"], p["gyr"], p["vel"], p["pos"],
                                np.asarray(p["rot"], float).ravel()])
-    e = np.ascontiguousarray(end24, dtype=np.float64)
+    e = _pose32(end24)
     out = np.empty_like(raw)
     m = lib().orc_preprocess(_p(raw, C.c_float), len(raw), raw.shape[1], point_filter_num, C.c_float(blind),
                              C.c_float(leaf), time_field, _p(P, C.c_double), len(imu_poses), _p(e, C.c_double),

@@ -179,3 +179,93 @@ def test_icp_not_enough_correspondences(oracle):
     dst = np.array([[100, 0, 0], [101, 0, 0], [100, 1, 0]], np.float32)
     res = oracle.icp_align(src, dst)
     assert not res["converged"] and res["state"] == 5 and res["iterations"] == 0
+
+
+# ---------------------------------------------------------------------------
+# SO3 * v as Eigen evaluates it (VERDICT r01 weak #2a): numpy transcription of
+# Eigen 3.3 QuaternionBase::_transformVector, element-wise in float64 with the
+# same operation order, compared bit for bit with the oracle's world points.
+def _np_cross(a, b):
+    return (a[1] * b[2] - a[2] * b[1], a[2] * b[0] - a[0] * b[2], a[0] * b[1] - a[1] * b[0])
+
+
+def _np_transform_vector(q, v):
+    """Eigen: uv = q.vec().cross(v); uv += uv; return v + q.w() * uv + q.vec().cross(uv)."""
+    w, qv = q[0], (q[1], q[2], q[3])
+    uv = _np_cross(qv, v)
+    uv = tuple(u + u for u in uv)
+    c = _np_cross(qv, uv)
+    return tuple((v[i] + w * uv[i]) + c[i] for i in range(3))
+
+
+def _np_mat_to_quat(m):
+    """Eigen 3.3 quaternionbase_assign_impl<Other,3,3>: trace = m00 + (m11 + m22)."""
+    t = m[0, 0] + (m[1, 1] + m[2, 2])
+    c = [0.0] * 4  # x y z w
+    if t > 0:
+        t = np.sqrt(t + 1.0)
+        c[3] = 0.5 * t
+        t = 0.5 / t
+        c[0] = (m[2, 1] - m[1, 2]) * t
+        c[1] = (m[0, 2] - m[2, 0]) * t
+        c[2] = (m[1, 0] - m[0, 1]) * t
+    else:
+        i = 0
+        if m[1, 1] > m[0, 0]:
+            i = 1
+        if m[2, 2] > m[i, i]:
+            i = 2
+        j, k = (i + 1) % 3, (i + 2) % 3
+        t = np.sqrt(m[i, i] - m[j, j] - m[k, k] + 1.0)
+        c[i] = 0.5 * t
+        t = 0.5 / t
+        c[3] = (m[k, j] - m[j, k]) * t
+        c[j] = (m[j, i] + m[i, j]) * t
+        c[k] = (m[k, i] + m[i, k]) * t
+    return np.array([c[3], c[0], c[1], c[2]])
+
+
+@pytest.mark.parametrize("from_matrix", [False, True])
+def test_world_points_follow_eigen_transform_vector(oracle, from_matrix):
+    """p_world = rot * (offset_R_L_I * p + t_LI) + pos (FAST-LIO pointBodyToWorld / h_share_model [U]),
+    both products through _transformVector, stored as float.  Non-unit quaternions included (the
+    state's quaternion is not renormalised between boxplus steps); with from_matrix the pose carries
+    only matrices and the quaternions come from Eigen's Matrix3 -> Quaternion conversion."""
+    rng = np.random.default_rng(42)
+    body = rng.uniform(-60, 60, (4000, 3)).astype(np.float32)
+    for trial in range(12):
+        q = synth.rotvec_to_quat(rng.normal(0, 1.2, 3)) * (1.0 + (trial % 3) * 1e-7)
+        qli = synth.rotvec_to_quat(rng.normal(0, 0.05, 3))
+        if trial == 0:
+            q = np.array([0.0, 0.0, 0.0, 1.0])  # trace < 0 branches of the matrix conversion
+        t = rng.uniform(-500, 500, 3)
+        tli = rng.normal(0, 0.5, 3)
+        R, RLI = synth.quat_to_mat(q), synth.quat_to_mat(qli)
+        if from_matrix:
+            p = np.concatenate([R.ravel(), t, RLI.ravel(), tli])  # no quaternions: derived from R
+            q, qli = _np_mat_to_quat(R), _np_mat_to_quat(RLI)
+        else:
+            p = np.concatenate([R.ravel(), t, RLI.ravel(), tli, q, qli])
+        w = oracle.body_to_world(p, body)
+        b = tuple(body[:, i].astype(np.float64) for i in range(3))
+        a = _np_transform_vector(qli, b)
+        a = tuple(a[i] + tli[i] for i in range(3))
+        g = _np_transform_vector(q, a)
+        ref = np.stack([g[i] + t[i] for i in range(3)], axis=1).astype(np.float32)
+        np.testing.assert_array_equal(w, ref)
+
+
+def test_icp_float_umeyama_mode_close_to_double(oracle):
+    """Fidelity study (VERDICT r01 weak #2b): the oracle's float restatement of pcl::umeyama (float
+    sums, Eigen JacobiSVD) against the double-statistics form the GPU path computes.  They agree to
+    PCL's own float noise (DESIGN.md §2 lists the measured gaps: ~2e-5 at 8k-30k points, ~2e-4 at
+    500k), and take the same iterations / convergence state."""
+    for n, seed in ((8000, 3), (30000, 5)):
+        src, dst, _ = synth.make_icp_pair(n_points=n, seed=seed)
+        rd = oracle.icp_align(src, dst)
+        p = oracle.default_icp_params()
+        p.umeyama_float = 1
+        rf = oracle.icp_align(src, dst, params=p)
+        assert rd["iterations"] == rf["iterations"] and rd["state"] == rf["state"]
+        np.testing.assert_allclose(rf["T"], rd["T"], atol=1e-4)
+        assert abs(rf["fitness"] - rd["fitness"]) <= 1e-4 * rd["fitness"]
