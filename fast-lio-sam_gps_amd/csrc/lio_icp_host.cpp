@@ -274,9 +274,13 @@ static int icp_prepare(lio_icp* h) {
     shard_range(h->ns, h->rank, h->world, h->sh_begin, h->sh_n);
     const int64_t n = std::max<int64_t>(h->sh_n, 1);
     if (n > h->cap) {
-        void* ptrs[] = {h->d_src, h->d_cur, h->d_fd2, h->d_fid, h->d_tiles, h->d_tcost, h->d_order};
-        for (void* q : ptrs)
-            if (q) IHIP(hipFree(q));
+        void** ptrs[] = {(void**)&h->d_src,   (void**)&h->d_cur,   (void**)&h->d_fd2,  (void**)&h->d_fid,
+                         (void**)&h->d_tiles, (void**)&h->d_tcost, (void**)&h->d_order};
+        h->cap = 0;  // a failed allocation below leaves no buffer that looks usable (and nothing freed twice)
+        for (void** q : ptrs) {
+            if (*q) (void)hipFree(*q);
+            *q = nullptr;
+        }
         IHIP(hipMalloc(&h->d_src, n * 3 * sizeof(float)));
         IHIP(hipMalloc(&h->d_cur, n * 3 * sizeof(float)));
         IHIP(hipMalloc(&h->d_fd2, n * sizeof(float)));
@@ -288,7 +292,10 @@ static int icp_prepare(lio_icp* h) {
     }
     const int64_t nsup_all = (h->ns + lio::kIcpSuper - 1) / lio::kIcpSuper + 1;
     if (nsup_all > h->super_cap) {
-        if (h->h_super) IHIP(hipHostFree(h->h_super));
+        if (h->h_super) (void)hipHostFree(h->h_super);
+        h->h_super = nullptr;
+        h->h_super_dev = nullptr;
+        h->super_cap = 0;
         IHIP(hipHostMalloc(&h->h_super, nsup_all * lio::kIcpStride * sizeof(double), hipHostMallocMapped));
         IHIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->h_super_dev), h->h_super, 0));
         h->super_cap = nsup_all;

@@ -50,8 +50,19 @@ def allgather_numpy(send: np.ndarray, group=None, device=None) -> np.ndarray:
 def make_allgather(group=None, device=None):
     """ctypes ``lio_allgather_fn`` doing the exchange with torch.distributed.
 
+    ``device``: where the exchanged tensor lives.  RCCL ("nccl") only moves device tensors, so with
+    that backend it defaults to the current CUDA device; gloo works on CPU tensors (None).
+    A failing callback makes ``lio_icp_align`` return LIO_ERR_STATE on that rank while the other
+    ranks wait inside the collective: the caller must then abort every rank (e.g. by raising,
+    which ends the torchrun job), never retry the alignment alone.
     Keep the returned object alive while the ICP handle uses it.
     """
+    import torch.distributed as dist
+
+    if device is None and dist.get_backend(group) == "nccl":
+        import torch
+
+        device = torch.device("cuda", torch.cuda.current_device())
 
     def _cb(send_p, n, recv_p, user):
         try:

@@ -41,11 +41,12 @@ for s in $STEPS; do
     rehearse) LIO_BENCH_REHEARSE=1 run rehearse2 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 100 --warmup 10 --icp-reps 2 ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
-               -- python bench.py --steps 100 --warmup 10 --no-cpu --icp-reps 3 ;;
+               -- python bench.py --steps 100 --warmup 10 --no-cpu --icp-reps 3 --streams '' ;;
     pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv \
-               -- python bench.py --steps 30 --warmup 3 --no-cpu --no-icp &&
+               -- python bench.py --steps 30 --warmup 3 --no-cpu --no-icp --streams '' &&
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv \
-               -- python bench.py --steps 30 --warmup 3 --no-cpu --no-icp ;;
+               -- python bench.py --steps 30 --warmup 3 --no-cpu --no-icp --streams '' ;;
+    pmcicp) run pmc_icp 900 bash scripts/pmc_icp.sh "$TAG/pmcicp" ;;
     *) echo "unknown step $s" ;;
     esac
 done
