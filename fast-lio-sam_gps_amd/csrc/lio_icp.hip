@@ -328,6 +328,163 @@ __global__ void __launch_bounds__(kIcpTileQ * NW) icp_tile_kernel(IcpArgs a) {
 }
 
 
+// ----------------------------------------------------------------------------
+// Exact 1-NN, one lane per query (icp_query_kernel, the default).
+//
+// The tile kernel above shares one candidate stream among a tile's 64 lanes, so
+// every lane tests every candidate of the tile's search box — a box sized by
+// the tile's WORST query (C4: ~570 candidates per query, ~4.2 k VALU per wave).
+// Here every lane searches its own sphere: queries stay in the binned (cell)
+// order, so a wave's 64 lanes are spatial neighbours that read the same target
+// cells (L1 / L2 hits), and each lane
+//   1. takes its previous correspondence as the first bound (later passes of an
+//      alignment), else scans its own 3x3x3 block of target cells (rows: one
+//      contiguous range of 3 cells each), growing the box (1 -> 3 -> 7 ... cells)
+//      while it has found nothing;
+//   2. scans every row of cells within sqrt(B) of the query, x-range trimmed to
+//      the sphere, rows pruned against the CURRENT best as it improves, minus
+//      the block of step 1.
+// Candidates are tested 4 per step (clamped indices: a repeated point leaves the
+// minimum unchanged).  Same total order (d2, id) and d2 formula as the tile
+// kernel, so the results are identical.
+// ----------------------------------------------------------------------------
+__device__ __forceinline__ void lane_scan_range(const GridDev& g, uint32_t b, uint32_t e, float x, float y, float z,
+                                                uint64_t& best, uint32_t& cand) {
+    if (b >= e) return;
+    cand += e - b;
+    const uint32_t last = e - 1;
+#pragma unroll 1
+    for (uint32_t j = b; j < e; j += 4) {
+        const float4 p0 = g.pts[j];
+        const float4 p1 = g.pts[min(j + 1, last)];
+        const float4 p2 = g.pts[min(j + 2, last)];
+        const float4 p3 = g.pts[min(j + 3, last)];
+        const uint64_t k0 = knn_key(sqdist3(x, y, z, p0.x, p0.y, p0.z), __float_as_int(p0.w));
+        const uint64_t k1 = knn_key(sqdist3(x, y, z, p1.x, p1.y, p1.z), __float_as_int(p1.w));
+        const uint64_t k2 = knn_key(sqdist3(x, y, z, p2.x, p2.y, p2.z), __float_as_int(p2.w));
+        const uint64_t k3 = knn_key(sqdist3(x, y, z, p3.x, p3.y, p3.z), __float_as_int(p3.w));
+        const uint64_t m01 = k0 < k1 ? k0 : k1, m23 = k2 < k3 ? k2 : k3;
+        const uint64_t m = m01 < m23 ? m01 : m23;
+        best = m < best ? m : best;
+    }
+}
+
+// rows (y, z) of box N minus the cells of box S (S may be empty: x0 > x1); with
+// prune, rows / x-ranges outside the sphere of the current best are skipped
+__device__ void lane_scan_box(const GridDev& g, const CellBox& N, const CellBox& S, bool prune, float x, float y,
+                              float z, uint64_t& best, uint32_t& cand) {
+    const float cs = g.cell, m = g.margin;
+    const bool sempty = S.x0 > S.x1;
+    const uint32_t gnx = (uint32_t)g.nx, gnxy = (uint32_t)g.nx * (uint32_t)g.ny;
+#pragma unroll 1
+    for (int rz = N.z0; rz <= N.z1; ++rz) {
+#pragma unroll 1
+        for (int ry = N.y0; ry <= N.y1; ++ry) {
+            int x0 = N.x0, x1 = N.x1;
+            if (prune) {
+                const float B = __uint_as_float((uint32_t)(best >> 32));
+                const float yl = g.oy + (float)ry * cs - m, zl = g.oz + (float)rz * cs - m;
+                const float g2 = axis_gap(y, yl, yl + cs + 2.f * m) + axis_gap(z, zl, zl + cs + 2.f * m);
+                if (g2 * 0.999999f > B) continue;
+                const float rx = sqrtf(fmaxf(B - g2 * 0.999999f, 0.f)) * 1.00001f + m;
+                x0 = max(x0, cell_coord(x - rx, g.ox, g.inv_cell));
+                x1 = min(x1, cell_coord(x + rx, g.ox, g.inv_cell));
+            }
+            if (x0 > x1) continue;
+            const uint32_t rowc = (uint32_t)rz * gnxy + (uint32_t)ry * gnx;
+            const bool inS = !sempty && ry >= S.y0 && ry <= S.y1 && rz >= S.z0 && rz <= S.z1;
+            const int lx1 = inS ? min(x1, S.x0 - 1) : x1;
+            if (x0 <= lx1) lane_scan_range(g, g.start[rowc + (uint32_t)x0], g.start[rowc + (uint32_t)lx1 + 1], x, y, z, best, cand);
+            const int rx0 = max(x0, S.x1 + 1);
+            if (inS && rx0 <= x1) lane_scan_range(g, g.start[rowc + (uint32_t)rx0], g.start[rowc + (uint32_t)x1 + 1], x, y, z, best, cand);
+        }
+    }
+}
+
+constexpr int kIcpQueryThreads = 256;
+
+__global__ void __launch_bounds__(kIcpQueryThreads) icp_query_kernel(IcpArgs a) {
+    const int blk = xcd_block(blockIdx.x, gridDim.x);  // neighbouring blocks (space) on one XCD's L2
+    const int q = blk * kIcpQueryThreads + threadIdx.x;
+    if (q >= a.n) return;  // per lane: no block-level synchronisation below
+    const int i = __float_as_int(a.qpts[q].w);
+    float x, y, z;
+    if (a.fitness) {  // getFitnessScore: original source * final
+        xform_pcl(a.T, a.src[3 * i], a.src[3 * i + 1], a.src[3 * i + 2], x, y, z);
+    } else {
+        x = a.cur[3 * i];
+        y = a.cur[3 * i + 1];
+        z = a.cur[3 * i + 2];
+        if (a.apply_T) {
+            float ox, oy, oz;
+            xform_pcl(a.T, x, y, z, ox, oy, oz);
+            x = ox;
+            y = oy;
+            z = oz;
+        }
+    }
+    const GridDev& g = a.grid;
+    uint64_t best = knn_key(INFINITY, kNone);
+    if (a.prior) {  // the previous correspondence: an exact candidate
+        const int prior = a.nn_id[i];
+        if (prior >= 0 && prior != kNone) {
+            const float4 p = a.tgt_by_id[prior];
+            best = knn_key(sqdist3(x, y, z, p.x, p.y, p.z), prior);
+        }
+    }
+    const int cx = cell_coord(x, g.ox, g.inv_cell), cy = cell_coord(y, g.oy, g.inv_cell),
+              cz = cell_coord(z, g.oz, g.inv_cell);
+    uint32_t cand = 0;
+    CellBox S{1, 0, 1, 0, 1, 0};  // scanned so far
+    if ((uint32_t)best == (uint32_t)kNone) {
+        // 1. bound: boxes of 1, 3, 7, ... cells around the query's cell until a candidate exists
+        for (int r = 1;; r = 2 * r + 1) {
+            const CellBox N{max(cx - r, 0), min(cx + r, g.nx - 1), max(cy - r, 0), min(cy + r, g.ny - 1),
+                            max(cz - r, 0), min(cz + r, g.nz - 1)};
+            if (N.x0 <= N.x1 && N.y0 <= N.y1 && N.z0 <= N.z1) {
+                CellBox Sc{max(S.x0, N.x0), min(S.x1, N.x1), max(S.y0, N.y0), min(S.y1, N.y1), max(S.z0, N.z0),
+                           min(S.z1, N.z1)};
+                if (Sc.x0 > Sc.x1 || Sc.y0 > Sc.y1 || Sc.z0 > Sc.z1) Sc = CellBox{1, 0, 1, 0, 1, 0};
+                lane_scan_box(g, N, Sc, false, x, y, z, best, cand);
+                S = N;
+            }
+            const bool full = cx - r <= 0 && cy - r <= 0 && cz - r <= 0 && cx + r >= g.nx - 1 && cy + r >= g.ny - 1 &&
+                              cz + r >= g.nz - 1;
+            if ((uint32_t)best != (uint32_t)kNone || full) break;
+        }
+    }
+    if ((uint32_t)best != (uint32_t)kNone) {
+        // 2. final: every row within sqrt(B) of the query, minus the scanned block
+        const float B = __uint_as_float((uint32_t)(best >> 32));
+        const float R = sqrtf(B) * 1.00001f + g.margin;
+        const CellBox N{max(cell_coord(x - R, g.ox, g.inv_cell), 0), min(cell_coord(x + R, g.ox, g.inv_cell), g.nx - 1),
+                        max(cell_coord(y - R, g.oy, g.inv_cell), 0), min(cell_coord(y + R, g.oy, g.inv_cell), g.ny - 1),
+                        max(cell_coord(z - R, g.oz, g.inv_cell), 0), min(cell_coord(z + R, g.oz, g.inv_cell), g.nz - 1)};
+        if (N.x0 <= N.x1 && N.y0 <= N.y1 && N.z0 <= N.z1) {
+            CellBox Sc{max(S.x0, N.x0), min(S.x1, N.x1), max(S.y0, N.y0), min(S.y1, N.y1), max(S.z0, N.z0), min(S.z1, N.z1)};
+            if (Sc.x0 > Sc.x1 || Sc.y0 > Sc.y1 || Sc.z0 > Sc.z1) Sc = CellBox{1, 0, 1, 0, 1, 0};
+            lane_scan_box(g, N, Sc, true, x, y, z, best, cand);
+        }
+    }
+    if (a.dbg) {
+        atomicAdd(a.dbg, (unsigned long long)cand);
+        if ((threadIdx.x & 63) == 0) atomicAdd(a.dbg + 2, 1ull);
+        atomicAdd(a.dbg + 3, 1ull);
+    }
+    if (a.fitness || a.apply_T) {
+        a.cur[3 * i] = x;
+        a.cur[3 * i + 1] = y;
+        a.cur[3 * i + 2] = z;
+    }
+    a.nn_d2[i] = __uint_as_float((uint32_t)(best >> 32));
+    a.nn_id[i] = (int)(uint32_t)best;
+}
+
+void launch_icp_query(const IcpArgs& a, hipStream_t st) {
+    if (a.n == 0) return;
+    icp_query_kernel<<<(a.n + kIcpQueryThreads - 1) / kIcpQueryThreads, kIcpQueryThreads, 0, st>>>(a);
+}
+
 // One block = one 4096-point record -> super[record][kIcpStride]: each lane
 // accumulates its 4 points (record-relative index lane + 1024 k, k ascending),
 // each wave sums its lanes (wave_sum32, recursive halving), and the 16 wave

@@ -333,6 +333,16 @@ static bool icp_order_on() {
     return on;
 }
 
+// LIO_ICP_KERNEL=tile: the round-1 tile kernel (one candidate stream per 64-query tile) instead of the
+// per-query kernel (A/B switch; both give identical correspondences).
+static bool icp_tile_kernel_on() {
+    static const bool on = [] {
+        const char* e = std::getenv("LIO_ICP_KERNEL");
+        return e && std::string(e) == "tile";
+    }();
+    return on;
+}
+
 // One correspondence (or fitness) pass: GPU kernels + exchange + ordered sum.
 static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, double max_d2, double out17[17]) {
     lio::IcpArgs a{};
@@ -367,26 +377,30 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     const int nsup_loc = (int)((h->sh_n + lio::kIcpSuper - 1) / lio::kIcpSuper);
     if (h->sh_n > 0) {
         if (h->timing) IHIP(hipEventRecord(h->ev.a, h->st));
-        lio::launch_icp_tiles(a, h->ntiles, h->st);
+        if (icp_tile_kernel_on())
+            lio::launch_icp_tiles(a, h->ntiles, h->st);
+        else
+            lio::launch_icp_query(a, h->st);
         lio::launch_icp_stats(a, h->h_super_dev, h->st);  // records straight to host memory
         if (h->timing) IHIP(hipEventRecord(h->ev.b, h->st));
         IHIP(hipGetLastError());
         IHIP(hipEventRecord(h->ev.done, h->st));
         // longest-first order for the next pass of this alignment: behind the records, so it runs
         // while the host does the SVD / convergence test
-        if (!fitness && icp_order_on()) lio::launch_icp_order(h->d_tcost, h->ntiles, h->d_order, h->st);
+        if (!fitness && icp_order_on() && icp_tile_kernel_on())
+            lio::launch_icp_order(h->d_tcost, h->ntiles, h->d_order, h->st);
         IHIP(hipGetLastError());
         IHIP(hipEventSynchronize(h->ev.done));
     } else {
         IHIP(hipStreamSynchronize(h->st));
     }
     h->have_prior = true;
-    if (!fitness && h->sh_n > 0 && icp_order_on()) h->have_order = true;
+    if (!fitness && h->sh_n > 0 && icp_order_on() && icp_tile_kernel_on()) h->have_order = true;
     if (dbg_on) {
         unsigned long long c[4];
         IHIP(hipMemcpy(c, h->d_dbg, sizeof(c), hipMemcpyDeviceToHost));
-        std::fprintf(stderr, "icp dbg: tiles %llu lanes %llu cand/tile %.1f rounds/tile %.2f cand/lane %.1f\n", c[2], c[3],
-                     (double)c[0] / c[2], (double)c[1] / c[2], (double)c[0] / c[3]);
+        std::fprintf(stderr, "icp dbg: tiles|waves %llu lanes %llu cand/tile %.1f rounds/tile %.2f cand/lane %.1f\n", c[2],
+                     c[3], (double)c[0] / c[2], (double)c[1] / c[2], (double)c[0] / c[3]);
     }
     if (h->timing && h->sh_n > 0) {
         float ms = 0.f;

@@ -130,6 +130,8 @@ constexpr int kIcpTileQ = 64;     // queries per tile (one wave)
 // the tile count (synchronises the stream once).  tiles: capacity n + n / 64 + 1.
 int icp_build_tiles(const GridBuf& q, uint2* tiles, uint32_t* scratch, void*& tmp, size_t& tmp_bytes, hipStream_t st);
 void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st);
+// exact 1-NN, one lane per query in binned order (default; LIO_ICP_KERNEL=tile selects the tile kernel)
+void launch_icp_query(const IcpArgs& a, hipStream_t st);
 // tile order for the next pass: descending log2(cost) buckets (one block)
 void launch_icp_order(const uint32_t* tile_cost, int ntiles, uint32_t* order, hipStream_t st);
 void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st);  // one record per 4096 points

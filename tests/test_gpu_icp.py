@@ -1,4 +1,5 @@
-"""Loop-closure ICP correspondence search on the GPU (icp_tile_kernel) vs brute force.
+"""Loop-closure ICP correspondence search on the GPU (icp_query_kernel; icp_tile_kernel behind
+LIO_ICP_KERNEL=tile) vs brute force.
 
 Every source point's 1-NN in the final (getFitnessScore) pass must be the exact
 (d2, id)-minimum over the target, d2 = float ((dx*dx + dy*dy) + dz*dz) — the
@@ -97,8 +98,12 @@ def test_icp_nn_multi_iteration_prior():
     check_nn(lc, ids, d2, dst)
 
 
-@pytest.mark.parametrize("env", [{"LIO_ICP_ORDER": "0"}, {"LIO_ICP_R0": "0"}, {"LIO_ICP_R0": "3"},
-                                 {"LIO_ICP_TILE_WAVES": "1"}, {"LIO_ICP_TILE_WAVES": "4"}])
+_TILE = {"LIO_ICP_KERNEL": "tile"}
+
+
+@pytest.mark.parametrize("env", [_TILE, dict(_TILE, LIO_ICP_ORDER="0"), dict(_TILE, LIO_ICP_R0="0"),
+                                 dict(_TILE, LIO_ICP_R0="3"), dict(_TILE, LIO_ICP_TILE_WAVES="1"),
+                                 dict(_TILE, LIO_ICP_TILE_WAVES="4")])
 def test_icp_switches_keep_exact_nn(env):
     """The ICP A/B switches (tile order, first bound box, waves per tile) change only the
     search schedule: the final-pass 1-NN stays exact.  Child process (switches are read once)."""

@@ -487,3 +487,16 @@ def test_h_model_many_blocks_matches_oracle(oracle, n_pts):
     p2[9:12] += np.array([0.02, -0.01, 0.005])
     o_reuse, _, _, _ = _oracle_eval(oracle, om, body, p2, nn, sel, planes, redo=False)
     _check_sums(hm(p2, False), o_reuse)
+
+
+def test_icp_c4_multi_iteration_matches_oracle(oracle):
+    """C4 at full size with a 2.5 m / 4 deg initial offset: 9 PCL iterations (each pass starting from the
+    previous correspondences); transform within 1e-5, iterations and convergence state identical."""
+    src, dst, _ = synth.make_icp_pair(n_points=500_000, seed=4321, disp=(2.5, 4.0))
+    lc = LC.LoopClosure(LC.LoopClosureConfig())
+    lc.icpAlignment(src, dst)
+    r = lc.last_result
+    o = oracle.icp_align(src, dst)
+    assert r.iterations == o["iterations"] >= 5 and r.state == o["state"]
+    np.testing.assert_allclose(_T(r), o["T"], atol=1e-5)
+    np.testing.assert_allclose(r.score, o["fitness"], rtol=1e-5)
