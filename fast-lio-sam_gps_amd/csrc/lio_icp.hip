@@ -66,11 +66,30 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-struct TileLds {
-    float4 pts[kTileCh];
+// staged candidates as structure of arrays: 4 consecutive x (y, z, id) are one
+// 16-byte broadcast read, and two candidates' coordinates sit in one register
+// pair for the packed FP32 distance (v_pk_add_f32 / v_pk_mul_f32)
+struct alignas(16) TileLds {
+    float x[kTileCh], y[kTileCh], z[kTileCh];
+    uint32_t id[kTileCh];
     uint32_t b[2 * kIcpTileQ];
     uint32_t off[2 * kIcpTileQ + 1];
 };
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// min of two (d2, id) keys as doubles: key = (d2 bits << 32 | id) with d2 >= +0 is a positive double
+// whose order is the unsigned order, so one v_min_f64 replaces compare + two selects.  Inline asm
+// skips the sNaN canonicalisation clang adds around fmin (keys are never NaN); d2 = 0 makes the key
+// an f64 denormal, which the default FP64 denormal mode keeps (tested: exact zero-distance ties).
+__device__ __forceinline__ double key_min(double a, double b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ double key_of(float d2, uint32_t id) {
+    return __longlong_as_double((long long)(((uint64_t)__float_as_uint(d2) << 32) | id));
+}
 
 __device__ __forceinline__ float wave_min_f(float v) {
 #pragma unroll
@@ -101,7 +120,7 @@ template <int NW>  // waves per tile: the tile's candidate stream is split over 
 __device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32_t b0, uint32_t n0, uint32_t b1,
                                             uint32_t n1, bool act, float x, float y, float z, uint64_t& best,
                                             unsigned long long& cand) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     const uint32_t n = n0 + n1;
     uint32_t incl = n;
 #pragma unroll
@@ -137,26 +156,35 @@ __device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32
             v[u] = g.pts[sb + (t - lo)];
         }
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (base + (uint32_t)(u * kIcpTileQ + lane) < T) L.pts[u * kIcpTileQ + lane] = v[u];
-        wave_sync();
-        const int cnt = (int)min((uint32_t)kTileCh, T - base);
-        if (act) {
-            int j = 0;
-#pragma unroll 1
-            for (; j + 2 <= cnt; j += 2) {
-                const float4 p0 = L.pts[j], p1 = L.pts[j + 1];
-                const uint64_t k0 = knn_key(sqdist3(x, y, z, p0.x, p0.y, p0.z), __float_as_int(p0.w));
-                const uint64_t k1 = knn_key(sqdist3(x, y, z, p1.x, p1.y, p1.z), __float_as_int(p1.w));
-                const uint64_t mm = k0 < k1 ? k0 : k1;
-                best = mm < best ? mm : best;
-            }
-            for (; j < cnt; ++j) {
-                const float4 p = L.pts[j];
-                const uint64_t kk = knn_key(sqdist3(x, y, z, p.x, p.y, p.z), __float_as_int(p.w));
-                best = kk < best ? kk : best;
-            }
+        for (int u = 0; u < U; ++u) {  // slots past the stream end: +inf points with id kNone (never win)
+            const int sl2 = u * kIcpTileQ + lane;
+            const bool in = base + (uint32_t)sl2 < T;
+            L.x[sl2] = in ? v[u].x : INFINITY;
+            L.y[sl2] = in ? v[u].y : INFINITY;
+            L.z[sl2] = in ? v[u].z : INFINITY;
+            L.id[sl2] = in ? __float_as_uint(v[u].w) : (uint32_t)kNone;
         }
+        wave_sync();
+        // every lane (active or not: uniform control flow) tests 4 staged candidates per step,
+        // distances two at a time in packed FP32 ((dx*dx + dy*dy) + dz*dz per element, no FMA)
+        const int cnt4 = ((int)min((uint32_t)kTileCh, T - base) + 3) & ~3;
+        const f2v qx = {x, x}, qy = {y, y}, qz = {z, z};
+        double bk = __longlong_as_double((long long)best);
+#pragma unroll 1
+        for (int j = 0; j < cnt4; j += 4) {
+            const float4 X = *reinterpret_cast<const float4*>(__builtin_assume_aligned(&L.x[j], 16));
+            const float4 Y = *reinterpret_cast<const float4*>(__builtin_assume_aligned(&L.y[j], 16));
+            const float4 Z = *reinterpret_cast<const float4*>(__builtin_assume_aligned(&L.z[j], 16));
+            const uint4 I = *reinterpret_cast<const uint4*>(__builtin_assume_aligned(&L.id[j], 16));
+            const f2v dx0 = qx - f2v{X.x, X.y}, dy0 = qy - f2v{Y.x, Y.y}, dz0 = qz - f2v{Z.x, Z.y};
+            const f2v dx1 = qx - f2v{X.z, X.w}, dy1 = qy - f2v{Y.z, Y.w}, dz1 = qz - f2v{Z.z, Z.w};
+            const f2v d0 = (dx0 * dx0 + dy0 * dy0) + dz0 * dz0;
+            const f2v d1 = (dx1 * dx1 + dy1 * dy1) + dz1 * dz1;
+            const double m0 = key_min(key_of(d0.x, I.x), key_of(d0.y, I.y));
+            const double m1 = key_min(key_of(d1.x, I.z), key_of(d1.y, I.w));
+            bk = key_min(bk, key_min(m0, m1));
+        }
+        best = (uint64_t)__double_as_longlong(bk);
         wave_sync();  // chunk consumed before it is overwritten
     }
 }

@@ -333,12 +333,12 @@ static bool icp_order_on() {
     return on;
 }
 
-// LIO_ICP_KERNEL=tile: the round-1 tile kernel (one candidate stream per 64-query tile) instead of the
-// per-query kernel (A/B switch; both give identical correspondences).
+// LIO_ICP_KERNEL=query: one lane per query (icp_query_kernel) instead of the tile kernel (one candidate
+// stream per 64-query tile) — A/B switch; both give identical correspondences.
 static bool icp_tile_kernel_on() {
     static const bool on = [] {
         const char* e = std::getenv("LIO_ICP_KERNEL");
-        return e && std::string(e) == "tile";
+        return !(e && std::string(e) == "query");
     }();
     return on;
 }

@@ -48,11 +48,11 @@ for s in $STEPS; do
                -- python bench.py --steps 30 --warmup 3 --no-cpu --no-icp --streams '' ;;
     pmcicp) run pmc_icp 900 bash scripts/pmc_icp.sh "$TAG/pmcicp" ;;
     icptest) run pytest_icp 600 python -u -m pytest tests/test_gpu_icp.py tests/test_gpu_parity.py -k icp -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
-    icpab) run icp_query 300 python scripts/icp_ab.py 1.0 &&
-           LIO_ICP_DEBUG=1 run icp_query_dbg 300 python scripts/icp_ab.py 1.0 1 &&
-           LIO_ICP_KERNEL=tile run icp_tile 300 python scripts/icp_ab.py 1.0 &&
-           run icp_query_c05 300 python scripts/icp_ab.py 0.5 &&
-           run icp_query_c07 300 python scripts/icp_ab.py 0.7 ;;
+    icpab) run icp_tile 300 python scripts/icp_ab.py 1.0 &&
+           LIO_ICP_DEBUG=1 run icp_tile_dbg 300 python scripts/icp_ab.py 1.0 1 &&
+           LIO_ICP_TILE_CELL=2.5 run icp_tile_t25 300 python scripts/icp_ab.py 1.0 &&
+           LIO_ICP_TILE_CELL=1.5 run icp_tile_t15 300 python scripts/icp_ab.py 1.0 &&
+           run icp_tile_c075 300 python scripts/icp_ab.py 0.75 ;;
     icpprof) run icp_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/icpprof" -o run --output-format csv -- python scripts/icp_ab.py 1.0 ;;
     *) echo "unknown step $s" ;;
     esac

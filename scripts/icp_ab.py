@@ -12,7 +12,7 @@ from lio_gpu import synth  # noqa: E402
 
 cell = float(sys.argv[1]) if len(sys.argv) > 1 else 1.0
 reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
-kern = os.environ.get("LIO_ICP_KERNEL", "query")
+kern = os.environ.get("LIO_ICP_KERNEL", "tile")
 for disp in ((0.3, 1.5), (2.5, 4.0)):
     src, dst, _ = synth.make_icp_pair(n_points=500_000, seed=4321, disp=disp)
     lc = LC.LoopClosure(LC.LoopClosureConfig(), cell_size=cell)

@@ -1,5 +1,5 @@
-"""Loop-closure ICP correspondence search on the GPU (icp_query_kernel; icp_tile_kernel behind
-LIO_ICP_KERNEL=tile) vs brute force.
+"""Loop-closure ICP correspondence search on the GPU (icp_tile_kernel; icp_query_kernel behind
+LIO_ICP_KERNEL=query) vs brute force.
 
 Every source point's 1-NN in the final (getFitnessScore) pass must be the exact
 (d2, id)-minimum over the target, d2 = float ((dx*dx + dy*dy) + dz*dz) — the
@@ -90,6 +90,18 @@ def test_icp_nn_ties_lowest_id():
     check_nn(lc, ids, d2, dst)
 
 
+def test_icp_nn_zero_distance_ties():
+    """Source points ON duplicated target points: d2 = 0 exactly, so the (d2, id) key the tile kernel
+    minimises as an f64 is a denormal (just the id) — the lowest id must still win."""
+    g = np.stack(np.meshgrid(np.arange(1, 9), np.arange(1, 9), np.arange(1, 4), indexing="ij"), -1).reshape(-1, 3)
+    g = g.astype(np.float32) * np.float32(0.75) + np.float32(3.0)
+    dst = np.concatenate([g, g[::-1], g]).astype(np.float32)  # every point three times, different ids
+    src = np.ascontiguousarray(g[np.random.default_rng(2).permutation(len(g))])
+    lc, r, ids, d2 = run(src, dst, 1.0, guess=np.eye(4, dtype=np.float32))
+    check_nn(lc, ids, d2, dst)
+    assert np.count_nonzero(d2 == 0) > len(src) // 2
+
+
 def test_icp_nn_multi_iteration_prior():
     # a larger displacement: several ICP iterations, later passes seeded with the previous NN
     src, dst, _ = synth.make_icp_pair(n_points=20_000, seed=9, disp=(1.0, 4.0))
@@ -98,12 +110,8 @@ def test_icp_nn_multi_iteration_prior():
     check_nn(lc, ids, d2, dst)
 
 
-_TILE = {"LIO_ICP_KERNEL": "tile"}
-
-
-@pytest.mark.parametrize("env", [_TILE, dict(_TILE, LIO_ICP_ORDER="0"), dict(_TILE, LIO_ICP_R0="0"),
-                                 dict(_TILE, LIO_ICP_R0="3"), dict(_TILE, LIO_ICP_TILE_WAVES="1"),
-                                 dict(_TILE, LIO_ICP_TILE_WAVES="4")])
+@pytest.mark.parametrize("env", [{"LIO_ICP_KERNEL": "query"}, {"LIO_ICP_ORDER": "0"}, {"LIO_ICP_R0": "0"},
+                                 {"LIO_ICP_R0": "3"}, {"LIO_ICP_TILE_WAVES": "1"}, {"LIO_ICP_TILE_WAVES": "4"}])
 def test_icp_switches_keep_exact_nn(env):
     """The ICP A/B switches (tile order, first bound box, waves per tile) change only the
     search schedule: the final-pass 1-NN stays exact.  Child process (switches are read once)."""
