@@ -53,7 +53,8 @@ for s in $STEPS; do
            LIO_ICP_TILE_CELL=2.5 run icp_tile_t25 300 python scripts/icp_ab.py 1.0 &&
            LIO_ICP_TILE_CELL=1.5 run icp_tile_t15 300 python scripts/icp_ab.py 1.0 &&
            run icp_tile_c075 300 python scripts/icp_ab.py 0.75 ;;
-    icpprof) run icp_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/icpprof" -o run --output-format csv -- python scripts/icp_ab.py 1.0 ;;
+    icpprof) run icp_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/icpprof" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
+             run icp_pmc_valu 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --kernel-trace -d "$OUT/icppmc" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 ;;
     *) echo "unknown step $s" ;;
     esac
 done
