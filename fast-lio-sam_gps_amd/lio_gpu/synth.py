@@ -21,8 +21,10 @@ Everything here is host-side numpy input generation; nothing is timed.
 """
 from __future__ import annotations
 
+import concurrent.futures
 import dataclasses
 import math
+import os
 
 import numpy as np
 
@@ -144,9 +146,22 @@ def _faces(scene: Scene):
     return out
 
 
+_SURFACE_CACHE: dict = {}
+
+
 def sample_surface(scene: Scene, n_points: int, seed: int = 1234, sigma: float = 0.01,
                    x_window=None) -> np.ndarray:
-    """Area-uniform surface samples (float32, no interior points, no duplicates)."""
+    """Area-uniform surface samples (float32, no interior points, no duplicates).  Deterministic, so
+    the full-size maps are generated once per process (cached; a copy is returned)."""
+    key = (scene.length, scene.boxes.tobytes(), n_points, seed, sigma, None if x_window is None else tuple(x_window))
+    if key not in _SURFACE_CACHE:
+        if len(_SURFACE_CACHE) >= 3:
+            _SURFACE_CACHE.pop(next(iter(_SURFACE_CACHE)))
+        _SURFACE_CACHE[key] = _sample_surface(scene, n_points, seed, sigma, x_window)
+    return _SURFACE_CACHE[key].copy()
+
+
+def _sample_surface(scene: Scene, n_points: int, seed: int, sigma: float, x_window) -> np.ndarray:
     rng = np.random.default_rng(seed + 7)
     faces = _faces(scene)
     if x_window is not None:  # drop faces entirely outside the window; the rest is rejection-sampled
@@ -201,15 +216,24 @@ def _raycast(scene: Scene, origin: np.ndarray, dirs: np.ndarray, max_range: floa
         # only boxes within range of the origin
         near = (B[:, 3] > origin[0] - max_range) & (B[:, 0] < origin[0] + max_range)
         B = B[near]
-        for s in range(0, n, 8192):
-            iv = inv[s:s + 8192]
-            t0 = (B[None, :, 0:3] - origin[None, None, :]) * iv[:, None, :]
-            t1 = (B[None, :, 3:6] - origin[None, None, :]) * iv[:, None, :]
-            tmin = np.nanmax(np.minimum(t0, t1), axis=2)
-            tmax = np.nanmin(np.maximum(t0, t1), axis=2)
-            hit = (tmax >= tmin) & (tmax > 0) & (tmin > 0)
-            th = np.where(hit, tmin, np.inf).min(axis=1)
-            best[s:s + 8192] = np.minimum(best[s:s + 8192], th)
+        def chunk(s):
+            with np.errstate(divide="ignore", invalid="ignore"):
+                iv = inv[s:s + 8192]
+                t0 = (B[None, :, 0:3] - origin[None, None, :]) * iv[:, None, :]
+                t1 = (B[None, :, 3:6] - origin[None, None, :]) * iv[:, None, :]
+                tmin = np.nanmax(np.minimum(t0, t1), axis=2)
+                tmax = np.nanmin(np.maximum(t0, t1), axis=2)
+                hit = (tmax >= tmin) & (tmax > 0) & (tmin > 0)
+                th = np.where(hit, tmin, np.inf).min(axis=1)
+                best[s:s + 8192] = np.minimum(best[s:s + 8192], th)
+
+        starts = list(range(0, n, 8192))
+        if len(starts) > 2:  # numpy releases the GIL on these array ops: chunks in parallel threads
+            with concurrent.futures.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+                list(ex.map(chunk, starts))
+        else:
+            for s in starts:
+                chunk(s)
     best[best > max_range] = np.inf
     return best
 

@@ -35,6 +35,7 @@
 #include <limits>
 #include <numeric>
 #include <unordered_map>
+#include <unordered_set>
 #include <vector>
 #ifdef _OPENMP
 #include <omp.h>
@@ -73,7 +74,10 @@ struct KdTree {
     std::vector<Node> nodes;
     static const int LEAF = 12;
 
-    int build_rec(int b, int e) {
+    // Median split on the widest axis, ties by id.  The top levels build their two subtrees as
+    // OpenMP tasks into separate node vectors that are then appended (indices shifted): the node
+    // numbering differs from a serial build, the tree (and every search result) does not.
+    int build_rec(std::vector<Node>& out, int b, int e, int depth) {
         Node nd;
         nd.begin = b;
         nd.end = e;
@@ -102,17 +106,37 @@ struct KdTree {
                                  });
                 nd.dim = dim;
                 nd.split = xyz[3 * (size_t)perm[m] + dim];
-                int self = (int)nodes.size();
-                nodes.push_back(nd);
-                int l = build_rec(b, m);
-                int r = build_rec(m, e);
-                nodes[self].left = l;
-                nodes[self].right = r;
+                const int self = (int)out.size();
+                out.push_back(nd);
+                if (depth < 4 && e - b > (1 << 16)) {
+                    std::vector<Node> L, R;
+#pragma omp task shared(L)
+                    build_rec(L, b, m, depth + 1);
+#pragma omp task shared(R)
+                    build_rec(R, m, e, depth + 1);
+#pragma omp taskwait
+                    out[self].left = append(out, L);
+                    out[self].right = append(out, R);
+                } else {
+                    const int l = build_rec(out, b, m, depth + 1);
+                    const int r = build_rec(out, m, e, depth + 1);
+                    out[self].left = l;
+                    out[self].right = r;
+                }
                 return self;
             }
         }
-        nodes.push_back(nd);
-        return (int)nodes.size() - 1;
+        out.push_back(nd);
+        return (int)out.size() - 1;
+    }
+    static int append(std::vector<Node>& out, const std::vector<Node>& sub) {
+        const int off = (int)out.size();
+        for (Node nd : sub) {
+            if (nd.left >= 0) nd.left += off;
+            if (nd.right >= 0) nd.right += off;
+            out.push_back(nd);
+        }
+        return off;  // the subtree's root is its first node
     }
 
     void build(const float* p, int64_t n) {
@@ -127,7 +151,11 @@ struct KdTree {
         const int64_t n = (int64_t)perm.size();
         nodes.clear();
         nodes.reserve(2 * (n / LEAF + 1) + 8);
-        if (n > 0) build_rec(0, (int)n);
+        if (n > 0) {
+#pragma omp parallel num_threads(8)
+#pragma omp single
+            build_rec(nodes, 0, (int)n, 0);
+        }
         pxyz.resize(3 * n);
         for (int64_t i = 0; i < n; ++i)
             for (int d = 0; d < 3; ++d) pxyz[3 * i + d] = xyz[3 * (size_t)perm[i] + d];
@@ -1474,8 +1502,21 @@ struct DynMap {
             return ((kx + (1 << 20)) << 42) | ((ky + (1 << 20)) << 21) | (kz + (1 << 20));
         };
         std::unordered_map<int64_t, std::vector<int64_t>> bmap, bnew;
-        for (int64_t id = 0; id < n_ids(); ++id)
-            if (alive[id]) bmap[bkey(&xyz[3 * id])].push_back(id);
+        {   // only the buckets a lookup below can reach (the 27 around each input point's bucket)
+            std::unordered_set<int64_t> need;
+            for (int64_t i = 0; i < n; ++i) {
+                const int64_t k0 = bkey(p + 3 * i);
+                for (int dx = -1; dx <= 1; ++dx)
+                    for (int dy = -1; dy <= 1; ++dy)
+                        for (int dz = -1; dz <= 1; ++dz)
+                            need.insert(k0 + (int64_t)dx * (int64_t(1) << 42) + (int64_t)dy * (int64_t(1) << 21) + dz);
+            }
+            for (int64_t id = 0; id < n_ids(); ++id)
+                if (alive[id]) {
+                    const int64_t k = bkey(&xyz[3 * id]);
+                    if (need.count(k)) bmap[k].push_back(id);
+                }
+        }
         auto gather = [&](std::unordered_map<int64_t, std::vector<int64_t>>& bm, int64_t k0, std::vector<int64_t>& out) {
             for (int dx = -1; dx <= 1; ++dx)
                 for (int dy = -1; dy <= 1; ++dy)
@@ -1572,13 +1613,21 @@ static void map_incremental(DynMap& dm, const float* body, int64_t n, const Pose
     dm.refresh();
     std::vector<float> to_add, no_need;
     int64_t skipped = 0;
+    // the unbounded 5-NN of every point against the map as it is before this call's adds
+    // (independent queries: parallel; the classification below stays sequential)
+    std::vector<int32_t> nn_all(5 * (size_t)n);
+    std::vector<int> found_all(n);
+#pragma omp parallel for schedule(dynamic, 512) num_threads(8)
     for (int64_t i = 0; i < n; ++i) {
-        float wk[3], w[3];
+        float wk[3], d2[5];
         body_to_world(pk, body + 3 * i, wk);
+        found_all[i] = dm.tree.knn(wk, 5, INFINITY, &nn_all[5 * (size_t)i], d2);
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        float w[3];
         body_to_world(pf, body + 3 * i, w);
-        int32_t nn[5];
-        float d2[5];
-        const int found = dm.tree.knn(wk, 5, INFINITY, nn, d2);
+        const int32_t* nn = &nn_all[5 * (size_t)i];
+        const int found = found_all[i];
         if (found == 0) {
             to_add.insert(to_add.end(), w, w + 3);
             continue;
@@ -1862,6 +1911,13 @@ int64_t orc_dmap_add(void* m, const float* xyz, int64_t n, int downsample, float
 }
 int64_t orc_dmap_delete_boxes(void* m, const float* boxes, int nb) {
     return ((orc::DynMap*)m)->delete_boxes(boxes, nb);
+}
+// the DynMap's kd-tree over its alive ids (refreshed): usable wherever an orc_map_build handle is
+// (orc_h_share_model, orc_ieskf_update), with the map's own ids.  Owned by the DynMap.
+void* orc_dmap_tree(void* m) {
+    auto* d = (orc::DynMap*)m;
+    d->refresh();
+    return &d->tree;
 }
 int orc_dmap_knn(void* m, const float* q, int64_t nq, int k, float range_sq, int32_t* idx, float* d2) {
     if (k < 1 || k > 8) return -1;

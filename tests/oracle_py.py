@@ -94,6 +94,8 @@ def lib():
         L.orc_dmap_delete_boxes.argtypes = [vp, C.POINTER(C.c_float), C.c_int]
         L.orc_dmap_knn.argtypes = [vp, C.POINTER(C.c_float), i64, C.c_int, C.c_float, C.POINTER(C.c_int32),
                                    C.POINTER(C.c_float)]
+        L.orc_dmap_tree.restype = vp
+        L.orc_dmap_tree.argtypes = [vp]
         L.orc_map_incremental.argtypes = [vp, C.POINTER(C.c_float), i64, C.POINTER(C.c_double),
                                           C.POINTER(C.c_double), C.c_double, C.c_float, C.POINTER(C.c_int64)]
         L.orc_voxel_grid.restype = i64
@@ -212,6 +214,13 @@ def icp_align(src, dst, params=None, guess=None, threads=8, max_trace=64, want_a
                 is_valid=bool(out[4]), trace=trace.reshape(max_trace, 20)[:it], aligned=aligned)
 
 
+class _TreeView:
+    """Borrowed kd-tree handle (owned by an OracleDynMap)."""
+
+    def __init__(self, h, owner):
+        self.h, self._owner = h, owner
+
+
 class OracleDynMap:
     """Incremental map restatement: ikd-Tree Add_Points / Delete_Point_Boxes and
     FAST-LIO map_incremental() semantics (oracle/lio_oracle.cpp DynMap)."""
@@ -253,6 +262,11 @@ class OracleDynMap:
         assert lib().orc_dmap_knn(self.h, _p(q, C.c_float), len(q), k, C.c_float(range_sq), _p(idx, C.c_int32),
                                   _p(d2, C.c_float)) == 0
         return idx, d2
+
+    def tree(self):
+        """A map handle (the DynMap's kd-tree over its alive ids, same ids) for h_share_model /
+        ieskf_update; valid until the DynMap changes."""
+        return _TreeView(lib().orc_dmap_tree(self.h), self)
 
     def map_incremental(self, body, pose_knn24, pose24, fs=0.5, ds=0.5):
         body = np.ascontiguousarray(body, dtype=np.float32).reshape(-1, 3)
