@@ -112,7 +112,7 @@ def test_c5_raw_scan_pipeline_three_scans(oracle):
         n_down = hm.preprocess_scan(raw, poses, F.pose_from_pose24(end24), point_filter_num=4, blind=2.0,
                                     filter_size_surf=0.5, time_field=4)
         o = oracle.preprocess(raw, poses, end24, point_filter_num=4, blind=2.0, leaf=0.5)
-        assert n_down == len(o) > 10_000
+        assert n_down == len(o) > 1000
         hm(_identity_pose(), True)
         body = hm.world()  # feats_down_body as the device holds it (identity pose: world == body)
         np.testing.assert_allclose(body, o[:, :3], rtol=2e-7, atol=2e-6)
