@@ -552,22 +552,28 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
     return LIO_OK;
 }
 
-int icp_align(const float* src, int64_t ns, const float* dst, int64_t nd, const lio_icp_params* p, float* T_out,
-              double* fitness, int* converged, int* iters, float* aligned) {
-    lio_icp* h = nullptr;
-    int rc = lio_icp_create(p, &h);
+int icp_align(const float* src, int64_t ns, const float* dst, int64_t nd, const lio_icp_params* p, int n_gpus,
+              float* T_out, double* fitness, int* converged, int* iters, float* aligned) {
+    if (!p) return ifail(LIO_ERR_ARG, "icp_align: NULL params");
+    // n_gpus > 1: devices p->device .. p->device + n_gpus - 1, source sharded, records all-gathered over
+    // RCCL (lio_icp_group); n_gpus <= 1: one handle on p->device
+    const int ng = n_gpus > 1 ? n_gpus : 1;
+    std::vector<int> devs(ng);
+    for (int r = 0; r < ng; ++r) devs[r] = p->device + r;
+    lio_icp_group* g = nullptr;
+    int rc = lio_icp_group_create(p, ng, devs.data(), &g);
     if (rc) return rc;
-    rc = lio_icp_set_target(h, dst, nd);
-    if (!rc) rc = lio_icp_set_source(h, src, ns);
+    rc = lio_icp_group_set_target(g, dst, nd);
+    if (!rc) rc = lio_icp_group_set_source(g, src, ns);
     lio_icp_result r{};
-    if (!rc) rc = lio_icp_align(h, nullptr, &r, aligned);
+    if (!rc) rc = lio_icp_group_align(g, nullptr, &r, aligned);
     if (!rc) {
         if (T_out) std::memcpy(T_out, r.T, sizeof(r.T));
         if (fitness) *fitness = r.score;
         if (converged) *converged = r.is_converged;
         if (iters) *iters = r.iterations;
     }
-    lio_icp_destroy(h);
+    lio_icp_group_destroy(g);
     return rc;
 }
 

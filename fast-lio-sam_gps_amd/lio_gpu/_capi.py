@@ -36,7 +36,9 @@ EXPORTS = [
     "lio_get_knn", "lio_get_planes", "lio_get_world", "lio_get_h_rows", "lio_ctx_knn_stats",
     "lio_ieskf_update",
     "lio_icp_create", "lio_icp_destroy", "lio_icp_set_target", "lio_icp_set_source", "lio_icp_set_shard",
-    "lio_icp_align", "icp_align", "lio_icp_shard_range", "lio_icp_combine", "lio_icp_get_correspondences",
+    "lio_icp_align", "icp_align", "lio_icp_group_create", "lio_icp_group_destroy", "lio_icp_group_size",
+    "lio_icp_group_uses_rccl", "lio_icp_group_set_target", "lio_icp_group_set_source", "lio_icp_group_align",
+    "lio_icp_shard_range", "lio_icp_combine", "lio_icp_get_correspondences",
     "lio_ctx_set_timing", "lio_ctx_get_timing", "lio_ctx_reset_timing", "lio_icp_set_timing", "lio_icp_get_timing",
 ]
 
@@ -189,8 +191,15 @@ def _declare(L):
         "lio_icp_set_shard": (C.c_int, [vp, C.c_int, C.c_int, ALLGATHER_FN, vp]),
         "lio_icp_align": (C.c_int, [vp, fp, C.POINTER(IcpResult), fp]),
         "lio_icp_get_correspondences": (C.c_int, [vp, C.POINTER(C.c_int32), fp]),
-        "icp_align": (C.c_int, [fp, C.c_int64, fp, C.c_int64, C.POINTER(IcpParams), fp, dp,
+        "icp_align": (C.c_int, [fp, C.c_int64, fp, C.c_int64, C.POINTER(IcpParams), C.c_int, fp, dp,
                                 C.POINTER(C.c_int), C.POINTER(C.c_int), fp]),
+        "lio_icp_group_create": (C.c_int, [C.POINTER(IcpParams), C.c_int, C.POINTER(C.c_int), C.POINTER(vp)]),
+        "lio_icp_group_destroy": (C.c_int, [vp]),
+        "lio_icp_group_size": (C.c_int, [vp]),
+        "lio_icp_group_uses_rccl": (C.c_int, [vp]),
+        "lio_icp_group_set_target": (C.c_int, [vp, fp, C.c_int64]),
+        "lio_icp_group_set_source": (C.c_int, [vp, fp, C.c_int64]),
+        "lio_icp_group_align": (C.c_int, [vp, fp, C.POINTER(IcpResult), fp]),
         "lio_icp_shard_range": (C.c_int, [C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
         "lio_icp_combine": (C.c_int, [dp, C.c_int64, C.c_int, dp]),
         "lio_ctx_set_timing": (C.c_int, [vp, C.c_int]),

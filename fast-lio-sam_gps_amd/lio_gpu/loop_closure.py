@@ -173,3 +173,55 @@ class LoopClosure:
             self.close()
         except Exception:
             pass
+
+
+class LoopClosureGroup:
+    """Single-process multi-GPU loop ICP (``lio_icp_group``): one handle per device, the source
+    sharded, the per-iteration records all-gathered over RCCL (or through host memory with
+    ``LIO_ICP_EXCHANGE=host`` / a device listed twice).  Same results as :class:`LoopClosure`, bit
+    for bit."""
+
+    def __init__(self, config: LoopClosureConfig, n_gpus: int, devices=None, cell_size: float = 1.0):
+        self.config_ = config
+        self._p = icp_params(config, cell_size, 0 if devices is None else int(devices[0]))
+        self._h = C.c_void_p()
+        devs = None
+        if devices is not None:
+            devs = (C.c_int * n_gpus)(*[int(d) for d in devices])
+        check(lib().lio_icp_group_create(C.byref(self._p), int(n_gpus), devs, C.byref(self._h)))
+        self.n_gpus = int(n_gpus)
+        self._ns = 0
+
+    @property
+    def uses_rccl(self) -> bool:
+        return bool(lib().lio_icp_group_uses_rccl(self._h))
+
+    def setInputTarget(self, dst: np.ndarray):
+        d = np.ascontiguousarray(_xyz(dst))
+        check(lib().lio_icp_group_set_target(self._h, d.ctypes.data_as(C.POINTER(C.c_float)), len(d)))
+
+    def setInputSource(self, src: np.ndarray):
+        s = np.ascontiguousarray(_xyz(src))
+        self._ns = len(s)
+        check(lib().lio_icp_group_set_source(self._h, s.ctypes.data_as(C.POINTER(C.c_float)), len(s)))
+
+    def align(self, guess: np.ndarray | None = None, keep_aligned: bool = True):
+        res = _capi.IcpResult()
+        g = None if guess is None else np.ascontiguousarray(guess, dtype=np.float32).reshape(16)
+        out = np.empty((self._ns, 3), np.float32) if keep_aligned else None
+        check(lib().lio_icp_group_align(self._h, None if g is None else g.ctypes.data_as(C.POINTER(C.c_float)),
+                                        C.byref(res), None if out is None else out.ctypes.data_as(C.POINTER(C.c_float))))
+        if out is not None:
+            self.aligned_ = out
+        return res
+
+    def close(self):
+        if self._h:
+            lib().lio_icp_group_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

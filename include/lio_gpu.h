@@ -261,9 +261,28 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
  * getFitnessScore pass) per source point of this rank's shard: target index
  * (input order of lio_icp_set_target) and float squared distance.          */
 int lio_icp_get_correspondences(lio_icp* h, int32_t* ids, float* d2);
-/* One-shot form of the above (SURVEY §8b signature).                       */
+/* Single-process multi-GPU loop ICP for a C++ host: one
+ * lio_icp per device (devices NULL => 0 .. n_gpus-1), the source sharded in
+ * 4096-point records, the target replicated; per iteration the ranks' records
+ * are all-gathered over RCCL (ncclCommInitAll + ncclAllGather; librccl is
+ * opened at creation) and summed in record order, so the transform is
+ * bit-identical to one GPU.  LIO_ICP_EXCHANGE=host (or the same device listed
+ * twice) swaps the records through host memory instead.  A failed rank aborts
+ * the group (recreate it).  Replaces LoopClosure's ICP instance
+ * (loop_closure.cpp:3-14) when several GPUs serve the loop-closure thread.  */
+typedef struct lio_icp_group lio_icp_group;
+int lio_icp_group_create(const lio_icp_params* p, int n_gpus, const int* devices, lio_icp_group** out);
+int lio_icp_group_destroy(lio_icp_group* g);
+int lio_icp_group_size(const lio_icp_group* g);
+int lio_icp_group_uses_rccl(const lio_icp_group* g);
+int lio_icp_group_set_target(lio_icp_group* g, const float* xyz, int64_t n);
+int lio_icp_group_set_source(lio_icp_group* g, const float* xyz, int64_t n);
+/* as lio_icp_align; aligned_opt is the whole n*3 cloud (each rank fills its shard) */
+int lio_icp_group_align(lio_icp_group* g, const float* guess16, lio_icp_result* out, float* aligned_opt);
+/* One-shot form (SURVEY §8(b) signature): n_gpus <= 1 runs on p->device, n_gpus > 1 on devices
+ * p->device .. p->device + n_gpus - 1 through lio_icp_group.                                     */
 int icp_align(const float* src_xyz, int64_t ns, const float* dst_xyz, int64_t nd, const lio_icp_params* p,
-              float* T_out, double* fitness, int* converged, int* iters, float* aligned_xyz_opt);
+              int n_gpus, float* T_out, double* fitness, int* converged, int* iters, float* aligned_xyz_opt);
 
 /* FAST-LIO map_incremental() [U] for the ctx's current scan: world points
  * with the final pose, Nearest_Points from the ctx's last kNN evaluation

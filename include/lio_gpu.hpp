@@ -455,4 +455,45 @@ private:
     lio_icp_result last_{};
 };
 
+// LoopClosure's ICP served by several GPUs from one process (lio_icp_group):
+// the source sharded, the per-iteration statistics all-gathered over RCCL;
+// results bit-identical to LoopClosureICP.  devices empty => 0 .. n_gpus-1.
+class LoopClosureICPGroup {
+public:
+    LoopClosureICPGroup(const LoopClosureConfig& cfg, int n_gpus, const std::vector<int>& devices = {},
+                        float cell_size = 1.0f) {
+        lio_icp_params p{cfg.icp_max_corr_dist_, 0.01, 0.01, 50, 0.0, cfg.icp_score_threshold_, cell_size,
+                         devices.empty() ? 0 : devices[0]};
+        check(lio_icp_group_create(&p, n_gpus, devices.empty() ? nullptr : devices.data(), &g_), "lio_icp_group_create");
+    }
+    ~LoopClosureICPGroup() { lio_icp_group_destroy(g_); }
+    LoopClosureICPGroup(const LoopClosureICPGroup&) = delete;
+    LoopClosureICPGroup& operator=(const LoopClosureICPGroup&) = delete;
+
+    template <typename P>
+    RegistrationOutput icpAlignment(const std::vector<P>& src, const std::vector<P>& dst,
+                                    std::vector<float>* aligned_xyz = nullptr) {
+        const std::vector<float> s = packed_xyz(src), d = packed_xyz(dst);
+        check(lio_icp_group_set_source(g_, s.data(), (int64_t)src.size()), "setInputSource");
+        check(lio_icp_group_set_target(g_, d.data(), (int64_t)dst.size()), "setInputTarget");
+        if (aligned_xyz) aligned_xyz->resize(s.size());
+        lio_icp_result r{};
+        check(lio_icp_group_align(g_, nullptr, &r, aligned_xyz ? aligned_xyz->data() : nullptr), "align");
+        RegistrationOutput out;
+        out.score_ = r.score;
+        if (r.is_valid) {
+            out.is_valid_ = out.is_converged_ = true;
+            for (int k = 0; k < 16; ++k) out.pose_between_eig_[k] = r.T[k];
+        }
+        last_ = r;
+        return out;
+    }
+    const lio_icp_result& last() const { return last_; }
+    bool uses_rccl() const { return lio_icp_group_uses_rccl(g_) != 0; }
+
+private:
+    lio_icp_group* g_ = nullptr;
+    lio_icp_result last_{};
+};
+
 }  // namespace lio_gpu

@@ -311,6 +311,27 @@ int main() {
         EXPECT(r.is_converged_ && r.is_valid_ && r.score_ < 0.05, "icpAlignment converged=%d score=%g", (int)r.is_converged_,
                r.score_);
         EXPECT(std::fabs(r.pose_between_eig_[3]) < 0.2 && std::fabs(r.pose_between_eig_[7]) < 0.2, "icp translation");
+        // the same alignment served by a group of 3 ranks (all on device 0 here: host exchange; distinct
+        // devices use RCCL) and by the one-shot icp_align: bit-identical transforms
+        lio_gpu::LoopClosureICPGroup grp(lio_gpu::LoopClosureConfig{}, 3, {0, 0, 0});
+        const lio_gpu::RegistrationOutput rg = grp.icpAlignment(src, dst);
+        bool same = rg.is_valid_ == r.is_valid_ && grp.last().iterations == icp.last().iterations &&
+                    grp.last().score == icp.last().score;
+        for (int k = 0; k < 16; ++k) same = same && grp.last().T[k] == icp.last().T[k];
+        EXPECT(same && !grp.uses_rccl(), "3-rank group bit-identical to one handle");
+        std::vector<float> s3, d3;
+        for (const auto& p : src) s3.insert(s3.end(), {p.x, p.y, p.z});
+        for (const auto& p : dst) d3.insert(d3.end(), {p.x, p.y, p.z});
+        lio_icp_params ip{52.5, 0.01, 0.01, 50, 0.0, 1.5, 1.0f, 0};
+        float T1[16];
+        double fit = 0.0;
+        int conv = 0, its = 0;
+        EXPECT(icp_align(s3.data(), (int64_t)src.size(), d3.data(), (int64_t)dst.size(), &ip, 1, T1, &fit, &conv, &its,
+                         nullptr) == LIO_OK,
+               "icp_align n_gpus=1");
+        bool same1 = its == icp.last().iterations && fit == icp.last().score;
+        for (int k = 0; k < 16; ++k) same1 = same1 && T1[k] == icp.last().T[k];
+        EXPECT(same1, "icp_align(n_gpus=1) bit-identical to lio_icp_align");
     }
 
     if (g_fail) {

@@ -79,3 +79,13 @@ def test_compute_fails_loudly_without_device():
     assert b"no HIP device" in L.lio_last_error() or b"gfx950" in L.lio_last_error()
     rc = L.lio_icp_create(C.byref(_capi.IcpParams(52.5, 0.01, 0.01, 50, 0.0, 1.5, 1.0, 0)), C.byref(h))
     assert rc == _capi.LIO_ERR_NODEV
+    # the multi-GPU group and the one-shot icp_align(n_gpus) fail the same way (no CPU path)
+    rc = L.lio_icp_group_create(C.byref(_capi.IcpParams(52.5, 0.01, 0.01, 50, 0.0, 1.5, 1.0, 0)), 2, None,
+                                C.byref(h))
+    assert rc == _capi.LIO_ERR_NODEV and not h.value
+    pts = np.zeros((8, 3), np.float32)
+    fp = pts.ctypes.data_as(C.POINTER(C.c_float))
+    T = (C.c_float * 16)()
+    rc = L.icp_align(fp, 8, fp, 8, C.byref(_capi.IcpParams(52.5, 0.01, 0.01, 50, 0.0, 1.5, 1.0, 0)), 4, T, None,
+                     None, None, None)
+    assert rc == _capi.LIO_ERR_NODEV

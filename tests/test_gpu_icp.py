@@ -133,3 +133,39 @@ print("ok")
     r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("n", [2, 4])
+def test_icp_group_bit_identical_to_one_handle(n):
+    """lio_icp_group (single-process multi-GPU): n ranks — all on device 0 on a one-GPU
+    box, so the records travel through host memory; distinct devices use RCCL — give the one-handle
+    transform, score, iterations and aligned cloud bit for bit."""
+    src, dst, _ = synth.make_icp_pair(n_points=60_000, seed=12, disp=(1.0, 3.0))
+    grp = LC.LoopClosureGroup(LC.LoopClosureConfig(), n, devices=[0] * n)
+    assert not grp.uses_rccl
+    grp.setInputSource(src)
+    grp.setInputTarget(dst)
+    rg = grp.align()
+    one = LC.LoopClosure(LC.LoopClosureConfig())
+    one.setInputSource(src)
+    one.setInputTarget(dst)
+    r1 = one.align()
+    assert rg.iterations == r1.iterations >= 2 and rg.score == r1.score and rg.state == r1.state
+    np.testing.assert_array_equal(np.array(list(rg.T)), np.array(list(r1.T)))
+    np.testing.assert_array_equal(grp.aligned_, one.aligned_)
+
+
+@pytest.mark.skipif(LC._capi.lib().lio_device_count() < 2, reason="RCCL exchange needs two distinct devices")
+def test_icp_group_rccl_bit_identical():
+    src, dst, _ = synth.make_icp_pair(n_points=60_000, seed=12, disp=(1.0, 3.0))
+    grp = LC.LoopClosureGroup(LC.LoopClosureConfig(), 2)
+    assert grp.uses_rccl
+    grp.setInputSource(src)
+    grp.setInputTarget(dst)
+    rg = grp.align()
+    one = LC.LoopClosure(LC.LoopClosureConfig())
+    one.setInputSource(src)
+    one.setInputTarget(dst)
+    r1 = one.align()
+    assert rg.iterations == r1.iterations and rg.score == r1.score
+    np.testing.assert_array_equal(np.array(list(rg.T)), np.array(list(r1.T)))
