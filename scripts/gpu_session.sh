@@ -35,7 +35,8 @@ for s in $STEPS; do
            run knn_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/knnprof" -o run --output-format csv -- python scripts/knn_timing.py C2 ;;
     quick) run bench_quick 400 python bench.py --steps 60 --warmup 5 --icp-reps 2 --cpu-scans 10 --cpu-warmup 2 ;;
     c3)    run bench_c3 600 python bench.py --config C3 --steps 60 --warmup 5 --no-icp --cpu-scans 10 --cpu-warmup 2 --pipeline 12 ;;
-    c5)    run bench_c5 600 python bench.py --config C5 --steps 60 --warmup 5 --no-icp --cpu-scans 10 --cpu-warmup 2 --pipeline 12 ;;
+    c2)    run bench_c2 600 python bench.py --config C2 --steps 200 --warmup 20 --no-icp --cpu-scans 20 --cpu-warmup 2 --streams '' ;;
+    c5)    run bench_c5 600 python bench.py --config C5 --steps 200 --warmup 20 --no-icp --cpu-scans 10 --cpu-warmup 2 --pipeline 12 --streams '' ;;
     ppprof) run rocprof_pipeline 600 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/ppprof" -o run \
                --output-format csv -- python bench.py --config C3 --steps 5 --warmup 2 --no-icp --no-cpu --pipeline 12 ;;
     rehearse) LIO_BENCH_REHEARSE=1 run rehearse2 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
