@@ -269,15 +269,16 @@ def main():
             traffic = None
     # unit of work = one kNN h-evaluation (112 B/pt), which runs as
     # knn_near_kernel + knn_far_kernel + plane_kernel back to back on the ctx
-    # stream; achieved = algorithmic bytes / the bracketed duration (HIP events
-    # on that stream, a separate pass after the timed loop)
+    # stream; achieved = algorithmic bytes / the sum of the three kernels' own
+    # execution spans (hipExtLaunchKernel start/stop events on that stream, a
+    # separate pass after the timed loop: the spans rocprofv3 reports, no gaps)
     roofline = {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
                 "traffic": traffic,
                 "kernel": "kNN h-evaluation = knn_near_kernel + knn_far_kernel + plane_kernel",
                 "bytes_per_launch": BYTES_PER_PT_KNN * n_pts, "avg_launch_ms": round(knn_avg_ms, 5),
                 "near_kernel_avg_ms": round(near_avg_ms, 5), "far_kernel_avg_ms": round(far_avg_ms, 5),
-                "plane_kernel_avg_ms": round(knn_avg_ms - near_avg_ms - far_avg_ms, 5),
+                "plane_kernel_avg_ms": round(tm["plane_ms"] / max(tm["plane_launches"], 1), 5),
                 "reuse_kernel_avg_ms": round(reuse_avg_ms, 5),
                 "reuse_achieved_gbs": round(BYTES_PER_PT_REUSE * n_pts / (reuse_avg_ms * 1e-3) / 1e9, 2)
                 if tm["reuse_launches"] else None}

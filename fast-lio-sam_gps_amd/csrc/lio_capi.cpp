@@ -163,7 +163,7 @@ struct lio_ctx {
     bool timing = false;
     lio_kernel_timing tm{};
     EventPair ev_main, ev_fin;
-    hipEvent_t ev_marks[2] = {nullptr, nullptr};  // after near / after far (redo)
+    hipEvent_t ev_marks[8] = {};  // kernel start / stop: near, far, plane, reuse (hipExtLaunchKernel)
     lio::FilterBuf filt;                          // scan preprocessing
     float* d_raw = nullptr;                       // raw records / preprocessed records
     int64_t raw_cap = 0;
@@ -710,7 +710,7 @@ int lio_match(lio_ctx* c, const lio_pose* pose_in, int redo_knn, double* sums) {
     }
     const auto t0 = std::chrono::steady_clock::now();
     if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.a, st));
-    const int nb = lio::launch_h_model(a, redo_knn != 0, st, c->timing && redo_knn ? c->ev_marks : nullptr);
+    const int nb = lio::launch_h_model(a, redo_knn != 0, st, c->timing ? c->ev_marks : nullptr);
     if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.b, st));
     lio::launch_finalize(a, nb, st);  // no-op: the last plane/reuse block publishes the sums
     if (c->timing) HIP_TRY(hipEventRecord(c->ev_fin.b, st));
@@ -737,14 +737,19 @@ int lio_match(lio_ctx* c, const lio_pose* pose_in, int redo_knn, double* sums) {
         HIP_TRY(hipEventSynchronize(c->ev_fin.b));
         EventPair f{c->ev_main.b, c->ev_fin.b};
         accum_event(f, c->tm.final_launches, c->tm.final_ms);
-        if (redo_knn) {
-            accum_event(c->ev_main, c->tm.knn_launches, c->tm.knn_ms);
-            EventPair n{c->ev_main.a, c->ev_marks[0]}, f{c->ev_marks[0], c->ev_marks[1]};
+        if (redo_knn) {  // kernel spans (hipExtLaunchKernel events): no launch gaps, as rocprofv3 reports
+            const double before = c->tm.near_ms + c->tm.far_ms + c->tm.plane_ms;
+            EventPair n{c->ev_marks[0], c->ev_marks[1]}, f{c->ev_marks[2], c->ev_marks[3]},
+                p{c->ev_marks[4], c->ev_marks[5]};
             accum_event(n, c->tm.near_launches, c->tm.near_ms);
-            accum_event(f, c->tm.far_launches, c->tm.far_ms);
+            if (a.max_shell > 1) accum_event(f, c->tm.far_launches, c->tm.far_ms);
+            accum_event(p, c->tm.plane_launches, c->tm.plane_ms);
+            c->tm.knn_ms += (c->tm.near_ms + c->tm.far_ms + c->tm.plane_ms) - before;
+            ++c->tm.knn_launches;
+        } else {
+            EventPair r{c->ev_marks[6], c->ev_marks[7]};
+            accum_event(r, c->tm.reuse_launches, c->tm.reuse_ms);
         }
-        else
-            accum_event(c->ev_main, c->tm.reuse_launches, c->tm.reuse_ms);
     }
     c->last_pose = *pose;
     c->have_eval = true;

@@ -99,6 +99,34 @@ __device__ __forceinline__ uint64_t knn_key(float d, int id) {
     return ((uint64_t)__float_as_uint(d) << 32) | (uint32_t)id;
 }
 
+// Keys as f64: knn_key(d2, id) with 0 <= d2 <= +inf float is the bit pattern of a positive, finite
+// double (exponent <= 0x7f8) whose numeric order is the key order, so v_min_f64 / v_max_f64 order
+// keys in one instruction each (instead of a 64-bit compare and two selects).  Inline asm: clang's
+// fmin/fmax add sNaN canonicalisation that keys never need.  d2 = 0 gives an f64 denormal, kept by
+// the default FP64 denormal mode (tested: exact zero-distance ties, tests/test_gpu_icp.py).
+__device__ __forceinline__ uint64_t key_min(uint64_t a, uint64_t b) {
+    double r;
+    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(__longlong_as_double((long long)a)), "v"(__longlong_as_double((long long)b)));
+    return (uint64_t)__double_as_longlong(r);
+}
+__device__ __forceinline__ uint64_t key_max(uint64_t a, uint64_t b) {
+    double r;
+    asm("v_max_f64 %0, %1, %2" : "=v"(r) : "v"(__longlong_as_double((long long)a)), "v"(__longlong_as_double((long long)b)));
+    return (uint64_t)__double_as_longlong(r);
+}
+
+typedef float f2v __attribute__((ext_vector_type(2)));
+
+// two candidates' squared distances with packed FP32 (v_pk_add_f32 / v_pk_mul_f32): per element
+// exactly sqdist3's ((dx*dx + dy*dy) + dz*dz) (no FMA: -ffp-contract=off)
+__device__ __forceinline__ void sqdist3_x2(float qx, float qy, float qz, const float4& a, const float4& b, float& da,
+                                           float& db) {
+    const f2v dx = f2v{qx, qx} - f2v{a.x, b.x}, dy = f2v{qy, qy} - f2v{a.y, b.y}, dz = f2v{qz, qz} - f2v{a.z, b.z};
+    const f2v d = (dx * dx + dy * dy) + dz * dz;
+    da = d.x;
+    db = d.y;
+}
+
 template <int K>
 struct TopK {
     uint64_t k[K];
@@ -111,15 +139,14 @@ struct TopK {
     __device__ __forceinline__ float worst() const { return d(K - 1); }
     // insertion: entry j takes k[j-1] if x sorts before it, else x if x sorts
     // before k[j] (old values throughout), one compare per slot
+    // (old values throughout: k[j] <- min(k[j], max(k[j-1], x)), k[0] <- min(k[0], x) is the sorted
+    // insertion of x dropping the largest; min / max as f64, no compares or selects)
     __device__ __forceinline__ void push(float dc, int ic) {
         const uint64_t x = knn_key(dc, ic);
         if (!(x < k[K - 1])) return;
-        bool c[K];
 #pragma unroll
-        for (int j = 0; j < K - 1; ++j) c[j] = x < k[j];
-#pragma unroll
-        for (int j = K - 1; j > 0; --j) k[j] = c[j - 1] ? k[j - 1] : ((j == K - 1 || c[j]) ? x : k[j]);
-        if (K == 1 || c[0]) k[0] = x;
+        for (int j = K - 1; j > 0; --j) k[j] = key_min(k[j], key_max(k[j - 1], x));
+        k[0] = key_min(k[0], x);
     }
     // every slot := the K-th entry (a filler that is never re-inserted)
     __device__ __forceinline__ void fill_with_worst() {
@@ -184,9 +211,8 @@ __device__ __forceinline__ float group_min(float v) {
 template <int K>
 __device__ __forceinline__ void cmpx(uint64_t (&v)[K], int i, int j) {
     const uint64_t a = v[i], b = v[j];
-    const bool sw = b < a;
-    v[i] = sw ? b : a;
-    v[j] = sw ? a : b;
+    v[i] = key_min(a, b);
+    v[j] = key_max(a, b);
 }
 template <int K>
 __device__ __forceinline__ void sort_bitonic(uint64_t (&v)[K]) {
@@ -212,7 +238,7 @@ __device__ __forceinline__ void group_merge(TopK<K>& tk) {
             const uint32_t lo = partner_u32<OFF>((uint32_t)tk.k[K - 1 - j]);
             const uint32_t hi = partner_u32<OFF>((uint32_t)(tk.k[K - 1 - j] >> 32));
             const uint64_t b = ((uint64_t)hi << 32) | lo;
-            c[j] = b < tk.k[j] ? b : tk.k[j];
+            c[j] = key_min(b, tk.k[j]);
         }
         sort_bitonic<K>(c);
 #pragma unroll
@@ -245,8 +271,12 @@ __device__ __forceinline__ void scan_cell_group2(const GridDev& g, uint32_t c, f
 #pragma unroll
         for (int u = 0; u < U; ++u) p[u] = g.pts[min(j + (uint32_t)(u * G), e - 1)];
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (j + (uint32_t)(u * G) < e) tk.push(sqdist3(qx, qy, qz, p[u].x, p[u].y, p[u].z), __float_as_int(p[u].w));
+        for (int u = 0; u < U; u += 2) {
+            float d0, d1;
+            sqdist3_x2(qx, qy, qz, p[u], p[u + 1], d0, d1);
+            if (j + (uint32_t)(u * G) < e) tk.push(d0, __float_as_int(p[u].w));
+            if (j + (uint32_t)((u + 1) * G) < e) tk.push(d1, __float_as_int(p[u + 1].w));
+        }
     }
 }
 
@@ -499,9 +529,14 @@ __device__ __forceinline__ void scan_table_strided(const GridDev& g, float qx, f
         float4 p[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) p[u] = g.pts[src[u]];
+        static_assert(U % 2 == 0, "scan_table_strided: pairs of loads");
 #pragma unroll
-        for (int u = 0; u < U; ++u)
-            if (t + (uint32_t)u * L < T) tk.push(sqdist3(qx, qy, qz, p[u].x, p[u].y, p[u].z), __float_as_int(p[u].w));
+        for (int u = 0; u < U; u += 2) {
+            float d0, d1;
+            sqdist3_x2(qx, qy, qz, p[u], p[u + 1], d0, d1);
+            if (t + (uint32_t)u * L < T) tk.push(d0, __float_as_int(p[u].w));
+            if (t + (uint32_t)(u + 1) * L < T) tk.push(d1, __float_as_int(p[u + 1].w));
+        }
     }
 }
 

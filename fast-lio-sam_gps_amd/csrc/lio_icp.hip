@@ -76,16 +76,9 @@ struct alignas(16) TileLds {
     uint32_t off[2 * kIcpTileQ + 1];
 };
 
-typedef float f2v __attribute__((ext_vector_type(2)));
-
-// min of two (d2, id) keys as doubles: key = (d2 bits << 32 | id) with d2 >= +0 is a positive double
-// whose order is the unsigned order, so one v_min_f64 replaces compare + two selects.  Inline asm
-// skips the sNaN canonicalisation clang adds around fmin (keys are never NaN); d2 = 0 makes the key
-// an f64 denormal, which the default FP64 denormal mode keeps (tested: exact zero-distance ties).
-__device__ __forceinline__ double key_min(double a, double b) {
-    double r;
-    asm("v_min_f64 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
+// (d2, id) keys minimised as f64: lio_dev.hpp key_min (one v_min_f64 instead of compare + two selects)
+__device__ __forceinline__ double key_min_d(double a, double b) {
+    return __longlong_as_double((long long)key_min((uint64_t)__double_as_longlong(a), (uint64_t)__double_as_longlong(b)));
 }
 __device__ __forceinline__ double key_of(float d2, uint32_t id) {
     return __longlong_as_double((long long)(((uint64_t)__float_as_uint(d2) << 32) | id));
@@ -180,9 +173,9 @@ __device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32
             const f2v dx1 = qx - f2v{X.z, X.w}, dy1 = qy - f2v{Y.z, Y.w}, dz1 = qz - f2v{Z.z, Z.w};
             const f2v d0 = (dx0 * dx0 + dy0 * dy0) + dz0 * dz0;
             const f2v d1 = (dx1 * dx1 + dy1 * dy1) + dz1 * dz1;
-            const double m0 = key_min(key_of(d0.x, I.x), key_of(d0.y, I.y));
-            const double m1 = key_min(key_of(d1.x, I.z), key_of(d1.y, I.w));
-            bk = key_min(bk, key_min(m0, m1));
+            const double m0 = key_min_d(key_of(d0.x, I.x), key_of(d0.y, I.y));
+            const double m1 = key_min_d(key_of(d1.x, I.z), key_of(d1.y, I.w));
+            bk = key_min_d(bk, key_min_d(m0, m1));
         }
         best = (uint64_t)__double_as_longlong(bk);
         wave_sync();  // chunk consumed before it is overwritten

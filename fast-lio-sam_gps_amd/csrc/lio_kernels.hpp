@@ -37,6 +37,8 @@ struct MatchArgs {
 };
 
 // marks (optional, redo only): events recorded after the near and the far kernel
+// marks (optional, timing): 8 events, start / stop of near, far, plane (redo) or reuse (marks[6..7]),
+// recorded by hipExtLaunchKernel at each kernel's own start and end
 int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* marks = nullptr);
 void launch_debug(const MatchArgs& a, float* world, float* d2, float* abcd_pd2, hipStream_t st);
 void launch_h_rows(const MatchArgs& a, double* rows, int64_t max_rows, int64_t* n_rows, hipStream_t st);

@@ -20,6 +20,8 @@
 //
 // The per-point dense H (effct x 12 doubles) of the reference is never
 // materialised: the IESKF only consumes H^T H and H^T h.
+#include <hip/hip_ext.h>
+
 #include "lio_dev.hpp"
 #include "lio_kernels.hpp"
 
@@ -495,26 +497,30 @@ __global__ void __launch_bounds__(1024) h_rows_kernel(MatchArgs a, double* __res
 int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* marks) {
     if (a.n == 0) return 0;
     const int nb = (a.n + kBlock - 1) / kBlock;
+    // hipExtLaunchKernelGGL with null events is a plain launch; with events (timing) the command
+    // processor stamps them at the kernel's own start / end
+    hipEvent_t m[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+    if (marks)
+        for (int k = 0; k < 8; ++k) m[k] = marks[k];
     if (redo) {
         const int nq = (a.n + kKnnBlock / kGroup - 1) / (kKnnBlock / kGroup);
         if (a.dbg)
-            knn_near_kernel<true, false><<<nq, kKnnBlock, 0, st>>>(a);
+            hipExtLaunchKernelGGL(knn_near_kernel<true, false>, dim3(nq), dim3(kKnnBlock), 0, st, m[0], m[1], 0, a);
         else if (a.prior)
-            knn_near_kernel<false, true><<<nq, kKnnBlock, 0, st>>>(a);
+            hipExtLaunchKernelGGL(knn_near_kernel<false, true>, dim3(nq), dim3(kKnnBlock), 0, st, m[0], m[1], 0, a);
         else
-            knn_near_kernel<false, false><<<nq, kKnnBlock, 0, st>>>(a);
-        if (marks) (void)hipEventRecord(marks[0], st);
+            hipExtLaunchKernelGGL(knn_near_kernel<false, false>, dim3(nq), dim3(kKnnBlock), 0, st, m[0], m[1], 0, a);
         static const int far_blocks = [] {  // LIO_FAR_BLOCKS: diagnostics override of the far-pass grid
             const char* e = std::getenv("LIO_FAR_BLOCKS");
             const int v = e ? std::atoi(e) : 0;
             return v > 0 ? std::min(v, 4096) : kFarBlocks;
         }();
-        if (a.max_shell > 1) knn_far_kernel<<<far_blocks, kFarBlock, 0, st>>>(a);
-        if (marks) (void)hipEventRecord(marks[1], st);
-        plane_kernel<<<nb, kBlock, 0, st>>>(a);
+        if (a.max_shell > 1)
+            hipExtLaunchKernelGGL(knn_far_kernel, dim3(far_blocks), dim3(kFarBlock), 0, st, m[2], m[3], 0, a);
+        hipExtLaunchKernelGGL(plane_kernel, dim3(nb), dim3(kBlock), 0, st, m[4], m[5], 0, a);
         return nb;
     }
-    h_model_reuse_kernel<<<nb, kBlock, 0, st>>>(a);
+    hipExtLaunchKernelGGL(h_model_reuse_kernel, dim3(nb), dim3(kBlock), 0, st, m[6], m[7], 0, a);
     return nb;
 }
 

@@ -375,16 +375,19 @@ int lio_map_build_pcd(lio_map* m, const char* path);
 
 /* ----------------------------------------------------------------- timing */
 typedef struct lio_kernel_timing {
-    int64_t knn_launches;   double knn_ms;     /* kNN h-evaluation: near + far + plane/H  */
-    int64_t reuse_launches; double reuse_ms;   /* converge=false re-evaluation kernel   */
-    int64_t final_launches; double final_ms;   /* block-partial finalize kernel          */
-    int64_t icp_launches;   double icp_ms;     /* ICP correspondence + statistics kernel */
-    int64_t near_launches;  double near_ms;    /* kNN near pass (inside knn_ms)          */
-    int64_t far_launches;   double far_ms;     /* kNN far pass (inside knn_ms)           */
+    int64_t knn_launches;   double knn_ms;     /* kNN h-evaluation: near + far + plane kernels  */
+    int64_t reuse_launches; double reuse_ms;   /* converge=false re-evaluation kernel         */
+    int64_t final_launches; double final_ms;   /* block-partial finalize kernel (LIO_FUSED_FINAL=0) */
+    int64_t icp_launches;   double icp_ms;     /* ICP correspondence + statistics kernels     */
+    int64_t near_launches;  double near_ms;    /* kNN near pass (inside knn_ms)                */
+    int64_t far_launches;   double far_ms;     /* kNN far pass (inside knn_ms)                 */
+    int64_t plane_launches; double plane_ms;   /* plane / H / reduction pass (inside knn_ms)   */
 } lio_kernel_timing;
 
-/* When enabled, HIP events bracket every hot-kernel launch on the handle's
- * stream and their elapsed times accumulate here.                          */
+/* When enabled, every front-end kernel is launched with hipExtLaunchKernel's
+ * start / stop events — the kernel's own execution span, as rocprofv3 reports
+ * it (no launch gaps) — and the spans accumulate here (knn_ms = near + far +
+ * plane).  The ICP handle brackets its pass (both kernels) with events.    */
 int lio_ctx_set_timing(lio_ctx* c, int enable);
 int lio_ctx_get_timing(lio_ctx* c, lio_kernel_timing* out);
 int lio_ctx_reset_timing(lio_ctx* c);

@@ -49,6 +49,10 @@ for s in $STEPS; do
                -- python bench.py --steps 30 --warmup 3 --no-cpu --no-icp --streams '' ;;
     pmcicp) run pmc_icp 900 bash scripts/pmc_icp.sh "$TAG/pmcicp" ;;
     fullsize) run pytest_fullsize 900 python -u -m pytest tests/test_gpu_fullsize.py -x -v -s -p no:cacheprovider --timeout 600 --timeout-method thread ;;
+    abknn) for rep in 1 2; do
+             LIO_GPU_LIB=build_ab/liblio_gpu_base.so run ab_base_$rep 300 python bench.py --steps 400 --warmup 20 --no-icp --no-cpu --streams '' &&
+             run ab_new_$rep 300 python bench.py --steps 400 --warmup 20 --no-icp --no-cpu --streams '' || exit 1
+           done ;;
     icptest) run pytest_icp 600 python -u -m pytest tests/test_gpu_icp.py tests/test_gpu_parity.py -k icp -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     icpab) run icp_tile 300 python scripts/icp_ab.py 1.0 &&
            LIO_ICP_DEBUG=1 run icp_tile_dbg 300 python scripts/icp_ab.py 1.0 1 &&
