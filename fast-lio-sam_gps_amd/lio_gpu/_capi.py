@@ -209,7 +209,10 @@ def _declare(L):
         "lio_icp_set_timing": (C.c_int, [vp, C.c_int]),
         "lio_icp_get_timing": (C.c_int, [vp, C.POINTER(KernelTiming)]),
     }
+    ab = bool(os.environ.get("LIO_GPU_LIB"))  # an older build for A/B timing may lack newer entry points
     for name, (res, args) in sig.items():
+        if ab and not hasattr(L, name):
+            continue
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
