@@ -18,6 +18,7 @@
 #include <vector>
 
 #include "ieskf.hpp"
+#include "ieskf_dev.hpp"
 #include "lio_error.hpp"
 #include "lio_kernels.hpp"
 #include "lio_filter.hpp"
@@ -171,6 +172,14 @@ struct lio_ctx {
     int64_t rec_cap = 0;
     lio::ImuPose* d_poses = nullptr;
     int64_t poses_cap = 0;
+    // device-resident IESKF (lio_ieskf_update): control block + host-mapped input / result
+    lio::IeskfCtl* d_ctl = nullptr;
+    double* h_iin = nullptr;     // kIeskfInWords
+    double* h_iin_dev = nullptr;
+    double* h_iout = nullptr;    // kIeskfOutWords + 2 (sequence number, checksum)
+    double* h_iout_dev = nullptr;
+    hipEvent_t ev_slots[6 * 8] = {};  // timing: near / far / slot kernel start-stop per slot
+    int ieskf_device = -1;            // lio_ctx_set_ieskf_mode: 1 device-resident, 0 host loop, -1 env / default (host)
 };
 
 extern "C" {
@@ -511,8 +520,12 @@ int lio_ctx_destroy(lio_ctx* c) {
     for (hipEvent_t e : c->ev_marks)
         if (e) (void)hipEventDestroy(e);
     lio::filter_free(c->filt);
-    for (void* q : {(void*)c->d_raw, (void*)c->d_rec, (void*)c->d_poses})
+    for (void* q : {(void*)c->d_raw, (void*)c->d_rec, (void*)c->d_poses, (void*)c->d_ctl})
         if (q) (void)hipFree(q);
+    for (double* q : {c->h_iin, c->h_iout})
+        if (q) (void)hipHostFree(q);
+    for (hipEvent_t e : c->ev_slots)
+        if (e) (void)hipEventDestroy(e);
     --c->map->n_ctx;
     delete c;
     return LIO_OK;
@@ -930,10 +943,166 @@ static void from_host(const lio::host::State& x, lio_state& s) {
     std::memcpy(s.grav, x.grav, sizeof(x.grav));
 }
 
+static lio_pose state_pose(const lio::host::State& s) {  // the pose an evaluation at state s uses
+    lio_pose pose;
+    lio::host::quat_to_mat(s.rot, pose.R);
+    lio::host::quat_to_mat(s.offR, pose.R_LI);
+    pose.q[0] = s.rot.w, pose.q[1] = s.rot.x, pose.q[2] = s.rot.y, pose.q[3] = s.rot.z;
+    pose.q_LI[0] = s.offR.w, pose.q_LI[1] = s.offR.x, pose.q_LI[2] = s.offR.y, pose.q_LI[3] = s.offR.z;
+    std::memcpy(pose.t, s.pos, sizeof(pose.t));
+    std::memcpy(pose.t_LI, s.offT, sizeof(pose.t_LI));
+    return pose;
+}
+
+// Device-resident update (opt-in: lio_ctx_set_ieskf_mode(c, 1) or LIO_IESKF_DEVICE=1; the host
+// loop is the default because it measured faster): the whole
+// update_iterated_dyn_share_modified enqueued as one launch sequence — init, then max_iteration + 1
+// evaluation slots whose block 0 runs the IESKF pre-step and whose last block the post-step
+// (ieskf_dev.hpp) — and one wait for the published result.  Returns 1 when the host loop must run
+// instead (dof < 23 branch, or a shape the sequence does not cover), 0 on success, < 0 on error.
+static int ieskf_device_default() {  // -1: not set in the environment
+    static const int v = [] {
+        const char* e = std::getenv("LIO_IESKF_DEVICE");
+        return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
+    }();
+    return v;
+}
+
+static int ieskf_update_device(lio_ctx* c, lio_state* xs, double* P, const lio_ieskf_params& pp, lio_ieskf_stats* st,
+                               const std::chrono::steady_clock::time_point& t_call) {
+    using clk = std::chrono::steady_clock;
+    if (c->n == 0 || c->map->n == 0 || c->map->grid.n_ids == 0 || pp.max_iteration < 0 || pp.max_iteration > 7)
+        return 1;
+    HIP_TRY(hipSetDevice(c->map->dev));
+    if (!c->d_ctl) {
+        if (hipMalloc(&c->d_ctl, lio::ieskf_ctl_bytes()) != hipSuccess) {
+            c->d_ctl = nullptr;
+            return fail(LIO_ERR_NOMEM, "lio_ieskf_update: control block allocation failed");
+        }
+        if (hipHostMalloc(&c->h_iin, lio::kIeskfInWords * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) !=
+                hipSuccess ||
+            hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_iin_dev), c->h_iin, 0) != hipSuccess ||
+            hipHostMalloc(&c->h_iout, (lio::kIeskfOutWords + 2) * sizeof(double),
+                          hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_iout_dev), c->h_iout, 0) != hipSuccess) {
+            (void)hipFree(c->d_ctl);
+            c->d_ctl = nullptr;
+            return fail(LIO_ERR_NOMEM, "lio_ieskf_update: host-mapped buffers allocation failed");
+        }
+        std::memset(c->h_iout, 0, (lio::kIeskfOutWords + 2) * sizeof(double));
+    }
+    if (c->timing && !c->ev_slots[0])
+        for (hipEvent_t& e : c->ev_slots) (void)hipEventCreate(&e);
+    // input: x, P, R, epsi, max_iteration
+    std::memcpy(c->h_iin, xs, lio::kStateWords * sizeof(double));
+    std::memcpy(c->h_iin + lio::kStateWords, P, LIO_STATE_DIM * LIO_STATE_DIM * sizeof(double));
+    c->h_iin[lio::kStateWords + 529] = pp.laser_point_cov;
+    c->h_iin[lio::kStateWords + 530] = pp.epsi;
+    c->h_iin[lio::kStateWords + 531] = (double)pp.max_iteration;
+    lio_pose dummy{};
+    dummy.q[0] = dummy.q_LI[0] = 1.0;
+    lio::MatchArgs a = make_args(c, dummy);
+    if (!a.fused_final) return 1;  // LIO_FUSED_FINAL=0 (separate finalize launches): the host loop
+    a.ctl = c->d_ctl;
+    a.ieskf_out = c->h_iout_dev;
+    const unsigned long long seq = ++c->seq;
+    const auto t0 = clk::now();
+    lio::launch_ieskf_dev(a, c->h_iin_dev, seq, pp.max_iteration, c->map->st, c->timing ? c->ev_slots : nullptr);
+    HIP_TRY(hipGetLastError());
+    const auto t1 = clk::now();
+    // wait for the published result (same checksummed one-round-trip protocol as wait_result)
+    const volatile uint64_t* w = reinterpret_cast<const volatile uint64_t*>(c->h_iout);
+    std::vector<uint64_t> bits(lio::kIeskfOutWords);
+    auto read = [&]() -> bool {
+        if (w[lio::kIeskfOutWords] != seq) return false;
+        uint64_t h = 0;
+        for (int l = 0; l < lio::kIeskfOutWords; ++l) {
+            bits[l] = w[l];
+            h ^= mix64(bits[l] ^ ((uint64_t)l * 0x9e3779b97f4a7c15ull));
+        }
+        return (h ^ mix64(seq)) == w[lio::kIeskfOutWords + 1];
+    };
+    for (uint64_t it = 0;; ++it) {
+        if (read()) break;
+        if ((it & 255) == 255) {
+            const hipError_t e = hipStreamQuery(c->map->st);
+            if (e != hipSuccess && e != hipErrorNotReady)
+                return fail(LIO_ERR_HIP, std::string("lio_ieskf_update: ") + hipGetErrorString(e));
+            if (e == hipSuccess && !read()) return fail(LIO_ERR_HIP, "lio_ieskf_update: the update produced no result");
+        }
+    }
+    const auto t2 = clk::now();
+    double out[lio::kIeskfOutWords];
+    std::memcpy(out, bits.data(), sizeof(out));
+    const int h_evals = (int)out[lio::kIeskfOutInts], knn_calls = (int)out[lio::kIeskfOutInts + 1],
+              converged = (int)out[lio::kIeskfOutInts + 2], n_eff = (int)out[lio::kIeskfOutInts + 3],
+              status = (int)out[lio::kIeskfOutInts + 4], knn_mask = (int)out[lio::kIeskfOutInts + 5];
+    if (status == lio::kIeskfSingular) return fail(LIO_ERR_STATE, "IESKF: singular matrix");
+    if (status == lio::kIeskfNeedHost) {
+        HIP_TRY(hipStreamSynchronize(c->map->st));  // the remaining (gated) slots drain
+        c->knn_valid = false;
+        return 1;
+    }
+    if (status != lio::kIeskfOk) return fail(LIO_ERR_HIP, "lio_ieskf_update: unexpected device status");
+    std::memcpy(xs, out + lio::kIeskfOutX, lio::kStateWords * sizeof(double));
+    std::memcpy(P, out + lio::kIeskfOutP, LIO_STATE_DIM * LIO_STATE_DIM * sizeof(double));
+    lio_state sk, sl;
+    std::memcpy(&sk, out + lio::kIeskfOutXKnn, sizeof(sk));
+    std::memcpy(&sl, out + lio::kIeskfOutXLast, sizeof(sl));
+    c->last_pose = state_pose(to_host(sl));
+    c->have_eval = true;
+    if (knn_calls > 0) {
+        c->knn_valid = true;
+        c->knn_map_version = c->map->version;
+        c->knn_pose = state_pose(to_host(sk));
+    }
+    if (c->timing) {  // kernel spans of the slots that ran (the gated ones are empty launches)
+        HIP_TRY(hipStreamSynchronize(c->map->st));
+        for (int e = 0; e < h_evals && e <= pp.max_iteration; ++e) {
+            hipEvent_t* m = c->ev_slots + 6 * e;
+            if (knn_mask & (1 << e)) {
+                const double before = c->tm.near_ms + c->tm.far_ms + c->tm.plane_ms;
+                EventPair n{m[0], m[1]}, f{m[2], m[3]}, pl{m[4], m[5]};
+                accum_event(n, c->tm.near_launches, c->tm.near_ms);
+                if (a.max_shell > 1) accum_event(f, c->tm.far_launches, c->tm.far_ms);
+                accum_event(pl, c->tm.plane_launches, c->tm.plane_ms);
+                c->tm.knn_ms += (c->tm.near_ms + c->tm.far_ms + c->tm.plane_ms) - before;
+                ++c->tm.knn_launches;
+            } else {
+                EventPair r{m[4], m[5]};
+                accum_event(r, c->tm.reuse_launches, c->tm.reuse_ms);
+            }
+        }
+    }
+    if (st) {
+        st->h_evals = h_evals;
+        st->knn_calls = knn_calls;
+        st->converged = converged;
+        st->n_eff = n_eff;
+        st->res_mean = out[lio::kIeskfOutRes];
+        st->solve_ms = 0.0;  // on the device, inside the slot kernels
+        st->launch_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        st->wait_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
+        st->wall_ms = std::chrono::duration<double, std::milli>(clk::now() - t_call).count();
+    }
+    return 0;
+}
+
+int lio_ctx_set_ieskf_mode(lio_ctx* c, int device) {
+    if (!c) return fail(LIO_ERR_ARG, "lio_ctx_set_ieskf_mode: bad arguments");
+    c->ieskf_device = device ? 1 : 0;
+    return LIO_OK;
+}
+
 int lio_ieskf_update(lio_ctx* c, lio_state* xs, double* P, const lio_ieskf_params* p, lio_ieskf_stats* st) {
     if (!c || !xs || !P) return fail(LIO_ERR_ARG, "lio_ieskf_update: bad arguments");
     const auto t_call = std::chrono::steady_clock::now();
     lio_ieskf_params pp = p ? *p : lio_ieskf_params{0.001, 3, 0.001};
+    const int env_mode = ieskf_device_default();
+    if (c->ieskf_device > 0 || (c->ieskf_device < 0 && env_mode == 1)) {
+        const int drc = ieskf_update_device(c, xs, P, pp, st, t_call);
+        if (drc <= 0) return drc;  // done (0) or failed (< 0); 1: the host loop below
+    }
     lio::host::State x = to_host(*xs);
     lio::host::Mat Pm(P, P + LIO_STATE_DIM * LIO_STATE_DIM);
     int err = LIO_OK;
@@ -948,13 +1117,7 @@ int lio_ieskf_update(lio_ctx* c, lio_state* xs, double* P, const lio_ieskf_param
             hm.rows.resize((size_t)std::min(nr, want) * 7);
             return 0;
         }
-        lio_pose pose;
-        lio::host::quat_to_mat(s.rot, pose.R);
-        lio::host::quat_to_mat(s.offR, pose.R_LI);
-        pose.q[0] = s.rot.w, pose.q[1] = s.rot.x, pose.q[2] = s.rot.y, pose.q[3] = s.rot.z;
-        pose.q_LI[0] = s.offR.w, pose.q_LI[1] = s.offR.x, pose.q_LI[2] = s.offR.y, pose.q_LI[3] = s.offR.z;
-        std::memcpy(pose.t, s.pos, sizeof(pose.t));
-        std::memcpy(pose.t_LI, s.offT, sizeof(pose.t_LI));
+        const lio_pose pose = state_pose(s);
         hm.rows.clear();
         c->last_launch_ms = c->last_wait_ms = 0.0;
         int rc = lio_match(c, &pose, redo ? 1 : 0, hm.sums);

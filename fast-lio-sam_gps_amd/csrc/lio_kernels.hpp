@@ -7,6 +7,8 @@
 
 namespace lio {
 
+struct IeskfCtl;  // ieskf_dev.hpp
+
 struct MatchArgs {
     PoseArg pose;
     GridDev grid;
@@ -34,12 +36,20 @@ struct MatchArgs {
     float plane_thr;
     double s_coef;
     double s_gate;
+    IeskfCtl* ctl;            // device-resident update: control block (state, pose, loop flags); else null
+    double* ieskf_out;        // device-resident update: host-mapped result (ieskf_dev.hpp layout)
 };
 
 // marks (optional, redo only): events recorded after the near and the far kernel
 // marks (optional, timing): 8 events, start / stop of near, far, plane (redo) or reuse (marks[6..7]),
 // recorded by hipExtLaunchKernel at each kernel's own start and end
 int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* marks = nullptr);
+// Device-resident lio_ieskf_update: the init kernel (reads `in`, host-mapped, kIeskfInWords doubles)
+// and max_iter + 1 evaluation slots (near, far, plane-or-reuse + IESKF step), enqueued on st without
+// a host round trip.  marks (optional, timing): 6 events per slot, start / stop of near, far, slot kernel.
+void launch_ieskf_dev(const MatchArgs& a, const double* in, unsigned long long seq, int max_iter, hipStream_t st,
+                      hipEvent_t* marks = nullptr);
+size_t ieskf_ctl_bytes();
 void launch_debug(const MatchArgs& a, float* world, float* d2, float* abcd_pd2, hipStream_t st);
 void launch_h_rows(const MatchArgs& a, double* rows, int64_t max_rows, int64_t* n_rows, hipStream_t st);
 void launch_finalize(const MatchArgs& a, int nblocks, hipStream_t st);  // no-op when fused_final

@@ -22,6 +22,7 @@
 // materialised: the IESKF only consumes H^T H and H^T h.
 #include <hip/hip_ext.h>
 
+#include "ieskf_dev.hpp"
 #include "lio_dev.hpp"
 #include "lio_kernels.hpp"
 
@@ -43,37 +44,15 @@ __device__ __forceinline__ double wave_sum(double v) {
     return v;
 }
 
-// Wave reduction of one lane's contribution [HTH(21), HTh(6), cnt, res, hh]
-// (wave_sum32, lio_dev.hpp: recursive halving); lane l < 32 stores value
-// wave_sum32_index(l): a fixed order, deterministic.
-__device__ __forceinline__ void wave_reduce_store(const double J[6], double h, double res, double cnt, double* dst) {
-    const int lane = threadIdx.x & 63;
-    double v[32];
-    int q = 0;
-#pragma unroll
-    for (int r = 0; r < 6; ++r)
-#pragma unroll
-        for (int c = r; c < 6; ++c) v[q++] = J[r] * J[c];
-#pragma unroll
-    for (int r = 0; r < 6; ++r) v[21 + r] = J[r] * h;
-    v[27] = cnt;
-    v[28] = res;
-    v[29] = h * h;
-    v[30] = 0.0;
-    v[31] = 0.0;
-    const double tot = wave_sum32(v, lane);
-    if (lane < 32) dst[wave_sum32_index(lane)] = tot;
-}
-
 // pd2 / s-gate / H row of one selected point (h_share_model [U])
-__device__ __forceinline__ bool residual_row(const MatchArgs& a, float bx, float by, float bz, float wx, float wy,
+__device__ __forceinline__ bool residual_row(const MatchArgs& a, const PoseArg& ps, float bx, float by, float bz, float wx, float wy,
                                              float wz, const float4& pl, double J[6], double& h, double& res) {
     const float pd2 = ((pl.x * wx + pl.y * wy) + pl.z * wz) + pl.w;
     const double b0 = bx, b1 = by, b2 = bz;
     const double pn = sqrt((b0 * b0 + b1 * b1) + b2 * b2);
     const float s = (float)(1.0 - a.s_coef * (double)fabsf(pd2) / sqrt(pn));
     if (!((double)s > a.s_gate)) return false;
-    h_row(a.pose, bx, by, bz, pl.x, pl.y, pl.z, J);
+    h_row(ps, bx, by, bz, pl.x, pl.y, pl.z, J);
     h = -(double)pd2;
     res = (double)fabsf(pd2);
     return true;
@@ -85,8 +64,11 @@ __device__ __forceinline__ bool residual_row(const MatchArgs& a, float bx, float
 // neighbourhoods, ~0.4% of a dense scan) are queued, with their list, for
 // the wave-per-query far pass instead of holding their wave: a kernel runs as
 // long as its slowest wave.  Written for 8 waves/SIMD (<= 64 VGPRs).
-template <bool DBG, bool SEEDED, int U = 4>
+template <bool DBG, bool SEEDED, int U = 4, bool DEV = false>
 __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) knn_near_kernel(MatchArgs a) {
+    if constexpr (DEV)  // device-resident update: this slot runs only while the loop asks for a kNN
+        if (a.ctl->done || !a.ctl->converge) return;
+    const PoseArg& ps = DEV ? a.ctl->pose : a.pose;
     constexpr int G = kGroup;
     constexpr int QPB = kKnnBlock / G;  // 64 queries per block
     __shared__ uint32_t s_tab[QPB][72];      // per-group shell-1 slot table
@@ -97,7 +79,7 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
     if (i >= a.n) return;
     const float bx = a.body[3 * i], by = a.body[3 * i + 1], bz = a.body[3 * i + 2];
     float wx, wy, wz;
-    body_to_world(a.pose, bx, by, bz, wx, wy, wz);
+    body_to_world(ps, bx, by, bz, wx, wy, wz);
     TopK<5> tk;
     tk.init(a.range_sq);
     SearchStats st{0, 0, 0};
@@ -158,14 +140,18 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
 // Pass 2: the queued queries, one block each (block_knn_box_flat over the
 // rest of the query's search box).  Fixed grid; every block strides the queue
 // and exits once past its end.
+template <bool DEV = false>
 __global__ void __launch_bounds__(kFarBlock) knn_far_kernel(MatchArgs a) {
+    if constexpr (DEV)
+        if (a.ctl->done || !a.ctl->converge) return;
+    const PoseArg& ps = DEV ? a.ctl->pose : a.pose;
     __shared__ uint32_t s_b[kFarBlock], s_off[kFarBlock + 1], s_w[kFarBlock / 64];
     __shared__ uint64_t s_lists[(kFarBlock / 64) * 5];
     const int cnt = *a.far_count;
     for (int f = blockIdx.x; f < cnt; f += gridDim.x) {
         const int i = a.far_list[f];
         float wx, wy, wz;
-        body_to_world(a.pose, a.body[3 * i], a.body[3 * i + 1], a.body[3 * i + 2], wx, wy, wz);
+        body_to_world(ps, a.body[3 * i], a.body[3 * i + 1], a.body[3 * i + 2], wx, wy, wz);
         TopK<5> tk;
 #pragma unroll
         for (int j = 0; j < 5; ++j) tk.k[j] = knn_key(a.far_d[5 * (size_t)f + j], a.far_id[5 * (size_t)f + j]);
@@ -218,9 +204,16 @@ __device__ __forceinline__ void publish_host(double t, double* out, unsigned lon
     else if (lane == 33) __hip_atomic_store((gull*)(seq_out + 1), h ^ mix64(seq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-__device__ __forceinline__ void publish_and_finalize(const MatchArgs& a, double (*red)[32]) {
+// Block partial -> global; returns true in the LAST block to finish, whose
+// lanes < 32 then hold the 32 fixed-order sums in `t` (wave 0; block-uniform
+// return value).  fused_final == 0: partial only, the finalize launch sums.
+// slot: this block's partial index (-1: none); npart partials are summed; ncount
+// blocks take part in the counter.  All threads of the block call it.
+__device__ __forceinline__ bool block_partial_last(const MatchArgs& a, double (*red)[32], double& t, int slot, int npart,
+                                                   int ncount) {
     __shared__ int s_last;
-    const int nb = (int)gridDim.x;
+    const int nb = npart;
+    t = 0.0;
     if (!a.fused_final) {  // separate finalize_kernel launch (A/B switch LIO_FUSED_FINAL=0)
         if (threadIdx.x < 32) {
             double s = 0.0;
@@ -228,23 +221,23 @@ __device__ __forceinline__ void publish_and_finalize(const MatchArgs& a, double 
             for (int w = 0; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
             a.partials[(size_t)blockIdx.x * 32 + threadIdx.x] = s;
         }
-        return;
+        return false;
     }
-    if (threadIdx.x < 32) {
+    if (slot >= 0 && threadIdx.x < 32) {
         double s = 0.0;
 #pragma unroll
         for (int w = 0; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
-        __hip_atomic_store((gdouble*)(a.partials + (size_t)blockIdx.x * 32 + threadIdx.x), s, __ATOMIC_RELAXED,
+        __hip_atomic_store((gdouble*)(a.partials + (size_t)slot * 32 + threadIdx.x), s, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing wave drains
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         const unsigned old = __hip_atomic_fetch_add((guint*)a.done_count, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_last = old == (unsigned)(nb - 1);
+        s_last = old == (unsigned)(ncount - 1);
     }
     __syncthreads();
-    if (!s_last) return;  // block-uniform
+    if (!s_last) return false;  // block-uniform
     // fixed-order sum: 8 row groups x 32 columns, then the groups in order
     const int col = threadIdx.x & 31, grp = threadIdx.x >> 5;
     constexpr int NG = kBlock / 32;
@@ -268,87 +261,207 @@ __device__ __forceinline__ void publish_and_finalize(const MatchArgs& a, double 
     __shared__ double sg[NG][33];
     sg[grp][col] = acc;
     __syncthreads();
-    if (threadIdx.x < 64) {
-        double t = 0.0;
-        if (threadIdx.x < 32)
+    if (threadIdx.x < 32)
 #pragma unroll
-            for (int g = 0; g < NG; ++g) t += sg[g][threadIdx.x];
-        if (threadIdx.x == 0)
-            __hip_atomic_store((guint*)a.done_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+        for (int g = 0; g < NG; ++g) t += sg[g][threadIdx.x];
+    if (threadIdx.x == 0)
+        __hip_atomic_store((guint*)a.done_count, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+    return true;
+}
+
+// the last block publishes the sums to the host (lio_match)
+__device__ __forceinline__ void publish_and_finalize(const MatchArgs& a, double (*red)[32]) {
+    double t;
+    if (block_partial_last(a, red, t, blockIdx.x, gridDim.x, gridDim.x) && threadIdx.x < 64)
         publish_host(t, a.sums_out, a.seq_out, a.seq);
+}
+
+// One lane's H-row contribution [HTH(21), HTh(6), cnt, res, hh] added into v[32].
+__device__ __forceinline__ void accum_row(double (&v)[32], const double J[6], double h, double res, double cnt) {
+    int q = 0;
+#pragma unroll
+    for (int r = 0; r < 6; ++r)
+#pragma unroll
+        for (int c = r; c < 6; ++c) v[q++] += J[r] * J[c];
+#pragma unroll
+    for (int r = 0; r < 6; ++r) v[21 + r] += J[r] * h;
+    v[27] += cnt;
+    v[28] += res;
+    v[29] += h * h;
+}
+
+// Points per lane of the plane / reuse kernels (LIO_PPL, default kPplDefault): PPL > 1 gives each
+// lane several points' loads in flight and fewer block partials for the last block to gather.
+constexpr int kPplDefault = 2;
+static int ppl_setting() {
+    static const int v = [] {
+        const char* e = std::getenv("LIO_PPL");
+        const int p = e ? std::atoi(e) : kPplDefault;
+        return (p == 1 || p == 2 || p == 4) ? p : kPplDefault;
+    }();
+    return v;
+}
+
+// Plane pass body, lane = PPL points (strided by the block size, coalesced): gate
+// (found == 5 && d2[4] <= 5), esti_plane, pd2, s-gate, H row, summed into v.
+template <int PPL>
+__device__ __forceinline__ void plane_points(const MatchArgs& a, const PoseArg& ps, int blk, double (&v)[32]) {
+    const int i0 = blk * kBlock * PPL + threadIdx.x;
+    // all points' ids first, then all neighbour gathers: PPL independent chains in flight
+    int id[PPL][5];
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+        const int i = i0 + k * kBlock;
+#pragma unroll
+        for (int j = 0; j < 5; ++j) id[k][j] = i < a.n ? a.nn_idx[5 * (size_t)i + j] : -1;
+    }
+    float P[PPL][5][3];
+#pragma unroll
+    for (int k = 0; k < PPL; ++k)
+        if (id[k][4] >= 0)
+#pragma unroll
+            for (int j = 0; j < 5; ++j) {
+                const float4 q = a.map_by_id[id[k][j]];
+                P[k][j][0] = q.x;
+                P[k][j][1] = q.y;
+                P[k][j][2] = q.z;
+            }
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+        const int i = i0 + k * kBlock;
+        if (i < a.n) {
+            // sorted list: the 5th exists => all exist, d2 <= range by construction
+            bool sel = id[k][4] >= 0;
+            if (sel) {
+                const float bx = a.body[3 * i], by = a.body[3 * i + 1], bz = a.body[3 * i + 2];
+                float abcd[4];
+                sel = esti_plane_dev(P[k], a.plane_thr, abcd);
+                const float4 pl = make_float4(abcd[0], abcd[1], abcd[2], abcd[3]);
+                a.planes[i] = pl;
+                if (sel) {
+                    float wx, wy, wz;
+                    body_to_world(ps, bx, by, bz, wx, wy, wz);
+                    double J[6], h, res;
+                    sel = residual_row(a, ps, bx, by, bz, wx, wy, wz, pl, J, h, res);
+                    if (sel) accum_row(v, J, h, res, 1.0);
+                }
+            }
+            a.sel[i] = sel ? 1 : 0;
+        }
     }
 }
 
-// Pass 3, lane = point: gate (found == 5 && d2[4] <= 5), esti_plane, pd2,
-// s-gate, H row, 4 wave partials combined in LDS -> block partial.  Resets
-// the far queue for the next kNN evaluation.
+// Reuse pass body (ekfom_data.converge == false: cached Nearest_Points / planes), PPL points per lane.
+template <int PPL>
+__device__ __forceinline__ void reuse_points(const MatchArgs& a, const PoseArg& ps, int blk, double (&v)[32]) {
+    const int i0 = blk * kBlock * PPL + threadIdx.x;
+    // every point's three loads issued together (one round trip instead of sel -> body/plane)
+    bool sel[PPL];
+    float b[PPL][3];
+    float4 pl[PPL];
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+        const int i = i0 + k * kBlock;
+        sel[k] = false;
+        if (i < a.n) {
+            sel[k] = a.sel[i] != 0;
+            b[k][0] = a.body[3 * i];
+            b[k][1] = a.body[3 * i + 1];
+            b[k][2] = a.body[3 * i + 2];
+            pl[k] = a.planes[i];
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < PPL; ++k) {
+        if (sel[k]) {
+            const int i = i0 + k * kBlock;
+            float wx, wy, wz;
+            body_to_world(ps, b[k][0], b[k][1], b[k][2], wx, wy, wz);
+            double J[6], h, res;
+            const bool s = residual_row(a, ps, b[k][0], b[k][1], b[k][2], wx, wy, wz, pl[k], J, h, res);
+            if (s) accum_row(v, J, h, res, 1.0);
+            a.sel[i] = s ? 1 : 0;
+        }
+    }
+}
+
+// Pass 3 (kNN evaluations): plane_points, wave sums, 4 wave partials combined in
+// LDS -> block partial; the last block publishes.  Resets the far queue for the
+// next kNN evaluation.
+template <int PPL>
 __global__ void __launch_bounds__(kBlock) plane_kernel(MatchArgs a) {
     __shared__ double red[kBlock / 64][32];
-    const int i = blockIdx.x * kBlock + threadIdx.x;
-    double J[6] = {0, 0, 0, 0, 0, 0};
-    double h = 0.0, res = 0.0, cnt = 0.0;
-    if (i < a.n) {
-        const int32_t* nn = a.nn_idx + 5 * (size_t)i;
-        // the body point is needed only for selected points, but loading it here keeps
-        // its latency off the chain nn_idx -> neighbours -> esti_plane
-        const float bx = a.body[3 * i], by = a.body[3 * i + 1], bz = a.body[3 * i + 2];
-        int id[5];
+    double v[32];
 #pragma unroll
-        for (int j = 0; j < 5; ++j) id[j] = nn[j];
-        bool sel = id[4] >= 0;  // sorted list: the 5th exists => all exist, d2 <= range by construction
-        if (sel) {
-            float P[5][3];
-#pragma unroll
-            for (int j = 0; j < 5; ++j) {
-                const float4 q = a.map_by_id[id[j]];
-                P[j][0] = q.x;
-                P[j][1] = q.y;
-                P[j][2] = q.z;
-            }
-            float abcd[4];
-            sel = esti_plane_dev(P, a.plane_thr, abcd);
-            const float4 pl = make_float4(abcd[0], abcd[1], abcd[2], abcd[3]);
-            a.planes[i] = pl;
-            if (sel) {
-                float wx, wy, wz;
-                body_to_world(a.pose, bx, by, bz, wx, wy, wz);
-                sel = residual_row(a, bx, by, bz, wx, wy, wz, pl, J, h, res);
-                cnt = sel ? 1.0 : 0.0;
-            }
-        }
-        a.sel[i] = sel ? 1 : 0;
-    }
-    const int wid = threadIdx.x >> 6;
-    wave_reduce_store(J, h, res, cnt, red[wid]);
+    for (int q = 0; q < 32; ++q) v[q] = 0.0;
+    plane_points<PPL>(a, a.pose, blockIdx.x, v);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const double tot = wave_sum32(v, lane);
+    if (lane < 32) red[wid][wave_sum32_index(lane)] = tot;
     __syncthreads();
     publish_and_finalize(a, red);
     if (blockIdx.x == 0 && threadIdx.x == 0) *a.far_count = 0;
 }
 
-// ekfom_data.converge == false: reuse Nearest_Points / planes.  256 threads,
-// one point per lane, 4 wave partials combined in LDS.
+// ekfom_data.converge == false: reuse_points, same reduction and publish.
+template <int PPL>
 __global__ void __launch_bounds__(kBlock) h_model_reuse_kernel(MatchArgs a) {
     __shared__ double red[kBlock / 64][32];
-    const int i = blockIdx.x * kBlock + threadIdx.x;
-    double J[6] = {0, 0, 0, 0, 0, 0};
-    double h = 0.0, res = 0.0, cnt = 0.0;
-    if (i < a.n) {
-        // all three loads issued together (one round trip instead of sel -> body/plane)
-        bool sel = a.sel[i] != 0;
-        const float bx = a.body[3 * i], by = a.body[3 * i + 1], bz = a.body[3 * i + 2];
-        const float4 pl = a.planes[i];
-        if (sel) {
-            float wx, wy, wz;
-            body_to_world(a.pose, bx, by, bz, wx, wy, wz);
-            sel = residual_row(a, bx, by, bz, wx, wy, wz, pl, J, h, res);
-            cnt = sel ? 1.0 : 0.0;
-            a.sel[i] = sel ? 1 : 0;
-        }
-    }
-    const int wid = threadIdx.x >> 6;
-    wave_reduce_store(J, h, res, cnt, red[wid]);
+    double v[32];
+#pragma unroll
+    for (int q = 0; q < 32; ++q) v[q] = 0.0;
+    reuse_points<PPL>(a, a.pose, blockIdx.x, v);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const double tot = wave_sum32(v, lane);
+    if (lane < 32) red[wid][wave_sum32_index(lane)] = tot;
     __syncthreads();
     publish_and_finalize(a, red);
+}
+
+// Device-resident update (lio_ieskf_update): one h-evaluation slot of
+// the enqueued sequence.  Gate and path come from the control block: nothing
+// once the loop has finished, the plane pass when this iteration redoes the
+// kNN (ekfom_data.converge), the reuse pass otherwise.  Grid = 1 + point
+// blocks: block 0 runs the IESKF pre-step (state-only part, ieskf_dev.hpp)
+// while blocks 1.. do the points; the last block to finish (any of them) sums
+// the partials and runs the post-step, which publishes the finished update.
+template <int PPL>
+__global__ void __launch_bounds__(kBlock) h_eval_dev_kernel(MatchArgs a) {
+    IeskfCtl* g = a.ctl;
+    if (g->done) return;
+    const bool knn = g->converge != 0;
+    __shared__ double red[kBlock / 64][32];
+    __shared__ IeskfShared S;
+    const int np = (int)gridDim.x - 1;  // point blocks
+    double t;
+    bool last;
+    if (blockIdx.x == 0) {
+        if (threadIdx.x < 64) ieskf_prestep(g, S);
+        last = block_partial_last(a, red, t, -1, np, np + 1);
+    } else {
+        double v[32];
+#pragma unroll
+        for (int q = 0; q < 32; ++q) v[q] = 0.0;
+        if (knn)
+            plane_points<PPL>(a, g->pose, blockIdx.x - 1, v);
+        else
+            reuse_points<PPL>(a, g->pose, blockIdx.x - 1, v);
+        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+        const double tot = wave_sum32(v, lane);
+        if (lane < 32) red[wid][wave_sum32_index(lane)] = tot;
+        __syncthreads();
+        if (knn && blockIdx.x == 1 && threadIdx.x == 0) *a.far_count = 0;
+        last = block_partial_last(a, red, t, blockIdx.x - 1, np, np + 1);
+    }
+    if (!last || threadIdx.x >= 64) return;
+    if (threadIdx.x < 32) S.sums[threadIdx.x] = t;
+    wsync();
+    ieskf_poststep(g, S, a.ieskf_out);
+}
+
+// Device-resident update: the control block from the host-mapped input (one block).
+__global__ void __launch_bounds__(256) ieskf_init_kernel(IeskfCtl* g, const double* in, unsigned long long seq) {
+    ieskf_init(g, in, seq);
 }
 
 // Fixed-order sum of nblocks x 32 partials -> 32 sums (one block of 1024):
@@ -496,7 +609,8 @@ __global__ void __launch_bounds__(1024) h_rows_kernel(MatchArgs a, double* __res
 // ---------------------------------------------------------------- launchers
 int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* marks) {
     if (a.n == 0) return 0;
-    const int nb = (a.n + kBlock - 1) / kBlock;
+    const int ppl = ppl_setting();
+    const int nb = (a.n + kBlock * ppl - 1) / (kBlock * ppl);
     // hipExtLaunchKernelGGL with null events is a plain launch; with events (timing) the command
     // processor stamps them at the kernel's own start / end
     hipEvent_t m[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -516,13 +630,57 @@ int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* ma
             return v > 0 ? std::min(v, 4096) : kFarBlocks;
         }();
         if (a.max_shell > 1)
-            hipExtLaunchKernelGGL(knn_far_kernel, dim3(far_blocks), dim3(kFarBlock), 0, st, m[2], m[3], 0, a);
-        hipExtLaunchKernelGGL(plane_kernel, dim3(nb), dim3(kBlock), 0, st, m[4], m[5], 0, a);
+            hipExtLaunchKernelGGL(knn_far_kernel<false>, dim3(far_blocks), dim3(kFarBlock), 0, st, m[2], m[3], 0, a);
+        if (ppl == 4)
+            hipExtLaunchKernelGGL(plane_kernel<4>, dim3(nb), dim3(kBlock), 0, st, m[4], m[5], 0, a);
+        else if (ppl == 2)
+            hipExtLaunchKernelGGL(plane_kernel<2>, dim3(nb), dim3(kBlock), 0, st, m[4], m[5], 0, a);
+        else
+            hipExtLaunchKernelGGL(plane_kernel<1>, dim3(nb), dim3(kBlock), 0, st, m[4], m[5], 0, a);
         return nb;
     }
-    hipExtLaunchKernelGGL(h_model_reuse_kernel, dim3(nb), dim3(kBlock), 0, st, m[6], m[7], 0, a);
+    if (ppl == 4)
+        hipExtLaunchKernelGGL(h_model_reuse_kernel<4>, dim3(nb), dim3(kBlock), 0, st, m[6], m[7], 0, a);
+    else if (ppl == 2)
+        hipExtLaunchKernelGGL(h_model_reuse_kernel<2>, dim3(nb), dim3(kBlock), 0, st, m[6], m[7], 0, a);
+    else
+        hipExtLaunchKernelGGL(h_model_reuse_kernel<1>, dim3(nb), dim3(kBlock), 0, st, m[6], m[7], 0, a);
     return nb;
 }
+
+void launch_ieskf_dev(const MatchArgs& a, const double* in, unsigned long long seq, int max_iter, hipStream_t st,
+                      hipEvent_t* marks) {
+    const int ppl = ppl_setting();
+    const int nb = (a.n + kBlock * ppl - 1) / (kBlock * ppl);
+    const int nq = (a.n + kKnnBlock / kGroup - 1) / (kKnnBlock / kGroup);
+    static const int far_blocks = [] {
+        const char* e = std::getenv("LIO_FAR_BLOCKS");
+        const int v = e ? std::atoi(e) : 0;
+        return v > 0 ? std::min(v, 4096) : kFarBlocks;
+    }();
+    ieskf_init_kernel<<<1, 256, 0, st>>>(a.ctl, in, seq);
+    for (int e = 0; e <= max_iter; ++e) {
+        hipEvent_t* m = marks ? marks + 6 * e : nullptr;
+        hipEvent_t m0 = m ? m[0] : nullptr, m1 = m ? m[1] : nullptr, m2 = m ? m[2] : nullptr, m3 = m ? m[3] : nullptr,
+                   m4 = m ? m[4] : nullptr, m5 = m ? m[5] : nullptr;
+        // slot 0 always redoes the kNN (converge starts true); later kNN slots are seeded by the
+        // scan's previous lists against the unchanged map
+        if (e == 0)
+            hipExtLaunchKernelGGL((knn_near_kernel<false, false, 4, true>), dim3(nq), dim3(kKnnBlock), 0, st, m0, m1, 0, a);
+        else
+            hipExtLaunchKernelGGL((knn_near_kernel<false, true, 4, true>), dim3(nq), dim3(kKnnBlock), 0, st, m0, m1, 0, a);
+        if (a.max_shell > 1)
+            hipExtLaunchKernelGGL(knn_far_kernel<true>, dim3(far_blocks), dim3(kFarBlock), 0, st, m2, m3, 0, a);
+        if (ppl == 4)
+            hipExtLaunchKernelGGL(h_eval_dev_kernel<4>, dim3(nb + 1), dim3(kBlock), 0, st, m4, m5, 0, a);
+        else if (ppl == 2)
+            hipExtLaunchKernelGGL(h_eval_dev_kernel<2>, dim3(nb + 1), dim3(kBlock), 0, st, m4, m5, 0, a);
+        else
+            hipExtLaunchKernelGGL(h_eval_dev_kernel<1>, dim3(nb + 1), dim3(kBlock), 0, st, m4, m5, 0, a);
+    }
+}
+
+size_t ieskf_ctl_bytes() { return sizeof(IeskfCtl); }
 
 void launch_debug(const MatchArgs& a, float* world, float* d2, float* abcd_pd2, hipStream_t st) {
     if (a.n == 0) return;
@@ -545,7 +703,7 @@ void launch_map_knn(const GridDev& g, const float* q, int n, float bound, int ma
 }
 
 int match_blocks(int n) {  // partial slots (plane / reuse kernels)
-    return (n + kBlock - 1) / kBlock;
+    return (n + kBlock - 1) / kBlock;  // the PPL = 1 count bounds every PPL
 }
 
 }  // namespace lio

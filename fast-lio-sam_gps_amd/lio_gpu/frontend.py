@@ -315,6 +315,11 @@ class HShareModelGPU:
         check(lib().lio_map_incremental(self._h, C.byref(pose), float(filter_size_map), C.byref(st)))
         return {k: int(getattr(st, k)) for k, _ in _capi.IncrementalStats._fields_}
 
+    def set_ieskf_mode(self, device: bool):
+        """lio_ieskf_update on this context: device-resident launch sequence (True, default) or the
+        host loop with one lio_match round trip per evaluation (False)."""
+        check(lib().lio_ctx_set_ieskf_mode(self._h, 1 if device else 0))
+
     # ---- timing (HIP events on the context's stream)
     def set_timing(self, on: bool):
         check(lib().lio_ctx_set_timing(self._h, 1 if on else 0))

@@ -209,8 +209,17 @@ typedef struct lio_ieskf_stats {
 } lio_ieskf_stats;
 
 /* esekf::update_iterated_dyn_share_modified(R, solve_time) [U IKFoM];
- * x and P (23x23 row-major) are updated in place.                          */
+ * x and P (23x23 row-major) are updated in place.  Default: the host loop
+ * (one h-evaluation launch + one zero-copy result per iteration, 23-dim
+ * algebra on the host).                                                     */
 int lio_ieskf_update(lio_ctx* c, lio_state* x, double* P, const lio_ieskf_params* p, lio_ieskf_stats* st);
+/* device = 1: lio_ieskf_update runs device-resident — the whole update as one
+ * enqueued launch sequence, the 23-dim step on the GPU (pre-step in block 0 of
+ * each evaluation's last kernel, post-step in its last block), no host round
+ * trip between evaluations (solve_ms = 0; the dof < 23 branch falls back to
+ * the host loop by itself).  0: the host loop (the default: measured faster,
+ * DESIGN.md §4).  LIO_IESKF_DEVICE=0/1 sets the default process-wide.        */
+int lio_ctx_set_ieskf_mode(lio_ctx* c, int device);
 
 /* ---------------------------------------------------------------- loop ICP */
 typedef struct lio_icp lio_icp;

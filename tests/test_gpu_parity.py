@@ -384,11 +384,51 @@ def test_seeded_second_knn_bit_exact(oracle, c1, shift):
     _check_sums(g, o)
 
 
-@pytest.mark.parametrize("env", [{"LIO_FUSED_FINAL": "0"}, {"LIO_KNN_SEED": "0"}])
+@pytest.mark.parametrize("cfg", ["C1", "C2"])
+def test_ieskf_device_matches_host_loop(cfg):
+    """The device-resident update (one enqueued launch sequence, 23-dim step in the last workgroup of
+    each evaluation) against the host loop (one lio_match round trip per evaluation, host algebra) on
+    the same scans: identical evaluation / kNN counts and effective points, state and covariance
+    equal to within device-vs-host libm differences (1e-10), and the same Nearest_Points / kNN pose
+    bookkeeping afterwards (map_incremental's inputs)."""
+    _, m, scans = synth.make_config(cfg, n_scans=3)
+    trees, kfs, hms = [], [], []
+    for device in (True, False):
+        tree = F.IkdTreeGPU()
+        tree.Build(m)
+        hm = F.HShareModelGPU(tree)
+        hm.set_ieskf_mode(device)
+        trees.append(tree)
+        hms.append(hm)
+        kfs.append(F.EsekfGPU(hm))
+    for sc in scans:
+        st = synth.initial_state(sc.pos_init, sc.rot_init)
+        P0 = synth.initial_cov()
+        out = []
+        for hm, kf in zip(hms, kfs):
+            hm.set_scan(sc.body)
+            out.append(kf.update_iterated_dyn_share_modified(st, P0))
+        (xd, Pd, sd), (xh, Ph, sh) = out
+        for k in ("h_evals", "knn_calls", "converged", "n_eff"):
+            assert sd[k] == sh[k], k
+        assert sd["solve_ms"] == 0.0 and sh["solve_ms"] > 0.0  # device path really ran
+        np.testing.assert_allclose(sd["res_mean"], sh["res_mean"], rtol=1e-9)
+        for k in xd:
+            np.testing.assert_allclose(xd[k], xh[k], rtol=0, atol=1e-10, err_msg=k)
+        np.testing.assert_allclose(Pd, Ph, rtol=1e-9, atol=1e-15)
+        np.testing.assert_allclose(hms[0].last_knn_pose24(), hms[1].last_knn_pose24(), rtol=0, atol=1e-10)
+        gi0, _ = hms[0].nearest_points()
+        gi1, _ = hms[1].nearest_points()
+        np.testing.assert_array_equal(gi0, gi1)
+
+
+@pytest.mark.parametrize("env", [{"LIO_FUSED_FINAL": "0"}, {"LIO_KNN_SEED": "0"}, {"LIO_IESKF_DEVICE": "1"},
+                                 {"LIO_PPL": "2"}, {"LIO_PPL": "4"}])
 def test_ieskf_alternative_paths(env):
-    """The A/B switches keep parity: the separate finalize launch (LIO_FUSED_FINAL=0) and the
-    unseeded later kNN evaluations (LIO_KNN_SEED=0), through a whole IESKF update against the
-    oracle.  Child process: the switches are read once per process."""
+    """The A/B switches keep parity: the separate finalize launch (LIO_FUSED_FINAL=0), the
+    unseeded later kNN evaluations (LIO_KNN_SEED=0), the device-resident IESKF (LIO_IESKF_DEVICE=1) and
+    2 / 4 points per lane in the plane / reuse kernels (LIO_PPL), through a whole IESKF update
+    against the oracle.  Child process: the switches are read once per process."""
     import os
     import subprocess
     import sys
