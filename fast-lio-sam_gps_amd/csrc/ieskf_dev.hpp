@@ -63,6 +63,7 @@ constexpr int kIeskfInWords = 26 + 529 + 3;
 
 struct IeskfCtl {          // HBM, one per ctx
     PoseArg pose;          // pose of the next evaluation
+    PoseArg pose_knn;      // pose of the last kNN evaluation (seeded near pass)
     DState x, xp;          // state, propagated state
     double P[kN * kN];     // working covariance (published)
     double Pp[kN * kN];    // propagated covariance
@@ -616,6 +617,11 @@ __device__ inline void ieskf_poststep(IeskfCtl* g, IeskfShared& S, double* out) 
         ctl_st(reinterpret_cast<double*>(&g->x_last) + lane, v);
         if (conv_in) ctl_st(reinterpret_cast<double*>(&g->x_knn) + lane, v);
     }
+    if (conv_in) {  // this evaluation's pose seeds the next kNN (read before it is overwritten below)
+        constexpr int kPoseWords = (int)(sizeof(PoseArg) / sizeof(double));
+        if (lane < kPoseWords)
+            ctl_st(reinterpret_cast<double*>(&g->pose_knn) + lane, ctl_ld(reinterpret_cast<const double*>(&g->pose) + lane));
+    }
     if (lane == 0) {
         ctl_sti(&g->h_evals, ctl_ldi(&g->h_evals) + 1);
         if (conv_in) {
@@ -832,6 +838,7 @@ __device__ inline void ieskf_init(IeskfCtl* g, const double* in, unsigned long l
         double* xw = reinterpret_cast<double*>(&x);
         for (int k = 0; k < kStateWords; ++k) xw[k] = in[k];
         dv::state_pose(x, g->pose);
+        g->pose_knn = g->pose;
     }
 }
 

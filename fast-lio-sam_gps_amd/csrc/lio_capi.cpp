@@ -157,6 +157,7 @@ struct lio_ctx {
     unsigned* d_done = nullptr;  // plane/reuse block counter (last block publishes)
     float* d_far_d = nullptr;
     int* d_far_id = nullptr;
+    float* d_d5 = nullptr;  // per point: 5th neighbour d2 of the last kNN (seeds the next one)
     bool have_eval = false;
     bool knn_valid = false;
     uint64_t knn_map_version = 0;  // map version of the last kNN evaluation
@@ -509,7 +510,8 @@ int lio_ctx_destroy(lio_ctx* c) {
     (void)hipSetDevice(c->map->dev);
     (void)hipStreamSynchronize(c->map->st);
     void* ptrs[] = {c->d_body,  c->d_nn,    c->d_planes,   c->d_sel,       c->d_partials, c->d_sums,
-                    c->d_rows,  c->d_nrows, c->d_far_list, c->d_far_count, c->d_far_d,    c->d_far_id, c->d_done};
+                    c->d_rows,  c->d_nrows, c->d_far_list, c->d_far_count, c->d_far_d,    c->d_far_id, c->d_done,
+                    c->d_d5};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (c->h_sums) (void)hipHostFree(c->h_sums);
@@ -533,10 +535,10 @@ int lio_ctx_destroy(lio_ctx* c) {
 
 static int ctx_reserve(lio_ctx* c, int64_t n) {
     if (n > c->cap || !c->d_body || !c->d_nn || !c->d_planes || !c->d_sel || !c->d_far_list || !c->d_far_d ||
-        !c->d_far_id) {
+        !c->d_far_id || !c->d_d5) {
         int64_t cap = std::max<int64_t>(n, c->cap + c->cap / 2);
         c->cap = 0;  // a failed reallocation below leaves no buffer that looks usable
-        void* ptrs[] = {c->d_body, c->d_nn, c->d_planes, c->d_sel, c->d_far_list, c->d_far_d, c->d_far_id};
+        void* ptrs[] = {c->d_body, c->d_nn, c->d_planes, c->d_sel, c->d_far_list, c->d_far_d, c->d_far_id, c->d_d5};
         for (void* q : ptrs)
             if (q) (void)hipFree(q);
         c->d_body = nullptr;
@@ -546,13 +548,15 @@ static int ctx_reserve(lio_ctx* c, int64_t n) {
         c->d_far_list = nullptr;
         c->d_far_d = nullptr;
         c->d_far_id = nullptr;
+        c->d_d5 = nullptr;
         if (hipMalloc(&c->d_body, cap * 3 * sizeof(float)) != hipSuccess ||
             hipMalloc(&c->d_nn, cap * 5 * sizeof(int32_t)) != hipSuccess ||
             hipMalloc(&c->d_planes, cap * sizeof(float4)) != hipSuccess ||
             hipMalloc(&c->d_sel, cap + 64) != hipSuccess ||
             hipMalloc(&c->d_far_list, cap * sizeof(int)) != hipSuccess ||
             hipMalloc(&c->d_far_d, cap * 5 * sizeof(float)) != hipSuccess ||
-            hipMalloc(&c->d_far_id, cap * 5 * sizeof(int)) != hipSuccess)
+            hipMalloc(&c->d_far_id, cap * 5 * sizeof(int)) != hipSuccess ||
+            hipMalloc(&c->d_d5, cap * sizeof(float)) != hipSuccess)
             return fail(LIO_ERR_NOMEM, "scan buffers: hipMalloc failed");
         c->cap = cap;
     }
@@ -605,6 +609,17 @@ static lio::MatchArgs make_args(lio_ctx* c, const lio_pose& pose_in) {
     a.body = body_ptr(c);
     a.map_by_id = c->map->grid.by_id;
     a.nn_idx = c->d_nn;
+    a.nn_d5 = c->d_d5;
+    static const float seed_scale = [] {  // LIO_KNN_SEED_SCALE: diagnostics (< 1 exercises the seeded-pass guard)
+        const char* e = std::getenv("LIO_KNN_SEED_SCALE");
+        const float v = e ? (float)std::atof(e) : 1.0f;
+        return v > 0.f && v <= 1.f ? v : 1.0f;
+    }();
+    a.seed_scale = seed_scale;
+    {
+        const lio_pose pk = filled(c->knn_pose);
+        std::memcpy(&a.pose_knn, &pk, sizeof(lio::PoseArg));
+    }
     a.planes = c->d_planes;
     a.sel = c->d_sel;
     a.partials = c->d_partials;

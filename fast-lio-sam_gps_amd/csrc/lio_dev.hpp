@@ -598,41 +598,38 @@ __device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, i
     return group_knn_exact_from<K, G>(g, qx, qy, qz, 2, max_shell, sub, tk);
 }
 
-// Near pass seeded by the query's previous neighbours (the second and later
-// kNN evaluations of a scan, map unchanged since): their keys recomputed at
-// the new position bound the answer — f = the largest of the five (capped at
-// the gate) — so every lane starts with f as filler (push keeps only keys
-// < f; a previous neighbour met again with key f is represented by the filler
-// itself, the others are found again), the 27 cells of the 3x3x3 block are
-// pruned against f and scanned in ONE flat pass, and one merge gives the
-// list.  Result contract as group_knn_near (TAIL = false): true when final.
+// Near pass seeded by the query's previous kNN (the second and later kNN
+// evaluations of a scan, map unchanged since): the previous 5th-neighbour
+// distance d5 (at the previous world position w_old) and the query's
+// displacement bound the answer by the triangle inequality — every previous
+// neighbour lies within sqrt(d5) + |w - w_old| of w — so no neighbour has to be
+// re-gathered.  bound = that radius squared (plus a float-rounding margin),
+// capped at the gate; every lane starts with (bound, kNone) as filler (push
+// keeps every key with d2 <= bound), the 27 cells of the 3x3x3 block are pruned
+// against it and scanned in ONE flat pass, and one merge gives the list.  A
+// list that is not full (impossible for a valid bound, kept as a guard) is
+// reset to range fillers and returns -1: the far pass then searches the whole
+// box, the 3x3x3 block included.  Returns 1 when final, 0 when the far pass
+// must search the box outside the block (group_knn_near's false).
 template <int K, int G, int U = 4>
-__device__ bool group_knn_seeded(const GridDev& g, const float4* __restrict__ by_id, const int32_t* prev, float qx,
-                                 float qy, float qz, float range_sq, int sub, TopK<K>& tk, uint32_t* lds) {
+__device__ int group_knn_seeded(const GridDev& g, float d5prev, float wox, float woy, float woz, float qx, float qy,
+                                 float qz, float range_sq, float scale, int sub, TopK<K>& tk, uint32_t* lds) {
     static_assert(K == 5, "group_knn_seeded: K = 5");
     const int cx = cell_coord(qx, g.ox, g.inv_cell);
     const int cy = cell_coord(qy, g.oy, g.inv_cell);
     const int cz = cell_coord(qz, g.oz, g.inv_cell);
     const bool inside = (unsigned)cx < (unsigned)g.nx && (unsigned)cy < (unsigned)g.ny && (unsigned)cz < (unsigned)g.nz;
-    uint32_t b4[shell1_cpl<G>()], n4[shell1_cpl<G>()];
-    if (inside) shell1_ranges<G, true>(g, cx, cy, cz, sub, b4, n4);  // in flight with the previous neighbours
-    uint64_t f = knn_key(range_sq, kNone);
-    int32_t id[5];
-#pragma unroll
-    for (int j = 0; j < 5; ++j) id[j] = prev[j];
-    if (id[4] >= 0) {  // a full previous list (sorted: the 5th exists => all exist)
-        uint64_t mx = 0;
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            const float4 p = by_id[id[j]];
-            const uint64_t k = knn_key(sqdist3(qx, qy, qz, p.x, p.y, p.z), id[j]);
-            mx = k > mx ? k : mx;
-        }
-        f = mx < f ? mx : f;
+    float bound = range_sq;
+    if (inside && d5prev <= range_sq) {  // the previous list was full
+        const double dx = (double)qx - (double)wox, dy = (double)qy - (double)woy, dz = (double)qz - (double)woz;
+        const double r = sqrt((double)d5prev) + sqrt((dx * dx + dy * dy) + dz * dz);
+        const double b = r * r * (1.0 + 4e-6) + 1e-12;  // float d2 rounding (a few ulp) stays inside
+        if (b < (double)range_sq) bound = (float)b * (1.0f + 1.2e-7f) * scale;  // scale: 1 (< 1 tests the guard)
     }
-#pragma unroll
-    for (int j = 0; j < K; ++j) tk.k[j] = f;
-    if (!inside) return false;  // the far pass scans the whole box from the filler list
+    tk.init(bound);
+    if (!inside) return 0;  // the far pass scans the whole box from range fillers
+    uint32_t b4[shell1_cpl<G>()], n4[shell1_cpl<G>()];
+    shell1_ranges<G, true>(g, cx, cy, cz, sub, b4, n4);
     const float cs = g.cell, m = g.margin;
     const float lox = g.ox + (float)cx * cs, loy = g.oy + (float)cy * cs, loz = g.oz + (float)cz * cs;
     float own = fminf(fminf(qx - lox, lox + cs - qx), fminf(qy - loy, loy + cs - qy));
@@ -643,8 +640,12 @@ __device__ bool group_knn_seeded(const GridDev& g, const float4* __restrict__ by
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     scan_table_strided<K, U>(g, qx, qy, qz, lds, T, (uint32_t)sub, (uint32_t)G, tk);
     group_merge<K, G>(tk);
+    if (tk.id(K - 1) == kNone && bound < range_sq) {  // guard: not full under a finite bound
+        tk.init(range_sq);
+        return -1;
+    }
     const float gr = own + cs;
-    return gr > 0.f && tk.worst() < gr * gr * 0.999999f;
+    return (gr > 0.f && tk.worst() < gr * gr * 0.999999f) ? 1 : 0;
 }
 
 // Far pass with a whole block (NT lanes) per query: the box cells outside
@@ -659,7 +660,7 @@ __device__ bool group_knn_seeded(const GridDev& g, const float4* __restrict__ by
 // by all NT threads of the block (it synchronises the block).
 template <int K, int NT>
 __device__ void block_knn_box_flat(const GridDev& g, float qx, float qy, float qz, uint32_t* s_b, uint32_t* s_off,
-                                   uint32_t* s_w, uint64_t* s_lists, TopK<K>& tk) {
+                                   uint32_t* s_w, uint64_t* s_lists, TopK<K>& tk, bool whole = false) {
     static_assert(NT % 64 == 0 && NT <= 1024, "block_knn_box_flat: NT = multiple of 64");
     constexpr int NW = NT / 64;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -667,7 +668,9 @@ __device__ void block_knn_box_flat(const GridDev& g, float qx, float qy, float q
     const int cy = cell_coord(qy, g.oy, g.inv_cell);
     const int cz = cell_coord(qz, g.oz, g.inv_cell);
     // the near pass covered the 3x3x3 block only for queries whose cell lies in the grid
-    const bool near_done = (unsigned)cx < (unsigned)g.nx && (unsigned)cy < (unsigned)g.ny && (unsigned)cz < (unsigned)g.nz;
+    // (whole: the near pass left the block unfinished, scan it too)
+    const bool near_done = !whole && (unsigned)cx < (unsigned)g.nx && (unsigned)cy < (unsigned)g.ny &&
+                           (unsigned)cz < (unsigned)g.nz;
     const float r = sqrtf(tk.worst()) + 2.f * g.margin;
     const int x0 = max(cell_coord(qx - r, g.ox, g.inv_cell), 0), x1 = min(cell_coord(qx + r, g.ox, g.inv_cell), g.nx - 1);
     const int y0 = max(cell_coord(qy - r, g.oy, g.inv_cell), 0), y1 = min(cell_coord(qy + r, g.oy, g.inv_cell), g.ny - 1);

@@ -15,6 +15,7 @@ struct MatchArgs {
     const float* body;        // n*3 feats_down_body
     const float4* map_by_id;  // map points in id order (neighbour coordinates)
     int32_t* nn_idx;          // n*5 Nearest_Points ids
+    float* nn_d5;             // n: 5th neighbour d2 of the last kNN (+inf when fewer than 5; seeds the next one)
     float4* planes;           // n plane (a,b,c,d) cache
     uint8_t* sel;             // n point_selected_surf
     double* partials;         // nblocks*32
@@ -36,6 +37,8 @@ struct MatchArgs {
     float plane_thr;
     double s_coef;
     double s_gate;
+    PoseArg pose_knn;         // pose of the previous kNN evaluation (seeded near pass: w_old)
+    float seed_scale;         // seeded bound factor: 1 (LIO_KNN_SEED_SCALE < 1 forces the not-full guard: tests)
     IeskfCtl* ctl;            // device-resident update: control block (state, pose, loop flags); else null
     double* ieskf_out;        // device-resident update: host-mapped result (ieskf_dev.hpp layout)
 };

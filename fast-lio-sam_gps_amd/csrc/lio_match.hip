@@ -83,12 +83,18 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
     TopK<5> tk;
     tk.init(a.range_sq);
     SearchStats st{0, 0, 0};
-    bool done;
-    if constexpr (SEEDED)  // nn_idx holds this scan's previous lists against the same map
-        done = group_knn_seeded<5, G, U>(a.grid, a.map_by_id, a.nn_idx + 5 * (size_t)i, wx, wy, wz, a.range_sq, sub, tk,
-                                      s_tab[threadIdx.x / G]);
-    else
+    bool done, whole = false;
+    if constexpr (SEEDED) {  // this scan's previous kNN against the same map: the triangle bound (no re-gathers)
+        const PoseArg& pk = DEV ? a.ctl->pose_knn : a.pose_knn;
+        float wox, woy, woz;
+        body_to_world(pk, bx, by, bz, wox, woy, woz);
+        const int r = group_knn_seeded<5, G, U>(a.grid, a.nn_d5[i], wox, woy, woz, wx, wy, wz, a.range_sq, a.seed_scale, sub, tk,
+                                                s_tab[threadIdx.x / G]);
+        done = r > 0;
+        whole = r < 0;
+    } else {
         done = group_knn_near<5, G, false, U>(a.grid, wx, wy, wz, 1, sub, tk, DBG ? &st : nullptr, s_tab[threadIdx.x / G]);
+    }
     const bool far = !done && a.max_shell > 1;
     if constexpr (DBG) {
 #pragma unroll
@@ -105,7 +111,7 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
     if (far) {
         if (sub == 0) {
             const int slot = atomicAdd(a.far_count, 1);
-            a.far_list[slot] = i;
+            a.far_list[slot] = whole ? (int)((unsigned)i | 0x80000000u) : i;  // sign bit: search the block too
 #pragma unroll
             for (int j = 0; j < 5; ++j) {
                 a.far_d[5 * (size_t)slot + j] = tk.d(j);
@@ -130,6 +136,7 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
             a.nn_idx[5 * (size_t)i + jj] = v == kNone ? -1 : v;
         }
     }
+    if (sub == 5) a.nn_d5[i] = tk.id(4) == kNone ? INFINITY : tk.d(4);
     if (a.tdbg && (threadIdx.x & 63) == 0) {
         const size_t wv = (size_t)blockIdx.x * (kKnnBlock / 64) + (threadIdx.x >> 6);
         a.tdbg[2 * wv] = t_beg;
@@ -149,16 +156,19 @@ __global__ void __launch_bounds__(kFarBlock) knn_far_kernel(MatchArgs a) {
     __shared__ uint64_t s_lists[(kFarBlock / 64) * 5];
     const int cnt = *a.far_count;
     for (int f = blockIdx.x; f < cnt; f += gridDim.x) {
-        const int i = a.far_list[f];
+        const int e = a.far_list[f];
+        const int i = e & 0x7fffffff;
         float wx, wy, wz;
         body_to_world(ps, a.body[3 * i], a.body[3 * i + 1], a.body[3 * i + 2], wx, wy, wz);
         TopK<5> tk;
 #pragma unroll
         for (int j = 0; j < 5; ++j) tk.k[j] = knn_key(a.far_d[5 * (size_t)f + j], a.far_id[5 * (size_t)f + j]);
-        block_knn_box_flat<5, kFarBlock>(a.grid, wx, wy, wz, s_b, s_off, s_w, s_lists, tk);
-        if (threadIdx.x == 0)
+        block_knn_box_flat<5, kFarBlock>(a.grid, wx, wy, wz, s_b, s_off, s_w, s_lists, tk, e < 0);
+        if (threadIdx.x == 0) {
 #pragma unroll
             for (int j = 0; j < 5; ++j) a.nn_idx[5 * (size_t)i + j] = tk.id(j) == kNone ? -1 : tk.id(j);
+            a.nn_d5[i] = tk.id(4) == kNone ? INFINITY : tk.d(4);
+        }
     }
 }
 

@@ -29,17 +29,19 @@ for name, d in per.items():
     kern[short]["dispatches"] = max(len(v) for v in d.values())
 
 
-def bytes_of(k):
-    d = kern.get(k, {})
-    return 1024.0 * (2.0 * d.get("FETCH_SIZE", 0.0) + d.get("WRITE_SIZE", 0.0))
+def bytes_of(prefix):
+    """per-dispatch bytes of the kernel(s) whose short name starts with prefix (template
+    instantiations such as plane_kernel<2>, knn_far_kernel<false>), weighted by dispatches"""
+    ks = [k for k in kern if k.split("<")[0] == prefix]
+    n = sum(kern[k]["dispatches"] for k in ks)
+    tot = sum(1024.0 * (2.0 * kern[k].get("FETCH_SIZE", 0.0) + kern[k].get("WRITE_SIZE", 0.0)) * kern[k]["dispatches"]
+              for k in ks)
+    return tot / max(n, 1)
 
 
-near = [k for k in kern if k.startswith("knn_near_kernel")]
 # one near pass per kNN evaluation: its instantiations (first / seeded later evaluations) are
 # averaged, weighted by their dispatch counts
-nd = sum(kern[k]["dispatches"] for k in near)
-near_bytes = sum(bytes_of(k) * kern[k]["dispatches"] for k in near) / max(nd, 1)
-total = near_bytes + sum(bytes_of(k) for k in ["knn_far_kernel", "plane_kernel"])
+total = sum(bytes_of(k) for k in ["knn_near_kernel", "knn_far_kernel", "plane_kernel"])
 res = {"config": cfg, "knn_hbm_bytes_per_launch": round(total),
        "reuse_hbm_bytes_per_launch": round(bytes_of("h_model_reuse_kernel")),
        "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes, --kernel-trace only); "

@@ -360,8 +360,8 @@ def test_bind_scan_device_matches_copy(c1):
 
 @pytest.mark.parametrize("shift", [0.02, 0.3, 3.0])
 def test_seeded_second_knn_bit_exact(oracle, c1, shift):
-    """A later kNN evaluation of the same scan (map unchanged) starts from the previous
-    neighbours' recomputed 5th key (group_knn_seeded): still the oracle's lists, bit-exact,
+    """A later kNN evaluation of the same scan (map unchanged) starts from the triangle bound
+    sqrt(previous d5) + displacement (group_knn_seeded): still the oracle's lists, bit-exact,
     for a small, a medium and a large pose change between the evaluations."""
     _, m, scans = c1
     sc = scans[0]
@@ -382,6 +382,41 @@ def test_seeded_second_knn_bit_exact(oracle, c1, shift):
     oi, od = om.knn(oracle.body_to_world(p24, sc.body), 5, 5.0)
     np.testing.assert_array_equal(gd, od)
     _check_sums(g, o)
+
+
+@pytest.mark.parametrize("scale", ["0.05", "0.5"])
+def test_seeded_guard_whole_box(scale):
+    """The seeded pass's guard: a bound shrunk below the true 5th distance (LIO_KNN_SEED_SCALE)
+    leaves lists that are not full; they are reset and the far pass searches the whole box, 3x3x3
+    block included — the lists stay bit-exact.  Child process (the switch is read once)."""
+    import os
+    import subprocess
+    import sys
+
+    code = r'''
+import sys, numpy as np
+sys.path[:0] = [r"%s", r"%s"]
+import oracle_py as O
+from lio_gpu import frontend as F, synth
+scene, m, scans = synth.make_config("C1", n_scans=1)
+sc = scans[0]
+om = O.OracleMap(m)
+tree = F.IkdTreeGPU(); tree.Build(m)
+hm = F.HShareModelGPU(tree); hm.set_scan(sc.body)
+st = synth.initial_state(sc.pos_init, sc.rot_init)
+hm(synth.pose24(st), converge=True)
+for shift in (0.02, 0.3):
+    st2 = dict(st); st2["pos"] = np.asarray(st["pos"]) + np.array([shift, -0.5 * shift, 0.25 * shift])
+    p24 = synth.pose24(st2)
+    hm(p24, converge=True)
+    gi, gd = hm.nearest_points()
+    oi, od = om.knn(O.body_to_world(p24, sc.body), 5, 5.0)
+    assert np.array_equal(gi, oi) and np.array_equal(gd, od)
+print("ok")
+''' % (os.path.join(os.path.dirname(__file__), "..", "fast-lio-sam_gps_amd"), os.path.dirname(__file__))
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, LIO_KNN_SEED_SCALE=scale),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
 
 
 @pytest.mark.parametrize("cfg", ["C1", "C2"])
