@@ -76,6 +76,17 @@ struct IeskfCtl {          // HBM, one per ctx
     unsigned long long seq;
 };
 
+// Host-mapped gate of a queued evaluation (launch_h_model_gated): the host writes the poses and
+// the command, then the sequence number the gate kernel waits for.
+struct GateIn {
+    unsigned long long seq;  // alone on its cache line: the only word the gate polls
+    unsigned long long pad0[15];
+    unsigned long long cmd;  // 1 run, 2 cancel
+    unsigned long long pad1[15];
+    PoseArg pose;            // the evaluation's pose
+    PoseArg pose_knn;        // the last kNN evaluation's pose (seeded near pass)
+};
+
 struct IeskfShared {  // the step's LDS
     double P[kN * kN];
     double L[kN * kN];

@@ -181,6 +181,14 @@ struct lio_ctx {
     double* h_iout_dev = nullptr;
     hipEvent_t ev_slots[6 * 8] = {};  // timing: near / far / slot kernel start-stop per slot
     int ieskf_device = -1;            // lio_ctx_set_ieskf_mode: 1 device-resident, 0 host loop, -1 env / default (host)
+    // the host loop's next evaluation, queued behind a gate before the host knows its pose
+    lio::GateIn* h_gate = nullptr;    // host-mapped
+    lio::GateIn* h_gate_dev = nullptr;
+    unsigned long long gate_seq = 0;
+    // queued evaluations in stream order: kind (kNN?), result sequence number, gate sequence number
+    int n_pend = 0, pend_head = 0;
+    bool pend_knn[8] = {};
+    unsigned long long pend_seq[8] = {}, pend_gate[8] = {};
 };
 
 extern "C" {
@@ -505,9 +513,12 @@ int lio_ctx_create(lio_map* m, const lio_match_params* p, lio_ctx** out) {
     return LIO_OK;
 }
 
+static void cancel_pending(lio_ctx* c);
+
 int lio_ctx_destroy(lio_ctx* c) {
     if (!c) return LIO_OK;
     (void)hipSetDevice(c->map->dev);
+    cancel_pending(c);
     (void)hipStreamSynchronize(c->map->st);
     void* ptrs[] = {c->d_body,  c->d_nn,    c->d_planes,   c->d_sel,       c->d_partials, c->d_sums,
                     c->d_rows,  c->d_nrows, c->d_far_list, c->d_far_count, c->d_far_d,    c->d_far_id, c->d_done,
@@ -526,6 +537,7 @@ int lio_ctx_destroy(lio_ctx* c) {
         if (q) (void)hipFree(q);
     for (double* q : {c->h_iin, c->h_iout})
         if (q) (void)hipHostFree(q);
+    if (c->h_gate) (void)hipHostFree(c->h_gate);
     for (hipEvent_t e : c->ev_slots)
         if (e) (void)hipEventDestroy(e);
     --c->map->n_ctx;
@@ -694,8 +706,102 @@ static int wait_result(lio_ctx* c, unsigned long long seq, double* sums) {
     }
 }
 
+// ---- queued evaluations (host loop of lio_ieskf_update, opt-in LIO_QUEUE_NEXT=1) ---
+// While the first evaluation of an update runs, the evaluations the loop will ask for if no later
+// step converges (IESKF hint chain) are queued, each behind a one-wave gate kernel; once the host
+// has done the algebra it publishes the pose and a run command with one store sequence (no launch
+// on the critical path: 1.9 us instead of 5.8 us from the decision to the kernel start,
+// scripts/micro/wait_value.hip).  A mispredicted evaluation cancels the rest of the chain (their
+// kernels exit at once) and the right one is launched normally.  Measured: the gaps between
+// dependent evaluations drop from 8.5 to 6.3 us, but scans/s end 2-4 % lower (more launches per
+// scan, host time per scan up), so it is off by default.
+static bool gating_enabled() {
+    static const bool v = [] {  // LIO_QUEUE_NEXT=1: queued evaluations (opt-in: measured 2-4 % slower)
+        const char* e = std::getenv("LIO_QUEUE_NEXT");
+        return e ? std::atoi(e) != 0 : false;
+    }();
+    return v;
+}
+
+static int ensure_gate(lio_ctx* c) {
+    if (!c->d_ctl) {
+        if (hipMalloc(&c->d_ctl, lio::ieskf_ctl_bytes()) != hipSuccess) {
+            c->d_ctl = nullptr;
+            return -1;
+        }
+    }
+    if (!c->h_gate) {
+        if (hipHostMalloc(&c->h_gate, sizeof(lio::GateIn), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+            hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_gate_dev), c->h_gate, 0) != hipSuccess) {
+            if (c->h_gate) (void)hipHostFree(c->h_gate);
+            c->h_gate = nullptr;
+            return -1;
+        }
+        std::memset(c->h_gate, 0, sizeof(lio::GateIn));
+    }
+    return 0;
+}
+
+static void gate_publish(lio_ctx* c, const lio_pose* pose, unsigned long long cmd, unsigned long long gseq) {
+    lio::GateIn* gi = c->h_gate;
+    if (pose) {
+        const lio_pose pf = filled(*pose), pk = filled(c->knn_pose);
+        std::memcpy(&gi->pose, &pf, sizeof(lio::PoseArg));
+        std::memcpy(&gi->pose_knn, &pk, sizeof(lio::PoseArg));
+    }
+    gi->cmd = cmd;
+    std::atomic_thread_fence(std::memory_order_release);  // pose and command before the sequence number
+    reinterpret_cast<volatile unsigned long long*>(&gi->seq)[0] = gseq;
+}
+
+// every queued evaluation exits without work (their gates all see seq >= theirs and cmd = cancel)
+static void cancel_pending(lio_ctx* c) {
+    if (c->n_pend == 0) return;
+    gate_publish(c, nullptr, 2, c->pend_gate[c->pend_head + c->n_pend - 1]);
+    c->n_pend = 0;
+    c->pend_head = 0;
+}
+
+// Queue the predicted evaluations (kinds[k]: 1 reuse, 2 kNN) behind gates, in order; cur_knn: the
+// evaluation just launched redoes the kNN (a queued kNN evaluation is then seeded by it).  Each is
+// a gate + its first kernel (kNN: the near pass; its far + plane passes follow at release).
+static void queue_chain(lio_ctx* c, const int* kinds, int n, bool cur_knn) {
+    if (n <= 0 || c->n_pend > 0 || c->timing || !gating_enabled() || c->n == 0 || c->map->n == 0) return;
+    if (ensure_gate(c)) return;  // no gate memory: evaluations are launched after the decision
+    lio::MatchArgs a = make_args(c, c->last_pose);
+    if (!a.fused_final) return;  // LIO_FUSED_FINAL=0: the sums need the finalize launch after the decision
+    a.ctl = c->d_ctl;
+    static const bool seed_ok = [] {
+        const char* e = std::getenv("LIO_KNN_SEED");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    bool knn_before = cur_knn || (c->knn_valid && c->knn_map_version == c->map->version);
+    n = std::min(n, 8);
+    for (int k = 0; k < n; ++k) {
+        const bool knn = kinds[k] == 2;
+        a.prior = (knn && seed_ok && knn_before) ? 1 : 0;
+        a.seq = ++c->seq;
+        ++c->gate_seq;
+        lio::launch_h_model_gated(a, knn, c->h_gate_dev, c->gate_seq, c->map->st);
+        if (hipGetLastError() != hipSuccess) break;  // the ones queued so far stay valid
+        c->pend_knn[k] = knn;
+        c->pend_seq[k] = a.seq;
+        c->pend_gate[k] = c->gate_seq;
+        c->n_pend = k + 1;
+        knn_before = knn_before || knn;
+    }
+    c->pend_head = 0;
+}
+
+static int match_impl(lio_ctx* c, const lio_pose* pose_in, int redo_knn, double* sums, const int* next, int n_next);
+
 int lio_match(lio_ctx* c, const lio_pose* pose_in, int redo_knn, double* sums) {
     if (!c || !pose_in || !sums) return fail(LIO_ERR_ARG, "lio_match: bad arguments");
+    cancel_pending(c);
+    return match_impl(c, pose_in, redo_knn, sums, nullptr, 0);
+}
+
+static int match_impl(lio_ctx* c, const lio_pose* pose_in, int redo_knn, double* sums, const int* next, int n_next) {
     const lio_pose pose_f = filled(*pose_in);
     const lio_pose* pose = &pose_f;
     if (c->map->grid.n_ids == 0) return fail(LIO_ERR_STATE, "lio_match: map is empty (call lio_map_build)");
@@ -737,15 +843,37 @@ int lio_match(lio_ctx* c, const lio_pose* pose_in, int redo_knn, double* sums) {
         a.tdbg = d_t;
     }
     const auto t0 = std::chrono::steady_clock::now();
-    if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.a, st));
-    const int nb = lio::launch_h_model(a, redo_knn != 0, st, c->timing ? c->ev_marks : nullptr);
-    if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.b, st));
-    lio::launch_finalize(a, nb, st);  // no-op: the last plane/reuse block publishes the sums
-    if (c->timing) HIP_TRY(hipEventRecord(c->ev_fin.b, st));
-    HIP_TRY(hipGetLastError());
+    bool queued = false;
+    if (c->n_pend > 0) {  // the evaluation queued for this call: release it, or cancel a misprediction
+        const int h = c->pend_head;
+        if (c->pend_knn[h] == (redo_knn != 0) && !tdir && !c->timing) {
+            --c->seq;  // the sequence number reserved above is not used
+            a.seq = c->pend_seq[h];
+            gate_publish(c, pose, 1, c->pend_gate[h]);
+            ++c->pend_head;
+            --c->n_pend;
+            queued = true;
+            if (redo_knn) lio::launch_knn_tail(a, st);  // far + plane behind the released near pass
+            HIP_TRY(hipGetLastError());
+        } else {
+            cancel_pending(c);
+        }
+    }
+    if (!queued) {
+        if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.a, st));
+        const int nb = lio::launch_h_model(a, redo_knn != 0, st, c->timing ? c->ev_marks : nullptr);
+        if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.b, st));
+        lio::launch_finalize(a, nb, st);  // no-op: the last plane/reuse block publishes the sums
+        if (c->timing) HIP_TRY(hipEventRecord(c->ev_fin.b, st));
+        HIP_TRY(hipGetLastError());
+    }
+    if (c->n_pend == 0 && next) queue_chain(c, next, n_next, redo_knn != 0);  // while this one runs
     const auto t1 = std::chrono::steady_clock::now();
     int rc = wait_result(c, a.seq, sums);
-    if (rc) return rc;
+    if (rc) {
+        cancel_pending(c);
+        return rc;
+    }
     const auto t2 = std::chrono::steady_clock::now();
     if (d_t) {
         std::vector<unsigned long long> h(nwaves * 2);
@@ -1124,6 +1252,7 @@ int lio_ieskf_update(lio_ctx* c, lio_state* xs, double* P, const lio_ieskf_param
     double launch_ms = 0.0, wait_ms = 0.0;
     auto hfn = [&](const lio::host::State& s, bool redo, bool want_rows, lio::host::HModel& hm) -> int {
         if (want_rows) {
+            cancel_pending(c);
             const int64_t want = (int64_t)hm.sums[LIO_SUMS_NEFF];
             hm.rows.assign((size_t)std::max<int64_t>(want, 1) * 7, 0.0);
             int64_t nr = 0;
@@ -1135,7 +1264,7 @@ int lio_ieskf_update(lio_ctx* c, lio_state* xs, double* P, const lio_ieskf_param
         const lio_pose pose = state_pose(s);
         hm.rows.clear();
         c->last_launch_ms = c->last_wait_ms = 0.0;
-        int rc = lio_match(c, &pose, redo ? 1 : 0, hm.sums);
+        int rc = match_impl(c, &pose, redo ? 1 : 0, hm.sums, hm.next, hm.n_next);
         if (rc) return err = rc;
         launch_ms += c->last_launch_ms;
         wait_ms += c->last_wait_ms;
@@ -1143,6 +1272,7 @@ int lio_ieskf_update(lio_ctx* c, lio_state* xs, double* P, const lio_ieskf_param
     };
     lio::host::IeskfResult r;
     int rc = lio::host::update_iterated(x, Pm, pp.laser_point_cov, pp.max_iteration, pp.epsi, hfn, r);
+    cancel_pending(c);  // a queued evaluation the loop did not ask for (it converged early)
     if (rc) return err ? err : fail(LIO_ERR_STATE, "IESKF: singular matrix");
     from_host(x, *xs);
     std::memcpy(P, Pm.data(), sizeof(double) * LIO_STATE_DIM * LIO_STATE_DIM);

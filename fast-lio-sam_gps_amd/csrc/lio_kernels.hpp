@@ -8,6 +8,7 @@
 namespace lio {
 
 struct IeskfCtl;  // ieskf_dev.hpp
+struct GateIn;
 
 struct MatchArgs {
     PoseArg pose;
@@ -47,6 +48,13 @@ struct MatchArgs {
 // marks (optional, timing): 8 events, start / stop of near, far, plane (redo) or reuse (marks[6..7]),
 // recorded by hipExtLaunchKernel at each kernel's own start and end
 int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* marks = nullptr);
+// An h-evaluation queued before the host knows its pose (lio_ieskf_update's host loop):
+// a one-wave gate kernel waits for `in->seq >= gate_seq` (host-mapped), copies the pose / command into
+// a.ctl, and the kernel behind it (kNN: the near pass; reuse: the reuse pass) reads its pose from a.ctl
+// (a cancelled one exits).  A released kNN evaluation's far + plane passes follow with launch_knn_tail
+// (their launch hides behind the near pass).
+void launch_h_model_gated(const MatchArgs& a, bool redo, const GateIn* in, unsigned long long gate_seq, hipStream_t st);
+int launch_knn_tail(const MatchArgs& a, hipStream_t st);
 // Device-resident lio_ieskf_update: the init kernel (reads `in`, host-mapped, kIeskfInWords doubles)
 // and max_iter + 1 evaluation slots (near, far, plane-or-reuse + IESKF step), enqueued on st without
 // a host round trip.  marks (optional, timing): 6 events per slot, start / stop of near, far, slot kernel.

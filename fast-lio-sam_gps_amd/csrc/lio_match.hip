@@ -398,13 +398,18 @@ __device__ __forceinline__ void reuse_points(const MatchArgs& a, const PoseArg& 
 // Pass 3 (kNN evaluations): plane_points, wave sums, 4 wave partials combined in
 // LDS -> block partial; the last block publishes.  Resets the far queue for the
 // next kNN evaluation.
-template <int PPL>
+// GATED: queued ahead of the host's decision (launch_h_model_gated): the pose comes from the control
+// block the gate kernel fills, and a cancelled evaluation (ctl->done) does nothing.
+template <int PPL, bool GATED = false>
 __global__ void __launch_bounds__(kBlock) plane_kernel(MatchArgs a) {
+    if constexpr (GATED)
+        if (a.ctl->done) return;
+    const PoseArg& ps = GATED ? a.ctl->pose : a.pose;
     __shared__ double red[kBlock / 64][32];
     double v[32];
 #pragma unroll
     for (int q = 0; q < 32; ++q) v[q] = 0.0;
-    plane_points<PPL>(a, a.pose, blockIdx.x, v);
+    plane_points<PPL>(a, ps, blockIdx.x, v);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const double tot = wave_sum32(v, lane);
     if (lane < 32) red[wid][wave_sum32_index(lane)] = tot;
@@ -414,13 +419,16 @@ __global__ void __launch_bounds__(kBlock) plane_kernel(MatchArgs a) {
 }
 
 // ekfom_data.converge == false: reuse_points, same reduction and publish.
-template <int PPL>
+template <int PPL, bool GATED = false>
 __global__ void __launch_bounds__(kBlock) h_model_reuse_kernel(MatchArgs a) {
+    if constexpr (GATED)
+        if (a.ctl->done) return;
+    const PoseArg& ps = GATED ? a.ctl->pose : a.pose;
     __shared__ double red[kBlock / 64][32];
     double v[32];
 #pragma unroll
     for (int q = 0; q < 32; ++q) v[q] = 0.0;
-    reuse_points<PPL>(a, a.pose, blockIdx.x, v);
+    reuse_points<PPL>(a, ps, blockIdx.x, v);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const double tot = wave_sum32(v, lane);
     if (lane < 32) red[wid][wave_sum32_index(lane)] = tot;
@@ -467,6 +475,51 @@ __global__ void __launch_bounds__(kBlock) h_eval_dev_kernel(MatchArgs a) {
     if (threadIdx.x < 32) S.sums[threadIdx.x] = t;
     wsync();
     ieskf_poststep(g, S, a.ieskf_out);
+}
+
+// Gate of an evaluation queued before the host's decision (launch_h_model_gated): one lane
+// waits for the host to publish gate word `seq` (host-mapped, written after the pose) and copies
+// the command and the poses into the control block, which the evaluation's kernels behind it read
+// (DEV near / far, GATED plane / reuse).  Command: 1 run, 2 cancel.  The wait is bounded (20 ms,
+// then cancel), so a host that never answers cannot hold the queue.
+__global__ void __launch_bounds__(64) eval_gate_kernel(IeskfCtl* g, const GateIn* in, unsigned long long seq, int knn) {
+    typedef __attribute__((address_space(1))) const unsigned long long cgull;
+    typedef __attribute__((address_space(1))) const double cgdouble;
+    const int lane = threadIdx.x;
+    int ok = 0;
+    if (lane == 0) {  // one lane polls (relaxed, uncached system-scope loads: an acquire would
+                      // invalidate the L2 on every poll); the others wait at the reconvergence point
+        const unsigned long long t0 = wall_clock64();
+        for (;;) {
+            if (__hip_atomic_load((cgull*)&in->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= seq) {
+                ok = 1;
+                break;
+            }
+            if (wall_clock64() - t0 > 2000000ull) break;  // 100 MHz constant clock: 20 ms
+            __builtin_amdgcn_s_sleep(8);  // ~0.2 us between PCIe polls
+        }
+    }
+    ok = __shfl(ok, 0, 64);
+    unsigned long long cmd = 2;
+    if (ok && lane == 0) cmd = __hip_atomic_load((cgull*)&in->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    cmd = __shfl(cmd, 0, 64);
+    if (cmd == 1) {
+        // the two poses (2 x 32 words) in ONE round trip: a word per lane, issued after seq was seen
+        // (the host wrote them before seq)
+        constexpr int W = (int)(sizeof(PoseArg) / sizeof(double));
+        static_assert(2 * W <= 64, "eval_gate_kernel: a pose word per lane");
+        if (lane < 2 * W && (knn || lane < W)) {
+            const double* src = lane < W ? reinterpret_cast<const double*>(&in->pose) + lane
+                                         : reinterpret_cast<const double*>(&in->pose_knn) + (lane - W);
+            double* dst = lane < W ? reinterpret_cast<double*>(&g->pose) + lane
+                                   : reinterpret_cast<double*>(&g->pose_knn) + (lane - W);
+            *dst = __hip_atomic_load((cgdouble*)src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
+    if (lane == 0) {
+        g->converge = knn;
+        g->done = cmd == 1 ? 0 : 1;
+    }
 }
 
 // Device-resident update: the control block from the host-mapped input (one block).
@@ -655,6 +708,41 @@ int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* ma
         hipExtLaunchKernelGGL(h_model_reuse_kernel<2>, dim3(nb), dim3(kBlock), 0, st, m[6], m[7], 0, a);
     else
         hipExtLaunchKernelGGL(h_model_reuse_kernel<1>, dim3(nb), dim3(kBlock), 0, st, m[6], m[7], 0, a);
+    return nb;
+}
+
+void launch_h_model_gated(const MatchArgs& a, bool redo, const GateIn* in, unsigned long long gate_seq, hipStream_t st) {
+    if (a.n == 0) return;
+    const int ppl = ppl_setting();
+    const int nb = (a.n + kBlock * ppl - 1) / (kBlock * ppl);
+    eval_gate_kernel<<<1, 64, 0, st>>>(a.ctl, in, gate_seq, redo ? 1 : 0);
+    if (redo) {  // only the near pass: far + plane are launched at release (launch_knn_tail), hidden behind it
+        const int nq = (a.n + kKnnBlock / kGroup - 1) / (kKnnBlock / kGroup);
+        if (a.prior)
+            knn_near_kernel<false, true, 4, true><<<nq, kKnnBlock, 0, st>>>(a);
+        else
+            knn_near_kernel<false, false, 4, true><<<nq, kKnnBlock, 0, st>>>(a);
+        return;
+    }
+    if (ppl == 4)
+        h_model_reuse_kernel<4, true><<<nb, kBlock, 0, st>>>(a);
+    else if (ppl == 2)
+        h_model_reuse_kernel<2, true><<<nb, kBlock, 0, st>>>(a);
+    else
+        h_model_reuse_kernel<1, true><<<nb, kBlock, 0, st>>>(a);
+}
+
+int launch_knn_tail(const MatchArgs& a, hipStream_t st) {
+    if (a.n == 0) return 0;
+    const int ppl = ppl_setting();
+    const int nb = (a.n + kBlock * ppl - 1) / (kBlock * ppl);
+    if (a.max_shell > 1) knn_far_kernel<false><<<kFarBlocks, kFarBlock, 0, st>>>(a);
+    if (ppl == 4)
+        plane_kernel<4, false><<<nb, kBlock, 0, st>>>(a);
+    else if (ppl == 2)
+        plane_kernel<2, false><<<nb, kBlock, 0, st>>>(a);
+    else
+        plane_kernel<1, false><<<nb, kBlock, 0, st>>>(a);
     return nb;
 }
 

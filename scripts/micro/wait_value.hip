@@ -30,6 +30,11 @@ __global__ void k_spin_flag(const unsigned long long* in, unsigned long long* ou
     }
 }
 
+__global__ void k_busy(unsigned long long ticks) {  // one wave busy for `ticks` of the 100 MHz clock
+    const unsigned long long t0 = wall_clock64();
+    while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(1);
+}
+
 static void report(const char* name, std::vector<double>& v) {
     std::sort(v.begin(), v.end());
     std::printf("%-44s median %7.2f us  p10 %7.2f  p90 %7.2f  (n=%zu)\n", name, v[v.size() / 2], v[v.size() / 10],
@@ -90,8 +95,48 @@ int main() {
         if (it > 100) vc.push_back(us(t0, clk::now()));
     }
     (void)hipStreamSynchronize(st);
+    // D: the host's store lands BEFORE the spinning gate starts (it is queued behind a 20 us kernel),
+    // as in lio_ieskf_update; time from the store to the gate's completion minus the busy kernel
+    std::vector<double> vd;
+    for (int it = 0; it < N; ++it) {
+        ++seq;
+        k_busy<<<1, 64, 0, st>>>(2000);  // 20 us
+        k_spin_flag<<<1, 64, 0, st>>>(din, dout, seq);
+        const auto t0 = clk::now();
+        *hin = seq;
+        while (*hout != seq) {
+        }
+        if (it > 100) vd.push_back(us(t0, clk::now()));
+    }
+    (void)hipStreamSynchronize(st);
+    // E / F: as D, but the host first writes a 576-byte payload next to the word (the gate block of
+    // lio_capi.cpp: seq, cmd, two poses), without (E) and with (F) an mfence after the word
+    unsigned long long *g, *gd;
+    (void)hipHostMalloc(&g, 1024, hipHostMallocMapped | hipHostMallocCoherent);
+    (void)hipHostGetDevicePointer((void**)&gd, g, 0);
+    std::vector<double> ve, vf;
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int it = 0; it < N; ++it) {
+            ++seq;
+            k_busy<<<1, 64, 0, st>>>(2000);
+            k_spin_flag<<<1, 64, 0, st>>>(gd, dout, seq);
+            const auto t0 = clk::now();
+            volatile double* pl = reinterpret_cast<volatile double*>(g + 2);
+            for (int k = 0; k < 72; ++k) pl[k] = (double)(seq + k);
+            reinterpret_cast<volatile unsigned long long*>(g)[1] = 1;
+            reinterpret_cast<volatile unsigned long long*>(g)[0] = seq;
+            if (pass == 1) __builtin_ia32_mfence();
+            while (*hout != seq) {
+            }
+            if (it > 100) (pass ? vf : ve).push_back(us(t0, clk::now()));
+        }
+        (void)hipStreamSynchronize(st);
+    }
     report("A launch after the decision", va);
     if (have_wait) report("B pre-enqueued behind hipStreamWaitValue64", vb);
     report("C pre-enqueued, one block spinning", vc);
+    report("D store before the gate starts (incl. 20 us busy)", vd);
+    report("E as D after a 576-B payload (incl. 20 us busy)", ve);
+    report("F as E + mfence (incl. 20 us busy)", vf);
     return 0;
 }

@@ -384,6 +384,48 @@ def test_seeded_second_knn_bit_exact(oracle, c1, shift):
     _check_sums(g, o)
 
 
+@pytest.mark.parametrize("queue", ["0", "1"])
+def test_ieskf_queued_evaluations_any_pattern(queue):
+    """LIO_QUEUE_NEXT=1: the host loop queues the evaluations it expects next behind gates before the
+    current result is in (reuse, then the kNN the loop forces).  Convergence limits and iteration caps
+    that make the loop converge early, late or never give every evaluation pattern — predictions that
+    hit, mispredictions that cancel the rest of the chain, queued evaluations left over when the loop
+    stops early — and the update still matches the oracle (counts identical, pose within 1e-5), with
+    the context usable right after.  Child process (the switch is read once)."""
+    import os
+    import subprocess
+    import sys
+
+    code = r'''
+import sys, numpy as np
+sys.path[:0] = [r"%s", r"%s"]
+import oracle_py as O
+from lio_gpu import frontend as F, synth
+scene, m, scans = synth.make_config("C1", n_scans=2)
+om = O.OracleMap(m)
+tree = F.IkdTreeGPU(); tree.Build(m)
+hm = F.HShareModelGPU(tree)
+for epsi, max_iter in [(0.001, 3), (0.05, 3), (1.0, 3), (1.0, 5), (0.001, 1), (0.02, 6)]:
+    kf = F.EsekfGPU(hm, max_iteration=max_iter, epsi=epsi)
+    for sc in scans:
+        hm.set_scan(sc.body)
+        st = synth.initial_state(sc.pos_init, sc.rot_init)
+        P0 = synth.initial_cov()
+        xg, Pg, sg = kf.update_iterated_dyn_share_modified(st, P0)
+        xo, Po, so, _ = O.ieskf_update(om, sc.body, st, P0, max_iter=max_iter, limit=epsi)
+        assert sg["h_evals"] == int(so[0]) and sg["knn_calls"] == int(so[1]) and sg["n_eff"] == int(so[3])
+        assert sg["converged"] == int(so[2])
+        assert np.allclose(xg["pos"], xo["pos"], atol=1e-5) and np.allclose(xg["rot"], xo["rot"], atol=1e-5)
+        assert np.allclose(Pg, Po, rtol=1e-5, atol=1e-10)
+        g = hm(synth.pose24(xg), converge=True)  # no queued evaluation left on the stream
+        assert g[27] > 0
+print("ok")
+''' % (os.path.join(os.path.dirname(__file__), "..", "fast-lio-sam_gps_amd"), os.path.dirname(__file__))
+    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, LIO_QUEUE_NEXT=queue), capture_output=True,
+                       text=True, timeout=300)
+    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+
+
 @pytest.mark.parametrize("scale", ["0.05", "0.5"])
 def test_seeded_guard_whole_box(scale):
     """The seeded pass's guard: a bound shrunk below the true 5th distance (LIO_KNN_SEED_SCALE)
@@ -457,7 +499,7 @@ def test_ieskf_device_matches_host_loop(cfg):
         np.testing.assert_array_equal(gi0, gi1)
 
 
-@pytest.mark.parametrize("env", [{"LIO_FUSED_FINAL": "0"}, {"LIO_KNN_SEED": "0"}, {"LIO_IESKF_DEVICE": "1"},
+@pytest.mark.parametrize("env", [{"LIO_FUSED_FINAL": "0"}, {"LIO_KNN_SEED": "0"}, {"LIO_IESKF_DEVICE": "1"}, {"LIO_QUEUE_NEXT": "1"},
                                  {"LIO_PPL": "2"}, {"LIO_PPL": "4"}])
 def test_ieskf_alternative_paths(env):
     """The A/B switches keep parity: the separate finalize launch (LIO_FUSED_FINAL=0), the
