@@ -631,6 +631,14 @@ static lio::MatchArgs make_args(lio_ctx* c, const lio_pose& pose_in) {
     {
         const lio_pose pk = filled(c->knn_pose);
         std::memcpy(&a.pose_knn, &pk, sizeof(lio::PoseArg));
+        // float affine map body -> world of that pose: [R R_LI | R t_LI + t]
+        for (int r = 0; r < 3; ++r) {
+            for (int k = 0; k < 3; ++k)
+                a.knn_M[4 * r + k] = (float)(pk.R[3 * r] * pk.R_LI[k] + pk.R[3 * r + 1] * pk.R_LI[3 + k] +
+                                             pk.R[3 * r + 2] * pk.R_LI[6 + k]);
+            a.knn_M[4 * r + 3] = (float)(pk.R[3 * r] * pk.t_LI[0] + pk.R[3 * r + 1] * pk.t_LI[1] +
+                                         pk.R[3 * r + 2] * pk.t_LI[2] + pk.t[r]);
+        }
     }
     a.planes = c->d_planes;
     a.sel = c->d_sel;

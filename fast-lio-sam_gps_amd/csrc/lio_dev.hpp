@@ -603,7 +603,8 @@ __device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, i
 // distance d5 (at the previous world position w_old) and the query's
 // displacement bound the answer by the triangle inequality — every previous
 // neighbour lies within sqrt(d5) + |w - w_old| of w — so no neighbour has to be
-// re-gathered.  bound = that radius squared (plus a float-rounding margin),
+// re-gathered.  bound = that radius squared (plus margins for float rounding and
+// for w_old from a float affine map),
 // capped at the gate; every lane starts with (bound, kNone) as filler (push
 // keeps every key with d2 <= bound), the 27 cells of the 3x3x3 block are pruned
 // against it and scanned in ONE flat pass, and one merge gives the list.  A
@@ -621,10 +622,13 @@ __device__ int group_knn_seeded(const GridDev& g, float d5prev, float wox, float
     const bool inside = (unsigned)cx < (unsigned)g.nx && (unsigned)cy < (unsigned)g.ny && (unsigned)cz < (unsigned)g.nz;
     float bound = range_sq;
     if (inside && d5prev <= range_sq) {  // the previous list was full
-        const double dx = (double)qx - (double)wox, dy = (double)qy - (double)woy, dz = (double)qz - (double)woz;
-        const double r = sqrt((double)d5prev) + sqrt((dx * dx + dy * dy) + dz * dz);
-        const double b = r * r * (1.0 + 4e-6) + 1e-12;  // float d2 rounding (a few ulp) stays inside
-        if (b < (double)range_sq) bound = (float)b * (1.0f + 1.2e-7f) * scale;  // scale: 1 (< 1 tests the guard)
+        // float throughout: w_old may come from a float affine map (~1e-5 m off at 100 m) and every
+        // step rounds, so the radius gets an absolute + relative margin and the square a relative one
+        const float dx = qx - wox, dy = qy - woy, dz = qz - woz;
+        const float eps = 1e-4f + 1e-6f * ((fabsf(qx) + fabsf(qy)) + fabsf(qz));
+        const float r = (sqrtf(d5prev) + sqrtf((dx * dx + dy * dy) + dz * dz)) + eps;
+        const float b = r * r * (1.0f + 1e-5f);
+        if (b < range_sq) bound = b * scale;  // scale: 1 (< 1 tests the guard)
     }
     tk.init(bound);
     if (!inside) return 0;  // the far pass scans the whole box from range fillers

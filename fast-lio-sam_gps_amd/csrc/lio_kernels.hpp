@@ -39,6 +39,8 @@ struct MatchArgs {
     double s_coef;
     double s_gate;
     PoseArg pose_knn;         // pose of the previous kNN evaluation (seeded near pass: w_old)
+    float knn_M[12];          // the same as one float affine map body -> world (row-major 3x4): the seeded
+                              // pass's displacement bound (error covered by a margin)
     float seed_scale;         // seeded bound factor: 1 (LIO_KNN_SEED_SCALE < 1 forces the not-full guard: tests)
     IeskfCtl* ctl;            // device-resident update: control block (state, pose, loop flags); else null
     double* ieskf_out;        // device-resident update: host-mapped result (ieskf_dev.hpp layout)

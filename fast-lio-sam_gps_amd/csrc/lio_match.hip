@@ -85,9 +85,15 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
     SearchStats st{0, 0, 0};
     bool done, whole = false;
     if constexpr (SEEDED) {  // this scan's previous kNN against the same map: the triangle bound (no re-gathers)
-        const PoseArg& pk = DEV ? a.ctl->pose_knn : a.pose_knn;
         float wox, woy, woz;
-        body_to_world(pk, bx, by, bz, wox, woy, woz);
+        if constexpr (DEV) {
+            body_to_world(a.ctl->pose_knn, bx, by, bz, wox, woy, woz);
+        } else {  // float affine map of the previous kNN pose: w_old within ~1e-5 m, covered by the bound's margin
+            const float* M = a.knn_M;
+            wox = ((M[0] * bx + M[1] * by) + M[2] * bz) + M[3];
+            woy = ((M[4] * bx + M[5] * by) + M[6] * bz) + M[7];
+            woz = ((M[8] * bx + M[9] * by) + M[10] * bz) + M[11];
+        }
         const int r = group_knn_seeded<5, G, U>(a.grid, a.nn_d5[i], wox, woy, woz, wx, wy, wz, a.range_sq, a.seed_scale, sub, tk,
                                                 s_tab[threadIdx.x / G]);
         done = r > 0;
