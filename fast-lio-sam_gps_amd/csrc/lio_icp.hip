@@ -109,10 +109,17 @@ __device__ __forceinline__ float interval_gap(float lo, float hi, float a, float
 // streamed through LDS in kTileCh chunks, wave w of the tile's NW
 // taking chunks w, w + NW, ...; every active lane keeps the minimum
 // (d2, id) key over the chunks its wave saw (merged across waves by the caller).
+//
+// Staging filter: a candidate whose squared distance to the tile's query box Q exceeds
+// every active lane's current best cannot win for any lane (each query lies in Q), so
+// it is dropped before the all-lanes test and the survivors are compacted into LDS.
+// The bound is the wave's own maximum best, refreshed per chunk (each wave's lanes
+// keep the best over the chunks that wave saw, which is all the filter needs); the
+// margin (1 - 1e-5) covers the float rounding of both the box gap and d2.
 template <int NW>  // waves per tile: the tile's candidate stream is split over them
 __device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32_t b0, uint32_t n0, uint32_t b1,
-                                            uint32_t n1, bool act, float x, float y, float z, uint64_t& best,
-                                            unsigned long long& cand) {
+                                            uint32_t n1, bool act, float x, float y, float z, const float (&qb)[6],
+                                            uint64_t& best, unsigned long long& cand, uint32_t& tested) {
     const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
     const uint32_t n = n0 + n1;
     uint32_t incl = n;
@@ -148,19 +155,37 @@ __device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32
             }
             v[u] = g.pts[sb + (t - lo)];
         }
+        // the wave's bound: its active lanes' largest best (+inf while one has none)
+        const float Bw = uni_f(wave_max_f(act ? __uint_as_float((uint32_t)(best >> 32)) : 0.f));
+        uint32_t cnt = 0;
 #pragma unroll
-        for (int u = 0; u < U; ++u) {  // slots past the stream end: +inf points with id kNone (never win)
-            const int sl2 = u * kIcpTileQ + lane;
-            const bool in = base + (uint32_t)sl2 < T;
-            L.x[sl2] = in ? v[u].x : INFINITY;
-            L.y[sl2] = in ? v[u].y : INFINITY;
-            L.z[sl2] = in ? v[u].z : INFINITY;
-            L.id[sl2] = in ? __float_as_uint(v[u].w) : (uint32_t)kNone;
+        for (int u = 0; u < U; ++u) {  // survivors compacted in stream order
+            const float gx = fmaxf(fmaxf(qb[0] - v[u].x, v[u].x - qb[1]), 0.f);
+            const float gy = fmaxf(fmaxf(qb[2] - v[u].y, v[u].y - qb[3]), 0.f);
+            const float gz = fmaxf(fmaxf(qb[4] - v[u].z, v[u].z - qb[5]), 0.f);
+            const float gap2 = (gx * gx + gy * gy) + gz * gz;
+            const bool in = base + (uint32_t)(u * kIcpTileQ + lane) < T && !(gap2 * (1.f - 1e-5f) > Bw);
+            const uint64_t m = __ballot(in);
+            const uint32_t r = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            if (in) {
+                L.x[r] = v[u].x;
+                L.y[r] = v[u].y;
+                L.z[r] = v[u].z;
+                L.id[r] = __float_as_uint(v[u].w);
+            }
+            cnt += (uint32_t)__popcll(m);
+        }
+        const int cnt4 = ((int)cnt + 3) & ~3;
+        tested += cnt;
+        if ((uint32_t)lane < (uint32_t)cnt4 - cnt) {  // pad to 4: +inf points with id kNone (never win)
+            L.x[cnt + lane] = INFINITY;
+            L.y[cnt + lane] = INFINITY;
+            L.z[cnt + lane] = INFINITY;
+            L.id[cnt + lane] = (uint32_t)kNone;
         }
         wave_sync();
         // every lane (active or not: uniform control flow) tests 4 staged candidates per step,
         // distances two at a time in packed FP32 ((dx*dx + dy*dy) + dz*dz per element, no FMA)
-        const int cnt4 = ((int)min((uint32_t)kTileCh, T - base) + 3) & ~3;
         const f2v qx = {x, x}, qy = {y, y}, qz = {z, z};
         double bk = __longlong_as_double((long long)best);
 #pragma unroll 1
@@ -193,9 +218,10 @@ struct CellBox {
 template <int NW>
 __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const CellBox& S, float B, float qx0, float qx1,
                           float qy0, float qy1, float qz0, float qz1, bool act, float x, float y, float z,
-                          uint64_t& best, unsigned long long& cand) {
+                          uint64_t& best, unsigned long long& cand, uint32_t& tested) {
     const int lane = threadIdx.x & 63;
     const float cs = g.cell, m = g.margin;
+    const float qb[6] = {qx0, qx1, qy0, qy1, qz0, qz1};
     const int ny = N.y1 - N.y0 + 1, nrows = ny * (N.z1 - N.z0 + 1);
     const bool sempty = S.x0 > S.x1;
     const uint32_t gnx = (uint32_t)g.nx, gnxy = (uint32_t)g.nx * (uint32_t)g.ny;
@@ -234,7 +260,7 @@ __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const 
                 }
             }
         }
-        scan_ranges<NW>(g, L, b0, n0, b1, n1, act, x, y, z, best, cand);
+        scan_ranges<NW>(g, L, b0, n0, b1, n1, act, x, y, z, qb, best, cand, tested);
     }
 }
 
@@ -298,7 +324,8 @@ __global__ void __launch_bounds__(kIcpTileQ * NW) icp_tile_kernel(IcpArgs a) {
                     min(max(cell_coord(qy1, g.oy, g.inv_cell), 0), g.ny - 1),
                     min(max(cell_coord(qz0, g.oz, g.inv_cell), 0), g.nz - 1),
                     min(max(cell_coord(qz1, g.oz, g.inv_cell), 0), g.nz - 1)};
-    unsigned long long cand = 0;
+    unsigned long long cand = 0;  // candidates streamed (wave 0 counts the tile's)
+    uint32_t tested = 0;          // candidates past the staging filter (this wave's chunks)
     int rounds = 0;
     // 1. bound: grow a box around Q until every lane holds a candidate;
     // 2. final: everything within sqrt(B) of the tile box, minus what was scanned
@@ -321,7 +348,7 @@ __global__ void __launch_bounds__(kIcpTileQ * NW) icp_tile_kernel(IcpArgs a) {
         // the scanned box may stick out of N (a grown box): clip it, the part outside N is not needed
         CellBox Sc{max(S.x0, N.x0), min(S.x1, N.x1), max(S.y0, N.y0), min(S.y1, N.y1), max(S.z0, N.z0), min(S.z1, N.z1)};
         if (Sc.y0 > Sc.y1 || Sc.z0 > Sc.z1) Sc.x0 = 1, Sc.x1 = 0;
-        scan_rows<NW>(g, L, N, Sc, B, qx0, qx1, qy0, qy1, qz0, qz1, act, x, y, z, best, cand);
+        scan_rows<NW>(g, L, N, Sc, B, qx0, qx1, qy0, qy1, qz0, qz1, act, x, y, z, best, cand, tested);
         best = tile_min<NW>(best, s_best);
         ++rounds;
         const bool full = N.x0 == 0 && N.y0 == 0 && N.z0 == 0 && N.x1 == g.nx - 1 && N.y1 == g.ny - 1 && N.z1 == g.nz - 1;
@@ -329,12 +356,20 @@ __global__ void __launch_bounds__(kIcpTileQ * NW) icp_tile_kernel(IcpArgs a) {
         S = N;
         r = 2 * r + 1;
     }
-    if (a.tile_cost && threadIdx.x == 0) a.tile_cost[tix] = (uint32_t)min(cand, 0xffffffffull);
+    // the tile's cost for the next pass's longest-first order: candidates tested over its waves
+    __shared__ uint32_t s_tested[NW];
+    if (lane == 0) s_tested[wv] = tested;
+    __syncthreads();
+    uint32_t tile_tested = 0;
+#pragma unroll
+    for (int v = 0; v < NW; ++v) tile_tested += s_tested[v];
+    if (a.tile_cost && threadIdx.x == 0) a.tile_cost[tix] = tile_tested;
     if (a.dbg && threadIdx.x == 0) {
         atomicAdd(a.dbg, cand);
         atomicAdd(a.dbg + 1, (unsigned long long)rounds);
         atomicAdd(a.dbg + 2, 1ull);
         atomicAdd(a.dbg + 3, (unsigned long long)tl.y);
+        atomicAdd(a.dbg + 4, (unsigned long long)tile_tested);
     }
     __syncthreads();       // every wave has read cur[i] before it is overwritten
     if (act && wv == 0) {

@@ -397,10 +397,11 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     h->have_prior = true;
     if (!fitness && h->sh_n > 0 && icp_order_on() && icp_tile_kernel_on()) h->have_order = true;
     if (dbg_on) {
-        unsigned long long c[4];
+        unsigned long long c[5];
         IHIP(hipMemcpy(c, h->d_dbg, sizeof(c), hipMemcpyDeviceToHost));
-        std::fprintf(stderr, "icp dbg: tiles|waves %llu lanes %llu cand/tile %.1f rounds/tile %.2f cand/lane %.1f\n", c[2],
-                     c[3], (double)c[0] / c[2], (double)c[1] / c[2], (double)c[0] / c[3]);
+        std::fprintf(stderr,
+                     "icp dbg: tiles|waves %llu lanes %llu cand/tile %.1f tested/tile %.1f rounds/tile %.2f cand/lane %.1f\n",
+                     c[2], c[3], (double)c[0] / c[2], (double)c[4] / c[2], (double)c[1] / c[2], (double)c[0] / c[3]);
     }
     if (h->timing && h->sh_n > 0) {
         float ms = 0.f;

@@ -59,6 +59,14 @@ for s in $STEPS; do
            LIO_ICP_TILE_CELL=2.5 run icp_tile_t25 300 python scripts/icp_ab.py 1.0 &&
            LIO_ICP_TILE_CELL=1.5 run icp_tile_t15 300 python scripts/icp_ab.py 1.0 &&
            run icp_tile_c075 300 python scripts/icp_ab.py 0.75 ;;
+    icpq)  run icp_tile 300 python scripts/icp_ab.py 1.0 &&
+           LIO_ICP_DEBUG=1 run icp_tile_dbg 300 python scripts/icp_ab.py 1.0 1 ;;
+    icpsweep) for tc in 1.5 2.5 3.0; do LIO_ICP_TILE_CELL=$tc run icp_t$tc 300 python scripts/icp_ab.py 1.0 || exit 1; done &&
+           LIO_ICP_TILE_WAVES=1 run icp_w1 300 python scripts/icp_ab.py 1.0 &&
+           LIO_ICP_TILE_WAVES=4 run icp_w4 300 python scripts/icp_ab.py 1.0 &&
+           run icp_c075 300 python scripts/icp_ab.py 0.75 &&
+           run icp_c125 300 python scripts/icp_ab.py 1.25 &&
+           run icp_base 300 python scripts/icp_ab.py 1.0 ;;
     icpprof) run icp_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/icpprof" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
              run icp_pmc_valu 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --kernel-trace -d "$OUT/icppmc" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 ;;
     *) echo "unknown step $s" ;;
