@@ -2,8 +2,8 @@
 // /root/reference/fast_lio_sam/src/loop_closure.cpp:3-14, aligned at :81) on gfx950.
 //
 // Per ICP iteration (this rank's shard of the source):
-//   icp_tile_kernel  one block (2 waves splitting the candidate stream) per
-//                    tile of <= 64 spatially compact source points (binned
+//   icp_tile_kernel  one wave (LIO_ICP_TILE_WAVES: 2 or 4 splitting the candidate
+//                    stream) per tile of <= 64 spatially compact source points (binned
 //                    once per setInputSource): apply the previous T_inc to
 //                    the incrementally transformed cloud (PCL transformCloud,
 //                    float SSE order [U]), exact unbounded 1-NN in the target
@@ -84,20 +84,69 @@ __device__ __forceinline__ double key_of(float d2, uint32_t id) {
     return __longlong_as_double((long long)(((uint64_t)__float_as_uint(d2) << 32) | id));
 }
 
-__device__ __forceinline__ float wave_min_f(float v) {
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) v = fminf(v, __shfl_xor(v, off, 64));
-    return v;
+// key (d[H], id[H]) of element H of a candidate pair in one v_pk_mov_b32: low word from the
+// id pair, high word from the packed distance pair (no register shuffling)
+template <int H>
+__device__ __forceinline__ double key_pk(uint32_t id0, uint32_t id1, f2v d) {
+    const double ids = __longlong_as_double((long long)(((uint64_t)id1 << 32) | id0));
+    double k;
+    if constexpr (H == 0)
+        asm("v_pk_mov_b32 %0, %1, %2 op_sel:[0,0]" : "=v"(k) : "v"(ids), "v"(d));
+    else
+        asm("v_pk_mov_b32 %0, %1, %2 op_sel:[1,1]" : "=v"(k) : "v"(ids), "v"(d));
+    return k;
 }
-__device__ __forceinline__ float wave_max_f(float v) {
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
-    return v;
+
+// wave maximum of non-negative floats (as integers: same order), wave-uniform: DPP inside
+// each row of 16 (quad swaps, half-row and row mirrors), then the four row maxima by readlane
+// — no LDS permutes on the per-chunk path
+__device__ __forceinline__ float wave_max_nonneg(float v) {
+    uint32_t u = __float_as_uint(v);
+    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp((int)u, (int)u, 0xb1, 0xf, 0xf, false));   // quad_perm 1,0,3,2
+    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp((int)u, (int)u, 0x4e, 0xf, 0xf, false));   // quad_perm 2,3,0,1
+    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp((int)u, (int)u, 0x141, 0xf, 0xf, false));  // row_half_mirror
+    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp((int)u, (int)u, 0x140, 0xf, 0xf, false));  // row_mirror
+    const uint32_t m = max(max((uint32_t)__builtin_amdgcn_readlane((int)u, 0), (uint32_t)__builtin_amdgcn_readlane((int)u, 16)),
+                           max((uint32_t)__builtin_amdgcn_readlane((int)u, 32), (uint32_t)__builtin_amdgcn_readlane((int)u, 48)));
+    return __uint_as_float(m);
 }
+
 // wave-uniform values to SGPRs (the compiler cannot see that a butterfly
 // result is uniform; keeping the box arithmetic scalar frees VGPRs)
 __device__ __forceinline__ float uni_f(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
 __device__ __forceinline__ uint32_t uni_u(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+// wave min / max of floats (any sign) by DPP inside each row of 16, then the four row
+// results by readlane: wave-uniform, no LDS permutes
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+template <bool MAX>
+__device__ __forceinline__ float wave_ext_dpp(float v) {
+    auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : fminf(a, b); };
+    v = op(v, dpp_f<0xb1>(v));   // quad_perm 1,0,3,2
+    v = op(v, dpp_f<0x4e>(v));   // quad_perm 2,3,0,1
+    v = op(v, dpp_f<0x141>(v));  // row_half_mirror
+    v = op(v, dpp_f<0x140>(v));  // row_mirror
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return uni_f(op(op(r0, r1), op(r2, r3)));
+}
+
+// inclusive prefix sum over the wave: DPP row shifts inside rows of 16, then row_bcast:15 /
+// row_bcast:31 carry the row totals forward (rows 1, 3 then rows 2, 3)
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
+}
 
 // squared gap between the closed intervals [lo, hi] and [a, b]
 __device__ __forceinline__ float interval_gap(float lo, float hi, float a, float b) {
@@ -120,15 +169,11 @@ template <int NW>  // waves per tile: the tile's candidate stream is split over 
 __device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32_t b0, uint32_t n0, uint32_t b1,
                                             uint32_t n1, bool act, float x, float y, float z, const float (&qb)[6],
                                             uint64_t& best, unsigned long long& cand, uint32_t& tested) {
-    const int lane = threadIdx.x & 63, w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // wave-uniform
+    // the wave's index within its tile (several one-wave tiles per block: always 0)
+    const int lane = threadIdx.x & 63, w = NW > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
     const uint32_t n = n0 + n1;
-    uint32_t incl = n;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t v = __shfl_up(incl, off, 64);
-        if (lane >= off) incl += v;
-    }
-    const uint32_t T = uni_u(__shfl(incl, 63, 64));
+    const uint32_t incl = wave_incl_scan_dpp(n);
+    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     if (T == 0) return;  // wave-uniform
     if (w == 0) cand += T;
     wave_sync();  // previous readers of the slot table are done
@@ -156,7 +201,7 @@ __device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32
             v[u] = g.pts[sb + (t - lo)];
         }
         // the wave's bound: its active lanes' largest best (+inf while one has none)
-        const float Bw = uni_f(wave_max_f(act ? __uint_as_float((uint32_t)(best >> 32)) : 0.f));
+        const float Bw = wave_max_nonneg(act ? __uint_as_float((uint32_t)(best >> 32)) : 0.f);
         uint32_t cnt = 0;
 #pragma unroll
         for (int u = 0; u < U; ++u) {  // survivors compacted in stream order
@@ -175,9 +220,9 @@ __device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32
             }
             cnt += (uint32_t)__popcll(m);
         }
-        const int cnt4 = ((int)cnt + 3) & ~3;
+        const int cnt8 = ((int)cnt + 7) & ~7;
         tested += cnt;
-        if ((uint32_t)lane < (uint32_t)cnt4 - cnt) {  // pad to 4: +inf points with id kNone (never win)
+        if ((uint32_t)lane < (uint32_t)cnt8 - cnt) {  // pad to 8: +inf points with id kNone (never win)
             L.x[cnt + lane] = INFINITY;
             L.y[cnt + lane] = INFINITY;
             L.z[cnt + lane] = INFINITY;
@@ -188,8 +233,8 @@ __device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32
         // distances two at a time in packed FP32 ((dx*dx + dy*dy) + dz*dz per element, no FMA)
         const f2v qx = {x, x}, qy = {y, y}, qz = {z, z};
         double bk = __longlong_as_double((long long)best);
-#pragma unroll 1
-        for (int j = 0; j < cnt4; j += 4) {
+        // four staged candidates -> the minimum of their (d2, id) keys
+        auto step4 = [&](int j) {
             const float4 X = *reinterpret_cast<const float4*>(__builtin_assume_aligned(&L.x[j], 16));
             const float4 Y = *reinterpret_cast<const float4*>(__builtin_assume_aligned(&L.y[j], 16));
             const float4 Z = *reinterpret_cast<const float4*>(__builtin_assume_aligned(&L.z[j], 16));
@@ -198,9 +243,14 @@ __device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32
             const f2v dx1 = qx - f2v{X.z, X.w}, dy1 = qy - f2v{Y.z, Y.w}, dz1 = qz - f2v{Z.z, Z.w};
             const f2v d0 = (dx0 * dx0 + dy0 * dy0) + dz0 * dz0;
             const f2v d1 = (dx1 * dx1 + dy1 * dy1) + dz1 * dz1;
-            const double m0 = key_min_d(key_of(d0.x, I.x), key_of(d0.y, I.y));
-            const double m1 = key_min_d(key_of(d1.x, I.z), key_of(d1.y, I.w));
-            bk = key_min_d(bk, key_min_d(m0, m1));
+            const double m0 = key_min_d(key_pk<0>(I.x, I.y, d0), key_pk<1>(I.x, I.y, d0));
+            const double m1 = key_min_d(key_pk<0>(I.z, I.w, d1), key_pk<1>(I.z, I.w, d1));
+            return key_min_d(m0, m1);
+        };
+#pragma unroll 1
+        for (int j = 0; j < cnt8; j += 8) {  // two steps per trip: 8 LDS reads in flight
+            const double ma = step4(j), mb = step4(j + 4);
+            bk = key_min_d(bk, key_min_d(ma, mb));
         }
         best = (uint64_t)__double_as_longlong(bk);
         wave_sync();  // chunk consumed before it is overwritten
@@ -267,6 +317,7 @@ __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const 
 // min over the tile's waves of every lane's key (all waves end with the same best)
 template <int NW>
 __device__ __forceinline__ uint64_t tile_min(uint64_t best, uint64_t (*s_best)[kIcpTileQ]) {
+    if constexpr (NW == 1) return best;  // one wave per tile: nothing to merge
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     __syncthreads();
     s_best[w][lane] = best;
@@ -279,13 +330,22 @@ __device__ __forceinline__ uint64_t tile_min(uint64_t best, uint64_t (*s_best)[k
     return best;
 }
 
-template <int NW>
-__global__ void __launch_bounds__(kIcpTileQ * NW) icp_tile_kernel(IcpArgs a) {
-    __shared__ TileLds Ls[NW];
+// NW waves split one tile's candidate stream (block-level merges), or (NW = 1) TPB
+// independent one-wave tiles share a block — more tiles resident per CU than one-wave
+// blocks allow, and no block barrier couples them.
+template <int NW, int TPB>
+__global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs a, int ntiles) {
+    static_assert(NW == 1 || TPB == 1, "icp_tile_kernel: several waves per tile or several tiles per block");
+    __shared__ TileLds Ls[NW * TPB];
     __shared__ uint64_t s_best[NW][kIcpTileQ];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     TileLds& L = Ls[wv];
-    const int tix = a.order ? (int)a.order[blockIdx.x] : xcd_block(blockIdx.x, gridDim.x);
+    // this wave's tile: slot k of the longest-first order, or (cell order) the XCD-remapped block's
+    // k-th tile; a wave past the end leaves at once (no block barriers when TPB > 1)
+    const int sub = TPB > 1 ? wv : 0;
+    const int k = a.order ? blockIdx.x * TPB + sub : xcd_block(blockIdx.x, gridDim.x) * TPB + sub;
+    if (TPB > 1 && k >= ntiles) return;
+    const int tix = a.order ? (int)a.order[k] : k;
     const uint2 tl = a.tiles[tix];
     const bool act = lane < (int)tl.y;
     const int i = act ? __float_as_int(a.qpts[tl.x + lane].w) : 0;
@@ -315,9 +375,9 @@ __global__ void __launch_bounds__(kIcpTileQ * NW) icp_tile_kernel(IcpArgs a) {
         best = knn_key(sqdist3(x, y, z, p.x, p.y, p.z), prior);
     }
     // tile bounding box (active lanes)
-    const float qx0 = uni_f(wave_min_f(act ? x : INFINITY)), qx1 = uni_f(wave_max_f(act ? x : -INFINITY));
-    const float qy0 = uni_f(wave_min_f(act ? y : INFINITY)), qy1 = uni_f(wave_max_f(act ? y : -INFINITY));
-    const float qz0 = uni_f(wave_min_f(act ? z : INFINITY)), qz1 = uni_f(wave_max_f(act ? z : -INFINITY));
+    const float qx0 = wave_ext_dpp<false>(act ? x : INFINITY), qx1 = wave_ext_dpp<true>(act ? x : -INFINITY);
+    const float qy0 = wave_ext_dpp<false>(act ? y : INFINITY), qy1 = wave_ext_dpp<true>(act ? y : -INFINITY);
+    const float qz0 = wave_ext_dpp<false>(act ? z : INFINITY), qz1 = wave_ext_dpp<true>(act ? z : -INFINITY);
     const CellBox Q{min(max(cell_coord(qx0, g.ox, g.inv_cell), 0), g.nx - 1),
                     min(max(cell_coord(qx1, g.ox, g.inv_cell), 0), g.nx - 1),
                     min(max(cell_coord(qy0, g.oy, g.inv_cell), 0), g.ny - 1),
@@ -339,7 +399,7 @@ __global__ void __launch_bounds__(kIcpTileQ * NW) icp_tile_kernel(IcpArgs a) {
             N = CellBox{max(Q.x0 - r, 0), min(Q.x1 + r, g.nx - 1), max(Q.y0 - r, 0), min(Q.y1 + r, g.ny - 1),
                         max(Q.z0 - r, 0), min(Q.z1 + r, g.nz - 1)};
         } else {
-            B = uni_f(wave_max_f(act ? __uint_as_float((uint32_t)(best >> 32)) : 0.f));
+            B = wave_max_nonneg(act ? __uint_as_float((uint32_t)(best >> 32)) : 0.f);
             const float R = sqrtf(B) * 1.00001f + g.margin;
             N = CellBox{max(cell_coord(qx0 - R, g.ox, g.inv_cell), 0), min(cell_coord(qx1 + R, g.ox, g.inv_cell), g.nx - 1),
                         max(cell_coord(qy0 - R, g.oy, g.inv_cell), 0), min(cell_coord(qy1 + R, g.oy, g.inv_cell), g.ny - 1),
@@ -357,22 +417,26 @@ __global__ void __launch_bounds__(kIcpTileQ * NW) icp_tile_kernel(IcpArgs a) {
         r = 2 * r + 1;
     }
     // the tile's cost for the next pass's longest-first order: candidates tested over its waves
-    __shared__ uint32_t s_tested[NW];
-    if (lane == 0) s_tested[wv] = tested;
-    __syncthreads();
-    uint32_t tile_tested = 0;
+    uint32_t tile_tested = tested;
+    if constexpr (NW > 1) {
+        __shared__ uint32_t s_tested[NW];
+        if (lane == 0) s_tested[wv] = tested;
+        __syncthreads();
+        tile_tested = 0;
 #pragma unroll
-    for (int v = 0; v < NW; ++v) tile_tested += s_tested[v];
-    if (a.tile_cost && threadIdx.x == 0) a.tile_cost[tix] = tile_tested;
-    if (a.dbg && threadIdx.x == 0) {
+        for (int v = 0; v < NW; ++v) tile_tested += s_tested[v];
+    }
+    const bool lead = NW > 1 ? threadIdx.x == 0 : lane == 0;
+    if (a.tile_cost && lead) a.tile_cost[tix] = tile_tested;
+    if (a.dbg && lead) {
         atomicAdd(a.dbg, cand);
         atomicAdd(a.dbg + 1, (unsigned long long)rounds);
         atomicAdd(a.dbg + 2, 1ull);
         atomicAdd(a.dbg + 3, (unsigned long long)tl.y);
         atomicAdd(a.dbg + 4, (unsigned long long)tile_tested);
     }
-    __syncthreads();       // every wave has read cur[i] before it is overwritten
-    if (act && wv == 0) {
+    if constexpr (NW > 1) __syncthreads();  // every wave has read cur[i] before it is overwritten
+    if (act && (NW == 1 || wv == 0)) {
         if (a.fitness || a.apply_T) {
             a.cur[3 * i] = x;
             a.cur[3 * i + 1] = y;
@@ -604,14 +668,24 @@ void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st) {
     if (a.n == 0 || ntiles == 0) return;
     static const int nw = [] {  // LIO_ICP_TILE_WAVES: diagnostics override (1, 2, 4)
         const char* e = std::getenv("LIO_ICP_TILE_WAVES");
-        return e ? std::atoi(e) : 2;
+        return e ? std::atoi(e) : 1;
     }();
-    if (nw == 1)
-        icp_tile_kernel<1><<<ntiles, kIcpTileQ, 0, st>>>(a);
+    static const int tpb = [] {  // LIO_ICP_TILES_PER_BLOCK: diagnostics override (1, 2, 4, 8)
+        const char* e = std::getenv("LIO_ICP_TILES_PER_BLOCK");
+        return e ? std::atoi(e) : 1;  // 2 / 4 / 8 measured no faster (profiles/r02_icp_tile_experiments.txt)
+    }();
+    if (nw == 2)
+        icp_tile_kernel<2, 1><<<ntiles, kIcpTileQ * 2, 0, st>>>(a, ntiles);
     else if (nw == 4)
-        icp_tile_kernel<4><<<ntiles, kIcpTileQ * 4, 0, st>>>(a);
-    else  // 2 waves per tile: measured best (scripts/icp_exp.sh)
-        icp_tile_kernel<2><<<ntiles, kIcpTileQ * 2, 0, st>>>(a);
+        icp_tile_kernel<4, 1><<<ntiles, kIcpTileQ * 4, 0, st>>>(a, ntiles);
+    else if (tpb == 4)
+        icp_tile_kernel<1, 4><<<(ntiles + 3) / 4, kIcpTileQ * 4, 0, st>>>(a, ntiles);
+    else if (tpb == 2)
+        icp_tile_kernel<1, 2><<<(ntiles + 1) / 2, kIcpTileQ * 2, 0, st>>>(a, ntiles);
+    else if (tpb == 8)
+        icp_tile_kernel<1, 8><<<(ntiles + 7) / 8, kIcpTileQ * 8, 0, st>>>(a, ntiles);
+    else  // 1 wave per tile: best since the staging filter (its bound then sees every chunk)
+        icp_tile_kernel<1, 1><<<ntiles, kIcpTileQ, 0, st>>>(a, ntiles);
 }
 
 // Longest-first tile order from the previous pass's candidate counts: tiles

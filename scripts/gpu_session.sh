@@ -25,6 +25,12 @@ run() {  # run <name> <seconds> <cmd...>
     return 0
 }
 
+runs() {  # as run, but any failure (tests included) ends the session
+    run "$@"
+    grep -qE "(^| )(failed|error)" "$OUT/$1.log" && { echo "!! $1 had failures: stopping the session"; exit 1; }
+    return 0
+}
+
 for s in $STEPS; do
     case $s in
     test)  run pytest_gpu 900 python -u -m pytest tests -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread ;;
@@ -53,7 +59,7 @@ for s in $STEPS; do
              LIO_GPU_LIB=build_ab/liblio_gpu_base.so run ab_base_$rep 300 python bench.py --steps 400 --warmup 20 --no-icp --no-cpu --streams '' &&
              run ab_new_$rep 300 python bench.py --steps 400 --warmup 20 --no-icp --no-cpu --streams '' || exit 1
            done ;;
-    icptest) run pytest_icp 600 python -u -m pytest tests/test_gpu_icp.py tests/test_gpu_parity.py -k icp -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    icptest) runs pytest_icp 600 python -u -m pytest tests/test_gpu_icp.py tests/test_gpu_parity.py -k icp -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     icpab) run icp_tile 300 python scripts/icp_ab.py 1.0 &&
            LIO_ICP_DEBUG=1 run icp_tile_dbg 300 python scripts/icp_ab.py 1.0 1 &&
            LIO_ICP_TILE_CELL=2.5 run icp_tile_t25 300 python scripts/icp_ab.py 1.0 &&
@@ -67,6 +73,9 @@ for s in $STEPS; do
            run icp_c075 300 python scripts/icp_ab.py 0.75 &&
            run icp_c125 300 python scripts/icp_ab.py 1.25 &&
            run icp_base 300 python scripts/icp_ab.py 1.0 ;;
+    icpr0) LIO_ICP_R0=0 run icp_r0 300 python scripts/icp_ab.py 1.0 &&
+           LIO_ICP_R0=0 LIO_ICP_DEBUG=1 run icp_r0_dbg 300 python scripts/icp_ab.py 1.0 1 ;;
+    icptpb) for t in 1 2 4 8; do LIO_ICP_TILES_PER_BLOCK=$t run icp_tpb$t 300 python scripts/icp_ab.py 1.0 || exit 1; done ;;
     icpprof) run icp_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/icpprof" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
              run icp_pmc_valu 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --kernel-trace -d "$OUT/icppmc" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 ;;
     *) echo "unknown step $s" ;;
