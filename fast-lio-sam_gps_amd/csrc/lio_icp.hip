@@ -74,6 +74,7 @@ struct alignas(16) TileLds {
     uint32_t id[kTileCh];
     uint32_t b[2 * kIcpTileQ];
     uint32_t off[2 * kIcpTileQ + 1];
+    uint4 perm[kIcpTileQ];  // a batch of rows (b0, n0, b1, n1), re-ordered nearest-first
 };
 
 // (d2, id) keys minimised as f64: lio_dev.hpp key_min (one v_min_f64 instead of compare + two selects)
@@ -279,13 +280,14 @@ __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const 
     for (int rb = 0; rb < nrows; rb += kIcpTileQ) {
         const int r = rb + lane;
         uint32_t b0 = 0, n0 = 0, b1 = 0, n1 = 0;
+        float g2 = INFINITY;
         if (r < nrows) {
             const int rz = N.z0 + r / ny, ry = N.y0 + r % ny;
             int x0 = N.x0, x1 = N.x1;
             bool keep = true;
+            const float yl = g.oy + (float)ry * cs - m, zl = g.oz + (float)rz * cs - m;
+            g2 = interval_gap(yl, yl + cs + 2.f * m, qy0, qy1) + interval_gap(zl, zl + cs + 2.f * m, qz0, qz1);
             if (B < INFINITY) {
-                const float yl = g.oy + (float)ry * cs - m, zl = g.oz + (float)rz * cs - m;
-                const float g2 = interval_gap(yl, yl + cs + 2.f * m, qy0, qy1) + interval_gap(zl, zl + cs + 2.f * m, qz0, qz1);
                 if (g2 * 0.999999f > B) {
                     keep = false;
                 } else {
@@ -310,7 +312,23 @@ __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const 
                 }
             }
         }
-        scan_ranges<NW>(g, L, b0, n0, b1, n1, act, x, y, z, qb, best, cand, tested);
+        // nearest rows first (stable partition by the row's (y, z) gap to the tile box: 0, <= 1,
+        // <= 2 cells, farther), so the staging filter's bound tightens early in the stream; any
+        // order gives the same minima (total order on (d2, id))
+        const float c2 = cs * cs;
+        const int cls = g2 == 0.f ? 0 : (g2 <= c2 ? 1 : (g2 <= 4.f * c2 ? 2 : 3));
+        uint32_t rank = 0, before = 0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const uint64_t mk = __ballot(cls == c);
+            if (cls == c) rank = before + __builtin_amdgcn_mbcnt_hi((uint32_t)(mk >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mk, 0u));
+            before += (uint32_t)__popcll(mk);
+        }
+        wave_sync();  // previous batch's reads of perm are done
+        L.perm[rank] = make_uint4(b0, n0, b1, n1);
+        wave_sync();
+        const uint4 pr = L.perm[lane];
+        scan_ranges<NW>(g, L, pr.x, pr.y, pr.z, pr.w, act, x, y, z, qb, best, cand, tested);
     }
 }
 
