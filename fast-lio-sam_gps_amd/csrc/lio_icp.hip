@@ -364,6 +364,7 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
     const int k = a.order ? blockIdx.x * TPB + sub : xcd_block(blockIdx.x, gridDim.x) * TPB + sub;
     if (TPB > 1 && k >= ntiles) return;
     const int tix = a.order ? (int)a.order[k] : k;
+    const unsigned long long t_start = a.times ? wall_clock64() : 0ull;
     const uint2 tl = a.tiles[tix];
     const bool act = lane < (int)tl.y;
     const int i = act ? __float_as_int(a.qpts[tl.x + lane].w) : 0;
@@ -446,6 +447,10 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
     }
     const bool lead = NW > 1 ? threadIdx.x == 0 : lane == 0;
     if (a.tile_cost && lead) a.tile_cost[tix] = tile_tested;
+    if (a.times && lead) {
+        a.times[2 * tix] = t_start;
+        a.times[2 * tix + 1] = wall_clock64();
+    }
     if (a.dbg && lead) {
         atomicAdd(a.dbg, cand);
         atomicAdd(a.dbg + 1, (unsigned long long)rounds);

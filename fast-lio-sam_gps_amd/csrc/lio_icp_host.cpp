@@ -374,6 +374,14 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
         IHIP(hipMemsetAsync(h->d_dbg, 0, 64, h->st));
         a.dbg = h->d_dbg;
     }
+    static const bool times_on = std::getenv("LIO_ICP_TIMES") != nullptr;  // per-tile timeline on stderr
+    std::vector<unsigned long long> h_times;
+    unsigned long long* d_times = nullptr;
+    if (times_on && h->ntiles > 0 && icp_tile_kernel_on()) {
+        IHIP(hipMalloc(&d_times, (size_t)h->ntiles * 2 * sizeof(unsigned long long)));
+        IHIP(hipMemsetAsync(d_times, 0, (size_t)h->ntiles * 2 * sizeof(unsigned long long), h->st));
+        a.times = d_times;
+    }
     const int nsup_loc = (int)((h->sh_n + lio::kIcpSuper - 1) / lio::kIcpSuper);
     if (h->sh_n > 0) {
         if (h->timing) IHIP(hipEventRecord(h->ev.a, h->st));
@@ -393,6 +401,30 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
         IHIP(hipEventSynchronize(h->ev.done));
     } else {
         IHIP(hipStreamSynchronize(h->st));
+    }
+    if (d_times) {  // tiles active over the pass (20 bins), tile duration percentiles (us, 100 MHz clock)
+        h_times.resize((size_t)h->ntiles * 2);
+        IHIP(hipMemcpy(h_times.data(), d_times, h_times.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        IHIP(hipFree(d_times));
+        unsigned long long t0 = ~0ull, t1 = 0;
+        std::vector<double> dur;
+        for (int t = 0; t < h->ntiles; ++t) {
+            t0 = std::min(t0, h_times[2 * t]);
+            t1 = std::max(t1, h_times[2 * t + 1]);
+            dur.push_back((double)(h_times[2 * t + 1] - h_times[2 * t]) * 0.01);
+        }
+        std::sort(dur.begin(), dur.end());
+        const double span = (double)(t1 - t0);
+        int bins[20] = {0};
+        for (int t = 0; t < h->ntiles; ++t)
+            for (int k = 0; k < 20; ++k) {
+                const double lo = t0 + span * k / 20, hi = t0 + span * (k + 1) / 20;
+                if ((double)h_times[2 * t] < hi && (double)h_times[2 * t + 1] > lo) ++bins[k];
+            }
+        std::fprintf(stderr, "icp times: span %.1f us, tile us p50 %.1f p90 %.1f p99 %.1f max %.1f; active per 5%%:", span * 0.01,
+                     dur[dur.size() / 2], dur[dur.size() * 9 / 10], dur[dur.size() * 99 / 100], dur.back());
+        for (int k = 0; k < 20; ++k) std::fprintf(stderr, " %d", bins[k]);
+        std::fprintf(stderr, "\n");
     }
     h->have_prior = true;
     if (!fitness && h->sh_n > 0 && icp_order_on() && icp_tile_kernel_on()) h->have_order = true;

@@ -143,6 +143,7 @@ struct IcpArgs {
     const uint32_t* order;  // optional tile visit order (heaviest first, from the previous pass's costs)
     uint32_t* tile_cost;    // per tile: candidates scanned in this pass
     unsigned long long* dbg;  // optional counters (diagnostics): candidates, rings, tiles, lanes
+    unsigned long long* times;  // optional per tile (start, end) wall clock (diagnostics: LIO_ICP_TIMES)
 };
 
 constexpr int kIcpSuper = 4096;    // points per exchanged partial (shard granule)
