@@ -72,9 +72,13 @@ __device__ __forceinline__ void wave_sync() {
 struct alignas(16) TileLds {
     float x[kTileCh], y[kTileCh], z[kTileCh];
     uint32_t id[kTileCh];
-    uint32_t b[2 * kIcpTileQ];
-    uint32_t off[2 * kIcpTileQ + 1];
-    uint4 perm[kIcpTileQ];  // a batch of rows (b0, n0, b1, n1), re-ordered nearest-first
+    union {  // the row permutation is read into registers before the slot table is written
+        struct {
+            uint32_t b[2 * kIcpTileQ];
+            uint32_t off[2 * kIcpTileQ + 1];
+        };
+        uint4 perm[kIcpTileQ];  // a batch of rows (b0, n0, b1, n1), re-ordered nearest-first
+    };
 };
 
 // (d2, id) keys minimised as f64: lio_dev.hpp key_min (one v_min_f64 instead of compare + two selects)
@@ -334,15 +338,15 @@ __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const 
 
 // min over the tile's waves of every lane's key (all waves end with the same best)
 template <int NW>
-__device__ __forceinline__ uint64_t tile_min(uint64_t best, uint64_t (*s_best)[kIcpTileQ]) {
+__device__ __forceinline__ uint64_t tile_min(uint64_t best, uint64_t* s_best) {
     if constexpr (NW == 1) return best;  // one wave per tile: nothing to merge
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     __syncthreads();
-    s_best[w][lane] = best;
+    s_best[w * kIcpTileQ + lane] = best;
     __syncthreads();
 #pragma unroll
     for (int v = 0; v < NW; ++v) {
-        const uint64_t o = s_best[v][lane];
+        const uint64_t o = s_best[v * kIcpTileQ + lane];
         best = o < best ? o : best;
     }
     return best;
@@ -355,7 +359,7 @@ template <int NW, int TPB>
 __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs a, int ntiles) {
     static_assert(NW == 1 || TPB == 1, "icp_tile_kernel: several waves per tile or several tiles per block");
     __shared__ TileLds Ls[NW * TPB];
-    __shared__ uint64_t s_best[NW][kIcpTileQ];
+    __shared__ uint64_t s_best[NW > 1 ? NW * kIcpTileQ : 1];  // cross-wave merge (NW > 1 only)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     TileLds& L = Ls[wv];
     // this wave's tile: slot k of the longest-first order, or (cell order) the XCD-remapped block's
