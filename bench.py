@@ -182,16 +182,17 @@ def main():
                                         yaw_gt=0.05 * np.sin(0.3 * k + 0.2), seed=5099 + k + 1000 * rank))
         d_grow = [torch.from_numpy(s.body).to(dev) for s in grow]
         torch.cuda.synchronize()
-        t_incr = 0.0
+        t_list = []
         added = 0
         for k, s in enumerate(grow):
             hm.set_scan_device(d_grow[k].data_ptr(), len(s.body))
             xg, _, _ = kf.update_iterated_dyn_share_modified(synth.initial_state(s.pos_init, s.rot_init), P0)
             ti = time.perf_counter()
             st_i = hm.map_incremental(synth.pose24(xg), 0.5)
-            t_incr += time.perf_counter() - ti
+            t_list.append(time.perf_counter() - ti)
             added += st_i["n_to_add"] + st_i["n_no_downsample"]
-        incr = {"scans": len(grow), "ms_per_scan": round(t_incr / len(grow) * 1e3, 3),
+        incr = {"scans": len(grow), "ms_per_scan": round(sum(t_list) / len(grow) * 1e3, 3),
+                "ms_per_scan_median": round(float(np.median(t_list)) * 1e3, 3),
                 "points_offered_per_scan": round(added / len(grow), 1), "map_size_after": tree.size(),
                 "map_ids_after": tree.num_ids()}
 

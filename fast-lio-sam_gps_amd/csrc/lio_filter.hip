@@ -423,15 +423,16 @@ int fgrow(T** p, int64_t& cap, int64_t need) {
     return 0;
 }
 
-int ftmp(FilterBuf& b, size_t need) {
+int ftmp(FilterBuf& b, size_t need) {  // grown geometrically (1 MiB floor): no per-call re-allocation
     if (need <= b.tmp_bytes && b.tmp) return 0;
     if (b.tmp) (void)hipFree(b.tmp);
     b.tmp = nullptr;
-    if (hipMalloc(&b.tmp, need) != hipSuccess) {
+    const size_t c = std::max(std::max(need, b.tmp_bytes + b.tmp_bytes / 2), (size_t)1 << 20);
+    if (hipMalloc(&b.tmp, c) != hipSuccess) {
         b.tmp_bytes = 0;
         return -5;
     }
-    b.tmp_bytes = need;
+    b.tmp_bytes = c;
     return 0;
 }
 

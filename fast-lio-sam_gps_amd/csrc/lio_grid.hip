@@ -216,15 +216,17 @@ __global__ void run_count_kernel(const uint32_t* __restrict__ ckeys, int64_t n, 
         }                                                                       \
     } while (0)
 
+// scratch grown geometrically (1 MiB floor): no re-allocation (a device-wide sync) per slightly larger call
 static int ensure(void** p, size_t& cap_bytes, size_t need) {
     if (need <= cap_bytes && *p) return 0;
     if (*p) (void)hipFree(*p);
     *p = nullptr;
-    if (hipMalloc(p, need) != hipSuccess) {
+    const size_t c = std::max(std::max(need, cap_bytes + cap_bytes / 2), (size_t)1 << 20);
+    if (hipMalloc(p, c) != hipSuccess) {
         cap_bytes = 0;
         return -5;
     }
-    cap_bytes = need;
+    cap_bytes = c;
     return 0;
 }
 
@@ -312,7 +314,11 @@ static int reserve_cells(GridBuf& g, uint32_t nc1) {
 int grid_build(GridBuf& g, const float* d_xyz, int64_t n, float cell, hipStream_t st) {
     if (n <= 0 || n >= (int64_t)0x7fffffff) return -1;
     g.n_ids = 0;
-    int rc = grid_reserve_ids(g, n, st);
+    // 1.5x headroom: the first map_incremental calls append without re-allocating (and copying) the map
+    const int64_t room = n + n / 2;
+    int rc = grid_reserve_ids(g, room, st);
+    if (rc) return rc;
+    rc = reserve_entries(g, room, st);
     if (rc) return rc;
     init_by_id_kernel<<<(int)((n + 255) / 256), 256, 0, st>>>(d_xyz, n, g.by_id);
     g.n_ids = n;

@@ -413,15 +413,18 @@ int ensure_buf(T** p, int64_t& cap, int64_t need) {
     return 0;
 }
 
+// sort / scan scratch: grown geometrically (with a 1 MiB floor), so scans of varying size do not
+// re-allocate (hipFree synchronises the device) on every call that needs a little more
 int ensure_tmp(MapUpdBuf& u, size_t need) {
     if (need <= u.tmp_bytes && u.tmp) return 0;
     if (u.tmp) (void)hipFree(u.tmp);
     u.tmp = nullptr;
-    if (hipMalloc(&u.tmp, need) != hipSuccess) {
+    const size_t c = std::max(std::max(need, u.tmp_bytes + u.tmp_bytes / 2), (size_t)1 << 20);
+    if (hipMalloc(&u.tmp, c) != hipSuccess) {
         u.tmp_bytes = 0;
         return -5;
     }
-    u.tmp_bytes = need;
+    u.tmp_bytes = c;
     return 0;
 }
 
