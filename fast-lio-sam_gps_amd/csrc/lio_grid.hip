@@ -168,11 +168,17 @@ __device__ __forceinline__ int64_t lower_bound_u32(const uint32_t* a, int64_t n,
 __global__ void merge_old_kernel(const float4* __restrict__ pts, const uint32_t* __restrict__ ckeys, int64_t n_old,
                                  const uint32_t* __restrict__ pos, const uint32_t* __restrict__ new_keys, int64_t n_new,
                                  float4* __restrict__ pts_out, uint32_t* __restrict__ ckeys_out) {
-    const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t j0 = blockIdx.x * (int64_t)blockDim.x, j = j0 + threadIdx.x;
+    // the block's entries are cell-sorted: their cells' new keys form one narrow window of new_keys
+    __shared__ int64_t s_lo, s_hi;
+    if (threadIdx.x == 0) s_lo = lower_bound_u32(new_keys, n_new, ckeys[j0]);
+    if (threadIdx.x == 1) s_hi = lower_bound_u32(new_keys, n_new, ckeys[min(j0 + (int64_t)blockDim.x, n_old) - 1] + 1u);
+    __syncthreads();
     if (j >= n_old) return;
     if (pos && pos[j + 1] == pos[j]) return;  // deleted
     const uint32_t c = ckeys[j];
-    const int64_t o = (pos ? (int64_t)pos[j] : j) + lower_bound_u32(new_keys, n_new, c);
+    const int64_t lo = s_lo;
+    const int64_t o = (pos ? (int64_t)pos[j] : j) + lo + lower_bound_u32(new_keys + lo, s_hi - lo, c);
     pts_out[o] = pts[j];
     ckeys_out[o] = c;
 }
@@ -193,18 +199,22 @@ __global__ void merge_new_kernel(const float4* __restrict__ by_id, const uint32_
     ckeys_out[o] = c;
 }
 
-// cell counts of the (cell-sorted) entries: a run's head subtracts its index
-// and its tail adds its end (two uncontended atomics per cell, mod 2^32), so no
-// lane walks a run — dense cells hold thousands of entries
-__global__ void run_count_kernel(const uint32_t* __restrict__ ckeys, int64_t n, uint32_t* __restrict__ counts) {
-    const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    const uint32_t k = ckeys[j];
-    const bool head = j == 0 || ckeys[j - 1] != k;
-    const bool tail = j + 1 == n || ckeys[j + 1] != k;
-    if (head && tail) counts[k] = 1u;
-    else if (head) atomicSub(&counts[k], (uint32_t)j);
-    else if (tail) atomicAdd(&counts[k], (uint32_t)(j + 1));
+// incremental cell table after a merge, in place: cell c starts after the surviving old entries of
+// earlier cells (pos[start_old[c]], or start_old[c] with no deletions) and the new entries of
+// earlier cells (lower bound of c in the sorted new keys).  Slot ncells gives the new total.
+// Replaces a clear + run count + scan over all cells.
+__global__ void start_update_kernel(uint32_t* __restrict__ start, uint32_t nc1, const uint32_t* __restrict__ pos,
+                                    const uint32_t* __restrict__ new_keys, int64_t n_new) {
+    const uint32_t c0 = blockIdx.x * 256u, c = c0 + threadIdx.x;
+    // the block's cells share a narrow window of the new keys: bound it once per block
+    __shared__ int64_t s_lo, s_hi;
+    if (threadIdx.x == 0) s_lo = lower_bound_u32(new_keys, n_new, c0);
+    if (threadIdx.x == 1) s_hi = lower_bound_u32(new_keys, n_new, c0 + 256u);
+    __syncthreads();
+    if (c >= nc1) return;
+    const int64_t lo = s_lo;
+    const uint32_t so = start[c];
+    start[c] = (pos ? pos[so] : so) + (uint32_t)(lo + lower_bound_u32(new_keys + lo, s_hi - lo, c));
 }
 
 #define HIPCHK(x)                                                               \
@@ -461,14 +471,7 @@ int grid_update(GridBuf& g, int64_t id0, bool deleted, float slack, hipStream_t 
     std::swap(g.ckeys, g.ckeys_alt);
     g.n = (int64_t)kept + n_new;
     const uint32_t nc1 = g.geom.ncells + 1;
-    uint32_t* counts = g.start + g.cells_cap;
-    HIPCHK(hipMemsetAsync(counts, 0, (size_t)nc1 * sizeof(uint32_t), st));
-    if (g.n > 0) run_count_kernel<<<(int)((g.n + 255) / 256), 256, 0, st>>>(g.ckeys, g.n, counts);
-    size_t scan_bytes = 0;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, counts, g.start, (int)nc1, st));
-    if (ensure(&g.tmp, g.tmp_bytes, scan_bytes) != 0) return -5;
-    size_t tb = g.tmp_bytes;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(g.tmp, tb, counts, g.start, (int)nc1, st));
+    start_update_kernel<<<(int)((nc1 + 255) / 256), 256, 0, st>>>(g.start, nc1, pos, nkeys, n_new);
     HIPCHK(hipGetLastError());
     return 0;
 }

@@ -122,8 +122,17 @@ __global__ void __launch_bounds__(256) voxel_resolve_kernel(const uint64_t* __re
         z0 = min(max(cell_coord(b.lo[2], g.oz, g.inv_cell), 0), g.nz - 1);
         z1 = min(max(cell_coord(nextafterf(b.hi[2], -INFINITY), g.oz, g.inv_cell), 0), g.nz - 1);
     }
+    // one pass over the box's cells: count, first nearest-to-centre point in visit order (a min over
+    // (d, visit index)), and each lane keeps its own in-box entries (up to kRec) for the tombstones,
+    // so the cells are walked again only when some lane saw more (rare: a voxel holds a few points)
+    constexpr int kRec = 2;
     int cnt_e = 0;
-    unsigned long long best = ~0ull;  // (float bits of d, visit index): first strict minimum
+    unsigned long long best = ~0ull, lbest = ~0ull;  // (float bits of d, visit index)
+    int lb_id = -1;
+    float lbx = 0.f, lby = 0.f, lbz = 0.f;
+    uint32_t rk[kRec] = {0u, 0u};
+    int rid[kRec] = {-1, -1};
+    bool ovf = false;
     uint32_t visit = 0;
     for (int z = z0; z <= z1; ++z)
         for (int y = y0; y <= y1; ++y)
@@ -133,36 +142,41 @@ __global__ void __launch_bounds__(256) voxel_resolve_kernel(const uint64_t* __re
                 for (uint32_t k = cb + (uint32_t)lane; k < ce; k += 64) {
                     const float4 p = g.pts[k];
                     if (!in_box(b, p.x, p.y, p.z)) continue;
+                    const int id = __float_as_int(p.w);
+                    if (cnt_e < kRec) {
+                        rk[cnt_e == 0 ? 0 : 1] = k;
+                        rid[cnt_e == 0 ? 0 : 1] = id;
+                    } else {
+                        ovf = true;
+                    }
                     ++cnt_e;
                     const float t = calc_dist(p.x, p.y, p.z, b.mid[0], b.mid[1], b.mid[2]);
                     const unsigned long long kk = ((unsigned long long)__float_as_uint(t) << 32) | (visit + (k - cb));
-                    best = kk < best ? kk : best;
+                    if (kk < lbest) {
+                        lbest = kk;
+                        lb_id = id;
+                        lbx = p.x;
+                        lby = p.y;
+                        lbz = p.z;
+                    }
                 }
                 visit += ce - cb;
             }
+    const int my_cnt = cnt_e;
     cnt_e = wave_sum_i32(cnt_e);
-    best = wave_min_u64(best);
-    // best's entry: re-locate by visit index (wave-uniform)
+    best = wave_min_u64(lbest);
+    const bool any_ovf = __any(ovf);
+    // best's entry: from the lane that holds it (visit indices are unique: exactly one lane)
     int best_id = -1;
     float bx = 0.f, by = 0.f, bz = 0.f, best_d = INFINITY;
     if (cnt_e > 0) {
-        uint32_t v = (uint32_t)best;
         best_d = __uint_as_float((uint32_t)(best >> 32));
-        for (int z = z0; z <= z1; ++z)
-            for (int y = y0; y <= y1; ++y)
-                for (int x = x0; x <= x1; ++x) {
-                    const uint32_t c = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
-                    const uint32_t cb = g.start[c], ce = g.start[c + 1];
-                    if (best_id < 0 && v < ce - cb) {
-                        const float4 p = g.pts[cb + v];
-                        best_id = __float_as_int(p.w);
-                        bx = p.x;
-                        by = p.y;
-                        bz = p.z;
-                    } else if (best_id < 0) {
-                        v -= ce - cb;
-                    }
-                }
+        const uint64_t wm = __ballot(lbest == best);
+        const int wl = __ffsll((unsigned long long)wm) - 1;
+        best_id = __builtin_amdgcn_readlane(lb_id, wl);
+        bx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbx), wl));
+        by = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lby), wl));
+        bz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbz), wl));
     }
     // ---- replay the run: the lanes load 64 of its points at a time (the run is
     // a prefix of the chunk: keys are sorted), every lane replays them in order
@@ -207,7 +221,18 @@ __global__ void __launch_bounds__(256) voxel_resolve_kernel(const uint64_t* __re
     }
     // ---- tombstones: every map point of the box except a surviving map point
     int dead = 0;
-    if (cnt_e > 0 && (surv_new >= 0 || cnt_e > 1)) {
+    if (cnt_e > 0 && (surv_new >= 0 || cnt_e > 1) && !any_ovf) {  // from the lanes' own records
+#pragma unroll
+        for (int r = 0; r < kRec; ++r) {
+            if (r >= my_cnt) break;
+            const int id = rid[r];
+            if (surv_new < 0 && id == best_id) continue;
+            by_id[id].w = 0.f;
+            entry_alive[rk[r]] = 0u;
+            ++dead;
+        }
+        dead = wave_sum_i32(dead);
+    } else if (cnt_e > 0 && (surv_new >= 0 || cnt_e > 1)) {
         for (int z = z0; z <= z1; ++z)
             for (int y = y0; y <= y1; ++y)
                 for (int x = x0; x <= x1; ++x) {
