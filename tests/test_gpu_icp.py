@@ -111,9 +111,11 @@ def test_icp_nn_multi_iteration_prior():
 
 
 @pytest.mark.parametrize("env", [{"LIO_ICP_KERNEL": "query"}, {"LIO_ICP_ORDER": "0"}, {"LIO_ICP_R0": "0"},
-                                 {"LIO_ICP_R0": "3"}, {"LIO_ICP_TILE_WAVES": "1"}, {"LIO_ICP_TILE_WAVES": "4"}])
+                                 {"LIO_ICP_R0": "3"}, {"LIO_ICP_TILE_WAVES": "2"}, {"LIO_ICP_TILE_WAVES": "4"},
+                                 {"LIO_ICP_TILES_PER_BLOCK": "4"}, {"LIO_ICP_TILES_PER_BLOCK": "8"}])
 def test_icp_switches_keep_exact_nn(env):
-    """The ICP A/B switches (tile order, first bound box, waves per tile) change only the
+    """The ICP A/B switches (tile order, first bound box, waves per tile — several waves splitting
+    a tile's stream with block-level merges —, several one-wave tiles per block) change only the
     search schedule: the final-pass 1-NN stays exact.  Child process (switches are read once)."""
     import os
     import subprocess
