@@ -72,30 +72,48 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
     constexpr int G = kGroup;
     constexpr int QPB = kKnnBlock / G;  // 64 queries per block
     __shared__ uint32_t s_tab[QPB][72];      // per-group shell-1 slot table
+    __shared__ float s_q[6][QPB];            // per query: world point (and the seeded pass's w_old)
     const int blk = xcd_block(blockIdx.x, gridDim.x);
     const int sub = threadIdx.x % G;
-    const int i = blk * QPB + threadIdx.x / G;
+    const int q = threadIdx.x / G;
+    const int i = blk * QPB + q;
     const unsigned long long t_beg = a.tdbg ? wall_clock64() : 0ull;
+    // the per-query transforms once per query, not once per lane of its group: wave 0, lane = query
+    if (threadIdx.x < QPB) {
+        const int iq = blk * QPB + (int)threadIdx.x;
+        if (iq < a.n) {
+            const float bx = a.body[3 * iq], by = a.body[3 * iq + 1], bz = a.body[3 * iq + 2];
+            float wx, wy, wz;
+            body_to_world(ps, bx, by, bz, wx, wy, wz);
+            s_q[0][threadIdx.x] = wx;
+            s_q[1][threadIdx.x] = wy;
+            s_q[2][threadIdx.x] = wz;
+            if constexpr (SEEDED) {
+                float wox, woy, woz;
+                if constexpr (DEV) {
+                    body_to_world(a.ctl->pose_knn, bx, by, bz, wox, woy, woz);
+                } else {  // float affine map of the previous kNN pose: w_old within ~1e-5 m, covered by the bound's margin
+                    const float* M = a.knn_M;
+                    wox = ((M[0] * bx + M[1] * by) + M[2] * bz) + M[3];
+                    woy = ((M[4] * bx + M[5] * by) + M[6] * bz) + M[7];
+                    woz = ((M[8] * bx + M[9] * by) + M[10] * bz) + M[11];
+                }
+                s_q[3][threadIdx.x] = wox;
+                s_q[4][threadIdx.x] = woy;
+                s_q[5][threadIdx.x] = woz;
+            }
+        }
+    }
+    __syncthreads();
     if (i >= a.n) return;
-    const float bx = a.body[3 * i], by = a.body[3 * i + 1], bz = a.body[3 * i + 2];
-    float wx, wy, wz;
-    body_to_world(ps, bx, by, bz, wx, wy, wz);
+    const float wx = s_q[0][q], wy = s_q[1][q], wz = s_q[2][q];
     TopK<5> tk;
     tk.init(a.range_sq);
     SearchStats st{0, 0, 0};
     bool done, whole = false;
     if constexpr (SEEDED) {  // this scan's previous kNN against the same map: the triangle bound (no re-gathers)
-        float wox, woy, woz;
-        if constexpr (DEV) {
-            body_to_world(a.ctl->pose_knn, bx, by, bz, wox, woy, woz);
-        } else {  // float affine map of the previous kNN pose: w_old within ~1e-5 m, covered by the bound's margin
-            const float* M = a.knn_M;
-            wox = ((M[0] * bx + M[1] * by) + M[2] * bz) + M[3];
-            woy = ((M[4] * bx + M[5] * by) + M[6] * bz) + M[7];
-            woz = ((M[8] * bx + M[9] * by) + M[10] * bz) + M[11];
-        }
-        const int r = group_knn_seeded<5, G, U>(a.grid, a.nn_d5[i], wox, woy, woz, wx, wy, wz, a.range_sq, a.seed_scale, sub, tk,
-                                                s_tab[threadIdx.x / G]);
+        const int r = group_knn_seeded<5, G, U>(a.grid, a.nn_d5[i], s_q[3][q], s_q[4][q], s_q[5][q], wx, wy, wz, a.range_sq,
+                                                a.seed_scale, sub, tk, s_tab[threadIdx.x / G]);
         done = r > 0;
         whole = r < 0;
     } else {
