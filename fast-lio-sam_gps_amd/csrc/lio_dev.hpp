@@ -563,11 +563,8 @@ __device__ __forceinline__ void scan_shell1_flat(const GridDev& g, float qx, flo
 // at all — queries outside the grid or unresolved after shell 1 return false
 // with their partial list and go to the far pass.
 template <int K, int G, bool TAIL = true, int U = 4>
-__device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, int max_shell, int sub, TopK<K>& tk,
-                               SearchStats* dbg, uint32_t* lds) {
-    const int cx = cell_coord(qx, g.ox, g.inv_cell);
-    const int cy = cell_coord(qy, g.oy, g.inv_cell);
-    const int cz = cell_coord(qz, g.oz, g.inv_cell);
+__device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, int cx, int cy, int cz, int max_shell,
+                               int sub, TopK<K>& tk, SearchStats* dbg, uint32_t* lds) {
     const bool inside = (unsigned)cx < (unsigned)g.nx && (unsigned)cy < (unsigned)g.ny && (unsigned)cz < (unsigned)g.nz;
     if (!inside || max_shell < 1) {
         if constexpr (TAIL) return group_knn_exact_from<K, G>(g, qx, qy, qz, 0, max_shell, sub, tk);
@@ -612,24 +609,28 @@ __device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, i
 // reset to range fillers and returns -1: the far pass then searches the whole
 // box, the 3x3x3 block included.  Returns 1 when final, 0 when the far pass
 // must search the box outside the block (group_knn_near's false).
-template <int K, int G, int U = 4>
-__device__ int group_knn_seeded(const GridDev& g, float d5prev, float wox, float woy, float woz, float qx, float qy,
-                                 float qz, float range_sq, float scale, int sub, TopK<K>& tk, uint32_t* lds) {
-    static_assert(K == 5, "group_knn_seeded: K = 5");
-    const int cx = cell_coord(qx, g.ox, g.inv_cell);
-    const int cy = cell_coord(qy, g.oy, g.inv_cell);
-    const int cz = cell_coord(qz, g.oz, g.inv_cell);
-    const bool inside = (unsigned)cx < (unsigned)g.nx && (unsigned)cy < (unsigned)g.ny && (unsigned)cz < (unsigned)g.nz;
+// The seeded pass's bound for query q (float throughout: w_old may come from a float affine map,
+// ~1e-5 m off at 100 m, and every step rounds, so the radius gets an absolute + relative margin and
+// the square a relative one); range_sq when the previous list was not full or q is outside the grid.
+__device__ __forceinline__ float seeded_bound(bool inside, float d5prev, float wox, float woy, float woz, float qx,
+                                             float qy, float qz, float range_sq, float scale) {
     float bound = range_sq;
     if (inside && d5prev <= range_sq) {  // the previous list was full
-        // float throughout: w_old may come from a float affine map (~1e-5 m off at 100 m) and every
-        // step rounds, so the radius gets an absolute + relative margin and the square a relative one
         const float dx = qx - wox, dy = qy - woy, dz = qz - woz;
         const float eps = 1e-4f + 1e-6f * ((fabsf(qx) + fabsf(qy)) + fabsf(qz));
         const float r = (sqrtf(d5prev) + sqrtf((dx * dx + dy * dy) + dz * dz)) + eps;
         const float b = r * r * (1.0f + 1e-5f);
         if (b < range_sq) bound = b * scale;  // scale: 1 (< 1 tests the guard)
     }
+    return bound;
+}
+
+// (cx, cy, cz) = the query's cell, bound = seeded_bound(...): computed once per query by the caller
+template <int K, int G, int U = 4>
+__device__ int group_knn_seeded(const GridDev& g, float bound, int cx, int cy, int cz, float qx, float qy, float qz,
+                                 float range_sq, int sub, TopK<K>& tk, uint32_t* lds) {
+    static_assert(K == 5, "group_knn_seeded: K = 5");
+    const bool inside = (unsigned)cx < (unsigned)g.nx && (unsigned)cy < (unsigned)g.ny && (unsigned)cz < (unsigned)g.nz;
     tk.init(bound);
     if (!inside) return 0;  // the far pass scans the whole box from range fillers
     uint32_t b4[shell1_cpl<G>()], n4[shell1_cpl<G>()];

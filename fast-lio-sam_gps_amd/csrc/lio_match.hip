@@ -72,7 +72,8 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
     constexpr int G = kGroup;
     constexpr int QPB = kKnnBlock / G;  // 64 queries per block
     __shared__ uint32_t s_tab[QPB][72];      // per-group shell-1 slot table
-    __shared__ float s_q[6][QPB];            // per query: world point (and the seeded pass's w_old)
+    __shared__ float s_q[4][QPB];            // per query: world point (and the seeded pass's bound)
+    __shared__ int s_c[3][QPB];              //            its cell
     const int blk = xcd_block(blockIdx.x, gridDim.x);
     const int sub = threadIdx.x % G;
     const int q = threadIdx.x / G;
@@ -88,6 +89,12 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
             s_q[0][threadIdx.x] = wx;
             s_q[1][threadIdx.x] = wy;
             s_q[2][threadIdx.x] = wz;
+            const int cx = cell_coord(wx, a.grid.ox, a.grid.inv_cell);
+            const int cy = cell_coord(wy, a.grid.oy, a.grid.inv_cell);
+            const int cz = cell_coord(wz, a.grid.oz, a.grid.inv_cell);
+            s_c[0][threadIdx.x] = cx;
+            s_c[1][threadIdx.x] = cy;
+            s_c[2][threadIdx.x] = cz;
             if constexpr (SEEDED) {
                 float wox, woy, woz;
                 if constexpr (DEV) {
@@ -98,9 +105,9 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
                     woy = ((M[4] * bx + M[5] * by) + M[6] * bz) + M[7];
                     woz = ((M[8] * bx + M[9] * by) + M[10] * bz) + M[11];
                 }
-                s_q[3][threadIdx.x] = wox;
-                s_q[4][threadIdx.x] = woy;
-                s_q[5][threadIdx.x] = woz;
+                const bool inside = (unsigned)cx < (unsigned)a.grid.nx && (unsigned)cy < (unsigned)a.grid.ny &&
+                                    (unsigned)cz < (unsigned)a.grid.nz;
+                s_q[3][threadIdx.x] = seeded_bound(inside, a.nn_d5[iq], wox, woy, woz, wx, wy, wz, a.range_sq, a.seed_scale);
             }
         }
     }
@@ -112,12 +119,13 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
     SearchStats st{0, 0, 0};
     bool done, whole = false;
     if constexpr (SEEDED) {  // this scan's previous kNN against the same map: the triangle bound (no re-gathers)
-        const int r = group_knn_seeded<5, G, U>(a.grid, a.nn_d5[i], s_q[3][q], s_q[4][q], s_q[5][q], wx, wy, wz, a.range_sq,
-                                                a.seed_scale, sub, tk, s_tab[threadIdx.x / G]);
+        const int r = group_knn_seeded<5, G, U>(a.grid, s_q[3][q], s_c[0][q], s_c[1][q], s_c[2][q], wx, wy, wz, a.range_sq, sub,
+                                                tk, s_tab[threadIdx.x / G]);
         done = r > 0;
         whole = r < 0;
     } else {
-        done = group_knn_near<5, G, false, U>(a.grid, wx, wy, wz, 1, sub, tk, DBG ? &st : nullptr, s_tab[threadIdx.x / G]);
+        done = group_knn_near<5, G, false, U>(a.grid, wx, wy, wz, s_c[0][q], s_c[1][q], s_c[2][q], 1, sub, tk,
+                                              DBG ? &st : nullptr, s_tab[threadIdx.x / G]);
     }
     const bool far = !done && a.max_shell > 1;
     if constexpr (DBG) {
