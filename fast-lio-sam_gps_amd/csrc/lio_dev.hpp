@@ -127,6 +127,20 @@ __device__ __forceinline__ void sqdist3_x2(float qx, float qy, float qz, const f
     db = d.y;
 }
 
+// a bitonic 5-list sorted in place (5 comparators suffice for bitonic inputs, 0-1 principle)
+__device__ __forceinline__ void sort_bitonic5(uint64_t (&v)[5]) {
+    auto cx = [&](int i, int j) {
+        const uint64_t x = v[i], y = v[j];
+        v[i] = key_min(x, y);
+        v[j] = key_max(x, y);
+    };
+    cx(0, 4);
+    cx(1, 3);
+    cx(1, 4);
+    cx(2, 4);
+    cx(3, 4);
+}
+
 template <int K>
 struct TopK {
     uint64_t k[K];
@@ -147,6 +161,18 @@ struct TopK {
 #pragma unroll
         for (int j = K - 1; j > 0; --j) k[j] = key_min(k[j], key_max(k[j - 1], x));
         k[0] = key_min(k[0], x);
+    }
+    // two candidates at once (K = 5): order them (one comparator), keep the 5 smallest of the two
+    // sorted lists — min(a[j], b[4 - j]) touches a[3], a[4] only, a bitonic sequence — and sort that
+    // (5 comparators): 14 min / max instead of up to 2 x 9 for two single insertions; same list
+    __device__ __forceinline__ void push2(uint64_t b0, uint64_t b1) {
+        static_assert(K == 5, "push2: K = 5");
+        const uint64_t lo = key_min(b0, b1);
+        if (!(lo < k[K - 1])) return;
+        const uint64_t hi = key_max(b0, b1);
+        k[4] = key_min(k[4], lo);
+        k[3] = key_min(k[3], hi);
+        sort_bitonic5(k);
     }
     // every slot := the K-th entry (a filler that is never re-inserted)
     __device__ __forceinline__ void fill_with_worst() {
@@ -534,8 +560,11 @@ __device__ __forceinline__ void scan_table_strided(const GridDev& g, float qx, f
         for (int u = 0; u < U; u += 2) {
             float d0, d1;
             sqdist3_x2(qx, qy, qz, p[u], p[u + 1], d0, d1);
-            if (t + (uint32_t)u * L < T) tk.push(d0, __float_as_int(p[u].w));
-            if (t + (uint32_t)(u + 1) * L < T) tk.push(d1, __float_as_int(p[u + 1].w));
+            // slots past the end: (+inf, kNone) keys, never below a list entry (not NaN patterns, which
+            // v_min / v_max_f64 would drop)
+            const bool in0 = t + (uint32_t)u * L < T, in1 = t + (uint32_t)(u + 1) * L < T;
+            tk.push2(knn_key(in0 ? d0 : INFINITY, in0 ? __float_as_int(p[u].w) : kNone),
+                     knn_key(in1 ? d1 : INFINITY, in1 ? __float_as_int(p[u + 1].w) : kNone));
         }
     }
 }
