@@ -300,8 +300,14 @@ __device__ __forceinline__ void scan_cell_group2(const GridDev& g, uint32_t c, f
         for (int u = 0; u < U; u += 2) {
             float d0, d1;
             sqdist3_x2(qx, qy, qz, p[u], p[u + 1], d0, d1);
-            if (j + (uint32_t)(u * G) < e) tk.push(d0, __float_as_int(p[u].w));
-            if (j + (uint32_t)((u + 1) * G) < e) tk.push(d1, __float_as_int(p[u + 1].w));
+            const bool in0 = j + (uint32_t)(u * G) < e, in1 = j + (uint32_t)((u + 1) * G) < e;
+            if constexpr (K == 5) {  // pairwise insertion; slots past the cell: (+inf, kNone) keys
+                tk.push2(knn_key(in0 ? d0 : INFINITY, in0 ? __float_as_int(p[u].w) : kNone),
+                         knn_key(in1 ? d1 : INFINITY, in1 ? __float_as_int(p[u + 1].w) : kNone));
+            } else {
+                if (in0) tk.push(d0, __float_as_int(p[u].w));
+                if (in1) tk.push(d1, __float_as_int(p[u + 1].w));
+            }
         }
     }
 }
