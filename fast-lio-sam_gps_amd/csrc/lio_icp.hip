@@ -41,10 +41,12 @@ __device__ __forceinline__ void xform_pcl(const float* T, float x, float y, floa
 // (icp_build_tiles): a tile is <= 64 source points of one cell, so its
 // bounding box Q is compact.  The target grid is x-fastest, so a row of cells
 // (fixed y, z) is ONE contiguous range of points: the wave works on rows,
-// one lane per row, and every range goes through the same staging step
-// (scan_ranges: wave prefix sum -> LDS chunks -> every lane tests every
-// staged point against its own query, LDS broadcast reads), so the candidate
-// points are loaded once per tile instead of once per query.
+// one lane per row (a batch of rows re-ordered nearest-first), and every range
+// goes through the same staging step (scan_ranges: wave prefix sum -> chunks
+// of 256 points, those farther from Q than every lane's current best dropped,
+// the rest compacted into LDS -> every lane tests every staged point against
+// its own query, LDS broadcast reads), so the candidate points are loaded once
+// per tile instead of once per query.
 //   1. bound: a lane starts from its previous correspondence when the pass
 //      has one (an exact candidate: its distance bounds the answer), else
 //      the rows of Q's own cells are scanned; while some lane has found
