@@ -203,8 +203,11 @@ def main():
     barrier()
     t_start = time.perf_counter()
     capi_ms = launch_ms = wait_ms = solve_ms = 0.0
+    t_steps = []
     for k in range(args.steps):
+        t_k = time.perf_counter()
         st = step(k)
+        t_steps.append(time.perf_counter() - t_k)
         capi_ms += st.wall_ms
         launch_ms += st.launch_ms
         wait_ms += st.wait_ms
@@ -464,6 +467,8 @@ def main():
                        "scan_points": sp, "map_points": mp, "resident_scans": len(scans),
                        "parallelism": f"replicas x{world} (front end does not shard)"},
             "ms_per_ieskf_iteration": round(ms_per_iter, 4),
+            "ms_per_step_pct": {q: round(float(np.percentile(t_steps, int(q[1:]))) * 1e3, 4)
+                                for q in ("p10", "p50", "p90", "p99")},  # this rank's per-step spread
             "capi_ms_per_scan": round(capi_ms / args.steps, 4),
             "host_ms_per_scan": {"launch": round(launch_ms / args.steps, 4), "wait": round(wait_ms / args.steps, 4),
                                  "ieskf_algebra": round(solve_ms / args.steps, 4)},
