@@ -1,66 +1,97 @@
-// Launch-path microbenchmark: per-evaluation host cost and round trip of
-// (a) 4 direct launches vs (b) one hipGraph of the same 4 kernels, each
-// followed by a zero-copy completion flag poll (as lio_match does).
+// Host cost of one kernel launch with a MatchArgs-sized (512 B) argument, and the decision -> kernel-start
+// latency, for the launch forms the front end could use (diagnostics for DESIGN §8):
+//   A. triple-chevron                      B. hipExtLaunchKernelGGL, null events (what lio_match does)
+//   C. hipModuleLaunchKernel on a hipFunction_t cached by hipGetFuncBySymbol (kernelParams)
+//   D. as C with the argument buffer passed through `extra` (HIP_LAUNCH_PARAM_BUFFER_POINTER)
+// Each: median host microseconds per launch call (1000 back-to-back launches of a 1-block kernel, the
+// queue drained between batches of 100), then a round trip: launch -> kernel writes a host-mapped
+// flag -> host sees it.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
+
+#include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <vector>
 
-struct Args { double pose[24]; const float* p[12]; int n; };
+struct Big {
+    unsigned long long* flag;
+    unsigned long long seq;
+    float pad[124];
+};
 
-__global__ void k_work(Args a, float* out) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < a.n) out[i] = out[i] * 0.5f + (float)a.pose[i % 24];
+typedef __attribute__((address_space(1))) unsigned long long gull;
+
+__global__ void k_big(Big a) {
+    if (threadIdx.x == 0 && a.flag) __hip_atomic_store((gull*)a.flag, a.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-__global__ void k_flag(volatile unsigned long long* flag, unsigned long long seq) {
-    if (threadIdx.x == 0) { __threadfence_system(); *flag = seq; }
+
+using clk = std::chrono::steady_clock;
+static double us(clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); }
+static double median(std::vector<double> v) {
+    std::sort(v.begin(), v.end());
+    return v[v.size() / 2];
 }
 
 int main() {
-    hipStream_t st; hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
-    float* buf; hipMalloc(&buf, 65536 * sizeof(float)); hipMemset(buf, 0, 65536 * sizeof(float));
-    unsigned long long* hflag; hipHostMalloc(&hflag, 64, hipHostMallocMapped | hipHostMallocCoherent);
-    unsigned long long* dflag; hipHostGetDevicePointer((void**)&dflag, hflag, 0);
-    *hflag = 0;
-    Args a{}; a.n = 65536;
-    using clk = std::chrono::steady_clock;
-    const int N = 2000;
-    unsigned long long seq = 0;
-    auto wait = [&](unsigned long long s) { while (*(volatile unsigned long long*)hflag != s) {} };
-    for (int mode = 0; mode < 2; ++mode) {
-        hipGraphExec_t ge = nullptr;
-        if (mode == 1) {
-            hipGraph_t g;
-            hipStreamBeginCapture(st, hipStreamCaptureModeGlobal);
-            k_work<<<256, 256, 0, st>>>(a, buf);
-            k_work<<<256, 256, 0, st>>>(a, buf);
-            k_work<<<256, 256, 0, st>>>(a, buf);
-            k_flag<<<1, 64, 0, st>>>(dflag, 0);  // seq patched below via node params is costly; use a counter
-            hipStreamEndCapture(st, &g);
-            hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    hipStream_t st;
+    (void)hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    unsigned long long *h, *d;
+    (void)hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent);
+    (void)hipHostGetDevicePointer((void**)&d, h, 0);
+    volatile unsigned long long* hv = h;
+    *hv = 0;
+    hipFunction_t f = nullptr;
+    if (hipGetFuncBySymbol(&f, reinterpret_cast<const void*>(&k_big)) != hipSuccess) {
+        std::printf("hipGetFuncBySymbol failed\n");
+        return 1;
+    }
+    Big a{};
+    a.flag = nullptr;
+    auto launch = [&](int form) {
+        switch (form) {
+        case 0: k_big<<<1, 64, 0, st>>>(a); break;
+        case 1: hipExtLaunchKernelGGL(k_big, dim3(1), dim3(64), 0, st, nullptr, nullptr, 0, a); break;
+        case 2: {
+            void* params[] = {&a};
+            (void)hipModuleLaunchKernel(f, 1, 1, 1, 64, 1, 1, 0, st, params, nullptr);
+            break;
         }
-        double launch = 0, total = 0;
-        for (int it = 0; it < N + 100; ++it) {
+        default: {
+            size_t sz = sizeof(a);
+            void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+            (void)hipModuleLaunchKernel(f, 1, 1, 1, 64, 1, 1, 0, st, nullptr, extra);
+        }
+        }
+    };
+    const char* names[] = {"A <<<>>>", "B hipExtLaunchKernelGGL", "C hipModuleLaunchKernel params", "D hipModuleLaunchKernel extra"};
+    for (int form = 0; form < 4; ++form) {
+        for (int w = 0; w < 200; ++w) launch(form);
+        (void)hipStreamSynchronize(st);
+        std::vector<double> per;
+        for (int b = 0; b < 10; ++b) {
+            for (int i = 0; i < 100; ++i) {
+                const auto t0 = clk::now();
+                launch(form);
+                per.push_back(us(t0, clk::now()));
+            }
+            (void)hipStreamSynchronize(st);
+        }
+        // round trip from an idle queue
+        std::vector<double> rt;
+        a.flag = d;
+        for (int i = 0; i < 500; ++i) {
+            a.seq = (unsigned long long)(form * 1000000 + i + 1);
             const auto t0 = clk::now();
-            ++seq;
-            if (mode == 0) {
-                k_work<<<256, 256, 0, st>>>(a, buf);
-                k_work<<<256, 256, 0, st>>>(a, buf);
-                k_work<<<256, 256, 0, st>>>(a, buf);
-                k_flag<<<1, 64, 0, st>>>(dflag, seq);
-            } else {
-                *hflag = 1;  // graph writes 0
-                hipGraphLaunch(ge, st);
+            launch(form);
+            while (*hv != a.seq) {
             }
-            const auto t1 = clk::now();
-            if (mode == 0) wait(seq); else { while (*(volatile unsigned long long*)hflag != 0) {} }
-            const auto t2 = clk::now();
-            if (it >= 100) {
-                launch += std::chrono::duration<double, std::micro>(t1 - t0).count();
-                total += std::chrono::duration<double, std::micro>(t2 - t0).count();
-            }
+            if (i > 50) rt.push_back(us(t0, clk::now()));
+            (void)hipStreamSynchronize(st);
         }
-        std::printf("%s: launch %.2f us, round trip %.2f us per evaluation\n", mode ? "graph " : "direct", launch / N,
-                    total / N);
+        a.flag = nullptr;
+        std::printf("%-34s launch call median %6.2f us   launch -> kernel flag median %6.2f us\n", names[form], median(per),
+                    median(rt));
     }
     return 0;
 }
