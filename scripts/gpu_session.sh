@@ -78,6 +78,10 @@ for s in $STEPS; do
     icptimes) LIO_ICP_TIMES=1 run icp_times 300 python scripts/icp_ab.py 1.0 1 &&
            LIO_ICP_TIMES=1 LIO_ICP_ORDER=0 run icp_times_o0 300 python scripts/icp_ab.py 1.0 1 ;;
     icptpb) for t in 1 2 4 8; do LIO_ICP_TILES_PER_BLOCK=$t run icp_tpb$t 300 python scripts/icp_ab.py 1.0 || exit 1; done ;;
+    icppmc2) run icp_trace 300 rocprofv3 --kernel-trace -d "$OUT/icptrace" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
+             run icp_pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_BUSY_CYCLES --kernel-trace -d "$OUT/icpsq" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
+             run icp_pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/icpfetch" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
+             run icp_pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/icpwrite" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 ;;
     icpprof) run icp_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/icpprof" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
              run icp_pmc_valu 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --kernel-trace -d "$OUT/icppmc" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 ;;
     *) echo "unknown step $s" ;;
