@@ -164,12 +164,28 @@ def main():
     st_c = type(F._capi.IeskfStats())()
     ptrs = [(d.data_ptr(), len(s.body)) for d, s in zip(d_scans, scans)]
 
+    # the C-ABI calls with their arguments prepared once (what a C++ caller's loop passes): bind the
+    # resident scan, reset state and covariance, one full lio_ieskf_update
+    lib_ = F._capi.lib()
+    s_addr, s_size = ctypes.addressof(s_c), ctypes.sizeof(s_c)
+    init_addr = [ctypes.addressof(c) for c in init_c]
+    P0_c = np.ascontiguousarray(P0, dtype=np.float64)
+    P_addr, P0_addr, P_bytes = P_c.ctypes.data, P0_c.ctypes.data, P_c.nbytes
+    bind_args = [(hm._h, ctypes.c_void_p(p), n) for p, n in ptrs]
+    upd_args = (kf.model._h, ctypes.byref(s_c), P_c.ctypes.data_as(ctypes.POINTER(ctypes.c_double)),
+                ctypes.byref(kf.params), ctypes.byref(st_c))
+    bind_fn, upd_fn, memmove = lib_.lio_scan_bind_device, lib_.lio_ieskf_update, ctypes.memmove
+
     def step(k):
         j = k % len(scans)
-        hm.bind_scan_device(*ptrs[j])  # scans stay resident in HBM (torch tensors)
-        ctypes.pointer(s_c)[0] = init_c[j]
-        np.copyto(P_c, P0)
-        kf.update_raw(s_c, P_c, st_c)
+        rc = bind_fn(*bind_args[j])  # scans stay resident in HBM (torch tensors)
+        if rc:
+            F.check(rc)
+        memmove(s_addr, init_addr[j], s_size)
+        memmove(P_addr, P0_addr, P_bytes)
+        rc = upd_fn(*upd_args)
+        if rc:
+            F.check(rc)
         return st_c
 
     # C3/C5: the map is grown through the insert path (FAST-LIO map_incremental
