@@ -293,7 +293,7 @@ int update_iterated(State& x, Mat& P, double R, int max_iter, double epsi, const
     using clk = std::chrono::steady_clock;
     const State x_prop = x;
     const Mat P_prop = P;
-    Mat K_x((size_t)N * N, 0.0);
+    Mat K_x((size_t)N * N, 0.0), Mm(36);
     double K_h[N], dx_new[N], dxu[N];
     bool converge = true;
     int t = 0;
@@ -384,11 +384,16 @@ int update_iterated(State& x, Mat& P, double R, int max_iter, double epsi, const
             // arithmetic; the IESKF parity bar is a tolerance).
             double HTH[36];
             unpack_hth(hm.sums, HTH);
-            Mat Mm(36);
+            // A = P / R on the first 6 columns, each element divided once (the same values the
+            // products below used when they divided inline)
+            double PR[N * 6];
+            for (int r = 0; r < N; ++r)
+                for (int m = 0; m < 6; ++m) PR[r * 6 + m] = P[(size_t)r * N + m] / R;
+            Mm.assign(36, 0.0);
             for (int a = 0; a < 6; ++a)
                 for (int b = 0; b < 6; ++b) {
                     double s = 0;
-                    for (int m = 0; m < 6; ++m) s += HTH[6 * a + m] * (P[(size_t)m * N + b] / R);
+                    for (int m = 0; m < 6; ++m) s += HTH[6 * a + m] * PR[m * 6 + b];
                     Mm[(size_t)a * 6 + b] = s + (a == b ? 1.0 : 0.0);
                 }
             if (!lu_inverse(Mm, 6)) return -4;
@@ -396,7 +401,7 @@ int update_iterated(State& x, Mat& P, double R, int max_iter, double epsi, const
                 double q[6];
                 for (int c = 0; c < 6; ++c) {
                     double s = 0;
-                    for (int m = 0; m < 6; ++m) s += (P[(size_t)r * N + m] / R) * Mm[(size_t)m * 6 + c];
+                    for (int m = 0; m < 6; ++m) s += PR[r * 6 + m] * Mm[(size_t)m * 6 + c];
                     q[c] = s;
                 }
                 double kh = 0;
@@ -409,9 +414,12 @@ int update_iterated(State& x, Mat& P, double R, int max_iter, double epsi, const
                 }
             }
         }
+        // (K_x - I) dx_new: K_x is zero outside its first 6 columns, so the rest of row r contributes
+        // exact zeros and -dx_new[r] (same sum, the zero terms skipped)
         for (int r = 0; r < N; ++r) {
             double s = 0;
-            for (int c = 0; c < N; ++c) s += (K_x[(size_t)r * N + c] - (r == c ? 1.0 : 0.0)) * dx_new[c];
+            for (int c = 0; c < 6; ++c) s += (K_x[(size_t)r * N + c] - (r == c ? 1.0 : 0.0)) * dx_new[c];
+            if (r >= 6) s += -dx_new[r];
             dxu[r] = K_h[r] + s;
         }
         boxplus(x, dxu);
@@ -441,10 +449,12 @@ int update_iterated(State& x, Mat& P, double R, int max_iter, double epsi, const
                 cols_apply(P, N, N, kS2, T2, 2);
             }
             Mat Pn((size_t)N * N);
+            // K_x columns 6..11 stay zero (the block transforms above mix rows only): their terms are
+            // exact zeros, skipped
             for (int r = 0; r < N; ++r)
                 for (int c = 0; c < N; ++c) {
                     double s = 0;
-                    for (int m = 0; m < 12; ++m) s += K_x[(size_t)r * N + m] * P[(size_t)m * N + c];
+                    for (int m = 0; m < 6; ++m) s += K_x[(size_t)r * N + m] * P[(size_t)m * N + c];
                     Pn[(size_t)r * N + c] = L[(size_t)r * N + c] - s;
                 }
             P.swap(Pn);
