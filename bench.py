@@ -426,12 +426,15 @@ def main():
         passes = itm["icp_launches"]
         shard_n = len(src) // world
         icp_kernel_ms = itm["icp_ms"] / max(passes, 1)
+        nn_ms = itm["icp_nn_ms"] / max(itm["icp_nn_launches"], 1)
         loop_icp = {"config": "C4: 500k vs 500k, voxel 0.3 m, 2.5 m / 4 deg initial offset, PCL ICP semantics",
                     "n_gpus": world, "passes_per_alignment": passes / max(args.icp_reps, 1),
                     "ms_per_alignment": round(icp_s / args.icp_reps * 1e3, 3),
                     "iterations": r.iterations, "ms_per_iteration": round(icp_s / max(iters, 1) * 1e3, 3),
                     "score": r.score, "converged": bool(r.is_converged), "scaling": "strong",
+                    # the pass (correspondence + statistics kernels) and the correspondence kernel alone
                     "kernel_ms_per_pass": round(icp_kernel_ms, 4),
+                    "nn_kernel_ms_per_pass": round(nn_ms, 4),
                     "kernel_gbs": round(BYTES_PER_PT_ICP * shard_n / (icp_kernel_ms * 1e-3) / 1e9, 2)
                     if passes else None}
 

@@ -125,6 +125,7 @@ void umeyama(const double* st, const double c0[3], float Ti[16]) {
 
 struct EvPair {
     hipEvent_t a = nullptr, b = nullptr;
+    hipEvent_t m = nullptr;     // between the correspondence and statistics kernels
     hipEvent_t done = nullptr;  // a pass's statistics have reached the host
 };
 
@@ -210,6 +211,7 @@ int lio_icp_create(const lio_icp_params* p, lio_icp** out) {
     }
     (void)hipEventCreate(&h->ev.a);
     (void)hipEventCreate(&h->ev.b);
+    (void)hipEventCreate(&h->ev.m);
     (void)hipEventCreateWithFlags(&h->ev.done, hipEventDisableTiming);
     *out = h;
     return LIO_OK;
@@ -227,6 +229,7 @@ int lio_icp_destroy(lio_icp* h) {
     if (h->h_super) (void)hipHostFree(h->h_super);
     if (h->ev.a) (void)hipEventDestroy(h->ev.a);
     if (h->ev.b) (void)hipEventDestroy(h->ev.b);
+    if (h->ev.m) (void)hipEventDestroy(h->ev.m);
     if (h->ev.done) (void)hipEventDestroy(h->ev.done);
     (void)hipStreamDestroy(h->st);
     delete h;
@@ -389,6 +392,7 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
             lio::launch_icp_tiles(a, h->ntiles, h->st);
         else
             lio::launch_icp_query(a, h->st);
+        if (h->timing) IHIP(hipEventRecord(h->ev.m, h->st));
         lio::launch_icp_stats(a, h->h_super_dev, h->st);  // records straight to host memory
         if (h->timing) IHIP(hipEventRecord(h->ev.b, h->st));
         IHIP(hipGetLastError());
@@ -440,6 +444,10 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
         if (hipEventElapsedTime(&ms, h->ev.a, h->ev.b) == hipSuccess) {
             h->tm.icp_ms += ms;
             ++h->tm.icp_launches;
+        }
+        if (hipEventElapsedTime(&ms, h->ev.a, h->ev.m) == hipSuccess) {
+            h->tm.icp_nn_ms += ms;
+            ++h->tm.icp_nn_launches;
         }
     }
     for (int k = 0; k < 17; ++k) out17[k] = 0.0;

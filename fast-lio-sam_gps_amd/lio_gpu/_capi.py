@@ -119,7 +119,8 @@ class KernelTiming(C.Structure):
                 ("reuse_ms", C.c_double), ("final_launches", C.c_int64), ("final_ms", C.c_double),
                 ("icp_launches", C.c_int64), ("icp_ms", C.c_double), ("near_launches", C.c_int64),
                 ("near_ms", C.c_double), ("far_launches", C.c_int64), ("far_ms", C.c_double),
-                ("plane_launches", C.c_int64), ("plane_ms", C.c_double)]
+                ("plane_launches", C.c_int64), ("plane_ms", C.c_double),
+                ("icp_nn_launches", C.c_int64), ("icp_nn_ms", C.c_double)]
 
 
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double), C.c_void_p)

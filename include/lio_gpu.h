@@ -391,12 +391,14 @@ typedef struct lio_kernel_timing {
     int64_t near_launches;  double near_ms;    /* kNN near pass (inside knn_ms)                */
     int64_t far_launches;   double far_ms;     /* kNN far pass (inside knn_ms)                 */
     int64_t plane_launches; double plane_ms;   /* plane / H / reduction pass (inside knn_ms)   */
+    int64_t icp_nn_launches; double icp_nn_ms; /* ICP correspondence kernel alone (inside icp_ms) */
 } lio_kernel_timing;
 
 /* When enabled, every front-end kernel is launched with hipExtLaunchKernel's
  * start / stop events — the kernel's own execution span, as rocprofv3 reports
  * it (no launch gaps) — and the spans accumulate here (knn_ms = near + far +
- * plane).  The ICP handle brackets its pass (both kernels) with events.    */
+ * plane).  The ICP handle brackets its pass (both kernels) with events, and its
+ * correspondence kernel alone (icp_nn_ms).                                    */
 int lio_ctx_set_timing(lio_ctx* c, int enable);
 int lio_ctx_get_timing(lio_ctx* c, lio_kernel_timing* out);
 int lio_ctx_reset_timing(lio_ctx* c);
