@@ -35,7 +35,7 @@ constexpr int kBlock = 256;  // plane / reuse: 1 point per lane (1024-thread blo
 
 constexpr int kGroup = 8;   // lanes cooperating on one query's kNN
 constexpr int kKnnBlock = 512;
-constexpr int kFarBlock = 256;
+constexpr int kFarBlock = 128;  // threads per far query (64 / 256 / 512: LIO_FAR_THREADS, measured slower)
 constexpr int kFarBlocks = 1024;  // blocks striding the far queue (one query per block)
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -179,13 +179,13 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
 // Pass 2: the queued queries, one block each (block_knn_box_flat over the
 // rest of the query's search box).  Fixed grid; every block strides the queue
 // and exits once past its end.
-template <bool DEV = false>
-__global__ void __launch_bounds__(kFarBlock) knn_far_kernel(MatchArgs a) {
+template <bool DEV = false, int NT = kFarBlock>
+__global__ void __launch_bounds__(NT) knn_far_kernel(MatchArgs a) {
     if constexpr (DEV)
         if (a.ctl->done || !a.ctl->converge) return;
     const PoseArg& ps = DEV ? a.ctl->pose : a.pose;
-    __shared__ uint32_t s_b[kFarBlock], s_off[kFarBlock + 1], s_w[kFarBlock / 64];
-    __shared__ uint64_t s_lists[(kFarBlock / 64) * 5];
+    __shared__ uint32_t s_b[NT], s_off[NT + 1], s_w[NT / 64];
+    __shared__ uint64_t s_lists[(NT / 64) * 5];
     const int cnt = *a.far_count;
     for (int f = blockIdx.x; f < cnt; f += gridDim.x) {
         const int e = a.far_list[f];
@@ -195,7 +195,7 @@ __global__ void __launch_bounds__(kFarBlock) knn_far_kernel(MatchArgs a) {
         TopK<5> tk;
 #pragma unroll
         for (int j = 0; j < 5; ++j) tk.k[j] = knn_key(a.far_d[5 * (size_t)f + j], a.far_id[5 * (size_t)f + j]);
-        block_knn_box_flat<5, kFarBlock>(a.grid, wx, wy, wz, s_b, s_off, s_w, s_lists, tk, e < 0);
+        block_knn_box_flat<5, NT>(a.grid, wx, wy, wz, s_b, s_off, s_w, s_lists, tk, e < 0);
         if (threadIdx.x == 0) {
 #pragma unroll
             for (int j = 0; j < 5; ++j) a.nn_idx[5 * (size_t)i + j] = tk.id(j) == kNone ? -1 : tk.id(j);
@@ -724,8 +724,20 @@ int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* ma
             const int v = e ? std::atoi(e) : 0;
             return v > 0 ? std::min(v, 4096) : kFarBlocks;
         }();
-        if (a.max_shell > 1)
-            hipExtLaunchKernelGGL(knn_far_kernel<false>, dim3(far_blocks), dim3(kFarBlock), 0, st, m[2], m[3], 0, a);
+        static const int far_nt = [] {  // LIO_FAR_THREADS: threads per far query (diagnostics: 64 / 256 / 512)
+            const char* e = std::getenv("LIO_FAR_THREADS");
+            return e ? std::atoi(e) : kFarBlock;
+        }();
+        if (a.max_shell > 1) {
+            if (far_nt == 64)
+                hipExtLaunchKernelGGL((knn_far_kernel<false, 64>), dim3(far_blocks), dim3(64), 0, st, m[2], m[3], 0, a);
+            else if (far_nt == 256)
+                hipExtLaunchKernelGGL((knn_far_kernel<false, 256>), dim3(far_blocks), dim3(256), 0, st, m[2], m[3], 0, a);
+            else if (far_nt == 512)
+                hipExtLaunchKernelGGL((knn_far_kernel<false, 512>), dim3(far_blocks), dim3(512), 0, st, m[2], m[3], 0, a);
+            else
+                hipExtLaunchKernelGGL(knn_far_kernel<false>, dim3(far_blocks), dim3(kFarBlock), 0, st, m[2], m[3], 0, a);
+        }
         if (ppl == 4)
             hipExtLaunchKernelGGL(plane_kernel<4>, dim3(nb), dim3(kBlock), 0, st, m[4], m[5], 0, a);
         else if (ppl == 2)
