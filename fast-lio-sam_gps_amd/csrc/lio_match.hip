@@ -251,6 +251,7 @@ __device__ __forceinline__ void publish_host(double t, double* out, unsigned lon
 // return value).  fused_final == 0: partial only, the finalize launch sums.
 // slot: this block's partial index (-1: none); npart partials are summed; ncount
 // blocks take part in the counter.  All threads of the block call it.
+template <int BS = kBlock>
 __device__ __forceinline__ bool block_partial_last(const MatchArgs& a, double (*red)[32], double& t, int slot, int npart,
                                                    int ncount) {
     __shared__ int s_last;
@@ -260,7 +261,7 @@ __device__ __forceinline__ bool block_partial_last(const MatchArgs& a, double (*
         if (threadIdx.x < 32) {
             double s = 0.0;
 #pragma unroll
-            for (int w = 0; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
+            for (int w = 0; w < BS / 64; ++w) s += red[w][threadIdx.x];
             a.partials[(size_t)blockIdx.x * 32 + threadIdx.x] = s;
         }
         return false;
@@ -268,7 +269,7 @@ __device__ __forceinline__ bool block_partial_last(const MatchArgs& a, double (*
     if (slot >= 0 && threadIdx.x < 32) {
         double s = 0.0;
 #pragma unroll
-        for (int w = 0; w < kBlock / 64; ++w) s += red[w][threadIdx.x];
+        for (int w = 0; w < BS / 64; ++w) s += red[w][threadIdx.x];
         __hip_atomic_store((gdouble*)(a.partials + (size_t)slot * 32 + threadIdx.x), s, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the storing wave drains
@@ -282,7 +283,7 @@ __device__ __forceinline__ bool block_partial_last(const MatchArgs& a, double (*
     if (!s_last) return false;  // block-uniform
     // fixed-order sum: 8 row groups x 32 columns, then the groups in order
     const int col = threadIdx.x & 31, grp = threadIdx.x >> 5;
-    constexpr int NG = kBlock / 32;
+    constexpr int NG = BS / 32;
     const int per = (nb + NG - 1) / NG;
     const int b0 = grp * per, b1 = min(nb, b0 + per);
     double acc = 0.0;
@@ -312,9 +313,10 @@ __device__ __forceinline__ bool block_partial_last(const MatchArgs& a, double (*
 }
 
 // the last block publishes the sums to the host (lio_match)
+template <int BS = kBlock>
 __device__ __forceinline__ void publish_and_finalize(const MatchArgs& a, double (*red)[32]) {
     double t;
-    if (block_partial_last(a, red, t, blockIdx.x, gridDim.x, gridDim.x) && threadIdx.x < 64)
+    if (block_partial_last<BS>(a, red, t, blockIdx.x, gridDim.x, gridDim.x) && threadIdx.x < 64)
         publish_host(t, a.sums_out, a.seq_out, a.seq);
 }
 
@@ -344,16 +346,27 @@ static int ppl_setting() {
     return v;
 }
 
+// Threads per plane / reuse block on the host-loop path (LIO_MATCH_BLOCK = 256 or 512; 512 with
+// PPL 1 or 2): BS * PPL points per block partial.
+static int match_block_setting() {
+    static const int v = [] {
+        const char* e = std::getenv("LIO_MATCH_BLOCK");
+        const int b = e ? std::atoi(e) : kBlock;
+        return (b == 512 && ppl_setting() <= 2) ? 512 : kBlock;
+    }();
+    return v;
+}
+
 // Plane pass body, lane = PPL points (strided by the block size, coalesced): gate
 // (found == 5 && d2[4] <= 5), esti_plane, pd2, s-gate, H row, summed into v.
-template <int PPL>
+template <int PPL, int BS = kBlock>
 __device__ __forceinline__ void plane_points(const MatchArgs& a, const PoseArg& ps, int blk, double (&v)[32]) {
-    const int i0 = blk * kBlock * PPL + threadIdx.x;
+    const int i0 = blk * BS * PPL + threadIdx.x;
     // all points' ids first, then all neighbour gathers: PPL independent chains in flight
     int id[PPL][5];
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
-        const int i = i0 + k * kBlock;
+        const int i = i0 + k * BS;
 #pragma unroll
         for (int j = 0; j < 5; ++j) id[k][j] = i < a.n ? a.nn_idx[5 * (size_t)i + j] : -1;
     }
@@ -370,7 +383,7 @@ __device__ __forceinline__ void plane_points(const MatchArgs& a, const PoseArg& 
             }
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
-        const int i = i0 + k * kBlock;
+        const int i = i0 + k * BS;
         if (i < a.n) {
             // sorted list: the 5th exists => all exist, d2 <= range by construction
             bool sel = id[k][4] >= 0;
@@ -394,16 +407,16 @@ __device__ __forceinline__ void plane_points(const MatchArgs& a, const PoseArg& 
 }
 
 // Reuse pass body (ekfom_data.converge == false: cached Nearest_Points / planes), PPL points per lane.
-template <int PPL>
+template <int PPL, int BS = kBlock>
 __device__ __forceinline__ void reuse_points(const MatchArgs& a, const PoseArg& ps, int blk, double (&v)[32]) {
-    const int i0 = blk * kBlock * PPL + threadIdx.x;
+    const int i0 = blk * BS * PPL + threadIdx.x;
     // every point's three loads issued together (one round trip instead of sel -> body/plane)
     bool sel[PPL];
     float b[PPL][3];
     float4 pl[PPL];
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
-        const int i = i0 + k * kBlock;
+        const int i = i0 + k * BS;
         sel[k] = false;
         if (i < a.n) {
             sel[k] = a.sel[i] != 0;
@@ -416,7 +429,7 @@ __device__ __forceinline__ void reuse_points(const MatchArgs& a, const PoseArg& 
 #pragma unroll
     for (int k = 0; k < PPL; ++k) {
         if (sel[k]) {
-            const int i = i0 + k * kBlock;
+            const int i = i0 + k * BS;
             float wx, wy, wz;
             body_to_world(ps, b[k][0], b[k][1], b[k][2], wx, wy, wz);
             double J[6], h, res;
@@ -432,40 +445,40 @@ __device__ __forceinline__ void reuse_points(const MatchArgs& a, const PoseArg& 
 // next kNN evaluation.
 // GATED: queued ahead of the host's decision (launch_h_model_gated): the pose comes from the control
 // block the gate kernel fills, and a cancelled evaluation (ctl->done) does nothing.
-template <int PPL, bool GATED = false>
-__global__ void __launch_bounds__(kBlock) plane_kernel(MatchArgs a) {
+template <int PPL, bool GATED = false, int BS = kBlock>
+__global__ void __launch_bounds__(BS) plane_kernel(MatchArgs a) {
     if constexpr (GATED)
         if (a.ctl->done) return;
     const PoseArg& ps = GATED ? a.ctl->pose : a.pose;
-    __shared__ double red[kBlock / 64][32];
+    __shared__ double red[BS / 64][32];
     double v[32];
 #pragma unroll
     for (int q = 0; q < 32; ++q) v[q] = 0.0;
-    plane_points<PPL>(a, ps, blockIdx.x, v);
+    plane_points<PPL, BS>(a, ps, blockIdx.x, v);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const double tot = wave_sum32(v, lane);
     if (lane < 32) red[wid][wave_sum32_index(lane)] = tot;
     __syncthreads();
-    publish_and_finalize(a, red);
+    publish_and_finalize<BS>(a, red);
     if (blockIdx.x == 0 && threadIdx.x == 0) *a.far_count = 0;
 }
 
 // ekfom_data.converge == false: reuse_points, same reduction and publish.
-template <int PPL, bool GATED = false>
-__global__ void __launch_bounds__(kBlock) h_model_reuse_kernel(MatchArgs a) {
+template <int PPL, bool GATED = false, int BS = kBlock>
+__global__ void __launch_bounds__(BS) h_model_reuse_kernel(MatchArgs a) {
     if constexpr (GATED)
         if (a.ctl->done) return;
     const PoseArg& ps = GATED ? a.ctl->pose : a.pose;
-    __shared__ double red[kBlock / 64][32];
+    __shared__ double red[BS / 64][32];
     double v[32];
 #pragma unroll
     for (int q = 0; q < 32; ++q) v[q] = 0.0;
-    reuse_points<PPL>(a, ps, blockIdx.x, v);
+    reuse_points<PPL, BS>(a, ps, blockIdx.x, v);
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     const double tot = wave_sum32(v, lane);
     if (lane < 32) red[wid][wave_sum32_index(lane)] = tot;
     __syncthreads();
-    publish_and_finalize(a, red);
+    publish_and_finalize<BS>(a, red);
 }
 
 // Device-resident update (lio_ieskf_update): one h-evaluation slot of
@@ -704,8 +717,8 @@ __global__ void __launch_bounds__(1024) h_rows_kernel(MatchArgs a, double* __res
 // ---------------------------------------------------------------- launchers
 int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* marks) {
     if (a.n == 0) return 0;
-    const int ppl = ppl_setting();
-    const int nb = (a.n + kBlock * ppl - 1) / (kBlock * ppl);
+    const int ppl = ppl_setting(), bs = match_block_setting();
+    const int nb = (a.n + bs * ppl - 1) / (bs * ppl);
     // hipExtLaunchKernelGGL with null events is a plain launch; with events (timing) the command
     // processor stamps them at the kernel's own start / end
     hipEvent_t m[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -738,7 +751,11 @@ int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* ma
             else
                 hipExtLaunchKernelGGL(knn_far_kernel<false>, dim3(far_blocks), dim3(kFarBlock), 0, st, m[2], m[3], 0, a);
         }
-        if (ppl == 4)
+        if (bs == 512 && ppl == 2)
+            hipExtLaunchKernelGGL((plane_kernel<2, false, 512>), dim3(nb), dim3(512), 0, st, m[4], m[5], 0, a);
+        else if (bs == 512)
+            hipExtLaunchKernelGGL((plane_kernel<1, false, 512>), dim3(nb), dim3(512), 0, st, m[4], m[5], 0, a);
+        else if (ppl == 4)
             hipExtLaunchKernelGGL(plane_kernel<4>, dim3(nb), dim3(kBlock), 0, st, m[4], m[5], 0, a);
         else if (ppl == 2)
             hipExtLaunchKernelGGL(plane_kernel<2>, dim3(nb), dim3(kBlock), 0, st, m[4], m[5], 0, a);
@@ -746,7 +763,11 @@ int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* ma
             hipExtLaunchKernelGGL(plane_kernel<1>, dim3(nb), dim3(kBlock), 0, st, m[4], m[5], 0, a);
         return nb;
     }
-    if (ppl == 4)
+    if (bs == 512 && ppl == 2)
+        hipExtLaunchKernelGGL((h_model_reuse_kernel<2, false, 512>), dim3(nb), dim3(512), 0, st, m[6], m[7], 0, a);
+    else if (bs == 512)
+        hipExtLaunchKernelGGL((h_model_reuse_kernel<1, false, 512>), dim3(nb), dim3(512), 0, st, m[6], m[7], 0, a);
+    else if (ppl == 4)
         hipExtLaunchKernelGGL(h_model_reuse_kernel<4>, dim3(nb), dim3(kBlock), 0, st, m[6], m[7], 0, a);
     else if (ppl == 2)
         hipExtLaunchKernelGGL(h_model_reuse_kernel<2>, dim3(nb), dim3(kBlock), 0, st, m[6], m[7], 0, a);
