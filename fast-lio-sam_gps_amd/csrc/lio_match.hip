@@ -346,14 +346,13 @@ static int ppl_setting() {
     return v;
 }
 
-// Threads per plane / reuse block on the host-loop path (LIO_MATCH_BLOCK = 256 or 512; 512 with
-// PPL 1 or 2): BS * PPL points per block partial.
-static int match_block_setting() {
-    static const int v = [] {
-        const char* e = std::getenv("LIO_MATCH_BLOCK");
-        const int b = e ? std::atoi(e) : kBlock;
-        return (b == 512 && ppl_setting() <= 2) ? 512 : kBlock;
-    }();
+// The plane kernel on the host-loop path: 512 threads, 1 point per lane (2 waves per SIMD at 88
+// VGPRs instead of 1 at 120 with 256 x 2; same partial count): plane 14.5 -> 13.5 us at C3, while the
+// reuse kernel stays at 256 x 2 (9.1 vs 9.4 us at 512 x 1).  An explicit LIO_PPL selects the 256-thread
+// plane kernel with that PPL (diagnostics).
+constexpr int kPlaneBlock = 512;
+static bool plane_wide() {
+    static const bool v = std::getenv("LIO_PPL") == nullptr;
     return v;
 }
 
@@ -717,8 +716,8 @@ __global__ void __launch_bounds__(1024) h_rows_kernel(MatchArgs a, double* __res
 // ---------------------------------------------------------------- launchers
 int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* marks) {
     if (a.n == 0) return 0;
-    const int ppl = ppl_setting(), bs = match_block_setting();
-    const int nb = (a.n + bs * ppl - 1) / (bs * ppl);
+    const int ppl = ppl_setting();
+    const int nb = (a.n + kBlock * ppl - 1) / (kBlock * ppl);
     // hipExtLaunchKernelGGL with null events is a plain launch; with events (timing) the command
     // processor stamps them at the kernel's own start / end
     hipEvent_t m[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -751,11 +750,12 @@ int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* ma
             else
                 hipExtLaunchKernelGGL(knn_far_kernel<false>, dim3(far_blocks), dim3(kFarBlock), 0, st, m[2], m[3], 0, a);
         }
-        if (bs == 512 && ppl == 2)
-            hipExtLaunchKernelGGL((plane_kernel<2, false, 512>), dim3(nb), dim3(512), 0, st, m[4], m[5], 0, a);
-        else if (bs == 512)
-            hipExtLaunchKernelGGL((plane_kernel<1, false, 512>), dim3(nb), dim3(512), 0, st, m[4], m[5], 0, a);
-        else if (ppl == 4)
+        if (plane_wide()) {
+            const int nbp = (a.n + kPlaneBlock - 1) / kPlaneBlock;
+            hipExtLaunchKernelGGL((plane_kernel<1, false, kPlaneBlock>), dim3(nbp), dim3(kPlaneBlock), 0, st, m[4], m[5], 0, a);
+            return nbp;
+        }
+        if (ppl == 4)
             hipExtLaunchKernelGGL(plane_kernel<4>, dim3(nb), dim3(kBlock), 0, st, m[4], m[5], 0, a);
         else if (ppl == 2)
             hipExtLaunchKernelGGL(plane_kernel<2>, dim3(nb), dim3(kBlock), 0, st, m[4], m[5], 0, a);
@@ -763,11 +763,7 @@ int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* ma
             hipExtLaunchKernelGGL(plane_kernel<1>, dim3(nb), dim3(kBlock), 0, st, m[4], m[5], 0, a);
         return nb;
     }
-    if (bs == 512 && ppl == 2)
-        hipExtLaunchKernelGGL((h_model_reuse_kernel<2, false, 512>), dim3(nb), dim3(512), 0, st, m[6], m[7], 0, a);
-    else if (bs == 512)
-        hipExtLaunchKernelGGL((h_model_reuse_kernel<1, false, 512>), dim3(nb), dim3(512), 0, st, m[6], m[7], 0, a);
-    else if (ppl == 4)
+    if (ppl == 4)
         hipExtLaunchKernelGGL(h_model_reuse_kernel<4>, dim3(nb), dim3(kBlock), 0, st, m[6], m[7], 0, a);
     else if (ppl == 2)
         hipExtLaunchKernelGGL(h_model_reuse_kernel<2>, dim3(nb), dim3(kBlock), 0, st, m[6], m[7], 0, a);

@@ -59,11 +59,9 @@ for s in $STEPS; do
              LIO_GPU_LIB=build_ab/liblio_gpu_base.so run ab_base_$rep 300 python bench.py --steps 400 --warmup 20 --no-icp --no-cpu --streams '' &&
              run ab_new_$rep 300 python bench.py --steps 400 --warmup 20 --no-icp --no-cpu --streams '' || exit 1
            done ;;
-    abblk) LIO_MATCH_BLOCK=512 LIO_PPL=1 runs parity_blk512 600 python -u -m pytest tests/test_gpu_parity.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread &&
-           for rep in 1 2; do
-             run blk256_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' &&
-             LIO_MATCH_BLOCK=512 LIO_PPL=1 run blk512p1_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' &&
-             LIO_MATCH_BLOCK=512 LIO_PPL=2 run blk512p2_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' || exit 1
+    abplane) for rep in 1 2; do
+             run plane512_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' &&
+             LIO_PPL=2 run plane256_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' || exit 1
            done ;;
     icptest) runs pytest_icp 600 python -u -m pytest tests/test_gpu_icp.py tests/test_gpu_parity.py -k icp -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     icpab) run icp_tile 300 python scripts/icp_ab.py 1.0 &&
