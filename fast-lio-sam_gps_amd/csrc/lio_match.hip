@@ -346,10 +346,10 @@ static int ppl_setting() {
     return v;
 }
 
-// The plane kernel on the host-loop path: 512 threads, 1 point per lane (2 waves per SIMD at 88
-// VGPRs instead of 1 at 120 with 256 x 2; same partial count): plane 14.5 -> 13.5 us at C3, while the
-// reuse kernel stays at 256 x 2 (9.1 vs 9.4 us at 512 x 1).  An explicit LIO_PPL selects the 256-thread
-// plane kernel with that PPL (diagnostics).
+// Host-loop path: the plane kernel in 512-thread blocks, 1 point per lane (2 waves per SIMD at 88
+// VGPRs instead of 1 at 120 with 256 x 2; same partial count): 14.5 -> 13.5 us at C3; the reuse kernel
+// in 512-thread blocks, 2 points per lane (half the partials for the last block): 9.1 -> 8.8 us.  An
+// explicit LIO_PPL selects the 256-thread kernels with that PPL (diagnostics).
 constexpr int kPlaneBlock = 512;
 static bool plane_wide() {
     static const bool v = std::getenv("LIO_PPL") == nullptr;
@@ -762,6 +762,11 @@ int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* ma
         else
             hipExtLaunchKernelGGL(plane_kernel<1>, dim3(nb), dim3(kBlock), 0, st, m[4], m[5], 0, a);
         return nb;
+    }
+    if (plane_wide()) {
+        const int nbr = (a.n + 2 * kPlaneBlock - 1) / (2 * kPlaneBlock);
+        hipExtLaunchKernelGGL((h_model_reuse_kernel<2, false, kPlaneBlock>), dim3(nbr), dim3(kPlaneBlock), 0, st, m[6], m[7], 0, a);
+        return nbr;
     }
     if (ppl == 4)
         hipExtLaunchKernelGGL(h_model_reuse_kernel<4>, dim3(nb), dim3(kBlock), 0, st, m[6], m[7], 0, a);

@@ -504,7 +504,8 @@ def test_ieskf_device_matches_host_loop(cfg):
 def test_ieskf_alternative_paths(env):
     """The A/B switches keep parity: the separate finalize launch (LIO_FUSED_FINAL=0), the
     unseeded later kNN evaluations (LIO_KNN_SEED=0), the device-resident IESKF (LIO_IESKF_DEVICE=1) and
-    2 / 4 points per lane in the plane / reuse kernels (LIO_PPL), through a whole IESKF update
+    2 / 4 points per lane in the plane / reuse kernels (LIO_PPL; set explicitly it also selects the
+    256-thread plane kernel instead of the default 512 x 1), through a whole IESKF update
     against the oracle.  Child process: the switches are read once per process."""
     import os
     import subprocess
