@@ -286,10 +286,9 @@ __device__ __forceinline__ void scan_cell_group(const GridDev& g, uint32_t c, fl
 
 // Lane-strided scan of one cell by the group, four loads in flight per lane
 // (the addresses clamped to the cell's last point; only real ones pushed).
-template <int K, int G>
+template <int K, int G, int U = 4>
 __device__ __forceinline__ void scan_cell_group2(const GridDev& g, uint32_t c, float qx, float qy, float qz, int sub,
                                                  TopK<K>& tk) {
-    constexpr int U = 4;
     const uint32_t b = g.start[c];
     const uint32_t e = g.start[c + 1];
     for (uint32_t j = b + (uint32_t)sub; j < e; j += U * G) {
@@ -597,7 +596,7 @@ __device__ __forceinline__ void scan_shell1_flat(const GridDev& g, float qx, flo
 // group_knn_exact_from.  TAIL = false (front-end near pass): no generic walk
 // at all — queries outside the grid or unresolved after shell 1 return false
 // with their partial list and go to the far pass.
-template <int K, int G, bool TAIL = true, int U = 4>
+template <int K, int G, bool TAIL = true, int U = 4, int UO = 4>  // UO: loads in flight in the own-cell scan
 __device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, int cx, int cy, int cz, int max_shell,
                                int sub, TopK<K>& tk, SearchStats* dbg, uint32_t* lds) {
     const bool inside = (unsigned)cx < (unsigned)g.nx && (unsigned)cy < (unsigned)g.ny && (unsigned)cz < (unsigned)g.nz;
@@ -613,7 +612,7 @@ __device__ bool group_knn_near(const GridDev& g, float qx, float qy, float qz, i
     const uint32_t c0 = (uint32_t)cz * nxy + (uint32_t)cy * nx + (uint32_t)cx;
     uint32_t b4[shell1_cpl<G>()], n4[shell1_cpl<G>()];
     shell1_ranges<G>(g, cx, cy, cz, sub, b4, n4);  // in flight during the own-cell scan
-    scan_cell_group2<K, G>(g, c0, qx, qy, qz, sub, tk);
+    scan_cell_group2<K, G, UO>(g, c0, qx, qy, qz, sub, tk);
     group_merge<K, G>(tk);
     if (dbg) dbg->shell = 0;
     if (own > 0.f && tk.worst() < own * own * 0.999999f) return true;

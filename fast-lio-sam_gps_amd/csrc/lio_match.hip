@@ -64,13 +64,13 @@ __device__ __forceinline__ bool residual_row(const MatchArgs& a, const PoseArg& 
 // neighbourhoods, ~0.4% of a dense scan) are queued, with their list, for
 // the wave-per-query far pass instead of holding their wave: a kernel runs as
 // long as its slowest wave.  Written for 8 waves/SIMD (<= 64 VGPRs).
-template <bool DBG, bool SEEDED, int U = 4, bool DEV = false>
-__global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) knn_near_kernel(MatchArgs a) {
+template <bool DBG, bool SEEDED, int U = 4, bool DEV = false, int NB = kKnnBlock, int UO = 4>
+__global__ void __launch_bounds__(NB) __attribute__((amdgpu_waves_per_eu(8, 8))) knn_near_kernel(MatchArgs a) {
     if constexpr (DEV)  // device-resident update: this slot runs only while the loop asks for a kNN
         if (a.ctl->done || !a.ctl->converge) return;
     const PoseArg& ps = DEV ? a.ctl->pose : a.pose;
     constexpr int G = kGroup;
-    constexpr int QPB = kKnnBlock / G;  // 64 queries per block
+    constexpr int QPB = NB / G;  // 64 queries per block
     __shared__ uint32_t s_tab[QPB][72];      // per-group shell-1 slot table
     __shared__ float s_q[4][QPB];            // per query: world point (and the seeded pass's bound)
     __shared__ int s_c[3][QPB];              //            its cell
@@ -124,7 +124,7 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
         done = r > 0;
         whole = r < 0;
     } else {
-        done = group_knn_near<5, G, false, U>(a.grid, wx, wy, wz, s_c[0][q], s_c[1][q], s_c[2][q], 1, sub, tk,
+        done = group_knn_near<5, G, false, U, UO>(a.grid, wx, wy, wz, s_c[0][q], s_c[1][q], s_c[2][q], 1, sub, tk,
                                               DBG ? &st : nullptr, s_tab[threadIdx.x / G]);
     }
     const bool far = !done && a.max_shell > 1;
@@ -151,7 +151,7 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
             }
         }
         if (a.tdbg && (threadIdx.x & 63) == 0) {
-            const size_t wv = (size_t)blockIdx.x * (kKnnBlock / 64) + (threadIdx.x >> 6);
+            const size_t wv = (size_t)blockIdx.x * (NB / 64) + (threadIdx.x >> 6);
             a.tdbg[2 * wv] = t_beg;
             a.tdbg[2 * wv + 1] = wall_clock64();
         }
@@ -170,7 +170,7 @@ __global__ void __launch_bounds__(kKnnBlock) __attribute__((amdgpu_waves_per_eu(
     }
     if (sub == 5) a.nn_d5[i] = tk.id(4) == kNone ? INFINITY : tk.d(4);
     if (a.tdbg && (threadIdx.x & 63) == 0) {
-        const size_t wv = (size_t)blockIdx.x * (kKnnBlock / 64) + (threadIdx.x >> 6);
+        const size_t wv = (size_t)blockIdx.x * (NB / 64) + (threadIdx.x >> 6);
         a.tdbg[2 * wv] = t_beg;
         a.tdbg[2 * wv + 1] = wall_clock64();
     }
@@ -714,6 +714,25 @@ __global__ void __launch_bounds__(1024) h_rows_kernel(MatchArgs a, double* __res
 }
 
 // ---------------------------------------------------------------- launchers
+// LIO_NEAR_NOSPILL=1: near pass with 2 loads in flight in the seeded table scan and the own-cell scan
+// (56 / 58 VGPRs, no scratch; the 4-load forms sit at the 64-VGPR cap with 8-12 B/lane of spills)
+static bool near_nospill() {
+    static const bool v = [] {
+        const char* e = std::getenv("LIO_NEAR_NOSPILL");
+        return e && std::atoi(e) == 1;
+    }();
+    return v;
+}
+
+// threads per near-pass block on the host-loop path (LIO_NEAR_BLOCK = 256: 32 queries per block)
+static int near_block() {
+    static const int v = [] {
+        const char* e = std::getenv("LIO_NEAR_BLOCK");
+        return (e && std::atoi(e) == 256) ? 256 : kKnnBlock;
+    }();
+    return v;
+}
+
 int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* marks) {
     if (a.n == 0) return 0;
     const int ppl = ppl_setting();
@@ -724,9 +743,18 @@ int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* ma
     if (marks)
         for (int k = 0; k < 8; ++k) m[k] = marks[k];
     if (redo) {
-        const int nq = (a.n + kKnnBlock / kGroup - 1) / (kKnnBlock / kGroup);
+        const int qpb = (a.dbg ? kKnnBlock : near_block()) / kGroup;
+        const int nq = (a.n + qpb - 1) / qpb;
         if (a.dbg)
             hipExtLaunchKernelGGL(knn_near_kernel<true, false>, dim3(nq), dim3(kKnnBlock), 0, st, m[0], m[1], 0, a);
+        else if (near_nospill() && a.prior)
+            hipExtLaunchKernelGGL((knn_near_kernel<false, true, 2>), dim3(nq), dim3(kKnnBlock), 0, st, m[0], m[1], 0, a);
+        else if (near_nospill())
+            hipExtLaunchKernelGGL((knn_near_kernel<false, false, 4, false, kKnnBlock, 2>), dim3(nq), dim3(kKnnBlock), 0, st, m[0], m[1], 0, a);
+        else if (near_block() == 256 && a.prior)
+            hipExtLaunchKernelGGL((knn_near_kernel<false, true, 4, false, 256>), dim3(nq), dim3(256), 0, st, m[0], m[1], 0, a);
+        else if (near_block() == 256)
+            hipExtLaunchKernelGGL((knn_near_kernel<false, false, 4, false, 256>), dim3(nq), dim3(256), 0, st, m[0], m[1], 0, a);
         else if (a.prior)
             hipExtLaunchKernelGGL(knn_near_kernel<false, true>, dim3(nq), dim3(kKnnBlock), 0, st, m[0], m[1], 0, a);
         else
