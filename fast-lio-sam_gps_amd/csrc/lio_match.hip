@@ -714,23 +714,48 @@ __global__ void __launch_bounds__(1024) h_rows_kernel(MatchArgs a, double* __res
 }
 
 // ---------------------------------------------------------------- launchers
-// LIO_NEAR_NOSPILL=1: near pass with 2 loads in flight in the seeded table scan and the own-cell scan
-// (56 / 58 VGPRs, no scratch; the 4-load forms sit at the 64-VGPR cap with 8-12 B/lane of spills)
+// Near pass on the host-loop path (A/B: profiles/r02_near_ab.txt):
+//  * 2 loads in flight in the seeded table scan and in the own-cell scan (56 / 58 VGPRs, no scratch):
+//    the 4-load forms sit at the 64-VGPR cap with 8-12 B/lane of spills (kNN h-evaluation traffic
+//    23.2 vs 18.6 MB at C3) for ~0.5 us less per pass; LIO_NEAR_NOSPILL=0 restores them;
+//  * 256-thread blocks (32 queries; finer grain for the second round of blocks at C3): near pass
+//    -0.5 to -0.8 us; LIO_NEAR_BLOCK=512 restores 64 queries per block.
 static bool near_nospill() {
     static const bool v = [] {
         const char* e = std::getenv("LIO_NEAR_NOSPILL");
-        return e && std::atoi(e) == 1;
+        return !(e && std::atoi(e) == 0);
     }();
     return v;
 }
 
-// threads per near-pass block on the host-loop path (LIO_NEAR_BLOCK = 256: 32 queries per block)
 static int near_block() {
     static const int v = [] {
         const char* e = std::getenv("LIO_NEAR_BLOCK");
-        return (e && std::atoi(e) == 256) ? 256 : kKnnBlock;
+        return (e && std::atoi(e) == 512) ? 512 : 256;
     }();
     return v;
+}
+
+template <int NB>
+static void launch_near_nb(const MatchArgs& a, int nq, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+    if (a.prior) {
+        if (near_nospill())
+            hipExtLaunchKernelGGL((knn_near_kernel<false, true, 2, false, NB, 4>), dim3(nq), dim3(NB), 0, st, e0, e1, 0, a);
+        else
+            hipExtLaunchKernelGGL((knn_near_kernel<false, true, 4, false, NB, 4>), dim3(nq), dim3(NB), 0, st, e0, e1, 0, a);
+    } else {
+        if (near_nospill())
+            hipExtLaunchKernelGGL((knn_near_kernel<false, false, 4, false, NB, 2>), dim3(nq), dim3(NB), 0, st, e0, e1, 0, a);
+        else
+            hipExtLaunchKernelGGL((knn_near_kernel<false, false, 4, false, NB, 4>), dim3(nq), dim3(NB), 0, st, e0, e1, 0, a);
+    }
+}
+
+static void launch_near(const MatchArgs& a, int nq, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
+    if (near_block() == 256)
+        launch_near_nb<256>(a, nq, st, e0, e1);
+    else
+        launch_near_nb<512>(a, nq, st, e0, e1);
 }
 
 int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* marks) {
@@ -747,18 +772,8 @@ int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* ma
         const int nq = (a.n + qpb - 1) / qpb;
         if (a.dbg)
             hipExtLaunchKernelGGL(knn_near_kernel<true, false>, dim3(nq), dim3(kKnnBlock), 0, st, m[0], m[1], 0, a);
-        else if (near_nospill() && a.prior)
-            hipExtLaunchKernelGGL((knn_near_kernel<false, true, 2>), dim3(nq), dim3(kKnnBlock), 0, st, m[0], m[1], 0, a);
-        else if (near_nospill())
-            hipExtLaunchKernelGGL((knn_near_kernel<false, false, 4, false, kKnnBlock, 2>), dim3(nq), dim3(kKnnBlock), 0, st, m[0], m[1], 0, a);
-        else if (near_block() == 256 && a.prior)
-            hipExtLaunchKernelGGL((knn_near_kernel<false, true, 4, false, 256>), dim3(nq), dim3(256), 0, st, m[0], m[1], 0, a);
-        else if (near_block() == 256)
-            hipExtLaunchKernelGGL((knn_near_kernel<false, false, 4, false, 256>), dim3(nq), dim3(256), 0, st, m[0], m[1], 0, a);
-        else if (a.prior)
-            hipExtLaunchKernelGGL(knn_near_kernel<false, true>, dim3(nq), dim3(kKnnBlock), 0, st, m[0], m[1], 0, a);
         else
-            hipExtLaunchKernelGGL(knn_near_kernel<false, false>, dim3(nq), dim3(kKnnBlock), 0, st, m[0], m[1], 0, a);
+            launch_near(a, nq, st, m[0], m[1]);
         static const int far_blocks = [] {  // LIO_FAR_BLOCKS: diagnostics override of the far-pass grid
             const char* e = std::getenv("LIO_FAR_BLOCKS");
             const int v = e ? std::atoi(e) : 0;

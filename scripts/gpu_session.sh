@@ -77,6 +77,10 @@ for s in $STEPS; do
                -- python bench.py --steps 30 --warmup 3 --no-cpu --no-icp --streams '' &&
            LIO_NEAR_NOSPILL=1 run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv \
                -- python bench.py --steps 30 --warmup 3 --no-cpu --no-icp --streams '' ;;
+    abnearfinal) for rep in 1 2; do
+             run nearnew_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' &&
+             LIO_NEAR_BLOCK=512 LIO_NEAR_NOSPILL=0 run nearold_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' || exit 1
+           done ;;
     icptest) runs pytest_icp 600 python -u -m pytest tests/test_gpu_icp.py tests/test_gpu_parity.py -k icp -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     icpab) run icp_tile 300 python scripts/icp_ab.py 1.0 &&
            LIO_ICP_DEBUG=1 run icp_tile_dbg 300 python scripts/icp_ab.py 1.0 1 &&

@@ -500,12 +500,13 @@ def test_ieskf_device_matches_host_loop(cfg):
 
 
 @pytest.mark.parametrize("env", [{"LIO_FUSED_FINAL": "0"}, {"LIO_KNN_SEED": "0"}, {"LIO_IESKF_DEVICE": "1"}, {"LIO_QUEUE_NEXT": "1"},
-                                 {"LIO_PPL": "2"}, {"LIO_PPL": "4"}])
+                                 {"LIO_PPL": "2"}, {"LIO_PPL": "4"}, {"LIO_NEAR_BLOCK": "512"}, {"LIO_NEAR_NOSPILL": "0"}])
 def test_ieskf_alternative_paths(env):
     """The A/B switches keep parity: the separate finalize launch (LIO_FUSED_FINAL=0), the
     unseeded later kNN evaluations (LIO_KNN_SEED=0), the device-resident IESKF (LIO_IESKF_DEVICE=1) and
     2 / 4 points per lane in the plane / reuse kernels (LIO_PPL; set explicitly it also selects the
-    256-thread plane kernel instead of the default 512 x 1), through a whole IESKF update
+    256-thread plane kernel instead of the default 512 x 1), the 64-query / 4-load near-pass forms
+    (LIO_NEAR_BLOCK=512, LIO_NEAR_NOSPILL=0), through a whole IESKF update
     against the oracle.  Child process: the switches are read once per process."""
     import os
     import subprocess
