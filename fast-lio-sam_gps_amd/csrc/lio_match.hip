@@ -731,7 +731,8 @@ static bool near_nospill() {
 static int near_block() {
     static const int v = [] {
         const char* e = std::getenv("LIO_NEAR_BLOCK");
-        return (e && std::atoi(e) == 512) ? 512 : 256;
+        const int b = e ? std::atoi(e) : 256;
+        return (b == 512 || b == 128) ? b : 256;
     }();
     return v;
 }
@@ -754,6 +755,8 @@ static void launch_near_nb(const MatchArgs& a, int nq, hipStream_t st, hipEvent_
 static void launch_near(const MatchArgs& a, int nq, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
     if (near_block() == 256)
         launch_near_nb<256>(a, nq, st, e0, e1);
+    else if (near_block() == 128)
+        launch_near_nb<128>(a, nq, st, e0, e1);
     else
         launch_near_nb<512>(a, nq, st, e0, e1);
 }

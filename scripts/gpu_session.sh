@@ -81,6 +81,11 @@ for s in $STEPS; do
              run nearnew_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' &&
              LIO_NEAR_BLOCK=512 LIO_NEAR_NOSPILL=0 run nearold_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' || exit 1
            done ;;
+    abnear128) LIO_NEAR_BLOCK=128 runs parity_near128 600 python -u -m pytest tests/test_gpu_parity.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread &&
+           for rep in 1 2 3; do
+             run n256_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' &&
+             LIO_NEAR_BLOCK=128 run n128_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' || exit 1
+           done ;;
     icptest) runs pytest_icp 600 python -u -m pytest tests/test_gpu_icp.py tests/test_gpu_parity.py -k icp -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     icpab) run icp_tile 300 python scripts/icp_ab.py 1.0 &&
            LIO_ICP_DEBUG=1 run icp_tile_dbg 300 python scripts/icp_ab.py 1.0 1 &&
