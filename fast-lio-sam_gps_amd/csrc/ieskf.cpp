@@ -304,11 +304,6 @@ int update_iterated(State& x, Mat& P, double R, int max_iter, double epsi, const
         const bool want_rows_hint = false;
         ++out.h_evals;
         if (converge) ++out.knn_calls;
-        // the evaluations of iterations i+1 .. max_iter-1 if no later step converges: reuse, except
-        // the one after iteration max_iter-2 while t == 0 (the loop forces converge: kNN)
-        hm.n_next = 0;
-        for (int j = i + 1; j <= max_iter - 1 && hm.n_next < 8; ++j)
-            hm.next[hm.n_next++] = (t == 0 && j - 1 == max_iter - 2) ? 2 : 1;
         int rc = hfn(x, converge, want_rows_hint, hm);
         if (rc != 0) return rc;
         const int dof = (int)hm.sums[27];
@@ -316,7 +311,6 @@ int update_iterated(State& x, Mat& P, double R, int max_iter, double epsi, const
         out.res_mean = dof > 0 ? hm.sums[28] / dof : 0.0;
         if (dof < 1) continue;  // ekfom_data.valid = false: "No Effective Points!"
         if (dof < N && hm.rows.size() != (size_t)7 * dof) {
-            hm.n_next = 0;
             rc = hfn(x, false, true, hm);  // fetch the H rows of this same evaluation
             if (rc != 0) return rc;
         }

@@ -30,11 +30,6 @@ using Mat = std::vector<double>;  // row-major, sized by caller
 struct HModel {
     double sums[32];          // LIO_SUMS_* layout
     std::vector<double> rows; // 7 doubles per effective point, only when n_eff < N
-    // set by update_iterated before each evaluation: the evaluations the loop will ask for next if no
-    // later step converges (1 reuse, 2 kNN; n_next of them), so the caller can queue them before
-    // this one's result is in
-    int next[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    int n_next = 0;
 };
 
 // h_share_model callback: (state, redo_knn, want_rows, out) -> status

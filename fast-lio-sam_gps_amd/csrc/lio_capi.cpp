@@ -18,7 +18,6 @@
 #include <vector>
 
 #include "ieskf.hpp"
-#include "ieskf_dev.hpp"
 #include "lio_error.hpp"
 #include "lio_kernels.hpp"
 #include "lio_filter.hpp"
@@ -98,11 +97,24 @@ void mat_to_quat(const double* m, double* q) {
 
 bool quat_zero(const double* q) { return q[0] == 0.0 && q[1] == 0.0 && q[2] == 0.0 && q[3] == 0.0; }
 
+// The quaternions take precedence over R / R_LI (include/lio_gpu.h lio_pose): the kernels rotate with
+// q / q_LI; a caller that fills only the matrices gets q derived from them.
 lio_pose filled(const lio_pose& p) {
     lio_pose o = p;
     if (quat_zero(o.q)) mat_to_quat(o.R, o.q);
     if (quat_zero(o.q_LI)) mat_to_quat(o.R_LI, o.q_LI);
     return o;
+}
+
+// Eigen QuaternionBase::toRotationMatrix (q = w, x, y, z; any norm is used as given)
+void quat_to_mat(const double* q, double* R) {
+    const double w = q[0], x = q[1], y = q[2], z = q[3];
+    const double tx = 2 * x, ty = 2 * y, tz = 2 * z;
+    const double twx = tx * w, twy = ty * w, twz = tz * w, txx = tx * x, txy = ty * x, txz = tz * x;
+    const double tyy = ty * y, tyz = tz * y, tzz = tz * z;
+    R[0] = 1 - (tyy + tzz), R[1] = txy - twz, R[2] = txz + twy;
+    R[3] = txy + twz, R[4] = 1 - (txx + tzz), R[5] = tyz - twx;
+    R[6] = txz - twy, R[7] = tyz + twx, R[8] = 1 - (txx + tyy);
 }
 
 }  // namespace
@@ -173,22 +185,7 @@ struct lio_ctx {
     int64_t rec_cap = 0;
     lio::ImuPose* d_poses = nullptr;
     int64_t poses_cap = 0;
-    // device-resident IESKF (lio_ieskf_update): control block + host-mapped input / result
-    lio::IeskfCtl* d_ctl = nullptr;
-    double* h_iin = nullptr;     // kIeskfInWords
-    double* h_iin_dev = nullptr;
-    double* h_iout = nullptr;    // kIeskfOutWords + 2 (sequence number, checksum)
-    double* h_iout_dev = nullptr;
-    hipEvent_t ev_slots[6 * 8] = {};  // timing: near / far / slot kernel start-stop per slot
-    int ieskf_device = -1;            // lio_ctx_set_ieskf_mode: 1 device-resident, 0 host loop, -1 env / default (host)
-    // the host loop's next evaluation, queued behind a gate before the host knows its pose
-    lio::GateIn* h_gate = nullptr;    // host-mapped
-    lio::GateIn* h_gate_dev = nullptr;
-    unsigned long long gate_seq = 0;
-    // queued evaluations in stream order: kind (kNN?), result sequence number, gate sequence number
-    int n_pend = 0, pend_head = 0;
-    bool pend_knn[8] = {};
-    unsigned long long pend_seq[8] = {}, pend_gate[8] = {};
+    float seed_scale = 1.0f;  // lio_ctx_set_seed_scale (test hook: < 1 exercises the seeded pass's guard)
 };
 
 extern "C" {
@@ -513,12 +510,9 @@ int lio_ctx_create(lio_map* m, const lio_match_params* p, lio_ctx** out) {
     return LIO_OK;
 }
 
-static void cancel_pending(lio_ctx* c);
-
 int lio_ctx_destroy(lio_ctx* c) {
     if (!c) return LIO_OK;
     (void)hipSetDevice(c->map->dev);
-    cancel_pending(c);
     (void)hipStreamSynchronize(c->map->st);
     void* ptrs[] = {c->d_body,  c->d_nn,    c->d_planes,   c->d_sel,       c->d_partials, c->d_sums,
                     c->d_rows,  c->d_nrows, c->d_far_list, c->d_far_count, c->d_far_d,    c->d_far_id, c->d_done,
@@ -533,13 +527,8 @@ int lio_ctx_destroy(lio_ctx* c) {
     for (hipEvent_t e : c->ev_marks)
         if (e) (void)hipEventDestroy(e);
     lio::filter_free(c->filt);
-    for (void* q : {(void*)c->d_raw, (void*)c->d_rec, (void*)c->d_poses, (void*)c->d_ctl})
+    for (void* q : {(void*)c->d_raw, (void*)c->d_rec, (void*)c->d_poses})
         if (q) (void)hipFree(q);
-    for (double* q : {c->h_iin, c->h_iout})
-        if (q) (void)hipHostFree(q);
-    if (c->h_gate) (void)hipHostFree(c->h_gate);
-    for (hipEvent_t e : c->ev_slots)
-        if (e) (void)hipEventDestroy(e);
     --c->map->n_ctx;
     delete c;
     return LIO_OK;
@@ -622,22 +611,21 @@ static lio::MatchArgs make_args(lio_ctx* c, const lio_pose& pose_in) {
     a.map_by_id = c->map->grid.by_id;
     a.nn_idx = c->d_nn;
     a.nn_d5 = c->d_d5;
-    static const float seed_scale = [] {  // LIO_KNN_SEED_SCALE: diagnostics (< 1 exercises the seeded-pass guard)
-        const char* e = std::getenv("LIO_KNN_SEED_SCALE");
-        const float v = e ? (float)std::atof(e) : 1.0f;
-        return v > 0.f && v <= 1.f ? v : 1.0f;
-    }();
-    a.seed_scale = seed_scale;
+    a.seed_scale = c->seed_scale;
     {
         const lio_pose pk = filled(c->knn_pose);
         std::memcpy(&a.pose_knn, &pk, sizeof(lio::PoseArg));
-        // float affine map body -> world of that pose: [R R_LI | R t_LI + t]
+        // float affine map body -> world of that pose, [R R_LI | R t_LI + t], from the quaternions the
+        // kernels rotate with (never from R / R_LI, which a caller may leave stale)
+        double R[9], RL[9];
+        quat_to_mat(pk.q, R);
+        quat_to_mat(pk.q_LI, RL);
         for (int r = 0; r < 3; ++r) {
             for (int k = 0; k < 3; ++k)
-                a.knn_M[4 * r + k] = (float)(pk.R[3 * r] * pk.R_LI[k] + pk.R[3 * r + 1] * pk.R_LI[3 + k] +
-                                             pk.R[3 * r + 2] * pk.R_LI[6 + k]);
-            a.knn_M[4 * r + 3] = (float)(pk.R[3 * r] * pk.t_LI[0] + pk.R[3 * r + 1] * pk.t_LI[1] +
-                                         pk.R[3 * r + 2] * pk.t_LI[2] + pk.t[r]);
+                a.knn_M[4 * r + k] =
+                    (float)(R[3 * r] * RL[k] + R[3 * r + 1] * RL[3 + k] + R[3 * r + 2] * RL[6 + k]);
+            a.knn_M[4 * r + 3] =
+                (float)(R[3 * r] * pk.t_LI[0] + R[3 * r + 1] * pk.t_LI[1] + R[3 * r + 2] * pk.t_LI[2] + pk.t[r]);
         }
     }
     a.planes = c->d_planes;
@@ -653,11 +641,6 @@ static lio::MatchArgs make_args(lio_ctx* c, const lio_pose& pose_in) {
     a.far_list = c->d_far_list;
     a.far_count = c->d_far_count;
     a.done_count = c->d_done;
-    static const int fused = [] {  // LIO_FUSED_FINAL=0: separate finalize launch (A/B diagnostics)
-        const char* e = std::getenv("LIO_FUSED_FINAL");
-        return e ? std::atoi(e) : 1;
-    }();
-    a.fused_final = fused;
     a.far_d = c->d_far_d;
     a.far_id = c->d_far_id;
     a.range_sq = c->p.knn_range_sq;
@@ -714,102 +697,14 @@ static int wait_result(lio_ctx* c, unsigned long long seq, double* sums) {
     }
 }
 
-// ---- queued evaluations (host loop of lio_ieskf_update, opt-in LIO_QUEUE_NEXT=1) ---
-// While the first evaluation of an update runs, the evaluations the loop will ask for if no later
-// step converges (IESKF hint chain) are queued, each behind a one-wave gate kernel; once the host
-// has done the algebra it publishes the pose and a run command with one store sequence (no launch
-// on the critical path: 1.9 us instead of 5.8 us from the decision to the kernel start,
-// scripts/micro/wait_value.hip).  A mispredicted evaluation cancels the rest of the chain (their
-// kernels exit at once) and the right one is launched normally.  Measured: the gaps between
-// dependent evaluations drop from 8.5 to 6.3 us, but scans/s end 2-4 % lower (more launches per
-// scan, host time per scan up), so it is off by default.
-static bool gating_enabled() {
-    static const bool v = [] {  // LIO_QUEUE_NEXT=1: queued evaluations (opt-in: measured 2-4 % slower)
-        const char* e = std::getenv("LIO_QUEUE_NEXT");
-        return e ? std::atoi(e) != 0 : false;
-    }();
-    return v;
-}
-
-static int ensure_gate(lio_ctx* c) {
-    if (!c->d_ctl) {
-        if (hipMalloc(&c->d_ctl, lio::ieskf_ctl_bytes()) != hipSuccess) {
-            c->d_ctl = nullptr;
-            return -1;
-        }
-    }
-    if (!c->h_gate) {
-        if (hipHostMalloc(&c->h_gate, sizeof(lio::GateIn), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-            hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_gate_dev), c->h_gate, 0) != hipSuccess) {
-            if (c->h_gate) (void)hipHostFree(c->h_gate);
-            c->h_gate = nullptr;
-            return -1;
-        }
-        std::memset(c->h_gate, 0, sizeof(lio::GateIn));
-    }
-    return 0;
-}
-
-static void gate_publish(lio_ctx* c, const lio_pose* pose, unsigned long long cmd, unsigned long long gseq) {
-    lio::GateIn* gi = c->h_gate;
-    if (pose) {
-        const lio_pose pf = filled(*pose), pk = filled(c->knn_pose);
-        std::memcpy(&gi->pose, &pf, sizeof(lio::PoseArg));
-        std::memcpy(&gi->pose_knn, &pk, sizeof(lio::PoseArg));
-    }
-    gi->cmd = cmd;
-    std::atomic_thread_fence(std::memory_order_release);  // pose and command before the sequence number
-    reinterpret_cast<volatile unsigned long long*>(&gi->seq)[0] = gseq;
-}
-
-// every queued evaluation exits without work (their gates all see seq >= theirs and cmd = cancel)
-static void cancel_pending(lio_ctx* c) {
-    if (c->n_pend == 0) return;
-    gate_publish(c, nullptr, 2, c->pend_gate[c->pend_head + c->n_pend - 1]);
-    c->n_pend = 0;
-    c->pend_head = 0;
-}
-
-// Queue the predicted evaluations (kinds[k]: 1 reuse, 2 kNN) behind gates, in order; cur_knn: the
-// evaluation just launched redoes the kNN (a queued kNN evaluation is then seeded by it).  Each is
-// a gate + its first kernel (kNN: the near pass; its far + plane passes follow at release).
-static void queue_chain(lio_ctx* c, const int* kinds, int n, bool cur_knn) {
-    if (n <= 0 || c->n_pend > 0 || c->timing || !gating_enabled() || c->n == 0 || c->map->n == 0) return;
-    if (ensure_gate(c)) return;  // no gate memory: evaluations are launched after the decision
-    lio::MatchArgs a = make_args(c, c->last_pose);
-    if (!a.fused_final) return;  // LIO_FUSED_FINAL=0: the sums need the finalize launch after the decision
-    a.ctl = c->d_ctl;
-    static const bool seed_ok = [] {
-        const char* e = std::getenv("LIO_KNN_SEED");
-        return e ? std::atoi(e) != 0 : true;
-    }();
-    bool knn_before = cur_knn || (c->knn_valid && c->knn_map_version == c->map->version);
-    n = std::min(n, 8);
-    for (int k = 0; k < n; ++k) {
-        const bool knn = kinds[k] == 2;
-        a.prior = (knn && seed_ok && knn_before) ? 1 : 0;
-        a.seq = ++c->seq;
-        ++c->gate_seq;
-        lio::launch_h_model_gated(a, knn, c->h_gate_dev, c->gate_seq, c->map->st);
-        if (hipGetLastError() != hipSuccess) break;  // the ones queued so far stay valid
-        c->pend_knn[k] = knn;
-        c->pend_seq[k] = a.seq;
-        c->pend_gate[k] = c->gate_seq;
-        c->n_pend = k + 1;
-        knn_before = knn_before || knn;
-    }
-    c->pend_head = 0;
-}
-
-static int match_impl(lio_ctx* c, const lio_pose* pose_in, int redo_knn, double* sums, const int* next, int n_next);
+static int match_impl(lio_ctx* c, const lio_pose* pose_in, int redo_knn, double* sums);
 
 int lio_match(lio_ctx* c, const lio_pose* pose_in, int redo_knn, double* sums) {
     if (!c || !pose_in || !sums) return fail(LIO_ERR_ARG, "lio_match: bad arguments");
-    cancel_pending(c);
-    return match_impl(c, pose_in, redo_knn, sums, nullptr, 0);
+    return match_impl(c, pose_in, redo_knn, sums);
 }
 
-static int match_impl(lio_ctx* c, const lio_pose* pose_in, int redo_knn, double* sums, const int* next, int n_next) {
+static int match_impl(lio_ctx* c, const lio_pose* pose_in, int redo_knn, double* sums) {
     const lio_pose pose_f = filled(*pose_in);
     const lio_pose* pose = &pose_f;
     if (c->map->grid.n_ids == 0) return fail(LIO_ERR_STATE, "lio_match: map is empty (call lio_map_build)");
@@ -837,70 +732,20 @@ static int match_impl(lio_ctx* c, const lio_pose* pose_in, int redo_knn, double*
     }
     a.seq = ++c->seq;
     // later kNN evaluations of the same scan against the same map start from the previous lists
-    static const bool seed_ok = [] {  // LIO_KNN_SEED=0: always the unseeded near pass (A/B diagnostics)
-        const char* e = std::getenv("LIO_KNN_SEED");
-        return e ? std::atoi(e) != 0 : true;
-    }();
-    a.prior = (seed_ok && redo_knn && c->knn_valid && c->knn_map_version == c->map->version) ? 1 : 0;
-    static const char* tdir = std::getenv("LIO_KNN_TDBG");  // diagnostics: per-wave near-pass timestamps
-    unsigned long long* d_t = nullptr;
-    const size_t nwaves = (size_t)((c->n + 63) / 64) * 8;
-    if (tdir && redo_knn) {
-        HIP_TRY(hipMalloc(&d_t, nwaves * 16));
-        HIP_TRY(hipMemsetAsync(d_t, 0, nwaves * 16, st));
-        a.tdbg = d_t;
-    }
+    a.prior = (redo_knn && c->knn_valid && c->knn_map_version == c->map->version) ? 1 : 0;
     const auto t0 = std::chrono::steady_clock::now();
-    bool queued = false;
-    if (c->n_pend > 0) {  // the evaluation queued for this call: release it, or cancel a misprediction
-        const int h = c->pend_head;
-        if (c->pend_knn[h] == (redo_knn != 0) && !tdir && !c->timing) {
-            --c->seq;  // the sequence number reserved above is not used
-            a.seq = c->pend_seq[h];
-            gate_publish(c, pose, 1, c->pend_gate[h]);
-            ++c->pend_head;
-            --c->n_pend;
-            queued = true;
-            if (redo_knn) lio::launch_knn_tail(a, st);  // far + plane behind the released near pass
-            HIP_TRY(hipGetLastError());
-        } else {
-            cancel_pending(c);
-        }
-    }
-    if (!queued) {
-        if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.a, st));
-        const int nb = lio::launch_h_model(a, redo_knn != 0, st, c->timing ? c->ev_marks : nullptr);
-        if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.b, st));
-        lio::launch_finalize(a, nb, st);  // no-op: the last plane/reuse block publishes the sums
-        if (c->timing) HIP_TRY(hipEventRecord(c->ev_fin.b, st));
-        HIP_TRY(hipGetLastError());
-    }
-    if (c->n_pend == 0 && next) queue_chain(c, next, n_next, redo_knn != 0);  // while this one runs
+    if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.a, st));
+    lio::launch_h_model(a, redo_knn != 0, st, c->timing ? c->ev_marks : nullptr);
+    if (c->timing) HIP_TRY(hipEventRecord(c->ev_main.b, st));
+    HIP_TRY(hipGetLastError());
     const auto t1 = std::chrono::steady_clock::now();
     int rc = wait_result(c, a.seq, sums);
-    if (rc) {
-        cancel_pending(c);
-        return rc;
-    }
+    if (rc) return rc;
     const auto t2 = std::chrono::steady_clock::now();
-    if (d_t) {
-        std::vector<unsigned long long> h(nwaves * 2);
-        HIP_TRY(hipMemcpy(h.data(), d_t, nwaves * 16, hipMemcpyDeviceToHost));
-        (void)hipFree(d_t);
-        static int k = 0;
-        char fn[512];
-        std::snprintf(fn, sizeof(fn), "%s/near_%d.bin", tdir, k++);
-        if (FILE* f = std::fopen(fn, "wb")) {
-            std::fwrite(h.data(), 8, h.size(), f);
-            std::fclose(f);
-        }
-    }
     c->last_launch_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
     c->last_wait_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
     if (c->timing) {
-        HIP_TRY(hipEventSynchronize(c->ev_fin.b));
-        EventPair f{c->ev_main.b, c->ev_fin.b};
-        accum_event(f, c->tm.final_launches, c->tm.final_ms);
+        HIP_TRY(hipEventSynchronize(c->ev_main.b));
         if (redo_knn) {  // kernel spans (hipExtLaunchKernel events): no launch gaps, as rocprofv3 reports
             const double before = c->tm.near_ms + c->tm.far_ms + c->tm.plane_ms;
             EventPair n{c->ev_marks[0], c->ev_marks[1]}, f{c->ev_marks[2], c->ev_marks[3]},
@@ -936,7 +781,7 @@ int lio_ctx_knn_stats(lio_ctx* c, const lio_pose* pose, double* sums, int32_t* s
     lio::MatchArgs a = make_args(c, *pose);
     a.dbg = d_dbg;
     a.seq = ++c->seq;
-    lio::launch_finalize(a, lio::launch_h_model(a, true, st), st);
+    lio::launch_h_model(a, true, st);
     hipError_t e2 = hipMemcpyAsync(stats3, d_dbg, c->n * 3 * sizeof(int), hipMemcpyDeviceToHost, st);
     hipError_t e3 = hipStreamSynchronize(st);
     (void)hipFree(d_dbg);
@@ -1105,143 +950,9 @@ static lio_pose state_pose(const lio::host::State& s) {  // the pose an evaluati
     return pose;
 }
 
-// Device-resident update (opt-in: lio_ctx_set_ieskf_mode(c, 1) or LIO_IESKF_DEVICE=1; the host
-// loop is the default because it measured faster): the whole
-// update_iterated_dyn_share_modified enqueued as one launch sequence — init, then max_iteration + 1
-// evaluation slots whose block 0 runs the IESKF pre-step and whose last block the post-step
-// (ieskf_dev.hpp) — and one wait for the published result.  Returns 1 when the host loop must run
-// instead (dof < 23 branch, or a shape the sequence does not cover), 0 on success, < 0 on error.
-static int ieskf_device_default() {  // -1: not set in the environment
-    static const int v = [] {
-        const char* e = std::getenv("LIO_IESKF_DEVICE");
-        return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
-    }();
-    return v;
-}
-
-static int ieskf_update_device(lio_ctx* c, lio_state* xs, double* P, const lio_ieskf_params& pp, lio_ieskf_stats* st,
-                               const std::chrono::steady_clock::time_point& t_call) {
-    using clk = std::chrono::steady_clock;
-    if (c->n == 0 || c->map->n == 0 || c->map->grid.n_ids == 0 || pp.max_iteration < 0 || pp.max_iteration > 7)
-        return 1;
-    HIP_TRY(hipSetDevice(c->map->dev));
-    if (!c->d_ctl) {
-        if (hipMalloc(&c->d_ctl, lio::ieskf_ctl_bytes()) != hipSuccess) {
-            c->d_ctl = nullptr;
-            return fail(LIO_ERR_NOMEM, "lio_ieskf_update: control block allocation failed");
-        }
-        if (hipHostMalloc(&c->h_iin, lio::kIeskfInWords * sizeof(double), hipHostMallocMapped | hipHostMallocCoherent) !=
-                hipSuccess ||
-            hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_iin_dev), c->h_iin, 0) != hipSuccess ||
-            hipHostMalloc(&c->h_iout, (lio::kIeskfOutWords + 2) * sizeof(double),
-                          hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-            hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_iout_dev), c->h_iout, 0) != hipSuccess) {
-            (void)hipFree(c->d_ctl);
-            c->d_ctl = nullptr;
-            return fail(LIO_ERR_NOMEM, "lio_ieskf_update: host-mapped buffers allocation failed");
-        }
-        std::memset(c->h_iout, 0, (lio::kIeskfOutWords + 2) * sizeof(double));
-    }
-    if (c->timing && !c->ev_slots[0])
-        for (hipEvent_t& e : c->ev_slots) (void)hipEventCreate(&e);
-    // input: x, P, R, epsi, max_iteration
-    std::memcpy(c->h_iin, xs, lio::kStateWords * sizeof(double));
-    std::memcpy(c->h_iin + lio::kStateWords, P, LIO_STATE_DIM * LIO_STATE_DIM * sizeof(double));
-    c->h_iin[lio::kStateWords + 529] = pp.laser_point_cov;
-    c->h_iin[lio::kStateWords + 530] = pp.epsi;
-    c->h_iin[lio::kStateWords + 531] = (double)pp.max_iteration;
-    lio_pose dummy{};
-    dummy.q[0] = dummy.q_LI[0] = 1.0;
-    lio::MatchArgs a = make_args(c, dummy);
-    if (!a.fused_final) return 1;  // LIO_FUSED_FINAL=0 (separate finalize launches): the host loop
-    a.ctl = c->d_ctl;
-    a.ieskf_out = c->h_iout_dev;
-    const unsigned long long seq = ++c->seq;
-    const auto t0 = clk::now();
-    lio::launch_ieskf_dev(a, c->h_iin_dev, seq, pp.max_iteration, c->map->st, c->timing ? c->ev_slots : nullptr);
-    HIP_TRY(hipGetLastError());
-    const auto t1 = clk::now();
-    // wait for the published result (same checksummed one-round-trip protocol as wait_result)
-    const volatile uint64_t* w = reinterpret_cast<const volatile uint64_t*>(c->h_iout);
-    std::vector<uint64_t> bits(lio::kIeskfOutWords);
-    auto read = [&]() -> bool {
-        if (w[lio::kIeskfOutWords] != seq) return false;
-        uint64_t h = 0;
-        for (int l = 0; l < lio::kIeskfOutWords; ++l) {
-            bits[l] = w[l];
-            h ^= mix64(bits[l] ^ ((uint64_t)l * 0x9e3779b97f4a7c15ull));
-        }
-        return (h ^ mix64(seq)) == w[lio::kIeskfOutWords + 1];
-    };
-    for (uint64_t it = 0;; ++it) {
-        if (read()) break;
-        if ((it & 255) == 255) {
-            const hipError_t e = hipStreamQuery(c->map->st);
-            if (e != hipSuccess && e != hipErrorNotReady)
-                return fail(LIO_ERR_HIP, std::string("lio_ieskf_update: ") + hipGetErrorString(e));
-            if (e == hipSuccess && !read()) return fail(LIO_ERR_HIP, "lio_ieskf_update: the update produced no result");
-        }
-    }
-    const auto t2 = clk::now();
-    double out[lio::kIeskfOutWords];
-    std::memcpy(out, bits.data(), sizeof(out));
-    const int h_evals = (int)out[lio::kIeskfOutInts], knn_calls = (int)out[lio::kIeskfOutInts + 1],
-              converged = (int)out[lio::kIeskfOutInts + 2], n_eff = (int)out[lio::kIeskfOutInts + 3],
-              status = (int)out[lio::kIeskfOutInts + 4], knn_mask = (int)out[lio::kIeskfOutInts + 5];
-    if (status == lio::kIeskfSingular) return fail(LIO_ERR_STATE, "IESKF: singular matrix");
-    if (status == lio::kIeskfNeedHost) {
-        HIP_TRY(hipStreamSynchronize(c->map->st));  // the remaining (gated) slots drain
-        c->knn_valid = false;
-        return 1;
-    }
-    if (status != lio::kIeskfOk) return fail(LIO_ERR_HIP, "lio_ieskf_update: unexpected device status");
-    std::memcpy(xs, out + lio::kIeskfOutX, lio::kStateWords * sizeof(double));
-    std::memcpy(P, out + lio::kIeskfOutP, LIO_STATE_DIM * LIO_STATE_DIM * sizeof(double));
-    lio_state sk, sl;
-    std::memcpy(&sk, out + lio::kIeskfOutXKnn, sizeof(sk));
-    std::memcpy(&sl, out + lio::kIeskfOutXLast, sizeof(sl));
-    c->last_pose = state_pose(to_host(sl));
-    c->have_eval = true;
-    if (knn_calls > 0) {
-        c->knn_valid = true;
-        c->knn_map_version = c->map->version;
-        c->knn_pose = state_pose(to_host(sk));
-    }
-    if (c->timing) {  // kernel spans of the slots that ran (the gated ones are empty launches)
-        HIP_TRY(hipStreamSynchronize(c->map->st));
-        for (int e = 0; e < h_evals && e <= pp.max_iteration; ++e) {
-            hipEvent_t* m = c->ev_slots + 6 * e;
-            if (knn_mask & (1 << e)) {
-                const double before = c->tm.near_ms + c->tm.far_ms + c->tm.plane_ms;
-                EventPair n{m[0], m[1]}, f{m[2], m[3]}, pl{m[4], m[5]};
-                accum_event(n, c->tm.near_launches, c->tm.near_ms);
-                if (a.max_shell > 1) accum_event(f, c->tm.far_launches, c->tm.far_ms);
-                accum_event(pl, c->tm.plane_launches, c->tm.plane_ms);
-                c->tm.knn_ms += (c->tm.near_ms + c->tm.far_ms + c->tm.plane_ms) - before;
-                ++c->tm.knn_launches;
-            } else {
-                EventPair r{m[4], m[5]};
-                accum_event(r, c->tm.reuse_launches, c->tm.reuse_ms);
-            }
-        }
-    }
-    if (st) {
-        st->h_evals = h_evals;
-        st->knn_calls = knn_calls;
-        st->converged = converged;
-        st->n_eff = n_eff;
-        st->res_mean = out[lio::kIeskfOutRes];
-        st->solve_ms = 0.0;  // on the device, inside the slot kernels
-        st->launch_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-        st->wait_ms = std::chrono::duration<double, std::milli>(t2 - t1).count();
-        st->wall_ms = std::chrono::duration<double, std::milli>(clk::now() - t_call).count();
-    }
-    return 0;
-}
-
-int lio_ctx_set_ieskf_mode(lio_ctx* c, int device) {
-    if (!c) return fail(LIO_ERR_ARG, "lio_ctx_set_ieskf_mode: bad arguments");
-    c->ieskf_device = device ? 1 : 0;
+int lio_ctx_set_seed_scale(lio_ctx* c, float scale) {
+    if (!c || !(scale > 0.f && scale <= 1.f)) return fail(LIO_ERR_ARG, "lio_ctx_set_seed_scale: scale in (0, 1]");
+    c->seed_scale = scale;
     return LIO_OK;
 }
 
@@ -1249,18 +960,12 @@ int lio_ieskf_update(lio_ctx* c, lio_state* xs, double* P, const lio_ieskf_param
     if (!c || !xs || !P) return fail(LIO_ERR_ARG, "lio_ieskf_update: bad arguments");
     const auto t_call = std::chrono::steady_clock::now();
     lio_ieskf_params pp = p ? *p : lio_ieskf_params{0.001, 3, 0.001};
-    const int env_mode = ieskf_device_default();
-    if (c->ieskf_device > 0 || (c->ieskf_device < 0 && env_mode == 1)) {
-        const int drc = ieskf_update_device(c, xs, P, pp, st, t_call);
-        if (drc <= 0) return drc;  // done (0) or failed (< 0); 1: the host loop below
-    }
     lio::host::State x = to_host(*xs);
     lio::host::Mat Pm(P, P + LIO_STATE_DIM * LIO_STATE_DIM);
     int err = LIO_OK;
     double launch_ms = 0.0, wait_ms = 0.0;
     auto hfn = [&](const lio::host::State& s, bool redo, bool want_rows, lio::host::HModel& hm) -> int {
         if (want_rows) {
-            cancel_pending(c);
             const int64_t want = (int64_t)hm.sums[LIO_SUMS_NEFF];
             hm.rows.assign((size_t)std::max<int64_t>(want, 1) * 7, 0.0);
             int64_t nr = 0;
@@ -1272,7 +977,7 @@ int lio_ieskf_update(lio_ctx* c, lio_state* xs, double* P, const lio_ieskf_param
         const lio_pose pose = state_pose(s);
         hm.rows.clear();
         c->last_launch_ms = c->last_wait_ms = 0.0;
-        int rc = match_impl(c, &pose, redo ? 1 : 0, hm.sums, hm.next, hm.n_next);
+        int rc = match_impl(c, &pose, redo ? 1 : 0, hm.sums);
         if (rc) return err = rc;
         launch_ms += c->last_launch_ms;
         wait_ms += c->last_wait_ms;
@@ -1280,7 +985,6 @@ int lio_ieskf_update(lio_ctx* c, lio_state* xs, double* P, const lio_ieskf_param
     };
     lio::host::IeskfResult r;
     int rc = lio::host::update_iterated(x, Pm, pp.laser_point_cov, pp.max_iteration, pp.epsi, hfn, r);
-    cancel_pending(c);  // a queued evaluation the loop did not ask for (it converged early)
     if (rc) return err ? err : fail(LIO_ERR_STATE, "IESKF: singular matrix");
     from_host(x, *xs);
     std::memcpy(P, Pm.data(), sizeof(double) * LIO_STATE_DIM * LIO_STATE_DIM);

@@ -2,8 +2,7 @@
 // /root/reference/fast_lio_sam/src/loop_closure.cpp:3-14, aligned at :81) on gfx950.
 //
 // Per ICP iteration (this rank's shard of the source):
-//   icp_tile_kernel  one wave (LIO_ICP_TILE_WAVES: 2 or 4 splitting the candidate
-//                    stream) per tile of <= 64 spatially compact source points (binned
+//   icp_tile_kernel  one wave per tile of <= 64 spatially compact source points (binned
 //                    once per setInputSource): apply the previous T_inc to
 //                    the incrementally transformed cloud (PCL transformCloud,
 //                    float SSE order [U]), exact unbounded 1-NN in the target
@@ -18,8 +17,6 @@
 // for any number of ranks).  The fitness pass is the same pipeline on the
 // ORIGINAL source transformed by the final T.
 #include <hipcub/hipcub.hpp>
-
-#include <cstdlib>
 
 #include "lio_dev.hpp"
 #include "lio_kernels.hpp"
@@ -370,7 +367,6 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
     const int k = a.order ? blockIdx.x * TPB + sub : xcd_block(blockIdx.x, gridDim.x) * TPB + sub;
     if (TPB > 1 && k >= ntiles) return;
     const int tix = a.order ? (int)a.order[k] : k;
-    const unsigned long long t_start = a.times ? wall_clock64() : 0ull;
     const uint2 tl = a.tiles[tix];
     const bool act = lane < (int)tl.y;
     const int i = act ? __float_as_int(a.qpts[tl.x + lane].w) : 0;
@@ -453,10 +449,6 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
     }
     const bool lead = NW > 1 ? threadIdx.x == 0 : lane == 0;
     if (a.tile_cost && lead) a.tile_cost[tix] = tile_tested;
-    if (a.times && lead) {
-        a.times[2 * tix] = t_start;
-        a.times[2 * tix + 1] = wall_clock64();
-    }
     if (a.dbg && lead) {
         atomicAdd(a.dbg, cand);
         atomicAdd(a.dbg + 1, (unsigned long long)rounds);
@@ -476,163 +468,6 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
     }
 }
 
-
-// ----------------------------------------------------------------------------
-// Exact 1-NN, one lane per query (icp_query_kernel, the default).
-//
-// The tile kernel above shares one candidate stream among a tile's 64 lanes, so
-// every lane tests every candidate of the tile's search box — a box sized by
-// the tile's WORST query (C4: ~570 candidates per query, ~4.2 k VALU per wave).
-// Here every lane searches its own sphere: queries stay in the binned (cell)
-// order, so a wave's 64 lanes are spatial neighbours that read the same target
-// cells (L1 / L2 hits), and each lane
-//   1. takes its previous correspondence as the first bound (later passes of an
-//      alignment), else scans its own 3x3x3 block of target cells (rows: one
-//      contiguous range of 3 cells each), growing the box (1 -> 3 -> 7 ... cells)
-//      while it has found nothing;
-//   2. scans every row of cells within sqrt(B) of the query, x-range trimmed to
-//      the sphere, rows pruned against the CURRENT best as it improves, minus
-//      the block of step 1.
-// Candidates are tested 4 per step (clamped indices: a repeated point leaves the
-// minimum unchanged).  Same total order (d2, id) and d2 formula as the tile
-// kernel, so the results are identical.
-// ----------------------------------------------------------------------------
-__device__ __forceinline__ void lane_scan_range(const GridDev& g, uint32_t b, uint32_t e, float x, float y, float z,
-                                                uint64_t& best, uint32_t& cand) {
-    if (b >= e) return;
-    cand += e - b;
-    const uint32_t last = e - 1;
-#pragma unroll 1
-    for (uint32_t j = b; j < e; j += 4) {
-        const float4 p0 = g.pts[j];
-        const float4 p1 = g.pts[min(j + 1, last)];
-        const float4 p2 = g.pts[min(j + 2, last)];
-        const float4 p3 = g.pts[min(j + 3, last)];
-        const uint64_t k0 = knn_key(sqdist3(x, y, z, p0.x, p0.y, p0.z), __float_as_int(p0.w));
-        const uint64_t k1 = knn_key(sqdist3(x, y, z, p1.x, p1.y, p1.z), __float_as_int(p1.w));
-        const uint64_t k2 = knn_key(sqdist3(x, y, z, p2.x, p2.y, p2.z), __float_as_int(p2.w));
-        const uint64_t k3 = knn_key(sqdist3(x, y, z, p3.x, p3.y, p3.z), __float_as_int(p3.w));
-        const uint64_t m01 = k0 < k1 ? k0 : k1, m23 = k2 < k3 ? k2 : k3;
-        const uint64_t m = m01 < m23 ? m01 : m23;
-        best = m < best ? m : best;
-    }
-}
-
-// rows (y, z) of box N minus the cells of box S (S may be empty: x0 > x1); with
-// prune, rows / x-ranges outside the sphere of the current best are skipped
-__device__ void lane_scan_box(const GridDev& g, const CellBox& N, const CellBox& S, bool prune, float x, float y,
-                              float z, uint64_t& best, uint32_t& cand) {
-    const float cs = g.cell, m = g.margin;
-    const bool sempty = S.x0 > S.x1;
-    const uint32_t gnx = (uint32_t)g.nx, gnxy = (uint32_t)g.nx * (uint32_t)g.ny;
-#pragma unroll 1
-    for (int rz = N.z0; rz <= N.z1; ++rz) {
-#pragma unroll 1
-        for (int ry = N.y0; ry <= N.y1; ++ry) {
-            int x0 = N.x0, x1 = N.x1;
-            if (prune) {
-                const float B = __uint_as_float((uint32_t)(best >> 32));
-                const float yl = g.oy + (float)ry * cs - m, zl = g.oz + (float)rz * cs - m;
-                const float g2 = axis_gap(y, yl, yl + cs + 2.f * m) + axis_gap(z, zl, zl + cs + 2.f * m);
-                if (g2 * 0.999999f > B) continue;
-                const float rx = sqrtf(fmaxf(B - g2 * 0.999999f, 0.f)) * 1.00001f + m;
-                x0 = max(x0, cell_coord(x - rx, g.ox, g.inv_cell));
-                x1 = min(x1, cell_coord(x + rx, g.ox, g.inv_cell));
-            }
-            if (x0 > x1) continue;
-            const uint32_t rowc = (uint32_t)rz * gnxy + (uint32_t)ry * gnx;
-            const bool inS = !sempty && ry >= S.y0 && ry <= S.y1 && rz >= S.z0 && rz <= S.z1;
-            const int lx1 = inS ? min(x1, S.x0 - 1) : x1;
-            if (x0 <= lx1) lane_scan_range(g, g.start[rowc + (uint32_t)x0], g.start[rowc + (uint32_t)lx1 + 1], x, y, z, best, cand);
-            const int rx0 = max(x0, S.x1 + 1);
-            if (inS && rx0 <= x1) lane_scan_range(g, g.start[rowc + (uint32_t)rx0], g.start[rowc + (uint32_t)x1 + 1], x, y, z, best, cand);
-        }
-    }
-}
-
-constexpr int kIcpQueryThreads = 256;
-
-__global__ void __launch_bounds__(kIcpQueryThreads) icp_query_kernel(IcpArgs a) {
-    const int blk = xcd_block(blockIdx.x, gridDim.x);  // neighbouring blocks (space) on one XCD's L2
-    const int q = blk * kIcpQueryThreads + threadIdx.x;
-    if (q >= a.n) return;  // per lane: no block-level synchronisation below
-    const int i = __float_as_int(a.qpts[q].w);
-    float x, y, z;
-    if (a.fitness) {  // getFitnessScore: original source * final
-        xform_pcl(a.T, a.src[3 * i], a.src[3 * i + 1], a.src[3 * i + 2], x, y, z);
-    } else {
-        x = a.cur[3 * i];
-        y = a.cur[3 * i + 1];
-        z = a.cur[3 * i + 2];
-        if (a.apply_T) {
-            float ox, oy, oz;
-            xform_pcl(a.T, x, y, z, ox, oy, oz);
-            x = ox;
-            y = oy;
-            z = oz;
-        }
-    }
-    const GridDev& g = a.grid;
-    uint64_t best = knn_key(INFINITY, kNone);
-    if (a.prior) {  // the previous correspondence: an exact candidate
-        const int prior = a.nn_id[i];
-        if (prior >= 0 && prior != kNone) {
-            const float4 p = a.tgt_by_id[prior];
-            best = knn_key(sqdist3(x, y, z, p.x, p.y, p.z), prior);
-        }
-    }
-    const int cx = cell_coord(x, g.ox, g.inv_cell), cy = cell_coord(y, g.oy, g.inv_cell),
-              cz = cell_coord(z, g.oz, g.inv_cell);
-    uint32_t cand = 0;
-    CellBox S{1, 0, 1, 0, 1, 0};  // scanned so far
-    if ((uint32_t)best == (uint32_t)kNone) {
-        // 1. bound: boxes of 1, 3, 7, ... cells around the query's cell until a candidate exists
-        for (int r = 1;; r = 2 * r + 1) {
-            const CellBox N{max(cx - r, 0), min(cx + r, g.nx - 1), max(cy - r, 0), min(cy + r, g.ny - 1),
-                            max(cz - r, 0), min(cz + r, g.nz - 1)};
-            if (N.x0 <= N.x1 && N.y0 <= N.y1 && N.z0 <= N.z1) {
-                CellBox Sc{max(S.x0, N.x0), min(S.x1, N.x1), max(S.y0, N.y0), min(S.y1, N.y1), max(S.z0, N.z0),
-                           min(S.z1, N.z1)};
-                if (Sc.x0 > Sc.x1 || Sc.y0 > Sc.y1 || Sc.z0 > Sc.z1) Sc = CellBox{1, 0, 1, 0, 1, 0};
-                lane_scan_box(g, N, Sc, false, x, y, z, best, cand);
-                S = N;
-            }
-            const bool full = cx - r <= 0 && cy - r <= 0 && cz - r <= 0 && cx + r >= g.nx - 1 && cy + r >= g.ny - 1 &&
-                              cz + r >= g.nz - 1;
-            if ((uint32_t)best != (uint32_t)kNone || full) break;
-        }
-    }
-    if ((uint32_t)best != (uint32_t)kNone) {
-        // 2. final: every row within sqrt(B) of the query, minus the scanned block
-        const float B = __uint_as_float((uint32_t)(best >> 32));
-        const float R = sqrtf(B) * 1.00001f + g.margin;
-        const CellBox N{max(cell_coord(x - R, g.ox, g.inv_cell), 0), min(cell_coord(x + R, g.ox, g.inv_cell), g.nx - 1),
-                        max(cell_coord(y - R, g.oy, g.inv_cell), 0), min(cell_coord(y + R, g.oy, g.inv_cell), g.ny - 1),
-                        max(cell_coord(z - R, g.oz, g.inv_cell), 0), min(cell_coord(z + R, g.oz, g.inv_cell), g.nz - 1)};
-        if (N.x0 <= N.x1 && N.y0 <= N.y1 && N.z0 <= N.z1) {
-            CellBox Sc{max(S.x0, N.x0), min(S.x1, N.x1), max(S.y0, N.y0), min(S.y1, N.y1), max(S.z0, N.z0), min(S.z1, N.z1)};
-            if (Sc.x0 > Sc.x1 || Sc.y0 > Sc.y1 || Sc.z0 > Sc.z1) Sc = CellBox{1, 0, 1, 0, 1, 0};
-            lane_scan_box(g, N, Sc, true, x, y, z, best, cand);
-        }
-    }
-    if (a.dbg) {
-        atomicAdd(a.dbg, (unsigned long long)cand);
-        if ((threadIdx.x & 63) == 0) atomicAdd(a.dbg + 2, 1ull);
-        atomicAdd(a.dbg + 3, 1ull);
-    }
-    if (a.fitness || a.apply_T) {
-        a.cur[3 * i] = x;
-        a.cur[3 * i + 1] = y;
-        a.cur[3 * i + 2] = z;
-    }
-    a.nn_d2[i] = __uint_as_float((uint32_t)(best >> 32));
-    a.nn_id[i] = (int)(uint32_t)best;
-}
-
-void launch_icp_query(const IcpArgs& a, hipStream_t st) {
-    if (a.n == 0) return;
-    icp_query_kernel<<<(a.n + kIcpQueryThreads - 1) / kIcpQueryThreads, kIcpQueryThreads, 0, st>>>(a);
-}
 
 // One block = one 4096-point record -> super[record][kIcpStride]: each lane
 // accumulates its 4 points (record-relative index lane + 1024 k, k ascending),
@@ -693,28 +528,11 @@ __global__ void __launch_bounds__(kIcpStatsThreads) icp_stats_kernel(IcpArgs a, 
     }
 }
 
+// one wave per tile (several waves per tile, or several one-wave tiles per block, measured no faster:
+// profiles/r02_icp_tile_experiments.txt)
 void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st) {
     if (a.n == 0 || ntiles == 0) return;
-    static const int nw = [] {  // LIO_ICP_TILE_WAVES: diagnostics override (1, 2, 4)
-        const char* e = std::getenv("LIO_ICP_TILE_WAVES");
-        return e ? std::atoi(e) : 1;
-    }();
-    static const int tpb = [] {  // LIO_ICP_TILES_PER_BLOCK: diagnostics override (1, 2, 4, 8)
-        const char* e = std::getenv("LIO_ICP_TILES_PER_BLOCK");
-        return e ? std::atoi(e) : 1;  // 2 / 4 / 8 measured no faster (profiles/r02_icp_tile_experiments.txt)
-    }();
-    if (nw == 2)
-        icp_tile_kernel<2, 1><<<ntiles, kIcpTileQ * 2, 0, st>>>(a, ntiles);
-    else if (nw == 4)
-        icp_tile_kernel<4, 1><<<ntiles, kIcpTileQ * 4, 0, st>>>(a, ntiles);
-    else if (tpb == 4)
-        icp_tile_kernel<1, 4><<<(ntiles + 3) / 4, kIcpTileQ * 4, 0, st>>>(a, ntiles);
-    else if (tpb == 2)
-        icp_tile_kernel<1, 2><<<(ntiles + 1) / 2, kIcpTileQ * 2, 0, st>>>(a, ntiles);
-    else if (tpb == 8)
-        icp_tile_kernel<1, 8><<<(ntiles + 7) / 8, kIcpTileQ * 8, 0, st>>>(a, ntiles);
-    else  // 1 wave per tile: best since the staging filter (its bound then sees every chunk)
-        icp_tile_kernel<1, 1><<<ntiles, kIcpTileQ, 0, st>>>(a, ntiles);
+    icp_tile_kernel<1, 1><<<ntiles, kIcpTileQ, 0, st>>>(a, ntiles);
 }
 
 // Longest-first tile order from the previous pass's candidate counts: tiles

@@ -103,6 +103,7 @@ struct lio_icp_group {
     int arrived = 0;
     uint64_t gen = 0;
     bool failed = false;
+    bool aborted = false;  // communicators aborted (and freed) once; destroy skips them
     std::vector<const double*> slots;
 };
 
@@ -123,15 +124,21 @@ bool host_barrier(lio_icp_group* g) {
     return !g->failed;
 }
 
+// Every rank that fails calls this; the communicators are aborted exactly once (ncclCommAbort frees
+// them: a second abort, or ncclCommDestroy afterwards, would be a use after free), under the lock.
 void fail_group(lio_icp_group* g) {
     {
         std::lock_guard<std::mutex> lk(g->mu);
         g->failed = true;
+        if (g->use_rccl && !g->aborted) {
+            g->aborted = true;
+            // ranks waiting on an all-gather's stream return once their communicators abort
+            for (ncclComm_t c : g->comms)
+                if (c) (void)g->rccl.CommAbort(c);
+            g->comms.clear();  // destroy sees no communicator
+        }
     }
     g->cv.notify_all();
-    if (g->use_rccl)  // ranks blocked inside ncclAllGather return once their communicators abort
-        for (ncclComm_t c : g->comms)
-            if (c) (void)g->rccl.CommAbort(c);
 }
 
 // lio_allgather_fn of rank r: `n` doubles from every rank, rank order
@@ -157,7 +164,14 @@ int group_allgather(const double* send, int64_t n, double* recv, void* user) {
     }
     if (hipMemcpyAsync(r->d_send, send, (size_t)n * sizeof(double), hipMemcpyHostToDevice, r->st) != hipSuccess)
         return -1;
-    if (g->rccl.AllGather(r->d_send, r->d_recv, (size_t)n, kNcclDouble, g->comms[r->rank], r->st) != 0) return -1;
+    {
+        // the enqueue (asynchronous: the wait is the stream sync below) runs under the lock that
+        // fail_group aborts under, so it never touches a communicator an abort has freed
+        std::lock_guard<std::mutex> lk(g->mu);
+        if (g->failed || g->comms.empty()) return -1;  // another rank failed: its abort freed the comms
+        if (g->rccl.AllGather(r->d_send, r->d_recv, (size_t)n, kNcclDouble, g->comms[r->rank], r->st) != 0)
+            return -1;
+    }
     if (hipMemcpyAsync(recv, r->d_recv, (size_t)n * g->world * sizeof(double), hipMemcpyDeviceToHost, r->st) !=
         hipSuccess)
         return -1;

@@ -162,7 +162,7 @@ struct lio_icp {
     uint32_t* d_tcost = nullptr;  // per tile: candidates of the last pass
     uint32_t* d_order = nullptr;  // longest-first tile order (valid when have_order)
     bool have_order = false;
-    unsigned long long* d_dbg = nullptr;  // LIO_ICP_DEBUG counters
+    unsigned long long* d_dbg = nullptr;  // search counters (diagnostics build: LIO_DIAG + LIO_ICP_DEBUG)
     double* h_super = nullptr;      // pinned, host-mapped: the pass's 4096-point records
     double* h_super_dev = nullptr;  // device view of h_super (the statistics kernel writes it, zero-copy)
     int64_t super_cap = 0;
@@ -201,10 +201,6 @@ int lio_icp_create(const lio_icp_params* p, lio_icp** out) {
     h->dev = p->device;
     h->p = *p;
     if (!(h->p.cell_size > 0.f)) h->p.cell_size = 1.0f;  // 0.3 m voxelised submaps: 1 m target cells (scripts/icp_cells.py)
-    if (const char* e = std::getenv("LIO_ICP_TILE_CELL")) {  // diagnostics override (scripts/icp_cells.py)
-        const float v = (float)std::atof(e);
-        if (v > 0.f) h->tile_cell = v;
-    }
     if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess) {
         delete h;
         return ifail(LIO_ERR_HIP, "icp stream/alloc failed");
@@ -327,25 +323,6 @@ static int icp_prepare(lio_icp* h) {
     return LIO_OK;
 }
 
-// LIO_ICP_ORDER=0 keeps every pass in cell order (A/B switch for the longest-first tile order).
-static bool icp_order_on() {
-    static const bool on = [] {
-        const char* e = std::getenv("LIO_ICP_ORDER");
-        return e ? std::atoi(e) != 0 : true;
-    }();
-    return on;
-}
-
-// LIO_ICP_KERNEL=query: one lane per query (icp_query_kernel) instead of the tile kernel (one candidate
-// stream per 64-query tile) — A/B switch; both give identical correspondences.
-static bool icp_tile_kernel_on() {
-    static const bool on = [] {
-        const char* e = std::getenv("LIO_ICP_KERNEL");
-        return !(e && std::string(e) == "query");
-    }();
-    return on;
-}
-
 // One correspondence (or fitness) pass: GPU kernels + exchange + ordered sum.
 static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, double max_d2, double out17[17]) {
     lio::IcpArgs a{};
@@ -360,38 +337,25 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     a.max_d2 = max_d2;
     a.fitness = fitness ? 1 : 0;
     a.prior = h->have_prior ? 1 : 0;
-    static const int r0 = [] {  // LIO_ICP_R0: first bound box growth (1: rounds/tile 2.73 -> 2.19 at C4)
-        const char* e = std::getenv("LIO_ICP_R0");
-        return e ? std::max(0, std::atoi(e)) : 1;
-    }();
-    a.r0 = r0;
+    a.r0 = 1;  // first bound box: the tile's cells grown by one target cell (rounds/tile 2.73 -> 2.19 at C4)
     a.nn_d2 = h->d_fd2;
     a.nn_id = h->d_fid;
     a.qpts = h->qgrid.pts;
     a.tiles = h->d_tiles;
     a.tile_cost = h->d_tcost;
     a.order = h->have_order ? h->d_order : nullptr;
-    static const bool dbg_on = std::getenv("LIO_ICP_DEBUG") != nullptr;  // search statistics on stderr
+#ifdef LIO_DIAG
+    static const bool dbg_on = std::getenv("LIO_ICP_DEBUG") != nullptr;  // diagnostics build: search statistics
     if (dbg_on) {
         if (!h->d_dbg) IHIP(hipMalloc(&h->d_dbg, 64));
         IHIP(hipMemsetAsync(h->d_dbg, 0, 64, h->st));
         a.dbg = h->d_dbg;
     }
-    static const bool times_on = std::getenv("LIO_ICP_TIMES") != nullptr;  // per-tile timeline on stderr
-    std::vector<unsigned long long> h_times;
-    unsigned long long* d_times = nullptr;
-    if (times_on && h->ntiles > 0 && icp_tile_kernel_on()) {
-        IHIP(hipMalloc(&d_times, (size_t)h->ntiles * 2 * sizeof(unsigned long long)));
-        IHIP(hipMemsetAsync(d_times, 0, (size_t)h->ntiles * 2 * sizeof(unsigned long long), h->st));
-        a.times = d_times;
-    }
+#endif
     const int nsup_loc = (int)((h->sh_n + lio::kIcpSuper - 1) / lio::kIcpSuper);
     if (h->sh_n > 0) {
         if (h->timing) IHIP(hipEventRecord(h->ev.a, h->st));
-        if (icp_tile_kernel_on())
-            lio::launch_icp_tiles(a, h->ntiles, h->st);
-        else
-            lio::launch_icp_query(a, h->st);
+        lio::launch_icp_tiles(a, h->ntiles, h->st);
         if (h->timing) IHIP(hipEventRecord(h->ev.m, h->st));
         lio::launch_icp_stats(a, h->h_super_dev, h->st);  // records straight to host memory
         if (h->timing) IHIP(hipEventRecord(h->ev.b, h->st));
@@ -399,39 +363,16 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
         IHIP(hipEventRecord(h->ev.done, h->st));
         // longest-first order for the next pass of this alignment: behind the records, so it runs
         // while the host does the SVD / convergence test
-        if (!fitness && icp_order_on() && icp_tile_kernel_on())
+        if (!fitness)
             lio::launch_icp_order(h->d_tcost, h->ntiles, h->d_order, h->st);
         IHIP(hipGetLastError());
         IHIP(hipEventSynchronize(h->ev.done));
     } else {
         IHIP(hipStreamSynchronize(h->st));
     }
-    if (d_times) {  // tiles active over the pass (20 bins), tile duration percentiles (us, 100 MHz clock)
-        h_times.resize((size_t)h->ntiles * 2);
-        IHIP(hipMemcpy(h_times.data(), d_times, h_times.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-        IHIP(hipFree(d_times));
-        unsigned long long t0 = ~0ull, t1 = 0;
-        std::vector<double> dur;
-        for (int t = 0; t < h->ntiles; ++t) {
-            t0 = std::min(t0, h_times[2 * t]);
-            t1 = std::max(t1, h_times[2 * t + 1]);
-            dur.push_back((double)(h_times[2 * t + 1] - h_times[2 * t]) * 0.01);
-        }
-        std::sort(dur.begin(), dur.end());
-        const double span = (double)(t1 - t0);
-        int bins[20] = {0};
-        for (int t = 0; t < h->ntiles; ++t)
-            for (int k = 0; k < 20; ++k) {
-                const double lo = t0 + span * k / 20, hi = t0 + span * (k + 1) / 20;
-                if ((double)h_times[2 * t] < hi && (double)h_times[2 * t + 1] > lo) ++bins[k];
-            }
-        std::fprintf(stderr, "icp times: span %.1f us, tile us p50 %.1f p90 %.1f p99 %.1f max %.1f; active per 5%%:", span * 0.01,
-                     dur[dur.size() / 2], dur[dur.size() * 9 / 10], dur[dur.size() * 99 / 100], dur.back());
-        for (int k = 0; k < 20; ++k) std::fprintf(stderr, " %d", bins[k]);
-        std::fprintf(stderr, "\n");
-    }
     h->have_prior = true;
-    if (!fitness && h->sh_n > 0 && icp_order_on() && icp_tile_kernel_on()) h->have_order = true;
+    if (!fitness && h->sh_n > 0) h->have_order = true;
+#ifdef LIO_DIAG
     if (dbg_on) {
         unsigned long long c[5];
         IHIP(hipMemcpy(c, h->d_dbg, sizeof(c), hipMemcpyDeviceToHost));
@@ -439,6 +380,7 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
                      "icp dbg: tiles|waves %llu lanes %llu cand/tile %.1f tested/tile %.1f rounds/tile %.2f cand/lane %.1f\n",
                      c[2], c[3], (double)c[0] / c[2], (double)c[4] / c[2], (double)c[1] / c[2], (double)c[0] / c[3]);
     }
+#endif
     if (h->timing && h->sh_n > 0) {
         float ms = 0.f;
         if (hipEventElapsedTime(&ms, h->ev.a, h->ev.b) == hipSuccess) {

@@ -7,9 +7,6 @@
 
 namespace lio {
 
-struct IeskfCtl;  // ieskf_dev.hpp
-struct GateIn;
-
 struct MatchArgs {
     PoseArg pose;
     GridDev grid;
@@ -24,11 +21,9 @@ struct MatchArgs {
     unsigned long long* seq_out;  // written with `seq` after sums_out (host-mapped)
     unsigned long long seq;
     int* dbg;                 // optional n*3 search statistics (diagnostics only)
-    unsigned long long* tdbg; // optional per-wave (start, end) wall clock of the near pass (diagnostics only)
     int* far_list;            // n: points queued for the far pass
     int* far_count;           // queue length (reset to 0 by plane_kernel)
     unsigned* done_count;     // blocks of plane/reuse finished (0 between launches; the last block resets it)
-    int fused_final;          // 1: the last plane/reuse block publishes the sums; 0: launch_finalize does
     float* far_d;             // n*5 their near-pass lists
     int* far_id;
     int n;
@@ -41,31 +36,14 @@ struct MatchArgs {
     PoseArg pose_knn;         // pose of the previous kNN evaluation (seeded near pass: w_old)
     float knn_M[12];          // the same as one float affine map body -> world (row-major 3x4): the seeded
                               // pass's displacement bound (error covered by a margin)
-    float seed_scale;         // seeded bound factor: 1 (LIO_KNN_SEED_SCALE < 1 forces the not-full guard: tests)
-    IeskfCtl* ctl;            // device-resident update: control block (state, pose, loop flags); else null
-    double* ieskf_out;        // device-resident update: host-mapped result (ieskf_dev.hpp layout)
+    float seed_scale;         // seeded bound factor: 1 (lio_ctx_set_seed_scale < 1 forces the not-full guard: tests)
 };
 
-// marks (optional, redo only): events recorded after the near and the far kernel
 // marks (optional, timing): 8 events, start / stop of near, far, plane (redo) or reuse (marks[6..7]),
-// recorded by hipExtLaunchKernel at each kernel's own start and end
+// recorded by hipExtLaunchKernel at each kernel's own start and end.  Returns the plane / reuse grid.
 int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* marks = nullptr);
-// An h-evaluation queued before the host knows its pose (lio_ieskf_update's host loop):
-// a one-wave gate kernel waits for `in->seq >= gate_seq` (host-mapped), copies the pose / command into
-// a.ctl, and the kernel behind it (kNN: the near pass; reuse: the reuse pass) reads its pose from a.ctl
-// (a cancelled one exits).  A released kNN evaluation's far + plane passes follow with launch_knn_tail
-// (their launch hides behind the near pass).
-void launch_h_model_gated(const MatchArgs& a, bool redo, const GateIn* in, unsigned long long gate_seq, hipStream_t st);
-int launch_knn_tail(const MatchArgs& a, hipStream_t st);
-// Device-resident lio_ieskf_update: the init kernel (reads `in`, host-mapped, kIeskfInWords doubles)
-// and max_iter + 1 evaluation slots (near, far, plane-or-reuse + IESKF step), enqueued on st without
-// a host round trip.  marks (optional, timing): 6 events per slot, start / stop of near, far, slot kernel.
-void launch_ieskf_dev(const MatchArgs& a, const double* in, unsigned long long seq, int max_iter, hipStream_t st,
-                      hipEvent_t* marks = nullptr);
-size_t ieskf_ctl_bytes();
 void launch_debug(const MatchArgs& a, float* world, float* d2, float* abcd_pd2, hipStream_t st);
 void launch_h_rows(const MatchArgs& a, double* rows, int64_t max_rows, int64_t* n_rows, hipStream_t st);
-void launch_finalize(const MatchArgs& a, int nblocks, hipStream_t st);  // no-op when fused_final
 int match_blocks(int n);
 // batch Nearest_Search: k <= 5 neighbours per query within d2 <= bound (INFINITY: unbounded)
 void launch_map_knn(const GridDev& g, const float* q, int n, float bound, int max_shell, int k, int32_t* idx,
@@ -143,7 +121,6 @@ struct IcpArgs {
     const uint32_t* order;  // optional tile visit order (heaviest first, from the previous pass's costs)
     uint32_t* tile_cost;    // per tile: candidates scanned in this pass
     unsigned long long* dbg;  // optional counters (diagnostics): candidates, rings, tiles, lanes
-    unsigned long long* times;  // optional per tile (start, end) wall clock (diagnostics: LIO_ICP_TIMES)
 };
 
 constexpr int kIcpSuper = 4096;    // points per exchanged partial (shard granule)
@@ -156,8 +133,6 @@ constexpr int kIcpTileQ = 64;     // queries per tile (one wave)
 // the tile count (synchronises the stream once).  tiles: capacity n + n / 64 + 1.
 int icp_build_tiles(const GridBuf& q, uint2* tiles, uint32_t* scratch, void*& tmp, size_t& tmp_bytes, hipStream_t st);
 void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st);
-// exact 1-NN, one lane per query in binned order (default; LIO_ICP_KERNEL=tile selects the tile kernel)
-void launch_icp_query(const IcpArgs& a, hipStream_t st);
 // tile order for the next pass: descending log2(cost) buckets (one block)
 void launch_icp_order(const uint32_t* tile_cost, int ntiles, uint32_t* order, hipStream_t st);
 void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st);  // one record per 4096 points

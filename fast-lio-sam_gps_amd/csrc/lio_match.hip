@@ -22,20 +22,21 @@
 // materialised: the IESKF only consumes H^T H and H^T h.
 #include <hip/hip_ext.h>
 
-#include "ieskf_dev.hpp"
 #include "lio_dev.hpp"
 #include "lio_kernels.hpp"
 
 #include <algorithm>
-#include <cstdlib>
 
 namespace lio {
 
-constexpr int kBlock = 256;  // plane / reuse: 1 point per lane (1024-thread blocks measured slower)
+constexpr int kBlock = 256;  // partial-slot granule (the plane / reuse grids below never exceed n / 256 blocks)
+constexpr int kPlaneBlock = 512;  // plane pass: 512 threads, 1 point per lane
+constexpr int kReuseBlock = 512;  // reuse pass: 512 threads, 2 points per lane
+constexpr int kReusePpl = 2;
+constexpr int kNearBlock = 256;   // near pass: 32 queries per block
 
 constexpr int kGroup = 8;   // lanes cooperating on one query's kNN
-constexpr int kKnnBlock = 512;
-constexpr int kFarBlock = 128;  // threads per far query (64 / 256 / 512: LIO_FAR_THREADS, measured slower)
+constexpr int kFarBlock = 128;  // threads per far query (64 / 256 / 512 measured slower)
 constexpr int kFarBlocks = 1024;  // blocks striding the far queue (one query per block)
 
 __device__ __forceinline__ double wave_sum(double v) {
@@ -64,11 +65,11 @@ __device__ __forceinline__ bool residual_row(const MatchArgs& a, const PoseArg& 
 // neighbourhoods, ~0.4% of a dense scan) are queued, with their list, for
 // the wave-per-query far pass instead of holding their wave: a kernel runs as
 // long as its slowest wave.  Written for 8 waves/SIMD (<= 64 VGPRs).
-template <bool DBG, bool SEEDED, int U = 4, bool DEV = false, int NB = kKnnBlock, int UO = 4>
+// U / UO: loads in flight in the seeded table scan / own-cell scan (2 keeps the kernel at <= 64 VGPRs
+// without scratch).
+template <bool DBG, bool SEEDED, int U, int NB, int UO>
 __global__ void __launch_bounds__(NB) __attribute__((amdgpu_waves_per_eu(8, 8))) knn_near_kernel(MatchArgs a) {
-    if constexpr (DEV)  // device-resident update: this slot runs only while the loop asks for a kNN
-        if (a.ctl->done || !a.ctl->converge) return;
-    const PoseArg& ps = DEV ? a.ctl->pose : a.pose;
+    const PoseArg& ps = a.pose;
     constexpr int G = kGroup;
     constexpr int QPB = NB / G;  // 64 queries per block
     __shared__ uint32_t s_tab[QPB][72];      // per-group shell-1 slot table
@@ -78,7 +79,6 @@ __global__ void __launch_bounds__(NB) __attribute__((amdgpu_waves_per_eu(8, 8)))
     const int sub = threadIdx.x % G;
     const int q = threadIdx.x / G;
     const int i = blk * QPB + q;
-    const unsigned long long t_beg = a.tdbg ? wall_clock64() : 0ull;
     // the per-query transforms once per query, not once per lane of its group: wave 0, lane = query
     if (threadIdx.x < QPB) {
         const int iq = blk * QPB + (int)threadIdx.x;
@@ -96,15 +96,11 @@ __global__ void __launch_bounds__(NB) __attribute__((amdgpu_waves_per_eu(8, 8)))
             s_c[1][threadIdx.x] = cy;
             s_c[2][threadIdx.x] = cz;
             if constexpr (SEEDED) {
-                float wox, woy, woz;
-                if constexpr (DEV) {
-                    body_to_world(a.ctl->pose_knn, bx, by, bz, wox, woy, woz);
-                } else {  // float affine map of the previous kNN pose: w_old within ~1e-5 m, covered by the bound's margin
-                    const float* M = a.knn_M;
-                    wox = ((M[0] * bx + M[1] * by) + M[2] * bz) + M[3];
-                    woy = ((M[4] * bx + M[5] * by) + M[6] * bz) + M[7];
-                    woz = ((M[8] * bx + M[9] * by) + M[10] * bz) + M[11];
-                }
+                // float affine map of the previous kNN pose: w_old within ~1e-5 m, covered by the bound's margin
+                const float* M = a.knn_M;
+                const float wox = ((M[0] * bx + M[1] * by) + M[2] * bz) + M[3];
+                const float woy = ((M[4] * bx + M[5] * by) + M[6] * bz) + M[7];
+                const float woz = ((M[8] * bx + M[9] * by) + M[10] * bz) + M[11];
                 const bool inside = (unsigned)cx < (unsigned)a.grid.nx && (unsigned)cy < (unsigned)a.grid.ny &&
                                     (unsigned)cz < (unsigned)a.grid.nz;
                 s_q[3][threadIdx.x] = seeded_bound(inside, a.nn_d5[iq], wox, woy, woz, wx, wy, wz, a.range_sq, a.seed_scale);
@@ -150,11 +146,6 @@ __global__ void __launch_bounds__(NB) __attribute__((amdgpu_waves_per_eu(8, 8)))
                 a.far_id[5 * (size_t)slot + j] = tk.id(j);
             }
         }
-        if (a.tdbg && (threadIdx.x & 63) == 0) {
-            const size_t wv = (size_t)blockIdx.x * (NB / 64) + (threadIdx.x >> 6);
-            a.tdbg[2 * wv] = t_beg;
-            a.tdbg[2 * wv + 1] = wall_clock64();
-        }
         return;
     }
 #pragma unroll
@@ -169,21 +160,14 @@ __global__ void __launch_bounds__(NB) __attribute__((amdgpu_waves_per_eu(8, 8)))
         }
     }
     if (sub == 5) a.nn_d5[i] = tk.id(4) == kNone ? INFINITY : tk.d(4);
-    if (a.tdbg && (threadIdx.x & 63) == 0) {
-        const size_t wv = (size_t)blockIdx.x * (NB / 64) + (threadIdx.x >> 6);
-        a.tdbg[2 * wv] = t_beg;
-        a.tdbg[2 * wv + 1] = wall_clock64();
-    }
 }
 
 // Pass 2: the queued queries, one block each (block_knn_box_flat over the
 // rest of the query's search box).  Fixed grid; every block strides the queue
 // and exits once past its end.
-template <bool DEV = false, int NT = kFarBlock>
+template <int NT = kFarBlock>
 __global__ void __launch_bounds__(NT) knn_far_kernel(MatchArgs a) {
-    if constexpr (DEV)
-        if (a.ctl->done || !a.ctl->converge) return;
-    const PoseArg& ps = DEV ? a.ctl->pose : a.pose;
+    const PoseArg& ps = a.pose;
     __shared__ uint32_t s_b[NT], s_off[NT + 1], s_w[NT / 64];
     __shared__ uint64_t s_lists[(NT / 64) * 5];
     const int cnt = *a.far_count;
@@ -248,7 +232,7 @@ __device__ __forceinline__ void publish_host(double t, double* out, unsigned lon
 
 // Block partial -> global; returns true in the LAST block to finish, whose
 // lanes < 32 then hold the 32 fixed-order sums in `t` (wave 0; block-uniform
-// return value).  fused_final == 0: partial only, the finalize launch sums.
+// return value).
 // slot: this block's partial index (-1: none); npart partials are summed; ncount
 // blocks take part in the counter.  All threads of the block call it.
 template <int BS = kBlock>
@@ -257,15 +241,6 @@ __device__ __forceinline__ bool block_partial_last(const MatchArgs& a, double (*
     __shared__ int s_last;
     const int nb = npart;
     t = 0.0;
-    if (!a.fused_final) {  // separate finalize_kernel launch (A/B switch LIO_FUSED_FINAL=0)
-        if (threadIdx.x < 32) {
-            double s = 0.0;
-#pragma unroll
-            for (int w = 0; w < BS / 64; ++w) s += red[w][threadIdx.x];
-            a.partials[(size_t)blockIdx.x * 32 + threadIdx.x] = s;
-        }
-        return false;
-    }
     if (slot >= 0 && threadIdx.x < 32) {
         double s = 0.0;
 #pragma unroll
@@ -332,28 +307,6 @@ __device__ __forceinline__ void accum_row(double (&v)[32], const double J[6], do
     v[27] += cnt;
     v[28] += res;
     v[29] += h * h;
-}
-
-// Points per lane of the plane / reuse kernels (LIO_PPL, default kPplDefault): PPL > 1 gives each
-// lane several points' loads in flight and fewer block partials for the last block to gather.
-constexpr int kPplDefault = 2;
-static int ppl_setting() {
-    static const int v = [] {
-        const char* e = std::getenv("LIO_PPL");
-        const int p = e ? std::atoi(e) : kPplDefault;
-        return (p == 1 || p == 2 || p == 4) ? p : kPplDefault;
-    }();
-    return v;
-}
-
-// Host-loop path: the plane kernel in 512-thread blocks, 1 point per lane (2 waves per SIMD at 88
-// VGPRs instead of 1 at 120 with 256 x 2; same partial count): 14.5 -> 13.5 us at C3; the reuse kernel
-// in 512-thread blocks, 2 points per lane (half the partials for the last block): 9.1 -> 8.8 us.  An
-// explicit LIO_PPL selects the 256-thread kernels with that PPL (diagnostics).
-constexpr int kPlaneBlock = 512;
-static bool plane_wide() {
-    static const bool v = std::getenv("LIO_PPL") == nullptr;
-    return v;
 }
 
 // Plane pass body, lane = PPL points (strided by the block size, coalesced): gate
@@ -439,16 +392,12 @@ __device__ __forceinline__ void reuse_points(const MatchArgs& a, const PoseArg& 
     }
 }
 
-// Pass 3 (kNN evaluations): plane_points, wave sums, 4 wave partials combined in
-// LDS -> block partial; the last block publishes.  Resets the far queue for the
-// next kNN evaluation.
-// GATED: queued ahead of the host's decision (launch_h_model_gated): the pose comes from the control
-// block the gate kernel fills, and a cancelled evaluation (ctl->done) does nothing.
-template <int PPL, bool GATED = false, int BS = kBlock>
+// Pass 3 (kNN evaluations): plane_points, wave sums, the block's wave partials
+// combined in LDS -> block partial; the last block publishes.  Resets the far
+// queue for the next kNN evaluation.
+template <int PPL, int BS>
 __global__ void __launch_bounds__(BS) plane_kernel(MatchArgs a) {
-    if constexpr (GATED)
-        if (a.ctl->done) return;
-    const PoseArg& ps = GATED ? a.ctl->pose : a.pose;
+    const PoseArg& ps = a.pose;
     __shared__ double red[BS / 64][32];
     double v[32];
 #pragma unroll
@@ -463,11 +412,9 @@ __global__ void __launch_bounds__(BS) plane_kernel(MatchArgs a) {
 }
 
 // ekfom_data.converge == false: reuse_points, same reduction and publish.
-template <int PPL, bool GATED = false, int BS = kBlock>
+template <int PPL, int BS>
 __global__ void __launch_bounds__(BS) h_model_reuse_kernel(MatchArgs a) {
-    if constexpr (GATED)
-        if (a.ctl->done) return;
-    const PoseArg& ps = GATED ? a.ctl->pose : a.pose;
+    const PoseArg& ps = a.pose;
     __shared__ double red[BS / 64][32];
     double v[32];
 #pragma unroll
@@ -478,131 +425,6 @@ __global__ void __launch_bounds__(BS) h_model_reuse_kernel(MatchArgs a) {
     if (lane < 32) red[wid][wave_sum32_index(lane)] = tot;
     __syncthreads();
     publish_and_finalize<BS>(a, red);
-}
-
-// Device-resident update (lio_ieskf_update): one h-evaluation slot of
-// the enqueued sequence.  Gate and path come from the control block: nothing
-// once the loop has finished, the plane pass when this iteration redoes the
-// kNN (ekfom_data.converge), the reuse pass otherwise.  Grid = 1 + point
-// blocks: block 0 runs the IESKF pre-step (state-only part, ieskf_dev.hpp)
-// while blocks 1.. do the points; the last block to finish (any of them) sums
-// the partials and runs the post-step, which publishes the finished update.
-template <int PPL>
-__global__ void __launch_bounds__(kBlock) h_eval_dev_kernel(MatchArgs a) {
-    IeskfCtl* g = a.ctl;
-    if (g->done) return;
-    const bool knn = g->converge != 0;
-    __shared__ double red[kBlock / 64][32];
-    __shared__ IeskfShared S;
-    const int np = (int)gridDim.x - 1;  // point blocks
-    double t;
-    bool last;
-    if (blockIdx.x == 0) {
-        if (threadIdx.x < 64) ieskf_prestep(g, S);
-        last = block_partial_last(a, red, t, -1, np, np + 1);
-    } else {
-        double v[32];
-#pragma unroll
-        for (int q = 0; q < 32; ++q) v[q] = 0.0;
-        if (knn)
-            plane_points<PPL>(a, g->pose, blockIdx.x - 1, v);
-        else
-            reuse_points<PPL>(a, g->pose, blockIdx.x - 1, v);
-        const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-        const double tot = wave_sum32(v, lane);
-        if (lane < 32) red[wid][wave_sum32_index(lane)] = tot;
-        __syncthreads();
-        if (knn && blockIdx.x == 1 && threadIdx.x == 0) *a.far_count = 0;
-        last = block_partial_last(a, red, t, blockIdx.x - 1, np, np + 1);
-    }
-    if (!last || threadIdx.x >= 64) return;
-    if (threadIdx.x < 32) S.sums[threadIdx.x] = t;
-    wsync();
-    ieskf_poststep(g, S, a.ieskf_out);
-}
-
-// Gate of an evaluation queued before the host's decision (launch_h_model_gated): one lane
-// waits for the host to publish gate word `seq` (host-mapped, written after the pose) and copies
-// the command and the poses into the control block, which the evaluation's kernels behind it read
-// (DEV near / far, GATED plane / reuse).  Command: 1 run, 2 cancel.  The wait is bounded (20 ms,
-// then cancel), so a host that never answers cannot hold the queue.
-__global__ void __launch_bounds__(64) eval_gate_kernel(IeskfCtl* g, const GateIn* in, unsigned long long seq, int knn) {
-    typedef __attribute__((address_space(1))) const unsigned long long cgull;
-    typedef __attribute__((address_space(1))) const double cgdouble;
-    const int lane = threadIdx.x;
-    int ok = 0;
-    if (lane == 0) {  // one lane polls (relaxed, uncached system-scope loads: an acquire would
-                      // invalidate the L2 on every poll); the others wait at the reconvergence point
-        const unsigned long long t0 = wall_clock64();
-        for (;;) {
-            if (__hip_atomic_load((cgull*)&in->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= seq) {
-                ok = 1;
-                break;
-            }
-            if (wall_clock64() - t0 > 2000000ull) break;  // 100 MHz constant clock: 20 ms
-            __builtin_amdgcn_s_sleep(8);  // ~0.2 us between PCIe polls
-        }
-    }
-    ok = __shfl(ok, 0, 64);
-    unsigned long long cmd = 2;
-    if (ok && lane == 0) cmd = __hip_atomic_load((cgull*)&in->cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    cmd = __shfl(cmd, 0, 64);
-    if (cmd == 1) {
-        // the two poses (2 x 32 words) in ONE round trip: a word per lane, issued after seq was seen
-        // (the host wrote them before seq)
-        constexpr int W = (int)(sizeof(PoseArg) / sizeof(double));
-        static_assert(2 * W <= 64, "eval_gate_kernel: a pose word per lane");
-        if (lane < 2 * W && (knn || lane < W)) {
-            const double* src = lane < W ? reinterpret_cast<const double*>(&in->pose) + lane
-                                         : reinterpret_cast<const double*>(&in->pose_knn) + (lane - W);
-            double* dst = lane < W ? reinterpret_cast<double*>(&g->pose) + lane
-                                   : reinterpret_cast<double*>(&g->pose_knn) + (lane - W);
-            *dst = __hip_atomic_load((cgdouble*)src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-    }
-    if (lane == 0) {
-        g->converge = knn;
-        g->done = cmd == 1 ? 0 : 1;
-    }
-}
-
-// Device-resident update: the control block from the host-mapped input (one block).
-__global__ void __launch_bounds__(256) ieskf_init_kernel(IeskfCtl* g, const double* in, unsigned long long seq) {
-    ieskf_init(g, in, seq);
-}
-
-// Fixed-order sum of nblocks x 32 partials -> 32 sums (one block of 1024):
-// 32 row groups x 32 columns, each thread issues its rows' loads 8 at a time
-// and adds them in row order, then the 32 group sums in group order
-// (deterministic for a given nblocks).  The sums go straight to the ctx's
-// host-mapped result (zero-copy), followed by the sequence number the host
-// waits on (no copy launch, no stream-sync round trip).
-__global__ void __launch_bounds__(1024) finalize_kernel(const double* __restrict__ partials, int nblocks,
-                                                       double* __restrict__ out, unsigned long long* seq_out,
-                                                       unsigned long long seq) {
-    __shared__ double sg[32][33];
-    const int col = threadIdx.x & 31, grp = threadIdx.x >> 5;
-    const int per = (nblocks + 31) / 32;
-    const int b0 = grp * per, b1 = min(nblocks, b0 + per);
-    double s = 0.0;
-    int b = b0;
-    for (; b + 8 <= b1; b += 8) {
-        double v[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) v[k] = partials[(size_t)(b + k) * 32 + col];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) s += v[k];
-    }
-    for (; b < b1; ++b) s += partials[(size_t)b * 32 + col];
-    sg[grp][col] = s;
-    __syncthreads();
-    if (threadIdx.x < 64) {
-        double t = 0.0;
-        if (threadIdx.x < 32)
-#pragma unroll
-            for (int g = 0; g < 32; ++g) t += sg[g][threadIdx.x];
-        publish_host(t, out, seq_out, seq);
-    }
 }
 
 // ikd-Tree Nearest_Search(point, k, Nearest_Points, Point_Distance, max_dist)
@@ -714,183 +536,40 @@ __global__ void __launch_bounds__(1024) h_rows_kernel(MatchArgs a, double* __res
 }
 
 // ---------------------------------------------------------------- launchers
-// Near pass on the host-loop path (A/B: profiles/r02_near_ab.txt):
-//  * 2 loads in flight in the seeded table scan and in the own-cell scan (56 / 58 VGPRs, no scratch):
-//    the 4-load forms sit at the 64-VGPR cap with 8-12 B/lane of spills (kNN h-evaluation traffic
-//    23.2 vs 18.6 MB at C3) for ~0.5 us less per pass; LIO_NEAR_NOSPILL=0 restores them;
-//  * 256-thread blocks (32 queries; finer grain for the second round of blocks at C3): near pass
-//    -0.5 to -0.8 us; LIO_NEAR_BLOCK=512 restores 64 queries per block.
-static bool near_nospill() {
-    static const bool v = [] {
-        const char* e = std::getenv("LIO_NEAR_NOSPILL");
-        return !(e && std::atoi(e) == 0);
-    }();
-    return v;
-}
-
-static int near_block() {
-    static const int v = [] {
-        const char* e = std::getenv("LIO_NEAR_BLOCK");
-        const int b = e ? std::atoi(e) : 256;
-        return (b == 512 || b == 128) ? b : 256;
-    }();
-    return v;
-}
-
-template <int NB>
-static void launch_near_nb(const MatchArgs& a, int nq, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
-    if (a.prior) {
-        if (near_nospill())
-            hipExtLaunchKernelGGL((knn_near_kernel<false, true, 2, false, NB, 4>), dim3(nq), dim3(NB), 0, st, e0, e1, 0, a);
-        else
-            hipExtLaunchKernelGGL((knn_near_kernel<false, true, 4, false, NB, 4>), dim3(nq), dim3(NB), 0, st, e0, e1, 0, a);
-    } else {
-        if (near_nospill())
-            hipExtLaunchKernelGGL((knn_near_kernel<false, false, 4, false, NB, 2>), dim3(nq), dim3(NB), 0, st, e0, e1, 0, a);
-        else
-            hipExtLaunchKernelGGL((knn_near_kernel<false, false, 4, false, NB, 4>), dim3(nq), dim3(NB), 0, st, e0, e1, 0, a);
-    }
-}
-
-static void launch_near(const MatchArgs& a, int nq, hipStream_t st, hipEvent_t e0, hipEvent_t e1) {
-    if (near_block() == 256)
-        launch_near_nb<256>(a, nq, st, e0, e1);
-    else if (near_block() == 128)
-        launch_near_nb<128>(a, nq, st, e0, e1);
-    else
-        launch_near_nb<512>(a, nq, st, e0, e1);
-}
-
+// The measured-best forms only (A/B history: DESIGN §4): near pass in 32-query blocks with 2 loads in
+// flight in the seeded table scan and in the own-cell scan (no scratch spills); far pass one
+// 128-thread block per queued query on a fixed 1024-block grid; plane pass 512 x 1 point per lane;
+// reuse pass 512 x 2 points per lane.
 int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* marks) {
     if (a.n == 0) return 0;
-    const int ppl = ppl_setting();
-    const int nb = (a.n + kBlock * ppl - 1) / (kBlock * ppl);
     // hipExtLaunchKernelGGL with null events is a plain launch; with events (timing) the command
     // processor stamps them at the kernel's own start / end
     hipEvent_t m[8] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
     if (marks)
         for (int k = 0; k < 8; ++k) m[k] = marks[k];
     if (redo) {
-        const int qpb = (a.dbg ? kKnnBlock : near_block()) / kGroup;
+        constexpr int qpb = kNearBlock / kGroup;
         const int nq = (a.n + qpb - 1) / qpb;
         if (a.dbg)
-            hipExtLaunchKernelGGL(knn_near_kernel<true, false>, dim3(nq), dim3(kKnnBlock), 0, st, m[0], m[1], 0, a);
+            hipExtLaunchKernelGGL((knn_near_kernel<true, false, 4, kNearBlock, 2>), dim3(nq), dim3(kNearBlock), 0, st,
+                                  m[0], m[1], 0, a);
+        else if (a.prior)
+            hipExtLaunchKernelGGL((knn_near_kernel<false, true, 2, kNearBlock, 4>), dim3(nq), dim3(kNearBlock), 0, st,
+                                  m[0], m[1], 0, a);
         else
-            launch_near(a, nq, st, m[0], m[1]);
-        static const int far_blocks = [] {  // LIO_FAR_BLOCKS: diagnostics override of the far-pass grid
-            const char* e = std::getenv("LIO_FAR_BLOCKS");
-            const int v = e ? std::atoi(e) : 0;
-            return v > 0 ? std::min(v, 4096) : kFarBlocks;
-        }();
-        static const int far_nt = [] {  // LIO_FAR_THREADS: threads per far query (diagnostics: 64 / 256 / 512)
-            const char* e = std::getenv("LIO_FAR_THREADS");
-            return e ? std::atoi(e) : kFarBlock;
-        }();
-        if (a.max_shell > 1) {
-            if (far_nt == 64)
-                hipExtLaunchKernelGGL((knn_far_kernel<false, 64>), dim3(far_blocks), dim3(64), 0, st, m[2], m[3], 0, a);
-            else if (far_nt == 256)
-                hipExtLaunchKernelGGL((knn_far_kernel<false, 256>), dim3(far_blocks), dim3(256), 0, st, m[2], m[3], 0, a);
-            else if (far_nt == 512)
-                hipExtLaunchKernelGGL((knn_far_kernel<false, 512>), dim3(far_blocks), dim3(512), 0, st, m[2], m[3], 0, a);
-            else
-                hipExtLaunchKernelGGL(knn_far_kernel<false>, dim3(far_blocks), dim3(kFarBlock), 0, st, m[2], m[3], 0, a);
-        }
-        if (plane_wide()) {
-            const int nbp = (a.n + kPlaneBlock - 1) / kPlaneBlock;
-            hipExtLaunchKernelGGL((plane_kernel<1, false, kPlaneBlock>), dim3(nbp), dim3(kPlaneBlock), 0, st, m[4], m[5], 0, a);
-            return nbp;
-        }
-        if (ppl == 4)
-            hipExtLaunchKernelGGL(plane_kernel<4>, dim3(nb), dim3(kBlock), 0, st, m[4], m[5], 0, a);
-        else if (ppl == 2)
-            hipExtLaunchKernelGGL(plane_kernel<2>, dim3(nb), dim3(kBlock), 0, st, m[4], m[5], 0, a);
-        else
-            hipExtLaunchKernelGGL(plane_kernel<1>, dim3(nb), dim3(kBlock), 0, st, m[4], m[5], 0, a);
-        return nb;
-    }
-    if (plane_wide()) {
-        const int nbr = (a.n + 2 * kPlaneBlock - 1) / (2 * kPlaneBlock);
-        hipExtLaunchKernelGGL((h_model_reuse_kernel<2, false, kPlaneBlock>), dim3(nbr), dim3(kPlaneBlock), 0, st, m[6], m[7], 0, a);
-        return nbr;
-    }
-    if (ppl == 4)
-        hipExtLaunchKernelGGL(h_model_reuse_kernel<4>, dim3(nb), dim3(kBlock), 0, st, m[6], m[7], 0, a);
-    else if (ppl == 2)
-        hipExtLaunchKernelGGL(h_model_reuse_kernel<2>, dim3(nb), dim3(kBlock), 0, st, m[6], m[7], 0, a);
-    else
-        hipExtLaunchKernelGGL(h_model_reuse_kernel<1>, dim3(nb), dim3(kBlock), 0, st, m[6], m[7], 0, a);
-    return nb;
-}
-
-void launch_h_model_gated(const MatchArgs& a, bool redo, const GateIn* in, unsigned long long gate_seq, hipStream_t st) {
-    if (a.n == 0) return;
-    const int ppl = ppl_setting();
-    const int nb = (a.n + kBlock * ppl - 1) / (kBlock * ppl);
-    eval_gate_kernel<<<1, 64, 0, st>>>(a.ctl, in, gate_seq, redo ? 1 : 0);
-    if (redo) {  // only the near pass: far + plane are launched at release (launch_knn_tail), hidden behind it
-        const int nq = (a.n + kKnnBlock / kGroup - 1) / (kKnnBlock / kGroup);
-        if (a.prior)
-            knn_near_kernel<false, true, 4, true><<<nq, kKnnBlock, 0, st>>>(a);
-        else
-            knn_near_kernel<false, false, 4, true><<<nq, kKnnBlock, 0, st>>>(a);
-        return;
-    }
-    if (ppl == 4)
-        h_model_reuse_kernel<4, true><<<nb, kBlock, 0, st>>>(a);
-    else if (ppl == 2)
-        h_model_reuse_kernel<2, true><<<nb, kBlock, 0, st>>>(a);
-    else
-        h_model_reuse_kernel<1, true><<<nb, kBlock, 0, st>>>(a);
-}
-
-int launch_knn_tail(const MatchArgs& a, hipStream_t st) {
-    if (a.n == 0) return 0;
-    const int ppl = ppl_setting();
-    const int nb = (a.n + kBlock * ppl - 1) / (kBlock * ppl);
-    if (a.max_shell > 1) knn_far_kernel<false><<<kFarBlocks, kFarBlock, 0, st>>>(a);
-    if (ppl == 4)
-        plane_kernel<4, false><<<nb, kBlock, 0, st>>>(a);
-    else if (ppl == 2)
-        plane_kernel<2, false><<<nb, kBlock, 0, st>>>(a);
-    else
-        plane_kernel<1, false><<<nb, kBlock, 0, st>>>(a);
-    return nb;
-}
-
-void launch_ieskf_dev(const MatchArgs& a, const double* in, unsigned long long seq, int max_iter, hipStream_t st,
-                      hipEvent_t* marks) {
-    const int ppl = ppl_setting();
-    const int nb = (a.n + kBlock * ppl - 1) / (kBlock * ppl);
-    const int nq = (a.n + kKnnBlock / kGroup - 1) / (kKnnBlock / kGroup);
-    static const int far_blocks = [] {
-        const char* e = std::getenv("LIO_FAR_BLOCKS");
-        const int v = e ? std::atoi(e) : 0;
-        return v > 0 ? std::min(v, 4096) : kFarBlocks;
-    }();
-    ieskf_init_kernel<<<1, 256, 0, st>>>(a.ctl, in, seq);
-    for (int e = 0; e <= max_iter; ++e) {
-        hipEvent_t* m = marks ? marks + 6 * e : nullptr;
-        hipEvent_t m0 = m ? m[0] : nullptr, m1 = m ? m[1] : nullptr, m2 = m ? m[2] : nullptr, m3 = m ? m[3] : nullptr,
-                   m4 = m ? m[4] : nullptr, m5 = m ? m[5] : nullptr;
-        // slot 0 always redoes the kNN (converge starts true); later kNN slots are seeded by the
-        // scan's previous lists against the unchanged map
-        if (e == 0)
-            hipExtLaunchKernelGGL((knn_near_kernel<false, false, 4, true>), dim3(nq), dim3(kKnnBlock), 0, st, m0, m1, 0, a);
-        else
-            hipExtLaunchKernelGGL((knn_near_kernel<false, true, 4, true>), dim3(nq), dim3(kKnnBlock), 0, st, m0, m1, 0, a);
+            hipExtLaunchKernelGGL((knn_near_kernel<false, false, 4, kNearBlock, 2>), dim3(nq), dim3(kNearBlock), 0, st,
+                                  m[0], m[1], 0, a);
         if (a.max_shell > 1)
-            hipExtLaunchKernelGGL(knn_far_kernel<true>, dim3(far_blocks), dim3(kFarBlock), 0, st, m2, m3, 0, a);
-        if (ppl == 4)
-            hipExtLaunchKernelGGL(h_eval_dev_kernel<4>, dim3(nb + 1), dim3(kBlock), 0, st, m4, m5, 0, a);
-        else if (ppl == 2)
-            hipExtLaunchKernelGGL(h_eval_dev_kernel<2>, dim3(nb + 1), dim3(kBlock), 0, st, m4, m5, 0, a);
-        else
-            hipExtLaunchKernelGGL(h_eval_dev_kernel<1>, dim3(nb + 1), dim3(kBlock), 0, st, m4, m5, 0, a);
+            hipExtLaunchKernelGGL(knn_far_kernel<kFarBlock>, dim3(kFarBlocks), dim3(kFarBlock), 0, st, m[2], m[3], 0, a);
+        const int nbp = (a.n + kPlaneBlock - 1) / kPlaneBlock;
+        hipExtLaunchKernelGGL((plane_kernel<1, kPlaneBlock>), dim3(nbp), dim3(kPlaneBlock), 0, st, m[4], m[5], 0, a);
+        return nbp;
     }
+    const int nbr = (a.n + kReusePpl * kReuseBlock - 1) / (kReusePpl * kReuseBlock);
+    hipExtLaunchKernelGGL((h_model_reuse_kernel<kReusePpl, kReuseBlock>), dim3(nbr), dim3(kReuseBlock), 0, st, m[6],
+                          m[7], 0, a);
+    return nbr;
 }
-
-size_t ieskf_ctl_bytes() { return sizeof(IeskfCtl); }
 
 void launch_debug(const MatchArgs& a, float* world, float* d2, float* abcd_pd2, hipStream_t st) {
     if (a.n == 0) return;
@@ -901,19 +580,14 @@ void launch_h_rows(const MatchArgs& a, double* rows, int64_t max_rows, int64_t* 
     h_rows_kernel<<<1, 1024, 0, st>>>(a, rows, max_rows, n_rows);
 }
 
-
-void launch_finalize(const MatchArgs& a, int nblocks, hipStream_t st) {
-    if (!a.fused_final) finalize_kernel<<<1, 1024, 0, st>>>(a.partials, nblocks, a.sums_out, a.seq_out, a.seq);
-}
-
 void launch_map_knn(const GridDev& g, const float* q, int n, float bound, int max_shell, int k, int32_t* idx,
                     float* d2, hipStream_t st) {
     if (n <= 0) return;
     map_knn_kernel<<<(n + 256 / kGroup - 1) / (256 / kGroup), 256, 0, st>>>(g, q, n, bound, max_shell, k, idx, d2);
 }
 
-int match_blocks(int n) {  // partial slots (plane / reuse kernels)
-    return (n + kBlock - 1) / kBlock;  // the PPL = 1 count bounds every PPL
+int match_blocks(int n) {  // partial slots (plane / reuse kernels): n / 256 bounds both grids
+    return (n + kBlock - 1) / kBlock;
 }
 
 }  // namespace lio

@@ -34,7 +34,7 @@ EXPORTS = [
     "lio_pcd_write_binary", "lio_pcd_read", "lio_map_build_pcd",
     "lio_ctx_create", "lio_ctx_destroy", "lio_scan_set", "lio_scan_set_device", "lio_scan_bind_device", "lio_match",
     "lio_get_knn", "lio_get_planes", "lio_get_world", "lio_get_h_rows", "lio_ctx_knn_stats",
-    "lio_ieskf_update", "lio_ctx_set_ieskf_mode",
+    "lio_ieskf_update", "lio_ctx_set_seed_scale",
     "lio_icp_create", "lio_icp_destroy", "lio_icp_set_target", "lio_icp_set_source", "lio_icp_set_shard",
     "lio_icp_align", "icp_align", "lio_icp_group_create", "lio_icp_group_destroy", "lio_icp_group_size",
     "lio_icp_group_uses_rccl", "lio_icp_group_set_target", "lio_icp_group_set_source", "lio_icp_group_align",
@@ -116,7 +116,7 @@ class CloudField(C.Structure):
 
 class KernelTiming(C.Structure):
     _fields_ = [("knn_launches", C.c_int64), ("knn_ms", C.c_double), ("reuse_launches", C.c_int64),
-                ("reuse_ms", C.c_double), ("final_launches", C.c_int64), ("final_ms", C.c_double),
+                ("reuse_ms", C.c_double),
                 ("icp_launches", C.c_int64), ("icp_ms", C.c_double), ("near_launches", C.c_int64),
                 ("near_ms", C.c_double), ("far_launches", C.c_int64), ("far_ms", C.c_double),
                 ("plane_launches", C.c_int64), ("plane_ms", C.c_double),
@@ -186,7 +186,7 @@ def _declare(L):
         "lio_get_h_rows": (C.c_int, [vp, dp, C.c_int64, C.POINTER(C.c_int64)]),
         "lio_ctx_knn_stats": (C.c_int, [vp, C.POINTER(Pose), dp, C.POINTER(C.c_int32)]),
         "lio_ieskf_update": (C.c_int, [vp, C.POINTER(State), dp, C.POINTER(IeskfParams), C.POINTER(IeskfStats)]),
-        "lio_ctx_set_ieskf_mode": (C.c_int, [vp, C.c_int]),
+        "lio_ctx_set_seed_scale": (C.c_int, [vp, C.c_float]),
         "lio_icp_create": (C.c_int, [C.POINTER(IcpParams), C.POINTER(vp)]),
         "lio_icp_destroy": (C.c_int, [vp]),
         "lio_icp_set_target": (C.c_int, [vp, fp, C.c_int64]),

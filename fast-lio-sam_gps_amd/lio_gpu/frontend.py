@@ -315,10 +315,10 @@ class HShareModelGPU:
         check(lib().lio_map_incremental(self._h, C.byref(pose), float(filter_size_map), C.byref(st)))
         return {k: int(getattr(st, k)) for k, _ in _capi.IncrementalStats._fields_}
 
-    def set_ieskf_mode(self, device: bool):
-        """lio_ieskf_update on this context: device-resident launch sequence (True, default) or the
-        host loop with one lio_match round trip per evaluation (False)."""
-        check(lib().lio_ctx_set_ieskf_mode(self._h, 1 if device else 0))
+    def set_seed_scale(self, scale: float):
+        """Test hook (lio_ctx_set_seed_scale): shrink the seeded kNN pass's bound by ``scale`` in
+        (0, 1] so its not-full guard (whole-box far search) runs."""
+        check(lib().lio_ctx_set_seed_scale(self._h, float(scale)))
 
     # ---- timing (HIP events on the context's stream)
     def set_timing(self, on: bool):

@@ -142,7 +142,9 @@ typedef struct lio_match_params {
  * them exactly as Eigen's QuaternionBase::_transformVector does.  R / R_LI are
  * the same rotations as row-major matrices.  A caller holding only matrices
  * leaves q (q_LI) all zero: it is then derived from R (R_LI) with Eigen's
- * Matrix3 -> Quaternion conversion.                                         */
+ * Matrix3 -> Quaternion conversion.  A non-zero q takes precedence: R / R_LI
+ * are then not read by any computation (so a stale R cannot disagree with
+ * the kernels' rotation).                                                   */
 typedef struct lio_pose {
     double R[9];
     double t[3];
@@ -213,13 +215,10 @@ typedef struct lio_ieskf_stats {
  * (one h-evaluation launch + one zero-copy result per iteration, 23-dim
  * algebra on the host).                                                     */
 int lio_ieskf_update(lio_ctx* c, lio_state* x, double* P, const lio_ieskf_params* p, lio_ieskf_stats* st);
-/* device = 1: lio_ieskf_update runs device-resident — the whole update as one
- * enqueued launch sequence, the 23-dim step on the GPU (pre-step in block 0 of
- * each evaluation's last kernel, post-step in its last block), no host round
- * trip between evaluations (solve_ms = 0; the dof < 23 branch falls back to
- * the host loop by itself).  0: the host loop (the default: measured faster,
- * DESIGN.md §4).  LIO_IESKF_DEVICE=0/1 sets the default process-wide.        */
-int lio_ctx_set_ieskf_mode(lio_ctx* c, int device);
+/* Test hook: the seeded kNN pass's bound (later kNN evaluations of a scan) is
+ * multiplied by scale in (0, 1]; < 1 shrinks it below the true 5th distance so
+ * the not-full guard (whole-box far search) is exercised.  Default 1.        */
+int lio_ctx_set_seed_scale(lio_ctx* c, float scale);
 
 /* ---------------------------------------------------------------- loop ICP */
 typedef struct lio_icp lio_icp;
@@ -386,7 +385,6 @@ int lio_map_build_pcd(lio_map* m, const char* path);
 typedef struct lio_kernel_timing {
     int64_t knn_launches;   double knn_ms;     /* kNN h-evaluation: near + far + plane kernels  */
     int64_t reuse_launches; double reuse_ms;   /* converge=false re-evaluation kernel         */
-    int64_t final_launches; double final_ms;   /* block-partial finalize kernel (LIO_FUSED_FINAL=0) */
     int64_t icp_launches;   double icp_ms;     /* ICP correspondence + statistics kernels     */
     int64_t near_launches;  double near_ms;    /* kNN near pass (inside knn_ms)                */
     int64_t far_launches;   double far_ms;     /* kNN far pass (inside knn_ms)                 */

@@ -1759,14 +1759,81 @@ struct ImuPoseO {
     double acc[3], gyr[3], vel[3], pos[3], rot[9];
 };
 
-// FAST-LIO so3_math.h Exp(ang_vel, dt) [U]
+static inline unsigned long long dbits(double v) {
+    unsigned long long u;
+    std::memcpy(&u, &v, sizeof(u));
+    return u;
+}
+static inline double bitsd(unsigned long long u) {
+    double v;
+    std::memcpy(&v, &u, sizeof(v));
+    return v;
+}
+// sin / cos for UndistortPcl's SO3 Exp.  The reference calls libm sin / cos, whose last bit is
+// implementation-defined (glibc, the device's ocml and PCL's build may differ by an ulp); the
+// restatement pins ONE fixed-order routine, and the GPU path (lio_filter.hip) evaluates the same
+// published algorithm, so undistorted points agree bit for bit.  tests/test_oracle.py checks it
+// against numpy sin / cos (<= 1 ulp).  The published
+// fdlibm algorithm: Cody-Waite reduction by pi/2 in three 33-bit parts (exact products for
+// |n| < 2^20), then the __kernel_sin / __kernel_cos minimax polynomials on [-pi/4, pi/4]; < 1 ulp
+// from the true value.  Arguments beyond 2^19 pi/2 do not occur (angular rate x dt of one sweep).
+static inline double ksin_fixed(double x) {
+    const double S1 = -1.66666666666666324348e-01, S2 = 8.33333333332248946124e-03,
+                 S3 = -1.98412698298579493134e-04, S4 = 2.75573137070700676789e-06,
+                 S5 = -2.50507602534068634195e-08, S6 = 1.58969099521155010221e-10;
+    if (std::fabs(x) < 7.450580596923828125e-09) return x;  // 2^-27
+    const double z = x * x, v = z * x;
+    const double r = S2 + z * (S3 + z * (S4 + z * (S5 + z * S6)));
+    return x + v * (S1 + z * r);
+}
+static inline double kcos_fixed(double x) {
+    const double C1 = 4.16666666666666019037e-02, C2 = -1.38888888888741095749e-03,
+                 C3 = 2.48015872894767294178e-05, C4 = -2.75573143513906633035e-07,
+                 C5 = 2.08757232129817482790e-09, C6 = -1.13596475577881948265e-11;
+    const double ax = std::fabs(x);
+    if (ax < 7.450580596923828125e-09) return 1.0;
+    const double z = x * x;
+    const double r = z * (C1 + z * (C2 + z * (C3 + z * (C4 + z * (C5 + z * C6)))));
+    if (ax < 0.3) return 1.0 - (0.5 * z - z * r);
+    double qx;
+    if (ax > 0.78125) {
+        qx = 0.28125;
+    } else {  // |x| / 4 with the low word cleared
+        const unsigned long long hi = (unsigned long long)dbits(ax) >> 32;
+        qx = bitsd((hi - 0x00200000ull) << 32);
+    }
+    const double hz = 0.5 * z - qx, a = 1.0 - qx;
+    return a - (hz - z * r);
+}
+void sincos_fixed(double x, double* s, double* c) {
+    const double invpio2 = 6.36619772367581382433e-01, pio2_1 = 1.57079632673412561417e+00,
+                 pio2_2 = 6.07710050630396597660e-11, pio2_3 = 2.02226624871116645580e-21;
+    int n = 0;
+    double r = x;
+    if (!(std::fabs(x) <= 7.85398163397448278999e-01)) {  // pi/4
+        const double fn = std::nearbyint(x * invpio2);
+        n = (int)fn;
+        r = ((x - fn * pio2_1) - fn * pio2_2) - fn * pio2_3;
+    }
+    const double ks = ksin_fixed(r), kc = kcos_fixed(r);
+    switch (n & 3) {
+        case 0: *s = ks, *c = kc; break;
+        case 1: *s = kc, *c = -ks; break;
+        case 2: *s = -ks, *c = -kc; break;
+        default: *s = -kc, *c = ks; break;
+    }
+}
+
+// FAST-LIO so3_math.h Exp(ang_vel, dt) [U] (sin / cos: sincos_fixed above)
 static void so3_exp(const double w[3], double dt, double E[9]) {
     const double nrm = std::sqrt((w[0] * w[0] + w[1] * w[1]) + w[2] * w[2]);
     for (int k = 0; k < 9; ++k) E[k] = (k % 4 == 0) ? 1.0 : 0.0;
     if (!(nrm > 0.0000001)) return;
     const double r[3] = {w[0] / nrm, w[1] / nrm, w[2] / nrm};
     const double K[9] = {0.0, -r[2], r[1], r[2], 0.0, -r[0], -r[1], r[0], 0.0};
-    const double a = nrm * dt, sn = std::sin(a), c1 = 1.0 - std::cos(a);
+    double sn, co;
+    sincos_fixed(nrm * dt, &sn, &co);
+    const double c1 = 1.0 - co;
     for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) {
             // ((1 - cos) K) * K: Eigen's coefficient-based 3x3 product sums e0 + (e1 + e2)
@@ -1853,6 +1920,11 @@ static int64_t preprocess(const float* raw, int64_t n, int stride, int every, fl
 // C ABI for ctypes (tests / bench cpu_baseline only)
 // =============================================================================
 extern "C" {
+
+// sincos_fixed over an array (tests/test_oracle.py pins it against numpy within 1 ulp)
+void orc_sincos(const double* a, int64_t n, double* s, double* c) {
+    for (int64_t i = 0; i < n; ++i) orc::sincos_fixed(a[i], s + i, c + i);
+}
 
 struct orc_match_params { float knn_range_sq; float plane_thr; double s_coef; double s_gate; };
 struct orc_state {

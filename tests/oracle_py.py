@@ -50,6 +50,15 @@ def _p(a, t):
     return a.ctypes.data_as(C.POINTER(t))
 
 
+def sincos(a):
+    """the restatement's fixed sin / cos (UndistortPcl's SO3 Exp; lio_oracle.cpp sincos_fixed)"""
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    s = np.empty_like(a)
+    c = np.empty_like(a)
+    lib().orc_sincos(_p(a, C.c_double), len(a), _p(s, C.c_double), _p(c, C.c_double))
+    return s, c
+
+
 def build():
     subprocess.run(["make", "-s", "-C", ORACLE_DIR], check=True)
 
@@ -60,6 +69,7 @@ def lib():
         if not os.path.exists(LIB_PATH):
             build()
         L = C.CDLL(LIB_PATH)
+        L.orc_sincos.argtypes = [C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double), C.POINTER(C.c_double)]
         L.orc_map_build.restype = C.c_void_p
         L.orc_map_build.argtypes = [C.POINTER(C.c_float), C.c_int64]
         L.orc_map_free.argtypes = [C.c_void_p]

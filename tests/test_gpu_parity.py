@@ -384,157 +384,57 @@ def test_seeded_second_knn_bit_exact(oracle, c1, shift):
     _check_sums(g, o)
 
 
-@pytest.mark.parametrize("queue", ["0", "1"])
-def test_ieskf_queued_evaluations_any_pattern(queue):
-    """LIO_QUEUE_NEXT=1: the host loop queues the evaluations it expects next behind gates before the
-    current result is in (reuse, then the kNN the loop forces).  Convergence limits and iteration caps
-    that make the loop converge early, late or never give every evaluation pattern — predictions that
-    hit, mispredictions that cancel the rest of the chain, queued evaluations left over when the loop
-    stops early — and the update still matches the oracle (counts identical, pose within 1e-5), with
-    the context usable right after.  Child process (the switch is read once)."""
-    import os
-    import subprocess
-    import sys
+@pytest.mark.parametrize("scale", [0.05, 0.5])
+def test_seeded_guard_whole_box(oracle, scale):
+    """The seeded pass's guard: a bound shrunk below the true 5th distance (lio_ctx_set_seed_scale)
+    leaves lists that are not full; they are reset and the far pass searches the whole box, 3x3x3
+    block included — the lists stay bit-exact."""
+    scene, m, scans = synth.make_config("C1", n_scans=1)
+    sc = scans[0]
+    om = oracle.OracleMap(m)
+    tree = F.IkdTreeGPU()
+    tree.Build(m)
+    hm = F.HShareModelGPU(tree)
+    hm.set_seed_scale(scale)
+    hm.set_scan(sc.body)
+    st = synth.initial_state(sc.pos_init, sc.rot_init)
+    hm(synth.pose24(st), converge=True)
+    for shift in (0.02, 0.3):
+        st2 = dict(st)
+        st2["pos"] = np.asarray(st["pos"]) + np.array([shift, -0.5 * shift, 0.25 * shift])
+        p24 = synth.pose24(st2)
+        hm(p24, converge=True)
+        gi, gd = hm.nearest_points()
+        oi, od = om.knn(oracle.body_to_world(p24, sc.body), 5, 5.0)
+        np.testing.assert_array_equal(gi, oi)
+        np.testing.assert_array_equal(gd, od)
+    hm.close()
 
-    code = r'''
-import sys, numpy as np
-sys.path[:0] = [r"%s", r"%s"]
-import oracle_py as O
-from lio_gpu import frontend as F, synth
-scene, m, scans = synth.make_config("C1", n_scans=2)
-om = O.OracleMap(m)
-tree = F.IkdTreeGPU(); tree.Build(m)
-hm = F.HShareModelGPU(tree)
-for epsi, max_iter in [(0.001, 3), (0.05, 3), (1.0, 3), (1.0, 5), (0.001, 1), (0.02, 6)]:
+
+@pytest.mark.parametrize("epsi,max_iter", [(0.001, 3), (0.05, 3), (1.0, 3), (1.0, 5), (0.001, 1), (0.02, 6)])
+def test_ieskf_evaluation_patterns(oracle, epsi, max_iter):
+    """Convergence limits and iteration caps that make the IESKF loop converge early, late or never
+    give every redo / reuse evaluation pattern; the update matches the oracle (counts identical,
+    pose within 1e-5) and the context is usable right after."""
+    scene, m, scans = synth.make_config("C1", n_scans=2)
+    om = oracle.OracleMap(m)
+    tree = F.IkdTreeGPU()
+    tree.Build(m)
+    hm = F.HShareModelGPU(tree)
     kf = F.EsekfGPU(hm, max_iteration=max_iter, epsi=epsi)
     for sc in scans:
         hm.set_scan(sc.body)
         st = synth.initial_state(sc.pos_init, sc.rot_init)
         P0 = synth.initial_cov()
         xg, Pg, sg = kf.update_iterated_dyn_share_modified(st, P0)
-        xo, Po, so, _ = O.ieskf_update(om, sc.body, st, P0, max_iter=max_iter, limit=epsi)
+        xo, Po, so, _ = oracle.ieskf_update(om, sc.body, st, P0, max_iter=max_iter, limit=epsi)
         assert sg["h_evals"] == int(so[0]) and sg["knn_calls"] == int(so[1]) and sg["n_eff"] == int(so[3])
         assert sg["converged"] == int(so[2])
-        assert np.allclose(xg["pos"], xo["pos"], atol=1e-5) and np.allclose(xg["rot"], xo["rot"], atol=1e-5)
-        assert np.allclose(Pg, Po, rtol=1e-5, atol=1e-10)
-        g = hm(synth.pose24(xg), converge=True)  # no queued evaluation left on the stream
-        assert g[27] > 0
-print("ok")
-''' % (os.path.join(os.path.dirname(__file__), "..", "fast-lio-sam_gps_amd"), os.path.dirname(__file__))
-    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, LIO_QUEUE_NEXT=queue), capture_output=True,
-                       text=True, timeout=300)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
-
-
-@pytest.mark.parametrize("scale", ["0.05", "0.5"])
-def test_seeded_guard_whole_box(scale):
-    """The seeded pass's guard: a bound shrunk below the true 5th distance (LIO_KNN_SEED_SCALE)
-    leaves lists that are not full; they are reset and the far pass searches the whole box, 3x3x3
-    block included — the lists stay bit-exact.  Child process (the switch is read once)."""
-    import os
-    import subprocess
-    import sys
-
-    code = r'''
-import sys, numpy as np
-sys.path[:0] = [r"%s", r"%s"]
-import oracle_py as O
-from lio_gpu import frontend as F, synth
-scene, m, scans = synth.make_config("C1", n_scans=1)
-sc = scans[0]
-om = O.OracleMap(m)
-tree = F.IkdTreeGPU(); tree.Build(m)
-hm = F.HShareModelGPU(tree); hm.set_scan(sc.body)
-st = synth.initial_state(sc.pos_init, sc.rot_init)
-hm(synth.pose24(st), converge=True)
-for shift in (0.02, 0.3):
-    st2 = dict(st); st2["pos"] = np.asarray(st["pos"]) + np.array([shift, -0.5 * shift, 0.25 * shift])
-    p24 = synth.pose24(st2)
-    hm(p24, converge=True)
-    gi, gd = hm.nearest_points()
-    oi, od = om.knn(O.body_to_world(p24, sc.body), 5, 5.0)
-    assert np.array_equal(gi, oi) and np.array_equal(gd, od)
-print("ok")
-''' % (os.path.join(os.path.dirname(__file__), "..", "fast-lio-sam_gps_amd"), os.path.dirname(__file__))
-    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, LIO_KNN_SEED_SCALE=scale),
-                       capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
-
-
-@pytest.mark.parametrize("cfg", ["C1", "C2"])
-def test_ieskf_device_matches_host_loop(cfg):
-    """The device-resident update (one enqueued launch sequence, 23-dim step in the last workgroup of
-    each evaluation) against the host loop (one lio_match round trip per evaluation, host algebra) on
-    the same scans: identical evaluation / kNN counts and effective points, state and covariance
-    equal to within device-vs-host libm differences (1e-10), and the same Nearest_Points / kNN pose
-    bookkeeping afterwards (map_incremental's inputs)."""
-    _, m, scans = synth.make_config(cfg, n_scans=3)
-    trees, kfs, hms = [], [], []
-    for device in (True, False):
-        tree = F.IkdTreeGPU()
-        tree.Build(m)
-        hm = F.HShareModelGPU(tree)
-        hm.set_ieskf_mode(device)
-        trees.append(tree)
-        hms.append(hm)
-        kfs.append(F.EsekfGPU(hm))
-    for sc in scans:
-        st = synth.initial_state(sc.pos_init, sc.rot_init)
-        P0 = synth.initial_cov()
-        out = []
-        for hm, kf in zip(hms, kfs):
-            hm.set_scan(sc.body)
-            out.append(kf.update_iterated_dyn_share_modified(st, P0))
-        (xd, Pd, sd), (xh, Ph, sh) = out
-        for k in ("h_evals", "knn_calls", "converged", "n_eff"):
-            assert sd[k] == sh[k], k
-        assert sd["solve_ms"] == 0.0 and sh["solve_ms"] > 0.0  # device path really ran
-        np.testing.assert_allclose(sd["res_mean"], sh["res_mean"], rtol=1e-9)
-        for k in xd:
-            np.testing.assert_allclose(xd[k], xh[k], rtol=0, atol=1e-10, err_msg=k)
-        np.testing.assert_allclose(Pd, Ph, rtol=1e-9, atol=1e-15)
-        np.testing.assert_allclose(hms[0].last_knn_pose24(), hms[1].last_knn_pose24(), rtol=0, atol=1e-10)
-        gi0, _ = hms[0].nearest_points()
-        gi1, _ = hms[1].nearest_points()
-        np.testing.assert_array_equal(gi0, gi1)
-
-
-@pytest.mark.parametrize("env", [{"LIO_FUSED_FINAL": "0"}, {"LIO_KNN_SEED": "0"}, {"LIO_IESKF_DEVICE": "1"}, {"LIO_QUEUE_NEXT": "1"},
-                                 {"LIO_PPL": "2"}, {"LIO_PPL": "4"}, {"LIO_NEAR_BLOCK": "512"}, {"LIO_NEAR_NOSPILL": "0"}])
-def test_ieskf_alternative_paths(env):
-    """The A/B switches keep parity: the separate finalize launch (LIO_FUSED_FINAL=0), the
-    unseeded later kNN evaluations (LIO_KNN_SEED=0), the device-resident IESKF (LIO_IESKF_DEVICE=1) and
-    2 / 4 points per lane in the plane / reuse kernels (LIO_PPL; set explicitly it also selects the
-    256-thread plane kernel instead of the default 512 x 1), the 64-query / 4-load near-pass forms
-    (LIO_NEAR_BLOCK=512, LIO_NEAR_NOSPILL=0), through a whole IESKF update
-    against the oracle.  Child process: the switches are read once per process."""
-    import os
-    import subprocess
-    import sys
-
-    code = r'''
-import sys, numpy as np
-sys.path[:0] = [r"%s", r"%s"]
-import oracle_py as O
-from lio_gpu import frontend as F, synth
-scene, m, scans = synth.make_config("C1", n_scans=2)
-om = O.OracleMap(m)
-tree = F.IkdTreeGPU(); tree.Build(m)
-hm = F.HShareModelGPU(tree); kf = F.EsekfGPU(hm)
-for sc in scans:
-    hm.set_scan(sc.body)
-    st = synth.initial_state(sc.pos_init, sc.rot_init)
-    P0 = synth.initial_cov()
-    xg, Pg, sg = kf.update_iterated_dyn_share_modified(st, P0)
-    xo, Po, so, _ = O.ieskf_update(om, sc.body, st, P0)
-    assert sg["h_evals"] == int(so[0]) and sg["knn_calls"] == int(so[1]) and sg["n_eff"] == int(so[3])
-    assert np.allclose(xg["pos"], xo["pos"], atol=1e-5) and np.allclose(xg["rot"], xo["rot"], atol=1e-5)
-    assert np.allclose(Pg, Po, rtol=1e-5, atol=1e-10)
-print("ok")
-''' % (os.path.join(os.path.dirname(__file__), "..", "fast-lio-sam_gps_amd"), os.path.dirname(__file__))
-    r = subprocess.run([sys.executable, "-c", code], env=dict(os.environ, **env), capture_output=True, text=True,
-                       timeout=300)
-    assert r.returncode == 0 and "ok" in r.stdout, r.stdout + r.stderr
+        np.testing.assert_allclose(xg["pos"], xo["pos"], atol=1e-5)
+        np.testing.assert_allclose(xg["rot"], xo["rot"], atol=1e-5)
+        np.testing.assert_allclose(Pg, Po, rtol=1e-5, atol=1e-10)
+        assert hm(synth.pose24(xg), converge=True)[27] > 0
+    hm.close()
 
 
 def test_sums_handoff_under_load(c1):

@@ -269,3 +269,20 @@ def test_icp_float_umeyama_mode_close_to_double(oracle):
         assert rd["iterations"] == rf["iterations"] and rd["state"] == rf["state"]
         np.testing.assert_allclose(rf["T"], rd["T"], atol=1e-4)
         assert abs(rf["fitness"] - rd["fitness"]) <= 1e-4 * rd["fitness"]
+
+
+def test_sincos_fixed_within_one_ulp(oracle):
+    """UndistortPcl's sin / cos in the restatement: one fixed-order routine (fdlibm algorithm) that the
+    GPU evaluates identically; pinned here against numpy (libm) to <= 1 ulp (1e-30 absolute next to
+    the zeros), equal in > 80 % of the samples."""
+    rng = np.random.default_rng(11)
+    a = np.concatenate([rng.uniform(-1e-3, 1e-3, 20000), rng.uniform(-1, 1, 50000), rng.uniform(-50, 50, 50000),
+                        [0.0, -0.0, 1e-30, np.pi / 4, 0.3, 0.78125, np.pi / 2, np.pi, 3 * np.pi / 2, 1e5]])
+    s, c = oracle.sincos(a)
+    for got, ref in ((s, np.sin(a)), (c, np.cos(a))):
+        # relative to 1 ulp, or (near the zeros of sin / cos, where the 3-part pi/2 reduction
+        # cancels) to 1e-30 absolute
+        ulp = np.maximum(np.spacing(np.abs(ref)), 1e-30)
+        err = np.abs(got - ref) / ulp
+        assert err.max() <= 1.0, err.max()
+        assert np.mean(got == ref) > 0.8  # glibc rounds correctly more often; never by more than 1 ulp
