@@ -81,9 +81,12 @@ def parse():
     ap.add_argument("--cpu-scans", type=int, default=50, help="CPU baseline: median per-scan latency of this "
                     "many full IESKF updates after --cpu-warmup ones, at 1, 3 and all usable threads (SURVEY §8d)")
     ap.add_argument("--cpu-warmup", type=int, default=5)
-    ap.add_argument("--pipeline", type=int, default=0, metavar="N",
-                    help="also time N raw scans through the whole front end: Preprocess + UndistortPcl + "
-                         "downSizeFilterSurf -> IESKF update -> map_incremental (reported under 'pipeline')")
+    ap.add_argument("--pipeline", type=int, default=8, metavar="N",
+                    help="secondary figure (rank 0): the C5 stream (BASELINE.json configs[4]) — N raw 120k-point "
+                         "sweeps on the 10M map, half out and half back past the same places 40 s later, each "
+                         "through Preprocess + UndistortPcl + downSizeFilterSurf -> IESKF update -> map_incremental "
+                         "-> keyframe, then the loop leg (fetchClosestKeyframeIdx -> setSrcAndDstCloud -> "
+                         "icpAlignment) on the newest keyframe; reported under 'pipeline' (0: skip)")
     ap.add_argument("--grow-scans", type=int, default=20,
                     help="C3/C5: scans appended through map_incremental before timing (SURVEY §8d)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"),
@@ -91,8 +94,26 @@ def parse():
     return ap.parse_args()
 
 
+def _spawn_ranks(args) -> int:
+    """`bench.py --gpus N` (N > 1) outside a launcher: start N rank processes through
+    torch.distributed.run (one per GPU, 127.0.0.1 rendezvous) BEFORE this process touches the GPU, and
+    return their exit status; rank 0 prints the JSON line."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(_spawn_ranks(args))
     import numpy as np
     import torch
 
@@ -307,48 +328,61 @@ def main():
                 "reuse_achieved_gbs": round(BYTES_PER_PT_REUSE * n_pts / (reuse_avg_ms * 1e-3) / 1e9, 2)
                 if tm["reuse_launches"] else None}
 
-    # ------------------------------------------------- full front-end pipeline (optional)
+    # ------------------------------------------------- C5 stream with its loop leg (secondary)
     pipeline = None
-    if args.pipeline > 0:
-        raws = []
-        for k in range(args.pipeline):
-            x0 = -0.15 * L + 0.9 + (k + rank * args.pipeline) * 3.7
-            raws.append(synth.make_raw_scan(scene, sp, kind if kind != "ouster64" else "kitti64", seed=777 + k,
-                                            origin=(x0, 0.4 * np.sin(0.5 * k), 0.0), yaw0=0.04 * np.sin(0.2 * k)))
-        hp = F.HShareModelGPU(tree)
-        kp = F.EsekfGPU(hp, laser_point_cov=0.001, max_iteration=3, epsi=0.001)
-        delta = synth.rotvec_to_quat(np.deg2rad([0.5, -0.4, 1.0]))
+    if args.pipeline > 0 and rank == 0:
+        from lio_gpu import pipeline as PL
 
-        def run_raw(r):
-            raw, poses, end24 = r
-            t0 = time.perf_counter()
-            n_down = hp.preprocess_scan(raw, poses, F.pose_from_pose24(end24), point_filter_num=4, blind=2.0,
-                                        filter_size_surf=0.5, time_field=4)
-            t1 = time.perf_counter()
-            R_e = end24[0:9].reshape(3, 3)  # yaw-only trajectory
-            q_e = synth.rotvec_to_quat([0.0, 0.0, float(np.arctan2(R_e[1, 0], R_e[0, 0]))])
-            st0 = synth.initial_state(end24[9:12] + np.array([0.10, -0.08, 0.05]), synth.quat_mul(q_e, delta))
-            xg, _, _ = kp.update_iterated_dyn_share_modified(st0, P0)
-            t2 = time.perf_counter()
-            hp.map_incremental(synth.pose24(xg), 0.5)
-            t3 = time.perf_counter()
-            return n_down, t1 - t0, t2 - t1, t3 - t2, float(np.linalg.norm(xg["pos"] - end24[9:12]))
-
-        run_raw(raws[0])  # warm-up (also grows the map once)
-        acc = np.zeros(4)
-        errs = []
-        for r in raws[1:]:
-            n_down, a, b, c, e = run_raw(r)
-            acc += [n_down, a, b, c]
-            errs.append(e)
-        m = max(len(raws) - 1, 1)
-        pipeline = {"scans": m, "raw_points": sp, "down_points_mean": round(acc[0] / m, 1),
-                    "ms_per_scan": round((acc[1] + acc[2] + acc[3]) / m * 1e3, 3),
-                    "scans_per_s": round(m / max(acc[1] + acc[2] + acc[3], 1e-9), 1),
-                    "preprocess_ms": round(acc[1] / m * 1e3, 3), "update_ms": round(acc[2] / m * 1e3, 3),
-                    "map_incremental_ms": round(acc[3] / m * 1e3, 3),
-                    "pos_err_m": round(float(np.mean(errs)), 4) if errs else None,
-                    "note": "raw float records uploaded from host per scan (PCIe included)"}
+        pmp, pL, psp, pkind = synth.CONFIGS["C5"]
+        tg = time.time()
+        pscene = synth.make_scene(pL, 1234)
+        pmap = synth.sample_surface(pscene, pmp, 1234)
+        stream = synth.make_loop_stream(pscene, n_out=max(args.pipeline // 2, 1), n_points=psp, kind=pkind)
+        pgen = time.time() - tg
+        d_pmap = torch.from_numpy(pmap).to(dev)
+        ptree = F.IkdTreeGPU(cell_size=args.cell, downsample_size=0.5, device=local)
+        ptree.Build_device(d_pmap.data_ptr(), len(pmap))
+        fs = PL.FastLioSamStream(ptree, LC.LoopClosureConfig(), device=local)
+        sweeps = [fs.process(raw, poses, end24, st0, P0, t) for raw, poses, end24, st0, t in stream]
+        idx, out, _ = fs.loop(submap_range=2)
+        # the loop leg's two stages timed separately (median of 5): submap assembly on the GPU
+        # (transformPcd of the keyframes + voxelizePcd, host keyframes uploaded) and icpAlignment
+        q = fs.keyframes[-1]
+        t_sub, t_icp = [], []
+        for _ in range(5):
+            ta = time.perf_counter()
+            src_c, dst_c = fs.lc.setSrcAndDstCloud(fs.keyframes, q.idx_, idx, 2, fs.config.voxel_res_)
+            tb = time.perf_counter()
+            reg = fs.lc.icpAlignment(src_c, dst_c)
+            t_icp.append(time.perf_counter() - tb)
+            t_sub.append(tb - ta)
+        steady = sweeps[1:] if len(sweeps) > 1 else sweeps  # the first sweep allocates the stream's buffers
+        med = {k: float(np.median([w["ms"][k] for w in steady])) for k in steady[0]["ms"]}
+        per_sweep = float(np.median([sum(w["ms"].values()) for w in steady]))
+        pipeline = {
+            "config": f"C5: {len(stream)} raw {psp}-pt {pkind} sweeps ({len(stream) // 2} out, {len(stream) - len(stream) // 2} "
+                      f"back 40 s later) on the {pmp}-pt map, keyframe every sweep, loop leg on the newest",
+            "sweeps": len(sweeps), "raw_points": psp,
+            "down_points_mean": round(float(np.mean([w["n_down"] for w in sweeps])), 1),
+            "undistorted_points_mean": round(float(np.mean([w["n_undistorted"] for w in sweeps])), 1),
+            "ms_per_sweep_median": round(per_sweep, 3), "sweeps_per_s": round(1e3 / per_sweep, 1),
+            "stage_ms_median": {k: round(v, 3) for k, v in med.items()},
+            "h_evals_per_sweep": round(float(np.mean([w["stats"]["h_evals"] for w in sweeps])), 2),
+            "pos_err_m": round(float(np.mean([np.linalg.norm(w["state"]["pos"] - e[2][9:12])
+                                               for w, e in zip(sweeps, stream)])), 4),
+            "map_size_after": ptree.size(),
+            "loop": {"query_idx": q.idx_, "closest_idx": int(idx), "is_valid": bool(reg.is_valid_),
+                     "score": round(float(reg.score_), 5), "iterations": int(reg.iterations),
+                     "src_points": int(len(src_c)), "dst_points": int(len(dst_c)),
+                     "submaps_ms": round(float(np.median(t_sub)) * 1e3, 3),
+                     "icp_ms": round(float(np.median(t_icp)) * 1e3, 3),
+                     "ms": round(float(np.median(t_sub) + np.median(t_icp)) * 1e3, 3)},
+            "input_gen_s": round(pgen, 1),
+            "note": "host wall times; raw sweeps uploaded from host memory per sweep (PCIe included); the keyframe "
+                    "stage copies feats_undistort back and builds the PosePcd on the host (fast_lio_sam glue)"}
+        fs.close()
+        ptree.close()
+        del d_pmap
 
     # ------------------------------------------------- several scan streams on one GPU (secondary)
     # One stream is latency-bound (host round trip per h-evaluation); independent sensors / robots
@@ -401,11 +435,18 @@ def main():
         src, dst, Tgt = synth.make_icp_pair(n_points=500_000, seed=4321, disp=(2.5, 4.0))
         lc = LC.LoopClosure(LC.LoopClosureConfig(), device=local)
         cb = None
+        exchange = "none (1 rank)"
         if world > 1:
             from lio_gpu import dist as ldist
 
-            cb = ldist.make_allgather(device=coll_dev)
-            lc.set_shard(rank, world, cb)
+            if rehearse:  # gloo on CPU tensors: the records pass through host memory
+                cb = ldist.make_allgather(device=coll_dev)
+                lc.set_shard(rank, world, cb)
+                exchange = "host (gloo rehearsal)"
+            else:  # RCCL all-gather of device buffers on the ICP handle's stream, record-order sum on the GPU
+                cb = ldist.DeviceExchange()
+                lc.set_shard_device(rank, world, cb)
+                exchange = "device (RCCL all_gather_into_tensor on the handle's stream)"
         lc.setInputSource(src)
         lc.setInputTarget(dst)
         lc.align(keep_aligned=False)
@@ -423,6 +464,13 @@ def main():
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             icp_s = float(t.item())
         itm = lc.timing()
+        lc.set_timing(False)
+        tf = time.perf_counter()  # the whole icpAlignment (warm handle): source binning + target grid + align
+        lc.setInputSource(src)
+        lc.setInputTarget(dst)
+        lc.align(keep_aligned=False)
+        barrier()
+        full_ms = (time.perf_counter() - tf) * 1e3
         passes = itm["icp_launches"]
         shard_n = len(src) // world
         icp_kernel_ms = itm["icp_ms"] / max(passes, 1)
@@ -431,6 +479,7 @@ def main():
                     "n_gpus": world, "passes_per_alignment": passes / max(args.icp_reps, 1),
                     "ms_per_alignment": round(icp_s / args.icp_reps * 1e3, 3),
                     "iterations": r.iterations, "ms_per_iteration": round(icp_s / max(iters, 1) * 1e3, 3),
+                    "exchange": exchange, "ms_full_icpAlignment": round(full_ms, 3),
                     "score": r.score, "converged": bool(r.is_converged), "scaling": "strong",
                     # the pass (correspondence + statistics kernels) and the correspondence kernel alone
                     "kernel_ms_per_pass": round(icp_kernel_ms, 4),
@@ -467,6 +516,25 @@ def main():
             by_thr[nthr] = {"median_ms_per_scan": round(med * 1e3, 3), "scans_per_s": round(1.0 / med, 3),
                             "ms_per_iteration": round(tot / max(its, 1) * 1e3, 3)}
         top = by_thr[threads]
+        if loop_icp is not None:
+            # the loop ICP on the host cores: the restatement's kd-tree + float-order
+            # Umeyama ICP, the whole icpAlignment (target tree built inside align, as PCL does lazily)
+            # on the same C4 pair B, median of `reps` alignments per thread count
+            icp_by = {}
+            for nthr, reps in sorted({(1, 1), (3, 1), (threads, 3)}):
+                lat = []
+                for _ in range(reps):
+                    tc = time.perf_counter()
+                    ro = O.icp_align(src, dst, threads=nthr)
+                    lat.append(time.perf_counter() - tc)
+                icp_by[str(nthr)] = {"ms_per_alignment": round(float(np.median(lat)) * 1e3, 1),
+                                     "iterations": int(ro["iterations"])}
+            loop_icp["cpu_baseline"] = {
+                "ms_per_alignment": icp_by[str(threads)]["ms_per_alignment"], "cores": threads, "kind": "port",
+                "sample": f"median of 3 full icpAlignment calls on C4 pair B ({len(src)} vs {len(dst)} pts), "
+                          "oracle/lio_oracle.cpp kd-tree 1-NN + Umeyama ICP with PCL's criteria, OpenMP over "
+                          f"the correspondence search; {how}",
+                "by_threads": icp_by, "gpu_full_ms": loop_icp.get("ms_full_icpAlignment")}
         cpu = {"value": top["scans_per_s"], "unit": "scans/s", "cores": threads, "kind": "port",
                "sample": f"1 / median per-scan latency of {args.cpu_scans} full IESKF updates (after "
                          f"{args.cpu_warmup} warm-ups) of {args.config} scans ({sp} pts) vs the same "

@@ -186,6 +186,8 @@ struct lio_ctx {
     lio::ImuPose* d_poses = nullptr;
     int64_t poses_cap = 0;
     float seed_scale = 1.0f;  // lio_ctx_set_seed_scale (test hook: < 1 exercises the seeded pass's guard)
+    int64_t undist_n = -1;    // feats_undistort of the last lio_scan_preprocess* (records in filt.c); -1: none
+    int undist_stride = 0;
 };
 
 extern "C" {
@@ -215,6 +217,7 @@ int lio_map_create(const lio_map_params* p, lio_map** out) {
     auto* m = new lio_map();
     m->dev = pp.device;
     m->p = pp;
+    m->grid.gapped = true;  // per-cell blocks: map_incremental updates in O(points changed)
     if (hipStreamCreateWithFlags(&m->st, hipStreamNonBlocking) != hipSuccess) {
         delete m;
         return fail(LIO_ERR_HIP, "hipStreamCreate failed");
@@ -495,8 +498,8 @@ int lio_ctx_create(lio_map* m, const lio_match_params* p, lio_ctx** out) {
         hipHostGetDevicePointer(reinterpret_cast<void**>(&c->h_sums_dev), c->h_sums, 0) != hipSuccess ||
         hipMalloc(&c->d_nrows, sizeof(int64_t)) != hipSuccess ||
         hipMalloc(&c->d_far_count, sizeof(int)) != hipSuccess ||
-        hipMemset(c->d_far_count, 0, sizeof(int)) != hipSuccess || hipMalloc(&c->d_done, 64) != hipSuccess ||
-        hipMemset(c->d_done, 0, 64) != hipSuccess) {
+        hipMemsetAsync(c->d_far_count, 0, sizeof(int), m->st) != hipSuccess || hipMalloc(&c->d_done, 64) != hipSuccess ||
+        hipMemsetAsync(c->d_done, 0, 64, m->st) != hipSuccess) {  // on the map's stream: it does not wait for the null stream
         --m->n_ctx;
         delete c;
         return fail(LIO_ERR_NOMEM, "context allocation failed");
@@ -1180,9 +1183,13 @@ int lio_scan_preprocess(lio_ctx* c, const float* raw, int64_t n, int stride, con
         HIP_TRY(hipMemcpyAsync(c->d_poses, poses, (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
     const lio::ScanPrepParams sp{p->point_filter_num, p->blind, p->filter_size_surf, p->time_field};
     int64_t m = 0;
+    c->undist_n = -1;
+    int64_t mu = 0;
     rc = lio::scan_preprocess(c->filt, c->d_raw, n, stride, sp, c->d_poses, n_poses, undistort_end(end), c->d_rec, &m,
-                              st);
+                              st, &mu);
     if (rc) return filter_status(rc, "lio_scan_preprocess");
+    c->undist_n = mu;
+    c->undist_stride = stride;
     rc = ctx_reserve(c, m);
     if (rc) return rc;
     rc = lio::records_to_xyz(c->d_rec, m, stride, c->d_body, st);
@@ -1190,6 +1197,20 @@ int lio_scan_preprocess(lio_ctx* c, const float* raw, int64_t n, int stride, con
     HIP_TRY(hipMemsetAsync(c->d_sel, 0, (size_t)std::max<int64_t>(m, 1), st));
     HIP_TRY(hipStreamSynchronize(st));
     if (n_down) *n_down = m;
+    return LIO_OK;
+}
+
+int lio_scan_get_undistorted(lio_ctx* c, float* out, int64_t cap_points, int64_t* n_points, int* stride) {
+    if (!c || !n_points) return fail(LIO_ERR_ARG, "lio_scan_get_undistorted: bad arguments");
+    if (c->undist_n < 0) return fail(LIO_ERR_STATE, "lio_scan_get_undistorted: no lio_scan_preprocess* on this ctx");
+    *n_points = c->undist_n;
+    if (stride) *stride = c->undist_stride;
+    if (!out || c->undist_n == 0) return LIO_OK;
+    if (cap_points < c->undist_n) return fail(LIO_ERR_ARG, "lio_scan_get_undistorted: out too small");
+    HIP_TRY(hipSetDevice(c->map->dev));
+    HIP_TRY(hipMemcpyAsync(out, c->filt.c, (size_t)c->undist_n * c->undist_stride * sizeof(float),
+                           hipMemcpyDeviceToHost, c->map->st));
+    HIP_TRY(hipStreamSynchronize(c->map->st));
     return LIO_OK;
 }
 
@@ -1271,9 +1292,13 @@ int lio_scan_preprocess_cloud2(lio_ctx* c, const uint8_t* data, int64_t n_points
     if (rc) return filter_status(rc, "lio_scan_preprocess_cloud2");
     const lio::ScanPrepParams sp{pp.point_filter_num, pp.blind, pp.filter_size_surf, 4};
     int64_t m = 0;
+    c->undist_n = -1;
+    int64_t mu = 0;
     rc = lio::scan_preprocess(c->filt, c->d_raw, n_points, 5, sp, c->d_poses, n_poses, undistort_end(end), c->d_rec, &m,
-                              st);
+                              st, &mu);
     if (rc) return filter_status(rc, "lio_scan_preprocess_cloud2");
+    c->undist_n = mu;
+    c->undist_stride = 5;
     rc = ctx_reserve(c, m);
     if (rc) return rc;
     rc = lio::records_to_xyz(c->d_rec, m, 5, c->d_body, st);

@@ -28,8 +28,9 @@ namespace lio {
 constexpr int kNone = 0x7fffffff;
 
 struct GridDev {
-    const float4* pts;      // sorted by cell
-    const uint32_t* start;  // ncells + 1
+    const float4* pts;      // points grouped by cell
+    const uint32_t* start;  // dense grids (ICP): ncells + 1 CSR offsets, a row of cells one contiguous range
+    const uint2* rng;       // map grids: per cell its live slots [x, y) (gapped CSR: blocks with spare room)
     float ox, oy, oz;       // grid origin (min corner)
     float cell, inv_cell;
     float margin;           // conservative slack for cell assignment rounding
@@ -276,8 +277,8 @@ __device__ __forceinline__ void group_merge(TopK<K>& tk) {
 template <int K, int G>
 __device__ __forceinline__ void scan_cell_group(const GridDev& g, uint32_t c, float qx, float qy, float qz, int sub,
                                                 TopK<K>& tk) {
-    const uint32_t b = g.start[c];
-    const uint32_t e = g.start[c + 1];
+    const uint2 r = g.rng[c];
+    const uint32_t b = r.x, e = r.y;
     for (uint32_t j = b + (uint32_t)sub; j < e; j += G) {
         const float4 p = g.pts[j];
         tk.push(sqdist3(qx, qy, qz, p.x, p.y, p.z), __float_as_int(p.w));
@@ -289,8 +290,8 @@ __device__ __forceinline__ void scan_cell_group(const GridDev& g, uint32_t c, fl
 template <int K, int G, int U = 4>
 __device__ __forceinline__ void scan_cell_group2(const GridDev& g, uint32_t c, float qx, float qy, float qz, int sub,
                                                  TopK<K>& tk) {
-    const uint32_t b = g.start[c];
-    const uint32_t e = g.start[c + 1];
+    const uint2 r = g.rng[c];
+    const uint32_t b = r.x, e = r.y;
     for (uint32_t j = b + (uint32_t)sub; j < e; j += U * G) {
         float4 p[U];
 #pragma unroll
@@ -387,8 +388,8 @@ __device__ bool group_knn_exact(const GridDev& g, float qx, float qy, float qz, 
 template <int K>
 __device__ __forceinline__ void scan_cell_seq(const GridDev& g, uint32_t c, float qx, float qy, float qz,
                                               TopK<K>& tk) {
-    const uint32_t b = g.start[c];
-    const uint32_t e = g.start[c + 1];
+    const uint2 r = g.rng[c];
+    const uint32_t b = r.x, e = r.y;
     uint32_t j = b;
     for (; j + 4 <= e; j += 4) {
         const float4 p0 = g.pts[j], p1 = g.pts[j + 1], p2 = g.pts[j + 2], p3 = g.pts[j + 3];
@@ -462,8 +463,9 @@ __device__ __forceinline__ void shell1_ranges(const GridDev& g, int cx, int cy, 
         uint32_t b = 0, e = 0;
         if (ok) {
             const uint32_t c = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
-            b = g.start[c];
-            e = g.start[c + 1];
+            const uint2 r = g.rng[c];
+            b = r.x;
+            e = r.y;
         }
         b4[j] = b;
         n4[j] = e - b;
@@ -730,8 +732,9 @@ __device__ void block_knn_box_flat(const GridDev& g, float qx, float qy, float q
                 const float bd = (axis_gap(qx, xl, xl + w) + axis_gap(qy, yl, yl + w)) + axis_gap(qz, zl, zl + w);
                 if (!(bd * 0.999999f > bound)) {
                     const uint32_t c = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
-                    b = g.start[c];
-                    n = g.start[c + 1] - b;
+                    const uint2 rc = g.rng[c];
+                    b = rc.x;
+                    n = rc.y - rc.x;
                 }
             }
         }

@@ -689,8 +689,9 @@ int transform_segments(const float* d_in, int64_t n, int stride, const int64_t* 
 
 int scan_preprocess(FilterBuf& b, const float* d_raw, int64_t n, int stride, const ScanPrepParams& p,
                     const ImuPose* d_poses, int np, const UndistortEnd& end, float* d_out, int64_t* n_out,
-                    hipStream_t st) {
+                    hipStream_t st, int64_t* n_undist) {
     *n_out = 0;
+    if (n_undist) *n_undist = 0;
     if (n <= 0) return 0;
     if (stride < 4 || stride > kMaxFields || p.time_field < 3 || p.time_field >= stride) return -1;
     if (reserve(b, n)) return -5;
@@ -706,6 +707,7 @@ int scan_preprocess(FilterBuf& b, const float* d_raw, int64_t n, int stride, con
     FCHK(hipMemcpyAsync(b.h_small, b.vid + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     FCHK(hipStreamSynchronize(st));
     const int64_t m = (uint32_t)b.h_small[0];
+    if (n_undist) *n_undist = m;
     if (m == 0) return 0;
     // 2. sort by time (stable), 3. undistort
     time_key_kernel<<<nblk(m), 256, 0, st>>>(b.a, m, stride, p.time_field, b.keys, b.vals);

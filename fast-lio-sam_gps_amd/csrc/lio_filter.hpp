@@ -66,10 +66,12 @@ int voxel_grid(FilterBuf& b, const float* d_in, int64_t n, int stride, const flo
 // points of segment s ([seg_off[s], seg_off[s+1]), nseg segments, seg_off[nseg] = n) through T16[s]
 int transform_segments(const float* d_in, int64_t n, int stride, const int64_t* d_seg_off, int nseg,
                        const double* d_T16, float* d_out, hipStream_t st);
-// selection -> stable sort by time -> undistortion (np >= 2 poses) -> voxel grid
+// selection -> stable sort by time -> undistortion (np >= 2 poses) -> voxel grid.  The undistorted,
+// time-sorted records before the voxel grid (FAST-LIO feats_undistort) stay in b.c, *n_undist of them,
+// until the next call on b.
 int scan_preprocess(FilterBuf& b, const float* d_raw, int64_t n, int stride, const ScanPrepParams& p,
                     const ImuPose* d_poses, int np, const UndistortEnd& end, float* d_out, int64_t* n_out,
-                    hipStream_t st);
+                    hipStream_t st, int64_t* n_undist = nullptr);
 
 int records_to_xyz(const float* d_rec, int64_t n, int stride, float* d_xyz, hipStream_t st);
 

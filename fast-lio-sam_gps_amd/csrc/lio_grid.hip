@@ -134,87 +134,124 @@ __global__ void gather_kernel(const float4* __restrict__ by_id, int64_t n, const
     ckeys[j] = sorted_keys[j];
 }
 
-// ---- incremental maintenance (merge path) ----------------------------------
-// keys of the appended ids [id0, id0+n): all alive; flags points outside the grid
-__global__ void new_key_kernel(const float4* __restrict__ by_id, int64_t id0, int64_t n, GridGeom g,
-                               uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, int* __restrict__ outside) {
-    const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (k >= n) return;
-    const float4 p = by_id[id0 + k];
-    keys[k] = cell_key_of(g, 1.0f / g.cell, p.x, p.y, p.z, outside);
-    vals[k] = (uint32_t)(id0 + k);
+// ---- gapped (map) grids -------------------------------------------------------
+// block capacity of a cell holding `cnt` points at a (re)build: room for a few more (a 1 m cell of a
+// 0.5 m-downsampled map holds at most 8 downsampled points, map_incremental adds a handful per scan)
+__device__ __forceinline__ uint32_t cell_capacity(uint32_t cnt) { return cnt ? cnt + max(4u, cnt >> 2) : 0u; }
+
+// lim[c] = capacity of cell c (counts: the dense CSR start[]); lim[ncells] = 0 for the scan total
+__global__ void cap_kernel(const uint32_t* __restrict__ start, uint32_t nc, uint32_t* __restrict__ lim) {
+    const uint32_t c = blockIdx.x * 256u + threadIdx.x;
+    if (c > nc) return;
+    lim[c] = c < nc ? cell_capacity(start[c + 1] - start[c]) : 0u;
 }
 
-// survivor flags of the current cell-sorted entries (slot n = 0 for the scan total)
-__global__ void alive_flag_kernel(const float4* __restrict__ pts, const float4* __restrict__ by_id, int64_t n,
-                                  uint32_t* __restrict__ flag) {
-    const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (j > n) return;
-    flag[j] = j < n ? (by_id[__float_as_int(pts[j].w)].w != 0.f ? 1u : 0u) : 0u;
-}
-
-__device__ __forceinline__ int64_t lower_bound_u32(const uint32_t* a, int64_t n, uint32_t v) {
-    int64_t lo = 0, hi = n;
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if (a[mid] < v) lo = mid + 1;
-        else hi = mid;
+// gbase = exclusive scan of the capacities: rng[c] = {gbase[c], gbase[c] + count}, lim[c] = gbase[c + 1]
+__global__ void rng_kernel(const uint32_t* __restrict__ start, const uint32_t* __restrict__ gbase, uint32_t nc,
+                           uint2* __restrict__ rng, uint32_t* __restrict__ lim, uint32_t* __restrict__ bump) {
+    const uint32_t c = blockIdx.x * 256u + threadIdx.x;
+    if (c >= nc) {
+        if (c == nc) *bump = gbase[nc];
+        return;
     }
-    return lo;
+    const uint32_t b = gbase[c];
+    rng[c] = make_uint2(b, b + (start[c + 1] - start[c]));
+    lim[c] = gbase[c + 1];
 }
 
-// old entry j -> its compacted rank + the number of new entries in earlier
-// cells (ties: old ids are smaller than every appended id, so old first)
-__global__ void merge_old_kernel(const float4* __restrict__ pts, const uint32_t* __restrict__ ckeys, int64_t n_old,
-                                 const uint32_t* __restrict__ pos, const uint32_t* __restrict__ new_keys, int64_t n_new,
-                                 float4* __restrict__ pts_out, uint32_t* __restrict__ ckeys_out) {
-    const int64_t j0 = blockIdx.x * (int64_t)blockDim.x, j = j0 + threadIdx.x;
-    // the block's entries are cell-sorted: their cells' new keys form one narrow window of new_keys
-    __shared__ int64_t s_lo, s_hi;
-    if (threadIdx.x == 0) s_lo = lower_bound_u32(new_keys, n_new, ckeys[j0]);
-    if (threadIdx.x == 1) s_hi = lower_bound_u32(new_keys, n_new, ckeys[min(j0 + (int64_t)blockDim.x, n_old) - 1] + 1u);
-    __syncthreads();
-    if (j >= n_old) return;
-    if (pos && pos[j + 1] == pos[j]) return;  // deleted
-    const uint32_t c = ckeys[j];
-    const int64_t lo = s_lo;
-    const int64_t o = (pos ? (int64_t)pos[j] : j) + lo + lower_bound_u32(new_keys + lo, s_hi - lo, c);
-    pts_out[o] = pts[j];
-    ckeys_out[o] = c;
-}
-
-// new entry k (sorted) -> k + the number of surviving old entries in cells <= its cell
-__global__ void merge_new_kernel(const float4* __restrict__ by_id, const uint32_t* __restrict__ new_keys,
-                                 const uint32_t* __restrict__ new_ids, int64_t n_new,
-                                 const uint32_t* __restrict__ ckeys, int64_t n_old, const uint32_t* __restrict__ pos,
-                                 float4* __restrict__ pts_out, uint32_t* __restrict__ ckeys_out) {
-    const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (k >= n_new) return;
-    const uint32_t c = new_keys[k];
-    const int64_t u = c == 0xffffffffu ? n_old : lower_bound_u32(ckeys, n_old, c + 1);
-    const int64_t o = k + (pos ? (int64_t)pos[u] : u);
-    const uint32_t id = new_ids[k];
+// sorted entry j of cell ck -> slot gbase[ck] + (j - start[ck]) (rank inside the cell kept: id order)
+__global__ void gather_gapped_kernel(const float4* __restrict__ by_id, int64_t n, const uint32_t* __restrict__ sorted_ids,
+                                     const uint32_t* __restrict__ sorted_keys, const uint32_t* __restrict__ start,
+                                     const uint2* __restrict__ rng, float4* __restrict__ pts) {
+    const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    const uint32_t id = sorted_ids[j], ck = sorted_keys[j];
     const float4 p = by_id[id];
-    pts_out[o] = make_float4(p.x, p.y, p.z, __int_as_float((int)id));
-    ckeys_out[o] = c;
+    pts[rng[ck].x + (uint32_t)(j - start[ck])] = make_float4(p.x, p.y, p.z, __int_as_float((int)id));
 }
 
-// incremental cell table after a merge, in place: cell c starts after the surviving old entries of
-// earlier cells (pos[start_old[c]], or start_old[c] with no deletions) and the new entries of
-// earlier cells (lower bound of c in the sorted new keys).  Slot ncells gives the new total.
-// Replaces a clear + run count + scan over all cells.
-__global__ void start_update_kernel(uint32_t* __restrict__ start, uint32_t nc1, const uint32_t* __restrict__ pos,
-                                    const uint32_t* __restrict__ new_keys, int64_t n_new) {
-    const uint32_t c0 = blockIdx.x * 256u, c = c0 + threadIdx.x;
-    // the block's cells share a narrow window of the new keys: bound it once per block
-    __shared__ int64_t s_lo, s_hi;
-    if (threadIdx.x == 0) s_lo = lower_bound_u32(new_keys, n_new, c0);
-    if (threadIdx.x == 1) s_hi = lower_bound_u32(new_keys, n_new, c0 + 256u);
-    __syncthreads();
-    if (c >= nc1) return;
-    const int64_t lo = s_lo;
-    const uint32_t so = start[c];
-    start[c] = (pos ? pos[so] : so) + (uint32_t)(lo + lower_bound_u32(new_keys + lo, s_hi - lo, c));
+// one lane per listed cell (grid-stride): drop the entries marked dead (id bits kNone), keep the
+// order, clear the cell's dirty byte
+__global__ void compact_cells_kernel(float4* __restrict__ pts, uint2* __restrict__ rng, uint8_t* __restrict__ dirty,
+                                     const uint32_t* __restrict__ dlist, const uint32_t* __restrict__ d_ndirty,
+                                     uint32_t dcap) {
+    const uint32_t nd = min(*d_ndirty, dcap);
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nd; k += gridDim.x * blockDim.x) {
+        const uint32_t c = dlist[k];
+        const uint2 r = rng[c];
+        uint32_t o = r.x;
+        for (uint32_t j = r.x; j < r.y; ++j) {
+            const float4 p = pts[j];
+            if (__float_as_int(p.w) == kNone) continue;
+            if (o != j) pts[o] = p;
+            ++o;
+        }
+        rng[c].y = o;
+        dirty[c] = 0;
+    }
+}
+
+// new id j (0 <= j < *d_nnew): its cell and its rank among this update's points of that cell
+__global__ void insert_rank_kernel(const float4* __restrict__ by_id, int64_t id0, const uint32_t* __restrict__ d_nnew,
+                                   GridGeom g, uint32_t* __restrict__ addc, uint32_t* __restrict__ tmp_cell,
+                                   uint32_t* __restrict__ tmp_rank, uint32_t* __restrict__ tlist,
+                                   uint32_t* __restrict__ d_ntouch, uint32_t* __restrict__ flags) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= *d_nnew) return;
+    const float4 p = by_id[id0 + j];
+    int out = 0;
+    const uint32_t c = cell_key_of(g, 1.0f / g.cell, p.x, p.y, p.z, &out);
+    if (out) atomicOr(flags, 1u);
+    const uint32_t r = atomicAdd(&addc[c], 1u);
+    if (r == 0) tlist[atomicAdd(d_ntouch, 1u)] = c;
+    tmp_cell[j] = c;
+    tmp_rank[j] = r;
+}
+
+// one lane per touched cell: room for its new points (a bigger block from the pool when the cell's is
+// full: the live points move, the old block is left behind); addc[c] becomes the first new slot
+__global__ void insert_alloc_kernel(float4* __restrict__ pts, uint2* __restrict__ rng, uint32_t* __restrict__ lim,
+                                    uint32_t* __restrict__ addc, const uint32_t* __restrict__ tlist,
+                                    const uint32_t* __restrict__ d_ntouch, uint32_t* __restrict__ bump,
+                                    uint32_t slots_cap, uint32_t* __restrict__ flags) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= *d_ntouch) return;
+    const uint32_t c = tlist[k];
+    const uint32_t add = addc[c];
+    uint2 r = rng[c];
+    const uint32_t live = r.y - r.x;
+    if (r.y + add > lim[c]) {
+        const uint32_t cap = max(8u, 2u * (live + add));
+        const uint32_t base = atomicAdd(bump, cap);
+        if ((uint64_t)base + cap > (uint64_t)slots_cap) {  // pool exhausted: the caller rebuilds
+            atomicOr(flags, 2u);
+            addc[c] = 0xffffffffu;
+            return;
+        }
+        for (uint32_t j = 0; j < live; ++j) pts[base + j] = pts[r.x + j];
+        r = make_uint2(base, base + live);
+        lim[c] = base + cap;
+    }
+    addc[c] = r.y;
+    rng[c] = make_uint2(r.x, r.y + add);
+}
+
+__global__ void insert_write_kernel(const float4* __restrict__ by_id, int64_t id0, const uint32_t* __restrict__ d_nnew,
+                                    const uint32_t* __restrict__ tmp_cell, const uint32_t* __restrict__ tmp_rank,
+                                    const uint32_t* __restrict__ addc, float4* __restrict__ pts) {
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= *d_nnew) return;
+    const uint32_t base = addc[tmp_cell[j]];
+    if (base == 0xffffffffu) return;
+    const uint32_t id = (uint32_t)(id0 + j);
+    const float4 p = by_id[id];
+    pts[base + tmp_rank[j]] = make_float4(p.x, p.y, p.z, __int_as_float((int)id));
+}
+
+__global__ void insert_clear_kernel(uint32_t* __restrict__ addc, const uint32_t* __restrict__ tlist,
+                                    const uint32_t* __restrict__ d_ntouch) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k < *d_ntouch) addc[tlist[k]] = 0u;
 }
 
 #define HIPCHK(x)                                                               \
@@ -242,17 +279,20 @@ static int ensure(void** p, size_t& cap_bytes, size_t need) {
 
 void grid_free(GridBuf& g) {
     void* ptrs[] = {g.pts, g.by_id, g.start, g.keys, g.keys_alt, g.vals, g.vals_alt, g.tmp, g.aabb, g.xyz,
-                    g.ckeys, g.pts_alt, g.ckeys_alt, g.flag, g.pos};
+                    g.ckeys, g.rng, g.lim, g.addc, g.dirty, g.bump};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     if (g.aabb_host) (void)hipHostFree(g.aabb_host);
+    const bool gapped = g.gapped;
     g = GridBuf{};
+    g.gapped = gapped;
 }
 
 GridDev grid_view(const GridBuf& g) {
     GridDev v;
     v.pts = g.pts;
     v.start = g.start;
+    v.rng = g.rng;
     v.ox = g.geom.ox;
     v.oy = g.geom.oy;
     v.oz = g.geom.oz;
@@ -281,42 +321,61 @@ int grid_reserve_ids(GridBuf& g, int64_t n_ids, hipStream_t st) {
     return 0;
 }
 
-// per-entry buffers (cell-sorted arrays, sort scratch) for n ids; the live
-// cell-sorted entries (pts, ckeys: g.n of them) are carried over
-static int reserve_entries(GridBuf& g, int64_t n, hipStream_t st) {
-    if (n <= g.cap && g.pts) return 0;
+// per-entry buffers for n ids: the (key, id) sort scratch, and for dense grids the cell-sorted
+// arrays (gapped grids keep their points in the slot pool, reserve_slots)
+static int reserve_entries(GridBuf& g, int64_t n) {
+    if (n <= g.cap && g.keys) return 0;
     const int64_t cap = std::max<int64_t>(n, g.cap + g.cap / 2);
-    float4* pts = nullptr;
-    uint32_t* ck = nullptr;
-    HIPCHK(hipMalloc(&pts, cap * sizeof(float4)));
-    HIPCHK(hipMalloc(&ck, cap * sizeof(uint32_t)));
-    if (g.pts && g.n > 0) {
-        HIPCHK(hipMemcpyAsync(pts, g.pts, g.n * sizeof(float4), hipMemcpyDeviceToDevice, st));
-        HIPCHK(hipMemcpyAsync(ck, g.ckeys, g.n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st));
-    }
-    HIPCHK(hipStreamSynchronize(st));
-    void* bufs[] = {g.pts, g.keys, g.keys_alt, g.vals, g.vals_alt, g.ckeys, g.pts_alt, g.ckeys_alt, g.flag, g.pos};
+    void* bufs[] = {g.keys, g.keys_alt, g.vals, g.vals_alt};
     for (void* p : bufs)
         if (p) HIPCHK(hipFree(p));
-    g.pts = pts;
-    g.ckeys = ck;
-    HIPCHK(hipMalloc(&g.pts_alt, cap * sizeof(float4)));
     HIPCHK(hipMalloc(&g.keys, cap * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&g.keys_alt, cap * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&g.vals, cap * sizeof(uint32_t)));
     HIPCHK(hipMalloc(&g.vals_alt, cap * sizeof(uint32_t)));
-    HIPCHK(hipMalloc(&g.ckeys_alt, cap * sizeof(uint32_t)));
-    HIPCHK(hipMalloc(&g.flag, (cap + 1) * sizeof(uint32_t)));
-    HIPCHK(hipMalloc(&g.pos, (cap + 1) * sizeof(uint32_t)));
+    if (!g.gapped) {
+        if (g.pts) HIPCHK(hipFree(g.pts));
+        if (g.ckeys) HIPCHK(hipFree(g.ckeys));
+        g.pts = nullptr;
+        g.ckeys = nullptr;
+        HIPCHK(hipMalloc(&g.pts, cap * sizeof(float4)));
+        HIPCHK(hipMalloc(&g.ckeys, cap * sizeof(uint32_t)));
+    }
     g.cap = cap;
+    return 0;
+}
+
+// gapped grids: the slot pool (contents are rewritten by the rebuild that asks for it)
+static int reserve_slots(GridBuf& g, int64_t slots) {
+    if (slots <= g.slots_cap && g.pts) return 0;
+    if (slots >= (int64_t)0xffffffffu) return -1;
+    if (g.pts) HIPCHK(hipFree(g.pts));
+    g.pts = nullptr;
+    g.slots_cap = 0;
+    HIPCHK(hipMalloc(&g.pts, (size_t)slots * sizeof(float4)));
+    g.slots_cap = slots;
     return 0;
 }
 
 static int reserve_cells(GridBuf& g, uint32_t nc1) {
     if (nc1 <= g.cells_cap && g.start) return 0;
-    if (g.start) HIPCHK(hipFree(g.start));
+    void* bufs[] = {g.start, g.rng, g.lim, g.addc, g.dirty};
+    for (void* p : bufs)
+        if (p) HIPCHK(hipFree(p));
+    g.start = nullptr;
+    g.rng = nullptr;
+    g.lim = nullptr;
+    g.addc = nullptr;
+    g.dirty = nullptr;
     const uint32_t cap = std::max<uint32_t>(nc1, g.cells_cap + g.cells_cap / 2);
     HIPCHK(hipMalloc(&g.start, 2 * (size_t)cap * sizeof(uint32_t)));  // + histogram scratch
+    if (g.gapped) {
+        HIPCHK(hipMalloc(&g.rng, (size_t)cap * sizeof(uint2)));
+        HIPCHK(hipMalloc(&g.lim, (size_t)cap * sizeof(uint32_t)));
+        HIPCHK(hipMalloc(&g.addc, (size_t)cap * sizeof(uint32_t)));
+        HIPCHK(hipMalloc(&g.dirty, (size_t)cap + 4));  // + 4: flagged through 32-bit words
+        if (!g.bump) HIPCHK(hipMalloc(&g.bump, sizeof(uint32_t)));
+    }
     g.cells_cap = cap;
     return 0;
 }
@@ -328,7 +387,7 @@ int grid_build(GridBuf& g, const float* d_xyz, int64_t n, float cell, hipStream_
     const int64_t room = n + n / 2;
     int rc = grid_reserve_ids(g, room, st);
     if (rc) return rc;
-    rc = reserve_entries(g, room, st);
+    rc = reserve_entries(g, room);
     if (rc) return rc;
     init_by_id_kernel<<<(int)((n + 255) / 256), 256, 0, st>>>(d_xyz, n, g.by_id);
     g.n_ids = n;
@@ -338,7 +397,7 @@ int grid_build(GridBuf& g, const float* d_xyz, int64_t n, float cell, hipStream_
 int grid_rebuild(GridBuf& g, float cell, float slack, hipStream_t st) {
     const int64_t n_ids = g.n_ids;
     if (!(cell > 0.f)) cell = 1.0f;
-    int rc = reserve_entries(g, std::max<int64_t>(n_ids, 1), st);
+    int rc = reserve_entries(g, std::max<int64_t>(n_ids, 1));
     if (rc) return rc;
     if (!g.aabb) HIPCHK(hipMalloc(&g.aabb, 6 * 1024 * sizeof(float) + 64));
     if (!g.aabb_host) HIPCHK(hipHostMalloc(&g.aabb_host, 64));
@@ -406,74 +465,58 @@ int grid_rebuild(GridBuf& g, float cell, float slack, hipStream_t st) {
                                                   bits, st));
     tb = g.tmp_bytes;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(g.tmp, tb, counts, g.start, (int)nc1, st));
+    if (!g.gapped) {
+        if (n_alive)
+            gather_kernel<<<(int)((n_alive + 255) / 256), 256, 0, st>>>(g.by_id, n_alive, g.vals_alt, g.keys_alt,
+                                                                        g.pts, g.ckeys);
+        HIPCHK(hipGetLastError());
+        g.n = n_alive;
+        return 0;
+    }
+    // gapped: block capacities -> block bases (scan into the histogram scratch, free after the dense scan)
+    uint32_t* gbase = counts;
+    const int nbc = (int)((nc1 + 255) / 256);
+    cap_kernel<<<nbc, 256, 0, st>>>(g.start, geo.ncells, g.lim);
+    tb = g.tmp_bytes;
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(g.tmp, tb, g.lim, gbase, (int)nc1, st));
+    rng_kernel<<<nbc, 256, 0, st>>>(g.start, gbase, geo.ncells, g.rng, g.lim, g.bump);
+    HIPCHK(hipMemsetAsync(g.addc, 0, (size_t)geo.ncells * sizeof(uint32_t), st));
+    HIPCHK(hipMemsetAsync(g.dirty, 0, (size_t)geo.ncells, st));
+    uint32_t used = 0;
+    HIPCHK(hipMemcpyAsync(g.aabb_host + 9, gbase + geo.ncells, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    std::memcpy(&used, g.aabb_host + 9, sizeof(uint32_t));
+    // pool: the blocks + room for the cells that will outgrow theirs before the next rebuild
+    const int64_t pool = (int64_t)used + std::max<int64_t>((int64_t)1 << 20, (int64_t)used / 2);
+    rc = reserve_slots(g, pool);
+    if (rc) return rc;
     if (n_alive)
-        gather_kernel<<<(int)((n_alive + 255) / 256), 256, 0, st>>>(g.by_id, n_alive, g.vals_alt, g.keys_alt, g.pts,
-                                                                    g.ckeys);
+        gather_gapped_kernel<<<(int)((n_alive + 255) / 256), 256, 0, st>>>(g.by_id, n_alive, g.vals_alt, g.keys_alt,
+                                                                           g.start, g.rng, g.pts);
     HIPCHK(hipGetLastError());
+    g.slots_used = used;
     g.n = n_alive;
     return 0;
 }
 
-// Incremental update after ids [id0, n_ids) were appended to by_id (alive) and
-// (when `deleted`) some earlier ids were marked dead: surviving entries and
-// the new ones are merged in cell order (no full sort), start[] recounted.
-// Falls back to grid_rebuild (geometry + slack) when a new point lies outside
-// the grid.  Synchronises the stream once.
-int grid_reserve_entries(GridBuf& g, int64_t n, hipStream_t st) { return reserve_entries(g, std::max<int64_t>(n, 1), st); }
+void grid_compact_cells(GridBuf& g, const uint32_t* dlist, const uint32_t* d_ndirty, uint32_t dcap, int n_max,
+                        hipStream_t st) {
+    if (n_max <= 0) return;
+    compact_cells_kernel<<<std::min(256, (n_max + 255) / 256), 256, 0, st>>>(g.pts, g.rng, g.dirty, dlist, d_ndirty,
+                                                                              dcap);
+}
 
-int grid_update(GridBuf& g, int64_t id0, bool deleted, float slack, hipStream_t st) {
-    const int64_t n_new = g.n_ids - id0, n_old = g.n;
-    if (n_new < 0) return -1;
-    if (g.flags_ready && g.cap < g.n_ids) return -1;  // the caller reserved the entries first
-    int rc = reserve_entries(g, std::max<int64_t>(g.n_ids, 1), st);
-    if (rc) return rc;
-    int* d_out = reinterpret_cast<int*>(g.aabb + 7);  // outside flag
-    HIPCHK(hipMemsetAsync(d_out, 0, sizeof(int), st));
-    uint32_t* nkeys = g.keys_alt;  // sorted new (key, id)
-    uint32_t* nids = g.vals_alt;
-    if (n_new > 0) {
-        new_key_kernel<<<(int)((n_new + 255) / 256), 256, 0, st>>>(g.by_id, id0, n_new, g.geom, g.keys, g.vals, d_out);
-        size_t sort_bytes = 0;
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, g.keys, g.keys_alt, g.vals, g.vals_alt,
-                                                  (int)n_new, 0, 32, st));
-        if (ensure(&g.tmp, g.tmp_bytes, sort_bytes) != 0) return -5;
-        size_t tb = g.tmp_bytes;
-        HIPCHK(hipcub::DeviceRadixSort::SortPairs(g.tmp, tb, g.keys, g.keys_alt, g.vals, g.vals_alt, (int)n_new, 0,
-                                                  32, st));
-    }
-    uint32_t* pos = nullptr;
-    if (deleted && n_old > 0) {
-        if (!g.flags_ready)  // survivor flags from the alive bits (else set by the caller's kernels)
-            alive_flag_kernel<<<(int)((n_old + 1 + 255) / 256), 256, 0, st>>>(g.pts, g.by_id, n_old, g.flag);
-        size_t scan_bytes = 0;
-        HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, g.flag, g.pos, (int)(n_old + 1), st));
-        if (ensure(&g.tmp, g.tmp_bytes, scan_bytes) != 0) return -5;
-        size_t tb = g.tmp_bytes;
-        HIPCHK(hipcub::DeviceScan::ExclusiveSum(g.tmp, tb, g.flag, g.pos, (int)(n_old + 1), st));
-        pos = g.pos;
-        HIPCHK(hipMemcpyAsync(g.aabb_host + 8, g.pos + n_old, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    }
-    HIPCHK(hipMemcpyAsync(g.aabb_host + 7, d_out, sizeof(int), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    int outside = 0;
-    std::memcpy(&outside, g.aabb_host + 7, sizeof(int));
-    g.flags_ready = false;
-    if (outside || g.n == 0) return grid_rebuild(g, g.geom.cell, slack, st);
-    uint32_t kept = (uint32_t)n_old;
-    if (pos) std::memcpy(&kept, g.aabb_host + 8, sizeof(uint32_t));
-    if (n_old > 0)
-        merge_old_kernel<<<(int)((n_old + 255) / 256), 256, 0, st>>>(g.pts, g.ckeys, n_old, pos, nkeys, n_new,
-                                                                     g.pts_alt, g.ckeys_alt);
-    if (n_new > 0)
-        merge_new_kernel<<<(int)((n_new + 255) / 256), 256, 0, st>>>(g.by_id, nkeys, nids, n_new, g.ckeys, n_old,
-                                                                     pos, g.pts_alt, g.ckeys_alt);
-    std::swap(g.pts, g.pts_alt);
-    std::swap(g.ckeys, g.ckeys_alt);
-    g.n = (int64_t)kept + n_new;
-    const uint32_t nc1 = g.geom.ncells + 1;
-    start_update_kernel<<<(int)((nc1 + 255) / 256), 256, 0, st>>>(g.start, nc1, pos, nkeys, n_new);
-    HIPCHK(hipGetLastError());
-    return 0;
+void grid_insert_ids(GridBuf& g, int64_t id0, const uint32_t* d_nnew, int n_max, GridInsertScratch s,
+                     uint32_t* flags, hipStream_t st) {
+    if (n_max <= 0) return;
+    const int nb = (n_max + 255) / 256;
+    (void)hipMemsetAsync(s.d_ntouch, 0, sizeof(uint32_t), st);
+    insert_rank_kernel<<<nb, 256, 0, st>>>(g.by_id, id0, d_nnew, g.geom, g.addc, s.tmp_cell, s.tmp_rank, s.tlist,
+                                           s.d_ntouch, flags);
+    insert_alloc_kernel<<<nb, 256, 0, st>>>(g.pts, g.rng, g.lim, g.addc, s.tlist, s.d_ntouch, g.bump,
+                                            (uint32_t)std::min<int64_t>(g.slots_cap, 0xffffffffll), flags);
+    insert_write_kernel<<<nb, 256, 0, st>>>(g.by_id, id0, d_nnew, s.tmp_cell, s.tmp_rank, g.addc, g.pts);
+    insert_clear_kernel<<<nb, 256, 0, st>>>(g.addc, s.tlist, s.d_ntouch);
 }
 
 }  // namespace lio

@@ -608,6 +608,162 @@ int icp_build_tiles(const GridBuf& q, uint2* tiles, uint32_t* scratch, void*& tm
     return (int)total;
 }
 
+// ----------------------------------------------------------------------------
+// PCL-order fidelity mode (lio_icp_params.umeyama_float): the float statistics of
+// pcl::umeyama(cloud_src, cloud_tgt, false) as TransformationEstimationSVD<PointXYZI,
+// PointXYZI, float> builds them [U] (common/impl/eigen.hpp, a copy of Eigen 3.3's
+// Umeyama.h): the accepted correspondences in source order,
+//   src_mean = src.rowwise().sum() * one_over_n   (a sequential float sum per row,
+//              starting from the first element: Eigen's redux over a strided row)
+//   sigma    = one_over_n * dst_demean * src_demean^T  (the depth sum sequential)
+// A float sum's value depends on its order, so each of the 6 + 9 chains runs on ONE
+// lane, in order; the block stages the correspondences through LDS around it.
+// Single rank only (the chains cannot be split).  icp_pcl_means_kernel also writes the
+// compacted pairs (src xyz, tgt xyz) for icp_pcl_sigma_kernel.
+// ----------------------------------------------------------------------------
+constexpr int kPclThreads = 1024;  // one block: a chunk of 1024 correspondences per round
+
+// block-exclusive prefix count of `flag` (1024 threads): returns this thread's slot, *total = chunk count
+__device__ __forceinline__ uint32_t block_compact_slot(bool flag, uint32_t* s_w, uint32_t& total) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const uint64_t m = __ballot(flag);
+    const uint32_t in_wave = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (lane == 0) s_w[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    uint32_t before = 0, tot = 0;
+#pragma unroll
+    for (int k = 0; k < kPclThreads / 64; ++k) {
+        const uint32_t c = s_w[k];
+        before += k < w ? c : 0u;
+        tot += c;
+    }
+    total = tot;
+    return before + in_wave;
+}
+
+// one lane adds col[0 .. cnt) to acc in order (loads 8 ahead; the adds stay one dependent chain)
+__device__ __forceinline__ void serial_add(const float* col, uint32_t cnt, float& acc, bool& first) {
+    uint32_t k = 0;
+    if (first && cnt > 0) {  // Eigen's redux starts from the first coefficient
+        acc = col[0];
+        first = false;
+        k = 1;
+    }
+    for (; k + 8 <= cnt; k += 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = col[k + u];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; k < cnt; ++k) acc += col[k];
+}
+
+// out[0..5] = float sums (src x y z, tgt x y z), out[6] = count (uint32 bits); pairs: n x 6 compacted
+__global__ void __launch_bounds__(kPclThreads) icp_pcl_means_kernel(IcpArgs a, float* __restrict__ pairs,
+                                                                    float* __restrict__ out) {
+    __shared__ float s[6][kPclThreads];
+    __shared__ uint32_t s_w[kPclThreads / 64];
+    float acc = 0.f;
+    bool first = true;
+    uint32_t done = 0;
+    for (int base = 0; base < a.n; base += kPclThreads) {
+        const int i = base + (int)threadIdx.x;
+        bool ok = false;
+        float v[6];
+        if (i < a.n) {
+            const int id = a.nn_id[i];
+            const float d2 = a.nn_d2[i];
+            ok = id >= 0 && id != kNone && !((double)d2 > a.max_d2);
+            if (ok) {
+                const float4 q = a.tgt_by_id[id];
+                v[0] = a.cur[3 * i], v[1] = a.cur[3 * i + 1], v[2] = a.cur[3 * i + 2];
+                v[3] = q.x, v[4] = q.y, v[5] = q.z;
+            }
+        }
+        uint32_t cnt;
+        const uint32_t slot = block_compact_slot(ok, s_w, cnt);
+        if (ok) {
+#pragma unroll
+            for (int d = 0; d < 6; ++d) {
+                s[d][slot] = v[d];
+                pairs[6 * (size_t)(done + slot) + d] = v[d];
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x < 6) serial_add(s[threadIdx.x], cnt, acc, first);
+        done += cnt;
+        __syncthreads();  // the chunk is consumed before the next overwrites it (and s_w is reused)
+    }
+    if (threadIdx.x < 6) out[threadIdx.x] = acc;
+    if (threadIdx.x == 0) out[6] = __uint_as_float(done);
+}
+
+// sums / count from icp_pcl_means_kernel -> out[7 + 3 r + c] = sum_k (tgt_r - dm_r) (src_c - sm_c), in order
+__global__ void __launch_bounds__(kPclThreads) icp_pcl_sigma_kernel(const float* __restrict__ pairs,
+                                                                    float* __restrict__ out) {
+    __shared__ float s[6][kPclThreads];
+    const uint32_t n = __float_as_uint(out[6]);
+    const float one_over_n = 1.f / (float)n;
+    // lane t < 9: row r (target), column c (source) of the row-major accumulator
+    const int r = (int)threadIdx.x / 3, c = (int)threadIdx.x % 3;
+    float dm = 0.f, sm = 0.f, acc = 0.f;
+    if (threadIdx.x < 9) {
+        dm = out[3 + r] * one_over_n;
+        sm = out[c] * one_over_n;
+    }
+    for (uint32_t base = 0; base < n; base += kPclThreads) {
+        const uint32_t cnt = min((uint32_t)kPclThreads, n - base);
+        for (uint32_t e = threadIdx.x; e < 6 * cnt; e += kPclThreads) {  // coalesced: pair-major in memory
+            const uint32_t k = e / 6, d = e % 6;
+            s[d][k] = pairs[6 * (size_t)base + e];
+        }
+        __syncthreads();
+        if (threadIdx.x < 9) {
+            const float* dst = s[3 + r];
+            const float* src = s[c];
+            uint32_t k = 0;
+            for (; k + 8 <= cnt; k += 8) {
+                float pr[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const float dv = dst[k + u] - dm, sv = src[k + u] - sm;
+                    pr[u] = dv * sv;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) acc += pr[u];
+            }
+            for (; k < cnt; ++k) {
+                const float dv = dst[k] - dm, sv = src[k] - sm;
+                acc += dv * sv;
+            }
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x < 9) out[7 + threadIdx.x] = acc;
+}
+
+void launch_icp_pcl_stats(const IcpArgs& a, float* pairs, float* out16, hipStream_t st) {
+    icp_pcl_means_kernel<<<1, kPclThreads, 0, st>>>(a, pairs, out16);
+    icp_pcl_sigma_kernel<<<1, kPclThreads, 0, st>>>(pairs, out16);
+}
+
+__global__ void __launch_bounds__(64) icp_combine_kernel(const double* __restrict__ recv, int64_t nsup, int world,
+                                                        int64_t slot, double* __restrict__ out17) {
+    const int k = threadIdx.x;
+    if (k >= 17) return;
+    double acc = 0.0;
+    for (int r = 0; r < world; ++r) {
+        const int64_t s0 = nsup * r / world, s1 = nsup * (r + 1) / world;
+        for (int64_t s = s0; s < s1; ++s) acc += recv[((size_t)r * slot + (size_t)(s - s0)) * kIcpStride + k];
+    }
+    out17[k] = acc;
+}
+
+void launch_icp_combine(const double* recv, int64_t nsup, int world, int64_t slot, double* out17, hipStream_t st) {
+    icp_combine_kernel<<<1, 64, 0, st>>>(recv, nsup, world, slot, out17);
+}
+
 void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st) {
     if (a.n == 0) return;
     icp_stats_kernel<<<(a.n + kIcpSuper - 1) / kIcpSuper, kIcpStatsThreads, 0, st>>>(a, super);

@@ -9,9 +9,12 @@
 // ICP iteration each rank publishes its records' Umeyama statistics and the
 // group all-gathers them:
 //   * RCCL (default when the devices are distinct): one communicator per
-//     device from ncclCommInitAll, ncclAllGather of the records over xGMI on a
-//     per-rank stream (librccl is opened at group creation, not linked: the
-//     library loads without it and reuses a copy already in the process);
+//     device from ncclCommInitAll; each handle's statistics kernel writes its
+//     records into a device buffer, ncclAllGather moves them over xGMI on the
+//     handle's own stream and a one-block kernel sums them in record order
+//     behind it (lio_icp_set_shard_device: no host copies, one host wait per
+//     pass).  librccl is opened at group creation, not linked: the library
+//     loads without it and reuses a copy already in the process;
 //   * host (LIO_ICP_EXCHANGE=host, or several ranks on one device): the
 //     ranks' threads swap the records through shared memory behind a barrier.
 // Every rank then sums all records in record order (lio_icp_combine), so every
@@ -82,10 +85,6 @@ struct lio_icp_group;
 struct IcpRank {
     lio_icp_group* g = nullptr;
     int rank = 0;
-    hipStream_t st = nullptr;
-    double* d_send = nullptr;
-    double* d_recv = nullptr;
-    int64_t cap = 0;
 };
 
 struct lio_icp_group {
@@ -141,41 +140,28 @@ void fail_group(lio_icp_group* g) {
     g->cv.notify_all();
 }
 
-// lio_allgather_fn of rank r: `n` doubles from every rank, rank order
+// host exchange (LIO_ICP_EXCHANGE=host, or ranks sharing a device): lio_allgather_fn of rank r,
+// `n` doubles from every rank in rank order, through shared host memory behind a barrier
 int group_allgather(const double* send, int64_t n, double* recv, void* user) {
     IcpRank* r = static_cast<IcpRank*>(user);
     lio_icp_group* g = r->g;
-    if (!g->use_rccl) {
-        g->slots[r->rank] = send;
-        if (!host_barrier(g)) return -1;  // every rank's send is published
-        for (int k = 0; k < g->world; ++k) std::memcpy(recv + (size_t)k * n, g->slots[k], (size_t)n * sizeof(double));
-        return host_barrier(g) ? 0 : -1;  // every rank has copied before the sends change
-    }
-    if (hipSetDevice(g->dev[r->rank]) != hipSuccess) return -1;
-    if (n > r->cap) {
-        if (r->d_send) (void)hipFree(r->d_send);
-        if (r->d_recv) (void)hipFree(r->d_recv);
-        r->d_send = r->d_recv = nullptr;
-        r->cap = 0;
-        if (hipMalloc(&r->d_send, (size_t)n * sizeof(double)) != hipSuccess ||
-            hipMalloc(&r->d_recv, (size_t)n * g->world * sizeof(double)) != hipSuccess)
-            return -1;
-        r->cap = n;
-    }
-    if (hipMemcpyAsync(r->d_send, send, (size_t)n * sizeof(double), hipMemcpyHostToDevice, r->st) != hipSuccess)
-        return -1;
-    {
-        // the enqueue (asynchronous: the wait is the stream sync below) runs under the lock that
-        // fail_group aborts under, so it never touches a communicator an abort has freed
-        std::lock_guard<std::mutex> lk(g->mu);
-        if (g->failed || g->comms.empty()) return -1;  // another rank failed: its abort freed the comms
-        if (g->rccl.AllGather(r->d_send, r->d_recv, (size_t)n, kNcclDouble, g->comms[r->rank], r->st) != 0)
-            return -1;
-    }
-    if (hipMemcpyAsync(recv, r->d_recv, (size_t)n * g->world * sizeof(double), hipMemcpyDeviceToHost, r->st) !=
-        hipSuccess)
-        return -1;
-    return hipStreamSynchronize(r->st) == hipSuccess ? 0 : -1;
+    g->slots[r->rank] = send;
+    if (!host_barrier(g)) return -1;  // every rank's send is published
+    for (int k = 0; k < g->world; ++k) std::memcpy(recv + (size_t)k * n, g->slots[k], (size_t)n * sizeof(double));
+    return host_barrier(g) ? 0 : -1;  // every rank has copied before the sends change
+}
+
+// RCCL exchange: lio_allgather_dev_fn of rank r — the handle's device send buffer all-gathered into its
+// device recv buffer on the handle's own stream (enqueued only; the handle sums the records behind it
+// and waits once per pass).  The enqueue runs under the lock fail_group aborts under, so it never
+// touches a communicator an abort has freed.
+int group_allgather_dev(const double* d_send, int64_t n, double* d_recv, void* stream, void* user) {
+    IcpRank* r = static_cast<IcpRank*>(user);
+    lio_icp_group* g = r->g;
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (g->failed || g->comms.empty()) return -1;  // another rank failed: its abort freed the comms
+    return g->rccl.AllGather(d_send, d_recv, (size_t)n, kNcclDouble, g->comms[r->rank], (hipStream_t)stream) == 0 ? 0
+                                                                                                                 : -1;
 }
 
 }  // namespace
@@ -208,11 +194,9 @@ int lio_icp_group_create(const lio_icp_params* p, int n_gpus, const int* devices
         rc = lio_icp_create(&pr, &g->h[r]);
         g->rk[r].g = g;
         g->rk[r].rank = r;
-        if (rc == LIO_OK && n_gpus > 1) rc = lio_icp_set_shard(g->h[r], r, n_gpus, group_allgather, &g->rk[r]);
-        if (rc == LIO_OK && g->use_rccl &&
-            (hipSetDevice(g->dev[r]) != hipSuccess ||
-             hipStreamCreateWithFlags(&g->rk[r].st, hipStreamNonBlocking) != hipSuccess))
-            rc = gfail(LIO_ERR_HIP, "lio_icp_group_create: stream creation failed");
+        if (rc == LIO_OK && n_gpus > 1)
+            rc = g->use_rccl ? lio_icp_set_shard_device(g->h[r], r, n_gpus, group_allgather_dev, &g->rk[r])
+                             : lio_icp_set_shard(g->h[r], r, n_gpus, group_allgather, &g->rk[r]);
     }
     if (rc == LIO_OK && g->use_rccl) {
         std::string why;
@@ -237,16 +221,9 @@ int lio_icp_group_create(const lio_icp_params* p, int n_gpus, const int* devices
 
 int lio_icp_group_destroy(lio_icp_group* g) {
     if (!g) return LIO_OK;
+    for (lio_icp* h : g->h) lio_icp_destroy(h);  // drains each handle's stream first
     for (ncclComm_t c : g->comms)
         if (c) (void)g->rccl.CommDestroy(c);
-    for (size_t r = 0; r < g->rk.size(); ++r) {
-        IcpRank& k = g->rk[r];
-        if (k.st || k.d_send || k.d_recv) (void)hipSetDevice(g->dev[r]);
-        if (k.d_send) (void)hipFree(k.d_send);
-        if (k.d_recv) (void)hipFree(k.d_recv);
-        if (k.st) (void)hipStreamDestroy(k.st);
-    }
-    for (lio_icp* h : g->h) lio_icp_destroy(h);
     delete g;  // librccl stays loaded (other users in the process may share it)
     return LIO_OK;
 }

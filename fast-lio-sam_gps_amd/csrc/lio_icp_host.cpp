@@ -123,6 +123,142 @@ void umeyama(const double* st, const double c0[3], float Ti[16]) {
     Ti[15] = 1.f;
 }
 
+// ---- PCL-order fidelity mode (lio_icp_params.umeyama_float): the host half of pcl::umeyama(src, dst,
+// false) in float [U] (Eigen 3.3 Umeyama.h / JacobiSVD.h / Jacobi.h as PCL 1.10 instantiates them for
+// Scalar = float, no FMA).  The GPU returns the sequential float sums (means) and the sequential
+// sigma accumulator (lio_icp.hip icp_pcl_*); here: sigma = one_over_n * acc, the two-sided Jacobi SVD
+// of the 3x3, R = U S V^T (S(2) = -1 when det U det V < 0), t = dst_mean - R src_mean.
+struct Rot2 {
+    float c, s;
+};
+
+// JacobiRotation::makeJacobi(x, y, z) for real scalars
+Rot2 make_jacobi_f(float x, float y, float z) {
+    const float deno = 2.f * std::fabs(y);
+    if (deno < FLT_MIN) return {1.f, 0.f};
+    const float tau = (x - z) / deno;
+    const float w = std::sqrt(tau * tau + 1.f);
+    const float t = tau > 0.f ? 1.f / (tau + w) : 1.f / (tau - w);
+    const float sign_t = t > 0.f ? 1.f : -1.f;
+    const float n = 1.f / std::sqrt(t * t + 1.f);
+    return {n, ((-sign_t) * (y / std::fabs(y))) * std::fabs(t) * n};
+}
+
+// apply_rotation_in_the_plane(x, y, j) over 3 elements with stride `inc` (a no-op for the identity)
+void plane_rot(float* x, float* y, int inc, Rot2 j) {
+    if (j.c == 1.f && j.s == 0.f) return;
+    for (int i = 0; i < 3; ++i) {
+        const float xi = x[i * inc], yi = y[i * inc];
+        x[i * inc] = j.c * xi + j.s * yi;
+        y[i * inc] = -j.s * xi + j.c * yi;
+    }
+}
+
+// JacobiSVD<Matrix3f>(A, ComputeFullU | ComputeFullV), column-major storage M[3 * col + row]
+void jacobi_svd3_f(const float* A, float* U, float* V, float* sv) {
+    float scale = 0.f;
+    for (int i = 0; i < 9; ++i) scale = std::max(scale, std::fabs(A[i]));
+    if (scale == 0.f) scale = 1.f;
+    float W[9];
+    for (int i = 0; i < 9; ++i) {
+        W[i] = A[i] / scale;
+        U[i] = V[i] = (i % 4 == 0) ? 1.f : 0.f;
+    }
+    auto at = [&](int r, int c) -> float& { return W[3 * c + r]; };
+    const float precision = 2.f * FLT_EPSILON;
+    float max_diag = std::max(std::max(std::fabs(at(0, 0)), std::fabs(at(1, 1))), std::fabs(at(2, 2)));
+    for (bool finished = false; !finished;) {
+        finished = true;
+        for (int p = 1; p < 3; ++p)
+            for (int q = 0; q < p; ++q) {
+                const float thr = std::max(FLT_MIN, precision * max_diag);
+                if (!(std::fabs(at(p, q)) > thr || std::fabs(at(q, p)) > thr)) continue;
+                finished = false;
+                // real_2x2_jacobi_svd: rot1 makes the 2x2 block symmetric, then makeJacobi on it
+                float m00 = at(p, p), m01 = at(p, q), m10 = at(q, p), m11 = at(q, q);
+                Rot2 rot1{1.f, 0.f};
+                const float t = m00 + m11, d = m10 - m01;
+                if (!(std::fabs(d) < FLT_MIN)) {
+                    const float u = t / d;
+                    const float tmp = std::sqrt(1.f + u * u);
+                    rot1 = {u / tmp, 1.f / tmp};
+                }
+                if (!(rot1.c == 1.f && rot1.s == 0.f)) {  // m.applyOnTheLeft(0, 1, rot1)
+                    const float a0 = m00, b0 = m10, a1 = m01, b1 = m11;
+                    m00 = rot1.c * a0 + rot1.s * b0;
+                    m10 = -rot1.s * a0 + rot1.c * b0;
+                    m01 = rot1.c * a1 + rot1.s * b1;
+                    m11 = -rot1.s * a1 + rot1.c * b1;
+                }
+                const Rot2 jr = make_jacobi_f(m00, m01, m11);
+                const Rot2 jrt{jr.c, -jr.s};
+                const Rot2 jl{rot1.c * jrt.c - rot1.s * jrt.s, rot1.c * jrt.s + rot1.s * jrt.c};  // rot1 * j_right^T
+                plane_rot(W + p, W + q, 3, jl);            // W.applyOnTheLeft(p, q, j_left): rows
+                plane_rot(U + 3 * p, U + 3 * q, 1, {jl.c, -jl.s});  // U.applyOnTheRight(p, q, j_left^T): columns
+                plane_rot(W + 3 * p, W + 3 * q, 1, {jr.c, -jr.s});  // W.applyOnTheRight(p, q, j_right)
+                plane_rot(V + 3 * p, V + 3 * q, 1, {jr.c, -jr.s});  // V.applyOnTheRight(p, q, j_right)
+                max_diag = std::max(max_diag, std::max(std::fabs(at(p, p)), std::fabs(at(q, q))));
+            }
+    }
+    for (int i = 0; i < 3; ++i) {
+        const float a = at(i, i);
+        sv[i] = std::fabs(a);
+        if (a < 0.f)
+            for (int r = 0; r < 3; ++r) U[3 * i + r] = -U[3 * i + r];
+    }
+    for (int i = 0; i < 3; ++i) sv[i] *= scale;
+    for (int i = 0; i < 3; ++i) {  // descending; maxCoeff keeps the first maximum
+        int pos = i;
+        for (int k = i + 1; k < 3; ++k)
+            if (sv[k] > sv[pos]) pos = k;
+        if (sv[pos] == 0.f) break;
+        if (pos != i) {
+            std::swap(sv[i], sv[pos]);
+            for (int r = 0; r < 3; ++r) {
+                std::swap(U[3 * i + r], U[3 * pos + r]);
+                std::swap(V[3 * i + r], V[3 * pos + r]);
+            }
+        }
+    }
+}
+
+float det3_f(const float* M) {  // column-major; Eigen determinant_impl<3>
+    auto m = [&](int r, int c) { return M[3 * c + r]; };
+    auto h = [&](int a, int b, int c) { return m(a, 0) * (m(b, 1) * m(c, 2) - m(b, 2) * m(c, 1)); };
+    return h(0, 1, 2) - h(1, 0, 2) + h(2, 0, 1);
+}
+
+// out16 from launch_icp_pcl_stats -> the incremental transform (row-major 4x4 float)
+void umeyama_pcl_float(const float* out16, float Ti[16]) {
+    const uint32_t n = [&] {
+        uint32_t u;
+        std::memcpy(&u, out16 + 6, sizeof(u));
+        return u;
+    }();
+    const float one_over_n = 1.f / (float)n;
+    float sm[3], dm[3];
+    for (int d = 0; d < 3; ++d) {
+        sm[d] = out16[d] * one_over_n;
+        dm[d] = out16[3 + d] * one_over_n;
+    }
+    float sigma[9];  // column-major
+    for (int r = 0; r < 3; ++r)
+        for (int c = 0; c < 3; ++c) sigma[3 * c + r] = one_over_n * out16[7 + 3 * r + c];
+    float U[9], V[9], sv[3];
+    jacobi_svd3_f(sigma, U, V, sv);
+    const float S2 = det3_f(U) * det3_f(V) < 0.f ? -1.f : 1.f;
+    std::memset(Ti, 0, 16 * sizeof(float));
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) {  // (U S) V^T, each entry e0 + (e1 + e2)
+            const float e0 = U[r] * V[c], e1 = U[3 + r] * V[3 + c], e2 = (U[6 + r] * S2) * V[6 + c];
+            Ti[4 * r + c] = e0 + (e1 + e2);
+        }
+    }
+    for (int r = 0; r < 3; ++r)
+        Ti[4 * r + 3] = dm[r] - (Ti[4 * r] * sm[0] + (Ti[4 * r + 1] * sm[1] + Ti[4 * r + 2] * sm[2]));
+    Ti[15] = 1.f;
+}
+
 struct EvPair {
     hipEvent_t a = nullptr, b = nullptr;
     hipEvent_t m = nullptr;     // between the correspondence and statistics kernels
@@ -144,6 +280,14 @@ struct lio_icp {
     int rank = 0, world = 1;
     lio_allgather_fn fn = nullptr;
     void* user = nullptr;
+    lio_allgather_dev_fn fn_dev = nullptr;  // device-side exchange (lio_icp_set_shard_device)
+    void* user_dev = nullptr;
+    double* d_xsend = nullptr;  // exchange buffers: this rank's records / all ranks' (device)
+    double* d_xrecv = nullptr;
+    int64_t x_len = 0;          // doubles per rank they hold
+    bool x_ext = false;         // caller-owned (lio_icp_set_exchange_buffers)
+    double* h_out17 = nullptr;  // host-mapped record-order sums (device exchange)
+    double* h_out17_dev = nullptr;
     // shard buffers
     int64_t sh_begin = 0, sh_n = 0, cap = 0;
     float* d_src = nullptr;
@@ -167,6 +311,10 @@ struct lio_icp {
     double* h_super_dev = nullptr;  // device view of h_super (the statistics kernel writes it, zero-copy)
     int64_t super_cap = 0;
     bool src_dirty = true;
+    float* d_pairs = nullptr;  // umeyama_float: compacted correspondence pairs (cap * 6)
+    int64_t pairs_cap = 0;
+    float* d_pcl16 = nullptr;  // umeyama_float: the serial float sums (launch_icp_pcl_stats)
+    float* h_pcl16 = nullptr;  // pinned copy
     bool timing = false;
     lio_kernel_timing tm{};
     EvPair ev;
@@ -219,10 +367,17 @@ int lio_icp_destroy(lio_icp* h) {
     (void)hipStreamSynchronize(h->st);
     lio::grid_free(h->tgt);
     lio::grid_free(h->qgrid);
-    void* ptrs[] = {h->d_tgt, h->d_src, h->d_cur, h->d_fd2, h->d_fid, h->d_tiles, h->d_tscratch, h->d_ttmp, h->d_dbg, h->d_tcost, h->d_order};
+    void* ptrs[] = {h->d_tgt,   h->d_src,     h->d_cur,  h->d_fd2,   h->d_fid,   h->d_tiles, h->d_tscratch,
+                    h->d_ttmp,  h->d_dbg,     h->d_tcost, h->d_order, h->d_pairs, h->d_pcl16};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (h->h_super) (void)hipHostFree(h->h_super);
+    if (h->h_pcl16) (void)hipHostFree(h->h_pcl16);
+    if (h->h_out17) (void)hipHostFree(h->h_out17);
+    if (!h->x_ext) {
+        if (h->d_xsend) (void)hipFree(h->d_xsend);
+        if (h->d_xrecv) (void)hipFree(h->d_xrecv);
+    }
     if (h->ev.a) (void)hipEventDestroy(h->ev.a);
     if (h->ev.b) (void)hipEventDestroy(h->ev.b);
     if (h->ev.m) (void)hipEventDestroy(h->ev.m);
@@ -264,7 +419,71 @@ int lio_icp_set_shard(lio_icp* h, int rank, int world, lio_allgather_fn fn, void
     h->world = world;
     h->fn = fn;
     h->user = user;
+    h->fn_dev = nullptr;
+    h->user_dev = nullptr;
     h->src_dirty = true;
+    return LIO_OK;
+}
+
+int lio_icp_set_shard_device(lio_icp* h, int rank, int world, lio_allgather_dev_fn fn, void* user) {
+    if (!h || world < 1 || rank < 0 || rank >= world || (world > 1 && !fn))
+        return ifail(LIO_ERR_ARG, "lio_icp_set_shard_device: bad arguments");
+    h->rank = rank;
+    h->world = world;
+    h->fn = nullptr;
+    h->user = nullptr;
+    h->fn_dev = fn;
+    h->user_dev = user;
+    h->src_dirty = true;
+    return LIO_OK;
+}
+
+static int64_t exchange_len(int64_t ns, int world) {
+    const int64_t nsup = (ns + lio::kIcpSuper - 1) / lio::kIcpSuper;
+    return ((nsup + world - 1) / world) * lio::kIcpStride;
+}
+
+int lio_icp_exchange_len(int64_t n_source, int world, int64_t* n_per_rank) {
+    if (n_source < 0 || world < 1 || !n_per_rank) return ifail(LIO_ERR_ARG, "lio_icp_exchange_len: bad arguments");
+    *n_per_rank = std::max<int64_t>(exchange_len(n_source, world), lio::kIcpStride);
+    return LIO_OK;
+}
+
+int lio_icp_set_exchange_buffers(lio_icp* h, double* d_send, double* d_recv, int64_t n_per_rank) {
+    if (!h || !d_send || !d_recv || n_per_rank <= 0) return ifail(LIO_ERR_ARG, "lio_icp_set_exchange_buffers: bad arguments");
+    IHIP(hipSetDevice(h->dev));
+    if (!h->x_ext) {
+        if (h->d_xsend) IHIP(hipFree(h->d_xsend));
+        if (h->d_xrecv) IHIP(hipFree(h->d_xrecv));
+    }
+    h->d_xsend = d_send;
+    h->d_xrecv = d_recv;
+    h->x_len = n_per_rank;
+    h->x_ext = true;
+    return LIO_OK;
+}
+
+// device exchange buffers for the current source (the handle's own unless the caller's are large enough)
+static int exchange_reserve(lio_icp* h) {
+    const int64_t need = std::max<int64_t>(exchange_len(h->ns, h->world), lio::kIcpStride);
+    if (h->x_ext) {
+        if (h->x_len < need)
+            return ifail(LIO_ERR_ARG, "lio_icp_align: caller exchange buffers too small (lio_icp_exchange_len)");
+        return LIO_OK;
+    }
+    if (h->x_len < need || !h->d_xsend || !h->d_xrecv) {
+        if (h->d_xsend) IHIP(hipFree(h->d_xsend));
+        if (h->d_xrecv) IHIP(hipFree(h->d_xrecv));
+        h->d_xsend = h->d_xrecv = nullptr;
+        h->x_len = 0;
+        IHIP(hipMalloc(&h->d_xsend, (size_t)need * sizeof(double)));
+        IHIP(hipMalloc(&h->d_xrecv, (size_t)need * h->world * sizeof(double)));
+        h->x_len = need;
+    }
+    if (!h->h_out17) {
+        IHIP(hipHostMalloc(&h->h_out17, 32 * sizeof(double), hipHostMallocMapped));
+        IHIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->h_out17_dev), h->h_out17, 0));
+    }
     return LIO_OK;
 }
 
@@ -324,7 +543,8 @@ static int icp_prepare(lio_icp* h) {
 }
 
 // One correspondence (or fitness) pass: GPU kernels + exchange + ordered sum.
-static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, double max_d2, double out17[17]) {
+static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, double max_d2, double out17[17],
+                    float* pcl16 = nullptr) {
     lio::IcpArgs a{};
     a.grid = lio::grid_view(h->tgt);
     a.tgt_by_id = h->tgt.by_id;
@@ -353,12 +573,30 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     }
 #endif
     const int nsup_loc = (int)((h->sh_n + lio::kIcpSuper - 1) / lio::kIcpSuper);
-    if (h->sh_n > 0) {
+    const bool dev_x = h->world > 1 && h->fn_dev;  // device-side exchange: records stay on the device
+    if (dev_x) {
+        const int rc = exchange_reserve(h);
+        if (rc) return rc;
+    }
+    if (h->sh_n > 0 || dev_x) {
         if (h->timing) IHIP(hipEventRecord(h->ev.a, h->st));
-        lio::launch_icp_tiles(a, h->ntiles, h->st);
+        if (h->sh_n > 0) lio::launch_icp_tiles(a, h->ntiles, h->st);
         if (h->timing) IHIP(hipEventRecord(h->ev.m, h->st));
-        lio::launch_icp_stats(a, h->h_super_dev, h->st);  // records straight to host memory
+        if (dev_x) {  // records -> device send buffer -> in-stream all-gather -> record-order sum
+            if (h->sh_n > 0) lio::launch_icp_stats(a, h->d_xsend, h->st);
+            IHIP(hipGetLastError());
+            if (h->fn_dev(h->d_xsend, h->x_len, h->d_xrecv, (void*)h->st, h->user_dev) != 0)
+                return ifail(LIO_ERR_STATE, "device all-gather callback failed");
+            const int64_t nsup = (h->ns + lio::kIcpSuper - 1) / lio::kIcpSuper;
+            lio::launch_icp_combine(h->d_xrecv, nsup, h->world, h->x_len / lio::kIcpStride, h->h_out17_dev, h->st);
+        } else {
+            lio::launch_icp_stats(a, h->h_super_dev, h->st);  // records straight to host memory
+        }
         if (h->timing) IHIP(hipEventRecord(h->ev.b, h->st));
+        if (pcl16) {  // PCL-order fidelity mode: the serial float sums of this pass's correspondences
+            lio::launch_icp_pcl_stats(a, h->d_pairs, h->d_pcl16, h->st);
+            IHIP(hipMemcpyAsync(h->h_pcl16, h->d_pcl16, 16 * sizeof(float), hipMemcpyDeviceToHost, h->st));
+        }
         IHIP(hipGetLastError());
         IHIP(hipEventRecord(h->ev.done, h->st));
         // longest-first order for the next pass of this alignment: behind the records, so it runs
@@ -391,6 +629,11 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
             h->tm.icp_nn_ms += ms;
             ++h->tm.icp_nn_launches;
         }
+    }
+    if (pcl16) std::memcpy(pcl16, h->h_pcl16, 16 * sizeof(float));
+    if (dev_x) {  // the record-order sums of every rank's records, computed on the device
+        std::memcpy(out17, h->h_out17, 17 * sizeof(double));
+        return LIO_OK;
     }
     for (int k = 0; k < 17; ++k) out17[k] = 0.0;
     if (h->world == 1) {
@@ -434,8 +677,22 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
     if (!h || !out) return ifail(LIO_ERR_ARG, "lio_icp_align: bad arguments");
     if (h->nt == 0) return ifail(LIO_ERR_STATE, "lio_icp_align: no target");
     IHIP(hipSetDevice(h->dev));
+    const bool pcl_float = h->p.umeyama_float != 0;
+    if (pcl_float && h->world > 1)
+        return ifail(LIO_ERR_ARG, "lio_icp_align: umeyama_float (PCL-order float sums) runs on one rank only");
     int rc = icp_prepare(h);
     if (rc) return rc;
+    if (pcl_float) {
+        if (h->sh_n > h->pairs_cap || !h->d_pairs) {
+            if (h->d_pairs) IHIP(hipFree(h->d_pairs));
+            h->d_pairs = nullptr;
+            h->pairs_cap = 0;
+            IHIP(hipMalloc(&h->d_pairs, (size_t)std::max<int64_t>(h->sh_n, 1) * 6 * sizeof(float)));
+            h->pairs_cap = std::max<int64_t>(h->sh_n, 1);
+        }
+        if (!h->d_pcl16) IHIP(hipMalloc(&h->d_pcl16, 16 * sizeof(float)));
+        if (!h->h_pcl16) IHIP(hipHostMalloc(&h->h_pcl16, 16 * sizeof(float), hipHostMallocDefault));
+    }
     float fin[16], G[16];
     bool ident = true;
     for (int i = 0; i < 16; ++i) {
@@ -459,7 +716,8 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
     out->is_converged = 0;
     for (;;) {
         double st[17];
-        rc = icp_pass(h, false, apply, Tapply, max_d2, st);
+        float pcl16[16];
+        rc = icp_pass(h, false, apply, Tapply, max_d2, st, pcl_float ? pcl16 : nullptr);
         if (rc) return rc;
         out->last_corr = (int64_t)st[0];
         if (st[0] < 3) {
@@ -468,7 +726,10 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
             break;
         }
         float Ti[16];
-        umeyama(st, h->c0, Ti);
+        if (pcl_float)
+            umeyama_pcl_float(pcl16, Ti);
+        else
+            umeyama(st, h->c0, Ti);
         float nf[16];
         for (int r = 0; r < 4; ++r)
             for (int c = 0; c < 4; ++c) {

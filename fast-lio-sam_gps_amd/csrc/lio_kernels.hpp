@@ -59,22 +59,32 @@ struct GridGeom {
 // Device buffers owned by a grid (map or ICP target).
 //   by_id[id]   (x, y, z, alive 1/0) for every id ever inserted (ids are
 //               insertion order; deleted ids stay as tombstones)
-//   pts[j]      alive points sorted by (cell, id), w = id bits; ckeys[j] = cell
-//   start[c]    CSR offsets into pts, ncells + 1
+//   dense grids (ICP target / source binning): pts[j] sorted by (cell, id),
+//               start[c] CSR offsets (ncells + 1): a row of cells is one range
+//   gapped grids (the front-end map, `gapped`): each cell owns a block of slots
+//               [rng[c].x, lim[c]) of which [rng[c].x, rng[c].y) are live,
+//               (cell, id)-sorted; inserts fill a block's spare room or move the
+//               cell to a bigger block bump-allocated at the end of pts, deletes
+//               compact the block in place — O(points changed) per update, the
+//               whole map is re-laid only when the slot pool runs out.
 struct GridBuf {
-    float4* pts = nullptr;      // sorted by cell
-    uint32_t* ckeys = nullptr;  // cell of pts[j]
+    float4* pts = nullptr;      // points grouped by cell
+    uint32_t* ckeys = nullptr;  // dense grids: cell of pts[j]
     float4* by_id = nullptr;    // id order
     uint32_t* start = nullptr;  // ncells + 1 (+ histogram scratch)
-    int64_t n = 0, cap = 0;     // alive entries / entry capacity
+    int64_t n = 0, cap = 0;     // alive entries / entry capacity (sort scratch, dense pts)
     int64_t n_ids = 0, id_cap = 0;
     uint32_t cells_cap = 0;
     GridGeom geom{};
-    float4* pts_alt = nullptr;  // merge targets
-    uint32_t* ckeys_alt = nullptr;
-    uint32_t* flag = nullptr;  // per-entry survivor flags (+ slot n = 0)
-    uint32_t* pos = nullptr;
-    bool flags_ready = false;  // flag[] already set by the caller (grid_update skips the by_id gather)
+    // gapped (map) grids
+    bool gapped = false;
+    uint2* rng = nullptr;        // ncells: live slots of each cell
+    uint32_t* lim = nullptr;     // ncells + 1: end of each cell's block
+    uint32_t* addc = nullptr;    // ncells: per-cell insert counter (zero between updates)
+    uint8_t* dirty = nullptr;    // ncells: cell holds deleted entries this update (zero between updates)
+    uint32_t* bump = nullptr;    // device: next free slot of the pool
+    int64_t slots_cap = 0;       // pts capacity in slots
+    int64_t slots_used = 0;      // bump value after the last rebuild (host view; the pool's live share)
     // temporaries
     uint32_t* keys = nullptr;
     uint32_t* keys_alt = nullptr;
@@ -87,18 +97,32 @@ struct GridBuf {
     float* xyz = nullptr;        // staging for host input, cap*3
 };
 
-// Build grid from device xyz (n*3), ids 0..n-1.  Synchronises the stream once (AABB).
+// Build grid from device xyz (n*3), ids 0..n-1.  Synchronises the stream (AABB, pool size).
 int grid_build(GridBuf& g, const float* d_xyz, int64_t n, float cell, hipStream_t st);
 // Full rebuild over the alive ids of by_id; geometry = AABB + slack (+1-cell pad).
 int grid_rebuild(GridBuf& g, float cell, float slack, hipStream_t st);
-// Merge update after appending ids [id0, n_ids) and/or marking ids dead.
-int grid_update(GridBuf& g, int64_t id0, bool deleted, float slack, hipStream_t st);
-// Entry buffers for n entries (the live cell-sorted entries are kept).
-int grid_reserve_entries(GridBuf& g, int64_t n, hipStream_t st);
 // Grow by_id to hold n_ids ids (contents kept).
 int grid_reserve_ids(GridBuf& g, int64_t n_ids, hipStream_t st);
 void grid_free(GridBuf& g);
 GridDev grid_view(const GridBuf& g);
+
+// Gapped-grid maintenance, enqueued without host synchronisation (counts live on the device):
+//   compact the cells listed in dlist[0 .. *d_ndirty) (entries marked dead: id bits kNone), clearing
+//   their dirty flags; then insert the ids [id0, id0 + *d_nnew) of by_id: per-cell ranks by atomics,
+//   one lane per touched cell grows its block (a bigger one from the pool when full), one lane per
+//   point writes it.  flags[0] |= 1: a point outside the grid, flags[0] |= 2: the pool ran out — the
+//   caller then rebuilds (by_id is complete either way).  Scratch: n_max entries in tmp_cell /
+//   tmp_rank / tlist (n_max >= the number of new ids and of dirty cells).
+struct GridInsertScratch {
+    uint32_t* tmp_cell;  // n_max
+    uint32_t* tmp_rank;  // n_max
+    uint32_t* tlist;     // n_max: touched cells
+    uint32_t* d_ntouch;  // counter
+};
+void grid_compact_cells(GridBuf& g, const uint32_t* dlist, const uint32_t* d_ndirty, uint32_t dcap, int n_max,
+                        hipStream_t st);
+void grid_insert_ids(GridBuf& g, int64_t id0, const uint32_t* d_nnew, int n_max, GridInsertScratch s,
+                     uint32_t* flags, hipStream_t st);
 
 // ---------------------------------------------------------------------- ICP
 struct IcpArgs {
@@ -136,5 +160,11 @@ void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st);
 // tile order for the next pass: descending log2(cost) buckets (one block)
 void launch_icp_order(const uint32_t* tile_cost, int ntiles, uint32_t* order, hipStream_t st);
 void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st);  // one record per 4096 points
+// the all-gathered records (world slots of `slot` records) summed in global record order, one thread
+// per statistic (the order of lio_icp_combine: bit-identical) -> out17 (host-mapped)
+void launch_icp_combine(const double* recv, int64_t nsup, int world, int64_t slot, double* out17, hipStream_t st);
+// PCL-order fidelity mode: out16[0..5] float sums (src, tgt), [6] count bits, [7..15] sigma accumulator
+// (row-major target x source) — serial float chains (one block); pairs: n * 6 floats scratch
+void launch_icp_pcl_stats(const IcpArgs& a, float* pairs, float* out16, hipStream_t st);
 
 }  // namespace lio

@@ -5,17 +5,22 @@
 //   incremental  FAST-LIO map_incremental() [U] over a ctx's scan
 //
 // Add_Points processes its points one after another; the only coupling
-// between points is through their downsample voxel, so the GPU sorts the
-// points by voxel (stable: input order inside a voxel) and one lane replays
-// each voxel's sequence against the map points already in that voxel
-// (found through the grid).  Survivors are appended to the id-order array,
-// replaced points become tombstones, and the cell-sorted grid is merged
-// (lio_grid.hip: grid_update), never fully re-sorted.
+// between points is through their downsample voxel, so the GPU groups the
+// points by voxel (a hash table of voxel keys, a chain of input indices per
+// voxel) and one lane per voxel replays its points in input order against the
+// map points already in that voxel (found through the grid).  Survivors are
+// appended to the id-order array in input order, replaced points become
+// tombstones (by_id alive bit cleared, their grid slots compacted away) and the
+// new ids go into the gapped grid's per-cell blocks (lio_grid.hip) — every step
+// is O(points of this call), none touches the rest of the map, and an update is
+// enqueued with ONE host synchronisation at its end (the counts stay on the
+// device; launch sizes are the call's upper bounds).
 // Semantics restated in oracle/lio_oracle.cpp (DynMap, map_incremental).
 #include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstring>
+#include <vector>
 
 #include "lio_kernels.hpp"
 #include "lio_mapupd.hpp"
@@ -54,156 +59,164 @@ __device__ __forceinline__ bool in_box(const VoxBox& b, float x, float y, float 
     return b.lo[0] <= x && b.hi[0] > x && b.lo[1] <= y && b.hi[1] > y && b.lo[2] <= z && b.hi[2] > z;
 }
 
-__global__ void voxel_key_kernel(const float* __restrict__ xyz, int n, float ds, uint64_t* __restrict__ keys,
-                                 uint32_t* __restrict__ vals) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    uint64_t k = 0;
+// per-call counters (device, u32: MapUpdBuf::d_cnt)
+enum : int {
+    kCTrig = 0,    // Add_Points triggers (voxels that changed)
+    kCDead = 1,    // map points replaced (tombstones)
+    kCAdd = 2,     // points offered to the downsampled add (PointToAdd)
+    kCNoNeed = 3,  // PointNoNeedDownsample
+    kCVox = 4,     // voxels touched by the downsampled add
+    kCNew = 5,     // ids appended (survivors + no-need)
+    kCSurv = 6,    // survivors of the downsampled add
+    kCDirty = 7,   // grid cells holding tombstones
+    kCPend = 8,    // map_incremental points queued for the unbounded kNN
+    kCFlags = 9,   // 1 a point outside the grid, 2 slot pool exhausted, 4 tombstone cell list full
+    kCTouch = 10,  // grid cells receiving points
+};
+
+constexpr unsigned long long kEmptyKey = ~0ull;
+
+__device__ __forceinline__ unsigned long long voxel_key(float x, float y, float z, float ds) {
+    const float p[3] = {x, y, z};
+    unsigned long long k = 0;
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
-        const float f = floorf(xyz[3 * i + d] / ds);
+        const float f = floorf(p[d] / ds);
         const int v = (int)fminf(fmaxf(f, (float)-kVoxOff), (float)(kVoxOff - 1));
-        k = (k << kVoxBits) | (uint64_t)(uint32_t)(v + kVoxOff);
+        k = (k << kVoxBits) | (unsigned long long)(uint32_t)(v + kVoxOff);
     }
-    keys[i] = k;
-    vals[i] = (uint32_t)i;
+    return k;
 }
 
-// One wave per voxel run of the sorted keys: replay Add_Points' sequence for
-// the run's points against the alive map points in the voxel.
-//   S := map points in the box; for each new point q (input order):
-//     winner = q unless some s in S has calc_dist(s, mid) < calc_dist(q, mid)
+__device__ __forceinline__ uint32_t hash_slot(unsigned long long k, uint32_t mask) {  // splitmix64 finaliser
+    k = (k ^ (k >> 30)) * 0xbf58476d1ce4e5b9ull;
+    k = (k ^ (k >> 27)) * 0x94d049bb133111ebull;
+    return (uint32_t)(k ^ (k >> 31)) & mask;
+}
+
+// Group the points [0, cnt[kCAdd]) by downsample voxel: an open-addressing table of voxel keys
+// (linear probing, CAS), each slot the head of a chain of input indices (next[]); the point that
+// starts a chain lists the voxel.
+__global__ void vox_group_kernel(const float* __restrict__ xyz, float ds, unsigned long long* __restrict__ hkey,
+                                 int* __restrict__ hhead, uint32_t hmask, int* __restrict__ next,
+                                 uint32_t* __restrict__ vlist, uint32_t* __restrict__ cnt) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= cnt[kCAdd]) return;
+    const unsigned long long key = voxel_key(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], ds);
+    uint32_t h = hash_slot(key, hmask);
+    for (uint32_t probe = 0;; ++probe) {  // load <= 1/4: a free slot is always near
+        const unsigned long long prev = atomicCAS(&hkey[h], kEmptyKey, key);
+        if (prev == kEmptyKey || prev == key) break;
+        if (probe > hmask) return;  // unreachable for a clean table (guard)
+        h = (h + 1) & hmask;
+    }
+    const int old = atomicExch(&hhead[h], (int)i);
+    next[i] = old;
+    if (old < 0) vlist[atomicAdd(&cnt[kCVox], 1u)] = h;
+}
+
+// the cells a box [lo, hi) can touch: a point with lo <= p < hi has its (clamped) cell between the
+// cells of lo and of the largest float below hi (the build's assignment is monotone per coordinate)
+struct CellRange {
+    int x0, x1, y0, y1, z0, z1;
+};
+__device__ __forceinline__ CellRange box_cells(const GridDev& g, const VoxBox& b, int grid_n) {
+    CellRange r{0, -1, 0, -1, 0, -1};
+    if (grid_n <= 0) return r;
+    r.x0 = min(max(cell_coord(b.lo[0], g.ox, g.inv_cell), 0), g.nx - 1);
+    r.x1 = min(max(cell_coord(nextafterf(b.hi[0], -INFINITY), g.ox, g.inv_cell), 0), g.nx - 1);
+    r.y0 = min(max(cell_coord(b.lo[1], g.oy, g.inv_cell), 0), g.ny - 1);
+    r.y1 = min(max(cell_coord(nextafterf(b.hi[1], -INFINITY), g.oy, g.inv_cell), 0), g.ny - 1);
+    r.z0 = min(max(cell_coord(b.lo[2], g.oz, g.inv_cell), 0), g.nz - 1);
+    r.z1 = min(max(cell_coord(nextafterf(b.hi[2], -INFINITY), g.oz, g.inv_cell), 0), g.nz - 1);
+    return r;
+}
+
+constexpr int kChain = 16;  // chain entries a lane sorts in registers (a longer chain: selection walks)
+
+// One lane per voxel: Add_Points' sequence for the voxel's points (input order) against the alive
+// map points in its box [U] (oracle DynMap::add_points):
+//   S := map points in the box; for each new point q:
+//     winner = q unless some s in S has calc_dist(s, mid) < calc_dist(q, mid) (strict: among equal
+//              distances the first in id order);
 //     if |S| > 1 or same_point(q, winner): S := {winner}, counter++
-// The 64 lanes stride the box's cells (count + first nearest-to-centre point
-// in visit order = a min over (d, visit index)), lane 0 replays the run's few
-// new points, and the lanes stride again to write the tombstones
-// (by_id[id].w = 0 and the entry's survivor flag) of replaced map points.
-// add_flag[i] marks the new point that survives (at most one per voxel).
-__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-        const unsigned long long o = __shfl_xor(v, off, 64);
-        v = o < v ? o : v;
-    }
-    return v;
-}
-__device__ __forceinline__ int wave_sum_i32(int v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
-
-__global__ void __launch_bounds__(256) voxel_resolve_kernel(const uint64_t* __restrict__ skeys,
-                                                           const uint32_t* __restrict__ svals, int n,
-                                                           const float* __restrict__ xyz, float ds, GridDev g,
-                                                           int grid_n, float4* __restrict__ by_id,
-                                                           uint32_t* __restrict__ entry_alive,
-                                                           uint8_t* __restrict__ add_flag, int* __restrict__ trig_out,
-                                                           int* __restrict__ dead_out) {
-    const int lane = threadIdx.x & 63;
-    const int j = blockIdx.x * 4 + (threadIdx.x >> 6);  // one sorted position per wave
-    if (j >= n) return;
-    const uint64_t key = skeys[j];
-    if (j > 0 && skeys[j - 1] == key) {  // not a run head (wave-uniform)
-        if (lane == 0) trig_out[j] = dead_out[j] = 0;
-        return;
-    }
-    const int i0 = (int)svals[j];
-    const VoxBox b = vox_box(xyz[3 * i0], xyz[3 * i0 + 1], xyz[3 * i0 + 2], ds);
-    // ---- map points in the box: a point p with lo <= p < hi has its (clamped) cell
-    // between the cells of lo and of the largest float below hi — the build's
-    // cell assignment is monotone in each coordinate — so no margin is needed
-    int x0 = 0, x1 = -1, y0 = 0, y1 = -1, z0 = 0, z1 = -1;
-    if (grid_n > 0) {
-        x0 = min(max(cell_coord(b.lo[0], g.ox, g.inv_cell), 0), g.nx - 1);
-        x1 = min(max(cell_coord(nextafterf(b.hi[0], -INFINITY), g.ox, g.inv_cell), 0), g.nx - 1);
-        y0 = min(max(cell_coord(b.lo[1], g.oy, g.inv_cell), 0), g.ny - 1);
-        y1 = min(max(cell_coord(nextafterf(b.hi[1], -INFINITY), g.oy, g.inv_cell), 0), g.ny - 1);
-        z0 = min(max(cell_coord(b.lo[2], g.oz, g.inv_cell), 0), g.nz - 1);
-        z1 = min(max(cell_coord(nextafterf(b.hi[2], -INFINITY), g.oz, g.inv_cell), 0), g.nz - 1);
-    }
-    // one pass over the box's cells: count, first nearest-to-centre point in visit order (a min over
-    // (d, visit index)), and each lane keeps its own in-box entries (up to kRec) for the tombstones,
-    // so the cells are walked again only when some lane saw more (rare: a voxel holds a few points)
-    constexpr int kRec = 2;
-    int cnt_e = 0;
-    unsigned long long best = ~0ull, lbest = ~0ull;  // (float bits of d, visit index)
-    int lb_id = -1;
-    float lbx = 0.f, lby = 0.f, lbz = 0.f;
-    uint32_t rk[kRec] = {0u, 0u};
-    int rid[kRec] = {-1, -1};
-    bool ovf = false;
-    uint32_t visit = 0;
-    for (int z = z0; z <= z1; ++z)
-        for (int y = y0; y <= y1; ++y)
-            for (int x = x0; x <= x1; ++x) {
-                const uint32_t c = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
-                const uint32_t cb = g.start[c], ce = g.start[c + 1];
-                for (uint32_t k = cb + (uint32_t)lane; k < ce; k += 64) {
-                    const float4 p = g.pts[k];
-                    if (!in_box(b, p.x, p.y, p.z)) continue;
-                    const int id = __float_as_int(p.w);
-                    if (cnt_e < kRec) {
-                        rk[cnt_e == 0 ? 0 : 1] = k;
-                        rid[cnt_e == 0 ? 0 : 1] = id;
-                    } else {
-                        ovf = true;
-                    }
-                    ++cnt_e;
-                    const float t = calc_dist(p.x, p.y, p.z, b.mid[0], b.mid[1], b.mid[2]);
-                    const unsigned long long kk = ((unsigned long long)__float_as_uint(t) << 32) | (visit + (k - cb));
-                    if (kk < lbest) {
-                        lbest = kk;
-                        lb_id = id;
-                        lbx = p.x;
-                        lby = p.y;
-                        lbz = p.z;
+// then every map point of the box except a surviving map point becomes a tombstone (by_id alive
+// bit cleared, its grid slot marked (id bits kNone) for grid_compact_cells, its cell listed once),
+// and add_flag marks the new point that survives (at most one per voxel).  The table slot is reset
+// for the next call.
+__global__ void __launch_bounds__(256) vox_resolve_kernel(
+    const uint32_t* __restrict__ vlist, unsigned long long* __restrict__ hkey, int* __restrict__ hhead,
+    const int* __restrict__ next, const float* __restrict__ xyz, float ds, GridDev g, int grid_n,
+    float4* __restrict__ pts, float4* __restrict__ by_id, uint8_t* __restrict__ dirty, uint32_t* __restrict__ dlist,
+    uint32_t dcap, uint32_t* __restrict__ cnt, uint32_t* __restrict__ add_flag) {
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t triggers = 0, dead = 0;
+    const int n_pts = (int)cnt[kCAdd];  // chain entries are input indices < n_pts (guards below)
+    if (v < cnt[kCVox] && hhead[vlist[v]] >= 0) {
+        const uint32_t h = vlist[v];
+        const int head = hhead[h];
+        int idx[kChain];
+        int nc = 0, total = 0, first_i = 0x7fffffff;
+        for (int i = head; i >= 0 && i < n_pts && total < n_pts; i = next[i]) {
+            if (nc < kChain) idx[nc++] = i;
+            first_i = min(first_i, i);
+            ++total;
+        }
+        hkey[h] = kEmptyKey;  // the table is clean again for the next call
+        hhead[h] = -1;
+        for (int a = 1; a < nc; ++a) {  // ascending input order
+            const int t = idx[a];
+            int c = a - 1;
+            while (c >= 0 && idx[c] > t) {
+                idx[c + 1] = idx[c];
+                --c;
+            }
+            idx[c + 1] = t;
+        }
+        const VoxBox b = vox_box(xyz[3 * first_i], xyz[3 * first_i + 1], xyz[3 * first_i + 2], ds);
+        const CellRange cr = box_cells(g, b, grid_n);
+        // map points in the box: how many, and the nearest to the centre (lowest id among equals)
+        int cnt_e = 0;
+        unsigned long long best = ~0ull;
+        float bx = 0.f, by = 0.f, bz = 0.f;
+        for (int z = cr.z0; z <= cr.z1; ++z)
+            for (int y = cr.y0; y <= cr.y1; ++y)
+                for (int x = cr.x0; x <= cr.x1; ++x) {
+                    const uint2 r = g.rng[((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x];
+                    for (uint32_t k = r.x; k < r.y; ++k) {
+                        const float4 p = pts[k];
+                        if (!in_box(b, p.x, p.y, p.z)) continue;
+                        ++cnt_e;
+                        const float t = calc_dist(p.x, p.y, p.z, b.mid[0], b.mid[1], b.mid[2]);
+                        const unsigned long long kk =
+                            ((unsigned long long)__float_as_uint(t) << 32) | (uint32_t)__float_as_int(p.w);
+                        if (kk < best) {
+                            best = kk;
+                            bx = p.x;
+                            by = p.y;
+                            bz = p.z;
+                        }
                     }
                 }
-                visit += ce - cb;
+        const int best_id = cnt_e > 0 ? (int)(uint32_t)best : -1;
+        // replay the voxel's new points in input order
+        int surv_new = -1;
+        float sx = bx, sy = by, sz = bz, sd = cnt_e > 0 ? __uint_as_float((uint32_t)(best >> 32)) : INFINITY;
+        int prev = -1;
+        for (int e = 0; e < total; ++e) {
+            int i = 0x7fffffff;
+            if (total <= kChain) {
+                i = idx[e];
+            } else {  // the smallest index after `prev` by a walk of the chain
+                int steps = 0;
+                for (int j = head; j >= 0 && j < n_pts && steps < total; j = next[j], ++steps)
+                    if (j > prev && j < i) i = j;
+                if (i >= n_pts) break;
             }
-    const int my_cnt = cnt_e;
-    cnt_e = wave_sum_i32(cnt_e);
-    best = wave_min_u64(lbest);
-    const bool any_ovf = __any(ovf);
-    // best's entry: from the lane that holds it (visit indices are unique: exactly one lane)
-    int best_id = -1;
-    float bx = 0.f, by = 0.f, bz = 0.f, best_d = INFINITY;
-    if (cnt_e > 0) {
-        best_d = __uint_as_float((uint32_t)(best >> 32));
-        const uint64_t wm = __ballot(lbest == best);
-        const int wl = __ffsll((unsigned long long)wm) - 1;
-        best_id = __builtin_amdgcn_readlane(lb_id, wl);
-        bx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbx), wl));
-        by = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lby), wl));
-        bz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lbz), wl));
-    }
-    // ---- replay the run: the lanes load 64 of its points at a time (the run is
-    // a prefix of the chunk: keys are sorted), every lane replays them in order
-    // from the broadcast values (wave-uniform state)
-    int surv_new = -1;
-    float sx = bx, sy = by, sz = bz, sd = best_d;
-    int triggers = 0;
-    bool first = true;
-    for (int k = j;; k += 64) {
-        const int kk = k + lane;
-        const bool in = kk < n && skeys[kk] == key;
-        const int m = __popcll(__ballot(in));
-        int il = 0;
-        float lx = 0.f, ly = 0.f, lz = 0.f;
-        if (in) {
-            il = (int)svals[kk];
-            lx = xyz[3 * il];
-            ly = xyz[3 * il + 1];
-            lz = xyz[3 * il + 2];
-        }
-        for (int l = 0; l < m; ++l) {
-            const int i = __builtin_amdgcn_readlane(il, l);
-            const float qx = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lx), l));
-            const float qy = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(ly), l));
-            const float qz = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(lz), l));
+            prev = i;
+            const float qx = xyz[3 * i], qy = xyz[3 * i + 1], qz = xyz[3 * i + 2];
             const float qd = calc_dist(qx, qy, qz, b.mid[0], b.mid[1], b.mid[2]);
-            const int size_s = first ? cnt_e : 1;
+            const int size_s = e == 0 ? cnt_e : 1;
             const bool q_wins = size_s == 0 || !(sd < qd);
             if (size_s > 1 || q_wins || same_point(qx, qy, qz, sx, sy, sz)) {
                 ++triggers;
@@ -215,72 +228,79 @@ __global__ void __launch_bounds__(256) voxel_resolve_kernel(const uint64_t* __re
                     sd = qd;
                 }
             }
-            first = false;
         }
-        if (m < 64) break;
-    }
-    // ---- tombstones: every map point of the box except a surviving map point
-    int dead = 0;
-    if (cnt_e > 0 && (surv_new >= 0 || cnt_e > 1) && !any_ovf) {  // from the lanes' own records
-#pragma unroll
-        for (int r = 0; r < kRec; ++r) {
-            if (r >= my_cnt) break;
-            const int id = rid[r];
-            if (surv_new < 0 && id == best_id) continue;
-            by_id[id].w = 0.f;
-            entry_alive[rk[r]] = 0u;
-            ++dead;
-        }
-        dead = wave_sum_i32(dead);
-    } else if (cnt_e > 0 && (surv_new >= 0 || cnt_e > 1)) {
-        for (int z = z0; z <= z1; ++z)
-            for (int y = y0; y <= y1; ++y)
-                for (int x = x0; x <= x1; ++x) {
-                    const uint32_t c = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
-                    for (uint32_t k = g.start[c] + (uint32_t)lane; k < g.start[c + 1]; k += 64) {
-                        const float4 p = g.pts[k];
-                        if (!in_box(b, p.x, p.y, p.z)) continue;
-                        const int id = __float_as_int(p.w);
-                        if (surv_new < 0 && id == best_id) continue;
-                        by_id[id].w = 0.f;
-                        entry_alive[k] = 0u;
-                        ++dead;
+        if (cnt_e > 0 && (surv_new >= 0 || cnt_e > 1)) {
+            for (int z = cr.z0; z <= cr.z1; ++z)
+                for (int y = cr.y0; y <= cr.y1; ++y)
+                    for (int x = cr.x0; x <= cr.x1; ++x) {
+                        const uint32_t c = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
+                        const uint2 r = g.rng[c];
+                        bool marked = false;
+                        for (uint32_t k = r.x; k < r.y; ++k) {
+                            const float4 p = pts[k];
+                            if (!in_box(b, p.x, p.y, p.z)) continue;
+                            const int id = __float_as_int(p.w);
+                            if (surv_new < 0 && id == best_id) continue;
+                            by_id[id].w = 0.f;
+                            pts[k].w = __int_as_float(kNone);
+                            ++dead;
+                            marked = true;
+                        }
+                        if (marked) {  // list the cell once: the lane that sets its dirty byte
+                            unsigned int* wp = reinterpret_cast<unsigned int*>(dirty + (c & ~3u));
+                            const unsigned int bit = 1u << (8u * (c & 3u));
+                            if (!(atomicOr(wp, bit) & bit)) {
+                                const uint32_t slot = atomicAdd(&cnt[kCDirty], 1u);
+                                if (slot < dcap) dlist[slot] = c;
+                                else atomicOr(&cnt[kCFlags], 4u);  // list full: the caller rebuilds the grid
+                            }
+                        }
                     }
-                }
-        dead = wave_sum_i32(dead);
+        }
+        if (surv_new >= 0) add_flag[surv_new] = 1u;
     }
-    if (lane == 0) {  // per-run counts, summed by a reduction (no contended atomics)
-        if (surv_new >= 0) add_flag[surv_new] = 1;
-        trig_out[j] = triggers;
-        dead_out[j] = dead;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {  // one atomic per wave (every lane reaches here)
+        triggers += __shfl_xor(triggers, off, 64);
+        dead += __shfl_xor(dead, off, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (triggers) atomicAdd(&cnt[kCTrig], triggers);
+        if (dead) atomicAdd(&cnt[kCDead], dead);
     }
 }
 
-// append the flagged points (pos = exclusive scan of the flags) as ids id0 + pos
-__global__ void append_flagged_kernel(const float* __restrict__ xyz, const uint8_t* __restrict__ flag,
-                                      const uint32_t* __restrict__ pos, int n, int64_t id0,
-                                      float4* __restrict__ by_id) {
+// survivors (add_flag, pos = its exclusive scan) then the no-need points appended as ids id0 ..;
+// thread 0 publishes the counts
+__global__ void append_kernel(const float* __restrict__ xyz_a, const uint32_t* __restrict__ add_flag,
+                              const uint32_t* __restrict__ pos, const float* __restrict__ xyz_b, int n_max, int64_t id0,
+                              float4* __restrict__ by_id, uint32_t* __restrict__ cnt) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n || !flag[i]) return;
-    by_id[id0 + pos[i]] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], 1.f);
+    const uint32_t n_add = cnt[kCAdd], n_nn = cnt[kCNoNeed];
+    const uint32_t n_surv = pos[n_add];
+    if (i == 0) {
+        cnt[kCSurv] = n_surv;
+        cnt[kCNew] = n_surv + n_nn;
+    }
+    if (i >= n_max) return;
+    if ((uint32_t)i < n_add && add_flag[i])
+        by_id[id0 + pos[i]] = make_float4(xyz_a[3 * i], xyz_a[3 * i + 1], xyz_a[3 * i + 2], 1.f);
+    if ((uint32_t)i < n_nn) by_id[id0 + n_surv + i] = make_float4(xyz_b[3 * i], xyz_b[3 * i + 1], xyz_b[3 * i + 2], 1.f);
 }
 
-__global__ void append_all_kernel(const float* __restrict__ xyz, int n, int64_t id0, float4* __restrict__ by_id) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    by_id[id0 + i] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], 1.f);
-}
+__global__ void set_u32_kernel(uint32_t* __restrict__ p, uint32_t v) { *p = v; }
 
-__global__ void u8_to_u32_kernel(const uint8_t* __restrict__ f, int n, uint32_t* __restrict__ o) {
+// add_flag[0 .. n] = 0 (the scan's slot n included)
+__global__ void zero_u32_kernel(uint32_t* __restrict__ p, int n1) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i <= n) o[i] = i < n ? (uint32_t)f[i] : 0u;
+    if (i < n1) p[i] = 0u;
 }
 
 // Delete_Point_Boxes: alive ids inside any box (min <= x < max) -> tombstones
 __global__ void delete_boxes_kernel(float4* __restrict__ by_id, int64_t n, const float* __restrict__ boxes, int nb,
-                                    int* __restrict__ counter) {
+                                    uint32_t* __restrict__ counter) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    int hit = 0;
+    uint32_t hit = 0;
     if (i < n) {
         const float4 p = by_id[i];
         if (p.w != 0.f) {
@@ -294,12 +314,8 @@ __global__ void delete_boxes_kernel(float4* __restrict__ by_id, int64_t n, const
             }
         }
     }
-    // per-block count (summed by a reduction: no contended atomics)
-    __shared__ int s_cnt[4];
-    const unsigned long long m = __ballot(hit);
-    if ((threadIdx.x & 63) == 0) s_cnt[threadIdx.x >> 6] = __popcll(m);
-    __syncthreads();
-    if (threadIdx.x == 0) counter[blockIdx.x] = s_cnt[0] + s_cnt[1] + s_cnt[2] + s_cnt[3];
+    const uint32_t m = (uint32_t)__popcll(__ballot(hit));
+    if ((threadIdx.x & 63) == 0 && m) atomicAdd(counter, m);
 }
 
 // ---- map_incremental ---------------------------------------------------------
@@ -396,23 +412,30 @@ __global__ void __launch_bounds__(256) incr_pending_kernel(IncrArgs a) {
     }
 }
 
-// class flags for the two compactions (slot n = 0 for the scan totals)
-__global__ void incr_flags_kernel(const uint8_t* __restrict__ cls, int n, uint32_t* __restrict__ f_add,
-                                  uint32_t* __restrict__ f_nn) {
+// packed class flags for ONE scan of both compactions: low word PointToAdd, high word no-need
+// (slot n = 0: the totals); also clears the survivor flags for this call
+__global__ void incr_flags_kernel(const uint8_t* __restrict__ cls, int n, unsigned long long* __restrict__ f,
+                                  uint32_t* __restrict__ add_flag) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i > n) return;
     const uint8_t c = i < n ? cls[i] : kSkip;
-    f_add[i] = c == kToAdd;
-    f_nn[i] = c == kNoNeed;
+    f[i] = (c == kToAdd ? 1ull : 0ull) | (c == kNoNeed ? (1ull << 32) : 0ull);
+    add_flag[i] = 0u;
 }
 
 __global__ void incr_scatter_kernel(const float* __restrict__ world, const uint8_t* __restrict__ cls, int n,
-                                    const uint32_t* __restrict__ p_add, const uint32_t* __restrict__ p_nn,
-                                    float* __restrict__ o_add, float* __restrict__ o_nn) {
+                                    const unsigned long long* __restrict__ pos, float* __restrict__ o_add,
+                                    float* __restrict__ o_nn, uint32_t* __restrict__ cnt) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    if (i > n) return;
+    if (i == n) {
+        cnt[kCAdd] = (uint32_t)pos[n];
+        cnt[kCNoNeed] = (uint32_t)(pos[n] >> 32);
+        return;
+    }
     const uint8_t c = cls[i];
-    float* o = c == kToAdd ? o_add + 3 * (size_t)p_add[i] : (c == kNoNeed ? o_nn + 3 * (size_t)p_nn[i] : nullptr);
+    float* o = c == kToAdd ? o_add + 3 * (size_t)(uint32_t)pos[i]
+                           : (c == kNoNeed ? o_nn + 3 * (size_t)(uint32_t)(pos[i] >> 32) : nullptr);
     if (!o) return;
     o[0] = world[3 * i];
     o[1] = world[3 * i + 1];
@@ -438,8 +461,8 @@ int ensure_buf(T** p, int64_t& cap, int64_t need) {
     return 0;
 }
 
-// sort / scan scratch: grown geometrically (with a 1 MiB floor), so scans of varying size do not
-// re-allocate (hipFree synchronises the device) on every call that needs a little more
+// scan scratch: grown geometrically (1 MiB floor), so scans of varying size do not re-allocate
+// (hipFree synchronises the device) on every call that needs a little more
 int ensure_tmp(MapUpdBuf& u, size_t need) {
     if (need <= u.tmp_bytes && u.tmp) return 0;
     if (u.tmp) (void)hipFree(u.tmp);
@@ -453,33 +476,43 @@ int ensure_tmp(MapUpdBuf& u, size_t need) {
     return 0;
 }
 
-int ensure_pts(MapUpdBuf& u, int64_t n) {
-    if (n <= u.cap && u.keys) return 0;
+// per-point scratch for calls of up to n points (the voxel table at <= 1/4 load).  The table is
+// initialised on `st`, the map's (non-blocking) stream: a plain hipMemset runs on the null stream,
+// which a non-blocking stream does not wait for.
+int ensure_pts(MapUpdBuf& u, int64_t n, hipStream_t st) {
+    if (!u.cnt) {
+        UPD_CHK(hipMalloc(&u.cnt, 32 * sizeof(uint32_t)));
+        UPD_CHK(hipHostMalloc(&u.h_cnt, 32 * sizeof(uint32_t)));
+    }
+    if (n <= u.cap && u.world) return 0;
     const int64_t c = std::max<int64_t>(n, u.cap + u.cap / 2);
-    void* bufs[] = {u.keys, u.keys_alt, u.vals, u.vals_alt, u.flag, u.pos, u.flag2, u.pos2, u.cls, u.world,
-                    u.xyz_a, u.xyz_b, u.pending};
+    void* bufs[] = {u.f64, u.pos64, u.add_flag, u.pos, u.cls, u.world, u.xyz_a, u.xyz_b, u.pending, u.next, u.vlist,
+                    u.dlist, u.tmp_cell, u.tmp_rank, u.tlist, u.hkey, u.hhead};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
-    UPD_CHK(hipMalloc(&u.keys, c * sizeof(uint64_t)));
-    UPD_CHK(hipMalloc(&u.keys_alt, c * sizeof(uint64_t)));
-    UPD_CHK(hipMalloc(&u.vals, c * sizeof(uint32_t)));
-    UPD_CHK(hipMalloc(&u.vals_alt, c * sizeof(uint32_t)));
-    UPD_CHK(hipMalloc(&u.flag, (c + 1) * sizeof(uint32_t)));
+    UPD_CHK(hipMalloc(&u.f64, (c + 1) * sizeof(unsigned long long)));
+    UPD_CHK(hipMalloc(&u.pos64, (c + 1) * sizeof(unsigned long long)));
+    UPD_CHK(hipMalloc(&u.add_flag, (c + 1) * sizeof(uint32_t)));
     UPD_CHK(hipMalloc(&u.pos, (c + 1) * sizeof(uint32_t)));
-    UPD_CHK(hipMalloc(&u.flag2, (c + 1) * sizeof(uint32_t)));
-    UPD_CHK(hipMalloc(&u.pos2, (c + 1) * sizeof(uint32_t)));
     UPD_CHK(hipMalloc(&u.cls, c + 64));
     UPD_CHK(hipMalloc(&u.world, c * 3 * sizeof(float)));
     UPD_CHK(hipMalloc(&u.xyz_a, c * 3 * sizeof(float)));
     UPD_CHK(hipMalloc(&u.xyz_b, c * 3 * sizeof(float)));
     UPD_CHK(hipMalloc(&u.pending, c * sizeof(int)));
+    UPD_CHK(hipMalloc(&u.next, c * sizeof(int)));
+    UPD_CHK(hipMalloc(&u.vlist, c * sizeof(uint32_t)));
+    UPD_CHK(hipMalloc(&u.dlist, c * 27 * sizeof(uint32_t)));  // dirty cells: <= 27 per voxel box at any cell size
+    UPD_CHK(hipMalloc(&u.tmp_cell, c * sizeof(uint32_t)));
+    UPD_CHK(hipMalloc(&u.tmp_rank, c * sizeof(uint32_t)));
+    UPD_CHK(hipMalloc(&u.tlist, c * sizeof(uint32_t)));
+    uint32_t hc = 1024;
+    while ((int64_t)hc < 4 * c) hc <<= 1;
+    UPD_CHK(hipMalloc(&u.hkey, (size_t)hc * sizeof(unsigned long long)));
+    UPD_CHK(hipMalloc(&u.hhead, (size_t)hc * sizeof(int)));
+    UPD_CHK(hipMemsetAsync(u.hkey, 0xff, (size_t)hc * sizeof(unsigned long long), st));  // empty keys
+    UPD_CHK(hipMemsetAsync(u.hhead, 0xff, (size_t)hc * sizeof(int), st));                // empty chains (-1)
+    u.hcap = hc;
     u.cap = c;
-    return 0;
-}
-
-int ensure_small(MapUpdBuf& u) {
-    if (!u.d_small) UPD_CHK(hipMalloc(&u.d_small, 64 * sizeof(int)));
-    if (!u.h_small) UPD_CHK(hipHostMalloc(&u.h_small, 64 * sizeof(int)));
     return 0;
 }
 
@@ -492,170 +525,139 @@ int exclusive_scan(MapUpdBuf& u, const uint32_t* in, uint32_t* out, int n1, hipS
     return 0;
 }
 
-// Downsampled add of n device points (xyz): voxel sort + resolve; survivors'
-// flags in u.cls[0..n) (as u8), their count -> *n_surv (host), triggers /
-// tombstones -> counters.  Does not touch by_id beyond the tombstones.
-int resolve_downsample(GridBuf& g, MapUpdBuf& u, const float* xyz, int n, float ds, int64_t extra_ids,
-                       hipStream_t st) {
-    const int nb = (n + 255) / 256;
-    voxel_key_kernel<<<nb, 256, 0, st>>>(xyz, n, ds, u.keys, u.vals);
+int exclusive_scan64(MapUpdBuf& u, const unsigned long long* in, unsigned long long* out, int n1, hipStream_t st) {
     size_t bytes = 0;
-    UPD_CHK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, u.keys, u.keys_alt, u.vals, u.vals_alt, n, 0,
-                                               3 * kVoxBits, st));
+    UPD_CHK(hipcub::DeviceScan::ExclusiveSum(nullptr, bytes, in, out, n1, st));
     if (ensure_tmp(u, bytes)) return -5;
     bytes = u.tmp_bytes;
-    UPD_CHK(hipcub::DeviceRadixSort::SortPairs(u.tmp, bytes, u.keys, u.keys_alt, u.vals, u.vals_alt, n, 0,
-                                               3 * kVoxBits, st));
-    UPD_CHK(hipMemsetAsync(u.cls, 0, n, st));
-    // survivor flags of the cell-sorted entries, cleared by the resolve kernel for the
-    // entries it replaces (grid_update then skips its by_id gather)
-    int rc = grid_reserve_entries(g, g.n_ids + n + extra_ids, st);  // no re-allocation before grid_update
+    UPD_CHK(hipcub::DeviceScan::ExclusiveSum(u.tmp, bytes, in, out, n1, st));
+    return 0;
+}
+
+// The downsampled add of the cnt[kCAdd] points xyz[0 ..) (<= n_max) and the append of the
+// cnt[kCNoNeed] points xyz_nn, then the grid: tombstoned cells compacted, new ids inserted.  All
+// enqueued; cnt[] holds the counts once the stream reaches the end.
+int enqueue_add(GridBuf& g, MapUpdBuf& u, const float* xyz, int n_max, const float* xyz_nn, float ds, int64_t id0,
+                hipStream_t st) {
+    const int nb = (n_max + 255) / 256;
+    vox_group_kernel<<<nb, 256, 0, st>>>(xyz, ds, u.hkey, u.hhead, u.hcap - 1, u.next, u.vlist, u.cnt);
+    vox_resolve_kernel<<<nb, 256, 0, st>>>(u.vlist, u.hkey, u.hhead, u.next, xyz, ds, grid_view(g), (int)g.n, g.pts,
+                                           g.by_id, g.dirty, u.dlist, (uint32_t)(u.cap * 27), u.cnt, u.add_flag);
+    int rc = exclusive_scan(u, u.add_flag, u.pos, n_max + 1, st);
     if (rc) return rc;
-    UPD_CHK(hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(g.flag), 1, (size_t)g.n, st));
-    UPD_CHK(hipMemsetAsync(g.flag + g.n, 0, sizeof(uint32_t), st));
-    g.flags_ready = true;
-    int* trig = reinterpret_cast<int*>(u.pos2);  // n + n ints of scratch (pos2 / flag2 free here)
-    int* dead = reinterpret_cast<int*>(u.flag2);
-    voxel_resolve_kernel<<<(n + 3) / 4, 256, 0, st>>>(u.keys_alt, u.vals_alt, n, xyz, ds, grid_view(g), (int)g.n,
-                                                     g.by_id, g.flag, u.cls, trig, dead);
-    size_t rbytes = 0;
-    UPD_CHK(hipcub::DeviceReduce::Sum(nullptr, rbytes, trig, u.d_small, n, st));
-    if (ensure_tmp(u, rbytes)) return -5;
-    rbytes = u.tmp_bytes;
-    UPD_CHK(hipcub::DeviceReduce::Sum(u.tmp, rbytes, trig, u.d_small, n, st));
-    rbytes = u.tmp_bytes;
-    UPD_CHK(hipcub::DeviceReduce::Sum(u.tmp, rbytes, dead, u.d_small + 1, n, st));
+    append_kernel<<<nb, 256, 0, st>>>(xyz, u.add_flag, u.pos, xyz_nn, n_max, id0, g.by_id, u.cnt);
+    grid_compact_cells(g, u.dlist, u.cnt + kCDirty, (uint32_t)(u.cap * 27), n_max * 27, st);
+    GridInsertScratch sc{u.tmp_cell, u.tmp_rank, u.tlist, u.cnt + kCTouch};
+    grid_insert_ids(g, id0, u.cnt + kCNew, n_max, sc, u.cnt + kCFlags, st);
+    UPD_CHK(hipGetLastError());
+    return 0;
+}
+
+// the one host synchronisation of an update: counts back, the map's host view updated; a point
+// outside the grid or an exhausted slot pool -> full rebuild (by_id is complete either way)
+int finish_add(GridBuf& g, MapUpdBuf& u, int64_t id0, float slack, hipStream_t st) {
+    UPD_CHK(hipMemcpyAsync(u.h_cnt, u.cnt, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    UPD_CHK(hipStreamSynchronize(st));
+    const uint32_t* c = u.h_cnt;
+    g.n_ids = id0 + c[kCNew];
+    g.n = g.n - (int64_t)c[kCDead] + (int64_t)c[kCNew];
+    if (c[kCFlags]) return grid_rebuild(g, g.geom.cell, slack, st);
     return 0;
 }
 
 }  // namespace
 
 void mapupd_free(MapUpdBuf& u) {
-    void* bufs[] = {u.keys, u.keys_alt, u.vals, u.vals_alt, u.flag, u.pos, u.flag2, u.pos2, u.cls, u.world,
-                    u.xyz_a, u.xyz_b, u.pending, u.tmp, u.d_small, u.boxes};
+    void* bufs[] = {u.f64,  u.pos64,    u.add_flag, u.pos,   u.cls,   u.world, u.xyz_a, u.xyz_b, u.pending, u.next,
+                    u.vlist, u.dlist,   u.tmp_cell, u.tmp_rank, u.tlist, u.hkey, u.hhead, u.tmp,   u.cnt,     u.boxes};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
-    if (u.h_small) (void)hipHostFree(u.h_small);
+    if (u.h_cnt) (void)hipHostFree(u.h_cnt);
     u = MapUpdBuf{};
 }
 
-// Add_Points(xyz[0..n), downsample) for device points; out: [triggers/added, tombstones]
+// Add_Points(xyz[0..n), downsample) for device points; out: [triggers / added, tombstones]
 int map_add_device(GridBuf& g, MapUpdBuf& u, const float* d_xyz, int64_t n64, bool downsample, float ds,
                    float slack, int64_t out[2], hipStream_t st) {
     out[0] = out[1] = 0;
     if (n64 <= 0) return 0;
     if (n64 >= (int64_t)1 << 30) return -1;
     const int n = (int)n64;
-    if (ensure_pts(u, n) || ensure_small(u)) return -5;
+    if (ensure_pts(u, n, st)) return -5;
     const int64_t id0 = g.n_ids;
-    if (!downsample) {
-        int rc = grid_reserve_ids(g, id0 + n, st);
-        if (rc) return rc;
-        append_all_kernel<<<(n + 255) / 256, 256, 0, st>>>(d_xyz, n, id0, g.by_id);
-        g.n_ids = id0 + n;
-        out[0] = n;
-        return grid_update(g, id0, false, slack, st);
+    int rc = grid_reserve_ids(g, id0 + n, st);
+    if (rc) return rc;
+    UPD_CHK(hipMemsetAsync(u.cnt, 0, 16 * sizeof(uint32_t), st));
+    zero_u32_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(u.add_flag, n + 1);
+    if (downsample) {
+        set_u32_kernel<<<1, 1, 0, st>>>(u.cnt + kCAdd, (uint32_t)n);
+        rc = enqueue_add(g, u, d_xyz, n, nullptr, ds, id0, st);
+    } else {  // every point appended (as the no-need points of map_incremental)
+        set_u32_kernel<<<1, 1, 0, st>>>(u.cnt + kCNoNeed, (uint32_t)n);
+        rc = enqueue_add(g, u, nullptr, n, d_xyz, ds, id0, st);
     }
-    UPD_CHK(hipMemsetAsync(u.d_small, 0, 4 * sizeof(int), st));
-    int rc = resolve_downsample(g, u, d_xyz, n, ds, 0, st);
     if (rc) return rc;
-    u8_to_u32_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(u.cls, n, u.flag);
-    rc = exclusive_scan(u, u.flag, u.pos, n + 1, st);
-    if (rc) return rc;
-    UPD_CHK(hipMemcpyAsync(u.h_small, u.d_small, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
-    UPD_CHK(hipMemcpyAsync(u.h_small + 2, u.pos + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    UPD_CHK(hipStreamSynchronize(st));
-    const int64_t n_surv = (uint32_t)u.h_small[2];
-    out[0] = u.h_small[0];
-    out[1] = u.h_small[1];
-    rc = grid_reserve_ids(g, id0 + n_surv, st);
-    if (rc) return rc;
-    append_flagged_kernel<<<(n + 255) / 256, 256, 0, st>>>(d_xyz, u.cls, u.pos, n, id0, g.by_id);
-    g.n_ids = id0 + n_surv;
-    return grid_update(g, id0, out[1] > 0, slack, st);
+    rc = finish_add(g, u, id0, slack, st);
+    out[0] = downsample ? (int64_t)u.h_cnt[kCTrig] : n;
+    out[1] = u.h_cnt[kCDead];
+    return rc;
 }
 
 int map_delete_boxes(GridBuf& g, MapUpdBuf& u, const float* boxes, int nb, float slack, int64_t* n_deleted,
                      hipStream_t st) {
     *n_deleted = 0;
-    g.flags_ready = false;  // tombstones come from the alive bits here
     if (nb <= 0 || g.n_ids == 0) return 0;
-    if (ensure_small(u)) return -5;
+    if (ensure_pts(u, 1, st)) return -5;
     if (!u.boxes || nb > u.boxes_cap) {
         if (u.boxes) (void)hipFree(u.boxes);
         UPD_CHK(hipMalloc(&u.boxes, (size_t)nb * 6 * sizeof(float)));
         u.boxes_cap = nb;
     }
     UPD_CHK(hipMemcpyAsync(u.boxes, boxes, (size_t)nb * 6 * sizeof(float), hipMemcpyHostToDevice, st));
-    const int nblk = (int)((g.n_ids + 255) / 256);
-    if (ensure_pts(u, nblk)) return -5;
-    int* cnt = reinterpret_cast<int*>(u.flag2);
-    delete_boxes_kernel<<<nblk, 256, 0, st>>>(g.by_id, g.n_ids, u.boxes, nb, cnt);
-    size_t bytes = 0;
-    UPD_CHK(hipcub::DeviceReduce::Sum(nullptr, bytes, cnt, u.d_small, nblk, st));
-    if (ensure_tmp(u, bytes)) return -5;
-    bytes = u.tmp_bytes;
-    UPD_CHK(hipcub::DeviceReduce::Sum(u.tmp, bytes, cnt, u.d_small, nblk, st));
-    UPD_CHK(hipMemcpyAsync(u.h_small, u.d_small, sizeof(int), hipMemcpyDeviceToHost, st));
+    UPD_CHK(hipMemsetAsync(u.cnt, 0, 16 * sizeof(uint32_t), st));
+    delete_boxes_kernel<<<(int)((g.n_ids + 255) / 256), 256, 0, st>>>(g.by_id, g.n_ids, u.boxes, nb, u.cnt + kCDead);
+    UPD_CHK(hipMemcpyAsync(u.h_cnt, u.cnt, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     UPD_CHK(hipStreamSynchronize(st));
-    *n_deleted = u.h_small[0];
+    *n_deleted = u.h_cnt[kCDead];
     if (*n_deleted == 0) return 0;
-    return grid_update(g, g.n_ids, true, slack, st);
+    return grid_rebuild(g, g.geom.cell, slack, st);  // bulk deletes (the local map moved): re-lay once
 }
 
 // map_incremental(): classification (+ unbounded 5-NN for queued points), then
-// Add_Points(PointToAdd, true) and Add_Points(PointNoNeedDownsample, false)
-// with one grid merge.  out: [to_add, no_need, skipped, added_by_downsample_call]
+// Add_Points(PointToAdd, true) and Add_Points(PointNoNeedDownsample, false) with one grid update and
+// one host synchronisation.  out: [to_add, no_need, skipped, added_by_downsample_call]
 int map_incremental(GridBuf& g, MapUpdBuf& u, IncrArgs a, float ds, float slack, int64_t out[4], hipStream_t st) {
     for (int k = 0; k < 4; ++k) out[k] = 0;
     const int n = a.n;
     if (n <= 0) return 0;
-    if (ensure_pts(u, n) || ensure_small(u)) return -5;
+    if (ensure_pts(u, n, st)) return -5;
+    const int64_t id0 = g.n_ids;
+    int rc = grid_reserve_ids(g, id0 + n, st);
+    if (rc) return rc;
     a.grid = grid_view(g);
     a.map_by_id = g.by_id;
     a.map_alive = g.n;
     a.world = u.world;
     a.cls = u.cls;
     a.pending = u.pending;
-    a.pending_count = u.d_small + 8;
-    UPD_CHK(hipMemsetAsync(u.d_small, 0, 16 * sizeof(int), st));
+    a.pending_count = reinterpret_cast<int*>(u.cnt + kCPend);
+    UPD_CHK(hipMemsetAsync(u.cnt, 0, 16 * sizeof(uint32_t), st));
     const int nb = (n + 255) / 256;
     incr_classify_kernel<<<nb, 256, 0, st>>>(a);
     incr_pending_kernel<<<128, 256, 0, st>>>(a);
-    incr_flags_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(u.cls, n, u.flag, u.flag2);
-    int rc = exclusive_scan(u, u.flag, u.pos, n + 1, st);
+    incr_flags_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(u.cls, n, u.f64, u.add_flag);
+    rc = exclusive_scan64(u, u.f64, u.pos64, n + 1, st);
     if (rc) return rc;
-    rc = exclusive_scan(u, u.flag2, u.pos2, n + 1, st);
+    incr_scatter_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(u.world, u.cls, n, u.pos64, u.xyz_a, u.xyz_b, u.cnt);
+    rc = enqueue_add(g, u, u.xyz_a, n, u.xyz_b, ds, id0, st);
     if (rc) return rc;
-    incr_scatter_kernel<<<nb, 256, 0, st>>>(u.world, u.cls, n, u.pos, u.pos2, u.xyz_a, u.xyz_b);
-    UPD_CHK(hipMemcpyAsync(u.h_small + 2, u.pos + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    UPD_CHK(hipMemcpyAsync(u.h_small + 3, u.pos2 + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    UPD_CHK(hipStreamSynchronize(st));
-    const int n_add = (int)(uint32_t)u.h_small[2], n_nn = (int)(uint32_t)u.h_small[3];
-    out[0] = n_add;
-    out[1] = n_nn;
-    out[2] = n - n_add - n_nn;
-    const int64_t id0 = g.n_ids;
-    int64_t n_surv = 0, dead = 0;
-    if (n_add > 0) {
-        rc = resolve_downsample(g, u, u.xyz_a, n_add, ds, n_nn, st);  // cls reused as survivor flags
-        if (rc) return rc;
-        u8_to_u32_kernel<<<(n_add + 1 + 255) / 256, 256, 0, st>>>(u.cls, n_add, u.flag);
-        rc = exclusive_scan(u, u.flag, u.pos, n_add + 1, st);
-        if (rc) return rc;
-        UPD_CHK(hipMemcpyAsync(u.h_small, u.d_small, 2 * sizeof(int), hipMemcpyDeviceToHost, st));
-        UPD_CHK(hipMemcpyAsync(u.h_small + 2, u.pos + n_add, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        UPD_CHK(hipStreamSynchronize(st));
-        out[3] = u.h_small[0];
-        dead = u.h_small[1];
-        n_surv = (uint32_t)u.h_small[2];
-    }
-    rc = grid_reserve_ids(g, id0 + n_surv + n_nn, st);
-    if (rc) return rc;
-    if (n_surv > 0) append_flagged_kernel<<<(n_add + 255) / 256, 256, 0, st>>>(u.xyz_a, u.cls, u.pos, n_add, id0, g.by_id);
-    if (n_nn > 0) append_all_kernel<<<(n_nn + 255) / 256, 256, 0, st>>>(u.xyz_b, n_nn, id0 + n_surv, g.by_id);
-    g.n_ids = id0 + n_surv + n_nn;
-    return grid_update(g, id0, dead > 0, slack, st);
+    rc = finish_add(g, u, id0, slack, st);
+    const uint32_t* c = u.h_cnt;
+    out[0] = c[kCAdd];
+    out[1] = c[kCNoNeed];
+    out[2] = n - (int64_t)c[kCAdd] - (int64_t)c[kCNoNeed];
+    out[3] = c[kCTrig];
+    return rc;
 }
 
 namespace {

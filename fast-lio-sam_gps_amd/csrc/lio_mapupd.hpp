@@ -7,26 +7,31 @@
 
 namespace lio {
 
-// Scratch owned by a map handle.
+// Scratch owned by a map handle (sized for the largest call so far).
 struct MapUpdBuf {
-    uint64_t* keys = nullptr;  // voxel keys
-    uint64_t* keys_alt = nullptr;
-    uint32_t* vals = nullptr;
-    uint32_t* vals_alt = nullptr;
-    uint32_t* flag = nullptr;
-    uint32_t* pos = nullptr;
-    uint32_t* flag2 = nullptr;
-    uint32_t* pos2 = nullptr;
-    uint8_t* cls = nullptr;  // per point class / survivor flag
-    float* world = nullptr;  // n*3 world points (map_incremental)
-    float* xyz_a = nullptr;  // PointToAdd
-    float* xyz_b = nullptr;  // PointNoNeedDownsample
-    int* pending = nullptr;
+    unsigned long long* f64 = nullptr;    // packed class flags (map_incremental)
+    unsigned long long* pos64 = nullptr;  // their exclusive scan
+    uint32_t* add_flag = nullptr;         // survivor of the downsampled add, per offered point
+    uint32_t* pos = nullptr;              // its exclusive scan (survivor ids)
+    uint8_t* cls = nullptr;               // per point class
+    float* world = nullptr;               // n*3 world points (map_incremental)
+    float* xyz_a = nullptr;               // PointToAdd
+    float* xyz_b = nullptr;               // PointNoNeedDownsample
+    int* pending = nullptr;               // points queued for the unbounded kNN
+    int* next = nullptr;                  // voxel chains (input indices)
+    uint32_t* vlist = nullptr;            // voxels touched
+    uint32_t* dlist = nullptr;            // grid cells holding tombstones
+    uint32_t* tmp_cell = nullptr;         // grid insert scratch
+    uint32_t* tmp_rank = nullptr;
+    uint32_t* tlist = nullptr;
+    unsigned long long* hkey = nullptr;   // voxel table: keys (all ones = empty) ...
+    int* hhead = nullptr;                 // ... and chain heads (-1), clean between calls
+    uint32_t hcap = 0;
     int64_t cap = 0;
     void* tmp = nullptr;
     size_t tmp_bytes = 0;
-    int* d_small = nullptr;  // counters
-    int* h_small = nullptr;  // pinned
+    uint32_t* cnt = nullptr;    // per-call counters (lio_mapupd.hip kC*)
+    uint32_t* h_cnt = nullptr;  // pinned copy
     float* boxes = nullptr;
     int boxes_cap = 0;
 };

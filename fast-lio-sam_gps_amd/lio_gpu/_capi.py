@@ -34,8 +34,9 @@ EXPORTS = [
     "lio_pcd_write_binary", "lio_pcd_read", "lio_map_build_pcd",
     "lio_ctx_create", "lio_ctx_destroy", "lio_scan_set", "lio_scan_set_device", "lio_scan_bind_device", "lio_match",
     "lio_get_knn", "lio_get_planes", "lio_get_world", "lio_get_h_rows", "lio_ctx_knn_stats",
-    "lio_ieskf_update", "lio_ctx_set_seed_scale",
+    "lio_ieskf_update", "lio_ctx_set_seed_scale", "lio_scan_get_undistorted",
     "lio_icp_create", "lio_icp_destroy", "lio_icp_set_target", "lio_icp_set_source", "lio_icp_set_shard",
+    "lio_icp_set_shard_device", "lio_icp_exchange_len", "lio_icp_set_exchange_buffers",
     "lio_icp_align", "icp_align", "lio_icp_group_create", "lio_icp_group_destroy", "lio_icp_group_size",
     "lio_icp_group_uses_rccl", "lio_icp_group_set_target", "lio_icp_group_set_source", "lio_icp_group_align",
     "lio_icp_shard_range", "lio_icp_combine", "lio_icp_get_correspondences",
@@ -83,7 +84,7 @@ class IeskfStats(C.Structure):
 class IcpParams(C.Structure):
     _fields_ = [("max_corr_dist", C.c_double), ("trans_eps", C.c_double), ("fitness_eps", C.c_double),
                 ("max_iter", C.c_int), ("rot_eps", C.c_double), ("score_threshold", C.c_double),
-                ("cell_size", C.c_float), ("device", C.c_int)]
+                ("cell_size", C.c_float), ("device", C.c_int), ("umeyama_float", C.c_int)]
 
 
 class IcpResult(C.Structure):
@@ -124,6 +125,8 @@ class KernelTiming(C.Structure):
 
 
 ALLGATHER_FN = C.CFUNCTYPE(C.c_int, C.POINTER(C.c_double), C.c_int64, C.POINTER(C.c_double), C.c_void_p)
+# lio_allgather_dev_fn(d_send, n, d_recv, stream, user): device pointers, enqueue on `stream`
+ALLGATHER_DEV_FN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p)
 
 _lib = None
 
@@ -187,11 +190,15 @@ def _declare(L):
         "lio_ctx_knn_stats": (C.c_int, [vp, C.POINTER(Pose), dp, C.POINTER(C.c_int32)]),
         "lio_ieskf_update": (C.c_int, [vp, C.POINTER(State), dp, C.POINTER(IeskfParams), C.POINTER(IeskfStats)]),
         "lio_ctx_set_seed_scale": (C.c_int, [vp, C.c_float]),
+        "lio_scan_get_undistorted": (C.c_int, [vp, fp, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int)]),
         "lio_icp_create": (C.c_int, [C.POINTER(IcpParams), C.POINTER(vp)]),
         "lio_icp_destroy": (C.c_int, [vp]),
         "lio_icp_set_target": (C.c_int, [vp, fp, C.c_int64]),
         "lio_icp_set_source": (C.c_int, [vp, fp, C.c_int64]),
         "lio_icp_set_shard": (C.c_int, [vp, C.c_int, C.c_int, ALLGATHER_FN, vp]),
+        "lio_icp_set_shard_device": (C.c_int, [vp, C.c_int, C.c_int, ALLGATHER_DEV_FN, vp]),
+        "lio_icp_exchange_len": (C.c_int, [C.c_int64, C.c_int, C.POINTER(C.c_int64)]),
+        "lio_icp_set_exchange_buffers": (C.c_int, [vp, vp, vp, C.c_int64]),
         "lio_icp_align": (C.c_int, [vp, fp, C.POINTER(IcpResult), fp]),
         "lio_icp_get_correspondences": (C.c_int, [vp, C.POINTER(C.c_int32), fp]),
         "icp_align": (C.c_int, [fp, C.c_int64, fp, C.c_int64, C.POINTER(IcpParams), C.c_int, fp, dp,

@@ -78,3 +78,53 @@ def make_allgather(group=None, device=None):
             return -1
 
     return _capi.ALLGATHER_FN(_cb)
+
+
+def exchange_len(n_source: int, world: int) -> int:
+    """doubles per rank of the device-side exchange (lio_icp_exchange_len)"""
+    n = C.c_int64()
+    check(lib().lio_icp_exchange_len(n_source, world, C.byref(n)))
+    return n.value
+
+
+class DeviceExchange:
+    """Device-side record exchange for one rank (``lio_icp_set_shard_device``) over torch.distributed
+    with the NCCL (= RCCL) backend: the send / recv buffers are torch tensors on this rank's GPU,
+    handed to the ICP handle, and the callback runs ``all_gather_into_tensor`` on the handle's own
+    HIP stream (``torch.cuda.ExternalStream``) — the records never leave the device and the handle
+    waits once per pass for 17 sums.  Keep the object alive while the handle uses it."""
+
+    def __init__(self, group=None):
+        import torch
+        import torch.distributed as dist
+
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.device = torch.device("cuda", torch.cuda.current_device())
+        self.send = self.recv = None
+        self.n = 0
+
+        def _cb(send_p, n, recv_p, stream, user):
+            try:
+                assert send_p == self.send.data_ptr() and recv_p == self.recv.data_ptr() and n <= self.n
+                with torch.cuda.stream(torch.cuda.ExternalStream(stream, device=self.device)):
+                    dist.all_gather_into_tensor(self.recv[: n * self.world], self.send[:n], group=self.group)
+                return 0
+            except Exception:  # the C side turns a non-zero status into LIO_ERR_STATE
+                import traceback
+
+                traceback.print_exc()
+                return -1
+
+        self.fn = _capi.ALLGATHER_DEV_FN(_cb)
+
+    def attach(self, handle, n_source: int):
+        """(Re)size the buffers for a source of n_source points and hand them to the ICP handle."""
+        import torch
+
+        n = exchange_len(n_source, self.world)
+        if n > self.n:
+            self.send = torch.zeros(n, dtype=torch.float64, device=self.device)
+            self.recv = torch.zeros(n * self.world, dtype=torch.float64, device=self.device)
+            self.n = n
+        check(lib().lio_icp_set_exchange_buffers(handle, self.send.data_ptr(), self.recv.data_ptr(), self.n))

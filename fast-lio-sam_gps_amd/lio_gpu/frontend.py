@@ -280,6 +280,16 @@ class HShareModelGPU:
         self.n = int(n.value)
         return self.n
 
+    def undistorted(self) -> np.ndarray:
+        """feats_undistort of the last preprocess_scan / preprocess_cloud2: the undistorted,
+        time-sorted records (x, y, z, intensity, time, ...) before downSizeFilterSurf."""
+        n = C.c_int64(0)
+        stride = C.c_int(0)
+        check(lib().lio_scan_get_undistorted(self._h, None, 0, C.byref(n), C.byref(stride)))
+        out = np.empty((n.value, max(stride.value, 1)), np.float32)
+        check(lib().lio_scan_get_undistorted(self._h, _fp(out), n.value, C.byref(n), C.byref(stride)))
+        return out
+
     def preprocess_cloud2(self, data, n_points: int, point_step: int, fields, imu_poses, end_pose, big_endian=False,
                           point_filter_num=4, blind=2.0, filter_size_surf=0.5) -> int:
         """preprocess_scan from sensor_msgs/PointCloud2 bytes; fields = 5 (offset, datatype[, scale]) for

@@ -53,16 +53,19 @@ def _xyz(cloud) -> np.ndarray:
     return a.reshape(-1, 3) if a.ndim == 1 else a[:, :3]
 
 
-def icp_params(config: LoopClosureConfig, cell_size: float = 1.0, device: int = 0) -> _capi.IcpParams:
+def icp_params(config: LoopClosureConfig, cell_size: float = 1.0, device: int = 0,
+               umeyama_float: bool = False) -> _capi.IcpParams:
     # setTransformationEpsilon(0.01), setEuclideanFitnessEpsilon(0.01), setMaximumIterations(50)
     return _capi.IcpParams(config.icp_max_corr_dist_, 0.01, 0.01, 50, 0.0, config.icp_score_threshold_,
-                           cell_size, device)
+                           cell_size, device, 1 if umeyama_float else 0)
 
 
 class LoopClosure:
-    def __init__(self, config: LoopClosureConfig, cell_size: float = 1.0, device: int = 0):
+    def __init__(self, config: LoopClosureConfig, cell_size: float = 1.0, device: int = 0,
+                 umeyama_float: bool = False):
+        """umeyama_float: PCL-order fidelity mode (float pcl::umeyama restated; single rank)."""
         self.config_ = config
-        self._p = icp_params(config, cell_size, device)
+        self._p = icp_params(config, cell_size, device, umeyama_float)
         self._h = C.c_void_p()
         check(lib().lio_icp_create(C.byref(self._p), C.byref(self._h)))
         self.aligned_ = np.zeros((0, 3), np.float32)
@@ -70,10 +73,20 @@ class LoopClosure:
         self._cb = None
 
     def set_shard(self, rank: int, world: int, allgather=None):
-        """Shard the source over ``world`` ranks; ``allgather`` from lio_gpu.dist.make_allgather."""
+        """Shard the source over ``world`` ranks; ``allgather`` from lio_gpu.dist.make_allgather
+        (host-side exchange: the records pass through host memory)."""
         self._cb = allgather
+        self._dx = None
         fn = allgather if allgather is not None else _capi.ALLGATHER_FN()
         check(lib().lio_icp_set_shard(self._h, rank, world, fn, None))
+        self._shard = (rank, world)
+
+    def set_shard_device(self, rank: int, world: int, exchange):
+        """Shard the source over ``world`` ranks with the device-side exchange (``exchange``: a
+        lio_gpu.dist.DeviceExchange; torch.distributed NCCL = RCCL backend)."""
+        self._cb = None
+        self._dx = exchange
+        check(lib().lio_icp_set_shard_device(self._h, rank, world, exchange.fn, None))
         self._shard = (rank, world)
 
     def set_timing(self, on: bool):
@@ -92,6 +105,8 @@ class LoopClosure:
         s = np.ascontiguousarray(_xyz(src), dtype=np.float32)
         check(lib().lio_icp_set_source(self._h, s.ctypes.data_as(C.POINTER(C.c_float)), len(s)))
         self._ns = len(s)
+        if getattr(self, "_dx", None) is not None:
+            self._dx.attach(self._h, len(s))
 
     def align(self, guess: np.ndarray | None = None, keep_aligned: bool = True):
         res = _capi.IcpResult()
@@ -121,6 +136,36 @@ class LoopClosure:
         check(lib().lio_icp_get_correspondences(self._h, ids.ctypes.data_as(C.POINTER(C.c_int32)),
                                                 d2.ctypes.data_as(C.POINTER(C.c_float))))
         return ids, d2
+
+    def fetchClosestKeyframeIdx(self, front_keyframe: PosePcd, keyframes) -> int:
+        """loop_closure.cpp:18-40: among keyframes[0 .. size-2], the closest (translation of
+        pose_corrected_eig_) within loop_detection_radius_ whose timestamp is more than
+        loop_detection_timediff_threshold_ older; -1 if none."""
+        radi = self.config_.loop_detection_radius_
+        shortest = radi * 3.0
+        closest = -1
+        p = np.asarray(front_keyframe.pose_corrected_eig_, np.float64)[:3, 3]
+        for kf in keyframes[:len(keyframes) - 1]:
+            d = float(np.linalg.norm(np.asarray(kf.pose_corrected_eig_, np.float64)[:3, 3] - p))
+            if radi > d and self.config_.loop_detection_timediff_threshold_ < (front_keyframe.timestamp_ - kf.timestamp_):
+                if d < shortest:
+                    shortest = d
+                    closest = kf.idx_
+        return closest
+
+    def performLoopClosure(self, query_keyframe: PosePcd, keyframes, closest_keyframe_idx: int | None = None,
+                           submap_range: int | None = None) -> RegistrationOutput:
+        """loop_closure.cpp:95-126: submaps around the query and the closest keyframe
+        (num_submap_keyframes_, voxel_res_), then icpAlignment(src, dst)."""
+        if closest_keyframe_idx is None:
+            closest_keyframe_idx = self.fetchClosestKeyframeIdx(query_keyframe, keyframes)
+        self.closest_keyframe_idx_ = closest_keyframe_idx
+        if closest_keyframe_idx < 0:
+            return RegistrationOutput()
+        rng = self.config_.num_submap_keyframes_ if submap_range is None else submap_range
+        self.src_cloud_, self.dst_cloud_ = self.setSrcAndDstCloud(keyframes, query_keyframe.idx_, closest_keyframe_idx,
+                                                                  rng, self.config_.voxel_res_)
+        return self.icpAlignment(self.src_cloud_, self.dst_cloud_)
 
     def setSrcAndDstCloud(self, keyframes, src_idx: int, dst_idx: int, submap_range: int, voxel_res: float):
         """loop_closure.cpp:42-67 on the GPU: per side, transformPcd of keyframes

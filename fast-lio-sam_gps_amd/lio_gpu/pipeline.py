@@ -1,0 +1,142 @@
+"""The C5 stream on the GPU hot path (BASELINE.json configs[4]): FAST-LIO's per-sweep front end, the
+keyframe it hands to fast_lio_sam, and fast_lio_sam's loop leg.
+
+Per sweep (FAST-LIO laserMapping [U], the Kodifly fork's submodule is empty: SURVEY §8):
+  Preprocess + UndistortPcl + downSizeFilterSurf  -> HShareModelGPU.preprocess_scan   (GPU)
+  kf.update_iterated_dyn_share_modified           -> EsekfGPU                         (GPU + host 23-dim step)
+  map_incremental()                               -> HShareModelGPU.map_incremental   (GPU)
+  publish /Odometry + /cloud_registered (dense_publish_en: feats_undistort, kitti.yaml:31) in the world
+  frame -> fast_lio_sam's PosePcd (pose_pcd.hpp:22-42: the cloud taken back to the odometry frame with
+  pose_eig_.inverse())                            -> keyframe_from_odometry            (host glue)
+Loop leg (fast_lio_sam.cpp:682-730 loopTimerFunc -> loop_closure.cpp:18-40 fetchClosestKeyframeIdx ->
+:101-126 performLoopClosure -> :42-67 setSrcAndDstCloud -> :69-92 icpAlignment): LoopClosure (GPU
+submap assembly + ICP).
+
+Node plumbing stays out (ROS, GTSAM pose graph, keyframe-threshold bookkeeping: keyframe_threshold is
+0 in config.yaml, so every processed sweep is a keyframe here).
+"""
+from __future__ import annotations
+
+import time
+
+import numpy as np
+
+from . import frontend as F
+from . import loop_closure as LC
+from . import synth
+
+
+def quat_rotate(q, v, conj: bool = False) -> np.ndarray:
+    """Eigen 3.3 QuaternionBase::_transformVector in Eigen's operation order (float64 rows):
+    uv = q.vec x v; uv += uv; v + w uv + q.vec x uv (the restatement's quat_rotate, lio_oracle.cpp)."""
+    w = float(q[0])
+    s = -1.0 if conj else 1.0
+    x, y, z = s * float(q[1]), s * float(q[2]), s * float(q[3])
+    v0, v1, v2 = v[:, 0], v[:, 1], v[:, 2]
+    u0 = y * v2 - z * v1
+    u1 = z * v0 - x * v2
+    u2 = x * v1 - y * v0
+    u0 = u0 + u0
+    u1 = u1 + u1
+    u2 = u2 + u2
+    c0 = y * u2 - z * u1
+    c1 = z * u0 - x * u2
+    c2 = x * u1 - y * u0
+    return np.stack([(v0 + w * u0) + c0, (v1 + w * u1) + c1, (v2 + w * u2) + c2], axis=1)
+
+
+def state_world(state: dict, xyz: np.ndarray) -> np.ndarray:
+    """FAST-LIO pointBodyToWorld [U]: rot * (offset_R_L_I * p + offset_T_L_I) + pos in double, stored
+    float (the frame of /cloud_registered)."""
+    b = np.asarray(xyz, np.float32)[:, :3].astype(np.float64)
+    a = quat_rotate(state["offset_R_L_I"], b) + np.asarray(state["offset_T_L_I"], np.float64)
+    w = quat_rotate(state["rot"], a) + np.asarray(state["pos"], np.float64)
+    return w.astype(np.float32)
+
+
+def odom_matrix(state: dict) -> np.ndarray:
+    """pose_pcd.hpp:26-36: the /Odometry orientation through tf::Matrix3x3(q) (tf's setRotation:
+    s = 2 / |q|^2) and the position -> pose_eig_ (4x4 double)."""
+    w, x, y, z = (float(v) for v in state["rot"])
+    d = x * x + y * y + z * z + w * w
+    s = 2.0 / d
+    xs, ys, zs = x * s, y * s, z * s
+    wx, wy, wz = w * xs, w * ys, w * zs
+    xx, xy, xz = x * xs, x * ys, x * zs
+    yy, yz, zz = y * ys, y * zs, z * zs
+    T = np.eye(4)
+    T[:3, :3] = [[1.0 - (yy + zz), xy - wz, xz + wy], [xy + wz, 1.0 - (xx + zz), yz - wx],
+                 [xz - wy, yz + wx, 1.0 - (xx + yy)]]
+    T[:3, 3] = np.asarray(state["pos"], np.float64)
+    return T
+
+
+def transform_pcd(cloud: np.ndarray, T: np.ndarray) -> np.ndarray:
+    """utilities.hpp:132-143 transformPcd (pcl::transformPointCloud with a Matrix4d [U]): xyz through
+    ((m0 x + m1 y) + m2 z) + m3 in double, stored float; the other fields copied (the GPU's
+    transform_segs_kernel and the restatement's transformPcd use the same order)."""
+    c = np.asarray(cloud, np.float32)
+    out = c.copy()
+    p = c[:, :3].astype(np.float64)
+    m = np.asarray(T, np.float64)
+    for r in range(3):
+        out[:, r] = (((m[r, 0] * p[:, 0] + m[r, 1] * p[:, 1]) + m[r, 2] * p[:, 2]) + m[r, 3]).astype(np.float32)
+    return out
+
+
+def keyframe_from_odometry(state: dict, world_xyzi: np.ndarray, timestamp: float, idx: int) -> LC.PosePcd:
+    """PosePcd(odom, cloud, idx) (pose_pcd.hpp:22-42): pcd_ = transformPcd(cloud, pose_eig_.inverse())."""
+    T = odom_matrix(state)
+    pcd = transform_pcd(world_xyzi, np.linalg.inv(T))
+    return LC.PosePcd(pcd_=pcd, pose_corrected_eig_=T.copy(), pose_eig_=T.copy(), timestamp_=float(timestamp), idx_=idx)
+
+
+class FastLioSamStream:
+    """One sensor stream through the GPU front end plus the loop leg, keyframes kept on the host
+    (fast_lio_sam keeps them in a std::vector<PosePcd>)."""
+
+    def __init__(self, tree: F.IkdTreeGPU, config: LC.LoopClosureConfig | None = None, filter_size_map: float = 0.5,
+                 max_iteration: int = 3, point_filter_num: int = 4, blind: float = 2.0, filter_size_surf: float = 0.5,
+                 device: int = 0):
+        self.tree = tree
+        self.hm = F.HShareModelGPU(tree)
+        self.kf = F.EsekfGPU(self.hm, laser_point_cov=0.001, max_iteration=max_iteration, epsi=0.001)
+        self.config = config or LC.LoopClosureConfig()
+        self.lc = LC.LoopClosure(self.config, device=device)
+        self.fs_map = filter_size_map
+        self.prep = dict(point_filter_num=point_filter_num, blind=blind, filter_size_surf=filter_size_surf, time_field=4)
+        self.keyframes: list[LC.PosePcd] = []
+
+    def process(self, raw: np.ndarray, imu_poses, end_pose24, init_state: dict, P0: np.ndarray, timestamp: float) -> dict:
+        """One sweep: preprocess -> IESKF update -> map_incremental -> keyframe.  Returns the state and the
+        per-stage host wall times (ms)."""
+        t0 = time.perf_counter()
+        n_down = self.hm.preprocess_scan(raw, imu_poses, F.pose_from_pose24(end_pose24), **self.prep)
+        t1 = time.perf_counter()
+        x, P, st = self.kf.update_iterated_dyn_share_modified(init_state, P0)
+        t2 = time.perf_counter()
+        inc = self.hm.map_incremental(synth.pose24(x), self.fs_map)
+        t3 = time.perf_counter()
+        und = self.hm.undistorted()
+        world = np.concatenate([state_world(x, und[:, :3]), und[:, 3:4]], axis=1)
+        self.keyframes.append(keyframe_from_odometry(x, world, timestamp, len(self.keyframes)))
+        t4 = time.perf_counter()
+        return dict(state=x, P=P, stats=st, incremental=inc, n_down=n_down, n_undistorted=len(und),
+                    ms=dict(preprocess=(t1 - t0) * 1e3, update=(t2 - t1) * 1e3, map_incremental=(t3 - t2) * 1e3,
+                            keyframe=(t4 - t3) * 1e3))
+
+    def loop(self, submap_range: int | None = None):
+        """loopTimerFunc's work on the newest keyframe: (closest index, RegistrationOutput, ms)."""
+        if not self.keyframes:
+            return -1, LC.RegistrationOutput(), 0.0
+        t0 = time.perf_counter()
+        q = self.keyframes[-1]
+        idx = self.lc.fetchClosestKeyframeIdx(q, self.keyframes)
+        if idx < 0:
+            return idx, LC.RegistrationOutput(), (time.perf_counter() - t0) * 1e3
+        out = self.lc.performLoopClosure(q, self.keyframes, idx, submap_range)
+        return idx, out, (time.perf_counter() - t0) * 1e3
+
+    def close(self):
+        self.hm.close()
+        self.lc.close()

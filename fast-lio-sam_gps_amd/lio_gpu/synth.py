@@ -185,10 +185,18 @@ def _sample_surface(scene: Scene, n_points: int, seed: int, sigma: float, x_wind
         p = p[~_inside_any_box(p, scene.boxes)]
         pts.append(p.astype(np.float32))
         need -= len(p)
-    p = np.concatenate(pts)[:n_points]
-    _, first = np.unique(p, axis=0, return_index=True)
-    if len(first) != len(p):
-        p = p[np.sort(first)]
+    p = np.ascontiguousarray(np.concatenate(pts)[:n_points], dtype=np.float32)
+    # exact duplicates removed, first occurrence kept (np.unique(p, axis=0) semantics; a stable
+    # lexsort of the coordinate bits instead of the structured sort: 10 M points 21 s -> 3 s)
+    b = p.view(np.uint32).reshape(-1, 3)
+    k1 = (b[:, 0].astype(np.uint64) << np.uint64(32)) | b[:, 1].astype(np.uint64)
+    order = np.lexsort((b[:, 2], k1))
+    s1, s2 = k1[order], b[order, 2]
+    dup = (s1[1:] == s1[:-1]) & (s2[1:] == s2[:-1])
+    if dup.any():
+        keep = np.ones(len(p), bool)
+        keep[order[1:][dup]] = False
+        p = p[keep]
     return np.ascontiguousarray(p, dtype=np.float32)
 
 
@@ -493,3 +501,26 @@ def make_raw_scan(scene: Scene, n: int = 120_000, kind: str = "kitti64", seed: i
     q_e = np.array([math.cos(0.5 * yaw_e), 0.0, 0.0, math.sin(0.5 * yaw_e)])  # state rot (yaw-only)
     end24 = np.concatenate([R_e.ravel(), p_e, R_LI.ravel(), T_LI, q_e, [1.0, 0.0, 0.0, 0.0]]).astype(np.float64)
     return raw, poses, end24
+
+
+def make_loop_stream(scene: Scene, n_out: int = 4, n_points: int = 120_000, kind: str = "kitti64",
+                     x0: float | None = None):
+    """A C5-style stream with a loop: n_out raw sweeps driving out along +x, then n_out driving back
+    along -x 40 s later past the same places (fast_lio_sam's loop_detection_timediff_threshold is
+    30 s, config.yaml).  Returns [(raw, imu_poses, end24, initial_state, timestamp)]: the initial
+    state is the sweep-end IMU pose off by (0.10, -0.08, 0.05) m and (0.5, -0.4, 1.0) deg, as the
+    other configurations' scans."""
+    delta = rotvec_to_quat(np.deg2rad([0.5, -0.4, 1.0]))
+    if x0 is None:
+        x0 = -0.15 * scene.length + 0.9
+    plan = [(x0 + 3.7 * k, 0.4 * math.sin(0.5 * k), 0.04 * math.sin(0.2 * k), 0.1 * k) for k in range(n_out)]
+    plan += [(x0 + 3.7 * (n_out - 1 - j) + 1.5, -0.3 + 0.2 * math.sin(0.7 * j), math.pi + 0.03 * math.sin(0.4 * j),
+              40.0 + 0.1 * j) for j in range(n_out)]
+    out = []
+    for k, (ox, oy, yaw0, t) in enumerate(plan):
+        raw, poses, end24 = make_raw_scan(scene, n_points, kind, seed=777 + k, origin=(ox, oy, 0.0), yaw0=yaw0)
+        R_e = end24[0:9].reshape(3, 3)
+        q_e = rotvec_to_quat([0.0, 0.0, float(np.arctan2(R_e[1, 0], R_e[0, 0]))])
+        st0 = initial_state(end24[9:12] + np.array([0.10, -0.08, 0.05]), quat_mul(q_e, delta))
+        out.append((raw, poses, end24, st0, t))
+    return out

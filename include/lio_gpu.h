@@ -232,6 +232,12 @@ typedef struct lio_icp_params {
     double score_threshold; /* icp_score_threshold (config.yaml:16)                   */
     float cell_size;        /* target grid cell [m]; 0 => 1.0                        */
     int device;
+    /* 0 (default): the Umeyama statistics in double about a fixed centre (deterministic, shardable).
+     * 1: PCL-order fidelity mode — TransformationEstimationSVD<PointXYZI, PointXYZI, float>'s
+     *    pcl::umeyama restated: float means as sequential sums over the correspondences in source
+     *    order, float sigma (sequential depth sum), float JacobiSVD on the host (single rank only;
+     *    ~1.5 ms per iteration at 500 k points: serial float chains on the GPU).                 */
+    int umeyama_float;
 } lio_icp_params;
 
 typedef struct lio_icp_result {  /* RegistrationOutput (loop_closure.h:21-27) + diagnostics */
@@ -262,6 +268,17 @@ int lio_icp_set_shard(lio_icp* h, int rank, int world, lio_allgather_fn fn, void
  * ceil(records/world)*20 doubles, as lio_allgather_fn delivers them.       */
 int lio_icp_shard_range(int64_t n_source, int rank, int world, int64_t* begin, int64_t* count);
 int lio_icp_combine(const double* recv, int64_t n_source, int world, double* out17);
+/* Device-side exchange (the form to use with RCCL): per pass the statistics kernel writes this rank's
+ * records into a DEVICE send buffer, `fn` enqueues the all-gather of n doubles per rank into the
+ * device recv buffer (world * n, rank order) ordered on `stream` (RCCL in-stream, or a collective on
+ * torch.cuda.ExternalStream(stream)), the handle enqueues the record-order sum behind it and reads 17
+ * doubles back: one host wait per pass, no host copies of the records.  Buffers: the handle's own,
+ * or the caller's (lio_icp_set_exchange_buffers, e.g. tensors a collective library registered);
+ * n = lio_icp_exchange_len(n_source, world).                                                        */
+typedef int (*lio_allgather_dev_fn)(const double* d_send, int64_t n, double* d_recv, void* stream, void* user);
+int lio_icp_set_shard_device(lio_icp* h, int rank, int world, lio_allgather_dev_fn fn, void* user);
+int lio_icp_exchange_len(int64_t n_source, int world, int64_t* n_per_rank);
+int lio_icp_set_exchange_buffers(lio_icp* h, double* d_send, double* d_recv, int64_t n_per_rank);
 /* align(guess) + getFitnessScore() + is_valid decision (loop_closure.cpp:81-90).
  * aligned_opt (n*3, this rank's shard only when sharded) may be NULL.      */
 int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* aligned_opt);
@@ -349,6 +366,12 @@ int lio_preprocess(lio_filter* f, const float* raw, int64_t n, int stride, const
 /* straight into the ctx's scan (feats_down_body) without a host round trip; *n_down points */
 int lio_scan_preprocess(lio_ctx* c, const float* raw, int64_t n, int stride, const lio_scan_prep_params* p,
                         const lio_imu_pose* poses, int n_poses, const lio_pose* end, int64_t* n_down);
+
+/* feats_undistort of the ctx's last lio_scan_preprocess*: the undistorted, time-sorted records
+ * before downSizeFilterSurf — what FAST-LIO publishes on /cloud_registered with dense_publish_en
+ * (kitti.yaml:31), transformed to the world frame, and what fast_lio_sam keeps per keyframe
+ * (pose_pcd.hpp:37-39).  *n_points (and *stride) always set; out (cap_points records) optional.    */
+int lio_scan_get_undistorted(lio_ctx* c, float* out, int64_t cap_points, int64_t* n_points, int* stride);
 
 /* ------------------------------------------- wire / disk formats (§8(f) row 4) */
 /* One output column of a packed point record: byte offset, sensor_msgs/PointField datatype

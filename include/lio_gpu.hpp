@@ -422,7 +422,7 @@ struct RegistrationOutput {  // loop_closure.h:31-37
 class LoopClosureICP {
 public:
     explicit LoopClosureICP(const LoopClosureConfig& cfg = {}, int device = 0, float cell_size = 1.0f) {
-        lio_icp_params p{cfg.icp_max_corr_dist_, 0.01, 0.01, 50, 0.0, cfg.icp_score_threshold_, cell_size, device};
+        lio_icp_params p{cfg.icp_max_corr_dist_, 0.01, 0.01, 50, 0.0, cfg.icp_score_threshold_, cell_size, device, 0};
         check(lio_icp_create(&p, &h_), "lio_icp_create");
     }
     ~LoopClosureICP() { lio_icp_destroy(h_); }
@@ -463,7 +463,7 @@ public:
     LoopClosureICPGroup(const LoopClosureConfig& cfg, int n_gpus, const std::vector<int>& devices = {},
                         float cell_size = 1.0f) {
         lio_icp_params p{cfg.icp_max_corr_dist_, 0.01, 0.01, 50, 0.0, cfg.icp_score_threshold_, cell_size,
-                         devices.empty() ? 0 : devices[0]};
+                         devices.empty() ? 0 : devices[0], 0};
         check(lio_icp_group_create(&p, n_gpus, devices.empty() ? nullptr : devices.data(), &g_), "lio_icp_group_create");
     }
     ~LoopClosureICPGroup() { lio_icp_group_destroy(g_); }

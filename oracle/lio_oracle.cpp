@@ -806,7 +806,7 @@ static void cols_xform(std::vector<double>& M, int nrows, int ncols, int idx, co
 
 int ieskf_update(const KdTree& map, const float* body, int64_t n, State& x, std::vector<double>& P,
                  const MatchParams& mp, double R, int max_iter, double limit, int threads,
-                 IeskfStats* st, double* trace /* optional: per h-eval 8 doubles */) {
+                 IeskfStats* st, double* trace /* optional: per h-eval 8 doubles */, State* knn_state = nullptr) {
     std::vector<int32_t> nn_idx(5 * n, -1);
     std::vector<uint8_t> sel(n, 0);
     std::vector<float> planes(4 * n, 0.f);
@@ -826,6 +826,7 @@ int ieskf_update(const KdTree& map, const float* body, int64_t n, State& x, std:
         double sums[S_LEN];
         ++evals;
         if (converge) ++knns;
+        if (converge && knn_state) *knn_state = x;  // the state Nearest_Points belong to (map_incremental)
         h_share_model(map, body, n, ps, converge ? 1 : 0, nn_idx.data(), sel.data(), planes.data(), mp,
                       sums, threads, &rows);
         int dof = (int)sums[S_NEFF];
@@ -2072,14 +2073,16 @@ static void from_state(const orc::State& x, orc_state* s) {
 // stats_out: [iterations, knn_calls, converged, last_neff, last_res_sum]
 int orc_ieskf_update(void* m, const float* body, int64_t n, orc_state* state, double* P529,
                      const orc_match_params* mp, double R, int max_iter, double limit, int threads,
-                     double* stats_out, double* trace) {
+                     double* stats_out, double* trace, orc_state* knn_state_out) {
     orc::State x;
     to_state(state, x);
     std::vector<double> P(P529, P529 + 529);
     orc::MatchParams p{mp->knn_range_sq, mp->plane_thr, mp->s_coef, mp->s_gate};
     orc::IeskfStats st{};
-    int rc = orc::ieskf_update(*(orc::KdTree*)m, body, n, x, P, p, R, max_iter, limit, threads, &st, trace);
+    orc::State xk = x;
+    int rc = orc::ieskf_update(*(orc::KdTree*)m, body, n, x, P, p, R, max_iter, limit, threads, &st, trace, &xk);
     from_state(x, state);
+    if (knn_state_out) from_state(xk, knn_state_out);
     std::memcpy(P529, P.data(), sizeof(double) * 529);
     if (stats_out) {
         stats_out[0] = st.iterations;

@@ -68,7 +68,7 @@ int main() {
         std::vector<double> P(529, 0.0);
         for (int i = 0; i < 23; ++i) P[24 * i] = 1e-3;
         double stats[8], trace[64];
-        orc_ieskf_update(t, q.data(), 300, &s, P.data(), &mp, 0.001, 3, 0.001, 2, stats, trace);
+        orc_ieskf_update(t, q.data(), 300, &s, P.data(), &mp, 0.001, 3, 0.001, 2, stats, trace, nullptr);
         orc_map_free(t);
     }
 

@@ -33,13 +33,18 @@ runs() {  # as run, but any failure (tests included) ends the session
 
 for s in $STEPS; do
     case $s in
-    test)  run pytest_gpu 900 python -u -m pytest tests -q -m gpu -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+    test)  run pytest_gpu 1100 python -u -m pytest tests -q -m gpu -p no:cacheprovider --timeout 600 --timeout-method thread ;;
+    pipe)  runs pytest_pipe 600 python -u -m pytest tests/test_gpu_pipeline.py -x -v -s -p no:cacheprovider --timeout 500 --timeout-method thread ;;
+    icpf)  runs pytest_icpf 600 python -u -m pytest tests/test_gpu_icp.py -k "float or double" -x -v -s -p no:cacheprovider --timeout 500 --timeout-method thread ;;
+    icpx)  runs pytest_icpx 600 python -u -m pytest tests/test_gpu_icp.py -k "exchange or group" -x -v -s -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    spawn2) LIO_BENCH_REHEARSE=1 run spawn2 500 python bench.py --gpus 2 --steps 50 --warmup 5 --pipeline 0 --no-cpu --streams '' --icp-reps 2 ;;
+    map)   runs pytest_map 900 python -u -m pytest tests/test_gpu_map.py tests/test_gpu_fullsize.py -x -v -p no:cacheprovider --timeout 600 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench) run bench 600 python bench.py --steps 200 --warmup 20 ;;
     knn)   run knn_timing 300 python scripts/knn_timing.py C2 &&
-           LIO_FAR_BLOCKS=8 run knn_timing_fb8 300 python scripts/knn_timing.py C2 &&
            run knn_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/knnprof" -o run --output-format csv -- python scripts/knn_timing.py C2 ;;
     quick) run bench_quick 400 python bench.py --steps 60 --warmup 5 --icp-reps 2 --cpu-scans 10 --cpu-warmup 2 ;;
+    driver) run bench_driver 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
     c3)    run bench_c3 600 python bench.py --config C3 --steps 60 --warmup 5 --no-icp --cpu-scans 10 --cpu-warmup 2 --pipeline 12 ;;
     c2)    run bench_c2 600 python bench.py --config C2 --steps 200 --warmup 20 --no-icp --cpu-scans 20 --cpu-warmup 2 --streams '' ;;
     c5)    run bench_c5 600 python bench.py --config C5 --steps 200 --warmup 20 --no-icp --cpu-scans 10 --cpu-warmup 2 --pipeline 12 --streams '' ;;
@@ -48,63 +53,14 @@ for s in $STEPS; do
     rehearse) LIO_BENCH_REHEARSE=1 run rehearse2 500 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 100 --warmup 10 --icp-reps 2 ;;
     prof)  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
-               -- python bench.py --steps 100 --warmup 10 --no-cpu --icp-reps 3 --streams '' ;;
+               -- python bench.py --steps 100 --warmup 10 --no-cpu --icp-reps 3 --streams '' --pipeline 0 ;;
     pmc)   run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv \
-               -- python bench.py --steps 30 --warmup 3 --no-cpu --no-icp --streams '' &&
+               -- python bench.py --steps 30 --warmup 3 --no-cpu --no-icp --streams '' --pipeline 0 &&
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv \
-               -- python bench.py --steps 30 --warmup 3 --no-cpu --no-icp --streams '' ;;
+               -- python bench.py --steps 30 --warmup 3 --no-cpu --no-icp --streams '' --pipeline 0 ;;
     pmcicp) run pmc_icp 900 bash scripts/pmc_icp.sh "$TAG/pmcicp" ;;
     fullsize) run pytest_fullsize 900 python -u -m pytest tests/test_gpu_fullsize.py -x -v -s -p no:cacheprovider --timeout 600 --timeout-method thread ;;
-    abknn) for rep in 1 2; do
-             LIO_GPU_LIB=build_ab/liblio_gpu_base.so run ab_base_$rep 300 python bench.py --steps 400 --warmup 20 --no-icp --no-cpu --streams '' &&
-             run ab_new_$rep 300 python bench.py --steps 400 --warmup 20 --no-icp --no-cpu --streams '' || exit 1
-           done ;;
-    abplane) for rep in 1 2; do
-             run plane512_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' &&
-             LIO_PPL=2 run plane256_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' || exit 1
-           done ;;
-    abnear) LIO_NEAR_BLOCK=256 runs parity_near256 600 python -u -m pytest tests/test_gpu_parity.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread &&
-           for rep in 1 2 3; do
-             run near512_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' &&
-             LIO_NEAR_BLOCK=256 run near256_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' || exit 1
-           done ;;
-    abspill) LIO_NEAR_NOSPILL=1 runs parity_nospill 600 python -u -m pytest tests/test_gpu_parity.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread &&
-           for rep in 1 2 3; do
-             run spill_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' &&
-             LIO_NEAR_NOSPILL=1 run nospill_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' || exit 1
-           done &&
-           LIO_NEAR_NOSPILL=1 run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/pmc_fetch" -o run --output-format csv \
-               -- python bench.py --steps 30 --warmup 3 --no-cpu --no-icp --streams '' &&
-           LIO_NEAR_NOSPILL=1 run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv \
-               -- python bench.py --steps 30 --warmup 3 --no-cpu --no-icp --streams '' ;;
-    abnearfinal) for rep in 1 2; do
-             run nearnew_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' &&
-             LIO_NEAR_BLOCK=512 LIO_NEAR_NOSPILL=0 run nearold_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' || exit 1
-           done ;;
-    abnear128) LIO_NEAR_BLOCK=128 runs parity_near128 600 python -u -m pytest tests/test_gpu_parity.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread &&
-           for rep in 1 2 3; do
-             run n256_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' &&
-             LIO_NEAR_BLOCK=128 run n128_$rep 300 python bench.py --steps 600 --warmup 20 --no-icp --no-cpu --streams '' || exit 1
-           done ;;
     icptest) runs pytest_icp 600 python -u -m pytest tests/test_gpu_icp.py tests/test_gpu_parity.py -k icp -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
-    icpab) run icp_tile 300 python scripts/icp_ab.py 1.0 &&
-           LIO_ICP_DEBUG=1 run icp_tile_dbg 300 python scripts/icp_ab.py 1.0 1 &&
-           LIO_ICP_TILE_CELL=2.5 run icp_tile_t25 300 python scripts/icp_ab.py 1.0 &&
-           LIO_ICP_TILE_CELL=1.5 run icp_tile_t15 300 python scripts/icp_ab.py 1.0 &&
-           run icp_tile_c075 300 python scripts/icp_ab.py 0.75 ;;
-    icpq)  run icp_tile 300 python scripts/icp_ab.py 1.0 &&
-           LIO_ICP_DEBUG=1 run icp_tile_dbg 300 python scripts/icp_ab.py 1.0 1 ;;
-    icpsweep) for tc in 1.5 2.5 3.0; do LIO_ICP_TILE_CELL=$tc run icp_t$tc 300 python scripts/icp_ab.py 1.0 || exit 1; done &&
-           LIO_ICP_TILE_WAVES=1 run icp_w1 300 python scripts/icp_ab.py 1.0 &&
-           LIO_ICP_TILE_WAVES=4 run icp_w4 300 python scripts/icp_ab.py 1.0 &&
-           run icp_c075 300 python scripts/icp_ab.py 0.75 &&
-           run icp_c125 300 python scripts/icp_ab.py 1.25 &&
-           run icp_base 300 python scripts/icp_ab.py 1.0 ;;
-    icpr0) LIO_ICP_R0=0 run icp_r0 300 python scripts/icp_ab.py 1.0 &&
-           LIO_ICP_R0=0 LIO_ICP_DEBUG=1 run icp_r0_dbg 300 python scripts/icp_ab.py 1.0 1 ;;
-    icptimes) LIO_ICP_TIMES=1 run icp_times 300 python scripts/icp_ab.py 1.0 1 &&
-           LIO_ICP_TIMES=1 LIO_ICP_ORDER=0 run icp_times_o0 300 python scripts/icp_ab.py 1.0 1 ;;
-    icptpb) for t in 1 2 4 8; do LIO_ICP_TILES_PER_BLOCK=$t run icp_tpb$t 300 python scripts/icp_ab.py 1.0 || exit 1; done ;;
     icppmc2) run icp_trace 300 rocprofv3 --kernel-trace -d "$OUT/icptrace" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
              run icp_pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_BUSY_CYCLES --kernel-trace -d "$OUT/icpsq" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
              run icp_pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/icpfetch" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&

@@ -322,7 +322,7 @@ int main() {
         std::vector<float> s3, d3;
         for (const auto& p : src) s3.insert(s3.end(), {p.x, p.y, p.z});
         for (const auto& p : dst) d3.insert(d3.end(), {p.x, p.y, p.z});
-        lio_icp_params ip{52.5, 0.01, 0.01, 50, 0.0, 1.5, 1.0f, 0};
+        lio_icp_params ip{52.5, 0.01, 0.01, 50, 0.0, 1.5, 1.0f, 0, 0};
         float T1[16];
         double fit = 0.0;
         int conv = 0, its = 0;

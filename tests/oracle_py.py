@@ -84,7 +84,8 @@ def lib():
                                         C.c_int]
         L.orc_ieskf_update.argtypes = [C.c_void_p, C.POINTER(C.c_float), C.c_int64, C.POINTER(State),
                                        C.POINTER(C.c_double), C.POINTER(MatchParams), C.c_double, C.c_int,
-                                       C.c_double, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double)]
+                                       C.c_double, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_double),
+                                       C.POINTER(State)]
         L.orc_icp_align.argtypes = [C.POINTER(C.c_float), C.c_int64, C.POINTER(C.c_float), C.c_int64,
                                     C.POINTER(IcpParams), C.POINTER(C.c_float), C.POINTER(C.c_float),
                                     C.POINTER(C.c_double), C.POINTER(C.c_float), C.POINTER(C.c_double),
@@ -191,18 +192,22 @@ def state_from_c(s: State) -> dict:
     return {k: np.array(list(getattr(s, k))) for k, _ in State._fields_}
 
 
-def ieskf_update(omap: OracleMap, body, state: dict, P, mp=None, R=0.001, max_iter=3, limit=0.001, threads=8):
+def ieskf_update(omap: OracleMap, body, state: dict, P, mp=None, R=0.001, max_iter=3, limit=0.001, threads=8,
+                 knn_state=False):
+    """(state, P, stats, trace[, state of the last kNN evaluation when knn_state])"""
     mp = mp or default_match_params()
     body = np.ascontiguousarray(body, dtype=np.float32)
     s = state_to_c(state)
+    sk = State()
     Pc = np.ascontiguousarray(P, dtype=np.float64).copy()
     stats = np.zeros(8)
     trace = np.zeros(8 * 8)
     rc = lib().orc_ieskf_update(omap.h, _p(body, C.c_float), len(body), C.byref(s), _p(Pc, C.c_double),
                                 C.byref(mp), R, max_iter, limit, threads, _p(stats, C.c_double),
-                                _p(trace, C.c_double))
+                                _p(trace, C.c_double), C.byref(sk))
     assert rc == 0
-    return state_from_c(s), Pc, stats, trace.reshape(8, 8)
+    out = (state_from_c(s), Pc, stats, trace.reshape(8, 8))
+    return out + (state_from_c(sk),) if knn_state else out
 
 
 def icp_align(src, dst, params=None, guess=None, threads=8, max_trace=64, want_aligned=False):

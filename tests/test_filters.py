@@ -141,3 +141,23 @@ def test_preprocess_matches_python():
     a = O.preprocess(raw2, poses, end, point_filter_num=1, leaf=0.0)
     b = py_preprocess(raw2, poses, end, every=1, leaf=0.0)
     np.testing.assert_allclose(a, b, rtol=2e-7, atol=1e-6)
+
+
+def test_pipeline_glue_world_transform_matches_restatement(oracle):
+    """lio_gpu.pipeline.state_world (the keyframe glue's pointBodyToWorld, numpy in Eigen's operation
+    order) equals the restatement's body_to_world bit for bit; transform_pcd round-trips through
+    odom_matrix's inverse to within float rounding."""
+    from lio_gpu import pipeline as PL
+    from lio_gpu import synth
+
+    rng = np.random.default_rng(0)
+    for _ in range(4):
+        st = synth.initial_state(rng.normal(size=3) * 50, synth.rotvec_to_quat(rng.normal(size=3)))
+        xyz = (rng.normal(size=(20000, 3)) * 30).astype(np.float32)
+        w = PL.state_world(st, xyz)
+        np.testing.assert_array_equal(w, oracle.body_to_world(synth.pose24(st), xyz))
+        T = PL.odom_matrix(st)
+        back = PL.transform_pcd(np.concatenate([w, xyz[:, :1]], axis=1), np.linalg.inv(T))
+        ref = (xyz.astype(np.float64) @ synth.quat_to_mat(st["offset_R_L_I"]).T + st["offset_T_L_I"])
+        np.testing.assert_allclose(back[:, :3], ref, atol=1e-4)
+        np.testing.assert_array_equal(back[:, 3], xyz[:, 0])
