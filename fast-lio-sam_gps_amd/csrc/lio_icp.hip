@@ -58,6 +58,33 @@ __device__ __forceinline__ void xform_pcl(const float* T, float x, float y, floa
 // ----------------------------------------------------------------------------
 constexpr int kTileCh = 256;  // candidates staged per LDS round
 
+// Tiles -> blocks (launch_icp_tiles: 8 x (kIcpSegs / 8) x ceil(n / kIcpSegs) blocks; block b runs on
+// XCD b % 8).  The cell-ordered tiles form kIcpSegs contiguous segments; XCD x owns segments x, x + 8,
+// ...: its blocks walk those in cell order (first pass) or in the order icp_order_kernel wrote for its
+// share (later passes).  -1: a slot past the XCD's share.
+constexpr int kIcpSegs = 64;
+__device__ __forceinline__ int icp_seg_begin(int s, int n) { return (int)(((int64_t)s * n) / kIcpSegs); }
+__device__ __forceinline__ int icp_seg_xcd(int t, int n) {  // XCD owning tile t
+    int s = (int)(((int64_t)t * kIcpSegs) / n);
+    while (s > 0 && icp_seg_begin(s, n) > t) --s;  // integer rounding at segment edges
+    while (s + 1 < kIcpSegs && icp_seg_begin(s + 1, n) <= t) ++s;
+    return s & 7;
+}
+__device__ __forceinline__ int icp_tile_of(const uint32_t* order, int b, int n) {
+    const int x = b & 7;
+    int slot = b >> 3;
+    if (order) {
+        const int lo = (int)order[n + x], hi = (int)order[n + x + 1];
+        return lo + slot < hi ? (int)order[lo + slot] : -1;
+    }
+    for (int s = x; s < kIcpSegs; s += 8) {
+        const int b0 = icp_seg_begin(s, n), sz = icp_seg_begin(s + 1, n) - b0;
+        if (slot < sz) return b0 + slot;
+        slot -= sz;
+    }
+    return -1;
+}
+
 // LDS handoff between the lanes of ONE wave (each wave owns its staging area)
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -361,12 +388,12 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
     __shared__ uint64_t s_best[NW > 1 ? NW * kIcpTileQ : 1];  // cross-wave merge (NW > 1 only)
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     TileLds& L = Ls[wv];
-    // this wave's tile: slot k of the longest-first order, or (cell order) the XCD-remapped block's
-    // k-th tile; a wave past the end leaves at once (no block barriers when TPB > 1)
-    const int sub = TPB > 1 ? wv : 0;
-    const int k = a.order ? blockIdx.x * TPB + sub : xcd_block(blockIdx.x, gridDim.x) * TPB + sub;
-    if (TPB > 1 && k >= ntiles) return;
-    const int tix = a.order ? (int)a.order[k] : k;
+    // this wave's tile: its XCD's next tile in cell order (first pass) or in the per-XCD longest-first
+    // order of the previous pass's costs (icp_tile_of)
+    static_assert(TPB == 1, "icp_tile_kernel: one tile per block (icp_tile_of)");
+    (void)wv;
+    const int tix = icp_tile_of(a.order, (int)blockIdx.x, ntiles);
+    if (tix < 0) return;  // block-uniform: a slot past its XCD's share
     const uint2 tl = a.tiles[tix];
     const bool act = lane < (int)tl.y;
     const int i = act ? __float_as_int(a.qpts[tl.x + lane].w) : 0;
@@ -529,37 +556,44 @@ __global__ void __launch_bounds__(kIcpStatsThreads) icp_stats_kernel(IcpArgs a, 
 }
 
 // one wave per tile (several waves per tile, or several one-wave tiles per block, measured no faster:
-// profiles/r02_icp_tile_experiments.txt)
+// profiles/r02_icp_tile_experiments.txt); grid = 8 XCD shares of the largest size (icp_tile_of)
 void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st) {
     if (a.n == 0 || ntiles == 0) return;
-    icp_tile_kernel<1, 1><<<ntiles, kIcpTileQ, 0, st>>>(a, ntiles);
+    const int seg = (ntiles + kIcpSegs - 1) / kIcpSegs;
+    icp_tile_kernel<1, 1><<<8 * (kIcpSegs / 8) * seg, kIcpTileQ, 0, st>>>(a, ntiles);
 }
 
-// Longest-first tile order from the previous pass's candidate counts: tiles
-// bucketed by floor(log2(cost)), buckets in descending order (counting sort in
-// one block; order inside a bucket is arbitrary: it affects speed only).  The
-// heavy tiles (misaligned regions) start first instead of forming the tail.
+// Tile order for the next pass from this pass's candidate counts.  The cell-ordered tiles are cut
+// into kIcpSegs contiguous segments (spatially compact: their target neighbourhoods stay in one
+// XCD's L2), XCD x owns segments x, x + 8, ... (a misaligned region, which is spatially concentrated,
+// is shared by every XCD), and inside each XCD's share the tiles run longest-first (log2 buckets of
+// the count, descending) so the heavy ones do not form the tail.  Layout: order[0 .. n) the eight
+// shares one after another, order[n + x] the first entry of share x (order[n + 8] = n).
 __global__ void __launch_bounds__(1024) icp_order_kernel(const uint32_t* __restrict__ cost, int n,
                                                          uint32_t* __restrict__ order) {
-    __shared__ uint32_t hist[33], base[33];
-    if (threadIdx.x < 33) hist[threadIdx.x] = 0;
+    __shared__ uint32_t hist[8][33], base[8][33];
+    for (int t = threadIdx.x; t < 8 * 33; t += blockDim.x) hist[t / 33][t % 33] = 0;
     __syncthreads();
     for (int t = threadIdx.x; t < n; t += blockDim.x) {
         const uint32_t c = cost[t];
-        atomicAdd(&hist[c ? 32 - __clz(c) : 0], 1u);
+        atomicAdd(&hist[icp_seg_xcd(t, n)][c ? 32 - __clz(c) : 0], 1u);
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t acc = 0;
-        for (int b = 32; b >= 0; --b) {
-            base[b] = acc;
-            acc += hist[b];
+        for (int x = 0; x < 8; ++x) {
+            order[n + x] = acc;
+            for (int b = 32; b >= 0; --b) {
+                base[x][b] = acc;
+                acc += hist[x][b];
+            }
         }
+        order[n + 8] = acc;
     }
     __syncthreads();
     for (int t = threadIdx.x; t < n; t += blockDim.x) {
         const uint32_t c = cost[t];
-        order[atomicAdd(&base[c ? 32 - __clz(c) : 0], 1u)] = (uint32_t)t;
+        order[atomicAdd(&base[icp_seg_xcd(t, n)][c ? 32 - __clz(c) : 0], 1u)] = (uint32_t)t;
     }
 }
 void launch_icp_order(const uint32_t* tile_cost, int ntiles, uint32_t* order, hipStream_t st) {

@@ -505,7 +505,7 @@ static int icp_prepare(lio_icp* h) {
         IHIP(hipMalloc(&h->d_fid, n * sizeof(int)));
         IHIP(hipMalloc(&h->d_tiles, (n + n / lio::kIcpTileQ + 1) * sizeof(uint2)));
         IHIP(hipMalloc(&h->d_tcost, (n + n / lio::kIcpTileQ + 1) * sizeof(uint32_t)));
-        IHIP(hipMalloc(&h->d_order, (n + n / lio::kIcpTileQ + 1) * sizeof(uint32_t)));
+        IHIP(hipMalloc(&h->d_order, (n + n / lio::kIcpTileQ + 64) * sizeof(uint32_t)));  // + the 9 share offsets
         h->cap = n;
     }
     const int64_t nsup_all = (h->ns + lio::kIcpSuper - 1) / lio::kIcpSuper + 1;
