@@ -194,7 +194,9 @@ void jacobi_svd3_f(const float* A, float* U, float* V, float* sv) {
                 const Rot2 jrt{jr.c, -jr.s};
                 const Rot2 jl{rot1.c * jrt.c - rot1.s * jrt.s, rot1.c * jrt.s + rot1.s * jrt.c};  // rot1 * j_right^T
                 plane_rot(W + p, W + q, 3, jl);            // W.applyOnTheLeft(p, q, j_left): rows
-                plane_rot(U + 3 * p, U + 3 * q, 1, {jl.c, -jl.s});  // U.applyOnTheRight(p, q, j_left^T): columns
+                // U.applyOnTheRight(p, q, j_left^T): columns, and applyOnTheRight rotates by the transpose of
+                // its argument, so the plane rotation is j_left itself
+                plane_rot(U + 3 * p, U + 3 * q, 1, jl);
                 plane_rot(W + 3 * p, W + 3 * q, 1, {jr.c, -jr.s});  // W.applyOnTheRight(p, q, j_right)
                 plane_rot(V + 3 * p, V + 3 * q, 1, {jr.c, -jr.s});  // V.applyOnTheRight(p, q, j_right)
                 max_diag = std::max(max_diag, std::max(std::fabs(at(p, p)), std::fabs(at(q, q))));
@@ -655,6 +657,12 @@ extern "C" int lio_icp_shard_range(int64_t ns, int rank, int world, int64_t* beg
     if (ns < 0 || world < 1 || rank < 0 || rank >= world || !begin || !count)
         return ifail(LIO_ERR_ARG, "lio_icp_shard_range: bad arguments");
     shard_range(ns, rank, world, *begin, *count);
+    return LIO_OK;
+}
+
+extern "C" int lio_icp_umeyama_pcl_float(const float* sums16, float* T16) {
+    if (!sums16 || !T16) return ifail(LIO_ERR_ARG, "lio_icp_umeyama_pcl_float: bad arguments");
+    umeyama_pcl_float(sums16, T16);
     return LIO_OK;
 }
 

@@ -39,7 +39,7 @@ EXPORTS = [
     "lio_icp_set_shard_device", "lio_icp_exchange_len", "lio_icp_set_exchange_buffers",
     "lio_icp_align", "icp_align", "lio_icp_group_create", "lio_icp_group_destroy", "lio_icp_group_size",
     "lio_icp_group_uses_rccl", "lio_icp_group_set_target", "lio_icp_group_set_source", "lio_icp_group_align",
-    "lio_icp_shard_range", "lio_icp_combine", "lio_icp_get_correspondences",
+    "lio_icp_shard_range", "lio_icp_combine", "lio_icp_umeyama_pcl_float", "lio_icp_get_correspondences",
     "lio_ctx_set_timing", "lio_ctx_get_timing", "lio_ctx_reset_timing", "lio_icp_set_timing", "lio_icp_get_timing",
 ]
 
@@ -212,6 +212,7 @@ def _declare(L):
         "lio_icp_group_align": (C.c_int, [vp, fp, C.POINTER(IcpResult), fp]),
         "lio_icp_shard_range": (C.c_int, [C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
         "lio_icp_combine": (C.c_int, [dp, C.c_int64, C.c_int, dp]),
+        "lio_icp_umeyama_pcl_float": (C.c_int, [fp, fp]),
         "lio_ctx_set_timing": (C.c_int, [vp, C.c_int]),
         "lio_ctx_get_timing": (C.c_int, [vp, C.POINTER(KernelTiming)]),
         "lio_ctx_reset_timing": (C.c_int, [vp]),

@@ -268,6 +268,11 @@ int lio_icp_set_shard(lio_icp* h, int rank, int world, lio_allgather_fn fn, void
  * ceil(records/world)*20 doubles, as lio_allgather_fn delivers them.       */
 int lio_icp_shard_range(int64_t n_source, int rank, int world, int64_t* begin, int64_t* count);
 int lio_icp_combine(const double* recv, int64_t n_source, int world, double* out17);
+/* Host half of the PCL-order fidelity mode (no device needed): sums16 = the float sums the GPU
+ * returns per pass [sum src xyz(3), sum tgt xyz(3), count (uint32 bits), sigma accumulator (9,
+ * row-major target x source)] -> the incremental transform (row-major 4x4 float) through the
+ * float JacobiSVD (pcl::umeyama(src, dst, false) [U], Eigen 3.3 Umeyama.h).                  */
+int lio_icp_umeyama_pcl_float(const float* sums16, float* T16);
 /* Device-side exchange (the form to use with RCCL): per pass the statistics kernel writes this rank's
  * records into a DEVICE send buffer, `fn` enqueues the all-gather of n doubles per rank into the
  * device recv buffer (world * n, rank order) ordered on `stream` (RCCL in-stream, or a collective on

@@ -89,3 +89,45 @@ def test_compute_fails_loudly_without_device():
     rc = L.icp_align(fp, 8, fp, 8, C.byref(_capi.IcpParams(52.5, 0.01, 0.01, 50, 0.0, 1.5, 1.0, 0)), 4, T, None,
                      None, None, None)
     assert rc == _capi.LIO_ERR_NODEV
+
+
+def _rot(axis, ang):
+    a = np.asarray(axis, np.float64) / np.linalg.norm(axis)
+    K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+    return np.eye(3) + np.sin(ang) * K + (1 - np.cos(ang)) * K @ K
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 3])
+def test_icp_umeyama_pcl_float_host(seed):
+    """Host half of the PCL-order fidelity mode (float JacobiSVD, lio_icp_umeyama_pcl_float): the sums
+    the GPU returns (sequential float sums over the pairs) -> the rigid transform.  Checked against the
+    known motion and numpy's double SVD Umeyama on the same pairs: within 1e-5 (float)."""
+    rng = np.random.default_rng(seed)
+    n = 2000
+    src = (rng.standard_normal((n, 3)) * [8.0, 5.0, 1.5] + [30.0, -12.0, 2.0]).astype(np.float32)
+    R = _rot(rng.standard_normal(3), rng.uniform(0.01, 0.3))
+    t = rng.uniform(-2, 2, 3)
+    tgt = (src.astype(np.float64) @ R.T + t + rng.standard_normal((n, 3)) * 0.01).astype(np.float32)
+    sums = np.zeros(16, np.float32)
+    sums[0:3] = np.cumsum(src, axis=0, dtype=np.float32)[-1]  # sequential float sums, Eigen's redux order
+    sums[3:6] = np.cumsum(tgt, axis=0, dtype=np.float32)[-1]
+    sums[6] = np.array([n], np.uint32).view(np.float32)[0]
+    inv = np.float32(1.0) / np.float32(n)
+    sm, dm = sums[0:3] * inv, sums[3:6] * inv
+    prod = (tgt - dm)[:, :, None] * (src - sm)[:, None, :]  # float32 products, row r target, col c source
+    sums[7:16] = np.cumsum(prod.reshape(n, 9), axis=0, dtype=np.float32)[-1]
+    T = np.zeros(16, np.float32)
+    L = _capi.lib()
+    assert L.lio_icp_umeyama_pcl_float(sums.ctypes.data_as(_capi.fp), T.ctypes.data_as(_capi.fp)) == 0
+    T = T.reshape(4, 4).astype(np.float64)
+    # numpy double Umeyama on the same pairs
+    s64, d64 = src.astype(np.float64), tgt.astype(np.float64)
+    ms, md = s64.mean(0), d64.mean(0)
+    U, _, Vt = np.linalg.svd((d64 - md).T @ (s64 - ms) / n)
+    S = np.diag([1, 1, np.sign(np.linalg.det(U) * np.linalg.det(Vt))])
+    Rn = U @ S @ Vt
+    tn = md - Rn @ ms
+    assert np.abs(T[:3, :3] - Rn).max() < 1e-5 and np.abs(T[:3, 3] - tn).max() < 2e-4
+    assert np.abs(T[:3, :3] - R).max() < 1e-3
+    assert np.abs(T[3] - [0, 0, 0, 1]).max() == 0
+    assert abs(np.linalg.det(T[:3, :3]) - 1) < 1e-5
