@@ -468,6 +468,11 @@ int lio_icp_set_exchange_buffers(lio_icp* h, double* d_send, double* d_recv, int
 // device exchange buffers for the current source (the handle's own unless the caller's are large enough)
 static int exchange_reserve(lio_icp* h) {
     const int64_t need = std::max<int64_t>(exchange_len(h->ns, h->world), lio::kIcpStride);
+    if (!h->h_out17) {  // the record-order sums land here whoever owns the exchange buffers
+        IHIP(hipHostMalloc(&h->h_out17, 32 * sizeof(double), hipHostMallocMapped));
+        IHIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->h_out17_dev), h->h_out17, 0));
+    }
+    if (!h->h_out17_dev) return ifail(LIO_ERR_STATE, "lio_icp_align: no device view of the result block");
     if (h->x_ext) {
         if (h->x_len < need)
             return ifail(LIO_ERR_ARG, "lio_icp_align: caller exchange buffers too small (lio_icp_exchange_len)");
@@ -481,10 +486,6 @@ static int exchange_reserve(lio_icp* h) {
         IHIP(hipMalloc(&h->d_xsend, (size_t)need * sizeof(double)));
         IHIP(hipMalloc(&h->d_xrecv, (size_t)need * h->world * sizeof(double)));
         h->x_len = need;
-    }
-    if (!h->h_out17) {
-        IHIP(hipHostMalloc(&h->h_out17, 32 * sizeof(double), hipHostMallocMapped));
-        IHIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->h_out17_dev), h->h_out17, 0));
     }
     return LIO_OK;
 }
