@@ -480,6 +480,25 @@ int lio_map_get_grid(lio_map* m, double* out7) {
     return LIO_OK;
 }
 
+int lio_map_get_stats(lio_map* m, int64_t* out8) {
+    if (!m || !out8) return fail(LIO_ERR_ARG, "bad arguments");
+    HIP_TRY(hipSetDevice(m->dev));
+    uint32_t bump = 0;
+    if (m->grid.bump) {
+        HIP_TRY(hipMemcpyAsync(&bump, m->grid.bump, sizeof(bump), hipMemcpyDeviceToHost, m->st));
+        HIP_TRY(hipStreamSynchronize(m->st));
+    }
+    out8[0] = m->grid.rebuilds;
+    out8[1] = m->grid.slots_cap;
+    out8[2] = bump;
+    out8[3] = m->grid.n;
+    out8[4] = m->grid.n_ids;
+    out8[5] = m->grid.geom.ncells;
+    out8[6] = m->upd.h_cnt ? (int64_t)m->upd.h_cnt[9] : 0;  // lio_mapupd.hip kCFlags
+    out8[7] = 0;
+    return LIO_OK;
+}
+
 // =============================================================================
 // h_share_model context
 // =============================================================================

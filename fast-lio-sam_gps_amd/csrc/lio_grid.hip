@@ -396,6 +396,7 @@ int grid_build(GridBuf& g, const float* d_xyz, int64_t n, float cell, hipStream_
 
 int grid_rebuild(GridBuf& g, float cell, float slack, hipStream_t st) {
     const int64_t n_ids = g.n_ids;
+    ++g.rebuilds;
     if (!(cell > 0.f)) cell = 1.0f;
     int rc = reserve_entries(g, std::max<int64_t>(n_ids, 1));
     if (rc) return rc;

@@ -64,12 +64,6 @@ constexpr int kTileCh = 256;  // candidates staged per LDS round
 // share (later passes).  -1: a slot past the XCD's share.
 constexpr int kIcpSegs = 64;
 __device__ __forceinline__ int icp_seg_begin(int s, int n) { return (int)(((int64_t)s * n) / kIcpSegs); }
-__device__ __forceinline__ int icp_seg_xcd(int t, int n) {  // XCD owning tile t
-    int s = (int)(((int64_t)t * kIcpSegs) / n);
-    while (s > 0 && icp_seg_begin(s, n) > t) --s;  // integer rounding at segment edges
-    while (s + 1 < kIcpSegs && icp_seg_begin(s + 1, n) <= t) ++s;
-    return s & 7;
-}
 __device__ __forceinline__ int icp_tile_of(const uint32_t* order, int b, int n) {
     const int x = b & 7;
     int slot = b >> 3;
@@ -569,35 +563,37 @@ void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st) {
 // is shared by every XCD), and inside each XCD's share the tiles run longest-first (log2 buckets of
 // the count, descending) so the heavy ones do not form the tail.  Layout: order[0 .. n) the eight
 // shares one after another, order[n + x] the first entry of share x (order[n + 8] = n).
-__global__ void __launch_bounds__(1024) icp_order_kernel(const uint32_t* __restrict__ cost, int n,
-                                                         uint32_t* __restrict__ order) {
-    __shared__ uint32_t hist[8][33], base[8][33];
-    for (int t = threadIdx.x; t < 8 * 33; t += blockDim.x) hist[t / 33][t % 33] = 0;
+// One block per share (the share sizes follow from the segment bounds, so no block waits for
+// another): it sits between two dependent passes, so it has to be short.
+__device__ __forceinline__ uint32_t cost_bucket(uint32_t c) { return c ? 32u - (uint32_t)__clz(c) : 0u; }
+__global__ void __launch_bounds__(256) icp_order_kernel(const uint32_t* __restrict__ cost, int n,
+                                                        uint32_t* __restrict__ order) {
+    __shared__ uint32_t hist[33], base[33];
+    const int x = (int)blockIdx.x;
+    if (threadIdx.x < 33) hist[threadIdx.x] = 0;
     __syncthreads();
-    for (int t = threadIdx.x; t < n; t += blockDim.x) {
-        const uint32_t c = cost[t];
-        atomicAdd(&hist[icp_seg_xcd(t, n)][c ? 32 - __clz(c) : 0], 1u);
-    }
+    for (int s = x; s < kIcpSegs; s += 8)
+        for (int t = icp_seg_begin(s, n) + (int)threadIdx.x; t < icp_seg_begin(s + 1, n); t += 256)
+            atomicAdd(&hist[cost_bucket(cost[t])], 1u);
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t acc = 0;
-        for (int x = 0; x < 8; ++x) {
-            order[n + x] = acc;
-            for (int b = 32; b >= 0; --b) {
-                base[x][b] = acc;
-                acc += hist[x][b];
-            }
+        uint32_t acc = 0;  // this share's first entry: the sizes of shares 0 .. x-1
+        for (int s = 0; s < kIcpSegs; ++s)
+            if ((s & 7) < x) acc += (uint32_t)(icp_seg_begin(s + 1, n) - icp_seg_begin(s, n));
+        order[n + x] = acc;
+        if (x == 0) order[n + 8] = (uint32_t)n;
+        for (int b = 32; b >= 0; --b) {  // longest first
+            base[b] = acc;
+            acc += hist[b];
         }
-        order[n + 8] = acc;
     }
     __syncthreads();
-    for (int t = threadIdx.x; t < n; t += blockDim.x) {
-        const uint32_t c = cost[t];
-        order[atomicAdd(&base[icp_seg_xcd(t, n)][c ? 32 - __clz(c) : 0], 1u)] = (uint32_t)t;
-    }
+    for (int s = x; s < kIcpSegs; s += 8)
+        for (int t = icp_seg_begin(s, n) + (int)threadIdx.x; t < icp_seg_begin(s + 1, n); t += 256)
+            order[atomicAdd(&base[cost_bucket(cost[t])], 1u)] = (uint32_t)t;
 }
 void launch_icp_order(const uint32_t* tile_cost, int ntiles, uint32_t* order, hipStream_t st) {
-    if (ntiles > 0) icp_order_kernel<<<1, 1024, 0, st>>>(tile_cost, ntiles, order);
+    if (ntiles > 0) icp_order_kernel<<<8, 256, 0, st>>>(tile_cost, ntiles, order);
 }
 
 // per cell: number of tiles (ceil(count / 64)); slot ncells = 0 for the scan's total

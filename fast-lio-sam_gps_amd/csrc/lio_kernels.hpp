@@ -85,6 +85,7 @@ struct GridBuf {
     uint32_t* bump = nullptr;    // device: next free slot of the pool
     int64_t slots_cap = 0;       // pts capacity in slots
     int64_t slots_used = 0;      // bump value after the last rebuild (host view; the pool's live share)
+    int64_t rebuilds = 0;        // full rebuilds so far (diagnostics: lio_map_get_stats)
     // temporaries
     uint32_t* keys = nullptr;
     uint32_t* keys_alt = nullptr;

@@ -27,7 +27,7 @@ SUMS_HTH, SUMS_HTh, SUMS_NEFF, SUMS_RES, SUMS_HH = 0, 21, 27, 28, 29
 EXPORTS = [
     "lio_device_count", "lio_last_error", "lio_build_info",
     "lio_map_create", "lio_map_destroy", "lio_map_set_params", "lio_map_build", "lio_map_build_device", "lio_map_size",
-    "lio_map_get_points", "lio_map_get_grid", "lio_map_num_ids", "lio_map_get_by_id", "lio_map_nearest_search", "lio_map_gather", "lio_map_add",
+    "lio_map_get_points", "lio_map_get_grid", "lio_map_get_stats", "lio_map_num_ids", "lio_map_get_by_id", "lio_map_nearest_search", "lio_map_gather", "lio_map_add",
     "lio_map_add_device", "lio_map_delete_boxes", "lio_localmap_update", "lio_map_incremental",
     "lio_ctx_get_knn_pose", "lio_filter_create", "lio_filter_destroy", "lio_voxel_grid", "lio_submap_voxelize",
     "lio_preprocess", "lio_scan_preprocess", "lio_cloud2_decode", "lio_cloud2_encode", "lio_scan_preprocess_cloud2",
@@ -148,6 +148,7 @@ def _declare(L):
         "lio_map_size": (C.c_int64, [vp]),
         "lio_map_get_points": (C.c_int, [vp, fp]),
         "lio_map_get_grid": (C.c_int, [vp, dp]),
+        "lio_map_get_stats": (C.c_int, [vp, C.POINTER(C.c_int64)]),
         "lio_map_num_ids": (C.c_int64, [vp]),
         "lio_map_get_by_id": (C.c_int, [vp, fp, C.POINTER(C.c_uint8)]),
         "lio_map_nearest_search": (C.c_int, [vp, fp, C.c_int64, C.c_int, C.c_float, C.POINTER(C.c_int32), fp]),

@@ -159,6 +159,12 @@ class IkdTreeGPU:
         check(lib().lio_map_get_points(self._h, _fp(out)))
         return out
 
+    def stats(self) -> dict:
+        """Diagnostics (lio_map_get_stats): rebuilds so far, slot pool, sizes, last update's flags."""
+        o = (C.c_int64 * 8)()
+        check(lib().lio_map_get_stats(self._h, o))
+        return dict(rebuilds=o[0], slots_cap=o[1], slots_used=o[2], alive=o[3], ids=o[4], cells=o[5], flags=o[6])
+
     def grid(self):
         g = np.zeros(7)
         check(lib().lio_map_get_grid(self._h, _dp(g)))

@@ -124,6 +124,10 @@ int lio_localmap_update(lio_localmap* lm, const double pos_lid[3], double cube_l
                         float mov_threshold, float boxes_out[18], int* n_boxes);
 /* grid geometry: origin[3], cell, dims[3] (as doubles)                     */
 int lio_map_get_grid(lio_map* m, double* out7);
+/* diagnostics: out8 = [full grid rebuilds so far, slot pool capacity, slots handed out (device bump),
+ * alive points, ids, grid cells, flags of the last update (1 outside the grid, 2 pool exhausted,
+ * 4 tombstone cell list full: each forces a rebuild), reserved]                                  */
+int lio_map_get_stats(lio_map* m, int64_t* out8);
 
 /* ------------------------------------------------------------ h-model ctx */
 typedef struct lio_ctx lio_ctx;

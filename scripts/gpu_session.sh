@@ -67,6 +67,8 @@ for s in $STEPS; do
              run icp_pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/icpwrite" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 ;;
     icpprof) run icp_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/icpprof" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
              run icp_pmc_valu 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --kernel-trace -d "$OUT/icppmc" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 ;;
+    mapt)  run map_timing 400 python scripts/map_incr_timing.py 20 ;;
+    mapprof) run map_prof 400 rocprofv3 --kernel-trace --stats -d "$OUT/mapprof" -o run --output-format csv -- python scripts/map_incr_timing.py 20 ;;
     *) echo "unknown step $s" ;;
     esac
 done
