@@ -95,24 +95,46 @@ __device__ __forceinline__ uint32_t hash_slot(unsigned long long k, uint32_t mas
 }
 
 // Group the points [0, cnt[kCAdd]) by downsample voxel: an open-addressing table of voxel keys
-// (linear probing, CAS), each slot the head of a chain of input indices (next[]); the point that
-// starts a chain lists the voxel.
+// (linear probing, CAS), the lane that claims a slot lists the voxel; every point emits (slot, index)
+// for a stable sort (points past the count: the sentinel slot hcap, sorted last), so each voxel's
+// points end up contiguous and in input order whatever the voxel's size.
 __global__ void vox_group_kernel(const float* __restrict__ xyz, float ds, unsigned long long* __restrict__ hkey,
-                                 int* __restrict__ hhead, uint32_t hmask, int* __restrict__ next,
+                                 uint32_t hmask, int n_max, uint32_t* __restrict__ skey, uint32_t* __restrict__ sval,
                                  uint32_t* __restrict__ vlist, uint32_t* __restrict__ cnt) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= cnt[kCAdd]) return;
+    if ((int)i >= n_max) return;
+    sval[i] = i;
+    if (i >= cnt[kCAdd]) {
+        skey[i] = hmask + 1;
+        return;
+    }
     const unsigned long long key = voxel_key(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], ds);
     uint32_t h = hash_slot(key, hmask);
     for (uint32_t probe = 0;; ++probe) {  // load <= 1/4: a free slot is always near
         const unsigned long long prev = atomicCAS(&hkey[h], kEmptyKey, key);
-        if (prev == kEmptyKey || prev == key) break;
-        if (probe > hmask) return;  // unreachable for a clean table (guard)
+        if (prev == kEmptyKey) {
+            vlist[atomicAdd(&cnt[kCVox], 1u)] = h;
+            break;
+        }
+        if (prev == key) break;
+        if (probe > hmask) {  // unreachable for a clean table (guard): the point joins no voxel
+            h = hmask + 1;
+            break;
+        }
         h = (h + 1) & hmask;
     }
-    const int old = atomicExch(&hhead[h], (int)i);
-    next[i] = old;
-    if (old < 0) vlist[atomicAdd(&cnt[kCVox], 1u)] = h;
+    skey[i] = h;
+}
+
+// the sorted run of each voxel: hhead[slot] = first entry, hend[slot] = one past the last
+__global__ void vox_runs_kernel(const uint32_t* __restrict__ skey2, int n_max, uint32_t hmask, int* __restrict__ hhead,
+                                int* __restrict__ hend) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n_max) return;
+    const uint32_t k = skey2[j];
+    if (k > hmask) return;
+    if (j == 0 || skey2[j - 1] != k) hhead[k] = j;
+    if (j == n_max - 1 || skey2[j + 1] != k) hend[k] = j + 1;
 }
 
 // the cells a box [lo, hi) can touch: a point with lo <= p < hi has its (clamped) cell between the
@@ -132,8 +154,6 @@ __device__ __forceinline__ CellRange box_cells(const GridDev& g, const VoxBox& b
     return r;
 }
 
-constexpr int kChain = 16;  // chain entries a lane sorts in registers (a longer chain: selection walks)
-
 // One lane per voxel: Add_Points' sequence for the voxel's points (input order) against the alive
 // map points in its box [U] (oracle DynMap::add_points):
 //   S := map points in the box; for each new point q:
@@ -143,58 +163,49 @@ constexpr int kChain = 16;  // chain entries a lane sorts in registers (a longer
 // then every map point of the box except a surviving map point becomes a tombstone (by_id alive
 // bit cleared, its grid slot marked (id bits kNone) for grid_compact_cells, its cell listed once),
 // and add_flag marks the new point that survives (at most one per voxel).  The table slot is reset
-// for the next call.
+// for the next call.  The voxel's points are sval2[hhead .. hend), ascending input indices.
 __global__ void __launch_bounds__(256) vox_resolve_kernel(
     const uint32_t* __restrict__ vlist, unsigned long long* __restrict__ hkey, int* __restrict__ hhead,
-    const int* __restrict__ next, const float* __restrict__ xyz, float ds, GridDev g, int grid_n,
-    float4* __restrict__ pts, float4* __restrict__ by_id, uint8_t* __restrict__ dirty, uint32_t* __restrict__ dlist,
-    uint32_t dcap, uint32_t* __restrict__ cnt, uint32_t* __restrict__ add_flag) {
+    const int* __restrict__ hend, const uint32_t* __restrict__ sval2, const float* __restrict__ xyz, float ds, GridDev g,
+    int grid_n, float4* __restrict__ pts, float4* __restrict__ by_id, uint8_t* __restrict__ dirty,
+    uint32_t* __restrict__ dlist, uint32_t dcap, uint32_t* __restrict__ cnt, uint32_t* __restrict__ add_flag) {
     const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t triggers = 0, dead = 0;
-    const int n_pts = (int)cnt[kCAdd];  // chain entries are input indices < n_pts (guards below)
     if (v < cnt[kCVox] && hhead[vlist[v]] >= 0) {
         const uint32_t h = vlist[v];
-        const int head = hhead[h];
-        int idx[kChain];
-        int nc = 0, total = 0, first_i = 0x7fffffff;
-        for (int i = head; i >= 0 && i < n_pts && total < n_pts; i = next[i]) {
-            if (nc < kChain) idx[nc++] = i;
-            first_i = min(first_i, i);
-            ++total;
-        }
+        const int s0 = hhead[h], s1 = hend[h];
         hkey[h] = kEmptyKey;  // the table is clean again for the next call
         hhead[h] = -1;
-        for (int a = 1; a < nc; ++a) {  // ascending input order
-            const int t = idx[a];
-            int c = a - 1;
-            while (c >= 0 && idx[c] > t) {
-                idx[c + 1] = idx[c];
-                --c;
-            }
-            idx[c + 1] = t;
-        }
+        const int first_i = (int)sval2[s0];
         const VoxBox b = vox_box(xyz[3 * first_i], xyz[3 * first_i + 1], xyz[3 * first_i + 2], ds);
         const CellRange cr = box_cells(g, b, grid_n);
-        // map points in the box: how many, and the nearest to the centre (lowest id among equals)
+        // map points in the box: how many, and the nearest to the centre (lowest id among equals);
+        // loads four at a time (independent of the running minimum)
         int cnt_e = 0;
         unsigned long long best = ~0ull;
         float bx = 0.f, by = 0.f, bz = 0.f;
         for (int z = cr.z0; z <= cr.z1; ++z)
             for (int y = cr.y0; y <= cr.y1; ++y)
                 for (int x = cr.x0; x <= cr.x1; ++x) {
-                    const uint2 r = g.rng[((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x];
-                    for (uint32_t k = r.x; k < r.y; ++k) {
-                        const float4 p = pts[k];
-                        if (!in_box(b, p.x, p.y, p.z)) continue;
-                        ++cnt_e;
-                        const float t = calc_dist(p.x, p.y, p.z, b.mid[0], b.mid[1], b.mid[2]);
-                        const unsigned long long kk =
-                            ((unsigned long long)__float_as_uint(t) << 32) | (uint32_t)__float_as_int(p.w);
-                        if (kk < best) {
-                            best = kk;
-                            bx = p.x;
-                            by = p.y;
-                            bz = p.z;
+                    const uint4 r = g.rng[((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x];
+                    for (uint32_t k0 = r.x; k0 < r.y; k0 += 4) {
+                        float4 p4[4];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) p4[u] = pts[min(k0 + (uint32_t)u, r.y - 1)];
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const float4 p = p4[u];
+                            if (k0 + (uint32_t)u >= r.y || !in_box(b, p.x, p.y, p.z)) continue;
+                            ++cnt_e;
+                            const float t = calc_dist(p.x, p.y, p.z, b.mid[0], b.mid[1], b.mid[2]);
+                            const unsigned long long kk =
+                                ((unsigned long long)__float_as_uint(t) << 32) | (uint32_t)__float_as_int(p.w);
+                            if (kk < best) {
+                                best = kk;
+                                bx = p.x;
+                                by = p.y;
+                                bz = p.z;
+                            }
                         }
                     }
                 }
@@ -202,21 +213,11 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
         // replay the voxel's new points in input order
         int surv_new = -1;
         float sx = bx, sy = by, sz = bz, sd = cnt_e > 0 ? __uint_as_float((uint32_t)(best >> 32)) : INFINITY;
-        int prev = -1;
-        for (int e = 0; e < total; ++e) {
-            int i = 0x7fffffff;
-            if (total <= kChain) {
-                i = idx[e];
-            } else {  // the smallest index after `prev` by a walk of the chain
-                int steps = 0;
-                for (int j = head; j >= 0 && j < n_pts && steps < total; j = next[j], ++steps)
-                    if (j > prev && j < i) i = j;
-                if (i >= n_pts) break;
-            }
-            prev = i;
+        for (int e = s0; e < s1; ++e) {
+            const int i = (int)sval2[e];
             const float qx = xyz[3 * i], qy = xyz[3 * i + 1], qz = xyz[3 * i + 2];
             const float qd = calc_dist(qx, qy, qz, b.mid[0], b.mid[1], b.mid[2]);
-            const int size_s = e == 0 ? cnt_e : 1;
+            const int size_s = e == s0 ? cnt_e : 1;
             const bool q_wins = size_s == 0 || !(sd < qd);
             if (size_s > 1 || q_wins || same_point(qx, qy, qz, sx, sy, sz)) {
                 ++triggers;
@@ -234,7 +235,7 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
                 for (int y = cr.y0; y <= cr.y1; ++y)
                     for (int x = cr.x0; x <= cr.x1; ++x) {
                         const uint32_t c = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
-                        const uint2 r = g.rng[c];
+                        const uint4 r = g.rng[c];
                         bool marked = false;
                         for (uint32_t k = r.x; k < r.y; ++k) {
                             const float4 p = pts[k];
@@ -486,8 +487,9 @@ int ensure_pts(MapUpdBuf& u, int64_t n, hipStream_t st) {
     }
     if (n <= u.cap && u.world) return 0;
     const int64_t c = std::max<int64_t>(n, u.cap + u.cap / 2);
-    void* bufs[] = {u.f64, u.pos64, u.add_flag, u.pos, u.cls, u.world, u.xyz_a, u.xyz_b, u.pending, u.next, u.vlist,
-                    u.dlist, u.tmp_cell, u.tmp_rank, u.tlist, u.hkey, u.hhead};
+    void* bufs[] = {u.f64,   u.pos64, u.add_flag, u.pos,      u.cls,      u.world,    u.xyz_a, u.xyz_b, u.pending,
+                    u.skey,  u.sval,  u.skey2,    u.sval2,    u.vlist,    u.dlist,    u.tmp_cell, u.tmp_rank,
+                    u.tlist, u.hkey,  u.hhead,    u.hend};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     UPD_CHK(hipMalloc(&u.f64, (c + 1) * sizeof(unsigned long long)));
@@ -499,16 +501,25 @@ int ensure_pts(MapUpdBuf& u, int64_t n, hipStream_t st) {
     UPD_CHK(hipMalloc(&u.xyz_a, c * 3 * sizeof(float)));
     UPD_CHK(hipMalloc(&u.xyz_b, c * 3 * sizeof(float)));
     UPD_CHK(hipMalloc(&u.pending, c * sizeof(int)));
-    UPD_CHK(hipMalloc(&u.next, c * sizeof(int)));
+    UPD_CHK(hipMalloc(&u.skey, c * sizeof(uint32_t)));
+    UPD_CHK(hipMalloc(&u.sval, c * sizeof(uint32_t)));
+    UPD_CHK(hipMalloc(&u.skey2, c * sizeof(uint32_t)));
+    UPD_CHK(hipMalloc(&u.sval2, c * sizeof(uint32_t)));
     UPD_CHK(hipMalloc(&u.vlist, c * sizeof(uint32_t)));
     UPD_CHK(hipMalloc(&u.dlist, c * 27 * sizeof(uint32_t)));  // dirty cells: <= 27 per voxel box at any cell size
     UPD_CHK(hipMalloc(&u.tmp_cell, c * sizeof(uint32_t)));
     UPD_CHK(hipMalloc(&u.tmp_rank, c * sizeof(uint32_t)));
     UPD_CHK(hipMalloc(&u.tlist, c * sizeof(uint32_t)));
     uint32_t hc = 1024;
-    while ((int64_t)hc < 4 * c) hc <<= 1;
+    int hb = 10;
+    while ((int64_t)hc < 4 * c) {
+        hc <<= 1;
+        ++hb;
+    }
     UPD_CHK(hipMalloc(&u.hkey, (size_t)hc * sizeof(unsigned long long)));
     UPD_CHK(hipMalloc(&u.hhead, (size_t)hc * sizeof(int)));
+    UPD_CHK(hipMalloc(&u.hend, (size_t)hc * sizeof(int)));
+    u.hbits = hb;
     UPD_CHK(hipMemsetAsync(u.hkey, 0xff, (size_t)hc * sizeof(unsigned long long), st));  // empty keys
     UPD_CHK(hipMemsetAsync(u.hhead, 0xff, (size_t)hc * sizeof(int), st));                // empty chains (-1)
     u.hcap = hc;
@@ -540,8 +551,18 @@ int exclusive_scan64(MapUpdBuf& u, const unsigned long long* in, unsigned long l
 int enqueue_add(GridBuf& g, MapUpdBuf& u, const float* xyz, int n_max, const float* xyz_nn, float ds, int64_t id0,
                 hipStream_t st) {
     const int nb = (n_max + 255) / 256;
-    vox_group_kernel<<<nb, 256, 0, st>>>(xyz, ds, u.hkey, u.hhead, u.hcap - 1, u.next, u.vlist, u.cnt);
-    vox_resolve_kernel<<<nb, 256, 0, st>>>(u.vlist, u.hkey, u.hhead, u.next, xyz, ds, grid_view(g), (int)g.n, g.pts,
+    vox_group_kernel<<<nb, 256, 0, st>>>(xyz, ds, u.hkey, u.hcap - 1, n_max, u.skey, u.sval, u.vlist, u.cnt);
+    {  // (slot, index) stable by slot: every voxel's points contiguous in input order (slot hcap: unused)
+        size_t bytes = 0;
+        UPD_CHK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, u.skey, u.skey2, u.sval, u.sval2, n_max, 0,
+                                                   u.hbits + 1, st));
+        if (ensure_tmp(u, bytes)) return -5;
+        bytes = u.tmp_bytes;
+        UPD_CHK(hipcub::DeviceRadixSort::SortPairs(u.tmp, bytes, u.skey, u.skey2, u.sval, u.sval2, n_max, 0,
+                                                   u.hbits + 1, st));
+    }
+    vox_runs_kernel<<<nb, 256, 0, st>>>(u.skey2, n_max, u.hcap - 1, u.hhead, u.hend);
+    vox_resolve_kernel<<<nb, 256, 0, st>>>(u.vlist, u.hkey, u.hhead, u.hend, u.sval2, xyz, ds, grid_view(g), (int)g.n, g.pts,
                                            g.by_id, g.dirty, u.dlist, (uint32_t)(u.cap * 27), u.cnt, u.add_flag);
     int rc = exclusive_scan(u, u.add_flag, u.pos, n_max + 1, st);
     if (rc) return rc;
@@ -568,8 +589,9 @@ int finish_add(GridBuf& g, MapUpdBuf& u, int64_t id0, float slack, hipStream_t s
 }  // namespace
 
 void mapupd_free(MapUpdBuf& u) {
-    void* bufs[] = {u.f64,  u.pos64,    u.add_flag, u.pos,   u.cls,   u.world, u.xyz_a, u.xyz_b, u.pending, u.next,
-                    u.vlist, u.dlist,   u.tmp_cell, u.tmp_rank, u.tlist, u.hkey, u.hhead, u.tmp,   u.cnt,     u.boxes};
+    void* bufs[] = {u.f64,   u.pos64, u.add_flag, u.pos,   u.cls,    u.world,    u.xyz_a,    u.xyz_b, u.pending,
+                    u.skey,  u.sval,  u.skey2,    u.sval2, u.vlist,  u.dlist,    u.tmp_cell, u.tmp_rank, u.tlist,
+                    u.hkey,  u.hhead, u.hend,     u.tmp,   u.cnt,    u.boxes};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (u.h_cnt) (void)hipHostFree(u.h_cnt);

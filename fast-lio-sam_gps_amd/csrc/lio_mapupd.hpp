@@ -18,15 +18,20 @@ struct MapUpdBuf {
     float* xyz_a = nullptr;               // PointToAdd
     float* xyz_b = nullptr;               // PointNoNeedDownsample
     int* pending = nullptr;               // points queued for the unbounded kNN
-    int* next = nullptr;                  // voxel chains (input indices)
+    uint32_t* skey = nullptr;             // voxel grouping: (table slot, input index) pairs, and the
+    uint32_t* sval = nullptr;             // stable sort's output (each voxel's points contiguous,
+    uint32_t* skey2 = nullptr;            // in input order)
+    uint32_t* sval2 = nullptr;
     uint32_t* vlist = nullptr;            // voxels touched
     uint32_t* dlist = nullptr;            // grid cells holding tombstones
     uint32_t* tmp_cell = nullptr;         // grid insert scratch
     uint32_t* tmp_rank = nullptr;
     uint32_t* tlist = nullptr;
     unsigned long long* hkey = nullptr;   // voxel table: keys (all ones = empty) ...
-    int* hhead = nullptr;                 // ... and chain heads (-1), clean between calls
+    int* hhead = nullptr;                 // ... and the voxel's first sorted entry (-1), clean between calls
+    int* hend = nullptr;                  // one past the voxel's last sorted entry
     uint32_t hcap = 0;
+    int hbits = 0;                        // log2(hcap)
     int64_t cap = 0;
     void* tmp = nullptr;
     size_t tmp_bytes = 0;

@@ -30,14 +30,14 @@ for k in range(n_grow):
                                 yaw_gt=0.05 * np.sin(0.3 * k + 0.2), seed=5099 + k))
 d_grow = [torch.from_numpy(s.body).to(dev) for s in grow]
 torch.cuda.synchronize()
-print("grid0", [round(v, 2) for v in tree.grid()], flush=True)
+print("grid0", tree.grid(), tree.stats(), flush=True)
 for k, s in enumerate(grow):
     hm.set_scan_device(d_grow[k].data_ptr(), len(s.body))
     xg, _, _ = kf.update_iterated_dyn_share_modified(synth.initial_state(s.pos_init, s.rot_init), P0)
-    g0 = tree.grid()
+    g0 = str(tree.grid())
     ti = time.perf_counter()
     st = hm.map_incremental(synth.pose24(xg), 0.5)
     ms = (time.perf_counter() - ti) * 1e3
-    g1 = tree.grid()
+    g1 = str(tree.grid())
     print(f"call {k:2d} {ms:8.3f} ms  to_add {st['n_to_add']:6d} no_need {st['n_no_downsample']:6d} "
           f"size {tree.size()} geometry changed {g0 != g1} {tree.stats()}", flush=True)
