@@ -188,6 +188,8 @@ struct lio_ctx {
     float seed_scale = 1.0f;  // lio_ctx_set_seed_scale (test hook: < 1 exercises the seeded pass's guard)
     int64_t undist_n = -1;    // feats_undistort of the last lio_scan_preprocess* (records in filt.c); -1: none
     int undist_stride = 0;
+    float* d_kf = nullptr;    // lio_scan_keyframe_cloud output (n x 4)
+    int64_t kf_cap = 0;
 };
 
 extern "C" {
@@ -549,7 +551,7 @@ int lio_ctx_destroy(lio_ctx* c) {
     for (hipEvent_t e : c->ev_marks)
         if (e) (void)hipEventDestroy(e);
     lio::filter_free(c->filt);
-    for (void* q : {(void*)c->d_raw, (void*)c->d_rec, (void*)c->d_poses})
+    for (void* q : {(void*)c->d_raw, (void*)c->d_rec, (void*)c->d_poses, (void*)c->d_kf})
         if (q) (void)hipFree(q);
     --c->map->n_ctx;
     delete c;
@@ -1229,6 +1231,25 @@ int lio_scan_get_undistorted(lio_ctx* c, float* out, int64_t cap_points, int64_t
     HIP_TRY(hipSetDevice(c->map->dev));
     HIP_TRY(hipMemcpyAsync(out, c->filt.c, (size_t)c->undist_n * c->undist_stride * sizeof(float),
                            hipMemcpyDeviceToHost, c->map->st));
+    HIP_TRY(hipStreamSynchronize(c->map->st));
+    return LIO_OK;
+}
+
+int lio_scan_keyframe_cloud(lio_ctx* c, const lio_pose* pose, const double* T16, float* out, int64_t cap_points,
+                            int64_t* n_points) {
+    if (!c || !pose || !T16 || !n_points) return fail(LIO_ERR_ARG, "lio_scan_keyframe_cloud: bad arguments");
+    if (c->undist_n < 0) return fail(LIO_ERR_STATE, "lio_scan_keyframe_cloud: no lio_scan_preprocess* on this ctx");
+    *n_points = c->undist_n;
+    if (!out || c->undist_n == 0) return LIO_OK;
+    if (cap_points < c->undist_n) return fail(LIO_ERR_ARG, "lio_scan_keyframe_cloud: out too small");
+    HIP_TRY(hipSetDevice(c->map->dev));
+    int rc = grow(&c->d_kf, c->kf_cap, c->undist_n * 4);
+    if (rc) return rc;
+    lio::PoseArg ps;
+    std::memcpy(&ps, pose, sizeof(ps));
+    if (lio::keyframe_cloud(c->filt.c, c->undist_n, c->undist_stride, ps, T16, c->d_kf, c->map->st))
+        return fail(LIO_ERR_HIP, "keyframe cloud kernel failed");
+    HIP_TRY(hipMemcpyAsync(out, c->d_kf, (size_t)c->undist_n * 4 * sizeof(float), hipMemcpyDeviceToHost, c->map->st));
     HIP_TRY(hipStreamSynchronize(c->map->st));
     return LIO_OK;
 }

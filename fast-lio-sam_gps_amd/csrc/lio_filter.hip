@@ -687,6 +687,40 @@ int transform_segments(const float* d_in, int64_t n, int stride, const int64_t* 
     return 0;
 }
 
+// fast_lio_sam's keyframe cloud, fused: FAST-LIO publishes /cloud_registered = feats_undistort through
+// pointBodyToWorld (laserMapping [U]: double, stored float; dense_publish_en, kitti.yaml:31) and
+// PosePcd takes it back with transformPcd(cloud, pose_eig_.inverse()) (pose_pcd.hpp:22-42,
+// utilities.hpp:132-143: ((m0 x + m1 y) + m2 z) + m3 in double, stored float; other fields copied).
+struct Mat16d {
+    double m[16];
+};
+__global__ void keyframe_cloud_kernel(const float* __restrict__ rec, int64_t n, int stride, PoseArg ps, Mat16d T,
+                                      float* __restrict__ out) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const float* q = rec + (size_t)i * stride;
+    float wx, wy, wz;
+    body_to_world(ps, q[0], q[1], q[2], wx, wy, wz);
+    const double x = wx, y = wy, z = wz;
+    const double* m = T.m;
+    float* o = out + 4 * (size_t)i;
+    o[0] = (float)(((m[0] * x + m[1] * y) + m[2] * z) + m[3]);
+    o[1] = (float)(((m[4] * x + m[5] * y) + m[6] * z) + m[7]);
+    o[2] = (float)(((m[8] * x + m[9] * y) + m[10] * z) + m[11]);
+    o[3] = q[3];
+}
+
+int keyframe_cloud(const float* d_rec, int64_t n, int stride, const PoseArg& ps, const double* T16, float* d_out,
+                   hipStream_t st) {
+    if (n <= 0) return 0;
+    if (stride < 4) return -1;
+    Mat16d T;
+    for (int k = 0; k < 16; ++k) T.m[k] = T16[k];
+    keyframe_cloud_kernel<<<nblk(n), 256, 0, st>>>(d_rec, n, stride, ps, T, d_out);
+    FCHK(hipGetLastError());
+    return 0;
+}
+
 int scan_preprocess(FilterBuf& b, const float* d_raw, int64_t n, int stride, const ScanPrepParams& p,
                     const ImuPose* d_poses, int np, const UndistortEnd& end, float* d_out, int64_t* n_out,
                     hipStream_t st, int64_t* n_undist) {

@@ -75,6 +75,11 @@ int scan_preprocess(FilterBuf& b, const float* d_raw, int64_t n, int stride, con
 
 int records_to_xyz(const float* d_rec, int64_t n, int stride, float* d_xyz, hipStream_t st);
 
+// d_out (n x 4: x, y, z, intensity) = T16 (row-major, double) * pointBodyToWorld(ps, record xyz) — the
+// keyframe cloud fast_lio_sam builds from /cloud_registered (lio_scan_keyframe_cloud)
+int keyframe_cloud(const float* d_rec, int64_t n, int stride, const PoseArg& ps, const double* T16, float* d_out,
+                   hipStream_t st);
+
 // One output column of a packed point record (sensor_msgs/PointField or a PCD field):
 // byte offset, PointField datatype (1..8, 0 = absent -> 0), scale (e.g. time unit -> ms).
 struct CloudField {

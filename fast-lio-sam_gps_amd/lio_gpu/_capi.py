@@ -34,7 +34,7 @@ EXPORTS = [
     "lio_pcd_write_binary", "lio_pcd_read", "lio_map_build_pcd",
     "lio_ctx_create", "lio_ctx_destroy", "lio_scan_set", "lio_scan_set_device", "lio_scan_bind_device", "lio_match",
     "lio_get_knn", "lio_get_planes", "lio_get_world", "lio_get_h_rows", "lio_ctx_knn_stats",
-    "lio_ieskf_update", "lio_ctx_set_seed_scale", "lio_scan_get_undistorted",
+    "lio_ieskf_update", "lio_ctx_set_seed_scale", "lio_scan_get_undistorted", "lio_scan_keyframe_cloud",
     "lio_icp_create", "lio_icp_destroy", "lio_icp_set_target", "lio_icp_set_source", "lio_icp_set_shard",
     "lio_icp_set_shard_device", "lio_icp_exchange_len", "lio_icp_set_exchange_buffers",
     "lio_icp_align", "icp_align", "lio_icp_group_create", "lio_icp_group_destroy", "lio_icp_group_size",
@@ -192,6 +192,7 @@ def _declare(L):
         "lio_ieskf_update": (C.c_int, [vp, C.POINTER(State), dp, C.POINTER(IeskfParams), C.POINTER(IeskfStats)]),
         "lio_ctx_set_seed_scale": (C.c_int, [vp, C.c_float]),
         "lio_scan_get_undistorted": (C.c_int, [vp, fp, C.c_int64, C.POINTER(C.c_int64), C.POINTER(C.c_int)]),
+        "lio_scan_keyframe_cloud": (C.c_int, [vp, C.POINTER(Pose), dp, fp, C.c_int64, C.POINTER(C.c_int64)]),
         "lio_icp_create": (C.c_int, [C.POINTER(IcpParams), C.POINTER(vp)]),
         "lio_icp_destroy": (C.c_int, [vp]),
         "lio_icp_set_target": (C.c_int, [vp, fp, C.c_int64]),

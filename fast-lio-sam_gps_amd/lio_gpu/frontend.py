@@ -296,6 +296,16 @@ class HShareModelGPU:
         check(lib().lio_scan_get_undistorted(self._h, _fp(out), n.value, C.byref(n), C.byref(stride)))
         return out
 
+    def keyframe_cloud(self, pose: _capi.Pose, T: np.ndarray) -> np.ndarray:
+        """lio_scan_keyframe_cloud: (n, 4) float32 = T * pointBodyToWorld(pose, feats_undistort) with the
+        intensity — fast_lio_sam's PosePcd cloud from /cloud_registered when T = pose_eig_.inverse()."""
+        n = C.c_int64(0)
+        T = np.ascontiguousarray(T, dtype=np.float64).reshape(16)
+        check(lib().lio_scan_keyframe_cloud(self._h, C.byref(pose), _dp(T), None, 0, C.byref(n)))
+        out = np.empty((n.value, 4), np.float32)
+        check(lib().lio_scan_keyframe_cloud(self._h, C.byref(pose), _dp(T), _fp(out), n.value, C.byref(n)))
+        return out
+
     def preprocess_cloud2(self, data, n_points: int, point_step: int, fields, imu_poses, end_pose, big_endian=False,
                           point_filter_num=4, blind=2.0, filter_size_surf=0.5) -> int:
         """preprocess_scan from sensor_msgs/PointCloud2 bytes; fields = 5 (offset, datatype[, scale]) for

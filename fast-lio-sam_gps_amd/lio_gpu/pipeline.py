@@ -7,7 +7,8 @@ Per sweep (FAST-LIO laserMapping [U], the Kodifly fork's submodule is empty: SUR
   map_incremental()                               -> HShareModelGPU.map_incremental   (GPU)
   publish /Odometry + /cloud_registered (dense_publish_en: feats_undistort, kitti.yaml:31) in the world
   frame -> fast_lio_sam's PosePcd (pose_pcd.hpp:22-42: the cloud taken back to the odometry frame with
-  pose_eig_.inverse())                            -> keyframe_from_odometry            (host glue)
+  pose_eig_.inverse())                            -> lio_scan_keyframe_cloud (GPU, fused); keyframe_host is
+                                                     the numpy form it is tested against
 Loop leg (fast_lio_sam.cpp:682-730 loopTimerFunc -> loop_closure.cpp:18-40 fetchClosestKeyframeIdx ->
 :101-126 performLoopClosure -> :42-67 setSrcAndDstCloud -> :69-92 icpAlignment): LoopClosure (GPU
 submap assembly + ICP).
@@ -117,13 +118,25 @@ class FastLioSamStream:
         t2 = time.perf_counter()
         inc = self.hm.map_incremental(synth.pose24(x), self.fs_map)
         t3 = time.perf_counter()
-        und = self.hm.undistorted()
-        world = np.concatenate([state_world(x, und[:, :3]), und[:, 3:4]], axis=1)
-        self.keyframes.append(keyframe_from_odometry(x, world, timestamp, len(self.keyframes)))
+        kf = self.keyframe_device(x, timestamp, len(self.keyframes))
+        self.keyframes.append(kf)
         t4 = time.perf_counter()
-        return dict(state=x, P=P, stats=st, incremental=inc, n_down=n_down, n_undistorted=len(und),
+        return dict(state=x, P=P, stats=st, incremental=inc, n_down=n_down, n_undistorted=len(kf.pcd_),
                     ms=dict(preprocess=(t1 - t0) * 1e3, update=(t2 - t1) * 1e3, map_incremental=(t3 - t2) * 1e3,
                             keyframe=(t4 - t3) * 1e3))
+
+    def keyframe_device(self, x: dict, timestamp: float, idx: int) -> LC.PosePcd:
+        """The keyframe of this sweep, its cloud built on the GPU (lio_scan_keyframe_cloud): the same
+        numbers as keyframe_from_odometry(x, world cloud) on the host, one kernel + one copy."""
+        T = odom_matrix(x)
+        pcd = self.hm.keyframe_cloud(F.pose_from_pose24(synth.pose24(x)), np.linalg.inv(T))
+        return LC.PosePcd(pcd_=pcd, pose_corrected_eig_=T.copy(), pose_eig_=T.copy(), timestamp_=float(timestamp), idx_=idx)
+
+    def keyframe_host(self, x: dict, timestamp: float, idx: int) -> LC.PosePcd:
+        """The host form of the glue (numpy): /cloud_registered in the world frame, then PosePcd."""
+        und = self.hm.undistorted()
+        world = np.concatenate([state_world(x, und[:, :3]), und[:, 3:4]], axis=1)
+        return keyframe_from_odometry(x, world, timestamp, idx)
 
     def loop(self, submap_range: int | None = None):
         """loopTimerFunc's work on the newest keyframe: (closest index, RegistrationOutput, ms)."""

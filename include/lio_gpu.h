@@ -381,6 +381,12 @@ int lio_scan_preprocess(lio_ctx* c, const float* raw, int64_t n, int stride, con
  * (kitti.yaml:31), transformed to the world frame, and what fast_lio_sam keeps per keyframe
  * (pose_pcd.hpp:37-39).  *n_points (and *stride) always set; out (cap_points records) optional.    */
 int lio_scan_get_undistorted(lio_ctx* c, float* out, int64_t cap_points, int64_t* n_points, int* stride);
+/* The keyframe cloud fast_lio_sam builds from FAST-LIO's /cloud_registered, on the device: out (n x 4:
+ * x, y, z, intensity) = T16 * pointBodyToWorld(pose, feats_undistort), T16 row-major double — pass
+ * pose_eig_.inverse() for PosePcd::pcd_ (pose_pcd.hpp:22-42; utilities.hpp:132-143 transformPcd order).
+ * out = NULL: count only.                                                                          */
+int lio_scan_keyframe_cloud(lio_ctx* c, const lio_pose* pose, const double* T16, float* out, int64_t cap_points,
+                            int64_t* n_points);
 
 /* ------------------------------------------- wire / disk formats (§8(f) row 4) */
 /* One output column of a packed point record: byte offset, sensor_msgs/PointField datatype

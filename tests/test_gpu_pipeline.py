@@ -10,6 +10,7 @@ its own poses, its keyframes).  Then fast_lio_sam's loop leg on the newest keyfr
 
 Bars:
 * per sweep: feats_down_body and feats_undistort bit-exact; pose within 1e-5; evaluation counts equal;
+  the keyframe cloud made on the GPU bit-exact against the numpy glue (pointBodyToWorld + transformPcd);
 * the loop candidate index equal;
 * stage parity on the GPU's keyframes: submaps bit-exact, ICP transform within 1e-5, iterations and
   convergence state identical, fitness score within 1e-5 relative;
@@ -52,6 +53,10 @@ def test_c5_stream_with_loop_closure(oracle):
         body = np.ascontiguousarray(o_down[:, :3])
         xo, Po, so, _, xk = oracle.ieskf_update(om.tree(), body, st0, P0, knn_state=True)
         xg, sg = g["state"], g["stats"]
+        # the keyframe cloud built on the GPU (lio_scan_keyframe_cloud) = the numpy glue, bit for bit
+        kh = gs.keyframe_host(xg, t, k)
+        np.testing.assert_array_equal(gs.keyframes[-1].pcd_, kh.pcd_)
+        np.testing.assert_array_equal(gs.keyframes[-1].pose_eig_, kh.pose_eig_)
         assert sg["h_evals"] == int(so[0]) and sg["knn_calls"] == int(so[1]) and sg["n_eff"] == int(so[3])
         np.testing.assert_allclose(xg["pos"], xo["pos"], atol=1e-5)
         np.testing.assert_allclose(xg["rot"], xo["rot"], atol=1e-5)
