@@ -237,15 +237,21 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
                         const uint32_t c = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
                         const uint4 r = g.rng[c];
                         bool marked = false;
-                        for (uint32_t k = r.x; k < r.y; ++k) {
-                            const float4 p = pts[k];
-                            if (!in_box(b, p.x, p.y, p.z)) continue;
-                            const int id = __float_as_int(p.w);
-                            if (surv_new < 0 && id == best_id) continue;
-                            by_id[id].w = 0.f;
-                            pts[k].w = __int_as_float(kNone);
-                            ++dead;
-                            marked = true;
+                        for (uint32_t k0 = r.x; k0 < r.y; k0 += 4) {  // four loads in flight, then the marks
+                            float4 p4[4];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) p4[u] = pts[min(k0 + (uint32_t)u, r.y - 1)];
+#pragma unroll
+                            for (int u = 0; u < 4; ++u) {
+                                const float4 p = p4[u];
+                                if (k0 + (uint32_t)u >= r.y || !in_box(b, p.x, p.y, p.z)) continue;
+                                const int id = __float_as_int(p.w);
+                                if (surv_new < 0 && id == best_id) continue;
+                                by_id[id].w = 0.f;
+                                pts[k0 + (uint32_t)u].w = __int_as_float(kNone);
+                                ++dead;
+                                marked = true;
+                            }
                         }
                         if (marked) {  // list the cell once: the lane that sets its dirty byte
                             unsigned int* wp = reinterpret_cast<unsigned int*>(dirty + (c & ~3u));
