@@ -71,7 +71,7 @@ def test_c5_stream_with_loop_closure(oracle):
     assert idx == gs.lc.fetchClosestKeyframeIdx(kfo[-1], kfo) == 0
     r = gs.lc.last_result
     src_g, dst_g = gs.lc.src_cloud_, gs.lc.dst_cloud_
-    assert len(src_g) > 10_000 and len(dst_g) > 10_000
+    assert len(src_g) > 5_000 and len(dst_g) > 5_000
 
     def submaps(kfs, center):
         ids = [i for i in range(center - 2, center + 3) if 0 <= i < len(kfs) - 1]
