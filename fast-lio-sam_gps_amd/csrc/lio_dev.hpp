@@ -30,51 +30,12 @@ constexpr int kNone = 0x7fffffff;
 struct GridDev {
     const float4* pts;      // points grouped by cell
     const uint32_t* start;  // dense grids (ICP): ncells + 1 CSR offsets, a row of cells one contiguous range
-    const uint4* rng;       // map grids: per cell its live slots [x, y) (gapped CSR: blocks with spare room) and
-                            // the x-slab offsets (z, w: slab_range)
+    const uint2* rng;       // map grids: per cell its live slots [x, y) (gapped CSR: blocks with spare room)
     float ox, oy, oz;       // grid origin (min corner)
     float cell, inv_cell;
     float margin;           // conservative slack for cell assignment rounding
     int nx, ny, nz;
 };
-
-// x-slabs of a map cell: its live points are stored partitioned by kSlabs equal slices of the cell
-// along x (any order inside a slice), rng[c].z = o1 | o2 << 16, rng[c].w = o3 | untrimmed << 16 with
-// o_k the number of points in slices below k; so a sphere's x-extent selects one contiguous
-// sub-range of the cell.  untrimmed (a cell of >= 65536 points): the offsets are not kept.
-constexpr int kSlabs = 4;
-constexpr uint32_t kSlabMaxCount = 0xffffu;
-// slice of x in the cell whose x index is cx (build / insert assignment; clamped)
-__device__ __forceinline__ uint32_t slab_of(float x, float ox, float cell, float inv_cell, int cx) {
-    const float x0 = ox + (float)cx * cell;
-    const float f = floorf((x - x0) * ((float)kSlabs * inv_cell));
-    return (uint32_t)fminf(fmaxf(f, 0.f), (float)(kSlabs - 1));
-}
-// offset (from the cell's first slot) of slice k, 0 <= k <= kSlabs
-__device__ __forceinline__ uint32_t slab_off(const uint4& r, int k) {
-    switch (k) {
-        case 0: return 0u;
-        case 1: return r.z & 0xffffu;
-        case 2: return r.z >> 16;
-        case 3: return r.w & 0xffffu;
-        default: return r.y - r.x;
-    }
-}
-// the slots of cell r (x index cx) that can hold points with x in [xlo, xhi] (conservative by the
-// grid's margin): [b, e)
-__device__ __forceinline__ void slab_range(const uint4& r, float xlo, float xhi, float ox, float cell, float inv_cell,
-                                           float margin, int cx, uint32_t& b, uint32_t& e) {
-    if ((r.w >> 16) != 0u) {
-        b = r.x;
-        e = r.y;
-        return;
-    }
-    const float x0 = ox + (float)cx * cell, s = (float)kSlabs * inv_cell;
-    const int s0 = (int)fminf(fmaxf(floorf((xlo - margin - x0) * s), 0.f), (float)(kSlabs - 1));
-    const int s1 = (int)fminf(fmaxf(floorf((xhi + margin - x0) * s), 0.f), (float)(kSlabs - 1));
-    b = r.x + slab_off(r, s0);
-    e = r.x + slab_off(r, s1 + 1);
-}
 
 struct PoseArg {  // lio_pose
     double R[9];
@@ -316,7 +277,7 @@ __device__ __forceinline__ void group_merge(TopK<K>& tk) {
 template <int K, int G>
 __device__ __forceinline__ void scan_cell_group(const GridDev& g, uint32_t c, float qx, float qy, float qz, int sub,
                                                 TopK<K>& tk) {
-    const uint4 r = g.rng[c];
+    const uint2 r = g.rng[c];
     const uint32_t b = r.x, e = r.y;
     for (uint32_t j = b + (uint32_t)sub; j < e; j += G) {
         const float4 p = g.pts[j];
@@ -329,7 +290,7 @@ __device__ __forceinline__ void scan_cell_group(const GridDev& g, uint32_t c, fl
 template <int K, int G, int U = 4>
 __device__ __forceinline__ void scan_cell_group2(const GridDev& g, uint32_t c, float qx, float qy, float qz, int sub,
                                                  TopK<K>& tk) {
-    const uint4 r = g.rng[c];
+    const uint2 r = g.rng[c];
     const uint32_t b = r.x, e = r.y;
     for (uint32_t j = b + (uint32_t)sub; j < e; j += U * G) {
         float4 p[U];
@@ -427,7 +388,7 @@ __device__ bool group_knn_exact(const GridDev& g, float qx, float qy, float qz, 
 template <int K>
 __device__ __forceinline__ void scan_cell_seq(const GridDev& g, uint32_t c, float qx, float qy, float qz,
                                               TopK<K>& tk) {
-    const uint4 r = g.rng[c];
+    const uint2 r = g.rng[c];
     const uint32_t b = r.x, e = r.y;
     uint32_t j = b;
     for (; j + 4 <= e; j += 4) {
@@ -488,22 +449,9 @@ constexpr int shell1_cpl() {  // cells of the 3x3x3 block per lane
     return (27 + G - 1) / G;
 }
 
-// cell r (x index cx) trimmed to the x-slices a sphere of squared radius `bound` around q can reach,
-// gyz = the (margin-widened, so never too large) squared (y, z) gap from q to the cell
-__device__ __forceinline__ void trim_cell(const GridDev& g, const uint4& r, int cx, float qx, float bound, float gyz,
-                                          uint32_t& b, uint32_t& n) {
-    const float rx = sqrtf(fmaxf(bound - gyz, 0.f)) * 1.00001f;
-    uint32_t e;
-    slab_range(r, qx - rx, qx + rx, g.ox, g.cell, g.inv_cell, g.margin, cx, b, e);
-    n = e - b;
-}
-
-// OWN: the own cell (k = 13) is a range too.  TRIM (the bound is known up front, seeded pass): cells
-// beyond `bound` from q are dropped and the rest trimmed to their x-slices within reach.
-template <int G, bool OWN = false, bool TRIM = false>
+template <int G, bool OWN = false>  // OWN: the own cell (k = 13) is a range too
 __device__ __forceinline__ void shell1_ranges(const GridDev& g, int cx, int cy, int cz, int sub,
-                                              uint32_t* b4, uint32_t* n4, float qx = 0.f, float qy = 0.f,
-                                              float qz = 0.f, float bound = 0.f) {
+                                              uint32_t* b4, uint32_t* n4) {
     constexpr int CPL = shell1_cpl<G>();
 #pragma unroll
     for (int j = 0; j < CPL; ++j) {
@@ -512,34 +460,25 @@ __device__ __forceinline__ void shell1_ranges(const GridDev& g, int cx, int cy, 
         const int x = cx + dx, y = cy + dy, z = cz + dz;
         const bool ok = k < 27 && (OWN || k != 13) && (unsigned)x < (unsigned)g.nx && (unsigned)y < (unsigned)g.ny &&
                         (unsigned)z < (unsigned)g.nz;
-        uint32_t b = 0, n = 0;
+        uint32_t b = 0, e = 0;
         if (ok) {
             const uint32_t c = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
-            const uint4 r = g.rng[c];
-            if constexpr (TRIM) {
-                const float cs = g.cell, m = g.margin, w = cs + 2.f * m;
-                const float xl = g.ox + (float)x * cs - m, yl = g.oy + (float)y * cs - m, zl = g.oz + (float)z * cs - m;
-                const float gyz = axis_gap(qy, yl, yl + w) + axis_gap(qz, zl, zl + w);
-                if (!((axis_gap(qx, xl, xl + w) + gyz) * 0.999999f > bound)) trim_cell(g, r, x, qx, bound, gyz, b, n);
-            } else {
-                b = r.x;
-                n = r.y - r.x;
-            }
+            const uint2 r = g.rng[c];
+            b = r.x;
+            e = r.y;
         }
         b4[j] = b;
-        n4[j] = n;
+        n4[j] = e - b;
     }
 }
 
 // The pruned shell-1 ranges of a group's query, concatenated into the
 // group's LDS slot table (lds[0..32) range starts, lds[32..65) offsets);
 // returns the total point count T (group-uniform).
-// TRIM: every cell that survives the pruning is re-read (an L2 hit: shell1_ranges loaded it) and
-// trimmed to its x-slices within reach of the bound (unseeded pass: the bound is known only here).
-template <int K, int G, bool TRIM = false>
-__device__ __forceinline__ uint32_t shell1_table(const GridDev& g, float qx, float qy, float qz, int cx, int cy, int cz,
-                                                 float lox, float loy, float loz, int sub, uint32_t* lds, uint32_t* b4,
-                                                 uint32_t* n4, float bound, SearchStats* dbg) {
+template <int K, int G>
+__device__ __forceinline__ uint32_t shell1_table(const GridDev& g, float qx, float qy, float qz, float lox, float loy,
+                                                 float loz, int sub, uint32_t* lds, uint32_t* b4, uint32_t* n4,
+                                                 float bound, SearchStats* dbg) {
     constexpr int CPL = shell1_cpl<G>();
     static_assert(CPL * G == 32, "shell1_table: slot table = 32 range starts + 33 offsets");
     const float cs = g.cell, m = g.margin, w = cs + 2.f * m;
@@ -551,15 +490,8 @@ __device__ __forceinline__ uint32_t shell1_table(const GridDev& g, float qx, flo
         const int k = CPL * sub + j;
         const int dx = k % 3 - 1, dy = (k / 3) % 3 - 1, dz = k / 9 - 1;
         const float xl = lox + (float)dx * cs - m, yl = loy + (float)dy * cs - m, zl = loz + (float)dz * cs - m;
-        const float gy = axis_gap(qy, yl, yl + w), gz = axis_gap(qz, zl, zl + w);
-        const float bd = (axis_gap(qx, xl, xl + w) + gy) + gz;
-        if (bd * 0.999999f > bound) {
-            n4[j] = 0;
-        } else if (TRIM && n4[j]) {
-            const int x = cx + dx;
-            const uint32_t c = ((uint32_t)(cz + dz) * (uint32_t)g.ny + (uint32_t)(cy + dy)) * (uint32_t)g.nx + (uint32_t)x;
-            trim_cell(g, g.rng[c], x, qx, bound, gy + gz, b4[j], n4[j]);
-        }
+        const float bd = (axis_gap(qx, xl, xl + w) + axis_gap(qy, yl, yl + w)) + axis_gap(qz, zl, zl + w);
+        if (bd * 0.999999f > bound) n4[j] = 0;
         if (dbg && n4[j]) dbg->cells += 1;
         packed += n4[j] + (n4[j] ? (1u << 24) : 0u);
     }
@@ -648,7 +580,8 @@ template <int K, int G, int U = 4>
 __device__ __forceinline__ void scan_shell1_flat(const GridDev& g, float qx, float qy, float qz, int cx, int cy,
                                                  int cz, float lox, float loy, float loz, int sub, uint32_t* lds,
                                                  uint32_t* b4, uint32_t* n4, TopK<K>& tk, SearchStats* dbg) {
-    const uint32_t T = shell1_table<K, G, true>(g, qx, qy, qz, cx, cy, cz, lox, loy, loz, sub, lds, b4, n4, tk.worst(), dbg);
+    (void)cx, (void)cy, (void)cz;
+    const uint32_t T = shell1_table<K, G>(g, qx, qy, qz, lox, loy, loz, sub, lds, b4, n4, tk.worst(), dbg);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -737,12 +670,12 @@ __device__ int group_knn_seeded(const GridDev& g, float bound, int cx, int cy, i
     tk.init(bound);
     if (!inside) return 0;  // the far pass scans the whole box from range fillers
     uint32_t b4[shell1_cpl<G>()], n4[shell1_cpl<G>()];
-    shell1_ranges<G, true, true>(g, cx, cy, cz, sub, b4, n4, qx, qy, qz, bound);  // pruned and trimmed
+    shell1_ranges<G, true>(g, cx, cy, cz, sub, b4, n4);
     const float cs = g.cell, m = g.margin;
     const float lox = g.ox + (float)cx * cs, loy = g.oy + (float)cy * cs, loz = g.oz + (float)cz * cs;
     float own = fminf(fminf(qx - lox, lox + cs - qx), fminf(qy - loy, loy + cs - qy));
     own = fminf(own, fminf(qz - loz, loz + cs - qz)) - m;
-    const uint32_t T = shell1_table<K, G>(g, qx, qy, qz, cx, cy, cz, lox, loy, loz, sub, lds, b4, n4, tk.worst(), nullptr);
+    const uint32_t T = shell1_table<K, G>(g, qx, qy, qz, lox, loy, loz, sub, lds, b4, n4, tk.worst(), nullptr);
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -799,7 +732,9 @@ __device__ void block_knn_box_flat(const GridDev& g, float qx, float qy, float q
                 const float bd = (axis_gap(qx, xl, xl + w) + axis_gap(qy, yl, yl + w)) + axis_gap(qz, zl, zl + w);
                 if (!(bd * 0.999999f > bound)) {
                     const uint32_t c = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
-                    trim_cell(g, g.rng[c], x, qx, bound, axis_gap(qy, yl, yl + w) + axis_gap(qz, zl, zl + w), b, n);
+                    const uint2 rc = g.rng[c];
+                    b = rc.x;
+                    n = rc.y - rc.x;
                 }
             }
         }

@@ -123,24 +123,6 @@ __global__ void cell_key_kernel(const float4* __restrict__ by_id, int64_t n, Gri
     vals[i] = (uint32_t)i;
 }
 
-// gapped grids: key = cell * kSlabs + x-slice (the points of a cell stored slice by slice); dead ids
-// get the sentinel ncells * kSlabs
-__global__ void cell_slab_key_kernel(const float4* __restrict__ by_id, int64_t n, GridGeom g, uint32_t* __restrict__ keys,
-                                     uint32_t* __restrict__ vals, uint32_t* __restrict__ counts) {
-    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const float4 p = by_id[i];
-    uint32_t k = g.ncells * (uint32_t)kSlabs;
-    if (p.w != 0.f) {
-        const float inv = 1.0f / g.cell;
-        const uint32_t c = cell_key_of(g, inv, p.x, p.y, p.z);
-        k = c * (uint32_t)kSlabs + slab_of(p.x, g.ox, g.cell, inv, (int)(c % (uint32_t)g.nx));
-        atomicAdd(&counts[k], 1u);
-    }
-    keys[i] = k;
-    vals[i] = (uint32_t)i;
-}
-
 __global__ void gather_kernel(const float4* __restrict__ by_id, int64_t n, const uint32_t* __restrict__ sorted_ids,
                               const uint32_t* __restrict__ sorted_keys, float4* __restrict__ pts,
                               uint32_t* __restrict__ ckeys) {
@@ -157,56 +139,48 @@ __global__ void gather_kernel(const float4* __restrict__ by_id, int64_t n, const
 // 0.5 m-downsampled map holds at most 8 downsampled points, map_incremental adds a handful per scan)
 __device__ __forceinline__ uint32_t cell_capacity(uint32_t cnt) { return cnt ? cnt + max(4u, cnt >> 2) : 0u; }
 
-// lim[c] = capacity of cell c (counts from start4, the per (cell, slice) CSR); lim[ncells] = 0 for the
-// scan total
-__global__ void cap_kernel(const uint32_t* __restrict__ start4, uint32_t nc, uint32_t* __restrict__ lim) {
+// lim[c] = capacity of cell c (counts: the dense CSR start[]); lim[ncells] = 0 for the scan total
+__global__ void cap_kernel(const uint32_t* __restrict__ start, uint32_t nc, uint32_t* __restrict__ lim) {
     const uint32_t c = blockIdx.x * 256u + threadIdx.x;
     if (c > nc) return;
-    lim[c] = c < nc ? cell_capacity(start4[kSlabs * (c + 1)] - start4[kSlabs * c]) : 0u;
+    lim[c] = c < nc ? cell_capacity(start[c + 1] - start[c]) : 0u;
 }
 
-// gbase = exclusive scan of the capacities: rng[c] = {gbase[c], gbase[c] + count, slice offsets},
-// lim[c] = gbase[c + 1]
-__global__ void rng_kernel(const uint32_t* __restrict__ start4, const uint32_t* __restrict__ gbase, uint32_t nc,
-                           uint4* __restrict__ rng, uint32_t* __restrict__ lim, uint32_t* __restrict__ bump) {
+// gbase = exclusive scan of the capacities: rng[c] = {gbase[c], gbase[c] + count}, lim[c] = gbase[c + 1]
+__global__ void rng_kernel(const uint32_t* __restrict__ start, const uint32_t* __restrict__ gbase, uint32_t nc,
+                           uint2* __restrict__ rng, uint32_t* __restrict__ lim, uint32_t* __restrict__ bump) {
     const uint32_t c = blockIdx.x * 256u + threadIdx.x;
     if (c >= nc) {
         if (c == nc) *bump = gbase[nc];
         return;
     }
-    const uint32_t b = gbase[c], s0 = start4[kSlabs * c];
-    const uint32_t cnt = start4[kSlabs * (c + 1)] - s0;
-    const uint32_t o1 = start4[kSlabs * c + 1] - s0, o2 = start4[kSlabs * c + 2] - s0, o3 = start4[kSlabs * c + 3] - s0;
-    rng[c] = cnt > kSlabMaxCount ? make_uint4(b, b + cnt, 0u, 1u << 16) : make_uint4(b, b + cnt, o1 | (o2 << 16), o3);
+    const uint32_t b = gbase[c];
+    rng[c] = make_uint2(b, b + (start[c + 1] - start[c]));
     lim[c] = gbase[c + 1];
 }
 
-// sorted entry j of (cell, slice) key -> slot gbase[cell] + (j - start4[kSlabs * cell]): slice by
-// slice, ids ascending inside a slice
+// sorted entry j of cell ck -> slot gbase[ck] + (j - start[ck]) (rank inside the cell kept: id order)
 __global__ void gather_gapped_kernel(const float4* __restrict__ by_id, int64_t n, const uint32_t* __restrict__ sorted_ids,
-                                     const uint32_t* __restrict__ sorted_keys, const uint32_t* __restrict__ start4,
-                                     const uint4* __restrict__ rng, float4* __restrict__ pts) {
+                                     const uint32_t* __restrict__ sorted_keys, const uint32_t* __restrict__ start,
+                                     const uint2* __restrict__ rng, float4* __restrict__ pts) {
     const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (j >= n) return;
-    const uint32_t id = sorted_ids[j], ck = sorted_keys[j] / (uint32_t)kSlabs;
+    const uint32_t id = sorted_ids[j], ck = sorted_keys[j];
     const float4 p = by_id[id];
-    pts[rng[ck].x + (uint32_t)(j - start4[kSlabs * ck])] = make_float4(p.x, p.y, p.z, __int_as_float((int)id));
+    pts[rng[ck].x + (uint32_t)(j - start[ck])] = make_float4(p.x, p.y, p.z, __int_as_float((int)id));
 }
 
 // one lane per listed cell (grid-stride): drop the entries marked dead (id bits kNone), keep the
-// order (so the slices stay in place; their offsets shrink by the dead entries before them), clear
-// the cell's dirty byte
-__global__ void compact_cells_kernel(float4* __restrict__ pts, uint4* __restrict__ rng, uint8_t* __restrict__ dirty,
+// order, clear the cell's dirty byte
+__global__ void compact_cells_kernel(float4* __restrict__ pts, uint2* __restrict__ rng, uint8_t* __restrict__ dirty,
                                      const uint32_t* __restrict__ dlist, const uint32_t* __restrict__ d_ndirty,
                                      uint32_t dcap) {
     const uint32_t nd = min(*d_ndirty, dcap);
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nd; k += gridDim.x * blockDim.x) {
         const uint32_t c = dlist[k];
-        const uint4 r = rng[c];
-        const bool trimmed = (r.w >> 16) == 0u;
-        uint32_t o = r.x, live[kSlabs] = {0u, 0u, 0u, 0u};
-        int sl = 0;
-        for (uint32_t j0 = r.x; j0 < r.y; j0 += 4) {  // four loads in flight (stores only go below j0)
+        const uint2 r = rng[c];
+        uint32_t o = r.x;
+        for (uint32_t j0 = r.x; j0 < r.y; j0 += 4) {  // four loads in flight (the stores only go below them)
             float4 p4[4];
 #pragma unroll
             for (int u = 0; u < 4; ++u) p4[u] = pts[min(j0 + (uint32_t)u, r.y - 1)];
@@ -214,15 +188,12 @@ __global__ void compact_cells_kernel(float4* __restrict__ pts, uint4* __restrict
             for (int u = 0; u < 4; ++u) {
                 const uint32_t j = j0 + (uint32_t)u;
                 if (j >= r.y) break;
-                while (trimmed && sl < kSlabs - 1 && j - r.x >= slab_off(r, sl + 1)) ++sl;
                 if (__float_as_int(p4[u].w) == kNone) continue;
                 if (o != j) pts[o] = p4[u];
                 ++o;
-                ++live[sl];
             }
         }
-        const uint32_t o1 = live[0], o2 = o1 + live[1], o3 = o2 + live[2];
-        rng[c] = trimmed ? make_uint4(r.x, o, o1 | (o2 << 16), o3) : make_uint4(r.x, o, 0u, 1u << 16);
+        rng[c].y = o;
         dirty[c] = 0;
     }
 }
@@ -245,8 +216,8 @@ __global__ void insert_rank_kernel(const float4* __restrict__ by_id, int64_t id0
 }
 
 // one lane per touched cell: room for its new points (a bigger block from the pool when the cell's is
-// full: the live points move in order, the old block is left behind); addc[c] becomes the first new slot
-__global__ void insert_alloc_kernel(float4* __restrict__ pts, uint4* __restrict__ rng, uint32_t* __restrict__ lim,
+// full: the live points move, the old block is left behind); addc[c] becomes the first new slot
+__global__ void insert_alloc_kernel(float4* __restrict__ pts, uint2* __restrict__ rng, uint32_t* __restrict__ lim,
                                     uint32_t* __restrict__ addc, const uint32_t* __restrict__ tlist,
                                     const uint32_t* __restrict__ d_ntouch, uint32_t* __restrict__ bump,
                                     uint32_t slots_cap, uint32_t* __restrict__ flags) {
@@ -254,7 +225,7 @@ __global__ void insert_alloc_kernel(float4* __restrict__ pts, uint4* __restrict_
     if (k >= *d_ntouch) return;
     const uint32_t c = tlist[k];
     const uint32_t add = addc[c];
-    uint4 r = rng[c];
+    uint2 r = rng[c];
     const uint32_t live = r.y - r.x;
     if (r.y + add > lim[c]) {
         const uint32_t cap = max(8u, 2u * (live + add));
@@ -264,14 +235,19 @@ __global__ void insert_alloc_kernel(float4* __restrict__ pts, uint4* __restrict_
             addc[c] = 0xffffffffu;
             return;
         }
-        for (uint32_t j = 0; j < live; ++j) pts[base + j] = pts[r.x + j];
-        r.x = base;
-        r.y = base + live;
+        for (uint32_t j0 = 0; j0 < live; j0 += 4) {  // four loads in flight (the new block is disjoint)
+            float4 p4[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) p4[u] = pts[r.x + min(j0 + (uint32_t)u, live - 1)];
+#pragma unroll
+            for (int u = 0; u < 4; ++u)
+                if (j0 + (uint32_t)u < live) pts[base + j0 + (uint32_t)u] = p4[u];
+        }
+        r = make_uint2(base, base + live);
         lim[c] = base + cap;
     }
     addc[c] = r.y;
-    r.y += add;
-    rng[c] = r;  // slice offsets: still those of the old points (insert_slice_kernel files the new ones)
+    rng[c] = make_uint2(r.x, r.y + add);
 }
 
 __global__ void insert_write_kernel(const float4* __restrict__ by_id, int64_t id0, const uint32_t* __restrict__ d_nnew,
@@ -284,41 +260,6 @@ __global__ void insert_write_kernel(const float4* __restrict__ by_id, int64_t id
     const uint32_t id = (uint32_t)(id0 + j);
     const float4 p = by_id[id];
     pts[base + tmp_rank[j]] = make_float4(p.x, p.y, p.z, __int_as_float((int)id));
-}
-
-// one lane per touched cell: the new points (slots [addc[c], rng[c].y)) filed into their x-slices one
-// at a time — the first point of each higher slice moves to that slice's end, the hole this opens
-// moves down to the end of the new point's slice (<= kSlabs - 1 moves per point; order inside a
-// slice is free: every consumer is order-independent)
-__global__ void insert_slice_kernel(float4* __restrict__ pts, uint4* __restrict__ rng, const uint32_t* __restrict__ addc,
-                                    const uint32_t* __restrict__ tlist, const uint32_t* __restrict__ d_ntouch, GridGeom g) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= *d_ntouch) return;
-    const uint32_t c = tlist[k];
-    const uint32_t first = addc[c];
-    if (first == 0xffffffffu) return;
-    uint4 r = rng[c];
-    if ((r.w >> 16) != 0u) return;  // untrimmed cell
-    if (r.y - r.x > kSlabMaxCount) {  // too many points for 16-bit offsets: scanned whole from now on
-        rng[c] = make_uint4(r.x, r.y, 0u, 1u << 16);
-        return;
-    }
-    const int cx = (int)(c % (uint32_t)g.nx);
-    const float inv = 1.0f / g.cell;
-    uint32_t off[kSlabs] = {0u, r.z & 0xffffu, r.z >> 16, r.w & 0xffffu};  // slice starts (relative)
-    for (uint32_t i = first; i < r.y; ++i) {
-        const float4 p = pts[i];
-        const int s = (int)slab_of(p.x, g.ox, g.cell, inv, cx);
-        uint32_t hole = i;
-        for (int q = kSlabs - 1; q > s; --q) {
-            const uint32_t f = r.x + off[q];
-            pts[hole] = pts[f];
-            hole = f;
-            ++off[q];
-        }
-        pts[hole] = p;
-    }
-    rng[c] = make_uint4(r.x, r.y, off[1] | (off[2] << 16), off[3]);
 }
 
 __global__ void insert_clear_kernel(uint32_t* __restrict__ addc, const uint32_t* __restrict__ tlist,
@@ -441,11 +382,9 @@ static int reserve_cells(GridBuf& g, uint32_t nc1) {
     g.addc = nullptr;
     g.dirty = nullptr;
     const uint32_t cap = std::max<uint32_t>(nc1, g.cells_cap + g.cells_cap / 2);
-    // start[] (+ the histogram scratch behind it): per cell, or per (cell, x-slice) for gapped grids
-    const size_t per = g.gapped ? (size_t)kSlabs : 1u;
-    HIPCHK(hipMalloc(&g.start, 2 * (per * cap + 1) * sizeof(uint32_t)));
+    HIPCHK(hipMalloc(&g.start, 2 * (size_t)cap * sizeof(uint32_t)));  // + histogram scratch
     if (g.gapped) {
-        HIPCHK(hipMalloc(&g.rng, (size_t)cap * sizeof(uint4)));
+        HIPCHK(hipMalloc(&g.rng, (size_t)cap * sizeof(uint2)));
         HIPCHK(hipMalloc(&g.lim, (size_t)cap * sizeof(uint32_t)));
         HIPCHK(hipMalloc(&g.addc, (size_t)cap * sizeof(uint32_t)));
         HIPCHK(hipMalloc(&g.dirty, (size_t)cap + 4));  // + 4: flagged through 32-bit words
@@ -522,25 +461,17 @@ int grid_rebuild(GridBuf& g, float cell, float slack, hipStream_t st) {
     const uint32_t nc1 = geo.ncells + 1;
     rc = reserve_cells(g, nc1);
     if (rc) return rc;
-    // keys: the cell, or (gapped) the (cell, x-slice) pair; nk1 = keys + 1 (the scan's total)
-    const uint32_t per = g.gapped ? (uint32_t)kSlabs : 1u;
-    const uint64_t nkeys = (uint64_t)geo.ncells * per;
-    if (nkeys >= 0xffffffffull) return -1;
-    const uint32_t nk1 = (uint32_t)nkeys + 1;
-    uint32_t* counts = g.start + ((size_t)per * g.cells_cap + 1);
-    HIPCHK(hipMemsetAsync(counts, 0, (size_t)nk1 * sizeof(uint32_t), st));
+    uint32_t* counts = g.start + g.cells_cap;
+    HIPCHK(hipMemsetAsync(counts, 0, (size_t)nc1 * sizeof(uint32_t), st));
     const int nb = (int)std::max<int64_t>(1, (n_ids + 255) / 256);
-    if (n_ids) {
-        if (g.gapped) cell_slab_key_kernel<<<nb, 256, 0, st>>>(g.by_id, n_ids, geo, g.keys, g.vals, counts);
-        else cell_key_kernel<<<nb, 256, 0, st>>>(g.by_id, n_ids, geo, g.keys, g.vals, counts);
-    }
-    // ---- sort (key, id): stable, so ids ascend inside a cell (slice); dead ids (key nkeys) last
+    if (n_ids) cell_key_kernel<<<nb, 256, 0, st>>>(g.by_id, n_ids, geo, g.keys, g.vals, counts);
+    // ---- sort (key, id): stable, so ids ascend inside a cell; dead ids (key ncells) last
     int bits = 1;
-    while (bits < 32 && ((uint64_t)1 << bits) <= nkeys) ++bits;
+    while (bits < 32 && ((uint64_t)1 << bits) <= (uint64_t)geo.ncells) ++bits;
     size_t sort_bytes = 0, scan_bytes = 0;
     HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, g.keys, g.keys_alt, g.vals, g.vals_alt,
                                               (int)std::max<int64_t>(n_ids, 1), 0, bits, st));
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, counts, g.start, (int)nk1, st));
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, counts, g.start, (int)nc1, st));
     size_t need = std::max(sort_bytes, scan_bytes);
     if (ensure(&g.tmp, g.tmp_bytes, need) != 0) return -5;
     size_t tb = g.tmp_bytes;
@@ -548,7 +479,7 @@ int grid_rebuild(GridBuf& g, float cell, float slack, hipStream_t st) {
         HIPCHK(hipcub::DeviceRadixSort::SortPairs(g.tmp, tb, g.keys, g.keys_alt, g.vals, g.vals_alt, (int)n_ids, 0,
                                                   bits, st));
     tb = g.tmp_bytes;
-    HIPCHK(hipcub::DeviceScan::ExclusiveSum(g.tmp, tb, counts, g.start, (int)nk1, st));
+    HIPCHK(hipcub::DeviceScan::ExclusiveSum(g.tmp, tb, counts, g.start, (int)nc1, st));
     if (!g.gapped) {
         if (n_alive)
             gather_kernel<<<(int)((n_alive + 255) / 256), 256, 0, st>>>(g.by_id, n_alive, g.vals_alt, g.keys_alt,
@@ -600,7 +531,6 @@ void grid_insert_ids(GridBuf& g, int64_t id0, const uint32_t* d_nnew, int n_max,
     insert_alloc_kernel<<<nb, 256, 0, st>>>(g.pts, g.rng, g.lim, g.addc, s.tlist, s.d_ntouch, g.bump,
                                             (uint32_t)std::min<int64_t>(g.slots_cap, 0xffffffffll), flags);
     insert_write_kernel<<<nb, 256, 0, st>>>(g.by_id, id0, d_nnew, s.tmp_cell, s.tmp_rank, g.addc, g.pts);
-    insert_slice_kernel<<<nb, 256, 0, st>>>(g.pts, g.rng, g.addc, s.tlist, s.d_ntouch, g.geom);
     insert_clear_kernel<<<nb, 256, 0, st>>>(g.addc, s.tlist, s.d_ntouch);
 }
 

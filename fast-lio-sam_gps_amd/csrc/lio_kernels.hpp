@@ -78,7 +78,7 @@ struct GridBuf {
     GridGeom geom{};
     // gapped (map) grids
     bool gapped = false;
-    uint4* rng = nullptr;        // ncells: live slots of each cell + x-slice offsets (lio_dev.hpp kSlabs)
+    uint2* rng = nullptr;        // ncells: live slots of each cell
     uint32_t* lim = nullptr;     // ncells + 1: end of each cell's block
     uint32_t* addc = nullptr;    // ncells: per-cell insert counter (zero between updates)
     uint8_t* dirty = nullptr;    // ncells: cell holds deleted entries this update (zero between updates)

@@ -187,7 +187,7 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
         for (int z = cr.z0; z <= cr.z1; ++z)
             for (int y = cr.y0; y <= cr.y1; ++y)
                 for (int x = cr.x0; x <= cr.x1; ++x) {
-                    const uint4 r = g.rng[((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x];
+                    const uint2 r = g.rng[((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x];
                     for (uint32_t k0 = r.x; k0 < r.y; k0 += 4) {
                         float4 p4[4];
 #pragma unroll
@@ -213,20 +213,36 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
         // replay the voxel's new points in input order
         int surv_new = -1;
         float sx = bx, sy = by, sz = bz, sd = cnt_e > 0 ? __uint_as_float((uint32_t)(best >> 32)) : INFINITY;
-        for (int e = s0; e < s1; ++e) {
-            const int i = (int)sval2[e];
-            const float qx = xyz[3 * i], qy = xyz[3 * i + 1], qz = xyz[3 * i + 2];
-            const float qd = calc_dist(qx, qy, qz, b.mid[0], b.mid[1], b.mid[2]);
-            const int size_s = e == s0 ? cnt_e : 1;
-            const bool q_wins = size_s == 0 || !(sd < qd);
-            if (size_s > 1 || q_wins || same_point(qx, qy, qz, sx, sy, sz)) {
-                ++triggers;
-                if (q_wins) {
-                    surv_new = i;
-                    sx = qx;
-                    sy = qy;
-                    sz = qz;
-                    sd = qd;
+        constexpr int kB = 8;  // a batch of the voxel's points loaded at once (indices, then coordinates)
+        for (int e0 = s0; e0 < s1; e0 += kB) {
+            int ib[kB];
+            float bq[kB][3];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) ib[u] = (int)sval2[min(e0 + u, s1 - 1)];
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                bq[u][0] = xyz[3 * ib[u]];
+                bq[u][1] = xyz[3 * ib[u] + 1];
+                bq[u][2] = xyz[3 * ib[u] + 2];
+            }
+#pragma unroll
+            for (int u = 0; u < kB; ++u) {
+                const int e = e0 + u;
+                if (e >= s1) break;
+                const int i = ib[u];
+                const float qx = bq[u][0], qy = bq[u][1], qz = bq[u][2];
+                const float qd = calc_dist(qx, qy, qz, b.mid[0], b.mid[1], b.mid[2]);
+                const int size_s = e == s0 ? cnt_e : 1;
+                const bool q_wins = size_s == 0 || !(sd < qd);
+                if (size_s > 1 || q_wins || same_point(qx, qy, qz, sx, sy, sz)) {
+                    ++triggers;
+                    if (q_wins) {
+                        surv_new = i;
+                        sx = qx;
+                        sy = qy;
+                        sz = qz;
+                        sd = qd;
+                    }
                 }
             }
         }
@@ -235,7 +251,7 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
                 for (int y = cr.y0; y <= cr.y1; ++y)
                     for (int x = cr.x0; x <= cr.x1; ++x) {
                         const uint32_t c = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
-                        const uint4 r = g.rng[c];
+                        const uint2 r = g.rng[c];
                         bool marked = false;
                         for (uint32_t k0 = r.x; k0 < r.y; k0 += 4) {  // four loads in flight, then the marks
                             float4 p4[4];

@@ -69,6 +69,7 @@ for s in $STEPS; do
              run icp_pmc_valu 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --kernel-trace -d "$OUT/icppmc" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 ;;
     mapt)  run map_timing 400 python scripts/map_incr_timing.py 20 ;;
     mapprof) run map_prof 400 rocprofv3 --kernel-trace --stats -d "$OUT/mapprof" -o run --output-format csv -- python scripts/map_incr_timing.py 20 ;;
+    nearab) run near_ab 600 bash -c 'for r in 1 2; do python scripts/near_ab.py C3 && LIO_GPU_LIB=build_ab/noslab/liblio_gpu.so python scripts/near_ab.py C3 || exit $?; done' ;;
     *) echo "unknown step $s" ;;
     esac
 done
