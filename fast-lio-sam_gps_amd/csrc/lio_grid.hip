@@ -170,31 +170,33 @@ __global__ void gather_gapped_kernel(const float4* __restrict__ by_id, int64_t n
     pts[rng[ck].x + (uint32_t)(j - start[ck])] = make_float4(p.x, p.y, p.z, __int_as_float((int)id));
 }
 
-// one lane per listed cell (grid-stride): drop the entries marked dead (id bits kNone), keep the
-// order, clear the cell's dirty byte
-__global__ void compact_cells_kernel(float4* __restrict__ pts, uint2* __restrict__ rng, uint8_t* __restrict__ dirty,
-                                     const uint32_t* __restrict__ dlist, const uint32_t* __restrict__ d_ndirty,
-                                     uint32_t dcap) {
+// one WAVE per listed cell (grid-stride): drop the entries marked dead (id bits kNone), keep the
+// order (64 entries at a time: ballot + mbcnt give each survivor its slot), clear the cell's dirty byte
+__global__ void __launch_bounds__(256) compact_cells_kernel(float4* __restrict__ pts, uint2* __restrict__ rng,
+                                                            uint8_t* __restrict__ dirty, const uint32_t* __restrict__ dlist,
+                                                            const uint32_t* __restrict__ d_ndirty, uint32_t dcap) {
     const uint32_t nd = min(*d_ndirty, dcap);
-    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < nd; k += gridDim.x * blockDim.x) {
+    const int lane = threadIdx.x & 63;
+    for (uint32_t k = blockIdx.x * 4u + (threadIdx.x >> 6); k < nd; k += gridDim.x * 4u) {  // wave-uniform
         const uint32_t c = dlist[k];
         const uint2 r = rng[c];
         uint32_t o = r.x;
-        for (uint32_t j0 = r.x; j0 < r.y; j0 += 4) {  // four loads in flight (the stores only go below them)
-            float4 p4[4];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) p4[u] = pts[min(j0 + (uint32_t)u, r.y - 1)];
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                const uint32_t j = j0 + (uint32_t)u;
-                if (j >= r.y) break;
-                if (__float_as_int(p4[u].w) == kNone) continue;
-                if (o != j) pts[o] = p4[u];
-                ++o;
-            }
+        for (uint32_t j0 = r.x; j0 < r.y; j0 += 64u) {
+            const uint32_t j = j0 + (uint32_t)lane;
+            float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (j < r.y) p = pts[j];
+            const bool keep = j < r.y && __float_as_int(p.w) != kNone;
+            const uint64_t m = __ballot(keep);
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+            // every lane has its entry in registers before any store: slots below j0 + 64 only
+            __builtin_amdgcn_wave_barrier();
+            if (keep && o + rank != j) pts[o + rank] = p;
+            o += (uint32_t)__popcll(m);
         }
-        rng[c].y = o;
-        dirty[c] = 0;
+        if (lane == 0) {
+            rng[c].y = o;
+            dirty[c] = 0;
+        }
     }
 }
 
@@ -517,8 +519,7 @@ int grid_rebuild(GridBuf& g, float cell, float slack, hipStream_t st) {
 void grid_compact_cells(GridBuf& g, const uint32_t* dlist, const uint32_t* d_ndirty, uint32_t dcap, int n_max,
                         hipStream_t st) {
     if (n_max <= 0) return;
-    compact_cells_kernel<<<std::min(256, (n_max + 255) / 256), 256, 0, st>>>(g.pts, g.rng, g.dirty, dlist, d_ndirty,
-                                                                              dcap);
+    compact_cells_kernel<<<std::min(2048, (n_max + 3) / 4), 256, 0, st>>>(g.pts, g.rng, g.dirty, dlist, d_ndirty, dcap);
 }
 
 void grid_insert_ids(GridBuf& g, int64_t id0, const uint32_t* d_nnew, int n_max, GridInsertScratch s,

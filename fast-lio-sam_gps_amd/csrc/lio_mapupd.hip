@@ -154,7 +154,49 @@ __device__ __forceinline__ CellRange box_cells(const GridDev& g, const VoxBox& b
     return r;
 }
 
-// One lane per voxel: Add_Points' sequence for the voxel's points (input order) against the alive
+// wave scans for vox_resolve_kernel (64 lanes)
+__device__ __forceinline__ float wave_excl_min(float v, float init) {  // min(init, v of lanes below)
+    const int lane = threadIdx.x & 63;
+    float x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const float y = __shfl_up(x, off, 64);
+        if (lane >= off) x = fminf(x, y);
+    }
+    const float ex = __shfl_up(x, 1, 64);
+    return lane == 0 ? init : fminf(ex, init);
+}
+__device__ __forceinline__ int wave_excl_max(int v) {  // max(-1, v of lanes below)
+    const int lane = threadIdx.x & 63;
+    int x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(x, off, 64);
+        if (lane >= off) x = max(x, y);
+    }
+    const int ex = __shfl_up(x, 1, 64);
+    return lane == 0 ? -1 : ex;
+}
+__device__ __forceinline__ float wave_min_f(float v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v = fminf(v, __shfl_xor(v, off, 64));
+    return v;
+}
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long o = __shfl_xor(v, off, 64);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+__device__ __forceinline__ int wave_sum_i(int v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// One WAVE per voxel: Add_Points' sequence for the voxel's points (input order) against the alive
 // map points in its box [U] (oracle DynMap::add_points):
 //   S := map points in the box; for each new point q:
 //     winner = q unless some s in S has calc_dist(s, mid) < calc_dist(q, mid) (strict: among equal
@@ -164,88 +206,86 @@ __device__ __forceinline__ CellRange box_cells(const GridDev& g, const VoxBox& b
 // bit cleared, its grid slot marked (id bits kNone) for grid_compact_cells, its cell listed once),
 // and add_flag marks the new point that survives (at most one per voxel).  The table slot is reset
 // for the next call.  The voxel's points are sval2[hhead .. hend), ascending input indices.
+// The lanes stride the box's cells (count, nearest map point, tombstones), and the sequence runs 64
+// points at a time as scans: q wins iff !(running minimum before it < its distance), the running
+// minimum is a prefix min, the winner q is compared with (same_point) is the last earlier winner
+// (a prefix max of winner positions), the survivor is the last winner — the sequential result.
 __global__ void __launch_bounds__(256) vox_resolve_kernel(
     const uint32_t* __restrict__ vlist, unsigned long long* __restrict__ hkey, int* __restrict__ hhead,
     const int* __restrict__ hend, const uint32_t* __restrict__ sval2, const float* __restrict__ xyz, float ds, GridDev g,
     int grid_n, float4* __restrict__ pts, float4* __restrict__ by_id, uint8_t* __restrict__ dirty,
     uint32_t* __restrict__ dlist, uint32_t dcap, uint32_t* __restrict__ cnt, uint32_t* __restrict__ add_flag) {
-    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t triggers = 0, dead = 0;
-    if (v < cnt[kCVox] && hhead[vlist[v]] >= 0) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t nvox = cnt[kCVox];
+    for (uint32_t v = blockIdx.x * 4u + (threadIdx.x >> 6); v < nvox; v += gridDim.x * 4u) {  // wave-uniform
         const uint32_t h = vlist[v];
         const int s0 = hhead[h], s1 = hend[h];
-        hkey[h] = kEmptyKey;  // the table is clean again for the next call
-        hhead[h] = -1;
+        if (s0 < 0) continue;
         const int first_i = (int)sval2[s0];
         const VoxBox b = vox_box(xyz[3 * first_i], xyz[3 * first_i + 1], xyz[3 * first_i + 2], ds);
         const CellRange cr = box_cells(g, b, grid_n);
-        // map points in the box: how many, and the nearest to the centre (lowest id among equals);
-        // loads four at a time (independent of the running minimum)
-        int cnt_e = 0;
-        unsigned long long best = ~0ull;
-        float bx = 0.f, by = 0.f, bz = 0.f;
+        // map points in the box: how many, and the nearest to the centre (lowest id among equals)
+        int cnt_l = 0;
+        unsigned long long best_l = ~0ull;
         for (int z = cr.z0; z <= cr.z1; ++z)
             for (int y = cr.y0; y <= cr.y1; ++y)
                 for (int x = cr.x0; x <= cr.x1; ++x) {
                     const uint2 r = g.rng[((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x];
-                    for (uint32_t k0 = r.x; k0 < r.y; k0 += 4) {
-                        float4 p4[4];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) p4[u] = pts[min(k0 + (uint32_t)u, r.y - 1)];
-#pragma unroll
-                        for (int u = 0; u < 4; ++u) {
-                            const float4 p = p4[u];
-                            if (k0 + (uint32_t)u >= r.y || !in_box(b, p.x, p.y, p.z)) continue;
-                            ++cnt_e;
-                            const float t = calc_dist(p.x, p.y, p.z, b.mid[0], b.mid[1], b.mid[2]);
-                            const unsigned long long kk =
-                                ((unsigned long long)__float_as_uint(t) << 32) | (uint32_t)__float_as_int(p.w);
-                            if (kk < best) {
-                                best = kk;
-                                bx = p.x;
-                                by = p.y;
-                                bz = p.z;
-                            }
-                        }
+                    for (uint32_t k = r.x + (uint32_t)lane; k < r.y; k += 64u) {
+                        const float4 p = pts[k];
+                        if (!in_box(b, p.x, p.y, p.z)) continue;
+                        ++cnt_l;
+                        const float t = calc_dist(p.x, p.y, p.z, b.mid[0], b.mid[1], b.mid[2]);
+                        const unsigned long long kk =
+                            ((unsigned long long)__float_as_uint(t) << 32) | (uint32_t)__float_as_int(p.w);
+                        best_l = kk < best_l ? kk : best_l;
                     }
                 }
+        const int cnt_e = wave_sum_i(cnt_l);
+        const unsigned long long best = wave_min_u64(best_l);
         const int best_id = cnt_e > 0 ? (int)(uint32_t)best : -1;
-        // replay the voxel's new points in input order
-        int surv_new = -1;
-        float sx = bx, sy = by, sz = bz, sd = cnt_e > 0 ? __uint_as_float((uint32_t)(best >> 32)) : INFINITY;
-        constexpr int kB = 8;  // a batch of the voxel's points loaded at once (indices, then coordinates)
-        for (int e0 = s0; e0 < s1; e0 += kB) {
-            int ib[kB];
-            float bq[kB][3];
-#pragma unroll
-            for (int u = 0; u < kB; ++u) ib[u] = (int)sval2[min(e0 + u, s1 - 1)];
-#pragma unroll
-            for (int u = 0; u < kB; ++u) {
-                bq[u][0] = xyz[3 * ib[u]];
-                bq[u][1] = xyz[3 * ib[u] + 1];
-                bq[u][2] = xyz[3 * ib[u] + 2];
-            }
-#pragma unroll
-            for (int u = 0; u < kB; ++u) {
-                const int e = e0 + u;
-                if (e >= s1) break;
-                const int i = ib[u];
-                const float qx = bq[u][0], qy = bq[u][1], qz = bq[u][2];
-                const float qd = calc_dist(qx, qy, qz, b.mid[0], b.mid[1], b.mid[2]);
-                const int size_s = e == s0 ? cnt_e : 1;
-                const bool q_wins = size_s == 0 || !(sd < qd);
-                if (size_s > 1 || q_wins || same_point(qx, qy, qz, sx, sy, sz)) {
-                    ++triggers;
-                    if (q_wins) {
-                        surv_new = i;
-                        sx = qx;
-                        sy = qy;
-                        sz = qz;
-                        sd = qd;
-                    }
-                }
-            }
+        float sx = 0.f, sy = 0.f, sz = 0.f;  // the current winner (the nearest map point first)
+        if (cnt_e > 0) {
+            const float4 bp = by_id[best_id];
+            sx = bp.x;
+            sy = bp.y;
+            sz = bp.z;
         }
+        // the sequence, 64 points at a time
+        float sd = cnt_e > 0 ? __uint_as_float((uint32_t)(best >> 32)) : INFINITY;
+        int surv_new = -1;
+        uint32_t triggers = 0;
+        for (int e0 = s0; e0 < s1; e0 += 64) {
+            const int e = e0 + lane;
+            const bool act = e < s1;
+            int i = 0;
+            float qx = 0.f, qy = 0.f, qz = 0.f, qd = INFINITY;
+            if (act) {
+                i = (int)sval2[e];
+                qx = xyz[3 * i];
+                qy = xyz[3 * i + 1];
+                qz = xyz[3 * i + 2];
+                qd = calc_dist(qx, qy, qz, b.mid[0], b.mid[1], b.mid[2]);
+            }
+            const float before = wave_excl_min(act ? qd : INFINITY, sd);
+            const bool wins = act && !(before < qd);
+            const int lw = wave_excl_max(wins ? lane : -1);  // last winner lane below this one
+            const int src = lw < 0 ? 0 : lw;
+            const float wx = __shfl(qx, src, 64), wy = __shfl(qy, src, 64), wz = __shfl(qz, src, 64);
+            const bool tr = act && ((e == s0 && cnt_e > 1) || wins ||
+                                    same_point(qx, qy, qz, lw < 0 ? sx : wx, lw < 0 ? sy : wy, lw < 0 ? sz : wz));
+            triggers += (uint32_t)__popcll(__ballot(tr));
+            const unsigned long long wm = __ballot(wins);
+            if (wm) {
+                const int last = 63 - __clzll((long long)wm);
+                sx = __shfl(qx, last, 64);
+                sy = __shfl(qy, last, 64);
+                sz = __shfl(qz, last, 64);
+                surv_new = __shfl(i, last, 64);
+            }
+            sd = fminf(sd, wave_min_f(act ? qd : INFINITY));
+        }
+        int dead = 0;
         if (cnt_e > 0 && (surv_new >= 0 || cnt_e > 1)) {
             for (int z = cr.z0; z <= cr.z1; ++z)
                 for (int y = cr.y0; y <= cr.y1; ++y)
@@ -253,23 +293,17 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
                         const uint32_t c = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
                         const uint2 r = g.rng[c];
                         bool marked = false;
-                        for (uint32_t k0 = r.x; k0 < r.y; k0 += 4) {  // four loads in flight, then the marks
-                            float4 p4[4];
-#pragma unroll
-                            for (int u = 0; u < 4; ++u) p4[u] = pts[min(k0 + (uint32_t)u, r.y - 1)];
-#pragma unroll
-                            for (int u = 0; u < 4; ++u) {
-                                const float4 p = p4[u];
-                                if (k0 + (uint32_t)u >= r.y || !in_box(b, p.x, p.y, p.z)) continue;
-                                const int id = __float_as_int(p.w);
-                                if (surv_new < 0 && id == best_id) continue;
-                                by_id[id].w = 0.f;
-                                pts[k0 + (uint32_t)u].w = __int_as_float(kNone);
-                                ++dead;
-                                marked = true;
-                            }
+                        for (uint32_t k = r.x + (uint32_t)lane; k < r.y; k += 64u) {
+                            const float4 p = pts[k];
+                            if (!in_box(b, p.x, p.y, p.z)) continue;
+                            const int id = __float_as_int(p.w);
+                            if (surv_new < 0 && id == best_id) continue;
+                            by_id[id].w = 0.f;
+                            pts[k].w = __int_as_float(kNone);
+                            ++dead;
+                            marked = true;
                         }
-                        if (marked) {  // list the cell once: the lane that sets its dirty byte
+                        if (__ballot(marked) && lane == 0) {  // list the cell once: the wave that sets its dirty byte
                             unsigned int* wp = reinterpret_cast<unsigned int*>(dirty + (c & ~3u));
                             const unsigned int bit = 1u << (8u * (c & 3u));
                             if (!(atomicOr(wp, bit) & bit)) {
@@ -280,16 +314,14 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
                         }
                     }
         }
-        if (surv_new >= 0) add_flag[surv_new] = 1u;
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {  // one atomic per wave (every lane reaches here)
-        triggers += __shfl_xor(triggers, off, 64);
-        dead += __shfl_xor(dead, off, 64);
-    }
-    if ((threadIdx.x & 63) == 0) {
-        if (triggers) atomicAdd(&cnt[kCTrig], triggers);
-        if (dead) atomicAdd(&cnt[kCDead], dead);
+        dead = wave_sum_i(dead);
+        if (lane == 0) {
+            if (surv_new >= 0) add_flag[surv_new] = 1u;
+            if (triggers) atomicAdd(&cnt[kCTrig], triggers);
+            if (dead) atomicAdd(&cnt[kCDead], (uint32_t)dead);
+            hkey[h] = kEmptyKey;  // the table is clean again for the next call
+            hhead[h] = -1;
+        }
     }
 }
 
@@ -584,7 +616,7 @@ int enqueue_add(GridBuf& g, MapUpdBuf& u, const float* xyz, int n_max, const flo
                                                    u.hbits + 1, st));
     }
     vox_runs_kernel<<<nb, 256, 0, st>>>(u.skey2, n_max, u.hcap - 1, u.hhead, u.hend);
-    vox_resolve_kernel<<<nb, 256, 0, st>>>(u.vlist, u.hkey, u.hhead, u.hend, u.sval2, xyz, ds, grid_view(g), (int)g.n, g.pts,
+    vox_resolve_kernel<<<std::min(2048, (n_max + 3) / 4), 256, 0, st>>>(u.vlist, u.hkey, u.hhead, u.hend, u.sval2, xyz, ds, grid_view(g), (int)g.n, g.pts,
                                            g.by_id, g.dirty, u.dlist, (uint32_t)(u.cap * 27), u.cnt, u.add_flag);
     int rc = exclusive_scan(u, u.add_flag, u.pos, n_max + 1, st);
     if (rc) return rc;
