@@ -220,13 +220,38 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
     for (uint32_t v = blockIdx.x * 4u + (threadIdx.x >> 6); v < nvox; v += gridDim.x * 4u) {  // wave-uniform
         const uint32_t h = vlist[v];
         const int s0 = hhead[h], s1 = hend[h];
+        const unsigned long long vkey = hkey[h];
         if (s0 < 0) continue;
-        const int first_i = (int)sval2[s0];
-        const VoxBox b = vox_box(xyz[3 * first_i], xyz[3 * first_i + 1], xyz[3 * first_i + 2], ds);
+        // the first chunk of the voxel's points, loaded while the map side runs
+        int i = 0;
+        float qx = 0.f, qy = 0.f, qz = 0.f;
+        if (s0 + lane < s1) {
+            i = (int)sval2[s0 + lane];
+            qx = xyz[3 * i];
+            qy = xyz[3 * i + 1];
+            qz = xyz[3 * i + 2];
+        }
+        // the box from the voxel key (floor(p / ds) per axis, vox_box's own values) unless an axis was
+        // clamped in the key: then from the voxel's first point, as before
+        VoxBox b;
+        bool clamped = false;
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            const int idx = (int)((vkey >> (kVoxBits * (2 - d))) & ((1ull << kVoxBits) - 1)) - kVoxOff;
+            clamped |= idx <= -kVoxOff || idx >= kVoxOff - 1;
+            b.lo[d] = (float)idx * ds;
+            b.hi[d] = b.lo[d] + ds;
+            b.mid[d] = (float)((double)b.lo[d] + (double)(b.hi[d] - b.lo[d]) / 2.0);
+        }
+        if (clamped) {
+            const int first_i = (int)sval2[s0];
+            b = vox_box(xyz[3 * first_i], xyz[3 * first_i + 1], xyz[3 * first_i + 2], ds);
+        }
         const CellRange cr = box_cells(g, b, grid_n);
         // map points in the box: how many, and the nearest to the centre (lowest id among equals)
         int cnt_l = 0;
         unsigned long long best_l = ~0ull;
+        float blx = 0.f, bly = 0.f, blz = 0.f;
         for (int z = cr.z0; z <= cr.z1; ++z)
             for (int y = cr.y0; y <= cr.y1; ++y)
                 for (int x = cr.x0; x <= cr.x1; ++x) {
@@ -238,18 +263,24 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
                         const float t = calc_dist(p.x, p.y, p.z, b.mid[0], b.mid[1], b.mid[2]);
                         const unsigned long long kk =
                             ((unsigned long long)__float_as_uint(t) << 32) | (uint32_t)__float_as_int(p.w);
-                        best_l = kk < best_l ? kk : best_l;
+                        if (kk < best_l) {
+                            best_l = kk;
+                            blx = p.x;
+                            bly = p.y;
+                            blz = p.z;
+                        }
                     }
                 }
         const int cnt_e = wave_sum_i(cnt_l);
         const unsigned long long best = wave_min_u64(best_l);
         const int best_id = cnt_e > 0 ? (int)(uint32_t)best : -1;
         float sx = 0.f, sy = 0.f, sz = 0.f;  // the current winner (the nearest map point first)
-        if (cnt_e > 0) {
-            const float4 bp = by_id[best_id];
-            sx = bp.x;
-            sy = bp.y;
-            sz = bp.z;
+        if (cnt_e > 0) {  // from the lane that holds it (keys are unique: (distance, id))
+            const unsigned long long hm = __ballot(best_l == best);
+            const int src = __ffsll((long long)hm) - 1;
+            sx = __shfl(blx, src, 64);
+            sy = __shfl(bly, src, 64);
+            sz = __shfl(blz, src, 64);
         }
         // the sequence, 64 points at a time
         float sd = cnt_e > 0 ? __uint_as_float((uint32_t)(best >> 32)) : INFINITY;
@@ -258,15 +289,17 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
         for (int e0 = s0; e0 < s1; e0 += 64) {
             const int e = e0 + lane;
             const bool act = e < s1;
-            int i = 0;
-            float qx = 0.f, qy = 0.f, qz = 0.f, qd = INFINITY;
-            if (act) {
-                i = (int)sval2[e];
-                qx = xyz[3 * i];
-                qy = xyz[3 * i + 1];
-                qz = xyz[3 * i + 2];
-                qd = calc_dist(qx, qy, qz, b.mid[0], b.mid[1], b.mid[2]);
+            if (e0 != s0) {  // the first chunk was loaded up front
+                i = 0;
+                qx = qy = qz = 0.f;
+                if (act) {
+                    i = (int)sval2[e];
+                    qx = xyz[3 * i];
+                    qy = xyz[3 * i + 1];
+                    qz = xyz[3 * i + 2];
+                }
             }
+            const float qd = act ? calc_dist(qx, qy, qz, b.mid[0], b.mid[1], b.mid[2]) : INFINITY;
             const float before = wave_excl_min(act ? qd : INFINITY, sd);
             const bool wins = act && !(before < qd);
             const int lw = wave_excl_max(wins ? lane : -1);  // last winner lane below this one
