@@ -196,6 +196,54 @@ __device__ __forceinline__ int wave_sum_i(int v) {
     return v;
 }
 
+// The box's cells cb .. cb + 63 (of nbc): lane l loads cell cb + l's range; tb[0 .. 64) range starts,
+// tb[64 .. 129) exclusive offsets (tb[64 + 64] = total).  Returns the round's point count T.
+__device__ __forceinline__ uint32_t box_cell_index(const GridDev& g, const CellRange& cr, int k, int bnx, int bny) {
+    const int x = cr.x0 + k % bnx, y = cr.y0 + (k / bnx) % bny, z = cr.z0 + k / (bnx * bny);
+    return ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
+}
+__device__ __forceinline__ uint32_t box_table(const GridDev& g, const CellRange& cr, int cb, int nbc, int bnx, int bny,
+                                              uint32_t* tb) {
+    const int lane = threadIdx.x & 63;
+    const int k = cb + lane;
+    uint32_t rb = 0, rn = 0;
+    if (k < nbc) {
+        const uint2 r = g.rng[box_cell_index(g, cr, k, bnx, bny)];
+        rb = r.x;
+        rn = r.y - r.x;
+    }
+    uint32_t incl = rn;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(incl, off, 64);
+        if (lane >= off) incl += y;
+    }
+    const uint32_t T = (uint32_t)__shfl(incl, 63, 64);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous round's readers are done
+    __builtin_amdgcn_wave_barrier();
+    tb[lane] = rb;
+    tb[64 + lane] = incl - rn;
+    if (lane == 63) tb[128] = T;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return T;
+}
+// the table entry (box cell of this round) holding concatenated point t: last k with off[k] <= t
+__device__ __forceinline__ int box_cell_of(const uint32_t* tb, uint32_t t) {
+    int lo = 0, hi = 64;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (tb[64 + mid] <= t) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ uint32_t box_slot(const uint32_t* tb, uint32_t t) {
+    const int k = box_cell_of(tb, t);
+    return tb[k] + (t - tb[64 + k]);
+}
+
 // One WAVE per voxel: Add_Points' sequence for the voxel's points (input order) against the alive
 // map points in its box [U] (oracle DynMap::add_points):
 //   S := map points in the box; for each new point q:
@@ -215,6 +263,7 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
     const int* __restrict__ hend, const uint32_t* __restrict__ sval2, const float* __restrict__ xyz, float ds, GridDev g,
     int grid_n, float4* __restrict__ pts, float4* __restrict__ by_id, uint8_t* __restrict__ dirty,
     uint32_t* __restrict__ dlist, uint32_t dcap, uint32_t* __restrict__ cnt, uint32_t* __restrict__ add_flag) {
+    __shared__ uint32_t s_tab[4][2 * 64 + 1 + 64];  // per wave: box-cell table + tombstone flags
     const int lane = threadIdx.x & 63;
     const uint32_t nvox = cnt[kCVox];
     for (uint32_t v = blockIdx.x * 4u + (threadIdx.x >> 6); v < nvox; v += gridDim.x * 4u) {  // wave-uniform
@@ -248,29 +297,32 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
             b = vox_box(xyz[3 * first_i], xyz[3 * first_i + 1], xyz[3 * first_i + 2], ds);
         }
         const CellRange cr = box_cells(g, b, grid_n);
+        // the box's cells (<= 64 handled per round: one per lane), their ranges concatenated through the
+        // wave's LDS table so the lanes stride all the box's map points at once (no per-cell round trips)
+        const int bnx = cr.x1 - cr.x0 + 1, bny = cr.y1 - cr.y0 + 1;
+        const int nbc = cr.x0 > cr.x1 ? 0 : bnx * bny * (cr.z1 - cr.z0 + 1);
+        uint32_t* tb = s_tab[threadIdx.x >> 6];
         // map points in the box: how many, and the nearest to the centre (lowest id among equals)
         int cnt_l = 0;
         unsigned long long best_l = ~0ull;
         float blx = 0.f, bly = 0.f, blz = 0.f;
-        for (int z = cr.z0; z <= cr.z1; ++z)
-            for (int y = cr.y0; y <= cr.y1; ++y)
-                for (int x = cr.x0; x <= cr.x1; ++x) {
-                    const uint2 r = g.rng[((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x];
-                    for (uint32_t k = r.x + (uint32_t)lane; k < r.y; k += 64u) {
-                        const float4 p = pts[k];
-                        if (!in_box(b, p.x, p.y, p.z)) continue;
-                        ++cnt_l;
-                        const float t = calc_dist(p.x, p.y, p.z, b.mid[0], b.mid[1], b.mid[2]);
-                        const unsigned long long kk =
-                            ((unsigned long long)__float_as_uint(t) << 32) | (uint32_t)__float_as_int(p.w);
-                        if (kk < best_l) {
-                            best_l = kk;
-                            blx = p.x;
-                            bly = p.y;
-                            blz = p.z;
-                        }
-                    }
+        for (int cb = 0; cb < nbc; cb += 64) {
+            const uint32_t T = box_table(g, cr, cb, nbc, bnx, bny, tb);
+            for (uint32_t t = (uint32_t)lane; t < T; t += 64u) {
+                const float4 p = pts[box_slot(tb, t)];
+                if (!in_box(b, p.x, p.y, p.z)) continue;
+                ++cnt_l;
+                const float dd = calc_dist(p.x, p.y, p.z, b.mid[0], b.mid[1], b.mid[2]);
+                const unsigned long long kk =
+                    ((unsigned long long)__float_as_uint(dd) << 32) | (uint32_t)__float_as_int(p.w);
+                if (kk < best_l) {
+                    best_l = kk;
+                    blx = p.x;
+                    bly = p.y;
+                    blz = p.z;
                 }
+            }
+        }
         const int cnt_e = wave_sum_i(cnt_l);
         const unsigned long long best = wave_min_u64(best_l);
         const int best_id = cnt_e > 0 ? (int)(uint32_t)best : -1;
@@ -320,32 +372,38 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
         }
         int dead = 0;
         if (cnt_e > 0 && (surv_new >= 0 || cnt_e > 1)) {
-            for (int z = cr.z0; z <= cr.z1; ++z)
-                for (int y = cr.y0; y <= cr.y1; ++y)
-                    for (int x = cr.x0; x <= cr.x1; ++x) {
-                        const uint32_t c = ((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x;
-                        const uint2 r = g.rng[c];
-                        bool marked = false;
-                        for (uint32_t k = r.x + (uint32_t)lane; k < r.y; k += 64u) {
-                            const float4 p = pts[k];
-                            if (!in_box(b, p.x, p.y, p.z)) continue;
-                            const int id = __float_as_int(p.w);
-                            if (surv_new < 0 && id == best_id) continue;
-                            by_id[id].w = 0.f;
-                            pts[k].w = __int_as_float(kNone);
-                            ++dead;
-                            marked = true;
-                        }
-                        if (__ballot(marked) && lane == 0) {  // list the cell once: the wave that sets its dirty byte
-                            unsigned int* wp = reinterpret_cast<unsigned int*>(dirty + (c & ~3u));
-                            const unsigned int bit = 1u << (8u * (c & 3u));
-                            if (!(atomicOr(wp, bit) & bit)) {
-                                const uint32_t slot = atomicAdd(&cnt[kCDirty], 1u);
-                                if (slot < dcap) dlist[slot] = c;
-                                else atomicOr(&cnt[kCFlags], 4u);  // list full: the caller rebuilds the grid
-                            }
-                        }
+            for (int cb = 0; cb < nbc; cb += 64) {
+                const uint32_t T = box_table(g, cr, cb, nbc, bnx, bny, tb);
+                uint32_t* marked = tb + 2 * 64 + 1;  // per box cell of this round: holds a new tombstone
+                marked[lane] = 0u;
+                __builtin_amdgcn_wave_barrier();
+                for (uint32_t t = (uint32_t)lane; t < T; t += 64u) {
+                    const uint32_t slot = box_slot(tb, t);
+                    const float4 p = pts[slot];
+                    if (!in_box(b, p.x, p.y, p.z)) continue;
+                    const int id = __float_as_int(p.w);
+                    if (surv_new < 0 && id == best_id) continue;
+                    by_id[id].w = 0.f;
+                    pts[slot].w = __int_as_float(kNone);
+                    ++dead;
+                    marked[box_cell_of(tb, t)] = 1u;
+                }
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const int kk = cb + lane;
+                if (kk < nbc && marked[lane]) {  // list the cell once: the wave that sets its dirty byte
+                    const uint32_t c = box_cell_index(g, cr, kk, bnx, bny);
+                    unsigned int* wp = reinterpret_cast<unsigned int*>(dirty + (c & ~3u));
+                    const unsigned int bit = 1u << (8u * (c & 3u));
+                    if (!(atomicOr(wp, bit) & bit)) {
+                        const uint32_t sl = atomicAdd(&cnt[kCDirty], 1u);
+                        if (sl < dcap) dlist[sl] = c;
+                        else atomicOr(&cnt[kCFlags], 4u);  // list full: the caller rebuilds the grid
                     }
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
         }
         dead = wave_sum_i(dead);
         if (lane == 0) {
