@@ -127,14 +127,17 @@ __global__ void vox_group_kernel(const float* __restrict__ xyz, float ds, unsign
 }
 
 // the sorted run of each voxel: hhead[slot] = first entry, hend[slot] = one past the last
-__global__ void vox_runs_kernel(const uint32_t* __restrict__ skey2, int n_max, uint32_t hmask, int* __restrict__ hhead,
-                                int* __restrict__ hend) {
+__global__ void vox_runs_kernel(const uint32_t* __restrict__ skey2, const uint32_t* __restrict__ sval2,
+                                const float* __restrict__ xyz, int n_max, uint32_t hmask, int* __restrict__ hhead,
+                                int* __restrict__ hend, float4* __restrict__ xs) {
     const int j = blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= n_max) return;
     const uint32_t k = skey2[j];
     if (k > hmask) return;
     if (j == 0 || skey2[j - 1] != k) hhead[k] = j;
     if (j == n_max - 1 || skey2[j + 1] != k) hend[k] = j + 1;
+    const uint32_t i = sval2[j];  // the point in sorted order: one contiguous 16-B load per point later
+    xs[j] = make_float4(xyz[3 * i], xyz[3 * i + 1], xyz[3 * i + 2], 0.f);
 }
 
 // the cells a box [lo, hi) can touch: a point with lo <= p < hi has its (clamped) cell between the
@@ -154,28 +157,33 @@ __device__ __forceinline__ CellRange box_cells(const GridDev& g, const VoxBox& b
     return r;
 }
 
-// wave scans for vox_resolve_kernel (64 lanes)
+// wave scans for vox_resolve_kernel (64 lanes, DPP: row shifts inside rows of 16, then row_bcast:15 /
+// row_bcast:31 carry the row results forward; lanes without a source keep the identity)
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ float dpp_id_f(float v, float id) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(id), __float_as_int(v), CTRL, ROWS, 0xf, false));
+}
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ int dpp_id_i(int v, int id) {
+    return __builtin_amdgcn_update_dpp(id, v, CTRL, ROWS, 0xf, false);
+}
 __device__ __forceinline__ float wave_excl_min(float v, float init) {  // min(init, v of lanes below)
-    const int lane = threadIdx.x & 63;
-    float x = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const float y = __shfl_up(x, off, 64);
-        if (lane >= off) x = fminf(x, y);
-    }
-    const float ex = __shfl_up(x, 1, 64);
-    return lane == 0 ? init : fminf(ex, init);
+    v = fminf(v, dpp_id_f<0x111>(v, INFINITY));  // row_shr:1
+    v = fminf(v, dpp_id_f<0x112>(v, INFINITY));  // row_shr:2
+    v = fminf(v, dpp_id_f<0x114>(v, INFINITY));  // row_shr:4
+    v = fminf(v, dpp_id_f<0x118>(v, INFINITY));  // row_shr:8
+    v = fminf(v, dpp_id_f<0x142, 0xa>(v, INFINITY));  // row_bcast:15
+    v = fminf(v, dpp_id_f<0x143, 0xc>(v, INFINITY));  // row_bcast:31
+    return fminf(dpp_id_f<0x138>(v, INFINITY), init);  // wave_shr:1 -> exclusive
 }
 __device__ __forceinline__ int wave_excl_max(int v) {  // max(-1, v of lanes below)
-    const int lane = threadIdx.x & 63;
-    int x = v;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(x, off, 64);
-        if (lane >= off) x = max(x, y);
-    }
-    const int ex = __shfl_up(x, 1, 64);
-    return lane == 0 ? -1 : ex;
+    v = max(v, dpp_id_i<0x111>(v, -1));
+    v = max(v, dpp_id_i<0x112>(v, -1));
+    v = max(v, dpp_id_i<0x114>(v, -1));
+    v = max(v, dpp_id_i<0x118>(v, -1));
+    v = max(v, dpp_id_i<0x142, 0xa>(v, -1));
+    v = max(v, dpp_id_i<0x143, 0xc>(v, -1));
+    return dpp_id_i<0x138>(v, -1);
 }
 __device__ __forceinline__ float wave_min_f(float v) {
 #pragma unroll
@@ -260,7 +268,8 @@ __device__ __forceinline__ uint32_t box_slot(const uint32_t* tb, uint32_t t) {
 // (a prefix max of winner positions), the survivor is the last winner — the sequential result.
 __global__ void __launch_bounds__(256) vox_resolve_kernel(
     const uint32_t* __restrict__ vlist, unsigned long long* __restrict__ hkey, int* __restrict__ hhead,
-    const int* __restrict__ hend, const uint32_t* __restrict__ sval2, const float* __restrict__ xyz, float ds, GridDev g,
+    const int* __restrict__ hend, const uint32_t* __restrict__ sval2, const float4* __restrict__ xs,
+    const float* __restrict__ xyz, float ds, GridDev g,
     int grid_n, float4* __restrict__ pts, float4* __restrict__ by_id, uint8_t* __restrict__ dirty,
     uint32_t* __restrict__ dlist, uint32_t dcap, uint32_t* __restrict__ cnt, uint32_t* __restrict__ add_flag) {
     __shared__ uint32_t s_tab[4][2 * 64 + 1 + 64];  // per wave: box-cell table + tombstone flags
@@ -272,14 +281,8 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
         const unsigned long long vkey = hkey[h];
         if (s0 < 0) continue;
         // the first chunk of the voxel's points, loaded while the map side runs
-        int i = 0;
-        float qx = 0.f, qy = 0.f, qz = 0.f;
-        if (s0 + lane < s1) {
-            i = (int)sval2[s0 + lane];
-            qx = xyz[3 * i];
-            qy = xyz[3 * i + 1];
-            qz = xyz[3 * i + 2];
-        }
+        float4 q = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (s0 + lane < s1) q = xs[s0 + lane];
         // the box from the voxel key (floor(p / ds) per axis, vox_box's own values) unless an axis was
         // clamped in the key: then from the voxel's first point, as before
         VoxBox b;
@@ -334,25 +337,18 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
             sy = __shfl(bly, src, 64);
             sz = __shfl(blz, src, 64);
         }
-        // the sequence, 64 points at a time
+        // the sequence, 64 points at a time (the next chunk's load issued before this chunk's scans)
         float sd = cnt_e > 0 ? __uint_as_float((uint32_t)(best >> 32)) : INFINITY;
-        int surv_new = -1;
+        int surv_pos = -1;  // sorted position of the last new winner
         uint32_t triggers = 0;
         for (int e0 = s0; e0 < s1; e0 += 64) {
             const int e = e0 + lane;
             const bool act = e < s1;
-            if (e0 != s0) {  // the first chunk was loaded up front
-                i = 0;
-                qx = qy = qz = 0.f;
-                if (act) {
-                    i = (int)sval2[e];
-                    qx = xyz[3 * i];
-                    qy = xyz[3 * i + 1];
-                    qz = xyz[3 * i + 2];
-                }
-            }
+            float4 qn = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (e + 64 < s1) qn = xs[e + 64];
+            const float qx = q.x, qy = q.y, qz = q.z;
             const float qd = act ? calc_dist(qx, qy, qz, b.mid[0], b.mid[1], b.mid[2]) : INFINITY;
-            const float before = wave_excl_min(act ? qd : INFINITY, sd);
+            const float before = wave_excl_min(qd, sd);
             const bool wins = act && !(before < qd);
             const int lw = wave_excl_max(wins ? lane : -1);  // last winner lane below this one
             const int src = lw < 0 ? 0 : lw;
@@ -366,10 +362,12 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
                 sx = __shfl(qx, last, 64);
                 sy = __shfl(qy, last, 64);
                 sz = __shfl(qz, last, 64);
-                surv_new = __shfl(i, last, 64);
+                surv_pos = e0 + last;
             }
-            sd = fminf(sd, wave_min_f(act ? qd : INFINITY));
+            sd = fminf(sd, wave_min_f(qd));
+            q = qn;
         }
+        const int surv_new = surv_pos >= 0 ? (int)sval2[surv_pos] : -1;
         int dead = 0;
         if (cnt_e > 0 && (surv_new >= 0 || cnt_e > 1)) {
             for (int cb = 0; cb < nbc; cb += 64) {
@@ -633,7 +631,7 @@ int ensure_pts(MapUpdBuf& u, int64_t n, hipStream_t st) {
     if (n <= u.cap && u.world) return 0;
     const int64_t c = std::max<int64_t>(n, u.cap + u.cap / 2);
     void* bufs[] = {u.f64,   u.pos64, u.add_flag, u.pos,      u.cls,      u.world,    u.xyz_a, u.xyz_b, u.pending,
-                    u.skey,  u.sval,  u.skey2,    u.sval2,    u.vlist,    u.dlist,    u.tmp_cell, u.tmp_rank,
+                    u.skey,  u.sval,  u.skey2,    u.sval2,    u.xs,       u.vlist,    u.dlist,    u.tmp_cell, u.tmp_rank,
                     u.tlist, u.hkey,  u.hhead,    u.hend};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
@@ -650,6 +648,7 @@ int ensure_pts(MapUpdBuf& u, int64_t n, hipStream_t st) {
     UPD_CHK(hipMalloc(&u.sval, c * sizeof(uint32_t)));
     UPD_CHK(hipMalloc(&u.skey2, c * sizeof(uint32_t)));
     UPD_CHK(hipMalloc(&u.sval2, c * sizeof(uint32_t)));
+    UPD_CHK(hipMalloc(&u.xs, c * sizeof(float4)));
     UPD_CHK(hipMalloc(&u.vlist, c * sizeof(uint32_t)));
     UPD_CHK(hipMalloc(&u.dlist, c * 27 * sizeof(uint32_t)));  // dirty cells: <= 27 per voxel box at any cell size
     UPD_CHK(hipMalloc(&u.tmp_cell, c * sizeof(uint32_t)));
@@ -706,8 +705,8 @@ int enqueue_add(GridBuf& g, MapUpdBuf& u, const float* xyz, int n_max, const flo
         UPD_CHK(hipcub::DeviceRadixSort::SortPairs(u.tmp, bytes, u.skey, u.skey2, u.sval, u.sval2, n_max, 0,
                                                    u.hbits + 1, st));
     }
-    vox_runs_kernel<<<nb, 256, 0, st>>>(u.skey2, n_max, u.hcap - 1, u.hhead, u.hend);
-    vox_resolve_kernel<<<std::min(2048, (n_max + 3) / 4), 256, 0, st>>>(u.vlist, u.hkey, u.hhead, u.hend, u.sval2, xyz, ds, grid_view(g), (int)g.n, g.pts,
+    vox_runs_kernel<<<nb, 256, 0, st>>>(u.skey2, u.sval2, xyz, n_max, u.hcap - 1, u.hhead, u.hend, u.xs);
+    vox_resolve_kernel<<<std::min(2048, (n_max + 3) / 4), 256, 0, st>>>(u.vlist, u.hkey, u.hhead, u.hend, u.sval2, u.xs, xyz, ds, grid_view(g), (int)g.n, g.pts,
                                            g.by_id, g.dirty, u.dlist, (uint32_t)(u.cap * 27), u.cnt, u.add_flag);
     int rc = exclusive_scan(u, u.add_flag, u.pos, n_max + 1, st);
     if (rc) return rc;
@@ -735,7 +734,7 @@ int finish_add(GridBuf& g, MapUpdBuf& u, int64_t id0, float slack, hipStream_t s
 
 void mapupd_free(MapUpdBuf& u) {
     void* bufs[] = {u.f64,   u.pos64, u.add_flag, u.pos,   u.cls,    u.world,    u.xyz_a,    u.xyz_b, u.pending,
-                    u.skey,  u.sval,  u.skey2,    u.sval2, u.vlist,  u.dlist,    u.tmp_cell, u.tmp_rank, u.tlist,
+                    u.skey,  u.sval,  u.skey2,    u.sval2, u.xs,     u.vlist,    u.dlist,    u.tmp_cell, u.tmp_rank, u.tlist,
                     u.hkey,  u.hhead, u.hend,     u.tmp,   u.cnt,    u.boxes};
     for (void* p : bufs)
         if (p) (void)hipFree(p);

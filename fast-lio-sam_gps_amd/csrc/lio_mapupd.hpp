@@ -22,6 +22,7 @@ struct MapUpdBuf {
     uint32_t* sval = nullptr;             // stable sort's output (each voxel's points contiguous,
     uint32_t* skey2 = nullptr;            // in input order)
     uint32_t* sval2 = nullptr;
+    float4* xs = nullptr;                 // the offered points in that sorted order (x, y, z, -)
     uint32_t* vlist = nullptr;            // voxels touched
     uint32_t* dlist = nullptr;            // grid cells holding tombstones
     uint32_t* tmp_cell = nullptr;         // grid insert scratch
