@@ -51,6 +51,8 @@ struct Rccl {
     ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
     ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
     ncclResult_t (*AllGather)(const void*, void*, size_t, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
     const char* (*GetErrorString)(ncclResult_t) = nullptr;
 };
 
@@ -70,8 +72,11 @@ bool load_rccl(Rccl& r, std::string& why) {
     r.CommDestroy = (decltype(r.CommDestroy))dlsym(r.so, "ncclCommDestroy");
     r.CommAbort = (decltype(r.CommAbort))dlsym(r.so, "ncclCommAbort");
     r.AllGather = (decltype(r.AllGather))dlsym(r.so, "ncclAllGather");
+    r.GroupStart = (decltype(r.GroupStart))dlsym(r.so, "ncclGroupStart");
+    r.GroupEnd = (decltype(r.GroupEnd))dlsym(r.so, "ncclGroupEnd");
     r.GetErrorString = (decltype(r.GetErrorString))dlsym(r.so, "ncclGetErrorString");
-    if (!r.CommInitAll || !r.CommDestroy || !r.CommAbort || !r.AllGather || !r.GetErrorString) {
+    if (!r.CommInitAll || !r.CommDestroy || !r.CommAbort || !r.AllGather || !r.GroupStart || !r.GroupEnd ||
+        !r.GetErrorString) {
         why = "librccl lacks ncclCommInitAll / ncclAllGather";
         return false;
     }
@@ -164,6 +169,36 @@ int group_allgather_dev(const double* d_send, int64_t n, double* d_recv, void* s
                                                                                                                  : -1;
 }
 
+// One all-gather on every communicator from this thread, inside a group call: the connections RCCL
+// sets up lazily at a communicator's first collective (a step that waits for every peer) exist before
+// the ranks' threads enqueue theirs one at a time under the group lock.
+int rccl_warmup(lio_icp_group* g) {
+    const int n = g->world;
+    std::vector<double*> buf(n, nullptr);
+    int rc = LIO_OK;
+    for (int r = 0; r < n && rc == LIO_OK; ++r) {
+        if (hipSetDevice(g->dev[r]) != hipSuccess || hipMalloc(&buf[r], (size_t)(n + 1) * sizeof(double)) != hipSuccess)
+            rc = gfail(LIO_ERR_NOMEM, "lio_icp_group_create: warm-up buffers");
+        else if (hipMemset(buf[r], 0, (size_t)(n + 1) * sizeof(double)) != hipSuccess)
+            rc = gfail(LIO_ERR_HIP, "lio_icp_group_create: warm-up buffers");
+    }
+    if (rc == LIO_OK) {
+        ncclResult_t nr = g->rccl.GroupStart();
+        for (int r = 0; r < n && nr == 0; ++r)
+            nr = g->rccl.AllGather(buf[r] + n, buf[r], 1, kNcclDouble, g->comms[r], nullptr);
+        const ncclResult_t ne = g->rccl.GroupEnd();
+        if (nr == 0) nr = ne;
+        if (nr != 0) rc = gfail(LIO_ERR_STATE, std::string("RCCL warm-up all-gather: ") + g->rccl.GetErrorString(nr));
+    }
+    for (int r = 0; r < n; ++r) {
+        if (!buf[r]) continue;
+        (void)hipSetDevice(g->dev[r]);
+        if (hipDeviceSynchronize() != hipSuccess && rc == LIO_OK) rc = gfail(LIO_ERR_HIP, "RCCL warm-up: device error");
+        (void)hipFree(buf[r]);
+    }
+    return rc;
+}
+
 }  // namespace
 
 extern "C" {
@@ -208,6 +243,8 @@ int lio_icp_group_create(const lio_icp_params* p, int n_gpus, const int* devices
             if (nr != 0) {
                 g->comms.clear();
                 rc = gfail(LIO_ERR_STATE, std::string("ncclCommInitAll: ") + g->rccl.GetErrorString(nr));
+            } else {
+                rc = rccl_warmup(g);
             }
         }
     }

@@ -129,6 +129,26 @@ def test_icp_group_bit_identical_to_one_handle(n):
     np.testing.assert_array_equal(grp.aligned_, one.aligned_)
 
 
+def test_icp_group_failure_is_reported_and_sticky():
+    """A rank that fails mid-alignment (here: every rank, no target) releases the others (ADVICE r2:
+    the communicators / barrier are torn down once), the group reports the rank's error, refuses later
+    alignments, and is destroyed cleanly afterwards."""
+    src, dst, _ = synth.make_icp_pair(n_points=20_000, seed=12, disp=(1.0, 3.0))
+    grp = LC.LoopClosureGroup(LC.LoopClosureConfig(), 3, devices=[0, 0, 0])
+    grp.setInputSource(src)
+    with pytest.raises(LC._capi.LioError, match="rank"):
+        grp.align()
+    grp.setInputTarget(dst)
+    with pytest.raises(LC._capi.LioError, match="failed earlier"):
+        grp.align()
+    grp.close()
+    ok = LC.LoopClosureGroup(LC.LoopClosureConfig(), 3, devices=[0, 0, 0])  # a new group works
+    ok.setInputSource(src)
+    ok.setInputTarget(dst)
+    assert ok.align().iterations >= 1
+    ok.close()
+
+
 @pytest.mark.skipif(LC._capi.lib().lio_device_count() < 2, reason="RCCL exchange needs two distinct devices")
 def test_icp_group_rccl_bit_identical():
     src, dst, _ = synth.make_icp_pair(n_points=60_000, seed=12, disp=(1.0, 3.0))
