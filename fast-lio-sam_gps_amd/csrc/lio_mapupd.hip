@@ -309,8 +309,10 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
         int cnt_l = 0;
         unsigned long long best_l = ~0ull;
         float blx = 0.f, bly = 0.f, blz = 0.f;
+        uint32_t T1 = 0;  // one round (<= 64 box cells): the table stays in LDS for the tombstone pass
         for (int cb = 0; cb < nbc; cb += 64) {
             const uint32_t T = box_table(g, cr, cb, nbc, bnx, bny, tb);
+            T1 = T;
             for (uint32_t t = (uint32_t)lane; t < T; t += 64u) {
                 const float4 p = pts[box_slot(tb, t)];
                 if (!in_box(b, p.x, p.y, p.z)) continue;
@@ -371,7 +373,7 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
         int dead = 0;
         if (cnt_e > 0 && (surv_new >= 0 || cnt_e > 1)) {
             for (int cb = 0; cb < nbc; cb += 64) {
-                const uint32_t T = box_table(g, cr, cb, nbc, bnx, bny, tb);
+                const uint32_t T = nbc <= 64 ? T1 : box_table(g, cr, cb, nbc, bnx, bny, tb);
                 uint32_t* marked = tb + 2 * 64 + 1;  // per box cell of this round: holds a new tombstone
                 marked[lane] = 0u;
                 __builtin_amdgcn_wave_barrier();
