@@ -212,9 +212,17 @@ __global__ void insert_rank_kernel(const float4* __restrict__ by_id, int64_t id0
     const uint32_t c = cell_key_of(g, 1.0f / g.cell, p.x, p.y, p.z, &out);
     if (out) atomicOr(flags, 1u);
     const uint32_t r = atomicAdd(&addc[c], 1u);
-    if (r == 0) tlist[atomicAdd(d_ntouch, 1u)] = c;
     tmp_cell[j] = c;
     tmp_rank[j] = r;
+    // the wave's newly touched cells listed with one counter add (one hot counter serialises)
+    const uint64_t m = __ballot(r == 0);
+    if (r == 0) {
+        const int leader = __ffsll((long long)m) - 1;
+        uint32_t base = 0;
+        if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(d_ntouch, (uint32_t)__popcll(m));
+        base = (uint32_t)__shfl((int)base, leader, 64);
+        tlist[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = c;
+    }
 }
 
 // one lane per touched cell: room for its new points (a bigger block from the pool when the cell's is
