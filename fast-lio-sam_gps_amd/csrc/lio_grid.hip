@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 
+#include "lio_grid_dev.hpp"
 #include "lio_kernels.hpp"
 
 namespace lio {
@@ -87,21 +88,6 @@ __global__ void __launch_bounds__(256) aabb_final_kernel(const float* __restrict
     if (threadIdx.x < 6) out[threadIdx.x] = s[threadIdx.x][0];
 }
 
-// cell index of a point, clamped into the grid (build assignment); *out is set
-// when the unclamped index leaves the grid (a point the geometry cannot hold)
-__device__ __forceinline__ uint32_t cell_key_of(const GridGeom& g, float inv, float x, float y, float z,
-                                                int* out = nullptr) {
-    int cx = cell_coord(x, g.ox, inv);
-    int cy = cell_coord(y, g.oy, inv);
-    int cz = cell_coord(z, g.oz, inv);
-    if (out && ((unsigned)cx >= (unsigned)g.nx || (unsigned)cy >= (unsigned)g.ny || (unsigned)cz >= (unsigned)g.nz))
-        *out = 1;
-    cx = min(max(cx, 0), g.nx - 1);
-    cy = min(max(cy, 0), g.ny - 1);
-    cz = min(max(cz, 0), g.nz - 1);
-    return ((uint32_t)cz * (uint32_t)g.ny + (uint32_t)cy) * (uint32_t)g.nx + (uint32_t)cx;
-}
-
 __global__ void init_by_id_kernel(const float* __restrict__ xyz, int64_t n, float4* __restrict__ by_id) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
@@ -170,34 +156,13 @@ __global__ void gather_gapped_kernel(const float4* __restrict__ by_id, int64_t n
     pts[rng[ck].x + (uint32_t)(j - start[ck])] = make_float4(p.x, p.y, p.z, __int_as_float((int)id));
 }
 
-// one WAVE per listed cell (grid-stride): drop the entries marked dead (id bits kNone), keep the
-// order (64 entries at a time: ballot + mbcnt give each survivor its slot), clear the cell's dirty byte
+// one WAVE per listed cell (grid-stride): lio_grid_dev.hpp compact_cell_wave
 __global__ void __launch_bounds__(256) compact_cells_kernel(float4* __restrict__ pts, uint2* __restrict__ rng,
                                                             uint8_t* __restrict__ dirty, const uint32_t* __restrict__ dlist,
                                                             const uint32_t* __restrict__ d_ndirty, uint32_t dcap) {
     const uint32_t nd = min(*d_ndirty, dcap);
-    const int lane = threadIdx.x & 63;
-    for (uint32_t k = blockIdx.x * 4u + (threadIdx.x >> 6); k < nd; k += gridDim.x * 4u) {  // wave-uniform
-        const uint32_t c = dlist[k];
-        const uint2 r = rng[c];
-        uint32_t o = r.x;
-        for (uint32_t j0 = r.x; j0 < r.y; j0 += 64u) {
-            const uint32_t j = j0 + (uint32_t)lane;
-            float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (j < r.y) p = pts[j];
-            const bool keep = j < r.y && __float_as_int(p.w) != kNone;
-            const uint64_t m = __ballot(keep);
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            // every lane has its entry in registers before any store: slots below j0 + 64 only
-            __builtin_amdgcn_wave_barrier();
-            if (keep && o + rank != j) pts[o + rank] = p;
-            o += (uint32_t)__popcll(m);
-        }
-        if (lane == 0) {
-            rng[c].y = o;
-            dirty[c] = 0;
-        }
-    }
+    for (uint32_t k = blockIdx.x * 4u + (threadIdx.x >> 6); k < nd; k += gridDim.x * 4u)  // wave-uniform
+        compact_cell_wave(pts, rng, dirty, dlist[k]);
 }
 
 // new id j (0 <= j < *d_nnew): its cell and its rank among this update's points of that cell
@@ -206,23 +171,10 @@ __global__ void insert_rank_kernel(const float4* __restrict__ by_id, int64_t id0
                                    uint32_t* __restrict__ tmp_rank, uint32_t* __restrict__ tlist,
                                    uint32_t* __restrict__ d_ntouch, uint32_t* __restrict__ flags) {
     const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= *d_nnew) return;
-    const float4 p = by_id[id0 + j];
-    int out = 0;
-    const uint32_t c = cell_key_of(g, 1.0f / g.cell, p.x, p.y, p.z, &out);
-    if (out) atomicOr(flags, 1u);
-    const uint32_t r = atomicAdd(&addc[c], 1u);
-    tmp_cell[j] = c;
-    tmp_rank[j] = r;
-    // the wave's newly touched cells listed with one counter add (one hot counter serialises)
-    const uint64_t m = __ballot(r == 0);
-    if (r == 0) {
-        const int leader = __ffsll((long long)m) - 1;
-        uint32_t base = 0;
-        if ((int)(threadIdx.x & 63) == leader) base = atomicAdd(d_ntouch, (uint32_t)__popcll(m));
-        base = (uint32_t)__shfl((int)base, leader, 64);
-        tlist[base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u))] = c;
-    }
+    const bool act = j < *d_nnew;
+    float4 p = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (act) p = by_id[id0 + j];
+    insert_rank_point(act, j, p.x, p.y, p.z, g, addc, tmp_cell, tmp_rank, tlist, d_ntouch, flags);
 }
 
 // one lane per touched cell: room for its new points (a bigger block from the pool when the cell's is
@@ -537,6 +489,13 @@ void grid_insert_ids(GridBuf& g, int64_t id0, const uint32_t* d_nnew, int n_max,
     (void)hipMemsetAsync(s.d_ntouch, 0, sizeof(uint32_t), st);
     insert_rank_kernel<<<nb, 256, 0, st>>>(g.by_id, id0, d_nnew, g.geom, g.addc, s.tmp_cell, s.tmp_rank, s.tlist,
                                            s.d_ntouch, flags);
+    grid_insert_finish(g, id0, d_nnew, n_max, s, flags, st);
+}
+
+void grid_insert_finish(GridBuf& g, int64_t id0, const uint32_t* d_nnew, int n_max, GridInsertScratch s,
+                        uint32_t* flags, hipStream_t st) {
+    if (n_max <= 0) return;
+    const int nb = (n_max + 255) / 256;
     insert_alloc_kernel<<<nb, 256, 0, st>>>(g.pts, g.rng, g.lim, g.addc, s.tlist, s.d_ntouch, g.bump,
                                             (uint32_t)std::min<int64_t>(g.slots_cap, 0xffffffffll), flags);
     insert_write_kernel<<<nb, 256, 0, st>>>(g.by_id, id0, d_nnew, s.tmp_cell, s.tmp_rank, g.addc, g.pts);

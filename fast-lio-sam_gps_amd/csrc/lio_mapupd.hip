@@ -17,11 +17,14 @@
 // device; launch sizes are the call's upper bounds).
 // Semantics restated in oracle/lio_oracle.cpp (DynMap, map_incremental).
 #include <hipcub/hipcub.hpp>
+#include <rocprim/block/block_radix_sort.hpp>
+#include <rocprim/block/block_scan.hpp>
 
 #include <algorithm>
 #include <cstring>
 #include <vector>
 
+#include "lio_grid_dev.hpp"
 #include "lio_kernels.hpp"
 #include "lio_mapupd.hpp"
 
@@ -72,7 +75,15 @@ enum : int {
     kCPend = 8,    // map_incremental points queued for the unbounded kNN
     kCFlags = 9,   // 1 a point outside the grid, 2 slot pool exhausted, 4 tombstone cell list full
     kCTouch = 10,  // grid cells receiving points
+    kCRuns = 11,   // voxel runs listed by group_sort_kernel
 };
+// kCFlags bit 16: some voxel's points span more than kMaxRuns sort blocks (group_sort_kernel): the update
+// did nothing but reset the voxel table, and the host redoes it through the globally sorted path
+constexpr uint32_t kFlagRuns = 16u;
+// grouped update: sort blocks of kGrpB consecutive points (group_sort_kernel), the append in the same
+// blocks (update_kernel)
+constexpr int kGrpT = 256, kGrpI = 8, kGrpB = kGrpT * kGrpI;
+constexpr int kMaxRuns = 64;  // runs a voxel may have (its points spread over <= 64 sort blocks)
 // vox_resolve_kernel's trigger / tombstone totals: one pair of counters per 64-byte line, kSpread of them
 // (block b adds to line b % kSpread), folded into cnt[kCTrig] / cnt[kCDead] and cleared by append_kernel.
 // Thousands of waves adding to ONE device-scope counter serialise at the memory-side atomic unit
@@ -81,6 +92,9 @@ constexpr int kSpread = 64, kSpreadOff = 32, kSpreadStride = 16;
 constexpr int kCntWords = kSpreadOff + kSpread * kSpreadStride;
 
 constexpr unsigned long long kEmptyKey = ~0ull;
+
+// map_incremental point classes
+enum : uint8_t { kSkip = 0, kToAdd = 1, kNoNeed = 2 };
 
 __device__ __forceinline__ unsigned long long voxel_key(float x, float y, float z, float ds) {
     const float p[3] = {x, y, z};
@@ -288,43 +302,165 @@ __device__ __forceinline__ uint32_t box_slot(const uint32_t* tb, uint32_t t) {
 // points at a time as scans: q wins iff !(running minimum before it < its distance), the running
 // minimum is a prefix min, the winner q is compared with (same_point) is the last earlier winner
 // (a prefix max of winner positions), the survivor is the last winner — the sequential result.
-__global__ void __launch_bounds__(256) vox_resolve_kernel(
-    const uint32_t* __restrict__ vlist, unsigned long long* __restrict__ hkey, int* __restrict__ hhead,
-    const int* __restrict__ hend, const uint32_t* __restrict__ sval2, const float4* __restrict__ xs,
-    const float* __restrict__ xyz, float ds, GridDev g,
-    int grid_n, float4* __restrict__ pts, float4* __restrict__ by_id, uint8_t* __restrict__ dirty,
-    uint32_t* __restrict__ dlist, uint32_t dcap, uint32_t* __restrict__ cnt, uint32_t* __restrict__ add_flag) {
+//
+// The voxel's points come as runs of sorted positions: RUNS = false, one run sval2 / xs[hhead .. hend)
+// of the globally sorted arrays; RUNS = true, the runs group_sort_kernel listed for the voxel (one per
+// sort block holding its points, each in input order), sorted by position here, so that their
+// concatenation is the voxel's points in input order.  The wave's run table (starts, offsets) maps a
+// voxel position p (0 .. c) to a sorted position.
+struct VoxArgs {
+    const uint32_t* vlist;
+    unsigned long long* hkey;
+    int* hhead;              // RUNS = false: first sorted entry; RUNS = true: the voxel's run list (-1)
+    const int* hend;         // RUNS = false: one past the last entry
+    uint32_t* vnruns;        // RUNS = true: runs per voxel (reset here)
+    const uint4* runs;       // RUNS = true: run records {first sorted position, count, next, -}
+    const uint32_t* sval;    // input index at each sorted position
+    const float4* xs;        // its coordinates
+    const float* xyz;
+    float ds;
+    GridDev g;
+    int grid_n;
+    float4* pts;
+    float4* by_id;
+    uint8_t* dirty;
+    uint32_t* dlist;
+    uint32_t dcap;
+    uint32_t* cnt;
+    uint32_t* add_flag;
+    uint32_t* blk_surv;      // RUNS = true: survivors per sort block (the append ranks)
+};
+
+// sorted position of voxel position p (rt: run starts, ro: run offsets, R runs, ro[R] = count)
+__device__ __forceinline__ uint32_t run_pos(const uint32_t* rt, const uint32_t* ro, int R, uint32_t p) {
+    int lo = 0, hi = R;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (ro[mid] <= p) lo = mid;
+        else hi = mid;
+    }
+    return rt[lo] + (p - ro[lo]);
+}
+// lane's K points p0 .. p0 + K - 1 (< c) through the run table (one search, then run steps)
+__device__ __forceinline__ void load_super_runs(const float4* __restrict__ xs, const uint32_t* rt, const uint32_t* ro,
+                                                int R, uint32_t p0, uint32_t c, float4 (&q)[kVoxK]) {
+    if (R == 1) {  // wave-uniform: one contiguous run
+        load_super(xs, (int)(rt[0] + p0), (int)(rt[0] + c), q);
+        return;
+    }
+    int lo = 0, hi = R;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (ro[mid] <= p0) lo = mid;
+        else hi = mid;
+    }
+#pragma unroll
+    for (int k = 0; k < kVoxK; ++k) {
+        const uint32_t p = p0 + (uint32_t)k;
+        while (lo + 1 < R && ro[lo + 1] <= p) ++lo;
+        q[k] = p < c ? xs[rt[lo] + (p - ro[lo])] : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+}
+
+template <bool RUNS>
+__global__ void __launch_bounds__(256) vox_resolve_kernel(VoxArgs a) {
     __shared__ uint32_t s_tab[4][2 * 64 + 1 + 64];  // per wave: box-cell table + tombstone flags
+    __shared__ uint32_t s_run[4][2 * 64 + 1];       // per wave: run table (starts, offsets)
     const int lane = threadIdx.x & 63;
     __shared__ uint32_t s_tot[2][4];
-    const uint32_t nvox = cnt[kCVox];
+    const uint32_t nvox = a.cnt[kCVox];
+    const GridDev& g = a.g;
+    // RUNS: a voxel spanning too many sort blocks -> reset the table only (the host redoes the update)
+    const bool abandon = RUNS && (a.cnt[kCFlags] & kFlagRuns);
     uint32_t trig_acc = 0, dead_acc = 0;  // this lane's share of the block's totals
     for (uint32_t v = blockIdx.x * 4u + (threadIdx.x >> 6); v < nvox; v += gridDim.x * 4u) {  // wave-uniform
-        const uint32_t h = vlist[v];
-        const int s0 = hhead[h], s1 = hend[h];
-        const unsigned long long vkey = hkey[h];
-        if (s0 < 0) continue;
+        const uint32_t h = a.vlist[v];
+        const unsigned long long vkey = a.hkey[h];
+        uint32_t* rt = s_run[threadIdx.x >> 6];
+        uint32_t* ro = rt + 64;
+        int R = 1;
+        uint32_t c = 0;
+        if constexpr (RUNS) {
+            if (abandon) {
+                if (lane == 0) {
+                    a.hkey[h] = kEmptyKey;
+                    a.hhead[h] = -1;
+                    a.vnruns[h] = 0u;
+                }
+                continue;
+            }
+            // walk the voxel's run list (a few runs: one per sort block holding its points), lane r keeps
+            // run r; sort the runs by position (bitonic over the wave), prefix their counts
+            int rec = a.hhead[h];
+            unsigned long long key = ~0ull;
+            R = 0;
+            while (rec >= 0 && R < 64) {  // wave-uniform (group_sort_kernel flags > kMaxRuns runs)
+                const uint4 rr = a.runs[rec];
+                if (lane == R) key = ((unsigned long long)rr.x << 32) | rr.y;
+                rec = (int)rr.z;
+                ++R;
+            }
+            if (R == 0) continue;
+            if (R > 1) {
+#pragma unroll
+                for (int k = 2; k <= 64; k <<= 1)
+#pragma unroll
+                    for (int j = k >> 1; j > 0; j >>= 1) {
+                        const unsigned long long o = __shfl_xor(key, j, 64);
+                        const bool keep_min = ((lane & k) == 0) == ((lane & j) == 0);
+                        key = keep_min ? (o < key ? o : key) : (o > key ? o : key);
+                    }
+            }
+            const uint32_t cntr = lane < R ? (uint32_t)key : 0u;
+            uint32_t incl = cntr;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t y = __shfl_up(incl, off, 64);
+                if (lane >= off) incl += y;
+            }
+            c = (uint32_t)__shfl((int)incl, 63, 64);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");  // the previous voxel's readers are done
+            __builtin_amdgcn_wave_barrier();
+            rt[lane] = (uint32_t)(key >> 32);
+            ro[lane] = incl - cntr;
+            if (lane == 63) ro[64] = c;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        } else {
+            const int s0 = a.hhead[h], s1 = a.hend[h];
+            if (s0 < 0) continue;
+            c = (uint32_t)(s1 - s0);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (lane == 0) rt[0] = (uint32_t)s0, ro[0] = 0u, ro[1] = c;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
         // the first super-chunk of the voxel's points (lane l: points l * K .. l * K + K - 1, contiguous),
         // loaded while the map side runs
         float4 q[kVoxK];
-        load_super(xs, s0 + lane * kVoxK, s1, q);
+        load_super_runs(a.xs, rt, ro, R, (uint32_t)(lane * kVoxK), c, q);
         // the box from the voxel key (floor(p / ds) per axis, vox_box's own values) unless an axis was
         // clamped in the key: then from the voxel's first point, as before
         VoxBox b;
         bool clamped = false;
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
+            const float ds = a.ds;
             const int idx = (int)((vkey >> (kVoxBits * (2 - d))) & ((1ull << kVoxBits) - 1)) - kVoxOff;
             clamped |= idx <= -kVoxOff || idx >= kVoxOff - 1;
             b.lo[d] = (float)idx * ds;
             b.hi[d] = b.lo[d] + ds;
             b.mid[d] = (float)((double)b.lo[d] + (double)(b.hi[d] - b.lo[d]) / 2.0);
         }
+        const float ds = a.ds;
         if (clamped) {
-            const int first_i = (int)sval2[s0];
-            b = vox_box(xyz[3 * first_i], xyz[3 * first_i + 1], xyz[3 * first_i + 2], ds);
+            const int first_i = (int)a.sval[rt[0]];
+            b = vox_box(a.xyz[3 * first_i], a.xyz[3 * first_i + 1], a.xyz[3 * first_i + 2], ds);
         }
-        const CellRange cr = box_cells(g, b, grid_n);
+        const CellRange cr = box_cells(g, b, a.grid_n);
         // the box's cells (<= 64 handled per round: one per lane), their ranges concatenated through the
         // wave's LDS table so the lanes stride all the box's map points at once (no per-cell round trips)
         const int bnx = cr.x1 - cr.x0 + 1, bny = cr.y1 - cr.y0 + 1;
@@ -339,7 +475,7 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
             const uint32_t T = box_table(g, cr, cb, nbc, bnx, bny, tb);
             T1 = T;
             for (uint32_t t = (uint32_t)lane; t < T; t += 64u) {
-                const float4 p = pts[box_slot(tb, t)];
+                const float4 p = a.pts[box_slot(tb, t)];
                 if (!in_box(b, p.x, p.y, p.z)) continue;
                 ++cnt_l;
                 const float dd = calc_dist(p.x, p.y, p.z, b.mid[0], b.mid[1], b.mid[2]);
@@ -369,9 +505,10 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
         // exclusive last-winner scan, its triggers), so a voxel of c points costs c / (64 K) wave scans
         // instead of c / 64 (the densest voxel of a Livox scan holds thousands of points)
         float sd = cnt_e > 0 ? __uint_as_float((uint32_t)(best >> 32)) : INFINITY;
-        int surv_pos = -1;  // sorted position of the last new winner
+        int surv_pos = -1;  // voxel position of the last new winner
+        const int s0 = 0, s1 = (int)c;
         for (int e0 = s0; e0 < s1; e0 += 64 * kVoxK) {
-            if (e0 != s0) load_super(xs, e0 + lane * kVoxK, s1, q);
+            if (e0 != s0) load_super_runs(a.xs, rt, ro, R, (uint32_t)(e0 + lane * kVoxK), c, q);
             const int lb = e0 + lane * kVoxK;  // this lane's first point
             float qd[kVoxK];
             float m = INFINITY;
@@ -419,7 +556,7 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
             }
             sd = fminf(sd, wave_min_f(m));
         }
-        const int surv_new = surv_pos >= 0 ? (int)sval2[surv_pos] : -1;
+        const int surv_new = surv_pos >= 0 ? (int)a.sval[run_pos(rt, ro, R, (uint32_t)surv_pos)] : -1;
         if (cnt_e > 0 && (surv_new >= 0 || cnt_e > 1)) {
             for (int cb = 0; cb < nbc; cb += 64) {
                 const uint32_t T = nbc <= 64 ? T1 : box_table(g, cr, cb, nbc, bnx, bny, tb);
@@ -428,12 +565,12 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
                 __builtin_amdgcn_wave_barrier();
                 for (uint32_t t = (uint32_t)lane; t < T; t += 64u) {
                     const uint32_t slot = box_slot(tb, t);
-                    const float4 p = pts[slot];
+                    const float4 p = a.pts[slot];
                     if (!in_box(b, p.x, p.y, p.z)) continue;
                     const int id = __float_as_int(p.w);
                     if (surv_new < 0 && id == best_id) continue;
-                    by_id[id].w = 0.f;
-                    pts[slot].w = __int_as_float(kNone);
+                    a.by_id[id].w = 0.f;
+                    a.pts[slot].w = __int_as_float(kNone);
                     ++dead_acc;
                     marked[box_cell_of(tb, t)] = 1u;
                 }
@@ -441,33 +578,36 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
                 __builtin_amdgcn_wave_barrier();
                 __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
                 const int kk = cb + lane;
-                uint32_t c = 0;
+                uint32_t cc = 0;
                 bool fresh = false;  // list the cell once: the wave that sets its dirty byte
                 if (kk < nbc && marked[lane]) {
-                    c = box_cell_index(g, cr, kk, bnx, bny);
-                    unsigned int* wp = reinterpret_cast<unsigned int*>(dirty + (c & ~3u));
-                    const unsigned int bit = 1u << (8u * (c & 3u));
+                    cc = box_cell_index(g, cr, kk, bnx, bny);
+                    unsigned int* wp = reinterpret_cast<unsigned int*>(a.dirty + (cc & ~3u));
+                    const unsigned int bit = 1u << (8u * (cc & 3u));
                     fresh = !(atomicOr(wp, bit) & bit);
                 }
                 const uint64_t fm = __ballot(fresh);
                 if (fm) {  // the wave's fresh cells listed with one counter add
                     uint32_t base = 0;
-                    if (lane == 0) base = atomicAdd(&cnt[kCDirty], (uint32_t)__popcll(fm));
+                    if (lane == 0) base = atomicAdd(&a.cnt[kCDirty], (uint32_t)__popcll(fm));
                     base = (uint32_t)__builtin_amdgcn_readfirstlane((int)base);
                     if (fresh) {
-                        const uint32_t sl =
-                            base + __builtin_amdgcn_mbcnt_hi((uint32_t)(fm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fm, 0u));
-                        if (sl < dcap) dlist[sl] = c;
-                        else atomicOr(&cnt[kCFlags], 4u);  // list full: the caller rebuilds the grid
+                        const uint32_t sl = base + lane_rank(fm);
+                        if (sl < a.dcap) a.dlist[sl] = cc;
+                        else atomicOr(&a.cnt[kCFlags], 4u);  // list full: the caller rebuilds the grid
                     }
                 }
                 __builtin_amdgcn_wave_barrier();
             }
         }
         if (lane == 0) {
-            if (surv_new >= 0) add_flag[surv_new] = 1u;
-            hkey[h] = kEmptyKey;  // the table is clean again for the next call
-            hhead[h] = -1;
+            if (surv_new >= 0) {
+                a.add_flag[surv_new] = 1u;
+                if constexpr (RUNS) atomicAdd(&a.blk_surv[surv_new / kGrpB], 1u);
+            }
+            a.hkey[h] = kEmptyKey;  // the table is clean again for the next call
+            a.hhead[h] = -1;
+            if constexpr (RUNS) a.vnruns[h] = 0u;
         }
     }
     // the block's totals: one add per counter to this block's spread line
@@ -479,7 +619,7 @@ __global__ void __launch_bounds__(256) vox_resolve_kernel(
     __syncthreads();
     if (threadIdx.x < 2) {
         const uint32_t t = s_tot[threadIdx.x][0] + s_tot[threadIdx.x][1] + s_tot[threadIdx.x][2] + s_tot[threadIdx.x][3];
-        if (t) atomicAdd(&cnt[kSpreadOff + (blockIdx.x % kSpread) * kSpreadStride + threadIdx.x], t);
+        if (t) atomicAdd(&a.cnt[kSpreadOff + (blockIdx.x % kSpread) * kSpreadStride + threadIdx.x], t);
     }
 }
 
@@ -513,6 +653,270 @@ __global__ void append_kernel(const float* __restrict__ xyz_a, const uint32_t* _
 
 __global__ void set_u32_kernel(uint32_t* __restrict__ p, uint32_t v) { *p = v; }
 
+// ---- grouped update: voxels grouped inside sort blocks, no global sort ------------------------
+//
+// group_sort_kernel: one block per kGrpB consecutive points.  Each point offered to the downsampled add
+// claims its voxel's table slot (CAS; the claimer lists the voxel), the block sorts its points by slot
+// (LSD radix sort: stable, so each slot's points stay in input order) and lists one run per slot present
+// in the block on the slot's run list {first sorted position, count, next}.  A voxel's points are the
+// concatenation of its runs in block order (vox_resolve_kernel<true> sorts the few runs by position).
+// Replaces the global (slot, index) sort: one launch instead of ten (rocprim block sort + 7 merges).
+
+struct GroupArgs {
+    const float* xyz;   // n x 3
+    const uint8_t* cls; // per point class, or null: every point is all_cls
+    int all_cls;
+    int n;
+    float ds;
+    unsigned long long* hkey;
+    uint32_t hmask;
+    int hbits;
+    int* vhead;         // per slot: run list head (-1)
+    uint32_t* vnruns;   // per slot: runs listed
+    uint4* runs;        // run records
+    uint32_t* sidx;     // n: input index at each sorted position
+    float4* xs;         // n: its coordinates
+    uint32_t* vlist;
+    uint32_t* add_flag; // n: cleared here (vox_resolve marks the survivors)
+    uint32_t* cnt;
+    uint32_t* blk_surv; // per block: survivors (zeroed here, counted by vox_resolve)
+    uint32_t* blk_nn;   // per block: no-need points
+};
+
+__global__ void __launch_bounds__(kGrpT) group_sort_kernel(GroupArgs a) {
+    using Sort = rocprim::block_radix_sort<uint32_t, kGrpT, kGrpI, uint32_t>;
+    using Scan = rocprim::block_scan<uint32_t, kGrpT>;
+    __shared__ typename Sort::storage_type s_sort;
+    __shared__ typename Scan::storage_type s_scan;
+    __shared__ uint32_t s_keys[kGrpB + 1];
+    __shared__ uint32_t s_add[2][4];
+    const int lane = threadIdx.x & 63;
+    const int base = (int)blockIdx.x * kGrpB;
+    const uint32_t sent = a.hmask + 1;  // sorts last: points not offered to the downsampled add
+    // 1. striped (item base + j * kGrpT + t: 64 consecutive points per wave and j): classify, voxel key,
+    // claim.  Points of one voxel are mostly consecutive, so the wave's lanes are grouped by key first
+    // (ballot matching) and only one lane per distinct key probes the table — thousands of CAS on one
+    // slot (a dense voxel) would serialise at the atomic unit.
+    uint32_t n_add = 0, n_nn = 0;
+#pragma unroll 1
+    for (int j = 0; j < kGrpI; ++j) {
+        const int off = j * kGrpT + (int)threadIdx.x, i = base + off;
+        bool want = false;
+        unsigned long long vk = 0;
+        if (i < a.n) {
+            a.add_flag[i] = 0u;
+            const int c = a.cls ? (int)a.cls[i] : a.all_cls;
+            if (c == kToAdd) {
+                vk = voxel_key(a.xyz[3 * i], a.xyz[3 * i + 1], a.xyz[3 * i + 2], a.ds);
+                want = true;
+                ++n_add;
+            }
+            n_nn += c == kNoNeed ? 1u : 0u;
+        }
+        // runs of equal keys among neighbouring lanes: the run's first lane probes for all of them (all
+        // run leaders probe at once; a key repeated further away probes again and finds its slot)
+        const unsigned long long vprev = (unsigned long long)__shfl_up((long long)vk, 1, 64);
+        const bool wprev = __shfl_up((int)want, 1, 64) != 0;
+        const uint64_t starts = __ballot(want && (lane == 0 || !wprev || vprev != vk));
+        const int ld = want ? 63 - __clzll((long long)(starts & (~0ull >> (63 - lane)))) : lane;
+        uint32_t h = 0, mine = 0;
+        bool listed = false;  // this lane claimed a new voxel's slot (`mine`)
+        if (want && ld == lane) {
+            h = hash_slot(vk, a.hmask);
+            for (uint32_t probe = 0;; ++probe) {  // load <= 1/4: a free slot is always near
+                const unsigned long long prev = atomicCAS(&a.hkey[h], kEmptyKey, vk);
+                if (prev == kEmptyKey) {
+                    listed = true;
+                    mine = h;
+                    break;
+                }
+                if (prev == vk) break;
+                if (probe > a.hmask) {  // unreachable for a clean table (guard): the points join no voxel
+                    h = sent;
+                    break;
+                }
+                h = (h + 1u) & a.hmask;
+            }
+        }
+        h = (uint32_t)__shfl((int)h, ld, 64);
+        const uint32_t slot = want ? h : sent;
+        s_keys[off] = slot;
+        const uint64_t lm = __ballot(listed);
+        if (lm) {  // the wave's new voxels listed with one counter add
+            uint32_t b0 = 0;
+            if (lane == 0) b0 = atomicAdd(&a.cnt[kCVox], (uint32_t)__popcll(lm));
+            b0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)b0);
+            if (listed) a.vlist[b0 + lane_rank(lm)] = mine;
+        }
+    }
+    {  // points offered to the downsampled add: one counter add per block; the block's no-need points
+        const int w = wave_sum_i((int)n_add), w2 = wave_sum_i((int)n_nn);
+        if (lane == 0) s_add[0][threadIdx.x >> 6] = (uint32_t)w, s_add[1][threadIdx.x >> 6] = (uint32_t)w2;
+    }
+    __syncthreads();
+    // 2. blocked (thread t: points t K .. t K + K - 1, the sort's input order) for the stable sort
+    uint32_t key[kGrpI], val[kGrpI];
+#pragma unroll
+    for (int j = 0; j < kGrpI; ++j) {
+        key[j] = s_keys[threadIdx.x * kGrpI + j];
+        val[j] = (uint32_t)(base + (int)threadIdx.x * kGrpI + j);
+    }
+    __syncthreads();  // s_keys is rewritten below
+    Sort().sort(key, val, s_sort, 0, (unsigned)a.hbits + 1u);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t t = s_add[0][0] + s_add[0][1] + s_add[0][2] + s_add[0][3];
+        if (t) atomicAdd(&a.cnt[kCAdd], t);
+        a.blk_nn[blockIdx.x] = s_add[1][0] + s_add[1][1] + s_add[1][2] + s_add[1][3];
+        a.blk_surv[blockIdx.x] = 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < kGrpI; ++j) s_keys[threadIdx.x * kGrpI + j] = key[j];
+    if (threadIdx.x == 0) s_keys[kGrpB] = ~0u;
+    __syncthreads();
+    uint32_t st[kGrpI];
+    bool end[kGrpI];
+#pragma unroll
+    for (int j = 0; j < kGrpI; ++j) {
+        const uint32_t p = threadIdx.x * kGrpI + (uint32_t)j;
+        st[j] = (p == 0 || s_keys[p - 1] != key[j]) ? p : 0u;
+        end[j] = s_keys[p + 1] != key[j];
+    }
+    uint32_t rs[kGrpI];  // each point's run start: inclusive max scan of the start positions
+    Scan().inclusive_scan(st, rs, s_scan, rocprim::maximum<uint32_t>());
+#pragma unroll
+    for (int j = 0; j < kGrpI; ++j) {
+        const uint32_t p = threadIdx.x * kGrpI + (uint32_t)j;
+        const bool valid = key[j] < sent;
+        if (valid) {
+            const uint32_t i = val[j];
+            a.sidx[base + p] = i;
+            a.xs[base + p] = make_float4(a.xyz[3 * i], a.xyz[3 * i + 1], a.xyz[3 * i + 2], 0.f);
+        }
+        const bool emit = valid && end[j];
+        const uint64_t m = __ballot(emit);
+        if (m) {  // the wave's runs: one counter add, then each run pushed on its slot's list
+            uint32_t b0 = 0;
+            if (lane == 0) b0 = atomicAdd(&a.cnt[kCRuns], (uint32_t)__popcll(m));
+            b0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)b0);
+            if (emit) {
+                const uint32_t rec = b0 + lane_rank(m);
+                const int next = atomicExch(&a.vhead[key[j]], (int)rec);
+                a.runs[rec] = make_uint4((uint32_t)base + rs[j], p - rs[j] + 1u, (uint32_t)next, 0u);
+                if (atomicAdd(&a.vnruns[key[j]], 1u) >= (uint32_t)kMaxRuns) atomicOr(&a.cnt[kCFlags], kFlagRuns);
+            }
+        }
+    }
+}
+
+// One launch for everything between vox_resolve and the block growth: blocks [0, nb_app) take the
+// sort blocks' points again (kGrpB each) and append the survivors (ids id0 + rank, input order), then
+// the no-need points (id0 + survivors + rank) to by_id, ranking each new id in its grid cell
+// (insert_rank_point); a rank = the earlier blocks' counts (blk_surv / blk_nn, <= a few hundred) + a
+// block scan, so no device-wide scan.  The other blocks compact the cells holding tombstones (one wave
+// per cell): disjoint state.  Block 0 also folds vox_resolve's spread counters and publishes the counts.
+struct UpdArgs {
+    const float* xyz;
+    const uint8_t* cls;
+    int all_cls;
+    int n;
+    const uint32_t* add_flag;
+    const uint32_t* blk_surv;
+    const uint32_t* blk_nn;
+    int64_t id0;
+    float4* by_id;
+    GridGeom geom;
+    uint32_t* addc;
+    uint32_t* tmp_cell;
+    uint32_t* tmp_rank;
+    uint32_t* tlist;
+    uint32_t* cnt;
+    float4* pts;
+    uint2* rng;
+    uint8_t* dirty;
+    const uint32_t* dlist;
+    uint32_t dcap;
+    int nb_app;
+};
+
+__global__ void __launch_bounds__(kGrpT) update_kernel(UpdArgs a) {
+    using Scan = rocprim::block_scan<unsigned long long, kGrpT>;
+    __shared__ typename Scan::storage_type s_scan;
+    __shared__ uint32_t s_pre[3];
+    if (a.cnt[kCFlags] & kFlagRuns) return;  // abandoned update (block-uniform)
+    const int lane = threadIdx.x & 63;
+    const int b = (int)blockIdx.x;
+    if (b < a.nb_app) {
+        if (threadIdx.x < 64) {  // wave 0: the earlier blocks' counts and the survivor total
+            uint32_t sb = 0, nb = 0, st = 0, nt = 0;
+            for (int k = lane; k < a.nb_app; k += 64) {
+                const uint32_t s1 = a.blk_surv[k], n1 = a.blk_nn[k];
+                st += s1;
+                nt += n1;
+                if (k < b) sb += s1, nb += n1;
+            }
+            sb = (uint32_t)wave_sum_i((int)sb);
+            nb = (uint32_t)wave_sum_i((int)nb);
+            st = (uint32_t)wave_sum_i((int)st);
+            nt = (uint32_t)wave_sum_i((int)nt);
+            if (lane == 0) {
+                s_pre[0] = sb;
+                s_pre[1] = nb;
+                s_pre[2] = st;
+                if (b == 0) {
+                    a.cnt[kCSurv] = st;
+                    a.cnt[kCNew] = st + nt;
+                    a.cnt[kCNoNeed] = nt;
+                }
+            }
+            if (b == 0) {  // vox_resolve's spread totals -> cnt[kCTrig], cnt[kCDead]
+                uint32_t* sp = a.cnt + kSpreadOff + threadIdx.x * kSpreadStride;
+                const int t = wave_sum_i((int)sp[0]), d = wave_sum_i((int)sp[1]);
+                sp[0] = 0u;
+                sp[1] = 0u;
+                if (threadIdx.x == 0) {
+                    a.cnt[kCTrig] += (uint32_t)t;
+                    a.cnt[kCDead] += (uint32_t)d;
+                }
+            }
+        }
+        unsigned long long f[kGrpI], r[kGrpI];
+#pragma unroll
+        for (int j = 0; j < kGrpI; ++j) {  // blocked, as group_sort_kernel: input order
+            const int i = b * kGrpB + (int)threadIdx.x * kGrpI + j;
+            f[j] = 0ull;
+            if (i < a.n) {
+                const int c = a.cls ? (int)a.cls[i] : a.all_cls;
+                f[j] = (unsigned long long)(a.add_flag[i] ? 1u : 0u) | ((unsigned long long)(c == kNoNeed ? 1u : 0u) << 32);
+            }
+        }
+        Scan().exclusive_scan(f, r, 0ull, s_scan);  // (survivor, no-need) ranks inside the block
+        __syncthreads();
+        const uint32_t sb = s_pre[0], nb = s_pre[1], st = s_pre[2];
+#pragma unroll
+        for (int j = 0; j < kGrpI; ++j) {
+            const int i = b * kGrpB + (int)threadIdx.x * kGrpI + j;
+            const bool act = f[j] != 0ull;
+            uint32_t id = 0;
+            float x = 0.f, y = 0.f, z = 0.f;
+            if (act) {
+                id = (f[j] & 1ull) ? sb + (uint32_t)r[j] : st + nb + (uint32_t)(r[j] >> 32);
+                x = a.xyz[3 * i];
+                y = a.xyz[3 * i + 1];
+                z = a.xyz[3 * i + 2];
+                a.by_id[a.id0 + id] = make_float4(x, y, z, 1.f);
+            }
+            insert_rank_point(act, id, x, y, z, a.geom, a.addc, a.tmp_cell, a.tmp_rank, a.tlist, a.cnt + kCTouch,
+                              a.cnt + kCFlags);
+        }
+    } else {
+        const uint32_t nd = min(a.cnt[kCDirty], a.dcap);
+        const uint32_t nw = (gridDim.x - (uint32_t)a.nb_app) * 4u;
+        for (uint32_t k = ((uint32_t)b - (uint32_t)a.nb_app) * 4u + (threadIdx.x >> 6); k < nd; k += nw)
+            compact_cell_wave(a.pts, a.rng, a.dirty, a.dlist[k]);
+    }
+}
+
 // add_flag[0 .. n] = 0 (the scan's slot n included)
 __global__ void zero_u32_kernel(uint32_t* __restrict__ p, int n1) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -542,7 +946,6 @@ __global__ void delete_boxes_kernel(float4* __restrict__ by_id, int64_t n, const
 }
 
 // ---- map_incremental ---------------------------------------------------------
-enum : uint8_t { kSkip = 0, kToAdd = 1, kNoNeed = 2 };
 
 // FAST-LIO map_incremental() classification of one point given its nearest
 // points (ascending, nf >= 1 of them).  The reference's list holds
@@ -712,7 +1115,7 @@ int ensure_pts(MapUpdBuf& u, int64_t n, hipStream_t st) {
     const int64_t c = std::max<int64_t>(n, u.cap + u.cap / 2);
     void* bufs[] = {u.f64,   u.pos64, u.add_flag, u.pos,      u.cls,      u.world,    u.xyz_a, u.xyz_b, u.pending,
                     u.skey,  u.sval,  u.skey2,    u.sval2,    u.xs,       u.vlist,    u.dlist,    u.tmp_cell, u.tmp_rank,
-                    u.tlist, u.hkey,  u.hhead,    u.hend};
+                    u.tlist, u.hkey,  u.hhead,    u.hend,     u.vnruns,   u.runs, u.blk};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     UPD_CHK(hipMalloc(&u.f64, (c + 1) * sizeof(unsigned long long)));
@@ -743,6 +1146,11 @@ int ensure_pts(MapUpdBuf& u, int64_t n, hipStream_t st) {
     UPD_CHK(hipMalloc(&u.hkey, (size_t)hc * sizeof(unsigned long long)));
     UPD_CHK(hipMalloc(&u.hhead, (size_t)hc * sizeof(int)));
     UPD_CHK(hipMalloc(&u.hend, (size_t)hc * sizeof(int)));
+    UPD_CHK(hipMalloc(&u.vnruns, (size_t)hc * sizeof(uint32_t)));
+    UPD_CHK(hipMalloc(&u.runs, c * sizeof(uint4)));  // a run holds >= 1 point
+    u.blk_cap = (c + kGrpB - 1) / kGrpB + 1;
+    UPD_CHK(hipMalloc(&u.blk, 2 * u.blk_cap * sizeof(uint32_t)));  // survivors | no-need per sort block
+    UPD_CHK(hipMemsetAsync(u.vnruns, 0, (size_t)hc * sizeof(uint32_t), st));
     u.hbits = hb;
     UPD_CHK(hipMemsetAsync(u.hkey, 0xff, (size_t)hc * sizeof(unsigned long long), st));  // empty keys
     UPD_CHK(hipMemsetAsync(u.hhead, 0xff, (size_t)hc * sizeof(int), st));                // empty chains (-1)
@@ -786,8 +1194,9 @@ int enqueue_add(GridBuf& g, MapUpdBuf& u, const float* xyz, int n_max, const flo
                                                    u.hbits + 1, st));
     }
     vox_runs_kernel<<<nb, 256, 0, st>>>(u.skey2, u.sval2, xyz, n_max, u.hcap - 1, u.hhead, u.hend, u.xs);
-    vox_resolve_kernel<<<std::min(2048, (n_max + 3) / 4), 256, 0, st>>>(u.vlist, u.hkey, u.hhead, u.hend, u.sval2, u.xs, xyz, ds, grid_view(g), (int)g.n, g.pts,
-                                           g.by_id, g.dirty, u.dlist, (uint32_t)(u.cap * 27), u.cnt, u.add_flag);
+    VoxArgs va{u.vlist, u.hkey, u.hhead, u.hend, nullptr, nullptr, u.sval2, u.xs, xyz, ds, grid_view(g), (int)g.n,
+               g.pts, g.by_id, g.dirty, u.dlist, (uint32_t)(u.cap * 27), u.cnt, u.add_flag};
+    vox_resolve_kernel<false><<<std::min(2048, (n_max + 3) / 4), 256, 0, st>>>(va);
     int rc = exclusive_scan(u, u.add_flag, u.pos, n_max + 1, st);
     if (rc) return rc;
     append_kernel<<<nb, 256, 0, st>>>(xyz, u.add_flag, u.pos, xyz_nn, n_max, id0, g.by_id, u.cnt);
@@ -798,12 +1207,38 @@ int enqueue_add(GridBuf& g, MapUpdBuf& u, const float* xyz, int n_max, const flo
     return 0;
 }
 
+// The grouped update of n points xyz (class per point: cls, or all_cls for all): PointToAdd points
+// through the downsampled add, then the no-need points appended — group_sort, vox_resolve<true>, one
+// scan, the fused append / rank / compaction kernel, the block growth.  Counters zeroed by the caller.
+int enqueue_grouped(GridBuf& g, MapUpdBuf& u, const float* xyz, const uint8_t* cls, int all_cls, int n, float ds,
+                    int64_t id0, hipStream_t st) {
+    GroupArgs ga{xyz,      cls,    all_cls, n,    ds,   u.hkey,     u.hcap - 1, u.hbits, u.hhead,
+                 u.vnruns, u.runs, u.sval2, u.xs, u.vlist, u.add_flag, u.cnt,      u.blk,   u.blk + u.blk_cap};
+    const int nblk = (n + kGrpB - 1) / kGrpB;
+    group_sort_kernel<<<nblk, kGrpT, 0, st>>>(ga);
+    const uint32_t dcap = (uint32_t)(u.cap * 27);
+    VoxArgs va{u.vlist, u.hkey,   u.hhead, nullptr,    u.vnruns, u.runs, u.sval2, u.xs,   xyz,       ds,  grid_view(g),
+               (int)g.n, g.pts,   g.by_id, g.dirty,    u.dlist,  dcap,   u.cnt,   u.add_flag, u.blk};
+    vox_resolve_kernel<true><<<std::min(2048, (n + 3) / 4), 256, 0, st>>>(va);
+    const int nb_comp = std::min(512, std::max(8, nblk * 8));
+    UpdArgs ua{xyz,    cls,        all_cls,    n,      u.add_flag, u.blk, u.blk + u.blk_cap, id0,   g.by_id, g.geom, g.addc,
+               u.tmp_cell, u.tmp_rank, u.tlist, u.cnt,  g.pts,      g.rng, g.dirty,            u.dlist, dcap,    nblk};
+    update_kernel<<<nblk + nb_comp, kGrpT, 0, st>>>(ua);
+    GridInsertScratch sc{u.tmp_cell, u.tmp_rank, u.tlist, u.cnt + kCTouch};
+    grid_insert_finish(g, id0, u.cnt + kCNew, n, sc, u.cnt + kCFlags, st);
+    UPD_CHK(hipGetLastError());
+    return 0;
+}
+
+constexpr int kRedo = 1;  // finish_add: the grouped update was abandoned (kFlagRuns), nothing changed
+
 // the one host synchronisation of an update: counts back, the map's host view updated; a point
 // outside the grid or an exhausted slot pool -> full rebuild (by_id is complete either way)
 int finish_add(GridBuf& g, MapUpdBuf& u, int64_t id0, float slack, hipStream_t st) {
     UPD_CHK(hipMemcpyAsync(u.h_cnt, u.cnt, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     UPD_CHK(hipStreamSynchronize(st));
     const uint32_t* c = u.h_cnt;
+    if (c[kCFlags] & kFlagRuns) return kRedo;
     g.n_ids = id0 + c[kCNew];
     g.n = g.n - (int64_t)c[kCDead] + (int64_t)c[kCNew];
     if (c[kCFlags]) return grid_rebuild(g, g.geom.cell, slack, st);
@@ -815,7 +1250,7 @@ int finish_add(GridBuf& g, MapUpdBuf& u, int64_t id0, float slack, hipStream_t s
 void mapupd_free(MapUpdBuf& u) {
     void* bufs[] = {u.f64,   u.pos64, u.add_flag, u.pos,   u.cls,    u.world,    u.xyz_a,    u.xyz_b, u.pending,
                     u.skey,  u.sval,  u.skey2,    u.sval2, u.xs,     u.vlist,    u.dlist,    u.tmp_cell, u.tmp_rank, u.tlist,
-                    u.hkey,  u.hhead, u.hend,     u.tmp,   u.cnt,    u.boxes};
+                    u.hkey,  u.hhead, u.hend,     u.tmp,   u.cnt,    u.boxes, u.vnruns, u.runs, u.blk};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (u.h_cnt) (void)hipHostFree(u.h_cnt);
@@ -833,6 +1268,16 @@ int map_add_device(GridBuf& g, MapUpdBuf& u, const float* d_xyz, int64_t n64, bo
     const int64_t id0 = g.n_ids;
     int rc = grid_reserve_ids(g, id0 + n, st);
     if (rc) return rc;
+    UPD_CHK(hipMemsetAsync(u.cnt, 0, 16 * sizeof(uint32_t), st));
+    rc = enqueue_grouped(g, u, d_xyz, nullptr, downsample ? kToAdd : kNoNeed, n, ds, id0, st);
+    if (rc) return rc;
+    rc = finish_add(g, u, id0, slack, st);
+    if (rc != kRedo) {
+        out[0] = downsample ? (int64_t)u.h_cnt[kCTrig] : n;
+        out[1] = u.h_cnt[kCDead];
+        return rc;
+    }
+    // a voxel spread over more than kMaxRuns sort blocks: the globally sorted path
     UPD_CHK(hipMemsetAsync(u.cnt, 0, 16 * sizeof(uint32_t), st));
     zero_u32_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(u.add_flag, n + 1);
     if (downsample) {
@@ -891,14 +1336,24 @@ int map_incremental(GridBuf& g, MapUpdBuf& u, IncrArgs a, float ds, float slack,
     const int nb = (n + 255) / 256;
     incr_classify_kernel<<<nb, 256, 0, st>>>(a);
     incr_pending_kernel<<<128, 256, 0, st>>>(a);
-    incr_flags_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(u.cls, n, u.f64, u.add_flag);
-    rc = exclusive_scan64(u, u.f64, u.pos64, n + 1, st);
-    if (rc) return rc;
-    incr_scatter_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(u.world, u.cls, n, u.pos64, u.xyz_a, u.xyz_b, u.cnt);
-    rc = enqueue_add(g, u, u.xyz_a, n, u.xyz_b, ds, id0, st);
+    // the classes are final: PointToAdd / PointNoNeedDownsample straight from the per-point classes
+    rc = enqueue_grouped(g, u, u.world, u.cls, 0, n, ds, id0, st);
     if (rc) return rc;
     rc = finish_add(g, u, id0, slack, st);
+    uint32_t n_add = u.h_cnt[kCAdd];
+    if (rc == kRedo) {  // a voxel spread over more than kMaxRuns sort blocks: compact, then the sorted path
+        UPD_CHK(hipMemsetAsync(u.cnt, 0, 16 * sizeof(uint32_t), st));
+        incr_flags_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(u.cls, n, u.f64, u.add_flag);
+        rc = exclusive_scan64(u, u.f64, u.pos64, n + 1, st);
+        if (rc) return rc;
+        incr_scatter_kernel<<<(n + 1 + 255) / 256, 256, 0, st>>>(u.world, u.cls, n, u.pos64, u.xyz_a, u.xyz_b, u.cnt);
+        rc = enqueue_add(g, u, u.xyz_a, n, u.xyz_b, ds, id0, st);
+        if (rc) return rc;
+        rc = finish_add(g, u, id0, slack, st);
+        n_add = u.h_cnt[kCAdd];
+    }
     const uint32_t* c = u.h_cnt;
+    (void)n_add;
     out[0] = c[kCAdd];
     out[1] = c[kCNoNeed];
     out[2] = n - (int64_t)c[kCAdd] - (int64_t)c[kCNoNeed];

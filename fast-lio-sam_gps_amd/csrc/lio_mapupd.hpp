@@ -29,8 +29,13 @@ struct MapUpdBuf {
     uint32_t* tmp_rank = nullptr;
     uint32_t* tlist = nullptr;
     unsigned long long* hkey = nullptr;   // voxel table: keys (all ones = empty) ...
-    int* hhead = nullptr;                 // ... and the voxel's first sorted entry (-1), clean between calls
+    int* hhead = nullptr;                 // ... and the voxel's first sorted entry / run list head (-1), clean
+                                          // between calls
     int* hend = nullptr;                  // one past the voxel's last sorted entry
+    uint32_t* vnruns = nullptr;           // grouped update: runs per voxel slot (zero between calls)
+    uint4* runs = nullptr;                // grouped update: run records {first sorted position, count, next}
+    uint32_t* blk = nullptr;              // grouped update: survivors | no-need points per sort block
+    int64_t blk_cap = 0;
     uint32_t hcap = 0;
     int hbits = 0;                        // log2(hcap)
     int64_t cap = 0;

@@ -58,6 +58,42 @@ def test_add_points_downsample_parity(oracle, scene_scans):
     _knn_parity(tree, om, scans[3].body + np.float32([3.0, 1.0, 0.0]))
 
 
+def test_add_points_scrambled_order(oracle, scene_scans):
+    """Voxels whose points are spread over many of the grouped update's 2048-point sort blocks (input
+    order shuffled): the runs are re-ordered per voxel, so counters and map stay bit-exact."""
+    _, m, scans = scene_scans
+    base = m[:50000]
+    tree = F.IkdTreeGPU(cell_size=1.0, downsample_size=0.5)
+    tree.Build(base)
+    om = oracle.OracleDynMap(base)
+    rng = np.random.default_rng(11)
+    w = np.concatenate([oracle.body_to_world(synth.pose24(synth.initial_state(sc.pos_gt, sc.rot_gt)), sc.body)
+                        for sc in scans[:3]])
+    w = w[rng.permutation(len(w))]
+    w = np.concatenate([w, w[:5000]])  # exact duplicates later in the order (ties on the centre distance)
+    assert tree.Add_Points(w, True) == om.add(w, True, 0.5)
+    _same_map(tree, om)
+
+
+def test_add_points_voxel_over_many_blocks(oracle, scene_scans):
+    """One voxel offered 150k points (> 64 sort blocks): the grouped update is abandoned on the device
+    and redone through the globally sorted path — same result."""
+    _, m, _ = scene_scans
+    base = m[:20000]
+    tree = F.IkdTreeGPU(cell_size=1.0, downsample_size=0.5)
+    tree.Build(base)
+    om = oracle.OracleDynMap(base)
+    rng = np.random.default_rng(5)
+    c = np.floor(base[123] / 0.5) * 0.5
+    pts = (c + rng.uniform(0.01, 0.49, size=(150_000, 3))).astype(np.float32)
+    pts[1000:1100] = pts[10]  # repeated points
+    assert tree.Add_Points(pts, True) == om.add(pts, True, 0.5)
+    _same_map(tree, om)
+    small = (c + np.float32([2.0, 0.0, 0.0]) + rng.uniform(0.0, 0.5, size=(3000, 3))).astype(np.float32)
+    assert tree.Add_Points(small, True) == om.add(small, True, 0.5)  # the grouped path again afterwards
+    _same_map(tree, om)
+
+
 def test_add_points_plain_and_delete_boxes(oracle, scene_scans):
     _, m, scans = scene_scans
     base = m[:40000]
