@@ -89,6 +89,9 @@ def parse():
                          "icpAlignment) on the newest keyframe; reported under 'pipeline' (0: skip)")
     ap.add_argument("--grow-scans", type=int, default=20,
                     help="C3/C5: scans appended through map_incremental before timing (SURVEY §8d)")
+    ap.add_argument("--watchdog-s", type=float, default=240.0,
+                    help="N > 1: seconds after the headline measurement before rank 0 prints what it has and every "
+                         "rank exits (a collective of the secondary sections that never returns)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"),
                     help="per-launch HBM traffic measured with rocprofv3 --pmc (profiles/)")
     return ap.parse_args()
@@ -108,6 +111,67 @@ def _spawn_ranks(args) -> int:
            "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
     return subprocess.run(cmd, env=env).returncode
+
+
+def _loop_icp(args, LC, synth, local, world, rank, dist, rehearse, coll_dev, barrier, torch):
+    """The C4 loop ICP (secondary key loop_icp), sharded over the ranks; returns (loop_icp, src, dst)."""
+    # C4 with a 2.5 m / 4 deg initial offset: PCL's criteria with the reference's epsilons take 9
+    # iterations (the 0.3 m / 1.5 deg pair of round 1 converged after 1, so ms/iteration meant nothing)
+    src, dst, Tgt = synth.make_icp_pair(n_points=500_000, seed=4321, disp=(2.5, 4.0))
+    lc = LC.LoopClosure(LC.LoopClosureConfig(), device=local)
+    cb = None
+    exchange = "none (1 rank)"
+    if world > 1:
+        from lio_gpu import dist as ldist
+
+        if rehearse:  # gloo on CPU tensors: the records pass through host memory
+            cb = ldist.make_allgather(device=coll_dev)
+            lc.set_shard(rank, world, cb)
+            exchange = "host (gloo rehearsal)"
+        else:  # RCCL all-gather of device buffers on the ICP handle's stream, record-order sum on the GPU
+            cb = ldist.DeviceExchange()
+            lc.set_shard_device(rank, world, cb)
+            exchange = "device (RCCL all_gather_into_tensor on the handle's stream)"
+    lc.setInputSource(src)
+    lc.setInputTarget(dst)
+    lc.align(keep_aligned=False)
+    lc.set_timing(True)
+    barrier()
+    ti = time.perf_counter()
+    iters = 0
+    for _ in range(args.icp_reps):
+        r = lc.align(keep_aligned=False)
+        iters += r.iterations
+    barrier()
+    icp_s = time.perf_counter() - ti
+    if dist is not None:
+        t = torch.tensor([icp_s], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        icp_s = float(t.item())
+    itm = lc.timing()
+    lc.set_timing(False)
+    tf = time.perf_counter()  # the whole icpAlignment (warm handle): source binning + target grid + align
+    lc.setInputSource(src)
+    lc.setInputTarget(dst)
+    lc.align(keep_aligned=False)
+    barrier()
+    full_ms = (time.perf_counter() - tf) * 1e3
+    passes = itm["icp_launches"]
+    shard_n = len(src) // world
+    icp_kernel_ms = itm["icp_ms"] / max(passes, 1)
+    nn_ms = itm["icp_nn_ms"] / max(itm["icp_nn_launches"], 1)
+    loop_icp = {"config": "C4: 500k vs 500k, voxel 0.3 m, 2.5 m / 4 deg initial offset, PCL ICP semantics",
+                "n_gpus": world, "passes_per_alignment": passes / max(args.icp_reps, 1),
+                "ms_per_alignment": round(icp_s / args.icp_reps * 1e3, 3),
+                "iterations": r.iterations, "ms_per_iteration": round(icp_s / max(iters, 1) * 1e3, 3),
+                "exchange": exchange, "ms_full_icpAlignment": round(full_ms, 3),
+                "score": r.score, "converged": bool(r.is_converged), "scaling": "strong",
+                # the pass (correspondence + statistics kernels) and the correspondence kernel alone
+                "kernel_ms_per_pass": round(icp_kernel_ms, 4),
+                "nn_kernel_ms_per_pass": round(nn_ms, 4),
+                "kernel_gbs": round(BYTES_PER_PT_ICP * shard_n / (icp_kernel_ms * 1e-3) / 1e9, 2)
+                if passes else None}
+    return loop_icp, src, dst
 
 
 def main():
@@ -328,6 +392,53 @@ def main():
                 "reuse_achieved_gbs": round(BYTES_PER_PT_REUSE * n_pts / (reuse_avg_ms * 1e-3) / 1e9, 2)
                 if tm["reuse_launches"] else None}
 
+    line = {
+        "metric": "scans/sec (100k-pt scan vs N-pt map) + ms/IESKF-iteration, 1 GPU",
+        "value": round(value, 3), "unit": "scans/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "f32/f64",
+        "data": "synthetic (seeded urban-canyon scene, ray-cast scans; no datasets offline)",
+        "config": {"workload": f"{args.config}: {sp}-pt {kind} scan vs {mp}-pt "
+                               + (f"map grown by {incr['scans']} scans (map_incremental)" if incr else "static map")
+                               + ", "
+                               "max_iteration=3 (<=4 h-evals/scan)",
+                   "scan_points": sp, "map_points": mp, "resident_scans": len(scans),
+                   "parallelism": f"replicas x{world} (front end does not shard)"},
+        "ms_per_ieskf_iteration": round(ms_per_iter, 4),
+        "ms_per_step_pct": {q: round(float(np.percentile(t_steps, int(q[1:]))) * 1e3, 4)
+                            for q in ("p10", "p50", "p90", "p99")},  # this rank's per-step spread
+        "capi_ms_per_scan": round(capi_ms / args.steps, 4),
+        "host_ms_per_scan": {"launch": round(launch_ms / args.steps, 4), "wait": round(wait_ms / args.steps, 4),
+                             "ieskf_algebra": round(solve_ms / args.steps, 4)},
+        "h_evals_per_scan": round(h_evals / args.steps, 3), "knn_evals_per_scan": round(knn_calls / args.steps, 3),
+        "pos_err_m": round(float(np.mean(pos_err)), 5) if pos_err else None,
+        "map_build_ms": round(build_ms, 2), "input_gen_s": round(gen_s, 1),
+        "upload_inclusive": {"scans_per_s": round(args.steps / up_s, 3),
+                             "ms_per_step": round(up_s / args.steps * 1e3, 4),
+                             "bytes_per_scan": 12 * sp,
+                             "note": "scan uploaded from pinned host memory by lio_scan_set inside each step "
+                                     "(rank-local; PCIe included)"},
+        "roofline": roofline, "cpu_baseline": None, "loop_icp": None, "multi_stream": None, "map_incremental": incr,
+        "pipeline": None,
+    }
+
+    # the headline is measured; the secondary keys follow.  N > 1: a watchdog prints what rank 0 has if a
+    # collective of the secondary sections (the loop ICP's RCCL exchange) never returns, so a hang there
+    # cannot cost the scaling run its line
+    watchdog = None
+    if dist is not None:
+        import threading
+
+        def _abandon():
+            if rank == 0:
+                line["watchdog"] = f"secondary sections abandoned after {args.watchdog_s:.0f} s"
+                print(json.dumps(line), flush=True)
+            os._exit(0)
+
+        watchdog = threading.Timer(args.watchdog_s, _abandon)
+        watchdog.daemon = True
+        watchdog.start()
+
     # ------------------------------------------------- C5 stream with its loop leg (secondary)
     pipeline = None
     if args.pipeline > 0 and rank == 0:
@@ -383,6 +494,7 @@ def main():
         fs.close()
         ptree.close()
         del d_pmap
+    line["pipeline"] = pipeline
 
     # ------------------------------------------------- several scan streams on one GPU (secondary)
     # One stream is latency-bound (host round trip per h-evaluation); independent sensors / robots
@@ -427,65 +539,20 @@ def main():
                 h_s.close()
             del sess
 
-    # ------------------------------------------------------------- loop ICP (sharded)
-    loop_icp = None
-    if not args.no_icp:
-        # C4 with a 2.5 m / 4 deg initial offset: PCL's criteria with the reference's epsilons take 9
-        # iterations (the 0.3 m / 1.5 deg pair of round 1 converged after 1, so ms/iteration meant nothing)
-        src, dst, Tgt = synth.make_icp_pair(n_points=500_000, seed=4321, disp=(2.5, 4.0))
-        lc = LC.LoopClosure(LC.LoopClosureConfig(), device=local)
-        cb = None
-        exchange = "none (1 rank)"
-        if world > 1:
-            from lio_gpu import dist as ldist
+    line["multi_stream"] = multi
 
-            if rehearse:  # gloo on CPU tensors: the records pass through host memory
-                cb = ldist.make_allgather(device=coll_dev)
-                lc.set_shard(rank, world, cb)
-                exchange = "host (gloo rehearsal)"
-            else:  # RCCL all-gather of device buffers on the ICP handle's stream, record-order sum on the GPU
-                cb = ldist.DeviceExchange()
-                lc.set_shard_device(rank, world, cb)
-                exchange = "device (RCCL all_gather_into_tensor on the handle's stream)"
-        lc.setInputSource(src)
-        lc.setInputTarget(dst)
-        lc.align(keep_aligned=False)
-        lc.set_timing(True)
-        barrier()
-        ti = time.perf_counter()
-        iters = 0
-        for _ in range(args.icp_reps):
-            r = lc.align(keep_aligned=False)
-            iters += r.iterations
-        barrier()
-        icp_s = time.perf_counter() - ti
-        if dist is not None:
-            t = torch.tensor([icp_s], dtype=torch.float64, device=coll_dev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            icp_s = float(t.item())
-        itm = lc.timing()
-        lc.set_timing(False)
-        tf = time.perf_counter()  # the whole icpAlignment (warm handle): source binning + target grid + align
-        lc.setInputSource(src)
-        lc.setInputTarget(dst)
-        lc.align(keep_aligned=False)
-        barrier()
-        full_ms = (time.perf_counter() - tf) * 1e3
-        passes = itm["icp_launches"]
-        shard_n = len(src) // world
-        icp_kernel_ms = itm["icp_ms"] / max(passes, 1)
-        nn_ms = itm["icp_nn_ms"] / max(itm["icp_nn_launches"], 1)
-        loop_icp = {"config": "C4: 500k vs 500k, voxel 0.3 m, 2.5 m / 4 deg initial offset, PCL ICP semantics",
-                    "n_gpus": world, "passes_per_alignment": passes / max(args.icp_reps, 1),
-                    "ms_per_alignment": round(icp_s / args.icp_reps * 1e3, 3),
-                    "iterations": r.iterations, "ms_per_iteration": round(icp_s / max(iters, 1) * 1e3, 3),
-                    "exchange": exchange, "ms_full_icpAlignment": round(full_ms, 3),
-                    "score": r.score, "converged": bool(r.is_converged), "scaling": "strong",
-                    # the pass (correspondence + statistics kernels) and the correspondence kernel alone
-                    "kernel_ms_per_pass": round(icp_kernel_ms, 4),
-                    "nn_kernel_ms_per_pass": round(nn_ms, 4),
-                    "kernel_gbs": round(BYTES_PER_PT_ICP * shard_n / (icp_kernel_ms * 1e-3) / 1e9, 2)
-                    if passes else None}
+    # ------------------------------------------------------------- loop ICP (sharded)
+    loop_icp = src = dst = None
+    if not args.no_icp:
+        try:
+            loop_icp, src, dst = _loop_icp(args, LC, synth, local, world, rank, dist, rehearse, coll_dev, barrier, torch)
+        except Exception as e:  # N > 1: an exchange failure must not cost the headline line
+            if world == 1:
+                raise
+            import traceback
+
+            traceback.print_exc()
+            loop_icp = {"error": f"{type(e).__name__}: {e}"}
 
     # ------------------------------------------------------------- CPU baseline
     cpu = None
@@ -544,35 +611,10 @@ def main():
                "by_threads": {str(k): v for k, v in by_thr.items()},
                "host_cpus": os.cpu_count(), "cpu_model": _cpu_model()}
 
+    if watchdog is not None:
+        watchdog.cancel()
     if rank == 0:
-        line = {
-            "metric": "scans/sec (100k-pt scan vs N-pt map) + ms/IESKF-iteration, 1 GPU",
-            "value": round(value, 3), "unit": "scans/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f32/f64",
-            "data": "synthetic (seeded urban-canyon scene, ray-cast scans; no datasets offline)",
-            "config": {"workload": f"{args.config}: {sp}-pt {kind} scan vs {mp}-pt "
-                                   + (f"map grown by {incr['scans']} scans (map_incremental)" if incr else "static map")
-                                   + ", "
-                                   "max_iteration=3 (<=4 h-evals/scan)",
-                       "scan_points": sp, "map_points": mp, "resident_scans": len(scans),
-                       "parallelism": f"replicas x{world} (front end does not shard)"},
-            "ms_per_ieskf_iteration": round(ms_per_iter, 4),
-            "ms_per_step_pct": {q: round(float(np.percentile(t_steps, int(q[1:]))) * 1e3, 4)
-                                for q in ("p10", "p50", "p90", "p99")},  # this rank's per-step spread
-            "capi_ms_per_scan": round(capi_ms / args.steps, 4),
-            "host_ms_per_scan": {"launch": round(launch_ms / args.steps, 4), "wait": round(wait_ms / args.steps, 4),
-                                 "ieskf_algebra": round(solve_ms / args.steps, 4)},
-            "h_evals_per_scan": round(h_evals / args.steps, 3), "knn_evals_per_scan": round(knn_calls / args.steps, 3),
-            "pos_err_m": round(float(np.mean(pos_err)), 5) if pos_err else None,
-            "map_build_ms": round(build_ms, 2), "input_gen_s": round(gen_s, 1),
-            "upload_inclusive": {"scans_per_s": round(args.steps / up_s, 3),
-                                 "ms_per_step": round(up_s / args.steps * 1e3, 4),
-                                 "bytes_per_scan": 12 * sp,
-                                 "note": "scan uploaded from pinned host memory by lio_scan_set inside each step "
-                                         "(rank-local; PCIe included)"},
-            "roofline": roofline, "cpu_baseline": cpu, "loop_icp": loop_icp, "multi_stream": multi, "map_incremental": incr, "pipeline": pipeline,
-        }
+        line.update({"cpu_baseline": cpu, "loop_icp": loop_icp, "multi_stream": multi, "pipeline": pipeline})
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()

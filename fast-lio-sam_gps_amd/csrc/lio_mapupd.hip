@@ -82,7 +82,7 @@ enum : int {
 constexpr uint32_t kFlagRuns = 16u;
 // grouped update: sort blocks of kGrpB consecutive points (group_sort_kernel), the append in the same
 // blocks (update_kernel)
-constexpr int kGrpT = 256, kGrpI = 8, kGrpB = kGrpT * kGrpI;
+constexpr int kGrpT = 256, kGrpI = 4, kGrpB = kGrpT * kGrpI;
 constexpr int kMaxRuns = 64;  // runs a voxel may have (its points spread over <= 64 sort blocks)
 // vox_resolve_kernel's trigger / tombstone totals: one pair of counters per 64-byte line, kSpread of them
 // (block b adds to line b % kSpread), folded into cnt[kCTrig] / cnt[kCDead] and cleared by append_kernel.

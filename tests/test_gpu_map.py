@@ -59,7 +59,7 @@ def test_add_points_downsample_parity(oracle, scene_scans):
 
 
 def test_add_points_scrambled_order(oracle, scene_scans):
-    """Voxels whose points are spread over many of the grouped update's 2048-point sort blocks (input
+    """Voxels whose points are spread over many of the grouped update's 1024-point sort blocks (input
     order shuffled): the runs are re-ordered per voxel, so counters and map stay bit-exact."""
     _, m, scans = scene_scans
     base = m[:50000]
@@ -70,13 +70,17 @@ def test_add_points_scrambled_order(oracle, scene_scans):
     w = np.concatenate([oracle.body_to_world(synth.pose24(synth.initial_state(sc.pos_gt, sc.rot_gt)), sc.body)
                         for sc in scans[:3]])
     w = w[rng.permutation(len(w))]
-    w = np.concatenate([w, w[:5000]])  # exact duplicates later in the order (ties on the centre distance)
-    assert tree.Add_Points(w, True) == om.add(w, True, 0.5)
+    # <= 32 sort blocks: every voxel stays on the run-list path (up to 32 runs re-ordered per voxel)
+    part = np.concatenate([w[:28000], w[:4000]])  # exact duplicates later in the order (ties on the centre distance)
+    assert tree.Add_Points(part, True) == om.add(part, True, 0.5)
+    _same_map(tree, om)
+    rest = w[28000:]  # all of it: dense voxels may span > 64 blocks (the sorted fallback)
+    assert tree.Add_Points(rest, True) == om.add(rest, True, 0.5)
     _same_map(tree, om)
 
 
 def test_add_points_voxel_over_many_blocks(oracle, scene_scans):
-    """One voxel offered 150k points (> 64 sort blocks): the grouped update is abandoned on the device
+    """One voxel offered 150k points (> 64 sort blocks of 1024): the grouped update is abandoned on the device
     and redone through the globally sorted path — same result."""
     _, m, _ = scene_scans
     base = m[:20000]
