@@ -71,6 +71,7 @@ for s in $STEPS; do
     mapprof) run map_prof 400 rocprofv3 --kernel-trace --stats -d "$OUT/mapprof" -o run --output-format csv -- python scripts/map_incr_timing.py 20 ;;
     nearab) run near_ab 600 bash -c 'for r in 1 2; do python scripts/near_ab.py C3 && LIO_GPU_LIB=build_ab/noslab/liblio_gpu.so python scripts/near_ab.py C3 || exit $?; done' ;;
     icpseed) run icpseed_ab 600 bash -c 'for r in 1 2; do python scripts/icp_ab.py 1.0 5 && LIO_GPU_LIB=fast-lio-sam_gps_amd/build_ab/noseed/liblio_gpu.so python scripts/icp_ab.py 1.0 5 || exit $?; done' ;;
+    icppre) run icppre_ab 900 bash -c 'for r in 1 2; do for v in default pre0 pre4 pre025; do if [ $v = default ]; then python scripts/icp_ab.py 1.0 5; else LIO_GPU_LIB=fast-lio-sam_gps_amd/build_ab/$v/liblio_gpu.so python scripts/icp_ab.py 1.0 5; fi || exit $?; echo "^ $v"; done; done' ;;
     icptrace) run icp_trace 300 rocprofv3 --kernel-trace -d "$OUT/icptrace" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 ;;
     watchdog) LIO_BENCH_REHEARSE=1 run watchdog2 300 python bench.py --gpus 2 --steps 20 --warmup 2 --pipeline 0 --no-cpu --streams '' --icp-reps 1 --watchdog-s 0.5 ;;
     *) echo "unknown step $s" ;;
