@@ -63,9 +63,6 @@ constexpr int kTileCh = 256;  // candidates staged per LDS round
 // ...: its blocks walk those in cell order (first pass) or in the order icp_order_kernel wrote for its
 // share (later passes).  -1: a slot past the XCD's share.
 constexpr int kIcpSegs = 64;
-#ifndef LIO_ICP_CONTIG
-#define LIO_ICP_CONTIG 0  // A/B: 1 = later passes in cost-balanced contiguous XCD shares, 2 = first pass contiguous too
-#endif
 __device__ __forceinline__ int icp_seg_begin(int s, int n) { return (int)(((int64_t)s * n) / kIcpSegs); }
 __device__ __forceinline__ int icp_tile_of(const uint32_t* order, int b, int n) {
     const int x = b & 7;
@@ -74,12 +71,6 @@ __device__ __forceinline__ int icp_tile_of(const uint32_t* order, int b, int n) 
         const int lo = (int)order[n + x], hi = (int)order[n + x + 1];
         return lo + slot < hi ? (int)order[lo + slot] : -1;
     }
-#if LIO_ICP_CONTIG >= 2
-    {
-        const int lo = (int)(((int64_t)x * n) >> 3), hi = (int)(((int64_t)(x + 1) * n) >> 3);
-        return lo + slot < hi ? lo + slot : -1;
-    }
-#endif
     for (int s = x; s < kIcpSegs; s += 8) {
         const int b0 = icp_seg_begin(s, n), sz = icp_seg_begin(s + 1, n) - b0;
         if (slot < sz) return b0 + slot;
@@ -563,14 +554,7 @@ __global__ void __launch_bounds__(kIcpStatsThreads) icp_stats_kernel(IcpArgs a, 
 void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st) {
     if (a.n == 0 || ntiles == 0) return;
     const int seg = (ntiles + kIcpSegs - 1) / kIcpSegs;
-    int blocks = 8 * (kIcpSegs / 8) * seg;
-#if LIO_ICP_CONTIG >= 1
-    if (a.order) blocks = 8 * (ntiles / 4 + 2);  // a cost-balanced share holds at most n/4 + 1 tiles
-#endif
-#if LIO_ICP_CONTIG >= 2
-    if (!a.order) blocks = 8 * ((ntiles + 7) / 8);
-#endif
-    icp_tile_kernel<1, 1><<<blocks, kIcpTileQ, 0, st>>>(a, ntiles);
+    icp_tile_kernel<1, 1><<<8 * (kIcpSegs / 8) * seg, kIcpTileQ, 0, st>>>(a, ntiles);
 }
 
 // Tile order for the next pass from this pass's candidate counts.  The cell-ordered tiles are cut
@@ -587,63 +571,6 @@ __global__ void __launch_bounds__(256) icp_order_kernel(const uint32_t* __restri
     __shared__ uint32_t hist[33], base[33];
     const int x = (int)blockIdx.x;
     if (threadIdx.x < 33) hist[threadIdx.x] = 0;
-#if LIO_ICP_CONTIG >= 1
-    // XCD x owns the contiguous cell-order range [lo, hi) that carries 1/8 of the pass's cost (+1 per
-    // tile), each boundary clamped to k n / 8 +- n / 16 (a share holds at most n / 4 + 1 tiles: the
-    // grid launch_icp_tiles sizes).  Every block computes the same integer prefix, so the shares tile
-    // [0, n) exactly.
-    {
-        __shared__ unsigned long long s_sum[256];
-        __shared__ uint32_t s_cnt[2];
-        const int per = (n + 255) / 256, t0 = min((int)threadIdx.x * per, n), t1 = min(t0 + per, n);
-        unsigned long long own = 0;
-        for (int t = t0; t < t1; ++t) own += (unsigned long long)cost[t] + 1ull;
-        s_sum[threadIdx.x] = own;
-        if (threadIdx.x < 2) s_cnt[threadIdx.x] = 0;
-        __syncthreads();
-        for (int d = 1; d < 256; d <<= 1) {  // inclusive scan (Hillis-Steele)
-            const unsigned long long v = threadIdx.x >= (unsigned)d ? s_sum[threadIdx.x - d] : 0ull;
-            __syncthreads();
-            s_sum[threadIdx.x] += v;
-            __syncthreads();
-        }
-        const unsigned long long total = s_sum[255];
-        unsigned long long run = s_sum[threadIdx.x] - own;  // exclusive prefix of t0
-        const unsigned long long k0 = (unsigned long long)x * total, k1 = (unsigned long long)(x + 1) * total;
-        uint32_t c0 = 0, c1 = 0;  // tiles whose exclusive prefix lies below k / 8 of the total
-        for (int t = t0; t < t1; ++t) {
-            c0 += run * 8ull < k0;
-            c1 += run * 8ull < k1;
-            run += (unsigned long long)cost[t] + 1ull;
-        }
-        if (c0) atomicAdd(&s_cnt[0], c0);
-        if (c1) atomicAdd(&s_cnt[1], c1);
-        __syncthreads();
-        auto clampb = [n](int k, int b) {
-            if (k <= 0) return 0;
-            if (k >= 8) return n;
-            const int c = (int)(((int64_t)k * n) >> 3), w = n / 16;
-            return min(max(b, max(c - w, 0)), min(c + w, n));
-        };
-        const int lo = clampb(x, (int)s_cnt[0]), hi = clampb(x + 1, (int)s_cnt[1]);
-        if (threadIdx.x == 0) {
-            order[n + x] = (uint32_t)lo;
-            if (x == 0) order[n + 8] = (uint32_t)n;
-        }
-        for (int t = lo + (int)threadIdx.x; t < hi; t += 256) atomicAdd(&hist[cost_bucket(cost[t])], 1u);
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            uint32_t acc = (uint32_t)lo;
-            for (int b = 32; b >= 0; --b) {  // longest first
-                base[b] = acc;
-                acc += hist[b];
-            }
-        }
-        __syncthreads();
-        for (int t = lo + (int)threadIdx.x; t < hi; t += 256) order[atomicAdd(&base[cost_bucket(cost[t])], 1u)] = (uint32_t)t;
-        return;
-    }
-#endif
     __syncthreads();
     for (int s = x; s < kIcpSegs; s += 8)
         for (int t = icp_seg_begin(s, n) + (int)threadIdx.x; t < icp_seg_begin(s + 1, n); t += 256)
