@@ -8,7 +8,7 @@
 //                    float SSE order [U]), exact unbounded 1-NN in the target
 //                    grid with the candidate points staged through LDS once
 //                    per tile; tiles visited longest-first in the pass after
-//                    the first (icp_order_kernel, from this pass's counts)
+//                    the first (icp_order_share, from this pass's counts)
 //   icp_stats_kernel one 1024-thread block per 4096-point record: Umeyama
 //                    sufficient statistics of the accepted correspondences
 //                    (d2 <= 52.5^2) in double about a fixed centre c0:
@@ -60,7 +60,7 @@ constexpr int kTileCh = 256;  // candidates staged per LDS round
 
 // Tiles -> blocks (launch_icp_tiles: 8 x (kIcpSegs / 8) x ceil(n / kIcpSegs) blocks; block b runs on
 // XCD b % 8).  The cell-ordered tiles form kIcpSegs contiguous segments; XCD x owns segments x, x + 8,
-// ...: its blocks walk those in cell order (first pass) or in the order icp_order_kernel wrote for its
+// ...: its blocks walk those in cell order (first pass) or in the order icp_order_share wrote for its
 // share (later passes).  -1: a slot past the XCD's share.
 constexpr int kIcpSegs = 64;
 __device__ __forceinline__ int icp_seg_begin(int s, int n) { return (int)(((int64_t)s * n) / kIcpSegs); }
@@ -496,7 +496,18 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
 // sums are added in wave order.  A fixed order for a given record, so the
 // records (what ranks all-gather) are bit-identical for any number of ranks.
 constexpr int kIcpStatsThreads = 1024;
-__global__ void __launch_bounds__(kIcpStatsThreads) icp_stats_kernel(IcpArgs a, double* __restrict__ super) {
+template <int NT>
+__device__ void icp_order_share(const uint32_t* __restrict__ cost, int n, uint32_t* __restrict__ order, int x);
+
+// Blocks [0, nsup) write the records; when `order` is given, blocks nsup .. nsup + 7 build the next
+// pass's tile order for the eight XCD shares in the same launch (they only read this pass's tile costs),
+// so the order runs beside the records instead of between them and the next pass.
+__global__ void __launch_bounds__(kIcpStatsThreads) icp_stats_kernel(IcpArgs a, double* __restrict__ super, int nsup,
+                                                                     uint32_t* __restrict__ order, int ntiles) {
+    if ((int)blockIdx.x >= nsup) {  // block-uniform
+        icp_order_share<kIcpStatsThreads>(a.tile_cost, ntiles, order, (int)blockIdx.x - nsup);
+        return;
+    }
     constexpr int NW = kIcpStatsThreads / 64, PER = kIcpSuper / kIcpStatsThreads;
     __shared__ double red[NW][kIcpStride];
     double v[32];
@@ -560,21 +571,33 @@ void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st) {
 // Tile order for the next pass from this pass's candidate counts.  The cell-ordered tiles are cut
 // into kIcpSegs contiguous segments (spatially compact: their target neighbourhoods stay in one
 // XCD's L2), XCD x owns segments x, x + 8, ... (a misaligned region, which is spatially concentrated,
-// is shared by every XCD), and inside each XCD's share the tiles run longest-first (log2 buckets of
-// the count, descending) so the heavy ones do not form the tail.  Layout: order[0 .. n) the eight
-// shares one after another, order[n + x] the first entry of share x (order[n + 8] = n).
-// One block per share (the share sizes follow from the segment bounds, so no block waits for
-// another): it sits between two dependent passes, so it has to be short.
+// is shared by every XCD; contiguous cost-balanced shares measured slower, profiles/r03_icp_contig_ab.txt),
+// and inside each XCD's share the tiles run longest-first (log2 buckets of the count, descending) so the
+// heavy ones do not form the tail.  Layout: order[0 .. n) the eight shares one after another,
+// order[n + x] the first entry of share x (order[n + 8] = n).  One block per share (the share sizes
+// follow from the segment bounds, so no block waits for another), run by icp_stats_kernel's last eight
+// blocks beside the records.
 __device__ __forceinline__ uint32_t cost_bucket(uint32_t c) { return c ? 32u - (uint32_t)__clz(c) : 0u; }
-__global__ void __launch_bounds__(256) icp_order_kernel(const uint32_t* __restrict__ cost, int n,
-                                                        uint32_t* __restrict__ order) {
+// entry f of share x in cell order (-1 past its end)
+__device__ __forceinline__ int icp_share_tile(int x, int f, int n) {
+#pragma unroll
+    for (int j = 0; j < kIcpSegs / 8; ++j) {
+        const int b0 = icp_seg_begin(x + 8 * j, n), sz = icp_seg_begin(x + 8 * j + 1, n) - b0;
+        if (f < sz) return b0 + f;
+        f -= sz;
+    }
+    return -1;
+}
+template <int NT>
+__device__ void icp_order_share(const uint32_t* __restrict__ cost, int n, uint32_t* __restrict__ order, int x) {
     __shared__ uint32_t hist[33], base[33];
-    const int x = (int)blockIdx.x;
     if (threadIdx.x < 33) hist[threadIdx.x] = 0;
     __syncthreads();
-    for (int s = x; s < kIcpSegs; s += 8)
-        for (int t = icp_seg_begin(s, n) + (int)threadIdx.x; t < icp_seg_begin(s + 1, n); t += 256)
-            atomicAdd(&hist[cost_bucket(cost[t])], 1u);
+    for (int f = (int)threadIdx.x;; f += NT) {
+        const int t = icp_share_tile(x, f, n);
+        if (t < 0) break;
+        atomicAdd(&hist[cost_bucket(cost[t])], 1u);
+    }
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t acc = 0;  // this share's first entry: the sizes of shares 0 .. x-1
@@ -588,12 +611,11 @@ __global__ void __launch_bounds__(256) icp_order_kernel(const uint32_t* __restri
         }
     }
     __syncthreads();
-    for (int s = x; s < kIcpSegs; s += 8)
-        for (int t = icp_seg_begin(s, n) + (int)threadIdx.x; t < icp_seg_begin(s + 1, n); t += 256)
-            order[atomicAdd(&base[cost_bucket(cost[t])], 1u)] = (uint32_t)t;
-}
-void launch_icp_order(const uint32_t* tile_cost, int ntiles, uint32_t* order, hipStream_t st) {
-    if (ntiles > 0) icp_order_kernel<<<8, 256, 0, st>>>(tile_cost, ntiles, order);
+    for (int f = (int)threadIdx.x;; f += NT) {
+        const int t = icp_share_tile(x, f, n);
+        if (t < 0) break;
+        order[atomicAdd(&base[cost_bucket(cost[t])], 1u)] = (uint32_t)t;
+    }
 }
 
 // per cell: number of tiles (ceil(count / 64)); slot ncells = 0 for the scan's total
@@ -794,9 +816,11 @@ void launch_icp_combine(const double* recv, int64_t nsup, int world, int64_t slo
     icp_combine_kernel<<<1, 64, 0, st>>>(recv, nsup, world, slot, out17);
 }
 
-void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st) {
+void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st, uint32_t* order, int ntiles) {
     if (a.n == 0) return;
-    icp_stats_kernel<<<(a.n + kIcpSuper - 1) / kIcpSuper, kIcpStatsThreads, 0, st>>>(a, super);
+    const int nsup = (a.n + kIcpSuper - 1) / kIcpSuper;
+    const bool ord = order && ntiles > 0;
+    icp_stats_kernel<<<nsup + (ord ? 8 : 0), kIcpStatsThreads, 0, st>>>(a, super, nsup, ord ? order : nullptr, ntiles);
 }
 
 }  // namespace lio

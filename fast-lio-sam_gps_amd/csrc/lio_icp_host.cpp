@@ -586,14 +586,15 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
         if (h->sh_n > 0) lio::launch_icp_tiles(a, h->ntiles, h->st);
         if (h->timing) IHIP(hipEventRecord(h->ev.m, h->st));
         if (dev_x) {  // records -> device send buffer -> in-stream all-gather -> record-order sum
-            if (h->sh_n > 0) lio::launch_icp_stats(a, h->d_xsend, h->st);
+            if (h->sh_n > 0) lio::launch_icp_stats(a, h->d_xsend, h->st, fitness ? nullptr : h->d_order, h->ntiles);
             IHIP(hipGetLastError());
             if (h->fn_dev(h->d_xsend, h->x_len, h->d_xrecv, (void*)h->st, h->user_dev) != 0)
                 return ifail(LIO_ERR_STATE, "device all-gather callback failed");
             const int64_t nsup = (h->ns + lio::kIcpSuper - 1) / lio::kIcpSuper;
             lio::launch_icp_combine(h->d_xrecv, nsup, h->world, h->x_len / lio::kIcpStride, h->h_out17_dev, h->st);
         } else {
-            lio::launch_icp_stats(a, h->h_super_dev, h->st);  // records straight to host memory
+            // records straight to host memory; the next pass's tile order in the same launch
+            lio::launch_icp_stats(a, h->h_super_dev, h->st, fitness ? nullptr : h->d_order, h->ntiles);
         }
         if (h->timing) IHIP(hipEventRecord(h->ev.b, h->st));
         if (pcl16) {  // PCL-order fidelity mode: the serial float sums of this pass's correspondences
@@ -602,11 +603,6 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
         }
         IHIP(hipGetLastError());
         IHIP(hipEventRecord(h->ev.done, h->st));
-        // longest-first order for the next pass of this alignment: behind the records, so it runs
-        // while the host does the SVD / convergence test
-        if (!fitness)
-            lio::launch_icp_order(h->d_tcost, h->ntiles, h->d_order, h->st);
-        IHIP(hipGetLastError());
         IHIP(hipEventSynchronize(h->ev.done));
     } else {
         IHIP(hipStreamSynchronize(h->st));

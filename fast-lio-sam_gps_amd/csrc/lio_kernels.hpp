@@ -159,8 +159,8 @@ constexpr int kIcpTileQ = 64;     // queries per tile (one wave)
 int icp_build_tiles(const GridBuf& q, uint2* tiles, uint32_t* scratch, void*& tmp, size_t& tmp_bytes, hipStream_t st);
 void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st);
 // tile order for the next pass: descending log2(cost) buckets (one block)
-void launch_icp_order(const uint32_t* tile_cost, int ntiles, uint32_t* order, hipStream_t st);
-void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st);  // one record per 4096 points
+// one record per 4096 points; with `order`, the next pass's tile order from a.tile_cost in the same launch
+void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st, uint32_t* order = nullptr, int ntiles = 0);
 // the all-gathered records (world slots of `slot` records) summed in global record order, one thread
 // per statistic (the order of lio_icp_combine: bit-identical) -> out17 (host-mapped)
 void launch_icp_combine(const double* recv, int64_t nsup, int world, int64_t slot, double* out17, hipStream_t st);

@@ -2,7 +2,7 @@
 # ICP tile-order A/B (GPU box): default (64 interleaved segments) vs cost-balanced contiguous XCD shares
 # in later passes (contig1) and in every pass (contig2).  Per variant: parity (ICP tests), 2 x 5 alignments
 # per pair (scripts/icp_ab.py), FETCH_SIZE / WRITE_SIZE per icp_tile_kernel dispatch.
-# usage: scripts/icp_contig_ab.sh <outdir> [variants...]
+# usage: [NOPMC=1] scripts/icp_contig_ab.sh <outdir> [variants...]   (variant: default = the in-tree build, else build_ab/<name>)
 set -u
 OUT=${1:-gpurun_out/icpab}; shift || true
 VARS=${*:-"default contig1 contig2"}
@@ -26,6 +26,7 @@ for r in 1 2; do
         step "time_${v}_$r" 200 python scripts/icp_ab.py 1.0 5
     done
 done
+[ -n "${NOPMC:-}" ] && { echo "icp ab done (no PMC)"; exit 0; }
 for v in $VARS; do
     export LIO_GPU_LIB=$(lib $v)
     for c in FETCH_SIZE WRITE_SIZE; do
