@@ -89,12 +89,8 @@ __device__ __forceinline__ void wave_sync() {
 // staged candidates as structure of arrays: 4 consecutive x (y, z, id) are one
 // 16-byte broadcast read, and two candidates' coordinates sit in one register
 // pair for the packed FP32 distance (v_pk_add_f32 / v_pk_mul_f32)
-#ifndef LIO_ICP_MFMA
-#define LIO_ICP_MFMA 1  // staged candidates tested by v_mfma_f32_16x16x4_f32 (0: the packed-FP32 VALU test)
-#endif
-constexpr int kLs = kTileCh + 16;  // coordinate array stride: the 4 lane groups of the MFMA operand read hit distinct banks
 struct alignas(16) TileLds {
-    float x[kLs], y[kLs], z[kLs], w[kLs];  // staged candidates (w = |p - c|^2 about the tile centre c)
+    float x[kTileCh], y[kTileCh], z[kTileCh];
     uint32_t id[kTileCh];
     union {  // the row permutation is read into registers before the slot table is written
         struct {
@@ -125,27 +121,6 @@ __device__ __forceinline__ double key_pk(uint32_t id0, uint32_t id1, f2v d) {
         asm("v_pk_mov_b32 %0, %1, %2 op_sel:[1,1]" : "=v"(k) : "v"(ids), "v"(d));
     return k;
 }
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// Per-lane state of the MFMA candidate test.  The staged candidates are tested 16 at a time against
-// the 64 queries as four 16 x 16 blocks: D = A B, A[m][k] = (p'_m, |p'_m|^2), B[k][n] = (-2 q'_n, 1),
-// p' = p - c, q' = q - c about the tile centre c, so D[m][n] + |q'_n|^2 approximates |q_n - p_m|^2.
-// v_mfma_f32_16x16x4_f32: lane l supplies A[l & 15][l >> 4] and B[l >> 4][l & 15] and receives
-// D[4 (l >> 4) + r][l & 15], r = 0..3 — so lane l follows queries (l & 15) + 16 b, b = 0..3 (slot b),
-// each over a quarter of the candidates.  The approximation only FILTERS: an entry whose D is within
-// thr = best + eps - |q'|^2 (eps bounds the MFMA / translation / float rounding, 10x margin) gets the
-// exact float ((dx*dx + dy*dy) + dz*dz) from the absolute coordinates and the (d2, id) minimum, so the
-// result is the exact 1-NN whatever the approximation error below the margin.
-struct TileQ {
-    float c0, c1, c2;          // tile centre (wave-uniform)
-    float ck;                  // the centre's component k = lane >> 4 (0 for k = 3)
-    float bq[4];               // B operand of slot b
-    float qx[4], qy[4], qz[4]; // slot b's query (absolute)
-    float qn2[4];              // |q'|^2 of slot b's query (+inf: inactive slot)
-    float thr[4];
-    double bk[4];              // slot b's (d2, id) key over the candidates this lane saw (merged per chunk)
-};
 
 // wave maximum of non-negative floats (as integers: same order), wave-uniform: DPP inside
 // each row of 16 (quad swaps, half-row and row mirrors), then the four row maxima by readlane
@@ -215,19 +190,10 @@ __device__ __forceinline__ float interval_gap(float lo, float hi, float a, float
 // The bound is the wave's own maximum best, refreshed per chunk (each wave's lanes
 // keep the best over the chunks that wave saw, which is all the filter needs); the
 // margin (1 - 1e-5) covers the float rounding of both the box gap and d2.
-// filter threshold of a slot: an entry can hold a key <= the slot's best only if D <= best + eps - |q'|^2;
-// eps = 1e-5 (best + W + |q'|^2) + 1e-7 bounds the MFMA (an fma chain), |p'|^2, |q'|^2, translation and
-// exact-d2 rounding (each <= ~16 u (W + |q'|^2 + best), u = 2^-24) ten times over; W = max |p'|^2 of the
-// chunk.  -inf for an inactive slot (never flagged), +inf while the slot has no candidate.
-__device__ __forceinline__ float icp_thr(double bk, float qn2, float W) {
-    const float b = __uint_as_float((uint32_t)((uint64_t)__double_as_longlong(bk) >> 32));
-    return qn2 == INFINITY ? -INFINITY : (b + 1e-5f * ((b + W) + qn2) + 1e-7f) - qn2;
-}
-
 template <int NW>  // waves per tile: the tile's candidate stream is split over them
 __device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32_t b0, uint32_t n0, uint32_t b1,
                                             uint32_t n1, bool act, float x, float y, float z, const float (&qb)[6],
-                                            uint64_t& best, unsigned long long& cand, uint32_t& tested, TileQ& tq) {
+                                            uint64_t& best, unsigned long long& cand, uint32_t& tested) {
     // the wave's index within its tile (several one-wave tiles per block: always 0)
     const int lane = threadIdx.x & 63, w = NW > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
     const uint32_t n = n0 + n1;
@@ -262,7 +228,6 @@ __device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32
         // the wave's bound: its active lanes' largest best (+inf while one has none)
         const float Bw = wave_max_nonneg(act ? __uint_as_float((uint32_t)(best >> 32)) : 0.f);
         uint32_t cnt = 0;
-        float wmax = 0.f;
 #pragma unroll
         for (int u = 0; u < U; ++u) {  // survivors compacted in stream order
             const float gx = fmaxf(fmaxf(qb[0] - v[u].x, v[u].x - qb[1]), 0.f);
@@ -277,82 +242,18 @@ __device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32
                 L.y[r] = v[u].y;
                 L.z[r] = v[u].z;
                 L.id[r] = __float_as_uint(v[u].w);
-#if LIO_ICP_MFMA
-                const float px = v[u].x - tq.c0, py = v[u].y - tq.c1, pz = v[u].z - tq.c2;
-                const float w = (px * px + py * py) + pz * pz;
-                L.w[r] = w;
-                wmax = fmaxf(wmax, w);
-#endif
             }
             cnt += (uint32_t)__popcll(m);
         }
-#if LIO_ICP_MFMA
-        constexpr int kPad = 16;
-#else
-        constexpr int kPad = 8;
-#endif
-        const int cntp = ((int)cnt + kPad - 1) & ~(kPad - 1);
+        const int cnt8 = ((int)cnt + 7) & ~7;
         tested += cnt;
-        if ((uint32_t)lane < (uint32_t)cntp - cnt) {  // pad: +inf points with id kNone (never win)
+        if ((uint32_t)lane < (uint32_t)cnt8 - cnt) {  // pad to 8: +inf points with id kNone (never win)
             L.x[cnt + lane] = INFINITY;
             L.y[cnt + lane] = INFINITY;
             L.z[cnt + lane] = INFINITY;
-            L.w[cnt + lane] = INFINITY;
             L.id[cnt + lane] = (uint32_t)kNone;
         }
         wave_sync();
-#if LIO_ICP_MFMA
-        {
-            const int k = lane >> 4, col = lane & 15;
-            const float W = wave_max_nonneg(wmax);
-#pragma unroll
-            for (int b = 0; b < 4; ++b) tq.thr[b] = icp_thr(tq.bk[b], tq.qn2[b], W);
-            const float* LA = &L.x[0] + k * kLs + col;  // x, y, z, w arrays kLs apart: lane group k reads component k
-            const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-            for (int j = 0; j < cntp; j += 16) {
-                const float av = LA[j] - tq.ck;
-                f32x4 d[4];
-#pragma unroll
-                for (int b = 0; b < 4; ++b) d[b] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, tq.bq[b], zero, 0, 0, 0);
-                // an entry is flagged when it may hold a key below the slot's: D within the threshold and
-                // not the slot's current best point itself (a pass's prior correspondence would otherwise
-                // flag every query once per pass); NaN entries (+inf padding) are never flagged
-                const uint4 ids = *reinterpret_cast<const uint4*>(__builtin_assume_aligned(&L.id[j + 4 * k], 16));
-                bool f = false;
-#pragma unroll
-                for (int b = 0; b < 4; ++b) {
-                    const uint32_t bid = (uint32_t)__double_as_longlong(tq.bk[b]);
-                    f |= (d[b][0] <= tq.thr[b] && ids.x != bid) | (d[b][1] <= tq.thr[b] && ids.y != bid) |
-                         (d[b][2] <= tq.thr[b] && ids.z != bid) | (d[b][3] <= tq.thr[b] && ids.w != bid);
-                }
-                if (__any(f)) {  // exact test of the flagged entries (rare once the bounds are tight)
-#pragma unroll
-                    for (int b = 0; b < 4; ++b) {
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) {
-                            const uint32_t idr = r == 0 ? ids.x : (r == 1 ? ids.y : (r == 2 ? ids.z : ids.w));
-                            if (d[b][r] <= tq.thr[b] && idr != (uint32_t)__double_as_longlong(tq.bk[b])) {
-                                const int m = j + 4 * k + r;
-                                const float dd = sqdist3(tq.qx[b], tq.qy[b], tq.qz[b], L.x[m], L.y[m], L.z[m]);
-                                tq.bk[b] = key_min_d(tq.bk[b], key_of(dd, idr));
-                            }
-                        }
-                        tq.thr[b] = icp_thr(tq.bk[b], tq.qn2[b], W);
-                    }
-                }
-            }
-            // the four lanes of each query (l & 15 + 16 g) merge their keys: every lane then holds the
-            // exact minimum so far of all four of its slots; the lane's own query is slot l >> 4
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                tq.bk[b] = key_min_d(tq.bk[b], __shfl_xor(tq.bk[b], 16, 64));
-                tq.bk[b] = key_min_d(tq.bk[b], __shfl_xor(tq.bk[b], 32, 64));
-            }
-            const double own = k == 0 ? tq.bk[0] : (k == 1 ? tq.bk[1] : (k == 2 ? tq.bk[2] : tq.bk[3]));
-            best = (uint64_t)__double_as_longlong(own);
-        }
-#else
         // every lane (active or not: uniform control flow) tests 4 staged candidates per step,
         // distances two at a time in packed FP32 ((dx*dx + dy*dy) + dz*dz per element, no FMA)
         const f2v qx = {x, x}, qy = {y, y}, qz = {z, z};
@@ -372,12 +273,11 @@ __device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32
             return key_min_d(m0, m1);
         };
 #pragma unroll 1
-        for (int j = 0; j < cntp; j += 8) {  // two steps per trip: 8 LDS reads in flight
+        for (int j = 0; j < cnt8; j += 8) {  // two steps per trip: 8 LDS reads in flight
             const double ma = step4(j), mb = step4(j + 4);
             bk = key_min_d(bk, key_min_d(ma, mb));
         }
         best = (uint64_t)__double_as_longlong(bk);
-#endif
         wave_sync();  // chunk consumed before it is overwritten
     }
 }
@@ -393,7 +293,7 @@ struct CellBox {
 template <int NW>
 __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const CellBox& S, float B, float qx0, float qx1,
                           float qy0, float qy1, float qz0, float qz1, bool act, float x, float y, float z,
-                          uint64_t& best, unsigned long long& cand, uint32_t& tested, TileQ& tq) {
+                          uint64_t& best, unsigned long long& cand, uint32_t& tested) {
     const int lane = threadIdx.x & 63;
     const float cs = g.cell, m = g.margin;
     const float qb[6] = {qx0, qx1, qy0, qy1, qz0, qz1};
@@ -452,7 +352,7 @@ __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const 
         L.perm[rank] = make_uint4(b0, n0, b1, n1);
         wave_sync();
         const uint4 pr = L.perm[lane];
-        scan_ranges<NW>(g, L, pr.x, pr.y, pr.z, pr.w, act, x, y, z, qb, best, cand, tested, tq);
+        scan_ranges<NW>(g, L, pr.x, pr.y, pr.z, pr.w, act, x, y, z, qb, best, cand, tested);
     }
 }
 
@@ -526,29 +426,6 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
                     min(max(cell_coord(qy1, g.oy, g.inv_cell), 0), g.ny - 1),
                     min(max(cell_coord(qz0, g.oz, g.inv_cell), 0), g.nz - 1),
                     min(max(cell_coord(qz1, g.oz, g.inv_cell), 0), g.nz - 1)};
-    TileQ tq;
-#if LIO_ICP_MFMA
-    {
-        tq.c0 = uni_f(0.5f * (qx0 + qx1));
-        tq.c1 = uni_f(0.5f * (qy0 + qy1));
-        tq.c2 = uni_f(0.5f * (qz0 + qz1));
-        const int k = lane >> 4;
-        tq.ck = k == 0 ? tq.c0 : (k == 1 ? tq.c1 : (k == 2 ? tq.c2 : 0.f));
-        const double bself = __longlong_as_double((long long)best);
-#pragma unroll
-        for (int b = 0; b < 4; ++b) {
-            const int src = 16 * b + (lane & 15);
-            const float sx = __shfl(x, src, 64), sy = __shfl(y, src, 64), sz = __shfl(z, src, 64);
-            const float px = sx - tq.c0, py = sy - tq.c1, pz = sz - tq.c2;
-            tq.qx[b] = sx;
-            tq.qy[b] = sy;
-            tq.qz[b] = sz;
-            tq.qn2[b] = src < (int)tl.y ? (px * px + py * py) + pz * pz : INFINITY;
-            tq.bq[b] = k == 0 ? -2.f * px : (k == 1 ? -2.f * py : (k == 2 ? -2.f * pz : 1.f));
-            tq.bk[b] = __shfl(bself, src, 64);
-        }
-    }
-#endif
     unsigned long long cand = 0;  // candidates streamed (wave 0 counts the tile's)
     uint32_t tested = 0;          // candidates past the staging filter (this wave's chunks)
     int rounds = 0;
@@ -573,7 +450,7 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
         // the scanned box may stick out of N (a grown box): clip it, the part outside N is not needed
         CellBox Sc{max(S.x0, N.x0), min(S.x1, N.x1), max(S.y0, N.y0), min(S.y1, N.y1), max(S.z0, N.z0), min(S.z1, N.z1)};
         if (Sc.y0 > Sc.y1 || Sc.z0 > Sc.z1) Sc.x0 = 1, Sc.x1 = 0;
-        scan_rows<NW>(g, L, N, Sc, B, qx0, qx1, qy0, qy1, qz0, qz1, act, x, y, z, best, cand, tested, tq);
+        scan_rows<NW>(g, L, N, Sc, B, qx0, qx1, qy0, qy1, qz0, qz1, act, x, y, z, best, cand, tested);
         best = tile_min<NW>(best, s_best);
         ++rounds;
         const bool full = N.x0 == 0 && N.y0 == 0 && N.z0 == 0 && N.x1 == g.nx - 1 && N.y1 == g.ny - 1 && N.z1 == g.nz - 1;

@@ -7,9 +7,8 @@ cd "$(dirname "$0")/../fast-lio-sam_gps_amd"
 name=$1; src=$2; shift 2
 d=build_ab/$name; mkdir -p "$d"
 obj=$(basename "${src%.*}").o
-extra=""; [ "$obj" = lio_icp.o ] && extra="-mllvm -amdgpu-mfma-vgpr-form"
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC -ffp-contract=off --offload-arch=gfx950 -Wall -I../include -Icsrc \
-    -D__HIP_PLATFORM_AMD__ $extra "$@" -x hip -c "$src" -o "$d/$obj"
+    -D__HIP_PLATFORM_AMD__ "$@" -x hip -c "$src" -o "$d/$obj"
 objs=$(ls build/*.o | grep -v "/$obj\$")
 /opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 -o "$d/liblio_gpu.so" $objs "$d/$obj" -ldl -lpthread
 echo "built $d/liblio_gpu.so"
