@@ -56,7 +56,7 @@ __device__ __forceinline__ void xform_pcl(const float* T, float x, float y, floa
 // Total order (d2, id), d2 = float ((dx*dx + dy*dy) + dz*dz): the result
 // does not depend on the tiling.
 // ----------------------------------------------------------------------------
-[[maybe_unused]] constexpr int kTileCh = 256;  // candidates staged per LDS round (flat staging)
+constexpr int kTileCh = 256;  // candidates staged per LDS round
 
 // Tiles -> blocks (launch_icp_tiles: 8 x (kIcpSegs / 8) x ceil(n / kIcpSegs) blocks; block b runs on
 // XCD b % 8).  The cell-ordered tiles form kIcpSegs contiguous segments; XCD x owns segments x, x + 8,
@@ -89,28 +89,6 @@ __device__ __forceinline__ void wave_sync() {
 // staged candidates as structure of arrays: 4 consecutive x (y, z, id) are one
 // 16-byte broadcast read, and two candidates' coordinates sit in one register
 // pair for the packed FP32 distance (v_pk_add_f32 / v_pk_mul_f32)
-#ifndef LIO_ICP_SUB
-#define LIO_ICP_SUB 1  // per-row staging lists (0: one staged list tested by all 64 lanes)
-#endif
-#if LIO_ICP_SUB
-// Per-row staging: the tile's queries sit in Morton order on the lanes (icp_tile_kernel), so each
-// row of 16 lanes covers a compact quarter of the tile; a streamed candidate is staged into row k's
-// list when its distance to row k's query box is within row k's largest best, and a lane tests only
-// its row's list.  kSubCh candidates per round; row k's list at lst[k * kSubStride] (x, y, z, id
-// arrays kSubCh apart; the 4-word skew puts the four rows' broadcast reads in different banks).
-constexpr int kSubCh = 128;
-constexpr int kSubStride = 4 * kSubCh + 4;
-struct alignas(16) TileLds {
-    float lst[4 * kSubStride];
-    union {  // the row permutation is read into registers before the slot table is written
-        struct {
-            uint32_t b[2 * kIcpTileQ];
-            uint32_t off[2 * kIcpTileQ + 1];
-        };
-        uint4 perm[kIcpTileQ];  // a batch of rows (b0, n0, b1, n1), re-ordered nearest-first
-    };
-};
-#else
 struct alignas(16) TileLds {
     float x[kTileCh], y[kTileCh], z[kTileCh];
     uint32_t id[kTileCh];
@@ -121,12 +99,6 @@ struct alignas(16) TileLds {
         };
         uint4 perm[kIcpTileQ];  // a batch of rows (b0, n0, b1, n1), re-ordered nearest-first
     };
-};
-#endif
-
-// the query box of each row of 16 lanes (wave-uniform; empty rows: +inf / -inf)
-struct RowBoxes {
-    float x0[4], x1[4], y0[4], y1[4], z0[4], z1[4];
 };
 
 // (d2, id) keys minimised as f64: lio_dev.hpp key_min (one v_min_f64 instead of compare + two selects)
@@ -189,28 +161,6 @@ __device__ __forceinline__ float wave_ext_dpp(float v) {
     return uni_f(op(op(r0, r1), op(r2, r3)));
 }
 
-// per-row extreme (rows of 16 lanes) by the same DPP steps as wave_ext_dpp, row k's value in out[k]
-template <bool MAX>
-__device__ __forceinline__ void row_ext4(float v, float (&out)[4]) {
-    auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : fminf(a, b); };
-    v = op(v, dpp_f<0xb1>(v));
-    v = op(v, dpp_f<0x4e>(v));
-    v = op(v, dpp_f<0x141>(v));
-    v = op(v, dpp_f<0x140>(v));
-#pragma unroll
-    for (int k = 0; k < 4; ++k) out[k] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16 * k));
-}
-// per-row maximum of non-negative floats (as integers)
-__device__ __forceinline__ void row_max_nonneg4(float v, float (&out)[4]) {
-    uint32_t u = __float_as_uint(v);
-    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp((int)u, (int)u, 0xb1, 0xf, 0xf, false));
-    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp((int)u, (int)u, 0x4e, 0xf, 0xf, false));
-    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp((int)u, (int)u, 0x141, 0xf, 0xf, false));
-    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp((int)u, (int)u, 0x140, 0xf, 0xf, false));
-#pragma unroll
-    for (int k = 0; k < 4; ++k) out[k] = __uint_as_float((uint32_t)__builtin_amdgcn_readlane((int)u, 16 * k));
-}
-
 // inclusive prefix sum over the wave: DPP row shifts inside rows of 16, then row_bcast:15 /
 // row_bcast:31 carry the row totals forward (rows 1, 3 then rows 2, 3)
 __device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
@@ -243,8 +193,7 @@ __device__ __forceinline__ float interval_gap(float lo, float hi, float a, float
 template <int NW>  // waves per tile: the tile's candidate stream is split over them
 __device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32_t b0, uint32_t n0, uint32_t b1,
                                             uint32_t n1, bool act, float x, float y, float z, const float (&qb)[6],
-                                            uint64_t& best, unsigned long long& cand, uint32_t& tested,
-                                            const RowBoxes& rb) {
+                                            uint64_t& best, unsigned long long& cand, uint32_t& tested) {
     // the wave's index within its tile (several one-wave tiles per block: always 0)
     const int lane = threadIdx.x & 63, w = NW > 1 ? __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) : 0;
     const uint32_t n = n0 + n1;
@@ -261,97 +210,6 @@ __device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32
     wave_sync();
     int sl = 0;
     uint32_t lo = 0, hi = L.off[1], sb = L.b[0];
-#if LIO_ICP_SUB
-    static_assert(NW == 1, "per-row staging: one wave per tile");
-    (void)qb;
-    const int kk = lane >> 4;
-    const f2v qx = {x, x}, qy = {y, y}, qz = {z, z};
-#pragma unroll 1
-    for (uint32_t base = 0; base < T; base += kSubCh) {
-        constexpr int U = kSubCh / kIcpTileQ;
-        float4 v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {  // slot walk first (clamped to the last point), U loads in flight
-            const uint32_t t = min(base + (uint32_t)(u * kIcpTileQ + lane), T - 1);
-            while (t >= hi) {
-                ++sl;
-                lo = hi;
-                hi = L.off[sl + 1];
-                sb = L.b[sl];
-            }
-            v[u] = g.pts[sb + (t - lo)];
-        }
-        // each row's bound: its active lanes' largest best (+inf while one has none)
-        float Bk[4];
-        row_max_nonneg4(act ? __uint_as_float((uint32_t)(best >> 32)) : 0.f, Bk);
-        uint32_t cnt[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool valid = base + (uint32_t)(u * kIcpTileQ + lane) < T;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {  // row k's survivors compacted in stream order
-                const float gx = fmaxf(fmaxf(rb.x0[k] - v[u].x, v[u].x - rb.x1[k]), 0.f);
-                const float gy = fmaxf(fmaxf(rb.y0[k] - v[u].y, v[u].y - rb.y1[k]), 0.f);
-                const float gz = fmaxf(fmaxf(rb.z0[k] - v[u].z, v[u].z - rb.z1[k]), 0.f);
-                const float gap2 = (gx * gx + gy * gy) + gz * gz;
-                const bool in = valid && !(gap2 * (1.f - 1e-5f) > Bk[k]);
-                const uint64_t m = __ballot(in);
-                if (in) {
-                    const uint32_t r = cnt[k] + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-                    float* Lk = L.lst + k * kSubStride;
-                    Lk[r] = v[u].x;
-                    Lk[kSubCh + r] = v[u].y;
-                    Lk[2 * kSubCh + r] = v[u].z;
-                    Lk[3 * kSubCh + r] = v[u].w;  // id bits
-                }
-                cnt[k] += (uint32_t)__popcll(m);
-            }
-        }
-        uint32_t cmax = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {  // pad each list to 8: +inf points with id kNone (never win)
-            cmax = max(cmax, cnt[k]);
-            const uint32_t pad = ((cnt[k] + 7u) & ~7u) - cnt[k];
-            if ((uint32_t)lane < pad) {
-                float* Lk = L.lst + k * kSubStride;
-                Lk[cnt[k] + lane] = INFINITY;
-                Lk[kSubCh + cnt[k] + lane] = INFINITY;
-                Lk[2 * kSubCh + cnt[k] + lane] = INFINITY;
-                Lk[3 * kSubCh + cnt[k] + lane] = __uint_as_float((uint32_t)kNone);
-            }
-        }
-        tested += cmax;
-        wave_sync();
-        const uint32_t mine = kk == 0 ? cnt[0] : (kk == 1 ? cnt[1] : (kk == 2 ? cnt[2] : cnt[3]));
-        const int mine8 = (int)((mine + 7u) & ~7u), cmax8 = (int)((cmax + 7u) & ~7u);
-        const float* Lx = L.lst + kk * kSubStride;
-        double bk = __longlong_as_double((long long)best);
-        auto step4 = [&](int j) {
-            const float4 X = *reinterpret_cast<const float4*>(__builtin_assume_aligned(&Lx[j], 16));
-            const float4 Y = *reinterpret_cast<const float4*>(__builtin_assume_aligned(&Lx[kSubCh + j], 16));
-            const float4 Z = *reinterpret_cast<const float4*>(__builtin_assume_aligned(&Lx[2 * kSubCh + j], 16));
-            const uint4 I = *reinterpret_cast<const uint4*>(__builtin_assume_aligned(&Lx[3 * kSubCh + j], 16));
-            const f2v dx0 = qx - f2v{X.x, X.y}, dy0 = qy - f2v{Y.x, Y.y}, dz0 = qz - f2v{Z.x, Z.y};
-            const f2v dx1 = qx - f2v{X.z, X.w}, dy1 = qy - f2v{Y.z, Y.w}, dz1 = qz - f2v{Z.z, Z.w};
-            const f2v d0 = (dx0 * dx0 + dy0 * dy0) + dz0 * dz0;
-            const f2v d1 = (dx1 * dx1 + dy1 * dy1) + dz1 * dz1;
-            const double m0 = key_min_d(key_pk<0>(I.x, I.y, d0), key_pk<1>(I.x, I.y, d0));
-            const double m1 = key_min_d(key_pk<0>(I.z, I.w, d1), key_pk<1>(I.z, I.w, d1));
-            return key_min_d(m0, m1);
-        };
-#pragma unroll 1
-        for (int j = 0; j < cmax8; j += 8) {  // the row's own list (rows with shorter lists idle)
-            if (j < mine8) {
-                const double ma = step4(j), mb = step4(j + 4);
-                bk = key_min_d(bk, key_min_d(ma, mb));
-            }
-        }
-        best = (uint64_t)__double_as_longlong(bk);
-        wave_sync();  // lists consumed before they are overwritten
-    }
-    return;
-#endif
-#if !LIO_ICP_SUB
 #pragma unroll 1
     for (uint32_t base = (uint32_t)w * kTileCh; base < T; base += NW * kTileCh) {
         constexpr int U = kTileCh / kIcpTileQ;
@@ -422,7 +280,6 @@ __device__ __forceinline__ void scan_ranges(const GridDev& g, TileLds& L, uint32
         best = (uint64_t)__double_as_longlong(bk);
         wave_sync();  // chunk consumed before it is overwritten
     }
-#endif
 }
 
 struct CellBox {
@@ -436,7 +293,7 @@ struct CellBox {
 template <int NW>
 __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const CellBox& S, float B, float qx0, float qx1,
                           float qy0, float qy1, float qz0, float qz1, bool act, float x, float y, float z,
-                          uint64_t& best, unsigned long long& cand, uint32_t& tested, const RowBoxes& rbx) {
+                          uint64_t& best, unsigned long long& cand, uint32_t& tested) {
     const int lane = threadIdx.x & 63;
     const float cs = g.cell, m = g.margin;
     const float qb[6] = {qx0, qx1, qy0, qy1, qz0, qz1};
@@ -495,7 +352,7 @@ __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const 
         L.perm[rank] = make_uint4(b0, n0, b1, n1);
         wave_sync();
         const uint4 pr = L.perm[lane];
-        scan_ranges<NW>(g, L, pr.x, pr.y, pr.z, pr.w, act, x, y, z, qb, best, cand, tested, rbx);
+        scan_ranges<NW>(g, L, pr.x, pr.y, pr.z, pr.w, act, x, y, z, qb, best, cand, tested);
     }
 }
 
@@ -533,7 +390,7 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
     if (tix < 0) return;  // block-uniform: a slot past its XCD's share
     const uint2 tl = a.tiles[tix];
     const bool act = lane < (int)tl.y;
-    int i = act ? __float_as_int(a.qpts[tl.x + lane].w) : 0;
+    const int i = act ? __float_as_int(a.qpts[tl.x + lane].w) : 0;
     float x = 0.f, y = 0.f, z = 0.f;
     int prior = -1;
     if (act) {
@@ -554,57 +411,15 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
         }
     }
     const GridDev& g = a.grid;
-    // tile bounding box (active lanes)
-    const float qx0 = wave_ext_dpp<false>(act ? x : INFINITY), qx1 = wave_ext_dpp<true>(act ? x : -INFINITY);
-    const float qy0 = wave_ext_dpp<false>(act ? y : INFINITY), qy1 = wave_ext_dpp<true>(act ? y : -INFINITY);
-    const float qz0 = wave_ext_dpp<false>(act ? z : INFINITY), qz1 = wave_ext_dpp<true>(act ? z : -INFINITY);
-    RowBoxes rb;
-#if LIO_ICP_SUB
-    {
-        // queries -> lanes in Morton order of their position in the tile box (4 bits per axis), so
-        // each row of 16 lanes holds a compact quarter of the tile; active lanes stay first (lane < count)
-        auto q4 = [](float v, float lo, float hi) {
-            const float e = hi - lo;
-            const int c = e > 0.f ? (int)((v - lo) * (16.f / e)) : 0;
-            return (uint32_t)min(max(c, 0), 15);
-        };
-        uint32_t code = 4096u;
-        if (act) {
-            const uint32_t ix = q4(x, qx0, qx1), iy = q4(y, qy0, qy1), iz = q4(z, qz0, qz1);
-            code = 0u;
-#pragma unroll
-            for (int bt = 0; bt < 4; ++bt)
-                code |= (((ix >> bt) & 1u) << (3 * bt)) | (((iy >> bt) & 1u) << (3 * bt + 1)) | (((iz >> bt) & 1u) << (3 * bt + 2));
-        }
-        uint32_t key = (code << 6) | (uint32_t)lane;
-#pragma unroll
-        for (int kb = 2; kb <= 64; kb <<= 1) {  // bitonic sort of the 64 keys across the lanes
-#pragma unroll
-            for (int jb = kb >> 1; jb > 0; jb >>= 1) {
-                const uint32_t o = (uint32_t)__shfl_xor((int)key, jb, 64);
-                const bool up = (lane & kb) == 0, low = (lane & jb) == 0;
-                key = (low == up) ? min(key, o) : max(key, o);
-            }
-        }
-        const int src = (int)(key & 63u);
-        x = __shfl(x, src, 64);
-        y = __shfl(y, src, 64);
-        z = __shfl(z, src, 64);
-        i = __shfl(i, src, 64);
-        prior = __shfl(prior, src, 64);
-        row_ext4<false>(act ? x : INFINITY, rb.x0);
-        row_ext4<true>(act ? x : -INFINITY, rb.x1);
-        row_ext4<false>(act ? y : INFINITY, rb.y0);
-        row_ext4<true>(act ? y : -INFINITY, rb.y1);
-        row_ext4<false>(act ? z : INFINITY, rb.z0);
-        row_ext4<true>(act ? z : -INFINITY, rb.z1);
-    }
-#endif
     uint64_t best = knn_key(INFINITY, kNone);
     if (prior >= 0 && prior != kNone) {  // the previous correspondence: an exact candidate
         const float4 p = a.tgt_by_id[prior];
         best = knn_key(sqdist3(x, y, z, p.x, p.y, p.z), prior);
     }
+    // tile bounding box (active lanes)
+    const float qx0 = wave_ext_dpp<false>(act ? x : INFINITY), qx1 = wave_ext_dpp<true>(act ? x : -INFINITY);
+    const float qy0 = wave_ext_dpp<false>(act ? y : INFINITY), qy1 = wave_ext_dpp<true>(act ? y : -INFINITY);
+    const float qz0 = wave_ext_dpp<false>(act ? z : INFINITY), qz1 = wave_ext_dpp<true>(act ? z : -INFINITY);
     const CellBox Q{min(max(cell_coord(qx0, g.ox, g.inv_cell), 0), g.nx - 1),
                     min(max(cell_coord(qx1, g.ox, g.inv_cell), 0), g.nx - 1),
                     min(max(cell_coord(qy0, g.oy, g.inv_cell), 0), g.ny - 1),
@@ -635,7 +450,7 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
         // the scanned box may stick out of N (a grown box): clip it, the part outside N is not needed
         CellBox Sc{max(S.x0, N.x0), min(S.x1, N.x1), max(S.y0, N.y0), min(S.y1, N.y1), max(S.z0, N.z0), min(S.z1, N.z1)};
         if (Sc.y0 > Sc.y1 || Sc.z0 > Sc.z1) Sc.x0 = 1, Sc.x1 = 0;
-        scan_rows<NW>(g, L, N, Sc, B, qx0, qx1, qy0, qy1, qz0, qz1, act, x, y, z, best, cand, tested, rb);
+        scan_rows<NW>(g, L, N, Sc, B, qx0, qx1, qy0, qy1, qz0, qz1, act, x, y, z, best, cand, tested);
         best = tile_min<NW>(best, s_best);
         ++rounds;
         const bool full = N.x0 == 0 && N.y0 == 0 && N.z0 == 0 && N.x1 == g.nx - 1 && N.y1 == g.ny - 1 && N.z1 == g.nz - 1;
