@@ -2,7 +2,7 @@
 # GPU-box session: parity tests, smoke, bench, rocprof.  Each GPU step has its
 # own time limit; any fault / abort / timeout (exit status other than 0 or 1)
 # ends the session immediately — nothing else touches the GPU after it.
-# usage: scripts/gpu_session.sh <tag> [steps...]   steps: test smoke bench prof pmc c3 c5 ppprof quick knn rehearse
+# usage: scripts/gpu_session.sh <tag> [steps...]   steps: test smoke bench prof pmc c3 c5 ppprof quick knn rehearse rccl
 set -u
 TAG=${1:-r01}; shift || true
 STEPS=${*:-"test smoke bench prof"}
@@ -73,6 +73,8 @@ for s in $STEPS; do
     icpseed) run icpseed_ab 600 bash -c 'for r in 1 2; do python scripts/icp_ab.py 1.0 5 && LIO_GPU_LIB=fast-lio-sam_gps_amd/build_ab/noseed/liblio_gpu.so python scripts/icp_ab.py 1.0 5 || exit $?; done' ;;
     icppre) run icppre_ab 900 bash -c 'for r in 1 2; do for v in default pre0 pre4 pre025; do if [ $v = default ]; then python scripts/icp_ab.py 1.0 5; else LIO_GPU_LIB=fast-lio-sam_gps_amd/build_ab/$v/liblio_gpu.so python scripts/icp_ab.py 1.0 5; fi || exit $?; echo "^ $v"; done; done' ;;
     icptrace) run icp_trace 300 rocprofv3 --kernel-trace -d "$OUT/icptrace" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 ;;
+    rccl)  run rccl_one_gpu 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+               --master-port 29531 scripts/rccl_one_gpu.py ;;
     watchdog) LIO_BENCH_REHEARSE=1 run watchdog2 300 python bench.py --gpus 2 --steps 20 --warmup 2 --pipeline 0 --no-cpu --streams '' --icp-reps 1 --watchdog-s 0.5 ;;
     *) echo "unknown step $s" ;;
     esac
