@@ -60,13 +60,17 @@ constexpr int kTileCh = 256;  // candidates staged per LDS round
 
 // Tiles -> blocks (launch_icp_tiles: 8 x (kIcpSegs / 8) x ceil(n / kIcpSegs) blocks; block b runs on
 // XCD b % 8).  The cell-ordered tiles form kIcpSegs contiguous segments; XCD x owns segments x, x + 8,
-// ...: its blocks walk those in cell order (first pass, icp_tile_of) or in the order icp_order_share
-// wrote for its share (later passes: IcpArgs::ord).  -1: a slot past the XCD's share.
+// ...: its blocks walk those in cell order (first pass) or in the order icp_order_share wrote for its
+// share (later passes).  -1: a slot past the XCD's share.
 constexpr int kIcpSegs = 64;
 __device__ __forceinline__ int icp_seg_begin(int s, int n) { return (int)(((int64_t)s * n) / kIcpSegs); }
-__device__ __forceinline__ int icp_tile_of(int b, int n) {  // first pass (cell order)
+__device__ __forceinline__ int icp_tile_of(const uint32_t* order, int b, int n) {
     const int x = b & 7;
     int slot = b >> 3;
+    if (order) {
+        const int lo = (int)order[n + x], hi = (int)order[n + x + 1];
+        return lo + slot < hi ? (int)order[lo + slot] : -1;
+    }
     for (int s = x; s < kIcpSegs; s += 8) {
         const int b0 = icp_seg_begin(s, n), sz = icp_seg_begin(s + 1, n) - b0;
         if (slot < sz) return b0 + slot;
@@ -382,39 +386,21 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
     // order of the previous pass's costs (icp_tile_of)
     static_assert(TPB == 1, "icp_tile_kernel: one tile per block (icp_tile_of)");
     (void)wv;
-    int tix;
-    uint2 tl;
-    if (a.ord) {  // later passes: the entry carries the tile
-        const uint4 e = a.ord[(blockIdx.x & 7) * (uint32_t)a.ord_cap + (blockIdx.x >> 3)];
-        if (e.y == 0) return;  // block-uniform: a slot past its XCD's share
-        tl = make_uint2(e.x, e.y);
-        tix = (int)e.z;
-    } else {
-        tix = icp_tile_of((int)blockIdx.x, ntiles);
-        if (tix < 0) return;  // block-uniform: a slot past its XCD's share
-        tl = a.tiles[tix];
-    }
+    const int tix = icp_tile_of(a.order, (int)blockIdx.x, ntiles);
+    if (tix < 0) return;  // block-uniform: a slot past its XCD's share
+    const uint2 tl = a.tiles[tix];
     const bool act = lane < (int)tl.y;
-    const uint32_t p = tl.x + (uint32_t)lane;  // the query's position in tile order
-    int i = 0;
+    const int i = act ? __float_as_int(a.qpts[tl.x + lane].w) : 0;
     float x = 0.f, y = 0.f, z = 0.f;
     int prior = -1;
-    if (act) {  // one round trip: the binned source point, the current cloud and the prior id in tile order
-        const float4 q = a.qpts[p];
-        i = __float_as_int(q.w);
-        if (a.prior) prior = a.nnid_t[p];
+    if (act) {
+        if (a.prior) prior = a.nn_id[i];
         if (a.fitness) {  // getFitnessScore: original source * final; kept in cur for `aligned_`
-            xform_pcl(a.T, q.x, q.y, q.z, x, y, z);
+            xform_pcl(a.T, a.src[3 * i], a.src[3 * i + 1], a.src[3 * i + 2], x, y, z);
         } else {
-            if (a.cur_from_q) {
-                x = q.x;
-                y = q.y;
-                z = q.z;
-            } else {
-                x = a.cur_t[3 * p];
-                y = a.cur_t[3 * p + 1];
-                z = a.cur_t[3 * p + 2];
-            }
+            x = a.cur[3 * i];
+            y = a.cur[3 * i + 1];
+            z = a.cur[3 * i + 2];
             if (a.apply_T) {
                 float ox, oy, oz;
                 xform_pcl(a.T, x, y, z, ox, oy, oz);
@@ -493,16 +479,10 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
     }
     if constexpr (NW > 1) __syncthreads();  // every wave has read cur[i] before it is overwritten
     if (act && (NW == 1 || wv == 0)) {
-        if (a.fitness || a.apply_T) {  // source order: the statistics, PCL's sums and `aligned_` read it
+        if (a.fitness || a.apply_T) {
             a.cur[3 * i] = x;
             a.cur[3 * i + 1] = y;
             a.cur[3 * i + 2] = z;
-        }
-        if (!a.fitness) {  // tile order: the next pass's head
-            a.cur_t[3 * p] = x;
-            a.cur_t[3 * p + 1] = y;
-            a.cur_t[3 * p + 2] = z;
-            a.nnid_t[p] = (int)(uint32_t)best;
         }
         a.nn_d2[i] = __uint_as_float((uint32_t)(best >> 32));
         a.nn_id[i] = (int)(uint32_t)best;
@@ -517,16 +497,15 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
 // records (what ranks all-gather) are bit-identical for any number of ranks.
 constexpr int kIcpStatsThreads = 1024;
 template <int NT>
-__device__ void icp_order_share(const uint32_t* __restrict__ cost, const uint2* __restrict__ tiles, int n,
-                                uint4* __restrict__ ord, int cap, int x);
+__device__ void icp_order_share(const uint32_t* __restrict__ cost, int n, uint32_t* __restrict__ order, int x);
 
 // Blocks [0, nsup) write the records; when `order` is given, blocks nsup .. nsup + 7 build the next
 // pass's tile order for the eight XCD shares in the same launch (they only read this pass's tile costs),
 // so the order runs beside the records instead of between them and the next pass.
 __global__ void __launch_bounds__(kIcpStatsThreads) icp_stats_kernel(IcpArgs a, double* __restrict__ super, int nsup,
-                                                                     uint4* __restrict__ ord, int ntiles) {
+                                                                     uint32_t* __restrict__ order, int ntiles) {
     if ((int)blockIdx.x >= nsup) {  // block-uniform
-        icp_order_share<kIcpStatsThreads>(a.tile_cost, a.tiles, ntiles, ord, icp_ord_cap(ntiles), (int)blockIdx.x - nsup);
+        icp_order_share<kIcpStatsThreads>(a.tile_cost, ntiles, order, (int)blockIdx.x - nsup);
         return;
     }
     constexpr int NW = kIcpStatsThreads / 64, PER = kIcpSuper / kIcpStatsThreads;
@@ -610,8 +589,7 @@ __device__ __forceinline__ int icp_share_tile(int x, int f, int n) {
     return -1;
 }
 template <int NT>
-__device__ void icp_order_share(const uint32_t* __restrict__ cost, const uint2* __restrict__ tiles, int n,
-                                uint4* __restrict__ ord, int cap, int x) {
+__device__ void icp_order_share(const uint32_t* __restrict__ cost, int n, uint32_t* __restrict__ order, int x) {
     __shared__ uint32_t hist[33], base[33];
     if (threadIdx.x < 33) hist[threadIdx.x] = 0;
     __syncthreads();
@@ -622,23 +600,22 @@ __device__ void icp_order_share(const uint32_t* __restrict__ cost, const uint2* 
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        uint32_t acc = (uint32_t)x * (uint32_t)cap;  // share x's fixed slot range
+        uint32_t acc = 0;  // this share's first entry: the sizes of shares 0 .. x-1
+        for (int s = 0; s < kIcpSegs; ++s)
+            if ((s & 7) < x) acc += (uint32_t)(icp_seg_begin(s + 1, n) - icp_seg_begin(s, n));
+        order[n + x] = acc;
+        if (x == 0) order[n + 8] = (uint32_t)n;
         for (int b = 32; b >= 0; --b) {  // longest first
             base[b] = acc;
             acc += hist[b];
         }
-        hist[0] = acc - (uint32_t)x * (uint32_t)cap;  // the share's size (hist is consumed)
     }
     __syncthreads();
-    const int size = (int)hist[0];  // this share's tile count
     for (int f = (int)threadIdx.x;; f += NT) {
         const int t = icp_share_tile(x, f, n);
         if (t < 0) break;
-        const uint2 tl = tiles[t];
-        ord[atomicAdd(&base[cost_bucket(cost[t])], 1u)] = make_uint4(tl.x, tl.y, (uint32_t)t, 0u);
+        order[atomicAdd(&base[cost_bucket(cost[t])], 1u)] = (uint32_t)t;
     }
-    for (int f = size + (int)threadIdx.x; f < cap; f += NT)  // past the share's end: count 0
-        ord[(size_t)x * cap + f] = make_uint4(0u, 0u, 0u, 0u);
 }
 
 // per cell: number of tiles (ceil(count / 64)); slot ncells = 0 for the scan's total
@@ -839,12 +816,11 @@ void launch_icp_combine(const double* recv, int64_t nsup, int world, int64_t slo
     icp_combine_kernel<<<1, 64, 0, st>>>(recv, nsup, world, slot, out17);
 }
 
-void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st, uint4* ord, int ntiles) {
+void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st, uint32_t* order, int ntiles) {
     if (a.n == 0) return;
     const int nsup = (a.n + kIcpSuper - 1) / kIcpSuper;
-    const bool with_ord = ord && ntiles > 0;
-    icp_stats_kernel<<<nsup + (with_ord ? 8 : 0), kIcpStatsThreads, 0, st>>>(a, super, nsup, with_ord ? ord : nullptr,
-                                                                              ntiles);
+    const bool ord = order && ntiles > 0;
+    icp_stats_kernel<<<nsup + (ord ? 8 : 0), kIcpStatsThreads, 0, st>>>(a, super, nsup, ord ? order : nullptr, ntiles);
 }
 
 }  // namespace lio

@@ -306,9 +306,7 @@ struct lio_icp {
     float tile_cell = 2.0f;
     bool have_prior = false;  // nn ids of this alignment's previous pass are in d_fid
     uint32_t* d_tcost = nullptr;  // per tile: candidates of the last pass
-    uint4* d_ord = nullptr;       // per-XCD longest-first tile order entries (valid when have_order)
-    float* d_cur_t = nullptr;     // the incrementally transformed shard in tile order
-    int* d_nnid_t = nullptr;      // the last pass's correspondence ids in tile order
+    uint32_t* d_order = nullptr;  // longest-first tile order (valid when have_order)
     bool have_order = false;
     unsigned long long* d_dbg = nullptr;  // search counters (diagnostics build: LIO_DIAG + LIO_ICP_DEBUG)
     double* h_super = nullptr;      // pinned, host-mapped: the pass's 4096-point records
@@ -372,7 +370,7 @@ int lio_icp_destroy(lio_icp* h) {
     lio::grid_free(h->tgt);
     lio::grid_free(h->qgrid);
     void* ptrs[] = {h->d_tgt,   h->d_src,     h->d_cur,  h->d_fd2,   h->d_fid,   h->d_tiles, h->d_tscratch,
-                    h->d_ttmp,  h->d_dbg,     h->d_tcost, h->d_ord, h->d_cur_t, h->d_nnid_t, h->d_pairs, h->d_pcl16};
+                    h->d_ttmp,  h->d_dbg,     h->d_tcost, h->d_order, h->d_pairs, h->d_pcl16};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (h->h_super) (void)hipHostFree(h->h_super);
@@ -498,8 +496,7 @@ static int icp_prepare(lio_icp* h) {
     const int64_t n = std::max<int64_t>(h->sh_n, 1);
     if (n > h->cap) {
         void** ptrs[] = {(void**)&h->d_src,   (void**)&h->d_cur,   (void**)&h->d_fd2,  (void**)&h->d_fid,
-                         (void**)&h->d_tiles, (void**)&h->d_tcost, (void**)&h->d_ord,
-                         (void**)&h->d_cur_t, (void**)&h->d_nnid_t};
+                         (void**)&h->d_tiles, (void**)&h->d_tcost, (void**)&h->d_order};
         h->cap = 0;  // a failed allocation below leaves no buffer that looks usable (and nothing freed twice)
         for (void** q : ptrs) {
             if (*q) (void)hipFree(*q);
@@ -511,9 +508,7 @@ static int icp_prepare(lio_icp* h) {
         IHIP(hipMalloc(&h->d_fid, n * sizeof(int)));
         IHIP(hipMalloc(&h->d_tiles, (n + n / lio::kIcpTileQ + 1) * sizeof(uint2)));
         IHIP(hipMalloc(&h->d_tcost, (n + n / lio::kIcpTileQ + 1) * sizeof(uint32_t)));
-        IHIP(hipMalloc(&h->d_ord, (size_t)8 * lio::icp_ord_cap((int)(n + n / lio::kIcpTileQ + 1)) * sizeof(uint4)));
-        IHIP(hipMalloc(&h->d_cur_t, n * 3 * sizeof(float)));
-        IHIP(hipMalloc(&h->d_nnid_t, n * sizeof(int)));
+        IHIP(hipMalloc(&h->d_order, (n + n / lio::kIcpTileQ + 64) * sizeof(uint32_t)));  // + the 9 share offsets
         h->cap = n;
     }
     const int64_t nsup_all = (h->ns + lio::kIcpSuper - 1) / lio::kIcpSuper + 1;
@@ -571,11 +566,7 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     a.qpts = h->qgrid.pts;
     a.tiles = h->d_tiles;
     a.tile_cost = h->d_tcost;
-    a.ord = h->have_order ? h->d_ord : nullptr;
-    a.ord_cap = lio::icp_ord_cap(h->ntiles);
-    a.cur_t = h->d_cur_t;
-    a.nnid_t = h->d_nnid_t;
-    a.cur_from_q = h->have_prior ? 0 : 1;  // first pass of the alignment: the binned source itself
+    a.order = h->have_order ? h->d_order : nullptr;
 #ifdef LIO_DIAG
     static const bool dbg_on = std::getenv("LIO_ICP_DEBUG") != nullptr;  // diagnostics build: search statistics
     if (dbg_on) {
@@ -595,7 +586,7 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
         if (h->sh_n > 0) lio::launch_icp_tiles(a, h->ntiles, h->st);
         if (h->timing) IHIP(hipEventRecord(h->ev.m, h->st));
         if (dev_x) {  // records -> device send buffer -> in-stream all-gather -> record-order sum
-            if (h->sh_n > 0) lio::launch_icp_stats(a, h->d_xsend, h->st, fitness ? nullptr : h->d_ord, h->ntiles);
+            if (h->sh_n > 0) lio::launch_icp_stats(a, h->d_xsend, h->st, fitness ? nullptr : h->d_order, h->ntiles);
             IHIP(hipGetLastError());
             if (h->fn_dev(h->d_xsend, h->x_len, h->d_xrecv, (void*)h->st, h->user_dev) != 0)
                 return ifail(LIO_ERR_STATE, "device all-gather callback failed");
@@ -603,7 +594,7 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
             lio::launch_icp_combine(h->d_xrecv, nsup, h->world, h->x_len / lio::kIcpStride, h->h_out17_dev, h->st);
         } else {
             // records straight to host memory; the next pass's tile order in the same launch
-            lio::launch_icp_stats(a, h->h_super_dev, h->st, fitness ? nullptr : h->d_ord, h->ntiles);
+            lio::launch_icp_stats(a, h->h_super_dev, h->st, fitness ? nullptr : h->d_order, h->ntiles);
         }
         if (h->timing) IHIP(hipEventRecord(h->ev.b, h->st));
         if (pcl16) {  // PCL-order fidelity mode: the serial float sums of this pass's correspondences

@@ -143,16 +143,7 @@ struct IcpArgs {
     int* nn_id;          //            1-NN target id
     const float4* qpts;  // source binned by tile cell: (x, y, z, local index bits), cell order
     const uint2* tiles;  // (first entry in qpts, query count <= kIcpTileQ) per tile
-    // optional tile visit order of the later passes (per-XCD longest-first, from the previous pass's
-    // costs): XCD x's share at ord[x * ord_cap ...], entries (first, count, tile index, 0), count 0 past
-    // the share's end — one load gives a wave its tile
-    const uint4* ord;
-    int ord_cap;
-    // the query side in tile (qpts) order, so a tile's head loads are one coalesced round trip: the
-    // incrementally transformed cloud and the previous pass's correspondence ids
-    float* cur_t;        // n*3 (written every correspondence pass; read when !cur_from_q)
-    int* nnid_t;         // n
-    int cur_from_q;      // first pass of an alignment: the cloud is the binned source itself
+    const uint32_t* order;  // optional tile visit order (heaviest first, from the previous pass's costs)
     uint32_t* tile_cost;    // per tile: candidates scanned in this pass
     unsigned long long* dbg;  // optional counters (diagnostics): candidates, rings, tiles, lanes
 };
@@ -169,9 +160,7 @@ int icp_build_tiles(const GridBuf& q, uint2* tiles, uint32_t* scratch, void*& tm
 void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st);
 // tile order for the next pass: descending log2(cost) buckets (one block)
 // one record per 4096 points; with `order`, the next pass's tile order from a.tile_cost in the same launch
-void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st, uint4* ord = nullptr, int ntiles = 0);
-// capacity of one XCD share of the tile order (icp_order_share): 8 segments of <= ceil(ntiles / 64) tiles
-__host__ __device__ inline int icp_ord_cap(int ntiles) { return 8 * ((ntiles + 63) / 64); }
+void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st, uint32_t* order = nullptr, int ntiles = 0);
 // the all-gathered records (world slots of `slot` records) summed in global record order, one thread
 // per statistic (the order of lio_icp_combine: bit-identical) -> out17 (host-mapped)
 void launch_icp_combine(const double* recv, int64_t nsup, int world, int64_t slot, double* out17, hipStream_t st);
