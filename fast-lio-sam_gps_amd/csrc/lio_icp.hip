@@ -388,6 +388,9 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
     (void)wv;
     const int tix = icp_tile_of(a.order, (int)blockIdx.x, ntiles);
     if (tix < 0) return;  // block-uniform: a slot past its XCD's share
+#ifdef LIO_DIAG
+    const uint64_t t_start = wall_clock64();  // per-tile timeline (diagnostics build)
+#endif
     const uint2 tl = a.tiles[tix];
     const bool act = lane < (int)tl.y;
     const int i = act ? __float_as_int(a.qpts[tl.x + lane].w) : 0;
@@ -471,11 +474,17 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
     const bool lead = NW > 1 ? threadIdx.x == 0 : lane == 0;
     if (a.tile_cost && lead) a.tile_cost[tix] = tile_tested;
     if (a.dbg && lead) {
+#ifdef LIO_DIAG
+        a.dbg[8 + 2 * (size_t)tix] = t_start;
+        a.dbg[8 + 2 * (size_t)tix + 1] = wall_clock64();
+#endif
+#ifndef LIO_DIAG_TIMELINE  // the timeline build leaves out the same-address counters (they serialise)
         atomicAdd(a.dbg, cand);
         atomicAdd(a.dbg + 1, (unsigned long long)rounds);
         atomicAdd(a.dbg + 2, 1ull);
         atomicAdd(a.dbg + 3, (unsigned long long)tl.y);
         atomicAdd(a.dbg + 4, (unsigned long long)tile_tested);
+#endif
     }
     if constexpr (NW > 1) __syncthreads();  // every wave has read cur[i] before it is overwritten
     if (act && (NW == 1 || wv == 0)) {

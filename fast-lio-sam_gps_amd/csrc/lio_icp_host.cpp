@@ -309,6 +309,7 @@ struct lio_icp {
     uint32_t* d_order = nullptr;  // longest-first tile order (valid when have_order)
     bool have_order = false;
     unsigned long long* d_dbg = nullptr;  // search counters (diagnostics build: LIO_DIAG + LIO_ICP_DEBUG)
+    size_t dbg_bytes = 0;
     double* h_super = nullptr;      // pinned, host-mapped: the pass's 4096-point records
     double* h_super_dev = nullptr;  // device view of h_super (the statistics kernel writes it, zero-copy)
     int64_t super_cap = 0;
@@ -570,8 +571,17 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
 #ifdef LIO_DIAG
     static const bool dbg_on = std::getenv("LIO_ICP_DEBUG") != nullptr;  // diagnostics build: search statistics
     if (dbg_on) {
-        if (!h->d_dbg) IHIP(hipMalloc(&h->d_dbg, 64));
-        IHIP(hipMemsetAsync(h->d_dbg, 0, 64, h->st));
+        // 8 counters + (start, end) wall clock per tile
+        const size_t bytes = (8 + 2 * (size_t)std::max(h->ntiles, 1)) * sizeof(unsigned long long);
+        if (h->d_dbg && h->dbg_bytes < bytes) {
+            IHIP(hipFree(h->d_dbg));
+            h->d_dbg = nullptr;
+        }
+        if (!h->d_dbg) {
+            IHIP(hipMalloc(&h->d_dbg, bytes));
+            h->dbg_bytes = bytes;
+        }
+        IHIP(hipMemsetAsync(h->d_dbg, 0, bytes, h->st));
         a.dbg = h->d_dbg;
     }
 #endif
@@ -616,6 +626,35 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
         std::fprintf(stderr,
                      "icp dbg: tiles|waves %llu lanes %llu cand/tile %.1f tested/tile %.1f rounds/tile %.2f cand/lane %.1f\n",
                      c[2], c[3], (double)c[0] / c[2], (double)c[4] / c[2], (double)c[1] / c[2], (double)c[0] / c[3]);
+        // per-tile timeline (wall clock, 100 MHz): span, duration percentiles, the tail
+        std::vector<unsigned long long> tt(2 * (size_t)h->ntiles);
+        std::vector<uint32_t> cost(h->ntiles);
+        IHIP(hipMemcpy(tt.data(), h->d_dbg + 8, tt.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+        IHIP(hipMemcpy(cost.data(), h->d_tcost, cost.size() * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        unsigned long long t0 = ~0ull, t1 = 0;
+        std::vector<double> dur(h->ntiles);
+        int imax = 0;
+        for (int t = 0; t < h->ntiles; ++t) {
+            t0 = std::min(t0, tt[2 * t]);
+            t1 = std::max(t1, tt[2 * t + 1]);
+            dur[t] = (double)(tt[2 * t + 1] - tt[2 * t]) * 0.01;  // us
+            if (dur[t] > dur[imax]) imax = t;
+        }
+        unsigned long long last_start = 0;
+        int late = 0;
+        for (int t = 0; t < h->ntiles; ++t) {
+            last_start = std::max(last_start, tt[2 * t]);
+            if (tt[2 * t] > t0 + (t1 - t0) / 2) ++late;
+        }
+        std::vector<double> sd = dur;
+        std::sort(sd.begin(), sd.end());
+        auto pct = [&](double q) { return sd[std::min(sd.size() - 1, (size_t)(q * (double)sd.size()))]; };
+        std::fprintf(stderr,
+                     "icp tiles: span %.1f us | tile us p50 %.2f p90 %.2f p99 %.2f max %.2f (cost %u, median cost %u) | "
+                     "last tile starts at %.1f us | tiles starting in the second half %d of %d\n",
+                     (double)(t1 - t0) * 0.01, pct(0.5), pct(0.9), pct(0.99), sd.back(), cost[imax],
+                     [&] { std::vector<uint32_t> c2 = cost; std::nth_element(c2.begin(), c2.begin() + c2.size() / 2, c2.end()); return c2[c2.size() / 2]; }(),
+                     (double)(last_start - t0) * 0.01, late, h->ntiles);
     }
 #endif
     if (h->timing && h->sh_n > 0) {
