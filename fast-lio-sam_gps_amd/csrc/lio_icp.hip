@@ -64,14 +64,12 @@ constexpr int kTileCh = 256;  // candidates staged per LDS round
 // share (later passes).  -1: a slot past the XCD's share.
 constexpr int kIcpSegs = 64;
 __device__ __forceinline__ int icp_seg_begin(int s, int n) { return (int)(((int64_t)s * n) / kIcpSegs); }
-// Entries: tile index | part << 26 | (parts - 1) << 28 — a split tile (the heaviest of the previous pass)
-// appears once per part, each part scanning its own class of target rows (split_rows).
-__device__ __forceinline__ int icp_tile_of(const uint32_t* order, int cap, int b, int n) {
+__device__ __forceinline__ int icp_tile_of(const uint32_t* order, int b, int n) {
     const int x = b & 7;
     int slot = b >> 3;
     if (order) {
-        const int size = (int)order[8 * cap + x];
-        return slot < size ? (int)order[x * cap + slot] : -1;
+        const int lo = (int)order[n + x], hi = (int)order[n + x + 1];
+        return lo + slot < hi ? (int)order[lo + slot] : -1;
     }
     for (int s = x; s < kIcpSegs; s += 8) {
         const int b0 = icp_seg_begin(s, n), sz = icp_seg_begin(s + 1, n) - b0;
@@ -295,7 +293,7 @@ struct CellBox {
 template <int NW>
 __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const CellBox& S, float B, float qx0, float qx1,
                           float qy0, float qy1, float qz0, float qz1, bool act, float x, float y, float z,
-                          uint64_t& best, unsigned long long& cand, uint32_t& tested, int part, int parts) {
+                          uint64_t& best, unsigned long long& cand, uint32_t& tested) {
     const int lane = threadIdx.x & 63;
     const float cs = g.cell, m = g.margin;
     const float qb[6] = {qx0, qx1, qy0, qy1, qz0, qz1};
@@ -310,9 +308,7 @@ __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const 
         if (r < nrows) {
             const int rz = N.z0 + r / ny, ry = N.y0 + r % ny;
             int x0 = N.x0, x1 = N.x1;
-            // a split tile's part scans one class of rows, fixed by the row's own (y, z), so the parts'
-            // boxes may differ (each covers its lanes' spheres) and every row still belongs to one part
-            bool keep = parts == 1 || (int)((uint32_t)(ry + 3 * rz) % (uint32_t)parts) == part;
+            bool keep = true;
             const float yl = g.oy + (float)ry * cs - m, zl = g.oz + (float)rz * cs - m;
             g2 = interval_gap(yl, yl + cs + 2.f * m, qy0, qy1) + interval_gap(zl, zl + cs + 2.f * m, qz0, qz1);
             if (B < INFINITY) {
@@ -390,9 +386,8 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
     // order of the previous pass's costs (icp_tile_of)
     static_assert(TPB == 1, "icp_tile_kernel: one tile per block (icp_tile_of)");
     (void)wv;
-    const int ent = icp_tile_of(a.order, a.ord_cap, (int)blockIdx.x, ntiles);
-    if (ent < 0) return;  // block-uniform: a slot past its XCD's share
-    const int tix = ent & ((1 << 26) - 1), part = (ent >> 26) & 3, parts = ((ent >> 28) & 3) + 1;
+    const int tix = icp_tile_of(a.order, (int)blockIdx.x, ntiles);
+    if (tix < 0) return;  // block-uniform: a slot past its XCD's share
 #ifdef LIO_DIAG
     const uint64_t t_start = wall_clock64();  // per-tile timeline (diagnostics build)
 #endif
@@ -406,9 +401,9 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
         if (a.fitness) {  // getFitnessScore: original source * final; kept in cur for `aligned_`
             xform_pcl(a.T, a.src[3 * i], a.src[3 * i + 1], a.src[3 * i + 2], x, y, z);
         } else {
-            x = a.cur_in[3 * i];
-            y = a.cur_in[3 * i + 1];
-            z = a.cur_in[3 * i + 2];
+            x = a.cur[3 * i];
+            y = a.cur[3 * i + 1];
+            z = a.cur[3 * i + 2];
             if (a.apply_T) {
                 float ox, oy, oz;
                 xform_pcl(a.T, x, y, z, ox, oy, oz);
@@ -458,7 +453,7 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
         // the scanned box may stick out of N (a grown box): clip it, the part outside N is not needed
         CellBox Sc{max(S.x0, N.x0), min(S.x1, N.x1), max(S.y0, N.y0), min(S.y1, N.y1), max(S.z0, N.z0), min(S.z1, N.z1)};
         if (Sc.y0 > Sc.y1 || Sc.z0 > Sc.z1) Sc.x0 = 1, Sc.x1 = 0;
-        scan_rows<NW>(g, L, N, Sc, B, qx0, qx1, qy0, qy1, qz0, qz1, act, x, y, z, best, cand, tested, part, parts);
+        scan_rows<NW>(g, L, N, Sc, B, qx0, qx1, qy0, qy1, qz0, qz1, act, x, y, z, best, cand, tested);
         best = tile_min<NW>(best, s_best);
         ++rounds;
         const bool full = N.x0 == 0 && N.y0 == 0 && N.z0 == 0 && N.x1 == g.nx - 1 && N.y1 == g.ny - 1 && N.z1 == g.nz - 1;
@@ -477,10 +472,7 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
         for (int v = 0; v < NW; ++v) tile_tested += s_tested[v];
     }
     const bool lead = NW > 1 ? threadIdx.x == 0 : lane == 0;
-    if (a.tile_cost && lead) {
-        if (parts == 1) a.tile_cost[tix] = tile_tested;
-        else atomicAdd(&a.tile_cost[tix], tile_tested);
-    }
+    if (a.tile_cost && lead) a.tile_cost[tix] = tile_tested;
     if (a.dbg && lead) {
 #ifdef LIO_DIAG
         a.dbg[8 + 2 * (size_t)tix] = t_start;
@@ -496,14 +488,13 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
     }
     if constexpr (NW > 1) __syncthreads();  // every wave has read cur[i] before it is overwritten
     if (act && (NW == 1 || wv == 0)) {
-        if (part == 0) {  // every pass writes the cloud it used (cur_in and cur are swapped after it)
+        if (a.fitness || a.apply_T) {
             a.cur[3 * i] = x;
             a.cur[3 * i + 1] = y;
             a.cur[3 * i + 2] = z;
         }
-        // the exact (d2, id) minimum over the parts (one part: the only writer)
-        if (parts == 1) a.key[i] = best;
-        else atomicMin(&a.key[i], (unsigned long long)best);
+        a.nn_d2[i] = __uint_as_float((uint32_t)(best >> 32));
+        a.nn_id[i] = (int)(uint32_t)best;
     }
 }
 
@@ -515,7 +506,7 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
 // records (what ranks all-gather) are bit-identical for any number of ranks.
 constexpr int kIcpStatsThreads = 1024;
 template <int NT>
-__device__ void icp_order_share(uint32_t* __restrict__ cost, int n, uint32_t* __restrict__ order, int cap, int x);
+__device__ void icp_order_share(const uint32_t* __restrict__ cost, int n, uint32_t* __restrict__ order, int x);
 
 // Blocks [0, nsup) write the records; when `order` is given, blocks nsup .. nsup + 7 build the next
 // pass's tile order for the eight XCD shares in the same launch (they only read this pass's tile costs),
@@ -523,7 +514,7 @@ __device__ void icp_order_share(uint32_t* __restrict__ cost, int n, uint32_t* __
 __global__ void __launch_bounds__(kIcpStatsThreads) icp_stats_kernel(IcpArgs a, double* __restrict__ super, int nsup,
                                                                      uint32_t* __restrict__ order, int ntiles) {
     if ((int)blockIdx.x >= nsup) {  // block-uniform
-        icp_order_share<kIcpStatsThreads>(a.tile_cost, ntiles, order, a.ord_cap, (int)blockIdx.x - nsup);
+        icp_order_share<kIcpStatsThreads>(a.tile_cost, ntiles, order, (int)blockIdx.x - nsup);
         return;
     }
     constexpr int NW = kIcpStatsThreads / 64, PER = kIcpSuper / kIcpStatsThreads;
@@ -537,16 +528,8 @@ __global__ void __launch_bounds__(kIcpStatsThreads) icp_stats_kernel(IcpArgs a, 
 #pragma unroll
     for (int k = 0; k < PER; ++k) {  // all correspondence loads first: one round trip
         const int i = base + k * kIcpStatsThreads;
-        ids[k] = -1;
-        d2s[k] = 0.f;
-        if (i < a.n) {  // the pass's key -> nn_id / nn_d2 (the next pass's prior), key reset for the next pass
-            const unsigned long long kk = a.key[i];
-            ids[k] = (int)(uint32_t)kk;
-            d2s[k] = __uint_as_float((uint32_t)(kk >> 32));
-            a.nn_id[i] = ids[k];
-            a.nn_d2[i] = d2s[k];
-            a.key[i] = ~0ull;
-        }
+        ids[k] = i < a.n ? a.nn_id[i] : -1;
+        d2s[k] = i < a.n ? a.nn_d2[i] : 0.f;
     }
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
@@ -591,8 +574,7 @@ __global__ void __launch_bounds__(kIcpStatsThreads) icp_stats_kernel(IcpArgs a, 
 void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st) {
     if (a.n == 0 || ntiles == 0) return;
     const int seg = (ntiles + kIcpSegs - 1) / kIcpSegs;
-    const int blocks = a.order ? 8 * a.ord_cap : 8 * (kIcpSegs / 8) * seg;  // later passes: split tiles' extra parts
-    icp_tile_kernel<1, 1><<<blocks, kIcpTileQ, 0, st>>>(a, ntiles);
+    icp_tile_kernel<1, 1><<<8 * (kIcpSegs / 8) * seg, kIcpTileQ, 0, st>>>(a, ntiles);
 }
 
 // Tile order for the next pass from this pass's candidate counts.  The cell-ordered tiles are cut
@@ -616,8 +598,8 @@ __device__ __forceinline__ int icp_share_tile(int x, int f, int n) {
     return -1;
 }
 template <int NT>
-__device__ void icp_order_share(uint32_t* __restrict__ cost, int n, uint32_t* __restrict__ order, int cap, int x) {
-    __shared__ uint32_t hist[33], base[33], s_mb, s_split;
+__device__ void icp_order_share(const uint32_t* __restrict__ cost, int n, uint32_t* __restrict__ order, int x) {
+    __shared__ uint32_t hist[33], base[33];
     if (threadIdx.x < 33) hist[threadIdx.x] = 0;
     __syncthreads();
     for (int f = (int)threadIdx.x;; f += NT) {
@@ -627,44 +609,21 @@ __device__ void icp_order_share(uint32_t* __restrict__ cost, int n, uint32_t* __
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        // the share's median bucket; tiles >= 4x the median (bucket >= mb + 2) are split into 4 parts
-        // when the share's slots allow it (the parts run as separate waves: the pass is as long as its
-        // slowest tile, profiles/r03_icp_tile_timeline.txt)
-        uint32_t tot = 0, acc = 0, mb = 0, heavy = 0;
-        for (int b = 0; b <= 32; ++b) tot += hist[b];
-        for (int b = 0; b <= 32; ++b) {
-            acc += hist[b];
-            if (2 * acc >= tot) {
-                mb = (uint32_t)b;
-                break;
-            }
-        }
-        for (int b = (int)mb + 2; b <= 32; ++b) heavy += hist[b];
-        const uint32_t split = tot + 3 * heavy <= (uint32_t)cap && heavy > 0 ? 1u : 0u;
-        s_mb = mb;
-        s_split = split;
-        uint32_t pos = (uint32_t)x * (uint32_t)cap;  // share x's fixed slot range
+        uint32_t acc = 0;  // this share's first entry: the sizes of shares 0 .. x-1
+        for (int s = 0; s < kIcpSegs; ++s)
+            if ((s & 7) < x) acc += (uint32_t)(icp_seg_begin(s + 1, n) - icp_seg_begin(s, n));
+        order[n + x] = acc;
+        if (x == 0) order[n + 8] = (uint32_t)n;
         for (int b = 32; b >= 0; --b) {  // longest first
-            base[b] = pos;
-            pos += hist[b] * ((split && b >= (int)mb + 2) ? 4u : 1u);
+            base[b] = acc;
+            acc += hist[b];
         }
-        order[8 * cap + x] = pos - (uint32_t)x * (uint32_t)cap;  // the share's entry count
     }
     __syncthreads();
-    const int mb = (int)s_mb;
-    const bool split = s_split != 0;
     for (int f = (int)threadIdx.x;; f += NT) {
         const int t = icp_share_tile(x, f, n);
         if (t < 0) break;
-        const int b = (int)cost_bucket(cost[t]);
-        cost[t] = 0;  // the next pass accumulates its parts' costs from zero
-        if (split && b >= mb + 2) {
-            const uint32_t o = atomicAdd(&base[b], 4u);
-#pragma unroll
-            for (int k = 0; k < 4; ++k) order[o + k] = (uint32_t)t | ((uint32_t)k << 26) | (3u << 28);
-        } else {
-            order[atomicAdd(&base[b], 1u)] = (uint32_t)t;
-        }
+        order[atomicAdd(&base[cost_bucket(cost[t])], 1u)] = (uint32_t)t;
     }
 }
 

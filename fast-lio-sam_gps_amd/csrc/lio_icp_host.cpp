@@ -293,8 +293,7 @@ struct lio_icp {
     // shard buffers
     int64_t sh_begin = 0, sh_n = 0, cap = 0;
     float* d_src = nullptr;
-    float* d_cur = nullptr;   // the incrementally transformed shard (after the last pass)
-    float* d_cur2 = nullptr;  // the next pass's output (swapped with d_cur after each pass)
+    float* d_cur = nullptr;
     float* d_fd2 = nullptr;
     int* d_fid = nullptr;
     lio::GridBuf qgrid;      // the shard's source binned by tile cell (icp_build_tiles)
@@ -308,7 +307,6 @@ struct lio_icp {
     bool have_prior = false;  // nn ids of this alignment's previous pass are in d_fid
     uint32_t* d_tcost = nullptr;  // per tile: candidates of the last pass
     uint32_t* d_order = nullptr;  // longest-first tile order (valid when have_order)
-    unsigned long long* d_key = nullptr;  // per point: the pass's (d2, id) key (reset to ~0 by the statistics)
     bool have_order = false;
     unsigned long long* d_dbg = nullptr;  // search counters (diagnostics build: LIO_DIAG + LIO_ICP_DEBUG)
     size_t dbg_bytes = 0;
@@ -372,8 +370,8 @@ int lio_icp_destroy(lio_icp* h) {
     (void)hipStreamSynchronize(h->st);
     lio::grid_free(h->tgt);
     lio::grid_free(h->qgrid);
-    void* ptrs[] = {h->d_tgt,   h->d_src,     h->d_cur,  h->d_cur2, h->d_fd2,   h->d_fid,   h->d_tiles, h->d_tscratch,
-                    h->d_ttmp,  h->d_dbg,     h->d_tcost, h->d_order, h->d_key, h->d_pairs, h->d_pcl16};
+    void* ptrs[] = {h->d_tgt,   h->d_src,     h->d_cur,  h->d_fd2,   h->d_fid,   h->d_tiles, h->d_tscratch,
+                    h->d_ttmp,  h->d_dbg,     h->d_tcost, h->d_order, h->d_pairs, h->d_pcl16};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (h->h_super) (void)hipHostFree(h->h_super);
@@ -498,8 +496,8 @@ static int icp_prepare(lio_icp* h) {
     shard_range(h->ns, h->rank, h->world, h->sh_begin, h->sh_n);
     const int64_t n = std::max<int64_t>(h->sh_n, 1);
     if (n > h->cap) {
-        void** ptrs[] = {(void**)&h->d_src,   (void**)&h->d_cur,   (void**)&h->d_cur2, (void**)&h->d_fd2,  (void**)&h->d_fid,
-                         (void**)&h->d_tiles, (void**)&h->d_tcost, (void**)&h->d_order, (void**)&h->d_key};
+        void** ptrs[] = {(void**)&h->d_src,   (void**)&h->d_cur,   (void**)&h->d_fd2,  (void**)&h->d_fid,
+                         (void**)&h->d_tiles, (void**)&h->d_tcost, (void**)&h->d_order};
         h->cap = 0;  // a failed allocation below leaves no buffer that looks usable (and nothing freed twice)
         for (void** q : ptrs) {
             if (*q) (void)hipFree(*q);
@@ -507,15 +505,11 @@ static int icp_prepare(lio_icp* h) {
         }
         IHIP(hipMalloc(&h->d_src, n * 3 * sizeof(float)));
         IHIP(hipMalloc(&h->d_cur, n * 3 * sizeof(float)));
-        IHIP(hipMalloc(&h->d_cur2, n * 3 * sizeof(float)));
         IHIP(hipMalloc(&h->d_fd2, n * sizeof(float)));
         IHIP(hipMalloc(&h->d_fid, n * sizeof(int)));
         IHIP(hipMalloc(&h->d_tiles, (n + n / lio::kIcpTileQ + 1) * sizeof(uint2)));
         IHIP(hipMalloc(&h->d_tcost, (n + n / lio::kIcpTileQ + 1) * sizeof(uint32_t)));
-        IHIP(hipMalloc(&h->d_order, (8 * (size_t)lio::icp_ord_cap((int)(n + n / lio::kIcpTileQ + 1)) + 8) *
-                                        sizeof(uint32_t)));  // 8 shares + their sizes
-        IHIP(hipMalloc(&h->d_key, n * sizeof(unsigned long long)));
-        IHIP(hipMemsetAsync(h->d_key, 0xff, n * sizeof(unsigned long long), h->st));
+        IHIP(hipMalloc(&h->d_order, (n + n / lio::kIcpTileQ + 64) * sizeof(uint32_t)));  // + the 9 share offsets
         h->cap = n;
     }
     const int64_t nsup_all = (h->ns + lio::kIcpSuper - 1) / lio::kIcpSuper + 1;
@@ -558,8 +552,7 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     lio::IcpArgs a{};
     a.grid = lio::grid_view(h->tgt);
     a.tgt_by_id = h->tgt.by_id;
-    a.cur_in = h->d_cur;
-    a.cur = h->d_cur2;
+    a.cur = h->d_cur;
     a.src = h->d_src;
     a.n = (int)h->sh_n;
     a.apply_T = apply_T ? 1 : 0;
@@ -575,8 +568,6 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     a.tiles = h->d_tiles;
     a.tile_cost = h->d_tcost;
     a.order = h->have_order ? h->d_order : nullptr;
-    a.ord_cap = lio::icp_ord_cap(h->ntiles);
-    a.key = h->d_key;
 #ifdef LIO_DIAG
     static const bool dbg_on = std::getenv("LIO_ICP_DEBUG") != nullptr;  // diagnostics build: search statistics
     if (dbg_on) {
@@ -628,7 +619,6 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     }
     h->have_prior = true;
     if (!fitness && h->sh_n > 0) h->have_order = true;
-    if (h->sh_n > 0) std::swap(h->d_cur, h->d_cur2);  // the pass's cloud becomes the current one
 #ifdef LIO_DIAG
     if (dbg_on) {
         unsigned long long c[5];

@@ -129,8 +129,7 @@ void grid_insert_ids(GridBuf& g, int64_t id0, const uint32_t* d_nnew, int n_max,
 struct IcpArgs {
     GridDev grid;
     const float4* tgt_by_id;
-    const float* cur_in; // n*3 incrementally transformed source before this pass (this rank's shard)
-    float* cur;          // n*3 after it (written by part 0 of each tile: the parts of a split tile read cur_in)
+    float* cur;          // n*3 incrementally transformed source (this rank's shard)
     const float* src;    // n*3 original source (fitness pass)
     int n;               // points in this shard
     int apply_T;         // apply T (float 4x4 row-major) to cur before the NN (incremental transform)
@@ -145,11 +144,7 @@ struct IcpArgs {
     const float4* qpts;  // source binned by tile cell: (x, y, z, local index bits), cell order
     const uint2* tiles;  // (first entry in qpts, query count <= kIcpTileQ) per tile
     const uint32_t* order;  // optional tile visit order (heaviest first, from the previous pass's costs)
-    uint32_t* tile_cost;    // per tile: candidates scanned in this pass (zeroed by the order build that reads it)
-    int ord_cap;            // slots of one XCD share in `order` (icp_ord_cap)
-    // per point: the pass's (d2, id) key, min-combined over the parts of a split tile (atomicMin); the
-    // statistics kernel decodes it into nn_d2 / nn_id and resets it to ~0
-    unsigned long long* key;
+    uint32_t* tile_cost;    // per tile: candidates scanned in this pass
     unsigned long long* dbg;  // optional counters (diagnostics): candidates, rings, tiles, lanes
 };
 
@@ -166,12 +161,6 @@ void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st);
 // tile order for the next pass: descending log2(cost) buckets (one block)
 // one record per 4096 points; with `order`, the next pass's tile order from a.tile_cost in the same launch
 void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st, uint32_t* order = nullptr, int ntiles = 0);
-// slots of one XCD share of the tile order: 8 segments of <= ceil(ntiles / 64) tiles, + 1/4 for the
-// extra parts of split tiles; the buffer holds 8 shares + 8 share sizes
-__host__ __device__ inline int icp_ord_cap(int ntiles) {
-    const int base = 8 * ((ntiles + 63) / 64);
-    return base + base / 4 + 4;
-}
 // the all-gathered records (world slots of `slot` records) summed in global record order, one thread
 // per statistic (the order of lio_icp_combine: bit-identical) -> out17 (host-mapped)
 void launch_icp_combine(const double* recv, int64_t nsup, int world, int64_t slot, double* out17, hipStream_t st);
