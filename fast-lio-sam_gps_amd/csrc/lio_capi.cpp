@@ -1246,7 +1246,8 @@ int lio_scan_keyframe_cloud(lio_ctx* c, const lio_pose* pose, const double* T16,
     int rc = grow(&c->d_kf, c->kf_cap, c->undist_n * 4);
     if (rc) return rc;
     lio::PoseArg ps;
-    std::memcpy(&ps, pose, sizeof(ps));
+    const lio_pose pf = filled(*pose);  // matrix-only callers: q / q_LI derived from R / R_LI (body_to_world rotates with them)
+    std::memcpy(&ps, &pf, sizeof(ps));
     if (lio::keyframe_cloud(c->filt.c, c->undist_n, c->undist_stride, ps, T16, c->d_kf, c->map->st))
         return fail(LIO_ERR_HIP, "keyframe cloud kernel failed");
     HIP_TRY(hipMemcpyAsync(out, c->d_kf, (size_t)c->undist_n * 4 * sizeof(float), hipMemcpyDeviceToHost, c->map->st));

@@ -809,6 +809,10 @@ void launch_icp_pcl_stats(const IcpArgs& a, float* pairs, float* out16, hipStrea
     icp_pcl_sigma_kernel<<<1, kPclThreads, 0, st>>>(pairs, out16);
 }
 
+void launch_icp_pcl_means_serial(const IcpArgs& a, float* pairs, float* out16, hipStream_t st) {
+    icp_pcl_means_kernel<<<1, kPclThreads, 0, st>>>(a, pairs, out16);
+}
+
 __global__ void __launch_bounds__(64) icp_combine_kernel(const double* __restrict__ recv, int64_t nsup, int world,
                                                         int64_t slot, double* __restrict__ out17) {
     const int k = threadIdx.x;

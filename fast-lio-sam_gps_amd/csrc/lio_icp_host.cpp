@@ -14,6 +14,8 @@
 // order, so the result is bit-identical for any number of ranks.
 #include <hip/hip_runtime.h>
 
+#include "lio_pcl.hpp"
+
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
@@ -230,8 +232,9 @@ float det3_f(const float* M) {  // column-major; Eigen determinant_impl<3>
     return h(0, 1, 2) - h(1, 0, 2) + h(2, 0, 1);
 }
 
-// out16 from launch_icp_pcl_stats -> the incremental transform (row-major 4x4 float)
-void umeyama_pcl_float(const float* out16, float Ti[16]) {
+// out16 from the fidelity statistics -> the incremental transform (row-major 4x4 float); order 1 returns
+// the raw sequential sigma accumulator (scaled here), orders 2 / 3 sigma as Eigen's GEMM leaves it
+void umeyama_pcl_float(const float* out16, float Ti[16], int order = 1) {
     const uint32_t n = [&] {
         uint32_t u;
         std::memcpy(&u, out16 + 6, sizeof(u));
@@ -245,7 +248,7 @@ void umeyama_pcl_float(const float* out16, float Ti[16]) {
     }
     float sigma[9];  // column-major
     for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) sigma[3 * c + r] = one_over_n * out16[7 + 3 * r + c];
+        for (int c = 0; c < 3; ++c) sigma[3 * c + r] = order == 1 ? one_over_n * out16[7 + 3 * r + c] : out16[7 + 3 * r + c];
     float U[9], V[9], sv[3];
     jacobi_svd3_f(sigma, U, V, sv);
     const float S2 = det3_f(U) * det3_f(V) < 0.f ? -1.f : 1.f;
@@ -314,10 +317,14 @@ struct lio_icp {
     double* h_super_dev = nullptr;  // device view of h_super (the statistics kernel writes it, zero-copy)
     int64_t super_cap = 0;
     bool src_dirty = true;
-    float* d_pairs = nullptr;  // umeyama_float: compacted correspondence pairs (cap * 6)
-    int64_t pairs_cap = 0;
-    float* d_pcl16 = nullptr;  // umeyama_float: the serial float sums (launch_icp_pcl_stats)
+    float* d_pcl16 = nullptr;  // umeyama_float: the serial float sums (launch_icp_pcl_stats: the fallback)
     float* h_pcl16 = nullptr;  // pinned copy
+    lio::PclBuf pcl;           // umeyama_float: compacted pairs + seqsum chains
+    float* d_pclout = nullptr; // pcl_pack output (kPclOutWords)
+    float* h_pclout = nullptr; // pinned copy
+    int64_t fid_stats[4] = {0, 0, 0, 0};  // re-passes, serial fallbacks, events of the last pass, passes
+    int fid_flags = 0;
+    int64_t fid_evcap = 0;
     bool timing = false;
     lio_kernel_timing tm{};
     EvPair ev;
@@ -371,11 +378,14 @@ int lio_icp_destroy(lio_icp* h) {
     lio::grid_free(h->tgt);
     lio::grid_free(h->qgrid);
     void* ptrs[] = {h->d_tgt,   h->d_src,     h->d_cur,  h->d_fd2,   h->d_fid,   h->d_tiles, h->d_tscratch,
-                    h->d_ttmp,  h->d_dbg,     h->d_tcost, h->d_order, h->d_pairs, h->d_pcl16};
+                    h->d_ttmp,  h->d_dbg,     h->d_tcost, h->d_order, h->d_pcl16};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (h->h_super) (void)hipHostFree(h->h_super);
     if (h->h_pcl16) (void)hipHostFree(h->h_pcl16);
+    lio::pcl_free(h->pcl);
+    if (h->d_pclout) (void)hipFree(h->d_pclout);
+    if (h->h_pclout) (void)hipHostFree(h->h_pclout);
     if (h->h_out17) (void)hipHostFree(h->h_out17);
     if (!h->x_ext) {
         if (h->d_xsend) (void)hipFree(h->d_xsend);
@@ -546,6 +556,58 @@ static int icp_prepare(lio_icp* h) {
     return LIO_OK;
 }
 
+// Float fidelity statistics of the pass (h_pclout after the pass's wait): a chain that failed its
+// verification is re-run with the predictions of its reconstruction (passes 2, 3); an event-list overflow
+// or a third failure falls back to the serial kernels (one lane per chain, the sums in order).
+static uint32_t pcl_word(const lio_icp* h, int w) {
+    uint32_t u;
+    std::memcpy(&u, h->h_pclout + 16 + w, sizeof(u));
+    return u;
+}
+
+static int pcl_finish(lio_icp* h, const lio::IcpArgs& a) {
+    const int order = h->p.umeyama_float;
+    ++h->fid_stats[3];
+    {
+        int ev;
+        std::memcpy(&ev, h->h_pclout + 18, sizeof(ev));
+        h->fid_stats[2] = ev;
+    }
+    int pass = 1;
+    while ((pcl_word(h, 0) | pcl_word(h, 1)) != 0 && pass < 3) {
+        const uint32_t bad = pcl_word(h, 0), over = pcl_word(h, 1);
+        if (over) break;  // more passes only add events
+        ++pass;
+        ++h->fid_stats[0];
+        ++h->fid_stats[3];
+        if (bad & 0x3fu) {  // the means (sigma depends on them: its chains restart from pass 1)
+            lio::launch_pcl_means(h->pcl, pass, h->st);
+            lio::launch_pcl_sigma(h->pcl, order, 1, h->st);
+        } else {
+            lio::launch_pcl_sigma(h->pcl, order, pass, h->st);
+        }
+        lio::launch_pcl_pack(h->pcl, order, h->d_pclout, h->st);
+        IHIP(hipMemcpyAsync(h->h_pclout, h->d_pclout, lio::kPclOutWords * sizeof(float), hipMemcpyDeviceToHost, h->st));
+        IHIP(hipStreamSynchronize(h->st));
+    }
+    if ((pcl_word(h, 0) | pcl_word(h, 1)) != 0) {  // the serial kernels: one lane per chain
+        ++h->fid_stats[1];
+        if (order == lio::kPclSeq) {
+            lio::launch_icp_pcl_stats(a, h->pcl.pairs, h->d_pcl16, h->st);
+            IHIP(hipMemcpyAsync(h->h_pclout, h->d_pcl16, 16 * sizeof(float), hipMemcpyDeviceToHost, h->st));
+        } else {
+            lio::launch_icp_pcl_means_serial(a, h->pcl.pairs, h->d_pcl16, h->st);
+            lio::launch_pcl_sigma(h->pcl, order, 1, h->st, h->d_pcl16);
+            lio::launch_pcl_pack(h->pcl, order, h->d_pclout, h->st, h->d_pcl16);
+            IHIP(hipMemcpyAsync(h->h_pclout, h->d_pclout, lio::kPclOutWords * sizeof(float), hipMemcpyDeviceToHost, h->st));
+        }
+        IHIP(hipStreamSynchronize(h->st));
+        h->h_pclout[16] = h->h_pclout[17] = 0.f;
+    }
+    IHIP(hipGetLastError());
+    return LIO_OK;
+}
+
 // One correspondence (or fitness) pass: GPU kernels + exchange + ordered sum.
 static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, double max_d2, double out17[17],
                     float* pcl16 = nullptr) {
@@ -607,9 +669,13 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
             lio::launch_icp_stats(a, h->h_super_dev, h->st, fitness ? nullptr : h->d_order, h->ntiles);
         }
         if (h->timing) IHIP(hipEventRecord(h->ev.b, h->st));
-        if (pcl16) {  // PCL-order fidelity mode: the serial float sums of this pass's correspondences
-            lio::launch_icp_pcl_stats(a, h->d_pairs, h->d_pcl16, h->st);
-            IHIP(hipMemcpyAsync(h->h_pcl16, h->d_pcl16, 16 * sizeof(float), hipMemcpyDeviceToHost, h->st));
+        if (pcl16) {  // float fidelity mode: pcl::umeyama's float sums of this pass's correspondences
+            const int order = h->p.umeyama_float;
+            lio::launch_pcl_compact(a, h->pcl, h->st);
+            lio::launch_pcl_means(h->pcl, 1, h->st);
+            lio::launch_pcl_sigma(h->pcl, order, 1, h->st);
+            lio::launch_pcl_pack(h->pcl, order, h->d_pclout, h->st);
+            IHIP(hipMemcpyAsync(h->h_pclout, h->d_pclout, lio::kPclOutWords * sizeof(float), hipMemcpyDeviceToHost, h->st));
         }
         IHIP(hipGetLastError());
         IHIP(hipEventRecord(h->ev.done, h->st));
@@ -668,7 +734,11 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
             ++h->tm.icp_nn_launches;
         }
     }
-    if (pcl16) std::memcpy(pcl16, h->h_pcl16, 16 * sizeof(float));
+    if (pcl16) {
+        const int rc = pcl_finish(h, a);
+        if (rc) return rc;
+        std::memcpy(pcl16, h->h_pclout, 16 * sizeof(float));
+    }
     if (dev_x) {  // the record-order sums of every rank's records, computed on the device
         std::memcpy(out17, h->h_out17, 17 * sizeof(double));
         return LIO_OK;
@@ -702,6 +772,67 @@ extern "C" int lio_icp_umeyama_pcl_float(const float* sums16, float* T16) {
     return LIO_OK;
 }
 
+extern "C" int lio_icp_umeyama_pcl_float_order(const float* sums16, int order, float* T16) {
+    if (!sums16 || !T16 || order < 1 || order > 3) return ifail(LIO_ERR_ARG, "lio_icp_umeyama_pcl_float_order: bad arguments");
+    umeyama_pcl_float(sums16, T16, order);
+    return LIO_OK;
+}
+
+extern "C" int lio_icp_get_fidelity_stats(lio_icp* h, int64_t* out4) {
+    if (!h || !out4) return ifail(LIO_ERR_ARG, "lio_icp_get_fidelity_stats: bad arguments");
+    std::memcpy(out4, h->fid_stats, sizeof(h->fid_stats));
+    return LIO_OK;
+}
+
+extern "C" int lio_icp_set_fidelity_debug(lio_icp* h, int flags, int64_t evcap) {
+    if (!h || evcap < 0) return ifail(LIO_ERR_ARG, "lio_icp_set_fidelity_debug: bad arguments");
+    h->fid_flags = flags;
+    h->fid_evcap = evcap;
+    return LIO_OK;
+}
+
+// test hook: the seqsum path on 6 interleaved chains, re-passes as in pcl_finish; -1 passes: serial needed
+extern "C" int lio_seqsum6(int device, const float* x, int64_t n, int flags, float* sums6, int* passes_out) {
+    if (!x || n < 1 || !sums6 || n >= ((int64_t)1 << 31)) return ifail(LIO_ERR_ARG, "lio_seqsum6: bad arguments");
+    int rc = icp_check_dev(device);
+    if (rc) return rc;
+    IHIP(hipSetDevice(device));
+    hipStream_t st;
+    IHIP(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    lio::SeqSumBuf b;
+    b.dbg_noinc = flags & 1;
+    float* d_x = nullptr;
+    uint32_t* d_n = nullptr;
+    uint32_t stat[2] = {0, 0};
+    int passes = 0;
+    const uint32_t n32 = (uint32_t)n;
+    auto done = [&](int code, const char* msg) {
+        lio::seqsum_free(b);
+        if (d_x) (void)hipFree(d_x);
+        if (d_n) (void)hipFree(d_n);
+        (void)hipStreamDestroy(st);
+        return code ? ifail(code, msg) : LIO_OK;
+    };
+    if (lio::seqsum_reserve(b, 6, n, st) || hipMalloc(&d_x, (size_t)n * 6 * sizeof(float)) != hipSuccess ||
+        hipMalloc(&d_n, sizeof(uint32_t)) != hipSuccess)
+        return done(LIO_ERR_NOMEM, "lio_seqsum6: allocation");
+    if (flags & 2) b.evcap = std::min<int64_t>(4, b.evcap_alloc);  // overflow: the caller's serial fallback
+    if (hipMemcpyAsync(d_x, x, (size_t)n * 6 * sizeof(float), hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(d_n, &n32, sizeof(n32), hipMemcpyHostToDevice, st) != hipSuccess)
+        return done(LIO_ERR_HIP, "lio_seqsum6: upload");
+    for (int pass = 1; pass <= 3; ++pass) {
+        lio::seqsum_launch(lio::SeqPairs{d_x}, 6, d_n, b, pass, st);
+        if (hipMemcpyAsync(stat, b.status, sizeof(stat), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipMemcpyAsync(sums6, b.result, 6 * sizeof(float), hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess)
+            return done(LIO_ERR_HIP, "lio_seqsum6: kernels");
+        passes = pass;
+        if ((stat[0] | stat[1]) == 0 || stat[1]) break;
+    }
+    if (passes_out) *passes_out = (stat[0] | stat[1]) ? -1 : passes;
+    return done(LIO_OK, "");
+}
+
 extern "C" int lio_icp_combine(const double* recv, int64_t ns, int world, double* out17) {
     if (!recv || !out17 || world < 1 || ns < 0) return ifail(LIO_ERR_ARG, "lio_icp_combine: bad arguments");
     const int64_t nsup = (ns + lio::kIcpSuper - 1) / lio::kIcpSuper;
@@ -722,20 +853,21 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
     if (h->nt == 0) return ifail(LIO_ERR_STATE, "lio_icp_align: no target");
     IHIP(hipSetDevice(h->dev));
     const bool pcl_float = h->p.umeyama_float != 0;
+    if (h->p.umeyama_float < 0 || h->p.umeyama_float > 3)
+        return ifail(LIO_ERR_ARG, "lio_icp_align: umeyama_float must be 0 (double statistics) or 1..3 (float orders)");
     if (pcl_float && h->world > 1)
         return ifail(LIO_ERR_ARG, "lio_icp_align: umeyama_float (PCL-order float sums) runs on one rank only");
     int rc = icp_prepare(h);
     if (rc) return rc;
     if (pcl_float) {
-        if (h->sh_n > h->pairs_cap || !h->d_pairs) {
-            if (h->d_pairs) IHIP(hipFree(h->d_pairs));
-            h->d_pairs = nullptr;
-            h->pairs_cap = 0;
-            IHIP(hipMalloc(&h->d_pairs, (size_t)std::max<int64_t>(h->sh_n, 1) * 6 * sizeof(float)));
-            h->pairs_cap = std::max<int64_t>(h->sh_n, 1);
-        }
+        if (lio::pcl_reserve(h->pcl, std::max<int64_t>(h->sh_n, 1), h->p.umeyama_float, h->st))
+            return ifail(LIO_ERR_NOMEM, "lio_icp_align: fidelity buffers");
+        h->pcl.means.dbg_noinc = h->pcl.sig.dbg_noinc = h->fid_flags & 1;
+        for (lio::SeqSumBuf* b : {&h->pcl.means, &h->pcl.sig})
+            b->evcap = h->fid_evcap > 0 ? std::min(h->fid_evcap, b->evcap_alloc) : b->evcap_alloc;
         if (!h->d_pcl16) IHIP(hipMalloc(&h->d_pcl16, 16 * sizeof(float)));
-        if (!h->h_pcl16) IHIP(hipHostMalloc(&h->h_pcl16, 16 * sizeof(float), hipHostMallocDefault));
+        if (!h->d_pclout) IHIP(hipMalloc(&h->d_pclout, 32 * sizeof(float)));
+        if (!h->h_pclout) IHIP(hipHostMalloc(&h->h_pclout, 32 * sizeof(float), hipHostMallocDefault));
     }
     float fin[16], G[16];
     bool ident = true;
@@ -771,7 +903,7 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
         }
         float Ti[16];
         if (pcl_float)
-            umeyama_pcl_float(pcl16, Ti);
+            umeyama_pcl_float(pcl16, Ti, h->p.umeyama_float);
         else
             umeyama(st, h->c0, Ti);
         float nf[16];

@@ -1,0 +1,295 @@
+// lio_pcl.hip — the float statistics of pcl::umeyama for the ICP fidelity modes (lio_icp_params.umeyama_float).
+//
+// PCL 1.10 TransformationEstimationSVD<PointXYZI, PointXYZI, float> (use_umeyama_) hands the accepted
+// correspondences, in source order, to pcl::umeyama(cloud_src, cloud_tgt, false) (common/impl/eigen.hpp,
+// Eigen 3.3 Umeyama.h) [U]:
+//   src_mean = src.rowwise().sum() * one_over_n      one sequential float chain per row (Eigen's redux of a
+//   dst_mean = dst.rowwise().sum() * one_over_n      strided row starts from the first coefficient)
+//   sigma    = one_over_n * dst_demean * src_demean^T  order 1: one sequential chain per entry, scaled at
+//              the end; orders 2 / 3: Eigen 3.3's GEMM, the depth blocked by kc(L1 32 / 48 KiB) and
+//              res += alpha * (block's sequential sum) per block (oracle/lio_oracle.cpp UmeyamaOrder)
+// Here:
+//   pcl_count / pcl_scan / pcl_scatter   the accepted pairs compacted in source order (n on the device)
+//   seqsum (lio_seqsum.hip)              the six mean chains (and order 1's nine sigma chains), bit-exact
+//                                        sequential float results computed in parallel
+//   pcl_sigma_blocks                     orders 2 / 3: one wave per kc block, nine sequential lanes from LDS
+//   pcl_pack                             res += alpha * C_b in block order; sums, count, sigma, status
+// Single rank only (the correspondence order is global).
+#include "lio_kernels.hpp"
+#include "lio_pcl.hpp"
+
+#include <algorithm>
+
+namespace lio {
+
+namespace {
+
+constexpr int kPT = 256;           // threads per compaction block
+constexpr int kPPer = 4;           // consecutive source points per thread
+constexpr int kPB = kPT * kPPer;   // source points per compaction block
+constexpr int kMaxKc = 1016;       // kc at a 48 KiB L1 (the largest modelled)
+
+__device__ __forceinline__ bool pcl_accept(const IcpArgs& a, int i) {
+    const int id = a.nn_id[i];
+    const float d2 = a.nn_d2[i];
+    return id >= 0 && id != kNone && !((double)d2 > a.max_d2);
+}
+
+__device__ __forceinline__ uint32_t block_excl_u32(uint32_t v, uint32_t* s_w, uint32_t& tot) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t u = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += u;
+    }
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    uint32_t off = 0, t = 0;
+    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
+        if (i < w) off += s_w[i];
+        t += s_w[i];
+    }
+    __syncthreads();
+    tot = t;
+    return off + inc - v;
+}
+
+__global__ void __launch_bounds__(kPT) pcl_count_kernel(IcpArgs a, uint32_t* __restrict__ bcnt) {
+    __shared__ uint32_t s_w[kPT / 64];
+    const int i0 = blockIdx.x * kPB + threadIdx.x * kPPer;
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < kPPer; ++i)
+        if (i0 + i < a.n && pcl_accept(a, i0 + i)) ++c;
+    uint32_t tot;
+    block_excl_u32(c, s_w, tot);
+    if (threadIdx.x == 0) bcnt[blockIdx.x] = tot;
+}
+
+// exclusive scan of the block counts in place, the total -> *d_n
+__global__ void __launch_bounds__(kPT) pcl_scan_kernel(uint32_t* __restrict__ bcnt, int nb, uint32_t* __restrict__ d_n) {
+    __shared__ uint32_t s_w[kPT / 64];
+    uint32_t base = 0;
+    for (int j0 = 0; j0 < nb; j0 += kPT) {
+        const int j = j0 + (int)threadIdx.x;
+        const uint32_t v = j < nb ? bcnt[j] : 0u;
+        uint32_t tot;
+        const uint32_t ex = block_excl_u32(v, s_w, tot);
+        if (j < nb) bcnt[j] = base + ex;
+        base += tot;
+    }
+    if (threadIdx.x == 0) *d_n = base;
+}
+
+__global__ void __launch_bounds__(kPT) pcl_scatter_kernel(IcpArgs a, const uint32_t* __restrict__ boff,
+                                                          float* __restrict__ pairs) {
+    __shared__ uint32_t s_w[kPT / 64];
+    const int i0 = blockIdx.x * kPB + threadIdx.x * kPPer;
+    bool ok[kPPer];
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < kPPer; ++i) {
+        ok[i] = i0 + i < a.n && pcl_accept(a, i0 + i);
+        c += ok[i] ? 1u : 0u;
+    }
+    uint32_t tot;
+    uint32_t slot = boff[blockIdx.x] + block_excl_u32(c, s_w, tot);
+#pragma unroll
+    for (int i = 0; i < kPPer; ++i)
+        if (ok[i]) {
+            const int p = i0 + i;
+            const float4 q = a.tgt_by_id[a.nn_id[p]];
+            float* o = pairs + 6 * (size_t)slot;
+            o[0] = a.cur[3 * p];
+            o[1] = a.cur[3 * p + 1];
+            o[2] = a.cur[3 * p + 2];
+            o[3] = q.x;
+            o[4] = q.y;
+            o[5] = q.z;
+            ++slot;
+        }
+}
+
+// float means of the sequential sums (order 1's sigma chains read them)
+__global__ void pcl_mean6_kernel(const float* __restrict__ sums6, const uint32_t* __restrict__ d_n,
+                                 float* __restrict__ mean6) {
+    const uint32_t n = *d_n;
+    const float oon = 1.f / (float)n;
+    if (threadIdx.x < 6) mean6[threadIdx.x] = sums6[threadIdx.x] * oon;
+}
+
+// orders 2 / 3: block q of the depth = pairs [q kc, (q + 1) kc): lane e < 9 (r = e / 3, c = e % 3) adds
+// (tgt_r - dm_r) * (src_c - sm_c) in order from 0 (gebp's 1 x 1 remainder path: C0 += A0 * B0, no FMA)
+__global__ void __launch_bounds__(64) pcl_sigma_blocks_kernel(const float* __restrict__ pairs,
+                                                              const uint32_t* __restrict__ d_n,
+                                                              const float* __restrict__ sums6, int l1,
+                                                              float* __restrict__ Cb) {
+    __shared__ float s[6][kMaxKc];
+    const uint32_t n = *d_n;
+    if (n + 6 < 20) return;  // the lazy coefficient-based product: pcl_pack
+    const int64_t kc = eigen_gemm_kc((int64_t)n, l1);
+    const int64_t nkc = ((int64_t)n + kc - 1) / kc;
+    const int lane = threadIdx.x;
+    const float oon = 1.f / (float)n;
+    const int r = lane / 3, c = lane % 3;
+    const float dm = lane < 9 ? sums6[3 + r] * oon : 0.f;
+    const float sm = lane < 9 ? sums6[c] * oon : 0.f;
+    for (int64_t q = blockIdx.x; q < nkc; q += gridDim.x) {
+        const int64_t k0 = q * kc;
+        const int cnt = (int)((int64_t)n - k0 < kc ? (int64_t)n - k0 : kc);
+        for (int e = lane; e < 6 * cnt; e += 64) s[e % 6][e / 6] = pairs[6 * k0 + e];  // coalesced, pair-major
+        __syncthreads();
+        if (lane < 9) {
+            const float* dv = s[3 + r];
+            const float* sv = s[c];
+            float C0 = 0.f;
+            int j = 0;
+            for (; j + 8 <= cnt; j += 8) {
+                float p[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) p[u] = (dv[j + u] - dm) * (sv[j + u] - sm);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) C0 += p[u];
+            }
+            for (; j < cnt; ++j) C0 += (dv[j] - dm) * (sv[j] - sm);
+            Cb[q * 9 + lane] = C0;
+        }
+        __syncthreads();
+    }
+}
+
+// out[0..5] float sums (src xyz, tgt xyz), out[6] count bits, out[7 + 3r + c] sigma (orders 2 / 3: scaled by
+// one_over_n as Eigen leaves it; order 1: the raw sequential accumulator, scaled on the host), out[16]
+// verification failures (means bits 0-5, sigma chains 8-16), out[17] event-list overflows (same bits)
+__global__ void __launch_bounds__(64) pcl_pack_kernel(const float* __restrict__ pairs, const uint32_t* __restrict__ d_n,
+                                                      const float* __restrict__ sums6, const float* __restrict__ sig9,
+                                                      const float* __restrict__ Cb, int order, int l1,
+                                                      const uint32_t* __restrict__ st_means,
+                                                      const uint32_t* __restrict__ st_sig,
+                                                      const int* __restrict__ nev6, float* __restrict__ out) {
+    __shared__ float s_c[9][256];
+    const uint32_t n = *d_n;
+    const int lane = threadIdx.x;
+    const float oon = 1.f / (float)n;
+    if (lane < 6) out[lane] = sums6[lane];
+    if (lane == 6) out[6] = __uint_as_float(n);
+    const int r = lane / 3, c = lane % 3;
+    float res = 0.f;
+    if (order == 1 || n == 0) {
+        if (lane < 9) res = order == 1 ? sig9[lane] : 0.f;
+    } else if (n + 6 < 20) {
+        // generic_product_impl::evalTo below EIGEN_GEMM_TO_COEFFBASED_THRESHOLD: the lazy product,
+        // (alpha * dst_demean).row(r) . src_demean.row(c) summed from the first term
+        if (lane < 9) {
+            const float dm = sums6[3 + r] * oon, sm = sums6[c] * oon;
+            res = (oon * (pairs[3 + r] - dm)) * (pairs[c] - sm);
+            for (uint32_t k = 1; k < n; ++k) res += (oon * (pairs[6 * k + 3 + r] - dm)) * (pairs[6 * k + c] - sm);
+        }
+    } else {
+        const int64_t kc = eigen_gemm_kc((int64_t)n, l1);
+        const int64_t nkc = ((int64_t)n + kc - 1) / kc;
+        for (int64_t q0 = 0; q0 < nkc; q0 += 256) {  // dst.setZero(); res(r, c) += alpha * C0 per depth block
+            const int m = (int)(nkc - q0 < 256 ? nkc - q0 : 256);
+            for (int e = lane; e < 9 * m; e += 64) s_c[e % 9][e / 9] = Cb[q0 * 9 + e];
+            __syncthreads();
+            if (lane < 9)
+                for (int q = 0; q < m; ++q) {
+                    const float t = oon * s_c[lane][q];
+                    res = res + t;
+                }
+            __syncthreads();
+        }
+    }
+    if (lane < 9) out[7 + lane] = res;
+    if (lane == 0) {
+        const uint32_t f = (st_means[0] & 0x3fu) | (order == 1 ? (st_sig[0] & 0x1ffu) << 8 : 0u);
+        const uint32_t o = (st_means[1] & 0x3fu) | (order == 1 ? (st_sig[1] & 0x1ffu) << 8 : 0u);
+        out[16] = __uint_as_float(f);
+        out[17] = __uint_as_float(o);
+        int ev = 0;
+        if (nev6)
+            for (int k = 0; k < 6; ++k) ev = max(ev, nev6[k]);
+        out[18] = __int_as_float(ev);
+    }
+}
+
+}  // namespace
+
+int pcl_reserve(PclBuf& p, int64_t n, int order, hipStream_t st) {
+    n = n < 1 ? 1 : n;
+    if (n > p.cap) {
+        void* ptrs[] = {p.pairs, p.bcnt, p.Cb};
+        for (void* q : ptrs)
+            if (q) (void)hipFree(q);
+        p.pairs = nullptr;
+        p.bcnt = nullptr;
+        p.Cb = nullptr;
+        p.cap = 0;
+        const int64_t nb = (n + kPB - 1) / kPB;
+        const int64_t nkc = n / 340 + 2;  // kc >= max_kc / 2 >= 340 once the depth is blocked
+        if (hipMalloc(&p.pairs, (size_t)n * 6 * sizeof(float)) != hipSuccess ||
+            hipMalloc(&p.bcnt, (size_t)nb * sizeof(uint32_t)) != hipSuccess ||
+            hipMalloc(&p.Cb, (size_t)nkc * 9 * sizeof(float)) != hipSuccess)
+            return -5;
+        p.cap = n;
+    }
+    if (!p.small) {
+        if (hipMalloc(&p.small, 64 * sizeof(float)) != hipSuccess) return -5;
+        (void)hipMemsetAsync(p.small, 0, 64 * sizeof(float), st);
+    }
+    if (seqsum_reserve(p.means, 6, n, st)) return -5;
+    if (order == 1 && seqsum_reserve(p.sig, 9, n, st)) return -5;
+    return 0;
+}
+
+void pcl_free(PclBuf& p) {
+    void* ptrs[] = {p.pairs, p.bcnt, p.Cb, p.small};
+    for (void* q : ptrs)
+        if (q) (void)hipFree(q);
+    seqsum_free(p.means);
+    seqsum_free(p.sig);
+    p = PclBuf{};
+}
+
+void launch_pcl_compact(const IcpArgs& a, PclBuf& p, hipStream_t st) {
+    const int nb = (a.n + kPB - 1) / kPB;
+    uint32_t* d_n = p.small + kPclN;
+    if (nb == 0) {
+        (void)hipMemsetAsync(d_n, 0, sizeof(uint32_t), st);
+        return;
+    }
+    pcl_count_kernel<<<nb, kPT, 0, st>>>(a, p.bcnt);
+    pcl_scan_kernel<<<1, kPT, 0, st>>>(p.bcnt, nb, d_n);
+    pcl_scatter_kernel<<<nb, kPT, 0, st>>>(a, p.bcnt, p.pairs);
+}
+
+void launch_pcl_means(PclBuf& p, int pass, hipStream_t st) {
+    seqsum_launch(SeqPairs{p.pairs}, 6, p.small + kPclN, p.means, pass, st);
+}
+
+void launch_pcl_sigma(PclBuf& p, int order, int pass, hipStream_t st, const float* sums6) {
+    const uint32_t* d_n = p.small + kPclN;
+    if (!sums6) sums6 = p.means.result;
+    if (order == 1) {
+        float* mean6 = reinterpret_cast<float*>(p.small + kPclMean6);
+        pcl_mean6_kernel<<<1, 64, 0, st>>>(sums6, d_n, mean6);
+        seqsum_launch(SeqSigma{p.pairs, mean6}, 9, d_n, p.sig, pass, st);
+    } else {
+        const int64_t grid = std::min<int64_t>(p.cap / 340 + 2, 4096);
+        pcl_sigma_blocks_kernel<<<(int)grid, 64, 0, st>>>(p.pairs, d_n, sums6, pcl_l1(order), p.Cb);
+    }
+}
+
+void launch_pcl_pack(PclBuf& p, int order, float* out, hipStream_t st, const float* sums6) {
+    const uint32_t* d_n = p.small + kPclN;
+    const uint32_t* zero = p.small + kPclZero;  // the serial fallback's sums need no verification
+    const bool serial = sums6 != nullptr;
+    if (!sums6) sums6 = p.means.result;
+    pcl_pack_kernel<<<1, 64, 0, st>>>(p.pairs, d_n, sums6, order == 1 ? p.sig.result : sums6, p.Cb, order,
+                                      pcl_l1(order), serial ? zero : p.means.status,
+                                      order == 1 && !serial ? p.sig.status : zero,
+                                      serial ? nullptr : p.means.floor_e + p.means.nch, out);
+}
+
+}  // namespace lio

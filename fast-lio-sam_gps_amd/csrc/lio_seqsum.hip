@@ -1,0 +1,539 @@
+// lio_seqsum.hip — sequential float summation chains evaluated in parallel, bit-exact (lio_seqsum.hpp).
+//
+// Per pass, for every chain (grid.y = chain):
+//   seq_bsum     block double prefix (prediction) totals, sum |x| (bound on |s|)
+//   seq_scan1    per chain, sequential over blocks: double block offsets, the binade floor
+//   seq_count    per element: predicted binade, event flag, fixed-point increment -> block totals
+//   seq_scan2    per chain: exclusive block offsets of increments and events
+//   seq_events   the events in element order: position, increment prefix, x
+//   seq_walk     one wave per chain replays the events (run sums exact in double) -> event results, sum
+//   seq_verify   every s_k rebuilt from the events; s_k == fl(s_{k-1} + x_k) checked for every k
+#include "lio_seqsum.hpp"
+
+#include <cmath>
+
+namespace lio {
+
+namespace {
+
+constexpr int kSpecial = -1000;  // zero, subnormal or non-finite: no binade
+
+__device__ __forceinline__ int binade_f(float f) {
+    const uint32_t b = __float_as_uint(f);
+    const int e = (int)((b >> 23) & 0xffu);
+    return (e == 0 || e == 255) ? kSpecial : e - 127;
+}
+
+template <typename T>
+__device__ __forceinline__ T wave_incl(T v) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const T u = __shfl_up(v, d, 64);
+        if (lane >= d) v = v + u;
+    }
+    return v;
+}
+
+// exclusive block prefix of v (integer types: any order is exact); total -> *tot (all threads)
+template <typename T>
+__device__ __forceinline__ T block_excl(T v, T* s_w, T& tot) {
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const T inc = wave_incl(v);
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    T off = 0, t = 0;
+#pragma unroll
+    for (int i = 0; i < kSeqThreads / 64; ++i) {
+        const T c = s_w[i];
+        if (i < w) off = off + c;
+        t = t + c;
+    }
+    __syncthreads();
+    tot = t;
+    return off + inc - v;
+}
+
+// The block's double prefix D_local[i] of its elements (thread t holds elements 4t .. 4t + 3) and the block
+// total, in ONE fixed order: seq_bsum stores the total, seq_count rebuilds every D_k from the same code, so
+// the prediction of the block's last element (boff[b] + total) equals the next block's boff bit for bit.
+__device__ __forceinline__ double block_dprefix(const float (&x)[kSeqPer], double (&D)[kSeqPer], double* s_w, double& tot) {
+    double run = (double)x[0];
+    double loc[kSeqPer];
+    loc[0] = run;
+#pragma unroll
+    for (int i = 1; i < kSeqPer; ++i) {
+        run = run + (double)x[i];
+        loc[i] = run;
+    }
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const double inc = wave_incl(run);
+    double ex = __shfl_up(inc, 1, 64);
+    if (lane == 0) ex = 0.0;
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    double off = 0.0;
+    for (int i = 0; i < w; ++i) off = off + s_w[i];
+    const double base = off + ex;
+#pragma unroll
+    for (int i = 0; i < kSeqPer; ++i) D[i] = base + loc[i];
+    __syncthreads();
+    // the total IS the last element's D (not a separately ordered sum of the wave totals)
+    if (threadIdx.x == kSeqThreads - 1) s_w[0] = D[kSeqPer - 1];
+    __syncthreads();
+    tot = s_w[0];
+    __syncthreads();
+    return base;
+}
+
+struct ElemInfo {
+    float x[kSeqPer];
+    int e[kSeqPer];   // predicted binade of s_k
+    int ep;           // predicted binade of the element before this thread's first
+};
+
+// event / increment of element k >= 1 from its value, predicted binade e, the predecessor's ep, the floor
+__device__ __forceinline__ bool seq_event(float x, int e, int ep, int floor_e, bool forced, bool noinc, uint64_t& inc) {
+    inc = 0;
+    if (forced || e == kSpecial || ep == kSpecial || (e > ep && !noinc) || e < floor_e || e - floor_e > 60) return true;
+    if (!(fabsf(x) <= 3.402823466e38f)) return true;  // non-finite
+    const double t = ldexp((double)x, 23 - e);
+    if (!(fabs(t) < 0x1p52)) return true;
+    const double r = rint(t);
+    if (fabs(t - r) == 0.5) return true;  // a tie: the parity of the running sum decides
+    const int64_t m = (int64_t)r;
+    inc = (uint64_t)m << (e - floor_e);
+    return false;
+}
+
+template <class Src>
+__device__ __forceinline__ void load_x(const Src& src, int c, int64_t k0, int64_t n, float (&x)[kSeqPer]) {
+#pragma unroll
+    for (int i = 0; i < kSeqPer; ++i) {
+        const int64_t k = k0 + i;
+        x[i] = k < n ? src(c, k) : 0.f;
+    }
+}
+
+__device__ __forceinline__ bool forced_bit(const uint32_t* f, int64_t k) { return f && ((f[k >> 5] >> (k & 31)) & 1u); }
+
+// predictions for this thread's elements (pass 1: double prefix; later: the previous reconstruction)
+template <class Src>
+__device__ __forceinline__ void predict(const Src& src, const SeqSumBuf& b, int c, int64_t n, int pass, ElemInfo& in,
+                                        double* s_wd) {
+    const int blk = blockIdx.x;
+    const int64_t k0 = (int64_t)blk * kSeqBlock + (int64_t)threadIdx.x * kSeqPer;
+    load_x(src, c, k0, n, in.x);
+    if (pass <= 1) {
+        double D[kSeqPer], tot;
+        block_dprefix(in.x, D, s_wd, tot);
+        const double bo = b.boff[(size_t)c * b.nblk + blk];
+#pragma unroll
+        for (int i = 0; i < kSeqPer; ++i) in.e[i] = binade_f((float)(bo + D[i]));
+        // predecessor of the thread's first element: the previous thread's last (block's first: boff)
+        int prev = __shfl_up(in.e[kSeqPer - 1], 1, 64);
+        __shared__ int s_last[kSeqThreads / 64];
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        if (lane == 63) s_last[w] = in.e[kSeqPer - 1];
+        __syncthreads();
+        if (lane == 0) prev = w > 0 ? s_last[w - 1] : binade_f((float)bo);
+        __syncthreads();
+        in.ep = prev;
+    } else {
+        const float* rc = b.recon + (size_t)c * b.nmax;
+#pragma unroll
+        for (int i = 0; i < kSeqPer; ++i) in.e[i] = k0 + i < n ? binade_f(rc[k0 + i]) : kSpecial;
+        in.ep = k0 > 0 ? binade_f(rc[k0 - 1]) : kSpecial;
+    }
+    if (k0 == 0) in.e[0] = binade_f(in.x[0]);  // s_0 = x_0 exactly
+}
+
+// per element: event flag and increment (element 0: the start, neither)
+template <class Src>
+__device__ __forceinline__ void classify(const SeqSumBuf& b, int c, int64_t n, const ElemInfo& in, int floor_e, int pass,
+                                         bool (&ev)[kSeqPer], uint64_t (&inc)[kSeqPer]) {
+    const bool noinc = b.dbg_noinc && pass <= 1;
+    const int64_t k0 = (int64_t)blockIdx.x * kSeqBlock + (int64_t)threadIdx.x * kSeqPer;
+    const uint32_t* fb = b.forced ? b.forced + (size_t)c * (b.nmax / 32 + 1) : nullptr;
+#pragma unroll
+    for (int i = 0; i < kSeqPer; ++i) {
+        const int64_t k = k0 + i;
+        ev[i] = false;
+        inc[i] = 0;
+        if (k == 0 || k >= n) continue;
+        const int ep = i == 0 ? in.ep : in.e[i - 1];
+        ev[i] = seq_event(in.x[i], in.e[i], ep, floor_e, forced_bit(fb, k), noinc, inc[i]);
+    }
+}
+
+template <class Src>
+__global__ void __launch_bounds__(kSeqThreads) seq_bsum(Src src, SeqSumBuf b, const uint32_t* d_n) {
+    __shared__ double s_wd[kSeqThreads / 64];
+    __shared__ double s_abs[kSeqThreads / 64];
+    const int c = blockIdx.y;
+    const int64_t n = *d_n;
+    if ((int64_t)blockIdx.x * kSeqBlock >= n) return;  // block-uniform
+    float x[kSeqPer];
+    load_x(src, c, (int64_t)blockIdx.x * kSeqBlock + (int64_t)threadIdx.x * kSeqPer, n, x);
+    double D[kSeqPer], tot;
+    block_dprefix(x, D, s_wd, tot);
+    double a = 0.0;
+#pragma unroll
+    for (int i = 0; i < kSeqPer; ++i) a += fabs((double)x[i]);
+    double atot;
+    block_excl(a, s_abs, atot);
+    if (threadIdx.x == 0) {
+        b.bsum[(size_t)c * b.nblk + blockIdx.x] = tot;
+        b.babs[(size_t)c * b.nblk + blockIdx.x] = atot;
+    }
+}
+
+// per chain: boff[j] = boff[j-1] + bsum[j-1] (sequential: the bits every block's prediction relies on),
+// the bound on |s| and the floor binade that keeps every run sum exact in double
+// the block values go through LDS in windows (coalesced loads by all lanes), the dependent chain runs on lane 0
+constexpr int kScanWin = 2048;
+
+__global__ void __launch_bounds__(256) seq_scan1(SeqSumBuf b, const uint32_t* d_n, int pass) {
+    __shared__ double s_sum[kScanWin], s_abs[kScanWin], s_off[kScanWin];
+    const int c = blockIdx.x;
+    const int64_t n = *d_n;
+    const int nb = (int)((n + kSeqBlock - 1) / kSeqBlock);
+    double off = 0.0, mb = 0.0;  // lane 0's running values
+    for (int w0 = 0; w0 < nb; w0 += kScanWin) {
+        const int m = min(kScanWin, nb - w0);
+        for (int j = threadIdx.x; j < m; j += blockDim.x) {
+            s_sum[j] = b.bsum[(size_t)c * b.nblk + w0 + j];
+            s_abs[j] = b.babs[(size_t)c * b.nblk + w0 + j];
+        }
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int j = 0; j < m; ++j) {
+                s_off[j] = off;
+                mb = fmax(mb, fabs(off) + s_abs[j]);
+                off = off + s_sum[j];
+            }
+        __syncthreads();
+        for (int j = threadIdx.x; j < m; j += blockDim.x) b.boff[(size_t)c * b.nblk + w0 + j] = s_off[j];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        // |s_k| < 2^(ilogb(mb) + 2) with a binade of margin for the float chain's own drift; a run's sum
+        // then has <= 53 significant bits when its binades stay >= floor
+        b.floor_e[c] = mb > 0.0 ? ilogb(mb) - 27 : -200;
+        if (c == 0 && pass <= 1) {
+            b.status[0] = 0u;
+            b.status[1] = 0u;
+        }
+    }
+}
+
+template <class Src>
+__global__ void __launch_bounds__(kSeqThreads) seq_count(Src src, SeqSumBuf b, const uint32_t* d_n, int pass) {
+    __shared__ double s_wd[kSeqThreads / 64];
+    __shared__ uint64_t s_u[kSeqThreads / 64];
+    __shared__ int s_i[kSeqThreads / 64];
+    const int c = blockIdx.y;
+    const int64_t n = *d_n;
+    if ((int64_t)blockIdx.x * kSeqBlock >= n) return;
+    ElemInfo in;
+    predict(src, b, c, n, pass, in, s_wd);
+    bool ev[kSeqPer];
+    uint64_t inc[kSeqPer];
+    classify<Src>(b, c, n, in, b.floor_e[c], pass, ev, inc);
+    uint64_t su = 0;
+    int se = 0;
+#pragma unroll
+    for (int i = 0; i < kSeqPer; ++i) {
+        su += inc[i];
+        se += ev[i] ? 1 : 0;
+    }
+    uint64_t tu;
+    int te;
+    block_excl(su, s_u, tu);
+    block_excl(se, s_i, te);
+    if (threadIdx.x == 0) {
+        b.btot[(size_t)c * b.nblk + blockIdx.x] = tu;
+        b.bev[(size_t)c * b.nblk + blockIdx.x] = te;
+    }
+}
+
+// exclusive block offsets of the increments (wrapping) and event counts: integers, any order is exact
+__global__ void __launch_bounds__(kSeqThreads) seq_scan2(SeqSumBuf b, const uint32_t* d_n) {
+    __shared__ uint64_t s_u[kSeqThreads / 64];
+    __shared__ int s_i[kSeqThreads / 64];
+    const int c = blockIdx.x;
+    const int64_t n = *d_n;
+    const int nb = (int)((n + kSeqBlock - 1) / kSeqBlock);
+    uint64_t P = 0;
+    int E = 0;
+    for (int j0 = 0; j0 < nb; j0 += kSeqThreads) {  // block-uniform trip count
+        const int j = j0 + (int)threadIdx.x;
+        const uint64_t u = j < nb ? b.btot[(size_t)c * b.nblk + j] : 0;
+        const int e = j < nb ? b.bev[(size_t)c * b.nblk + j] : 0;
+        uint64_t tu;
+        int te;
+        const uint64_t pu = block_excl(u, s_u, tu);
+        const int pe = block_excl(e, s_i, te);
+        if (j < nb) {
+            b.bPoff[(size_t)c * b.nblk + j] = P + pu;
+            b.bEoff[(size_t)c * b.nblk + j] = E + pe;
+        }
+        P += tu;
+        E += te;
+    }
+    if (threadIdx.x == 0) {
+        b.ptot[c] = P;
+        b.floor_e[b.nch + c] = E;  // events of the chain
+        if (E > b.evcap) atomicOr(&b.status[1], 1u << c);
+    }
+}
+
+// the block's elements with their exclusive increment prefix and inclusive event count
+template <class Src>
+__device__ __forceinline__ void block_scan_elems(const Src& src, const SeqSumBuf& b, int c, int64_t n, int pass,
+                                                 ElemInfo& in, bool (&ev)[kSeqPer], uint64_t (&Pex)[kSeqPer],
+                                                 int (&Ein)[kSeqPer]) {
+    __shared__ double s_wd[kSeqThreads / 64];
+    __shared__ uint64_t s_u[kSeqThreads / 64];
+    __shared__ int s_i[kSeqThreads / 64];
+    predict(src, b, c, n, pass, in, s_wd);
+    uint64_t inc[kSeqPer];
+    classify<Src>(b, c, n, in, b.floor_e[c], pass, ev, inc);
+    uint64_t su = 0;
+    int se = 0;
+#pragma unroll
+    for (int i = 0; i < kSeqPer; ++i) {
+        su += inc[i];
+        se += ev[i] ? 1 : 0;
+    }
+    uint64_t tu;
+    int te;
+    uint64_t pu = block_excl(su, s_u, tu) + b.bPoff[(size_t)c * b.nblk + blockIdx.x];
+    int pe = block_excl(se, s_i, te) + b.bEoff[(size_t)c * b.nblk + blockIdx.x];
+#pragma unroll
+    for (int i = 0; i < kSeqPer; ++i) {
+        Pex[i] = pu;
+        pu += inc[i];
+        pe += ev[i] ? 1 : 0;
+        Ein[i] = pe;
+    }
+}
+
+template <class Src>
+__global__ void __launch_bounds__(kSeqThreads) seq_events(Src src, SeqSumBuf b, const uint32_t* d_n, int pass) {
+    const int c = blockIdx.y;
+    const int64_t n = *d_n;
+    if ((int64_t)blockIdx.x * kSeqBlock >= n) return;
+    ElemInfo in;
+    bool ev[kSeqPer];
+    uint64_t Pex[kSeqPer];
+    int Ein[kSeqPer];
+    block_scan_elems(src, b, c, n, pass, in, ev, Pex, Ein);
+    const int64_t k0 = (int64_t)blockIdx.x * kSeqBlock + (int64_t)threadIdx.x * kSeqPer;
+#pragma unroll
+    for (int i = 0; i < kSeqPer; ++i)
+        if (ev[i]) {
+            const int idx = Ein[i] - 1;
+            if (idx < b.evcap) {
+                b.ev_pos[(size_t)c * b.evcap + idx] = (int)(k0 + i);
+                b.ev_P[(size_t)c * b.evcap + idx] = Pex[i];
+                b.ev_x[(size_t)c * b.evcap + idx] = in.x[i];
+            }
+        }
+}
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+    const uint64_t u = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// one wave per chain: s_{event-1} = s_{previous event} + run sum (exact double), s_event = fl(that + x_event)
+template <class Src>
+__global__ void __launch_bounds__(64) seq_walk(Src src, SeqSumBuf b, const uint32_t* d_n) {
+    const int c = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int64_t n = *d_n;
+    if (n <= 0) {
+        if (lane == 0) b.result[c] = 0.f;
+        return;
+    }
+    if ((b.status[1] >> c) & 1u) return;  // event overflow: the caller falls back
+    const int nev = b.floor_e[b.nch + c];
+    const double unit = ldexp(1.0, b.floor_e[c] - 23);
+    const uint64_t* EP = b.ev_P + (size_t)c * b.evcap;
+    const float* EX = b.ev_x + (size_t)c * b.evcap;
+    float* ES = b.ev_s + (size_t)c * b.evcap;
+    double s = (double)src(c, 0);
+    uint64_t Pbase = 0;
+    for (int base = 0; base < nev; base += 64) {
+        const int i = base + lane;
+        const bool ok = i < nev;
+        const uint64_t P = ok ? EP[i] : 0;
+        const float xv = ok ? EX[i] : 0.f;
+        uint64_t Pp = __shfl_up(P, 1, 64);
+        if (lane == 0) Pp = Pbase;
+        const double R = (double)(int64_t)(P - Pp) * unit;  // a run sum: exact (<= 53 significant bits)
+        const int cnt = min(64, nev - base);
+        float mine = 0.f;
+        for (int l = 0; l < cnt; ++l) {
+            const double r = readlane_d(R, l);
+            const float xl = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), l));
+            const float f = (float)(s + r) + xl;  // s + r is the float s_{event-1}; the event's add rounds once
+            s = (double)f;
+            if (lane == l) mine = f;
+        }
+        if (ok) ES[i] = mine;
+        const uint64_t Pl = __shfl(P, cnt - 1, 64);
+        Pbase = Pl;
+    }
+    if (lane == 0) b.result[c] = (float)(s + (double)(int64_t)(b.ptot[c] - Pbase) * unit);
+}
+
+// s_k for every element from the events; checks s_k == fl(s_{k-1} + x_k); stores the reconstruction
+template <class Src>
+__global__ void __launch_bounds__(kSeqThreads) seq_verify(Src src, SeqSumBuf b, const uint32_t* d_n, int pass) {
+    __shared__ float s_lastv[kSeqThreads / 64];
+    __shared__ uint32_t s_bad;
+    const int c = blockIdx.y;
+    const int64_t n = *d_n;
+    if ((int64_t)blockIdx.x * kSeqBlock >= n) return;
+    if ((b.status[1] >> c) & 1u) return;
+    if (threadIdx.x == 0) s_bad = 0;
+    ElemInfo in;
+    bool ev[kSeqPer];
+    uint64_t Pex[kSeqPer];
+    int Ein[kSeqPer];
+    block_scan_elems(src, b, c, n, pass, in, ev, Pex, Ein);
+    const double unit = ldexp(1.0, b.floor_e[c] - 23);
+    const uint64_t* EP = b.ev_P + (size_t)c * b.evcap;
+    const float* ES = b.ev_s + (size_t)c * b.evcap;
+    const float x0 = src(c, 0);
+    const int64_t k0 = (int64_t)blockIdx.x * kSeqBlock + (int64_t)threadIdx.x * kSeqPer;
+    // s of element k from (inclusive event count E, inclusive increment prefix P, is-event)
+    auto rebuild = [&](bool is_ev, int E, uint64_t Pin) -> float {
+        const int idx = E - 1;
+        if (is_ev) return ES[idx];
+        const float bs = idx >= 0 ? ES[idx] : x0;
+        const uint64_t bp = idx >= 0 ? EP[idx] : 0;
+        return (float)((double)bs + (double)(int64_t)(Pin - bp) * unit);
+    };
+    // inclusive increment prefix = exclusive + the element's own increment (classify is deterministic)
+    float s[kSeqPer];
+    {
+        bool ev2[kSeqPer];
+        uint64_t inc2[kSeqPer];
+        classify<Src>(b, c, n, in, b.floor_e[c], pass, ev2, inc2);
+#pragma unroll
+        for (int i = 0; i < kSeqPer; ++i) {
+            const int64_t k = k0 + i;
+            s[i] = k == 0 ? x0 : (k < n ? rebuild(ev[i], Ein[i], Pex[i] + inc2[i]) : 0.f);
+        }
+    }
+    // predecessor of the thread's first element
+    float prev = __shfl_up(s[kSeqPer - 1], 1, 64);
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    if (lane == 63) s_lastv[w] = s[kSeqPer - 1];
+    __syncthreads();
+    if (lane == 0) {
+        if (w > 0) {
+            prev = s_lastv[w - 1];
+        } else if (k0 > 0) {
+            // the previous block's last element: bEoff / bPoff of this block are its inclusive values; whether
+            // it is an event is read back from the event list (position)
+            const int E = b.bEoff[(size_t)c * b.nblk + blockIdx.x];
+            const uint64_t Pin = b.bPoff[(size_t)c * b.nblk + blockIdx.x];
+            const bool is_ev = E > 0 && b.ev_pos[(size_t)c * b.evcap + (E - 1)] == (int)(k0 - 1);
+            prev = rebuild(is_ev, E, Pin);
+        }
+    }
+    bool bad = false;
+#pragma unroll
+    for (int i = 0; i < kSeqPer; ++i) {
+        const int64_t k = k0 + i;
+        if (k >= n) break;
+        const float sp = i == 0 ? prev : s[i - 1];
+        if (k > 0) {
+            const float want = sp + in.x[i];
+            if (__float_as_uint(want) != __float_as_uint(s[i]) && !(want != want && s[i] != s[i])) {
+                bad = true;
+                uint32_t* fb = b.forced + (size_t)c * (b.nmax / 32 + 1);
+                atomicOr(&fb[k >> 5], 1u << (k & 31));
+            }
+        }
+        b.recon[(size_t)c * b.nmax + k] = s[i];
+    }
+    if (bad) s_bad = 1;
+    __syncthreads();
+    if (threadIdx.x == 0 && s_bad) atomicOr(&b.status[0], 1u << c);
+}
+
+template <class Src>
+void seqsum_launch_impl(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, hipStream_t st) {
+    const dim3 g(b.nblk, nch);
+    if (pass <= 1) {
+        // the forced-event bits of a previous alignment's failures are stale
+        (void)hipMemsetAsync(b.forced, 0, (size_t)nch * (b.nmax / 32 + 1) * sizeof(uint32_t), st);
+        seq_bsum<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n);
+        seq_scan1<<<nch, 256, 0, st>>>(b, d_n, pass);
+    } else {
+        (void)hipMemsetAsync(b.status, 0, 2 * sizeof(uint32_t), st);
+    }
+    seq_count<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
+    seq_scan2<<<nch, kSeqThreads, 0, st>>>(b, d_n);
+    seq_events<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
+    seq_walk<Src><<<nch, 64, 0, st>>>(src, b, d_n);
+    seq_verify<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
+}
+
+}  // namespace
+
+template <class Src>
+void seqsum_launch(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, hipStream_t st) {
+    seqsum_launch_impl(src, nch, d_n, b, pass, st);
+}
+template void seqsum_launch<SeqPairs>(const SeqPairs&, int, const uint32_t*, SeqSumBuf&, int, hipStream_t);
+template void seqsum_launch<SeqSigma>(const SeqSigma&, int, const uint32_t*, SeqSumBuf&, int, hipStream_t);
+
+int seqsum_reserve(SeqSumBuf& b, int nch, int64_t nmax, hipStream_t st) {
+    if (nch > kSeqMaxChains || nch < 1) return -1;
+    nmax = nmax < 1 ? 1 : nmax;
+    if (b.nch >= nch && b.nmax >= nmax) return 0;
+    const int dbg = b.dbg_noinc;
+    seqsum_free(b);
+    b.dbg_noinc = dbg;
+    b.nch = nch;
+    b.nmax = nmax;
+    b.nblk = (int)((nmax + kSeqBlock - 1) / kSeqBlock);
+    b.evcap = b.evcap_alloc = nmax / 4 + 1024;  // events are ~0.3 % of a C4 chain; past a quarter the serial kernel is as fast
+    const size_t nb = (size_t)nch * b.nblk;
+    bool ok = hipMalloc(&b.bsum, nb * sizeof(double)) == hipSuccess && hipMalloc(&b.babs, nb * sizeof(double)) == hipSuccess &&
+              hipMalloc(&b.boff, nb * sizeof(double)) == hipSuccess && hipMalloc(&b.btot, nb * sizeof(uint64_t)) == hipSuccess &&
+              hipMalloc(&b.bev, nb * sizeof(int)) == hipSuccess && hipMalloc(&b.bPoff, nb * sizeof(uint64_t)) == hipSuccess &&
+              hipMalloc(&b.bEoff, nb * sizeof(int)) == hipSuccess && hipMalloc(&b.floor_e, 3 * nch * sizeof(int)) == hipSuccess &&
+              hipMalloc(&b.ptot, nch * sizeof(uint64_t)) == hipSuccess &&
+              hipMalloc(&b.ev_pos, (size_t)nch * b.evcap * sizeof(int)) == hipSuccess &&
+              hipMalloc(&b.ev_P, (size_t)nch * b.evcap * sizeof(uint64_t)) == hipSuccess &&
+              hipMalloc(&b.ev_x, (size_t)nch * b.evcap * sizeof(float)) == hipSuccess &&
+              hipMalloc(&b.ev_s, (size_t)nch * b.evcap * sizeof(float)) == hipSuccess &&
+              hipMalloc(&b.recon, (size_t)nch * nmax * sizeof(float)) == hipSuccess &&
+              hipMalloc(&b.forced, (size_t)nch * (nmax / 32 + 1) * sizeof(uint32_t)) == hipSuccess &&
+              hipMalloc(&b.status, 4 * sizeof(uint32_t)) == hipSuccess && hipMalloc(&b.result, nch * sizeof(float)) == hipSuccess;
+    if (!ok) {
+        seqsum_free(b);
+        return -5;
+    }
+    (void)hipMemsetAsync(b.status, 0, 4 * sizeof(uint32_t), st);
+    return 0;
+}
+
+void seqsum_free(SeqSumBuf& b) {
+    void* ptrs[] = {b.bsum, b.babs, b.boff, b.btot, b.bev, b.bPoff, b.bEoff, b.floor_e, b.ptot, b.ev_pos,
+                    b.ev_P, b.ev_x, b.ev_s, b.recon, b.forced, b.status, b.result};
+    for (void* p : ptrs)
+        if (p) (void)hipFree(p);
+    b = SeqSumBuf{};
+}
+
+}  // namespace lio

@@ -53,17 +53,23 @@ def _xyz(cloud) -> np.ndarray:
     return a.reshape(-1, 3) if a.ndim == 1 else a[:, :3]
 
 
+# float fidelity orders (lio_icp_params.umeyama_float): 0 double statistics, 1 sequential-order
+# restatement, 2 Eigen 3.3 GEMM model (32 KiB L1; the recommended fidelity mode), 3 as 2 with 48 KiB
+FIDELITY_ORDER = 2
+
+
 def icp_params(config: LoopClosureConfig, cell_size: float = 1.0, device: int = 0,
-               umeyama_float: bool = False) -> _capi.IcpParams:
+               umeyama_float: int | bool = 0) -> _capi.IcpParams:
     # setTransformationEpsilon(0.01), setEuclideanFitnessEpsilon(0.01), setMaximumIterations(50)
     return _capi.IcpParams(config.icp_max_corr_dist_, 0.01, 0.01, 50, 0.0, config.icp_score_threshold_,
-                           cell_size, device, 1 if umeyama_float else 0)
+                           cell_size, device, int(umeyama_float))
 
 
 class LoopClosure:
     def __init__(self, config: LoopClosureConfig, cell_size: float = 1.0, device: int = 0,
-                 umeyama_float: bool = False):
-        """umeyama_float: PCL-order fidelity mode (float pcl::umeyama restated; single rank)."""
+                 umeyama_float: int | bool = 0):
+        """umeyama_float: 0 double statistics (shardable); 1..3 a float fidelity order of pcl::umeyama
+        (single rank; True = 1, the sequential-order restatement)."""
         self.config_ = config
         self._p = icp_params(config, cell_size, device, umeyama_float)
         self._h = C.c_void_p()
@@ -91,6 +97,16 @@ class LoopClosure:
 
     def set_timing(self, on: bool):
         check(lib().lio_icp_set_timing(self._h, 1 if on else 0))
+
+    def fidelity_stats(self) -> dict:
+        """float fidelity modes: seqsum verification re-passes, serial fallbacks, events of the last pass
+        (max over chains), passes run — since the handle was created"""
+        out = (C.c_int64 * 4)()
+        check(lib().lio_icp_get_fidelity_stats(self._h, out))
+        return dict(repasses=out[0], serial=out[1], events=out[2], passes=out[3])
+
+    def set_fidelity_debug(self, flags: int = 0, evcap: int = 0):
+        check(lib().lio_icp_set_fidelity_debug(self._h, int(flags), int(evcap)))
 
     def timing(self) -> dict:
         t = _capi.KernelTiming()

@@ -237,10 +237,16 @@ typedef struct lio_icp_params {
     float cell_size;        /* target grid cell [m]; 0 => 1.0                        */
     int device;
     /* 0 (default): the Umeyama statistics in double about a fixed centre (deterministic, shardable).
-     * 1: PCL-order fidelity mode — TransformationEstimationSVD<PointXYZI, PointXYZI, float>'s
-     *    pcl::umeyama restated: float means as sequential sums over the correspondences in source
-     *    order, float sigma (sequential depth sum), float JacobiSVD on the host (single rank only;
-     *    ~1.5 ms per iteration at 500 k points: serial float chains on the GPU).                 */
+     * 1..3: float fidelity modes — TransformationEstimationSVD<PointXYZI, PointXYZI, float>'s
+     *    pcl::umeyama restated in float (single rank only) with the float summation order of a given
+     *    PCL/Eigen build (parity with a real PCL build unpinned: no PCL here):
+     *    1 sequential-order restatement: means and sigma's depth as single sequential chains;
+     *    2 Eigen 3.3 model (32 KiB L1): sequential means, sigma by Eigen's GEMM — depth blocked by
+     *      kc = 680, res += alpha * block sum — the recommended fidelity mode;
+     *    3 as 2 with a 48 KiB L1 (kc = 1016).
+     *    The sequential float chains are evaluated in parallel and verified bit-exact on the GPU
+     *    (lio_seqsum: predicted binades, event replay, full verification; serial kernel fallback).
+     *    Float JacobiSVD on the host.                                                            */
     int umeyama_float;
 } lio_icp_params;
 
@@ -272,11 +278,24 @@ int lio_icp_set_shard(lio_icp* h, int rank, int world, lio_allgather_fn fn, void
  * ceil(records/world)*20 doubles, as lio_allgather_fn delivers them.       */
 int lio_icp_shard_range(int64_t n_source, int rank, int world, int64_t* begin, int64_t* count);
 int lio_icp_combine(const double* recv, int64_t n_source, int world, double* out17);
-/* Host half of the PCL-order fidelity mode (no device needed): sums16 = the float sums the GPU
+/* Host half of the float fidelity modes (no device needed): sums16 = the float sums the GPU
  * returns per pass [sum src xyz(3), sum tgt xyz(3), count (uint32 bits), sigma accumulator (9,
- * row-major target x source)] -> the incremental transform (row-major 4x4 float) through the
- * float JacobiSVD (pcl::umeyama(src, dst, false) [U], Eigen 3.3 Umeyama.h).                  */
+ * row-major target x source): unscaled for order 1] -> the incremental transform (row-major 4x4
+ * float) through the float JacobiSVD (pcl::umeyama(src, dst, false) [U], Eigen 3.3 Umeyama.h).  */
 int lio_icp_umeyama_pcl_float(const float* sums16, float* T16);
+/* As above for summation order `order` (lio_icp_params.umeyama_float 1..3: orders 2 / 3 return sigma
+ * already scaled by 1/n, as Eigen's GEMM leaves it).                                            */
+int lio_icp_umeyama_pcl_float_order(const float* sums16, int order, float* T16);
+/* Diagnostics of the float fidelity modes: out4 = [verification re-passes, serial fallbacks, events of
+ * the last pass (max over chains), passes run] since the handle was created.  Test hook: flags bit 0
+ * makes the first seqsum pass skip its grid-coarsening event rule (verification then fails and the
+ * re-pass path runs); evcap > 0 caps the events per chain (overflow -> the serial fallback).       */
+int lio_icp_get_fidelity_stats(lio_icp* h, int64_t* out4);
+int lio_icp_set_fidelity_debug(lio_icp* h, int flags, int64_t evcap);
+/* Test hook: sequential float sums of 6 interleaved chains (x: n x 6 host floats) on `device` through
+ * the seqsum path — sums6[c] = fl(...fl(x[0][c] + x[1][c]) ... + x[n-1][c]); passes_out = passes used
+ * (-1: the serial kernel was needed).                                                             */
+int lio_seqsum6(int device, const float* x, int64_t n, int flags, float* sums6, int* passes_out);
 /* Device-side exchange (the form to use with RCCL): per pass the statistics kernel writes this rank's
  * records into a DEVICE send buffer, `fn` enqueues the all-gather of n doubles per rank into the
  * device recv buffer (world * n, rank order) ordered on `stream` (RCCL in-stream, or a collective on

@@ -1001,9 +1001,22 @@ struct IcpParams {
     int max_iter;           // 50
     double rot_eps;         // 0 => 1 - trans_eps
     double score_threshold; // 1.5 (config.yaml:16)
-    int umeyama_float = 0;  // 1: pcl::umeyama in float + Eigen JacobiSVD (umeyama_pcl_float) instead of the
-                            //    double statistics — a fidelity study mode, not what the GPU path computes
+    int umeyama_float = 0;  // 0: double statistics (the GPU default); > 0: pcl::umeyama in float + Eigen
+                            //    JacobiSVD (umeyama_pcl_float), the float summation order picked by the
+                            //    code (UmeyamaOrder below) — PCL's own order depends on its Eigen build
 };
+
+// Float summation orders of pcl::umeyama (IcpParams::umeyama_float > 0).  Eigen-plausible variants of the
+// same arithmetic; their spread at C4 bounds how far "PCL's float result" is defined at all.
+//   1 kSeqSeq       means: sequential row sums; sigma: one sequential depth sum, scaled once at the end
+//   2 kSeqGemm32    means: sequential; sigma: Eigen 3.3 GEMM, depth blocked by kc from a 32 KiB L1
+//                   (res += alpha * block sum per kc block; SSE2 float gebp, mr = 8, nr = 4 => kc = 680)
+//   3 kSeqGemm48    as 2 with a 48 KiB L1 (kc = 1016)
+//   4 kPacketSeq    means: Eigen's vectorised redux (two 4-float packet accumulators, predux, scalar tail),
+//                   which Eigen applies only to contiguous rows — NOT to the strided rows of a col-major
+//                   3 x N matrix; kept as a deliberately different order; sigma sequential
+//   5 kPacketGemm32 means as 4, sigma as 2
+enum UmeyamaOrder { kSeqSeq = 1, kSeqGemm32 = 2, kSeqGemm48 = 3, kPacketSeq = 4, kPacketGemm32 = 5 };
 
 static inline void xform_pt(const float T[16], const float* p, float* o) {
     // T row-major 4x4
@@ -1108,10 +1121,12 @@ static void umeyama(const double* st, const double c0[3], double Rout[9], double
 //   one_over_n = 1 / n; src_mean = src.rowwise().sum() * one_over_n (likewise dst);
 //   demean; sigma = one_over_n * dst_demean * src_demean^T; JacobiSVD(sigma, FullU | FullV);
 //   S = I, S(2) = -1 if det(U) det(V) < 0; R = U S V^T; t = dst_mean - R src_mean.
-// Restated in float: the row sums are sequential (Eigen 3.3's partial redux over a strided row is
-// not vectorised); sigma's depth sum is sequential too — Eigen's GEMM blocks the depth by an
-// L1-size-dependent kc and adds alpha * (block sum) per block, which this does NOT model, so the
-// last bits of sigma can differ from a given PCL build.  JacobiSVD (Eigen 3.3 JacobiSVD::compute,
+// Restated in float.  The summation order is a build property of PCL's Eigen, so it is a parameter
+// (UmeyamaOrder): the row sums are sequential in Eigen 3.3 (its partial redux over a strided row is not
+// vectorised; order 4/5 models the vectorised redux of a contiguous row as a deliberately different
+// order); sigma's depth sum is one sequential chain (order 1) or, as Eigen 3.3's GEMM evaluates a
+// 3 x N by N x 3 product past 13 columns, blocked by an L1-size-dependent kc with res += alpha * (block
+// sum) per block (orders 2/3/5, eigen_gemm_kc).  JacobiSVD (Eigen 3.3 JacobiSVD::compute,
 // real_2x2_jacobi_svd, JacobiRotation::makeJacobi, apply_rotation_in_the_plane) is restated exactly.
 // Small fixed products (R = U S V^T, R * src_mean) sum their 3 terms as e0 + (e1 + e2).
 // ---------------------------------------------------------------------------
@@ -1227,31 +1242,104 @@ static float det3f_colmajor(const float* M) {  // Eigen determinant_impl<3>: bru
     return h(0, 1, 2) - h(1, 0, 2) + h(2, 0, 1);
 }
 
-// src / tgt: the correspondence pairs in correspondence (source index) order, xyz interleaved
-static void umeyama_pcl_float(const std::vector<float>& src, const std::vector<float>& tgt, float Ti[16]) {
+// Eigen 3.3 evaluateProductBlockingSizesHeuristic (GeneralBlockPanelKernel.h), one thread: the depth
+// block kc of a 3 x k by k x 3 float GEMM on an SSE2 build (no FMA: gebp_traits<float, float> mr = 8,
+// nr = 4; KcFactor 1) whose L1 data cache holds l1 bytes.  Problems below 48 are not blocked.
+int64_t eigen_gemm_kc(int64_t k, int64_t l1) {
+    const int64_t mr = 8, nr = 4, k_peeling = 8;
+    const int64_t k_div = mr * 4 + nr * 4, k_sub = mr * nr * 4;
+    if (std::max<int64_t>(k, 3) < 48) return k;
+    const int64_t max_kc = std::max<int64_t>(((l1 - k_sub) / k_div) & ~(k_peeling - 1), 1);
+    if (k > max_kc)
+        k = (k % max_kc) == 0 ? max_kc
+                              : max_kc - k_peeling * ((max_kc - 1 - (k % max_kc)) / (k_peeling * (k / max_kc + 1)));
+    return k;
+}
+
+// A row sum of pcl::umeyama: sequential from the first coefficient (Eigen redux, DefaultTraversal) or,
+// packet4, Eigen's LinearVectorizedTraversal (packets p0 / p1 alternating over 8-float strides, p0 += p1,
+// one more packet if it fits, predux = (p0[0] + p0[2]) + (p0[1] + p0[3]), then the scalar tail).
+static float row_sum(const std::vector<float>& v, int d, int64_t n, bool packet4) {
+    auto x = [&](int64_t i) { return v[3 * i + d]; };
+    if (!packet4 || n < 4) {
+        float a = x(0);
+        for (int64_t i = 1; i < n; ++i) a += x(i);
+        return a;
+    }
+    const int64_t end2 = (n / 8) * 8, end1 = (n / 4) * 4;
+    float p0[4], p1[4];
+    for (int l = 0; l < 4; ++l) p0[l] = x(l);
+    if (end1 > 4) {
+        for (int l = 0; l < 4; ++l) p1[l] = x(4 + l);
+        for (int64_t i = 8; i < end2; i += 8)
+            for (int l = 0; l < 4; ++l) {
+                p0[l] += x(i + l);
+                p1[l] += x(i + 4 + l);
+            }
+        for (int l = 0; l < 4; ++l) p0[l] += p1[l];
+        if (end1 > end2)
+            for (int l = 0; l < 4; ++l) p0[l] += x(end2 + l);
+    }
+    float a = (p0[0] + p0[2]) + (p0[1] + p0[3]);
+    for (int64_t i = end1; i < n; ++i) a += x(i);
+    return a;
+}
+
+// src / tgt: the correspondence pairs in correspondence (source index) order, xyz interleaved;
+// order: UmeyamaOrder (summation order of the means and of sigma's depth)
+void umeyama_pcl_float(const std::vector<float>& src, const std::vector<float>& tgt, float Ti[16], int order,
+                       float* stats15 = nullptr) {
     const int64_t n = (int64_t)(src.size() / 3);
     const float one_over_n = 1.f / (float)n;
+    const bool packet = order == kPacketSeq || order == kPacketGemm32;
     float sm[3], dm[3];
     for (int d = 0; d < 3; ++d) {
-        float a = src[d], b = tgt[d];
-        for (int64_t i = 1; i < n; ++i) {
-            a += src[3 * i + d];
-            b += tgt[3 * i + d];
-        }
-        sm[d] = a * one_over_n;
-        dm[d] = b * one_over_n;
-    }
-    float acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // sum_k dst_demean(r, k) src_demean(c, k), row-major r, c
-    for (int64_t i = 0; i < n; ++i) {
-        const float s0 = src[3 * i] - sm[0], s1 = src[3 * i + 1] - sm[1], s2 = src[3 * i + 2] - sm[2];
-        const float d0 = tgt[3 * i] - dm[0], d1 = tgt[3 * i + 1] - dm[1], d2 = tgt[3 * i + 2] - dm[2];
-        const float sv[3] = {s0, s1, s2}, dv[3] = {d0, d1, d2};
-        for (int r = 0; r < 3; ++r)
-            for (int c = 0; c < 3; ++c) acc[3 * r + c] += dv[r] * sv[c];
+        sm[d] = row_sum(src, d, n, packet) * one_over_n;
+        dm[d] = row_sum(tgt, d, n, packet) * one_over_n;
     }
     float sigma[9];  // column-major
-    for (int r = 0; r < 3; ++r)
-        for (int c = 0; c < 3; ++c) sigma[3 * c + r] = one_over_n * acc[3 * r + c];
+    auto prod = [&](int64_t i, int r, int c) {  // dst_demean(r, i) * src_demean(c, i), both demeaned in float
+        return (tgt[3 * i + r] - dm[r]) * (src[3 * i + c] - sm[c]);
+    };
+    const int64_t l1 = (order == kSeqGemm48) ? 48 * 1024 : 32 * 1024;
+    if (order == kSeqGemm32 || order == kSeqGemm48 || order == kPacketGemm32) {
+        if (n + 3 + 3 < 20) {
+            // generic_product_impl::evalTo: rhs.rows() + dst.rows() + dst.cols() < 20 => the lazy
+            // coefficient-based product, (alpha * dst_demean).row(r) . src_demean.row(c), sequential
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) {
+                    float a = (one_over_n * (tgt[r] - dm[r])) * (src[c] - sm[c]);
+                    for (int64_t i = 1; i < n; ++i) a += (one_over_n * (tgt[3 * i + r] - dm[r])) * (src[3 * i + c] - sm[c]);
+                    sigma[3 * c + r] = a;
+                }
+        } else {
+            // dst.setZero(); gemm: for each depth block, gebp's 1 x 1 remainder path (3 rows < LhsProgress 4,
+            // 3 cols < nr 4): C0 = sequential sum of the block's products; res(r, c) += alpha * C0
+            const int64_t kc = eigen_gemm_kc(n, l1);
+            for (int i = 0; i < 9; ++i) sigma[i] = 0.f;
+            for (int64_t k2 = 0; k2 < n; k2 += kc) {
+                const int64_t k3 = std::min(n, k2 + kc);
+                for (int r = 0; r < 3; ++r)
+                    for (int c = 0; c < 3; ++c) {
+                        float C0 = 0.f;
+                        for (int64_t i = k2; i < k3; ++i) C0 += prod(i, r, c);
+                        sigma[3 * c + r] += one_over_n * C0;
+                    }
+            }
+        }
+    } else {
+        float acc[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0};  // sum_k dst_demean(r, k) src_demean(c, k), row-major r, c
+        for (int64_t i = 0; i < n; ++i)
+            for (int r = 0; r < 3; ++r)
+                for (int c = 0; c < 3; ++c) acc[3 * r + c] += prod(i, r, c);
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) sigma[3 * c + r] = one_over_n * acc[3 * r + c];
+    }
+    if (stats15) {  // src mean, tgt mean, sigma row-major
+        for (int d = 0; d < 3; ++d) stats15[d] = sm[d], stats15[3 + d] = dm[d];
+        for (int r = 0; r < 3; ++r)
+            for (int c = 0; c < 3; ++c) stats15[6 + 3 * r + c] = sigma[3 * c + r];
+    }
     float U[9], V[9], svals[3];
     jacobi_svd3f(sigma, U, V, svals);
     float S[3] = {1.f, 1.f, 1.f};
@@ -1345,7 +1433,7 @@ int icp_align(const float* src, int64_t ns, const float* dst, int64_t nd, const 
                 ps.insert(ps.end(), &cur[3 * i], &cur[3 * i] + 3);
                 qs.insert(qs.end(), dst + 3 * (size_t)nn[i], dst + 3 * (size_t)nn[i] + 3);
             }
-            umeyama_pcl_float(ps, qs, Ti);
+            umeyama_pcl_float(ps, qs, Ti, ip.umeyama_float);
         } else {
             double Rd[9], td[3];
             umeyama(st, c0, Rd, td);
@@ -1806,7 +1894,17 @@ static inline double kcos_fixed(double x) {
     const double hz = 0.5 * z - qx, a = 1.0 - qx;
     return a - (hz - z * r);
 }
+// Measurement switch (orc_set_sincos_libm): UndistortPcl's Exp through the host libm std::sin / std::cos,
+// as the reference's build calls them, instead of the pinned routine — to count how many undistorted
+// points the choice changes.  Off by default; the GPU path evaluates sincos_fixed.
+static bool g_sincos_libm = false;
+
 void sincos_fixed(double x, double* s, double* c) {
+    if (g_sincos_libm) {
+        *s = std::sin(x);
+        *c = std::cos(x);
+        return;
+    }
     const double invpio2 = 6.36619772367581382433e-01, pio2_1 = 1.57079632673412561417e+00,
                  pio2_2 = 6.07710050630396597660e-11, pio2_3 = 2.02226624871116645580e-21;
     int n = 0;
@@ -1939,7 +2037,25 @@ struct orc_icp_params {
     int umeyama_float;  // 1: float pcl::umeyama + JacobiSVD restatement (fidelity study)
 };
 
-int orc_version(void) { return 3; }
+int orc_version(void) { return 4; }
+
+// UndistortPcl through libm sin / cos (1) or the pinned sincos_fixed (0, default); returns the old value
+int orc_set_sincos_libm(int on) {
+    const int old = orc::g_sincos_libm ? 1 : 0;
+    orc::g_sincos_libm = on != 0;
+    return old;
+}
+
+// pcl::umeyama in float over n correspondence pairs (xyz interleaved) in summation order `order`
+// (UmeyamaOrder 1..5) -> the row-major 4x4 incremental transform
+int orc_umeyama_float(const float* src, const float* tgt, int64_t n, int order, float* T16, float* stats15) {
+    if (n < 1 || order < 1 || order > 5) return -1;
+    std::vector<float> s(src, src + 3 * n), t(tgt, tgt + 3 * n);
+    orc::umeyama_pcl_float(s, t, T16, order, stats15);
+    return 0;
+}
+
+int64_t orc_eigen_gemm_kc(int64_t k, int64_t l1) { return orc::eigen_gemm_kc(k, l1); }
 
 // ---- filters ----
 int64_t orc_voxel_grid(const float* p, int64_t n, int stride, const float* leaf3, float* out) {

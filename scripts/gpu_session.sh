@@ -45,6 +45,13 @@ for s in $STEPS; do
            run knn_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/knnprof" -o run --output-format csv -- python scripts/knn_timing.py C2 ;;
     quick) run bench_quick 400 python bench.py --steps 60 --warmup 5 --icp-reps 2 --cpu-scans 10 --cpu-warmup 2 ;;
     driver) run bench_driver 600 python bench.py --gpus 1 --steps 20 --warmup 5 ;;
+    driverq) run bench_driverq1 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu --pipeline 0 --streams '' --no-icp &&
+             run bench_driverq2 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu --pipeline 0 --streams '' --no-icp &&
+             run bench_driverq3 300 python bench.py --gpus 1 --steps 50 --warmup 5 --no-cpu --pipeline 0 --streams '' --no-icp ;;
+    micro) run graph_cost 120 scripts/micro/graph_cost ;;
+    fid)   runs pytest_fid 900 python -u -m pytest tests/test_gpu_seqsum.py tests/test_gpu_icp.py -k "seqsum or fidelity or double" -x -v -s -p no:cacheprovider --timeout 300 --timeout-method thread &&
+           run icp_fid_time 300 env LIO_ICP_ORDER=2 python scripts/icp_ab.py 1.0 5 &&
+           run icp_fid_time1 300 env LIO_ICP_ORDER=1 python scripts/icp_ab.py 1.0 3 ;;
     c3)    run bench_c3 600 python bench.py --config C3 --steps 60 --warmup 5 --no-icp --cpu-scans 10 --cpu-warmup 2 --pipeline 12 ;;
     c2)    run bench_c2 600 python bench.py --config C2 --steps 200 --warmup 20 --no-icp --cpu-scans 20 --cpu-warmup 2 --streams '' ;;
     c5)    run bench_c5 600 python bench.py --config C5 --steps 200 --warmup 20 --no-icp --cpu-scans 10 --cpu-warmup 2 --pipeline 12 --streams '' ;;

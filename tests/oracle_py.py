@@ -37,6 +37,12 @@ class IcpParams(C.Structure):
                 ("umeyama_float", C.c_int)]
 
 
+# pcl::umeyama float summation orders (lio_oracle.cpp UmeyamaOrder); 0 = double statistics
+UMEYAMA_ORDERS = {1: "sequential means, sequential sigma", 2: "sequential means, Eigen GEMM sigma kc(32 KiB L1)",
+                  3: "sequential means, Eigen GEMM sigma kc(48 KiB L1)", 4: "packet-4 means, sequential sigma",
+                  5: "packet-4 means, Eigen GEMM sigma kc(32 KiB L1)"}
+
+
 def default_match_params():
     return MatchParams(5.0, 0.1, 0.9, 0.9)
 
@@ -57,6 +63,29 @@ def sincos(a):
     c = np.empty_like(a)
     lib().orc_sincos(_p(a, C.c_double), len(a), _p(s, C.c_double), _p(c, C.c_double))
     return s, c
+
+
+def set_sincos_libm(on: bool) -> bool:
+    """UndistortPcl's Exp through libm sin / cos (measurement switch); returns the previous setting"""
+    return bool(lib().orc_set_sincos_libm(1 if on else 0))
+
+
+def umeyama_float(src, tgt, order, stats=False):
+    """pcl::umeyama(src, tgt, false) in float, correspondence pairs in order, summation order `order`;
+    stats: also (src mean, tgt mean, sigma 3x3) as float32"""
+    src = np.ascontiguousarray(src, dtype=np.float32)
+    tgt = np.ascontiguousarray(tgt, dtype=np.float32)
+    T = np.zeros(16, np.float32)
+    st = np.zeros(15, np.float32)
+    assert lib().orc_umeyama_float(_p(src, C.c_float), _p(tgt, C.c_float), len(src), int(order), _p(T, C.c_float),
+                                   _p(st, C.c_float)) == 0
+    if stats:
+        return T.reshape(4, 4), st[0:3], st[3:6], st[6:15].reshape(3, 3)
+    return T.reshape(4, 4)
+
+
+def eigen_gemm_kc(k, l1):
+    return int(lib().orc_eigen_gemm_kc(int(k), int(l1)))
 
 
 def build():
@@ -114,6 +143,11 @@ def lib():
         L.orc_submap_voxelize.restype = i64
         L.orc_submap_voxelize.argtypes = [C.POINTER(C.c_float), C.POINTER(C.c_int64), C.c_int, C.c_int,
                                           C.POINTER(C.c_double), C.c_float, C.POINTER(C.c_float)]
+        L.orc_set_sincos_libm.argtypes = [C.c_int]
+        L.orc_umeyama_float.argtypes = [C.POINTER(C.c_float), C.POINTER(C.c_float), i64, C.c_int,
+                                        C.POINTER(C.c_float), C.POINTER(C.c_float)]
+        L.orc_eigen_gemm_kc.restype = i64
+        L.orc_eigen_gemm_kc.argtypes = [i64, i64]
         L.orc_preprocess.restype = i64
         L.orc_preprocess.argtypes = [C.POINTER(C.c_float), i64, C.c_int, C.c_int, C.c_float, C.c_float, C.c_int,
                                      C.POINTER(C.c_double), C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_float)]

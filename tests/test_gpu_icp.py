@@ -165,49 +165,80 @@ def test_icp_group_rccl_bit_identical():
     np.testing.assert_array_equal(np.array(list(rg.T)), np.array(list(r1.T)))
 
 
-def _float_params(oracle):
+def _float_params(oracle, order=1):
     p = oracle.default_icp_params()
-    p.umeyama_float = 1
+    p.umeyama_float = order
     return p
 
 
-@pytest.mark.parametrize("n,disp", [(30_000, (1.0, 3.0)), (500_000, (0.3, 1.5)), (500_000, (2.5, 4.0))])
-def test_icp_pcl_float_mode_matches_oracle_float(oracle, n, disp):
-    """umeyama_float (PCL-order fidelity mode): pcl::umeyama's float means / sigma as sequential sums in
-    correspondence order + float JacobiSVD, on the GPU path and in the restatement — transform within
-    1e-5 (bit-exact in practice: same sums in the same order), iterations / state identical.  At 500 k
-    (BASELINE configs[3], pairs A and B) this is the reference's float arithmetic at full size."""
+_FID_CASES = [(30_000, (1.0, 3.0)), (500_000, (0.3, 1.5)), (500_000, (2.5, 4.0))]
+
+
+@pytest.mark.parametrize("order", [1, 2, 3])
+@pytest.mark.parametrize("n,disp", _FID_CASES)
+def test_icp_float_fidelity_matches_oracle(oracle, n, disp, order):
+    """Float fidelity orders (lio_icp_params.umeyama_float; oracle UmeyamaOrder): pcl::umeyama's float means
+    and sigma in the order of a given Eigen build — 1 sequential, 2 / 3 Eigen 3.3 GEMM blocking (32 / 48 KiB
+    L1) — with the sequential float chains computed in parallel by seqsum (verified on the device) and
+    the float JacobiSVD on the host: the transform bit-identical to the restatement (<= 1e-5 asserted),
+    iterations / state identical, no serial fallback.  At 500 k (BASELINE configs[3], pairs A and B) this is
+    the reference's float arithmetic at full size."""
     src, dst, _ = synth.make_icp_pair(n_points=n, seed=4321 if n > 100_000 else 12, disp=disp)
-    lc = LC.LoopClosure(LC.LoopClosureConfig(), umeyama_float=True)
+    lc = LC.LoopClosure(LC.LoopClosureConfig(), umeyama_float=order)
     lc.setInputSource(src)
     lc.setInputTarget(dst)
     r = lc.align(keep_aligned=False)
-    o = oracle.icp_align(src, dst, params=_float_params(oracle))
+    o = oracle.icp_align(src, dst, params=_float_params(oracle, order))
     T = np.array(list(r.T), np.float32).reshape(4, 4)
-    print(f"n={n} disp={disp}: iters {r.iterations} |dT|max {np.abs(T - o['T']).max():.3g} "
-          f"bit-exact {np.array_equal(T, o['T'])}")
+    fs = lc.fidelity_stats()
+    print(f"order {order} n={n} disp={disp}: iters {r.iterations} |dT|max {np.abs(T - o['T']).max():.3g} "
+          f"bit-exact {np.array_equal(T, o['T'])} {fs}")
     assert r.iterations == o["iterations"] and r.state == o["state"]
     np.testing.assert_allclose(T, o["T"], atol=1e-5)
     np.testing.assert_allclose(r.score, o["fitness"], rtol=1e-5)
+    assert fs["serial"] == 0 and fs["passes"] >= r.iterations
+
+
+def test_icp_fidelity_recovery_paths(oracle):
+    """The seqsum re-pass (a first pass that skips the grid-coarsening rule: verification fails, pass 2
+    repairs) and the serial fallback (event lists capped at 8) give the same transform bits as the normal
+    path."""
+    src, dst, _ = synth.make_icp_pair(n_points=60_000, seed=12, disp=(1.0, 3.0))
+    out = {}
+    for name, flags, evcap in (("normal", 0, 0), ("repass", 1, 0), ("serial", 0, 8)):
+        lc = LC.LoopClosure(LC.LoopClosureConfig(), umeyama_float=2)
+        lc.set_fidelity_debug(flags, evcap)
+        lc.setInputSource(src)
+        lc.setInputTarget(dst)
+        r = lc.align(keep_aligned=False)
+        out[name] = (np.array(list(r.T), np.float32), r.iterations, lc.fidelity_stats())
+    assert out["repass"][2]["repasses"] > 0 and out["repass"][2]["serial"] == 0
+    assert out["serial"][2]["serial"] > 0
+    for k in ("repass", "serial"):
+        np.testing.assert_array_equal(out[k][0], out["normal"][0])
+        assert out[k][1] == out["normal"][1]
 
 
 @pytest.mark.parametrize("disp", [(0.3, 1.5), (2.5, 4.0)])
-def test_icp_double_statistics_vs_pcl_float_at_c4(oracle, disp):
-    """The default mode (double statistics about a fixed centre, shardable) against the restated
-    PCL float arithmetic at C4 (500 k vs 500 k): the gap is PCL's own float-summation noise; bound
-    recorded in DESIGN.md §2 and asserted here."""
+def test_icp_double_statistics_vs_pcl_float_orders_at_c4(oracle, disp):
+    """The default mode (double statistics about a fixed centre, shardable) against the restated PCL float
+    arithmetic at C4 (500 k vs 500 k).  The Eigen 3.3 float orders agree with each other to 3.2e-6 (pair A)
+    / 3.8e-5 (pair B) (tests/test_oracle.py, scripts/umeyama_spread.py); the double statistics sit
+    1.86e-4 / 1.2e-4 from them — outside the 1e-5 bar, which is why the timed loop ICP is fidelity order 2
+    (DESIGN §2).  Asserted: same iterations and state, the recorded bound."""
     src, dst, _ = synth.make_icp_pair(n_points=500_000, seed=4321, disp=disp)
     lc = LC.LoopClosure(LC.LoopClosureConfig())
     lc.setInputSource(src)
     lc.setInputTarget(dst)
     r = lc.align(keep_aligned=False)
-    o = oracle.icp_align(src, dst, params=_float_params(oracle))
     T = np.array(list(r.T), np.float32).reshape(4, 4)
-    gap = float(np.abs(T - o["T"]).max())
-    print(f"C4 disp={disp}: double-mode vs PCL-float |dT|max {gap:.3g} (rot {np.abs(T[:3, :3] - o['T'][:3, :3]).max():.3g}, "
-          f"trans {np.abs(T[:3, 3] - o['T'][:3, 3]).max():.3g}), iters {r.iterations} vs {o['iterations']}")
-    assert r.iterations == o["iterations"] and r.state == o["state"]
-    assert gap < 1e-3
+    for order in (1, 2, 3):
+        o = oracle.icp_align(src, dst, params=_float_params(oracle, order))
+        gap = float(np.abs(T - o["T"]).max())
+        print(f"C4 disp={disp}: double-mode vs float order {order} |dT|max {gap:.3g} "
+              f"(rot {np.abs(T[:3, :3] - o['T'][:3, :3]).max():.3g}, trans {np.abs(T[:3, 3] - o['T'][:3, 3]).max():.3g})")
+        assert r.iterations == o["iterations"] and r.state == o["state"]
+        assert gap < 1e-3
 
 
 @pytest.mark.parametrize("world", [2, 3])

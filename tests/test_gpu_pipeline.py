@@ -57,6 +57,13 @@ def test_c5_stream_with_loop_closure(oracle):
         kh = gs.keyframe_host(xg, t, k)
         np.testing.assert_array_equal(gs.keyframes[-1].pcd_, kh.pcd_)
         np.testing.assert_array_equal(gs.keyframes[-1].pose_eig_, kh.pose_eig_)
+        if k == 0:  # a matrix-only pose (no quaternions): q / q_LI derived from R / R_LI, same cloud
+            Tk = PL.odom_matrix(xg)
+            p_mat = F.pose_from_pose24(np.asarray(synth.pose24(xg), np.float64)[:24])
+            assert not any(p_mat.q) and not any(p_mat.q_LI)
+            # (the derived quaternion may differ from the state's in its last bits: float-store tolerance)
+            np.testing.assert_allclose(gs.hm.keyframe_cloud(p_mat, np.linalg.inv(Tk)), gs.keyframes[-1].pcd_,
+                                       rtol=0, atol=1e-4)
         assert sg["h_evals"] == int(so[0]) and sg["knn_calls"] == int(so[1]) and sg["n_eff"] == int(so[3])
         np.testing.assert_allclose(xg["pos"], xo["pos"], atol=1e-5)
         np.testing.assert_allclose(xg["rot"], xo["rot"], atol=1e-5)
