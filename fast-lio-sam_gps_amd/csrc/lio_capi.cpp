@@ -482,6 +482,13 @@ int lio_map_get_grid(lio_map* m, double* out7) {
     return LIO_OK;
 }
 
+int lio_map_set_test_limits(lio_map* m, int64_t slot_headroom, int64_t dirty_cells) {
+    if (!m || slot_headroom < 0 || dirty_cells < 0) return fail(LIO_ERR_ARG, "lio_map_set_test_limits: bad arguments");
+    m->grid.slots_extra = slot_headroom;
+    m->upd.dcap_limit = dirty_cells;
+    return LIO_OK;
+}
+
 int lio_map_get_stats(lio_map* m, int64_t* out8) {
     if (!m || !out8) return fail(LIO_ERR_ARG, "bad arguments");
     HIP_TRY(hipSetDevice(m->dev));

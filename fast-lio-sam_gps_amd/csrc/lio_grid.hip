@@ -496,8 +496,9 @@ void grid_insert_finish(GridBuf& g, int64_t id0, const uint32_t* d_nnew, int n_m
                         uint32_t* flags, hipStream_t st) {
     if (n_max <= 0) return;
     const int nb = (n_max + 255) / 256;
+    const int64_t usable = g.slots_extra > 0 ? std::min<int64_t>(g.slots_cap, g.slots_used + g.slots_extra) : g.slots_cap;
     insert_alloc_kernel<<<nb, 256, 0, st>>>(g.pts, g.rng, g.lim, g.addc, s.tlist, s.d_ntouch, g.bump,
-                                            (uint32_t)std::min<int64_t>(g.slots_cap, 0xffffffffll), flags);
+                                            (uint32_t)std::min<int64_t>(usable, 0xffffffffll), flags);
     insert_write_kernel<<<nb, 256, 0, st>>>(g.by_id, id0, d_nnew, s.tmp_cell, s.tmp_rank, g.addc, g.pts);
     insert_clear_kernel<<<nb, 256, 0, st>>>(g.addc, s.tlist, s.d_ntouch);
 }

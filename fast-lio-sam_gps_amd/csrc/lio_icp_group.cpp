@@ -33,6 +33,7 @@
 
 #include "../../include/lio_gpu.h"
 #include "lio_error.hpp"
+#include "lio_rccl.hpp"
 
 namespace {
 
@@ -41,47 +42,10 @@ int gfail(int code, const std::string& msg) {
     return code;
 }
 
-// ---- the few RCCL entry points used, resolved from librccl at run time (rccl.h ABI)
-typedef struct ncclComm* ncclComm_t;
-typedef int ncclResult_t;  // ncclSuccess = 0
-constexpr int kNcclDouble = 8;  // ncclFloat64
-struct Rccl {
-    void* so = nullptr;
-    ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
-    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
-    ncclResult_t (*CommAbort)(ncclComm_t) = nullptr;
-    ncclResult_t (*AllGather)(const void*, void*, size_t, int, ncclComm_t, hipStream_t) = nullptr;
-    ncclResult_t (*GroupStart)() = nullptr;
-    ncclResult_t (*GroupEnd)() = nullptr;
-    const char* (*GetErrorString)(ncclResult_t) = nullptr;
-};
-
-bool load_rccl(Rccl& r, std::string& why) {
-    const char* env = std::getenv("LIO_RCCL_LIB");
-    const char* names[] = {env, "librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
-    for (const char* n : names) {
-        if (!n) continue;
-        r.so = dlopen(n, RTLD_NOW | RTLD_GLOBAL);
-        if (r.so) break;
-    }
-    if (!r.so) {
-        why = "librccl not found (set LIO_RCCL_LIB or LIO_ICP_EXCHANGE=host)";
-        return false;
-    }
-    r.CommInitAll = (decltype(r.CommInitAll))dlsym(r.so, "ncclCommInitAll");
-    r.CommDestroy = (decltype(r.CommDestroy))dlsym(r.so, "ncclCommDestroy");
-    r.CommAbort = (decltype(r.CommAbort))dlsym(r.so, "ncclCommAbort");
-    r.AllGather = (decltype(r.AllGather))dlsym(r.so, "ncclAllGather");
-    r.GroupStart = (decltype(r.GroupStart))dlsym(r.so, "ncclGroupStart");
-    r.GroupEnd = (decltype(r.GroupEnd))dlsym(r.so, "ncclGroupEnd");
-    r.GetErrorString = (decltype(r.GetErrorString))dlsym(r.so, "ncclGetErrorString");
-    if (!r.CommInitAll || !r.CommDestroy || !r.CommAbort || !r.AllGather || !r.GroupStart || !r.GroupEnd ||
-        !r.GetErrorString) {
-        why = "librccl lacks ncclCommInitAll / ncclAllGather";
-        return false;
-    }
-    return true;
-}
+using lio::kNcclDouble;
+using lio::ncclComm_t;
+using lio::ncclResult_t;
+using lio::Rccl;
 
 }  // namespace
 
@@ -235,7 +199,7 @@ int lio_icp_group_create(const lio_icp_params* p, int n_gpus, const int* devices
     }
     if (rc == LIO_OK && g->use_rccl) {
         std::string why;
-        if (!load_rccl(g->rccl, why)) {
+        if (!lio::load_rccl(g->rccl, why)) {
             rc = gfail(LIO_ERR_STATE, "lio_icp_group_create: " + why);
         } else {
             g->comms.assign(n_gpus, nullptr);

@@ -322,6 +322,8 @@ struct lio_icp {
     lio::PclBuf pcl;           // umeyama_float: compacted pairs + seqsum chains
     float* d_pclout = nullptr; // pcl_pack output (kPclOutWords)
     float* h_pclout = nullptr; // pinned copy
+    void* x_owner = nullptr;   // exchange state owned by the handle (lio_icp_mp.cpp: shm segment, RCCL comm)
+    void (*x_owner_free)(void*) = nullptr;
     int64_t fid_stats[4] = {0, 0, 0, 0};  // re-passes, serial fallbacks, events of the last pass, passes
     int fid_flags = 0;
     int64_t fid_evcap = 0;
@@ -371,10 +373,25 @@ int lio_icp_create(const lio_icp_params* p, lio_icp** out) {
     return LIO_OK;
 }
 
+// internal (lio_icp_mp.cpp): hand the exchange state of a multi-process shard to the handle (freed with it,
+// or when another exchange replaces it)
+void lio_icp_set_exchange_owner(lio_icp* h, void* owner, void (*free_fn)(void*)) {
+    if (h->x_owner && h->x_owner_free) {
+        (void)hipSetDevice(h->dev);
+        (void)hipStreamSynchronize(h->st);
+        h->x_owner_free(h->x_owner);
+    }
+    h->x_owner = owner;
+    h->x_owner_free = free_fn;
+}
+
+int lio_icp_device(const lio_icp* h) { return h->dev; }
+
 int lio_icp_destroy(lio_icp* h) {
     if (!h) return LIO_OK;
     (void)hipSetDevice(h->dev);
     (void)hipStreamSynchronize(h->st);
+    lio_icp_set_exchange_owner(h, nullptr, nullptr);
     lio::grid_free(h->tgt);
     lio::grid_free(h->qgrid);
     void* ptrs[] = {h->d_tgt,   h->d_src,     h->d_cur,  h->d_fd2,   h->d_fid,   h->d_tiles, h->d_tscratch,

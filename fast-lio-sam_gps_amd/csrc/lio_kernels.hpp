@@ -86,6 +86,7 @@ struct GridBuf {
     int64_t slots_cap = 0;       // pts capacity in slots
     int64_t slots_used = 0;      // bump value after the last rebuild (host view; the pool's live share)
     int64_t rebuilds = 0;        // full rebuilds so far (diagnostics: lio_map_get_stats)
+    int64_t slots_extra = 0;     // test hook (lio_map_set_test_limits): usable pool = slots_used + this (0: all)
     // temporaries
     uint32_t* keys = nullptr;
     uint32_t* keys_alt = nullptr;

@@ -1180,6 +1180,12 @@ int exclusive_scan64(MapUpdBuf& u, const unsigned long long* in, unsigned long l
 // The downsampled add of the cnt[kCAdd] points xyz[0 ..) (<= n_max) and the append of the
 // cnt[kCNoNeed] points xyz_nn, then the grid: tombstoned cells compacted, new ids inserted.  All
 // enqueued; cnt[] holds the counts once the stream reaches the end.
+// tombstone cell list capacity (cells per update: <= 27 per offered point; tests may shorten it)
+uint32_t dcap_of(const MapUpdBuf& u) {
+    const int64_t d = u.cap * 27;
+    return (uint32_t)(u.dcap_limit > 0 ? std::min<int64_t>(d, u.dcap_limit) : d);
+}
+
 int enqueue_add(GridBuf& g, MapUpdBuf& u, const float* xyz, int n_max, const float* xyz_nn, float ds, int64_t id0,
                 hipStream_t st) {
     const int nb = (n_max + 255) / 256;
@@ -1195,12 +1201,12 @@ int enqueue_add(GridBuf& g, MapUpdBuf& u, const float* xyz, int n_max, const flo
     }
     vox_runs_kernel<<<nb, 256, 0, st>>>(u.skey2, u.sval2, xyz, n_max, u.hcap - 1, u.hhead, u.hend, u.xs);
     VoxArgs va{u.vlist, u.hkey, u.hhead, u.hend, nullptr, nullptr, u.sval2, u.xs, xyz, ds, grid_view(g), (int)g.n,
-               g.pts, g.by_id, g.dirty, u.dlist, (uint32_t)(u.cap * 27), u.cnt, u.add_flag};
+               g.pts, g.by_id, g.dirty, u.dlist, dcap_of(u), u.cnt, u.add_flag};
     vox_resolve_kernel<false><<<std::min(2048, (n_max + 3) / 4), 256, 0, st>>>(va);
     int rc = exclusive_scan(u, u.add_flag, u.pos, n_max + 1, st);
     if (rc) return rc;
     append_kernel<<<nb, 256, 0, st>>>(xyz, u.add_flag, u.pos, xyz_nn, n_max, id0, g.by_id, u.cnt);
-    grid_compact_cells(g, u.dlist, u.cnt + kCDirty, (uint32_t)(u.cap * 27), n_max * 27, st);
+    grid_compact_cells(g, u.dlist, u.cnt + kCDirty, dcap_of(u), n_max * 27, st);
     GridInsertScratch sc{u.tmp_cell, u.tmp_rank, u.tlist, u.cnt + kCTouch};
     grid_insert_ids(g, id0, u.cnt + kCNew, n_max, sc, u.cnt + kCFlags, st);
     UPD_CHK(hipGetLastError());
@@ -1216,7 +1222,7 @@ int enqueue_grouped(GridBuf& g, MapUpdBuf& u, const float* xyz, const uint8_t* c
                  u.vnruns, u.runs, u.sval2, u.xs, u.vlist, u.add_flag, u.cnt,      u.blk,   u.blk + u.blk_cap};
     const int nblk = (n + kGrpB - 1) / kGrpB;
     group_sort_kernel<<<nblk, kGrpT, 0, st>>>(ga);
-    const uint32_t dcap = (uint32_t)(u.cap * 27);
+    const uint32_t dcap = dcap_of(u);
     VoxArgs va{u.vlist, u.hkey,   u.hhead, nullptr,    u.vnruns, u.runs, u.sval2, u.xs,   xyz,       ds,  grid_view(g),
                (int)g.n, g.pts,   g.by_id, g.dirty,    u.dlist,  dcap,   u.cnt,   u.add_flag, u.blk};
     vox_resolve_kernel<true><<<std::min(2048, (n + 3) / 4), 256, 0, st>>>(va);

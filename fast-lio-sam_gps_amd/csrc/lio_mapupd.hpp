@@ -39,6 +39,7 @@ struct MapUpdBuf {
     uint32_t hcap = 0;
     int hbits = 0;                        // log2(hcap)
     int64_t cap = 0;
+    int64_t dcap_limit = 0;               // test hook (lio_map_set_test_limits): tombstone cell list length (0: cap * 27)
     void* tmp = nullptr;
     size_t tmp_bytes = 0;
     uint32_t* cnt = nullptr;    // per-call counters (lio_mapupd.hip kC*)

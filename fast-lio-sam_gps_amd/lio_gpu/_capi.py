@@ -42,6 +42,8 @@ EXPORTS = [
     "lio_icp_shard_range", "lio_icp_combine", "lio_icp_umeyama_pcl_float", "lio_icp_get_correspondences",
     "lio_ctx_set_timing", "lio_ctx_get_timing", "lio_ctx_reset_timing", "lio_icp_set_timing", "lio_icp_get_timing",
     "lio_icp_umeyama_pcl_float_order", "lio_icp_get_fidelity_stats", "lio_icp_set_fidelity_debug", "lio_seqsum6",
+    "lio_map_set_test_limits", "lio_rccl_unique_id", "lio_icp_set_shard_rccl", "lio_icp_set_shard_shm",
+    "lio_shm_exchange_open", "lio_shm_exchange_allgather", "lio_shm_exchange_close",
 ]
 
 
@@ -150,6 +152,13 @@ def _declare(L):
         "lio_map_get_points": (C.c_int, [vp, fp]),
         "lio_map_get_grid": (C.c_int, [vp, dp]),
         "lio_map_get_stats": (C.c_int, [vp, C.POINTER(C.c_int64)]),
+        "lio_map_set_test_limits": (C.c_int, [vp, C.c_int64, C.c_int64]),
+        "lio_rccl_unique_id": (C.c_int, [C.POINTER(C.c_uint8)]),
+        "lio_icp_set_shard_rccl": (C.c_int, [vp, C.c_int, C.c_int, C.POINTER(C.c_uint8)]),
+        "lio_icp_set_shard_shm": (C.c_int, [vp, C.c_int, C.c_int, C.c_char_p, C.c_int64]),
+        "lio_shm_exchange_open": (C.c_int, [C.c_char_p, C.c_int, C.c_int, C.c_int64, C.POINTER(vp)]),
+        "lio_shm_exchange_allgather": (C.c_int, [vp, dp, C.c_int64, dp]),
+        "lio_shm_exchange_close": (C.c_int, [vp]),
         "lio_map_num_ids": (C.c_int64, [vp]),
         "lio_map_get_by_id": (C.c_int, [vp, fp, C.POINTER(C.c_uint8)]),
         "lio_map_nearest_search": (C.c_int, [vp, fp, C.c_int64, C.c_int, C.c_float, C.POINTER(C.c_int32), fp]),

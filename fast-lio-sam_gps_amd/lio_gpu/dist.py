@@ -128,3 +128,66 @@ class DeviceExchange:
             self.recv = torch.zeros(n * self.world, dtype=torch.float64, device=self.device)
             self.n = n
         check(lib().lio_icp_set_exchange_buffers(handle, self.send.data_ptr(), self.recv.data_ptr(), self.n))
+
+
+# ---------------------------------------------------------------- C++ exchanges (no Python per pass)
+def rccl_unique_id() -> bytes:
+    """ncclGetUniqueId through the library's run-time-loaded librccl (rank 0 only)."""
+    buf = (C.c_uint8 * 128)()
+    check(lib().lio_rccl_unique_id(buf))
+    return bytes(buf)
+
+
+def broadcast_bytes(data: bytes | None, n: int, group=None) -> bytes:
+    """rank 0's n bytes to every rank, once, through torch.distributed (set-up only, never per pass)."""
+    import torch
+    import torch.distributed as dist
+
+    dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else torch.device("cpu")
+    t = torch.zeros(n, dtype=torch.uint8, device=dev)
+    if dist.get_rank(group) == 0:
+        t.copy_(torch.tensor(list(data), dtype=torch.uint8))
+    dist.broadcast(t, src=0, group=group)
+    return bytes(t.cpu().tolist())
+
+
+def attach_rccl(handle, rank: int, world: int, group=None) -> None:
+    """One RCCL communicator per rank created in C++ (lio_icp_set_shard_rccl): the unique id crosses
+    torch.distributed once; every pass's all-gather is then enqueued by the library on the handle's stream."""
+    uid = broadcast_bytes(rccl_unique_id() if rank == 0 else None, 128, group)
+    buf = (C.c_uint8 * 128).from_buffer_copy(uid)
+    check(lib().lio_icp_set_shard_rccl(handle, rank, world, buf))
+
+
+def attach_shm(handle, rank: int, world: int, name: str, max_source_points: int, group=None) -> None:
+    """The shared-memory exchange (lio_icp_set_shard_shm): rank 0 creates the segment, a barrier, the other
+    ranks open it; every pass then exchanges in C++."""
+    import torch.distributed as dist
+
+    if rank == 0:
+        check(lib().lio_icp_set_shard_shm(handle, rank, world, name.encode(), int(max_source_points)))
+    dist.barrier(group)
+    if rank != 0:
+        check(lib().lio_icp_set_shard_shm(handle, rank, world, name.encode(), int(max_source_points)))
+    dist.barrier(group)
+
+
+class ShmExchange:
+    """The bare shared-memory all-gather (lio_shm_exchange_*; host only): n doubles from every rank."""
+
+    def __init__(self, name: str, rank: int, world: int, n: int):
+        self._h = C.c_void_p()
+        check(lib().lio_shm_exchange_open(name.encode(), rank, world, n, C.byref(self._h)))
+        self.world = world
+
+    def allgather(self, send: np.ndarray) -> np.ndarray:
+        send = np.ascontiguousarray(send, dtype=np.float64)
+        recv = np.empty(self.world * send.size)
+        check(lib().lio_shm_exchange_allgather(self._h, send.ctypes.data_as(C.POINTER(C.c_double)), send.size,
+                                               recv.ctypes.data_as(C.POINTER(C.c_double))))
+        return recv
+
+    def close(self):
+        if self._h:
+            lib().lio_shm_exchange_close(self._h)
+            self._h = C.c_void_p()

@@ -165,6 +165,10 @@ class IkdTreeGPU:
         check(lib().lio_map_get_stats(self._h, o))
         return dict(rebuilds=o[0], slots_cap=o[1], slots_used=o[2], alive=o[3], ids=o[4], cells=o[5], flags=o[6])
 
+    def set_test_limits(self, slot_headroom: int = 0, dirty_cells: int = 0):
+        """Test hook: a small slot pool / tombstone cell list, so the rebuild recovery paths run."""
+        check(lib().lio_map_set_test_limits(self._h, int(slot_headroom), int(dirty_cells)))
+
     def grid(self):
         g = np.zeros(7)
         check(lib().lio_map_get_grid(self._h, _dp(g)))

@@ -95,6 +95,25 @@ class LoopClosure:
         check(lib().lio_icp_set_shard_device(self._h, rank, world, exchange.fn, None))
         self._shard = (rank, world)
 
+    def set_shard_rccl(self, rank: int, world: int, group=None):
+        """Shard the source over ``world`` ranks with a per-rank RCCL communicator created in C++
+        (lio_icp_set_shard_rccl): the all-gather of every pass is enqueued by the library, no Python."""
+        from . import dist as ld
+
+        self._cb = None
+        self._dx = None
+        ld.attach_rccl(self._h, rank, world, group)
+        self._shard = (rank, world)
+
+    def set_shard_shm(self, rank: int, world: int, name: str, max_source_points: int, group=None):
+        """Shard over ranks on ONE node through the C++ shared-memory exchange (lio_icp_set_shard_shm)."""
+        from . import dist as ld
+
+        self._cb = None
+        self._dx = None
+        ld.attach_shm(self._h, rank, world, name, max_source_points, group)
+        self._shard = (rank, world)
+
     def set_timing(self, on: bool):
         check(lib().lio_icp_set_timing(self._h, 1 if on else 0))
 

@@ -128,6 +128,10 @@ int lio_map_get_grid(lio_map* m, double* out7);
  * alive points, ids, grid cells, flags of the last update (1 outside the grid, 2 pool exhausted,
  * 4 tombstone cell list full: each forces a rebuild), reserved]                                  */
 int lio_map_get_stats(lio_map* m, int64_t* out8);
+/* Test hook: cap the slot pool at (slots in use after the last rebuild + slot_headroom) and the per-update
+ * list of cells holding tombstones at dirty_cells (0: no cap), so that the pool-exhausted (flag 2) and
+ * list-full (flag 4) recovery paths run on small maps.                                          */
+int lio_map_set_test_limits(lio_map* m, int64_t slot_headroom, int64_t dirty_cells);
 
 /* ------------------------------------------------------------ h-model ctx */
 typedef struct lio_ctx lio_ctx;
@@ -307,6 +311,20 @@ typedef int (*lio_allgather_dev_fn)(const double* d_send, int64_t n, double* d_r
 int lio_icp_set_shard_device(lio_icp* h, int rank, int world, lio_allgather_dev_fn fn, void* user);
 int lio_icp_exchange_len(int64_t n_source, int world, int64_t* n_per_rank);
 int lio_icp_set_exchange_buffers(lio_icp* h, double* d_send, double* d_recv, int64_t n_per_rank);
+/* Multi-process exchanges in C++ (no callback into the caller per pass; lio_icp_mp.cpp):
+ *  RCCL: rank 0 calls lio_rccl_unique_id, the caller broadcasts the 128 bytes to every rank ONCE (e.g. over
+ *  torch.distributed), then every rank calls lio_icp_set_shard_rccl (collective: ncclCommInitRank on the
+ *  handle's device); per pass ncclAllGather is enqueued on the handle's stream and the records are summed in
+ *  record order behind it.  The communicator is owned by the handle.                                       */
+int lio_rccl_unique_id(uint8_t* id128);
+int lio_icp_set_shard_rccl(lio_icp* h, int rank, int world, const uint8_t* id128);
+/*  Shared memory (ranks on one node without RCCL, e.g. several ranks on one GPU): `name` = a POSIX shm name
+ *  ("/..."), rank 0 opens first (the caller orders it, e.g. a barrier), max_source_points sizes the segment.
+ *  The bare primitive (host only, no device): lio_shm_exchange_* — n doubles from every rank, rank order.  */
+int lio_icp_set_shard_shm(lio_icp* h, int rank, int world, const char* name, int64_t max_source_points);
+int lio_shm_exchange_open(const char* name, int rank, int world, int64_t n_per_rank, void** out);
+int lio_shm_exchange_allgather(void* ex, const double* send, int64_t n, double* recv);
+int lio_shm_exchange_close(void* ex);
 /* align(guess) + getFitnessScore() + is_valid decision (loop_closure.cpp:81-90).
  * aligned_opt (n*3, this rank's shard only when sharded) may be NULL.      */
 int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* aligned_opt);

@@ -27,7 +27,7 @@ for cell in cells:
         hm(p24, True)
     t = hm.timing()
     print(f"{cfg} cell={cell:.2f} grid={tree.grid()['dims'].tolist()} n_eff={int(sums[27])} "
-          f"knn_avg_us={t['knn_ms'] / t['knn_launches'] * 1e3:.1f} fin_us={t['final_ms'] / t['final_launches'] * 1e3:.1f} | "
+          f"knn_avg_us={t['knn_ms'] / t['knn_launches'] * 1e3:.1f} | "
           f"cells mean {s[:, 0].mean():.1f} p99 {np.percentile(s[:, 0], 99):.0f} max {s[:, 0].max()} | "
           f"points mean {s[:, 1].mean():.1f} p99 {np.percentile(s[:, 1], 99):.0f} max {s[:, 1].max()} | "
           f"shell hist {np.bincount(s[:, 2], minlength=5).tolist()}", flush=True)

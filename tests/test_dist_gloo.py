@@ -85,3 +85,60 @@ def test_sharded_icp_exchange_gloo(world):
     ref = ld.combine(recs.ravel(), NS, 1)
     for rank, b in got:
         np.testing.assert_array_equal(np.frombuffer(b), ref)
+
+
+def _shm_worker(rank, world, name, rounds, q):
+    """Rank of the C++ shared-memory all-gather (lio_shm_exchange_*, the transport of lio_icp_set_shard_shm):
+    rank 0 opens first (ordered here by a queue handshake), then `rounds` exchanges of record sets with no
+    Python callback inside the library; every rank's combine of every round must equal one rank's."""
+    import sys
+    import time
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "fast-lio-sam_gps_amd"))
+    from lio_gpu import dist as ld
+
+    if rank != 0:
+        time.sleep(0.3)  # rank 0 creates the segment first (the library retries the open for 5 s anyway)
+    recs = _records(NS)
+    nrec = len(recs)
+    slot = -(-nrec // world)
+    b, n = ld.shard_range(NS, rank, world)
+    r0 = b // 4096
+    ex = ld.ShmExchange(name, rank, world, slot * 20)
+    outs = []
+    for k in range(rounds):
+        mine = recs[r0: r0 + (n + 4095) // 4096] * (k + 1)  # different data every round (buffer reuse)
+        send = np.zeros((slot, 20))
+        send[: len(mine)] = mine
+        recv = ex.allgather(send.ravel())
+        outs.append(ld.combine(recv, NS, world).tobytes())
+    ex.close()
+    q.put((rank, outs))
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_shm_exchange_cpp(world):
+    """The C++ shared-memory exchange the one-node multi-rank loop ICP uses (no Python in
+    the per-pass exchange): 50 rounds, alternating buffer sets, one barrier per round; every rank's record-order
+    combine equals the single-rank combine of the same records, round by round."""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "fast-lio-sam_gps_amd"))
+    from lio_gpu import dist as ld
+
+    rounds = 50
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    name = f"/lio_test_{os.getpid()}_{world}"
+    procs = [ctx.Process(target=_shm_worker, args=(r, world, name, rounds, q)) for r in range(world)]
+    [p.start() for p in procs]
+    got = [q.get(timeout=120) for _ in range(world)]
+    [p.join(timeout=60) for p in procs]
+    assert all(p.exitcode == 0 for p in procs)
+    recs = _records(NS)
+    for rank, outs in got:
+        assert len(outs) == rounds
+        for k, b in enumerate(outs):
+            np.testing.assert_array_equal(np.frombuffer(b), ld.combine((recs * (k + 1)).ravel(), NS, 1))

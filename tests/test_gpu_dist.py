@@ -35,8 +35,11 @@ rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
 dist.init_process_group("gloo", rank=rank, world_size=world)
 src, dst, _ = synth.make_icp_pair(n_points=%d, seed=7, disp=(%f, %f))
 lc = LC.LoopClosure(LC.LoopClosureConfig(), device=0)
-cb = ld.make_allgather()
-lc.set_shard(rank, world, cb)
+if os.environ.get("LIO_TEST_EXCHANGE") == "shm":  # the C++ shared-memory exchange: no Python per pass
+    lc.set_shard_shm(rank, world, "/lio_gpudist_%%s" %% os.environ["MASTER_PORT"], len(src))
+else:
+    cb = ld.make_allgather()
+    lc.set_shard(rank, world, cb)
 lc.setInputTarget(dst)
 lc.setInputSource(src)
 r = lc.align(keep_aligned=False)
@@ -53,8 +56,11 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("world,disp", [(2, (0.3, 1.5)), (3, (2.5, 4.0))])
-def test_sharded_icp_multiprocess_gpu_records(world, disp):
+@pytest.mark.parametrize("world,disp,exchange", [(2, (0.3, 1.5), "gloo"), (3, (2.5, 4.0), "gloo"),
+                                                  (2, (2.5, 4.0), "shm"), (3, (1.0, 3.0), "shm")])
+def test_sharded_icp_multiprocess_gpu_records(world, disp, exchange):
+    """exchange "gloo": the records through a ctypes callback into torch.distributed; "shm": the C++
+    shared-memory exchange (lio_icp_set_shard_shm) — no Python call inside the alignment."""
     n = 60_000
     src, dst, _ = synth.make_icp_pair(n_points=n, seed=7, disp=disp)
     lc = LC.LoopClosure(LC.LoopClosureConfig(), device=0)
@@ -67,7 +73,7 @@ def test_sharded_icp_multiprocess_gpu_records(world, disp):
     procs = []
     for rank in range(world):
         env = dict(os.environ, RANK=str(rank), WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0")
+                   MASTER_PORT=str(port), HSA_ENABLE_IPC_MODE_LEGACY="0", LIO_TEST_EXCHANGE=exchange)
         procs.append(subprocess.Popen([sys.executable, "-c", code], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
     outs = []

@@ -250,3 +250,39 @@ def test_long_drive_with_fov_segment(oracle):
     # odometry stays sane; the parity above is the point of the test
     assert np.all(np.isfinite(errs)) and max(errs) < 1.0
     _knn_parity(tree, om, scans[-1].body + np.float32([1.0, 0.5, 0.0]))
+
+
+@pytest.mark.parametrize("headroom,dirty", [(64, 0), (0, 3), (64, 3)])
+def test_pool_and_tombstone_list_recovery(oracle, scene_scans, headroom, dirty):
+    """the gapped grid's two recovery paths — the slot pool exhausted while a cell moves to a
+    bigger block (flag 2) and the per-update list of cells holding tombstones full (flag 4) — each end in a
+    full re-lay from by_id.  Forced here with a pool capped at (slots in use + headroom) and a 3-cell list:
+    Add_Points with downsample (replacements -> tombstones) and map_incremental stay bit-exact against the
+    oracle, the rebuild counter goes up with the flags, and the kNN over the re-laid grid is exact."""
+    _, m, scans = scene_scans
+    base = m[:60000]
+    tree = F.IkdTreeGPU(cell_size=1.0, downsample_size=0.5)
+    tree.Build(base)
+    om = oracle.OracleDynMap(base)
+    tree.set_test_limits(headroom, dirty)
+    r0 = tree.stats()["rebuilds"]
+    seen = 0
+    for sc in scans[:3]:
+        w = oracle.body_to_world(synth.pose24(synth.initial_state(sc.pos_gt, sc.rot_gt)), sc.body)
+        assert tree.Add_Points(w, True) == om.add(w, True, 0.5)
+        seen |= tree.stats()["flags"]
+        _same_map(tree, om)
+    sc = scans[3]
+    hm = F.HShareModelGPU(tree)
+    hm.set_scan(sc.body)
+    kf = F.EsekfGPU(hm, laser_point_cov=0.001, max_iteration=3, epsi=0.001)
+    x, _, _ = kf.update_iterated_dyn_share_modified(synth.initial_state(sc.pos_init, sc.rot_init), synth.initial_cov())
+    p_knn, p_fin = hm.last_knn_pose24(), synth.pose24(x)
+    assert hm.map_incremental(p_fin, 0.5) == om.map_incremental(sc.body, p_knn, p_fin, 0.5, 0.5)
+    seen |= tree.stats()["flags"]
+    hm.close()
+    _same_map(tree, om)
+    want = (2 if headroom else 0) | (4 if dirty else 0)
+    assert seen & want == want, (seen, want)
+    assert tree.stats()["rebuilds"] > r0
+    _knn_parity(tree, om, scans[0].body + np.float32([2.0, -1.0, 0.0]))
