@@ -24,6 +24,7 @@
 #include <cstring>
 #include <limits>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/lio_gpu.h"
@@ -278,9 +279,16 @@ struct lio_icp {
     lio_icp_params p{};
     lio::GridBuf tgt;
     float* d_tgt = nullptr;
+    int64_t tgt_cap = 0;
     int64_t nt = 0;
+    bool tgt_dirty = false;      // setInputTarget staged; uploaded and gridded at the next align (as PCL builds
+                                 // its kd-tree lazily in align), on st2, overlapped with the source preparation
+    hipStream_t st2 = nullptr;
+    float* h_tgt = nullptr;      // pinned staging: the target, the full source
+    int64_t h_tgt_cap = 0;
+    float* h_src = nullptr;
+    int64_t h_src_cap = 0;
     double c0[3] = {0, 0, 0};
-    std::vector<float> src;  // full source (host copy)
     int64_t ns = 0;
     int rank = 0, world = 1;
     lio_allgather_fn fn = nullptr;
@@ -361,7 +369,9 @@ int lio_icp_create(const lio_icp_params* p, lio_icp** out) {
     h->dev = p->device;
     h->p = *p;
     if (!(h->p.cell_size > 0.f)) h->p.cell_size = 1.0f;  // 0.3 m voxelised submaps: 1 m target cells (scripts/icp_cells.py)
-    if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess) {
+    if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->st2, hipStreamNonBlocking) != hipSuccess) {
+        if (h->st) (void)hipStreamDestroy(h->st);
         delete h;
         return ifail(LIO_ERR_HIP, "icp stream/alloc failed");
     }
@@ -412,31 +422,84 @@ int lio_icp_destroy(lio_icp* h) {
     if (h->ev.b) (void)hipEventDestroy(h->ev.b);
     if (h->ev.m) (void)hipEventDestroy(h->ev.m);
     if (h->ev.done) (void)hipEventDestroy(h->ev.done);
+    if (h->h_tgt) (void)hipHostFree(h->h_tgt);
+    if (h->h_src) (void)hipHostFree(h->h_src);
+    (void)hipStreamSynchronize(h->st2);
+    (void)hipStreamDestroy(h->st2);
     (void)hipStreamDestroy(h->st);
     delete h;
+    return LIO_OK;
+}
+
+// host copy into the handle's pinned staging buffer (grown geometrically), split over a few threads for
+// large clouds: the caller's buffer may go away after the call (PCL copies the cloud too)
+static int stage_pinned(float*& buf, int64_t& cap, const float* xyz, int64_t n) {
+    if (n > cap || !buf) {
+        if (buf) (void)hipHostFree(buf);
+        buf = nullptr;
+        cap = 0;
+        const int64_t c = std::max<int64_t>(n, 1) + std::max<int64_t>(n, 1) / 4;
+        if (hipHostMalloc(reinterpret_cast<void**>(&buf), (size_t)c * 3 * sizeof(float), hipHostMallocDefault) != hipSuccess)
+            return ifail(LIO_ERR_NOMEM, "ICP staging: hipHostMalloc failed");
+        cap = c;
+    }
+    const size_t bytes = (size_t)n * 3 * sizeof(float);
+    const int nt = bytes >= ((size_t)4 << 20) ? 4 : 1;
+    if (nt == 1) {
+        std::memcpy(buf, xyz, bytes);
+    } else {
+        std::vector<std::thread> th;
+        const int64_t per = (3 * n + nt - 1) / nt;
+        for (int t = 0; t < nt; ++t) {
+            const int64_t b = std::min<int64_t>(3 * n, t * per), e = std::min<int64_t>(3 * n, b + per);
+            th.emplace_back([=] { std::memcpy(buf + b, xyz + b, (size_t)(e - b) * sizeof(float)); });
+        }
+        for (std::thread& t : th) t.join();
+    }
     return LIO_OK;
 }
 
 int lio_icp_set_target(lio_icp* h, const float* xyz, int64_t n) {
     if (!h || n <= 0 || !xyz) return ifail(LIO_ERR_ARG, "lio_icp_set_target: bad arguments");
     IHIP(hipSetDevice(h->dev));
-    if (h->d_tgt) IHIP(hipFree(h->d_tgt));
-    h->d_tgt = nullptr;
-    IHIP(hipMalloc(&h->d_tgt, (size_t)n * 3 * sizeof(float)));
-    IHIP(hipMemcpyAsync(h->d_tgt, xyz, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice, h->st));
-    int rc = lio::grid_build(h->tgt, h->d_tgt, n, h->p.cell_size, h->st);
-    if (rc) return ifail(rc == -5 ? LIO_ERR_NOMEM : LIO_ERR_HIP, "target grid build failed");
-    IHIP(hipStreamSynchronize(h->st));
+    IHIP(hipStreamSynchronize(h->st2));  // a previous target upload may still read the staging buffer
+    const int rc = stage_pinned(h->h_tgt, h->h_tgt_cap, xyz, n);
+    if (rc) return rc;
     h->nt = n;
+    h->tgt_dirty = true;
+    return LIO_OK;
+}
+
+// the staged target: upload + grid + accumulation centre, on st2 (called from a helper thread)
+static int target_build(lio_icp* h) {
+    IHIP(hipSetDevice(h->dev));
+    const int64_t n = h->nt;
+    if (n > h->tgt_cap || !h->d_tgt) {
+        if (h->d_tgt) IHIP(hipFree(h->d_tgt));
+        h->d_tgt = nullptr;
+        h->tgt_cap = 0;
+        IHIP(hipMalloc(&h->d_tgt, (size_t)n * 3 * sizeof(float)));
+        h->tgt_cap = n;
+    }
+    IHIP(hipMemcpyAsync(h->d_tgt, h->h_tgt, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice, h->st2));
+    int rc = lio::grid_build(h->tgt, h->d_tgt, n, h->p.cell_size, h->st2);
+    if (rc) return ifail(rc == -5 ? LIO_ERR_NOMEM : LIO_ERR_HIP, "target grid build failed");
+    IHIP(hipStreamSynchronize(h->st2));
     // fixed accumulation centre: target bounding-box centre (float)
     const float* bb = h->tgt.aabb_host;
     for (int d = 0; d < 3; ++d) h->c0[d] = (double)(0.5f * (bb[d] + bb[3 + d]));
+    h->tgt_dirty = false;
     return LIO_OK;
 }
 
 int lio_icp_set_source(lio_icp* h, const float* xyz, int64_t n) {
     if (!h || n < 0 || (n > 0 && !xyz) || n >= (int64_t)1 << 30) return ifail(LIO_ERR_ARG, "lio_icp_set_source: bad arguments");
-    h->src.assign(xyz, xyz + 3 * n);
+    IHIP(hipSetDevice(h->dev));
+    IHIP(hipStreamSynchronize(h->st));  // the previous source upload may still read the staging buffer
+    if (n > 0) {
+        const int rc = stage_pinned(h->h_src, h->h_src_cap, xyz, n);
+        if (rc) return rc;
+    }
     h->ns = n;
     h->src_dirty = true;
     return LIO_OK;
@@ -552,7 +615,7 @@ static int icp_prepare(lio_icp* h) {
     h->ntiles = 0;
     h->have_order = false;  // new tiles: cell order until a pass has measured them
     if (h->sh_n > 0) {
-        IHIP(hipMemcpyAsync(h->d_src, h->src.data() + 3 * h->sh_begin, h->sh_n * 3 * sizeof(float),
+        IHIP(hipMemcpyAsync(h->d_src, h->h_src + 3 * h->sh_begin, h->sh_n * 3 * sizeof(float),
                             hipMemcpyHostToDevice, h->st));
         // bin the shard by tile cell: tiles of <= 64 spatially compact queries (perf only: every
         // query's 1-NN is exact whatever tile it is in)
@@ -590,19 +653,22 @@ static int pcl_finish(lio_icp* h, const lio::IcpArgs& a) {
         std::memcpy(&ev, h->h_pclout + 18, sizeof(ev));
         h->fid_stats[2] = ev;
     }
-    int pass = 1;
-    while ((pcl_word(h, 0) | pcl_word(h, 1)) != 0 && pass < 3) {
+    constexpr int kMaxPasses = 4;  // per chain set; the verification makes any pass count safe
+    int mpass = 1, spass = 1;
+    while ((pcl_word(h, 0) | pcl_word(h, 1)) != 0) {
         const uint32_t bad = pcl_word(h, 0), over = pcl_word(h, 1);
         if (over) break;  // more passes only add events
-        ++pass;
+        if (bad & 0x3fu) {  // the means (sigma depends on them: its chains restart from pass 1)
+            if (mpass >= kMaxPasses) break;
+            lio::launch_pcl_means(h->pcl, ++mpass, h->st);
+            spass = 1;
+            lio::launch_pcl_sigma(h->pcl, order, spass, h->st);
+        } else {
+            if (spass >= kMaxPasses) break;
+            lio::launch_pcl_sigma(h->pcl, order, ++spass, h->st);
+        }
         ++h->fid_stats[0];
         ++h->fid_stats[3];
-        if (bad & 0x3fu) {  // the means (sigma depends on them: its chains restart from pass 1)
-            lio::launch_pcl_means(h->pcl, pass, h->st);
-            lio::launch_pcl_sigma(h->pcl, order, 1, h->st);
-        } else {
-            lio::launch_pcl_sigma(h->pcl, order, pass, h->st);
-        }
         lio::launch_pcl_pack(h->pcl, order, h->d_pclout, h->st);
         IHIP(hipMemcpyAsync(h->h_pclout, h->d_pclout, lio::kPclOutWords * sizeof(float), hipMemcpyDeviceToHost, h->st));
         IHIP(hipStreamSynchronize(h->st));
@@ -874,7 +940,18 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
         return ifail(LIO_ERR_ARG, "lio_icp_align: umeyama_float must be 0 (double statistics) or 1..3 (float orders)");
     if (pcl_float && h->world > 1)
         return ifail(LIO_ERR_ARG, "lio_icp_align: umeyama_float (PCL-order float sums) runs on one rank only");
-    int rc = icp_prepare(h);
+    // the target (st2, helper thread) and the source (st, this thread) prepared side by side
+    int rc = LIO_OK, trc = LIO_OK;
+    std::string terr;
+    std::thread tth;
+    if (h->tgt_dirty)
+        tth = std::thread([&] {
+            trc = target_build(h);
+            if (trc) terr = lio::last_error();
+        });
+    rc = icp_prepare(h);
+    if (tth.joinable()) tth.join();
+    if (trc) return ifail(trc, terr);
     if (rc) return rc;
     if (pcl_float) {
         if (lio::pcl_reserve(h->pcl, std::max<int64_t>(h->sh_n, 1), h->p.umeyama_float, h->st))

@@ -17,11 +17,25 @@ namespace lio {
 namespace {
 
 constexpr int kSpecial = -1000;  // zero, subnormal or non-finite: no binade
+// prediction slack near binade edges (mantissa bits): pass 1 predicts from a double prefix sum that drifts
+// from the float chain by its accumulated rounding (measured: a few units on C4 chains of |s| ~ 1e4-1e5,
+// ~2^-12 relative), later passes from a reconstruction within a few ulps of it
+constexpr int kPredSlack1 = 13;  // 2^-10 relative
+constexpr int kPredSlack2 = 4;   // 16 ulps
 
 __device__ __forceinline__ int binade_f(float f) {
     const uint32_t b = __float_as_uint(f);
     const int e = (int)((b >> 23) & 0xffu);
     return (e == 0 || e == 255) ? kSpecial : e - 127;
+}
+
+// a prediction within 2^-(23 - lg) of a binade edge (lg mantissa bits of slack) is ambiguous: kSpecial
+// makes the element (and its successor) an event, replayed exactly by the walker
+__device__ __forceinline__ int binade_pred(float f, int lg) {
+    const uint32_t m = __float_as_uint(f) & 0x7fffffu;
+    const uint32_t tol = 1u << lg;
+    if (m < tol || m > 0x7fffffu - tol) return kSpecial;
+    return binade_f(f);
 }
 
 template <typename T>
@@ -129,21 +143,21 @@ __device__ __forceinline__ void predict(const Src& src, const SeqSumBuf& b, int 
         block_dprefix(in.x, D, s_wd, tot);
         const double bo = b.boff[(size_t)c * b.nblk + blk];
 #pragma unroll
-        for (int i = 0; i < kSeqPer; ++i) in.e[i] = binade_f((float)(bo + D[i]));
+        for (int i = 0; i < kSeqPer; ++i) in.e[i] = binade_pred((float)(bo + D[i]), kPredSlack1);
         // predecessor of the thread's first element: the previous thread's last (block's first: boff)
         int prev = __shfl_up(in.e[kSeqPer - 1], 1, 64);
         __shared__ int s_last[kSeqThreads / 64];
         const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
         if (lane == 63) s_last[w] = in.e[kSeqPer - 1];
         __syncthreads();
-        if (lane == 0) prev = w > 0 ? s_last[w - 1] : binade_f((float)bo);
+        if (lane == 0) prev = w > 0 ? s_last[w - 1] : binade_pred((float)bo, kPredSlack1);
         __syncthreads();
         in.ep = prev;
     } else {
         const float* rc = b.recon + (size_t)c * b.nmax;
 #pragma unroll
-        for (int i = 0; i < kSeqPer; ++i) in.e[i] = k0 + i < n ? binade_f(rc[k0 + i]) : kSpecial;
-        in.ep = k0 > 0 ? binade_f(rc[k0 - 1]) : kSpecial;
+        for (int i = 0; i < kSeqPer; ++i) in.e[i] = k0 + i < n ? binade_pred(rc[k0 + i], kPredSlack2) : kSpecial;
+        in.ep = k0 > 0 ? binade_pred(rc[k0 - 1], kPredSlack2) : kSpecial;
     }
     if (k0 == 0) in.e[0] = binade_f(in.x[0]);  // s_0 = x_0 exactly
 }

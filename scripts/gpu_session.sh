@@ -49,7 +49,9 @@ for s in $STEPS; do
              run bench_driverq2 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu --pipeline 0 --streams '' --no-icp &&
              run bench_driverq3 300 python bench.py --gpus 1 --steps 50 --warmup 5 --no-cpu --pipeline 0 --streams '' --no-icp ;;
     micro) run graph_cost 120 scripts/micro/graph_cost ;;
-    setup) run icp_setup 300 python scripts/icp_setup_timing.py ;;
+    setup) run icp_setup 300 python scripts/icp_setup_timing.py &&
+           run icp_setup_pre 300 env LIO_GPU_LIB=build_ab/pre_setup/liblio_gpu.so python scripts/icp_setup_timing.py &&
+           run icp_setup2 300 python scripts/icp_setup_timing.py ;;
     msab)  run msab 900 bash -c 'for r in 1 2; do for lib in HEAD build_ab/r02/liblio_gpu.so; do if [ $lib = HEAD ]; then python bench.py --steps 60 --warmup 5 --no-cpu --no-icp --pipeline 0 --streams 1,2,8; else LIO_GPU_LIB=$lib python bench.py --steps 60 --warmup 5 --no-cpu --no-icp --pipeline 0 --streams 1,2,8; fi | python -c "import json,sys; d=json.loads([l for l in sys.stdin if l.startswith(\"{\")][-1]); print(\"$lib\", d[\"value\"], d[\"multi_stream\"])" || exit $?; done; done' ;;
     pmcsq) run pmcsq_c3 300 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmcsq_c3" -o run --output-format csv -- python bench.py --steps 30 --warmup 3 --no-cpu --no-icp --streams '' --pipeline 0 &&
            run pmcsq_icp 300 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmcsq_icp" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
