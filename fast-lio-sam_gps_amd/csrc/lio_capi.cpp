@@ -258,6 +258,10 @@ static int map_build_impl(lio_map* m, const float* d_xyz, int64_t n) {
     if (rc == -5) return fail(LIO_ERR_NOMEM, "grid build: out of device memory");
     if (rc == -1) return fail(LIO_ERR_ARG, "grid build: invalid points (empty, too many, or non-finite)");
     if (rc != 0) return fail(LIO_ERR_HIP, "grid build failed");
+    // the map_incremental scratch for a scan of up to 256 k points (C3 131 k, C5 ~30 k undistorted), so the
+    // stream's first update allocates nothing; larger scans grow it then
+    rc = lio::mapupd_presize(m->upd, (int64_t)1 << 18, m->st);
+    if (rc) return fail(rc == -5 ? LIO_ERR_NOMEM : LIO_ERR_HIP, "map update scratch");
     HIP_TRY(hipStreamSynchronize(m->st));
     m->n = m->grid.n;
     ++m->version;

@@ -1323,6 +1323,19 @@ int map_delete_boxes(GridBuf& g, MapUpdBuf& u, const float* boxes, int nb, float
 // map_incremental(): classification (+ unbounded 5-NN for queued points), then
 // Add_Points(PointToAdd, true) and Add_Points(PointNoNeedDownsample, false) with one grid update and
 // one host synchronisation.  out: [to_add, no_need, skipped, added_by_downsample_call]
+// The update scratch sized for n offered points before the first update (lio_map_build): the first
+// map_incremental of a stream then allocates nothing (~8 ms of set-up on the first call)
+int mapupd_presize(MapUpdBuf& u, int64_t n, hipStream_t st) {
+    if (n <= 0) return 0;
+    if (n >= (int64_t)1 << 30) return -1;
+    if (ensure_pts(u, n, st)) return -5;
+    size_t b1 = 0, b2 = 0, b3 = 0;
+    UPD_CHK(hipcub::DeviceScan::ExclusiveSum(nullptr, b1, u.add_flag, u.pos, (int)n + 1, st));
+    UPD_CHK(hipcub::DeviceScan::ExclusiveSum(nullptr, b2, u.f64, u.pos64, (int)n + 1, st));
+    UPD_CHK(hipcub::DeviceRadixSort::SortPairs(nullptr, b3, u.skey, u.skey2, u.sval, u.sval2, (int)n, 0, u.hbits + 1, st));
+    return ensure_tmp(u, std::max(b1, std::max(b2, b3))) ? -5 : 0;
+}
+
 int map_incremental(GridBuf& g, MapUpdBuf& u, IncrArgs a, float ds, float slack, int64_t out[4], hipStream_t st) {
     for (int k = 0; k < 4; ++k) out[k] = 0;
     const int n = a.n;

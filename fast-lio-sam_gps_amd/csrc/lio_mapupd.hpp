@@ -68,6 +68,8 @@ struct IncrArgs {
 };
 
 void mapupd_free(MapUpdBuf& u);
+// scratch for updates of up to n offered points, allocated ahead of the first one
+int mapupd_presize(MapUpdBuf& u, int64_t n, hipStream_t st);
 int map_add_device(GridBuf& g, MapUpdBuf& u, const float* d_xyz, int64_t n, bool downsample, float ds, float slack,
                    int64_t out[2], hipStream_t st);
 int map_delete_boxes(GridBuf& g, MapUpdBuf& u, const float* boxes, int nb, float slack, int64_t* n_deleted,

@@ -49,6 +49,9 @@ for s in $STEPS; do
              run bench_driverq2 300 python bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu --pipeline 0 --streams '' --no-icp &&
              run bench_driverq3 300 python bench.py --gpus 1 --steps 50 --warmup 5 --no-cpu --pipeline 0 --streams '' --no-icp ;;
     micro) run graph_cost 120 scripts/micro/graph_cost ;;
+    first) run map_first 300 python scripts/map_first_call.py &&
+           run map_first_pre 300 env LIO_GPU_LIB=build_ab/pre_setup/liblio_gpu.so python scripts/map_first_call.py &&
+           run map_first_nodefer 300 env HIP_ENABLE_DEFERRED_LOADING=0 python scripts/map_first_call.py ;;
     setup) run icp_setup 300 python scripts/icp_setup_timing.py &&
            run icp_setup_pre 300 env LIO_GPU_LIB=build_ab/pre_setup/liblio_gpu.so python scripts/icp_setup_timing.py &&
            run icp_setup2 300 python scripts/icp_setup_timing.py ;;
