@@ -1082,6 +1082,53 @@ static lio::UndistortEnd undistort_end(const lio_pose* e) {
 
 static_assert(sizeof(lio_imu_pose) == sizeof(lio::ImuPose), "lio_imu_pose layout");
 
+// LIO_PREP_UPLOAD=full (A/B hook): the whole sweep uploaded from the caller's memory and selected on the
+// device, as before the staged upload
+static bool prep_upload_full() {
+    static const bool full = [] {
+        const char* e = std::getenv("LIO_PREP_UPLOAD");
+        return e && std::strcmp(e, "full") == 0;
+    }();
+    return full;
+}
+
+// The host half of a sweep upload: rows i % every == 0 — Preprocess's point_filter_num drops the others
+// by index alone, so they never cross PCIe — and the IMU poses packed into the filter's pinned staging
+// buffer, for one DMA each (pageable sources would be staged by the runtime anyway).  *u = rows staged;
+// the poses start at byte *pose_off.
+static int stage_sweep(lio::FilterBuf& b, const void* rows, int64_t n, size_t row_bytes, int every,
+                       const lio_imu_pose* poses, int np, int64_t* u, size_t* pose_off) {
+    every = std::max(every, 1);
+    *u = (n + every - 1) / every;
+    *pose_off = ((size_t)*u * row_bytes + 255) & ~(size_t)255;
+    const size_t need = *pose_off + (size_t)np * sizeof(lio_imu_pose);
+    if (need > b.stage_bytes || !b.h_stage) {
+        if (b.h_stage) (void)hipHostFree(b.h_stage);
+        b.h_stage = nullptr;
+        const size_t c = std::max(need, b.stage_bytes + b.stage_bytes / 2);
+        if (hipHostMalloc(&b.h_stage, c) != hipSuccess) {
+            b.stage_bytes = 0;
+            return fail(LIO_ERR_NOMEM, "sweep staging: hipHostMalloc failed");
+        }
+        b.stage_bytes = c;
+    }
+    auto* dst = static_cast<uint8_t*>(b.h_stage);
+    const auto* src = static_cast<const uint8_t*>(rows);
+    if (every == 1) {
+        std::memcpy(dst, src, (size_t)n * row_bytes);
+    } else if (row_bytes % 4 == 0 && row_bytes <= 4 * lio::kMaxFields) {
+        const int nw = (int)(row_bytes / 4);
+        const auto* s = reinterpret_cast<const float*>(rows);
+        auto* d = reinterpret_cast<float*>(dst);
+        for (int64_t r = 0; r < *u; ++r)
+            for (int k = 0; k < nw; ++k) d[r * nw + k] = s[r * every * nw + k];
+    } else {
+        for (int64_t r = 0; r < *u; ++r) std::memcpy(dst + r * row_bytes, src + r * every * row_bytes, row_bytes);
+    }
+    if (np) std::memcpy(dst + *pose_off, poses, (size_t)np * sizeof(lio_imu_pose));
+    return LIO_OK;
+}
+
 int lio_filter_create(int device, lio_filter** out) {
     if (!out) return fail(LIO_ERR_ARG, "out is NULL");
     *out = nullptr;
@@ -1181,21 +1228,72 @@ int lio_preprocess(lio_filter* f, const float* raw, int64_t n, int stride, const
     *n_out = 0;
     if (n == 0) return LIO_OK;
     HIP_TRY(hipSetDevice(f->dev));
-    rc = grow(&f->d_in, f->in_cap, n * stride);
-    if (!rc) rc = grow(&f->d_out, f->out_cap, n * stride);
+    hipStream_t st = f->st;
+    const bool full = prep_upload_full();
+    lio::ScanPrepParams sp{p->point_filter_num, p->blind, p->filter_size_surf, p->time_field};
+    int64_t rows = n;
+    size_t pose_off = 0;
+    if (!full) {
+        rc = stage_sweep(f->b, raw, n, (size_t)stride * sizeof(float), p->point_filter_num, poses, n_poses, &rows,
+                         &pose_off);
+        if (rc) return rc;
+        sp.point_filter_num = 1;
+    }
+    rc = grow(&f->d_in, f->in_cap, rows * stride);
+    if (!rc) rc = grow(&f->d_out, f->out_cap, rows * stride);
     if (!rc && n_poses) rc = grow(&f->d_poses, f->poses_cap, n_poses);
     if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(f->d_in, raw, (size_t)n * stride * sizeof(float), hipMemcpyHostToDevice, f->st));
+    const auto* stage = static_cast<const uint8_t*>(f->b.h_stage);
+    HIP_TRY(hipMemcpyAsync(f->d_in, full ? (const void*)raw : stage, (size_t)rows * stride * sizeof(float),
+                           hipMemcpyHostToDevice, st));
     if (n_poses)
-        HIP_TRY(hipMemcpyAsync(f->d_poses, poses, (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, f->st));
-    const lio::ScanPrepParams sp{p->point_filter_num, p->blind, p->filter_size_surf, p->time_field};
+        HIP_TRY(hipMemcpyAsync(f->d_poses, full ? (const void*)poses : stage + pose_off,
+                               (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
     int64_t m = 0;
-    rc = lio::scan_preprocess(f->b, f->d_in, n, stride, sp, f->d_poses, n_poses, undistort_end(end), f->d_out, &m,
-                              f->st);
-    if (rc) return filter_status(rc, "lio_preprocess");
-    if (m) HIP_TRY(hipMemcpyAsync(out, f->d_out, (size_t)m * stride * sizeof(float), hipMemcpyDeviceToHost, f->st));
-    HIP_TRY(hipStreamSynchronize(f->st));
+    rc = lio::scan_preprocess_enqueue(f->b, f->d_in, rows, stride, sp, f->d_poses, n_poses, undistort_end(end),
+                                      f->d_out, st);
+    if (!rc) rc = lio::scan_preprocess_finish(f->b, stride, f->d_out, &m, nullptr, st);
+    if (rc < 0) {
+        (void)hipStreamSynchronize(st);  // the staging buffer is reused by the next call
+        return filter_status(rc, "lio_preprocess");
+    }
+    if (m) HIP_TRY(hipMemcpyAsync(out, f->d_out, (size_t)m * stride * sizeof(float), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
     *n_out = m;
+    return LIO_OK;
+}
+
+// the device half shared by lio_scan_preprocess and lio_scan_preprocess_cloud2: c->d_raw holds `rows`
+// records; every stage is queued, the scan buffers set up behind it, and the host waits once
+static int scan_prep_device(lio_ctx* c, int64_t rows, int stride, const lio::ScanPrepParams& sp, int n_poses,
+                            const lio_pose* end, int64_t* n_down, const char* what) {
+    hipStream_t st = c->map->st;
+    c->undist_n = -1;
+    auto bail = [&](int r) {
+        (void)hipStreamSynchronize(st);  // nothing queued may outlive the call (the staging buffer is reused)
+        return r;
+    };
+    int rc = lio::scan_preprocess_enqueue(c->filt, c->d_raw, rows, stride, sp, c->d_poses, n_poses,
+                                          undistort_end(end), c->d_rec, st);
+    if (rc) return bail(filter_status(rc, what));
+    rc = ctx_reserve(c, rows);  // sized for the row bound; c->n set to the count below
+    if (rc) return bail(rc);
+    rc = lio::records_to_xyz(c->d_rec, rows, stride, c->d_body, st);
+    if (rc) return bail(filter_status(rc, what));
+    if (hipMemsetAsync(c->d_sel, 0, (size_t)std::max<int64_t>(rows, 1), st) != hipSuccess)
+        return bail(fail(LIO_ERR_HIP, std::string(what) + ": memset failed"));
+    int64_t m = 0, mu = 0;
+    rc = lio::scan_preprocess_finish(c->filt, stride, c->d_rec, &m, &mu, st);
+    if (rc < 0) return bail(filter_status(rc, what));
+    if (rc == 1) {  // VoxelGrid index overflow: the output is the undistorted input, its xyz again
+        rc = lio::records_to_xyz(c->d_rec, m, stride, c->d_body, st);
+        if (rc) return bail(filter_status(rc, what));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    c->n = m;
+    c->undist_n = mu;
+    c->undist_stride = stride;
+    if (n_down) *n_down = m;
     return LIO_OK;
 }
 
@@ -1206,30 +1304,28 @@ int lio_scan_preprocess(lio_ctx* c, const float* raw, int64_t n, int stride, con
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->map->dev));
     hipStream_t st = c->map->st;
-    rc = grow(&c->d_raw, c->raw_cap, std::max<int64_t>(n, 1) * stride);
-    if (!rc) rc = grow(&c->d_rec, c->rec_cap, std::max<int64_t>(n, 1) * stride);
+    const bool full = prep_upload_full();
+    lio::ScanPrepParams sp{p->point_filter_num, p->blind, p->filter_size_surf, p->time_field};
+    int64_t rows = n;
+    size_t pose_off = 0;
+    if (!full) {
+        rc = stage_sweep(c->filt, raw, n, (size_t)stride * sizeof(float), p->point_filter_num, poses, n_poses, &rows,
+                         &pose_off);
+        if (rc) return rc;
+        sp.point_filter_num = 1;
+    }
+    rc = grow(&c->d_raw, c->raw_cap, std::max<int64_t>(rows, 1) * stride);
+    if (!rc) rc = grow(&c->d_rec, c->rec_cap, std::max<int64_t>(rows, 1) * stride);
     if (!rc && n_poses) rc = grow(&c->d_poses, c->poses_cap, n_poses);
     if (rc) return rc;
-    if (n) HIP_TRY(hipMemcpyAsync(c->d_raw, raw, (size_t)n * stride * sizeof(float), hipMemcpyHostToDevice, st));
+    const auto* stage = static_cast<const uint8_t*>(c->filt.h_stage);
+    if (rows)
+        HIP_TRY(hipMemcpyAsync(c->d_raw, full ? (const void*)raw : stage, (size_t)rows * stride * sizeof(float),
+                               hipMemcpyHostToDevice, st));
     if (n_poses)
-        HIP_TRY(hipMemcpyAsync(c->d_poses, poses, (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
-    const lio::ScanPrepParams sp{p->point_filter_num, p->blind, p->filter_size_surf, p->time_field};
-    int64_t m = 0;
-    c->undist_n = -1;
-    int64_t mu = 0;
-    rc = lio::scan_preprocess(c->filt, c->d_raw, n, stride, sp, c->d_poses, n_poses, undistort_end(end), c->d_rec, &m,
-                              st, &mu);
-    if (rc) return filter_status(rc, "lio_scan_preprocess");
-    c->undist_n = mu;
-    c->undist_stride = stride;
-    rc = ctx_reserve(c, m);
-    if (rc) return rc;
-    rc = lio::records_to_xyz(c->d_rec, m, stride, c->d_body, st);
-    if (rc) return filter_status(rc, "lio_scan_preprocess");
-    HIP_TRY(hipMemsetAsync(c->d_sel, 0, (size_t)std::max<int64_t>(m, 1), st));
-    HIP_TRY(hipStreamSynchronize(st));
-    if (n_down) *n_down = m;
-    return LIO_OK;
+        HIP_TRY(hipMemcpyAsync(c->d_poses, full ? (const void*)poses : stage + pose_off,
+                               (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
+    return scan_prep_device(c, rows, stride, sp, n_poses, end, n_down, "lio_scan_preprocess");
 }
 
 int lio_scan_get_undistorted(lio_ctx* c, float* out, int64_t cap_points, int64_t* n_points, int* stride) {
@@ -1331,34 +1427,34 @@ int lio_scan_preprocess_cloud2(lio_ctx* c, const uint8_t* data, int64_t n_points
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->map->dev));
     hipStream_t st = c->map->st;
-    const int64_t bytes = n_points * point_step;
-    rc = grow(&c->d_rec, c->rec_cap, std::max<int64_t>((bytes + 3) / 4, n_points * 5 + 1));  // staging for the bytes
-    if (!rc) rc = grow(&c->d_raw, c->raw_cap, std::max<int64_t>(n_points, 1) * 5);
+    const bool full = prep_upload_full();
+    lio::ScanPrepParams sp{pp.point_filter_num, pp.blind, pp.filter_size_surf, 4};
+    int64_t rows = n_points;
+    size_t pose_off = 0;
+    if (!full) {  // the records Preprocess keeps by index, still packed
+        rc = stage_sweep(c->filt, data, n_points, (size_t)point_step, pp.point_filter_num, poses, n_poses, &rows,
+                         &pose_off);
+        if (rc) return rc;
+        sp.point_filter_num = 1;
+    }
+    const int64_t bytes = rows * point_step;
+    rc = grow(&c->d_rec, c->rec_cap, std::max<int64_t>((bytes + 3) / 4, rows * 5 + 1));  // staging for the bytes
+    if (!rc) rc = grow(&c->d_raw, c->raw_cap, std::max<int64_t>(rows, 1) * 5);
     if (!rc && n_poses) rc = grow(&c->d_poses, c->poses_cap, n_poses);
     if (rc) return rc;
-    if (n_points) HIP_TRY(hipMemcpyAsync(c->d_rec, data, (size_t)bytes, hipMemcpyHostToDevice, st));
+    const auto* stage = static_cast<const uint8_t*>(c->filt.h_stage);
+    if (rows)
+        HIP_TRY(hipMemcpyAsync(c->d_rec, full ? (const void*)data : stage, (size_t)bytes, hipMemcpyHostToDevice, st));
     if (n_poses)
-        HIP_TRY(hipMemcpyAsync(c->d_poses, poses, (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
-    rc = lio::cloud_decode(reinterpret_cast<const uint8_t*>(c->d_rec), n_points, point_step, is_bigendian != 0,
+        HIP_TRY(hipMemcpyAsync(c->d_poses, full ? (const void*)poses : stage + pose_off,
+                               (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
+    rc = lio::cloud_decode(reinterpret_cast<const uint8_t*>(c->d_rec), rows, point_step, is_bigendian != 0,
                            reinterpret_cast<const lio::CloudField*>(fields), 5, c->d_raw, st);
-    if (rc) return filter_status(rc, "lio_scan_preprocess_cloud2");
-    const lio::ScanPrepParams sp{pp.point_filter_num, pp.blind, pp.filter_size_surf, 4};
-    int64_t m = 0;
-    c->undist_n = -1;
-    int64_t mu = 0;
-    rc = lio::scan_preprocess(c->filt, c->d_raw, n_points, 5, sp, c->d_poses, n_poses, undistort_end(end), c->d_rec, &m,
-                              st, &mu);
-    if (rc) return filter_status(rc, "lio_scan_preprocess_cloud2");
-    c->undist_n = mu;
-    c->undist_stride = 5;
-    rc = ctx_reserve(c, m);
-    if (rc) return rc;
-    rc = lio::records_to_xyz(c->d_rec, m, 5, c->d_body, st);
-    if (rc) return filter_status(rc, "lio_scan_preprocess_cloud2");
-    HIP_TRY(hipMemsetAsync(c->d_sel, 0, (size_t)std::max<int64_t>(m, 1), st));
-    HIP_TRY(hipStreamSynchronize(st));
-    if (n_down) *n_down = m;
-    return LIO_OK;
+    if (rc) {
+        (void)hipStreamSynchronize(st);
+        return filter_status(rc, "lio_scan_preprocess_cloud2");
+    }
+    return scan_prep_device(c, rows, 5, sp, n_poses, end, n_down, "lio_scan_preprocess_cloud2");
 }
 
 int lio_pcd_write_binary(const char* path, const float* rec, int64_t n, int stride, const char* const* names) {

@@ -30,8 +30,41 @@ namespace {
 
 constexpr uint32_t kInvalid = 0xffffffffu;
 
-__global__ void minmax_partial_kernel(const float* __restrict__ p, int64_t n, int stride, float* __restrict__ part) {
+// min / max over 256 lanes of the block (lo[3], hi[3] per lane) into s[0..2][0] / s[3..5][0]
+__device__ __forceinline__ void block_minmax(float (*s)[256], const float* lo, const float* hi) {
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        s[d][threadIdx.x] = lo[d];
+        s[3 + d][threadIdx.x] = hi[d];
+    }
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) {
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                s[d][threadIdx.x] = fminf(s[d][threadIdx.x], s[d][threadIdx.x + w]);
+                s[3 + d][threadIdx.x] = fmaxf(s[3 + d][threadIdx.x], s[3 + d][threadIdx.x + w]);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// AABB of the finite points (getMinMax3D) and PCL's voxel geometry in one launch: every block writes its
+// partial min / max, the last block to finish (a ticket counter, reset by that block for the next launch)
+// reduces the partials and derives
+//   inverse_leaf = 1 / leaf;  min_b = floor(min_p * inv), max_b = floor(max_p * inv)
+//   div_b = max_b - min_b + 1; divb_mul = (1, div_b.x, div_b.x * div_b.y)
+//   overflow when div_b.x * div_b.y * div_b.z > INT_MAX (PCL then returns the input)
+// cnt (optional): the rows in use, <= n (the bound the grid is sized for)
+__global__ void __launch_bounds__(256) minmax_geom_kernel(const float* __restrict__ p, int64_t n,
+                                                          const uint32_t* __restrict__ cnt, int stride,
+                                                          float* __restrict__ part, unsigned* __restrict__ ticket,
+                                                          float lx, float ly, float lz, VoxelGeom* __restrict__ out) {
+    __shared__ float s[6][256];
+    __shared__ bool last;
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    if (cnt) n = min<int64_t>(n, *cnt);
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const float* q = p + (size_t)i * stride;
         const float x = q[0], y = q[1], z = q[2];
@@ -43,58 +76,27 @@ __global__ void minmax_partial_kernel(const float* __restrict__ p, int64_t n, in
         hi[1] = fmaxf(hi[1], y);
         hi[2] = fmaxf(hi[2], z);
     }
-    __shared__ float s[6][256];
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        s[d][threadIdx.x] = lo[d];
-        s[3 + d][threadIdx.x] = hi[d];
-    }
-    __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w) {
-#pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                s[d][threadIdx.x] = fminf(s[d][threadIdx.x], s[d][threadIdx.x + w]);
-                s[3 + d][threadIdx.x] = fmaxf(s[3 + d][threadIdx.x], s[3 + d][threadIdx.x + w]);
-            }
-        }
-        __syncthreads();
-    }
+    block_minmax(s, lo, hi);
     if (threadIdx.x < 6) part[blockIdx.x * 6 + threadIdx.x] = s[threadIdx.x][0];
-}
-
-// min/max of the partials, then PCL's voxel geometry:
-//   inverse_leaf = 1 / leaf;  min_b = floor(min_p * inv), max_b = floor(max_p * inv)
-//   div_b = max_b - min_b + 1; divb_mul = (1, div_b.x, div_b.x * div_b.y)
-//   overflow when div_b.x * div_b.y * div_b.z > INT_MAX (PCL then returns the input)
-__global__ void __launch_bounds__(256) voxel_geom_kernel(const float* __restrict__ part, int nb, float lx, float ly,
-                                                         float lz, VoxelGeom* __restrict__ out) {
-    __shared__ float s[6][256];
-    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    for (int b = threadIdx.x; b < nb; b += 256) {
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    const volatile float* vp = part;  // the other blocks' partials, past this CU's cache
+    for (int d = 0; d < 3; ++d) lo[d] = INFINITY, hi[d] = -INFINITY;
+    for (int b = threadIdx.x; b < (int)gridDim.x; b += 256) {
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-            lo[d] = fminf(lo[d], part[b * 6 + d]);
-            hi[d] = fmaxf(hi[d], part[b * 6 + 3 + d]);
+            lo[d] = fminf(lo[d], vp[b * 6 + d]);
+            hi[d] = fmaxf(hi[d], vp[b * 6 + 3 + d]);
         }
-    }
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {
-        s[d][threadIdx.x] = lo[d];
-        s[3 + d][threadIdx.x] = hi[d];
     }
     __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w) {
-#pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                s[d][threadIdx.x] = fminf(s[d][threadIdx.x], s[d][threadIdx.x + w]);
-                s[3 + d][threadIdx.x] = fmaxf(s[3 + d][threadIdx.x], s[3 + d][threadIdx.x + w]);
-            }
-        }
-        __syncthreads();
-    }
+    block_minmax(s, lo, hi);
     if (threadIdx.x != 0) return;
+    ticket[0] = 0u;
     VoxelGeom g;
     const float inv[3] = {1.0f / lx, 1.0f / ly, 1.0f / lz};
     int64_t div[3];
@@ -113,14 +115,15 @@ __global__ void __launch_bounds__(256) voxel_geom_kernel(const float* __restrict
 }
 
 // PCL: ijk = (int)(floor(p * inv) - (float)min_b); idx = ijk . divb_mul; non-finite points skipped
-__global__ void voxel_key_kernel(const float* __restrict__ p, int64_t n, int stride, const VoxelGeom* __restrict__ gp,
-                                 uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+__global__ void voxel_key_kernel(const float* __restrict__ p, int64_t n, const uint32_t* __restrict__ cnt, int stride,
+                                 const VoxelGeom* __restrict__ gp, uint32_t* __restrict__ keys,
+                                 uint32_t* __restrict__ vals) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
     const VoxelGeom g = *gp;
     const float* q = p + (size_t)i * stride;
     uint32_t k = kInvalid;
-    if (isfinite(q[0]) && isfinite(q[1]) && isfinite(q[2]) && !g.overflow) {
+    if ((!cnt || i < (int64_t)*cnt) && isfinite(q[0]) && isfinite(q[1]) && isfinite(q[2]) && !g.overflow) {
         const int i0 = (int)(floorf(q[0] * g.inv[0]) - (float)g.min_b[0]);
         const int i1 = (int)(floorf(q[1] * g.inv[1]) - (float)g.min_b[1]);
         const int i2 = (int)(floorf(q[2] * g.inv[2]) - (float)g.min_b[2]);
@@ -292,44 +295,24 @@ __global__ void transform_segs_kernel(const float* __restrict__ in, int64_t n, i
 }
 
 // ---- scan preprocessing --------------------------------------------------------
-// Preprocess (point_filter_num, blind) [U]: keep input i when i % every == 0 and
-// x*x + y*y + z*z > blind^2 (float); stable compaction.
-__global__ void scan_select_flags_kernel(const float* __restrict__ p, int64_t n, int stride, int every, float blind2,
-                                         uint32_t* __restrict__ flag) {
+// Preprocess (point_filter_num, blind) [U] and the time sort's key in one pass: input i is selected when
+// i % every == 0 and x*x + y*y + z*z > blind^2 (float); its key is the float bits of the point time
+// (curvature, ms) mapped to an unsigned order (negative times below every positive one), capped one below
+// the largest key, which marks the rows not selected.  The stable sort then leaves the selected rows
+// first, in time order and, inside a tie, in input order — compaction and sort in one.
+constexpr uint32_t kNotSelected = 0xffffffffu;
+__global__ void scan_key_kernel(const float* __restrict__ p, int64_t n, int stride, int every, float blind2,
+                                int tfield, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (i > n) return;
-    uint32_t f = 0;
-    if (i < n && i % every == 0) {
-        const float* q = p + (size_t)i * stride;
-        f = (q[0] * q[0] + q[1] * q[1] + q[2] * q[2]) > blind2 ? 1u : 0u;
+    if (i >= n) return;
+    uint32_t k = kNotSelected;
+    const float* q = p + (size_t)i * stride;
+    if (i % every == 0 && (q[0] * q[0] + q[1] * q[1] + q[2] * q[2]) > blind2) {
+        const uint32_t b = __float_as_uint(q[tfield]);
+        k = min((b & 0x80000000u) ? ~b : (b | 0x80000000u), kNotSelected - 1);
     }
-    flag[i] = f;
-}
-
-__global__ void compact_kernel(const float* __restrict__ p, int64_t n, int stride, const uint32_t* __restrict__ flag,
-                               const uint32_t* __restrict__ pos, float* __restrict__ out) {
-    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (i >= n || !flag[i]) return;
-    for (int f = 0; f < stride; ++f) out[(size_t)pos[i] * stride + f] = p[(size_t)i * stride + f];
-}
-
-// sort key of the point time (curvature, ms): float bits of a non-negative
-// float order like the values; negative times map below every positive one
-__global__ void time_key_kernel(const float* __restrict__ p, int64_t n, int stride, int tfield,
-                                uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
-    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const uint32_t b = __float_as_uint(p[(size_t)i * stride + tfield]);
-    keys[i] = (b & 0x80000000u) ? ~b : (b | 0x80000000u);
+    keys[i] = k;
     vals[i] = (uint32_t)i;
-}
-
-__global__ void gather_rows_kernel(const float* __restrict__ p, int64_t n, int stride,
-                                   const uint32_t* __restrict__ order, float* __restrict__ out) {
-    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    const float* q = p + (size_t)order[i] * stride;
-    for (int f = 0; f < stride; ++f) out[(size_t)i * stride + f] = q[f];
 }
 
 // sin / cos of the undistortion's SO3 Exp with ONE fixed-order routine on the device and in the
@@ -409,9 +392,9 @@ __device__ __forceinline__ void mv3(const double* M, const double* v, double* o)
     for (int r = 0; r < 3; ++r) o[r] = M[3 * r] * v[0] + (M[3 * r + 1] * v[1] + M[3 * r + 2] * v[2]);
 }
 
-__device__ __forceinline__ void compensate(float* q, int tfield, const ImuPose& hd, const ImuPose& tl,
+__device__ __forceinline__ void compensate(float* q, float tms, const ImuPose& hd, const ImuPose& tl,
                                            const UndistortEnd& end) {
-    const double dt = (double)q[tfield] / double(1000) - hd.offset_time;
+    const double dt = (double)tms / double(1000) - hd.offset_time;
     double E[9], Ri[9];
     so3_exp(tl.gyr, dt, E);
     for (int r = 0; r < 3; ++r)
@@ -434,29 +417,47 @@ __device__ __forceinline__ void compensate(float* q, int tfield, const ImuPose& 
     q[2] = (float)a[2];
 }
 
-// UndistortPcl backward propagation, one lane per (time-sorted) point: head =
-// the last IMU pose whose offset_time is < t (tail = head + 1 gives acc/gyr);
-// points at or before the first pose are left unchanged, as the reference's
-// loop never reaches them.  The reference's loop `break`s at the first point
-// without stepping past it, so that point is compensated again by every older
-// segment (head h-1, ..., 0) — reproduced for point 0.
-__global__ void undistort_kernel(float* __restrict__ p, int64_t n, int stride, int tfield,
-                                 const ImuPose* __restrict__ poses, int np, UndistortEnd end) {
+// UndistortPcl backward propagation, one lane per time-sorted row, gathered from the input through the
+// sort's permutation: the lane at the end of the selected rows stores their count (cnt[0]).  head = the
+// last IMU pose whose offset_time is < t (tail = head + 1 gives acc/gyr); points at or before the first
+// pose are left unchanged, as the reference's loop never reaches them.  The reference's loop `break`s at
+// the first point without stepping past it, so that point is compensated again by every older segment
+// (head h-1, ..., 0) — reproduced for point 0.  np < 2: the rows are only gathered.
+__global__ void undistort_gather_kernel(const float* __restrict__ in, int64_t n, int stride, int tfield,
+                                        const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ order,
+                                        const ImuPose* __restrict__ poses, int np, UndistortEnd end,
+                                        float* __restrict__ out, uint32_t* __restrict__ cnt) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
-    float* q = p + (size_t)i * stride;
-    const double t = (double)q[tfield] / double(1000);
-    int h = -1;
-    for (int k = np - 2; k >= 0; --k)
-        if (t > poses[k].offset_time) {
-            h = k;
-            break;
+    const uint32_t key = skeys[i];
+    if (key == kNotSelected) {
+        if (i == 0 || skeys[i - 1] != kNotSelected) cnt[0] = (uint32_t)i;
+        return;
+    }
+    if (i + 1 == n) cnt[0] = (uint32_t)n;
+    const float* r = in + (size_t)order[i] * stride;
+    float* o = out + (size_t)i * stride;
+    for (int f = 3; f < stride; ++f) o[f] = r[f];
+    float q[3] = {r[0], r[1], r[2]};
+    const float tms = r[tfield];
+    if (np >= 2) {
+        const double t = (double)tms / double(1000);
+        int h = -1;
+        for (int k = np - 2; k >= 0; --k)
+            if (t > poses[k].offset_time) {
+                h = k;
+                break;
+            }
+        if (h >= 0) {
+            compensate(q, tms, poses[h], poses[h + 1], end);
+            if (i == 0)  // the time field is not changed by the compensation
+                for (int k = h - 1; k >= 0; --k)
+                    if (t > poses[k].offset_time) compensate(q, tms, poses[k], poses[k + 1], end);
         }
-    if (h < 0) return;
-    compensate(q, tfield, poses[h], poses[h + 1], end);
-    if (i == 0)
-        for (int k = h - 1; k >= 0; --k)
-            if ((double)q[tfield] / double(1000) > poses[k].offset_time) compensate(q, tfield, poses[k], poses[k + 1], end);
+    }
+    o[0] = q[0];
+    o[1] = q[1];
+    o[2] = q[2];
 }
 
 #define FCHK(x)                           \
@@ -508,6 +509,10 @@ int reserve(FilterBuf& b, int64_t n) {
     if (!b.part) FCHK(hipMalloc(&b.part, 6 * 1024 * sizeof(float)));
     if (!b.geom) FCHK(hipMalloc(&b.geom, sizeof(VoxelGeom)));
     if (!b.h_small) FCHK(hipHostMalloc(&b.h_small, 256));
+    if (!b.cnt) {  // [0] selected count, [1] minmax_geom_kernel's ticket (zero between launches)
+        FCHK(hipMalloc(&b.cnt, 64));
+        FCHK(hipMemset(b.cnt, 0, 64));
+    }
     return 0;
 }
 
@@ -633,24 +638,25 @@ int records_to_xyz(const float* d_rec, int64_t n, int stride, float* d_xyz, hipS
 }
 
 void filter_free(FilterBuf& b) {
-    void* bufs[] = {b.keys, b.keys_alt, b.vals,  b.vals_alt, b.head, b.vid, b.big,
-                    b.part, b.geom,     b.tmp,  b.a,         b.c,    b.aux};
+    void* bufs[] = {b.keys, b.keys_alt, b.vals, b.vals_alt, b.head, b.vid, b.big,
+                    b.part, b.geom,     b.tmp,  b.a,    b.c,        b.aux,  b.cnt};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     if (b.h_small) (void)hipHostFree(b.h_small);
+    if (b.h_stage) (void)hipHostFree(b.h_stage);
     b = FilterBuf{};
 }
 
-int voxel_grid(FilterBuf& b, const float* d_in, int64_t n, int stride, const float leaf[3], float* d_out,
-               int64_t* n_out, hipStream_t st) {
-    *n_out = 0;
-    if (n <= 0) return 0;
+// Everything up to the centroids, with the output count and the geometry copied to b.h_small ([0] voxels,
+// [1..] VoxelGeom) behind them: nothing waits for the device.  cnt (optional, device): rows in use <= n.
+int voxel_grid_enqueue(FilterBuf& b, const float* d_in, int64_t n, const uint32_t* cnt, int stride, const float leaf[3],
+                       float* d_out, hipStream_t st) {
     if (stride < 3 || stride > kMaxFields || n >= (int64_t)0x7fffffff) return -1;
     if (reserve(b, n)) return -5;
     const int nbA = (int)std::min<int64_t>(1024, (n + 255) / 256);
-    minmax_partial_kernel<<<nbA, 256, 0, st>>>(d_in, n, stride, b.part);
-    voxel_geom_kernel<<<1, 256, 0, st>>>(b.part, nbA, leaf[0], leaf[1], leaf[2], b.geom);
-    voxel_key_kernel<<<nblk(n), 256, 0, st>>>(d_in, n, stride, b.geom, b.keys, b.vals);
+    minmax_geom_kernel<<<nbA, 256, 0, st>>>(d_in, n, cnt, stride, b.part, b.cnt + 1, leaf[0], leaf[1], leaf[2],
+                                            b.geom);
+    voxel_key_kernel<<<nblk(n), 256, 0, st>>>(d_in, n, cnt, stride, b.geom, b.keys, b.vals);
     int rc = sort_pairs(b, n, st);
     if (rc) return rc;
     run_head_kernel<<<nblk(n + 1), 256, 0, st>>>(b.keys_alt, n, b.head);
@@ -665,16 +671,35 @@ int voxel_grid(FilterBuf& b, const float* d_in, int64_t n, int stride, const flo
                                                    d_out);
     FCHK(hipMemcpyAsync(b.h_small, b.vid + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
     FCHK(hipMemcpyAsync(b.h_small + 1, b.geom, sizeof(VoxelGeom), hipMemcpyDeviceToHost, st));
-    FCHK(hipStreamSynchronize(st));
+    return 0;
+}
+
+// after the stream has drained: the voxel count, or — PCL's "Leaf size is too small ... Integer indices
+// would overflow" — the m input rows copied to the output (returns 1 then; the copy is enqueued, not waited on)
+static int voxel_grid_result(FilterBuf& b, const float* d_in, int64_t m, int stride, float* d_out, int64_t* n_out,
+                             hipStream_t st) {
     VoxelGeom g;
     std::memcpy(&g, b.h_small + 1, sizeof(VoxelGeom));
-    if (g.overflow) {  // PCL: "Leaf size is too small ... Integer indices would overflow" -> output = input
-        copy_strided_kernel<<<nblk(n * stride), 256, 0, st>>>(d_in, n * stride, d_out);
-        FCHK(hipStreamSynchronize(st));
-        *n_out = n;
-        return 0;
+    if (g.overflow) {
+        if (m > 0) copy_strided_kernel<<<nblk(m * stride), 256, 0, st>>>(d_in, m * stride, d_out);
+        FCHK(hipGetLastError());
+        *n_out = m;
+        return 1;
     }
-    *n_out = b.h_small[0];
+    *n_out = (uint32_t)b.h_small[0];
+    return 0;
+}
+
+int voxel_grid(FilterBuf& b, const float* d_in, int64_t n, int stride, const float leaf[3], float* d_out,
+               int64_t* n_out, hipStream_t st) {
+    *n_out = 0;
+    if (n <= 0) return 0;
+    int rc = voxel_grid_enqueue(b, d_in, n, nullptr, stride, leaf, d_out, st);
+    if (rc) return rc;
+    FCHK(hipStreamSynchronize(st));
+    rc = voxel_grid_result(b, d_in, n, stride, d_out, n_out, st);
+    if (rc < 0) return rc;
+    if (rc == 1) FCHK(hipStreamSynchronize(st));
     return 0;
 }
 
@@ -721,42 +746,59 @@ int keyframe_cloud(const float* d_rec, int64_t n, int stride, const PoseArg& ps,
     return 0;
 }
 
+int scan_preprocess_enqueue(FilterBuf& b, const float* d_raw, int64_t n, int stride, const ScanPrepParams& p,
+                            const ImuPose* d_poses, int np, const UndistortEnd& end, float* d_out, hipStream_t st) {
+    b.prep_n = 0;
+    if (n <= 0) return 0;
+    if (stride < 4 || stride > kMaxFields || p.time_field < 3 || p.time_field >= stride || n >= (int64_t)0x7fffffff)
+        return -1;
+    if (reserve(b, n)) return -5;
+    int rc = fgrow(&b.c, b.c_cap, n * stride);
+    if (rc) return rc;
+    // 1. Preprocess selection + 2. stable time sort in one sort over the n rows (the selected first),
+    // 3. gather + undistort; the selected count m stays on the device (b.cnt[0])
+    const int every = p.point_filter_num > 0 ? p.point_filter_num : 1;
+    scan_key_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, every, p.blind * p.blind, p.time_field, b.keys, b.vals);
+    rc = sort_pairs(b, n, st);
+    if (rc) return rc;
+    undistort_gather_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, p.time_field, b.keys_alt, b.vals_alt, d_poses,
+                                                     np, end, b.c, b.cnt);
+    FCHK(hipMemcpyAsync(b.h_small + kHostSel, b.cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    // 4. downSizeFilterSurf
+    b.prep_leaf = p.leaf > 0.f;
+    b.prep_n = n;
+    if (b.prep_leaf) {
+        const float leaf[3] = {p.leaf, p.leaf, p.leaf};
+        return voxel_grid_enqueue(b, b.c, n, b.cnt, stride, leaf, d_out, st);
+    }
+    FCHK(hipMemcpyAsync(d_out, b.c, (size_t)n * stride * sizeof(float), hipMemcpyDeviceToDevice, st));
+    return 0;
+}
+
+int scan_preprocess_finish(FilterBuf& b, int stride, float* d_out, int64_t* n_out, int64_t* n_undist, hipStream_t st) {
+    *n_out = 0;
+    if (n_undist) *n_undist = 0;
+    FCHK(hipStreamSynchronize(st));
+    if (b.prep_n <= 0) return 0;
+    const int64_t m = (uint32_t)b.h_small[kHostSel];
+    if (n_undist) *n_undist = m;
+    if (!b.prep_leaf) {
+        *n_out = m;
+        return 0;
+    }
+    return voxel_grid_result(b, b.c, m, stride, d_out, n_out, st);
+}
+
 int scan_preprocess(FilterBuf& b, const float* d_raw, int64_t n, int stride, const ScanPrepParams& p,
                     const ImuPose* d_poses, int np, const UndistortEnd& end, float* d_out, int64_t* n_out,
                     hipStream_t st, int64_t* n_undist) {
     *n_out = 0;
     if (n_undist) *n_undist = 0;
-    if (n <= 0) return 0;
-    if (stride < 4 || stride > kMaxFields || p.time_field < 3 || p.time_field >= stride) return -1;
-    if (reserve(b, n)) return -5;
-    int rc = fgrow(&b.a, b.a_cap, n * stride);
-    if (!rc) rc = fgrow(&b.c, b.c_cap, n * stride);
+    int rc = scan_preprocess_enqueue(b, d_raw, n, stride, p, d_poses, np, end, d_out, st);
     if (rc) return rc;
-    // 1. Preprocess selection (stable)
-    const int every = p.point_filter_num > 0 ? p.point_filter_num : 1;
-    scan_select_flags_kernel<<<nblk(n + 1), 256, 0, st>>>(d_raw, n, stride, every, p.blind * p.blind, b.head);
-    rc = exscan(b, b.head, b.vid, n + 1, st);
-    if (rc) return rc;
-    compact_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, b.head, b.vid, b.a);
-    FCHK(hipMemcpyAsync(b.h_small, b.vid + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    FCHK(hipStreamSynchronize(st));
-    const int64_t m = (uint32_t)b.h_small[0];
-    if (n_undist) *n_undist = m;
-    if (m == 0) return 0;
-    // 2. sort by time (stable), 3. undistort
-    time_key_kernel<<<nblk(m), 256, 0, st>>>(b.a, m, stride, p.time_field, b.keys, b.vals);
-    rc = sort_pairs(b, m, st);
-    if (rc) return rc;
-    gather_rows_kernel<<<nblk(m), 256, 0, st>>>(b.a, m, stride, b.vals_alt, b.c);
-    if (np >= 2) undistort_kernel<<<nblk(m), 256, 0, st>>>(b.c, m, stride, p.time_field, d_poses, np, end);
-    // 4. downSizeFilterSurf
-    if (p.leaf > 0.f) {
-        const float leaf[3] = {p.leaf, p.leaf, p.leaf};
-        return voxel_grid(b, b.c, m, stride, leaf, d_out, n_out, st);
-    }
-    FCHK(hipMemcpyAsync(d_out, b.c, (size_t)m * stride * sizeof(float), hipMemcpyDeviceToDevice, st));
-    FCHK(hipStreamSynchronize(st));
-    *n_out = m;
+    rc = scan_preprocess_finish(b, stride, d_out, n_out, n_undist, st);
+    if (rc < 0) return rc;
+    if (rc == 1) FCHK(hipStreamSynchronize(st));
     return 0;
 }
 

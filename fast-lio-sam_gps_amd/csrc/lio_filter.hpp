@@ -50,14 +50,20 @@ struct FilterBuf {
     VoxelGeom* geom = nullptr;
     void* tmp = nullptr;
     size_t tmp_bytes = 0;
-    int* h_small = nullptr;  // pinned
+    int* h_small = nullptr;  // pinned: [0] voxel count, [1..] VoxelGeom, [kHostSel] selected count
+    uint32_t* cnt = nullptr; // device: [0] scan_preprocess's selected count
     float* a = nullptr;      // staging records
     int64_t a_cap = 0;
     float* c = nullptr;
     int64_t c_cap = 0;
     void* aux = nullptr;     // caller-side scratch (host API uploads)
     size_t aux_bytes = 0;
+    void* h_stage = nullptr; // pinned host staging of the sweep uploads (lio_capi stage_sweep)
+    size_t stage_bytes = 0;
+    int64_t prep_n = 0;      // row bound of the last scan_preprocess_enqueue (0: nothing pending)
+    bool prep_leaf = false;
 };
+constexpr int kHostSel = 16;
 
 void filter_free(FilterBuf& b);
 // d_out capacity: n * stride floats.  Synchronises the stream (output count).
@@ -72,6 +78,13 @@ int transform_segments(const float* d_in, int64_t n, int stride, const int64_t* 
 int scan_preprocess(FilterBuf& b, const float* d_raw, int64_t n, int stride, const ScanPrepParams& p,
                     const ImuPose* d_poses, int np, const UndistortEnd& end, float* d_out, int64_t* n_out,
                     hipStream_t st, int64_t* n_undist = nullptr);
+// The same in two halves, one host wait: _enqueue queues every stage (d_out and the ctx buffers sized
+// for the row bound n; rows past the count are scratch), _finish waits for the stream and reads the
+// counts.  _finish returns 1 when VoxelGrid's index overflow replaced the output by its input: that
+// copy is queued, not waited on, and the caller's follow-up work on d_out must be queued again.
+int scan_preprocess_enqueue(FilterBuf& b, const float* d_raw, int64_t n, int stride, const ScanPrepParams& p,
+                            const ImuPose* d_poses, int np, const UndistortEnd& end, float* d_out, hipStream_t st);
+int scan_preprocess_finish(FilterBuf& b, int stride, float* d_out, int64_t* n_out, int64_t* n_undist, hipStream_t st);
 
 int records_to_xyz(const float* d_rec, int64_t n, int stride, float* d_xyz, hipStream_t st);
 

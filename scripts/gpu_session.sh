@@ -60,6 +60,9 @@ for s in $STEPS; do
            run pmcsq_icp 300 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmcsq_icp" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
            python scripts/pmc_sq_summary.py "$OUT/pmcsq_c3" "$OUT/pmcsq_c3.json" > "$OUT/pmcsq_c3_summary.txt" 2>&1;
            python scripts/pmc_sq_summary.py "$OUT/pmcsq_icp" "$OUT/pmcsq_icp.json" > "$OUT/pmcsq_icp_summary.txt" 2>&1; true ;;
+    prep)  runs pytest_prep 600 python -u -m pytest tests/test_gpu_filters.py tests/test_gpu_formats.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread &&
+           run prep_time 300 bash -c 'python scripts/prep_timing.py 80 && LIO_PREP_UPLOAD=full python scripts/prep_timing.py 80 && LIO_GPU_LIB=build_ab/pre_setup/liblio_gpu.so python scripts/prep_timing.py 80' &&
+           run rocprof_prep 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof_prep" -o run --output-format csv -- python scripts/prep_timing.py 40 ;;
     maprec) runs pytest_maprec 600 python -u -m pytest tests/test_gpu_map.py tests/test_gpu_pipeline.py -x -v -p no:cacheprovider --timeout 500 --timeout-method thread ;;
     fid)   runs pytest_fid 900 python -u -m pytest tests/test_gpu_seqsum.py tests/test_gpu_icp.py -k "seqsum or fidelity or double" -x -v -s -p no:cacheprovider --timeout 300 --timeout-method thread &&
            run icp_fid_time 300 env LIO_ICP_ORDER=2 python scripts/icp_ab.py 1.0 5 &&

@@ -99,3 +99,38 @@ def test_scan_preprocess_into_ctx(oracle):
     p24[12:21] = np.eye(3).ravel()
     hm(p24, True)
     np.testing.assert_array_equal(hm.world(), o[:, :3])
+
+
+def test_preprocess_staged_upload_edges(oracle):
+    """The staged upload (rows i % point_filter_num == 0 packed on the host, one DMA) and the single host
+    wait: ragged row counts, wider records, nothing selected, one row, VoxelGrid's index overflow (output =
+    the undistorted input) and the staging buffer growing and shrinking between calls — each bit-exact
+    against the oracle, through the filter API and into a ctx (feats_down_body and feats_undistort)."""
+    scene = synth.make_scene(400.0, 1234)
+    raw, poses, end24 = synth.make_raw_scan(scene, 120_000, seed=8)
+    end = F.pose_from_pose24(end24)
+    rng = np.random.default_rng(3)
+    wide = np.concatenate([raw[:, :4], rng.uniform(0, 1, (len(raw), 1)).astype(f32), raw[:, 4:5]], axis=1)
+    m = synth.sample_surface(scene, 100_000, 1234)
+    tree = F.IkdTreeGPU(cell_size=1.0)
+    tree.Build(m)
+    hm = F.HShareModelGPU(tree)
+    cases = [(raw[:120_001 - 7], 3, 2.0, 0.5, 4), (raw[:5_000], 4, 2.0, 0.5, 4), (wide[:60_017], 5, 2.0, 0.5, 5),
+             (raw[:1], 1, 0.0, 0.5, 4), (raw[:2_000], 4, 1e4, 0.5, 4), (raw[:40_000], 2, 2.0, 1e-4, 4),
+             (raw, 4, 2.0, 0.0, 4), (raw[:777], 7, 2.0, 0.3, 4)]
+    for rows, every, blind, leaf, tf in cases:
+        end_tf = end
+        o_down = oracle.preprocess(rows, poses, end24, point_filter_num=every, blind=blind, leaf=leaf, time_field=tf)
+        o_und = oracle.preprocess(rows, poses, end24, point_filter_num=every, blind=blind, leaf=0.0, time_field=tf)
+        pp = FL.ScanPreprocessor(point_filter_num=every, blind=blind, filter_size_surf=leaf, time_field=tf)
+        _close(pp.process(rows, poses, end_tf), o_down)
+        n = hm.preprocess_scan(rows, poses, end_tf, point_filter_num=every, blind=blind, filter_size_surf=leaf,
+                               time_field=tf)
+        assert n == len(o_down), (len(rows), every, blind, leaf)
+        _close(hm.undistorted(), o_und)
+        if n:
+            p24 = np.zeros(24)
+            p24[0:9] = np.eye(3).ravel()
+            p24[12:21] = np.eye(3).ravel()
+            hm(p24, True)
+            np.testing.assert_array_equal(hm.world(), o_down[:, :3])
