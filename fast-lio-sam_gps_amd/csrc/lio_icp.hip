@@ -290,52 +290,75 @@ struct CellBox {
 // S inside N or empty).  With a finite bound B, rows whose (y, z) gap to the
 // tile box exceeds sqrt(B) are skipped and each row's x-range is trimmed to
 // [qx0 - r, qx1 + r], r = sqrt(B - gap^2) (conservatively rounded).
+// Row r of box N (y fastest) minus the cells of box S: its point ranges [b0, b0+n0), [b1, b1+n1) and the
+// squared (y, z) gap g2 of the row to the tile box qb
+__device__ __forceinline__ void row_pieces(const GridDev& g, const CellBox& N, const CellBox& S, float B,
+                                           const float (&qb)[6], int r, uint32_t& b0, uint32_t& n0, uint32_t& b1,
+                                           uint32_t& n1, float& g2) {
+    const float cs = g.cell, m = g.margin;
+    const int ny = N.y1 - N.y0 + 1;
+    const bool sempty = S.x0 > S.x1;
+    const uint32_t gnx = (uint32_t)g.nx, gnxy = (uint32_t)g.nx * (uint32_t)g.ny;
+    const int rz = N.z0 + r / ny, ry = N.y0 + r % ny;
+    int x0 = N.x0, x1 = N.x1;
+    bool keep = true;
+    const float yl = g.oy + (float)ry * cs - m, zl = g.oz + (float)rz * cs - m;
+    g2 = interval_gap(yl, yl + cs + 2.f * m, qb[2], qb[3]) + interval_gap(zl, zl + cs + 2.f * m, qb[4], qb[5]);
+    if (B < INFINITY) {
+        if (g2 * 0.999999f > B) {
+            keep = false;
+        } else {
+            const float rx = sqrtf(fmaxf(B - g2 * 0.999999f, 0.f)) * 1.00001f + m;
+            x0 = max(x0, cell_coord(qb[0] - rx, g.ox, g.inv_cell));
+            x1 = min(x1, cell_coord(qb[1] + rx, g.ox, g.inv_cell));
+        }
+    }
+    if (keep && x0 <= x1) {
+        const uint32_t rowc = (uint32_t)rz * gnxy + (uint32_t)ry * gnx;
+        const bool inS = !sempty && ry >= S.y0 && ry <= S.y1 && rz >= S.z0 && rz <= S.z1;
+        // piece left of S (or the whole row), piece right of S
+        const int lx1 = inS ? min(x1, S.x0 - 1) : x1;
+        if (x0 <= lx1) {
+            b0 = g.start[rowc + (uint32_t)x0];
+            n0 = g.start[rowc + (uint32_t)lx1 + 1] - b0;
+        }
+        const int rx0 = max(x0, S.x1 + 1);
+        if (inS && rx0 <= x1) {
+            b1 = g.start[rowc + (uint32_t)rx0];
+            n1 = g.start[rowc + (uint32_t)x1 + 1] - b1;
+        }
+    }
+}
+
+// candidates scan_rows would stream for (N, S, B): wave-uniform, the row table only (no points read)
+__device__ uint32_t count_rows(const GridDev& g, const CellBox& N, const CellBox& S, float B, const float (&qb)[6]) {
+    const int lane = threadIdx.x & 63;
+    const int nrows = (N.y1 - N.y0 + 1) * (N.z1 - N.z0 + 1);
+    uint32_t tot = 0;
+#pragma unroll 1
+    for (int rb = 0; rb < nrows; rb += kIcpTileQ) {
+        uint32_t b0 = 0, n0 = 0, b1 = 0, n1 = 0;
+        float g2 = INFINITY;
+        if (rb + lane < nrows) row_pieces(g, N, S, B, qb, rb + lane, b0, n0, b1, n1, g2);
+        tot += (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_dpp(n0 + n1), 63);
+    }
+    return tot;
+}
+
 template <int NW>
 __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const CellBox& S, float B, float qx0, float qx1,
                           float qy0, float qy1, float qz0, float qz1, bool act, float x, float y, float z,
                           uint64_t& best, unsigned long long& cand, uint32_t& tested) {
     const int lane = threadIdx.x & 63;
-    const float cs = g.cell, m = g.margin;
+    const float cs = g.cell;
     const float qb[6] = {qx0, qx1, qy0, qy1, qz0, qz1};
-    const int ny = N.y1 - N.y0 + 1, nrows = ny * (N.z1 - N.z0 + 1);
-    const bool sempty = S.x0 > S.x1;
-    const uint32_t gnx = (uint32_t)g.nx, gnxy = (uint32_t)g.nx * (uint32_t)g.ny;
+    const int nrows = (N.y1 - N.y0 + 1) * (N.z1 - N.z0 + 1);
 #pragma unroll 1
     for (int rb = 0; rb < nrows; rb += kIcpTileQ) {
         const int r = rb + lane;
         uint32_t b0 = 0, n0 = 0, b1 = 0, n1 = 0;
         float g2 = INFINITY;
-        if (r < nrows) {
-            const int rz = N.z0 + r / ny, ry = N.y0 + r % ny;
-            int x0 = N.x0, x1 = N.x1;
-            bool keep = true;
-            const float yl = g.oy + (float)ry * cs - m, zl = g.oz + (float)rz * cs - m;
-            g2 = interval_gap(yl, yl + cs + 2.f * m, qy0, qy1) + interval_gap(zl, zl + cs + 2.f * m, qz0, qz1);
-            if (B < INFINITY) {
-                if (g2 * 0.999999f > B) {
-                    keep = false;
-                } else {
-                    const float rx = sqrtf(fmaxf(B - g2 * 0.999999f, 0.f)) * 1.00001f + m;
-                    x0 = max(x0, cell_coord(qx0 - rx, g.ox, g.inv_cell));
-                    x1 = min(x1, cell_coord(qx1 + rx, g.ox, g.inv_cell));
-                }
-            }
-            if (keep && x0 <= x1) {
-                const uint32_t rowc = (uint32_t)rz * gnxy + (uint32_t)ry * gnx;
-                const bool inS = !sempty && ry >= S.y0 && ry <= S.y1 && rz >= S.z0 && rz <= S.z1;
-                // piece left of S (or the whole row), piece right of S
-                const int lx1 = inS ? min(x1, S.x0 - 1) : x1;
-                if (x0 <= lx1) {
-                    b0 = g.start[rowc + (uint32_t)x0];
-                    n0 = g.start[rowc + (uint32_t)lx1 + 1] - b0;
-                }
-                const int rx0 = max(x0, S.x1 + 1);
-                if (inS && rx0 <= x1) {
-                    b1 = g.start[rowc + (uint32_t)rx0];
-                    n1 = g.start[rowc + (uint32_t)x1 + 1] - b1;
-                }
-            }
-        }
+        if (r < nrows) row_pieces(g, N, S, B, qb, r, b0, n0, b1, n1, g2);
         // nearest rows first (stable partition by the row's (y, z) gap to the tile box: 0, <= 1,
         // <= 2 cells, farther), so the staging filter's bound tightens early in the stream; any
         // order gives the same minima (total order on (d2, id))
@@ -372,22 +395,15 @@ __device__ __forceinline__ uint64_t tile_min(uint64_t best, uint64_t* s_best) {
     return best;
 }
 
-// NW waves split one tile's candidate stream (block-level merges), or (NW = 1) TPB
-// independent one-wave tiles share a block — more tiles resident per CU than one-wave
-// blocks allow, and no block barrier couples them.
-template <int NW, int TPB>
-__global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs a, int ntiles) {
-    static_assert(NW == 1 || TPB == 1, "icp_tile_kernel: several waves per tile or several tiles per block");
-    __shared__ TileLds Ls[NW * TPB];
-    __shared__ uint64_t s_best[NW > 1 ? NW * kIcpTileQ : 1];  // cross-wave merge (NW > 1 only)
+// One tile's exact 1-NN.  NW waves split the tile's candidate stream (block-level merges).  DEFER (the
+// main launch of a pass without previous correspondences): a tile whose final box holds more than
+// a.defer_cand candidates stops after its bound, leaves each lane's best as the prior (nn_id / nn_d2,
+// cur transformed), and queues itself on a.heavy for icp_heavy_kernel, which splits its stream over
+// kIcpHeavyNW waves on an otherwise idle chip — the first pass's tail is a few such tiles, each
+// one wave sharing its SIMD with seven others (profiles/r03_icp_tile_timeline.txt).
+template <int NW, bool DEFER>
+__device__ __forceinline__ void icp_tile_body(const IcpArgs& a, int tix, TileLds& L, uint64_t* s_best) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    TileLds& L = Ls[wv];
-    // this wave's tile: its XCD's next tile in cell order (first pass) or in the per-XCD longest-first
-    // order of the previous pass's costs (icp_tile_of)
-    static_assert(TPB == 1, "icp_tile_kernel: one tile per block (icp_tile_of)");
-    (void)wv;
-    const int tix = icp_tile_of(a.order, (int)blockIdx.x, ntiles);
-    if (tix < 0) return;  // block-uniform: a slot past its XCD's share
 #ifdef LIO_DIAG
     const uint64_t t_start = wall_clock64();  // per-tile timeline (diagnostics build)
 #endif
@@ -453,6 +469,27 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
         // the scanned box may stick out of N (a grown box): clip it, the part outside N is not needed
         CellBox Sc{max(S.x0, N.x0), min(S.x1, N.x1), max(S.y0, N.y0), min(S.y1, N.y1), max(S.z0, N.z0), min(S.z1, N.z1)};
         if (Sc.y0 > Sc.y1 || Sc.z0 > Sc.z1) Sc.x0 = 1, Sc.x1 = 0;
+        if constexpr (DEFER) {
+            if (!grow) {
+                const float qb[6] = {qx0, qx1, qy0, qy1, qz0, qz1};
+                if (count_rows(g, N, Sc, B, qb) > a.defer_cand) {  // wave-uniform
+                    if (act) {
+                        if (a.fitness || a.apply_T) {
+                            a.cur[3 * i] = x;
+                            a.cur[3 * i + 1] = y;
+                            a.cur[3 * i + 2] = z;
+                        }
+                        a.nn_d2[i] = __uint_as_float((uint32_t)(best >> 32));
+                        a.nn_id[i] = (int)(uint32_t)best;
+                    }
+                    if (lane == 0) {
+                        a.heavy[2 + atomicAdd(a.heavy, 1u)] = (uint32_t)tix;
+                        if (a.dbg) atomicAdd(a.dbg + 5, 1ull);
+                    }
+                    return;
+                }
+            }
+        }
         scan_rows<NW>(g, L, N, Sc, B, qx0, qx1, qy0, qy1, qz0, qz1, act, x, y, z, best, cand, tested);
         best = tile_min<NW>(best, s_best);
         ++rounds;
@@ -498,6 +535,33 @@ __global__ void __launch_bounds__(kIcpTileQ * NW * TPB) icp_tile_kernel(IcpArgs 
     }
 }
 
+
+// the main launch: one wave per tile, tile = its XCD's next one (icp_tile_of)
+template <bool DEFER>
+__global__ void __launch_bounds__(kIcpTileQ) __attribute__((amdgpu_waves_per_eu(7))) icp_tile_kernel(IcpArgs a, int ntiles) {
+    __shared__ TileLds L;
+    const int tix = icp_tile_of(a.order, (int)blockIdx.x, ntiles);
+    if (tix < 0) return;  // block-uniform: a slot past its XCD's share
+    icp_tile_body<1, DEFER>(a, tix, L, nullptr);
+}
+
+// the deferred tiles (a.heavy: [0] count, [1] finish ticket, [2 ..] tiles), kIcpHeavyNW waves each; the
+// last block to finish clears the count and the ticket for the next pass
+constexpr int kIcpHeavyNW = 8, kIcpHeavyBlocks = 256;
+__global__ void __launch_bounds__(kIcpTileQ * kIcpHeavyNW) icp_heavy_kernel(IcpArgs a) {
+    __shared__ TileLds Ls[kIcpHeavyNW];
+    __shared__ uint64_t s_best[kIcpHeavyNW * kIcpTileQ];
+    const int nh = (int)a.heavy[0];
+    for (int h = blockIdx.x; h < nh; h += gridDim.x)
+        icp_tile_body<kIcpHeavyNW, false>(a, (int)a.heavy[2 + h], Ls[threadIdx.x >> 6], s_best);
+    if (threadIdx.x == 0) {
+        __threadfence();
+        if (atomicAdd(a.heavy + 1, 1u) == gridDim.x - 1) {
+            a.heavy[0] = 0u;
+            a.heavy[1] = 0u;
+        }
+    }
+}
 
 // One block = one 4096-point record -> super[record][kIcpStride]: each lane
 // accumulates its 4 points (record-relative index lane + 1024 k, k ascending),
@@ -574,7 +638,16 @@ __global__ void __launch_bounds__(kIcpStatsThreads) icp_stats_kernel(IcpArgs a, 
 void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st) {
     if (a.n == 0 || ntiles == 0) return;
     const int seg = (ntiles + kIcpSegs - 1) / kIcpSegs;
-    icp_tile_kernel<1, 1><<<8 * (kIcpSegs / 8) * seg, kIcpTileQ, 0, st>>>(a, ntiles);
+    const int grid = 8 * (kIcpSegs / 8) * seg;
+    if (!a.heavy || a.defer_cand == 0 || a.prior) {
+        icp_tile_kernel<false><<<grid, kIcpTileQ, 0, st>>>(a, ntiles);
+        return;
+    }
+    icp_tile_kernel<true><<<grid, kIcpTileQ, 0, st>>>(a, ntiles);
+    IcpArgs h = a;  // the deferred tiles resume from the bounds they left (cur already transformed)
+    h.apply_T = 0;
+    h.prior = 1;
+    icp_heavy_kernel<<<kIcpHeavyBlocks, kIcpTileQ * kIcpHeavyNW, 0, st>>>(h);
 }
 
 // Tile order for the next pass from this pass's candidate counts.  The cell-ordered tiles are cut

@@ -318,6 +318,8 @@ struct lio_icp {
     bool have_prior = false;  // nn ids of this alignment's previous pass are in d_fid
     uint32_t* d_tcost = nullptr;  // per tile: candidates of the last pass
     uint32_t* d_order = nullptr;  // longest-first tile order (valid when have_order)
+    uint32_t* d_heavy = nullptr;  // first-pass deferred tiles (lio_icp.hip icp_heavy_kernel)
+    int64_t defer_cand = -1;      // lio_icp_set_defer_threshold; -1: icp_defer_cand()
     bool have_order = false;
     unsigned long long* d_dbg = nullptr;  // search counters (diagnostics build: LIO_DIAG + LIO_ICP_DEBUG)
     size_t dbg_bytes = 0;
@@ -405,7 +407,7 @@ int lio_icp_destroy(lio_icp* h) {
     lio::grid_free(h->tgt);
     lio::grid_free(h->qgrid);
     void* ptrs[] = {h->d_tgt,   h->d_src,     h->d_cur,  h->d_fd2,   h->d_fid,   h->d_tiles, h->d_tscratch,
-                    h->d_ttmp,  h->d_dbg,     h->d_tcost, h->d_order, h->d_pcl16};
+                    h->d_ttmp,  h->d_dbg,     h->d_tcost, h->d_order, h->d_pcl16, h->d_heavy};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (h->h_super) (void)hipHostFree(h->h_super);
@@ -587,7 +589,7 @@ static int icp_prepare(lio_icp* h) {
     const int64_t n = std::max<int64_t>(h->sh_n, 1);
     if (n > h->cap) {
         void** ptrs[] = {(void**)&h->d_src,   (void**)&h->d_cur,   (void**)&h->d_fd2,  (void**)&h->d_fid,
-                         (void**)&h->d_tiles, (void**)&h->d_tcost, (void**)&h->d_order};
+                         (void**)&h->d_tiles, (void**)&h->d_tcost, (void**)&h->d_order, (void**)&h->d_heavy};
         h->cap = 0;  // a failed allocation below leaves no buffer that looks usable (and nothing freed twice)
         for (void** q : ptrs) {
             if (*q) (void)hipFree(*q);
@@ -600,6 +602,8 @@ static int icp_prepare(lio_icp* h) {
         IHIP(hipMalloc(&h->d_tiles, (n + n / lio::kIcpTileQ + 1) * sizeof(uint2)));
         IHIP(hipMalloc(&h->d_tcost, (n + n / lio::kIcpTileQ + 1) * sizeof(uint32_t)));
         IHIP(hipMalloc(&h->d_order, (n + n / lio::kIcpTileQ + 64) * sizeof(uint32_t)));  // + the 9 share offsets
+        IHIP(hipMalloc(&h->d_heavy, (n + n / lio::kIcpTileQ + 3) * sizeof(uint32_t)));
+        IHIP(hipMemsetAsync(h->d_heavy, 0, 2 * sizeof(uint32_t), h->st));  // count and ticket: zero between passes
         h->cap = n;
     }
     const int64_t nsup_all = (h->ns + lio::kIcpSuper - 1) / lio::kIcpSuper + 1;
@@ -691,6 +695,17 @@ static int pcl_finish(lio_icp* h, const lio::IcpArgs& a) {
     return LIO_OK;
 }
 
+// A pass without previous correspondences defers the tiles whose final box streams more candidates than
+// this to a second launch with several waves per tile (lio_icp.hip icp_heavy_kernel); LIO_ICP_DEFER
+// overrides it (0: off) for A/B runs
+static uint32_t icp_defer_cand() {
+    static const uint32_t v = [] {
+        const char* e = std::getenv("LIO_ICP_DEFER");
+        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 3072u;
+    }();
+    return v;
+}
+
 // One correspondence (or fitness) pass: GPU kernels + exchange + ordered sum.
 static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, double max_d2, double out17[17],
                     float* pcl16 = nullptr) {
@@ -713,6 +728,8 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     a.tiles = h->d_tiles;
     a.tile_cost = h->d_tcost;
     a.order = h->have_order ? h->d_order : nullptr;
+    a.heavy = h->d_heavy;
+    a.defer_cand = h->defer_cand >= 0 ? (uint32_t)h->defer_cand : icp_defer_cand();
 #ifdef LIO_DIAG
     static const bool dbg_on = std::getenv("LIO_ICP_DEBUG") != nullptr;  // diagnostics build: search statistics
     if (dbg_on) {
@@ -770,11 +787,12 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     if (!fitness && h->sh_n > 0) h->have_order = true;
 #ifdef LIO_DIAG
     if (dbg_on) {
-        unsigned long long c[5];
+        unsigned long long c[6];
         IHIP(hipMemcpy(c, h->d_dbg, sizeof(c), hipMemcpyDeviceToHost));
         std::fprintf(stderr,
-                     "icp dbg: tiles|waves %llu lanes %llu cand/tile %.1f tested/tile %.1f rounds/tile %.2f cand/lane %.1f\n",
-                     c[2], c[3], (double)c[0] / c[2], (double)c[4] / c[2], (double)c[1] / c[2], (double)c[0] / c[3]);
+                     "icp dbg: tiles|waves %llu lanes %llu cand/tile %.1f tested/tile %.1f rounds/tile %.2f cand/lane %.1f "
+                     "deferred %llu\n",
+                     c[2], c[3], (double)c[0] / c[2], (double)c[4] / c[2], (double)c[1] / c[2], (double)c[0] / c[3], c[5]);
         // per-tile timeline (wall clock, 100 MHz): span, duration percentiles, the tail
         std::vector<unsigned long long> tt(2 * (size_t)h->ntiles);
         std::vector<uint32_t> cost(h->ntiles);
@@ -871,6 +889,12 @@ extern "C" int lio_icp_set_fidelity_debug(lio_icp* h, int flags, int64_t evcap) 
     if (!h || evcap < 0) return ifail(LIO_ERR_ARG, "lio_icp_set_fidelity_debug: bad arguments");
     h->fid_flags = flags;
     h->fid_evcap = evcap;
+    return LIO_OK;
+}
+
+extern "C" int lio_icp_set_defer_threshold(lio_icp* h, int64_t candidates) {
+    if (!h || candidates < -1 || candidates > 0xffffffffll) return ifail(LIO_ERR_ARG, "lio_icp_set_defer_threshold: bad arguments");
+    h->defer_cand = candidates;
     return LIO_OK;
 }
 
