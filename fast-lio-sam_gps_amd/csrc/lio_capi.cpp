@@ -1129,6 +1129,49 @@ static int stage_sweep(lio::FilterBuf& b, const void* rows, int64_t n, size_t ro
     return LIO_OK;
 }
 
+// Float records: Preprocess's whole selection made while packing (the host reads every row here anyway) —
+// i % point_filter_num == 0 and x*x + y*y + z*z > blind^2, in float and in that order as the device's
+// scan_key_kernel — so the device gets exactly the m selected rows, in input order; *sorted says whether
+// their times are non-decreasing (the stable time sort is then the identity and the device skips it).
+static int stage_sweep_select(lio::FilterBuf& b, const float* raw, int64_t n, int stride, const lio_scan_prep_params* p,
+                              const lio_imu_pose* poses, int np, int64_t* m, size_t* pose_off, bool* sorted) {
+    const int every = std::max(p->point_filter_num, 1);
+    const int64_t ub = (n + every - 1) / every;
+    *pose_off = ((size_t)ub * stride * sizeof(float) + 255) & ~(size_t)255;
+    const size_t need = *pose_off + (size_t)np * sizeof(lio_imu_pose);
+    if (need > b.stage_bytes || !b.h_stage) {
+        if (b.h_stage) (void)hipHostFree(b.h_stage);
+        b.h_stage = nullptr;
+        const size_t c = std::max(need, b.stage_bytes + b.stage_bytes / 2);
+        if (hipHostMalloc(&b.h_stage, c) != hipSuccess) {
+            b.stage_bytes = 0;
+            return fail(LIO_ERR_NOMEM, "sweep staging: hipHostMalloc failed");
+        }
+        b.stage_bytes = c;
+    }
+    const float blind2 = p->blind * p->blind;
+    const int tf = p->time_field;
+    auto* d = static_cast<float*>(b.h_stage);
+    int64_t k = 0;
+    uint32_t prev = 0;
+    bool sorted_ = true;
+    for (int64_t i = 0; i < n; i += every) {
+        const float* q = raw + i * stride;
+        if (!((q[0] * q[0] + q[1] * q[1] + q[2] * q[2]) > blind2)) continue;
+        uint32_t tb;
+        std::memcpy(&tb, &q[tf], 4);
+        const uint32_t key = (tb & 0x80000000u) ? ~tb : (tb | 0x80000000u);  // scan_key_kernel's time key
+        sorted_ = sorted_ && prev <= key;
+        prev = key;
+        for (int f = 0; f < stride; ++f) d[k * stride + f] = q[f];
+        ++k;
+    }
+    if (np) std::memcpy(static_cast<uint8_t*>(b.h_stage) + *pose_off, poses, (size_t)np * sizeof(lio_imu_pose));
+    *m = k;
+    *sorted = sorted_;
+    return LIO_OK;
+}
+
 int lio_filter_create(int device, lio_filter** out) {
     if (!out) return fail(LIO_ERR_ARG, "out is NULL");
     *out = nullptr;
@@ -1233,11 +1276,13 @@ int lio_preprocess(lio_filter* f, const float* raw, int64_t n, int stride, const
     lio::ScanPrepParams sp{p->point_filter_num, p->blind, p->filter_size_surf, p->time_field};
     int64_t rows = n;
     size_t pose_off = 0;
+    int presel = -1;
     if (!full) {
-        rc = stage_sweep(f->b, raw, n, (size_t)stride * sizeof(float), p->point_filter_num, poses, n_poses, &rows,
-                         &pose_off);
+        bool sorted = false;
+        rc = stage_sweep_select(f->b, raw, n, stride, p, poses, n_poses, &rows, &pose_off, &sorted);
         if (rc) return rc;
-        sp.point_filter_num = 1;
+        presel = sorted ? 1 : 0;
+        if (rows == 0) return LIO_OK;
     }
     rc = grow(&f->d_in, f->in_cap, rows * stride);
     if (!rc) rc = grow(&f->d_out, f->out_cap, rows * stride);
@@ -1250,9 +1295,13 @@ int lio_preprocess(lio_filter* f, const float* raw, int64_t n, int stride, const
         HIP_TRY(hipMemcpyAsync(f->d_poses, full ? (const void*)poses : stage + pose_off,
                                (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
     int64_t m = 0;
-    rc = lio::scan_preprocess_enqueue(f->b, f->d_in, rows, stride, sp, f->d_poses, n_poses, undistort_end(end),
-                                      f->d_out, st);
-    if (!rc) rc = lio::scan_preprocess_finish(f->b, stride, f->d_out, &m, nullptr, st);
+    rc = 2;
+    for (int attempt = 0; attempt < 2 && rc == 2; ++attempt) {  // 2: the voxel key width was learnt too narrow
+        rc = lio::scan_preprocess_enqueue(f->b, f->d_in, rows, stride, sp, f->d_poses, n_poses, undistort_end(end),
+                                          f->d_out, st, presel);
+        if (!rc) rc = lio::scan_preprocess_finish(f->b, stride, f->d_out, &m, nullptr, st);
+    }
+    if (rc == 2) rc = -2;
     if (rc < 0) {
         (void)hipStreamSynchronize(st);  // the staging buffer is reused by the next call
         return filter_status(rc, "lio_preprocess");
@@ -1266,24 +1315,26 @@ int lio_preprocess(lio_filter* f, const float* raw, int64_t n, int stride, const
 // the device half shared by lio_scan_preprocess and lio_scan_preprocess_cloud2: c->d_raw holds `rows`
 // records; every stage is queued, the scan buffers set up behind it, and the host waits once
 static int scan_prep_device(lio_ctx* c, int64_t rows, int stride, const lio::ScanPrepParams& sp, int n_poses,
-                            const lio_pose* end, int64_t* n_down, const char* what) {
+                            const lio_pose* end, int64_t* n_down, const char* what, int presel = -1) {
     hipStream_t st = c->map->st;
     c->undist_n = -1;
     auto bail = [&](int r) {
         (void)hipStreamSynchronize(st);  // nothing queued may outlive the call (the staging buffer is reused)
         return r;
     };
-    int rc = lio::scan_preprocess_enqueue(c->filt, c->d_raw, rows, stride, sp, c->d_poses, n_poses,
-                                          undistort_end(end), c->d_rec, st);
-    if (rc) return bail(filter_status(rc, what));
-    rc = ctx_reserve(c, rows);  // sized for the row bound; c->n set to the count below
+    int rc = ctx_reserve(c, rows);  // sized for the row bound; c->n set to the count below
     if (rc) return bail(rc);
-    rc = lio::records_to_xyz(c->d_rec, rows, stride, c->d_body, st);
-    if (rc) return bail(filter_status(rc, what));
-    if (hipMemsetAsync(c->d_sel, 0, (size_t)std::max<int64_t>(rows, 1), st) != hipSuccess)
-        return bail(fail(LIO_ERR_HIP, std::string(what) + ": memset failed"));
     int64_t m = 0, mu = 0;
-    rc = lio::scan_preprocess_finish(c->filt, stride, c->d_rec, &m, &mu, st);
+    rc = 2;
+    for (int attempt = 0; attempt < 2 && rc == 2; ++attempt) {  // 2: the voxel key width was learnt too narrow
+        rc = lio::scan_preprocess_enqueue(c->filt, c->d_raw, rows, stride, sp, c->d_poses, n_poses,
+                                          undistort_end(end), c->d_rec, st, presel);
+        if (rc) return bail(filter_status(rc, what));
+        rc = lio::records_to_xyz_sel(c->d_rec, rows, stride, c->d_body, c->d_sel, st);
+        if (rc) return bail(filter_status(rc, what));
+        rc = lio::scan_preprocess_finish(c->filt, stride, c->d_rec, &m, &mu, st);
+    }
+    if (rc == 2) rc = -2;
     if (rc < 0) return bail(filter_status(rc, what));
     if (rc == 1) {  // VoxelGrid index overflow: the output is the undistorted input, its xyz again
         rc = lio::records_to_xyz(c->d_rec, m, stride, c->d_body, st);
@@ -1308,11 +1359,12 @@ int lio_scan_preprocess(lio_ctx* c, const float* raw, int64_t n, int stride, con
     lio::ScanPrepParams sp{p->point_filter_num, p->blind, p->filter_size_surf, p->time_field};
     int64_t rows = n;
     size_t pose_off = 0;
+    int presel = -1;
     if (!full) {
-        rc = stage_sweep(c->filt, raw, n, (size_t)stride * sizeof(float), p->point_filter_num, poses, n_poses, &rows,
-                         &pose_off);
+        bool sorted = false;
+        rc = stage_sweep_select(c->filt, raw, n, stride, p, poses, n_poses, &rows, &pose_off, &sorted);
         if (rc) return rc;
-        sp.point_filter_num = 1;
+        presel = sorted ? 1 : 0;
     }
     rc = grow(&c->d_raw, c->raw_cap, std::max<int64_t>(rows, 1) * stride);
     if (!rc) rc = grow(&c->d_rec, c->rec_cap, std::max<int64_t>(rows, 1) * stride);
@@ -1325,7 +1377,7 @@ int lio_scan_preprocess(lio_ctx* c, const float* raw, int64_t n, int stride, con
     if (n_poses)
         HIP_TRY(hipMemcpyAsync(c->d_poses, full ? (const void*)poses : stage + pose_off,
                                (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
-    return scan_prep_device(c, rows, stride, sp, n_poses, end, n_down, "lio_scan_preprocess");
+    return scan_prep_device(c, rows, stride, sp, n_poses, end, n_down, "lio_scan_preprocess", presel);
 }
 
 int lio_scan_get_undistorted(lio_ctx* c, float* out, int64_t cap_points, int64_t* n_points, int* stride) {

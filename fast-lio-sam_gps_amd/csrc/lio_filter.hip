@@ -57,10 +57,14 @@ __device__ __forceinline__ void block_minmax(float (*s)[256], const float* lo, c
 //   div_b = max_b - min_b + 1; divb_mul = (1, div_b.x, div_b.x * div_b.y)
 //   overflow when div_b.x * div_b.y * div_b.z > INT_MAX (PCL then returns the input)
 // cnt (optional): the rows in use, <= n (the bound the grid is sized for)
+// SINGLE: one block covers the input (small clouds: no partials, no ticket, no fence); out_host: a
+// host-mapped copy of the geometry
+template <bool SINGLE>
 __global__ void __launch_bounds__(256) minmax_geom_kernel(const float* __restrict__ p, int64_t n,
                                                           const uint32_t* __restrict__ cnt, int stride,
                                                           float* __restrict__ part, unsigned* __restrict__ ticket,
-                                                          float lx, float ly, float lz, VoxelGeom* __restrict__ out) {
+                                                          float lx, float ly, float lz, VoxelGeom* __restrict__ out,
+                                                          VoxelGeom* __restrict__ out_host) {
     __shared__ float s[6][256];
     __shared__ bool last;
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
@@ -77,26 +81,28 @@ __global__ void __launch_bounds__(256) minmax_geom_kernel(const float* __restric
         hi[2] = fmaxf(hi[2], z);
     }
     block_minmax(s, lo, hi);
-    if (threadIdx.x < 6) part[blockIdx.x * 6 + threadIdx.x] = s[threadIdx.x][0];
-    __threadfence();
-    __syncthreads();
-    if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    const volatile float* vp = part;  // the other blocks' partials, past this CU's cache
-    for (int d = 0; d < 3; ++d) lo[d] = INFINITY, hi[d] = -INFINITY;
-    for (int b = threadIdx.x; b < (int)gridDim.x; b += 256) {
+    if constexpr (!SINGLE) {
+        if (threadIdx.x < 6) part[blockIdx.x * 6 + threadIdx.x] = s[threadIdx.x][0];
+        __threadfence();
+        __syncthreads();
+        if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == gridDim.x - 1;
+        __syncthreads();
+        if (!last) return;
+        __threadfence();
+        const volatile float* vp = part;  // the other blocks' partials, past this CU's cache
+        for (int d = 0; d < 3; ++d) lo[d] = INFINITY, hi[d] = -INFINITY;
+        for (int b = threadIdx.x; b < (int)gridDim.x; b += 256) {
 #pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            lo[d] = fminf(lo[d], vp[b * 6 + d]);
-            hi[d] = fmaxf(hi[d], vp[b * 6 + 3 + d]);
+            for (int d = 0; d < 3; ++d) {
+                lo[d] = fminf(lo[d], vp[b * 6 + d]);
+                hi[d] = fmaxf(hi[d], vp[b * 6 + 3 + d]);
+            }
         }
+        __syncthreads();
+        block_minmax(s, lo, hi);
     }
-    __syncthreads();
-    block_minmax(s, lo, hi);
     if (threadIdx.x != 0) return;
-    ticket[0] = 0u;
+    if constexpr (!SINGLE) ticket[0] = 0u;
     VoxelGeom g;
     const float inv[3] = {1.0f / lx, 1.0f / ly, 1.0f / lz};
     int64_t div[3];
@@ -111,14 +117,21 @@ __global__ void __launch_bounds__(256) minmax_geom_kernel(const float* __restric
     g.mul[0] = 1;
     g.mul[1] = (int)div[0];
     g.mul[2] = (int)(div[0] * div[1]);
+    const int64_t top = g.overflow ? 0 : div[0] * div[1] * div[2] - 1;
+    g.key_bits = top > 0 ? 64 - __clzll((unsigned long long)top) : 1;
     *out = g;
+    if (out_host) *out_host = g;
 }
 
 // PCL: ijk = (int)(floor(p * inv) - (float)min_b); idx = ijk . divb_mul; non-finite points skipped
+// keys past `bits` bits (the width the sort will use) raise flags[0]; i == 0 also clears the long-run
+// count of the centroid pass
 __global__ void voxel_key_kernel(const float* __restrict__ p, int64_t n, const uint32_t* __restrict__ cnt, int stride,
                                  const VoxelGeom* __restrict__ gp, uint32_t* __restrict__ keys,
-                                 uint32_t* __restrict__ vals) {
+                                 uint32_t* __restrict__ vals, int bits, uint32_t* __restrict__ flags,
+                                 uint32_t* __restrict__ n_big) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i == 0) *n_big = 0u;
     if (i >= n) return;
     const VoxelGeom g = *gp;
     const float* q = p + (size_t)i * stride;
@@ -128,6 +141,7 @@ __global__ void voxel_key_kernel(const float* __restrict__ p, int64_t n, const u
         const int i1 = (int)(floorf(q[1] * g.inv[1]) - (float)g.min_b[1]);
         const int i2 = (int)(floorf(q[2] * g.inv[2]) - (float)g.min_b[2]);
         k = (uint32_t)(i0 * g.mul[0] + i1 * g.mul[1] + i2 * g.mul[2]);
+        if (bits < 32 && k >= (1u << bits) - 1u) flags[0] = 1u;  // the all-ones pattern marks invalid keys
     }
     keys[i] = k;
     vals[i] = (uint32_t)i;
@@ -141,10 +155,17 @@ __global__ void run_head_kernel(const uint32_t* __restrict__ keys, int64_t n, ui
 
 // Voxel runs of the sorted keys: run r = [starts[r], ends[r]).  The run index
 // of element j is (inclusive head count) - 1 = vid[j] + head[j] - 1.
+// lane 0 also publishes the voxel count and the key-width flag to host-mapped memory (hsm[0], hsm[kHostFlags])
+// and clears the flag for the next call
 __global__ void voxel_bounds_kernel(const uint32_t* __restrict__ keys, int64_t n, const uint32_t* __restrict__ head,
                                     const uint32_t* __restrict__ vid, uint32_t* __restrict__ starts,
-                                    uint32_t* __restrict__ ends) {
+                                    uint32_t* __restrict__ ends, uint32_t* __restrict__ flags, int* __restrict__ hsm) {
     const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (j == 0) {
+        hsm[0] = (int)vid[n];
+        hsm[kHostFlags] = (int)flags[0];
+        flags[0] = 0u;
+    }
     if (j >= n) return;
     const uint32_t key = keys[j];
     if (key == kInvalid) return;
@@ -155,6 +176,7 @@ __global__ void voxel_bounds_kernel(const uint32_t* __restrict__ keys, int64_t n
 }
 
 constexpr int kLaneRun = 16;  // runs up to this length: one lane; longer: one wave
+constexpr int kBigBlocks = 128;  // waves striding the long-run list (a sweep has a few dozen long runs)
 
 template <int NF>
 __device__ __forceinline__ void write_centroid(float* __restrict__ o, const float* acc, int stride, uint32_t cnt) {
@@ -299,7 +321,8 @@ __global__ void transform_segs_kernel(const float* __restrict__ in, int64_t n, i
 // i % every == 0 and x*x + y*y + z*z > blind^2 (float); its key is the float bits of the point time
 // (curvature, ms) mapped to an unsigned order (negative times below every positive one), capped one below
 // the largest key, which marks the rows not selected.  The stable sort then leaves the selected rows
-// first, in time order and, inside a tie, in input order — compaction and sort in one.
+// first, in time order and, inside a tie, in input order — compaction and sort in one.  every = 0: no
+// selection (the host selected the rows), the time key only.
 constexpr uint32_t kNotSelected = 0xffffffffu;
 __global__ void scan_key_kernel(const float* __restrict__ p, int64_t n, int stride, int every, float blind2,
                                 int tfield, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
@@ -307,7 +330,7 @@ __global__ void scan_key_kernel(const float* __restrict__ p, int64_t n, int stri
     if (i >= n) return;
     uint32_t k = kNotSelected;
     const float* q = p + (size_t)i * stride;
-    if (i % every == 0 && (q[0] * q[0] + q[1] * q[1] + q[2] * q[2]) > blind2) {
+    if (every == 0 || (i % every == 0 && (q[0] * q[0] + q[1] * q[1] + q[2] * q[2]) > blind2)) {
         const uint32_t b = __float_as_uint(q[tfield]);
         k = min((b & 0x80000000u) ? ~b : (b | 0x80000000u), kNotSelected - 1);
     }
@@ -423,19 +446,23 @@ __device__ __forceinline__ void compensate(float* q, float tms, const ImuPose& h
 // pose are left unchanged, as the reference's loop never reaches them.  The reference's loop `break`s at
 // the first point without stepping past it, so that point is compensated again by every older segment
 // (head h-1, ..., 0) — reproduced for point 0.  np < 2: the rows are only gathered.
+// skeys == nullptr: every row is selected (the host selected them; no count to find); order == nullptr:
+// the rows are already in time order (identity).  hcnt: host-mapped copy of the count.
 __global__ void undistort_gather_kernel(const float* __restrict__ in, int64_t n, int stride, int tfield,
                                         const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ order,
                                         const ImuPose* __restrict__ poses, int np, UndistortEnd end,
-                                        float* __restrict__ out, uint32_t* __restrict__ cnt) {
+                                        float* __restrict__ out, uint32_t* __restrict__ cnt, int* __restrict__ hcnt) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const uint32_t key = skeys[i];
-    if (key == kNotSelected) {
-        if (i == 0 || skeys[i - 1] != kNotSelected) cnt[0] = (uint32_t)i;
-        return;
+    if (skeys) {
+        const uint32_t key = skeys[i];
+        if (key == kNotSelected) {
+            if (i == 0 || skeys[i - 1] != kNotSelected) cnt[0] = (uint32_t)i, *hcnt = (int)i;
+            return;
+        }
+        if (i + 1 == n) cnt[0] = (uint32_t)n, *hcnt = (int)n;
     }
-    if (i + 1 == n) cnt[0] = (uint32_t)n;
-    const float* r = in + (size_t)order[i] * stride;
+    const float* r = in + (size_t)(order ? order[i] : (uint32_t)i) * stride;
     float* o = out + (size_t)i * stride;
     for (int f = 3; f < stride; ++f) o[f] = r[f];
     float q[3] = {r[0], r[1], r[2]};
@@ -508,8 +535,11 @@ int reserve(FilterBuf& b, int64_t n) {
     b.cap = c;
     if (!b.part) FCHK(hipMalloc(&b.part, 6 * 1024 * sizeof(float)));
     if (!b.geom) FCHK(hipMalloc(&b.geom, sizeof(VoxelGeom)));
-    if (!b.h_small) FCHK(hipHostMalloc(&b.h_small, 256));
-    if (!b.cnt) {  // [0] selected count, [1] minmax_geom_kernel's ticket (zero between launches)
+    if (!b.h_small) {
+        FCHK(hipHostMalloc(&b.h_small, 256, hipHostMallocMapped));
+        FCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&b.d_small), b.h_small, 0));
+    }
+    if (!b.cnt) {  // [0] selected count, [1] minmax_geom_kernel's ticket, [2] key-width flag (zero between launches)
         FCHK(hipMalloc(&b.cnt, 64));
         FCHK(hipMemset(b.cnt, 0, 64));
     }
@@ -525,12 +555,13 @@ int exscan(FilterBuf& b, const uint32_t* in, uint32_t* out, int64_t n1, hipStrea
     return 0;
 }
 
-int sort_pairs(FilterBuf& b, int64_t n, hipStream_t st) {
+// stable sort of (keys, vals) on key bits [0, bits) into (keys_alt, vals_alt)
+int sort_pairs(FilterBuf& b, int64_t n, hipStream_t st, int bits = 32) {
     size_t bytes = 0;
-    FCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, b.keys, b.keys_alt, b.vals, b.vals_alt, (int)n, 0, 32, st));
+    FCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, b.keys, b.keys_alt, b.vals, b.vals_alt, (int)n, 0, bits, st));
     if (ftmp(b, bytes)) return -5;
     bytes = b.tmp_bytes;
-    FCHK(hipcub::DeviceRadixSort::SortPairs(b.tmp, bytes, b.keys, b.keys_alt, b.vals, b.vals_alt, (int)n, 0, 32, st));
+    FCHK(hipcub::DeviceRadixSort::SortPairs(b.tmp, bytes, b.keys, b.keys_alt, b.vals, b.vals_alt, (int)n, 0, bits, st));
     return 0;
 }
 
@@ -630,6 +661,23 @@ int cloud_encode(const float* d_rec, int64_t n, int stride, int point_step, cons
     return 0;
 }
 
+__global__ void records_xyz_sel_kernel(const float* __restrict__ rec, int64_t n, int stride, float* __restrict__ xyz,
+                                       uint8_t* __restrict__ sel) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    xyz[3 * i] = rec[(size_t)i * stride];
+    xyz[3 * i + 1] = rec[(size_t)i * stride + 1];
+    xyz[3 * i + 2] = rec[(size_t)i * stride + 2];
+    sel[i] = 0;
+}
+
+int records_to_xyz_sel(const float* d_rec, int64_t n, int stride, float* d_xyz, uint8_t* sel, hipStream_t st) {
+    if (n <= 0) return 0;
+    records_xyz_sel_kernel<<<nblk(n), 256, 0, st>>>(d_rec, n, stride, d_xyz, sel);
+    FCHK(hipGetLastError());
+    return 0;
+}
+
 int records_to_xyz(const float* d_rec, int64_t n, int stride, float* d_xyz, hipStream_t st) {
     if (n <= 0) return 0;
     records_xyz_kernel<<<nblk(n), 256, 0, st>>>(d_rec, n, stride, d_xyz);
@@ -647,39 +695,56 @@ void filter_free(FilterBuf& b) {
     b = FilterBuf{};
 }
 
-// Everything up to the centroids, with the output count and the geometry copied to b.h_small ([0] voxels,
-// [1..] VoxelGeom) behind them: nothing waits for the device.  cnt (optional, device): rows in use <= n.
+// Everything up to the centroids; the voxel count, the geometry and the key-width flag land in the
+// host-mapped b.h_small ([0], [1..], [kHostFlags]) behind them: nothing waits for the device, nothing is
+// copied.  cnt (optional, device): rows in use <= n.  The voxel sort uses b.vox_bits key bits (learnt from
+// the previous call; a key past them raises the flag and the caller runs the call again at full width).
 int voxel_grid_enqueue(FilterBuf& b, const float* d_in, int64_t n, const uint32_t* cnt, int stride, const float leaf[3],
                        float* d_out, hipStream_t st) {
     if (stride < 3 || stride > kMaxFields || n >= (int64_t)0x7fffffff) return -1;
     if (reserve(b, n)) return -5;
-    const int nbA = (int)std::min<int64_t>(1024, (n + 255) / 256);
-    minmax_geom_kernel<<<nbA, 256, 0, st>>>(d_in, n, cnt, stride, b.part, b.cnt + 1, leaf[0], leaf[1], leaf[2],
-                                            b.geom);
-    voxel_key_kernel<<<nblk(n), 256, 0, st>>>(d_in, n, cnt, stride, b.geom, b.keys, b.vals);
-    int rc = sort_pairs(b, n, st);
+    auto* hgeom = reinterpret_cast<VoxelGeom*>(b.d_small + 1);
+    if (n <= 256 * 64) {  // one block: no partials, no ticket
+        minmax_geom_kernel<true><<<1, 256, 0, st>>>(d_in, n, cnt, stride, b.part, b.cnt + 1, leaf[0], leaf[1], leaf[2],
+                                                    b.geom, hgeom);
+    } else {
+        const int nbA = (int)std::min<int64_t>(1024, (n + 255) / 256);
+        minmax_geom_kernel<false><<<nbA, 256, 0, st>>>(d_in, n, cnt, stride, b.part, b.cnt + 1, leaf[0], leaf[1],
+                                                       leaf[2], b.geom, hgeom);
+    }
+    const int bits = std::min(std::max(b.vox_bits, 1), 32);
+    voxel_key_kernel<<<nblk(n), 256, 0, st>>>(d_in, n, cnt, stride, b.geom, b.keys, b.vals, bits, b.cnt + 2,
+                                              b.big + b.cap);
+    int rc = sort_pairs(b, n, st, bits);
     if (rc) return rc;
     run_head_kernel<<<nblk(n + 1), 256, 0, st>>>(b.keys_alt, n, b.head);
     rc = exscan(b, b.head, b.vid, n + 1, st);
     if (rc) return rc;
     // runs -> [start, end) per voxel (b.keys / b.vals are free after the sort)
-    voxel_bounds_kernel<<<nblk(n), 256, 0, st>>>(b.keys_alt, n, b.head, b.vid, b.keys, b.vals);
-    FCHK(hipMemsetAsync(b.big + b.cap, 0, sizeof(uint32_t), st));
+    voxel_bounds_kernel<<<nblk(n), 256, 0, st>>>(b.keys_alt, n, b.head, b.vid, b.keys, b.vals, b.cnt + 2, b.d_small);
     voxel_centroid_kernel<<<nblk(n), 256, 0, st>>>(d_in, stride, b.vals_alt, b.keys, b.vals, b.vid + n, b.big,
                                                    b.big + b.cap, d_out);
-    voxel_centroid_big_kernel<<<1024, 64, 0, st>>>(d_in, stride, b.vals_alt, b.keys, b.vals, b.big, b.big + b.cap,
-                                                   d_out);
-    FCHK(hipMemcpyAsync(b.h_small, b.vid + n, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    FCHK(hipMemcpyAsync(b.h_small + 1, b.geom, sizeof(VoxelGeom), hipMemcpyDeviceToHost, st));
+    voxel_centroid_big_kernel<<<kBigBlocks, 64, 0, st>>>(d_in, stride, b.vals_alt, b.keys, b.vals, b.big,
+                                                         b.big + b.cap, d_out);
+    FCHK(hipGetLastError());
     return 0;
 }
 
-// after the stream has drained: the voxel count, or — PCL's "Leaf size is too small ... Integer indices
-// would overflow" — the m input rows copied to the output (returns 1 then; the copy is enqueued, not waited on)
+// After the stream has drained: the voxel count; 2 when the key width was too narrow (b.vox_bits reset to
+// 32: enqueue again), or 1 for PCL's "Leaf size is too small ... Integer indices would overflow": the m
+// input rows copied to the output (the copy is enqueued, not waited on).  Learns the next call's key width.
 static int voxel_grid_result(FilterBuf& b, const float* d_in, int64_t m, int stride, float* d_out, int64_t* n_out,
                              hipStream_t st) {
     VoxelGeom g;
     std::memcpy(&g, b.h_small + 1, sizeof(VoxelGeom));
+    const bool narrow = b.h_small[kHostFlags] != 0;
+    b.h_small[kHostFlags] = 0;
+    if (narrow && !g.overflow) {
+        b.vox_bits = 32;
+        return 2;
+    }
+    // one spare bit: a sweep's extent may grow a little before the next call has to repeat itself
+    b.vox_bits = g.overflow ? 32 : std::min(32, g.key_bits + 1);
     if (g.overflow) {
         if (m > 0) copy_strided_kernel<<<nblk(m * stride), 256, 0, st>>>(d_in, m * stride, d_out);
         FCHK(hipGetLastError());
@@ -694,11 +759,14 @@ int voxel_grid(FilterBuf& b, const float* d_in, int64_t n, int stride, const flo
                int64_t* n_out, hipStream_t st) {
     *n_out = 0;
     if (n <= 0) return 0;
-    int rc = voxel_grid_enqueue(b, d_in, n, nullptr, stride, leaf, d_out, st);
-    if (rc) return rc;
-    FCHK(hipStreamSynchronize(st));
-    rc = voxel_grid_result(b, d_in, n, stride, d_out, n_out, st);
-    if (rc < 0) return rc;
+    int rc = 2;
+    for (int attempt = 0; attempt < 2 && rc == 2; ++attempt) {
+        rc = voxel_grid_enqueue(b, d_in, n, nullptr, stride, leaf, d_out, st);
+        if (rc) return rc;
+        FCHK(hipStreamSynchronize(st));
+        rc = voxel_grid_result(b, d_in, n, stride, d_out, n_out, st);
+    }
+    if (rc < 0 || rc == 2) return rc < 0 ? rc : -2;
     if (rc == 1) FCHK(hipStreamSynchronize(st));
     return 0;
 }
@@ -747,29 +815,45 @@ int keyframe_cloud(const float* d_rec, int64_t n, int stride, const PoseArg& ps,
 }
 
 int scan_preprocess_enqueue(FilterBuf& b, const float* d_raw, int64_t n, int stride, const ScanPrepParams& p,
-                            const ImuPose* d_poses, int np, const UndistortEnd& end, float* d_out, hipStream_t st) {
+                            const ImuPose* d_poses, int np, const UndistortEnd& end, float* d_out, hipStream_t st,
+                            int presel) {
     b.prep_n = 0;
+    b.prep_sel = -1;
     if (n <= 0) return 0;
     if (stride < 4 || stride > kMaxFields || p.time_field < 3 || p.time_field >= stride || n >= (int64_t)0x7fffffff)
         return -1;
     if (reserve(b, n)) return -5;
     int rc = fgrow(&b.c, b.c_cap, n * stride);
     if (rc) return rc;
-    // 1. Preprocess selection + 2. stable time sort in one sort over the n rows (the selected first),
-    // 3. gather + undistort; the selected count m stays on the device (b.cnt[0])
-    const int every = p.point_filter_num > 0 ? p.point_filter_num : 1;
-    scan_key_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, every, p.blind * p.blind, p.time_field, b.keys, b.vals);
-    rc = sort_pairs(b, n, st);
-    if (rc) return rc;
-    undistort_gather_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, p.time_field, b.keys_alt, b.vals_alt, d_poses,
-                                                     np, end, b.c, b.cnt);
-    FCHK(hipMemcpyAsync(b.h_small + kHostSel, b.cnt, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    const uint32_t* cnt = nullptr;  // rows in use past this point: all n (host selection) or b.cnt[0]
+    if (presel == 1) {  // selected and already in time order: the stable sort is the identity
+        undistort_gather_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, p.time_field, nullptr, nullptr, d_poses,
+                                                         np, end, b.c, b.cnt, b.d_small + kHostSel);
+    } else if (presel == 0) {  // selected, times out of order: stable sort by time
+        scan_key_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, 0, 0.f, p.time_field, b.keys, b.vals);
+        rc = sort_pairs(b, n, st);
+        if (rc) return rc;
+        undistort_gather_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, p.time_field, nullptr, b.vals_alt, d_poses,
+                                                         np, end, b.c, b.cnt, b.d_small + kHostSel);
+    } else {
+        // 1. Preprocess selection + 2. stable time sort in one sort over the n rows (the selected first),
+        // 3. gather + undistort; the selected count stays on the device (b.cnt[0]) and in b.h_small
+        const int every = p.point_filter_num > 0 ? p.point_filter_num : 1;
+        scan_key_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, every, p.blind * p.blind, p.time_field, b.keys,
+                                                 b.vals);
+        rc = sort_pairs(b, n, st);
+        if (rc) return rc;
+        undistort_gather_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, p.time_field, b.keys_alt, b.vals_alt,
+                                                         d_poses, np, end, b.c, b.cnt, b.d_small + kHostSel);
+        cnt = b.cnt;
+    }
     // 4. downSizeFilterSurf
     b.prep_leaf = p.leaf > 0.f;
     b.prep_n = n;
+    b.prep_sel = presel >= 0 ? n : -1;
     if (b.prep_leaf) {
         const float leaf[3] = {p.leaf, p.leaf, p.leaf};
-        return voxel_grid_enqueue(b, b.c, n, b.cnt, stride, leaf, d_out, st);
+        return voxel_grid_enqueue(b, b.c, n, cnt, stride, leaf, d_out, st);
     }
     FCHK(hipMemcpyAsync(d_out, b.c, (size_t)n * stride * sizeof(float), hipMemcpyDeviceToDevice, st));
     return 0;
@@ -780,7 +864,7 @@ int scan_preprocess_finish(FilterBuf& b, int stride, float* d_out, int64_t* n_ou
     if (n_undist) *n_undist = 0;
     FCHK(hipStreamSynchronize(st));
     if (b.prep_n <= 0) return 0;
-    const int64_t m = (uint32_t)b.h_small[kHostSel];
+    const int64_t m = b.prep_sel >= 0 ? b.prep_sel : (uint32_t)b.h_small[kHostSel];
     if (n_undist) *n_undist = m;
     if (!b.prep_leaf) {
         *n_out = m;
@@ -794,10 +878,13 @@ int scan_preprocess(FilterBuf& b, const float* d_raw, int64_t n, int stride, con
                     hipStream_t st, int64_t* n_undist) {
     *n_out = 0;
     if (n_undist) *n_undist = 0;
-    int rc = scan_preprocess_enqueue(b, d_raw, n, stride, p, d_poses, np, end, d_out, st);
-    if (rc) return rc;
-    rc = scan_preprocess_finish(b, stride, d_out, n_out, n_undist, st);
-    if (rc < 0) return rc;
+    int rc = 2;
+    for (int attempt = 0; attempt < 2 && rc == 2; ++attempt) {  // 2: the voxel key width was learnt too narrow
+        rc = scan_preprocess_enqueue(b, d_raw, n, stride, p, d_poses, np, end, d_out, st);
+        if (rc) return rc;
+        rc = scan_preprocess_finish(b, stride, d_out, n_out, n_undist, st);
+    }
+    if (rc < 0 || rc == 2) return rc < 0 ? rc : -2;
     if (rc == 1) FCHK(hipStreamSynchronize(st));
     return 0;
 }

@@ -14,6 +14,7 @@ struct VoxelGeom {
     int mul[3];
     int overflow;
     int empty;
+    int key_bits;  // bits of the largest voxel index (div_b.x * div_b.y * div_b.z - 1)
 };
 
 // One IMUpose entry (FAST-LIO set_pose6d [U]): offset_time [s] from the scan
@@ -50,8 +51,10 @@ struct FilterBuf {
     VoxelGeom* geom = nullptr;
     void* tmp = nullptr;
     size_t tmp_bytes = 0;
-    int* h_small = nullptr;  // pinned: [0] voxel count, [1..] VoxelGeom, [kHostSel] selected count
-    uint32_t* cnt = nullptr; // device: [0] scan_preprocess's selected count
+    int* h_small = nullptr;  // pinned, host-mapped: [0] voxel count, [1..] VoxelGeom, [kHostSel] selected count,
+    int* d_small = nullptr;  //   [kHostFlags] flags (bit 0: a voxel key past vox_bits); d_small = the device view
+    uint32_t* cnt = nullptr; // device: [0] scan_preprocess's selected count, [1] minmax_geom_kernel's ticket
+    int vox_bits = 32;       // voxel-key bits the next voxel sort assumes (learnt, checked on the device)
     float* a = nullptr;      // staging records
     int64_t a_cap = 0;
     float* c = nullptr;
@@ -61,9 +64,10 @@ struct FilterBuf {
     void* h_stage = nullptr; // pinned host staging of the sweep uploads (lio_capi stage_sweep)
     size_t stage_bytes = 0;
     int64_t prep_n = 0;      // row bound of the last scan_preprocess_enqueue (0: nothing pending)
+    int64_t prep_sel = -1;   // its selected count when the host selected the rows (-1: on the device)
     bool prep_leaf = false;
 };
-constexpr int kHostSel = 16;
+constexpr int kHostSel = 16, kHostFlags = 17;
 
 void filter_free(FilterBuf& b);
 // d_out capacity: n * stride floats.  Synchronises the stream (output count).
@@ -82,9 +86,15 @@ int scan_preprocess(FilterBuf& b, const float* d_raw, int64_t n, int stride, con
 // for the row bound n; rows past the count are scratch), _finish waits for the stream and reads the
 // counts.  _finish returns 1 when VoxelGrid's index overflow replaced the output by its input: that
 // copy is queued, not waited on, and the caller's follow-up work on d_out must be queued again.
+// presel >= 0: the n rows are already Preprocess's selection, in input order (the host packed them), and
+// presel = 1 says their times are non-decreasing — the stable time sort is then the identity and is skipped.
+// _finish returns 2 when the learnt voxel-key width was too narrow: the caller enqueues again (same input).
 int scan_preprocess_enqueue(FilterBuf& b, const float* d_raw, int64_t n, int stride, const ScanPrepParams& p,
-                            const ImuPose* d_poses, int np, const UndistortEnd& end, float* d_out, hipStream_t st);
+                            const ImuPose* d_poses, int np, const UndistortEnd& end, float* d_out, hipStream_t st,
+                            int presel = -1);
 int scan_preprocess_finish(FilterBuf& b, int stride, float* d_out, int64_t* n_out, int64_t* n_undist, hipStream_t st);
+// records -> packed xyz, and sel[0 .. n) = 0 (the scan's selection flags) in the same pass
+int records_to_xyz_sel(const float* d_rec, int64_t n, int stride, float* d_xyz, uint8_t* sel, hipStream_t st);
 
 int records_to_xyz(const float* d_rec, int64_t n, int stride, float* d_xyz, hipStream_t st);
 

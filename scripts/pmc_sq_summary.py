@@ -2,8 +2,9 @@
 (VERDICT r03 #5).  Per kernel (mean per dispatch):
 
   valu_busy_frac = SQ_INSTS_VALU x 2 cycles (a wave64 VALU instruction issues over 2 cycles on a SIMD-32,
-                   MI355X_MICROARCH.md "Wave scheduling") / (1024 SIMDs x kernel cycles), kernel cycles =
-                   duration x effective clock (GRBM_GUI_ACTIVE / 8 / duration, same guide: DVFS give-back)
+                   MI355X_MICROARCH.md "Per-instruction cycle constants") / (1024 SIMDs x kernel cycles), kernel
+                   cycles = duration x 2.4 GHz for dispatches under 0.3 ms (the guide: GRBM_GUI_ACTIVE / 8 /
+                   duration "reads high on dispatches shorter than about 0.3 ms"), else x that effective clock
   wait_frac      = SQ_WAIT_ANY / SQ_WAVE_CYCLES       (waves parked on s_waitcnt / barriers: memory latency)
   issue_stall    = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES  (ready but not issued: pipe / dependency stalls)
   active_frac    = SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES (the three are disjoint and sum to ~1, same guide)
@@ -42,9 +43,11 @@ res = {}
 for k, lst in per.items():
     m = {c: sum(x.get(c, 0.0) for x in lst) / len(lst) for c in lst[0]}
     wc = m.get("SQ_WAVE_CYCLES", 0.0)
-    clock = m.get("GRBM_GUI_ACTIVE", 0.0) / 8.0 / m["_dur_s"] if m.get("GRBM_GUI_ACTIVE") else 2.4e9
+    grbm = m.get("GRBM_GUI_ACTIVE", 0.0) / 8.0 / m["_dur_s"] if m.get("GRBM_GUI_ACTIVE") else None
+    clock = grbm if (grbm and m["_dur_s"] >= 3e-4) else 2.4e9
     cyc = m["_dur_s"] * clock
     res[k] = {"dispatches": len(lst), "avg_us": round(m["_dur_s"] * 1e6, 2), "clock_ghz": round(clock / 1e9, 3),
+              "grbm_clock_ghz": round(grbm / 1e9, 3) if grbm else None,
               "valu_insts": round(m.get("SQ_INSTS_VALU", 0.0)),
               "valu_busy_frac": round(m.get("SQ_INSTS_VALU", 0.0) * 2.0 / (1024.0 * cyc), 4) if cyc else None,
               "wait_frac": round(m.get("SQ_WAIT_ANY", 0.0) / wc, 4) if wc else None,

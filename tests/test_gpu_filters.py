@@ -102,10 +102,13 @@ def test_scan_preprocess_into_ctx(oracle):
 
 
 def test_preprocess_staged_upload_edges(oracle):
-    """The staged upload (rows i % point_filter_num == 0 packed on the host, one DMA) and the single host
-    wait: ragged row counts, wider records, nothing selected, one row, VoxelGrid's index overflow (output =
-    the undistorted input) and the staging buffer growing and shrinking between calls — each bit-exact
-    against the oracle, through the filter API and into a ctx (feats_down_body and feats_undistort)."""
+    """The staged upload (Preprocess's selection made while the host packs the rows, one DMA), the single
+    host wait, the time sort skipped for rows already in time order and the learnt voxel-key width: ragged
+    row counts, wider records, shuffled times (sorted path), non-finite rows and negative times, nothing
+    selected, one row, a small extent followed by a large one (the learnt key width too narrow: the call
+    repeats at full width), VoxelGrid's index overflow (output = the undistorted input) and the staging
+    buffer growing and shrinking between calls — each bit-exact against the oracle, through the filter API
+    and into a ctx (feats_down_body and feats_undistort)."""
     scene = synth.make_scene(400.0, 1234)
     raw, poses, end24 = synth.make_raw_scan(scene, 120_000, seed=8)
     end = F.pose_from_pose24(end24)
@@ -115,9 +118,15 @@ def test_preprocess_staged_upload_edges(oracle):
     tree = F.IkdTreeGPU(cell_size=1.0)
     tree.Build(m)
     hm = F.HShareModelGPU(tree)
-    cases = [(raw[:120_001 - 7], 3, 2.0, 0.5, 4), (raw[:5_000], 4, 2.0, 0.5, 4), (wide[:60_017], 5, 2.0, 0.5, 5),
-             (raw[:1], 1, 0.0, 0.5, 4), (raw[:2_000], 4, 1e4, 0.5, 4), (raw[:40_000], 2, 2.0, 1e-4, 4),
-             (raw, 4, 2.0, 0.0, 4), (raw[:777], 7, 2.0, 0.3, 4)]
+    near = raw[np.linalg.norm(raw[:, :3], axis=1) < 6.0][:800]      # a small extent: few voxel-key bits learnt
+    shuffled = raw[rng.permutation(len(raw))[:50_000]]               # times out of order: the sorted path
+    holes = raw[:30_000].copy()
+    holes[::97, 1] = np.nan                                          # non-finite rows (never selected)
+    holes[5::211, 4] = -holes[5::211, 4]                             # negative times
+    cases = [(near, 1, 2.0, 0.5, 4), (raw[:120_001 - 7], 3, 2.0, 0.5, 4), (near, 2, 2.0, 0.5, 4),
+             (shuffled, 2, 2.0, 0.5, 4), (holes, 1, 2.0, 0.5, 4), (raw[:5_000], 4, 2.0, 0.5, 4),
+             (wide[:60_017], 5, 2.0, 0.5, 5), (raw[:1], 1, 0.0, 0.5, 4), (raw[:2_000], 4, 1e4, 0.5, 4),
+             (raw[:40_000], 2, 2.0, 1e-4, 4), (raw, 4, 2.0, 0.0, 4), (raw[:777], 7, 2.0, 0.3, 4)]
     for rows, every, blind, leaf, tf in cases:
         end_tf = end
         o_down = oracle.preprocess(rows, poses, end24, point_filter_num=every, blind=blind, leaf=leaf, time_field=tf)
