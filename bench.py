@@ -92,6 +92,8 @@ def parse():
     ap.add_argument("--watchdog-s", type=float, default=240.0,
                     help="N > 1: seconds after the headline measurement before rank 0 prints what it has and every "
                          "rank exits (a collective of the secondary sections that never returns)")
+    ap.add_argument("--pmc-sq", default=os.path.join(ROOT, "profiles", "r04_pmc_sq_c3.json"),
+                    help="SQ issue / wait breakdown per kernel (scripts/pmc_sq_summary.py of a rocprofv3 --pmc pass)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"),
                     help="per-launch HBM traffic measured with rocprofv3 --pmc (profiles/)")
     return ap.parse_args()
@@ -212,8 +214,22 @@ def _loop_icp(args, LC, synth, local, world, rank, dist, rehearse, coll_dev, bar
                 "kernel_ms_per_pass": round(icp_kernel_ms, 4),
                 "nn_kernel_ms_per_pass": round(nn_ms, 4),
                 "kernel_gbs": round(BYTES_PER_PT_ICP * shard_n / (icp_kernel_ms * 1e-3) / 1e9, 2)
-                if passes else None}
+                if passes else None,
+                "sq_breakdown": _icp_sq(args)}
     return loop_icp, src, dst
+
+
+def _icp_sq(args):
+    """the ICP correspondence kernels' issue / wait breakdown from the committed SQ counter pass (C4 pairs A
+    and B, scripts/icp_ab.py under rocprofv3 --pmc; scripts/pmc_sq_summary.py)"""
+    path = os.path.join(ROOT, "profiles", "r04_pmc_sq_icp.json")
+    try:
+        pm = json.load(open(path))
+    except Exception:
+        return None
+    out = {k: {f: v[f] for f in ("avg_us", "valu_busy_frac", "wait_frac", "issue_stall_frac")}
+           for k, v in pm.items() if k.startswith(("icp_tile_kernel", "icp_heavy_kernel"))}
+    return dict(out, source=os.path.relpath(path, ROOT)) if out else None
 
 
 def main():
@@ -433,6 +449,23 @@ def main():
     # stream; achieved = algorithmic bytes / the sum of the three kernels' own
     # execution spans (hipExtLaunchKernel start/stop events on that stream, a
     # separate pass after the timed loop: the spans rocprofv3 reports, no gaps)
+    # issue / wait breakdown of the evaluation's kernels from a separate SQ + GRBM counter pass on this config
+    # (profiles/, scripts/pmc_sq_summary.py: VALU busy at 2 cycles per wave64 instruction, wait = SQ_WAIT_ANY /
+    # SQ_WAVE_CYCLES, issue stall = SQ_WAIT_INST_ANY / SQ_WAVE_CYCLES)
+    sq = None
+    if args.config == "C3" and os.path.exists(args.pmc_sq):
+        try:
+            pm = json.load(open(args.pmc_sq))
+            pick = {"near_first": "knn_near_kernel<false, false", "near_seeded": "knn_near_kernel<false, true",
+                    "far": "knn_far_kernel", "plane": "plane_kernel", "reuse": "h_model_reuse_kernel"}
+            sq = {}
+            for name, pre in pick.items():
+                k = next((k for k in pm if k.startswith(pre)), None)
+                if k:
+                    sq[name] = {f: pm[k][f] for f in ("valu_busy_frac", "wait_frac", "issue_stall_frac")}
+            sq = sq or None
+        except Exception:
+            sq = None
     roofline = {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
                 "traffic": traffic,
@@ -442,7 +475,11 @@ def main():
                 "plane_kernel_avg_ms": round(tm["plane_ms"] / max(tm["plane_launches"], 1), 5),
                 "reuse_kernel_avg_ms": round(reuse_avg_ms, 5),
                 "reuse_achieved_gbs": round(BYTES_PER_PT_REUSE * n_pts / (reuse_avg_ms * 1e-3) / 1e9, 2)
-                if tm["reuse_launches"] else None}
+                if tm["reuse_launches"] else None,
+                "valu_busy_frac": sq["near_first"]["valu_busy_frac"] if sq and "near_first" in sq else None,
+                "wait_frac": sq["near_first"]["wait_frac"] if sq and "near_first" in sq else None,
+                "sq_breakdown": sq,
+                "sq_source": os.path.relpath(args.pmc_sq, ROOT) if sq else None}
 
     line = {
         "metric": "scans/sec (100k-pt scan vs N-pt map) + ms/IESKF-iteration, 1 GPU",

@@ -1312,10 +1312,21 @@ int lio_preprocess(lio_filter* f, const float* raw, int64_t n, int stride, const
     return LIO_OK;
 }
 
+// LIO_PREP_PROFILE=1 (diagnostics): host-side phases of every lio_scan_preprocess on stderr
+static bool prep_profile() {
+    static const bool on = std::getenv("LIO_PREP_PROFILE") != nullptr;
+    return on;
+}
+static double prep_us(std::chrono::steady_clock::time_point a, std::chrono::steady_clock::time_point b) {
+    return std::chrono::duration<double, std::micro>(b - a).count();
+}
+
 // the device half shared by lio_scan_preprocess and lio_scan_preprocess_cloud2: c->d_raw holds `rows`
 // records; every stage is queued, the scan buffers set up behind it, and the host waits once
 static int scan_prep_device(lio_ctx* c, int64_t rows, int stride, const lio::ScanPrepParams& sp, int n_poses,
-                            const lio_pose* end, int64_t* n_down, const char* what, int presel = -1) {
+                            const lio_pose* end, int64_t* n_down, const char* what, int presel = -1,
+                            const lio::ImuPose* d_poses = nullptr) {
+    if (!d_poses) d_poses = c->d_poses;
     hipStream_t st = c->map->st;
     c->undist_n = -1;
     auto bail = [&](int r) {
@@ -1327,17 +1338,23 @@ static int scan_prep_device(lio_ctx* c, int64_t rows, int stride, const lio::Sca
     int64_t m = 0, mu = 0;
     rc = 2;
     for (int attempt = 0; attempt < 2 && rc == 2; ++attempt) {  // 2: the voxel key width was learnt too narrow
-        rc = lio::scan_preprocess_enqueue(c->filt, c->d_raw, rows, stride, sp, c->d_poses, n_poses,
-                                          undistort_end(end), c->d_rec, st, presel);
+        const bool vox = sp.leaf > 0.f;  // the centroid pass writes the scan's xyz and flags itself
+        rc = lio::scan_preprocess_enqueue(c->filt, c->d_raw, rows, stride, sp, d_poses, n_poses,
+                                          undistort_end(end), c->d_rec, st, presel, vox ? c->d_body : nullptr,
+                                          vox ? c->d_sel : nullptr);
         if (rc) return bail(filter_status(rc, what));
-        rc = lio::records_to_xyz_sel(c->d_rec, rows, stride, c->d_body, c->d_sel, st);
+        if (!vox) rc = lio::records_to_xyz_sel(c->d_rec, rows, stride, c->d_body, c->d_sel, st);
         if (rc) return bail(filter_status(rc, what));
+        const auto tw = std::chrono::steady_clock::now();
         rc = lio::scan_preprocess_finish(c->filt, stride, c->d_rec, &m, &mu, st);
+        if (prep_profile())
+            std::fprintf(stderr, "prep_profile wait_us %.1f attempt %d\n", prep_us(tw, std::chrono::steady_clock::now()),
+                         attempt);
     }
     if (rc == 2) rc = -2;
     if (rc < 0) return bail(filter_status(rc, what));
     if (rc == 1) {  // VoxelGrid index overflow: the output is the undistorted input, its xyz again
-        rc = lio::records_to_xyz(c->d_rec, m, stride, c->d_body, st);
+        rc = lio::records_to_xyz_sel(c->d_rec, m, stride, c->d_body, c->d_sel, st);
         if (rc) return bail(filter_status(rc, what));
         HIP_TRY(hipStreamSynchronize(st));
     }
@@ -1353,6 +1370,7 @@ int lio_scan_preprocess(lio_ctx* c, const float* raw, int64_t n, int stride, con
     if (!c) return fail(LIO_ERR_ARG, "lio_scan_preprocess: NULL ctx");
     int rc = prep_args_ok(raw, n, stride, p, poses, n_poses);
     if (rc) return rc;
+    const auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipSetDevice(c->map->dev));
     hipStream_t st = c->map->st;
     const bool full = prep_upload_full();
@@ -1366,18 +1384,31 @@ int lio_scan_preprocess(lio_ctx* c, const float* raw, int64_t n, int stride, con
         if (rc) return rc;
         presel = sorted ? 1 : 0;
     }
-    rc = grow(&c->d_raw, c->raw_cap, std::max<int64_t>(rows, 1) * stride);
+    const auto t1 = std::chrono::steady_clock::now();
+    // staged: the rows and the poses behind them (pose_off, 256-B aligned) in one DMA into d_raw
+    const size_t staged = pose_off + (size_t)n_poses * sizeof(lio::ImuPose);
+    rc = grow(&c->d_raw, c->raw_cap, full ? std::max<int64_t>(rows, 1) * stride : (int64_t)((staged + 3) / 4) + 1);
     if (!rc) rc = grow(&c->d_rec, c->rec_cap, std::max<int64_t>(rows, 1) * stride);
-    if (!rc && n_poses) rc = grow(&c->d_poses, c->poses_cap, n_poses);
+    if (!rc && n_poses && full) rc = grow(&c->d_poses, c->poses_cap, n_poses);
     if (rc) return rc;
-    const auto* stage = static_cast<const uint8_t*>(c->filt.h_stage);
-    if (rows)
-        HIP_TRY(hipMemcpyAsync(c->d_raw, full ? (const void*)raw : stage, (size_t)rows * stride * sizeof(float),
-                               hipMemcpyHostToDevice, st));
-    if (n_poses)
-        HIP_TRY(hipMemcpyAsync(c->d_poses, full ? (const void*)poses : stage + pose_off,
-                               (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
-    return scan_prep_device(c, rows, stride, sp, n_poses, end, n_down, "lio_scan_preprocess", presel);
+    const lio::ImuPose* d_poses = c->d_poses;
+    if (full) {
+        if (rows)
+            HIP_TRY(hipMemcpyAsync(c->d_raw, raw, (size_t)rows * stride * sizeof(float), hipMemcpyHostToDevice, st));
+        if (n_poses)
+            HIP_TRY(hipMemcpyAsync(c->d_poses, poses, (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
+    } else {
+        if (staged) HIP_TRY(hipMemcpyAsync(c->d_raw, c->filt.h_stage, staged, hipMemcpyHostToDevice, st));
+        d_poses = reinterpret_cast<const lio::ImuPose*>(reinterpret_cast<const uint8_t*>(c->d_raw) + pose_off);
+    }
+    const auto t2 = std::chrono::steady_clock::now();
+    rc = scan_prep_device(c, rows, stride, sp, n_poses, end, n_down, "lio_scan_preprocess", presel, d_poses);
+    if (prep_profile()) {
+        const auto t3 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "prep_profile rows %lld presel %d stage_us %.1f upload_enqueue_us %.1f device_us %.1f total_us %.1f\n",
+                     (long long)rows, presel, prep_us(t0, t1), prep_us(t1, t2), prep_us(t2, t3), prep_us(t0, t3));
+    }
+    return rc;
 }
 
 int lio_scan_get_undistorted(lio_ctx* c, float* out, int64_t cap_points, int64_t* n_points, int* stride) {

@@ -30,15 +30,16 @@ namespace {
 
 constexpr uint32_t kInvalid = 0xffffffffu;
 
-// min / max over 256 lanes of the block (lo[3], hi[3] per lane) into s[0..2][0] / s[3..5][0]
-__device__ __forceinline__ void block_minmax(float (*s)[256], const float* lo, const float* hi) {
+// min / max over the NT lanes of the block (lo[3], hi[3] per lane) into s[0..2][0] / s[3..5][0]
+template <int NT>
+__device__ __forceinline__ void block_minmax(float (*s)[NT], const float* lo, const float* hi) {
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
         s[d][threadIdx.x] = lo[d];
         s[3 + d][threadIdx.x] = hi[d];
     }
     __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
+    for (int w = NT / 2; w > 0; w >>= 1) {
         if ((int)threadIdx.x < w) {
 #pragma unroll
             for (int d = 0; d < 3; ++d) {
@@ -59,26 +60,40 @@ __device__ __forceinline__ void block_minmax(float (*s)[256], const float* lo, c
 // cnt (optional): the rows in use, <= n (the bound the grid is sized for)
 // SINGLE: one block covers the input (small clouds: no partials, no ticket, no fence); out_host: a
 // host-mapped copy of the geometry
-template <bool SINGLE>
-__global__ void __launch_bounds__(256) minmax_geom_kernel(const float* __restrict__ p, int64_t n,
-                                                          const uint32_t* __restrict__ cnt, int stride,
-                                                          float* __restrict__ part, unsigned* __restrict__ ticket,
-                                                          float lx, float ly, float lz, VoxelGeom* __restrict__ out,
-                                                          VoxelGeom* __restrict__ out_host) {
-    __shared__ float s[6][256];
+template <bool SINGLE, int NT = 256>
+__global__ void __launch_bounds__(NT) minmax_geom_kernel(const float* __restrict__ p, int64_t n,
+                                                         const uint32_t* __restrict__ cnt, int stride,
+                                                         float* __restrict__ part, unsigned* __restrict__ ticket,
+                                                         float lx, float ly, float lz, VoxelGeom* __restrict__ out,
+                                                         VoxelGeom* __restrict__ out_host) {
+    __shared__ float s[6][NT];
     __shared__ bool last;
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     if (cnt) n = min<int64_t>(n, *cnt);
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float* q = p + (size_t)i * stride;
-        const float x = q[0], y = q[1], z = q[2];
-        if (!(isfinite(x) && isfinite(y) && isfinite(z))) continue;
-        lo[0] = fminf(lo[0], x);
-        lo[1] = fminf(lo[1], y);
-        lo[2] = fminf(lo[2], z);
-        hi[0] = fmaxf(hi[0], x);
-        hi[1] = fmaxf(hi[1], y);
-        hi[2] = fmaxf(hi[2], z);
+    // U rows per lane in flight (a lone block over a sweep is one chain of round trips otherwise)
+    constexpr int U = 8;
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < n; i0 += U * step) {
+        float v[U][3];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + u * step;
+            const float* q = p + (size_t)(i < n ? i : i0) * stride;
+            v[u][0] = q[0];
+            v[u][1] = q[1];
+            v[u][2] = q[2];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const float x = v[u][0], y = v[u][1], z = v[u][2];
+            if (i0 + u * step >= n || !(isfinite(x) && isfinite(y) && isfinite(z))) continue;
+            lo[0] = fminf(lo[0], x);
+            lo[1] = fminf(lo[1], y);
+            lo[2] = fminf(lo[2], z);
+            hi[0] = fmaxf(hi[0], x);
+            hi[1] = fmaxf(hi[1], y);
+            hi[2] = fmaxf(hi[2], z);
+        }
     }
     block_minmax(s, lo, hi);
     if constexpr (!SINGLE) {
@@ -91,7 +106,7 @@ __global__ void __launch_bounds__(256) minmax_geom_kernel(const float* __restric
         __threadfence();
         const volatile float* vp = part;  // the other blocks' partials, past this CU's cache
         for (int d = 0; d < 3; ++d) lo[d] = INFINITY, hi[d] = -INFINITY;
-        for (int b = threadIdx.x; b < (int)gridDim.x; b += 256) {
+        for (int b = threadIdx.x; b < (int)gridDim.x; b += NT) {
 #pragma unroll
             for (int d = 0; d < 3; ++d) {
                 lo[d] = fminf(lo[d], vp[b * 6 + d]);
@@ -175,110 +190,82 @@ __global__ void voxel_bounds_kernel(const uint32_t* __restrict__ keys, int64_t n
     if (j + 1 == n || keys[j + 1] != key) ends[r] = (uint32_t)(j + 1);
 }
 
-constexpr int kLaneRun = 16;  // runs up to this length: one lane; longer: one wave
-constexpr int kBigBlocks = 128;  // waves striding the long-run list (a sweep has a few dozen long runs)
-
-template <int NF>
-__device__ __forceinline__ void write_centroid(float* __restrict__ o, const float* acc, int stride, uint32_t cnt) {
-    const float c = (float)cnt;
+// PCL VoxelGrid centroid: a voxel's fields summed one point at a time in input order (float), divided by
+// the count.  One wave per 64 consecutive voxels, lane = voxel: their runs are one contiguous stretch of
+// the sorted order, which the wave streams through LDS kCentCh points at a time (4 per lane, the next
+// chunk's loads in flight while this one is summed); each lane then adds the staged points of its own
+// run in order.  The adds of a run are its serial part (PCL's order); the loads are one round trip per
+// chunk for all 64 voxels, whatever their run lengths.  xyz / sel (optional): the packed centroid xyz and
+// zeroed selection flags of the scan the output becomes (lio_scan_preprocess), in the same pass.
+constexpr int kCentCh = 256;
+__global__ void __launch_bounds__(64) voxel_centroid_wave_kernel(const float* __restrict__ p, int stride,
+                                                                  const uint32_t* __restrict__ vals,
+                                                                  const uint32_t* __restrict__ starts,
+                                                                  const uint32_t* __restrict__ ends,
+                                                                  const uint32_t* __restrict__ n_vox,
+                                                                  float* __restrict__ out, float* __restrict__ xyz,
+                                                                  uint8_t* __restrict__ sel) {
+    __shared__ float s_q[2][kCentCh * kMaxFields];
+    constexpr int PL = kCentCh / 64;
+    const int lane = threadIdx.x;
+    const uint32_t nv = *n_vox;
+    const uint32_t v0 = blockIdx.x * 64u;
+    if (v0 >= nv) return;  // block-uniform
+    const uint32_t v = v0 + (uint32_t)lane, vl = min(v0 + 63u, nv - 1u);
+    const bool mine = v < nv;
+    const uint32_t s = mine ? starts[v] : 0u, e = mine ? ends[v] : 0u;
+    const uint32_t R0 = starts[v0], R1 = ends[vl];  // the wave's stretch of the sorted order
+    float q[PL][kMaxFields];
+    auto load = [&](uint32_t k) {
 #pragma unroll
-    for (int f = 0; f < NF; ++f)
-        if (f < stride) o[f] = acc[f] / c;
-}
-
-// PCL VoxelGrid centroid: the voxel's fields summed one point at a time in
-// input order (float), divided by the count.  The chain of adds is serial, the
-// loads are not: short runs are summed by one lane with its loads issued four
-// points ahead; long runs (the dense ground next to the sensor) go to a wave.
-__global__ void voxel_centroid_kernel(const float* __restrict__ p, int stride, const uint32_t* __restrict__ vals,
-                                      const uint32_t* __restrict__ starts, const uint32_t* __restrict__ ends,
-                                      const uint32_t* __restrict__ n_vox, uint32_t* __restrict__ big,
-                                      uint32_t* __restrict__ n_big, float* __restrict__ out) {
-    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= *n_vox) return;
-    const uint32_t s = starts[v], e = ends[v];
-    if (e - s > (uint32_t)kLaneRun) {
-        big[atomicAdd(n_big, 1u)] = v;
-        return;
-    }
-    float acc[kMaxFields];
-#pragma unroll
-    for (int f = 0; f < kMaxFields; ++f) acc[f] = 0.f;
-    for (uint32_t k = s; k < e; k += 4) {
-        float q[4][kMaxFields];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const float* r = p + (size_t)vals[k + u < e ? k + u : s] * stride;
+        for (int u = 0; u < PL; ++u) {
+            const uint32_t t = k + (uint32_t)(u * 64 + lane);
+            const float* r = p + (size_t)vals[t < R1 ? t : R0] * stride;
 #pragma unroll
             for (int f = 0; f < kMaxFields; ++f) q[u][f] = f < stride ? r[f] : 0.f;
         }
+    };
+    auto stash = [&](int buf) {
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (k + u < e) {
-#pragma unroll
-                for (int f = 0; f < kMaxFields; ++f) acc[f] += q[u][f];
-            }
-    }
-    write_centroid<kMaxFields>(out + (size_t)v * stride, acc, stride, e - s);
-}
-
-// long runs, one wave (= block) each: the lanes load 64 points at a time into
-// LDS (the next chunk's loads in flight while this one is summed); lane f
-// then adds field f of the 64 points in order — one LDS read + one add per
-// point, the fields in parallel
-__global__ void __launch_bounds__(64) voxel_centroid_big_kernel(const float* __restrict__ p, int stride,
-                                                                 const uint32_t* __restrict__ vals,
-                                                                 const uint32_t* __restrict__ starts,
-                                                                 const uint32_t* __restrict__ ends,
-                                                                 const uint32_t* __restrict__ big,
-                                                                 const uint32_t* __restrict__ n_big,
-                                                                 float* __restrict__ out) {
-    __shared__ float s_q[2][64 * kMaxFields];
-    const int lane = threadIdx.x;
-    const uint32_t nb = *n_big;
-    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
-        const uint32_t v = big[b];
-        const uint32_t s = starts[v], e = ends[v];
-        float q[kMaxFields];
-        auto load = [&](uint32_t k) {
-            const float* r = p + (size_t)vals[k + lane < e ? k + lane : s] * stride;
-#pragma unroll
-            for (int f = 0; f < kMaxFields; ++f) q[f] = f < stride ? r[f] : 0.f;
-        };
-        auto stash = [&](int buf) {
+        for (int u = 0; u < PL; ++u)
 #pragma unroll
             for (int f = 0; f < kMaxFields; ++f)
-                if (f < stride) s_q[buf][lane * stride + f] = q[f];
-        };
-        float acc = 0.f;
-        load(s);
-        stash(0);
-        __syncthreads();
-        int buf = 0;
-        for (uint32_t k = s; k < e; k += 64) {
-            const bool more = k + 64 < e;
-            if (more) load(k + 64);
-            const uint32_t m = min(64u, e - k);
-            if (lane < stride) {
-                const float* col = s_q[buf] + lane;
-                uint32_t l = 0;
-                for (; l + 4 <= m; l += 4) {
-                    const float a0 = col[(l + 0) * stride], a1 = col[(l + 1) * stride];
-                    const float a2 = col[(l + 2) * stride], a3 = col[(l + 3) * stride];
-                    acc += a0;
-                    acc += a1;
-                    acc += a2;
-                    acc += a3;
-                }
-                for (; l < m; ++l) acc += col[l * stride];
-            }
-            if (more) {
-                stash(buf ^ 1);
-                buf ^= 1;
-            }
-            __syncthreads();
+                if (f < stride) s_q[buf][(u * 64 + lane) * stride + f] = q[u][f];
+    };
+    float acc[kMaxFields];
+#pragma unroll
+    for (int f = 0; f < kMaxFields; ++f) acc[f] = 0.f;
+    load(R0);
+    stash(0);
+    __syncthreads();
+    int buf = 0;
+    for (uint32_t k = R0; k < R1; k += kCentCh) {
+        const bool more = k + kCentCh < R1;
+        if (more) load(k + kCentCh);
+        const uint32_t lo = max(s, k), hi = min(e, k + (uint32_t)kCentCh);
+        for (uint32_t t = lo; t < hi; ++t) {
+            const float* r = s_q[buf] + (t - k) * stride;
+#pragma unroll
+            for (int f = 0; f < kMaxFields; ++f)
+                if (f < stride) acc[f] += r[f];
         }
-        if (lane < stride) out[(size_t)v * stride + lane] = acc / (float)(e - s);
+        if (more) {
+            stash(buf ^ 1);
+            buf ^= 1;
+        }
+        __syncthreads();
+    }
+    if (!mine) return;
+    const float c = (float)(e - s);
+    float* o = out + (size_t)v * stride;
+#pragma unroll
+    for (int f = 0; f < kMaxFields; ++f)
+        if (f < stride) o[f] = acc[f] / c;
+    if (xyz) {
+        xyz[3 * (size_t)v] = acc[0] / c;
+        xyz[3 * (size_t)v + 1] = acc[1] / c;
+        xyz[3 * (size_t)v + 2] = acc[2] / c;
+        sel[v] = 0;
     }
 }
 
@@ -700,13 +687,13 @@ void filter_free(FilterBuf& b) {
 // copied.  cnt (optional, device): rows in use <= n.  The voxel sort uses b.vox_bits key bits (learnt from
 // the previous call; a key past them raises the flag and the caller runs the call again at full width).
 int voxel_grid_enqueue(FilterBuf& b, const float* d_in, int64_t n, const uint32_t* cnt, int stride, const float leaf[3],
-                       float* d_out, hipStream_t st) {
+                       float* d_out, hipStream_t st, float* xyz = nullptr, uint8_t* sel = nullptr) {
     if (stride < 3 || stride > kMaxFields || n >= (int64_t)0x7fffffff) return -1;
     if (reserve(b, n)) return -5;
     auto* hgeom = reinterpret_cast<VoxelGeom*>(b.d_small + 1);
-    if (n <= 256 * 64) {  // one block: no partials, no ticket
-        minmax_geom_kernel<true><<<1, 256, 0, st>>>(d_in, n, cnt, stride, b.part, b.cnt + 1, leaf[0], leaf[1], leaf[2],
-                                                    b.geom, hgeom);
+    if (n <= 1024 * 64) {  // one block: no partials, no ticket, no fence
+        minmax_geom_kernel<true, 1024><<<1, 1024, 0, st>>>(d_in, n, cnt, stride, b.part, b.cnt + 1, leaf[0], leaf[1],
+                                                           leaf[2], b.geom, hgeom);
     } else {
         const int nbA = (int)std::min<int64_t>(1024, (n + 255) / 256);
         minmax_geom_kernel<false><<<nbA, 256, 0, st>>>(d_in, n, cnt, stride, b.part, b.cnt + 1, leaf[0], leaf[1],
@@ -722,10 +709,8 @@ int voxel_grid_enqueue(FilterBuf& b, const float* d_in, int64_t n, const uint32_
     if (rc) return rc;
     // runs -> [start, end) per voxel (b.keys / b.vals are free after the sort)
     voxel_bounds_kernel<<<nblk(n), 256, 0, st>>>(b.keys_alt, n, b.head, b.vid, b.keys, b.vals, b.cnt + 2, b.d_small);
-    voxel_centroid_kernel<<<nblk(n), 256, 0, st>>>(d_in, stride, b.vals_alt, b.keys, b.vals, b.vid + n, b.big,
-                                                   b.big + b.cap, d_out);
-    voxel_centroid_big_kernel<<<kBigBlocks, 64, 0, st>>>(d_in, stride, b.vals_alt, b.keys, b.vals, b.big,
-                                                         b.big + b.cap, d_out);
+    voxel_centroid_wave_kernel<<<(int)((n + 63) / 64), 64, 0, st>>>(d_in, stride, b.vals_alt, b.keys, b.vals, b.vid + n,
+                                                                     d_out, xyz, sel);
     FCHK(hipGetLastError());
     return 0;
 }
@@ -816,7 +801,7 @@ int keyframe_cloud(const float* d_rec, int64_t n, int stride, const PoseArg& ps,
 
 int scan_preprocess_enqueue(FilterBuf& b, const float* d_raw, int64_t n, int stride, const ScanPrepParams& p,
                             const ImuPose* d_poses, int np, const UndistortEnd& end, float* d_out, hipStream_t st,
-                            int presel) {
+                            int presel, float* xyz, uint8_t* sel) {
     b.prep_n = 0;
     b.prep_sel = -1;
     if (n <= 0) return 0;
@@ -853,7 +838,7 @@ int scan_preprocess_enqueue(FilterBuf& b, const float* d_raw, int64_t n, int str
     b.prep_sel = presel >= 0 ? n : -1;
     if (b.prep_leaf) {
         const float leaf[3] = {p.leaf, p.leaf, p.leaf};
-        return voxel_grid_enqueue(b, b.c, n, cnt, stride, leaf, d_out, st);
+        return voxel_grid_enqueue(b, b.c, n, cnt, stride, leaf, d_out, st, xyz, sel);
     }
     FCHK(hipMemcpyAsync(d_out, b.c, (size_t)n * stride * sizeof(float), hipMemcpyDeviceToDevice, st));
     return 0;

@@ -89,9 +89,11 @@ int scan_preprocess(FilterBuf& b, const float* d_raw, int64_t n, int stride, con
 // presel >= 0: the n rows are already Preprocess's selection, in input order (the host packed them), and
 // presel = 1 says their times are non-decreasing — the stable time sort is then the identity and is skipped.
 // _finish returns 2 when the learnt voxel-key width was too narrow: the caller enqueues again (same input).
+// xyz / sel (optional, leaf > 0): the output's packed xyz and zeroed selection flags written by the
+// centroid pass (rows past the voxel count untouched)
 int scan_preprocess_enqueue(FilterBuf& b, const float* d_raw, int64_t n, int stride, const ScanPrepParams& p,
                             const ImuPose* d_poses, int np, const UndistortEnd& end, float* d_out, hipStream_t st,
-                            int presel = -1);
+                            int presel = -1, float* xyz = nullptr, uint8_t* sel = nullptr);
 int scan_preprocess_finish(FilterBuf& b, int stride, float* d_out, int64_t* n_out, int64_t* n_undist, hipStream_t st);
 // records -> packed xyz, and sel[0 .. n) = 0 (the scan's selection flags) in the same pass
 int records_to_xyz_sel(const float* d_rec, int64_t n, int stride, float* d_xyz, uint8_t* sel, hipStream_t st);

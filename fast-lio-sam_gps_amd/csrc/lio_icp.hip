@@ -330,21 +330,6 @@ __device__ __forceinline__ void row_pieces(const GridDev& g, const CellBox& N, c
     }
 }
 
-// candidates scan_rows would stream for (N, S, B): wave-uniform, the row table only (no points read)
-__device__ uint32_t count_rows(const GridDev& g, const CellBox& N, const CellBox& S, float B, const float (&qb)[6]) {
-    const int lane = threadIdx.x & 63;
-    const int nrows = (N.y1 - N.y0 + 1) * (N.z1 - N.z0 + 1);
-    uint32_t tot = 0;
-#pragma unroll 1
-    for (int rb = 0; rb < nrows; rb += kIcpTileQ) {
-        uint32_t b0 = 0, n0 = 0, b1 = 0, n1 = 0;
-        float g2 = INFINITY;
-        if (rb + lane < nrows) row_pieces(g, N, S, B, qb, rb + lane, b0, n0, b1, n1, g2);
-        tot += (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_dpp(n0 + n1), 63);
-    }
-    return tot;
-}
-
 template <int NW>
 __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const CellBox& S, float B, float qx0, float qx1,
                           float qy0, float qy1, float qz0, float qz1, bool act, float x, float y, float z,
@@ -395,13 +380,9 @@ __device__ __forceinline__ uint64_t tile_min(uint64_t best, uint64_t* s_best) {
     return best;
 }
 
-// One tile's exact 1-NN.  NW waves split the tile's candidate stream (block-level merges).  DEFER (the
-// main launch of a pass without previous correspondences): a tile whose final box holds more than
-// a.defer_cand candidates stops after its bound, leaves each lane's best as the prior (nn_id / nn_d2,
-// cur transformed), and queues itself on a.heavy for icp_heavy_kernel, which splits its stream over
-// kIcpHeavyNW waves on an otherwise idle chip — the first pass's tail is a few such tiles, each
-// one wave sharing its SIMD with seven others (profiles/r03_icp_tile_timeline.txt).
-template <int NW, bool DEFER>
+// One tile's exact 1-NN (one wave per tile: NW = 1; NW > 1 splits the tile's candidate stream over NW
+// waves with block-level merges — measured no faster, profiles/r02_icp_tile_experiments.txt).
+template <int NW>
 __device__ __forceinline__ void icp_tile_body(const IcpArgs& a, int tix, TileLds& L, uint64_t* s_best) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #ifdef LIO_DIAG
@@ -469,27 +450,6 @@ __device__ __forceinline__ void icp_tile_body(const IcpArgs& a, int tix, TileLds
         // the scanned box may stick out of N (a grown box): clip it, the part outside N is not needed
         CellBox Sc{max(S.x0, N.x0), min(S.x1, N.x1), max(S.y0, N.y0), min(S.y1, N.y1), max(S.z0, N.z0), min(S.z1, N.z1)};
         if (Sc.y0 > Sc.y1 || Sc.z0 > Sc.z1) Sc.x0 = 1, Sc.x1 = 0;
-        if constexpr (DEFER) {
-            if (!grow) {
-                const float qb[6] = {qx0, qx1, qy0, qy1, qz0, qz1};
-                if (count_rows(g, N, Sc, B, qb) > a.defer_cand) {  // wave-uniform
-                    if (act) {
-                        if (a.fitness || a.apply_T) {
-                            a.cur[3 * i] = x;
-                            a.cur[3 * i + 1] = y;
-                            a.cur[3 * i + 2] = z;
-                        }
-                        a.nn_d2[i] = __uint_as_float((uint32_t)(best >> 32));
-                        a.nn_id[i] = (int)(uint32_t)best;
-                    }
-                    if (lane == 0) {
-                        a.heavy[2 + atomicAdd(a.heavy, 1u)] = (uint32_t)tix;
-                        if (a.dbg) atomicAdd(a.dbg + 5, 1ull);
-                    }
-                    return;
-                }
-            }
-        }
         scan_rows<NW>(g, L, N, Sc, B, qx0, qx1, qy0, qy1, qz0, qz1, act, x, y, z, best, cand, tested);
         best = tile_min<NW>(best, s_best);
         ++rounds;
@@ -536,31 +496,12 @@ __device__ __forceinline__ void icp_tile_body(const IcpArgs& a, int tix, TileLds
 }
 
 
-// the main launch: one wave per tile, tile = its XCD's next one (icp_tile_of)
-template <bool DEFER>
-__global__ void __launch_bounds__(kIcpTileQ) __attribute__((amdgpu_waves_per_eu(7))) icp_tile_kernel(IcpArgs a, int ntiles) {
+// one wave per tile, tile = its XCD's next one (icp_tile_of)
+__global__ void __launch_bounds__(kIcpTileQ) icp_tile_kernel(IcpArgs a, int ntiles) {
     __shared__ TileLds L;
     const int tix = icp_tile_of(a.order, (int)blockIdx.x, ntiles);
     if (tix < 0) return;  // block-uniform: a slot past its XCD's share
-    icp_tile_body<1, DEFER>(a, tix, L, nullptr);
-}
-
-// the deferred tiles (a.heavy: [0] count, [1] finish ticket, [2 ..] tiles), kIcpHeavyNW waves each; the
-// last block to finish clears the count and the ticket for the next pass
-constexpr int kIcpHeavyNW = 8, kIcpHeavyBlocks = 256;
-__global__ void __launch_bounds__(kIcpTileQ * kIcpHeavyNW) icp_heavy_kernel(IcpArgs a) {
-    __shared__ TileLds Ls[kIcpHeavyNW];
-    __shared__ uint64_t s_best[kIcpHeavyNW * kIcpTileQ];
-    const int nh = (int)a.heavy[0];
-    for (int h = blockIdx.x; h < nh; h += gridDim.x)
-        icp_tile_body<kIcpHeavyNW, false>(a, (int)a.heavy[2 + h], Ls[threadIdx.x >> 6], s_best);
-    if (threadIdx.x == 0) {
-        __threadfence();
-        if (atomicAdd(a.heavy + 1, 1u) == gridDim.x - 1) {
-            a.heavy[0] = 0u;
-            a.heavy[1] = 0u;
-        }
-    }
+    icp_tile_body<1>(a, tix, L, nullptr);
 }
 
 // One block = one 4096-point record -> super[record][kIcpStride]: each lane
@@ -638,16 +579,7 @@ __global__ void __launch_bounds__(kIcpStatsThreads) icp_stats_kernel(IcpArgs a, 
 void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st) {
     if (a.n == 0 || ntiles == 0) return;
     const int seg = (ntiles + kIcpSegs - 1) / kIcpSegs;
-    const int grid = 8 * (kIcpSegs / 8) * seg;
-    if (!a.heavy || a.defer_cand == 0 || a.prior) {
-        icp_tile_kernel<false><<<grid, kIcpTileQ, 0, st>>>(a, ntiles);
-        return;
-    }
-    icp_tile_kernel<true><<<grid, kIcpTileQ, 0, st>>>(a, ntiles);
-    IcpArgs h = a;  // the deferred tiles resume from the bounds they left (cur already transformed)
-    h.apply_T = 0;
-    h.prior = 1;
-    icp_heavy_kernel<<<kIcpHeavyBlocks, kIcpTileQ * kIcpHeavyNW, 0, st>>>(h);
+    icp_tile_kernel<<<8 * (kIcpSegs / 8) * seg, kIcpTileQ, 0, st>>>(a, ntiles);
 }
 
 // Tile order for the next pass from this pass's candidate counts.  The cell-ordered tiles are cut

@@ -318,8 +318,6 @@ struct lio_icp {
     bool have_prior = false;  // nn ids of this alignment's previous pass are in d_fid
     uint32_t* d_tcost = nullptr;  // per tile: candidates of the last pass
     uint32_t* d_order = nullptr;  // longest-first tile order (valid when have_order)
-    uint32_t* d_heavy = nullptr;  // first-pass deferred tiles (lio_icp.hip icp_heavy_kernel)
-    int64_t defer_cand = -1;      // lio_icp_set_defer_threshold; -1: icp_defer_cand()
     bool have_order = false;
     unsigned long long* d_dbg = nullptr;  // search counters (diagnostics build: LIO_DIAG + LIO_ICP_DEBUG)
     size_t dbg_bytes = 0;
@@ -340,7 +338,24 @@ struct lio_icp {
     bool timing = false;
     lio_kernel_timing tm{};
     EvPair ev;
+    // set-up started by lio_icp_set_target / _set_source that runs on behind the caller (the target's upload
+    // and grid on st2, the source's upload and binning on st): every other entry point joins them first; a
+    // failure leaves the dirty flag set, so lio_icp_align repeats the step and reports it
+    std::thread bg_tgt, bg_src;
 };
+
+static void icp_join(lio_icp* h) {
+    if (h->bg_src.joinable()) h->bg_src.join();
+    if (h->bg_tgt.joinable()) h->bg_tgt.join();
+}
+// the two set-ups touch disjoint state (target: st2, d_tgt, tgt grid, c0; source: st, the shard buffers),
+// so a new target only waits for the previous target's thread and a new source for the previous source's
+static void icp_join_tgt(lio_icp* h) {
+    if (h->bg_tgt.joinable()) h->bg_tgt.join();
+}
+static void icp_join_src(lio_icp* h) {
+    if (h->bg_src.joinable()) h->bg_src.join();
+}
 
 static int icp_check_dev(int dev) {
     int n = 0;
@@ -388,6 +403,7 @@ int lio_icp_create(const lio_icp_params* p, lio_icp** out) {
 // internal (lio_icp_mp.cpp): hand the exchange state of a multi-process shard to the handle (freed with it,
 // or when another exchange replaces it)
 void lio_icp_set_exchange_owner(lio_icp* h, void* owner, void (*free_fn)(void*)) {
+    icp_join(h);
     if (h->x_owner && h->x_owner_free) {
         (void)hipSetDevice(h->dev);
         (void)hipStreamSynchronize(h->st);
@@ -401,13 +417,14 @@ int lio_icp_device(const lio_icp* h) { return h->dev; }
 
 int lio_icp_destroy(lio_icp* h) {
     if (!h) return LIO_OK;
+    icp_join(h);
     (void)hipSetDevice(h->dev);
     (void)hipStreamSynchronize(h->st);
     lio_icp_set_exchange_owner(h, nullptr, nullptr);
     lio::grid_free(h->tgt);
     lio::grid_free(h->qgrid);
     void* ptrs[] = {h->d_tgt,   h->d_src,     h->d_cur,  h->d_fd2,   h->d_fid,   h->d_tiles, h->d_tscratch,
-                    h->d_ttmp,  h->d_dbg,     h->d_tcost, h->d_order, h->d_pcl16, h->d_heavy};
+                    h->d_ttmp,  h->d_dbg,     h->d_tcost, h->d_order, h->d_pcl16};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (h->h_super) (void)hipHostFree(h->h_super);
@@ -461,14 +478,20 @@ static int stage_pinned(float*& buf, int64_t& cap, const float* xyz, int64_t n) 
     return LIO_OK;
 }
 
+static int target_build(lio_icp* h);
+static int icp_prepare(lio_icp* h);
+
 int lio_icp_set_target(lio_icp* h, const float* xyz, int64_t n) {
     if (!h || n <= 0 || !xyz) return ifail(LIO_ERR_ARG, "lio_icp_set_target: bad arguments");
+    icp_join_tgt(h);
     IHIP(hipSetDevice(h->dev));
     IHIP(hipStreamSynchronize(h->st2));  // a previous target upload may still read the staging buffer
     const int rc = stage_pinned(h->h_tgt, h->h_tgt_cap, xyz, n);
     if (rc) return rc;
     h->nt = n;
     h->tgt_dirty = true;
+    // upload + grid on st2 behind the caller: overlaps the source's set-up and whatever the caller does next
+    h->bg_tgt = std::thread([h] { (void)target_build(h); });
     return LIO_OK;
 }
 
@@ -496,6 +519,7 @@ static int target_build(lio_icp* h) {
 
 int lio_icp_set_source(lio_icp* h, const float* xyz, int64_t n) {
     if (!h || n < 0 || (n > 0 && !xyz) || n >= (int64_t)1 << 30) return ifail(LIO_ERR_ARG, "lio_icp_set_source: bad arguments");
+    icp_join_src(h);
     IHIP(hipSetDevice(h->dev));
     IHIP(hipStreamSynchronize(h->st));  // the previous source upload may still read the staging buffer
     if (n > 0) {
@@ -504,11 +528,17 @@ int lio_icp_set_source(lio_icp* h, const float* xyz, int64_t n) {
     }
     h->ns = n;
     h->src_dirty = true;
+    // this rank's shard uploaded and binned on st behind the caller (a later lio_icp_set_shard* marks it
+    // dirty again and align repeats it for the new shard)
+    h->bg_src = std::thread([h] {
+        if (hipSetDevice(h->dev) == hipSuccess) (void)icp_prepare(h);
+    });
     return LIO_OK;
 }
 
 int lio_icp_set_shard(lio_icp* h, int rank, int world, lio_allgather_fn fn, void* user) {
     if (!h || world < 1 || rank < 0 || rank >= world || (world > 1 && !fn))
+    icp_join(h);
         return ifail(LIO_ERR_ARG, "lio_icp_set_shard: bad arguments");
     h->rank = rank;
     h->world = world;
@@ -522,6 +552,7 @@ int lio_icp_set_shard(lio_icp* h, int rank, int world, lio_allgather_fn fn, void
 
 int lio_icp_set_shard_device(lio_icp* h, int rank, int world, lio_allgather_dev_fn fn, void* user) {
     if (!h || world < 1 || rank < 0 || rank >= world || (world > 1 && !fn))
+    icp_join(h);
         return ifail(LIO_ERR_ARG, "lio_icp_set_shard_device: bad arguments");
     h->rank = rank;
     h->world = world;
@@ -546,6 +577,7 @@ int lio_icp_exchange_len(int64_t n_source, int world, int64_t* n_per_rank) {
 
 int lio_icp_set_exchange_buffers(lio_icp* h, double* d_send, double* d_recv, int64_t n_per_rank) {
     if (!h || !d_send || !d_recv || n_per_rank <= 0) return ifail(LIO_ERR_ARG, "lio_icp_set_exchange_buffers: bad arguments");
+    icp_join(h);
     IHIP(hipSetDevice(h->dev));
     if (!h->x_ext) {
         if (h->d_xsend) IHIP(hipFree(h->d_xsend));
@@ -589,7 +621,7 @@ static int icp_prepare(lio_icp* h) {
     const int64_t n = std::max<int64_t>(h->sh_n, 1);
     if (n > h->cap) {
         void** ptrs[] = {(void**)&h->d_src,   (void**)&h->d_cur,   (void**)&h->d_fd2,  (void**)&h->d_fid,
-                         (void**)&h->d_tiles, (void**)&h->d_tcost, (void**)&h->d_order, (void**)&h->d_heavy};
+                         (void**)&h->d_tiles, (void**)&h->d_tcost, (void**)&h->d_order};
         h->cap = 0;  // a failed allocation below leaves no buffer that looks usable (and nothing freed twice)
         for (void** q : ptrs) {
             if (*q) (void)hipFree(*q);
@@ -602,8 +634,6 @@ static int icp_prepare(lio_icp* h) {
         IHIP(hipMalloc(&h->d_tiles, (n + n / lio::kIcpTileQ + 1) * sizeof(uint2)));
         IHIP(hipMalloc(&h->d_tcost, (n + n / lio::kIcpTileQ + 1) * sizeof(uint32_t)));
         IHIP(hipMalloc(&h->d_order, (n + n / lio::kIcpTileQ + 64) * sizeof(uint32_t)));  // + the 9 share offsets
-        IHIP(hipMalloc(&h->d_heavy, (n + n / lio::kIcpTileQ + 3) * sizeof(uint32_t)));
-        IHIP(hipMemsetAsync(h->d_heavy, 0, 2 * sizeof(uint32_t), h->st));  // count and ticket: zero between passes
         h->cap = n;
     }
     const int64_t nsup_all = (h->ns + lio::kIcpSuper - 1) / lio::kIcpSuper + 1;
@@ -695,17 +725,6 @@ static int pcl_finish(lio_icp* h, const lio::IcpArgs& a) {
     return LIO_OK;
 }
 
-// A pass without previous correspondences defers the tiles whose final box streams more candidates than
-// this to a second launch with several waves per tile (lio_icp.hip icp_heavy_kernel); LIO_ICP_DEFER
-// overrides it (0: off) for A/B runs
-static uint32_t icp_defer_cand() {
-    static const uint32_t v = [] {
-        const char* e = std::getenv("LIO_ICP_DEFER");
-        return e ? (uint32_t)std::strtoul(e, nullptr, 10) : 3072u;
-    }();
-    return v;
-}
-
 // One correspondence (or fitness) pass: GPU kernels + exchange + ordered sum.
 static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, double max_d2, double out17[17],
                     float* pcl16 = nullptr) {
@@ -728,8 +747,6 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     a.tiles = h->d_tiles;
     a.tile_cost = h->d_tcost;
     a.order = h->have_order ? h->d_order : nullptr;
-    a.heavy = h->d_heavy;
-    a.defer_cand = h->defer_cand >= 0 ? (uint32_t)h->defer_cand : icp_defer_cand();
 #ifdef LIO_DIAG
     static const bool dbg_on = std::getenv("LIO_ICP_DEBUG") != nullptr;  // diagnostics build: search statistics
     if (dbg_on) {
@@ -787,12 +804,11 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     if (!fitness && h->sh_n > 0) h->have_order = true;
 #ifdef LIO_DIAG
     if (dbg_on) {
-        unsigned long long c[6];
+        unsigned long long c[5];
         IHIP(hipMemcpy(c, h->d_dbg, sizeof(c), hipMemcpyDeviceToHost));
         std::fprintf(stderr,
-                     "icp dbg: tiles|waves %llu lanes %llu cand/tile %.1f tested/tile %.1f rounds/tile %.2f cand/lane %.1f "
-                     "deferred %llu\n",
-                     c[2], c[3], (double)c[0] / c[2], (double)c[4] / c[2], (double)c[1] / c[2], (double)c[0] / c[3], c[5]);
+                     "icp dbg: tiles|waves %llu lanes %llu cand/tile %.1f tested/tile %.1f rounds/tile %.2f cand/lane %.1f\n",
+                     c[2], c[3], (double)c[0] / c[2], (double)c[4] / c[2], (double)c[1] / c[2], (double)c[0] / c[3]);
         // per-tile timeline (wall clock, 100 MHz): span, duration percentiles, the tail
         std::vector<unsigned long long> tt(2 * (size_t)h->ntiles);
         std::vector<uint32_t> cost(h->ntiles);
@@ -881,20 +897,16 @@ extern "C" int lio_icp_umeyama_pcl_float_order(const float* sums16, int order, f
 
 extern "C" int lio_icp_get_fidelity_stats(lio_icp* h, int64_t* out4) {
     if (!h || !out4) return ifail(LIO_ERR_ARG, "lio_icp_get_fidelity_stats: bad arguments");
+    icp_join(h);
     std::memcpy(out4, h->fid_stats, sizeof(h->fid_stats));
     return LIO_OK;
 }
 
 extern "C" int lio_icp_set_fidelity_debug(lio_icp* h, int flags, int64_t evcap) {
     if (!h || evcap < 0) return ifail(LIO_ERR_ARG, "lio_icp_set_fidelity_debug: bad arguments");
+    icp_join(h);
     h->fid_flags = flags;
     h->fid_evcap = evcap;
-    return LIO_OK;
-}
-
-extern "C" int lio_icp_set_defer_threshold(lio_icp* h, int64_t candidates) {
-    if (!h || candidates < -1 || candidates > 0xffffffffll) return ifail(LIO_ERR_ARG, "lio_icp_set_defer_threshold: bad arguments");
-    h->defer_cand = candidates;
     return LIO_OK;
 }
 
@@ -957,6 +969,7 @@ extern "C" int lio_icp_combine(const double* recv, int64_t ns, int world, double
 
 int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* aligned) {
     if (!h || !out) return ifail(LIO_ERR_ARG, "lio_icp_align: bad arguments");
+    icp_join(h);
     if (h->nt == 0) return ifail(LIO_ERR_STATE, "lio_icp_align: no target");
     IHIP(hipSetDevice(h->dev));
     const bool pcl_float = h->p.umeyama_float != 0;
@@ -1117,6 +1130,7 @@ int icp_align(const float* src, int64_t ns, const float* dst, int64_t nd, const 
 
 int lio_icp_get_correspondences(lio_icp* h, int32_t* ids, float* d2) {
     if (!h || !ids || !d2) return ifail(LIO_ERR_ARG, "bad arguments");
+    icp_join(h);
     if (!h->have_prior) return ifail(LIO_ERR_STATE, "lio_icp_get_correspondences: no pass run yet");
     IHIP(hipSetDevice(h->dev));
     if (h->sh_n > 0) {
@@ -1129,11 +1143,13 @@ int lio_icp_get_correspondences(lio_icp* h, int32_t* ids, float* d2) {
 
 int lio_icp_set_timing(lio_icp* h, int enable) {
     if (!h) return ifail(LIO_ERR_ARG, "NULL handle");
+    icp_join(h);
     h->timing = enable != 0;
     return LIO_OK;
 }
 int lio_icp_get_timing(lio_icp* h, lio_kernel_timing* out) {
     if (!h || !out) return ifail(LIO_ERR_ARG, "bad arguments");
+    icp_join(h);
     *out = h->tm;
     return LIO_OK;
 }

@@ -146,9 +146,7 @@ struct IcpArgs {
     const uint2* tiles;  // (first entry in qpts, query count <= kIcpTileQ) per tile
     const uint32_t* order;  // optional tile visit order (heaviest first, from the previous pass's costs)
     uint32_t* tile_cost;    // per tile: candidates scanned in this pass
-    unsigned long long* dbg;  // optional counters (diagnostics): candidates, rings, tiles, lanes, tested, deferred
-    uint32_t* heavy;          // optional: deferred tiles ([0] count, [1] ticket, [2 ..] tiles; zero between passes)
-    uint32_t defer_cand;      // passes without prior: defer tiles whose final box streams more candidates (0: off)
+    unsigned long long* dbg;  // optional counters (diagnostics): candidates, rings, tiles, lanes, tested
 };
 
 constexpr int kIcpSuper = 4096;    // points per exchanged partial (shard granule)

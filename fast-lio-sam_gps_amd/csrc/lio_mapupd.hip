@@ -1325,8 +1325,17 @@ int map_delete_boxes(GridBuf& g, MapUpdBuf& u, const float* boxes, int nb, float
 // one host synchronisation.  out: [to_add, no_need, skipped, added_by_downsample_call]
 // The update scratch sized for n offered points before the first update (lio_map_build): the first
 // map_incremental of a stream then allocates nothing (~8 ms of set-up on the first call)
+// an empty launch from this file: with HIP's deferred code-object loading the first launch from a code
+// object loads it (8-12 ms measured on the first map_incremental, 0.19 ms with HIP_ENABLE_DEFERRED_LOADING=0:
+// scripts/map_first_call.py), so lio_map_build pays it instead of the first update
+__global__ void mapupd_warm_kernel(uint32_t* __restrict__ p) {
+    if (p && threadIdx.x == 1024) p[0] = 0u;  // never true: keeps the kernel non-empty for the compiler
+}
+
 int mapupd_presize(MapUpdBuf& u, int64_t n, hipStream_t st) {
     if (n <= 0) return 0;
+    mapupd_warm_kernel<<<1, 64, 0, st>>>(nullptr);
+    UPD_CHK(hipGetLastError());
     if (n >= (int64_t)1 << 30) return -1;
     if (ensure_pts(u, n, st)) return -5;
     size_t b1 = 0, b2 = 0, b3 = 0;

@@ -41,7 +41,7 @@ EXPORTS = [
     "lio_icp_group_uses_rccl", "lio_icp_group_set_target", "lio_icp_group_set_source", "lio_icp_group_align",
     "lio_icp_shard_range", "lio_icp_combine", "lio_icp_umeyama_pcl_float", "lio_icp_get_correspondences",
     "lio_ctx_set_timing", "lio_ctx_get_timing", "lio_ctx_reset_timing", "lio_icp_set_timing", "lio_icp_get_timing",
-    "lio_icp_umeyama_pcl_float_order", "lio_icp_get_fidelity_stats", "lio_icp_set_fidelity_debug", "lio_icp_set_defer_threshold", "lio_seqsum6",
+    "lio_icp_umeyama_pcl_float_order", "lio_icp_get_fidelity_stats", "lio_icp_set_fidelity_debug", "lio_seqsum6",
     "lio_map_set_test_limits", "lio_rccl_unique_id", "lio_icp_set_shard_rccl", "lio_icp_set_shard_shm",
     "lio_shm_exchange_open", "lio_shm_exchange_allgather", "lio_shm_exchange_close",
 ]
@@ -228,7 +228,6 @@ def _declare(L):
         "lio_icp_umeyama_pcl_float_order": (C.c_int, [fp, C.c_int, fp]),
         "lio_icp_get_fidelity_stats": (C.c_int, [vp, C.POINTER(C.c_int64)]),
         "lio_icp_set_fidelity_debug": (C.c_int, [vp, C.c_int, C.c_int64]),
-        "lio_icp_set_defer_threshold": (C.c_int, [vp, C.c_int64]),
         "lio_seqsum6": (C.c_int, [C.c_int, fp, C.c_int64, C.c_int, fp, C.POINTER(C.c_int)]),
         "lio_ctx_set_timing": (C.c_int, [vp, C.c_int]),
         "lio_ctx_get_timing": (C.c_int, [vp, C.POINTER(KernelTiming)]),

@@ -83,16 +83,17 @@ def voxelize_submap(clouds, poses, voxel_res: float, handle: VoxelGrid | None = 
 
 
 def imu_poses_to_c(poses):
-    """poses: list of dicts offset_time, acc, gyr, vel, pos, rot (3x3)  ->  ctypes array."""
-    arr = (_capi.ImuPose * max(len(poses), 1))()
-    for k, p in enumerate(poses):
-        arr[k].offset_time = float(p["offset_time"])
-        for name in ("acc", "gyr", "vel", "pos"):
-            for i, v in enumerate(np.asarray(p[name], float).ravel()):
-                getattr(arr[k], name)[i] = v
-        for i, v in enumerate(np.asarray(p["rot"], float).ravel()):
-            arr[k].rot[i] = v
-    return arr
+    """poses: list of dicts offset_time, acc, gyr, vel, pos, rot (3x3)  ->  ctypes array (lio_imu_pose is 22
+    doubles in this order; filled through numpy, not element by element)."""
+    n = len(poses)
+    P = np.zeros((max(n, 1), 22), np.float64)
+    if n:
+        P[:n, 0] = [float(p["offset_time"]) for p in poses]
+        for j, name in ((1, "acc"), (4, "gyr"), (7, "vel"), (10, "pos")):
+            P[:n, j:j + 3] = np.asarray([np.asarray(p[name], float).ravel() for p in poses])
+        P[:n, 13:22] = np.asarray([np.asarray(p["rot"], float).ravel() for p in poses])
+    assert C.sizeof(_capi.ImuPose) == 22 * 8
+    return (_capi.ImuPose * max(n, 1)).from_buffer(P)
 
 
 class ScanPreprocessor(_Handle):

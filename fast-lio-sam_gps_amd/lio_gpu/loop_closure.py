@@ -127,11 +127,6 @@ class LoopClosure:
     def set_fidelity_debug(self, flags: int = 0, evcap: int = 0):
         check(lib().lio_icp_set_fidelity_debug(self._h, int(flags), int(evcap)))
 
-    def set_defer_threshold(self, candidates: int = -1):
-        """first-pass tiles with a final box of more candidates go to the several-waves launch (-1 default,
-        0 off); the 1-NN results do not depend on it"""
-        check(lib().lio_icp_set_defer_threshold(self._h, int(candidates)))
-
     def timing(self) -> dict:
         t = _capi.KernelTiming()
         check(lib().lio_icp_get_timing(self._h, C.byref(t)))

@@ -296,11 +296,6 @@ int lio_icp_umeyama_pcl_float_order(const float* sums16, int order, float* T16);
  * re-pass path runs); evcap > 0 caps the events per chain (overflow -> the serial fallback).       */
 int lio_icp_get_fidelity_stats(lio_icp* h, int64_t* out4);
 int lio_icp_set_fidelity_debug(lio_icp* h, int flags, int64_t evcap);
-/* Passes without previous correspondences (the first of an alignment) hand the tiles whose final search
- * box streams more than `candidates` target points to a second launch that splits each over 8 waves
- * (the first pass's tail).  -1: the default (3072, or LIO_ICP_DEFER); 0: off.  Results are identical
- * for every setting (exact 1-NN); this is a tuning / test knob. */
-int lio_icp_set_defer_threshold(lio_icp* h, int64_t candidates);
 /* Test hook: sequential float sums of 6 interleaved chains (x: n x 6 host floats) on `device` through
  * the seqsum path — sums6[c] = fl(...fl(x[0][c] + x[1][c]) ... + x[n-1][c]); passes_out = passes used
  * (-1: the serial kernel was needed).                                                             */

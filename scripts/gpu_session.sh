@@ -62,10 +62,9 @@ for s in $STEPS; do
            python scripts/pmc_sq_summary.py "$OUT/pmcsq_icp" "$OUT/pmcsq_icp.json" > "$OUT/pmcsq_icp_summary.txt" 2>&1; true ;;
     prep)  runs pytest_prep 600 python -u -m pytest tests/test_gpu_filters.py tests/test_gpu_formats.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread &&
            run prep_time 300 bash -c 'python scripts/prep_timing.py 80 && LIO_PREP_UPLOAD=full python scripts/prep_timing.py 80 && LIO_GPU_LIB=build_ab/pre_setup/liblio_gpu.so python scripts/prep_timing.py 80' &&
+           run prep_profile 300 bash -c "LIO_PREP_PROFILE=1 python scripts/prep_timing.py 60 2> $OUT/prep_profile.err && python scripts/prep_profile_summary.py $OUT/prep_profile.err" &&
            run rocprof_prep 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof_prep" -o run --output-format csv -- python scripts/prep_timing.py 40 ;;
-    defer) runs pytest_defer 600 python -u -m pytest tests/test_gpu_icp.py -k "deferral or nn_ or multi_iteration" -x -v -p no:cacheprovider --timeout 300 --timeout-method thread &&
-           run defer_ab 600 bash -c 'for r in 1 2; do for d in 0 1536 3072 6144; do echo "LIO_ICP_DEFER=$d"; LIO_ICP_DEFER=$d python scripts/icp_ab.py 1.0 5 || exit $?; done; done' &&
-           run defer_trace 300 rocprofv3 --kernel-trace --stats -d "$OUT/defer_trace" -o run --output-format csv -- python scripts/icp_ab.py 1.0 3 ;;
+    fidprof) run fid_prof 300 env LIO_ICP_ORDER=2 rocprofv3 --kernel-trace --stats -d "$OUT/fidprof" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 ;;
     maprec) runs pytest_maprec 600 python -u -m pytest tests/test_gpu_map.py tests/test_gpu_pipeline.py -x -v -p no:cacheprovider --timeout 500 --timeout-method thread ;;
     fid)   runs pytest_fid 900 python -u -m pytest tests/test_gpu_seqsum.py tests/test_gpu_icp.py -k "seqsum or fidelity or double" -x -v -s -p no:cacheprovider --timeout 300 --timeout-method thread &&
            run icp_fid_time 300 env LIO_ICP_ORDER=2 python scripts/icp_ab.py 1.0 5 &&

@@ -109,41 +109,6 @@ def test_icp_nn_multi_iteration_prior():
     check_nn(lc, ids, d2, dst)
 
 
-def _align_with_defer(src, dst, thr, guess=None):
-    lc = LC.LoopClosure(LC.LoopClosureConfig(), cell_size=1.0)
-    lc.set_defer_threshold(thr)
-    lc.setInputSource(src)
-    lc.setInputTarget(dst)
-    r = lc.align(guess=guess)
-    ids, d2 = lc.correspondences()
-    out = (np.asarray(r.T, np.float32).tobytes(), r.iterations, float(r.score).hex(), ids.tobytes(), d2.tobytes())
-    lc.close()
-    return out
-
-
-@pytest.mark.parametrize("case", ["c4", "far", "tiny", "disp"])
-def test_icp_first_pass_deferral_is_exact(case):
-    """The first pass (no previous correspondences) hands tiles with a large final box to a launch with 8
-    waves per tile (icp_heavy_kernel), resuming from the bound each lane found.  Threshold 1 defers almost
-    every tile, 64 the moderately heavy ones, -1 the default; the alignment (transform, iterations, score,
-    final correspondences) must be bit-identical to no deferral (0) — the 1-NN is exact either way."""
-    rng = np.random.default_rng(11)
-    if case == "c4":
-        src, dst, _ = synth.make_icp_pair(n_points=30_000, seed=5)
-    elif case == "disp":
-        src, dst, _ = synth.make_icp_pair(n_points=30_000, seed=4321, disp=(2.5, 4.0))
-    elif case == "far":
-        dst = rng.uniform(-5, 5, (4000, 3)).astype(np.float32)
-        src = np.concatenate([rng.uniform(-5, 5, (3000, 3)), rng.uniform(40, 60, (500, 3)),
-                              rng.uniform(-200, -150, (300, 3))]).astype(np.float32)
-    else:
-        dst = rng.uniform(-1, 1, (3, 3)).astype(np.float32)
-        src = rng.uniform(-30, 30, (5000, 3)).astype(np.float32)
-    ref = _align_with_defer(src, dst, 0)
-    for thr in (1, 64, -1):
-        assert _align_with_defer(src, dst, thr) == ref, f"defer threshold {thr}"
-
-
 @pytest.mark.parametrize("n", [2, 4])
 def test_icp_group_bit_identical_to_one_handle(n):
     """lio_icp_group (single-process multi-GPU): n ranks — all on device 0 on a one-GPU
