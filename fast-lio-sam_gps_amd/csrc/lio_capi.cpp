@@ -1129,6 +1129,33 @@ static int stage_sweep(lio::FilterBuf& b, const void* rows, int64_t n, size_t ro
     return LIO_OK;
 }
 
+// rows i % every == 0 with x*x + y*y + z*z > blind2 (float, left to right: scan_key_kernel's order) copied to
+// d in input order; every row is written at the cursor and the cursor advances by the keep flag (no branch
+// on the data); sorted: the kept rows' time keys (scan_key_kernel's) never decrease
+extern "C++" {  // inside the file's extern "C" block
+template <int S>
+static int64_t select_rows(const float* __restrict__ raw, int64_t n, int every, float blind2, int tf,
+                           float* __restrict__ d, bool& sorted) {
+    int64_t k = 0;
+    uint32_t prev = 0, unsorted = 0;
+    for (int64_t i = 0; i < n; i += every) {
+        const float* q = raw + i * S;
+        float r[S];
+        for (int f = 0; f < S; ++f) r[f] = q[f];
+        const uint32_t keep = (r[0] * r[0] + r[1] * r[1] + r[2] * r[2]) > blind2 ? 1u : 0u;
+        uint32_t tb;
+        std::memcpy(&tb, &r[tf], 4);
+        const uint32_t key = (tb & 0x80000000u) ? ~tb : (tb | 0x80000000u);  // scan_key_kernel's time key
+        unsorted |= keep & (key < prev ? 1u : 0u);
+        prev = keep ? key : prev;
+        for (int f = 0; f < S; ++f) d[k * S + f] = r[f];
+        k += keep;
+    }
+    sorted = unsorted == 0;
+    return k;
+}
+}  // extern "C++"
+
 // Float records: Preprocess's whole selection made while packing (the host reads every row here anyway) —
 // i % point_filter_num == 0 and x*x + y*y + z*z > blind^2, in float and in that order as the device's
 // scan_key_kernel — so the device gets exactly the m selected rows, in input order; *sorted says whether
@@ -1150,21 +1177,15 @@ static int stage_sweep_select(lio::FilterBuf& b, const float* raw, int64_t n, in
         b.stage_bytes = c;
     }
     const float blind2 = p->blind * p->blind;
-    const int tf = p->time_field;
     auto* d = static_cast<float*>(b.h_stage);
-    int64_t k = 0;
-    uint32_t prev = 0;
     bool sorted_ = true;
-    for (int64_t i = 0; i < n; i += every) {
-        const float* q = raw + i * stride;
-        if (!((q[0] * q[0] + q[1] * q[1] + q[2] * q[2]) > blind2)) continue;
-        uint32_t tb;
-        std::memcpy(&tb, &q[tf], 4);
-        const uint32_t key = (tb & 0x80000000u) ? ~tb : (tb | 0x80000000u);  // scan_key_kernel's time key
-        sorted_ = sorted_ && prev <= key;
-        prev = key;
-        for (int f = 0; f < stride; ++f) d[k * stride + f] = q[f];
-        ++k;
+    int64_t k;
+    switch (stride) {  // the record width as a constant: the row copy unrolls, the loop stays branch-free
+        case 4: k = select_rows<4>(raw, n, every, blind2, p->time_field, d, sorted_); break;
+        case 5: k = select_rows<5>(raw, n, every, blind2, p->time_field, d, sorted_); break;
+        case 6: k = select_rows<6>(raw, n, every, blind2, p->time_field, d, sorted_); break;
+        case 7: k = select_rows<7>(raw, n, every, blind2, p->time_field, d, sorted_); break;
+        default: k = select_rows<8>(raw, n, every, blind2, p->time_field, d, sorted_); break;  // prep_args_ok: <= 8
     }
     if (np) std::memcpy(static_cast<uint8_t*>(b.h_stage) + *pose_off, poses, (size_t)np * sizeof(lio_imu_pose));
     *m = k;

@@ -50,18 +50,16 @@ for s in $STEPS; do
              run bench_driverq3 300 python bench.py --gpus 1 --steps 50 --warmup 5 --no-cpu --pipeline 0 --streams '' --no-icp ;;
     micro) run graph_cost 120 scripts/micro/graph_cost ;;
     first) run map_first 300 python scripts/map_first_call.py &&
-           run map_first_pre 300 env LIO_GPU_LIB=build_ab/pre_setup/liblio_gpu.so python scripts/map_first_call.py &&
            run map_first_nodefer 300 env HIP_ENABLE_DEFERRED_LOADING=0 python scripts/map_first_call.py ;;
     setup) run icp_setup 300 python scripts/icp_setup_timing.py &&
-           run icp_setup_pre 300 env LIO_GPU_LIB=build_ab/pre_setup/liblio_gpu.so python scripts/icp_setup_timing.py &&
            run icp_setup2 300 python scripts/icp_setup_timing.py ;;
-    msab)  run msab 900 bash -c 'for r in 1 2; do for lib in HEAD build_ab/r02/liblio_gpu.so; do if [ $lib = HEAD ]; then python bench.py --steps 60 --warmup 5 --no-cpu --no-icp --pipeline 0 --streams 1,2,8; else LIO_GPU_LIB=$lib python bench.py --steps 60 --warmup 5 --no-cpu --no-icp --pipeline 0 --streams 1,2,8; fi | python -c "import json,sys; d=json.loads([l for l in sys.stdin if l.startswith(\"{\")][-1]); print(\"$lib\", d[\"value\"], d[\"multi_stream\"])" || exit $?; done; done' ;;
+    msab)  echo "msab: the round-2 build it compared against is no longer kept (result: profiles/r04_multi_stream_ab.txt)" ;;
     pmcsq) run pmcsq_c3 300 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmcsq_c3" -o run --output-format csv -- python bench.py --steps 30 --warmup 3 --no-cpu --no-icp --streams '' --pipeline 0 &&
            run pmcsq_icp 300 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --kernel-trace -d "$OUT/pmcsq_icp" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
            python scripts/pmc_sq_summary.py "$OUT/pmcsq_c3" "$OUT/pmcsq_c3.json" > "$OUT/pmcsq_c3_summary.txt" 2>&1;
            python scripts/pmc_sq_summary.py "$OUT/pmcsq_icp" "$OUT/pmcsq_icp.json" > "$OUT/pmcsq_icp_summary.txt" 2>&1; true ;;
     prep)  runs pytest_prep 600 python -u -m pytest tests/test_gpu_filters.py tests/test_gpu_formats.py -x -v -p no:cacheprovider --timeout 300 --timeout-method thread &&
-           run prep_time 300 bash -c 'python scripts/prep_timing.py 80 && LIO_PREP_UPLOAD=full python scripts/prep_timing.py 80 && LIO_GPU_LIB=build_ab/pre_setup/liblio_gpu.so python scripts/prep_timing.py 80' &&
+           run prep_time 300 bash -c 'python scripts/prep_timing.py 80 && LIO_PREP_UPLOAD=full python scripts/prep_timing.py 80' &&
            run prep_profile 300 bash -c "LIO_PREP_PROFILE=1 python scripts/prep_timing.py 60 2> $OUT/prep_profile.err && python scripts/prep_profile_summary.py $OUT/prep_profile.err" &&
            run rocprof_prep 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof_prep" -o run --output-format csv -- python scripts/prep_timing.py 40 ;;
     fidprof) run fid_prof 300 env LIO_ICP_ORDER=2 rocprofv3 --kernel-trace --stats -d "$OUT/fidprof" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 ;;
