@@ -21,6 +21,7 @@
 #include "lio_error.hpp"
 #include "lio_kernels.hpp"
 #include "lio_filter.hpp"
+#include "lio_pool.hpp"
 #include "lio_mapupd.hpp"
 
 namespace {
@@ -1135,9 +1136,9 @@ static int stage_sweep(lio::FilterBuf& b, const void* rows, int64_t n, size_t ro
 extern "C++" {  // inside the file's extern "C" block
 template <int S>
 static int64_t select_rows(const float* __restrict__ raw, int64_t n, int every, float blind2, int tf,
-                           float* __restrict__ d, bool& sorted) {
+                           float* __restrict__ d, bool& sorted, uint32_t& first_key, uint32_t& last_key) {
     int64_t k = 0;
-    uint32_t prev = 0, unsorted = 0;
+    uint32_t prev = 0, unsorted = 0, first = 0xffffffffu;
     for (int64_t i = 0; i < n; i += every) {
         const float* q = raw + i * S;
         float r[S];
@@ -1147,11 +1148,14 @@ static int64_t select_rows(const float* __restrict__ raw, int64_t n, int every, 
         std::memcpy(&tb, &r[tf], 4);
         const uint32_t key = (tb & 0x80000000u) ? ~tb : (tb | 0x80000000u);  // scan_key_kernel's time key
         unsorted |= keep & (key < prev ? 1u : 0u);
+        first = (keep && k == 0) ? key : first;
         prev = keep ? key : prev;
         for (int f = 0; f < S; ++f) d[k * S + f] = r[f];
         k += keep;
     }
     sorted = unsorted == 0;
+    first_key = first;
+    last_key = prev;
     return k;
 }
 }  // extern "C++"
@@ -1160,10 +1164,21 @@ static int64_t select_rows(const float* __restrict__ raw, int64_t n, int every, 
 // i % point_filter_num == 0 and x*x + y*y + z*z > blind^2, in float and in that order as the device's
 // scan_key_kernel — so the device gets exactly the m selected rows, in input order; *sorted says whether
 // their times are non-decreasing (the stable time sort is then the identity and the device skips it).
+// Large sweeps are packed by the host pool in up to kStageChunks contiguous pieces, each at its own offset
+// of the staging buffer (the upper bound of its rows): the plan lists them, and the caller moves each
+// piece with its own DMA to where the concatenation puts it.
+constexpr int kStageChunks = 4;
+struct StagePlan {
+    int pieces = 0;
+    int64_t src_row[kStageChunks] = {};  // first staging row of the piece
+    int64_t rows[kStageChunks] = {};     // its selected rows
+};
+
 static int stage_sweep_select(lio::FilterBuf& b, const float* raw, int64_t n, int stride, const lio_scan_prep_params* p,
-                              const lio_imu_pose* poses, int np, int64_t* m, size_t* pose_off, bool* sorted) {
+                              const lio_imu_pose* poses, int np, int64_t* m, size_t* pose_off, bool* sorted,
+                              StagePlan* plan) {
     const int every = std::max(p->point_filter_num, 1);
-    const int64_t ub = (n + every - 1) / every;
+    const int64_t ub = (n + every - 1) / every;  // candidate rows (i % every == 0)
     *pose_off = ((size_t)ub * stride * sizeof(float) + 255) & ~(size_t)255;
     const size_t need = *pose_off + (size_t)np * sizeof(lio_imu_pose);
     if (need > b.stage_bytes || !b.h_stage) {
@@ -1178,18 +1193,62 @@ static int stage_sweep_select(lio::FilterBuf& b, const float* raw, int64_t n, in
     }
     const float blind2 = p->blind * p->blind;
     auto* d = static_cast<float*>(b.h_stage);
+    const int pieces = ub >= 16384 ? kStageChunks : 1;
+    const int64_t per = (ub + pieces - 1) / pieces;  // candidate rows per piece
+    int64_t k[kStageChunks] = {};
+    bool srt[kStageChunks] = {};
+    uint32_t first[kStageChunks] = {}, last[kStageChunks] = {};
+    auto piece = [&](int t) {
+        const int64_t c0 = std::min(ub, t * per), c1 = std::min(ub, c0 + per);
+        const float* src = raw + c0 * every * stride;
+        const int64_t nn = std::min(n - c0 * every, (c1 - c0) * every);  // raw rows of the piece
+        float* dst = d + c0 * stride;
+        bool s = true;
+        switch (stride) {  // the record width as a constant: the row copy unrolls, the loop stays branch-free
+            case 4: k[t] = select_rows<4>(src, nn, every, blind2, p->time_field, dst, s, first[t], last[t]); break;
+            case 5: k[t] = select_rows<5>(src, nn, every, blind2, p->time_field, dst, s, first[t], last[t]); break;
+            case 6: k[t] = select_rows<6>(src, nn, every, blind2, p->time_field, dst, s, first[t], last[t]); break;
+            case 7: k[t] = select_rows<7>(src, nn, every, blind2, p->time_field, dst, s, first[t], last[t]); break;
+            default: k[t] = select_rows<8>(src, nn, every, blind2, p->time_field, dst, s, first[t], last[t]); break;
+        }
+        srt[t] = s;
+    };
+    if (pieces == 1) piece(0);
+    else lio::HostPool::get().parallel_for(pieces, piece);
     bool sorted_ = true;
-    int64_t k;
-    switch (stride) {  // the record width as a constant: the row copy unrolls, the loop stays branch-free
-        case 4: k = select_rows<4>(raw, n, every, blind2, p->time_field, d, sorted_); break;
-        case 5: k = select_rows<5>(raw, n, every, blind2, p->time_field, d, sorted_); break;
-        case 6: k = select_rows<6>(raw, n, every, blind2, p->time_field, d, sorted_); break;
-        case 7: k = select_rows<7>(raw, n, every, blind2, p->time_field, d, sorted_); break;
-        default: k = select_rows<8>(raw, n, every, blind2, p->time_field, d, sorted_); break;  // prep_args_ok: <= 8
+    uint32_t prev = 0;
+    bool any = false;
+    int64_t total = 0;
+    plan->pieces = pieces;
+    for (int t = 0; t < pieces; ++t) {
+        plan->src_row[t] = std::min(ub, t * per);
+        plan->rows[t] = k[t];
+        total += k[t];
+        if (!k[t]) continue;
+        sorted_ = sorted_ && srt[t] && (!any || prev <= first[t]);  // and across the piece boundary
+        prev = last[t];
+        any = true;
     }
     if (np) std::memcpy(static_cast<uint8_t*>(b.h_stage) + *pose_off, poses, (size_t)np * sizeof(lio_imu_pose));
-    *m = k;
+    *m = total;
     *sorted = sorted_;
+    return LIO_OK;
+}
+
+// the staged pieces -> device rows [0, m) (one DMA per piece) and, when given, the poses
+static int upload_staged(const lio::FilterBuf& b, const StagePlan& plan, int stride, float* d_rows, size_t pose_off,
+                         int np, lio::ImuPose* d_poses, hipStream_t st) {
+    const auto* h = static_cast<const float*>(b.h_stage);
+    int64_t dst = 0;
+    for (int t = 0; t < plan.pieces; ++t) {
+        if (plan.rows[t])
+            HIP_TRY(hipMemcpyAsync(d_rows + dst * stride, h + plan.src_row[t] * stride,
+                                   (size_t)plan.rows[t] * stride * sizeof(float), hipMemcpyHostToDevice, st));
+        dst += plan.rows[t];
+    }
+    if (np)
+        HIP_TRY(hipMemcpyAsync(d_poses, static_cast<const uint8_t*>(b.h_stage) + pose_off,
+                               (size_t)np * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
     return LIO_OK;
 }
 
@@ -1298,9 +1357,10 @@ int lio_preprocess(lio_filter* f, const float* raw, int64_t n, int stride, const
     int64_t rows = n;
     size_t pose_off = 0;
     int presel = -1;
+    StagePlan plan;
     if (!full) {
         bool sorted = false;
-        rc = stage_sweep_select(f->b, raw, n, stride, p, poses, n_poses, &rows, &pose_off, &sorted);
+        rc = stage_sweep_select(f->b, raw, n, stride, p, poses, n_poses, &rows, &pose_off, &sorted, &plan);
         if (rc) return rc;
         presel = sorted ? 1 : 0;
         if (rows == 0) return LIO_OK;
@@ -1309,12 +1369,14 @@ int lio_preprocess(lio_filter* f, const float* raw, int64_t n, int stride, const
     if (!rc) rc = grow(&f->d_out, f->out_cap, rows * stride);
     if (!rc && n_poses) rc = grow(&f->d_poses, f->poses_cap, n_poses);
     if (rc) return rc;
-    const auto* stage = static_cast<const uint8_t*>(f->b.h_stage);
-    HIP_TRY(hipMemcpyAsync(f->d_in, full ? (const void*)raw : stage, (size_t)rows * stride * sizeof(float),
-                           hipMemcpyHostToDevice, st));
-    if (n_poses)
-        HIP_TRY(hipMemcpyAsync(f->d_poses, full ? (const void*)poses : stage + pose_off,
-                               (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
+    if (full) {
+        HIP_TRY(hipMemcpyAsync(f->d_in, raw, (size_t)rows * stride * sizeof(float), hipMemcpyHostToDevice, st));
+        if (n_poses)
+            HIP_TRY(hipMemcpyAsync(f->d_poses, poses, (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
+    } else {
+        rc = upload_staged(f->b, plan, stride, f->d_in, pose_off, n_poses, f->d_poses, st);
+        if (rc) return rc;
+    }
     int64_t m = 0;
     rc = 2;
     for (int attempt = 0; attempt < 2 && rc == 2; ++attempt) {  // 2: the voxel key width was learnt too narrow
@@ -1399,29 +1461,28 @@ int lio_scan_preprocess(lio_ctx* c, const float* raw, int64_t n, int stride, con
     int64_t rows = n;
     size_t pose_off = 0;
     int presel = -1;
+    StagePlan plan;
     if (!full) {
         bool sorted = false;
-        rc = stage_sweep_select(c->filt, raw, n, stride, p, poses, n_poses, &rows, &pose_off, &sorted);
+        rc = stage_sweep_select(c->filt, raw, n, stride, p, poses, n_poses, &rows, &pose_off, &sorted, &plan);
         if (rc) return rc;
         presel = sorted ? 1 : 0;
     }
     const auto t1 = std::chrono::steady_clock::now();
-    // staged: the rows and the poses behind them (pose_off, 256-B aligned) in one DMA into d_raw
-    const size_t staged = pose_off + (size_t)n_poses * sizeof(lio::ImuPose);
-    rc = grow(&c->d_raw, c->raw_cap, full ? std::max<int64_t>(rows, 1) * stride : (int64_t)((staged + 3) / 4) + 1);
+    rc = grow(&c->d_raw, c->raw_cap, std::max<int64_t>(rows, 1) * stride);
     if (!rc) rc = grow(&c->d_rec, c->rec_cap, std::max<int64_t>(rows, 1) * stride);
-    if (!rc && n_poses && full) rc = grow(&c->d_poses, c->poses_cap, n_poses);
+    if (!rc && n_poses) rc = grow(&c->d_poses, c->poses_cap, n_poses);
     if (rc) return rc;
-    const lio::ImuPose* d_poses = c->d_poses;
     if (full) {
         if (rows)
             HIP_TRY(hipMemcpyAsync(c->d_raw, raw, (size_t)rows * stride * sizeof(float), hipMemcpyHostToDevice, st));
         if (n_poses)
             HIP_TRY(hipMemcpyAsync(c->d_poses, poses, (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
     } else {
-        if (staged) HIP_TRY(hipMemcpyAsync(c->d_raw, c->filt.h_stage, staged, hipMemcpyHostToDevice, st));
-        d_poses = reinterpret_cast<const lio::ImuPose*>(reinterpret_cast<const uint8_t*>(c->d_raw) + pose_off);
+        rc = upload_staged(c->filt, plan, stride, c->d_raw, pose_off, n_poses, c->d_poses, st);
+        if (rc) return rc;
     }
+    const lio::ImuPose* d_poses = c->d_poses;
     const auto t2 = std::chrono::steady_clock::now();
     rc = scan_prep_device(c, rows, stride, sp, n_poses, end, n_down, "lio_scan_preprocess", presel, d_poses);
     if (prep_profile()) {

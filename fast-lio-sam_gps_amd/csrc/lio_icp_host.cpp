@@ -15,6 +15,7 @@
 #include <hip/hip_runtime.h>
 
 #include "lio_pcl.hpp"
+#include "lio_pool.hpp"
 
 #include <algorithm>
 #include <cfloat>
@@ -463,17 +464,15 @@ static int stage_pinned(float*& buf, int64_t& cap, const float* xyz, int64_t n) 
         cap = c;
     }
     const size_t bytes = (size_t)n * 3 * sizeof(float);
-    const int nt = bytes >= ((size_t)4 << 20) ? 4 : 1;
+    const int nt = bytes >= ((size_t)1 << 20) ? 4 : 1;  // the host pool's threads (no thread created per call)
     if (nt == 1) {
         std::memcpy(buf, xyz, bytes);
     } else {
-        std::vector<std::thread> th;
         const int64_t per = (3 * n + nt - 1) / nt;
-        for (int t = 0; t < nt; ++t) {
+        lio::HostPool::get().parallel_for(nt, [&](int t) {
             const int64_t b = std::min<int64_t>(3 * n, t * per), e = std::min<int64_t>(3 * n, b + per);
-            th.emplace_back([=] { std::memcpy(buf + b, xyz + b, (size_t)(e - b) * sizeof(float)); });
-        }
-        for (std::thread& t : th) t.join();
+            std::memcpy(buf + b, xyz + b, (size_t)(e - b) * sizeof(float));
+        });
     }
     return LIO_OK;
 }
