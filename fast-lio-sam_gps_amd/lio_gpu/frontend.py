@@ -45,23 +45,17 @@ def default_match_params(**kw) -> _capi.MatchParams:
 
 def pose_from_arrays(R, t, R_LI=np.eye(3), t_LI=np.zeros(3), q=None, q_LI=None) -> _capi.Pose:
     """lio_pose; q / q_LI = the state's quaternions (w, x, y, z) — left zero (derived from R on the
-    device side) when only matrices are given."""
-    p = _capi.Pose()
+    device side) when only matrices are given.  lio_pose is 32 doubles R, t, R_LI, t_LI, q, q_LI."""
+    v = np.zeros(32, np.float64)
+    v[0:9] = np.asarray(R, float).ravel()
+    v[9:12] = np.asarray(t, float).ravel()
+    v[12:21] = np.asarray(R_LI, float).ravel()
+    v[21:24] = np.asarray(t_LI, float).ravel()
     if q is not None:
-        for i, v in enumerate(np.asarray(q, float).ravel()):
-            p.q[i] = v
+        v[24:28] = np.asarray(q, float).ravel()
     if q_LI is not None:
-        for i, v in enumerate(np.asarray(q_LI, float).ravel()):
-            p.q_LI[i] = v
-    for i, v in enumerate(np.asarray(R, float).ravel()):
-        p.R[i] = v
-    for i, v in enumerate(np.asarray(t, float).ravel()):
-        p.t[i] = v
-    for i, v in enumerate(np.asarray(R_LI, float).ravel()):
-        p.R_LI[i] = v
-    for i, v in enumerate(np.asarray(t_LI, float).ravel()):
-        p.t_LI[i] = v
-    return p
+        v[28:32] = np.asarray(q_LI, float).ravel()
+    return _capi.Pose.from_buffer_copy(v)
 
 
 def pose_from_pose24(p24) -> _capi.Pose:
