@@ -537,8 +537,8 @@ int lio_icp_set_source(lio_icp* h, const float* xyz, int64_t n) {
 
 int lio_icp_set_shard(lio_icp* h, int rank, int world, lio_allgather_fn fn, void* user) {
     if (!h || world < 1 || rank < 0 || rank >= world || (world > 1 && !fn))
-    icp_join(h);
         return ifail(LIO_ERR_ARG, "lio_icp_set_shard: bad arguments");
+    icp_join(h);
     h->rank = rank;
     h->world = world;
     h->fn = fn;
@@ -551,8 +551,8 @@ int lio_icp_set_shard(lio_icp* h, int rank, int world, lio_allgather_fn fn, void
 
 int lio_icp_set_shard_device(lio_icp* h, int rank, int world, lio_allgather_dev_fn fn, void* user) {
     if (!h || world < 1 || rank < 0 || rank >= world || (world > 1 && !fn))
-    icp_join(h);
         return ifail(LIO_ERR_ARG, "lio_icp_set_shard_device: bad arguments");
+    icp_join(h);
     h->rank = rank;
     h->world = world;
     h->fn = nullptr;
