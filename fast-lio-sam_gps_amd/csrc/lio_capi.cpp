@@ -1235,20 +1235,20 @@ static int stage_sweep_select(lio::FilterBuf& b, const float* raw, int64_t n, in
     return LIO_OK;
 }
 
-// the staged pieces -> device rows [0, m) (one DMA per piece) and, when given, the poses
-static int upload_staged(const lio::FilterBuf& b, const StagePlan& plan, int stride, float* d_rows, size_t pose_off,
-                         int np, lio::ImuPose* d_poses, hipStream_t st) {
-    const auto* h = static_cast<const float*>(b.h_stage);
-    int64_t dst = 0;
+// the staging buffer (the pieces with their gaps, then the IMU poses at pose_off) -> d_buf in one DMA; the
+// piece table for the device (logical row -> staged row) and the poses' device address
+static int upload_staged(const lio::FilterBuf& b, const StagePlan& plan, size_t pose_off, int np, float* d_buf,
+                         hipStream_t st, lio::RowPieces* rp, const lio::ImuPose** d_poses) {
+    const size_t bytes = pose_off + (size_t)np * sizeof(lio::ImuPose);
+    if (bytes) HIP_TRY(hipMemcpyAsync(d_buf, b.h_stage, bytes, hipMemcpyHostToDevice, st));
+    rp->n = std::max(plan.pieces, 1);
+    uint32_t at = 0;
     for (int t = 0; t < plan.pieces; ++t) {
-        if (plan.rows[t])
-            HIP_TRY(hipMemcpyAsync(d_rows + dst * stride, h + plan.src_row[t] * stride,
-                                   (size_t)plan.rows[t] * stride * sizeof(float), hipMemcpyHostToDevice, st));
-        dst += plan.rows[t];
+        rp->start[t] = at;
+        rp->src[t] = (uint32_t)plan.src_row[t];
+        at += (uint32_t)plan.rows[t];
     }
-    if (np)
-        HIP_TRY(hipMemcpyAsync(d_poses, static_cast<const uint8_t*>(b.h_stage) + pose_off,
-                               (size_t)np * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
+    *d_poses = reinterpret_cast<const lio::ImuPose*>(reinterpret_cast<const uint8_t*>(d_buf) + pose_off);
     return LIO_OK;
 }
 
@@ -1365,23 +1365,26 @@ int lio_preprocess(lio_filter* f, const float* raw, int64_t n, int stride, const
         presel = sorted ? 1 : 0;
         if (rows == 0) return LIO_OK;
     }
-    rc = grow(&f->d_in, f->in_cap, rows * stride);
+    const size_t staged = pose_off + (size_t)n_poses * sizeof(lio::ImuPose);
+    rc = grow(&f->d_in, f->in_cap, full ? rows * stride : (int64_t)((staged + 3) / 4) + 1);
     if (!rc) rc = grow(&f->d_out, f->out_cap, rows * stride);
-    if (!rc && n_poses) rc = grow(&f->d_poses, f->poses_cap, n_poses);
+    if (!rc && n_poses && full) rc = grow(&f->d_poses, f->poses_cap, n_poses);
     if (rc) return rc;
+    lio::RowPieces rp;
+    const lio::ImuPose* d_poses = f->d_poses;
     if (full) {
         HIP_TRY(hipMemcpyAsync(f->d_in, raw, (size_t)rows * stride * sizeof(float), hipMemcpyHostToDevice, st));
         if (n_poses)
             HIP_TRY(hipMemcpyAsync(f->d_poses, poses, (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
     } else {
-        rc = upload_staged(f->b, plan, stride, f->d_in, pose_off, n_poses, f->d_poses, st);
+        rc = upload_staged(f->b, plan, pose_off, n_poses, f->d_in, st, &rp, &d_poses);
         if (rc) return rc;
     }
     int64_t m = 0;
     rc = 2;
     for (int attempt = 0; attempt < 2 && rc == 2; ++attempt) {  // 2: the voxel key width was learnt too narrow
-        rc = lio::scan_preprocess_enqueue(f->b, f->d_in, rows, stride, sp, f->d_poses, n_poses, undistort_end(end),
-                                          f->d_out, st, presel);
+        rc = lio::scan_preprocess_enqueue(f->b, f->d_in, rows, stride, sp, d_poses, n_poses, undistort_end(end),
+                                          f->d_out, st, presel, nullptr, nullptr, rp);
         if (!rc) rc = lio::scan_preprocess_finish(f->b, stride, f->d_out, &m, nullptr, st);
     }
     if (rc == 2) rc = -2;
@@ -1408,7 +1411,7 @@ static double prep_us(std::chrono::steady_clock::time_point a, std::chrono::stea
 // records; every stage is queued, the scan buffers set up behind it, and the host waits once
 static int scan_prep_device(lio_ctx* c, int64_t rows, int stride, const lio::ScanPrepParams& sp, int n_poses,
                             const lio_pose* end, int64_t* n_down, const char* what, int presel = -1,
-                            const lio::ImuPose* d_poses = nullptr) {
+                            const lio::ImuPose* d_poses = nullptr, const lio::RowPieces& rp = lio::RowPieces{}) {
     if (!d_poses) d_poses = c->d_poses;
     hipStream_t st = c->map->st;
     c->undist_n = -1;
@@ -1424,7 +1427,7 @@ static int scan_prep_device(lio_ctx* c, int64_t rows, int stride, const lio::Sca
         const bool vox = sp.leaf > 0.f;  // the centroid pass writes the scan's xyz and flags itself
         rc = lio::scan_preprocess_enqueue(c->filt, c->d_raw, rows, stride, sp, d_poses, n_poses,
                                           undistort_end(end), c->d_rec, st, presel, vox ? c->d_body : nullptr,
-                                          vox ? c->d_sel : nullptr);
+                                          vox ? c->d_sel : nullptr, rp);
         if (rc) return bail(filter_status(rc, what));
         if (!vox) rc = lio::records_to_xyz_sel(c->d_rec, rows, stride, c->d_body, c->d_sel, st);
         if (rc) return bail(filter_status(rc, what));
@@ -1469,22 +1472,25 @@ int lio_scan_preprocess(lio_ctx* c, const float* raw, int64_t n, int stride, con
         presel = sorted ? 1 : 0;
     }
     const auto t1 = std::chrono::steady_clock::now();
-    rc = grow(&c->d_raw, c->raw_cap, std::max<int64_t>(rows, 1) * stride);
+    // staged: the pieces (with their gaps) and the poses behind them in one DMA into d_raw
+    const size_t staged = pose_off + (size_t)n_poses * sizeof(lio::ImuPose);
+    rc = grow(&c->d_raw, c->raw_cap, full ? std::max<int64_t>(rows, 1) * stride : (int64_t)((staged + 3) / 4) + 1);
     if (!rc) rc = grow(&c->d_rec, c->rec_cap, std::max<int64_t>(rows, 1) * stride);
-    if (!rc && n_poses) rc = grow(&c->d_poses, c->poses_cap, n_poses);
+    if (!rc && n_poses && full) rc = grow(&c->d_poses, c->poses_cap, n_poses);
     if (rc) return rc;
+    lio::RowPieces rp;
+    const lio::ImuPose* d_poses = c->d_poses;
     if (full) {
         if (rows)
             HIP_TRY(hipMemcpyAsync(c->d_raw, raw, (size_t)rows * stride * sizeof(float), hipMemcpyHostToDevice, st));
         if (n_poses)
             HIP_TRY(hipMemcpyAsync(c->d_poses, poses, (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
     } else {
-        rc = upload_staged(c->filt, plan, stride, c->d_raw, pose_off, n_poses, c->d_poses, st);
+        rc = upload_staged(c->filt, plan, pose_off, n_poses, c->d_raw, st, &rp, &d_poses);
         if (rc) return rc;
     }
-    const lio::ImuPose* d_poses = c->d_poses;
     const auto t2 = std::chrono::steady_clock::now();
-    rc = scan_prep_device(c, rows, stride, sp, n_poses, end, n_down, "lio_scan_preprocess", presel, d_poses);
+    rc = scan_prep_device(c, rows, stride, sp, n_poses, end, n_down, "lio_scan_preprocess", presel, d_poses, rp);
     if (prep_profile()) {
         const auto t3 = std::chrono::steady_clock::now();
         std::fprintf(stderr, "prep_profile rows %lld presel %d stage_us %.1f upload_enqueue_us %.1f device_us %.1f total_us %.1f\n",

@@ -577,58 +577,6 @@ __device__ __forceinline__ void scan_table_strided(const GridDev& g, float qx, f
     }
 }
 
-// Lane `r` of `L` lanes takes one contiguous stretch [r c, (r + 1) c) of the concatenated table
-// (c = ceil(T / L)): its start slot by binary search over the offsets (one short chain of LDS reads),
-// then a slot walk that steps only where the stretch crosses a range — ~NR / L crossings per lane
-// instead of one per stride-L step (each crossing is a dependent LDS read).  The 8 lanes of a group
-// then load from 8 separate stretches (a cache line serves a lane's next 4 points).  Every point is
-// still pushed by exactly one lane: the merged result does not depend on the split.
-template <int K, int U = 4>
-__device__ __forceinline__ void scan_table_chunked(const GridDev& g, float qx, float qy, float qz, const uint32_t* lds,
-                                                   uint32_t T, uint32_t NR, uint32_t r, uint32_t L, TopK<K>& tk) {
-    const uint32_t* s_b = lds;
-    const uint32_t* s_off = lds + 32;
-    const uint32_t c = (T + L - 1) / L;
-    const uint32_t t0 = min(T, r * c), t1 = min(T, t0 + c);
-    if (t0 >= t1) return;
-    // the slot holding t0: the last of the NR (strictly increasing: empty ranges are compacted out)
-    // offsets that is <= t0, by binary search (s_off[0] = 0 <= t0 < s_off[NR] = T)
-    int sl = 0;
-#pragma unroll
-    for (int step = 16; step > 0; step >>= 1)
-        if (sl + step < (int)NR && s_off[sl + step] <= t0) sl += step;
-    uint32_t lo = s_off[sl], hi = s_off[sl + 1], sb = s_b[sl];
-    for (uint32_t t = t0; t < t1; t += U) {
-        uint32_t src[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const uint32_t tu = min(t + (uint32_t)u, t1 - 1);  // clamped: a valid address, pushed only if < t1
-            while (tu >= hi) {
-                lo = hi;
-                hi = s_off[++sl + 1];
-                sb = s_b[sl];
-            }
-            src[u] = sb + (tu - lo);
-        }
-        float4 p[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) p[u] = g.pts[src[u]];
-        static_assert(U % 2 == 0, "scan_table_chunked: pairs of loads");
-#pragma unroll
-        for (int u = 0; u < U; u += 2) {
-            float d0, d1;
-            sqdist3_x2(qx, qy, qz, p[u], p[u + 1], d0, d1);
-            const bool in0 = t + (uint32_t)u < t1, in1 = t + (uint32_t)(u + 1) < t1;
-            tk.push2(knn_key(in0 ? d0 : INFINITY, in0 ? __float_as_int(p[u].w) : kNone),
-                     knn_key(in1 ? d1 : INFINITY, in1 ? __float_as_int(p[u + 1].w) : kNone));
-        }
-    }
-}
-
-#ifndef LIO_TABLE_SCAN
-#define LIO_TABLE_SCAN scan_table_chunked
-#endif
-
 template <int K, int G, int U = 4>
 __device__ __forceinline__ void scan_shell1_flat(const GridDev& g, float qx, float qy, float qz, int cx, int cy,
                                                  int cz, float lox, float loy, float loz, int sub, uint32_t* lds,
@@ -638,7 +586,7 @@ __device__ __forceinline__ void scan_shell1_flat(const GridDev& g, float qx, flo
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    LIO_TABLE_SCAN<K, U>(g, qx, qy, qz, lds, TP & 0xffffffu, TP >> 24, (uint32_t)sub, (uint32_t)G, tk);
+    scan_table_strided<K, U>(g, qx, qy, qz, lds, TP & 0xffffffu, TP >> 24, (uint32_t)sub, (uint32_t)G, tk);
 }
 
 // Lean group walk for dense maps (front-end kNN, ICP near pass), written for
@@ -732,7 +680,7 @@ __device__ int group_knn_seeded(const GridDev& g, float bound, int cx, int cy, i
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    LIO_TABLE_SCAN<K, U>(g, qx, qy, qz, lds, TP & 0xffffffu, TP >> 24, (uint32_t)sub, (uint32_t)G, tk);
+    scan_table_strided<K, U>(g, qx, qy, qz, lds, TP & 0xffffffu, TP >> 24, (uint32_t)sub, (uint32_t)G, tk);
     group_merge<K, G>(tk);
     if (tk.id(K - 1) == kNone && bound < range_sq) {  // guard: not full under a finite bound
         tk.init(range_sq);

@@ -190,82 +190,123 @@ __global__ void voxel_bounds_kernel(const uint32_t* __restrict__ keys, int64_t n
     if (j + 1 == n || keys[j + 1] != key) ends[r] = (uint32_t)(j + 1);
 }
 
-// PCL VoxelGrid centroid: a voxel's fields summed one point at a time in input order (float), divided by
-// the count.  One wave per 64 consecutive voxels, lane = voxel: their runs are one contiguous stretch of
-// the sorted order, which the wave streams through LDS kCentCh points at a time (4 per lane, the next
-// chunk's loads in flight while this one is summed); each lane then adds the staged points of its own
-// run in order.  The adds of a run are its serial part (PCL's order); the loads are one round trip per
-// chunk for all 64 voxels, whatever their run lengths.  xyz / sel (optional): the packed centroid xyz and
-// zeroed selection flags of the scan the output becomes (lio_scan_preprocess), in the same pass.
-constexpr int kCentCh = 256;
-__global__ void __launch_bounds__(64) voxel_centroid_wave_kernel(const float* __restrict__ p, int stride,
-                                                                  const uint32_t* __restrict__ vals,
-                                                                  const uint32_t* __restrict__ starts,
-                                                                  const uint32_t* __restrict__ ends,
-                                                                  const uint32_t* __restrict__ n_vox,
-                                                                  float* __restrict__ out, float* __restrict__ xyz,
-                                                                  uint8_t* __restrict__ sel) {
-    __shared__ float s_q[2][kCentCh * kMaxFields];
-    constexpr int PL = kCentCh / 64;
-    const int lane = threadIdx.x;
-    const uint32_t nv = *n_vox;
-    const uint32_t v0 = blockIdx.x * 64u;
-    if (v0 >= nv) return;  // block-uniform
-    const uint32_t v = v0 + (uint32_t)lane, vl = min(v0 + 63u, nv - 1u);
-    const bool mine = v < nv;
-    const uint32_t s = mine ? starts[v] : 0u, e = mine ? ends[v] : 0u;
-    const uint32_t R0 = starts[v0], R1 = ends[vl];  // the wave's stretch of the sorted order
-    float q[PL][kMaxFields];
-    auto load = [&](uint32_t k) {
+constexpr int kLaneRun = 16;  // runs up to this length: one lane; longer: one wave (voxel_centroid_big_kernel,
+                              // one wave per run; round 4 measured one wave per 64 consecutive voxels instead:
+                              // 242 us per sweep, dense regions put ~10^4 points on one wave)
+constexpr int kBigBlocks = 1024;  // waves striding the long-run list
+
+template <int NF>
+__device__ __forceinline__ void write_centroid(float* __restrict__ o, const float* acc, int stride, uint32_t cnt) {
+    const float c = (float)cnt;
 #pragma unroll
-        for (int u = 0; u < PL; ++u) {
-            const uint32_t t = k + (uint32_t)(u * 64 + lane);
-            const float* r = p + (size_t)vals[t < R1 ? t : R0] * stride;
-#pragma unroll
-            for (int f = 0; f < kMaxFields; ++f) q[u][f] = f < stride ? r[f] : 0.f;
-        }
-    };
-    auto stash = [&](int buf) {
-#pragma unroll
-        for (int u = 0; u < PL; ++u)
-#pragma unroll
-            for (int f = 0; f < kMaxFields; ++f)
-                if (f < stride) s_q[buf][(u * 64 + lane) * stride + f] = q[u][f];
-    };
+    for (int f = 0; f < NF; ++f)
+        if (f < stride) o[f] = acc[f] / c;
+}
+
+// PCL VoxelGrid centroid: the voxel's fields summed one point at a time in
+// input order (float), divided by the count.  The chain of adds is serial, the
+// loads are not: short runs are summed by one lane with its loads issued four
+// points ahead; long runs (the dense ground next to the sensor) go to a wave.
+__global__ void voxel_centroid_kernel(const float* __restrict__ p, int stride, const uint32_t* __restrict__ vals,
+                                      const uint32_t* __restrict__ starts, const uint32_t* __restrict__ ends,
+                                      const uint32_t* __restrict__ n_vox, uint32_t* __restrict__ big,
+                                      uint32_t* __restrict__ n_big, float* __restrict__ out, float* __restrict__ xyz,
+                                      uint8_t* __restrict__ sel) {
+    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
+    if (v >= *n_vox) return;
+    const uint32_t s = starts[v], e = ends[v];
+    if (e - s > (uint32_t)kLaneRun) {
+        big[atomicAdd(n_big, 1u)] = v;
+        return;
+    }
     float acc[kMaxFields];
 #pragma unroll
     for (int f = 0; f < kMaxFields; ++f) acc[f] = 0.f;
-    load(R0);
-    stash(0);
-    __syncthreads();
-    int buf = 0;
-    for (uint32_t k = R0; k < R1; k += kCentCh) {
-        const bool more = k + kCentCh < R1;
-        if (more) load(k + kCentCh);
-        const uint32_t lo = max(s, k), hi = min(e, k + (uint32_t)kCentCh);
-        for (uint32_t t = lo; t < hi; ++t) {
-            const float* r = s_q[buf] + (t - k) * stride;
+    for (uint32_t k = s; k < e; k += 4) {
+        float q[4][kMaxFields];
 #pragma unroll
-            for (int f = 0; f < kMaxFields; ++f)
-                if (f < stride) acc[f] += r[f];
+        for (int u = 0; u < 4; ++u) {
+            const float* r = p + (size_t)vals[k + u < e ? k + u : s] * stride;
+#pragma unroll
+            for (int f = 0; f < kMaxFields; ++f) q[u][f] = f < stride ? r[f] : 0.f;
         }
-        if (more) {
-            stash(buf ^ 1);
-            buf ^= 1;
-        }
-        __syncthreads();
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+            if (k + u < e) {
+#pragma unroll
+                for (int f = 0; f < kMaxFields; ++f) acc[f] += q[u][f];
+            }
     }
-    if (!mine) return;
-    const float c = (float)(e - s);
-    float* o = out + (size_t)v * stride;
-#pragma unroll
-    for (int f = 0; f < kMaxFields; ++f)
-        if (f < stride) o[f] = acc[f] / c;
-    if (xyz) {
+    write_centroid<kMaxFields>(out + (size_t)v * stride, acc, stride, e - s);
+    if (xyz) {  // the scan the output becomes: packed xyz and cleared selection flags, same values
+        const float c = (float)(e - s);
         xyz[3 * (size_t)v] = acc[0] / c;
         xyz[3 * (size_t)v + 1] = acc[1] / c;
         xyz[3 * (size_t)v + 2] = acc[2] / c;
         sel[v] = 0;
+    }
+}
+
+// long runs, one wave (= block) each: the lanes load 64 points at a time into
+// LDS (the next chunk's loads in flight while this one is summed); lane f
+// then adds field f of the 64 points in order — one LDS read + one add per
+// point, the fields in parallel
+__global__ void __launch_bounds__(64) voxel_centroid_big_kernel(const float* __restrict__ p, int stride,
+                                                                 const uint32_t* __restrict__ vals,
+                                                                 const uint32_t* __restrict__ starts,
+                                                                 const uint32_t* __restrict__ ends,
+                                                                 const uint32_t* __restrict__ big,
+                                                                 const uint32_t* __restrict__ n_big,
+                                                                 float* __restrict__ out, float* __restrict__ xyz,
+                                                                 uint8_t* __restrict__ sel) {
+    __shared__ float s_q[2][64 * kMaxFields];
+    const int lane = threadIdx.x;
+    const uint32_t nb = *n_big;
+    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
+        const uint32_t v = big[b];
+        const uint32_t s = starts[v], e = ends[v];
+        float q[kMaxFields];
+        auto load = [&](uint32_t k) {
+            const float* r = p + (size_t)vals[k + lane < e ? k + lane : s] * stride;
+#pragma unroll
+            for (int f = 0; f < kMaxFields; ++f) q[f] = f < stride ? r[f] : 0.f;
+        };
+        auto stash = [&](int buf) {
+#pragma unroll
+            for (int f = 0; f < kMaxFields; ++f)
+                if (f < stride) s_q[buf][lane * stride + f] = q[f];
+        };
+        float acc = 0.f;
+        load(s);
+        stash(0);
+        __syncthreads();
+        int buf = 0;
+        for (uint32_t k = s; k < e; k += 64) {
+            const bool more = k + 64 < e;
+            if (more) load(k + 64);
+            const uint32_t m = min(64u, e - k);
+            if (lane < stride) {
+                const float* col = s_q[buf] + lane;
+                uint32_t l = 0;
+                for (; l + 4 <= m; l += 4) {
+                    const float a0 = col[(l + 0) * stride], a1 = col[(l + 1) * stride];
+                    const float a2 = col[(l + 2) * stride], a3 = col[(l + 3) * stride];
+                    acc += a0;
+                    acc += a1;
+                    acc += a2;
+                    acc += a3;
+                }
+                for (; l < m; ++l) acc += col[l * stride];
+            }
+            if (more) {
+                stash(buf ^ 1);
+                buf ^= 1;
+            }
+            __syncthreads();
+        }
+        if (lane < stride) out[(size_t)v * stride + lane] = acc / (float)(e - s);
+        if (xyz && lane < 3) xyz[3 * (size_t)v + lane] = acc / (float)(e - s);
+        if (xyz && lane == 0) sel[v] = 0;
     }
 }
 
@@ -311,12 +352,19 @@ __global__ void transform_segs_kernel(const float* __restrict__ in, int64_t n, i
 // first, in time order and, inside a tie, in input order — compaction and sort in one.  every = 0: no
 // selection (the host selected the rows), the time key only.
 constexpr uint32_t kNotSelected = 0xffffffffu;
+__device__ __forceinline__ uint32_t piece_row(const RowPieces& m, uint32_t i) {
+    uint32_t base = m.src[0], s0 = m.start[0];
+#pragma unroll
+    for (int t = 1; t < 4; ++t)
+        if (t < m.n && i >= m.start[t]) base = m.src[t], s0 = m.start[t];
+    return base + (i - s0);
+}
 __global__ void scan_key_kernel(const float* __restrict__ p, int64_t n, int stride, int every, float blind2,
-                                int tfield, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+                                int tfield, uint32_t* __restrict__ keys, uint32_t* __restrict__ vals, RowPieces rp) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
     uint32_t k = kNotSelected;
-    const float* q = p + (size_t)i * stride;
+    const float* q = p + (size_t)piece_row(rp, (uint32_t)i) * stride;
     if (every == 0 || (i % every == 0 && (q[0] * q[0] + q[1] * q[1] + q[2] * q[2]) > blind2)) {
         const uint32_t b = __float_as_uint(q[tfield]);
         k = min((b & 0x80000000u) ? ~b : (b | 0x80000000u), kNotSelected - 1);
@@ -438,7 +486,8 @@ __device__ __forceinline__ void compensate(float* q, float tms, const ImuPose& h
 __global__ void undistort_gather_kernel(const float* __restrict__ in, int64_t n, int stride, int tfield,
                                         const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ order,
                                         const ImuPose* __restrict__ poses, int np, UndistortEnd end,
-                                        float* __restrict__ out, uint32_t* __restrict__ cnt, int* __restrict__ hcnt) {
+                                        float* __restrict__ out, uint32_t* __restrict__ cnt, int* __restrict__ hcnt,
+                                        RowPieces rp) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
     if (skeys) {
@@ -449,7 +498,7 @@ __global__ void undistort_gather_kernel(const float* __restrict__ in, int64_t n,
         }
         if (i + 1 == n) cnt[0] = (uint32_t)n, *hcnt = (int)n;
     }
-    const float* r = in + (size_t)(order ? order[i] : (uint32_t)i) * stride;
+    const float* r = in + (size_t)piece_row(rp, order ? order[i] : (uint32_t)i) * stride;
     float* o = out + (size_t)i * stride;
     for (int f = 3; f < stride; ++f) o[f] = r[f];
     float q[3] = {r[0], r[1], r[2]};
@@ -709,8 +758,10 @@ int voxel_grid_enqueue(FilterBuf& b, const float* d_in, int64_t n, const uint32_
     if (rc) return rc;
     // runs -> [start, end) per voxel (b.keys / b.vals are free after the sort)
     voxel_bounds_kernel<<<nblk(n), 256, 0, st>>>(b.keys_alt, n, b.head, b.vid, b.keys, b.vals, b.cnt + 2, b.d_small);
-    voxel_centroid_wave_kernel<<<(int)((n + 63) / 64), 64, 0, st>>>(d_in, stride, b.vals_alt, b.keys, b.vals, b.vid + n,
-                                                                     d_out, xyz, sel);
+    voxel_centroid_kernel<<<nblk(n), 256, 0, st>>>(d_in, stride, b.vals_alt, b.keys, b.vals, b.vid + n, b.big,
+                                                   b.big + b.cap, d_out, xyz, sel);
+    voxel_centroid_big_kernel<<<kBigBlocks, 64, 0, st>>>(d_in, stride, b.vals_alt, b.keys, b.vals, b.big,
+                                                         b.big + b.cap, d_out, xyz, sel);
     FCHK(hipGetLastError());
     return 0;
 }
@@ -801,7 +852,7 @@ int keyframe_cloud(const float* d_rec, int64_t n, int stride, const PoseArg& ps,
 
 int scan_preprocess_enqueue(FilterBuf& b, const float* d_raw, int64_t n, int stride, const ScanPrepParams& p,
                             const ImuPose* d_poses, int np, const UndistortEnd& end, float* d_out, hipStream_t st,
-                            int presel, float* xyz, uint8_t* sel) {
+                            int presel, float* xyz, uint8_t* sel, const RowPieces& rp) {
     b.prep_n = 0;
     b.prep_sel = -1;
     if (n <= 0) return 0;
@@ -813,23 +864,23 @@ int scan_preprocess_enqueue(FilterBuf& b, const float* d_raw, int64_t n, int str
     const uint32_t* cnt = nullptr;  // rows in use past this point: all n (host selection) or b.cnt[0]
     if (presel == 1) {  // selected and already in time order: the stable sort is the identity
         undistort_gather_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, p.time_field, nullptr, nullptr, d_poses,
-                                                         np, end, b.c, b.cnt, b.d_small + kHostSel);
+                                                         np, end, b.c, b.cnt, b.d_small + kHostSel, rp);
     } else if (presel == 0) {  // selected, times out of order: stable sort by time
-        scan_key_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, 0, 0.f, p.time_field, b.keys, b.vals);
+        scan_key_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, 0, 0.f, p.time_field, b.keys, b.vals, rp);
         rc = sort_pairs(b, n, st);
         if (rc) return rc;
         undistort_gather_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, p.time_field, nullptr, b.vals_alt, d_poses,
-                                                         np, end, b.c, b.cnt, b.d_small + kHostSel);
+                                                         np, end, b.c, b.cnt, b.d_small + kHostSel, rp);
     } else {
         // 1. Preprocess selection + 2. stable time sort in one sort over the n rows (the selected first),
         // 3. gather + undistort; the selected count stays on the device (b.cnt[0]) and in b.h_small
         const int every = p.point_filter_num > 0 ? p.point_filter_num : 1;
         scan_key_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, every, p.blind * p.blind, p.time_field, b.keys,
-                                                 b.vals);
+                                                 b.vals, RowPieces{});
         rc = sort_pairs(b, n, st);
         if (rc) return rc;
         undistort_gather_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, p.time_field, b.keys_alt, b.vals_alt,
-                                                         d_poses, np, end, b.c, b.cnt, b.d_small + kHostSel);
+                                                         d_poses, np, end, b.c, b.cnt, b.d_small + kHostSel, RowPieces{});
         cnt = b.cnt;
     }
     // 4. downSizeFilterSurf

@@ -35,6 +35,15 @@ struct UndistortEnd {
     double q_LI[4];  // offset_R_L_I
 };
 
+// Where the host packed the selected rows: logical row i of piece t (start[t] <= i < start[t + 1]) lives at
+// staged row src[t] + (i - start[t]) (the pieces were packed in parallel, each at its own offset, and go
+// to the device in one DMA with the gaps).  n = 1, start = src = 0: rows in place.
+struct RowPieces {
+    int n = 1;
+    uint32_t start[4] = {0, 0, 0, 0};
+    uint32_t src[4] = {0, 0, 0, 0};
+};
+
 struct ScanPrepParams {
     int point_filter_num;  // keep every n-th input point (Preprocess, kitti.launch:6)
     float blind;           // drop points with |p| <= blind (kitti.yaml:13)
@@ -93,7 +102,8 @@ int scan_preprocess(FilterBuf& b, const float* d_raw, int64_t n, int stride, con
 // centroid pass (rows past the voxel count untouched)
 int scan_preprocess_enqueue(FilterBuf& b, const float* d_raw, int64_t n, int stride, const ScanPrepParams& p,
                             const ImuPose* d_poses, int np, const UndistortEnd& end, float* d_out, hipStream_t st,
-                            int presel = -1, float* xyz = nullptr, uint8_t* sel = nullptr);
+                            int presel = -1, float* xyz = nullptr, uint8_t* sel = nullptr,
+                            const RowPieces& pieces = RowPieces{});
 int scan_preprocess_finish(FilterBuf& b, int stride, float* d_out, int64_t* n_out, int64_t* n_undist, hipStream_t st);
 // records -> packed xyz, and sel[0 .. n) = 0 (the scan's selection flags) in the same pass
 int records_to_xyz_sel(const float* d_rec, int64_t n, int stride, float* d_xyz, uint8_t* sel, hipStream_t st);
