@@ -29,6 +29,7 @@ namespace lio {
 namespace {
 
 constexpr uint32_t kInvalid = 0xffffffffu;
+constexpr int kPartBlocks = 4096;  // AABB partials b.part holds (a fused producer needs one per 256-row block)
 
 // min / max over the NT lanes of the block (lo[3], hi[3] per lane) into s[0..2][0] / s[3..5][0]
 template <int NT>
@@ -51,81 +52,19 @@ __device__ __forceinline__ void block_minmax(float (*s)[NT], const float* lo, co
     }
 }
 
-// AABB of the finite points (getMinMax3D) and PCL's voxel geometry in one launch: every block writes its
-// partial min / max, the last block to finish (a ticket counter, reset by that block for the next launch)
-// reduces the partials and derives
+// PCL's voxel geometry from the cloud's AABB (getMinMax3D over finite points):
 //   inverse_leaf = 1 / leaf;  min_b = floor(min_p * inv), max_b = floor(max_p * inv)
 //   div_b = max_b - min_b + 1; divb_mul = (1, div_b.x, div_b.x * div_b.y)
 //   overflow when div_b.x * div_b.y * div_b.z > INT_MAX (PCL then returns the input)
-// cnt (optional): the rows in use, <= n (the bound the grid is sized for)
-// SINGLE: one block covers the input (small clouds: no partials, no ticket, no fence); out_host: a
-// host-mapped copy of the geometry
-template <bool SINGLE, int NT = 256>
-__global__ void __launch_bounds__(NT) minmax_geom_kernel(const float* __restrict__ p, int64_t n,
-                                                         const uint32_t* __restrict__ cnt, int stride,
-                                                         float* __restrict__ part, unsigned* __restrict__ ticket,
-                                                         float lx, float ly, float lz, VoxelGeom* __restrict__ out,
-                                                         VoxelGeom* __restrict__ out_host) {
-    __shared__ float s[6][NT];
-    __shared__ bool last;
-    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
-    if (cnt) n = min<int64_t>(n, *cnt);
-    // U rows per lane in flight (a lone block over a sweep is one chain of round trips otherwise)
-    constexpr int U = 8;
-    const int64_t step = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i0 = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i0 < n; i0 += U * step) {
-        float v[U][3];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t i = i0 + u * step;
-            const float* q = p + (size_t)(i < n ? i : i0) * stride;
-            v[u][0] = q[0];
-            v[u][1] = q[1];
-            v[u][2] = q[2];
-        }
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const float x = v[u][0], y = v[u][1], z = v[u][2];
-            if (i0 + u * step >= n || !(isfinite(x) && isfinite(y) && isfinite(z))) continue;
-            lo[0] = fminf(lo[0], x);
-            lo[1] = fminf(lo[1], y);
-            lo[2] = fminf(lo[2], z);
-            hi[0] = fmaxf(hi[0], x);
-            hi[1] = fmaxf(hi[1], y);
-            hi[2] = fmaxf(hi[2], z);
-        }
-    }
-    block_minmax(s, lo, hi);
-    if constexpr (!SINGLE) {
-        if (threadIdx.x < 6) part[blockIdx.x * 6 + threadIdx.x] = s[threadIdx.x][0];
-        __threadfence();
-        __syncthreads();
-        if (threadIdx.x == 0) last = atomicAdd(ticket, 1u) == gridDim.x - 1;
-        __syncthreads();
-        if (!last) return;
-        __threadfence();
-        const volatile float* vp = part;  // the other blocks' partials, past this CU's cache
-        for (int d = 0; d < 3; ++d) lo[d] = INFINITY, hi[d] = -INFINITY;
-        for (int b = threadIdx.x; b < (int)gridDim.x; b += NT) {
-#pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                lo[d] = fminf(lo[d], vp[b * 6 + d]);
-                hi[d] = fmaxf(hi[d], vp[b * 6 + 3 + d]);
-            }
-        }
-        __syncthreads();
-        block_minmax(s, lo, hi);
-    }
-    if (threadIdx.x != 0) return;
-    if constexpr (!SINGLE) ticket[0] = 0u;
+__device__ __forceinline__ VoxelGeom voxel_geom(const float* lo, const float* hi, float lx, float ly, float lz) {
     VoxelGeom g;
     const float inv[3] = {1.0f / lx, 1.0f / ly, 1.0f / lz};
     int64_t div[3];
-    g.empty = !(s[0][0] <= s[3][0]);
+    g.empty = !(lo[0] <= hi[0]);
     for (int d = 0; d < 3; ++d) {
         g.inv[d] = inv[d];
-        g.min_b[d] = g.empty ? 0 : (int)floorf(s[d][0] * inv[d]);
-        const int max_b = g.empty ? 0 : (int)floorf(s[3 + d][0] * inv[d]);
+        g.min_b[d] = g.empty ? 0 : (int)floorf(lo[d] * inv[d]);
+        const int max_b = g.empty ? 0 : (int)floorf(hi[d] * inv[d]);
         div[d] = (int64_t)max_b - g.min_b[d] + 1;
     }
     g.overflow = div[0] * div[1] * div[2] > (int64_t)0x7fffffff;
@@ -134,21 +73,86 @@ __global__ void __launch_bounds__(NT) minmax_geom_kernel(const float* __restrict
     g.mul[2] = (int)(div[0] * div[1]);
     const int64_t top = g.overflow ? 0 : div[0] * div[1] * div[2] - 1;
     g.key_bits = top > 0 ? 64 - __clzll((unsigned long long)top) : 1;
-    *out = g;
-    if (out_host) *out_host = g;
+    return g;
 }
 
-// PCL: ijk = (int)(floor(p * inv) - (float)min_b); idx = ijk . divb_mul; non-finite points skipped
+// per block: min / max of the finite points it covers -> part[6 blockIdx.x ..] (lo xyz, hi xyz); no
+// cross-block hand-off — the key kernel reduces the partials itself
+__global__ void __launch_bounds__(256) minmax_partial_kernel(const float* __restrict__ p, int64_t n, int stride,
+                                                             float* __restrict__ part) {
+    __shared__ float s[6][256];
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float* q = p + (size_t)i * stride;
+        const float x = q[0], y = q[1], z = q[2];
+        if (!(isfinite(x) && isfinite(y) && isfinite(z))) continue;
+        lo[0] = fminf(lo[0], x);
+        lo[1] = fminf(lo[1], y);
+        lo[2] = fminf(lo[2], z);
+        hi[0] = fmaxf(hi[0], x);
+        hi[1] = fmaxf(hi[1], y);
+        hi[2] = fmaxf(hi[2], z);
+    }
+    block_minmax<256>(s, lo, hi);
+    if (threadIdx.x < 6) part[blockIdx.x * 6 + threadIdx.x] = s[threadIdx.x][0];
+}
+
 // keys past `bits` bits (the width the sort will use) raise flags[0]; i == 0 also clears the long-run
 // count of the centroid pass
-__global__ void voxel_key_kernel(const float* __restrict__ p, int64_t n, const uint32_t* __restrict__ cnt, int stride,
-                                 const VoxelGeom* __restrict__ gp, uint32_t* __restrict__ keys,
-                                 uint32_t* __restrict__ vals, int bits, uint32_t* __restrict__ flags,
-                                 uint32_t* __restrict__ n_big) {
+// minmax_partial_kernel over the first *cnt of n rows
+__global__ void __launch_bounds__(256) minmax_partial_cnt_kernel(const float* __restrict__ p, int64_t n,
+                                                                 const uint32_t* __restrict__ cnt, int stride,
+                                                                 float* __restrict__ part) {
+    __shared__ float s[6][256];
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    n = min<int64_t>(n, *cnt);
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float* q = p + (size_t)i * stride;
+        const float x = q[0], y = q[1], z = q[2];
+        if (!(isfinite(x) && isfinite(y) && isfinite(z))) continue;
+        lo[0] = fminf(lo[0], x);
+        lo[1] = fminf(lo[1], y);
+        lo[2] = fminf(lo[2], z);
+        hi[0] = fmaxf(hi[0], x);
+        hi[1] = fmaxf(hi[1], y);
+        hi[2] = fmaxf(hi[2], z);
+    }
+    block_minmax<256>(s, lo, hi);
+    if (threadIdx.x < 6) part[blockIdx.x * 6 + threadIdx.x] = s[threadIdx.x][0];
+}
+
+// Every block first reduces the nbp AABB partials (a few KB from L2) and derives the voxel geometry itself
+// — no single-block hand-off kernel between the AABB and the keys; block 0 also stores the geometry for
+// the host (host-mapped gh).
+__global__ void __launch_bounds__(256) voxel_key_kernel(const float* __restrict__ p, int64_t n,
+                                                        const uint32_t* __restrict__ cnt, int stride,
+                                                        const float* __restrict__ part, int nbp, float lx, float ly,
+                                                        float lz, VoxelGeom* __restrict__ gh, uint32_t* __restrict__ keys,
+                                                        uint32_t* __restrict__ vals, int bits,
+                                                        uint32_t* __restrict__ flags, uint32_t* __restrict__ n_big) {
+    __shared__ float s[6][256];
+    __shared__ VoxelGeom s_g;
+    {
+        float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int b = threadIdx.x; b < nbp; b += 256) {
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                lo[d] = fminf(lo[d], part[b * 6 + d]);
+                hi[d] = fmaxf(hi[d], part[b * 6 + 3 + d]);
+            }
+        }
+        block_minmax<256>(s, lo, hi);
+        if (threadIdx.x == 0) {
+            const float l3[3] = {s[0][0], s[1][0], s[2][0]}, h3[3] = {s[3][0], s[4][0], s[5][0]};
+            s_g = voxel_geom(l3, h3, lx, ly, lz);
+            if (blockIdx.x == 0) *gh = s_g;
+        }
+        __syncthreads();
+    }
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i == 0) *n_big = 0u;
     if (i >= n) return;
-    const VoxelGeom g = *gp;
+    const VoxelGeom g = s_g;
     const float* q = p + (size_t)i * stride;
     uint32_t k = kInvalid;
     if ((!cnt || i < (int64_t)*cnt) && isfinite(q[0]) && isfinite(q[1]) && isfinite(q[2]) && !g.overflow) {
@@ -483,18 +487,17 @@ __device__ __forceinline__ void compensate(float* q, float tms, const ImuPose& h
 // (head h-1, ..., 0) — reproduced for point 0.  np < 2: the rows are only gathered.
 // skeys == nullptr: every row is selected (the host selected them; no count to find); order == nullptr:
 // the rows are already in time order (identity).  hcnt: host-mapped copy of the count.
-__global__ void undistort_gather_kernel(const float* __restrict__ in, int64_t n, int stride, int tfield,
-                                        const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ order,
-                                        const ImuPose* __restrict__ poses, int np, UndistortEnd end,
-                                        float* __restrict__ out, uint32_t* __restrict__ cnt, int* __restrict__ hcnt,
-                                        RowPieces rp) {
-    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (i >= n) return;
+// row i (< n): false when it is past the selected rows (writes the count at the boundary)
+__device__ __forceinline__ bool undistort_row(const float* __restrict__ in, int64_t i, int64_t n, int stride, int tfield,
+                                              const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ order,
+                                              const ImuPose* __restrict__ poses, int np, const UndistortEnd& end,
+                                              float* __restrict__ out, uint32_t* __restrict__ cnt,
+                                              int* __restrict__ hcnt, const RowPieces& rp) {
     if (skeys) {
         const uint32_t key = skeys[i];
         if (key == kNotSelected) {
             if (i == 0 || skeys[i - 1] != kNotSelected) cnt[0] = (uint32_t)i, *hcnt = (int)i;
-            return;
+            return false;
         }
         if (i + 1 == n) cnt[0] = (uint32_t)n, *hcnt = (int)n;
     }
@@ -521,6 +524,41 @@ __global__ void undistort_gather_kernel(const float* __restrict__ in, int64_t n,
     o[0] = q[0];
     o[1] = q[1];
     o[2] = q[2];
+    return true;
+}
+
+__global__ void undistort_gather_kernel(const float* __restrict__ in, int64_t n, int stride, int tfield,
+                                        const uint32_t* __restrict__ skeys, const uint32_t* __restrict__ order,
+                                        const ImuPose* __restrict__ poses, int np, UndistortEnd end,
+                                        float* __restrict__ out, uint32_t* __restrict__ cnt, int* __restrict__ hcnt,
+                                        RowPieces rp) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    (void)undistort_row(in, i, n, stride, tfield, skeys, order, poses, np, end, out, cnt, hcnt, rp);
+}
+
+// the same, with the block's AABB partial of the rows it wrote (part[6 blockIdx.x ..]) for the voxel grid
+// that follows: no separate pass over the undistorted rows
+__global__ void __launch_bounds__(256) undistort_gather_aabb_kernel(const float* __restrict__ in, int64_t n, int stride,
+                                                                    int tfield, const uint32_t* __restrict__ skeys,
+                                                                    const uint32_t* __restrict__ order,
+                                                                    const ImuPose* __restrict__ poses, int np,
+                                                                    UndistortEnd end, float* __restrict__ out,
+                                                                    uint32_t* __restrict__ cnt, int* __restrict__ hcnt,
+                                                                    RowPieces rp, float* __restrict__ part) {
+    __shared__ float s[6][256];
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    if (i < n && undistort_row(in, i, n, stride, tfield, skeys, order, poses, np, end, out, cnt, hcnt, rp)) {
+        const float* o = out + (size_t)i * stride;
+        const float x = o[0], y = o[1], z = o[2];
+        if (isfinite(x) && isfinite(y) && isfinite(z)) {
+            lo[0] = x, lo[1] = y, lo[2] = z;
+            hi[0] = x, hi[1] = y, hi[2] = z;
+        }
+    }
+    block_minmax<256>(s, lo, hi);
+    if (threadIdx.x < 6) part[blockIdx.x * 6 + threadIdx.x] = s[threadIdx.x][0];
 }
 
 #define FCHK(x)                           \
@@ -569,13 +607,13 @@ int reserve(FilterBuf& b, int64_t n) {
     FCHK(hipMalloc(&b.vid, (c + 1) * sizeof(uint32_t)));
     FCHK(hipMalloc(&b.big, (c + 1) * sizeof(uint32_t)));  // long-run list + its count at [c]
     b.cap = c;
-    if (!b.part) FCHK(hipMalloc(&b.part, 6 * 1024 * sizeof(float)));
+    if (!b.part) FCHK(hipMalloc(&b.part, 6 * kPartBlocks * sizeof(float)));
     if (!b.geom) FCHK(hipMalloc(&b.geom, sizeof(VoxelGeom)));
     if (!b.h_small) {
         FCHK(hipHostMalloc(&b.h_small, 256, hipHostMallocMapped));
         FCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&b.d_small), b.h_small, 0));
     }
-    if (!b.cnt) {  // [0] selected count, [1] minmax_geom_kernel's ticket, [2] key-width flag (zero between launches)
+    if (!b.cnt) {  // [0] selected count, [2] key-width flag (zero between launches)
         FCHK(hipMalloc(&b.cnt, 64));
         FCHK(hipMemset(b.cnt, 0, 64));
     }
@@ -735,22 +773,20 @@ void filter_free(FilterBuf& b) {
 // host-mapped b.h_small ([0], [1..], [kHostFlags]) behind them: nothing waits for the device, nothing is
 // copied.  cnt (optional, device): rows in use <= n.  The voxel sort uses b.vox_bits key bits (learnt from
 // the previous call; a key past them raises the flag and the caller runs the call again at full width).
+// nbp > 0: the producer of d_in already wrote nbp AABB partials into b.part (undistort_gather_aabb_kernel)
 int voxel_grid_enqueue(FilterBuf& b, const float* d_in, int64_t n, const uint32_t* cnt, int stride, const float leaf[3],
-                       float* d_out, hipStream_t st, float* xyz = nullptr, uint8_t* sel = nullptr) {
+                       float* d_out, hipStream_t st, float* xyz = nullptr, uint8_t* sel = nullptr, int nbp = 0) {
     if (stride < 3 || stride > kMaxFields || n >= (int64_t)0x7fffffff) return -1;
     if (reserve(b, n)) return -5;
     auto* hgeom = reinterpret_cast<VoxelGeom*>(b.d_small + 1);
-    if (n <= 1024 * 64) {  // one block: no partials, no ticket, no fence
-        minmax_geom_kernel<true, 1024><<<1, 1024, 0, st>>>(d_in, n, cnt, stride, b.part, b.cnt + 1, leaf[0], leaf[1],
-                                                           leaf[2], b.geom, hgeom);
-    } else {
-        const int nbA = (int)std::min<int64_t>(1024, (n + 255) / 256);
-        minmax_geom_kernel<false><<<nbA, 256, 0, st>>>(d_in, n, cnt, stride, b.part, b.cnt + 1, leaf[0], leaf[1],
-                                                       leaf[2], b.geom, hgeom);
+    if (nbp <= 0) {  // no producer wrote the AABB partials: one pass over the input
+        if (cnt) return -1;  // (the scan path's rows in use come with the undistortion's partials)
+        nbp = (int)std::min<int64_t>(1024, (n + 255) / 256);
+        minmax_partial_kernel<<<nbp, 256, 0, st>>>(d_in, n, stride, b.part);
     }
     const int bits = std::min(std::max(b.vox_bits, 1), 32);
-    voxel_key_kernel<<<nblk(n), 256, 0, st>>>(d_in, n, cnt, stride, b.geom, b.keys, b.vals, bits, b.cnt + 2,
-                                              b.big + b.cap);
+    voxel_key_kernel<<<nblk(n), 256, 0, st>>>(d_in, n, cnt, stride, b.part, nbp, leaf[0], leaf[1], leaf[2], hgeom,
+                                              b.keys, b.vals, bits, b.cnt + 2, b.big + b.cap);
     int rc = sort_pairs(b, n, st, bits);
     if (rc) return rc;
     run_head_kernel<<<nblk(n + 1), 256, 0, st>>>(b.keys_alt, n, b.head);
@@ -862,15 +898,23 @@ int scan_preprocess_enqueue(FilterBuf& b, const float* d_raw, int64_t n, int str
     int rc = fgrow(&b.c, b.c_cap, n * stride);
     if (rc) return rc;
     const uint32_t* cnt = nullptr;  // rows in use past this point: all n (host selection) or b.cnt[0]
+    // the undistortion writes the AABB partials of its rows when the voxel grid follows (one pass fewer)
+    const bool fuse = p.leaf > 0.f && nblk(n) <= kPartBlocks;
+    auto undistort = [&](const uint32_t* skeys, const uint32_t* order, const RowPieces& pr) {
+        if (fuse)
+            undistort_gather_aabb_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, p.time_field, skeys, order, d_poses,
+                                                                  np, end, b.c, b.cnt, b.d_small + kHostSel, pr, b.part);
+        else
+            undistort_gather_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, p.time_field, skeys, order, d_poses, np,
+                                                             end, b.c, b.cnt, b.d_small + kHostSel, pr);
+    };
     if (presel == 1) {  // selected and already in time order: the stable sort is the identity
-        undistort_gather_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, p.time_field, nullptr, nullptr, d_poses,
-                                                         np, end, b.c, b.cnt, b.d_small + kHostSel, rp);
+        undistort(nullptr, nullptr, rp);
     } else if (presel == 0) {  // selected, times out of order: stable sort by time
         scan_key_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, 0, 0.f, p.time_field, b.keys, b.vals, rp);
         rc = sort_pairs(b, n, st);
         if (rc) return rc;
-        undistort_gather_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, p.time_field, nullptr, b.vals_alt, d_poses,
-                                                         np, end, b.c, b.cnt, b.d_small + kHostSel, rp);
+        undistort(nullptr, b.vals_alt, rp);
     } else {
         // 1. Preprocess selection + 2. stable time sort in one sort over the n rows (the selected first),
         // 3. gather + undistort; the selected count stays on the device (b.cnt[0]) and in b.h_small
@@ -879,8 +923,7 @@ int scan_preprocess_enqueue(FilterBuf& b, const float* d_raw, int64_t n, int str
                                                  b.vals, RowPieces{});
         rc = sort_pairs(b, n, st);
         if (rc) return rc;
-        undistort_gather_kernel<<<nblk(n), 256, 0, st>>>(d_raw, n, stride, p.time_field, b.keys_alt, b.vals_alt,
-                                                         d_poses, np, end, b.c, b.cnt, b.d_small + kHostSel, RowPieces{});
+        undistort(b.keys_alt, b.vals_alt, RowPieces{});
         cnt = b.cnt;
     }
     // 4. downSizeFilterSurf
@@ -889,7 +932,11 @@ int scan_preprocess_enqueue(FilterBuf& b, const float* d_raw, int64_t n, int str
     b.prep_sel = presel >= 0 ? n : -1;
     if (b.prep_leaf) {
         const float leaf[3] = {p.leaf, p.leaf, p.leaf};
-        return voxel_grid_enqueue(b, b.c, n, cnt, stride, leaf, d_out, st, xyz, sel);
+        if (!fuse && cnt) {  // more rows than partial slots on the device-selection path: a separate AABB pass
+            minmax_partial_cnt_kernel<<<1024, 256, 0, st>>>(b.c, n, cnt, stride, b.part);
+            return voxel_grid_enqueue(b, b.c, n, cnt, stride, leaf, d_out, st, xyz, sel, 1024);
+        }
+        return voxel_grid_enqueue(b, b.c, n, cnt, stride, leaf, d_out, st, xyz, sel, fuse ? nblk(n) : 0);
     }
     FCHK(hipMemcpyAsync(d_out, b.c, (size_t)n * stride * sizeof(float), hipMemcpyDeviceToDevice, st));
     return 0;
