@@ -17,8 +17,7 @@
 namespace lio {
 
 // AABB (+ alive count) over the alive entries of the id-order array.
-__global__ void aabb_partial_kernel(const float4* __restrict__ by_id, int64_t n, float* __restrict__ part,
-                                    uint32_t* __restrict__ alive_count) {
+__global__ void aabb_partial_kernel(const float4* __restrict__ by_id, int64_t n, float* __restrict__ part) {
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
     uint32_t cnt = 0;
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -52,22 +51,30 @@ __global__ void aabb_partial_kernel(const float4* __restrict__ by_id, int64_t n,
         }
         __syncthreads();
     }
-    if (threadIdx.x < 6) part[blockIdx.x * 6 + threadIdx.x] = s[threadIdx.x][0];
-    if (threadIdx.x == 0 && sc) atomicAdd(alive_count, sc);
+    __syncthreads();  // sc complete
+    // partial = 6 floats + the alive count (8-word stride): no same-address device atomics (1024 blocks
+    // adding to one counter serialise at the memory-side atomic unit)
+    if (threadIdx.x < 6) part[blockIdx.x * 8 + threadIdx.x] = s[threadIdx.x][0];
+    if (threadIdx.x == 0) part[blockIdx.x * 8 + 6] = __uint_as_float(sc);
 }
 
 // min/max over the block partials: 256 threads stride the partials, then an
 // LDS tree (min/max are order-independent, so this is exact)
+// out[0..5] = AABB, out[6] = alive count (uint bits)
 __global__ void __launch_bounds__(256) aabb_final_kernel(const float* __restrict__ part, int nb,
                                                          float* __restrict__ out) {
     __shared__ float s[6][256];
+    __shared__ uint32_t s_cnt;
+    if (threadIdx.x == 0) s_cnt = 0;
     float lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    uint32_t cnt = 0;
     for (int b = threadIdx.x; b < nb; b += 256) {
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
-            lo[d] = fminf(lo[d], part[b * 6 + d]);
-            hi[d] = fmaxf(hi[d], part[b * 6 + 3 + d]);
+            lo[d] = fminf(lo[d], part[b * 8 + d]);
+            hi[d] = fmaxf(hi[d], part[b * 8 + 3 + d]);
         }
+        cnt += __float_as_uint(part[b * 8 + 6]);
     }
 #pragma unroll
     for (int d = 0; d < 3; ++d) {
@@ -85,7 +92,10 @@ __global__ void __launch_bounds__(256) aabb_final_kernel(const float* __restrict
         }
         __syncthreads();
     }
+    if (cnt) atomicAdd(&s_cnt, cnt);  // LDS
+    __syncthreads();
     if (threadIdx.x < 6) out[threadIdx.x] = s[threadIdx.x][0];
+    if (threadIdx.x == 0) out[6] = __uint_as_float(s_cnt);
 }
 
 __global__ void init_by_id_kernel(const float* __restrict__ xyz, int64_t n, float4* __restrict__ by_id) {
@@ -96,17 +106,30 @@ __global__ void init_by_id_kernel(const float* __restrict__ xyz, int64_t n, floa
 
 // keys of every id; dead ids get the sentinel ncells (sorted past the table)
 __global__ void cell_key_kernel(const float4* __restrict__ by_id, int64_t n, GridGeom g, uint32_t* __restrict__ keys,
-                                uint32_t* __restrict__ vals, uint32_t* __restrict__ counts) {
+                                uint32_t* __restrict__ vals) {
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     if (i >= n) return;
     const float4 p = by_id[i];
     uint32_t k = g.ncells;
-    if (p.w != 0.f) {
-        k = cell_key_of(g, 1.0f / g.cell, p.x, p.y, p.z);
-        atomicAdd(&counts[k], 1u);
-    }
+    if (p.w != 0.f) k = cell_key_of(g, 1.0f / g.cell, p.x, p.y, p.z);
     keys[i] = k;
     vals[i] = (uint32_t)i;
+}
+
+// per-cell counts from the SORTED keys: a wave's lanes hold runs of equal keys; the first lane of each run
+// (inside the wave) adds the run's length — one device atomic per run piece instead of one per point
+// (spatially ordered clouds put whole waves on one cell, which serialised the per-point adds)
+__global__ void sorted_counts_kernel(const uint32_t* __restrict__ keys, int64_t n, uint32_t ncells,
+                                     uint32_t* __restrict__ counts) {
+    const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63;
+    const uint32_t k = j < n ? keys[j] : ncells;
+    const uint32_t prev = (j > 0 && j < n) ? keys[j - 1] : ~k;
+    const bool head = lane == 0 || k != prev;
+    const uint64_t heads = __ballot(head);
+    const uint64_t above = lane == 63 ? 0ull : heads & (~0ull << (lane + 1));
+    const int next = above ? __ffsll((unsigned long long)above) - 1 : 64;
+    if (head && j < n && k < ncells) atomicAdd(&counts[k], (uint32_t)(next - lane));
 }
 
 __global__ void gather_kernel(const float4* __restrict__ by_id, int64_t n, const uint32_t* __restrict__ sorted_ids,
@@ -376,14 +399,12 @@ int grid_rebuild(GridBuf& g, float cell, float slack, hipStream_t st) {
     if (!(cell > 0.f)) cell = 1.0f;
     int rc = reserve_entries(g, std::max<int64_t>(n_ids, 1));
     if (rc) return rc;
-    if (!g.aabb) HIPCHK(hipMalloc(&g.aabb, 6 * 1024 * sizeof(float) + 64));
+    if (!g.aabb) HIPCHK(hipMalloc(&g.aabb, 8 * 1024 * sizeof(float) + 64));  // result + 8-word partials
     if (!g.aabb_host) HIPCHK(hipHostMalloc(&g.aabb_host, 64));
     // ---- AABB + alive count
     const int nbA = (int)std::max<int64_t>(1, std::min<int64_t>(1024, (n_ids + 255) / 256));
     float* part = g.aabb + 8;
-    uint32_t* d_cnt = reinterpret_cast<uint32_t*>(g.aabb + 6);
-    HIPCHK(hipMemsetAsync(d_cnt, 0, sizeof(uint32_t), st));
-    if (n_ids) aabb_partial_kernel<<<nbA, 256, 0, st>>>(g.by_id, n_ids, part, d_cnt);
+    if (n_ids) aabb_partial_kernel<<<nbA, 256, 0, st>>>(g.by_id, n_ids, part);
     aabb_final_kernel<<<1, 256, 0, st>>>(part, n_ids ? nbA : 0, g.aabb);
     HIPCHK(hipMemcpyAsync(g.aabb_host, g.aabb, 7 * sizeof(float), hipMemcpyDeviceToHost, st));
     HIPCHK(hipStreamSynchronize(st));
@@ -426,7 +447,7 @@ int grid_rebuild(GridBuf& g, float cell, float slack, hipStream_t st) {
     uint32_t* counts = g.start + g.cells_cap;
     HIPCHK(hipMemsetAsync(counts, 0, (size_t)nc1 * sizeof(uint32_t), st));
     const int nb = (int)std::max<int64_t>(1, (n_ids + 255) / 256);
-    if (n_ids) cell_key_kernel<<<nb, 256, 0, st>>>(g.by_id, n_ids, geo, g.keys, g.vals, counts);
+    if (n_ids) cell_key_kernel<<<nb, 256, 0, st>>>(g.by_id, n_ids, geo, g.keys, g.vals);
     // ---- sort (key, id): stable, so ids ascend inside a cell; dead ids (key ncells) last
     int bits = 1;
     while (bits < 32 && ((uint64_t)1 << bits) <= (uint64_t)geo.ncells) ++bits;
@@ -437,9 +458,11 @@ int grid_rebuild(GridBuf& g, float cell, float slack, hipStream_t st) {
     size_t need = std::max(sort_bytes, scan_bytes);
     if (ensure(&g.tmp, g.tmp_bytes, need) != 0) return -5;
     size_t tb = g.tmp_bytes;
-    if (n_ids)
+    if (n_ids) {
         HIPCHK(hipcub::DeviceRadixSort::SortPairs(g.tmp, tb, g.keys, g.keys_alt, g.vals, g.vals_alt, (int)n_ids, 0,
                                                   bits, st));
+        sorted_counts_kernel<<<nb, 256, 0, st>>>(g.keys_alt, n_ids, geo.ncells, counts);
+    }
     tb = g.tmp_bytes;
     HIPCHK(hipcub::DeviceScan::ExclusiveSum(g.tmp, tb, counts, g.start, (int)nc1, st));
     if (!g.gapped) {
