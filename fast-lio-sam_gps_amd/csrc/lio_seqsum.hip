@@ -356,16 +356,15 @@ __global__ void __launch_bounds__(kSeqThreads) seq_events(Src src, SeqSumBuf b, 
         }
 }
 
-__device__ __forceinline__ double readlane_d(double v, int l) {
-    const uint64_t u = (uint64_t)__double_as_longlong(v);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
-    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-
-// one wave per chain: s_{event-1} = s_{previous event} + run sum (exact double), s_event = fl(that + x_event)
+// one wave per chain: s_{event-1} = s_{previous event} + run sum (exact double), s_event = fl(that + x_event).
+// The chain of adds is the serial floor; everything else is kept off it: a batch of 64 events' run sums and
+// values goes through LDS first, the next kWalkU of them are read (broadcast) before their dependent adds, so
+// an event costs its two conversions and two adds, not a cross-lane read each.
+constexpr int kWalkU = 8;
 template <class Src>
 __global__ void __launch_bounds__(64) seq_walk(Src src, SeqSumBuf b, const uint32_t* d_n) {
+    __shared__ double s_R[64 + kWalkU];  // + the slack the unrolled reads of the last step may touch
+    __shared__ float s_x[64 + kWalkU], s_f[64];
     const int c = blockIdx.x;
     const int lane = threadIdx.x;
     const int64_t n = *d_n;
@@ -385,22 +384,32 @@ __global__ void __launch_bounds__(64) seq_walk(Src src, SeqSumBuf b, const uint3
         const int i = base + lane;
         const bool ok = i < nev;
         const uint64_t P = ok ? EP[i] : 0;
-        const float xv = ok ? EX[i] : 0.f;
         uint64_t Pp = __shfl_up(P, 1, 64);
         if (lane == 0) Pp = Pbase;
-        const double R = (double)(int64_t)(P - Pp) * unit;  // a run sum: exact (<= 53 significant bits)
+        s_R[lane] = (double)(int64_t)(P - Pp) * unit;  // a run sum: exact (<= 53 significant bits)
+        s_x[lane] = ok ? EX[i] : 0.f;
+        __syncthreads();
         const int cnt = min(64, nev - base);
-        float mine = 0.f;
-        for (int l = 0; l < cnt; ++l) {
-            const double r = readlane_d(R, l);
-            const float xl = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(xv), l));
-            const float f = (float)(s + r) + xl;  // s + r is the float s_{event-1}; the event's add rounds once
-            s = (double)f;
-            if (lane == l) mine = f;
+        for (int l = 0; l < cnt; l += kWalkU) {
+            double r[kWalkU];
+            float x[kWalkU];
+#pragma unroll
+            for (int u = 0; u < kWalkU; ++u) {
+                r[u] = s_R[l + u];
+                x[u] = s_x[l + u];
+            }
+#pragma unroll
+            for (int u = 0; u < kWalkU; ++u)
+                if (l + u < cnt) {  // wave-uniform
+                    const float f = (float)(s + r[u]) + x[u];  // s + r is the float s_{event-1}; the event rounds once
+                    s = (double)f;
+                    if (lane == 0) s_f[l + u] = f;
+                }
         }
-        if (ok) ES[i] = mine;
-        const uint64_t Pl = __shfl(P, cnt - 1, 64);
-        Pbase = Pl;
+        __syncthreads();
+        if (ok) ES[i] = s_f[lane];
+        Pbase = __shfl(P, cnt - 1, 64);
+        __syncthreads();  // the next batch overwrites s_R / s_x / s_f
     }
     if (lane == 0) b.result[c] = (float)(s + (double)(int64_t)(b.ptot[c] - Pbase) * unit);
 }
