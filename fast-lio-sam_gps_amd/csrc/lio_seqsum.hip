@@ -359,12 +359,14 @@ __global__ void __launch_bounds__(kSeqThreads) seq_events(Src src, SeqSumBuf b, 
 // one wave per chain: s_{event-1} = s_{previous event} + run sum (exact double), s_event = fl(that + x_event).
 // The chain of adds is the serial floor; everything else is kept off it: a batch of 64 events' run sums and
 // values goes through LDS first, the next kWalkU of them are read (broadcast) before their dependent adds, so
-// an event costs its two conversions and two adds, not a cross-lane read each.
+// an event costs its two conversions and two adds, not a cross-lane read each.  Full batches run without a
+// per-event guard and each lane picks its own event's s with a select beside the chain; the next batch's
+// records are loaded while this one's chain runs.
 constexpr int kWalkU = 8;
 template <class Src>
 __global__ void __launch_bounds__(64) seq_walk(Src src, SeqSumBuf b, const uint32_t* d_n) {
     __shared__ double s_R[64 + kWalkU];  // + the slack the unrolled reads of the last step may touch
-    __shared__ float s_x[64 + kWalkU], s_f[64];
+    __shared__ float s_x[64 + kWalkU];
     const int c = blockIdx.x;
     const int lane = threadIdx.x;
     const int64_t n = *d_n;
@@ -380,36 +382,50 @@ __global__ void __launch_bounds__(64) seq_walk(Src src, SeqSumBuf b, const uint3
     float* ES = b.ev_s + (size_t)c * b.evcap;
     double s = (double)src(c, 0);
     uint64_t Pbase = 0;
+    // the next batch's event records are loaded while this batch's chain runs
+    uint64_t Pn = lane < nev ? EP[lane] : 0;
+    float Xn = lane < nev ? EX[lane] : 0.f;
     for (int base = 0; base < nev; base += 64) {
         const int i = base + lane;
         const bool ok = i < nev;
-        const uint64_t P = ok ? EP[i] : 0;
+        const uint64_t P = Pn;
+        const float X = Xn;
+        const int inext = i + 64;
+        Pn = inext < nev ? EP[inext] : 0;
+        Xn = inext < nev ? EX[inext] : 0.f;
         uint64_t Pp = __shfl_up(P, 1, 64);
         if (lane == 0) Pp = Pbase;
         s_R[lane] = (double)(int64_t)(P - Pp) * unit;  // a run sum: exact (<= 53 significant bits)
-        s_x[lane] = ok ? EX[i] : 0.f;
+        s_x[lane] = ok ? X : 0.f;
         __syncthreads();
         const int cnt = min(64, nev - base);
-        for (int l = 0; l < cnt; l += kWalkU) {
-            double r[kWalkU];
-            float x[kWalkU];
+        float myf = 0.f;  // lane k keeps the batch's k-th s_event (a select beside the chain, not on it)
+        if (cnt == 64) {  // full batches: no per-event guard
+            for (int l = 0; l < 64; l += kWalkU) {
+                double r[kWalkU];
+                float x[kWalkU];
 #pragma unroll
-            for (int u = 0; u < kWalkU; ++u) {
-                r[u] = s_R[l + u];
-                x[u] = s_x[l + u];
-            }
+                for (int u = 0; u < kWalkU; ++u) {
+                    r[u] = s_R[l + u];
+                    x[u] = s_x[l + u];
+                }
 #pragma unroll
-            for (int u = 0; u < kWalkU; ++u)
-                if (l + u < cnt) {  // wave-uniform
+                for (int u = 0; u < kWalkU; ++u) {
                     const float f = (float)(s + r[u]) + x[u];  // s + r is the float s_{event-1}; the event rounds once
                     s = (double)f;
-                    if (lane == 0) s_f[l + u] = f;
+                    myf = (lane == l + u) ? f : myf;
                 }
+            }
+        } else {
+            for (int l = 0; l < cnt; ++l) {
+                const float f = (float)(s + s_R[l]) + s_x[l];
+                s = (double)f;
+                myf = (lane == l) ? f : myf;
+            }
         }
-        __syncthreads();
-        if (ok) ES[i] = s_f[lane];
+        if (ok) ES[i] = myf;
         Pbase = __shfl(P, cnt - 1, 64);
-        __syncthreads();  // the next batch overwrites s_R / s_x / s_f
+        __syncthreads();  // the next batch overwrites s_R / s_x
     }
     if (lane == 0) b.result[c] = (float)(s + (double)(int64_t)(b.ptot[c] - Pbase) * unit);
 }
