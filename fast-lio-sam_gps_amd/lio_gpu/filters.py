@@ -87,11 +87,14 @@ def imu_poses_to_c(poses):
     doubles in this order; filled through numpy, not element by element)."""
     n = len(poses)
     P = np.zeros((max(n, 1), 22), np.float64)
-    if n:
-        P[:n, 0] = [float(p["offset_time"]) for p in poses]
-        for j, name in ((1, "acc"), (4, "gyr"), (7, "vel"), (10, "pos")):
-            P[:n, j:j + 3] = np.asarray([np.asarray(p[name], float).ravel() for p in poses])
-        P[:n, 13:22] = np.asarray([np.asarray(p["rot"], float).ravel() for p in poses])
+    for i, p in enumerate(poses):  # row slices assigned directly (no per-field temporaries)
+        r = P[i]
+        r[0] = p["offset_time"]
+        r[1:4] = p["acc"]
+        r[4:7] = p["gyr"]
+        r[7:10] = p["vel"]
+        r[10:13] = p["pos"]
+        r[13:22] = np.ravel(p["rot"])
     assert C.sizeof(_capi.ImuPose) == 22 * 8
     return (_capi.ImuPose * max(n, 1)).from_buffer(P)
 

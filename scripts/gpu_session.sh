@@ -62,6 +62,14 @@ for s in $STEPS; do
            run prep_time 300 bash -c 'python scripts/prep_timing.py 80 && LIO_PREP_UPLOAD=full python scripts/prep_timing.py 80' &&
            run prep_profile 300 bash -c "LIO_PREP_PROFILE=1 python scripts/prep_timing.py 60 2> $OUT/prep_profile.err && python scripts/prep_profile_summary.py $OUT/prep_profile.err" &&
            run rocprof_prep 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof_prep" -o run --output-format csv -- python scripts/prep_timing.py 40 ;;
+    sortab) for v in onesweep bigblock; do
+               LIO_SORT=$v runs pytest_sort_$v 600 python -u -m pytest tests/test_gpu_filters.py tests/test_gpu_pipeline.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread || exit 1
+             done &&
+           LIO_CENTROID=lane LIO_VOX_RUNS=multi runs pytest_sort_old 600 python -u -m pytest tests/test_gpu_filters.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread &&
+           run sort_time 500 bash -c 'for r in 1 2; do for v in merge onesweep bigblock; do echo "sort=$v"; LIO_SORT=$v python scripts/prep_timing.py 80 || exit $?; done; echo "centroid=lane runs=multi"; LIO_CENTROID=lane LIO_VOX_RUNS=multi python scripts/prep_timing.py 80 || exit $?; done' &&
+           run sort_prof_def 300 rocprofv3 --kernel-trace --stats -d "$OUT/sort_def" -o run --output-format csv -- python scripts/prep_timing.py 40 &&
+           run sort_prof_one 300 env LIO_SORT=onesweep rocprofv3 --kernel-trace --stats -d "$OUT/sort_one" -o run --output-format csv -- python scripts/prep_timing.py 40 &&
+           run sort_prof_big 300 env LIO_SORT=bigblock rocprofv3 --kernel-trace --stats -d "$OUT/sort_big" -o run --output-format csv -- python scripts/prep_timing.py 40 ;;
     fidprof) run fid_prof 300 env LIO_ICP_ORDER=2 rocprofv3 --kernel-trace --stats -d "$OUT/fidprof" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 ;;
     maprec) runs pytest_maprec 600 python -u -m pytest tests/test_gpu_map.py tests/test_gpu_pipeline.py -x -v -p no:cacheprovider --timeout 500 --timeout-method thread ;;
     fid)   runs pytest_fid 900 python -u -m pytest tests/test_gpu_seqsum.py tests/test_gpu_icp.py -k "seqsum or fidelity or double" -x -v -s -p no:cacheprovider --timeout 300 --timeout-method thread &&
@@ -86,7 +94,8 @@ for s in $STEPS; do
     icppmc2) run icp_trace 300 rocprofv3 --kernel-trace -d "$OUT/icptrace" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
              run icp_pmc_sq 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_BUSY_CYCLES --kernel-trace -d "$OUT/icpsq" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
              run icp_pmc_fetch 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d "$OUT/icpfetch" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
-             run icp_pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/icpwrite" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 ;;
+             run icp_pmc_write 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/icpwrite" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
+             { python scripts/icp_pmc_traffic.py "$OUT" "$OUT/icp_traffic.json" > "$OUT/icp_traffic.txt" 2>&1; true; } ;;
     icpprof) run icp_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/icpprof" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
              run icp_pmc_valu 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --kernel-trace -d "$OUT/icppmc" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 ;;
     mapt)  run map_timing 400 python scripts/map_incr_timing.py 20 ;;
