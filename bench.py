@@ -215,8 +215,21 @@ def _loop_icp(args, LC, synth, local, world, rank, dist, rehearse, coll_dev, bar
                 "nn_kernel_ms_per_pass": round(nn_ms, 4),
                 "kernel_gbs": round(BYTES_PER_PT_ICP * shard_n / (icp_kernel_ms * 1e-3) / 1e9, 2)
                 if passes else None,
-                "sq_breakdown": _icp_sq(args)}
+                "sq_breakdown": _icp_sq(args), "traffic": _icp_traffic()}
     return loop_icp, src, dst
+
+
+def _icp_traffic():
+    """the ICP tile kernel's HBM traffic per pass from the committed FETCH_SIZE / WRITE_SIZE passes
+    (scripts/icp_pmc_traffic.py over scripts/icp_ab.py 1.0 1)"""
+    path = os.path.join(ROOT, "profiles", "r04_pmc_icp_traffic.json")
+    try:
+        pm = json.load(open(path))
+    except Exception:
+        return None
+    return {"mean_bytes_per_pass": pm["mean_hbm_traffic_bytes"], "x_algorithmic_mean": pm["mean_x_algorithmic"],
+            "x_algorithmic_max": pm["max_x_algorithmic"], "algorithmic_bytes": pm["algorithmic_bytes_per_pass"],
+            "source": os.path.relpath(path, ROOT)}
 
 
 def _icp_sq(args):

@@ -62,14 +62,10 @@ for s in $STEPS; do
            run prep_time 300 bash -c 'python scripts/prep_timing.py 80 && LIO_PREP_UPLOAD=full python scripts/prep_timing.py 80' &&
            run prep_profile 300 bash -c "LIO_PREP_PROFILE=1 python scripts/prep_timing.py 60 2> $OUT/prep_profile.err && python scripts/prep_profile_summary.py $OUT/prep_profile.err" &&
            run rocprof_prep 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof_prep" -o run --output-format csv -- python scripts/prep_timing.py 40 ;;
-    sortab) for v in onesweep bigblock; do
-               LIO_SORT=$v runs pytest_sort_$v 600 python -u -m pytest tests/test_gpu_filters.py tests/test_gpu_pipeline.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread || exit 1
-             done &&
-           LIO_CENTROID=lane LIO_VOX_RUNS=multi runs pytest_sort_old 600 python -u -m pytest tests/test_gpu_filters.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread &&
-           run sort_time 500 bash -c 'for r in 1 2; do for v in merge onesweep bigblock; do echo "sort=$v"; LIO_SORT=$v python scripts/prep_timing.py 80 || exit $?; done; echo "centroid=lane runs=multi"; LIO_CENTROID=lane LIO_VOX_RUNS=multi python scripts/prep_timing.py 80 || exit $?; done' &&
-           run sort_prof_def 300 rocprofv3 --kernel-trace --stats -d "$OUT/sort_def" -o run --output-format csv -- python scripts/prep_timing.py 40 &&
-           run sort_prof_one 300 env LIO_SORT=onesweep rocprofv3 --kernel-trace --stats -d "$OUT/sort_one" -o run --output-format csv -- python scripts/prep_timing.py 40 &&
-           run sort_prof_big 300 env LIO_SORT=bigblock rocprofv3 --kernel-trace --stats -d "$OUT/sort_big" -o run --output-format csv -- python scripts/prep_timing.py 40 ;;
+    sortab) LIO_CENTROID=lane LIO_VOX_RUNS=multi runs pytest_prep_old 600 python -u -m pytest tests/test_gpu_filters.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread &&
+           runs pytest_prep_new 600 python -u -m pytest tests/test_gpu_filters.py tests/test_gpu_pipeline.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread &&
+           run prep_ab 500 bash -c 'for r in 1 2 3; do echo "default"; python scripts/prep_timing.py 80 || exit $?; echo "centroid=lane runs=multi"; LIO_CENTROID=lane LIO_VOX_RUNS=multi python scripts/prep_timing.py 80 || exit $?; done' &&
+           run prep_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prep_prof" -o run --output-format csv -- python scripts/prep_timing.py 40 ;;
     fidprof) run fid_prof 300 env LIO_ICP_ORDER=2 rocprofv3 --kernel-trace --stats -d "$OUT/fidprof" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 ;;
     maprec) runs pytest_maprec 600 python -u -m pytest tests/test_gpu_map.py tests/test_gpu_pipeline.py -x -v -p no:cacheprovider --timeout 500 --timeout-method thread ;;
     fid)   runs pytest_fid 900 python -u -m pytest tests/test_gpu_seqsum.py tests/test_gpu_icp.py -k "seqsum or fidelity or double" -x -v -s -p no:cacheprovider --timeout 300 --timeout-method thread &&
