@@ -15,3 +15,5 @@ for ln in open(sys.argv[1]):
         except ValueError:
             pass
 print(" ".join(f"{k} p50 {statistics.median(v):.1f}" for k, v in vals.items() if k not in ("attempt",)))
+att = vals.get("attempt", [])
+print(f"calls {len(vals.get('total_us', []))} wait lines {len(att)} redo (attempt > 0) {sum(1 for a in att if a > 0)}")
