@@ -19,6 +19,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 
 #include "lio_dev.hpp"
@@ -194,6 +195,98 @@ __global__ void voxel_bounds_kernel(const uint32_t* __restrict__ keys, int64_t n
     if (j + 1 == n || keys[j + 1] != key) ends[r] = (uint32_t)(j + 1);
 }
 
+// Small inputs (n <= kRunsOneBlock): run heads, their exclusive count and the run bounds in ONE block —
+// instead of run_head + the device scan (2 kernels) + voxel_bounds: 4 launches -> 1.  The block covers the
+// sorted keys in kRunsTiles tiles of 4096 (16 B per lane per tile), all loads issued up front (one memory
+// round trip, not one per tile); each lane counts the run heads of its 4 keys per tile, a wave prefix sum
+// per tile from ballots (no shuffles) and the 16 wave totals per tile through LDS give every (tile, lane)
+// its first run index.
+// Publishes the count like voxel_bounds_kernel (hsm[0], the key-width flag) and stores it at *n_vox.
+constexpr int kRunsTiles = 8;
+constexpr int64_t kRunsOneBlock = 4096 * kRunsTiles;
+__global__ void __launch_bounds__(1024) voxel_runs_block_kernel(const uint32_t* __restrict__ keys, int64_t n,
+                                                                uint32_t* __restrict__ starts,
+                                                                uint32_t* __restrict__ ends,
+                                                                uint32_t* __restrict__ n_vox,
+                                                                uint32_t* __restrict__ flags, int* __restrict__ hsm) {
+    __shared__ uint32_t s_w[kRunsTiles][16];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint32_t k[kRunsTiles][4], prev[kRunsTiles], next[kRunsTiles];
+#pragma unroll
+    for (int t = 0; t < kRunsTiles; ++t) {
+        const int64_t j0 = 4096 * (int64_t)t + 4 * (int64_t)tid;
+        if (j0 + 3 < n) {
+            const uint4 v = *reinterpret_cast<const uint4*>(keys + j0);
+            k[t][0] = v.x, k[t][1] = v.y, k[t][2] = v.z, k[t][3] = v.w;
+        } else {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) k[t][u] = j0 + u < n ? keys[j0 + u] : kInvalid;
+        }
+        prev[t] = (j0 > 0 && j0 - 1 < n) ? keys[j0 - 1] : kInvalid;
+        next[t] = j0 + 4 < n ? keys[j0 + 4] : kInvalid;
+    }
+    uint32_t excl[kRunsTiles];
+#pragma unroll
+    for (int t = 0; t < kRunsTiles; ++t) {
+        const int64_t j0 = 4096 * (int64_t)t + 4 * (int64_t)tid;
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const uint32_t before = u == 0 ? prev[t] : k[t][u - 1];
+            cnt += (k[t][u] != kInvalid && (j0 + u == 0 || before != k[t][u])) ? 1u : 0u;
+        }
+        // wave exclusive prefix of cnt (0..4) from its three bit planes: a ballot and a masked popcount each
+        uint32_t ex = 0, wt = 0;
+#pragma unroll
+        for (int bit = 0; bit < 3; ++bit) {
+            const uint64_t m = __ballot((cnt >> bit) & 1u);
+            ex += (uint32_t)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u)) << bit;
+            wt += (uint32_t)__popcll(m) << bit;
+        }
+        if (lane == 0) s_w[t][w] = wt;
+        excl[t] = ex;
+    }
+    __syncthreads();
+    uint32_t run = 0;  // runs started before tile t
+#pragma unroll
+    for (int t = 0; t < kRunsTiles; ++t) {
+        const int64_t j0 = 4096 * (int64_t)t + 4 * (int64_t)tid;
+        uint32_t woff = 0, tot = 0;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const uint32_t x = s_w[t][i];
+            woff += i < w ? x : 0u;
+            tot += x;
+        }
+        uint32_t r = run + woff + excl[t];  // runs started before this lane's first key of the tile
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            if (k[t][u] == kInvalid) continue;
+            const uint32_t j = (uint32_t)(j0 + u);
+            const uint32_t before = u == 0 ? prev[t] : k[t][u - 1];
+            if (j == 0 || before != k[t][u]) starts[r++] = j;
+            const uint32_t after = u == 3 ? next[t] : k[t][u + 1];
+            if (after != k[t][u]) ends[r - 1] = j + 1;  // past the end reads kInvalid != any valid key
+        }
+        run += tot;
+    }
+    if (tid == 0) {
+        *n_vox = run;
+        hsm[0] = (int)run;
+        hsm[kHostFlags] = (int)flags[0];
+        flags[0] = 0u;
+    }
+}
+
+// LIO_VOX_RUNS=multi (A/B hook): the multi-kernel run bounds at every size
+bool runs_one_block(int64_t n) {
+    static const bool multi = [] {
+        const char* e = std::getenv("LIO_VOX_RUNS");
+        return e && std::strcmp(e, "multi") == 0;
+    }();
+    return !multi && n <= kRunsOneBlock;
+}
+
 constexpr int kLaneRun = 16;  // runs up to this length: one lane; longer: one wave (voxel_centroid_big_kernel,
                               // one wave per run; round 4 measured one wave per 64 consecutive voxels instead:
                               // 242 us per sweep, dense regions put ~10^4 points on one wave)
@@ -312,6 +405,79 @@ __global__ void __launch_bounds__(64) voxel_centroid_big_kernel(const float* __r
         if (xyz && lane < 3) xyz[3 * (size_t)v + lane] = acc / (float)(e - s);
         if (xyz && lane == 0) sel[v] = 0;
     }
+}
+
+// Every voxel on its own wave (4 per block, the grid striding the voxels): the wave loads up to 64 of the
+// run's points at once (index, then row: two dependent loads per chunk instead of one pair per point on
+// one lane; the next chunk's loads in flight while this one is summed), stashes them in its LDS slice,
+// and lane f adds field f over the chunk in input order — the same sums in the same order as
+// voxel_centroid_kernel / _big_kernel, without the long-run list.
+constexpr int kWaveCentroidBlocks = 1024;
+__global__ void __launch_bounds__(256) voxel_centroid_wave_kernel(const float* __restrict__ p, int stride,
+                                                                  const uint32_t* __restrict__ vals,
+                                                                  const uint32_t* __restrict__ starts,
+                                                                  const uint32_t* __restrict__ ends,
+                                                                  const uint32_t* __restrict__ n_vox,
+                                                                  float* __restrict__ out, float* __restrict__ xyz,
+                                                                  uint8_t* __restrict__ sel) {
+    __shared__ float s_q[4][64 * kMaxFields];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float* sq = s_q[wv];
+    const uint32_t nv = *n_vox;
+    for (uint32_t v = blockIdx.x * 4 + wv; v < nv; v += gridDim.x * 4) {
+        const uint32_t s = starts[v], e = ends[v];
+        float acc = 0.f;
+        float q[kMaxFields];
+        auto load = [&](uint32_t k) {  // chunk k's rows into registers (lanes past the run: nothing)
+            if (k + lane < e) {
+                const float* r = p + (size_t)vals[k + lane] * stride;
+#pragma unroll
+                for (int f = 0; f < kMaxFields; ++f) q[f] = f < stride ? r[f] : 0.f;
+            }
+        };
+        load(s);
+        for (uint32_t k = s; k < e; k += 64) {
+            const uint32_t m = min(64u, e - k);
+            if ((uint32_t)lane < m) {
+#pragma unroll
+                for (int f = 0; f < kMaxFields; ++f)
+                    if (f < stride) sq[lane * stride + f] = q[f];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (k + 64 < e) load(k + 64);  // the next chunk in flight while this one is summed
+            if (lane < stride) {
+                const float* col = sq + lane;
+                uint32_t l = 0;
+                for (; l + 4 <= m; l += 4) {
+                    const float a0 = col[(l + 0) * stride], a1 = col[(l + 1) * stride];
+                    const float a2 = col[(l + 2) * stride], a3 = col[(l + 3) * stride];
+                    acc += a0;
+                    acc += a1;
+                    acc += a2;
+                    acc += a3;
+                }
+                for (; l < m; ++l) acc += col[l * stride];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();  // the next chunk overwrites the slice
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+        const float c = (float)(e - s);
+        if (lane < stride) out[(size_t)v * stride + lane] = acc / c;
+        if (xyz && lane < 3) xyz[3 * (size_t)v + lane] = acc / c;
+        if (xyz && lane == 0) sel[v] = 0;
+    }
+}
+
+// LIO_CENTROID=lane (A/B hook): the lane-per-run kernel + the long-run wave kernel
+bool centroid_lane() {
+    static const bool on = [] {
+        const char* e = std::getenv("LIO_CENTROID");
+        return e && std::strcmp(e, "lane") == 0;
+    }();
+    return on;
 }
 
 __global__ void copy_strided_kernel(const float* __restrict__ a, int64_t nf, float* __restrict__ b) {
@@ -789,15 +955,26 @@ int voxel_grid_enqueue(FilterBuf& b, const float* d_in, int64_t n, const uint32_
                                               b.keys, b.vals, bits, b.cnt + 2, b.big + b.cap);
     int rc = sort_pairs(b, n, st, bits);
     if (rc) return rc;
-    run_head_kernel<<<nblk(n + 1), 256, 0, st>>>(b.keys_alt, n, b.head);
-    rc = exscan(b, b.head, b.vid, n + 1, st);
-    if (rc) return rc;
-    // runs -> [start, end) per voxel (b.keys / b.vals are free after the sort)
-    voxel_bounds_kernel<<<nblk(n), 256, 0, st>>>(b.keys_alt, n, b.head, b.vid, b.keys, b.vals, b.cnt + 2, b.d_small);
-    voxel_centroid_kernel<<<nblk(n), 256, 0, st>>>(d_in, stride, b.vals_alt, b.keys, b.vals, b.vid + n, b.big,
-                                                   b.big + b.cap, d_out, xyz, sel);
-    voxel_centroid_big_kernel<<<kBigBlocks, 64, 0, st>>>(d_in, stride, b.vals_alt, b.keys, b.vals, b.big,
-                                                         b.big + b.cap, d_out, xyz, sel);
+    // runs -> [start, end) per voxel (b.keys / b.vals are free after the sort); the count at b.vid[n]
+    if (runs_one_block(n)) {
+        voxel_runs_block_kernel<<<1, 1024, 0, st>>>(b.keys_alt, n, b.keys, b.vals, b.vid + n, b.cnt + 2, b.d_small);
+    } else {
+        run_head_kernel<<<nblk(n + 1), 256, 0, st>>>(b.keys_alt, n, b.head);
+        rc = exscan(b, b.head, b.vid, n + 1, st);
+        if (rc) return rc;
+        voxel_bounds_kernel<<<nblk(n), 256, 0, st>>>(b.keys_alt, n, b.head, b.vid, b.keys, b.vals, b.cnt + 2,
+                                                     b.d_small);
+    }
+    if (centroid_lane()) {
+        voxel_centroid_kernel<<<nblk(n), 256, 0, st>>>(d_in, stride, b.vals_alt, b.keys, b.vals, b.vid + n, b.big,
+                                                       b.big + b.cap, d_out, xyz, sel);
+        voxel_centroid_big_kernel<<<kBigBlocks, 64, 0, st>>>(d_in, stride, b.vals_alt, b.keys, b.vals, b.big,
+                                                             b.big + b.cap, d_out, xyz, sel);
+    } else {
+        const int nb = (int)std::min<int64_t>(kWaveCentroidBlocks, (n + 3) / 4);
+        voxel_centroid_wave_kernel<<<std::max(nb, 1), 256, 0, st>>>(d_in, stride, b.vals_alt, b.keys, b.vals,
+                                                                    b.vid + n, d_out, xyz, sel);
+    }
     FCHK(hipGetLastError());
     return 0;
 }
