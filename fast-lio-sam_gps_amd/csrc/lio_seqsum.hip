@@ -38,6 +38,17 @@ __device__ __forceinline__ int binade_pred(float f, int lg) {
     return binade_f(f);
 }
 
+// pass 1 also needs the prediction's absolute distance from the binade edges: the double prefix drifts from
+// the float chain by the chain's accumulated rounding, which near a zero crossing is large against |s| (C4
+// means chains: predictions of -0.98 with ~2.3 of drift).  delta bounds that drift (seq_scan1); an element whose
+// prediction lies within delta of an edge (or of zero) is ambiguous, i.e. an event.
+__device__ __forceinline__ int binade_pred_abs(float f, int lg, double delta) {
+    const int e = binade_pred(f, lg);
+    if (e == kSpecial) return e;
+    const double a = fabs((double)f), lo = ldexp(1.0, e);
+    return (a - lo < delta || 2.0 * lo - a < delta) ? kSpecial : e;
+}
+
 template <typename T>
 __device__ __forceinline__ T wave_incl(T v) {
     const int lane = threadIdx.x & 63;
@@ -142,15 +153,16 @@ __device__ __forceinline__ void predict(const Src& src, const SeqSumBuf& b, int 
         double D[kSeqPer], tot;
         block_dprefix(in.x, D, s_wd, tot);
         const double bo = b.boff[(size_t)c * b.nblk + blk];
+        const double dl = b.bdelta[(size_t)c * b.nblk + blk];
 #pragma unroll
-        for (int i = 0; i < kSeqPer; ++i) in.e[i] = binade_pred((float)(bo + D[i]), kPredSlack1);
+        for (int i = 0; i < kSeqPer; ++i) in.e[i] = binade_pred_abs((float)(bo + D[i]), kPredSlack1, dl);
         // predecessor of the thread's first element: the previous thread's last (block's first: boff)
         int prev = __shfl_up(in.e[kSeqPer - 1], 1, 64);
         __shared__ int s_last[kSeqThreads / 64];
         const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
         if (lane == 63) s_last[w] = in.e[kSeqPer - 1];
         __syncthreads();
-        if (lane == 0) prev = w > 0 ? s_last[w - 1] : binade_pred((float)bo, kPredSlack1);
+        if (lane == 0) prev = w > 0 ? s_last[w - 1] : binade_pred_abs((float)bo, kPredSlack1, dl);
         __syncthreads();
         in.ep = prev;
     } else {
@@ -207,12 +219,28 @@ __global__ void __launch_bounds__(kSeqThreads) seq_bsum(Src src, SeqSumBuf b, co
 // the block values go through LDS in windows (coalesced loads by all lanes), the dependent chain runs on lane 0
 constexpr int kScanWin = 2048;
 
+// The drift allowance: the float chain's rounding errors (at most half an ulp of |s| each) modelled as a random
+// walk, bounded per block by the block's largest |s| (|offset| + sum |x|): V += kSeqBlock (ulp / 2)^2,
+// delta = kDriftSigmas sqrt(V) through the block's end (non-decreasing, so conservative for every element of
+// the block).  Only a performance model: a drift past it fails verification and the chain takes a second pass.
+constexpr double kDriftSigmas = 2.0;
+
+// half an ulp of a float of magnitude v >= 0 (2^(ilogb(v) - 24); 0 for 0), from the exponent bits
+__device__ __forceinline__ double half_ulp_f32(double v) {
+    if (!(v > 0.0)) return 0.0;
+    const int64_t e = (int64_t)((__double_as_longlong(v) >> 52) & 0x7ff) - 1023;
+    if (e < -990) return 0.0;
+    return __longlong_as_double((long long)((uint64_t)(e - 24 + 1023) << 52));
+}
+
 __global__ void __launch_bounds__(256) seq_scan1(SeqSumBuf b, const uint32_t* d_n, int pass) {
-    __shared__ double s_sum[kScanWin], s_abs[kScanWin], s_off[kScanWin];
+    __shared__ double s_sum[kScanWin], s_abs[kScanWin], s_off[kScanWin], s_dl[kScanWin];
+    __shared__ double s_vw[256 / 64];
     const int c = blockIdx.x;
     const int64_t n = *d_n;
     const int nb = (int)((n + kSeqBlock - 1) / kSeqBlock);
     double off = 0.0, mb = 0.0;  // lane 0's running values
+    double var = 0.0;            // every thread's copy of the allowance's running variance
     for (int w0 = 0; w0 < nb; w0 += kScanWin) {
         const int m = min(kScanWin, nb - w0);
         for (int j = threadIdx.x; j < m; j += blockDim.x) {
@@ -227,7 +255,32 @@ __global__ void __launch_bounds__(256) seq_scan1(SeqSumBuf b, const uint32_t* d_
                 off = off + s_sum[j];
             }
         __syncthreads();
-        for (int j = threadIdx.x; j < m; j += blockDim.x) b.boff[(size_t)c * b.nblk + w0 + j] = s_off[j];
+        // the allowance off lane 0's chain: every thread its kScanWin / 256 consecutive blocks, one block prefix
+        {
+            constexpr int kPerT = kScanWin / 256;
+            double loc[kPerT], run = 0.0;
+#pragma unroll
+            for (int i = 0; i < kPerT; ++i) {
+                const int j = (int)threadIdx.x * kPerT + i;
+                const double big = j < m ? fabs(s_off[j]) + s_abs[j] : 0.0;
+                const double hu = half_ulp_f32(big);
+                run = run + (double)kSeqBlock * hu * hu;
+                loc[i] = run;
+            }
+            double tot;
+            const double ex = block_excl(run, s_vw, tot);  // fixed order: every thread sees the same total
+#pragma unroll
+            for (int i = 0; i < kPerT; ++i) {
+                const int j = (int)threadIdx.x * kPerT + i;
+                if (j < m) s_dl[j] = kDriftSigmas * sqrt(var + ex + loc[i]);
+            }
+            var = var + tot;
+        }
+        __syncthreads();
+        for (int j = threadIdx.x; j < m; j += blockDim.x) {
+            b.boff[(size_t)c * b.nblk + w0 + j] = s_off[j];
+            b.bdelta[(size_t)c * b.nblk + w0 + j] = s_dl[j];
+        }
         __syncthreads();
     }
     if (threadIdx.x == 0) {
@@ -548,7 +601,8 @@ int seqsum_reserve(SeqSumBuf& b, int nch, int64_t nmax, hipStream_t st) {
     b.evcap = b.evcap_alloc = nmax / 4 + 1024;  // events are ~0.3 % of a C4 chain; past a quarter the serial kernel is as fast
     const size_t nb = (size_t)nch * b.nblk;
     bool ok = hipMalloc(&b.bsum, nb * sizeof(double)) == hipSuccess && hipMalloc(&b.babs, nb * sizeof(double)) == hipSuccess &&
-              hipMalloc(&b.boff, nb * sizeof(double)) == hipSuccess && hipMalloc(&b.btot, nb * sizeof(uint64_t)) == hipSuccess &&
+              hipMalloc(&b.boff, nb * sizeof(double)) == hipSuccess && hipMalloc(&b.bdelta, nb * sizeof(double)) == hipSuccess &&
+              hipMalloc(&b.btot, nb * sizeof(uint64_t)) == hipSuccess &&
               hipMalloc(&b.bev, nb * sizeof(int)) == hipSuccess && hipMalloc(&b.bPoff, nb * sizeof(uint64_t)) == hipSuccess &&
               hipMalloc(&b.bEoff, nb * sizeof(int)) == hipSuccess && hipMalloc(&b.floor_e, 3 * nch * sizeof(int)) == hipSuccess &&
               hipMalloc(&b.ptot, nch * sizeof(uint64_t)) == hipSuccess &&
@@ -568,7 +622,7 @@ int seqsum_reserve(SeqSumBuf& b, int nch, int64_t nmax, hipStream_t st) {
 }
 
 void seqsum_free(SeqSumBuf& b) {
-    void* ptrs[] = {b.bsum, b.babs, b.boff, b.btot, b.bev, b.bPoff, b.bEoff, b.floor_e, b.ptot, b.ev_pos,
+    void* ptrs[] = {b.bsum, b.babs, b.boff, b.bdelta, b.btot, b.bev, b.bPoff, b.bEoff, b.floor_e, b.ptot, b.ev_pos,
                     b.ev_P, b.ev_x, b.ev_s, b.recon, b.forced, b.status, b.result};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);

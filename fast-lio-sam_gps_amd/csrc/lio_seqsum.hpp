@@ -39,6 +39,7 @@ struct SeqSumBuf {
     double* bsum = nullptr;     // [nch][nblk] double block sums (prediction)
     double* babs = nullptr;     // [nch][nblk] sum |x| (bound on |s|)
     double* boff = nullptr;     // [nch][nblk] exclusive prefix of bsum
+    double* bdelta = nullptr;   // [nch][nblk] drift allowance of the pass-1 prediction through the block's end
     uint64_t* btot = nullptr;   // [nch][nblk] block increment totals (fixed point, wrapping)
     int* bev = nullptr;         // [nch][nblk] block event counts
     uint64_t* bPoff = nullptr;  // [nch][nblk] exclusive prefix of btot
