@@ -62,9 +62,8 @@ for s in $STEPS; do
            run prep_time 300 bash -c 'python scripts/prep_timing.py 80 && LIO_PREP_UPLOAD=full python scripts/prep_timing.py 80' &&
            run prep_profile 300 bash -c "LIO_PREP_PROFILE=1 python scripts/prep_timing.py 60 2> $OUT/prep_profile.err && python scripts/prep_profile_summary.py $OUT/prep_profile.err" &&
            run rocprof_prep 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof_prep" -o run --output-format csv -- python scripts/prep_timing.py 40 ;;
-    sortab) LIO_CENTROID=lane LIO_VOX_RUNS=multi runs pytest_prep_old 600 python -u -m pytest tests/test_gpu_filters.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread &&
-           runs pytest_prep_new 600 python -u -m pytest tests/test_gpu_filters.py tests/test_gpu_pipeline.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread &&
-           run prep_ab 500 bash -c 'for r in 1 2 3; do echo "default"; python scripts/prep_timing.py 80 || exit $?; echo "centroid=lane runs=multi"; LIO_CENTROID=lane LIO_VOX_RUNS=multi python scripts/prep_timing.py 80 || exit $?; done' &&
+    sortab) runs pytest_prep_new 600 python -u -m pytest tests/test_gpu_filters.py tests/test_gpu_pipeline.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread &&
+           run prep_ab 500 bash -c 'for r in 1 2 3; do python scripts/prep_timing.py 80 || exit $?; done' &&
            run prep_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prep_prof" -o run --output-format csv -- python scripts/prep_timing.py 40 ;;
     c5prep) run c5_prep_profile 400 bash -c "LIO_PREP_PROFILE=1 python bench.py --config C5 --steps 20 --warmup 2 --no-icp --cpu-scans 2 --cpu-warmup 1 --pipeline 12 --streams '' > $OUT/c5prep.log 2> $OUT/c5prep.err && python scripts/prep_profile_summary.py $OUT/c5prep.err" ;;
     fidprof) run fid_prof 300 env LIO_ICP_ORDER=2 rocprofv3 --kernel-trace --stats -d "$OUT/fidprof" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 ;;
