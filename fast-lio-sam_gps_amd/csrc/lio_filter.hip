@@ -98,8 +98,6 @@ __global__ void __launch_bounds__(256) minmax_partial_kernel(const float* __rest
     if (threadIdx.x < 6) part[blockIdx.x * 6 + threadIdx.x] = s[threadIdx.x][0];
 }
 
-// keys past `bits` bits (the width the sort will use) raise flags[0]; i == 0 also clears the long-run
-// count of the centroid pass
 // minmax_partial_kernel over the first *cnt of n rows
 __global__ void __launch_bounds__(256) minmax_partial_cnt_kernel(const float* __restrict__ p, int64_t n,
                                                                  const uint32_t* __restrict__ cnt, int stride,
@@ -124,13 +122,13 @@ __global__ void __launch_bounds__(256) minmax_partial_cnt_kernel(const float* __
 
 // Every block first reduces the nbp AABB partials (a few KB from L2) and derives the voxel geometry itself
 // — no single-block hand-off kernel between the AABB and the keys; block 0 also stores the geometry for
-// the host (host-mapped gh).
+// the host (host-mapped gh).  Keys past `bits` bits (the width the sort will use) raise flags[0].
 __global__ void __launch_bounds__(256) voxel_key_kernel(const float* __restrict__ p, int64_t n,
                                                         const uint32_t* __restrict__ cnt, int stride,
                                                         const float* __restrict__ part, int nbp, float lx, float ly,
                                                         float lz, VoxelGeom* __restrict__ gh, uint32_t* __restrict__ keys,
                                                         uint32_t* __restrict__ vals, int bits,
-                                                        uint32_t* __restrict__ flags, uint32_t* __restrict__ n_big) {
+                                                        uint32_t* __restrict__ flags) {
     __shared__ float s[6][256];
     __shared__ VoxelGeom s_g;
     {
@@ -151,7 +149,6 @@ __global__ void __launch_bounds__(256) voxel_key_kernel(const float* __restrict_
         __syncthreads();
     }
     const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-    if (i == 0) *n_big = 0u;
     if (i >= n) return;
     const VoxelGeom g = s_g;
     const float* q = p + (size_t)i * stride;
@@ -278,140 +275,16 @@ __global__ void __launch_bounds__(1024) voxel_runs_block_kernel(const uint32_t* 
     }
 }
 
-// LIO_VOX_RUNS=multi (A/B hook): the multi-kernel run bounds at every size
-bool runs_one_block(int64_t n) {
-    static const bool multi = [] {
-        const char* e = std::getenv("LIO_VOX_RUNS");
-        return e && std::strcmp(e, "multi") == 0;
-    }();
-    return !multi && n <= kRunsOneBlock;
-}
-
-constexpr int kLaneRun = 16;  // runs up to this length: one lane; longer: one wave (voxel_centroid_big_kernel,
-                              // one wave per run; round 4 measured one wave per 64 consecutive voxels instead:
-                              // 242 us per sweep, dense regions put ~10^4 points on one wave)
-constexpr int kBigBlocks = 1024;  // waves striding the long-run list
-
-template <int NF>
-__device__ __forceinline__ void write_centroid(float* __restrict__ o, const float* acc, int stride, uint32_t cnt) {
-    const float c = (float)cnt;
-#pragma unroll
-    for (int f = 0; f < NF; ++f)
-        if (f < stride) o[f] = acc[f] / c;
-}
-
-// PCL VoxelGrid centroid: the voxel's fields summed one point at a time in
-// input order (float), divided by the count.  The chain of adds is serial, the
-// loads are not: short runs are summed by one lane with its loads issued four
-// points ahead; long runs (the dense ground next to the sensor) go to a wave.
-__global__ void voxel_centroid_kernel(const float* __restrict__ p, int stride, const uint32_t* __restrict__ vals,
-                                      const uint32_t* __restrict__ starts, const uint32_t* __restrict__ ends,
-                                      const uint32_t* __restrict__ n_vox, uint32_t* __restrict__ big,
-                                      uint32_t* __restrict__ n_big, float* __restrict__ out, float* __restrict__ xyz,
-                                      uint8_t* __restrict__ sel) {
-    const uint32_t v = blockIdx.x * blockDim.x + threadIdx.x;
-    if (v >= *n_vox) return;
-    const uint32_t s = starts[v], e = ends[v];
-    if (e - s > (uint32_t)kLaneRun) {
-        big[atomicAdd(n_big, 1u)] = v;
-        return;
-    }
-    float acc[kMaxFields];
-#pragma unroll
-    for (int f = 0; f < kMaxFields; ++f) acc[f] = 0.f;
-    for (uint32_t k = s; k < e; k += 4) {
-        float q[4][kMaxFields];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const float* r = p + (size_t)vals[k + u < e ? k + u : s] * stride;
-#pragma unroll
-            for (int f = 0; f < kMaxFields; ++f) q[u][f] = f < stride ? r[f] : 0.f;
-        }
-#pragma unroll
-        for (int u = 0; u < 4; ++u)
-            if (k + u < e) {
-#pragma unroll
-                for (int f = 0; f < kMaxFields; ++f) acc[f] += q[u][f];
-            }
-    }
-    write_centroid<kMaxFields>(out + (size_t)v * stride, acc, stride, e - s);
-    if (xyz) {  // the scan the output becomes: packed xyz and cleared selection flags, same values
-        const float c = (float)(e - s);
-        xyz[3 * (size_t)v] = acc[0] / c;
-        xyz[3 * (size_t)v + 1] = acc[1] / c;
-        xyz[3 * (size_t)v + 2] = acc[2] / c;
-        sel[v] = 0;
-    }
-}
-
-// long runs, one wave (= block) each: the lanes load 64 points at a time into
-// LDS (the next chunk's loads in flight while this one is summed); lane f
-// then adds field f of the 64 points in order — one LDS read + one add per
-// point, the fields in parallel
-__global__ void __launch_bounds__(64) voxel_centroid_big_kernel(const float* __restrict__ p, int stride,
-                                                                 const uint32_t* __restrict__ vals,
-                                                                 const uint32_t* __restrict__ starts,
-                                                                 const uint32_t* __restrict__ ends,
-                                                                 const uint32_t* __restrict__ big,
-                                                                 const uint32_t* __restrict__ n_big,
-                                                                 float* __restrict__ out, float* __restrict__ xyz,
-                                                                 uint8_t* __restrict__ sel) {
-    __shared__ float s_q[2][64 * kMaxFields];
-    const int lane = threadIdx.x;
-    const uint32_t nb = *n_big;
-    for (uint32_t b = blockIdx.x; b < nb; b += gridDim.x) {
-        const uint32_t v = big[b];
-        const uint32_t s = starts[v], e = ends[v];
-        float q[kMaxFields];
-        auto load = [&](uint32_t k) {
-            const float* r = p + (size_t)vals[k + lane < e ? k + lane : s] * stride;
-#pragma unroll
-            for (int f = 0; f < kMaxFields; ++f) q[f] = f < stride ? r[f] : 0.f;
-        };
-        auto stash = [&](int buf) {
-#pragma unroll
-            for (int f = 0; f < kMaxFields; ++f)
-                if (f < stride) s_q[buf][lane * stride + f] = q[f];
-        };
-        float acc = 0.f;
-        load(s);
-        stash(0);
-        __syncthreads();
-        int buf = 0;
-        for (uint32_t k = s; k < e; k += 64) {
-            const bool more = k + 64 < e;
-            if (more) load(k + 64);
-            const uint32_t m = min(64u, e - k);
-            if (lane < stride) {
-                const float* col = s_q[buf] + lane;
-                uint32_t l = 0;
-                for (; l + 4 <= m; l += 4) {
-                    const float a0 = col[(l + 0) * stride], a1 = col[(l + 1) * stride];
-                    const float a2 = col[(l + 2) * stride], a3 = col[(l + 3) * stride];
-                    acc += a0;
-                    acc += a1;
-                    acc += a2;
-                    acc += a3;
-                }
-                for (; l < m; ++l) acc += col[l * stride];
-            }
-            if (more) {
-                stash(buf ^ 1);
-                buf ^= 1;
-            }
-            __syncthreads();
-        }
-        if (lane < stride) out[(size_t)v * stride + lane] = acc / (float)(e - s);
-        if (xyz && lane < 3) xyz[3 * (size_t)v + lane] = acc / (float)(e - s);
-        if (xyz && lane == 0) sel[v] = 0;
-    }
-}
+// the one-block run bounds up to kRunsOneBlock keys (the C5 sweep); larger inputs (map build, submaps) use
+// run_head + the device scan + voxel_bounds
+inline bool runs_one_block(int64_t n) { return n <= kRunsOneBlock; }
 
 // Every voxel on its own wave (4 per block, the grid striding the voxels): the wave loads up to 64 of the
 // run's points at once (index, then row: two dependent loads per chunk instead of one pair per point on
 // one lane; the next chunk's loads in flight while this one is summed), stashes them in its LDS slice,
 // and lane f adds field f over the chunk in input order — the same sums in the same order as
-// voxel_centroid_kernel / _big_kernel, without the long-run list.
+// round 4's lane-per-short-run + wave-per-long-run pair (20.6 vs 9.1 µs at C5), without its
+// long-run list.
 constexpr int kWaveCentroidBlocks = 1024;
 __global__ void __launch_bounds__(256) voxel_centroid_wave_kernel(const float* __restrict__ p, int stride,
                                                                   const uint32_t* __restrict__ vals,
@@ -469,15 +342,6 @@ __global__ void __launch_bounds__(256) voxel_centroid_wave_kernel(const float* _
         if (xyz && lane < 3) xyz[3 * (size_t)v + lane] = acc / c;
         if (xyz && lane == 0) sel[v] = 0;
     }
-}
-
-// LIO_CENTROID=lane (A/B hook): the lane-per-run kernel + the long-run wave kernel
-bool centroid_lane() {
-    static const bool on = [] {
-        const char* e = std::getenv("LIO_CENTROID");
-        return e && std::strcmp(e, "lane") == 0;
-    }();
-    return on;
 }
 
 __global__ void copy_strided_kernel(const float* __restrict__ a, int64_t nf, float* __restrict__ b) {
@@ -762,7 +626,7 @@ int ftmp(FilterBuf& b, size_t need) {  // grown geometrically (1 MiB floor): no 
 int reserve(FilterBuf& b, int64_t n) {
     if (n <= b.cap && b.keys) return 0;
     const int64_t c = std::max<int64_t>(n, b.cap + b.cap / 2);
-    void* bufs[] = {b.keys, b.keys_alt, b.vals, b.vals_alt, b.head, b.vid, b.big};
+    void* bufs[] = {b.keys, b.keys_alt, b.vals, b.vals_alt, b.head, b.vid};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
     FCHK(hipMalloc(&b.keys, c * sizeof(uint32_t)));
@@ -771,7 +635,6 @@ int reserve(FilterBuf& b, int64_t n) {
     FCHK(hipMalloc(&b.vals_alt, c * sizeof(uint32_t)));
     FCHK(hipMalloc(&b.head, (c + 1) * sizeof(uint32_t)));
     FCHK(hipMalloc(&b.vid, (c + 1) * sizeof(uint32_t)));
-    FCHK(hipMalloc(&b.big, (c + 1) * sizeof(uint32_t)));  // long-run list + its count at [c]
     b.cap = c;
     if (!b.part) FCHK(hipMalloc(&b.part, 6 * kPartBlocks * sizeof(float)));
     if (!b.geom) FCHK(hipMalloc(&b.geom, sizeof(VoxelGeom)));
@@ -926,7 +789,7 @@ int records_to_xyz(const float* d_rec, int64_t n, int stride, float* d_xyz, hipS
 }
 
 void filter_free(FilterBuf& b) {
-    void* bufs[] = {b.keys, b.keys_alt, b.vals, b.vals_alt, b.head, b.vid, b.big,
+    void* bufs[] = {b.keys, b.keys_alt, b.vals, b.vals_alt, b.head, b.vid,
                     b.part, b.geom,     b.tmp,  b.a,    b.c,        b.aux,  b.cnt};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
@@ -952,7 +815,7 @@ int voxel_grid_enqueue(FilterBuf& b, const float* d_in, int64_t n, const uint32_
     }
     const int bits = std::min(std::max(b.vox_bits, 1), 32);
     voxel_key_kernel<<<nblk(n), 256, 0, st>>>(d_in, n, cnt, stride, b.part, nbp, leaf[0], leaf[1], leaf[2], hgeom,
-                                              b.keys, b.vals, bits, b.cnt + 2, b.big + b.cap);
+                                              b.keys, b.vals, bits, b.cnt + 2);
     int rc = sort_pairs(b, n, st, bits);
     if (rc) return rc;
     // runs -> [start, end) per voxel (b.keys / b.vals are free after the sort); the count at b.vid[n]
@@ -965,16 +828,9 @@ int voxel_grid_enqueue(FilterBuf& b, const float* d_in, int64_t n, const uint32_
         voxel_bounds_kernel<<<nblk(n), 256, 0, st>>>(b.keys_alt, n, b.head, b.vid, b.keys, b.vals, b.cnt + 2,
                                                      b.d_small);
     }
-    if (centroid_lane()) {
-        voxel_centroid_kernel<<<nblk(n), 256, 0, st>>>(d_in, stride, b.vals_alt, b.keys, b.vals, b.vid + n, b.big,
-                                                       b.big + b.cap, d_out, xyz, sel);
-        voxel_centroid_big_kernel<<<kBigBlocks, 64, 0, st>>>(d_in, stride, b.vals_alt, b.keys, b.vals, b.big,
-                                                             b.big + b.cap, d_out, xyz, sel);
-    } else {
-        const int nb = (int)std::min<int64_t>(kWaveCentroidBlocks, (n + 3) / 4);
-        voxel_centroid_wave_kernel<<<std::max(nb, 1), 256, 0, st>>>(d_in, stride, b.vals_alt, b.keys, b.vals,
-                                                                    b.vid + n, d_out, xyz, sel);
-    }
+    const int nbw = (int)std::min<int64_t>(kWaveCentroidBlocks, (n + 3) / 4);
+    voxel_centroid_wave_kernel<<<std::max(nbw, 1), 256, 0, st>>>(d_in, stride, b.vals_alt, b.keys, b.vals, b.vid + n,
+                                                                 d_out, xyz, sel);
     FCHK(hipGetLastError());
     return 0;
 }

@@ -54,7 +54,6 @@ struct ScanPrepParams {
 struct FilterBuf {
     uint32_t *keys = nullptr, *keys_alt = nullptr, *vals = nullptr, *vals_alt = nullptr;
     uint32_t *head = nullptr, *vid = nullptr;
-    uint32_t* big = nullptr;  // voxels with long runs (cap entries + count)
     int64_t cap = 0;
     float* part = nullptr;
     VoxelGeom* geom = nullptr;

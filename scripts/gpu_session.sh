@@ -65,6 +65,8 @@ for s in $STEPS; do
     sortab) runs pytest_prep_new 600 python -u -m pytest tests/test_gpu_filters.py tests/test_gpu_pipeline.py -x -q -p no:cacheprovider --timeout 300 --timeout-method thread &&
            run prep_ab 500 bash -c 'for r in 1 2 3; do python scripts/prep_timing.py 80 || exit $?; done' &&
            run prep_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/prep_prof" -o run --output-format csv -- python scripts/prep_timing.py 40 ;;
+    setupfid) run icp_setup_fid 300 env LIO_ICP_ORDER=2 python scripts/icp_setup_timing.py &&
+           run icp_setup_fid_b 300 env LIO_ICP_ORDER=2 python scripts/icp_setup_timing.py ;;
     c5prep) run c5_prep_profile 400 bash -c "LIO_PREP_PROFILE=1 python bench.py --config C5 --steps 20 --warmup 2 --no-icp --cpu-scans 2 --cpu-warmup 1 --pipeline 12 --streams '' > $OUT/c5prep.log 2> $OUT/c5prep.err && python scripts/prep_profile_summary.py $OUT/c5prep.err" ;;
     fidprof) run fid_prof 300 env LIO_ICP_ORDER=2 rocprofv3 --kernel-trace --stats -d "$OUT/fidprof" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 ;;
     maprec) runs pytest_maprec 600 python -u -m pytest tests/test_gpu_map.py tests/test_gpu_pipeline.py -x -v -p no:cacheprovider --timeout 500 --timeout-method thread ;;
