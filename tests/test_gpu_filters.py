@@ -39,6 +39,21 @@ def test_voxel_grid_bit_exact(oracle):
     np.testing.assert_array_equal(vg.filter(big), big)
 
 
+@pytest.mark.parametrize("n", [1, 2, 1023, 4096, 4097, 32767, 32768, 32769, 40000])
+def test_voxel_grid_sizes_around_one_block_runs(oracle, n):
+    """The run bounds of <= 32768 sorted keys come from one block (voxel_runs_block_kernel: 8 tiles of 4096,
+    loads up front, ballot prefix), larger inputs from run_head + the device scan + voxel_bounds; both feed
+    the one-wave-per-voxel centroids.  Bit-exact on either side of the switch, with long runs (> 64 points
+    per voxel: chunked sums) and NaN rows mixed in."""
+    rng = np.random.default_rng(n)
+    pts = rng.uniform(-20, 20, (n, 4)).astype(f32)
+    k = max(n // 200, 1)
+    pts[: 100 * k] = (rng.normal(0, 0.02, (min(100 * k, n), 4)) + np.repeat(rng.uniform(-5, 5, (k, 4)), 100, axis=0)[: min(100 * k, n)]).astype(f32)
+    pts[1::997, 1] = np.nan
+    vg = FL.VoxelGrid(0.5)
+    np.testing.assert_array_equal(vg.filter(pts), oracle.voxel_grid(pts, 0.5))
+
+
 def test_submap_voxelize_bit_exact(oracle):
     scene, m, scans = synth.make_config("C1", n_scans=6)
     rng = np.random.default_rng(5)
