@@ -23,6 +23,10 @@
 
 namespace lio {
 
+struct IcpT {  // a float 4x4 (row-major) by value in kernel arguments
+    float m[16];
+};
+
 // PCL 1.10 Transformer<float>::se3 (SSE): x' = m0*x + (m1*y + (m2*z + m3)) [U]
 __device__ __forceinline__ void xform_pcl(const float* T, float x, float y, float z, float& ox, float& oy,
                                           float& oz) {
@@ -536,6 +540,13 @@ __global__ void __launch_bounds__(kIcpStatsThreads) icp_stats_kernel(IcpArgs a, 
         ids[k] = i < a.n ? a.nn_id[i] : -1;
         d2s[k] = i < a.n ? a.nn_d2[i] : 0.f;
     }
+    if (a.aid && !a.fitness) {  // sharded PCL float modes: the accepted ids ride the all-gather (coalesced)
+#pragma unroll
+        for (int k = 0; k < PER; ++k) {
+            const int i = base + k * kIcpStatsThreads, id = ids[k];
+            if (i < a.n) a.aid[i] = (id >= 0 && id != kNone && !((double)d2s[k] > a.max_d2)) ? id : -1;
+        }
+    }
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
         const int i = base + k * kIcpStatsThreads, id = ids[k];
@@ -684,8 +695,9 @@ int icp_build_tiles(const GridBuf& q, uint2* tiles, uint32_t* scratch, void*& tm
 //   sigma    = one_over_n * dst_demean * src_demean^T  (the depth sum sequential)
 // A float sum's value depends on its order, so each of the 6 + 9 chains runs on ONE
 // lane, in order; the block stages the correspondences through LDS around it.
-// Single rank only (the chains cannot be split).  icp_pcl_means_kernel also writes the
-// compacted pairs (src xyz, tgt xyz) for icp_pcl_sigma_kernel.
+// The serial fallback of the parallel seqsum path (lio_seqsum.hip); sharded, it runs over the whole
+// source with the all-gathered ids.  icp_pcl_means_kernel also writes the compacted pairs (src xyz,
+// tgt xyz) for icp_pcl_sigma_kernel.
 // ----------------------------------------------------------------------------
 constexpr int kPclThreads = 1024;  // one block: a chunk of 1024 correspondences per round
 
@@ -739,7 +751,7 @@ __global__ void __launch_bounds__(kPclThreads) icp_pcl_means_kernel(IcpArgs a, f
         float v[6];
         if (i < a.n) {
             const int id = a.nn_id[i];
-            const float d2 = a.nn_d2[i];
+            const float d2 = a.nn_d2 ? a.nn_d2[i] : 0.f;  // no d2: the ids were gated already (-1 = rejected)
             ok = id >= 0 && id != kNone && !((double)d2 > a.max_d2);
             if (ok) {
                 const float4 q = a.tgt_by_id[id];
@@ -819,19 +831,61 @@ void launch_icp_pcl_means_serial(const IcpArgs& a, float* pairs, float* out16, h
 }
 
 __global__ void __launch_bounds__(64) icp_combine_kernel(const double* __restrict__ recv, int64_t nsup, int world,
-                                                        int64_t slot, double* __restrict__ out17) {
+                                                        int64_t rank_stride, double* __restrict__ out17) {
     const int k = threadIdx.x;
     if (k >= 17) return;
     double acc = 0.0;
     for (int r = 0; r < world; ++r) {
         const int64_t s0 = nsup * r / world, s1 = nsup * (r + 1) / world;
-        for (int64_t s = s0; s < s1; ++s) acc += recv[((size_t)r * slot + (size_t)(s - s0)) * kIcpStride + k];
+        for (int64_t s = s0; s < s1; ++s) acc += recv[(size_t)r * rank_stride + (size_t)(s - s0) * kIcpStride + k];
     }
     out17[k] = acc;
 }
 
-void launch_icp_combine(const double* recv, int64_t nsup, int world, int64_t slot, double* out17, hipStream_t st) {
-    icp_combine_kernel<<<1, 64, 0, st>>>(recv, nsup, world, slot, out17);
+void launch_icp_combine(const double* recv, int64_t nsup, int world, int64_t rank_stride, double* out17, hipStream_t st) {
+    icp_combine_kernel<<<1, 64, 0, st>>>(recv, nsup, world, rank_stride, out17);
+}
+
+// the rest of the whole source through T (the shard's points are transformed by icp_tile_kernel)
+__global__ void __launch_bounds__(256) icp_xform_rest_kernel(float* __restrict__ cur, int64_t ns, int64_t b, int64_t n,
+                                                             IcpT T) {
+    const int64_t rest = ns - n;
+    for (int64_t j = blockIdx.x * 256 + threadIdx.x; j < rest; j += (int64_t)gridDim.x * 256) {
+        const int64_t i = j < b ? j : j + n;
+        float x, y, z;
+        xform_pcl(T.m, cur[3 * i], cur[3 * i + 1], cur[3 * i + 2], x, y, z);
+        cur[3 * i] = x;
+        cur[3 * i + 1] = y;
+        cur[3 * i + 2] = z;
+    }
+}
+
+void launch_icp_xform_rest(float* cur, int64_t ns, int64_t b, int64_t n, const float* T16, hipStream_t st) {
+    if (ns - n <= 0) return;
+    IcpT T;
+    for (int k = 0; k < 16; ++k) T.m[k] = T16[k];
+    const int64_t nb = std::min<int64_t>((ns - n + 255) / 256, 4096);
+    icp_xform_rest_kernel<<<(int)nb, 256, 0, st>>>(cur, ns, b, n, T);
+}
+
+// blockIdx.y = rank r: its shard [b_r, b_r + n_r) of the source, ids at recv + r * rank_stride + id_off
+__global__ void __launch_bounds__(256) icp_gather_ids_kernel(const double* __restrict__ recv, int world,
+                                                             int64_t rank_stride, int64_t id_off, int64_t ns,
+                                                             int* __restrict__ gid) {
+    const int r = blockIdx.y;
+    const int64_t nsup = (ns + kIcpSuper - 1) / kIcpSuper;
+    const int64_t b0 = nsup * r / world * kIcpSuper, e0 = nsup * (r + 1) / world * kIcpSuper;
+    const int64_t b = b0 < ns ? b0 : ns, e = e0 < ns ? e0 : ns;
+    const int* ids = reinterpret_cast<const int*>(recv + (size_t)r * rank_stride + id_off);
+    for (int64_t j = blockIdx.x * 256 + threadIdx.x; j < e - b; j += (int64_t)gridDim.x * 256) gid[b + j] = ids[j];
+}
+
+void launch_icp_gather_ids(const double* recv, int world, int64_t rank_stride, int64_t id_off, int64_t ns, int* gid,
+                           hipStream_t st) {
+    if (ns <= 0) return;
+    const int64_t per = (ns + world - 1) / world;
+    const int64_t nb = std::max<int64_t>(std::min<int64_t>((per + 255) / 256, 1024), 1);
+    icp_gather_ids_kernel<<<dim3((unsigned)nb, (unsigned)world), 256, 0, st>>>(recv, world, rank_stride, id_off, ns, gid);
 }
 
 void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st, uint32_t* order, int ntiles) {

@@ -333,6 +333,13 @@ struct lio_icp {
     float* h_pclout = nullptr; // pinned copy
     void* x_owner = nullptr;   // exchange state owned by the handle (lio_icp_mp.cpp: shm segment, RCCL comm)
     void (*x_owner_free)(void*) = nullptr;
+    // sharded PCL float modes (fid_sharded): the whole source on every rank — the original and the
+    // incrementally transformed cloud (this rank's shard is the slice [sh_begin, sh_begin + sh_n) of it,
+    // the tile kernel transforms that slice, icp_xform_rest the rest) — and the all-gathered accepted ids
+    float* d_srcf = nullptr;
+    float* d_curf = nullptr;
+    int* d_gid = nullptr;
+    int64_t full_cap = 0;
     int64_t fid_stats[4] = {0, 0, 0, 0};  // re-passes, serial fallbacks, events of the last pass, passes
     int fid_flags = 0;
     int64_t fid_evcap = 0;
@@ -358,6 +365,11 @@ static void icp_join_src(lio_icp* h) {
     if (h->bg_src.joinable()) h->bg_src.join();
 }
 
+// the PCL float modes with more than one rank: the float chains need every rank's correspondences
+static bool fid_sharded(const lio_icp* h) { return h->p.umeyama_float > 0 && h->world > 1; }
+// the incrementally transformed cloud of this rank's shard
+static float* shard_cur(const lio_icp* h) { return fid_sharded(h) ? h->d_curf + 3 * h->sh_begin : h->d_cur; }
+
 static int icp_check_dev(int dev) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ifail(LIO_ERR_NODEV, "no HIP device (no CPU path)");
@@ -380,12 +392,18 @@ extern "C" {
 int lio_icp_create(const lio_icp_params* p, lio_icp** out) {
     if (!p || !out) return ifail(LIO_ERR_ARG, "bad arguments");
     *out = nullptr;
+    if (p->umeyama_float < LIO_ICP_UMEYAMA_DOUBLE || p->umeyama_float > LIO_ICP_UMEYAMA_PCL_GEMM48)
+        return ifail(LIO_ERR_ARG, "lio_icp_create: umeyama_float must be -1 (double statistics), 0 (default) or 1..3");
     int rc = icp_check_dev(p->device);
     if (rc) return rc;
     IHIP(hipSetDevice(p->device));
     auto* h = new lio_icp();
     h->dev = p->device;
     h->p = *p;
+    // the default is the reference's float arithmetic (Eigen 3.3 GEMM order, loop_closure.h:42); the double
+    // statistics are an explicit opt-in (-1), stored as 0 from here on
+    if (h->p.umeyama_float == LIO_ICP_UMEYAMA_DEFAULT) h->p.umeyama_float = LIO_ICP_UMEYAMA_PCL_GEMM32;
+    else if (h->p.umeyama_float == LIO_ICP_UMEYAMA_DOUBLE) h->p.umeyama_float = 0;
     if (!(h->p.cell_size > 0.f)) h->p.cell_size = 1.0f;  // 0.3 m voxelised submaps: 1 m target cells (scripts/icp_cells.py)
     if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&h->st2, hipStreamNonBlocking) != hipSuccess) {
@@ -424,8 +442,9 @@ int lio_icp_destroy(lio_icp* h) {
     lio_icp_set_exchange_owner(h, nullptr, nullptr);
     lio::grid_free(h->tgt);
     lio::grid_free(h->qgrid);
-    void* ptrs[] = {h->d_tgt,   h->d_src,     h->d_cur,  h->d_fd2,   h->d_fid,   h->d_tiles, h->d_tscratch,
-                    h->d_ttmp,  h->d_dbg,     h->d_tcost, h->d_order, h->d_pcl16};
+    void* ptrs[] = {h->d_tgt,  h->d_src,   h->d_cur,    h->d_fd2,   h->d_fid,  h->d_tiles, h->d_tscratch,
+                    h->d_ttmp, h->d_dbg,   h->d_tcost,  h->d_order, h->d_pcl16, h->d_srcf,  h->d_curf,
+                    h->d_gid};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (h->h_super) (void)hipHostFree(h->h_super);
@@ -563,9 +582,32 @@ int lio_icp_set_shard_device(lio_icp* h, int rank, int world, lio_allgather_dev_
     return LIO_OK;
 }
 
-static int64_t exchange_len(int64_t ns, int world) {
+// Exchange message of one rank, in doubles: its records (slot = ceil(records / world) of kIcpStride), then
+// in the PCL float modes its accepted 1-NN ids (int32, slot * kIcpSuper of them).  exchange_len is the
+// capacity; a pass sends exchange_count (records only unless `ids`).
+static int64_t exchange_slot(int64_t ns, int world) {
     const int64_t nsup = (ns + lio::kIcpSuper - 1) / lio::kIcpSuper;
-    return ((nsup + world - 1) / world) * lio::kIcpStride;
+    return (nsup + world - 1) / world;
+}
+static int64_t exchange_len(int64_t ns, int world) {
+    return exchange_slot(ns, world) * (lio::kIcpStride + lio::kIcpSuper / 2);
+}
+static int64_t exchange_count(int64_t ns, int world, bool ids) {
+    return exchange_slot(ns, world) * (ids ? lio::kIcpStride + lio::kIcpSuper / 2 : lio::kIcpStride);
+}
+static int64_t exchange_id_off(int64_t ns, int world) { return exchange_slot(ns, world) * lio::kIcpStride; }
+
+// the records of every rank (rank r at recv + r * stride doubles) summed in global record order
+static void combine_records(const double* recv, int64_t ns, int world, int64_t stride, double out17[17]) {
+    const int64_t nsup = (ns + lio::kIcpSuper - 1) / lio::kIcpSuper;
+    for (int k = 0; k < 17; ++k) out17[k] = 0.0;
+    for (int r = 0; r < world; ++r) {
+        const int64_t s0 = nsup * r / world, s1 = nsup * (r + 1) / world;
+        for (int64_t s = s0; s < s1; ++s) {
+            const double* rec = &recv[(size_t)r * (size_t)stride + (size_t)(s - s0) * lio::kIcpStride];
+            for (int k = 0; k < 17; ++k) out17[k] += rec[k];
+        }
+    }
 }
 
 int lio_icp_exchange_len(int64_t n_source, int world, int64_t* n_per_rank) {
@@ -647,6 +689,22 @@ static int icp_prepare(lio_icp* h) {
     }
     h->ntiles = 0;
     h->have_order = false;  // new tiles: cell order until a pass has measured them
+    if (fid_sharded(h)) {  // the whole source on every rank (the float chains run over all of it)
+        const int64_t nf = std::max<int64_t>(h->ns, 1);
+        if (nf > h->full_cap) {
+            for (void** q : {(void**)&h->d_srcf, (void**)&h->d_curf, (void**)&h->d_gid}) {
+                if (*q) (void)hipFree(*q);
+                *q = nullptr;
+            }
+            h->full_cap = 0;
+            IHIP(hipMalloc(&h->d_srcf, nf * 3 * sizeof(float)));
+            IHIP(hipMalloc(&h->d_curf, nf * 3 * sizeof(float)));
+            IHIP(hipMalloc(&h->d_gid, nf * sizeof(int)));
+            h->full_cap = nf;
+        }
+        if (h->ns > 0)
+            IHIP(hipMemcpyAsync(h->d_srcf, h->h_src, h->ns * 3 * sizeof(float), hipMemcpyHostToDevice, h->st));
+    }
     if (h->sh_n > 0) {
         IHIP(hipMemcpyAsync(h->d_src, h->h_src + 3 * h->sh_begin, h->sh_n * 3 * sizeof(float),
                             hipMemcpyHostToDevice, h->st));
@@ -724,13 +782,25 @@ static int pcl_finish(lio_icp* h, const lio::IcpArgs& a) {
     return LIO_OK;
 }
 
+// the float statistics of the pass's accepted pairs (pa: this rank's correspondences, or with the source
+// sharded all ranks' gathered ids over the whole cloud), enqueued; h_pclout once the stream gets there
+static int enqueue_pcl(lio_icp* h, const lio::IcpArgs& pa) {
+    const int order = h->p.umeyama_float;
+    lio::launch_pcl_compact(pa, h->pcl, h->st);
+    lio::launch_pcl_means(h->pcl, 1, h->st);
+    lio::launch_pcl_sigma(h->pcl, order, 1, h->st);
+    lio::launch_pcl_pack(h->pcl, order, h->d_pclout, h->st);
+    IHIP(hipMemcpyAsync(h->h_pclout, h->d_pclout, lio::kPclOutWords * sizeof(float), hipMemcpyDeviceToHost, h->st));
+    return LIO_OK;
+}
+
 // One correspondence (or fitness) pass: GPU kernels + exchange + ordered sum.
 static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, double max_d2, double out17[17],
                     float* pcl16 = nullptr) {
     lio::IcpArgs a{};
     a.grid = lio::grid_view(h->tgt);
     a.tgt_by_id = h->tgt.by_id;
-    a.cur = h->d_cur;
+    a.cur = shard_cur(h);
     a.src = h->d_src;
     a.n = (int)h->sh_n;
     a.apply_T = apply_T ? 1 : 0;
@@ -765,33 +835,46 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
 #endif
     const int nsup_loc = (int)((h->sh_n + lio::kIcpSuper - 1) / lio::kIcpSuper);
     const bool dev_x = h->world > 1 && h->fn_dev;  // device-side exchange: records stay on the device
-    if (dev_x) {
+    // sharded PCL float modes: the accepted ids ride the exchange, the float chains run over the whole cloud
+    const bool fsh = pcl16 && fid_sharded(h) && !fitness;
+    const int64_t cnt = exchange_count(h->ns, h->world, fsh);  // doubles per rank this pass
+    const int64_t id_off = exchange_id_off(h->ns, h->world);
+    if (dev_x || fsh) {
         const int rc = exchange_reserve(h);
         if (rc) return rc;
+        if (h->x_len < cnt) return ifail(LIO_ERR_STATE, "lio_icp_align: exchange buffers smaller than a pass");
     }
-    if (h->sh_n > 0 || dev_x) {
+    if (fsh) a.aid = reinterpret_cast<int*>(h->d_xsend + id_off);
+    lio::IcpArgs pa = a;  // the float statistics' correspondences
+    if (fsh) {
+        pa.n = (int)h->ns;
+        pa.cur = h->d_curf;
+        pa.nn_id = h->d_gid;
+        pa.nn_d2 = nullptr;  // gated by icp_stats_kernel (-1 = rejected)
+        pa.aid = nullptr;
+    }
+    if (h->sh_n > 0 || dev_x || fsh) {
+        if (fsh && apply_T) lio::launch_icp_xform_rest(h->d_curf, h->ns, h->sh_begin, h->sh_n, T, h->st);
         if (h->timing) IHIP(hipEventRecord(h->ev.a, h->st));
         if (h->sh_n > 0) lio::launch_icp_tiles(a, h->ntiles, h->st);
         if (h->timing) IHIP(hipEventRecord(h->ev.m, h->st));
         if (dev_x) {  // records -> device send buffer -> in-stream all-gather -> record-order sum
             if (h->sh_n > 0) lio::launch_icp_stats(a, h->d_xsend, h->st, fitness ? nullptr : h->d_order, h->ntiles);
             IHIP(hipGetLastError());
-            if (h->fn_dev(h->d_xsend, h->x_len, h->d_xrecv, (void*)h->st, h->user_dev) != 0)
+            if (h->fn_dev(h->d_xsend, cnt, h->d_xrecv, (void*)h->st, h->user_dev) != 0)
                 return ifail(LIO_ERR_STATE, "device all-gather callback failed");
             const int64_t nsup = (h->ns + lio::kIcpSuper - 1) / lio::kIcpSuper;
-            lio::launch_icp_combine(h->d_xrecv, nsup, h->world, h->x_len / lio::kIcpStride, h->h_out17_dev, h->st);
-        } else {
+            lio::launch_icp_combine(h->d_xrecv, nsup, h->world, cnt, h->h_out17_dev, h->st);
+            if (fsh) lio::launch_icp_gather_ids(h->d_xrecv, h->world, cnt, id_off, h->ns, h->d_gid, h->st);
+        } else if (h->sh_n > 0) {
             // records straight to host memory; the next pass's tile order in the same launch
             lio::launch_icp_stats(a, h->h_super_dev, h->st, fitness ? nullptr : h->d_order, h->ntiles);
         }
         if (h->timing) IHIP(hipEventRecord(h->ev.b, h->st));
-        if (pcl16) {  // float fidelity mode: pcl::umeyama's float sums of this pass's correspondences
-            const int order = h->p.umeyama_float;
-            lio::launch_pcl_compact(a, h->pcl, h->st);
-            lio::launch_pcl_means(h->pcl, 1, h->st);
-            lio::launch_pcl_sigma(h->pcl, order, 1, h->st);
-            lio::launch_pcl_pack(h->pcl, order, h->d_pclout, h->st);
-            IHIP(hipMemcpyAsync(h->h_pclout, h->d_pclout, lio::kPclOutWords * sizeof(float), hipMemcpyDeviceToHost, h->st));
+        // the float statistics now, unless the ids still have to cross the host exchange
+        if (pcl16 && (!fsh || dev_x)) {
+            const int rc = enqueue_pcl(h, pa);
+            if (rc) return rc;
         }
         IHIP(hipGetLastError());
         IHIP(hipEventRecord(h->ev.done, h->st));
@@ -850,29 +933,34 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
             ++h->tm.icp_nn_launches;
         }
     }
+    if (!dev_x && h->world > 1) {
+        // host exchange: fixed-size slots (max records per rank, then the ids), summed in global record order
+        std::vector<double> send((size_t)cnt, 0.0), recv((size_t)cnt * h->world);
+        std::memcpy(send.data(), h->h_super, (size_t)nsup_loc * lio::kIcpStride * sizeof(double));
+        if (fsh && h->sh_n > 0)
+            IHIP(hipMemcpy(send.data() + id_off, h->d_xsend + id_off, (size_t)h->sh_n * sizeof(int), hipMemcpyDeviceToHost));
+        if (h->fn(send.data(), cnt, recv.data(), h->user) != 0) return ifail(LIO_ERR_STATE, "allgather callback failed");
+        combine_records(recv.data(), h->ns, h->world, cnt, out17);
+        if (fsh) {  // every rank's ids back on the device, then the float statistics over the whole cloud
+            IHIP(hipMemcpyAsync(h->d_xrecv, recv.data(), recv.size() * sizeof(double), hipMemcpyHostToDevice, h->st));
+            lio::launch_icp_gather_ids(h->d_xrecv, h->world, cnt, id_off, h->ns, h->d_gid, h->st);
+            const int rc = enqueue_pcl(h, pa);
+            if (rc) return rc;
+            IHIP(hipStreamSynchronize(h->st));
+        }
+    } else if (dev_x) {  // the record-order sums of every rank's records, computed on the device
+        std::memcpy(out17, h->h_out17, 17 * sizeof(double));
+    } else {
+        for (int k = 0; k < 17; ++k) out17[k] = 0.0;
+        for (int s = 0; s < nsup_loc; ++s)
+            for (int k = 0; k < 17; ++k) out17[k] += h->h_super[(size_t)s * lio::kIcpStride + k];
+    }
     if (pcl16) {
-        const int rc = pcl_finish(h, a);
+        const int rc = pcl_finish(h, pa);
         if (rc) return rc;
         std::memcpy(pcl16, h->h_pclout, 16 * sizeof(float));
     }
-    if (dev_x) {  // the record-order sums of every rank's records, computed on the device
-        std::memcpy(out17, h->h_out17, 17 * sizeof(double));
-        return LIO_OK;
-    }
-    for (int k = 0; k < 17; ++k) out17[k] = 0.0;
-    if (h->world == 1) {
-        for (int s = 0; s < nsup_loc; ++s)
-            for (int k = 0; k < 17; ++k) out17[k] += h->h_super[(size_t)s * lio::kIcpStride + k];
-        return LIO_OK;
-    }
-    // sharded: all-gather fixed-size slots (max records per rank), sum in global record order
-    const int64_t nsup = (h->ns + lio::kIcpSuper - 1) / lio::kIcpSuper;
-    const int64_t slot = (nsup + h->world - 1) / h->world;
-    std::vector<double> send((size_t)slot * lio::kIcpStride, 0.0), recv((size_t)slot * lio::kIcpStride * h->world);
-    std::memcpy(send.data(), h->h_super, (size_t)nsup_loc * lio::kIcpStride * sizeof(double));
-    if (h->fn(send.data(), (int64_t)send.size(), recv.data(), h->user) != 0)
-        return ifail(LIO_ERR_STATE, "allgather callback failed");
-    return lio_icp_combine(recv.data(), h->ns, h->world, out17);
+    return LIO_OK;
 }
 
 extern "C" int lio_icp_shard_range(int64_t ns, int rank, int world, int64_t* begin, int64_t* count) {
@@ -951,18 +1039,30 @@ extern "C" int lio_seqsum6(int device, const float* x, int64_t n, int flags, flo
     return done(LIO_OK, "");
 }
 
+extern "C" int lio_icp_exchange_layout(int64_t ns, int world, int ids, int64_t* count, int64_t* id_off) {
+    if (ns < 0 || world < 1 || !count || !id_off) return ifail(LIO_ERR_ARG, "lio_icp_exchange_layout: bad arguments");
+    *count = exchange_count(ns, world, ids != 0);
+    *id_off = exchange_id_off(ns, world);
+    return LIO_OK;
+}
+
+// host mirror of icp_gather_ids_kernel (the sharded PCL float modes' id unpacking)
+extern "C" int lio_icp_gather_ids(const double* recv, int64_t ns, int world, int64_t count, int32_t* gid) {
+    if (!recv || !gid || ns < 0 || world < 1 || count < exchange_count(ns, world, true))
+        return ifail(LIO_ERR_ARG, "lio_icp_gather_ids: bad arguments");
+    const int64_t id_off = exchange_id_off(ns, world);
+    for (int r = 0; r < world; ++r) {
+        int64_t b = 0, n = 0;
+        shard_range(ns, r, world, b, n);
+        std::memcpy(gid + b, reinterpret_cast<const int32_t*>(recv + (size_t)r * (size_t)count + (size_t)id_off),
+                    (size_t)n * sizeof(int32_t));
+    }
+    return LIO_OK;
+}
+
 extern "C" int lio_icp_combine(const double* recv, int64_t ns, int world, double* out17) {
     if (!recv || !out17 || world < 1 || ns < 0) return ifail(LIO_ERR_ARG, "lio_icp_combine: bad arguments");
-    const int64_t nsup = (ns + lio::kIcpSuper - 1) / lio::kIcpSuper;
-    const int64_t slot = (nsup + world - 1) / world;
-    for (int k = 0; k < 17; ++k) out17[k] = 0.0;
-    for (int r = 0; r < world; ++r) {
-        const int64_t s0 = nsup * r / world, s1 = nsup * (r + 1) / world;
-        for (int64_t s = s0; s < s1; ++s) {
-            const double* rec = &recv[((size_t)r * slot + (size_t)(s - s0)) * lio::kIcpStride];
-            for (int k = 0; k < 17; ++k) out17[k] += rec[k];
-        }
-    }
+    combine_records(recv, ns, world, exchange_count(ns, world, false), out17);
     return LIO_OK;
 }
 
@@ -971,11 +1071,7 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
     icp_join(h);
     if (h->nt == 0) return ifail(LIO_ERR_STATE, "lio_icp_align: no target");
     IHIP(hipSetDevice(h->dev));
-    const bool pcl_float = h->p.umeyama_float != 0;
-    if (h->p.umeyama_float < 0 || h->p.umeyama_float > 3)
-        return ifail(LIO_ERR_ARG, "lio_icp_align: umeyama_float must be 0 (double statistics) or 1..3 (float orders)");
-    if (pcl_float && h->world > 1)
-        return ifail(LIO_ERR_ARG, "lio_icp_align: umeyama_float (PCL-order float sums) runs on one rank only");
+    const bool pcl_float = h->p.umeyama_float > 0;  // (normalised at create: 0 = the double statistics)
     // the target (st2, helper thread) and the source (st, this thread) prepared side by side
     int rc = LIO_OK, trc = LIO_OK;
     std::string terr;
@@ -990,7 +1086,7 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
     if (trc) return ifail(trc, terr);
     if (rc) return rc;
     if (pcl_float) {
-        if (lio::pcl_reserve(h->pcl, std::max<int64_t>(h->sh_n, 1), h->p.umeyama_float, h->st))
+        if (lio::pcl_reserve(h->pcl, std::max<int64_t>(fid_sharded(h) ? h->ns : h->sh_n, 1), h->p.umeyama_float, h->st))
             return ifail(LIO_ERR_NOMEM, "lio_icp_align: fidelity buffers");
         h->pcl.means.dbg_noinc = h->pcl.sig.dbg_noinc = h->fid_flags & 1;
         for (lio::SeqSumBuf* b : {&h->pcl.means, &h->pcl.sig})
@@ -1006,8 +1102,12 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
         fin[i] = G[i];
         if (G[i] != ((i % 5 == 0) ? 1.f : 0.f)) ident = false;
     }
-    if (h->sh_n > 0)
+    if (fid_sharded(h)) {  // the whole cloud restarts from the source on every rank
+        if (h->ns > 0)
+            IHIP(hipMemcpyAsync(h->d_curf, h->d_srcf, h->ns * 3 * sizeof(float), hipMemcpyDeviceToDevice, h->st));
+    } else if (h->sh_n > 0) {
         IHIP(hipMemcpyAsync(h->d_cur, h->d_src, h->sh_n * 3 * sizeof(float), hipMemcpyDeviceToDevice, h->st));
+    }
     h->have_prior = false;
     h->have_order = false;  // every alignment starts in cell order (its first pass measures the tiles)
     const double max_d2 = h->p.max_corr_dist * h->p.max_corr_dist;
@@ -1096,7 +1196,7 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
     out->score = fs[0] > 0 ? fs[16] / fs[0] : std::numeric_limits<double>::max();
     out->is_valid = (out->is_converged && out->score < h->p.score_threshold) ? 1 : 0;
     if (aligned && h->sh_n > 0) {
-        IHIP(hipMemcpyAsync(aligned, h->d_cur, h->sh_n * 3 * sizeof(float), hipMemcpyDeviceToHost, h->st));
+        IHIP(hipMemcpyAsync(aligned, shard_cur(h), h->sh_n * 3 * sizeof(float), hipMemcpyDeviceToHost, h->st));
         IHIP(hipStreamSynchronize(h->st));
     }
     return LIO_OK;

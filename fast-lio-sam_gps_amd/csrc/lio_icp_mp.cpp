@@ -39,13 +39,18 @@ int mfail(int code, const std::string& msg) {
 }
 
 // ------------------------------------------------------------------ shared-memory all-gather
+constexpr uint32_t kShmMagic = 0x4c494f58u;  // rank 0 has written world / n
+
 struct ShmHdr {
     std::atomic<uint64_t> arrive;
     std::atomic<uint64_t> gen;
     std::atomic<int> attached;
+    std::atomic<int> poisoned;   // a barrier timed out: the arrival count can no longer be trusted
+    std::atomic<uint32_t> magic;
     int world;
     int64_t n;
-    char pad[256 - 2 * sizeof(std::atomic<uint64_t>) - sizeof(std::atomic<int>) - sizeof(int) - sizeof(int64_t)];
+    char pad[256 - 2 * sizeof(std::atomic<uint64_t>) - 2 * sizeof(std::atomic<int>) - sizeof(std::atomic<uint32_t>) -
+             sizeof(int) - sizeof(int64_t) - 4];
 };
 static_assert(sizeof(ShmHdr) == 256, "shm header layout");
 static_assert(std::atomic<uint64_t>::is_always_lock_free, "shared-memory atomics must be lock-free");
@@ -58,17 +63,36 @@ struct ShmEx {
     ShmHdr* hdr = nullptr;
     double* data = nullptr;  // 2 x world x n
     uint64_t round = 0;
+    ino_t ino = 0;           // the segment's inode: a name is only unlinked while it still names THIS segment
+    double timeout_s = 60.0;
 };
+
+// unlink `name` if it still refers to the segment with inode `ino` (a later open of the same name may have
+// replaced it: that segment belongs to someone else)
+void unlink_if_ours(const std::string& name, ino_t ino) {
+    const int fd = shm_open(name.c_str(), O_RDONLY, 0600);
+    if (fd < 0) return;
+    struct stat sb;
+    const bool ours = fstat(fd, &sb) == 0 && sb.st_ino == ino;
+    close(fd);
+    if (ours) shm_unlink(name.c_str());
+}
 
 void shm_close(ShmEx* e) {
     if (!e) return;
+    // the name was unlinked when the last rank attached; a segment some rank never attached to is removed by
+    // rank 0 here, and only while the name still refers to it
+    if (e->hdr && e->rank == 0 && e->hdr->attached.load(std::memory_order_acquire) < e->world)
+        unlink_if_ours(e->name, e->ino);
     if (e->hdr) munmap(e->hdr, e->bytes);
-    if (e->rank == 0) shm_unlink(e->name.c_str());
     delete e;
 }
 
 // rank 0 creates the segment (a stale one of the same name is removed first); the other ranks open it
-// after rank 0 has (the caller orders the opens, e.g. a process-group barrier), retrying for a few seconds
+// after rank 0 has (the caller orders the opens, e.g. a process-group barrier), retrying for a few seconds,
+// and check that it was made for the same world size and at least their message size.  The rank whose
+// attach completes the world unlinks the name at once, so no later close can remove a newer segment that
+// reuses it.
 int shm_open_ex(const char* name, int rank, int world, int64_t n, ShmEx** out) {
     if (!name || name[0] != '/' || rank < 0 || rank >= world || n < 1) return mfail(LIO_ERR_ARG, "lio_shm_exchange_open: bad arguments");
     auto* e = new ShmEx();
@@ -101,6 +125,8 @@ int shm_open_ex(const char* name, int rank, int world, int64_t n, ShmEx** out) {
         delete e;
         return mfail(LIO_ERR_STATE, "lio_shm_exchange_open: cannot open shared memory " + nm);
     }
+    struct stat sb;
+    if (fstat(fd, &sb) == 0) e->ino = sb.st_ino;
     void* p = mmap(nullptr, e->bytes, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
     close(fd);
     if (p == MAP_FAILED) {
@@ -112,15 +138,29 @@ int shm_open_ex(const char* name, int rank, int world, int64_t n, ShmEx** out) {
     if (rank == 0) {
         e->hdr->world = world;
         e->hdr->n = n;
+        e->hdr->magic.store(kShmMagic, std::memory_order_release);
+    } else {
+        for (int t = 0; t < 500 && e->hdr->magic.load(std::memory_order_acquire) != kShmMagic; ++t) usleep(10000);
+        if (e->hdr->magic.load(std::memory_order_acquire) != kShmMagic || e->hdr->world != world || e->hdr->n < n) {
+            const std::string msg = "lio_shm_exchange_open: segment " + e->name + " was made for another world size or "
+                                    "a smaller message (world " + std::to_string(e->hdr->world) + ", n " +
+                                    std::to_string(e->hdr->n) + ")";
+            munmap(e->hdr, e->bytes);
+            delete e;
+            return mfail(LIO_ERR_STATE, msg);
+        }
     }
-    e->hdr->attached.fetch_add(1, std::memory_order_acq_rel);
+    if (e->hdr->attached.fetch_add(1, std::memory_order_acq_rel) + 1 == world) unlink_if_ours(e->name, e->ino);
     *out = e;
     return LIO_OK;
 }
 
-// generation barrier over the ranks of the segment; false after ~60 s (a rank died)
+// generation barrier over the ranks of the segment; false after the timeout (a rank died) — and then the
+// segment is poisoned for every rank: this rank's arrival stays counted, so a later barrier could release
+// before every rank has written its records
 bool shm_barrier(ShmEx* e) {
     ShmHdr* h = e->hdr;
+    if (h->poisoned.load(std::memory_order_acquire)) return false;
     const uint64_t g = h->gen.load(std::memory_order_acquire);
     if (h->arrive.fetch_add(1, std::memory_order_acq_rel) == (uint64_t)e->world - 1) {
         h->arrive.store(0, std::memory_order_relaxed);
@@ -128,10 +168,15 @@ bool shm_barrier(ShmEx* e) {
         return true;
     }
     const auto t0 = std::chrono::steady_clock::now();
+    const auto limit = std::chrono::duration<double>(e->timeout_s);
     for (uint64_t it = 0; h->gen.load(std::memory_order_acquire) == g; ++it) {
+        if (h->poisoned.load(std::memory_order_acquire)) return false;
         if (it > 2000) {
             sched_yield();
-            if ((it & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(60)) return false;
+            if ((it & 1023) == 0 && std::chrono::steady_clock::now() - t0 > limit) {
+                h->poisoned.store(1, std::memory_order_release);
+                return false;
+            }
         }
     }
     return true;
@@ -142,9 +187,12 @@ bool shm_barrier(ShmEx* e) {
 // after it has read this round's set
 int shm_allgather(ShmEx* e, const double* send, int64_t n, double* recv) {
     if (n > e->n) return mfail(LIO_ERR_ARG, "shared-memory exchange: more doubles than the segment holds");
+    if (e->hdr->poisoned.load(std::memory_order_acquire))
+        return mfail(LIO_ERR_STATE, "shared-memory exchange: the segment is poisoned (an earlier barrier timed out)");
     double* set = e->data + (size_t)(e->round & 1) * (size_t)e->world * (size_t)e->n;
     std::memcpy(set + (size_t)e->rank * (size_t)e->n, send, (size_t)n * sizeof(double));
-    if (!shm_barrier(e)) return mfail(LIO_ERR_STATE, "shared-memory exchange: a rank did not arrive within 60 s");
+    if (!shm_barrier(e))
+        return mfail(LIO_ERR_STATE, "shared-memory exchange: a rank did not arrive in time (segment poisoned)");
     for (int r = 0; r < e->world; ++r)
         std::memcpy(recv + (size_t)r * (size_t)n, set + (size_t)r * (size_t)e->n, (size_t)n * sizeof(double));
     ++e->round;
@@ -198,6 +246,12 @@ int lio_shm_exchange_allgather(void* ex, const double* send, int64_t n, double* 
 
 int lio_shm_exchange_close(void* ex) {
     shm_close(static_cast<ShmEx*>(ex));
+    return LIO_OK;
+}
+
+int lio_shm_exchange_set_timeout(void* ex, double seconds) {
+    if (!ex || !(seconds > 0.0)) return mfail(LIO_ERR_ARG, "lio_shm_exchange_set_timeout: bad arguments");
+    static_cast<ShmEx*>(ex)->timeout_s = seconds;
     return LIO_OK;
 }
 

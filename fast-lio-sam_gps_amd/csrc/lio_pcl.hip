@@ -14,7 +14,8 @@
 //                                        sequential float results computed in parallel
 //   pcl_sigma_blocks                     orders 2 / 3: one wave per kc block, nine sequential lanes from LDS
 //   pcl_pack                             res += alpha * C_b in block order; sums, count, sigma, status
-// Single rank only (the correspondence order is global).
+// Sharded (lio_icp_host.cpp fid_sharded): the correspondence order is global, so every rank runs these over
+// the whole source with the all-gathered accepted ids (IcpArgs::nn_d2 == nullptr: gated already).
 #include "lio_kernels.hpp"
 #include "lio_pcl.hpp"
 
@@ -29,9 +30,10 @@ constexpr int kPPer = 4;           // consecutive source points per thread
 constexpr int kPB = kPT * kPPer;   // source points per compaction block
 constexpr int kMaxKc = 1016;       // kc at a 48 KiB L1 (the largest modelled)
 
+// a.nn_d2 == nullptr (sharded): a.nn_id holds the all-gathered ids, the gate already applied (-1 = rejected)
 __device__ __forceinline__ bool pcl_accept(const IcpArgs& a, int i) {
     const int id = a.nn_id[i];
-    const float d2 = a.nn_d2[i];
+    const float d2 = a.nn_d2 ? a.nn_d2[i] : 0.f;
     return id >= 0 && id != kNone && !((double)d2 > a.max_d2);
 }
 

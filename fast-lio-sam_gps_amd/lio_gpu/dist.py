@@ -80,6 +80,23 @@ def make_allgather(group=None, device=None):
     return _capi.ALLGATHER_FN(_cb)
 
 
+def exchange_layout(n_source: int, world: int, ids: bool):
+    """(doubles per rank of one pass, offset of the int32 ids in doubles) — records only, or records + the
+    rank's accepted 1-NN ids (the default PCL float mode's correspondence passes)"""
+    cnt, off = C.c_int64(), C.c_int64()
+    check(lib().lio_icp_exchange_layout(n_source, world, 1 if ids else 0, C.byref(cnt), C.byref(off)))
+    return cnt.value, off.value
+
+
+def gather_ids(recv: np.ndarray, n_source: int, world: int, count: int) -> np.ndarray:
+    """every rank's accepted ids (rank r's message at recv[r * count:]) in source order (lio_icp_gather_ids)"""
+    recv = np.ascontiguousarray(recv, dtype=np.float64)
+    gid = np.empty(n_source, np.int32)
+    check(lib().lio_icp_gather_ids(recv.ctypes.data_as(C.POINTER(C.c_double)), n_source, world, count,
+                                   gid.ctypes.data_as(C.POINTER(C.c_int32))))
+    return gid
+
+
 def exchange_len(n_source: int, world: int) -> int:
     """doubles per rank of the device-side exchange (lio_icp_exchange_len)"""
     n = C.c_int64()
@@ -175,10 +192,12 @@ def attach_shm(handle, rank: int, world: int, name: str, max_source_points: int,
 class ShmExchange:
     """The bare shared-memory all-gather (lio_shm_exchange_*; host only): n doubles from every rank."""
 
-    def __init__(self, name: str, rank: int, world: int, n: int):
+    def __init__(self, name: str, rank: int, world: int, n: int, timeout_s: float | None = None):
         self._h = C.c_void_p()
         check(lib().lio_shm_exchange_open(name.encode(), rank, world, n, C.byref(self._h)))
         self.world = world
+        if timeout_s is not None:
+            check(lib().lio_shm_exchange_set_timeout(self._h, float(timeout_s)))
 
     def allgather(self, send: np.ndarray) -> np.ndarray:
         send = np.ascontiguousarray(send, dtype=np.float64)

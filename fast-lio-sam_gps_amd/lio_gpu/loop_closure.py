@@ -53,13 +53,16 @@ def _xyz(cloud) -> np.ndarray:
     return a.reshape(-1, 3) if a.ndim == 1 else a[:, :3]
 
 
-# float fidelity orders (lio_icp_params.umeyama_float): 0 double statistics, 1 sequential-order
-# restatement, 2 Eigen 3.3 GEMM model (32 KiB L1; the recommended fidelity mode), 3 as 2 with 48 KiB
+# lio_icp_params.umeyama_float: PCL's float Umeyama (TransformationEstimationSVD<PointXYZI, PointXYZI,
+# float>, loop_closure.h:42) in a summation order — 1 sequential-order restatement, 2 the Eigen 3.3 GEMM
+# model (32 KiB L1; THE DEFAULT: the reference's arithmetic), 3 as 2 with 48 KiB — or DOUBLE_STATS, the
+# opt-in double statistics (faster, 1.2-1.9e-4 from the float orders at C4: outside the 1e-5 bar)
 FIDELITY_ORDER = 2
+DOUBLE_STATS = -1
 
 
 def icp_params(config: LoopClosureConfig, cell_size: float = 1.0, device: int = 0,
-               umeyama_float: int | bool = 0) -> _capi.IcpParams:
+               umeyama_float: int = FIDELITY_ORDER) -> _capi.IcpParams:
     # setTransformationEpsilon(0.01), setEuclideanFitnessEpsilon(0.01), setMaximumIterations(50)
     return _capi.IcpParams(config.icp_max_corr_dist_, 0.01, 0.01, 50, 0.0, config.icp_score_threshold_,
                            cell_size, device, int(umeyama_float))
@@ -67,9 +70,10 @@ def icp_params(config: LoopClosureConfig, cell_size: float = 1.0, device: int = 
 
 class LoopClosure:
     def __init__(self, config: LoopClosureConfig, cell_size: float = 1.0, device: int = 0,
-                 umeyama_float: int | bool = 0):
-        """umeyama_float: 0 double statistics (shardable); 1..3 a float fidelity order of pcl::umeyama
-        (single rank; True = 1, the sequential-order restatement)."""
+                 umeyama_float: int = FIDELITY_ORDER):
+        """umeyama_float: 1..3 a float order of pcl::umeyama (default 2, the reference's arithmetic; sharded
+        ranks all-gather their correspondence ids and give the one-rank transform bit for bit);
+        DOUBLE_STATS (-1) the opt-in double statistics."""
         self.config_ = config
         self._p = icp_params(config, cell_size, device, umeyama_float)
         self._h = C.c_void_p()
@@ -257,13 +261,14 @@ class LoopClosure:
 
 class LoopClosureGroup:
     """Single-process multi-GPU loop ICP (``lio_icp_group``): one handle per device, the source
-    sharded, the per-iteration records all-gathered over RCCL (or through host memory with
+    sharded, the per-iteration records (and the accepted correspondence ids) all-gathered over RCCL (or through host memory with
     ``LIO_ICP_EXCHANGE=host`` / a device listed twice).  Same results as :class:`LoopClosure`, bit
     for bit."""
 
-    def __init__(self, config: LoopClosureConfig, n_gpus: int, devices=None, cell_size: float = 1.0):
+    def __init__(self, config: LoopClosureConfig, n_gpus: int, devices=None, cell_size: float = 1.0,
+                 umeyama_float: int = FIDELITY_ORDER):
         self.config_ = config
-        self._p = icp_params(config, cell_size, 0 if devices is None else int(devices[0]))
+        self._p = icp_params(config, cell_size, 0 if devices is None else int(devices[0]), umeyama_float)
         self._h = C.c_void_p()
         devs = None
         if devices is not None:

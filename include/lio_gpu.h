@@ -240,19 +240,29 @@ typedef struct lio_icp_params {
     double score_threshold; /* icp_score_threshold (config.yaml:16)                   */
     float cell_size;        /* target grid cell [m]; 0 => 1.0                        */
     int device;
-    /* 0 (default): the Umeyama statistics in double about a fixed centre (deterministic, shardable).
-     * 1..3: float fidelity modes — TransformationEstimationSVD<PointXYZI, PointXYZI, float>'s
-     *    pcl::umeyama restated in float (single rank only) with the float summation order of a given
-     *    PCL/Eigen build (parity with a real PCL build unpinned: no PCL here):
+    /* How TransformationEstimationSVD's Umeyama step is evaluated (LIO_ICP_UMEYAMA_*).
+     * 0 (LIO_ICP_UMEYAMA_DEFAULT, a zero-initialised struct) = 2: the reference's arithmetic.
+     * 1..3: PCL float modes — TransformationEstimationSVD<PointXYZI, PointXYZI, float>'s pcl::umeyama
+     *    (loop_closure.h:42, aligned at loop_closure.cpp:81) restated in float with the float summation
+     *    order of a given PCL/Eigen build (parity with a real PCL build unpinned: no PCL here):
      *    1 sequential-order restatement: means and sigma's depth as single sequential chains;
      *    2 Eigen 3.3 model (32 KiB L1): sequential means, sigma by Eigen's GEMM — depth blocked by
-     *      kc = 680, res += alpha * block sum — the recommended fidelity mode;
+     *      kc = 680, res += alpha * block sum — THE DEFAULT;
      *    3 as 2 with a 48 KiB L1 (kc = 1016).
      *    The sequential float chains are evaluated in parallel and verified bit-exact on the GPU
-     *    (lio_seqsum: predicted binades, event replay, full verification; serial kernel fallback).
-     *    Float JacobiSVD on the host.                                                            */
+     *    (lio_seqsum: predicted binades, event replay, full verification; serial kernel fallback);
+     *    float JacobiSVD on the host.  Sharded (world > 1): every rank's accepted correspondence ids
+     *    ride the records' all-gather and every rank evaluates the float chains over the whole
+     *    source, so the transform is the one-rank transform bit for bit.
+     * -1 (LIO_ICP_UMEYAMA_DOUBLE, opt-in): the statistics in double about a fixed centre — faster, but
+     *    1.2-1.9e-4 from PCL's float arithmetic at C4 (outside the 1e-5 parity bar).      */
     int umeyama_float;
 } lio_icp_params;
+#define LIO_ICP_UMEYAMA_DEFAULT 0
+#define LIO_ICP_UMEYAMA_PCL_SEQ 1
+#define LIO_ICP_UMEYAMA_PCL_GEMM32 2
+#define LIO_ICP_UMEYAMA_PCL_GEMM48 3
+#define LIO_ICP_UMEYAMA_DOUBLE (-1)
 
 typedef struct lio_icp_result {  /* RegistrationOutput (loop_closure.h:21-27) + diagnostics */
     int is_valid;
@@ -282,6 +292,12 @@ int lio_icp_set_shard(lio_icp* h, int rank, int world, lio_allgather_fn fn, void
  * ceil(records/world)*20 doubles, as lio_allgather_fn delivers them.       */
 int lio_icp_shard_range(int64_t n_source, int rank, int world, int64_t* begin, int64_t* count);
 int lio_icp_combine(const double* recv, int64_t n_source, int world, double* out17);
+/* The message of one rank per pass (host helpers, no device): *count doubles — the records, then with
+ * ids != 0 (the PCL float modes, non-fitness passes) the rank's accepted 1-NN ids (int32, -1 = rejected)
+ * from double *id_off on.  lio_icp_gather_ids unpacks every rank's ids of a recv (rank r at r * count)
+ * into gid[0 .. n_source) in source order, as the device does before the float statistics.            */
+int lio_icp_exchange_layout(int64_t n_source, int world, int ids, int64_t* count, int64_t* id_off);
+int lio_icp_gather_ids(const double* recv, int64_t n_source, int world, int64_t count, int32_t* gid);
 /* Host half of the float fidelity modes (no device needed): sums16 = the float sums the GPU
  * returns per pass [sum src xyz(3), sum tgt xyz(3), count (uint32 bits), sigma accumulator (9,
  * row-major target x source): unscaled for order 1] -> the incremental transform (row-major 4x4
@@ -306,7 +322,9 @@ int lio_seqsum6(int device, const float* x, int64_t n, int flags, float* sums6, 
  * torch.cuda.ExternalStream(stream)), the handle enqueues the record-order sum behind it and reads 17
  * doubles back: one host wait per pass, no host copies of the records.  Buffers: the handle's own,
  * or the caller's (lio_icp_set_exchange_buffers, e.g. tensors a collective library registered);
- * n = lio_icp_exchange_len(n_source, world).                                                        */
+ * capacity lio_icp_exchange_len(n_source, world) doubles per rank.  The n of a pass may be less than
+ * the capacity: records only (double statistics, fitness passes), or the records followed by the
+ * rank's accepted correspondence ids as int32 (the PCL float modes); recv holds rank r at r * n.      */
 typedef int (*lio_allgather_dev_fn)(const double* d_send, int64_t n, double* d_recv, void* stream, void* user);
 int lio_icp_set_shard_device(lio_icp* h, int rank, int world, lio_allgather_dev_fn fn, void* user);
 int lio_icp_exchange_len(int64_t n_source, int world, int64_t* n_per_rank);
@@ -325,6 +343,9 @@ int lio_icp_set_shard_shm(lio_icp* h, int rank, int world, const char* name, int
 int lio_shm_exchange_open(const char* name, int rank, int world, int64_t n_per_rank, void** out);
 int lio_shm_exchange_allgather(void* ex, const double* send, int64_t n, double* recv);
 int lio_shm_exchange_close(void* ex);
+/* barrier timeout of an exchange (default 60 s; tests shorten it).  A timed-out barrier POISONS the
+ * segment: every later all-gather on it, on every rank, fails (the arrival count is no longer exact).   */
+int lio_shm_exchange_set_timeout(void* ex, double seconds);
 /* align(guess) + getFitnessScore() + is_valid decision (loop_closure.cpp:81-90).
  * aligned_opt (n*3, this rank's shard only when sharded) may be NULL.      */
 int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* aligned_opt);

@@ -421,8 +421,11 @@ struct RegistrationOutput {  // loop_closure.h:31-37
 
 class LoopClosureICP {
 public:
-    explicit LoopClosureICP(const LoopClosureConfig& cfg = {}, int device = 0, float cell_size = 1.0f) {
-        lio_icp_params p{cfg.icp_max_corr_dist_, 0.01, 0.01, 50, 0.0, cfg.icp_score_threshold_, cell_size, device, 0};
+    // umeyama: LIO_ICP_UMEYAMA_DEFAULT = PCL's float Umeyama in the Eigen 3.3 order (the reference's arithmetic,
+    // loop_closure.h:42); LIO_ICP_UMEYAMA_DOUBLE opts into the double statistics (outside the 1e-5 bar)
+    explicit LoopClosureICP(const LoopClosureConfig& cfg = {}, int device = 0, float cell_size = 1.0f,
+                            int umeyama = LIO_ICP_UMEYAMA_DEFAULT) {
+        lio_icp_params p{cfg.icp_max_corr_dist_, 0.01, 0.01, 50, 0.0, cfg.icp_score_threshold_, cell_size, device, umeyama};
         check(lio_icp_create(&p, &h_), "lio_icp_create");
     }
     ~LoopClosureICP() { lio_icp_destroy(h_); }
@@ -456,14 +459,15 @@ private:
 };
 
 // LoopClosure's ICP served by several GPUs from one process (lio_icp_group):
-// the source sharded, the per-iteration statistics all-gathered over RCCL;
-// results bit-identical to LoopClosureICP.  devices empty => 0 .. n_gpus-1.
+// the source sharded, the per-iteration records (and, in the default PCL float
+// mode, the accepted correspondence ids) all-gathered over RCCL; results
+// bit-identical to LoopClosureICP.  devices empty => 0 .. n_gpus-1.
 class LoopClosureICPGroup {
 public:
     LoopClosureICPGroup(const LoopClosureConfig& cfg, int n_gpus, const std::vector<int>& devices = {},
-                        float cell_size = 1.0f) {
+                        float cell_size = 1.0f, int umeyama = LIO_ICP_UMEYAMA_DEFAULT) {
         lio_icp_params p{cfg.icp_max_corr_dist_, 0.01, 0.01, 50, 0.0, cfg.icp_score_threshold_, cell_size,
-                         devices.empty() ? 0 : devices[0], 0};
+                         devices.empty() ? 0 : devices[0], umeyama};
         check(lio_icp_group_create(&p, n_gpus, devices.empty() ? nullptr : devices.data(), &g_), "lio_icp_group_create");
     }
     ~LoopClosureICPGroup() { lio_icp_group_destroy(g_); }

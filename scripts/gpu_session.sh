@@ -106,6 +106,9 @@ for s in $STEPS; do
     rccl)  run rccl_one_gpu 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
                --master-port 29531 scripts/rccl_one_gpu.py ;;
     watchdog) LIO_BENCH_REHEARSE=1 run watchdog2 300 python bench.py --gpus 2 --steps 20 --warmup 2 --pipeline 0 --no-cpu --streams '' --icp-reps 1 --watchdog-s 0.5 ;;
+    icp5)  runs pytest_icp5 900 python -u -m pytest tests/test_gpu_icp.py tests/test_gpu_dist.py tests/test_golden.py tests/test_gpu_parity.py tests/test_gpu_fullsize.py -k "icp or ICP or sharded" -x -v -p no:cacheprovider --timeout 600 --timeout-method thread ;;
+    icpt)  run icp_time2 300 python scripts/icp_ab.py 1.0 5 &&
+           run icp_time_double 300 env LIO_ICP_ORDER=-1 python scripts/icp_ab.py 1.0 5 ;;
     *) echo "unknown step $s" ;;
     esac
 done

@@ -12,7 +12,7 @@ sys.path.insert(0, os.path.join(ROOT, "fast-lio-sam_gps_amd"))
 from lio_gpu import loop_closure as LC  # noqa: E402
 from lio_gpu import synth  # noqa: E402
 
-order = int(os.environ.get("LIO_ICP_ORDER", "0"))
+order = int(os.environ.get("LIO_ICP_ORDER", "2"))  # -1: the opt-in double statistics
 src, dst, _ = synth.make_icp_pair(n_points=500_000, seed=4321, disp=(2.5, 4.0))
 lc = LC.LoopClosure(LC.LoopClosureConfig(), umeyama_float=order)
 lc.setInputSource(src)

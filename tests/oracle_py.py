@@ -37,7 +37,10 @@ class IcpParams(C.Structure):
                 ("umeyama_float", C.c_int)]
 
 
-# pcl::umeyama float summation orders (lio_oracle.cpp UmeyamaOrder); 0 = double statistics
+# pcl::umeyama float summation orders (lio_oracle.cpp UmeyamaOrder); the oracle's 0 = double statistics
+# (the GPU's opt-in LIO_ICP_UMEYAMA_DOUBLE); the default is order 2, as on the GPU
+ORACLE_DOUBLE_STATS = 0
+DEFAULT_UMEYAMA_ORDER = 2
 UMEYAMA_ORDERS = {1: "sequential means, sequential sigma", 2: "sequential means, Eigen GEMM sigma kc(32 KiB L1)",
                   3: "sequential means, Eigen GEMM sigma kc(48 KiB L1)", 4: "packet-4 means, sequential sigma",
                   5: "packet-4 means, Eigen GEMM sigma kc(32 KiB L1)"}
@@ -48,8 +51,16 @@ def default_match_params():
 
 
 def default_icp_params():
-    # loop_closure.cpp:7-10, fast_lio_sam.cpp:73 (1.5 * 35 m), config.yaml:16
-    return IcpParams(52.5, 0.01, 0.01, 50, 0.0, 1.5, 0)
+    # loop_closure.cpp:7-10, fast_lio_sam.cpp:73 (1.5 * 35 m), config.yaml:16; PCL's float Umeyama in the
+    # Eigen 3.3 GEMM order (loop_closure.h:42), the GPU default
+    return IcpParams(52.5, 0.01, 0.01, 50, 0.0, 1.5, DEFAULT_UMEYAMA_ORDER)
+
+
+def double_icp_params():
+    """the opt-in double statistics (GPU: LoopClosure(umeyama_float=DOUBLE_STATS))"""
+    p = default_icp_params()
+    p.umeyama_float = ORACLE_DOUBLE_STATS
+    return p
 
 
 def _p(a, t):

@@ -142,3 +142,132 @@ def test_shm_exchange_cpp(world):
         assert len(outs) == rounds
         for k, b in enumerate(outs):
             np.testing.assert_array_equal(np.frombuffer(b), ld.combine((recs * (k + 1)).ravel(), NS, 1))
+
+
+def _ids_worker(rank, world, port, q):
+    """One rank of the default (PCL float) mode's exchange on CPU: the message is this rank's records followed
+    by its accepted 1-NN ids (int32, -1 = rejected) — lio_icp_exchange_layout — all-gathered through the same
+    ctypes callback the library calls; lio_icp_gather_ids then rebuilds the whole source's ids in source order
+    (what icp_gather_ids_kernel does on the device before the float chains) and the records combine as before."""
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.join(os.path.dirname(here), "fast-lio-sam_gps_amd"))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import ctypes as C
+
+        from lio_gpu import dist as ld
+
+        recs = _records(NS)
+        ids = _ids(NS)
+        b, n = ld.shard_range(NS, rank, world)
+        cnt, off = ld.exchange_layout(NS, world, True)
+        cnt_rec, _ = ld.exchange_layout(NS, world, False)
+        r0 = b // 4096
+        mine = recs[r0: r0 + (n + 4095) // 4096]
+        send = np.zeros(cnt)
+        send[: mine.size] = mine.ravel()
+        send.view(np.int32)[2 * off: 2 * off + n] = ids[b: b + n]
+        cb = ld.make_allgather()
+        recv = np.zeros(cnt * world)
+        assert cb(send.ctypes.data_as(C.POINTER(C.c_double)), cnt, recv.ctypes.data_as(C.POINTER(C.c_double)), None) == 0
+        gid = ld.gather_ids(recv, NS, world, cnt)
+        rec_only = np.concatenate([recv[r * cnt: r * cnt + cnt_rec] for r in range(world)])
+        q.put((rank, gid.tobytes(), ld.combine(rec_only, NS, world).tobytes()))
+    finally:
+        dist.destroy_process_group()
+
+
+def _ids(ns):
+    rng = np.random.default_rng(99)
+    ids = rng.integers(0, 500_000, ns).astype(np.int32)
+    ids[rng.random(ns) < 0.1] = -1
+    return ids
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_sharded_icp_id_exchange_gloo(world):
+    """VERDICT r04 next #2 (the float mode sharded): every rank recovers every rank's accepted ids in source
+    order, bit for bit, and the record combine is unchanged by the ids riding behind the records."""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "fast-lio-sam_gps_amd"))
+    from lio_gpu import dist as ld
+
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_ids_worker, args=(r, world, port, q)) for r in range(world)]
+    [p.start() for p in procs]
+    got = [q.get(timeout=120) for _ in range(world)]
+    [p.join(timeout=60) for p in procs]
+    assert all(p.exitcode == 0 for p in procs)
+    ref_ids = _ids(NS)
+    ref = ld.combine(_records(NS).ravel(), NS, 1)
+    for rank, gid, comb in got:
+        np.testing.assert_array_equal(np.frombuffer(gid, np.int32), ref_ids)
+        np.testing.assert_array_equal(np.frombuffer(comb), ref)
+
+
+def test_shm_exchange_reopen_same_name():
+    """a second segment under the same name (a handle re-sharded, or two handles sharing a name)
+    must survive the first one's close — the name is unlinked once every rank has attached, and a close only
+    unlinks a name that still refers to its own segment."""
+    import sys
+    import threading
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "fast-lio-sam_gps_amd"))
+    from lio_gpu import dist as ld
+
+    name = f"/lio_reopen_{os.getpid()}"
+    a0 = ld.ShmExchange(name, 0, 2, 8)
+    a1 = ld.ShmExchange(name, 1, 2, 8)
+    b0 = ld.ShmExchange(name, 0, 2, 8)  # same name again (rank 0 first, as the callers order it)
+    a0.close()  # must not remove b0's segment
+    a1.close()
+    b1 = ld.ShmExchange(name, 1, 2, 8)  # opens b0's segment (failed with the old close)
+    out = [None, None]
+
+    def run(ex, r):
+        out[r] = ex.allgather(np.full(8, float(r + 1)))
+
+    th = [threading.Thread(target=run, args=(ex, r)) for r, ex in enumerate((b0, b1))]
+    [t.start() for t in th]
+    [t.join(timeout=30) for t in th]
+    for r in range(2):
+        np.testing.assert_array_equal(out[r], np.concatenate([np.full(8, 1.0), np.full(8, 2.0)]))
+    b0.close()
+    b1.close()
+    assert not os.path.exists(f"/dev/shm{name}")
+
+
+def test_shm_exchange_timeout_poisons_segment():
+    """a barrier that times out leaves its arrival counted, so the segment is poisoned — every later
+    all-gather on it fails on every rank instead of releasing early with stale records."""
+    import sys
+
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "fast-lio-sam_gps_amd"))
+    from lio_gpu import _capi, dist as ld
+
+    name = f"/lio_poison_{os.getpid()}"
+    e0 = ld.ShmExchange(name, 0, 2, 4, timeout_s=0.2)
+    e1 = ld.ShmExchange(name, 1, 2, 4, timeout_s=0.2)
+    with pytest.raises(_capi.LioError, match="did not arrive"):
+        e0.allgather(np.ones(4))  # rank 1 never arrives
+    for ex in (e1, e0):
+        with pytest.raises(_capi.LioError, match="poisoned"):
+            ex.allgather(np.ones(4))
+    e0.close()
+    e1.close()
+    with pytest.raises(_capi.LioError, match="another world size"):  # checked on open by ranks other than 0
+        f0 = ld.ShmExchange(name, 0, 3, 4)
+        try:
+            ld.ShmExchange(name, 1, 2, 4)
+        finally:
+            f0.close()

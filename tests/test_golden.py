@@ -61,6 +61,7 @@ def test_oracle_reproduces_esti_plane_fixture(oracle):
 
 def test_oracle_reproduces_icp_fixture(oracle):
     f = _load("icp_small.npz")
+    assert int(f["umeyama_order"]) == 2  # the default arithmetic: PCL's float Umeyama, Eigen 3.3 order
     r = oracle.icp_align(f["src"], f["dst"], want_aligned=True)
     np.testing.assert_array_equal(r["T"], f["T"])
     assert r["iterations"] == int(f["iterations"]) and r["state"] == int(f["state"])

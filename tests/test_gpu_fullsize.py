@@ -133,11 +133,14 @@ def test_c5_raw_scan_pipeline_three_scans(oracle):
 
 
 @pytest.mark.timeout(600)
-def test_icp_c4_four_emulated_ranks_bit_identical():
-    """BASELINE.json configs[3]'s layout: the source sharded over 4 ranks (threads, one LoopClosure
-    each, in-process all-gather of the 4096-point records), target replicated."""
-    src, dst, _ = synth.make_icp_pair(n_points=500_000, seed=4321, disp=(2.5, 4.0))
-    world = 4
+@pytest.mark.parametrize("world,disp", [(4, (2.5, 4.0)), (2, (0.3, 1.5))])
+def test_icp_c4_emulated_ranks_bit_identical(oracle, world, disp):
+    """BASELINE.json configs[3]'s layout: the source sharded over `world` ranks (threads, one LoopClosure
+    each, in-process all-gather of the 4096-point records and the accepted correspondence ids), target
+    replicated, in the DEFAULT mode (PCL's float Umeyama, Eigen 3.3 order): every rank's transform equals the
+    one-rank transform bit for bit, and that transform is within 1e-5 of the oracle's float order 2 (VERDICT
+    r04 next #2: the multi-GPU loop ICP at the reference's arithmetic)."""
+    src, dst, _ = synth.make_icp_pair(n_points=500_000, seed=4321, disp=disp)
     bar = threading.Barrier(world)
     slots = [None] * world
     results = [None] * world
@@ -169,9 +172,12 @@ def test_icp_c4_four_emulated_ranks_bit_identical():
     single.setInputSource(src)
     single.setInputTarget(dst)
     r1 = single.align(keep_aligned=False)
-    assert r1.iterations >= 5
+    assert r1.iterations >= (5 if disp[0] > 1 else 1)
     T1 = np.array(list(r1.T), np.float32)
     for r in results:
         assert r is not None
         np.testing.assert_array_equal(np.array(list(r.T), np.float32), T1)
         assert r.score == r1.score and r.iterations == r1.iterations
+    o = oracle.icp_align(src, dst)  # float order 2 (oracle default)
+    assert r1.iterations == o["iterations"] and r1.state == o["state"]
+    np.testing.assert_allclose(T1.reshape(4, 4), o["T"], atol=1e-5)

@@ -157,7 +157,7 @@ def _umeyama_np(src, dst):
 
 def test_icp_first_step_matches_numpy_umeyama(oracle):
     src, dst, T = synth.make_icp_pair(n_points=20000, seed=11)
-    res = oracle.icp_align(src, dst)
+    res = oracle.icp_align(src, dst, params=oracle.double_icp_params())  # the double form vs numpy's SVD
     # first iteration: correspondences = unbounded 1-NN within 52.5 m
     tr = cKDTree(dst.astype(np.float64))
     d, i = tr.query(src.astype(np.float64))
@@ -262,7 +262,7 @@ def test_icp_float_umeyama_mode_close_to_double(oracle):
     500k), and take the same iterations / convergence state."""
     for n, seed in ((8000, 3), (30000, 5)):
         src, dst, _ = synth.make_icp_pair(n_points=n, seed=seed)
-        rd = oracle.icp_align(src, dst)
+        rd = oracle.icp_align(src, dst, params=oracle.double_icp_params())
         p = oracle.default_icp_params()
         p.umeyama_float = 1
         rf = oracle.icp_align(src, dst, params=p)
