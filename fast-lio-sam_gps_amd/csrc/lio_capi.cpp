@@ -207,6 +207,20 @@ const char* lio_build_info(void) {
     return "lio_gpu: gfx950 HIP kernels (grid kNN + esti_plane + H^T H reduction, ICP); -ffp-contract=off";
 }
 
+int lio_abi_struct_sizes(int64_t* out, int n) {
+    const int64_t sz[] = {(int64_t)sizeof(lio_map_params),   (int64_t)sizeof(lio_match_params),
+                          (int64_t)sizeof(lio_pose),         (int64_t)sizeof(lio_state),
+                          (int64_t)sizeof(lio_ieskf_params), (int64_t)sizeof(lio_ieskf_stats),
+                          (int64_t)sizeof(lio_icp_params),   (int64_t)sizeof(lio_icp_result),
+                          (int64_t)sizeof(lio_localmap),     (int64_t)sizeof(lio_incremental_stats),
+                          (int64_t)sizeof(lio_imu_pose),     (int64_t)sizeof(lio_scan_prep_params),
+                          (int64_t)sizeof(lio_cloud_field),  (int64_t)sizeof(lio_kernel_timing)};
+    constexpr int kN = (int)(sizeof(sz) / sizeof(sz[0]));
+    if (out)
+        for (int i = 0; i < n && i < kN; ++i) out[i] = sz[i];
+    return kN;
+}
+
 int lio_map_create(const lio_map_params* p, lio_map** out) {
     if (!out) return fail(LIO_ERR_ARG, "out is NULL");
     *out = nullptr;

@@ -25,7 +25,7 @@ SUMS_HTH, SUMS_HTh, SUMS_NEFF, SUMS_RES, SUMS_HH = 0, 21, 27, 28, 29
 
 # Every symbol include/lio_gpu.h declares (checked by tests/test_capi_symbols.py).
 EXPORTS = [
-    "lio_device_count", "lio_last_error", "lio_build_info",
+    "lio_device_count", "lio_last_error", "lio_build_info", "lio_abi_struct_sizes",
     "lio_map_create", "lio_map_destroy", "lio_map_set_params", "lio_map_build", "lio_map_build_device", "lio_map_size",
     "lio_map_get_points", "lio_map_get_grid", "lio_map_get_stats", "lio_map_num_ids", "lio_map_get_by_id", "lio_map_nearest_search", "lio_map_gather", "lio_map_add",
     "lio_map_add_device", "lio_map_delete_boxes", "lio_localmap_update", "lio_map_incremental",
@@ -144,6 +144,7 @@ def _declare(L):
         "lio_device_count": (C.c_int, []),
         "lio_last_error": (C.c_char_p, []),
         "lio_build_info": (C.c_char_p, []),
+        "lio_abi_struct_sizes": (C.c_int, [C.POINTER(C.c_int64), C.c_int]),
         "lio_map_create": (C.c_int, [C.POINTER(MapParams), C.POINTER(vp)]),
         "lio_map_destroy": (C.c_int, [vp]),
         "lio_map_set_params": (C.c_int, [vp, C.POINTER(MapParams)]),
@@ -281,8 +282,27 @@ def lib():
         _share_torch_hip_runtime()
         L = C.CDLL(LIB_PATH)
         _declare(L)
+        _check_abi(L)
         _lib = L
     return _lib
+
+
+# the ctypes mirrors of lio_abi_struct_sizes' structs, in its order
+_ABI_STRUCTS = ("MapParams", "MatchParams", "Pose", "State", "IeskfParams", "IeskfStats", "IcpParams", "IcpResult",
+                "LocalMap", "IncrementalStats", "ImuPose", "ScanPrepParams", "CloudField", "KernelTiming")
+
+
+def _check_abi(L):
+    """Refuse a library whose public structs differ from these mirrors: an output struct of another size
+    overruns the caller's buffer (how round 4's LIO_GPU_LIB A/B against a round-2 build corrupted the heap:
+    its lio_kernel_timing carried an extra finalize pair, 128 bytes written into a 112-byte ctypes struct)."""
+    n = int(L.lio_abi_struct_sizes(None, 0))
+    sizes = (C.c_int64 * n)()
+    L.lio_abi_struct_sizes(sizes, n)
+    mine = [C.sizeof(globals()[k]) for k in _ABI_STRUCTS]
+    if n != len(mine) or list(sizes) != mine:
+        raise ImportError(f"{LIB_PATH}: ABI mismatch with lio_gpu/_capi.py — library struct sizes {list(sizes)}, "
+                          f"binding {mine} ({', '.join(_ABI_STRUCTS)})")
 
 
 def check(rc):

@@ -55,6 +55,12 @@ extern "C" {
 int lio_device_count(void);
 const char* lio_last_error(void);
 const char* lio_build_info(void);
+/* ABI guard (no device needed): sizeof of the public structs, in the order map_params, match_params, pose,
+ * state, ieskf_params, ieskf_stats, icp_params, icp_result, localmap, incremental_stats, imu_pose,
+ * scan_prep_params, cloud_field, kernel_timing — the first min(n, count) into out; returns the count.
+ * A binding built against another header version must refuse the library (an output struct of the wrong
+ * size is a buffer overrun: round 4's A/B of a round-2 build segfaulted at exit that way).           */
+int lio_abi_struct_sizes(int64_t* out, int n);
 
 /* -------------------------------------------------------------------- map
  * Replaces `KD_TREE<PointType> ikdtree` [U: ikd-Tree ikd_Tree.h]: a dense

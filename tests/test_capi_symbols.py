@@ -131,3 +131,23 @@ def test_icp_umeyama_pcl_float_host(seed):
     assert np.abs(T[:3, :3] - R).max() < 1e-3
     assert np.abs(T[3] - [0, 0, 0, 1]).max() == 0
     assert abs(np.linalg.det(T[:3, :3]) - 1) < 1e-5
+
+
+def test_abi_struct_sizes_match_the_binding(monkeypatch):
+    """The round-4 segfault: an A/B of a round-2 build through LIO_GPU_LIB wrote its
+    128-byte lio_kernel_timing (an extra finalize pair) into HEAD's 112-byte ctypes struct — a heap overrun
+    that crashed the interpreter at exit.  The binding now compares every public struct's size with the
+    library's (lio_abi_struct_sizes) at load and refuses a mismatch."""
+    L = _capi.lib()
+    n = L.lio_abi_struct_sizes(None, 0)
+    sizes = (C.c_int64 * n)()
+    L.lio_abi_struct_sizes(sizes, n)
+    assert list(sizes) == [C.sizeof(getattr(_capi, k)) for k in _capi._ABI_STRUCTS]
+    _capi._check_abi(L)  # HEAD against HEAD: accepted
+
+    class RoundTwoTiming(C.Structure):  # the round-2 layout: one (launches, ms) pair more
+        _fields_ = _capi.KernelTiming._fields_ + [("final_launches", C.c_int64), ("final_ms", C.c_double)]
+
+    monkeypatch.setattr(_capi, "KernelTiming", RoundTwoTiming)
+    with pytest.raises(ImportError, match="ABI mismatch"):
+        _capi._check_abi(L)
