@@ -217,8 +217,18 @@ def _loop_icp(args, LC, synth, local, world, rank, dist, rehearse, coll_dev, bar
                 "nn_kernel_ms_per_pass": round(nn_ms, 4),
                 "kernel_gbs": round(BYTES_PER_PT_ICP * shard_n / (icp_kernel_ms * 1e-3) / 1e9, 2)
                 if passes else None,
-                "sq_breakdown": _icp_sq(args), "traffic": _icp_traffic()}
+                # NOT measured in this run: counter passes committed under profiles/ 
+                "from_profile": {"sq_breakdown": _icp_sq(args), "traffic": _icp_traffic()}}
     return loop_icp, src, dst
+
+
+def _profile_meta(path):
+    """where a figure read from a committed counter pass comes from: the file and the measurement it records"""
+    try:
+        pm = json.load(open(path))
+    except Exception:
+        pm = {}
+    return {"source": os.path.relpath(path, ROOT), "measured": pm.get("measured") if isinstance(pm, dict) else None}
 
 
 def _icp_traffic():
@@ -491,18 +501,19 @@ def main():
             sq = None
     roofline = {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
+                # traffic: HBM bytes per launch from a separate rocprofv3 --pmc pass (not this run)
                 "traffic": traffic,
-                "kernel": "kNN h-evaluation = knn_near_kernel + knn_far_kernel + plane_kernel",
+                "kernel": "kNN h-evaluation = near pass (knn_group_kernel once per scan + knn_cell_kernel) + "
+                          "knn_far_kernel + plane_kernel",
                 "bytes_per_launch": BYTES_PER_PT_KNN * n_pts, "avg_launch_ms": round(knn_avg_ms, 5),
                 "near_kernel_avg_ms": round(near_avg_ms, 5), "far_kernel_avg_ms": round(far_avg_ms, 5),
                 "plane_kernel_avg_ms": round(tm["plane_ms"] / max(tm["plane_launches"], 1), 5),
                 "reuse_kernel_avg_ms": round(reuse_avg_ms, 5),
                 "reuse_achieved_gbs": round(BYTES_PER_PT_REUSE * n_pts / (reuse_avg_ms * 1e-3) / 1e9, 2)
                 if tm["reuse_launches"] else None,
-                "valu_busy_frac": sq["near_first"]["valu_busy_frac"] if sq and "near_first" in sq else None,
-                "wait_frac": sq["near_first"]["wait_frac"] if sq and "near_first" in sq else None,
-                "sq_breakdown": sq,
-                "sq_source": os.path.relpath(args.pmc_sq, ROOT) if sq else None}
+                # NOT measured in this run: counter passes committed under profiles/ 
+                "from_profile": {"traffic": _profile_meta(args.pmc) if traffic is not None else None,
+                                 "sq_breakdown": sq, "sq": _profile_meta(args.pmc_sq) if sq else None}}
 
     line = {
         "metric": "scans/sec (100k-pt scan vs N-pt map) + ms/IESKF-iteration, 1 GPU",
@@ -609,6 +620,17 @@ def main():
         fs.close()
         ptree.close()
         del d_pmap
+        # the same stream driven from C++ (tests/cpp/c5_stream.cpp through include/lio_gpu.hpp): no Python
+        # between the stages; its own process, map and handles
+        try:
+            import tempfile
+
+            with tempfile.TemporaryDirectory() as td:
+                fin, fout = os.path.join(td, "in.bin"), os.path.join(td, "out.bin")
+                PL.write_stream_input(fin, pmap, stream, P0, submap_range=2)
+                pipeline["cpp"] = PL.run_cpp_stream(fin, fout, timeout=300)
+        except Exception as e:  # secondary section: report, never fail the bench line
+            pipeline["cpp"] = {"error": str(e)[-300:]}
     line["pipeline"] = pipeline
 
     # ------------------------------------------------- several scan streams on one GPU (secondary)

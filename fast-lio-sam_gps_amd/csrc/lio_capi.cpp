@@ -171,6 +171,8 @@ struct lio_ctx {
     float* d_far_d = nullptr;
     int* d_far_id = nullptr;
     float* d_d5 = nullptr;  // per point: 5th neighbour d2 of the last kNN (seeds the next one)
+    int* d_perm = nullptr;  // per point: the cell-grouped query order of the near pass (built per scan)
+    int near_mode = 0;      // 0: per-query near pass (8 lanes per query), 1: cell-grouped (LIO_KNN_NEAR=cell, A/B only)
     bool have_eval = false;
     bool knn_valid = false;
     uint64_t knn_map_version = 0;  // map version of the last kNN evaluation
@@ -556,6 +558,8 @@ int lio_ctx_create(lio_map* m, const lio_match_params* p, lio_ctx** out) {
         (void)hipEventCreate(&e->b);
     }
     for (hipEvent_t& e : c->ev_marks) (void)hipEventCreate(&e);
+    // A/B only: LIO_KNN_NEAR=cell selects the cell-grouped near pass (bit-identical, 12x slower measured: DESIGN §4)
+    if (const char* e = std::getenv("LIO_KNN_NEAR")) c->near_mode = std::strcmp(e, "cell") == 0 ? 1 : 0;
     *out = c;
     return LIO_OK;
 }
@@ -566,7 +570,7 @@ int lio_ctx_destroy(lio_ctx* c) {
     (void)hipStreamSynchronize(c->map->st);
     void* ptrs[] = {c->d_body,  c->d_nn,    c->d_planes,   c->d_sel,       c->d_partials, c->d_sums,
                     c->d_rows,  c->d_nrows, c->d_far_list, c->d_far_count, c->d_far_d,    c->d_far_id, c->d_done,
-                    c->d_d5};
+                    c->d_d5,    c->d_perm};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (c->h_sums) (void)hipHostFree(c->h_sums);
@@ -586,12 +590,14 @@ int lio_ctx_destroy(lio_ctx* c) {
 
 static int ctx_reserve(lio_ctx* c, int64_t n) {
     if (n > c->cap || !c->d_body || !c->d_nn || !c->d_planes || !c->d_sel || !c->d_far_list || !c->d_far_d ||
-        !c->d_far_id || !c->d_d5) {
+        !c->d_far_id || !c->d_d5 || !c->d_perm) {
         int64_t cap = std::max<int64_t>(n, c->cap + c->cap / 2);
         c->cap = 0;  // a failed reallocation below leaves no buffer that looks usable
-        void* ptrs[] = {c->d_body, c->d_nn, c->d_planes, c->d_sel, c->d_far_list, c->d_far_d, c->d_far_id, c->d_d5};
+        void* ptrs[] = {c->d_body, c->d_nn, c->d_planes, c->d_sel, c->d_far_list, c->d_far_d, c->d_far_id, c->d_d5,
+                        c->d_perm};
         for (void* q : ptrs)
             if (q) (void)hipFree(q);
+        c->d_perm = nullptr;
         c->d_body = nullptr;
         c->d_nn = nullptr;
         c->d_planes = nullptr;
@@ -607,7 +613,8 @@ static int ctx_reserve(lio_ctx* c, int64_t n) {
             hipMalloc(&c->d_far_list, cap * sizeof(int)) != hipSuccess ||
             hipMalloc(&c->d_far_d, cap * 5 * sizeof(float)) != hipSuccess ||
             hipMalloc(&c->d_far_id, cap * 5 * sizeof(int)) != hipSuccess ||
-            hipMalloc(&c->d_d5, cap * sizeof(float)) != hipSuccess)
+            hipMalloc(&c->d_d5, cap * sizeof(float)) != hipSuccess ||
+            hipMalloc(&c->d_perm, cap * sizeof(int)) != hipSuccess)
             return fail(LIO_ERR_NOMEM, "scan buffers: hipMalloc failed");
         c->cap = cap;
     }
@@ -693,6 +700,7 @@ static lio::MatchArgs make_args(lio_ctx* c, const lio_pose& pose_in) {
     a.done_count = c->d_done;
     a.far_d = c->d_far_d;
     a.far_id = c->d_far_id;
+    a.perm = c->near_mode ? c->d_perm : nullptr;
     a.range_sq = c->p.knn_range_sq;
     a.plane_thr = c->p.plane_thr;
     a.s_coef = c->p.s_coef;

@@ -700,10 +700,16 @@ __device__ int group_knn_seeded(const GridDev& g, float bound, int cx, int cy, i
 // the box, because the grid build's cell assignment (cell_coord, clamped) is
 // monotone in each coordinate.  Must be called
 // by all NT threads of the block (it synchronises the block).
-template <int K, int NT>
+// DEDUP: the caller's list (tk on entry) may hold points from OUTSIDE the query's 3x3x3 block (the cell-grouped
+// near pass scans the union of its wave's blocks): a candidate whose key is already in that list is not pushed
+// again, so the box outside the block never duplicates it.
+template <int K, int NT, bool DEDUP = false>
 __device__ void block_knn_box_flat(const GridDev& g, float qx, float qy, float qz, uint32_t* s_b, uint32_t* s_off,
                                    uint32_t* s_w, uint64_t* s_lists, TopK<K>& tk, bool whole = false) {
     static_assert(NT % 64 == 0 && NT <= 1024, "block_knn_box_flat: NT = multiple of 64");
+    [[maybe_unused]] uint64_t ex[K];
+#pragma unroll
+    for (int j = 0; j < K; ++j) ex[j] = tk.k[j];
     constexpr int NW = NT / 64;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int cx = cell_coord(qx, g.ox, g.inv_cell);
@@ -789,7 +795,16 @@ __device__ void block_knn_box_flat(const GridDev& g, float qx, float qy, float q
                 }
 #pragma unroll
                 for (int u = 0; u < 4; ++u)
-                    if (t + (uint32_t)u < c1) tk.push(sqdist3(qx, qy, qz, pp[u].x, pp[u].y, pp[u].z), __float_as_int(pp[u].w));
+                    if (t + (uint32_t)u < c1) {
+                        const float d = sqdist3(qx, qy, qz, pp[u].x, pp[u].y, pp[u].z);
+                        bool dup = false;
+                        if constexpr (DEDUP) {
+                            const uint64_t key = knn_key(d, __float_as_int(pp[u].w));
+#pragma unroll
+                            for (int j = 0; j < K; ++j) dup = dup || key == ex[j];
+                        }
+                        if (!dup) tk.push(d, __float_as_int(pp[u].w));
+                    }
             }
         }
     }
@@ -861,6 +876,89 @@ __device__ __forceinline__ double wave_sum32(double (&v)[32], int lane) {
     const double keep = up ? v[1] : v[0];
     const double t = keep + __shfl_xor(send, 16, 64);
     return t + __shfl_xor(t, 32, 64);
+}
+
+// ----------------------------------------------------------------------------
+// Wave-level helpers shared by the tile kernels (ICP 1-NN, lio_icp.hip; the cell-grouped kNN near pass,
+// lio_match.hip): LDS hand-off inside one wave, DPP reductions / scans, (d2, id) keys as f64.
+// ----------------------------------------------------------------------------
+// LDS handoff between the lanes of ONE wave (each wave owns its staging area)
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// (d2, id) keys minimised as f64: lio_dev.hpp key_min (one v_min_f64 instead of compare + two selects)
+__device__ __forceinline__ double key_min_d(double a, double b) {
+    return __longlong_as_double((long long)key_min((uint64_t)__double_as_longlong(a), (uint64_t)__double_as_longlong(b)));
+}
+__device__ __forceinline__ double key_of(float d2, uint32_t id) {
+    return __longlong_as_double((long long)(((uint64_t)__float_as_uint(d2) << 32) | id));
+}
+
+// key (d[H], id[H]) of element H of a candidate pair in one v_pk_mov_b32: low word from the
+// id pair, high word from the packed distance pair (no register shuffling)
+template <int H>
+__device__ __forceinline__ double key_pk(uint32_t id0, uint32_t id1, f2v d) {
+    const double ids = __longlong_as_double((long long)(((uint64_t)id1 << 32) | id0));
+    double k;
+    if constexpr (H == 0)
+        asm("v_pk_mov_b32 %0, %1, %2 op_sel:[0,0]" : "=v"(k) : "v"(ids), "v"(d));
+    else
+        asm("v_pk_mov_b32 %0, %1, %2 op_sel:[1,1]" : "=v"(k) : "v"(ids), "v"(d));
+    return k;
+}
+
+// wave maximum of non-negative floats (as integers: same order), wave-uniform: DPP inside
+// each row of 16 (quad swaps, half-row and row mirrors), then the four row maxima by readlane
+// — no LDS permutes on the per-chunk path
+__device__ __forceinline__ float wave_max_nonneg(float v) {
+    uint32_t u = __float_as_uint(v);
+    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp((int)u, (int)u, 0xb1, 0xf, 0xf, false));   // quad_perm 1,0,3,2
+    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp((int)u, (int)u, 0x4e, 0xf, 0xf, false));   // quad_perm 2,3,0,1
+    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp((int)u, (int)u, 0x141, 0xf, 0xf, false));  // row_half_mirror
+    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp((int)u, (int)u, 0x140, 0xf, 0xf, false));  // row_mirror
+    const uint32_t m = max(max((uint32_t)__builtin_amdgcn_readlane((int)u, 0), (uint32_t)__builtin_amdgcn_readlane((int)u, 16)),
+                           max((uint32_t)__builtin_amdgcn_readlane((int)u, 32), (uint32_t)__builtin_amdgcn_readlane((int)u, 48)));
+    return __uint_as_float(m);
+}
+
+// wave-uniform values to SGPRs (the compiler cannot see that a butterfly
+// result is uniform; keeping the box arithmetic scalar frees VGPRs)
+__device__ __forceinline__ float uni_f(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
+__device__ __forceinline__ uint32_t uni_u(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
+
+// wave min / max of floats (any sign) by DPP inside each row of 16, then the four row
+// results by readlane: wave-uniform, no LDS permutes
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float x) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), CTRL, 0xf, 0xf, false));
+}
+template <bool MAX>
+__device__ __forceinline__ float wave_ext_dpp(float v) {
+    auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : fminf(a, b); };
+    v = op(v, dpp_f<0xb1>(v));   // quad_perm 1,0,3,2
+    v = op(v, dpp_f<0x4e>(v));   // quad_perm 2,3,0,1
+    v = op(v, dpp_f<0x141>(v));  // row_half_mirror
+    v = op(v, dpp_f<0x140>(v));  // row_mirror
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return uni_f(op(op(r0, r1), op(r2, r3)));
+}
+
+// inclusive prefix sum over the wave: DPP row shifts inside rows of 16, then row_bcast:15 /
+// row_bcast:31 carry the row totals forward (rows 1, 3 then rows 2, 3)
+__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
+    return v;
 }
 
 // XCD-aware block order: the hardware deals blocks round-robin over the 8 XCDs

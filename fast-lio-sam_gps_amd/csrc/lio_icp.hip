@@ -83,13 +83,6 @@ __device__ __forceinline__ int icp_tile_of(const uint32_t* order, int b, int n) 
     return -1;
 }
 
-// LDS handoff between the lanes of ONE wave (each wave owns its staging area)
-__device__ __forceinline__ void wave_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 // staged candidates as structure of arrays: 4 consecutive x (y, z, id) are one
 // 16-byte broadcast read, and two candidates' coordinates sit in one register
 // pair for the packed FP32 distance (v_pk_add_f32 / v_pk_mul_f32)
@@ -104,78 +97,6 @@ struct alignas(16) TileLds {
         uint4 perm[kIcpTileQ];  // a batch of rows (b0, n0, b1, n1), re-ordered nearest-first
     };
 };
-
-// (d2, id) keys minimised as f64: lio_dev.hpp key_min (one v_min_f64 instead of compare + two selects)
-__device__ __forceinline__ double key_min_d(double a, double b) {
-    return __longlong_as_double((long long)key_min((uint64_t)__double_as_longlong(a), (uint64_t)__double_as_longlong(b)));
-}
-__device__ __forceinline__ double key_of(float d2, uint32_t id) {
-    return __longlong_as_double((long long)(((uint64_t)__float_as_uint(d2) << 32) | id));
-}
-
-// key (d[H], id[H]) of element H of a candidate pair in one v_pk_mov_b32: low word from the
-// id pair, high word from the packed distance pair (no register shuffling)
-template <int H>
-__device__ __forceinline__ double key_pk(uint32_t id0, uint32_t id1, f2v d) {
-    const double ids = __longlong_as_double((long long)(((uint64_t)id1 << 32) | id0));
-    double k;
-    if constexpr (H == 0)
-        asm("v_pk_mov_b32 %0, %1, %2 op_sel:[0,0]" : "=v"(k) : "v"(ids), "v"(d));
-    else
-        asm("v_pk_mov_b32 %0, %1, %2 op_sel:[1,1]" : "=v"(k) : "v"(ids), "v"(d));
-    return k;
-}
-
-// wave maximum of non-negative floats (as integers: same order), wave-uniform: DPP inside
-// each row of 16 (quad swaps, half-row and row mirrors), then the four row maxima by readlane
-// — no LDS permutes on the per-chunk path
-__device__ __forceinline__ float wave_max_nonneg(float v) {
-    uint32_t u = __float_as_uint(v);
-    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp((int)u, (int)u, 0xb1, 0xf, 0xf, false));   // quad_perm 1,0,3,2
-    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp((int)u, (int)u, 0x4e, 0xf, 0xf, false));   // quad_perm 2,3,0,1
-    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp((int)u, (int)u, 0x141, 0xf, 0xf, false));  // row_half_mirror
-    u = max(u, (uint32_t)__builtin_amdgcn_update_dpp((int)u, (int)u, 0x140, 0xf, 0xf, false));  // row_mirror
-    const uint32_t m = max(max((uint32_t)__builtin_amdgcn_readlane((int)u, 0), (uint32_t)__builtin_amdgcn_readlane((int)u, 16)),
-                           max((uint32_t)__builtin_amdgcn_readlane((int)u, 32), (uint32_t)__builtin_amdgcn_readlane((int)u, 48)));
-    return __uint_as_float(m);
-}
-
-// wave-uniform values to SGPRs (the compiler cannot see that a butterfly
-// result is uniform; keeping the box arithmetic scalar frees VGPRs)
-__device__ __forceinline__ float uni_f(float v) { return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v))); }
-__device__ __forceinline__ uint32_t uni_u(uint32_t v) { return (uint32_t)__builtin_amdgcn_readfirstlane((int)v); }
-
-// wave min / max of floats (any sign) by DPP inside each row of 16, then the four row
-// results by readlane: wave-uniform, no LDS permutes
-template <int CTRL>
-__device__ __forceinline__ float dpp_f(float x) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(x), __float_as_int(x), CTRL, 0xf, 0xf, false));
-}
-template <bool MAX>
-__device__ __forceinline__ float wave_ext_dpp(float v) {
-    auto op = [](float a, float b) { return MAX ? fmaxf(a, b) : fminf(a, b); };
-    v = op(v, dpp_f<0xb1>(v));   // quad_perm 1,0,3,2
-    v = op(v, dpp_f<0x4e>(v));   // quad_perm 2,3,0,1
-    v = op(v, dpp_f<0x141>(v));  // row_half_mirror
-    v = op(v, dpp_f<0x140>(v));  // row_mirror
-    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
-    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
-    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
-    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
-    return uni_f(op(op(r0, r1), op(r2, r3)));
-}
-
-// inclusive prefix sum over the wave: DPP row shifts inside rows of 16, then row_bcast:15 /
-// row_bcast:31 carry the row totals forward (rows 1, 3 then rows 2, 3)
-__device__ __forceinline__ uint32_t wave_incl_scan_dpp(uint32_t v) {
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xf, 0xf, false);  // row_shr:1
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xf, 0xf, false);  // row_shr:2
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xf, 0xf, false);  // row_shr:4
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xf, 0xf, false);  // row_shr:8
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xa, 0xf, false);  // row_bcast:15
-    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xc, 0xf, false);  // row_bcast:31
-    return v;
-}
 
 // squared gap between the closed intervals [lo, hi] and [a, b]
 __device__ __forceinline__ float interval_gap(float lo, float hi, float a, float b) {

@@ -350,6 +350,7 @@ struct lio_icp {
     // and grid on st2, the source's upload and binning on st): every other entry point joins them first; a
     // failure leaves the dirty flag set, so lio_icp_align repeats the step and reports it
     std::thread bg_tgt, bg_src;
+    std::string bg_tgt_err, bg_src_err;  // why a background set-up failed (reported if align's retry fails too)
 };
 
 static void icp_join(lio_icp* h) {
@@ -508,8 +509,17 @@ int lio_icp_set_target(lio_icp* h, const float* xyz, int64_t n) {
     if (rc) return rc;
     h->nt = n;
     h->tgt_dirty = true;
+    h->bg_tgt_err.clear();
     // upload + grid on st2 behind the caller: overlaps the source's set-up and whatever the caller does next
-    h->bg_tgt = std::thread([h] { (void)target_build(h); });
+    // (no thread: the set-up runs here; a failure of either form leaves tgt_dirty for align to retry)
+    auto job = [h] {
+        if (target_build(h) != LIO_OK) h->bg_tgt_err = lio::last_error();
+    };
+    try {
+        h->bg_tgt = std::thread(job);
+    } catch (...) {
+        job();
+    }
     return LIO_OK;
 }
 
@@ -546,11 +556,18 @@ int lio_icp_set_source(lio_icp* h, const float* xyz, int64_t n) {
     }
     h->ns = n;
     h->src_dirty = true;
+    h->bg_src_err.clear();
     // this rank's shard uploaded and binned on st behind the caller (a later lio_icp_set_shard* marks it
     // dirty again and align repeats it for the new shard)
-    h->bg_src = std::thread([h] {
-        if (hipSetDevice(h->dev) == hipSuccess) (void)icp_prepare(h);
-    });
+    auto job = [h] {
+        if (hipSetDevice(h->dev) != hipSuccess) h->bg_src_err = "hipSetDevice";
+        else if (icp_prepare(h) != LIO_OK) h->bg_src_err = lio::last_error();
+    };
+    try {
+        h->bg_src = std::thread(job);
+    } catch (...) {
+        job();
+    }
     return LIO_OK;
 }
 
@@ -738,6 +755,8 @@ static uint32_t pcl_word(const lio_icp* h, int w) {
 
 static int pcl_finish(lio_icp* h, const lio::IcpArgs& a) {
     const int order = h->p.umeyama_float;
+    if (pcl_word(h, 3) != 0)  // h_pclout[19]
+        return ifail(LIO_ERR_HIP, "lio_icp_align: the correspondence compaction's look-back timed out");
     ++h->fid_stats[3];
     {
         int ev;
@@ -1076,15 +1095,24 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
     int rc = LIO_OK, trc = LIO_OK;
     std::string terr;
     std::thread tth;
-    if (h->tgt_dirty)
-        tth = std::thread([&] {
+    if (h->tgt_dirty) {
+        auto job = [&] {
             trc = target_build(h);
             if (trc) terr = lio::last_error();
-        });
+        };
+        try {
+            tth = std::thread(job);
+        } catch (...) {
+            job();
+        }
+    }
     rc = icp_prepare(h);
     if (tth.joinable()) tth.join();
-    if (trc) return ifail(trc, terr);
-    if (rc) return rc;
+    // a set-up that failed in the background and again here: both reasons
+    if (trc) return ifail(trc, terr + (h->bg_tgt_err.empty() ? "" : " (setInputTarget: " + h->bg_tgt_err + ")"));
+    if (rc) return ifail(rc, lio::last_error() + (h->bg_src_err.empty() ? "" : " (setInputSource: " + h->bg_src_err + ")"));
+    h->bg_tgt_err.clear();
+    h->bg_src_err.clear();
     if (pcl_float) {
         if (lio::pcl_reserve(h->pcl, std::max<int64_t>(fid_sharded(h) ? h->ns : h->sh_n, 1), h->p.umeyama_float, h->st))
             return ifail(LIO_ERR_NOMEM, "lio_icp_align: fidelity buffers");

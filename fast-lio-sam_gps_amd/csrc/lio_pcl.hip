@@ -29,6 +29,7 @@ constexpr int kPT = 256;           // threads per compaction block
 constexpr int kPPer = 4;           // consecutive source points per thread
 constexpr int kPB = kPT * kPPer;   // source points per compaction block
 constexpr int kMaxKc = 1016;       // kc at a 48 KiB L1 (the largest modelled)
+constexpr int kPackWin = 1024;     // GEMM depth blocks staged per window in pcl_pack (36 KiB of LDS)
 
 // a.nn_d2 == nullptr (sharded): a.nn_id holds the all-gathered ids, the gate already applied (-1 = rejected)
 __device__ __forceinline__ bool pcl_accept(const IcpArgs& a, int i) {
@@ -57,37 +58,23 @@ __device__ __forceinline__ uint32_t block_excl_u32(uint32_t v, uint32_t* s_w, ui
     return off + inc - v;
 }
 
-__global__ void __launch_bounds__(kPT) pcl_count_kernel(IcpArgs a, uint32_t* __restrict__ bcnt) {
+// The accepted pairs compacted in source order in ONE launch (was count / scan / scatter, 3 launches): every
+// block takes a logical index by ticket (arrival order, so a block only ever waits for blocks already running),
+// publishes its count, and looks back over its predecessors' status words — (epoch, flag, value): flag 1 the
+// block's count, flag 2 its inclusive prefix — until an inclusive one; integers, so any look-back order is
+// exact.  The epoch (a per-launch counter) makes the previous pass's words stale without a memset; the last
+// logical block writes the total and resets the ticket.
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+__global__ void __launch_bounds__(kPT) pcl_compact_kernel(IcpArgs a, unsigned long long* __restrict__ st,
+                                                          uint32_t* __restrict__ ticket, uint32_t epoch,
+                                                          float* __restrict__ pairs, uint32_t* __restrict__ d_n,
+                                                          int nb) {
     __shared__ uint32_t s_w[kPT / 64];
-    const int i0 = blockIdx.x * kPB + threadIdx.x * kPPer;
-    uint32_t c = 0;
-#pragma unroll
-    for (int i = 0; i < kPPer; ++i)
-        if (i0 + i < a.n && pcl_accept(a, i0 + i)) ++c;
-    uint32_t tot;
-    block_excl_u32(c, s_w, tot);
-    if (threadIdx.x == 0) bcnt[blockIdx.x] = tot;
-}
-
-// exclusive scan of the block counts in place, the total -> *d_n
-__global__ void __launch_bounds__(kPT) pcl_scan_kernel(uint32_t* __restrict__ bcnt, int nb, uint32_t* __restrict__ d_n) {
-    __shared__ uint32_t s_w[kPT / 64];
-    uint32_t base = 0;
-    for (int j0 = 0; j0 < nb; j0 += kPT) {
-        const int j = j0 + (int)threadIdx.x;
-        const uint32_t v = j < nb ? bcnt[j] : 0u;
-        uint32_t tot;
-        const uint32_t ex = block_excl_u32(v, s_w, tot);
-        if (j < nb) bcnt[j] = base + ex;
-        base += tot;
-    }
-    if (threadIdx.x == 0) *d_n = base;
-}
-
-__global__ void __launch_bounds__(kPT) pcl_scatter_kernel(IcpArgs a, const uint32_t* __restrict__ boff,
-                                                          float* __restrict__ pairs) {
-    __shared__ uint32_t s_w[kPT / 64];
-    const int i0 = blockIdx.x * kPB + threadIdx.x * kPPer;
+    __shared__ uint32_t s_b, s_off;
+    if (threadIdx.x == 0) s_b = atomicAdd(ticket, 1u);
+    __syncthreads();
+    const int b = (int)s_b;
+    const int i0 = b * kPB + threadIdx.x * kPPer;
     bool ok[kPPer];
     uint32_t c = 0;
 #pragma unroll
@@ -96,7 +83,38 @@ __global__ void __launch_bounds__(kPT) pcl_scatter_kernel(IcpArgs a, const uint3
         c += ok[i] ? 1u : 0u;
     }
     uint32_t tot;
-    uint32_t slot = boff[blockIdx.x] + block_excl_u32(c, s_w, tot);
+    const uint32_t ex = block_excl_u32(c, s_w, tot);
+    if (threadIdx.x == 0) {
+        const unsigned long long E = (unsigned long long)epoch << 34;
+        uint32_t acc = 0;
+        if (b > 0) {
+            __hip_atomic_store((gu64*)(st + b), E | (1ull << 32) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // every predecessor took its ticket earlier and publishes its count before it waits itself, so the
+            // loop ends; the bound is a safety valve only (flagged in pcl_pack's output, the host then fails)
+            uint32_t spins = 0;
+            for (int j = b - 1;;) {
+                const unsigned long long v = __hip_atomic_load((gu64*)(st + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((uint32_t)(v >> 34) != epoch) {  // not yet published in this launch
+                    if (++spins > (1u << 26)) {
+                        atomicOr(ticket + 1, 1u);
+                        break;
+                    }
+                    continue;
+                }
+                acc += (uint32_t)v;
+                if (((v >> 32) & 3u) == 2u) break;
+                --j;
+            }
+        }
+        __hip_atomic_store((gu64*)(st + b), E | (2ull << 32) | (acc + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_off = acc;
+        if (b == nb - 1) {
+            *d_n = acc + tot;
+            *ticket = 0u;  // every block has taken its ticket (this one came last)
+        }
+    }
+    __syncthreads();
+    uint32_t slot = s_off + ex;
 #pragma unroll
     for (int i = 0; i < kPPer; ++i)
         if (ok[i]) {
@@ -169,8 +187,9 @@ __global__ void __launch_bounds__(64) pcl_pack_kernel(const float* __restrict__ 
                                                       const float* __restrict__ Cb, int order, int l1,
                                                       const uint32_t* __restrict__ st_means,
                                                       const uint32_t* __restrict__ st_sig,
-                                                      const int* __restrict__ nev6, float* __restrict__ out) {
-    __shared__ float s_c[9][256];
+                                                      const int* __restrict__ nev6, const uint32_t* __restrict__ flags,
+                                                      float* __restrict__ out) {
+    __shared__ float s_c[9][kPackWin];
     const uint32_t n = *d_n;
     const int lane = threadIdx.x;
     const float oon = 1.f / (float)n;
@@ -191,15 +210,21 @@ __global__ void __launch_bounds__(64) pcl_pack_kernel(const float* __restrict__ 
     } else {
         const int64_t kc = eigen_gemm_kc((int64_t)n, l1);
         const int64_t nkc = ((int64_t)n + kc - 1) / kc;
-        for (int64_t q0 = 0; q0 < nkc; q0 += 256) {  // dst.setZero(); res(r, c) += alpha * C0 per depth block
-            const int m = (int)(nkc - q0 < 256 ? nkc - q0 : 256);
-            for (int e = lane; e < 9 * m; e += 64) s_c[e % 9][e / 9] = Cb[q0 * 9 + e];
+        for (int64_t q0 = 0; q0 < nkc; q0 += kPackWin) {  // dst.setZero(); res(r, c) += alpha * C0 per depth block
+            const int m = (int)(nkc - q0 < kPackWin ? nkc - q0 : kPackWin);
+            for (int e = lane; e < 9 * m; e += 64) s_c[e % 9][e / 9] = Cb[q0 * 9 + e];  // every load in flight at once
             __syncthreads();
-            if (lane < 9)
-                for (int q = 0; q < m; ++q) {
-                    const float t = oon * s_c[lane][q];
-                    res = res + t;
+            if (lane < 9) {
+                int q = 0;
+                for (; q + 8 <= m; q += 8) {  // the LDS reads ahead of the dependent adds
+                    float t[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) t[u] = oon * s_c[lane][q + u];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) res = res + t[u];
                 }
+                for (; q < m; ++q) res = res + oon * s_c[lane][q];
+            }
             __syncthreads();
         }
     }
@@ -213,6 +238,7 @@ __global__ void __launch_bounds__(64) pcl_pack_kernel(const float* __restrict__ 
         if (nev6)
             for (int k = 0; k < 6; ++k) ev = max(ev, nev6[k]);
         out[18] = __int_as_float(ev);
+        out[19] = __uint_as_float(flags ? *flags : 0u);  // compaction look-back timed out (never expected)
     }
 }
 
@@ -221,19 +247,20 @@ __global__ void __launch_bounds__(64) pcl_pack_kernel(const float* __restrict__ 
 int pcl_reserve(PclBuf& p, int64_t n, int order, hipStream_t st) {
     n = n < 1 ? 1 : n;
     if (n > p.cap) {
-        void* ptrs[] = {p.pairs, p.bcnt, p.Cb};
+        void* ptrs[] = {p.pairs, p.bst, p.Cb};
         for (void* q : ptrs)
             if (q) (void)hipFree(q);
         p.pairs = nullptr;
-        p.bcnt = nullptr;
+        p.bst = nullptr;
         p.Cb = nullptr;
         p.cap = 0;
         const int64_t nb = (n + kPB - 1) / kPB;
         const int64_t nkc = n / 340 + 2;  // kc >= max_kc / 2 >= 340 once the depth is blocked
         if (hipMalloc(&p.pairs, (size_t)n * 6 * sizeof(float)) != hipSuccess ||
-            hipMalloc(&p.bcnt, (size_t)nb * sizeof(uint32_t)) != hipSuccess ||
+            hipMalloc(&p.bst, (size_t)nb * sizeof(unsigned long long)) != hipSuccess ||
             hipMalloc(&p.Cb, (size_t)nkc * 9 * sizeof(float)) != hipSuccess)
             return -5;
+        (void)hipMemsetAsync(p.bst, 0, (size_t)nb * sizeof(unsigned long long), st);  // epoch 0: never current
         p.cap = n;
     }
     if (!p.small) {
@@ -246,7 +273,7 @@ int pcl_reserve(PclBuf& p, int64_t n, int order, hipStream_t st) {
 }
 
 void pcl_free(PclBuf& p) {
-    void* ptrs[] = {p.pairs, p.bcnt, p.Cb, p.small};
+    void* ptrs[] = {p.pairs, p.bst, p.Cb, p.small};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     seqsum_free(p.means);
@@ -261,9 +288,8 @@ void launch_pcl_compact(const IcpArgs& a, PclBuf& p, hipStream_t st) {
         (void)hipMemsetAsync(d_n, 0, sizeof(uint32_t), st);
         return;
     }
-    pcl_count_kernel<<<nb, kPT, 0, st>>>(a, p.bcnt);
-    pcl_scan_kernel<<<1, kPT, 0, st>>>(p.bcnt, nb, d_n);
-    pcl_scatter_kernel<<<nb, kPT, 0, st>>>(a, p.bcnt, p.pairs);
+    p.epoch = p.epoch + 1u >= (1u << 30) ? 1u : p.epoch + 1u;  // 30 bits, 0 reserved for "never written"
+    pcl_compact_kernel<<<nb, kPT, 0, st>>>(a, p.bst, p.small + kPclTicket, p.epoch, p.pairs, d_n, nb);
 }
 
 void launch_pcl_means(PclBuf& p, int pass, hipStream_t st) {
@@ -291,7 +317,7 @@ void launch_pcl_pack(PclBuf& p, int order, float* out, hipStream_t st, const flo
     pcl_pack_kernel<<<1, 64, 0, st>>>(p.pairs, d_n, sums6, order == 1 ? p.sig.result : sums6, p.Cb, order,
                                       pcl_l1(order), serial ? zero : p.means.status,
                                       order == 1 && !serial ? p.sig.status : zero,
-                                      serial ? nullptr : p.means.floor_e + p.means.nch, out);
+                                      serial ? nullptr : p.means.floor_e + p.means.nch, p.small + kPclTicket + 1, out);
 }
 
 }  // namespace lio

@@ -15,11 +15,14 @@ inline int pcl_l1(int order) { return order == kPclGemm48 ? 48 * 1024 : 32 * 102
 constexpr int kPclN = 0;       // accepted correspondences of the pass
 constexpr int kPclMean6 = 8;   // float means (order 1's sigma chains)
 constexpr int kPclZero = 16;   // two zero words (status of sums that need no verification)
-constexpr int kPclOutWords = 19;  // pcl_pack output: 16 statistics, 2 status words, events (max over the means)
+constexpr int kPclTicket = 20; // compaction block ticket (reset by the last block); [21] look-back time-out flag
+constexpr int kPclOutWords = 20;  // pcl_pack output: 16 statistics, 2 status words, events (max over the means),
+                                  // the compaction's time-out flag
 
 struct PclBuf {
     float* pairs = nullptr;   // cap x 6: accepted (src xyz, tgt xyz) in source order
-    uint32_t* bcnt = nullptr; // per compaction block: count, then exclusive offset
+    unsigned long long* bst = nullptr;  // per compaction block: look-back status word (epoch, flag, value)
+    uint32_t epoch = 0;                 // compaction launches so far (mod 2^30, 0 skipped)
     float* Cb = nullptr;      // orders 2 / 3: per depth block, 9 sequential block sums
     uint32_t* small = nullptr;
     int64_t cap = 0;

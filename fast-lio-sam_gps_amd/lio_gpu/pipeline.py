@@ -18,6 +18,10 @@ Node plumbing stays out (ROS, GTSAM pose graph, keyframe-threshold bookkeeping: 
 """
 from __future__ import annotations
 
+import ctypes
+import os
+import struct
+import subprocess
 import time
 
 import numpy as np
@@ -153,3 +157,89 @@ class FastLioSamStream:
     def close(self):
         self.hm.close()
         self.lc.close()
+
+
+# ------------------------------------------------------------------ the C++ driver of the same stream
+# tests/cpp/c5_stream.cpp (built by the package Makefile next to liblio_gpu.so) runs FastLioSamStream and the
+# loop leg through include/lio_gpu.hpp; these helpers write its input and read its output (the file format is
+# documented in the driver).
+CPP_STREAM_EXE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "c5_stream")
+
+
+def write_stream_input(path: str, map_xyz: np.ndarray, stream, P0: np.ndarray, submap_range: int = 2) -> None:
+    """stream: [(raw, imu_poses, end_pose24, initial_state, timestamp)] as synth.make_loop_stream gives."""
+    from . import filters as FL
+    from . import frontend as F
+
+    m = np.ascontiguousarray(map_xyz, np.float32).reshape(-1, 3)
+    with open(path, "wb") as f:
+        f.write(b"LIOC5IN1")
+        f.write(struct.pack("<q", len(m)))
+        f.write(m.tobytes())
+        f.write(struct.pack("<i", len(stream)))
+        for raw, poses, end24, st0, t in stream:
+            r = np.ascontiguousarray(raw, np.float32)
+            f.write(struct.pack("<qi", r.shape[0], r.shape[1]))
+            f.write(r.tobytes())
+            f.write(struct.pack("<i", len(poses)))
+            if len(poses):
+                f.write(bytes(FL.imu_poses_to_c(poses)))
+            f.write(bytes(F.pose_from_pose24(end24)))
+            f.write(bytes(F.state_to_c(st0)))
+            f.write(struct.pack("<d", float(t)))
+        f.write(np.ascontiguousarray(P0, np.float64).reshape(23 * 23).tobytes())
+        f.write(struct.pack("<i", int(submap_range)))
+
+
+def read_stream_output(path: str) -> dict:
+    from . import _capi
+    from . import frontend as F
+
+    b = open(path, "rb").read()
+    assert b[:8] == b"LIOC5OU1", "c5_stream output: bad magic"
+    o = 8
+
+    def take(dtype, n):
+        nonlocal o
+        a = np.frombuffer(b, dtype, n, o)
+        o += a.nbytes
+        return a
+
+    n_sweeps = int(take(np.int32, 1)[0])
+    sweeps = []
+    ssz = ctypes.sizeof(_capi.State)
+    for _ in range(n_sweeps):
+        st = _capi.State.from_buffer_copy(b[o:o + ssz])
+        o += ssz
+        cnt = take(np.int32, 4)
+        n_down, n_und = (int(v) for v in take(np.int64, 2))
+        ms = take(np.float64, 4)
+        pose = take(np.float64, 16).reshape(4, 4)
+        kn = int(take(np.int64, 1)[0])
+        kf = take(np.float32, kn * 4).reshape(kn, 4)
+        sweeps.append(dict(state=F.state_from_c(st), h_evals=int(cnt[0]), knn_calls=int(cnt[1]), converged=int(cnt[2]),
+                           n_eff=int(cnt[3]), n_down=n_down, n_undistorted=n_und,
+                           ms=dict(zip(("preprocess", "update", "map_incremental", "keyframe"), (float(v) for v in ms))),
+                           pose_eig=pose.copy(), pcd=kf.copy()))
+    idx, valid = (int(v) for v in take(np.int32, 2))
+    score = float(take(np.float64, 1)[0])
+    T = take(np.float32, 16).reshape(4, 4).copy()
+    iters, state = (int(v) for v in take(np.int32, 2))
+    clouds = []
+    for _ in range(2):
+        n = int(take(np.int64, 1)[0])
+        clouds.append(take(np.float32, n * 4).reshape(n, 4).copy())
+    return dict(sweeps=sweeps, loop=dict(closest_idx=idx, is_valid=bool(valid), score=score, T=T, iterations=iters,
+                                         state=state, src=clouds[0], dst=clouds[1]))
+
+
+def run_cpp_stream(in_path: str, out_path: str, timeout: float = 600.0, exe: str = CPP_STREAM_EXE) -> dict:
+    """Run the C++ driver; returns its stdout JSON summary (stage-time medians)."""
+    import json
+
+    if not os.path.exists(exe):
+        raise FileNotFoundError(f"{exe} missing: build the package (make -C fast-lio-sam_gps_amd)")
+    r = subprocess.run([exe, in_path, out_path], capture_output=True, text=True, timeout=timeout)
+    if r.returncode != 0:
+        raise RuntimeError(f"c5_stream failed ({r.returncode}): {r.stderr[-2000:]}")
+    return json.loads(r.stdout.strip().splitlines()[-1])

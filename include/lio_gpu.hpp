@@ -17,10 +17,13 @@
 // pcl::PointXYZINormal, ...).  Errors throw lio_gpu::Error carrying
 // lio_last_error(); there is no CPU fallback behind any call.
 #pragma once
+#include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <stdexcept>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "lio_gpu.h"
@@ -242,6 +245,39 @@ public:
         return n;
     }
 
+    // the same from float records (n x stride, the time offset at params.time_field) and the scan-end pose
+    int64_t set_scan_raw(const float* raw, int64_t n, int stride, const lio_scan_prep_params& params,
+                         const lio_imu_pose* imu_poses, int n_poses, const lio_pose& end) {
+        int64_t m = 0;
+        check(lio_scan_preprocess(c_, raw, n, stride, &params, imu_poses, n_poses, &end, &m), "set_scan_raw");
+        return m;
+    }
+
+    // feats_undistort of the last set_scan_raw (n x *stride records, before downSizeFilterSurf)
+    std::vector<float> undistorted(int* stride = nullptr) {
+        int64_t n = 0;
+        int w = 0;
+        check(lio_scan_get_undistorted(c_, nullptr, 0, &n, &w), "undistorted");
+        std::vector<float> out((size_t)n * (size_t)std::max(w, 1));
+        check(lio_scan_get_undistorted(c_, out.data(), n, &n, &w), "undistorted");
+        if (stride) *stride = w;
+        return out;
+    }
+
+    // fast_lio_sam's keyframe cloud from FAST-LIO's /cloud_registered, built on the device: T16 (row-major)
+    // * pointBodyToWorld(x, feats_undistort), intensity kept — PosePcd::pcd_ with T16 = pose_eig_.inverse()
+    // (pose_pcd.hpp:22-42)
+    template <typename PointXYZI_T>
+    std::vector<PointXYZI_T> keyframe_cloud(const lio_state& x, const double T16[16]) {
+        static_assert(sizeof(PointXYZI_T) == 4 * sizeof(float), "keyframe_cloud: x, y, z, intensity records");
+        const lio_pose p = pose_of(x);
+        int64_t n = 0;
+        check(lio_scan_keyframe_cloud(c_, &p, T16, nullptr, 0, &n), "keyframe_cloud");
+        std::vector<PointXYZI_T> out((size_t)n);
+        check(lio_scan_keyframe_cloud(c_, &p, T16, reinterpret_cast<float*>(out.data()), n, &n), "keyframe_cloud");
+        return out;
+    }
+
     // kf.update_iterated_dyn_share_modified(LASER_POINT_COV, solve_H_time): x, P (23x23 row-major) in place
     lio_ieskf_stats update_iterated_dyn_share_modified(lio_state& x, double* P, double laser_point_cov = 0.001,
                                                        int max_iteration = 3, double epsi = 0.001) {
@@ -407,9 +443,13 @@ std::vector<PointT> loadPCDFile(FilterGPU& f, const std::string& path, const std
 // ---------------------------------------------------------------------------
 // LoopClosure::icpAlignment (loop_closure.cpp:69-92) with the reference's ICP
 // settings (loop_closure.cpp:6-11) and LoopClosureConfig fields.
-struct LoopClosureConfig {  // loop_closure.h:21-29, values from fast_lio_sam.cpp:64-80
-    double icp_max_corr_dist_ = 52.5;
+struct LoopClosureConfig {  // loop_closure.h:21-29, values from fast_lio_sam.cpp:64-80 + config.yaml
+    int num_submap_keyframes_ = 5;
+    double voxel_res_ = 0.3;
+    double loop_detection_radius_ = 35.0;
+    double loop_detection_timediff_threshold_ = 30.0;
     double icp_score_threshold_ = 1.5;
+    double icp_max_corr_dist_ = 52.5;  // 1.5 * loop_detection_radius_ (fast_lio_sam.cpp:73)
 };
 
 struct RegistrationOutput {  // loop_closure.h:31-37
@@ -498,6 +538,230 @@ public:
 private:
     lio_icp_group* g_ = nullptr;
     lio_icp_result last_{};
+};
+
+// ---------------------------------------------------------------------------
+// fast_lio_sam's keyframe and loop leg (pose_pcd.hpp, loop_closure.h / .cpp) and the C5 stream that feeds
+// it (FAST-LIO's per-sweep front end [U] + fast_lio_sam.cpp:367-573,682-730): the C++ form of
+// lio_gpu/pipeline.py, for a maintainer who drives the path without Python.
+struct PointXYZI {  // pcl::PointXYZI's float fields (x, y, z, intensity)
+    float x, y, z, intensity;
+};
+
+struct PosePcd {  // pose_pcd.hpp:7-19
+    std::vector<PointXYZI> pcd_;
+    double pose_eig_[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};            // row-major
+    double pose_corrected_eig_[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};  // row-major
+    double timestamp_ = 0.0;
+    int idx_ = 0;
+    bool processed_ = false;
+};
+
+// pose_pcd.hpp:26-36: /Odometry's orientation through tf::Matrix3x3(q) (setRotation: s = 2 / |q|^2) and the
+// position -> pose_eig_ (row-major)
+inline void odom_matrix(const lio_state& x, double T[16]) {
+    const double w = x.rot[0], qx = x.rot[1], qy = x.rot[2], qz = x.rot[3];
+    const double d = qx * qx + qy * qy + qz * qz + w * w, s = 2.0 / d;
+    const double xs = qx * s, ys = qy * s, zs = qz * s;
+    const double wx = w * xs, wy = w * ys, wz = w * zs;
+    const double xx = qx * xs, xy = qx * ys, xz = qx * zs;
+    const double yy = qy * ys, yz = qy * zs, zz = qz * zs;
+    const double R[9] = {1.0 - (yy + zz), xy - wz, xz + wy, xy + wz, 1.0 - (xx + zz), yz - wx,
+                         xz - wy, yz + wx, 1.0 - (xx + yy)};
+    for (int r = 0; r < 3; ++r) {
+        for (int c = 0; c < 3; ++c) T[4 * r + c] = R[3 * r + c];
+        T[4 * r + 3] = x.pos[r];
+    }
+    T[12] = T[13] = T[14] = 0.0;
+    T[15] = 1.0;
+}
+
+// Matrix4d::inverse() (pose_eig_.inverse()): the general 4x4 inverse through 2x2 sub-determinants
+// (cofactors / determinant); equal to Eigen's up to the last bits (the keyframe cloud's tolerance)
+inline void inverse4(const double m[16], double inv[16]) {
+    const double s0 = m[0] * m[5] - m[4] * m[1], s1 = m[0] * m[6] - m[4] * m[2], s2 = m[0] * m[7] - m[4] * m[3];
+    const double s3 = m[1] * m[6] - m[5] * m[2], s4 = m[1] * m[7] - m[5] * m[3], s5 = m[2] * m[7] - m[6] * m[3];
+    const double c5 = m[10] * m[15] - m[14] * m[11], c4 = m[9] * m[15] - m[13] * m[11];
+    const double c3 = m[9] * m[14] - m[13] * m[10], c2 = m[8] * m[15] - m[12] * m[11];
+    const double c1 = m[8] * m[14] - m[12] * m[10], c0 = m[8] * m[13] - m[12] * m[9];
+    const double det = s0 * c5 - s1 * c4 + s2 * c3 + s3 * c2 - s4 * c1 + s5 * c0;
+    if (!(std::fabs(det) > 0.0)) throw Error(LIO_ERR_ARG, "inverse4: singular pose");
+    const double id = 1.0 / det;
+    inv[0] = (m[5] * c5 - m[6] * c4 + m[7] * c3) * id;
+    inv[1] = (-m[1] * c5 + m[2] * c4 - m[3] * c3) * id;
+    inv[2] = (m[13] * s5 - m[14] * s4 + m[15] * s3) * id;
+    inv[3] = (-m[9] * s5 + m[10] * s4 - m[11] * s3) * id;
+    inv[4] = (-m[4] * c5 + m[6] * c2 - m[7] * c1) * id;
+    inv[5] = (m[0] * c5 - m[2] * c2 + m[3] * c1) * id;
+    inv[6] = (-m[12] * s5 + m[14] * s2 - m[15] * s1) * id;
+    inv[7] = (m[8] * s5 - m[10] * s2 + m[11] * s1) * id;
+    inv[8] = (m[4] * c4 - m[5] * c2 + m[7] * c0) * id;
+    inv[9] = (-m[0] * c4 + m[1] * c2 - m[3] * c0) * id;
+    inv[10] = (m[12] * s4 - m[13] * s2 + m[15] * s0) * id;
+    inv[11] = (-m[8] * s4 + m[9] * s2 - m[11] * s0) * id;
+    inv[12] = (-m[4] * c3 + m[5] * c1 - m[6] * c0) * id;
+    inv[13] = (m[0] * c3 - m[1] * c1 + m[2] * c0) * id;
+    inv[14] = (-m[12] * s3 + m[13] * s1 - m[14] * s0) * id;
+    inv[15] = (m[8] * s3 - m[9] * s1 + m[10] * s0) * id;
+}
+
+// LoopClosure (loop_closure.h:39-70): the loop leg with the GPU submap assembly and ICP behind it
+class LoopClosure {
+public:
+    explicit LoopClosure(const LoopClosureConfig& config, int device = 0, int umeyama = LIO_ICP_UMEYAMA_DEFAULT)
+        : config_(config), f_(device), icp_(config, device, 1.0f, umeyama) {}
+
+    // loop_closure.cpp:18-40: among keyframes[0 .. size-2] the closest (translation of pose_corrected_eig_)
+    // within loop_detection_radius_ and more than loop_detection_timediff_threshold_ older; -1 if none
+    int fetchClosestKeyframeIdx(const PosePcd& query_keyframe, const std::vector<PosePcd>& keyframes) const {
+        const double radi = config_.loop_detection_radius_;
+        double shortest = radi * 3.0;
+        int closest = -1;
+        const double* q = query_keyframe.pose_corrected_eig_;
+        for (size_t i = 0; i + 1 < keyframes.size(); ++i) {
+            const double* p = keyframes[i].pose_corrected_eig_;
+            const double dx = p[3] - q[3], dy = p[7] - q[7], dz = p[11] - q[11];
+            const double d = std::sqrt(dx * dx + dy * dy + dz * dz);
+            if (radi > d && config_.loop_detection_timediff_threshold_ < query_keyframe.timestamp_ - keyframes[i].timestamp_ &&
+                d < shortest) {
+                shortest = d;
+                closest = keyframes[i].idx_;
+            }
+        }
+        return closest;
+    }
+
+    // loop_closure.cpp:42-67: per side, transformPcd of keyframes [idx - range, idx + range] (never the newest:
+    // i < size - 1) by pose_corrected_eig_, concatenated, voxelizePcd(voxel_res) — on the GPU
+    std::pair<std::vector<PointXYZI>, std::vector<PointXYZI>> setSrcAndDstCloud(const std::vector<PosePcd>& keyframes,
+                                                                                int src_idx, int dst_idx,
+                                                                                int submap_range, double voxel_res) {
+        auto side = [&](int center) {
+            std::vector<const std::vector<PointXYZI>*> clouds;
+            std::vector<const double*> poses;
+            for (int i = center - submap_range; i <= center + submap_range; ++i)
+                if (i >= 0 && i + 1 < (int)keyframes.size()) {
+                    clouds.push_back(&keyframes[(size_t)i].pcd_);
+                    poses.push_back(keyframes[(size_t)i].pose_corrected_eig_);
+                }
+            return clouds.empty() ? std::vector<PointXYZI>{} : submap_voxelize(f_, clouds, poses, (float)voxel_res);
+        };
+        return {side(src_idx), side(dst_idx)};
+    }
+
+    // loop_closure.cpp:69-92
+    RegistrationOutput icpAlignment(const std::vector<PointXYZI>& src, const std::vector<PointXYZI>& dst) {
+        return icp_.icpAlignment(src, dst, &aligned_);
+    }
+
+    // loop_closure.cpp:95-126 (submap_range < 0: num_submap_keyframes_)
+    RegistrationOutput performLoopClosure(const PosePcd& query_keyframe, const std::vector<PosePcd>& keyframes,
+                                          int closest_keyframe_idx, int submap_range = -1) {
+        closest_keyframe_idx_ = closest_keyframe_idx;
+        if (closest_keyframe_idx < 0) return RegistrationOutput{};
+        const int rng = submap_range < 0 ? config_.num_submap_keyframes_ : submap_range;
+        auto sd = setSrcAndDstCloud(keyframes, query_keyframe.idx_, closest_keyframe_idx, rng, config_.voxel_res_);
+        src_cloud_ = std::move(sd.first);
+        dst_cloud_ = std::move(sd.second);
+        return icpAlignment(src_cloud_, dst_cloud_);
+    }
+    RegistrationOutput performLoopClosure(const PosePcd& query_keyframe, const std::vector<PosePcd>& keyframes) {
+        return performLoopClosure(query_keyframe, keyframes, fetchClosestKeyframeIdx(query_keyframe, keyframes));
+    }
+
+    const std::vector<PointXYZI>& getSourceCloud() const { return src_cloud_; }
+    const std::vector<PointXYZI>& getTargetCloud() const { return dst_cloud_; }
+    const std::vector<float>& getFinalAlignedCloud() const { return aligned_; }  // xyz of the aligned source
+    int getClosestKeyframeidx() const { return closest_keyframe_idx_; }
+    const lio_icp_result& last_result() const { return icp_.last(); }
+    const LoopClosureConfig& config() const { return config_; }
+
+private:
+    LoopClosureConfig config_;
+    FilterGPU f_;
+    LoopClosureICP icp_;
+    int closest_keyframe_idx_ = -1;
+    std::vector<PointXYZI> src_cloud_, dst_cloud_;
+    std::vector<float> aligned_;
+};
+
+// One sensor stream through the GPU front end plus the loop leg (lio_gpu/pipeline.py FastLioSamStream):
+// per sweep Preprocess + UndistortPcl + downSizeFilterSurf -> IESKF update -> map_incremental -> keyframe
+// (every processed sweep: keyframe_threshold is 0 in config.yaml); loop() runs loopTimerFunc's work on the
+// newest keyframe.  Stage times are host wall times (ms).
+struct SweepResult {
+    lio_state x{};
+    std::vector<double> P;  // 23 x 23 row-major
+    lio_ieskf_stats stats{};
+    lio_incremental_stats incremental{};
+    int64_t n_down = 0, n_undistorted = 0;
+    double ms_preprocess = 0, ms_update = 0, ms_map_incremental = 0, ms_keyframe = 0;
+};
+
+class FastLioSamStream {
+public:
+    template <typename P>
+    FastLioSamStream(KdTreeGPU<P>& tree, const LoopClosureConfig& config = {}, double filter_size_map = 0.5,
+                     int max_iteration = 3, int point_filter_num = 4, float blind = 2.0f, float filter_size_surf = 0.5f,
+                     int device = 0)
+        : sm_(tree), lc_(config, device), fs_map_(filter_size_map), max_iter_(max_iteration),
+          prep_{point_filter_num, blind, filter_size_surf, 4} {}
+
+    // one raw sweep (n float records of `stride`, the time offset [ms] at field 4), its IMU poses and the
+    // scan-end pose; init / P0 the propagated state and covariance
+    SweepResult process(const float* raw, int64_t n, int stride, const std::vector<lio_imu_pose>& imu_poses,
+                        const lio_pose& end, const lio_state& init, const double* P0, double timestamp) {
+        using clk = std::chrono::steady_clock;
+        auto ms = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+        SweepResult r;
+        const auto t0 = clk::now();
+        r.n_down = sm_.set_scan_raw(raw, n, stride, prep_, imu_poses.data(), (int)imu_poses.size(), end);
+        const auto t1 = clk::now();
+        r.x = init;
+        r.P.assign(P0, P0 + 23 * 23);
+        r.stats = sm_.update_iterated_dyn_share_modified(r.x, r.P.data(), 0.001, max_iter_, 0.001);
+        const auto t2 = clk::now();
+        r.incremental = sm_.map_incremental(r.x, fs_map_);
+        const auto t3 = clk::now();
+        PosePcd kf;
+        odom_matrix(r.x, kf.pose_eig_);
+        double inv[16];
+        inverse4(kf.pose_eig_, inv);
+        kf.pcd_ = sm_.keyframe_cloud<PointXYZI>(r.x, inv);
+        std::copy(kf.pose_eig_, kf.pose_eig_ + 16, kf.pose_corrected_eig_);
+        kf.timestamp_ = timestamp;
+        kf.idx_ = (int)keyframes_.size();
+        r.n_undistorted = (int64_t)kf.pcd_.size();
+        keyframes_.push_back(std::move(kf));
+        const auto t4 = clk::now();
+        r.ms_preprocess = ms(t0, t1);
+        r.ms_update = ms(t1, t2);
+        r.ms_map_incremental = ms(t2, t3);
+        r.ms_keyframe = ms(t3, t4);
+        return r;
+    }
+
+    // loopTimerFunc's work on the newest keyframe: the closest index (-1: none) and the registration
+    int loop(RegistrationOutput* out, int submap_range = -1) {
+        *out = RegistrationOutput{};
+        if (keyframes_.empty()) return -1;
+        const PosePcd& q = keyframes_.back();
+        const int idx = lc_.fetchClosestKeyframeIdx(q, keyframes_);
+        if (idx >= 0) *out = lc_.performLoopClosure(q, keyframes_, idx, submap_range);
+        return idx;
+    }
+
+    const std::vector<PosePcd>& keyframes() const { return keyframes_; }
+    ScanMatcherGPU& matcher() { return sm_; }
+    LoopClosure& loop_closure() { return lc_; }
+
+private:
+    ScanMatcherGPU sm_;
+    LoopClosure lc_;
+    double fs_map_;
+    int max_iter_;
+    lio_scan_prep_params prep_;
+    std::vector<PosePcd> keyframes_;
 };
 
 }  // namespace lio_gpu

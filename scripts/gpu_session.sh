@@ -109,6 +109,9 @@ for s in $STEPS; do
     icp5)  runs pytest_icp5 900 python -u -m pytest tests/test_gpu_icp.py tests/test_gpu_dist.py tests/test_golden.py tests/test_gpu_parity.py tests/test_gpu_fullsize.py -k "icp or ICP or sharded" -x -v -p no:cacheprovider --timeout 600 --timeout-method thread ;;
     icpt)  run icp_time2 300 python scripts/icp_ab.py 1.0 5 &&
            run icp_time_double 300 env LIO_ICP_ORDER=-1 python scripts/icp_ab.py 1.0 5 ;;
+    knn5)  runs pytest_knn5 900 python -u -m pytest tests/test_gpu_parity.py tests/test_golden.py tests/test_properties.py tests/test_gpu_map.py tests/test_gpu_fullsize.py tests/test_cpp_api.py -k "not icp" -m gpu -x -v -p no:cacheprovider --timeout 600 --timeout-method thread ;;
+    near5) run near5 600 bash -c 'for r in 1 2; do for c in C3 C2; do python scripts/near_ab.py $c && LIO_KNN_NEAR=cell python scripts/near_ab.py $c || exit $?; done; done' ;;
+    cpps)  runs pytest_cpps 900 python -u -m pytest tests/test_cpp_stream.py tests/test_cpp_api.py -x -v -s -p no:cacheprovider --timeout 800 --timeout-method thread ;;
     *) echo "unknown step $s" ;;
     esac
 done
