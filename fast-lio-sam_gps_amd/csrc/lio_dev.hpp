@@ -1156,4 +1156,74 @@ __device__ __forceinline__ void h_row(const PoseArg& ps, float bx, float by, flo
     J[5] = p0 * C1 - p1 * C0;
 }
 
+// ---------------------------------------------------------------------------------------------------------------
+// Decoupled look-back (one pass scans: compaction offsets, event offsets).  Block b (its logical id from a ticket,
+// so every predecessor was scheduled first) publishes a status word epoch << 34 | flag << 32 | value (flag 1: its
+// aggregate, 2: its inclusive prefix; epoch: the launch's, so no memset between launches), looks back over its
+// predecessors' words and publishes its inclusive prefix.  The look-back reads 64 predecessors per round with one
+// wave (lane l: block j - l) and stops at the nearest inclusive word; a window holding a word of an older epoch
+// (not yet published) is read again.  Words are 8-B agent-scope relaxed atomics (sc1) on both sides
+// (MI355X_MICROARCH.md, hand-off table row 1: one lane per workgroup stores, the poller loads sc1).
+typedef __attribute__((address_space(1))) unsigned long long lb_gu64;
+
+__device__ __forceinline__ unsigned long long lb_word(uint32_t epoch, uint32_t flag, uint32_t v) {
+    return ((unsigned long long)epoch << 34) | ((unsigned long long)flag << 32) | v;
+}
+__device__ __forceinline__ void lb_store(unsigned long long* st, int b, unsigned long long w) {
+    __hip_atomic_store((lb_gu64*)(st + b), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ unsigned long long lb_load(const unsigned long long* st, int j) {
+    return __hip_atomic_load((lb_gu64*)(st + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The exclusive prefix of block b (all 64 lanes of the calling wave; b > 0, its aggregate already published).
+// 64-bit second values ride along: aggregate / inclusive in agg64[j] / inc64[j], stored before the word that
+// announces them (store, s_waitcnt vmcnt(0), word) and loaded after it (the load's address depends on the flag).
+// spin bound: a safety valve only (sets *timeout), every predecessor publishes before it looks back itself.
+template <bool WITH64>
+__device__ inline uint32_t lookback_excl(const unsigned long long* st, const unsigned long long* agg64,
+                                         const unsigned long long* inc64, int b, uint32_t epoch, uint64_t& ex64,
+                                         bool& timeout) {
+    const int lane = threadIdx.x & 63;
+    uint32_t acc = 0;
+    uint64_t acc64 = 0;
+    timeout = false;
+    uint32_t spins = 0;
+    for (int j = b - 1; j >= 0;) {
+        const int idx = j - lane;
+        unsigned long long w = idx >= 0 ? lb_load(st, idx) : lb_word(epoch, 2u, 0u);
+        const bool valid = (uint32_t)(w >> 34) == epoch;
+        const uint32_t flag = (uint32_t)(w >> 32) & 3u;
+        const uint64_t incl = __ballot(valid && flag == 2u);
+        const uint64_t inval = __ballot(!valid);
+        const int fi = incl ? __builtin_ctzll(incl) : 64;   // nearest inclusive word
+        const int fv = inval ? __builtin_ctzll(inval) : 64; // nearest unpublished word
+        if (fv < fi) {  // a word before the nearest inclusive one is not published yet: read the window again
+            if (++spins > (1u << 24)) {
+                timeout = true;
+                break;
+            }
+            continue;
+        }
+        const int last = fi < 64 ? fi : 63;  // lanes 0 .. last contribute
+        const bool take = lane <= last;
+        uint32_t v = take ? (uint32_t)w : 0u;
+        uint64_t v64 = 0;
+        if constexpr (WITH64) {
+            if (take && idx >= 0) v64 = lb_load(flag == 2u ? inc64 : agg64, idx);
+        }
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            v += __shfl_xor(v, d, 64);
+            if constexpr (WITH64) v64 += __shfl_xor(v64, d, 64);
+        }
+        acc += v;
+        acc64 += v64;
+        if (fi < 64) break;
+        j -= 64;
+    }
+    ex64 = acc64;
+    return acc;
+}
+
 }  // namespace lio

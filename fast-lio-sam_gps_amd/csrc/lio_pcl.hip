@@ -64,7 +64,6 @@ __device__ __forceinline__ uint32_t block_excl_u32(uint32_t v, uint32_t* s_w, ui
 // block's count, flag 2 its inclusive prefix — until an inclusive one; integers, so any look-back order is
 // exact.  The epoch (a per-launch counter) makes the previous pass's words stale without a memset; the last
 // logical block writes the total and resets the ticket.
-typedef __attribute__((address_space(1))) unsigned long long gu64;
 __global__ void __launch_bounds__(kPT) pcl_compact_kernel(IcpArgs a, unsigned long long* __restrict__ st,
                                                           uint32_t* __restrict__ ticket, uint32_t epoch,
                                                           float* __restrict__ pairs, uint32_t* __restrict__ d_n,
@@ -84,33 +83,22 @@ __global__ void __launch_bounds__(kPT) pcl_compact_kernel(IcpArgs a, unsigned lo
     }
     uint32_t tot;
     const uint32_t ex = block_excl_u32(c, s_w, tot);
-    if (threadIdx.x == 0) {
-        const unsigned long long E = (unsigned long long)epoch << 34;
+    if (threadIdx.x < 64) {  // wave 0: publish, look back (64 predecessors per read), publish the prefix
         uint32_t acc = 0;
         if (b > 0) {
-            __hip_atomic_store((gu64*)(st + b), E | (1ull << 32) | tot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            // every predecessor took its ticket earlier and publishes its count before it waits itself, so the
-            // loop ends; the bound is a safety valve only (flagged in pcl_pack's output, the host then fails)
-            uint32_t spins = 0;
-            for (int j = b - 1;;) {
-                const unsigned long long v = __hip_atomic_load((gu64*)(st + j), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((uint32_t)(v >> 34) != epoch) {  // not yet published in this launch
-                    if (++spins > (1u << 26)) {
-                        atomicOr(ticket + 1, 1u);
-                        break;
-                    }
-                    continue;
-                }
-                acc += (uint32_t)v;
-                if (((v >> 32) & 3u) == 2u) break;
-                --j;
-            }
+            if (threadIdx.x == 0) lb_store(st, b, lb_word(epoch, 1u, tot));
+            uint64_t unused;
+            bool timeout;
+            acc = lookback_excl<false>(st, nullptr, nullptr, b, epoch, unused, timeout);
+            if (timeout && threadIdx.x == 0) atomicOr(ticket + 1, 1u);  // flagged in pcl_pack's output
         }
-        __hip_atomic_store((gu64*)(st + b), E | (2ull << 32) | (acc + tot), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        s_off = acc;
-        if (b == nb - 1) {
-            *d_n = acc + tot;
-            *ticket = 0u;  // every block has taken its ticket (this one came last)
+        if (threadIdx.x == 0) {
+            lb_store(st, b, lb_word(epoch, 2u, acc + tot));
+            s_off = acc;
+            if (b == nb - 1) {
+                *d_n = acc + tot;
+                *ticket = 0u;  // every block has taken its ticket (this one came last)
+            }
         }
     }
     __syncthreads();
