@@ -503,8 +503,7 @@ def main():
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 5) if achieved else None,
                 # traffic: HBM bytes per launch from a separate rocprofv3 --pmc pass (not this run)
                 "traffic": traffic,
-                "kernel": "kNN h-evaluation = near pass (knn_group_kernel once per scan + knn_cell_kernel) + "
-                          "knn_far_kernel + plane_kernel",
+                "kernel": "kNN h-evaluation = knn_near_kernel + knn_far_kernel + plane_kernel",
                 "bytes_per_launch": BYTES_PER_PT_KNN * n_pts, "avg_launch_ms": round(knn_avg_ms, 5),
                 "near_kernel_avg_ms": round(near_avg_ms, 5), "far_kernel_avg_ms": round(far_avg_ms, 5),
                 "plane_kernel_avg_ms": round(tm["plane_ms"] / max(tm["plane_launches"], 1), 5),
