@@ -234,7 +234,7 @@ def _profile_meta(path):
 def _icp_traffic():
     """the ICP tile kernel's HBM traffic per pass from the committed FETCH_SIZE / WRITE_SIZE passes
     (scripts/icp_pmc_traffic.py over scripts/icp_ab.py 1.0 1)"""
-    path = os.path.join(ROOT, "profiles", "r04_pmc_icp_traffic.json")
+    path = os.path.join(ROOT, "profiles", "r05_pmc_icp_traffic.json")
     try:
         pm = json.load(open(path))
     except Exception:

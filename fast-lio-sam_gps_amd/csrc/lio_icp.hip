@@ -564,31 +564,79 @@ __device__ void icp_order_share(const uint32_t* __restrict__ cost, int n, uint32
     }
 }
 
-// per cell: number of tiles (ceil(count / 64)); slot ncells = 0 for the scan's total
-__global__ void tile_count_kernel(const uint32_t* __restrict__ start, uint32_t ncells, uint32_t* __restrict__ tcount) {
-    const uint32_t c = blockIdx.x * 256u + threadIdx.x;
-    if (c > ncells) return;
-    tcount[c] = c < ncells ? (start[c + 1] - start[c] + kIcpTileQ - 1) / kIcpTileQ : 0u;
+// Tiles in Morton order of their cells (z, y, x bits interleaved): the kIcpSegs contiguous segments a pass
+// deals to the XCDs are then compact 3-D blobs of the cloud instead of thin slabs of the x-fastest cell order
+// (2 m tile cells: a slab one or two cells thick, whose target neighbourhood is mostly halo shared with the
+// slabs on other XCDs — each XCD's L2 then fetched the same target rows).  Perf only: every 1-NN is exact in
+// any tile order.  Grids wider than 1024 cells on an axis keep the cell order.
+__device__ __forceinline__ uint32_t spread3_10(uint32_t v) {  // bits 0..9 -> every third bit
+    v &= 0x3ffu;
+    v = (v | (v << 16)) & 0x030000ffu;
+    v = (v | (v << 8)) & 0x0300f00fu;
+    v = (v | (v << 4)) & 0x030c30c3u;
+    v = (v | (v << 2)) & 0x09249249u;
+    return v;
 }
-__global__ void tile_write_kernel(const uint32_t* __restrict__ start, uint32_t ncells, const uint32_t* __restrict__ toff,
-                                  uint2* __restrict__ tiles) {
+__global__ void tile_key_kernel(const uint32_t* __restrict__ start, GridGeom gm, int morton, uint32_t* __restrict__ key,
+                                uint32_t* __restrict__ cell) {
     const uint32_t c = blockIdx.x * 256u + threadIdx.x;
-    if (c >= ncells) return;
-    const uint32_t b = start[c], n = start[c + 1] - b, nt = toff[c + 1] - toff[c];
+    if (c >= gm.ncells) return;
+    uint32_t k = 0xffffffffu;  // empty cells sort last (and carry no tiles)
+    if (start[c + 1] > start[c]) {
+        if (morton) {
+            const uint32_t x = c % (uint32_t)gm.nx, yz = c / (uint32_t)gm.nx;
+            const uint32_t y = yz % (uint32_t)gm.ny, z = yz / (uint32_t)gm.ny;
+            k = (spread3_10(z) << 2) | (spread3_10(y) << 1) | spread3_10(x);
+        } else {
+            k = c;
+        }
+    }
+    key[c] = k;
+    cell[c] = c;
+}
+// per sorted cell: number of tiles (ceil(count / 64)); slot ncells = 0 for the scan's total
+__global__ void tile_count_kernel(const uint32_t* __restrict__ start, uint32_t ncells, const uint32_t* __restrict__ cell,
+                                  uint32_t* __restrict__ tcount) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i > ncells) return;
+    uint32_t t = 0;
+    if (i < ncells) {
+        const uint32_t c = cell[i];
+        t = (start[c + 1] - start[c] + kIcpTileQ - 1) / kIcpTileQ;
+    }
+    tcount[i] = t;
+}
+__global__ void tile_write_kernel(const uint32_t* __restrict__ start, uint32_t ncells, const uint32_t* __restrict__ cell,
+                                  const uint32_t* __restrict__ toff, uint2* __restrict__ tiles) {
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    if (i >= ncells) return;
+    const uint32_t c = cell[i];
+    const uint32_t b = start[c], n = start[c + 1] - b, nt = toff[i + 1] - toff[i];
     for (uint32_t t = 0; t < nt; ++t) {  // balanced split of the cell's points
         const uint32_t s0 = (uint32_t)((uint64_t)n * t / nt), s1 = (uint32_t)((uint64_t)n * (t + 1) / nt);
-        tiles[toff[c] + t] = make_uint2(b + s0, s1 - s0);
+        tiles[toff[i] + t] = make_uint2(b + s0, s1 - s0);
     }
 }
 
 int icp_build_tiles(const GridBuf& q, uint2* tiles, uint32_t* scratch, void*& tmp, size_t& tmp_bytes, hipStream_t st) {
     const uint32_t nc = q.geom.ncells;
-    uint32_t* tcount = scratch;          // nc + 1
-    uint32_t* toff = scratch + nc + 1;   // nc + 1
+    uint32_t* tcount = scratch;             // nc + 1
+    uint32_t* toff = tcount + nc + 1;       // nc + 1
+    uint32_t* key = toff + nc + 1;          // nc
+    uint32_t* key2 = key + nc;              // nc
+    uint32_t* cell = key2 + nc;             // nc
+    uint32_t* cell2 = cell + nc;            // nc
     const int nb = (int)((nc + 1 + 255) / 256);
-    tile_count_kernel<<<nb, 256, 0, st>>>(q.start, nc, tcount);
-    size_t need = 0;
-    if (hipcub::DeviceScan::ExclusiveSum(nullptr, need, tcount, toff, (int)(nc + 1), st) != hipSuccess) return -1;
+#ifndef LIO_TILE_MORTON
+#define LIO_TILE_MORTON 1  // A/B builds: 0 keeps the x-fastest cell order
+#endif
+    const int morton = LIO_TILE_MORTON && q.geom.nx <= 1024 && q.geom.ny <= 1024 && q.geom.nz <= 1024 ? 1 : 0;
+    tile_key_kernel<<<nb, 256, 0, st>>>(q.start, q.geom, morton, key, cell);
+    size_t need_scan = 0, need_sort = 0;
+    if (hipcub::DeviceScan::ExclusiveSum(nullptr, need_scan, tcount, toff, (int)(nc + 1), st) != hipSuccess ||
+        hipcub::DeviceRadixSort::SortPairs(nullptr, need_sort, key, key2, cell, cell2, (int)nc, 0, 32, st) != hipSuccess)
+        return -1;
+    const size_t need = std::max(need_scan, need_sort);
     if (need > tmp_bytes) {
         if (tmp) (void)hipFree(tmp);
         tmp = nullptr;
@@ -597,8 +645,11 @@ int icp_build_tiles(const GridBuf& q, uint2* tiles, uint32_t* scratch, void*& tm
         tmp_bytes = need;
     }
     size_t tb = tmp_bytes;
+    if (hipcub::DeviceRadixSort::SortPairs(tmp, tb, key, key2, cell, cell2, (int)nc, 0, 32, st) != hipSuccess) return -1;
+    tile_count_kernel<<<nb, 256, 0, st>>>(q.start, nc, cell2, tcount);
+    tb = tmp_bytes;
     if (hipcub::DeviceScan::ExclusiveSum(tmp, tb, tcount, toff, (int)(nc + 1), st) != hipSuccess) return -1;
-    tile_write_kernel<<<nb, 256, 0, st>>>(q.start, nc, toff, tiles);
+    tile_write_kernel<<<nb, 256, 0, st>>>(q.start, nc, cell2, toff, tiles);
     uint32_t total = 0;
     if (hipMemcpyAsync(&total, toff + nc, sizeof(uint32_t), hipMemcpyDeviceToHost, st) != hipSuccess ||
         hipStreamSynchronize(st) != hipSuccess || hipGetLastError() != hipSuccess)

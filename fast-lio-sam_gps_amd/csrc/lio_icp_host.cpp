@@ -729,7 +729,7 @@ static int icp_prepare(lio_icp* h) {
         // query's 1-NN is exact whatever tile it is in)
         int rc = lio::grid_build(h->qgrid, h->d_src, h->sh_n, h->tile_cell, h->st);
         if (rc) return ifail(rc == -5 ? LIO_ERR_NOMEM : LIO_ERR_HIP, "source binning failed");
-        const int64_t need = 2 * ((int64_t)h->qgrid.geom.ncells + 1);
+        const int64_t need = 6 * ((int64_t)h->qgrid.geom.ncells + 1);  // icp_build_tiles' scratch
         if (need > h->tscratch_cap) {
             if (h->d_tscratch) IHIP(hipFree(h->d_tscratch));
             h->d_tscratch = nullptr;

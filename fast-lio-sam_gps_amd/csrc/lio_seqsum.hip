@@ -162,7 +162,16 @@ __device__ __forceinline__ void predict(const Src& src, const SeqSumBuf& b, int 
         const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
         if (lane == 63) s_last[w] = in.e[kSeqPer - 1];
         __syncthreads();
-        if (lane == 0) prev = w > 0 ? s_last[w - 1] : binade_pred_abs((float)bo, kPredSlack1, dl);
+        if (lane == 0) {
+            if (w > 0) {
+                prev = s_last[w - 1];
+            } else if (blk > 0) {  // the previous block's last prediction, as that block computed it
+                const size_t pb = (size_t)c * b.nblk + blk - 1;
+                prev = binade_pred_abs((float)(b.boff[pb] + b.bsum[pb]), kPredSlack1, b.bdelta[pb]);
+            } else {
+                prev = binade_pred_abs((float)bo, kPredSlack1, dl);
+            }
+        }
         __syncthreads();
         in.ep = prev;
     } else {
@@ -239,8 +248,9 @@ __global__ void __launch_bounds__(256) seq_scan1(SeqSumBuf b, const uint32_t* d_
     const int c = blockIdx.x;
     const int64_t n = *d_n;
     const int nb = (int)((n + kSeqBlock - 1) / kSeqBlock);
-    double off = 0.0, mb = 0.0;  // lane 0's running values
+    double off = 0.0, mb = 0.0;  // the offsets carried over windows (every thread's copy); this thread's max
     double var = 0.0;            // every thread's copy of the allowance's running variance
+    constexpr int kPerT = kScanWin / 256;
     for (int w0 = 0; w0 < nb; w0 += kScanWin) {
         const int m = min(kScanWin, nb - w0);
         for (int j = threadIdx.x; j < m; j += blockDim.x) {
@@ -248,16 +258,34 @@ __global__ void __launch_bounds__(256) seq_scan1(SeqSumBuf b, const uint32_t* d_
             s_abs[j] = b.babs[(size_t)c * b.nblk + w0 + j];
         }
         __syncthreads();
-        if (threadIdx.x == 0)
-            for (int j = 0; j < m; ++j) {
-                s_off[j] = off;
-                mb = fmax(mb, fabs(off) + s_abs[j]);
-                off = off + s_sum[j];
+        // block offsets by a block prefix (thread t: blocks t kPerT .. +kPerT-1 in order, then the threads' runs
+        // in a fixed order): deterministic, and every kernel reads these stored offsets, so the predictions agree
+        // between seq_count / seq_events / seq_verify (predict() takes a block's first predecessor from
+        // boff[b-1] + bsum[b-1], the previous block's own last prediction)
+        {
+            double loc[kPerT], run = 0.0;
+#pragma unroll
+            for (int i = 0; i < kPerT; ++i) {
+                const int j = (int)threadIdx.x * kPerT + i;
+                loc[i] = run;  // exclusive within the thread
+                run = run + (j < m ? s_sum[j] : 0.0);
             }
+            double tot;
+            const double ex = block_excl(run, s_vw, tot);
+#pragma unroll
+            for (int i = 0; i < kPerT; ++i) {
+                const int j = (int)threadIdx.x * kPerT + i;
+                if (j < m) {
+                    const double o = off + (ex + loc[i]);
+                    s_off[j] = o;
+                    mb = fmax(mb, fabs(o) + s_abs[j]);
+                }
+            }
+            off = off + tot;
+        }
         __syncthreads();
         // the allowance off lane 0's chain: every thread its kScanWin / 256 consecutive blocks, one block prefix
         {
-            constexpr int kPerT = kScanWin / 256;
             double loc[kPerT], run = 0.0;
 #pragma unroll
             for (int i = 0; i < kPerT; ++i) {
@@ -282,6 +310,15 @@ __global__ void __launch_bounds__(256) seq_scan1(SeqSumBuf b, const uint32_t* d_
             b.bdelta[(size_t)c * b.nblk + w0 + j] = s_dl[j];
         }
         __syncthreads();
+    }
+    // the bound's max over the threads (max: any order is exact)
+    {
+        __shared__ double s_mb[256 / 64];
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) mb = fmax(mb, __shfl_xor(mb, d, 64));
+        if ((threadIdx.x & 63) == 0) s_mb[threadIdx.x >> 6] = mb;
+        __syncthreads();
+        mb = fmax(fmax(s_mb[0], s_mb[1]), fmax(s_mb[2], s_mb[3]));
     }
     if (threadIdx.x == 0) {
         // |s_k| < 2^(ilogb(mb) + 2) with a binade of margin for the float chain's own drift; a run's sum

@@ -25,7 +25,10 @@
 namespace lio {
 
 constexpr int kSeqThreads = 256;                 // threads per block
-constexpr int kSeqPer = 4;                       // consecutive elements per thread
+#ifndef LIO_SEQ_PER
+#define LIO_SEQ_PER 4  // A/B builds
+#endif
+constexpr int kSeqPer = LIO_SEQ_PER;             // consecutive elements per thread
 constexpr int kSeqBlock = kSeqThreads * kSeqPer;  // elements per block
 constexpr int kSeqMaxChains = 9;
 
