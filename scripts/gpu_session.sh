@@ -112,8 +112,10 @@ for s in $STEPS; do
     knn5)  runs pytest_knn5 900 python -u -m pytest tests/test_gpu_parity.py tests/test_golden.py tests/test_properties.py tests/test_gpu_map.py tests/test_gpu_fullsize.py tests/test_cpp_api.py -k "not icp" -m gpu -x -v -p no:cacheprovider --timeout 600 --timeout-method thread ;;
     near5) run near5 600 bash -c 'for r in 1 2; do for c in C3 C2; do python scripts/near_ab.py $c && LIO_KNN_NEAR=cell python scripts/near_ab.py $c || exit $?; done; done' ;;
     cpps)  runs pytest_cpps 900 python -u -m pytest tests/test_cpp_stream.py tests/test_cpp_api.py -x -v -s -p no:cacheprovider --timeout 800 --timeout-method thread ;;
-    mortab) run mortab 600 bash -c 'for r in 1 2; do for v in default cellorder; do if [ $v = default ]; then L=""; else L=fast-lio-sam_gps_amd/build_ab/$v/liblio_gpu.so; fi; LIO_GPU_LIB=$L LIO_ICP_ORDER=-1 python scripts/icp_ab.py 1.0 5 && LIO_GPU_LIB=$L python scripts/icp_ab.py 1.0 5 || exit $?; echo "^ $v round $r"; done; done' ;;
-    libab) run libab 900 bash -c 'for r in 1 2; do for v in default $LIBAB; do if [ $v = default ]; then L=""; else L=fast-lio-sam_gps_amd/build_ab/$v/liblio_gpu.so; fi; LIO_GPU_LIB=$L python scripts/icp_ab.py 1.0 5 || exit $?; echo "^ $v round $r"; done; done' ;;
+    mortab) run mortab 600 bash -c 'for r in 1 2; do for v in default cellorder; do if [ $v = default ]; then L=""; else L=fast-lio-sam_gps_amd/build_ab/$v/liblio_gpu.so; fi; LIO_GPU_LIB=$L LIO_ICP_ORDER=-1 python scripts/icp_ab.py 1.0 5 && LIO_GPU_LIB=$L python scripts/icp_ab.py 1.0 5 && LIO_GPU_LIB=$L LIO_ICP_ORDER=-1 python scripts/icp_ab.py 1.0 5 || exit $?; echo "^ $v round $r"; done; done' ;;
+    libab) run libab 900 bash -c 'for r in 1 2; do for v in default $LIBAB; do if [ $v = default ]; then L=""; else L=fast-lio-sam_gps_amd/build_ab/$v/liblio_gpu.so; fi; LIO_GPU_LIB=$L python scripts/icp_ab.py 1.0 5 && LIO_GPU_LIB=$L LIO_ICP_ORDER=-1 python scripts/icp_ab.py 1.0 5 || exit $?; echo "^ $v round $r"; done; done' ;;
+    abprof) run abprof_default 300 rocprofv3 --kernel-trace --stats -d "$OUT/abprof_default" -o run --output-format csv -- python scripts/icp_ab.py 1.0 3 &&
+            LIO_GPU_LIB=fast-lio-sam_gps_amd/build_ab/$LIBAB/liblio_gpu.so run abprof_ab 300 rocprofv3 --kernel-trace --stats -d "$OUT/abprof_ab" -o run --output-format csv -- python scripts/icp_ab.py 1.0 3 ;;
     *) echo "unknown step $s" ;;
     esac
 done
