@@ -605,30 +605,36 @@ inline void inverse4(const double m[16], double inv[16]) {
     inv[15] = (m[8] * s3 - m[9] * s1 + m[10] * s0) * id;
 }
 
+// loop_closure.cpp:18-40 (host logic): among keyframes[0 .. size-2] the closest (translation of
+// pose_corrected_eig_) within loop_detection_radius_ and more than loop_detection_timediff_threshold_ older;
+// its idx_, or -1
+inline int fetch_closest_keyframe_idx(const LoopClosureConfig& config, const PosePcd& query_keyframe,
+                                      const std::vector<PosePcd>& keyframes) {
+    const double radi = config.loop_detection_radius_;
+    double shortest = radi * 3.0;
+    int closest = -1;
+    const double* q = query_keyframe.pose_corrected_eig_;
+    for (size_t i = 0; i + 1 < keyframes.size(); ++i) {
+        const double* p = keyframes[i].pose_corrected_eig_;
+        const double dx = p[3] - q[3], dy = p[7] - q[7], dz = p[11] - q[11];
+        const double d = std::sqrt(dx * dx + dy * dy + dz * dz);
+        if (radi > d && config.loop_detection_timediff_threshold_ < query_keyframe.timestamp_ - keyframes[i].timestamp_ &&
+            d < shortest) {
+            shortest = d;
+            closest = keyframes[i].idx_;
+        }
+    }
+    return closest;
+}
+
 // LoopClosure (loop_closure.h:39-70): the loop leg with the GPU submap assembly and ICP behind it
 class LoopClosure {
 public:
     explicit LoopClosure(const LoopClosureConfig& config, int device = 0, int umeyama = LIO_ICP_UMEYAMA_DEFAULT)
         : config_(config), f_(device), icp_(config, device, 1.0f, umeyama) {}
 
-    // loop_closure.cpp:18-40: among keyframes[0 .. size-2] the closest (translation of pose_corrected_eig_)
-    // within loop_detection_radius_ and more than loop_detection_timediff_threshold_ older; -1 if none
     int fetchClosestKeyframeIdx(const PosePcd& query_keyframe, const std::vector<PosePcd>& keyframes) const {
-        const double radi = config_.loop_detection_radius_;
-        double shortest = radi * 3.0;
-        int closest = -1;
-        const double* q = query_keyframe.pose_corrected_eig_;
-        for (size_t i = 0; i + 1 < keyframes.size(); ++i) {
-            const double* p = keyframes[i].pose_corrected_eig_;
-            const double dx = p[3] - q[3], dy = p[7] - q[7], dz = p[11] - q[11];
-            const double d = std::sqrt(dx * dx + dy * dy + dz * dz);
-            if (radi > d && config_.loop_detection_timediff_threshold_ < query_keyframe.timestamp_ - keyframes[i].timestamp_ &&
-                d < shortest) {
-                shortest = d;
-                closest = keyframes[i].idx_;
-            }
-        }
-        return closest;
+        return fetch_closest_keyframe_idx(config_, query_keyframe, keyframes);
     }
 
     // loop_closure.cpp:42-67: per side, transformPcd of keyframes [idx - range, idx + range] (never the newest:

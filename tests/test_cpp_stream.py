@@ -35,6 +35,40 @@ def test_c5_stream_driver_compiles(tmp_path):
     assert r.returncode == 0, r.stderr[-4000:]
 
 
+def test_host_glue_matches_python(tmp_path):
+    """odom_matrix (bit for bit), inverse4 (within 1e-15 of numpy's inverse) and fetch_closest_keyframe_idx
+    of the C++ header against the Python glue — host code only, no GPU."""
+    import re
+
+    from lio_gpu import loop_closure as LC
+
+    exe = str(tmp_path / "glue")
+    cmd = ["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-Wall", "-Wextra", "-Werror",
+           "-I", os.path.join(ROOT, "include"), os.path.join(ROOT, "tests", "cpp", "test_host_glue.cpp"), "-o", exe,
+           "-L", LIBDIR, "-llio_gpu", "-Wl,-rpath," + LIBDIR, "-Wl,-rpath-link,/opt/rocm/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+    out = subprocess.run([exe], capture_output=True, text=True, timeout=60).stdout
+    T = np.array([float(v) for v in re.findall(r"^T \d+ (\S+)$", out, re.M)]).reshape(4, 4)
+    Ic = np.array([float(v) for v in re.findall(r"^I \d+ (\S+)$", out, re.M)]).reshape(4, 4)
+    st = dict(rot=np.array([0.9238795325112867, 0.0123, -0.0456, 0.3826834323650898]), pos=np.array([12.5, -3.25, 0.75]))
+    np.testing.assert_array_equal(T, PL.odom_matrix(st))
+    np.testing.assert_allclose(Ic, np.linalg.inv(T), rtol=0, atol=1e-14)
+    np.testing.assert_allclose(Ic @ T, np.eye(4), rtol=0, atol=1e-14)
+    kfs = []
+    for k in range(8):
+        P = np.eye(4)
+        P[0, 3] = 3.7 * k if k < 4 else 3.7 * (7 - k) + 1.5
+        P[1, 3] = 0.0 if k < 4 else -0.3
+        kfs.append(LC.PosePcd(pcd_=np.zeros((0, 4), np.float32), pose_corrected_eig_=P,
+                              timestamp_=0.1 * k if k < 4 else 40.0 + 0.1 * (k - 4), idx_=k))
+    lco = LC.LoopClosure.__new__(LC.LoopClosure)  # host logic only: no handle
+    lco.config_ = LC.LoopClosureConfig()
+    want = lco.fetchClosestKeyframeIdx(kfs[-1], kfs)
+    assert int(re.search(r"^closest (-?\d+)$", out, re.M).group(1)) == want == 0
+    assert int(re.search(r"^closest_early (-?\d+)$", out, re.M).group(1)) == lco.fetchClosestKeyframeIdx(kfs[3], kfs[:4]) == -1
+
+
 def test_stream_io_round_trip(tmp_path):
     """The input writer's layout (read back field by field) — host glue only."""
     import struct
