@@ -313,19 +313,52 @@ __device__ __forceinline__ void icp_tile_body(const IcpArgs& a, int tix, TileLds
 #ifdef LIO_DIAG
     const uint64_t t_start = wall_clock64();  // per-tile timeline (diagnostics build)
 #endif
+    // The pass's point from the binned source point (its coordinates are the source's, w its index) and the
+    // transforms applied so far: PCL transforms its cloud in place once per iteration (float, SSE order), so
+    // applying the history in order gives the stored cloud's bits without gathering it by index.  The history
+    // goes through LDS (its loads beside the head's own: a CU's first scalar reads would miss, the previous
+    // pass wrote it); x, y, z, id of the staging area are 1024 contiguous floats, free until the first round.
+    const bool lds_hist = NW == 1 && !a.fitness && a.nT > 0 && a.nT <= 64;
+    float hv[16];
+    if (lds_hist) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int t = r * 64 + lane;
+            hv[r] = t < a.nT * 16 ? a.thist[t] : 0.f;
+        }
+    }
     const uint2 tl = a.tiles[tix];
     const bool act = lane < (int)tl.y;
-    const int i = act ? __float_as_int(a.qpts[tl.x + lane].w) : 0;
+    const float4 q = act ? a.qpts[tl.x + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const int i = act ? __float_as_int(q.w) : 0;
+    const float* hist = a.thist;
+    if (lds_hist) {
+        float* sh = reinterpret_cast<float*>(&L);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int t = r * 64 + lane;
+            if (t < a.nT * 16) sh[t] = hv[r];
+        }
+        wave_sync();
+        hist = sh;
+    }
     float x = 0.f, y = 0.f, z = 0.f;
     int prior = -1;
     if (act) {
         if (a.prior) prior = a.nn_id[i];
         if (a.fitness) {  // getFitnessScore: original source * final; kept in cur for `aligned_`
-            xform_pcl(a.T, a.src[3 * i], a.src[3 * i + 1], a.src[3 * i + 2], x, y, z);
+            xform_pcl(a.T, q.x, q.y, q.z, x, y, z);
         } else {
-            x = a.cur[3 * i];
-            y = a.cur[3 * i + 1];
-            z = a.cur[3 * i + 2];
+            x = q.x;
+            y = q.y;
+            z = q.z;
+            for (int k = 0; k < a.nT; ++k) {
+                float ox, oy, oz;
+                xform_pcl(hist + 16 * k, x, y, z, ox, oy, oz);
+                x = ox;
+                y = oy;
+                z = oz;
+            }
             if (a.apply_T) {
                 float ox, oy, oz;
                 xform_pcl(a.T, x, y, z, ox, oy, oz);
@@ -335,6 +368,9 @@ __device__ __forceinline__ void icp_tile_body(const IcpArgs& a, int tix, TileLds
             }
         }
     }
+    if (lds_hist) wave_sync();  // every lane has read the history before the staging rounds overwrite it
+    // this pass's T joins the history of the later passes
+    if (a.apply_T && !a.fitness && tix == 0 && lane < 16) a.thist[16 * a.nT + lane] = a.T[lane];
     const GridDev& g = a.grid;
     uint64_t best = knn_key(INFINITY, kNone);
     if (prior >= 0 && prior != kNone) {  // the previous correspondence: an exact candidate

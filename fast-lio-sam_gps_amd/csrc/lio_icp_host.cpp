@@ -306,6 +306,8 @@ struct lio_icp {
     int64_t sh_begin = 0, sh_n = 0, cap = 0;
     float* d_src = nullptr;
     float* d_cur = nullptr;
+    float* d_thist = nullptr;  // transforms applied this alignment (the correspondence kernel's history)
+    int thist_cap = 0, nT = 0;
     float* d_fd2 = nullptr;
     int* d_fid = nullptr;
     lio::GridBuf qgrid;      // the shard's source binned by tile cell (icp_build_tiles)
@@ -443,7 +445,7 @@ int lio_icp_destroy(lio_icp* h) {
     lio_icp_set_exchange_owner(h, nullptr, nullptr);
     lio::grid_free(h->tgt);
     lio::grid_free(h->qgrid);
-    void* ptrs[] = {h->d_tgt,  h->d_src,   h->d_cur,    h->d_fd2,   h->d_fid,  h->d_tiles, h->d_tscratch,
+    void* ptrs[] = {h->d_thist, h->d_tgt,  h->d_src,   h->d_cur,    h->d_fd2,   h->d_fid,  h->d_tiles, h->d_tscratch,
                     h->d_ttmp, h->d_dbg,   h->d_tcost,  h->d_order, h->d_pcl16, h->d_srcf,  h->d_curf,
                     h->d_gid};
     for (void* q : ptrs)
@@ -821,6 +823,9 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     a.tgt_by_id = h->tgt.by_id;
     a.cur = shard_cur(h);
     a.src = h->d_src;
+    a.thist = h->d_thist;
+    a.nT = h->nT;
+    if (!fitness && apply_T && h->nT >= h->thist_cap) return ifail(LIO_ERR_STATE, "lio_icp_align: transform history full");
     a.n = (int)h->sh_n;
     a.apply_T = apply_T ? 1 : 0;
     std::memcpy(a.T, T, sizeof(a.T));
@@ -903,6 +908,7 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     }
     h->have_prior = true;
     if (!fitness && h->sh_n > 0) h->have_order = true;
+    if (!fitness && apply_T) ++h->nT;
 #ifdef LIO_DIAG
     if (dbg_on) {
         unsigned long long c[5];
@@ -1136,6 +1142,15 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
     } else if (h->sh_n > 0) {
         IHIP(hipMemcpyAsync(h->d_cur, h->d_src, h->sh_n * 3 * sizeof(float), hipMemcpyDeviceToDevice, h->st));
     }
+    const int hist_need = std::max(h->p.max_iter, 1) + 4;  // one T per iteration plus the guess
+    if (hist_need > h->thist_cap) {
+        if (h->d_thist) IHIP(hipFree(h->d_thist));
+        h->d_thist = nullptr;
+        h->thist_cap = 0;
+        IHIP(hipMalloc(&h->d_thist, (size_t)hist_need * 16 * sizeof(float)));
+        h->thist_cap = hist_need;
+    }
+    h->nT = 0;
     h->have_prior = false;
     h->have_order = false;  // every alignment starts in cell order (its first pass measures the tiles)
     const double max_d2 = h->p.max_corr_dist * h->p.max_corr_dist;

@@ -132,8 +132,13 @@ void grid_insert_ids(GridBuf& g, int64_t id0, const uint32_t* d_nnew, int n_max,
 struct IcpArgs {
     GridDev grid;
     const float4* tgt_by_id;
-    float* cur;          // n*3 incrementally transformed source (this rank's shard)
-    const float* src;    // n*3 original source (fitness pass)
+    float* cur;          // n*3 incrementally transformed source (this rank's shard): written by the correspondence
+                         // kernel for the statistics / compaction of the same pass
+    const float* src;    // n*3 original source
+    float* thist;        // the transforms applied before this pass (nT x 16 floats): the correspondence kernel
+                         // rebuilds its current point from the binned source point with them (no per-pass
+                         // gather of cur) and appends this pass's T
+    int nT;
     int n;               // points in this shard
     int apply_T;         // apply T (float 4x4 row-major) to cur before the NN (incremental transform)
     float T[16];
