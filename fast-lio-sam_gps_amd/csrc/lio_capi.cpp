@@ -1189,7 +1189,7 @@ static int64_t select_rows(const float* __restrict__ raw, int64_t n, int every, 
 // Large sweeps are packed by the host pool in up to kStageChunks contiguous pieces, each at its own offset
 // of the staging buffer (the upper bound of its rows): the plan lists them, and the caller moves each
 // piece with its own DMA to where the concatenation puts it.
-constexpr int kStageChunks = 4;
+constexpr int kStageChunks = lio::kMaxPieces;
 struct StagePlan {
     int pieces = 0;
     int64_t src_row[kStageChunks] = {};  // first staging row of the piece
@@ -1215,7 +1215,7 @@ static int stage_sweep_select(lio::FilterBuf& b, const float* raw, int64_t n, in
     }
     const float blind2 = p->blind * p->blind;
     auto* d = static_cast<float*>(b.h_stage);
-    const int pieces = ub >= 16384 ? kStageChunks : 1;
+    const int pieces = ub >= 16384 ? std::min(kStageChunks, lio::HostPool::get().threads()) : 1;
     const int64_t per = (ub + pieces - 1) / pieces;  // candidate rows per piece
     int64_t k[kStageChunks] = {};
     bool srt[kStageChunks] = {};

@@ -389,7 +389,7 @@ constexpr uint32_t kNotSelected = 0xffffffffu;
 __device__ __forceinline__ uint32_t piece_row(const RowPieces& m, uint32_t i) {
     uint32_t base = m.src[0], s0 = m.start[0];
 #pragma unroll
-    for (int t = 1; t < 4; ++t)
+    for (int t = 1; t < kMaxPieces; ++t)
         if (t < m.n && i >= m.start[t]) base = m.src[t], s0 = m.start[t];
     return base + (i - s0);
 }

@@ -38,10 +38,11 @@ struct UndistortEnd {
 // Where the host packed the selected rows: logical row i of piece t (start[t] <= i < start[t + 1]) lives at
 // staged row src[t] + (i - start[t]) (the pieces were packed in parallel, each at its own offset, and go
 // to the device in one DMA with the gaps).  n = 1, start = src = 0: rows in place.
+constexpr int kMaxPieces = 8;
 struct RowPieces {
     int n = 1;
-    uint32_t start[4] = {0, 0, 0, 0};
-    uint32_t src[4] = {0, 0, 0, 0};
+    uint32_t start[kMaxPieces] = {};
+    uint32_t src[kMaxPieces] = {};
 };
 
 struct ScanPrepParams {

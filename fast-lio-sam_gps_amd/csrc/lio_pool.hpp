@@ -4,6 +4,7 @@
 #pragma once
 #include <atomic>
 #include <condition_variable>
+#include <cstdlib>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -14,7 +15,12 @@ namespace lio {
 class HostPool {
   public:
     static HostPool& get() {
-        static HostPool pool(3);  // + the calling thread: 4 share a job
+        // + the calling thread: 4 share a job by default; LIO_HOST_THREADS (1..16) sets the total (A/B)
+        static HostPool pool([] {
+            const char* e = std::getenv("LIO_HOST_THREADS");
+            const int t = e ? std::atoi(e) : 4;
+            return (t >= 1 && t <= 16 ? t : 4) - 1;
+        }());
         return pool;
     }
     int threads() const { return (int)workers_.size() + 1; }
