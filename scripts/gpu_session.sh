@@ -117,6 +117,7 @@ for s in $STEPS; do
     abprof) run abprof_default 300 rocprofv3 --kernel-trace --stats -d "$OUT/abprof_default" -o run --output-format csv -- python scripts/icp_ab.py 1.0 3 &&
             LIO_GPU_LIB=fast-lio-sam_gps_amd/build_ab/$LIBAB/liblio_gpu.so run abprof_ab 300 rocprofv3 --kernel-trace --stats -d "$OUT/abprof_ab" -o run --output-format csv -- python scripts/icp_ab.py 1.0 3 ;;
     cppprof) run cpp_prof 400 python scripts/cpp_stream_profile.py 3 ;;
+    hwq)   run hwq 900 python scripts/hwq_ab.py ;;
     *) echo "unknown step $s" ;;
     esac
 done
