@@ -6,7 +6,7 @@
 //   seq_count    per element: predicted binade, event flag, fixed-point increment -> block totals
 //   seq_scan2    per chain: exclusive block offsets of increments and events
 //   seq_events   the events in element order: position, increment prefix, x
-//   seq_walk     one wave per chain replays the events (run sums exact in double) -> event results, sum
+//   seq_walk     one block per chain replays the events (run sums exact in double) -> event results, sum
 //   seq_verify   every s_k rebuilt from the events; s_k == fl(s_{k-1} + x_k) checked for every k
 #include "lio_seqsum.hpp"
 
@@ -446,22 +446,62 @@ __global__ void __launch_bounds__(kSeqThreads) seq_events(Src src, SeqSumBuf b, 
         }
 }
 
-// one wave per chain: s_{event-1} = s_{previous event} + run sum (exact double), s_event = fl(that + x_event).
-// The chain of adds is the serial floor; everything else is kept off it: a batch of 64 events' run sums and
-// values goes through LDS first, the next kWalkU of them are read (broadcast) before their dependent adds, so
-// an event costs its two conversions and two adds, not a cross-lane read each.  Full batches run without a
-// per-event guard and each lane picks its own event's s with a select beside the chain; the next batch's
-// records are loaded while this one's chain runs.
+// The walk: s_{event-1} = s_{previous event} + run sum R (exact), s_event = fl(s_{event-1} + x_event), one chain
+// per block.  The chain of dependent operations is the serial floor; everything else is kept off it:
+//   * the event records stream through LDS in chunks of kWalkChunk, double-buffered: while wave 0 walks chunk k,
+//     waves 1-3 prepare chunk k+1 (run sums from the increment prefixes, the fast-path test) and store chunk
+//     k-1's results, so the walk never waits on a global load;
+//   * fast groups: when every run sum R of a 64-event group is a float exactly (tested while preparing), the
+//     chain stays in float, two dependent adds per event: s_{event-1} = fl32(s + R) and s_event = fl32(that + x).
+//     That is the general form's value bit for bit: fl32(fl64(s + R)) = fl32(s + R) for the two binary32
+//     operands (53 >= 2 * 24 + 2: double rounding is innocuous for a sum), and when the increments are right
+//     s + R is the float s_{event-1} itself;
+//   * other groups (a run spanning more than 24 bits of the chain's fixed-point unit) take the general form,
+//     fl32(fl32(fl64(s + R)) + x).  seq_verify checks every element either way.
+constexpr int kWalkThreads = 256;
+constexpr int kWalkChunk = 1024;  // events per LDS chunk (x 2 buffers x 20 bytes)
 constexpr int kWalkU = 8;
+struct WalkChunk {
+    double R[kWalkChunk];  // run sums (exact)
+    float Rf[kWalkChunk];  // the same as floats (fast groups)
+    float x[kWalkChunk];
+    float f[kWalkChunk];   // the walk's results
+    int fast[kWalkChunk / 64];
+};
+
+// chunk k's records into B by the threads [t0, t0 + nt) (nt a multiple of 64, t0 wave-aligned)
+__device__ __forceinline__ void walk_prepare(WalkChunk& B, int k, int nev, double unit, const uint64_t* EP,
+                                             const float* EX, int t, int nt) {
+    const int e0 = k * kWalkChunk;
+    const int m = min(kWalkChunk, nev - e0);
+    for (int j = t; j < kWalkChunk; j += nt) {  // wave-uniform trip count: one 64-event group per wave and step
+        const int i = e0 + j;
+        double R = 0.0;
+        float X = 0.f;
+        if (j < m) {
+            const uint64_t P = EP[i];
+            const uint64_t Pp = i > 0 ? EP[i - 1] : 0;
+            R = (double)(int64_t)(P - Pp) * unit;  // a run sum: exact (<= 53 significant bits)
+            X = EX[i];
+        }
+        const float Rf = (float)R;
+        B.R[j] = R;
+        B.Rf[j] = Rf;
+        B.x[j] = X;
+        // a float exactly, and normal or zero (no denormal operand on the fast path)
+        const uint64_t all = __ballot((double)Rf == R && (Rf == 0.f || fabsf(Rf) >= 1.17549435e-38f));
+        if ((threadIdx.x & 63) == 0) B.fast[j >> 6] = all == ~0ull;
+    }
+}
+
 template <class Src>
-__global__ void __launch_bounds__(64) seq_walk(Src src, SeqSumBuf b, const uint32_t* d_n) {
-    __shared__ double s_R[64 + kWalkU];  // + the slack the unrolled reads of the last step may touch
-    __shared__ float s_x[64 + kWalkU];
+__global__ void __launch_bounds__(kWalkThreads) seq_walk(Src src, SeqSumBuf b, const uint32_t* d_n) {
+    __shared__ WalkChunk wb[2];
     const int c = blockIdx.x;
-    const int lane = threadIdx.x;
+    const int t = threadIdx.x, w = t >> 6;
     const int64_t n = *d_n;
     if (n <= 0) {
-        if (lane == 0) b.result[c] = 0.f;
+        if (t == 0) b.result[c] = 0.f;
         return;
     }
     if ((b.status[1] >> c) & 1u) return;  // event overflow: the caller falls back
@@ -470,54 +510,74 @@ __global__ void __launch_bounds__(64) seq_walk(Src src, SeqSumBuf b, const uint3
     const uint64_t* EP = b.ev_P + (size_t)c * b.evcap;
     const float* EX = b.ev_x + (size_t)c * b.evcap;
     float* ES = b.ev_s + (size_t)c * b.evcap;
-    double s = (double)src(c, 0);
-    uint64_t Pbase = 0;
-    // the next batch's event records are loaded while this batch's chain runs
-    uint64_t Pn = lane < nev ? EP[lane] : 0;
-    float Xn = lane < nev ? EX[lane] : 0.f;
-    for (int base = 0; base < nev; base += 64) {
-        const int i = base + lane;
-        const bool ok = i < nev;
-        const uint64_t P = Pn;
-        const float X = Xn;
-        const int inext = i + 64;
-        Pn = inext < nev ? EP[inext] : 0;
-        Xn = inext < nev ? EX[inext] : 0.f;
-        uint64_t Pp = __shfl_up(P, 1, 64);
-        if (lane == 0) Pp = Pbase;
-        s_R[lane] = (double)(int64_t)(P - Pp) * unit;  // a run sum: exact (<= 53 significant bits)
-        s_x[lane] = ok ? X : 0.f;
-        __syncthreads();
-        const int cnt = min(64, nev - base);
-        float myf = 0.f;  // lane k keeps the batch's k-th s_event (a select beside the chain, not on it)
-        if (cnt == 64) {  // full batches: no per-event guard
-            for (int l = 0; l < 64; l += kWalkU) {
-                double r[kWalkU];
-                float x[kWalkU];
+    const int nchunk = (nev + kWalkChunk - 1) / kWalkChunk;
+    float s = src(c, 0);  // the chain (lane 0 of wave 0)
+    if (nchunk > 0) walk_prepare(wb[0], 0, nev, unit, EP, EX, t, kWalkThreads);
+    __syncthreads();
+    for (int k = 0; k < nchunk; ++k) {
+        if (w == 0) {
+            if (t == 0) {
+                WalkChunk& B = wb[k & 1];
+                const int m = min(kWalkChunk, nev - k * kWalkChunk);
+                for (int g = 0; g < m; g += 64) {
+                    const int cnt = min(64, m - g);
+                    if (cnt == 64 && B.fast[g >> 6]) {
+                        for (int l = g; l < g + 64; l += kWalkU) {
+                            float r[kWalkU], x[kWalkU];
 #pragma unroll
-                for (int u = 0; u < kWalkU; ++u) {
-                    r[u] = s_R[l + u];
-                    x[u] = s_x[l + u];
-                }
+                            for (int u = 0; u < kWalkU; ++u) {
+                                r[u] = B.Rf[l + u];
+                                x[u] = B.x[l + u];
+                            }
 #pragma unroll
-                for (int u = 0; u < kWalkU; ++u) {
-                    const float f = (float)(s + r[u]) + x[u];  // s + r is the float s_{event-1}; the event rounds once
-                    s = (double)f;
-                    myf = (lane == l + u) ? f : myf;
+                            for (int u = 0; u < kWalkU; ++u) {
+                                s = (s + r[u]) + x[u];
+                                B.f[l + u] = s;
+                            }
+                        }
+                    } else if (cnt == 64) {
+                        for (int l = g; l < g + 64; l += kWalkU) {
+                            double r[kWalkU];
+                            float x[kWalkU];
+#pragma unroll
+                            for (int u = 0; u < kWalkU; ++u) {
+                                r[u] = B.R[l + u];
+                                x[u] = B.x[l + u];
+                            }
+#pragma unroll
+                            for (int u = 0; u < kWalkU; ++u) {
+                                s = (float)((double)s + r[u]) + x[u];
+                                B.f[l + u] = s;
+                            }
+                        }
+                    } else {
+                        for (int l = g; l < g + cnt; ++l) {
+                            s = (float)((double)s + B.R[l]) + B.x[l];
+                            B.f[l] = s;
+                        }
+                    }
                 }
             }
         } else {
-            for (int l = 0; l < cnt; ++l) {
-                const float f = (float)(s + s_R[l]) + s_x[l];
-                s = (double)f;
-                myf = (lane == l) ? f : myf;
+            if (k + 1 < nchunk) walk_prepare(wb[(k + 1) & 1], k + 1, nev, unit, EP, EX, t - 64, kWalkThreads - 64);
+            if (k > 0) {  // chunk k-1's results (its buffer's f: the preparation above writes only R, Rf, x)
+                const WalkChunk& B = wb[(k - 1) & 1];
+                const int e0 = (k - 1) * kWalkChunk;
+                for (int j = t - 64; j < kWalkChunk; j += kWalkThreads - 64) ES[e0 + j] = B.f[j];
             }
         }
-        if (ok) ES[i] = myf;
-        Pbase = __shfl(P, cnt - 1, 64);
-        __syncthreads();  // the next batch overwrites s_R / s_x
+        __syncthreads();
     }
-    if (lane == 0) b.result[c] = (float)(s + (double)(int64_t)(b.ptot[c] - Pbase) * unit);
+    if (nchunk > 0) {
+        const WalkChunk& B = wb[(nchunk - 1) & 1];
+        const int e0 = (nchunk - 1) * kWalkChunk;
+        const int m = nev - e0;
+        for (int j = t; j < m; j += kWalkThreads) ES[e0 + j] = B.f[j];
+    }
+    if (t == 0) {
+        const uint64_t Plast = nev > 0 ? EP[nev - 1] : 0;
+        b.result[c] = (float)((double)s + (double)(int64_t)(b.ptot[c] - Plast) * unit);
+    }
 }
 
 // s_k for every element from the events; checks s_k == fl(s_{k-1} + x_k); stores the reconstruction
@@ -612,7 +672,7 @@ void seqsum_launch_impl(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf&
     seq_count<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
     seq_scan2<<<nch, kSeqThreads, 0, st>>>(b, d_n);
     seq_events<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
-    seq_walk<Src><<<nch, 64, 0, st>>>(src, b, d_n);
+    seq_walk<Src><<<nch, kWalkThreads, 0, st>>>(src, b, d_n);
     seq_verify<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
 }
 

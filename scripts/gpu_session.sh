@@ -87,6 +87,7 @@ for s in $STEPS; do
            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d "$OUT/pmc_write" -o run --output-format csv \
                -- python bench.py --steps 30 --warmup 3 --no-cpu --no-icp --streams '' --pipeline 0 ;;
     pmcicp) run pmc_icp 900 bash scripts/pmc_icp.sh "$TAG/pmcicp" ;;
+    pmcfid) PMC_SCRIPT="scripts/icp_ab.py 1.0 1" PMC_FILTER="seq_|pcl_" run pmc_fid 900 bash scripts/pmc_icp.sh "$TAG/pmcfid" ;;
     fullsize) run pytest_fullsize 900 python -u -m pytest tests/test_gpu_fullsize.py -x -v -s -p no:cacheprovider --timeout 600 --timeout-method thread ;;
     icptest) runs pytest_icp 600 python -u -m pytest tests/test_gpu_icp.py tests/test_gpu_parity.py -k icp -x -v -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     icppmc2) run icp_trace 300 rocprofv3 --kernel-trace -d "$OUT/icptrace" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&

@@ -1,6 +1,8 @@
 #!/bin/bash
 # PMC passes over the ICP (C4) workload (one rocprofv3 run per pass; no
 # --pmc is ever combined with sys/runtime tracing).  Usage: scripts/pmc_icp.sh TAG [CFG unused] [CELL]
+# PMC_SCRIPT (default scripts/icp_cells.py CELL) and PMC_FILTER (kernel-name regex, default icp) select
+# another workload, e.g. the fidelity statistics: PMC_SCRIPT="scripts/icp_ab.py 1.0 1" PMC_FILTER="seq_|pcl_"
 set -u
 TAG=${1:-pmc}; CFG=${2:-C2}; CELL=${3:-1.0}
 OUT=gpurun_out/$TAG
@@ -12,7 +14,7 @@ while read -r ctrs; do
     i=$((i + 1))
     echo "== pass $i: $ctrs"
     timeout -k 10 300 rocprofv3 --pmc $ctrs --kernel-trace -d "$OUT/p$i" -o run --output-format csv \
-        -- python scripts/icp_cells.py "$CELL" > "$OUT/p$i.log" 2>&1
+        -- python ${PMC_SCRIPT:-scripts/icp_cells.py $CELL} > "$OUT/p$i.log" 2>&1
     rc=$?
     echo "rc=$rc"
     if [ $rc -ne 0 ]; then tail -5 "$OUT/p$i.log"; exit $rc; fi
@@ -23,16 +25,16 @@ SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_INST_C
 FETCH_SIZE
 WRITE_SIZE
 EOF
-python - "$OUT" <<'PY'
-import csv, glob, os, sys, collections
-out = sys.argv[1]
+python - "$OUT" "${PMC_FILTER:-icp}" <<'PY'
+import csv, glob, os, re, sys, collections
+out, filt = sys.argv[1], re.compile(sys.argv[2])
 agg = collections.defaultdict(lambda: collections.defaultdict(list))
 for f in sorted(glob.glob(os.path.join(out, "p*", "**", "*counter_collection.csv"), recursive=True)):
     for r in csv.DictReader(open(f)):
-        k = r.get("Kernel_Name", "")[:48]
+        k = r.get("Kernel_Name", "")[:64]
         agg[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, d in agg.items():
-    if "icp" not in k:
+    if not filt.search(k):
         continue
     print(k)
     for c, v in sorted(d.items()):
