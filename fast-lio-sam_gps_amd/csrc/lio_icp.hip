@@ -61,6 +61,9 @@ __device__ __forceinline__ void xform_pcl(const float* T, float x, float y, floa
 // does not depend on the tiling.
 // ----------------------------------------------------------------------------
 constexpr int kTileCh = 256;  // candidates staged per LDS round
+#ifndef LIO_ICP_GROW
+#define LIO_ICP_GROW 1  // box growth per round past r = 3 (0: doubling throughout)
+#endif
 
 // Tiles -> blocks (launch_icp_tiles: 8 x (kIcpSegs / 8) x ceil(n / kIcpSegs) blocks; block b runs on
 // XCD b % 8).  The cell-ordered tiles form kIcpSegs contiguous segments; XCD x owns segments x, x + 8,
@@ -308,7 +311,7 @@ __device__ __forceinline__ uint64_t tile_min(uint64_t best, uint64_t* s_best) {
 // One tile's exact 1-NN (one wave per tile: NW = 1; NW > 1 splits the tile's candidate stream over NW
 // waves with block-level merges — measured no faster, profiles/r02_icp_tile_experiments.txt).
 template <int NW>
-__device__ __forceinline__ void icp_tile_body(const IcpArgs& a, int tix, TileLds& L, uint64_t* s_best) {
+__device__ __forceinline__ void icp_tile_body(const IcpArgs& a, int tix, int ntiles, TileLds& L, uint64_t* s_best) {
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #ifdef LIO_DIAG
     const uint64_t t_start = wall_clock64();  // per-tile timeline (diagnostics build)
@@ -394,6 +397,10 @@ __device__ __forceinline__ void icp_tile_body(const IcpArgs& a, int tix, TileLds
     // 2. final: everything within sqrt(B) of the tile box, minus what was scanned
     CellBox S{1, 0, 1, 0, 1, 0};  // scanned so far (empty)
     int r = a.r0;
+#ifdef LIO_DIAG
+    unsigned long long dg_cand = 0;  // candidates streamed before the final round, final rows
+    int dg_rows = 0;
+#endif
     for (;;) {
         const bool grow = __any(act && (uint32_t)best == (uint32_t)kNone);  // block-uniform (lists merged)
         CellBox N;
@@ -411,13 +418,21 @@ __device__ __forceinline__ void icp_tile_body(const IcpArgs& a, int tix, TileLds
         // the scanned box may stick out of N (a grown box): clip it, the part outside N is not needed
         CellBox Sc{max(S.x0, N.x0), min(S.x1, N.x1), max(S.y0, N.y0), min(S.y1, N.y1), max(S.z0, N.z0), min(S.z1, N.z1)};
         if (Sc.y0 > Sc.y1 || Sc.z0 > Sc.z1) Sc.x0 = 1, Sc.x1 = 0;
+#ifdef LIO_DIAG
+        if (!grow) {
+            dg_cand = cand;
+            dg_rows = (N.y1 - N.y0 + 1) * (N.z1 - N.z0 + 1);
+        }
+#endif
         scan_rows<NW>(g, L, N, Sc, B, qx0, qx1, qy0, qy1, qz0, qz1, act, x, y, z, best, cand, tested);
         best = tile_min<NW>(best, s_best);
         ++rounds;
         const bool full = N.x0 == 0 && N.y0 == 0 && N.z0 == 0 && N.x1 == g.nx - 1 && N.y1 == g.ny - 1 && N.z1 == g.nz - 1;
         if (!grow || full) break;  // final pass done, or the whole grid scanned
         S = N;
-        r = 2 * r + 1;
+        // empty surroundings: the box doubles while small, then grows by LIO_ICP_GROW cells a round (a doubled
+        // box overshoots the nearest points by up to its own size, and every point it holds is streamed)
+        r = (LIO_ICP_GROW == 0 || r < 3) ? 2 * r + 1 : r + LIO_ICP_GROW;
     }
     // the tile's cost for the next pass's longest-first order: candidates tested over its waves
     uint32_t tile_tested = tested;
@@ -435,6 +450,11 @@ __device__ __forceinline__ void icp_tile_body(const IcpArgs& a, int tix, TileLds
 #ifdef LIO_DIAG
         a.dbg[8 + 2 * (size_t)tix] = t_start;
         a.dbg[8 + 2 * (size_t)tix + 1] = wall_clock64();
+        unsigned long long* ex = a.dbg + 8 + 2 * (size_t)ntiles + 4 * (size_t)tix;
+        ex[0] = dg_cand;
+        ex[1] = cand - dg_cand;
+        ex[2] = (unsigned long long)dg_rows;
+        ex[3] = (unsigned long long)rounds;
 #endif
 #ifndef LIO_DIAG_TIMELINE  // the timeline build leaves out the same-address counters (they serialise)
         atomicAdd(a.dbg, cand);
@@ -462,7 +482,7 @@ __global__ void __launch_bounds__(kIcpTileQ) icp_tile_kernel(IcpArgs a, int ntil
     __shared__ TileLds L;
     const int tix = icp_tile_of(a.order, (int)blockIdx.x, ntiles);
     if (tix < 0) return;  // block-uniform: a slot past its XCD's share
-    icp_tile_body<1>(a, tix, L, nullptr);
+    icp_tile_body<1>(a, tix, ntiles, L, nullptr);
 }
 
 // One block = one 4096-point record -> super[record][kIcpStride]: each lane

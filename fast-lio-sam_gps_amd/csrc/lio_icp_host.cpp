@@ -843,8 +843,8 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
 #ifdef LIO_DIAG
     static const bool dbg_on = std::getenv("LIO_ICP_DEBUG") != nullptr;  // diagnostics build: search statistics
     if (dbg_on) {
-        // 8 counters + (start, end) wall clock per tile
-        const size_t bytes = (8 + 2 * (size_t)std::max(h->ntiles, 1)) * sizeof(unsigned long long);
+        // 8 counters + (start, end) wall clock per tile + (growth candidates, final candidates, final rows, rounds)
+        const size_t bytes = (8 + 6 * (size_t)std::max(h->ntiles, 1)) * sizeof(unsigned long long);
         if (h->d_dbg && h->dbg_bytes < bytes) {
             IHIP(hipFree(h->d_dbg));
             h->d_dbg = nullptr;
@@ -945,6 +945,19 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
                      (double)(t1 - t0) * 0.01, pct(0.5), pct(0.9), pct(0.99), sd.back(), cost[imax],
                      [&] { std::vector<uint32_t> c2 = cost; std::nth_element(c2.begin(), c2.begin() + c2.size() / 2, c2.end()); return c2[c2.size() / 2]; }(),
                      (double)(last_start - t0) * 0.01, late, h->ntiles);
+        // the slowest tiles' search: candidates streamed while growing / in the final round, final rows, rounds
+        std::vector<unsigned long long> ex(4 * (size_t)h->ntiles);
+        IHIP(hipMemcpy(ex.data(), h->d_dbg + 8 + 2 * (size_t)h->ntiles, ex.size() * sizeof(unsigned long long),
+                       hipMemcpyDeviceToHost));
+        std::vector<int> idx(h->ntiles);
+        for (int t = 0; t < h->ntiles; ++t) idx[t] = t;
+        const int nshow = std::min(5, h->ntiles);
+        std::partial_sort(idx.begin(), idx.begin() + nshow, idx.end(), [&](int u, int v) { return dur[u] > dur[v]; });
+        for (int k = 0; k < nshow; ++k) {
+            const int t = idx[k];
+            std::fprintf(stderr, "  slow tile %d: %.1f us, starts %.1f us, growth cand %llu, final cand %llu, final rows %llu, rounds %llu, cost %u\n",
+                         t, dur[t], (double)(tt[2 * t] - t0) * 0.01, ex[4 * t], ex[4 * t + 1], ex[4 * t + 2], ex[4 * t + 3], cost[t]);
+        }
     }
 #endif
     if (h->timing && h->sh_n > 0) {

@@ -117,6 +117,7 @@ for s in $STEPS; do
     libab) run libab 900 bash -c 'for r in 1 2; do for v in default $LIBAB; do if [ $v = default ]; then L=""; else L=fast-lio-sam_gps_amd/build_ab/$v/liblio_gpu.so; fi; LIO_GPU_LIB=$L python scripts/icp_ab.py 1.0 5 && LIO_GPU_LIB=$L LIO_ICP_ORDER=-1 python scripts/icp_ab.py 1.0 5 || exit $?; echo "^ $v round $r"; done; done' ;;
     abprof) run abprof_default 300 rocprofv3 --kernel-trace --stats -d "$OUT/abprof_default" -o run --output-format csv -- python scripts/icp_ab.py 1.0 3 &&
             LIO_GPU_LIB=fast-lio-sam_gps_amd/build_ab/$LIBAB/liblio_gpu.so run abprof_ab 300 rocprofv3 --kernel-trace --stats -d "$OUT/abprof_ab" -o run --output-format csv -- python scripts/icp_ab.py 1.0 3 ;;
+    abicp) run abicp 900 bash -c 'for r in 1 2; do for v in default $LIBAB; do if [ $v = default ]; then L=""; else L=fast-lio-sam_gps_amd/build_ab/$v/liblio_gpu.so; fi; LIO_GPU_LIB=$L LIO_ICP_ORDER=-1 python scripts/icp_ab.py 1.0 5 || exit $?; echo "^ $v round $r"; done; done' ;;
     cppprof) run cpp_prof 400 python scripts/cpp_stream_profile.py 3 ;;
     hwq)   run hwq 900 python scripts/hwq_ab.py ;;
     *) echo "unknown step $s" ;;
