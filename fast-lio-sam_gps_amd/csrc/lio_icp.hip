@@ -766,7 +766,7 @@ __device__ __forceinline__ void serial_add(const float* col, uint32_t cnt, float
 }
 
 // out[0..5] = float sums (src x y z, tgt x y z), out[6] = count (uint32 bits); pairs: n x 6 compacted
-__global__ void __launch_bounds__(kPclThreads) icp_pcl_means_kernel(IcpArgs a, float* __restrict__ pairs,
+__global__ void __launch_bounds__(kPclThreads) icp_pcl_means_kernel(IcpArgs a, float* __restrict__ pairs, int64_t cap,
                                                                     float* __restrict__ out) {
     __shared__ float s[6][kPclThreads];
     __shared__ uint32_t s_w[kPclThreads / 64];
@@ -793,7 +793,7 @@ __global__ void __launch_bounds__(kPclThreads) icp_pcl_means_kernel(IcpArgs a, f
 #pragma unroll
             for (int d = 0; d < 6; ++d) {
                 s[d][slot] = v[d];
-                pairs[6 * (size_t)(done + slot) + d] = v[d];
+                pairs[d * cap + (int64_t)(done + slot)] = v[d];  // column-major (PclBuf::pairs)
             }
         }
         __syncthreads();
@@ -806,7 +806,7 @@ __global__ void __launch_bounds__(kPclThreads) icp_pcl_means_kernel(IcpArgs a, f
 }
 
 // sums / count from icp_pcl_means_kernel -> out[7 + 3 r + c] = sum_k (tgt_r - dm_r) (src_c - sm_c), in order
-__global__ void __launch_bounds__(kPclThreads) icp_pcl_sigma_kernel(const float* __restrict__ pairs,
+__global__ void __launch_bounds__(kPclThreads) icp_pcl_sigma_kernel(const float* __restrict__ pairs, int64_t cap,
                                                                     float* __restrict__ out) {
     __shared__ float s[6][kPclThreads];
     const uint32_t n = __float_as_uint(out[6]);
@@ -820,10 +820,9 @@ __global__ void __launch_bounds__(kPclThreads) icp_pcl_sigma_kernel(const float*
     }
     for (uint32_t base = 0; base < n; base += kPclThreads) {
         const uint32_t cnt = min((uint32_t)kPclThreads, n - base);
-        for (uint32_t e = threadIdx.x; e < 6 * cnt; e += kPclThreads) {  // coalesced: pair-major in memory
-            const uint32_t k = e / 6, d = e % 6;
-            s[d][k] = pairs[6 * (size_t)base + e];
-        }
+#pragma unroll
+        for (int d = 0; d < 6; ++d)  // coalesced: column-major in memory
+            for (uint32_t k = threadIdx.x; k < cnt; k += kPclThreads) s[d][k] = pairs[d * cap + (int64_t)(base + k)];
         __syncthreads();
         if (threadIdx.x < 9) {
             const float* dst = s[3 + r];
@@ -849,13 +848,13 @@ __global__ void __launch_bounds__(kPclThreads) icp_pcl_sigma_kernel(const float*
     if (threadIdx.x < 9) out[7 + threadIdx.x] = acc;
 }
 
-void launch_icp_pcl_stats(const IcpArgs& a, float* pairs, float* out16, hipStream_t st) {
-    icp_pcl_means_kernel<<<1, kPclThreads, 0, st>>>(a, pairs, out16);
-    icp_pcl_sigma_kernel<<<1, kPclThreads, 0, st>>>(pairs, out16);
+void launch_icp_pcl_stats(const IcpArgs& a, float* pairs, int64_t cap, float* out16, hipStream_t st) {
+    icp_pcl_means_kernel<<<1, kPclThreads, 0, st>>>(a, pairs, cap, out16);
+    icp_pcl_sigma_kernel<<<1, kPclThreads, 0, st>>>(pairs, cap, out16);
 }
 
-void launch_icp_pcl_means_serial(const IcpArgs& a, float* pairs, float* out16, hipStream_t st) {
-    icp_pcl_means_kernel<<<1, kPclThreads, 0, st>>>(a, pairs, out16);
+void launch_icp_pcl_means_serial(const IcpArgs& a, float* pairs, int64_t cap, float* out16, hipStream_t st) {
+    icp_pcl_means_kernel<<<1, kPclThreads, 0, st>>>(a, pairs, cap, out16);
 }
 
 __global__ void __launch_bounds__(64) icp_combine_kernel(const double* __restrict__ recv, int64_t nsup, int world,

@@ -788,10 +788,10 @@ static int pcl_finish(lio_icp* h, const lio::IcpArgs& a) {
     if ((pcl_word(h, 0) | pcl_word(h, 1)) != 0) {  // the serial kernels: one lane per chain
         ++h->fid_stats[1];
         if (order == lio::kPclSeq) {
-            lio::launch_icp_pcl_stats(a, h->pcl.pairs, h->d_pcl16, h->st);
+            lio::launch_icp_pcl_stats(a, h->pcl.pairs, h->pcl.cap, h->d_pcl16, h->st);
             IHIP(hipMemcpyAsync(h->h_pclout, h->d_pcl16, 16 * sizeof(float), hipMemcpyDeviceToHost, h->st));
         } else {
-            lio::launch_icp_pcl_means_serial(a, h->pcl.pairs, h->d_pcl16, h->st);
+            lio::launch_icp_pcl_means_serial(a, h->pcl.pairs, h->pcl.cap, h->d_pcl16, h->st);
             lio::launch_pcl_sigma(h->pcl, order, 1, h->st, h->d_pcl16);
             lio::launch_pcl_pack(h->pcl, order, h->d_pclout, h->st, h->d_pcl16);
             IHIP(hipMemcpyAsync(h->h_pclout, h->d_pclout, lio::kPclOutWords * sizeof(float), hipMemcpyDeviceToHost, h->st));

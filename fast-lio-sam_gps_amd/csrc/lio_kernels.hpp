@@ -184,8 +184,8 @@ void launch_icp_gather_ids(const double* recv, int world, int64_t rank_stride, i
                            int* gid, hipStream_t st);
 // PCL-order fidelity mode: out16[0..5] float sums (src, tgt), [6] count bits, [7..15] sigma accumulator
 // (row-major target x source) — serial float chains (one block); pairs: n * 6 floats scratch
-void launch_icp_pcl_stats(const IcpArgs& a, float* pairs, float* out16, hipStream_t st);
+void launch_icp_pcl_stats(const IcpArgs& a, float* pairs, int64_t cap, float* out16, hipStream_t st);
 // the serial means alone (out16[0..6]; pairs compacted as a by-product): the fidelity orders' fallback
-void launch_icp_pcl_means_serial(const IcpArgs& a, float* pairs, float* out16, hipStream_t st);
+void launch_icp_pcl_means_serial(const IcpArgs& a, float* pairs, int64_t cap, float* out16, hipStream_t st);
 
 }  // namespace lio

@@ -66,8 +66,8 @@ __device__ __forceinline__ uint32_t block_excl_u32(uint32_t v, uint32_t* s_w, ui
 // logical block writes the total and resets the ticket.
 __global__ void __launch_bounds__(kPT) pcl_compact_kernel(IcpArgs a, unsigned long long* __restrict__ st,
                                                           uint32_t* __restrict__ ticket, uint32_t epoch,
-                                                          float* __restrict__ pairs, uint32_t* __restrict__ d_n,
-                                                          int nb) {
+                                                          float* __restrict__ pairs, int64_t cap,
+                                                          uint32_t* __restrict__ d_n, int nb) {
     __shared__ uint32_t s_w[kPT / 64];
     __shared__ uint32_t s_b, s_off;
     if (threadIdx.x == 0) s_b = atomicAdd(ticket, 1u);
@@ -108,13 +108,9 @@ __global__ void __launch_bounds__(kPT) pcl_compact_kernel(IcpArgs a, unsigned lo
         if (ok[i]) {
             const int p = i0 + i;
             const float4 q = a.tgt_by_id[a.nn_id[p]];
-            float* o = pairs + 6 * (size_t)slot;
-            o[0] = a.cur[3 * p];
-            o[1] = a.cur[3 * p + 1];
-            o[2] = a.cur[3 * p + 2];
-            o[3] = q.x;
-            o[4] = q.y;
-            o[5] = q.z;
+            const float v[6] = {a.cur[3 * p], a.cur[3 * p + 1], a.cur[3 * p + 2], q.x, q.y, q.z};
+#pragma unroll
+            for (int d = 0; d < 6; ++d) pairs[d * cap + slot] = v[d];
             ++slot;
         }
 }
@@ -129,7 +125,7 @@ __global__ void pcl_mean6_kernel(const float* __restrict__ sums6, const uint32_t
 
 // orders 2 / 3: block q of the depth = pairs [q kc, (q + 1) kc): lane e < 9 (r = e / 3, c = e % 3) adds
 // (tgt_r - dm_r) * (src_c - sm_c) in order from 0 (gebp's 1 x 1 remainder path: C0 += A0 * B0, no FMA)
-__global__ void __launch_bounds__(64) pcl_sigma_blocks_kernel(const float* __restrict__ pairs,
+__global__ void __launch_bounds__(64) pcl_sigma_blocks_kernel(const float* __restrict__ pairs, int64_t cap,
                                                               const uint32_t* __restrict__ d_n,
                                                               const float* __restrict__ sums6, int l1,
                                                               float* __restrict__ Cb) {
@@ -146,7 +142,19 @@ __global__ void __launch_bounds__(64) pcl_sigma_blocks_kernel(const float* __res
     for (int64_t q = blockIdx.x; q < nkc; q += gridDim.x) {
         const int64_t k0 = q * kc;
         const int cnt = (int)((int64_t)n - k0 < kc ? (int64_t)n - k0 : kc);
-        for (int e = lane; e < 6 * cnt; e += 64) s[e % 6][e / 6] = pairs[6 * k0 + e];  // coalesced, pair-major
+#pragma unroll
+        for (int d = 0; d < 6; ++d) {  // coalesced per column, the column's loads in flight together
+            constexpr int T = (kMaxKc + 63) / 64;
+            float v[T];
+#pragma unroll
+            for (int t = 0; t < T; ++t) {
+                const int j = t * 64 + lane;
+                v[t] = j < cnt ? pairs[d * cap + k0 + j] : 0.f;
+            }
+#pragma unroll
+            for (int t = 0; t < T; ++t)
+                if (t * 64 + lane < cnt) s[d][t * 64 + lane] = v[t];
+        }
         __syncthreads();
         if (lane < 9) {
             const float* dv = s[3 + r];
@@ -170,7 +178,8 @@ __global__ void __launch_bounds__(64) pcl_sigma_blocks_kernel(const float* __res
 // out[0..5] float sums (src xyz, tgt xyz), out[6] count bits, out[7 + 3r + c] sigma (orders 2 / 3: scaled by
 // one_over_n as Eigen leaves it; order 1: the raw sequential accumulator, scaled on the host), out[16]
 // verification failures (means bits 0-5, sigma chains 8-16), out[17] event-list overflows (same bits)
-__global__ void __launch_bounds__(64) pcl_pack_kernel(const float* __restrict__ pairs, const uint32_t* __restrict__ d_n,
+__global__ void __launch_bounds__(64) pcl_pack_kernel(const float* __restrict__ pairs, int64_t cap,
+                                                      const uint32_t* __restrict__ d_n,
                                                       const float* __restrict__ sums6, const float* __restrict__ sig9,
                                                       const float* __restrict__ Cb, int order, int l1,
                                                       const uint32_t* __restrict__ st_means,
@@ -192,8 +201,10 @@ __global__ void __launch_bounds__(64) pcl_pack_kernel(const float* __restrict__ 
         // (alpha * dst_demean).row(r) . src_demean.row(c) summed from the first term
         if (lane < 9) {
             const float dm = sums6[3 + r] * oon, sm = sums6[c] * oon;
-            res = (oon * (pairs[3 + r] - dm)) * (pairs[c] - sm);
-            for (uint32_t k = 1; k < n; ++k) res += (oon * (pairs[6 * k + 3 + r] - dm)) * (pairs[6 * k + c] - sm);
+            const float* tr = pairs + (3 + r) * cap;
+            const float* sc = pairs + c * cap;
+            res = (oon * (tr[0] - dm)) * (sc[0] - sm);
+            for (uint32_t k = 1; k < n; ++k) res += (oon * (tr[k] - dm)) * (sc[k] - sm);
         }
     } else {
         const int64_t kc = eigen_gemm_kc((int64_t)n, l1);
@@ -277,11 +288,11 @@ void launch_pcl_compact(const IcpArgs& a, PclBuf& p, hipStream_t st) {
         return;
     }
     p.epoch = p.epoch + 1u >= (1u << 30) ? 1u : p.epoch + 1u;  // 30 bits, 0 reserved for "never written"
-    pcl_compact_kernel<<<nb, kPT, 0, st>>>(a, p.bst, p.small + kPclTicket, p.epoch, p.pairs, d_n, nb);
+    pcl_compact_kernel<<<nb, kPT, 0, st>>>(a, p.bst, p.small + kPclTicket, p.epoch, p.pairs, p.cap, d_n, nb);
 }
 
 void launch_pcl_means(PclBuf& p, int pass, hipStream_t st) {
-    seqsum_launch(SeqPairs{p.pairs}, 6, p.small + kPclN, p.means, pass, st);
+    seqsum_launch(SeqPairs{p.pairs, p.cap}, 6, p.small + kPclN, p.means, pass, st);
 }
 
 void launch_pcl_sigma(PclBuf& p, int order, int pass, hipStream_t st, const float* sums6) {
@@ -290,10 +301,10 @@ void launch_pcl_sigma(PclBuf& p, int order, int pass, hipStream_t st, const floa
     if (order == 1) {
         float* mean6 = reinterpret_cast<float*>(p.small + kPclMean6);
         pcl_mean6_kernel<<<1, 64, 0, st>>>(sums6, d_n, mean6);
-        seqsum_launch(SeqSigma{p.pairs, mean6}, 9, d_n, p.sig, pass, st);
+        seqsum_launch(SeqSigma{p.pairs, mean6, p.cap}, 9, d_n, p.sig, pass, st);
     } else {
         const int64_t grid = std::min<int64_t>(p.cap / 340 + 2, 4096);
-        pcl_sigma_blocks_kernel<<<(int)grid, 64, 0, st>>>(p.pairs, d_n, sums6, pcl_l1(order), p.Cb);
+        pcl_sigma_blocks_kernel<<<(int)grid, 64, 0, st>>>(p.pairs, p.cap, d_n, sums6, pcl_l1(order), p.Cb);
     }
 }
 
@@ -302,7 +313,7 @@ void launch_pcl_pack(PclBuf& p, int order, float* out, hipStream_t st, const flo
     const uint32_t* zero = p.small + kPclZero;  // the serial fallback's sums need no verification
     const bool serial = sums6 != nullptr;
     if (!sums6) sums6 = p.means.result;
-    pcl_pack_kernel<<<1, 64, 0, st>>>(p.pairs, d_n, sums6, order == 1 ? p.sig.result : sums6, p.Cb, order,
+    pcl_pack_kernel<<<1, 64, 0, st>>>(p.pairs, p.cap, d_n, sums6, order == 1 ? p.sig.result : sums6, p.Cb, order,
                                       pcl_l1(order), serial ? zero : p.means.status,
                                       order == 1 && !serial ? p.sig.status : zero,
                                       serial ? nullptr : p.means.floor_e + p.means.nch, p.small + kPclTicket + 1, out);

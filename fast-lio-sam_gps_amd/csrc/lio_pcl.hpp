@@ -20,7 +20,8 @@ constexpr int kPclOutWords = 20;  // pcl_pack output: 16 statistics, 2 status wo
                                   // the compaction's time-out flag
 
 struct PclBuf {
-    float* pairs = nullptr;   // cap x 6: accepted (src xyz, tgt xyz) in source order
+    float* pairs = nullptr;   // accepted (src xyz, tgt xyz) in source order, column-major: pairs[d * cap + k]
+                              // (the chains' per-thread loads are then contiguous, not 24 bytes apart)
     unsigned long long* bst = nullptr;  // per compaction block: look-back status word (epoch, flag, value)
     uint32_t epoch = 0;                 // compaction launches so far (mod 2^30, 0 skipped)
     float* Cb = nullptr;      // orders 2 / 3: per depth block, 9 sequential block sums

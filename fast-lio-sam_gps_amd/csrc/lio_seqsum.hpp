@@ -65,14 +65,19 @@ void seqsum_free(SeqSumBuf& b);
 // chain sources
 struct SeqPairs {  // means of pcl::umeyama: chain c < 6 = column c of the compacted pairs (src xyz, tgt xyz)
     const float* pairs;
-    __device__ __forceinline__ float operator()(int c, int64_t k) const { return pairs[6 * k + c]; }
+    int64_t cstride = 0;  // 0: pair-major (pairs[6 k + c]); else column-major (pairs[c cstride + k]: a wave's
+                          // loads of one chain are contiguous instead of 24 bytes apart)
+    __device__ __forceinline__ float operator()(int c, int64_t k) const {
+        return cstride ? pairs[c * cstride + k] : pairs[6 * k + c];
+    }
 };
 struct SeqSigma {  // sigma of the sequential order: chain c < 9 = (tgt_r - dm_r) * (src_col - sm_col), r = c / 3
-    const float* pairs;
+    const float* pairs;  // column-major (pairs[d * cstride + k])
     const float* mean6;  // device: src mean xyz, tgt mean xyz (float)
+    int64_t cstride;
     __device__ __forceinline__ float operator()(int c, int64_t k) const {
         const int r = c / 3, cc = c % 3;
-        return (pairs[6 * k + 3 + r] - mean6[3 + r]) * (pairs[6 * k + cc] - mean6[cc]);
+        return (pairs[(3 + r) * cstride + k] - mean6[3 + r]) * (pairs[cc * cstride + k] - mean6[cc]);
     }
 };
 
