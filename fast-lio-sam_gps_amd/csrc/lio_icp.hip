@@ -61,6 +61,9 @@ __device__ __forceinline__ void xform_pcl(const float* T, float x, float y, floa
 // does not depend on the tiling.
 // ----------------------------------------------------------------------------
 constexpr int kTileCh = 256;  // candidates staged per LDS round
+#ifndef LIO_ICP_ROW_TIGHTEN
+#define LIO_ICP_ROW_TIGHTEN 1  // rows trimmed per 64-row batch by the lanes' current bests (0: by the round's B)
+#endif
 #ifndef LIO_ICP_GROW
 #define LIO_ICP_GROW 1  // box growth per round past r = 3 (0: doubling throughout)
 #endif
@@ -271,7 +274,14 @@ __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const 
         const int r = rb + lane;
         uint32_t b0 = 0, n0 = 0, b1 = 0, n1 = 0;
         float g2 = INFINITY;
-        if (r < nrows) row_pieces(g, N, S, B, qb, r, b0, n0, b1, n1, g2);
+#if LIO_ICP_ROW_TIGHTEN
+        // the bound as it stands now: every active lane's best (+inf while one has none) only falls, so a row
+        // farther than all of them cannot improve any lane, in this round or in the final sphere that follows
+        const float Bb = fminf(B, wave_max_nonneg(act ? __uint_as_float((uint32_t)(best >> 32)) : 0.f));
+#else
+        const float Bb = B;
+#endif
+        if (r < nrows) row_pieces(g, N, S, Bb, qb, r, b0, n0, b1, n1, g2);
         // nearest rows first (stable partition by the row's (y, z) gap to the tile box: 0, <= 1,
         // <= 2 cells, farther), so the staging filter's bound tightens early in the stream; any
         // order gives the same minima (total order on (d2, id))

@@ -186,7 +186,7 @@ __global__ void __launch_bounds__(64) pcl_pack_kernel(const float* __restrict__ 
                                                       const uint32_t* __restrict__ st_sig,
                                                       const int* __restrict__ nev6, const uint32_t* __restrict__ flags,
                                                       float* __restrict__ out) {
-    __shared__ float s_c[9][kPackWin];
+    __shared__ float s_c[9][kPackWin + 1];  // +1: the nine lanes' rows in different banks
     const uint32_t n = *d_n;
     const int lane = threadIdx.x;
     const float oon = 1.f / (float)n;
@@ -211,7 +211,19 @@ __global__ void __launch_bounds__(64) pcl_pack_kernel(const float* __restrict__ 
         const int64_t nkc = ((int64_t)n + kc - 1) / kc;
         for (int64_t q0 = 0; q0 < nkc; q0 += kPackWin) {  // dst.setZero(); res(r, c) += alpha * C0 per depth block
             const int m = (int)(nkc - q0 < kPackWin ? nkc - q0 : kPackWin);
-            for (int e = lane; e < 9 * m; e += 64) s_c[e % 9][e / 9] = Cb[q0 * 9 + e];  // every load in flight at once
+            for (int e0 = 0; e0 < 9 * m; e0 += 64 * 16) {  // 16 loads per lane in flight, then their LDS stores
+                float v[16];
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    const int e = e0 + t * 64 + lane;
+                    v[t] = e < 9 * m ? Cb[q0 * 9 + e] : 0.f;
+                }
+#pragma unroll
+                for (int t = 0; t < 16; ++t) {
+                    const int e = e0 + t * 64 + lane;
+                    if (e < 9 * m) s_c[e % 9][e / 9] = v[t];
+                }
+            }
             __syncthreads();
             if (lane < 9) {
                 int q = 0;
