@@ -61,6 +61,9 @@ __device__ __forceinline__ void xform_pcl(const float* T, float x, float y, floa
 // does not depend on the tiling.
 // ----------------------------------------------------------------------------
 constexpr int kTileCh = 256;  // candidates staged per LDS round
+#ifndef LIO_ICP_ZORDER
+#define LIO_ICP_ZORDER 1  // a round's rows by z slice centre-out from the tile (0: z ascending)
+#endif
 #ifndef LIO_ICP_ROW_TIGHTEN
 #define LIO_ICP_ROW_TIGHTEN 1  // rows trimmed per 64-row batch by the lanes' current bests (0: by the round's B)
 #endif
@@ -223,14 +226,23 @@ struct CellBox {
 // [qx0 - r, qx1 + r], r = sqrt(B - gap^2) (conservatively rounded).
 // Row r of box N (y fastest) minus the cells of box S: its point ranges [b0, b0+n0), [b1, b1+n1) and the
 // squared (y, z) gap g2 of the row to the tile box qb
+// z slice j of [lo, hi] taken centre-out from c: c, c + 1, c - 1, c + 2, ... then the longer side's rest
+__device__ __forceinline__ int center_out(int j, int lo, int hi, int c) {
+    const int up = hi - c, dn = c - lo, m = min(up, dn);
+    if (j <= 2 * m) return j == 0 ? c : ((j & 1) ? c + (j + 1) / 2 : c - j / 2);
+    const int rest = j - 2 * m;
+    return up > dn ? c + m + rest : c - m - rest;
+}
+
 __device__ __forceinline__ void row_pieces(const GridDev& g, const CellBox& N, const CellBox& S, float B,
-                                           const float (&qb)[6], int r, uint32_t& b0, uint32_t& n0, uint32_t& b1,
-                                           uint32_t& n1, float& g2) {
+                                           const float (&qb)[6], int r, int zc, uint32_t& b0, uint32_t& n0,
+                                           uint32_t& b1, uint32_t& n1, float& g2) {
     const float cs = g.cell, m = g.margin;
     const int ny = N.y1 - N.y0 + 1;
     const bool sempty = S.x0 > S.x1;
     const uint32_t gnx = (uint32_t)g.nx, gnxy = (uint32_t)g.nx * (uint32_t)g.ny;
-    const int rz = N.z0 + r / ny, ry = N.y0 + r % ny;
+    // z slices nearest the tile first (its rows' batches come first, so the bests fall before the far slices)
+    const int rz = LIO_ICP_ZORDER ? center_out(r / ny, N.z0, N.z1, zc) : N.z0 + r / ny, ry = N.y0 + r % ny;
     int x0 = N.x0, x1 = N.x1;
     bool keep = true;
     const float yl = g.oy + (float)ry * cs - m, zl = g.oz + (float)rz * cs - m;
@@ -269,6 +281,7 @@ __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const 
     const float cs = g.cell;
     const float qb[6] = {qx0, qx1, qy0, qy1, qz0, qz1};
     const int nrows = (N.y1 - N.y0 + 1) * (N.z1 - N.z0 + 1);
+    const int zc = min(max((cell_coord(qz0, g.oz, g.inv_cell) + cell_coord(qz1, g.oz, g.inv_cell)) / 2, N.z0), N.z1);
 #pragma unroll 1
     for (int rb = 0; rb < nrows; rb += kIcpTileQ) {
         const int r = rb + lane;
@@ -281,7 +294,7 @@ __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const 
 #else
         const float Bb = B;
 #endif
-        if (r < nrows) row_pieces(g, N, S, Bb, qb, r, b0, n0, b1, n1, g2);
+        if (r < nrows) row_pieces(g, N, S, Bb, qb, r, zc, b0, n0, b1, n1, g2);
         // nearest rows first (stable partition by the row's (y, z) gap to the tile box: 0, <= 1,
         // <= 2 cells, farther), so the staging filter's bound tightens early in the stream; any
         // order gives the same minima (total order on (d2, id))
