@@ -64,6 +64,9 @@ constexpr int kTileCh = 256;  // candidates staged per LDS round
 #ifndef LIO_ICP_ZORDER
 #define LIO_ICP_ZORDER 1  // a round's rows by z slice centre-out from the tile (0: z ascending)
 #endif
+#ifndef LIO_ICP_YORDER
+#define LIO_ICP_YORDER 1  // and within a slice, rows by y centre-out (0: y ascending)
+#endif
 #ifndef LIO_ICP_ROW_TIGHTEN
 #define LIO_ICP_ROW_TIGHTEN 1  // rows trimmed per 64-row batch by the lanes' current bests (0: by the round's B)
 #endif
@@ -235,14 +238,15 @@ __device__ __forceinline__ int center_out(int j, int lo, int hi, int c) {
 }
 
 __device__ __forceinline__ void row_pieces(const GridDev& g, const CellBox& N, const CellBox& S, float B,
-                                           const float (&qb)[6], int r, int zc, uint32_t& b0, uint32_t& n0,
+                                           const float (&qb)[6], int r, int zc, int yc, uint32_t& b0, uint32_t& n0,
                                            uint32_t& b1, uint32_t& n1, float& g2) {
     const float cs = g.cell, m = g.margin;
     const int ny = N.y1 - N.y0 + 1;
     const bool sempty = S.x0 > S.x1;
     const uint32_t gnx = (uint32_t)g.nx, gnxy = (uint32_t)g.nx * (uint32_t)g.ny;
     // z slices nearest the tile first (its rows' batches come first, so the bests fall before the far slices)
-    const int rz = LIO_ICP_ZORDER ? center_out(r / ny, N.z0, N.z1, zc) : N.z0 + r / ny, ry = N.y0 + r % ny;
+    const int rz = LIO_ICP_ZORDER ? center_out(r / ny, N.z0, N.z1, zc) : N.z0 + r / ny;
+    const int ry = LIO_ICP_YORDER ? center_out(r % ny, N.y0, N.y1, yc) : N.y0 + r % ny;
     int x0 = N.x0, x1 = N.x1;
     bool keep = true;
     const float yl = g.oy + (float)ry * cs - m, zl = g.oz + (float)rz * cs - m;
@@ -282,6 +286,7 @@ __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const 
     const float qb[6] = {qx0, qx1, qy0, qy1, qz0, qz1};
     const int nrows = (N.y1 - N.y0 + 1) * (N.z1 - N.z0 + 1);
     const int zc = min(max((cell_coord(qz0, g.oz, g.inv_cell) + cell_coord(qz1, g.oz, g.inv_cell)) / 2, N.z0), N.z1);
+    const int yc = min(max((cell_coord(qy0, g.oy, g.inv_cell) + cell_coord(qy1, g.oy, g.inv_cell)) / 2, N.y0), N.y1);
 #pragma unroll 1
     for (int rb = 0; rb < nrows; rb += kIcpTileQ) {
         const int r = rb + lane;
@@ -294,7 +299,7 @@ __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const 
 #else
         const float Bb = B;
 #endif
-        if (r < nrows) row_pieces(g, N, S, Bb, qb, r, zc, b0, n0, b1, n1, g2);
+        if (r < nrows) row_pieces(g, N, S, Bb, qb, r, zc, yc, b0, n0, b1, n1, g2);
         // nearest rows first (stable partition by the row's (y, z) gap to the tile box: 0, <= 1,
         // <= 2 cells, farther), so the staging filter's bound tightens early in the stream; any
         // order gives the same minima (total order on (d2, id))
