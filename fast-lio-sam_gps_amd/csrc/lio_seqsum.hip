@@ -662,11 +662,15 @@ template <class Src>
 void seqsum_launch_impl(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, hipStream_t st) {
     const dim3 g(b.nblk, nch);
     if (pass <= 1) {
-        // the forced-event bits of a previous alignment's failures are stale
-        (void)hipMemsetAsync(b.forced, 0, (size_t)nch * (b.nmax / 32 + 1) * sizeof(uint32_t), st);
+        // the forced-event bits of a previous alignment's failures are stale (none were set unless a re-pass ran)
+        if (b.forced_dirty) {
+            (void)hipMemsetAsync(b.forced, 0, (size_t)nch * (b.nmax / 32 + 1) * sizeof(uint32_t), st);
+            b.forced_dirty = false;
+        }
         seq_bsum<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n);
         seq_scan1<<<nch, 256, 0, st>>>(b, d_n, pass);
     } else {
+        b.forced_dirty = true;  // the failures that led here set forced bits
         (void)hipMemsetAsync(b.status, 0, 2 * sizeof(uint32_t), st);
     }
     seq_count<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);

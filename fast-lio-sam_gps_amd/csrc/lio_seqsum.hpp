@@ -55,6 +55,9 @@ struct SeqSumBuf {
     float* ev_s = nullptr;      // [nch][evcap] the event's result (walker)
     float* recon = nullptr;     // [nch][nmax] reconstructed chain (verify; predictions of the next pass)
     uint32_t* forced = nullptr; // [nch][nmax / 32 + 1] elements forced to be events (failed verification)
+    bool forced_dirty = true;   // host: forced bits may be set (a re-pass ran since the last clear): the next
+                                // pass 1 clears them (verification sets bits only where it fails, and every
+                                // failure the caller acts on goes through a pass > 1)
     uint32_t* status = nullptr; // [0] chains failing verification (bits), [1] event overflow (bits)
     float* result = nullptr;    // [nch] final sums
 };
