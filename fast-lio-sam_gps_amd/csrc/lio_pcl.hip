@@ -178,7 +178,8 @@ __global__ void __launch_bounds__(64) pcl_sigma_blocks_kernel(const float* __res
 // out[0..5] float sums (src xyz, tgt xyz), out[6] count bits, out[7 + 3r + c] sigma (orders 2 / 3: scaled by
 // one_over_n as Eigen leaves it; order 1: the raw sequential accumulator, scaled on the host), out[16]
 // verification failures (means bits 0-5, sigma chains 8-16), out[17] event-list overflows (same bits)
-__global__ void __launch_bounds__(64) pcl_pack_kernel(const float* __restrict__ pairs, int64_t cap,
+constexpr int kPackThreads = 1024;  // the staging loads spread wide; lanes 0 .. 8 then add in order
+__global__ void __launch_bounds__(kPackThreads) pcl_pack_kernel(const float* __restrict__ pairs, int64_t cap,
                                                       const uint32_t* __restrict__ d_n,
                                                       const float* __restrict__ sums6, const float* __restrict__ sig9,
                                                       const float* __restrict__ Cb, int order, int l1,
@@ -211,16 +212,16 @@ __global__ void __launch_bounds__(64) pcl_pack_kernel(const float* __restrict__ 
         const int64_t nkc = ((int64_t)n + kc - 1) / kc;
         for (int64_t q0 = 0; q0 < nkc; q0 += kPackWin) {  // dst.setZero(); res(r, c) += alpha * C0 per depth block
             const int m = (int)(nkc - q0 < kPackWin ? nkc - q0 : kPackWin);
-            for (int e0 = 0; e0 < 9 * m; e0 += 64 * 16) {  // 16 loads per lane in flight, then their LDS stores
-                float v[16];
+            for (int e0 = 0; e0 < 9 * m; e0 += kPackThreads * 9) {  // the window in one round trip (9 loads per thread)
+                float v[9];
 #pragma unroll
-                for (int t = 0; t < 16; ++t) {
-                    const int e = e0 + t * 64 + lane;
+                for (int t = 0; t < 9; ++t) {
+                    const int e = e0 + t * kPackThreads + lane;
                     v[t] = e < 9 * m ? Cb[q0 * 9 + e] : 0.f;
                 }
 #pragma unroll
-                for (int t = 0; t < 16; ++t) {
-                    const int e = e0 + t * 64 + lane;
+                for (int t = 0; t < 9; ++t) {
+                    const int e = e0 + t * kPackThreads + lane;
                     if (e < 9 * m) s_c[e % 9][e / 9] = v[t];
                 }
             }
@@ -325,7 +326,7 @@ void launch_pcl_pack(PclBuf& p, int order, float* out, hipStream_t st, const flo
     const uint32_t* zero = p.small + kPclZero;  // the serial fallback's sums need no verification
     const bool serial = sums6 != nullptr;
     if (!sums6) sums6 = p.means.result;
-    pcl_pack_kernel<<<1, 64, 0, st>>>(p.pairs, p.cap, d_n, sums6, order == 1 ? p.sig.result : sums6, p.Cb, order,
+    pcl_pack_kernel<<<1, kPackThreads, 0, st>>>(p.pairs, p.cap, d_n, sums6, order == 1 ? p.sig.result : sums6, p.Cb, order,
                                       pcl_l1(order), serial ? zero : p.means.status,
                                       order == 1 && !serial ? p.sig.status : zero,
                                       serial ? nullptr : p.means.floor_e + p.means.nch, p.small + kPclTicket + 1, out);
