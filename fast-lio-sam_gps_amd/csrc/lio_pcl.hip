@@ -142,18 +142,21 @@ __global__ void __launch_bounds__(64) pcl_sigma_blocks_kernel(const float* __res
     for (int64_t q = blockIdx.x; q < nkc; q += gridDim.x) {
         const int64_t k0 = q * kc;
         const int cnt = (int)((int64_t)n - k0 < kc ? (int64_t)n - k0 : kc);
-#pragma unroll
-        for (int d = 0; d < 6; ++d) {  // coalesced per column, the column's loads in flight together
+        {  // coalesced per column; all six columns' loads in flight together (one round trip)
             constexpr int T = (kMaxKc + 63) / 64;
-            float v[T];
+            float v[6][T];
 #pragma unroll
-            for (int t = 0; t < T; ++t) {
-                const int j = t * 64 + lane;
-                v[t] = j < cnt ? pairs[d * cap + k0 + j] : 0.f;
-            }
+            for (int d = 0; d < 6; ++d)
 #pragma unroll
-            for (int t = 0; t < T; ++t)
-                if (t * 64 + lane < cnt) s[d][t * 64 + lane] = v[t];
+                for (int t = 0; t < T; ++t) {
+                    const int j = t * 64 + lane;
+                    v[d][t] = j < cnt ? pairs[d * cap + k0 + j] : 0.f;
+                }
+#pragma unroll
+            for (int d = 0; d < 6; ++d)
+#pragma unroll
+                for (int t = 0; t < T; ++t)
+                    if (t * 64 + lane < cnt) s[d][t * 64 + lane] = v[d][t];
         }
         __syncthreads();
         if (lane < 9) {
