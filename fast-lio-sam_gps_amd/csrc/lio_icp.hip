@@ -60,7 +60,10 @@ __device__ __forceinline__ void xform_pcl(const float* T, float x, float y, floa
 // Total order (d2, id), d2 = float ((dx*dx + dy*dy) + dz*dz): the result
 // does not depend on the tiling.
 // ----------------------------------------------------------------------------
-constexpr int kTileCh = 256;  // candidates staged per LDS round
+#ifndef LIO_TILE_CH
+#define LIO_TILE_CH 256
+#endif
+constexpr int kTileCh = LIO_TILE_CH;  // candidates staged per LDS round
 #ifndef LIO_ICP_ZORDER
 #define LIO_ICP_ZORDER 1  // a round's rows by z slice centre-out from the tile (0: z ascending)
 #endif
