@@ -171,8 +171,6 @@ struct lio_ctx {
     float* d_far_d = nullptr;
     int* d_far_id = nullptr;
     float* d_d5 = nullptr;  // per point: 5th neighbour d2 of the last kNN (seeds the next one)
-    int* d_perm = nullptr;  // per point: the cell-grouped query order of the near pass (built per scan)
-    int near_mode = 0;      // 0: per-query near pass (8 lanes per query), 1: cell-grouped (LIO_KNN_NEAR=cell, A/B only)
     bool have_eval = false;
     bool knn_valid = false;
     uint64_t knn_map_version = 0;  // map version of the last kNN evaluation
@@ -558,8 +556,6 @@ int lio_ctx_create(lio_map* m, const lio_match_params* p, lio_ctx** out) {
         (void)hipEventCreate(&e->b);
     }
     for (hipEvent_t& e : c->ev_marks) (void)hipEventCreate(&e);
-    // A/B only: LIO_KNN_NEAR=cell selects the cell-grouped near pass (bit-identical, 12x slower measured: DESIGN §4)
-    if (const char* e = std::getenv("LIO_KNN_NEAR")) c->near_mode = std::strcmp(e, "cell") == 0 ? 1 : 0;
     *out = c;
     return LIO_OK;
 }
@@ -570,7 +566,7 @@ int lio_ctx_destroy(lio_ctx* c) {
     (void)hipStreamSynchronize(c->map->st);
     void* ptrs[] = {c->d_body,  c->d_nn,    c->d_planes,   c->d_sel,       c->d_partials, c->d_sums,
                     c->d_rows,  c->d_nrows, c->d_far_list, c->d_far_count, c->d_far_d,    c->d_far_id, c->d_done,
-                    c->d_d5,    c->d_perm};
+                    c->d_d5};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     if (c->h_sums) (void)hipHostFree(c->h_sums);
@@ -590,14 +586,12 @@ int lio_ctx_destroy(lio_ctx* c) {
 
 static int ctx_reserve(lio_ctx* c, int64_t n) {
     if (n > c->cap || !c->d_body || !c->d_nn || !c->d_planes || !c->d_sel || !c->d_far_list || !c->d_far_d ||
-        !c->d_far_id || !c->d_d5 || !c->d_perm) {
+        !c->d_far_id || !c->d_d5) {
         int64_t cap = std::max<int64_t>(n, c->cap + c->cap / 2);
         c->cap = 0;  // a failed reallocation below leaves no buffer that looks usable
-        void* ptrs[] = {c->d_body, c->d_nn, c->d_planes, c->d_sel, c->d_far_list, c->d_far_d, c->d_far_id, c->d_d5,
-                        c->d_perm};
+        void* ptrs[] = {c->d_body, c->d_nn, c->d_planes, c->d_sel, c->d_far_list, c->d_far_d, c->d_far_id, c->d_d5};
         for (void* q : ptrs)
             if (q) (void)hipFree(q);
-        c->d_perm = nullptr;
         c->d_body = nullptr;
         c->d_nn = nullptr;
         c->d_planes = nullptr;
@@ -613,8 +607,7 @@ static int ctx_reserve(lio_ctx* c, int64_t n) {
             hipMalloc(&c->d_far_list, cap * sizeof(int)) != hipSuccess ||
             hipMalloc(&c->d_far_d, cap * 5 * sizeof(float)) != hipSuccess ||
             hipMalloc(&c->d_far_id, cap * 5 * sizeof(int)) != hipSuccess ||
-            hipMalloc(&c->d_d5, cap * sizeof(float)) != hipSuccess ||
-            hipMalloc(&c->d_perm, cap * sizeof(int)) != hipSuccess)
+            hipMalloc(&c->d_d5, cap * sizeof(float)) != hipSuccess)
             return fail(LIO_ERR_NOMEM, "scan buffers: hipMalloc failed");
         c->cap = cap;
     }
@@ -700,7 +693,6 @@ static lio::MatchArgs make_args(lio_ctx* c, const lio_pose& pose_in) {
     a.done_count = c->d_done;
     a.far_d = c->d_far_d;
     a.far_id = c->d_far_id;
-    a.perm = c->near_mode ? c->d_perm : nullptr;
     a.range_sq = c->p.knn_range_sq;
     a.plane_thr = c->p.plane_thr;
     a.s_coef = c->p.s_coef;
@@ -1105,16 +1097,6 @@ static lio::UndistortEnd undistort_end(const lio_pose* e) {
 
 static_assert(sizeof(lio_imu_pose) == sizeof(lio::ImuPose), "lio_imu_pose layout");
 
-// LIO_PREP_UPLOAD=full (A/B hook): the whole sweep uploaded from the caller's memory and selected on the
-// device, as before the staged upload
-static bool prep_upload_full() {
-    static const bool full = [] {
-        const char* e = std::getenv("LIO_PREP_UPLOAD");
-        return e && std::strcmp(e, "full") == 0;
-    }();
-    return full;
-}
-
 // The host half of a sweep upload: rows i % every == 0 — Preprocess's point_filter_num drops the others
 // by index alone, so they never cross PCIe — and the IMU poses packed into the filter's pinned staging
 // buffer, for one DMA each (pageable sources would be staged by the runtime anyway).  *u = rows staged;
@@ -1374,34 +1356,23 @@ int lio_preprocess(lio_filter* f, const float* raw, int64_t n, int stride, const
     if (n == 0) return LIO_OK;
     HIP_TRY(hipSetDevice(f->dev));
     hipStream_t st = f->st;
-    const bool full = prep_upload_full();
     lio::ScanPrepParams sp{p->point_filter_num, p->blind, p->filter_size_surf, p->time_field};
     int64_t rows = n;
     size_t pose_off = 0;
-    int presel = -1;
     StagePlan plan;
-    if (!full) {
-        bool sorted = false;
-        rc = stage_sweep_select(f->b, raw, n, stride, p, poses, n_poses, &rows, &pose_off, &sorted, &plan);
-        if (rc) return rc;
-        presel = sorted ? 1 : 0;
-        if (rows == 0) return LIO_OK;
-    }
+    bool sorted = false;
+    rc = stage_sweep_select(f->b, raw, n, stride, p, poses, n_poses, &rows, &pose_off, &sorted, &plan);
+    if (rc) return rc;
+    const int presel = sorted ? 1 : 0;
+    if (rows == 0) return LIO_OK;
     const size_t staged = pose_off + (size_t)n_poses * sizeof(lio::ImuPose);
-    rc = grow(&f->d_in, f->in_cap, full ? rows * stride : (int64_t)((staged + 3) / 4) + 1);
+    rc = grow(&f->d_in, f->in_cap, (int64_t)((staged + 3) / 4) + 1);
     if (!rc) rc = grow(&f->d_out, f->out_cap, rows * stride);
-    if (!rc && n_poses && full) rc = grow(&f->d_poses, f->poses_cap, n_poses);
     if (rc) return rc;
     lio::RowPieces rp;
     const lio::ImuPose* d_poses = f->d_poses;
-    if (full) {
-        HIP_TRY(hipMemcpyAsync(f->d_in, raw, (size_t)rows * stride * sizeof(float), hipMemcpyHostToDevice, st));
-        if (n_poses)
-            HIP_TRY(hipMemcpyAsync(f->d_poses, poses, (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
-    } else {
-        rc = upload_staged(f->b, plan, pose_off, n_poses, f->d_in, st, &rp, &d_poses);
-        if (rc) return rc;
-    }
+    rc = upload_staged(f->b, plan, pose_off, n_poses, f->d_in, st, &rp, &d_poses);
+    if (rc) return rc;
     int64_t m = 0;
     rc = 2;
     for (int attempt = 0; attempt < 2 && rc == 2; ++attempt) {  // 2: the voxel key width was learnt too narrow
@@ -1481,36 +1452,24 @@ int lio_scan_preprocess(lio_ctx* c, const float* raw, int64_t n, int stride, con
     const auto t0 = std::chrono::steady_clock::now();
     HIP_TRY(hipSetDevice(c->map->dev));
     hipStream_t st = c->map->st;
-    const bool full = prep_upload_full();
     lio::ScanPrepParams sp{p->point_filter_num, p->blind, p->filter_size_surf, p->time_field};
     int64_t rows = n;
     size_t pose_off = 0;
-    int presel = -1;
     StagePlan plan;
-    if (!full) {
-        bool sorted = false;
-        rc = stage_sweep_select(c->filt, raw, n, stride, p, poses, n_poses, &rows, &pose_off, &sorted, &plan);
-        if (rc) return rc;
-        presel = sorted ? 1 : 0;
-    }
+    bool sorted = false;
+    rc = stage_sweep_select(c->filt, raw, n, stride, p, poses, n_poses, &rows, &pose_off, &sorted, &plan);
+    if (rc) return rc;
+    const int presel = sorted ? 1 : 0;
     const auto t1 = std::chrono::steady_clock::now();
     // staged: the pieces (with their gaps) and the poses behind them in one DMA into d_raw
     const size_t staged = pose_off + (size_t)n_poses * sizeof(lio::ImuPose);
-    rc = grow(&c->d_raw, c->raw_cap, full ? std::max<int64_t>(rows, 1) * stride : (int64_t)((staged + 3) / 4) + 1);
+    rc = grow(&c->d_raw, c->raw_cap, (int64_t)((staged + 3) / 4) + 1);
     if (!rc) rc = grow(&c->d_rec, c->rec_cap, std::max<int64_t>(rows, 1) * stride);
-    if (!rc && n_poses && full) rc = grow(&c->d_poses, c->poses_cap, n_poses);
     if (rc) return rc;
     lio::RowPieces rp;
     const lio::ImuPose* d_poses = c->d_poses;
-    if (full) {
-        if (rows)
-            HIP_TRY(hipMemcpyAsync(c->d_raw, raw, (size_t)rows * stride * sizeof(float), hipMemcpyHostToDevice, st));
-        if (n_poses)
-            HIP_TRY(hipMemcpyAsync(c->d_poses, poses, (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
-    } else {
-        rc = upload_staged(c->filt, plan, pose_off, n_poses, c->d_raw, st, &rp, &d_poses);
-        if (rc) return rc;
-    }
+    rc = upload_staged(c->filt, plan, pose_off, n_poses, c->d_raw, st, &rp, &d_poses);
+    if (rc) return rc;
     const auto t2 = std::chrono::steady_clock::now();
     rc = scan_prep_device(c, rows, stride, sp, n_poses, end, n_down, "lio_scan_preprocess", presel, d_poses, rp);
     if (prep_profile()) {
@@ -1620,16 +1579,13 @@ int lio_scan_preprocess_cloud2(lio_ctx* c, const uint8_t* data, int64_t n_points
     if (rc) return rc;
     HIP_TRY(hipSetDevice(c->map->dev));
     hipStream_t st = c->map->st;
-    const bool full = prep_upload_full();
     lio::ScanPrepParams sp{pp.point_filter_num, pp.blind, pp.filter_size_surf, 4};
     int64_t rows = n_points;
     size_t pose_off = 0;
-    if (!full) {  // the records Preprocess keeps by index, still packed
-        rc = stage_sweep(c->filt, data, n_points, (size_t)point_step, pp.point_filter_num, poses, n_poses, &rows,
-                         &pose_off);
-        if (rc) return rc;
-        sp.point_filter_num = 1;
-    }
+    // the records Preprocess keeps by index, still packed
+    rc = stage_sweep(c->filt, data, n_points, (size_t)point_step, pp.point_filter_num, poses, n_poses, &rows, &pose_off);
+    if (rc) return rc;
+    sp.point_filter_num = 1;
     const int64_t bytes = rows * point_step;
     rc = grow(&c->d_rec, c->rec_cap, std::max<int64_t>((bytes + 3) / 4, rows * 5 + 1));  // staging for the bytes
     if (!rc) rc = grow(&c->d_raw, c->raw_cap, std::max<int64_t>(rows, 1) * 5);
@@ -1637,9 +1593,9 @@ int lio_scan_preprocess_cloud2(lio_ctx* c, const uint8_t* data, int64_t n_points
     if (rc) return rc;
     const auto* stage = static_cast<const uint8_t*>(c->filt.h_stage);
     if (rows)
-        HIP_TRY(hipMemcpyAsync(c->d_rec, full ? (const void*)data : stage, (size_t)bytes, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(c->d_rec, stage, (size_t)bytes, hipMemcpyHostToDevice, st));
     if (n_poses)
-        HIP_TRY(hipMemcpyAsync(c->d_poses, full ? (const void*)poses : stage + pose_off,
+        HIP_TRY(hipMemcpyAsync(c->d_poses, stage + pose_off,
                                (size_t)n_poses * sizeof(lio::ImuPose), hipMemcpyHostToDevice, st));
     rc = lio::cloud_decode(reinterpret_cast<const uint8_t*>(c->d_rec), rows, point_step, is_bigendian != 0,
                            reinterpret_cast<const lio::CloudField*>(fields), 5, c->d_raw, st);

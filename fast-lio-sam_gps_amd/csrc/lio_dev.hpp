@@ -700,16 +700,10 @@ __device__ int group_knn_seeded(const GridDev& g, float bound, int cx, int cy, i
 // the box, because the grid build's cell assignment (cell_coord, clamped) is
 // monotone in each coordinate.  Must be called
 // by all NT threads of the block (it synchronises the block).
-// DEDUP: the caller's list (tk on entry) may hold points from OUTSIDE the query's 3x3x3 block (the cell-grouped
-// near pass scans the union of its wave's blocks): a candidate whose key is already in that list is not pushed
-// again, so the box outside the block never duplicates it.
-template <int K, int NT, bool DEDUP = false>
+template <int K, int NT>
 __device__ void block_knn_box_flat(const GridDev& g, float qx, float qy, float qz, uint32_t* s_b, uint32_t* s_off,
                                    uint32_t* s_w, uint64_t* s_lists, TopK<K>& tk, bool whole = false) {
     static_assert(NT % 64 == 0 && NT <= 1024, "block_knn_box_flat: NT = multiple of 64");
-    [[maybe_unused]] uint64_t ex[K];
-#pragma unroll
-    for (int j = 0; j < K; ++j) ex[j] = tk.k[j];
     constexpr int NW = NT / 64;
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int cx = cell_coord(qx, g.ox, g.inv_cell);
@@ -797,13 +791,7 @@ __device__ void block_knn_box_flat(const GridDev& g, float qx, float qy, float q
                 for (int u = 0; u < 4; ++u)
                     if (t + (uint32_t)u < c1) {
                         const float d = sqdist3(qx, qy, qz, pp[u].x, pp[u].y, pp[u].z);
-                        bool dup = false;
-                        if constexpr (DEDUP) {
-                            const uint64_t key = knn_key(d, __float_as_int(pp[u].w));
-#pragma unroll
-                            for (int j = 0; j < K; ++j) dup = dup || key == ex[j];
-                        }
-                        if (!dup) tk.push(d, __float_as_int(pp[u].w));
+                        tk.push(d, __float_as_int(pp[u].w));
                     }
             }
         }

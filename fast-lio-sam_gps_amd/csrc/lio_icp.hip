@@ -60,22 +60,11 @@ __device__ __forceinline__ void xform_pcl(const float* T, float x, float y, floa
 // Total order (d2, id), d2 = float ((dx*dx + dy*dy) + dz*dz): the result
 // does not depend on the tiling.
 // ----------------------------------------------------------------------------
-#ifndef LIO_TILE_CH
-#define LIO_TILE_CH 256
-#endif
-constexpr int kTileCh = LIO_TILE_CH;  // candidates staged per LDS round
-#ifndef LIO_ICP_ZORDER
-#define LIO_ICP_ZORDER 1  // a round's rows by z slice centre-out from the tile (0: z ascending)
-#endif
-#ifndef LIO_ICP_YORDER
-#define LIO_ICP_YORDER 1  // and within a slice, rows by y centre-out (0: y ascending)
-#endif
-#ifndef LIO_ICP_ROW_TIGHTEN
-#define LIO_ICP_ROW_TIGHTEN 1  // rows trimmed per 64-row batch by the lanes' current bests (0: by the round's B)
-#endif
-#ifndef LIO_ICP_GROW
-#define LIO_ICP_GROW 1  // box growth per round past r = 3 (0: doubling throughout)
-#endif
+// The measured-best search shape (A/B history in DESIGN §4; the build switches that selected the variants are
+// gone): 256 candidates staged per LDS round (128 equal, 512 slower), a round's rows by z slice and then by y
+// row centre-out from the tile, rows trimmed per 64-row batch by the lanes' current bests, the growing box
+// doubled while r < 3 and then widened by one cell a round.
+constexpr int kTileCh = 256;  // candidates staged per LDS round
 
 // Tiles -> blocks (launch_icp_tiles: 8 x (kIcpSegs / 8) x ceil(n / kIcpSegs) blocks; block b runs on
 // XCD b % 8).  The cell-ordered tiles form kIcpSegs contiguous segments; XCD x owns segments x, x + 8,
@@ -112,6 +101,8 @@ struct alignas(16) TileLds {
         uint4 perm[kIcpTileQ];  // a batch of rows (b0, n0, b1, n1), re-ordered nearest-first
     };
 };
+// the transform history of up to 64 passes (64 x 16 floats) is staged in x, y, z, id before the first round
+static_assert(4 * kTileCh >= 64 * 16, "TileLds: the staging area must hold the LDS transform history");
 
 // squared gap between the closed intervals [lo, hi] and [a, b]
 __device__ __forceinline__ float interval_gap(float lo, float hi, float a, float b) {
@@ -248,8 +239,8 @@ __device__ __forceinline__ void row_pieces(const GridDev& g, const CellBox& N, c
     const bool sempty = S.x0 > S.x1;
     const uint32_t gnx = (uint32_t)g.nx, gnxy = (uint32_t)g.nx * (uint32_t)g.ny;
     // z slices nearest the tile first (its rows' batches come first, so the bests fall before the far slices)
-    const int rz = LIO_ICP_ZORDER ? center_out(r / ny, N.z0, N.z1, zc) : N.z0 + r / ny;
-    const int ry = LIO_ICP_YORDER ? center_out(r % ny, N.y0, N.y1, yc) : N.y0 + r % ny;
+    const int rz = center_out(r / ny, N.z0, N.z1, zc);
+    const int ry = center_out(r % ny, N.y0, N.y1, yc);
     int x0 = N.x0, x1 = N.x1;
     bool keep = true;
     const float yl = g.oy + (float)ry * cs - m, zl = g.oz + (float)rz * cs - m;
@@ -295,13 +286,9 @@ __device__ void scan_rows(const GridDev& g, TileLds& L, const CellBox& N, const 
         const int r = rb + lane;
         uint32_t b0 = 0, n0 = 0, b1 = 0, n1 = 0;
         float g2 = INFINITY;
-#if LIO_ICP_ROW_TIGHTEN
         // the bound as it stands now: every active lane's best (+inf while one has none) only falls, so a row
         // farther than all of them cannot improve any lane, in this round or in the final sphere that follows
         const float Bb = fminf(B, wave_max_nonneg(act ? __uint_as_float((uint32_t)(best >> 32)) : 0.f));
-#else
-        const float Bb = B;
-#endif
         if (r < nrows) row_pieces(g, N, S, Bb, qb, r, zc, yc, b0, n0, b1, n1, g2);
         // nearest rows first (stable partition by the row's (y, z) gap to the tile box: 0, <= 1,
         // <= 2 cells, farther), so the staging filter's bound tightens early in the stream; any
@@ -461,9 +448,9 @@ __device__ __forceinline__ void icp_tile_body(const IcpArgs& a, int tix, int nti
         const bool full = N.x0 == 0 && N.y0 == 0 && N.z0 == 0 && N.x1 == g.nx - 1 && N.y1 == g.ny - 1 && N.z1 == g.nz - 1;
         if (!grow || full) break;  // final pass done, or the whole grid scanned
         S = N;
-        // empty surroundings: the box doubles while small, then grows by LIO_ICP_GROW cells a round (a doubled
-        // box overshoots the nearest points by up to its own size, and every point it holds is streamed)
-        r = (LIO_ICP_GROW == 0 || r < 3) ? 2 * r + 1 : r + LIO_ICP_GROW;
+        // empty surroundings: the box doubles while small, then grows by one cell a round (a doubled box
+        // overshoots the nearest points by up to its own size, and every point it holds is streamed)
+        r = r < 3 ? 2 * r + 1 : r + 1;
     }
     // the tile's cost for the next pass's longest-first order: candidates tested over its waves
     uint32_t tile_tested = tested;
@@ -714,10 +701,7 @@ int icp_build_tiles(const GridBuf& q, uint2* tiles, uint32_t* scratch, void*& tm
     uint32_t* cell = key2 + nc;             // nc
     uint32_t* cell2 = cell + nc;            // nc
     const int nb = (int)((nc + 1 + 255) / 256);
-#ifndef LIO_TILE_MORTON
-#define LIO_TILE_MORTON 1  // A/B builds: 0 keeps the x-fastest cell order
-#endif
-    const int morton = LIO_TILE_MORTON && q.geom.nx <= 1024 && q.geom.ny <= 1024 && q.geom.nz <= 1024 ? 1 : 0;
+    const int morton = q.geom.nx <= 1024 && q.geom.ny <= 1024 && q.geom.nz <= 1024 ? 1 : 0;
     tile_key_kernel<<<nb, 256, 0, st>>>(q.start, q.geom, morton, key, cell);
     size_t need_scan = 0, need_sort = 0;
     if (hipcub::DeviceScan::ExclusiveSum(nullptr, need_scan, tcount, toff, (int)(nc + 1), st) != hipSuccess ||

@@ -757,8 +757,10 @@ static uint32_t pcl_word(const lio_icp* h, int w) {
 
 static int pcl_finish(lio_icp* h, const lio::IcpArgs& a) {
     const int order = h->p.umeyama_float;
-    if (pcl_word(h, 3) != 0)  // h_pclout[19]
-        return ifail(LIO_ERR_HIP, "lio_icp_align: the correspondence compaction's look-back timed out");
+    // the compaction's look-back timed out (h_pclout[19]; never expected): its pairs cannot be trusted, so the
+    // serial kernels below re-compact them; the flag is cleared here, or every later pass would see it
+    const bool lb_timeout = pcl_word(h, 3) != 0;
+    if (lb_timeout) IHIP(hipMemsetAsync(h->pcl.small + lio::kPclTicket + 1, 0, sizeof(uint32_t), h->st));
     ++h->fid_stats[3];
     {
         int ev;
@@ -767,8 +769,11 @@ static int pcl_finish(lio_icp* h, const lio::IcpArgs& a) {
     }
     constexpr int kMaxPasses = 4;  // per chain set; the verification makes any pass count safe
     int mpass = 1, spass = 1;
-    while ((pcl_word(h, 0) | pcl_word(h, 1)) != 0) {
+    while (!lb_timeout && (pcl_word(h, 0) | pcl_word(h, 1)) != 0) {
         const uint32_t bad = pcl_word(h, 0), over = pcl_word(h, 1);
+        // a failed verification set forced-event bits: whatever runs next (a re-pass, a restarted sigma pass 1,
+        // the serial fallback), the next pass 1 must clear them (stale bits only add events)
+        if (bad) h->pcl.means.forced_dirty = h->pcl.sig.forced_dirty = true;
         if (over) break;  // more passes only add events
         if (bad & 0x3fu) {  // the means (sigma depends on them: its chains restart from pass 1)
             if (mpass >= kMaxPasses) break;
@@ -785,7 +790,7 @@ static int pcl_finish(lio_icp* h, const lio::IcpArgs& a) {
         IHIP(hipMemcpyAsync(h->h_pclout, h->d_pclout, lio::kPclOutWords * sizeof(float), hipMemcpyDeviceToHost, h->st));
         IHIP(hipStreamSynchronize(h->st));
     }
-    if ((pcl_word(h, 0) | pcl_word(h, 1)) != 0) {  // the serial kernels: one lane per chain
+    if (lb_timeout || (pcl_word(h, 0) | pcl_word(h, 1)) != 0) {  // the serial kernels: one lane per chain
         ++h->fid_stats[1];
         if (order == lio::kPclSeq) {
             lio::launch_icp_pcl_stats(a, h->pcl.pairs, h->pcl.cap, h->d_pcl16, h->st);
@@ -808,6 +813,8 @@ static int pcl_finish(lio_icp* h, const lio::IcpArgs& a) {
 static int enqueue_pcl(lio_icp* h, const lio::IcpArgs& pa) {
     const int order = h->p.umeyama_float;
     lio::launch_pcl_compact(pa, h->pcl, h->st);
+    if (h->fid_flags & 4)  // test hook (lio_icp_set_fidelity_debug): report a look-back time-out for this pass
+        IHIP(hipMemsetAsync(h->pcl.small + lio::kPclTicket + 1, 1, sizeof(uint32_t), h->st));
     lio::launch_pcl_means(h->pcl, 1, h->st);
     lio::launch_pcl_sigma(h->pcl, order, 1, h->st);
     lio::launch_pcl_pack(h->pcl, order, h->d_pclout, h->st);
@@ -834,12 +841,8 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     a.fitness = fitness ? 1 : 0;
     a.prior = h->have_prior ? 1 : 0;
     // first bound box: the tile's own cells (r0 = 0; with the per-batch bound and the centre-out rows, pair A
-    // 0.221 -> 0.212 ms per alignment against r0 = 1, pair B unchanged: profiles/r05_icp_r0_ab.txt); LIO_ICP_R0
-    static const int r0 = [] {
-        const char* e = std::getenv("LIO_ICP_R0");
-        return e ? std::max(0, std::min(8, std::atoi(e))) : 0;
-    }();
-    a.r0 = r0;
+    // 0.221 -> 0.212 ms per alignment against r0 = 1, pair B unchanged: profiles/r05_icp_r0_ab.txt)
+    a.r0 = 0;
     a.nn_d2 = h->d_fd2;
     a.nn_id = h->d_fid;
     a.qpts = h->qgrid.pts;

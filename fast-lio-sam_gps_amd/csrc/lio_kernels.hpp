@@ -37,8 +37,6 @@ struct MatchArgs {
     float knn_M[12];          // the same as one float affine map body -> world (row-major 3x4): the seeded
                               // pass's displacement bound (error covered by a margin)
     float seed_scale;         // seeded bound factor: 1 (lio_ctx_set_seed_scale < 1 forces the not-full guard: tests)
-    int* perm;                // n: query order grouped by world cell (knn_group_kernel at a scan's first kNN
-                              // evaluation); nullptr: the per-query near pass (8 lanes per query)
 };
 
 // marks (optional, timing): 8 events, start / stop of near, far, plane (redo) or reuse (marks[6..7]),

@@ -162,253 +162,10 @@ __global__ void __launch_bounds__(NB) __attribute__((amdgpu_waves_per_eu(8, 8)))
     if (sub == 5) a.nn_d5[i] = tk.id(4) == kNone ? INFINITY : tk.d(4);
 }
 
-// ----------------------------------------------------------------------------
-// Cell-grouped near pass (opt-in A/B, LIO_KNN_NEAR=cell; VERDICT r04 next #5 — bit-identical but 12x slower
-// than the per-query pass at C3/C2, DESIGN §4: the wave tests every point of the union, which the per-query
-// box pruning never touches).  A C3 Livox scan puts its 131 k queries in ~2.2 k
-// map cells (median 8, p90 100 queries per 1 m cell), so queries of one cell share their 27-cell candidate set:
-//   knn_group_kernel  once per scan (the first kNN evaluation): each block of 1024 consecutive queries sorted
-//                     by world cell (bitonic, LDS) -> perm; 64 consecutive entries of perm = one wave's queries
-//                     (~3 distinct cells per wave at C3)
-//   knn_cell_kernel   one wave per 64 grouped queries, lane = query: the union of the wave's 3x3x3 blocks
-//                     (each cell once: a head cell's neighbour inside an earlier head's block is skipped),
-//                     own cells first, streamed through LDS in chunks of 256 with the ICP staging filter (a
-//                     point farther from the wave's query box than every lane's current 5th best cannot
-//                     enter any list), every lane testing every survivor (packed FP32 distances, TopK<5>
-//                     under the (d2, id) total order: the list does not depend on the arrival order)
-// The result contract is group_knn_near's / group_knn_seeded's: a query whose 5th best lies inside its block
-// (worst < (own + cell)^2) is final — its list is then the exact top-5 whatever extra cells the wave added —
-// and the others go to the far pass with their list, which is the exact top-5 over a superset of the block
-// (points of other lanes' blocks included: the far pass skips keys already in the list, DEDUP).  The
-// grouping only shapes the work: every lane transforms its own query with the current pose.
-// ----------------------------------------------------------------------------
-constexpr int kGroupSort = 1024;  // queries sorted per block
-constexpr int kCellBlock = 256;   // near pass: 4 waves of 64 grouped queries
-constexpr int kCellCh = 256;      // candidates staged per LDS round (per wave)
-
-__global__ void __launch_bounds__(kGroupSort) knn_group_kernel(MatchArgs a) {
-    __shared__ uint64_t s[kGroupSort];
-    const int tid = threadIdx.x;
-    const int base = blockIdx.x * kGroupSort;
-    const int i = base + tid;
-    uint64_t key = ~0ull;  // pads sort last
-    if (i < a.n) {
-        float wx, wy, wz;
-        body_to_world(a.pose, a.body[3 * i], a.body[3 * i + 1], a.body[3 * i + 2], wx, wy, wz);
-        const GridDev& g = a.grid;
-        const int cx = cell_coord(wx, g.ox, g.inv_cell), cy = cell_coord(wy, g.oy, g.inv_cell),
-                  cz = cell_coord(wz, g.oz, g.inv_cell);
-        const bool inside = (unsigned)cx < (unsigned)g.nx && (unsigned)cy < (unsigned)g.ny && (unsigned)cz < (unsigned)g.nz;
-        const uint32_t lin = inside ? ((uint32_t)cz * (uint32_t)g.ny + (uint32_t)cy) * (uint32_t)g.nx + (uint32_t)cx
-                                    : 0xfffffffeu;
-        key = ((uint64_t)lin << 32) | (uint32_t)tid;
-    }
-    s[tid] = key;
-    __syncthreads();
-    for (int k = 2; k <= kGroupSort; k <<= 1)
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            const int p = tid ^ j;
-            if (p > tid) {
-                const uint64_t x = s[tid], y = s[p];
-                if ((x > y) == ((tid & k) == 0)) {
-                    s[tid] = y;
-                    s[p] = x;
-                }
-            }
-            __syncthreads();
-        }
-    if (i < a.n) a.perm[i] = base + (int)(uint32_t)s[tid];
-}
-
-struct alignas(16) CellLds {
-    float x[kCellCh], y[kCellCh], z[kCellCh];  // staged candidates (structure of arrays)
-    uint32_t id[kCellCh];
-    uint32_t b[64];                            // this round's cell ranges: start, exclusive prefix (+ total)
-    uint32_t off[65];
-    int hx[64], hy[64], hz[64];                // the wave's distinct query cells (heads)
-};
-
-// One round: every lane contributes one cell range [b, b + n); the concatenation streams through LDS in
-// chunks of kCellCh, those farther from the wave's query box qb than every accepting lane's 5th best dropped
-// (margin 1e-5 for the rounding of the gap and of d2), the survivors compacted (ballot + mbcnt) and tested by
-// every lane.
-__device__ __forceinline__ void cell_scan_round(const GridDev& g, CellLds& L, uint32_t b, uint32_t n, bool take,
-                                                float qx, float qy, float qz, const float (&qb)[6], TopK<5>& tk) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t incl = wave_incl_scan_dpp(n);
-    const uint32_t T = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-    if (T == 0) return;  // wave-uniform
-    wave_sync();          // the previous round's readers of the slot table are done
-    L.b[lane] = b;
-    L.off[lane] = incl - n;
-    if (lane == 63) L.off[64] = T;
-    wave_sync();
-    int sl = 0;
-    uint32_t lo = 0, hi = L.off[1], sb = L.b[0];
-#pragma unroll 1
-    for (uint32_t base = 0; base < T; base += kCellCh) {
-        constexpr int U = kCellCh / 64;
-        float4 v[U];
-#pragma unroll
-        for (int u = 0; u < U; ++u) {  // slot walk first (clamped to the last point), U loads in flight
-            const uint32_t t = min(base + (uint32_t)(u * 64 + lane), T - 1);
-            while (t >= hi) {
-                ++sl;
-                lo = hi;
-                hi = L.off[sl + 1];
-                sb = L.b[sl];
-            }
-            v[u] = g.pts[sb + (t - lo)];
-        }
-        const float Bw = wave_max_nonneg(take ? tk.worst() : 0.f);
-        uint32_t cnt = 0;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const float gx = fmaxf(fmaxf(qb[0] - v[u].x, v[u].x - qb[1]), 0.f);
-            const float gy = fmaxf(fmaxf(qb[2] - v[u].y, v[u].y - qb[3]), 0.f);
-            const float gz = fmaxf(fmaxf(qb[4] - v[u].z, v[u].z - qb[5]), 0.f);
-            const float gap2 = (gx * gx + gy * gy) + gz * gz;
-            const bool in = base + (uint32_t)(u * 64 + lane) < T && !(gap2 * (1.f - 1e-5f) > Bw);
-            const uint64_t m = __ballot(in);
-            const uint32_t r = cnt + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-            if (in) {
-                L.x[r] = v[u].x;
-                L.y[r] = v[u].y;
-                L.z[r] = v[u].z;
-                L.id[r] = __float_as_uint(v[u].w);
-            }
-            cnt += (uint32_t)__popcll(m);
-        }
-        const uint32_t cnt2 = (cnt + 1u) & ~1u;
-        if (lane == 0 && cnt2 != cnt) {  // pad to a pair: +inf, kNone (never enters a list)
-            L.x[cnt] = INFINITY;
-            L.y[cnt] = INFINITY;
-            L.z[cnt] = INFINITY;
-            L.id[cnt] = (uint32_t)kNone;
-        }
-        wave_sync();
-        const f2v qx2 = {qx, qx}, qy2 = {qy, qy}, qz2 = {qz, qz};
-        for (uint32_t j = 0; j < cnt2; j += 2) {  // packed FP32 distances, ((dx*dx + dy*dy) + dz*dz) per element
-            const float2 X = *reinterpret_cast<const float2*>(&L.x[j]);
-            const float2 Y = *reinterpret_cast<const float2*>(&L.y[j]);
-            const float2 Z = *reinterpret_cast<const float2*>(&L.z[j]);
-            const uint2 I = *reinterpret_cast<const uint2*>(&L.id[j]);
-            const f2v dx = qx2 - f2v{X.x, X.y}, dy = qy2 - f2v{Y.x, Y.y}, dz = qz2 - f2v{Z.x, Z.y};
-            const f2v d = (dx * dx + dy * dy) + dz * dz;
-            tk.push2(knn_key(d.x, (int)I.x), knn_key(d.y, (int)I.y));
-        }
-        wave_sync();  // chunk consumed before it is overwritten
-    }
-}
-
-template <bool SEEDED>
-__global__ void __launch_bounds__(kCellBlock) knn_cell_kernel(MatchArgs a) {
-    __shared__ CellLds Ls[kCellBlock / 64];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    CellLds& L = Ls[wv];
-    const GridDev& g = a.grid;
-    const int slot = (xcd_block(blockIdx.x, gridDim.x) * (kCellBlock / 64) + wv) * 64 + lane;
-    const bool act = slot < a.n;
-    const int i = act ? a.perm[slot] : 0;
-    float bx = 0.f, by = 0.f, bz = 0.f, wx = 0.f, wy = 0.f, wz = 0.f;
-    if (act) {
-        bx = a.body[3 * i];
-        by = a.body[3 * i + 1];
-        bz = a.body[3 * i + 2];
-        body_to_world(a.pose, bx, by, bz, wx, wy, wz);
-    }
-    const int cx = cell_coord(wx, g.ox, g.inv_cell), cy = cell_coord(wy, g.oy, g.inv_cell),
-              cz = cell_coord(wz, g.oz, g.inv_cell);
-    const bool inside = act && (unsigned)cx < (unsigned)g.nx && (unsigned)cy < (unsigned)g.ny && (unsigned)cz < (unsigned)g.nz;
-    float bound = a.range_sq;
-    if constexpr (SEEDED) {
-        if (act) {  // the triangle bound from this scan's previous kNN (group_knn_seeded)
-            const float* M = a.knn_M;
-            const float wox = ((M[0] * bx + M[1] * by) + M[2] * bz) + M[3];
-            const float woy = ((M[4] * bx + M[5] * by) + M[6] * bz) + M[7];
-            const float woz = ((M[8] * bx + M[9] * by) + M[10] * bz) + M[11];
-            bound = seeded_bound(inside, a.nn_d5[i], wox, woy, woz, wx, wy, wz, a.range_sq, a.seed_scale);
-        }
-    }
-    TopK<5> tk;
-    tk.init(bound);
-    // lanes that take no candidate (inactive, or the query outside the grid: the far pass searches its whole
-    // box) test from a far-away point: d2 overflows to +inf and never enters the list
-    const float qx = inside ? wx : 1e30f, qy = inside ? wy : 1e30f, qz = inside ? wz : 1e30f;
-    const float qb[6] = {wave_ext_dpp<false>(inside ? wx : INFINITY), wave_ext_dpp<true>(inside ? wx : -INFINITY),
-                         wave_ext_dpp<false>(inside ? wy : INFINITY), wave_ext_dpp<true>(inside ? wy : -INFINITY),
-                         wave_ext_dpp<false>(inside ? wz : INFINITY), wave_ext_dpp<true>(inside ? wz : -INFINITY)};
-    // the wave's distinct cells: a lane whose cell differs from its left neighbour's is a head (equal cells that
-    // are not adjacent give a second head whose block is wholly inside the first's: skipped below)
-    const uint32_t lin = inside ? ((uint32_t)cz * (uint32_t)g.ny + (uint32_t)cy) * (uint32_t)g.nx + (uint32_t)cx
-                                : 0xffffffffu;
-    const uint32_t prv = (uint32_t)__shfl_up((int)lin, 1, 64);
-    const bool head = inside && (lane == 0 || lin != prv);
-    const uint64_t hm = __ballot(head);
-    const int D = __popcll(hm);
-    if (head) {
-        const int h = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(hm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)hm, 0u));
-        L.hx[h] = cx;
-        L.hy[h] = cy;
-        L.hz[h] = cz;
-    }
-    wave_sync();
-    const int ncand = 27 * D;  // (block offset o, head) pairs, offset-major: every head's own cell first
-#pragma unroll 1
-    for (int cb = 0; cb < ncand; cb += 64) {
-        const int j = cb + lane;
-        uint32_t b = 0, n = 0;
-        if (j < ncand) {
-            const int o = j / D, hh = j - o * D;
-            const int k = o == 0 ? 13 : (o <= 13 ? o - 1 : o);  // 13 = the block's centre
-            const int x = L.hx[hh] + k % 3 - 1, y = L.hy[hh] + (k / 3) % 3 - 1, z = L.hz[hh] + k / 9 - 1;
-            bool keep = (unsigned)x < (unsigned)g.nx && (unsigned)y < (unsigned)g.ny && (unsigned)z < (unsigned)g.nz;
-            for (int h2 = 0; keep && h2 < hh; ++h2)  // inside an earlier head's block: that head covers it
-                keep = !(abs(x - L.hx[h2]) <= 1 && abs(y - L.hy[h2]) <= 1 && abs(z - L.hz[h2]) <= 1);
-            if (keep) {
-                const uint2 r = g.rng[((uint32_t)z * (uint32_t)g.ny + (uint32_t)y) * (uint32_t)g.nx + (uint32_t)x];
-                b = r.x;
-                n = r.y - r.x;
-            }
-        }
-        cell_scan_round(g, L, b, n, inside, qx, qy, qz, qb, tk);
-    }
-    if (!act) return;
-    // final / far decision: group_knn_near's (unseeded) and group_knn_seeded's
-    bool done = false, whole = false;
-    if (inside) {
-        const float cs = g.cell, m = g.margin;
-        const float lox = g.ox + (float)cx * cs, loy = g.oy + (float)cy * cs, loz = g.oz + (float)cz * cs;
-        float own = fminf(fminf(wx - lox, lox + cs - wx), fminf(wy - loy, loy + cs - wy));
-        own = fminf(own, fminf(wz - loz, loz + cs - wz)) - m;
-        if constexpr (SEEDED) {
-            if (tk.id(4) == kNone && bound < a.range_sq) {  // guard: not full under a finite bound
-                tk.init(a.range_sq);
-                whole = true;
-            }
-        }
-        const float gr = own + cs;
-        done = !whole && gr > 0.f && tk.worst() < gr * gr * 0.999999f;
-    }
-    if (!done && a.max_shell > 1) {
-        const int fs = atomicAdd(a.far_count, 1);
-        a.far_list[fs] = whole ? (int)((unsigned)i | 0x80000000u) : i;  // sign bit: search the block too
-#pragma unroll
-        for (int j = 0; j < 5; ++j) {
-            a.far_d[5 * (size_t)fs + j] = tk.d(j);
-            a.far_id[5 * (size_t)fs + j] = tk.id(j);
-        }
-        return;
-    }
-#pragma unroll
-    for (int j = 0; j < 5; ++j) a.nn_idx[5 * (size_t)i + j] = tk.id(j) == kNone ? -1 : tk.id(j);
-    a.nn_d5[i] = tk.id(4) == kNone ? INFINITY : tk.d(4);
-}
-
 // Pass 2: the queued queries, one block each (block_knn_box_flat over the
 // rest of the query's search box).  Fixed grid; every block strides the queue
 // and exits once past its end.
-template <int NT = kFarBlock, bool DEDUP = false>
+template <int NT = kFarBlock>
 __global__ void __launch_bounds__(NT) knn_far_kernel(MatchArgs a) {
     const PoseArg& ps = a.pose;
     __shared__ uint32_t s_b[NT], s_off[NT + 1], s_w[NT / 64];
@@ -422,8 +179,7 @@ __global__ void __launch_bounds__(NT) knn_far_kernel(MatchArgs a) {
         TopK<5> tk;
 #pragma unroll
         for (int j = 0; j < 5; ++j) tk.k[j] = knn_key(a.far_d[5 * (size_t)f + j], a.far_id[5 * (size_t)f + j]);
-        // DEDUP: a cell-grouped near list may already hold points outside this query's 3x3x3 block
-        block_knn_box_flat<5, NT, DEDUP>(a.grid, wx, wy, wz, s_b, s_off, s_w, s_lists, tk, e < 0);
+        block_knn_box_flat<5, NT>(a.grid, wx, wy, wz, s_b, s_off, s_w, s_lists, tk, e < 0);
         if (threadIdx.x == 0) {
 #pragma unroll
             for (int j = 0; j < 5; ++j) a.nn_idx[5 * (size_t)i + j] = tk.id(j) == kNone ? -1 : tk.id(j);
@@ -797,15 +553,6 @@ int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* ma
         if (a.dbg) {  // search statistics (lio_ctx_knn_stats): the per-query group walk
             hipExtLaunchKernelGGL((knn_near_kernel<true, false, 4, kNearBlock, 2>), dim3(nq), dim3(kNearBlock), 0, st,
                                   m[0], m[1], 0, a);
-        } else if (a.perm) {  // cell-grouped near pass; the grouping once per scan (first kNN evaluation)
-            const int nc = (a.n + kCellBlock - 1) / kCellBlock;
-            if (!a.prior) {
-                hipExtLaunchKernelGGL(knn_group_kernel, dim3((a.n + kGroupSort - 1) / kGroupSort), dim3(kGroupSort), 0,
-                                      st, m[0], nullptr, 0, a);
-                hipExtLaunchKernelGGL(knn_cell_kernel<false>, dim3(nc), dim3(kCellBlock), 0, st, nullptr, m[1], 0, a);
-            } else {
-                hipExtLaunchKernelGGL(knn_cell_kernel<true>, dim3(nc), dim3(kCellBlock), 0, st, m[0], m[1], 0, a);
-            }
         } else if (a.prior) {
             hipExtLaunchKernelGGL((knn_near_kernel<false, true, 2, kNearBlock, 4>), dim3(nq), dim3(kNearBlock), 0, st,
                                   m[0], m[1], 0, a);
@@ -813,14 +560,8 @@ int launch_h_model(const MatchArgs& a, bool redo, hipStream_t st, hipEvent_t* ma
             hipExtLaunchKernelGGL((knn_near_kernel<false, false, 4, kNearBlock, 2>), dim3(nq), dim3(kNearBlock), 0, st,
                                   m[0], m[1], 0, a);
         }
-        if (a.max_shell > 1) {
-            if (a.perm && !a.dbg)
-                hipExtLaunchKernelGGL((knn_far_kernel<kFarBlock, true>), dim3(kFarBlocks), dim3(kFarBlock), 0, st, m[2],
-                                      m[3], 0, a);
-            else
-                hipExtLaunchKernelGGL((knn_far_kernel<kFarBlock, false>), dim3(kFarBlocks), dim3(kFarBlock), 0, st,
-                                      m[2], m[3], 0, a);
-        }
+        if (a.max_shell > 1)
+            hipExtLaunchKernelGGL((knn_far_kernel<kFarBlock>), dim3(kFarBlocks), dim3(kFarBlock), 0, st, m[2], m[3], 0, a);
         const int nbp = (a.n + kPlaneBlock - 1) / kPlaneBlock;
         hipExtLaunchKernelGGL((plane_kernel<1, kPlaneBlock>), dim3(nbp), dim3(kPlaneBlock), 0, st, m[4], m[5], 0, a);
         return nbp;

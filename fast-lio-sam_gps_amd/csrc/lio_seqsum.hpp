@@ -25,10 +25,7 @@
 namespace lio {
 
 constexpr int kSeqThreads = 256;                 // threads per block
-#ifndef LIO_SEQ_PER
-#define LIO_SEQ_PER 4  // A/B builds
-#endif
-constexpr int kSeqPer = LIO_SEQ_PER;             // consecutive elements per thread
+constexpr int kSeqPer = 4;                       // consecutive elements per thread (8: slower)
 constexpr int kSeqBlock = kSeqThreads * kSeqPer;  // elements per block
 constexpr int kSeqMaxChains = 9;
 

@@ -89,10 +89,46 @@ def transform_pcd(cloud: np.ndarray, T: np.ndarray) -> np.ndarray:
     return out
 
 
+def eigen_inverse4(T: np.ndarray) -> np.ndarray:
+    """Matrix4d::inverse() (pose_eig_.inverse(), pose_pcd.hpp:39) as an x86-64 Eigen 3.3 build evaluates it:
+    compute_inverse_size4<SSE, double> (Inverse_SSE.h, the 2x2-block "divide and conquer" inverse) on the
+    column-major storage, packet lanes as Python floats (IEEE double, no FMA) — the same operations as
+    include/lio_gpu.hpp inverse4, so the C++ and Python keyframe clouds are bit-identical.  Row-major in/out."""
+    M = np.asarray(T, np.float64).reshape(4, 4)
+    s = [float(M[k % 4, k // 4]) for k in range(16)]  # Eigen's column-major storage
+    A1, B1, A2, B2 = s[0:2], s[2:4], s[4:6], s[6:8]
+    C1, D1, C2, D2 = s[8:10], s[10:12], s[12:14], s[14:16]
+    dA = A1[0] * A2[1] - A1[1] * A2[0]
+    dB = B1[0] * B2[1] - B1[1] * B2[0]
+    AB1 = [B1[0] * A2[1] - B2[0] * A1[1], B1[1] * A2[1] - B2[1] * A1[1]]
+    AB2 = [B2[0] * A1[0] - B1[0] * A2[0], B2[1] * A1[0] - B1[1] * A2[0]]
+    dC = C1[0] * C2[1] - C1[1] * C2[0]
+    dD = D1[0] * D2[1] - D1[1] * D2[0]
+    DC1 = [C1[0] * D2[1] - C2[0] * D1[1], C1[1] * D2[1] - C2[1] * D1[1]]
+    DC2 = [C2[0] * D1[0] - C1[0] * D2[0], C2[1] * D1[0] - C1[1] * D2[0]]
+    rd = (AB1[0] * DC1[0] + AB2[0] * DC1[1]) + (AB1[1] * DC2[0] + AB2[1] * DC2[1])
+    iD1 = [D1[k] * dA - (AB1[k] * C1[0] + AB2[k] * C1[1]) for k in range(2)]
+    iD2 = [D2[k] * dA - (AB1[k] * C2[0] + AB2[k] * C2[1]) for k in range(2)]
+    iA1 = [A1[k] * dD - (DC1[k] * B1[0] + DC2[k] * B1[1]) for k in range(2)]
+    iA2 = [A2[k] * dD - (DC1[k] * B2[0] + DC2[k] * B2[1]) for k in range(2)]
+    det = (dA * dD + dB * dC) - rd
+    if not abs(det) > 0.0:
+        raise ValueError("eigen_inverse4: singular pose")
+    iB1 = [C1[0] * dB - (D1[0] * AB2[1] - D1[1] * AB2[0]), C1[1] * dB - (D1[1] * AB1[0] - D1[0] * AB1[1])]
+    iB2 = [C2[0] * dB - (D2[0] * AB2[1] - D2[1] * AB2[0]), C2[1] * dB - (D2[1] * AB1[0] - D2[0] * AB1[1])]
+    iC1 = [B1[0] * dC - (A1[0] * DC2[1] - A1[1] * DC2[0]), B1[1] * dC - (A1[1] * DC1[0] - A1[0] * DC1[1])]
+    iC2 = [B2[0] * dC - (A2[0] * DC2[1] - A2[1] * DC2[0]), B2[1] * dC - (A2[1] * DC1[0] - A2[0] * DC1[1])]
+    r = 1.0 / det
+    o = [0.0] * 16
+    for k, X1, X2 in ((0, iA1, iA2), (2, iB1, iB2), (8, iC1, iC2), (10, iD1, iD2)):
+        o[k], o[k + 1], o[k + 4], o[k + 5] = X2[1] * r, -(X1[1] * r), -(X2[0] * r), X1[0] * r
+    return np.array([[o[4 * c + rr] for c in range(4)] for rr in range(4)], np.float64)
+
+
 def keyframe_from_odometry(state: dict, world_xyzi: np.ndarray, timestamp: float, idx: int) -> LC.PosePcd:
     """PosePcd(odom, cloud, idx) (pose_pcd.hpp:22-42): pcd_ = transformPcd(cloud, pose_eig_.inverse())."""
     T = odom_matrix(state)
-    pcd = transform_pcd(world_xyzi, np.linalg.inv(T))
+    pcd = transform_pcd(world_xyzi, eigen_inverse4(T))
     return LC.PosePcd(pcd_=pcd, pose_corrected_eig_=T.copy(), pose_eig_=T.copy(), timestamp_=float(timestamp), idx_=idx)
 
 
@@ -133,7 +169,7 @@ class FastLioSamStream:
         """The keyframe of this sweep, its cloud built on the GPU (lio_scan_keyframe_cloud): the same
         numbers as keyframe_from_odometry(x, world cloud) on the host, one kernel + one copy."""
         T = odom_matrix(x)
-        pcd = self.hm.keyframe_cloud(F.pose_from_pose24(synth.pose24(x)), np.linalg.inv(T))
+        pcd = self.hm.keyframe_cloud(F.pose_from_pose24(synth.pose24(x)), eigen_inverse4(T))
         return LC.PosePcd(pcd_=pcd, pose_corrected_eig_=T.copy(), pose_eig_=T.copy(), timestamp_=float(timestamp), idx_=idx)
 
     def keyframe_host(self, x: dict, timestamp: float, idx: int) -> LC.PosePcd:

@@ -315,7 +315,9 @@ int lio_icp_umeyama_pcl_float_order(const float* sums16, int order, float* T16);
 /* Diagnostics of the float fidelity modes: out4 = [verification re-passes, serial fallbacks, events of
  * the last pass (max over chains), passes run] since the handle was created.  Test hook: flags bit 0
  * makes the first seqsum pass skip its grid-coarsening event rule (verification then fails and the
- * re-pass path runs); evcap > 0 caps the events per chain (overflow -> the serial fallback).       */
+ * re-pass path runs); flags & 4 reports a compaction look-back time-out on every pass (the pass then
+ * re-compacts on the serial kernels and clears the flag); evcap > 0 caps the events per chain
+ * (overflow -> the serial fallback).                                                              */
 int lio_icp_get_fidelity_stats(lio_icp* h, int64_t* out4);
 int lio_icp_set_fidelity_debug(lio_icp* h, int flags, int64_t evcap);
 /* Test hook: sequential float sums of 6 interleaved chains (x: n x 6 host floats) on `device` through

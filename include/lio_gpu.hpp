@@ -576,33 +576,60 @@ inline void odom_matrix(const lio_state& x, double T[16]) {
     T[15] = 1.0;
 }
 
-// Matrix4d::inverse() (pose_eig_.inverse()): the general 4x4 inverse through 2x2 sub-determinants
-// (cofactors / determinant); equal to Eigen's up to the last bits (the keyframe cloud's tolerance)
+// Matrix4d::inverse() (pose_eig_.inverse(), pose_pcd.hpp:39) as an x86-64 build of Eigen 3.3 evaluates it:
+// Architecture::Target is SSE (SSE2 is on by default), so compute_inverse_size4<SSE, double> (Inverse_SSE.h,
+// the "divide and conquer" 2x2-block inverse) runs on the column-major storage — restated here op for op
+// (packet lanes as scalars, no FMA), bit-identical to lio_gpu.pipeline.eigen_inverse4 on the Python side.
+// m, inv: row-major.  Restated from Eigen's published algorithm; a binary of the reference is not available to
+// pin it.
 inline void inverse4(const double m[16], double inv[16]) {
-    const double s0 = m[0] * m[5] - m[4] * m[1], s1 = m[0] * m[6] - m[4] * m[2], s2 = m[0] * m[7] - m[4] * m[3];
-    const double s3 = m[1] * m[6] - m[5] * m[2], s4 = m[1] * m[7] - m[5] * m[3], s5 = m[2] * m[7] - m[6] * m[3];
-    const double c5 = m[10] * m[15] - m[14] * m[11], c4 = m[9] * m[15] - m[13] * m[11];
-    const double c3 = m[9] * m[14] - m[13] * m[10], c2 = m[8] * m[15] - m[12] * m[11];
-    const double c1 = m[8] * m[14] - m[12] * m[10], c0 = m[8] * m[13] - m[12] * m[9];
-    const double det = s0 * c5 - s1 * c4 + s2 * c3 + s3 * c2 - s4 * c1 + s5 * c0;
+    double s[16];  // Eigen's column-major storage: s[k] = M(k % 4, k / 4)
+    for (int k = 0; k < 16; ++k) s[k] = m[4 * (k % 4) + k / 4];
+    const double A1[2] = {s[0], s[1]}, B1[2] = {s[2], s[3]}, A2[2] = {s[4], s[5]}, B2[2] = {s[6], s[7]};
+    const double C1[2] = {s[8], s[9]}, D1[2] = {s[10], s[11]}, C2[2] = {s[12], s[13]}, D2[2] = {s[14], s[15]};
+    const double dA = A1[0] * A2[1] - A1[1] * A2[0], dB = B1[0] * B2[1] - B1[1] * B2[0];
+    const double AB1[2] = {B1[0] * A2[1] - B2[0] * A1[1], B1[1] * A2[1] - B2[1] * A1[1]};  // A# B
+    const double AB2[2] = {B2[0] * A1[0] - B1[0] * A2[0], B2[1] * A1[0] - B1[1] * A2[0]};
+    const double dC = C1[0] * C2[1] - C1[1] * C2[0], dD = D1[0] * D2[1] - D1[1] * D2[0];
+    const double DC1[2] = {C1[0] * D2[1] - C2[0] * D1[1], C1[1] * D2[1] - C2[1] * D1[1]};  // D# C
+    const double DC2[2] = {C2[0] * D1[0] - C1[0] * D2[0], C2[1] * D1[0] - C1[1] * D2[0]};
+    const double rd = (AB1[0] * DC1[0] + AB2[0] * DC1[1]) + (AB1[1] * DC2[0] + AB2[1] * DC2[1]);  // tr(A#B D#C)
+    double iD1[2] = {AB1[0] * C1[0] + AB2[0] * C1[1], AB1[1] * C1[0] + AB2[1] * C1[1]};  // C A# B
+    double iD2[2] = {AB1[0] * C2[0] + AB2[0] * C2[1], AB1[1] * C2[0] + AB2[1] * C2[1]};
+    double iA1[2] = {DC1[0] * B1[0] + DC2[0] * B1[1], DC1[1] * B1[0] + DC2[1] * B1[1]};  // B D# C
+    double iA2[2] = {DC1[0] * B2[0] + DC2[0] * B2[1], DC1[1] * B2[0] + DC2[1] * B2[1]};
+    for (int k = 0; k < 2; ++k) {
+        iD1[k] = D1[k] * dA - iD1[k];
+        iD2[k] = D2[k] * dA - iD2[k];
+        iA1[k] = A1[k] * dD - iA1[k];
+        iA2[k] = A2[k] * dD - iA2[k];
+    }
+    const double d1 = dA * dD, d2 = dB * dC;
+    double iB1[2] = {D1[0] * AB2[1] - D1[1] * AB2[0], D1[1] * AB1[0] - D1[0] * AB1[1]};  // D (A# B)#
+    double iB2[2] = {D2[0] * AB2[1] - D2[1] * AB2[0], D2[1] * AB1[0] - D2[0] * AB1[1]};
+    const double det = (d1 + d2) - rd;
     if (!(std::fabs(det) > 0.0)) throw Error(LIO_ERR_ARG, "inverse4: singular pose");
-    const double id = 1.0 / det;
-    inv[0] = (m[5] * c5 - m[6] * c4 + m[7] * c3) * id;
-    inv[1] = (-m[1] * c5 + m[2] * c4 - m[3] * c3) * id;
-    inv[2] = (m[13] * s5 - m[14] * s4 + m[15] * s3) * id;
-    inv[3] = (-m[9] * s5 + m[10] * s4 - m[11] * s3) * id;
-    inv[4] = (-m[4] * c5 + m[6] * c2 - m[7] * c1) * id;
-    inv[5] = (m[0] * c5 - m[2] * c2 + m[3] * c1) * id;
-    inv[6] = (-m[12] * s5 + m[14] * s2 - m[15] * s1) * id;
-    inv[7] = (m[8] * s5 - m[10] * s2 + m[11] * s1) * id;
-    inv[8] = (m[4] * c4 - m[5] * c2 + m[7] * c0) * id;
-    inv[9] = (-m[0] * c4 + m[1] * c2 - m[3] * c0) * id;
-    inv[10] = (m[12] * s4 - m[13] * s2 + m[15] * s0) * id;
-    inv[11] = (-m[8] * s4 + m[9] * s2 - m[11] * s0) * id;
-    inv[12] = (-m[4] * c3 + m[5] * c1 - m[6] * c0) * id;
-    inv[13] = (m[0] * c3 - m[1] * c1 + m[2] * c0) * id;
-    inv[14] = (-m[12] * s3 + m[13] * s1 - m[14] * s0) * id;
-    inv[15] = (m[8] * s3 - m[9] * s1 + m[10] * s0) * id;
+    double iC1[2] = {A1[0] * DC2[1] - A1[1] * DC2[0], A1[1] * DC1[0] - A1[0] * DC1[1]};  // A (D# C)#
+    double iC2[2] = {A2[0] * DC2[1] - A2[1] * DC2[0], A2[1] * DC1[0] - A2[0] * DC1[1]};
+    const double r = 1.0 / det;
+    for (int k = 0; k < 2; ++k) {
+        iB1[k] = C1[k] * dB - iB1[k];
+        iB2[k] = C2[k] * dB - iB2[k];
+        iC1[k] = B1[k] * dC - iC1[k];
+        iC2[k] = B2[k] * dC - iC2[k];
+    }
+    double o[16];  // the packets written times (r, -r) / (-r, r)
+    auto put = [&](int k, const double* X1, const double* X2) {
+        o[k] = X2[1] * r;
+        o[k + 1] = -(X1[1] * r);
+        o[k + 4] = -(X2[0] * r);
+        o[k + 5] = X1[0] * r;
+    };
+    put(0, iA1, iA2);
+    put(2, iB1, iB2);
+    put(8, iC1, iC2);
+    put(10, iD1, iD2);
+    for (int k = 0; k < 16; ++k) inv[4 * (k % 4) + k / 4] = o[k];
 }
 
 // loop_closure.cpp:18-40 (host logic): among keyframes[0 .. size-2] the closest (translation of

@@ -1001,9 +1001,10 @@ struct IcpParams {
     int max_iter;           // 50
     double rot_eps;         // 0 => 1 - trans_eps
     double score_threshold; // 1.5 (config.yaml:16)
-    int umeyama_float = 0;  // 0: double statistics (the GPU default); > 0: pcl::umeyama in float + Eigen
-                            //    JacobiSVD (umeyama_pcl_float), the float summation order picked by the
-                            //    code (UmeyamaOrder below) — PCL's own order depends on its Eigen build
+    int umeyama_float = 2;  // internal: 0 = double statistics (the opt-in mode); > 0 = pcl::umeyama in float +
+                            //    Eigen JacobiSVD (umeyama_pcl_float) in that summation order (UmeyamaOrder
+                            //    below; PCL's own order depends on its Eigen build).  The C entry point takes
+                            //    the GPU's values: -1 double (LIO_ICP_UMEYAMA_DOUBLE), 0 default = order 2
 };
 
 // Float summation orders of pcl::umeyama (IcpParams::umeyama_float > 0).  Eigen-plausible variants of the
@@ -2034,7 +2035,7 @@ struct orc_icp_params {
     double max_corr_dist, trans_eps, fitness_eps;
     int max_iter;
     double rot_eps, score_threshold;
-    int umeyama_float;  // 1: float pcl::umeyama + JacobiSVD restatement (fidelity study)
+    int umeyama_float;  // as lio_icp_params: -1 double statistics, 0 the default (order 2), 1..5 UmeyamaOrder
 };
 
 int orc_version(void) { return 4; }
@@ -2214,8 +2215,10 @@ int orc_ieskf_update(void* m, const float* body, int64_t n, orc_state* state, do
 int orc_icp_align(const float* src, int64_t ns, const float* dst, int64_t nd, const orc_icp_params* ipp,
                   const float* guess16, float* T16, double* out8, float* aligned, double* trace,
                   int max_trace, int threads) {
+    // the GPU's sentinels (include/lio_gpu.h): -1 = double statistics, 0 = the default float order 2
+    const int mode = ipp->umeyama_float < 0 ? 0 : (ipp->umeyama_float == 0 ? 2 : ipp->umeyama_float);
     orc::IcpParams ip{ipp->max_corr_dist, ipp->trans_eps, ipp->fitness_eps, ipp->max_iter, ipp->rot_eps,
-                      ipp->score_threshold, ipp->umeyama_float};
+                      ipp->score_threshold, mode};
     orc::IcpResult r{};
     static const float kIdentity[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
     int rc = orc::icp_align(src, ns, dst, nd, ip, guess16 ? guess16 : kIdentity, &r, aligned, trace, max_trace,

@@ -81,7 +81,7 @@ int main() {
     {
         auto src = cloud(g, 1500, 5.f), dst = src;
         for (size_t i = 0; i < dst.size(); i += 3) dst[i] += 0.2f;
-        orc_icp_params ip{52.5, 0.01, 0.01, 50, 0.0, 1.5};
+        orc_icp_params ip{52.5, 0.01, 0.01, 50, 0.0, 1.5, -1};  // the double statistics first
         float T[16];
         double out8[8], tr[20 * 64];
         std::vector<float> al(src.size());

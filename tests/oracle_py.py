@@ -37,9 +37,9 @@ class IcpParams(C.Structure):
                 ("umeyama_float", C.c_int)]
 
 
-# pcl::umeyama float summation orders (lio_oracle.cpp UmeyamaOrder); the oracle's 0 = double statistics
-# (the GPU's opt-in LIO_ICP_UMEYAMA_DOUBLE); the default is order 2, as on the GPU
-ORACLE_DOUBLE_STATS = 0
+# pcl::umeyama float summation orders (lio_oracle.cpp UmeyamaOrder); the sentinels are the GPU's
+# (include/lio_gpu.h): -1 = the opt-in double statistics (LIO_ICP_UMEYAMA_DOUBLE), 0 = the default order 2
+ORACLE_DOUBLE_STATS = -1
 DEFAULT_UMEYAMA_ORDER = 2
 UMEYAMA_ORDERS = {1: "sequential means, sequential sigma", 2: "sequential means, Eigen GEMM sigma kc(32 KiB L1)",
                   3: "sequential means, Eigen GEMM sigma kc(48 KiB L1)", 4: "packet-4 means, sequential sigma",

@@ -36,8 +36,9 @@ def test_c5_stream_driver_compiles(tmp_path):
 
 
 def test_host_glue_matches_python(tmp_path):
-    """odom_matrix (bit for bit), inverse4 (within 1e-15 of numpy's inverse) and fetch_closest_keyframe_idx
-    of the C++ header against the Python glue — host code only, no GPU."""
+    """odom_matrix (bit for bit), inverse4 (bit for bit against the Python restatement of Eigen's SSE
+    Matrix4d::inverse, and within 1e-14 of numpy's inverse) and fetch_closest_keyframe_idx of the C++ header
+    against the Python glue — host code only, no GPU."""
     import re
 
     from lio_gpu import loop_closure as LC
@@ -53,6 +54,7 @@ def test_host_glue_matches_python(tmp_path):
     Ic = np.array([float(v) for v in re.findall(r"^I \d+ (\S+)$", out, re.M)]).reshape(4, 4)
     st = dict(rot=np.array([0.9238795325112867, 0.0123, -0.0456, 0.3826834323650898]), pos=np.array([12.5, -3.25, 0.75]))
     np.testing.assert_array_equal(T, PL.odom_matrix(st))
+    np.testing.assert_array_equal(Ic, PL.eigen_inverse4(T))
     np.testing.assert_allclose(Ic, np.linalg.inv(T), rtol=0, atol=1e-14)
     np.testing.assert_allclose(Ic @ T, np.eye(4), rtol=0, atol=1e-14)
     kfs = []
@@ -118,7 +120,7 @@ def test_cpp_c5_stream_matches_oracle(oracle, tmp_path):
         np.testing.assert_array_equal(g["pose_eig"], T)
         w_g = PL.state_world(xg, o_und[:, :3])
         kh = PL.keyframe_from_odometry(xg, np.concatenate([w_g, o_und[:, 3:4]], axis=1), t, k)
-        np.testing.assert_allclose(g["pcd"], kh.pcd_, rtol=2.4e-7, atol=1e-6)  # <= 2 float ulps
+        np.testing.assert_array_equal(g["pcd"], kh.pcd_)  # the same Eigen inverse restated on both sides
         om.map_incremental(body, synth.pose24(xk), synth.pose24(xo), 0.5, 0.5)  # the oracle's own poses
         w_o = oracle.body_to_world(synth.pose24(xo), o_und[:, :3])
         kfo.append(PL.keyframe_from_odometry(xo, np.concatenate([w_o, o_und[:, 3:4]], axis=1), t, k))

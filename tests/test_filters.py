@@ -161,3 +161,19 @@ def test_pipeline_glue_world_transform_matches_restatement(oracle):
         ref = (xyz.astype(np.float64) @ synth.quat_to_mat(st["offset_R_L_I"]).T + st["offset_T_L_I"])
         np.testing.assert_allclose(back[:, :3], ref, atol=1e-4)
         np.testing.assert_array_equal(back[:, 3], xyz[:, 0])
+
+
+def test_eigen_inverse4_is_an_inverse():
+    """lio_gpu.pipeline.eigen_inverse4 (Eigen 3.3's SSE Matrix4d::inverse restated) inverts general and
+    rigid 4x4 matrices to the last bits (structure check of the restatement: a misplaced lane or sign would
+    not give an inverse)."""
+    from lio_gpu import pipeline as PL
+
+    rng = np.random.default_rng(11)
+    for _ in range(20):
+        M = rng.normal(size=(4, 4))
+        np.testing.assert_allclose(PL.eigen_inverse4(M) @ M, np.eye(4), rtol=0, atol=1e-12)
+        q = rng.normal(size=4)
+        q /= np.linalg.norm(q)
+        T = PL.odom_matrix(dict(rot=q, pos=rng.uniform(-50, 50, 3)))
+        np.testing.assert_allclose(PL.eigen_inverse4(T), np.linalg.inv(T), rtol=0, atol=1e-13)

@@ -203,11 +203,11 @@ def test_icp_float_fidelity_matches_oracle(oracle, n, disp, order):
 
 def test_icp_fidelity_recovery_paths(oracle):
     """The seqsum re-pass (a first pass that skips the grid-coarsening rule: verification fails, pass 2
-    repairs) and the serial fallback (event lists capped at 8) give the same transform bits as the normal
-    path."""
+    repairs), the serial fallback (event lists capped at 8) and a compaction look-back time-out (test hook:
+    the pass re-compacts on the serial kernels) give the same transform bits as the normal path."""
     src, dst, _ = synth.make_icp_pair(n_points=60_000, seed=12, disp=(1.0, 3.0))
     out = {}
-    for name, flags, evcap in (("normal", 0, 0), ("repass", 1, 0), ("serial", 0, 8)):
+    for name, flags, evcap in (("normal", 0, 0), ("repass", 1, 0), ("serial", 0, 8), ("timeout", 4, 0)):
         lc = LC.LoopClosure(LC.LoopClosureConfig(), umeyama_float=2)
         lc.set_fidelity_debug(flags, evcap)
         lc.setInputSource(src)
@@ -215,10 +215,29 @@ def test_icp_fidelity_recovery_paths(oracle):
         r = lc.align(keep_aligned=False)
         out[name] = (np.array(list(r.T), np.float32), r.iterations, lc.fidelity_stats())
     assert out["repass"][2]["repasses"] > 0 and out["repass"][2]["serial"] == 0
-    assert out["serial"][2]["serial"] > 0
-    for k in ("repass", "serial"):
+    assert out["serial"][2]["serial"] > 0 and out["timeout"][2]["serial"] > 0
+    for k in ("repass", "serial", "timeout"):
         np.testing.assert_array_equal(out[k][0], out["normal"][0])
         assert out[k][1] == out["normal"][1]
+
+
+def test_icp_lookback_timeout_does_not_poison_the_handle(oracle):
+    """a compaction look-back time-out on one alignment (test hook) is cleared, so the next
+    alignment on the same handle takes the parallel path again with the same transform bits."""
+    src, dst, _ = synth.make_icp_pair(n_points=30_000, seed=12, disp=(1.0, 3.0))
+    lc = LC.LoopClosure(LC.LoopClosureConfig(), umeyama_float=2)
+    lc.setInputSource(src)
+    lc.setInputTarget(dst)
+    lc.set_fidelity_debug(4, 0)
+    r0 = lc.align(keep_aligned=False)
+    s0 = lc.fidelity_stats()
+    lc.set_fidelity_debug(0, 0)
+    r1 = lc.align(keep_aligned=False)
+    s1 = lc.fidelity_stats()
+    assert s0["serial"] > 0 and s1["serial"] == s0["serial"]  # the second alignment never fell back
+    np.testing.assert_array_equal(np.array(list(r0.T), np.float32), np.array(list(r1.T), np.float32))
+    o = oracle.icp_align(src, dst, params=_float_params(oracle, 2))
+    np.testing.assert_allclose(np.array(list(r1.T), np.float32).reshape(4, 4), o["T"], atol=1e-5)
 
 
 @pytest.mark.parametrize("disp", [(0.3, 1.5), (2.5, 4.0)])

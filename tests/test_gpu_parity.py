@@ -384,31 +384,6 @@ def test_seeded_second_knn_bit_exact(oracle, c1, shift):
     _check_sums(g, o)
 
 
-def test_cell_grouped_near_pass_opt_in_bit_exact(oracle, c1, monkeypatch):
-    """The cell-grouped near pass (LIO_KNN_NEAR=cell, A/B only: DESIGN §4) gives the oracle's lists,
-    unseeded and seeded; the far pass then skips keys already in a list (DEDUP)."""
-    monkeypatch.setenv("LIO_KNN_NEAR", "cell")
-    _, m, scans = c1
-    sc = scans[0]
-    tree = F.IkdTreeGPU()
-    tree.Build(m)
-    hm = F.HShareModelGPU(tree)  # the mode is read when the context is created
-    hm.set_scan(sc.body)
-    om = oracle.OracleMap(m)
-    st = synth.initial_state(sc.pos_init, sc.rot_init)
-    for shift in (0.0, 0.3):
-        st2 = dict(st)
-        st2["pos"] = np.asarray(st["pos"]) + np.array([shift, -0.5 * shift, 0.25 * shift])
-        p24 = synth.pose24(st2)
-        hm(p24, converge=True)
-        gi, gd = hm.nearest_points()
-        oi, od = om.knn(oracle.body_to_world(p24, sc.body), 5, 5.0)
-        np.testing.assert_array_equal(gi, oi)
-        np.testing.assert_array_equal(gd, od)
-    hm.close()
-
-
-@pytest.mark.parametrize("scale", [0.05, 0.5])
 def test_seeded_guard_whole_box(oracle, scale):
     """The seeded pass's guard: a bound shrunk below the true 5th distance (lio_ctx_set_seed_scale)
     leaves lists that are not full; they are reset and the far pass searches the whole box, 3x3x3
