@@ -89,6 +89,10 @@ def parse():
                          "through Preprocess + UndistortPcl + downSizeFilterSurf -> IESKF update -> map_incremental "
                          "-> keyframe, then the loop leg (fetchClosestKeyframeIdx -> setSrcAndDstCloud -> "
                          "icpAlignment) on the newest keyframe; reported under 'pipeline' (0: skip)")
+    ap.add_argument("--loop-seq", type=int, default=12, metavar="N",
+                    help="secondary figure (rank 0): the loop leg as the node runs it — N loopTimerFunc calls "
+                         "(fast_lio_sam.cpp:682-728) from C++ on one LoopClosure handle while the keyframe database "
+                         "grows, submaps of a different size on every call; reported under 'loop_sequence' (0: skip)")
     ap.add_argument("--grow-scans", type=int, default=20,
                     help="C3/C5: scans appended through map_incremental before timing (SURVEY §8d)")
     ap.add_argument("--watchdog-s", type=float, default=240.0,
@@ -544,7 +548,7 @@ def main():
                              "note": "scan uploaded from pinned host memory by lio_scan_set inside each step "
                                      "(rank-local; PCIe included)"},
         "roofline": roofline, "cpu_baseline": None, "loop_icp": None, "multi_stream": None, "map_incremental": incr,
-        "pipeline": None,
+        "pipeline": None, "loop_sequence": None,
     }
 
     # the headline is measured; the secondary keys follow.  N > 1: a watchdog prints what rank 0 has if a
@@ -631,6 +635,42 @@ def main():
         except Exception as e:  # secondary section: report, never fail the bench line
             pipeline["cpp"] = {"error": str(e)[-300:]}
     line["pipeline"] = pipeline
+
+    # ------------------------------------------------- the loop leg as the node runs it (secondary)
+    # tests/cpp/loop_sequence.cpp: one lio_gpu::LoopClosure, keyframes_ growing by one per call, each call timed
+    # like loopTimerFunc's "loop: %.1f" (fetchClosestKeyframeIdx + performLoopClosure); the first call is the
+    # cold one (buffers sized), the rest must not allocate (lio_alloc_count)
+    loop_seq = None
+    if args.loop_seq > 0 and rank == 0:
+        try:
+            import tempfile
+
+            from lio_gpu import pipeline as PL
+
+            n_back = args.loop_seq
+            tg = time.time()
+            kfs = PL.make_loop_keyframes(n_out=n_back, n_back=n_back)
+            lgen = time.time() - tg
+            with tempfile.TemporaryDirectory() as td:
+                fin = os.path.join(td, "ls.bin")
+                PL.write_loop_sequence(fin, kfs, range(n_back, 2 * n_back))
+                lo = PL.run_loop_sequence(fin, timeout=300)
+            pc = lo.pop("per_call")
+            loop_seq = {
+                "config": f"{2 * n_back} keyframes ({n_back} out, {n_back} back 40 s later with a growing odometry "
+                          f"drift), synthetic KITTI-64 scans of {len(kfs[0].pcd_)}..{len(kfs[-1].pcd_)} points; one "
+                          f"loopTimerFunc call per return keyframe (keyframes_ = keyframes[0..k]), C++ driver, PCL "
+                          f"float order 2",
+                **{k: (round(v, 4) if isinstance(v, float) else v) for k, v in lo.items()},
+                "warm_p99_over_p50": round(lo["warm_p99_ms"] / lo["warm_p50_ms"], 3) if lo["warm_p50_ms"] > 0 else None,
+                "per_call": [{"k": c["k"], "ms": round(c["ms"], 3), "closest": c["closest"], "n_src": c["n_src"],
+                              "n_dst": c["n_dst"], "iterations": c["iterations"], "valid": c["valid"],
+                              "allocs": c["allocs"]} for c in pc],
+                "input_gen_s": round(lgen, 1),
+            }
+        except Exception as e:  # secondary section: report, never fail the bench line
+            loop_seq = {"error": str(e)[-300:]}
+    line["loop_sequence"] = loop_seq
 
     # ------------------------------------------------- several scan streams on one GPU (secondary)
     # One stream is latency-bound (host round trip per h-evaluation); independent sensors / robots
@@ -770,7 +810,8 @@ def main():
     if watchdog is not None:
         watchdog.cancel()
     if rank == 0:
-        line.update({"cpu_baseline": cpu, "loop_icp": loop_icp, "multi_stream": multi, "pipeline": pipeline})
+        line.update({"cpu_baseline": cpu, "loop_icp": loop_icp, "multi_stream": multi, "pipeline": pipeline,
+                     "loop_sequence": loop_seq})
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()

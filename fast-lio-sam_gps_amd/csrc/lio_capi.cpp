@@ -55,6 +55,7 @@ int grow(T** p, int64_t& cap, int64_t need, size_t elems_per = 1) {
     if (*p) (void)hipFree(*p);
     *p = nullptr;
     int64_t c = std::max<int64_t>(need, cap + cap / 2);
+    lio::count_alloc();
     if (hipMalloc(p, (size_t)c * elems_per * sizeof(T)) != hipSuccess) {
         cap = 0;
         return fail(LIO_ERR_NOMEM, "hipMalloc failed");
@@ -600,6 +601,7 @@ static int ctx_reserve(lio_ctx* c, int64_t n) {
         c->d_far_d = nullptr;
         c->d_far_id = nullptr;
         c->d_d5 = nullptr;
+        lio::count_alloc(8);
         if (hipMalloc(&c->d_body, cap * 3 * sizeof(float)) != hipSuccess ||
             hipMalloc(&c->d_nn, cap * 5 * sizeof(int32_t)) != hipSuccess ||
             hipMalloc(&c->d_planes, cap * sizeof(float4)) != hipSuccess ||
@@ -1111,6 +1113,7 @@ static int stage_sweep(lio::FilterBuf& b, const void* rows, int64_t n, size_t ro
         if (b.h_stage) (void)hipHostFree(b.h_stage);
         b.h_stage = nullptr;
         const size_t c = std::max(need, b.stage_bytes + b.stage_bytes / 2);
+        lio::count_alloc();
         if (hipHostMalloc(&b.h_stage, c) != hipSuccess) {
             b.stage_bytes = 0;
             return fail(LIO_ERR_NOMEM, "sweep staging: hipHostMalloc failed");
@@ -1189,6 +1192,7 @@ static int stage_sweep_select(lio::FilterBuf& b, const float* raw, int64_t n, in
         if (b.h_stage) (void)hipHostFree(b.h_stage);
         b.h_stage = nullptr;
         const size_t c = std::max(need, b.stage_bytes + b.stage_bytes / 2);
+        lio::count_alloc();
         if (hipHostMalloc(&b.h_stage, c) != hipSuccess) {
             b.stage_bytes = 0;
             return fail(LIO_ERR_NOMEM, "sweep staging: hipHostMalloc failed");

@@ -23,6 +23,7 @@
 #include <cstring>
 
 #include "lio_dev.hpp"
+#include "lio_error.hpp"
 #include "lio_filter.hpp"
 
 namespace lio {
@@ -602,6 +603,7 @@ int fgrow(T** p, int64_t& cap, int64_t need) {
     if (*p) (void)hipFree(*p);
     *p = nullptr;
     const int64_t c = std::max<int64_t>(need, cap + cap / 2);
+    count_alloc();
     if (hipMalloc(p, (size_t)c * sizeof(T)) != hipSuccess) {
         cap = 0;
         return -5;
@@ -615,6 +617,7 @@ int ftmp(FilterBuf& b, size_t need) {  // grown geometrically (1 MiB floor): no 
     if (b.tmp) (void)hipFree(b.tmp);
     b.tmp = nullptr;
     const size_t c = std::max(std::max(need, b.tmp_bytes + b.tmp_bytes / 2), (size_t)1 << 20);
+    count_alloc();
     if (hipMalloc(&b.tmp, c) != hipSuccess) {
         b.tmp_bytes = 0;
         return -5;
@@ -629,6 +632,7 @@ int reserve(FilterBuf& b, int64_t n) {
     void* bufs[] = {b.keys, b.keys_alt, b.vals, b.vals_alt, b.head, b.vid};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
+    count_alloc(6);
     FCHK(hipMalloc(&b.keys, c * sizeof(uint32_t)));
     FCHK(hipMalloc(&b.keys_alt, c * sizeof(uint32_t)));
     FCHK(hipMalloc(&b.vals, c * sizeof(uint32_t)));

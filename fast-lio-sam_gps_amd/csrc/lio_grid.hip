@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstring>
 
+#include "lio_error.hpp"
 #include "lio_grid_dev.hpp"
 #include "lio_kernels.hpp"
 
@@ -268,6 +269,7 @@ static int ensure(void** p, size_t& cap_bytes, size_t need) {
     if (*p) (void)hipFree(*p);
     *p = nullptr;
     const size_t c = std::max(std::max(need, cap_bytes + cap_bytes / 2), (size_t)1 << 20);
+    count_alloc();
     if (hipMalloc(p, c) != hipSuccess) {
         cap_bytes = 0;
         return -5;
@@ -307,8 +309,9 @@ GridDev grid_view(const GridBuf& g) {
 
 int grid_reserve_ids(GridBuf& g, int64_t n_ids, hipStream_t st) {
     if (n_ids <= g.id_cap && g.by_id) return 0;
-    const int64_t cap = std::max<int64_t>(n_ids, g.id_cap + g.id_cap / 2);
+    const int64_t cap = std::max<int64_t>(std::max<int64_t>(n_ids, g.id_cap + g.id_cap / 2), g.min_entries);
     float4* nb = nullptr;
+    count_alloc();
     HIPCHK(hipMalloc(&nb, cap * sizeof(float4)));
     if (g.by_id) {
         if (g.n_ids) HIPCHK(hipMemcpyAsync(nb, g.by_id, g.n_ids * sizeof(float4), hipMemcpyDeviceToDevice, st));
@@ -324,7 +327,8 @@ int grid_reserve_ids(GridBuf& g, int64_t n_ids, hipStream_t st) {
 // arrays (gapped grids keep their points in the slot pool, reserve_slots)
 static int reserve_entries(GridBuf& g, int64_t n) {
     if (n <= g.cap && g.keys) return 0;
-    const int64_t cap = std::max<int64_t>(n, g.cap + g.cap / 2);
+    const int64_t cap = std::max<int64_t>(std::max<int64_t>(n, g.cap + g.cap / 2), g.min_entries);
+    count_alloc(g.gapped ? 4 : 6);
     void* bufs[] = {g.keys, g.keys_alt, g.vals, g.vals_alt};
     for (void* p : bufs)
         if (p) HIPCHK(hipFree(p));
@@ -351,6 +355,7 @@ static int reserve_slots(GridBuf& g, int64_t slots) {
     if (g.pts) HIPCHK(hipFree(g.pts));
     g.pts = nullptr;
     g.slots_cap = 0;
+    count_alloc();
     HIPCHK(hipMalloc(&g.pts, (size_t)slots * sizeof(float4)));
     g.slots_cap = slots;
     return 0;
@@ -366,7 +371,8 @@ static int reserve_cells(GridBuf& g, uint32_t nc1) {
     g.lim = nullptr;
     g.addc = nullptr;
     g.dirty = nullptr;
-    const uint32_t cap = std::max<uint32_t>(nc1, g.cells_cap + g.cells_cap / 2);
+    const uint32_t cap = std::max<uint32_t>(std::max<uint32_t>(nc1, g.cells_cap + g.cells_cap / 2), g.min_cells);
+    count_alloc(g.gapped ? 5 : 1);
     HIPCHK(hipMalloc(&g.start, 2 * (size_t)cap * sizeof(uint32_t)));  // + histogram scratch
     if (g.gapped) {
         HIPCHK(hipMalloc(&g.rng, (size_t)cap * sizeof(uint2)));

@@ -19,6 +19,7 @@
 #include <hipcub/hipcub.hpp>
 
 #include "lio_dev.hpp"
+#include "lio_error.hpp"
 #include "lio_kernels.hpp"
 
 namespace lio {
@@ -712,8 +713,10 @@ int icp_build_tiles(const GridBuf& q, uint2* tiles, uint32_t* scratch, void*& tm
         if (tmp) (void)hipFree(tmp);
         tmp = nullptr;
         tmp_bytes = 0;
-        if (hipMalloc(&tmp, need) != hipSuccess) return -5;
-        tmp_bytes = need;
+        const size_t c = std::max(need + need / 2, 2 * tmp_bytes);  // geometric: the next source rarely needs more
+        count_alloc();
+        if (hipMalloc(&tmp, c) != hipSuccess) return -5;
+        tmp_bytes = c;
     }
     size_t tb = tmp_bytes;
     if (hipcub::DeviceRadixSort::SortPairs(tmp, tb, key, key2, cell, cell2, (int)nc, 0, 32, st) != hipSuccess) return -1;

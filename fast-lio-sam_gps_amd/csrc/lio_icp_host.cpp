@@ -373,6 +373,13 @@ static bool fid_sharded(const lio_icp* h) { return h->p.umeyama_float > 0 && h->
 // the incrementally transformed cloud of this rank's shard
 static float* shard_cur(const lio_icp* h) { return fid_sharded(h) ? h->d_curf + 3 * h->sh_begin : h->d_cur; }
 
+// Capacities grow geometrically from a floor sized for the reference's largest submaps (C4: 500 k points): a
+// loop-closure node whose submaps change size on every 2 Hz loopTimerFunc call (fast_lio_sam.cpp:682-730) then
+// allocates on its first call and (almost) never again — a hipFree synchronises the device, and a re-allocation
+// per call showed up as a 9 ms cold loop leg against 1.1 ms warm.
+constexpr int64_t kIcpCapFloor = (int64_t)1 << 19;
+static int64_t icp_cap(int64_t need, int64_t cap) { return std::max(std::max(need + need / 2, 2 * cap), kIcpCapFloor); }
+
 static int icp_check_dev(int dev) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return ifail(LIO_ERR_NODEV, "no HIP device (no CPU path)");
@@ -408,6 +415,10 @@ int lio_icp_create(const lio_icp_params* p, lio_icp** out) {
     if (h->p.umeyama_float == LIO_ICP_UMEYAMA_DEFAULT) h->p.umeyama_float = LIO_ICP_UMEYAMA_PCL_GEMM32;
     else if (h->p.umeyama_float == LIO_ICP_UMEYAMA_DOUBLE) h->p.umeyama_float = 0;
     if (!(h->p.cell_size > 0.f)) h->p.cell_size = 1.0f;  // 0.3 m voxelised submaps: 1 m target cells (scripts/icp_cells.py)
+    // the grids' capacity floors: a C4-sized submap (500 k points, ~1 M target cells at 1 m) fits from the start
+    h->tgt.min_entries = h->qgrid.min_entries = kIcpCapFloor;
+    h->tgt.min_cells = 1u << 20;
+    h->qgrid.min_cells = 1u << 17;
     if (hipStreamCreateWithFlags(&h->st, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&h->st2, hipStreamNonBlocking) != hipSuccess) {
         if (h->st) (void)hipStreamDestroy(h->st);
@@ -480,7 +491,8 @@ static int stage_pinned(float*& buf, int64_t& cap, const float* xyz, int64_t n) 
         if (buf) (void)hipHostFree(buf);
         buf = nullptr;
         cap = 0;
-        const int64_t c = std::max<int64_t>(n, 1) + std::max<int64_t>(n, 1) / 4;
+        const int64_t c = icp_cap(n, cap);
+        lio::count_alloc();
         if (hipHostMalloc(reinterpret_cast<void**>(&buf), (size_t)c * 3 * sizeof(float), hipHostMallocDefault) != hipSuccess)
             return ifail(LIO_ERR_NOMEM, "ICP staging: hipHostMalloc failed");
         cap = c;
@@ -532,9 +544,11 @@ static int target_build(lio_icp* h) {
     if (n > h->tgt_cap || !h->d_tgt) {
         if (h->d_tgt) IHIP(hipFree(h->d_tgt));
         h->d_tgt = nullptr;
+        const int64_t c = icp_cap(n, h->tgt_cap);
         h->tgt_cap = 0;
-        IHIP(hipMalloc(&h->d_tgt, (size_t)n * 3 * sizeof(float)));
-        h->tgt_cap = n;
+        lio::count_alloc();
+        IHIP(hipMalloc(&h->d_tgt, (size_t)c * 3 * sizeof(float)));
+        h->tgt_cap = c;
     }
     IHIP(hipMemcpyAsync(h->d_tgt, h->h_tgt, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice, h->st2));
     int rc = lio::grid_build(h->tgt, h->d_tgt, n, h->p.cell_size, h->st2);
@@ -667,10 +681,12 @@ static int exchange_reserve(lio_icp* h) {
         if (h->d_xsend) IHIP(hipFree(h->d_xsend));
         if (h->d_xrecv) IHIP(hipFree(h->d_xrecv));
         h->d_xsend = h->d_xrecv = nullptr;
+        const int64_t c = std::max(need + need / 2, 2 * h->x_len);
         h->x_len = 0;
-        IHIP(hipMalloc(&h->d_xsend, (size_t)need * sizeof(double)));
-        IHIP(hipMalloc(&h->d_xrecv, (size_t)need * h->world * sizeof(double)));
-        h->x_len = need;
+        lio::count_alloc(2);
+        IHIP(hipMalloc(&h->d_xsend, (size_t)c * sizeof(double)));
+        IHIP(hipMalloc(&h->d_xrecv, (size_t)c * h->world * sizeof(double)));
+        h->x_len = c;
     }
     return LIO_OK;
 }
@@ -678,15 +694,16 @@ static int exchange_reserve(lio_icp* h) {
 static int icp_prepare(lio_icp* h) {
     if (!h->src_dirty) return LIO_OK;
     shard_range(h->ns, h->rank, h->world, h->sh_begin, h->sh_n);
-    const int64_t n = std::max<int64_t>(h->sh_n, 1);
-    if (n > h->cap) {
+    if (h->sh_n > h->cap || !h->d_src) {
         void** ptrs[] = {(void**)&h->d_src,   (void**)&h->d_cur,   (void**)&h->d_fd2,  (void**)&h->d_fid,
                          (void**)&h->d_tiles, (void**)&h->d_tcost, (void**)&h->d_order};
+        const int64_t n = icp_cap(h->sh_n, h->cap);
         h->cap = 0;  // a failed allocation below leaves no buffer that looks usable (and nothing freed twice)
         for (void** q : ptrs) {
             if (*q) (void)hipFree(*q);
             *q = nullptr;
         }
+        lio::count_alloc(7);
         IHIP(hipMalloc(&h->d_src, n * 3 * sizeof(float)));
         IHIP(hipMalloc(&h->d_cur, n * 3 * sizeof(float)));
         IHIP(hipMalloc(&h->d_fd2, n * sizeof(float)));
@@ -701,10 +718,12 @@ static int icp_prepare(lio_icp* h) {
         if (h->h_super) (void)hipHostFree(h->h_super);
         h->h_super = nullptr;
         h->h_super_dev = nullptr;
+        const int64_t c = icp_cap(nsup_all, h->super_cap * lio::kIcpSuper) / lio::kIcpSuper + 1;
         h->super_cap = 0;
-        IHIP(hipHostMalloc(&h->h_super, nsup_all * lio::kIcpStride * sizeof(double), hipHostMallocMapped));
+        lio::count_alloc();
+        IHIP(hipHostMalloc(&h->h_super, c * lio::kIcpStride * sizeof(double), hipHostMallocMapped));
         IHIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->h_super_dev), h->h_super, 0));
-        h->super_cap = nsup_all;
+        h->super_cap = c;
     }
     h->ntiles = 0;
     h->have_order = false;  // new tiles: cell order until a pass has measured them
@@ -735,8 +754,11 @@ static int icp_prepare(lio_icp* h) {
         if (need > h->tscratch_cap) {
             if (h->d_tscratch) IHIP(hipFree(h->d_tscratch));
             h->d_tscratch = nullptr;
-            IHIP(hipMalloc(&h->d_tscratch, need * sizeof(uint32_t)));
-            h->tscratch_cap = need;
+            const int64_t c = std::max(need + need / 2, 2 * h->tscratch_cap);
+            h->tscratch_cap = 0;
+            lio::count_alloc();
+            IHIP(hipMalloc(&h->d_tscratch, c * sizeof(uint32_t)));
+            h->tscratch_cap = c;
         }
         const int nt = lio::icp_build_tiles(h->qgrid, h->d_tiles, h->d_tscratch, h->d_ttmp, h->ttmp_bytes, h->st);
         if (nt < 0) return ifail(nt == -5 ? LIO_ERR_NOMEM : LIO_ERR_HIP, "tile list failed");
@@ -1010,6 +1032,8 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     return LIO_OK;
 }
 
+extern "C" int64_t lio_alloc_count(void) { return lio::alloc_counter().load(std::memory_order_relaxed); }
+
 extern "C" int lio_icp_shard_range(int64_t ns, int rank, int world, int64_t* begin, int64_t* count) {
     if (ns < 0 || world < 1 || rank < 0 || rank >= world || !begin || !count)
         return ifail(LIO_ERR_ARG, "lio_icp_shard_range: bad arguments");
@@ -1142,7 +1166,7 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
     h->bg_tgt_err.clear();
     h->bg_src_err.clear();
     if (pcl_float) {
-        if (lio::pcl_reserve(h->pcl, std::max<int64_t>(fid_sharded(h) ? h->ns : h->sh_n, 1), h->p.umeyama_float, h->st))
+        if (lio::pcl_reserve(h->pcl, std::max<int64_t>(fid_sharded(h) ? h->ns : h->sh_n, kIcpCapFloor), h->p.umeyama_float, h->st))
             return ifail(LIO_ERR_NOMEM, "lio_icp_align: fidelity buffers");
         h->pcl.means.dbg_noinc = h->pcl.sig.dbg_noinc = h->fid_flags & 1;
         for (lio::SeqSumBuf* b : {&h->pcl.means, &h->pcl.sig})

@@ -87,6 +87,8 @@ struct GridBuf {
     int64_t slots_used = 0;      // bump value after the last rebuild (host view; the pool's live share)
     int64_t rebuilds = 0;        // full rebuilds so far (diagnostics: lio_map_get_stats)
     int64_t slots_extra = 0;     // test hook (lio_map_set_test_limits): usable pool = slots_used + this (0: all)
+    int64_t min_entries = 0;     // capacity floors (the loop ICP's grids: sized once for its largest submaps)
+    uint32_t min_cells = 0;
     // temporaries
     uint32_t* keys = nullptr;
     uint32_t* keys_alt = nullptr;

@@ -16,6 +16,7 @@
 //   pcl_pack                             res += alpha * C_b in block order; sums, count, sigma, status
 // Sharded (lio_icp_host.cpp fid_sharded): the correspondence order is global, so every rank runs these over
 // the whole source with the all-gathered accepted ids (IcpArgs::nn_d2 == nullptr: gated already).
+#include "lio_error.hpp"
 #include "lio_kernels.hpp"
 #include "lio_pcl.hpp"
 
@@ -262,6 +263,8 @@ __global__ void __launch_bounds__(kPackThreads) pcl_pack_kernel(const float* __r
 int pcl_reserve(PclBuf& p, int64_t n, int order, hipStream_t st) {
     n = n < 1 ? 1 : n;
     if (n > p.cap) {
+        n = std::max<int64_t>(n + n / 2, 2 * p.cap);  // geometric: a growing submap sequence re-allocates rarely
+        count_alloc(3);
         void* ptrs[] = {p.pairs, p.bst, p.Cb};
         for (void* q : ptrs)
             if (q) (void)hipFree(q);
@@ -282,8 +285,8 @@ int pcl_reserve(PclBuf& p, int64_t n, int order, hipStream_t st) {
         if (hipMalloc(&p.small, 64 * sizeof(float)) != hipSuccess) return -5;
         (void)hipMemsetAsync(p.small, 0, 64 * sizeof(float), st);
     }
-    if (seqsum_reserve(p.means, 6, n, st)) return -5;
-    if (order == 1 && seqsum_reserve(p.sig, 9, n, st)) return -5;
+    if (seqsum_reserve(p.means, 6, p.cap, st)) return -5;
+    if (order == 1 && seqsum_reserve(p.sig, 9, p.cap, st)) return -5;
     return 0;
 }
 

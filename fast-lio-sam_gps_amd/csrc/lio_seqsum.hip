@@ -12,6 +12,8 @@
 
 #include <cmath>
 
+#include "lio_error.hpp"
+
 namespace lio {
 
 namespace {
@@ -699,6 +701,7 @@ int seqsum_reserve(SeqSumBuf& b, int nch, int64_t nmax, hipStream_t st) {
     b.nch = nch;
     b.nmax = nmax;
     b.nblk = (int)((nmax + kSeqBlock - 1) / kSeqBlock);
+    count_alloc(18);
     b.evcap = b.evcap_alloc = nmax / 4 + 1024;  // events are ~0.3 % of a C4 chain; past a quarter the serial kernel is as fast
     const size_t nb = (size_t)nch * b.nblk;
     bool ok = hipMalloc(&b.bsum, nb * sizeof(double)) == hipSuccess && hipMalloc(&b.babs, nb * sizeof(double)) == hipSuccess &&

@@ -25,7 +25,7 @@ SUMS_HTH, SUMS_HTh, SUMS_NEFF, SUMS_RES, SUMS_HH = 0, 21, 27, 28, 29
 
 # Every symbol include/lio_gpu.h declares (checked by tests/test_capi_symbols.py).
 EXPORTS = [
-    "lio_device_count", "lio_last_error", "lio_build_info", "lio_abi_struct_sizes",
+    "lio_device_count", "lio_last_error", "lio_build_info", "lio_abi_struct_sizes", "lio_alloc_count",
     "lio_map_create", "lio_map_destroy", "lio_map_set_params", "lio_map_build", "lio_map_build_device", "lio_map_size",
     "lio_map_get_points", "lio_map_get_grid", "lio_map_get_stats", "lio_map_num_ids", "lio_map_get_by_id", "lio_map_nearest_search", "lio_map_gather", "lio_map_add",
     "lio_map_add_device", "lio_map_delete_boxes", "lio_localmap_update", "lio_map_incremental",
@@ -142,6 +142,7 @@ vp = C.c_void_p
 def _declare(L):
     sig = {
         "lio_device_count": (C.c_int, []),
+        "lio_alloc_count": (C.c_int64, []),
         "lio_last_error": (C.c_char_p, []),
         "lio_build_info": (C.c_char_p, []),
         "lio_abi_struct_sizes": (C.c_int, [C.POINTER(C.c_int64), C.c_int]),

@@ -55,6 +55,10 @@ extern "C" {
 int lio_device_count(void);
 const char* lio_last_error(void);
 const char* lio_build_info(void);
+/* Diagnostics (no device needed): device / pinned allocations the library's growth paths (loop ICP, grids,
+ * filters, scan buffers) have made in this process.  A warm loop-closure sequence adds none (bench.py
+ * loop_sequence).                                                                                  */
+int64_t lio_alloc_count(void);
 /* ABI guard (no device needed): sizeof of the public structs, in the order map_params, match_params, pose,
  * state, ieskf_params, ieskf_stats, icp_params, icp_result, localmap, incremental_stats, imu_pose,
  * scan_prep_params, cloud_field, kernel_timing — the first min(n, count) into out; returns the count.

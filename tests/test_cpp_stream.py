@@ -154,3 +154,48 @@ def test_cpp_c5_stream_matches_oracle(oracle, tmp_path):
     np.testing.assert_allclose(lp["T"], oc["T"], atol=1e-5)
     # the C++ preprocess stage (<= 0.15 ms per sweep) is reported, not asserted here
     assert summary["sweeps"] == len(stream) and summary["stage_ms_median"]["preprocess"] > 0
+
+
+def test_loop_sequence_driver_compiles(tmp_path):
+    """tests/cpp/loop_sequence.cpp (the loop leg as the node runs it) builds against the C++ mirror with -Werror."""
+    assert os.path.exists(os.path.join(LIBDIR, "liblio_gpu.so")), "build the library first (make -C fast-lio-sam_gps_amd)"
+    cmd = ["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-Wall", "-Wextra", "-Werror",
+           "-I", os.path.join(ROOT, "include"), os.path.join(ROOT, "tests", "cpp", "loop_sequence.cpp"),
+           "-o", str(tmp_path / "loop_sequence"), "-L", LIBDIR, "-llio_gpu", "-Wl,-rpath," + LIBDIR,
+           "-Wl,-rpath-link,/opt/rocm/lib"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(900)
+def test_cpp_loop_sequence_matches_python_and_oracle(oracle, tmp_path):
+    """The loop leg as fast_lio_sam's loopTimerFunc runs it (fast_lio_sam.cpp:682-728), from C++: one
+    LoopClosure handle, the keyframe database growing by one keyframe per call, a drifted return leg.  Every
+    call's closest keyframe, submap sizes, iterations and transform equal the Python LoopClosure's on the same
+    keyframes bit for bit; two calls' ICP is within 1e-5 of the oracle (PCL float order 2) on the C++ submaps
+    recomputed by the Python glue; after the first call the handle allocates nothing (lio_alloc_count)."""
+    from lio_gpu import loop_closure as LC
+
+    kfs = PL.make_loop_keyframes(n_out=8, n_back=8, n0=12_000, dn=600)
+    calls = list(range(8, 16))
+    fin = str(tmp_path / "ls.bin")
+    PL.write_loop_sequence(fin, kfs, calls)
+    out = PL.run_loop_sequence(fin, timeout=600)
+    print({k: v for k, v in out.items() if k != "per_call"})
+    assert out["calls"] == len(calls) and out["warm_allocs"] == 0
+    lc = LC.LoopClosure(LC.LoopClosureConfig())
+    for c, k in zip(out["per_call"], calls):
+        keyframes = kfs[:k + 1]
+        closest = lc.fetchClosestKeyframeIdx(keyframes[-1], keyframes)
+        assert c["k"] == k and c["closest"] == closest >= 0
+        reg = lc.performLoopClosure(keyframes[-1], keyframes, closest)
+        assert (c["n_src"], c["n_dst"]) == (len(lc.src_cloud_), len(lc.dst_cloud_))
+        assert c["iterations"] == lc.last_result.iterations >= 1 and c["valid"] == reg.is_valid_
+        np.testing.assert_array_equal(c["T"], np.array(list(lc.last_result.T), np.float32).reshape(4, 4))
+        if k in (calls[0], calls[-1]):
+            o = oracle.icp_align(np.ascontiguousarray(lc.src_cloud_[:, :3]), np.ascontiguousarray(lc.dst_cloud_[:, :3]),
+                                 params=oracle.default_icp_params())
+            assert o["iterations"] == c["iterations"]
+            np.testing.assert_allclose(c["T"], o["T"], atol=1e-5)
+    lc.close()
