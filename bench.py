@@ -665,6 +665,7 @@ def main():
                 "warm_p99_over_p50": round(lo["warm_p99_ms"] / lo["warm_p50_ms"], 3) if lo["warm_p50_ms"] > 0 else None,
                 "per_call": [{"k": c["k"], "ms": round(c["ms"], 3), "closest": c["closest"], "n_src": c["n_src"],
                               "n_dst": c["n_dst"], "iterations": c["iterations"], "valid": c["valid"],
+                              "submaps_ms": round(c["submaps_ms"], 3), "icp_ms": round(c["icp_ms"], 3),
                               "allocs": c["allocs"]} for c in pc],
                 "input_gen_s": round(lgen, 1),
             }

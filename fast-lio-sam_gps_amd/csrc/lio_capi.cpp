@@ -1322,10 +1322,15 @@ int lio_submap_voxelize(lio_filter* f, const float* pts, const int64_t* seg_off,
     if (n == 0) return LIO_OK;
     if (!pts || !out) return fail(LIO_ERR_ARG, "lio_submap_voxelize: bad arguments");
     HIP_TRY(hipSetDevice(f->dev));
-    int rc = grow(&f->d_in, f->in_cap, n * stride);
-    if (!rc) rc = grow(&f->d_out, f->out_cap, 2 * n * stride);
-    if (!rc) rc = grow(&f->d_seg, f->seg_cap, nk + 1);
-    if (!rc) rc = grow(&f->d_T, f->T_cap, 16 * (int64_t)nk);
+    // the loop leg's submaps change size on every loop timer call: the buffers are sized once for a C4-sized
+    // submap (2 x 11 keyframes) and grow geometrically past it
+    constexpr int64_t kSubmapFloor = (int64_t)1 << 19;
+    f->b.min_cap = kSubmapFloor;
+    const int64_t nf = std::max(n, kSubmapFloor);
+    int rc = grow(&f->d_in, f->in_cap, nf * stride);
+    if (!rc) rc = grow(&f->d_out, f->out_cap, 2 * nf * stride);
+    if (!rc) rc = grow(&f->d_seg, f->seg_cap, std::max<int64_t>(nk + 1, 64));
+    if (!rc) rc = grow(&f->d_T, f->T_cap, 16 * std::max<int64_t>(nk, 64));
     if (rc) return rc;
     HIP_TRY(hipMemcpyAsync(f->d_in, pts, (size_t)n * stride * sizeof(float), hipMemcpyHostToDevice, f->st));
     HIP_TRY(hipMemcpyAsync(f->d_seg, seg_off, (size_t)(nk + 1) * sizeof(int64_t), hipMemcpyHostToDevice, f->st));

@@ -628,7 +628,7 @@ int ftmp(FilterBuf& b, size_t need) {  // grown geometrically (1 MiB floor): no 
 
 int reserve(FilterBuf& b, int64_t n) {
     if (n <= b.cap && b.keys) return 0;
-    const int64_t c = std::max<int64_t>(n, b.cap + b.cap / 2);
+    const int64_t c = std::max<int64_t>(std::max<int64_t>(n, b.cap + b.cap / 2), b.min_cap);
     void* bufs[] = {b.keys, b.keys_alt, b.vals, b.vals_alt, b.head, b.vid};
     for (void* p : bufs)
         if (p) (void)hipFree(p);
@@ -650,7 +650,11 @@ int reserve(FilterBuf& b, int64_t n) {
         FCHK(hipMalloc(&b.cnt, 64));
         FCHK(hipMemset(b.cnt, 0, 64));
     }
-    return 0;
+    // the sort / scan scratch for the whole capacity now, so a call up to it never re-allocates the scratch
+    size_t sb = 0, xb = 0;
+    FCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, sb, b.keys, b.keys_alt, b.vals, b.vals_alt, (int)c, 0, 32));
+    FCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, xb, b.head, b.vid, (int)(c + 1)));
+    return ftmp(b, std::max(sb, xb));
 }
 
 int exscan(FilterBuf& b, const uint32_t* in, uint32_t* out, int64_t n1, hipStream_t st) {

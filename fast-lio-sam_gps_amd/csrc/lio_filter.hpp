@@ -56,6 +56,7 @@ struct FilterBuf {
     uint32_t *keys = nullptr, *keys_alt = nullptr, *vals = nullptr, *vals_alt = nullptr;
     uint32_t *head = nullptr, *vid = nullptr;
     int64_t cap = 0;
+    int64_t min_cap = 0;     // capacity floor (the loop leg's submaps: sized once, lio_submap_voxelize)
     float* part = nullptr;
     VoxelGeom* geom = nullptr;
     void* tmp = nullptr;

@@ -295,7 +295,7 @@ def make_loop_keyframes(scene: synth.Scene | None = None, n_out: int = 12, n_bac
     KITTI-64 scan of n0 + dn * k points in its LiDAR frame with its pose (the world <- LiDAR transform) as
     pose_corrected_eig_, so later keyframes are denser and the submaps of a call sequence grow (the 2 Hz loop
     timer then sees a different submap size on every call).  The return leg's poses carry an odometry drift
-    growing along it (up to ~0.6 m / 1.4 deg), which is what the loop closure's ICP then corrects."""
+    growing along it (0.17 m / 0.23 deg per keyframe), which is what the loop closure's ICP then corrects."""
     if scene is None:
         scene = synth.make_scene()
     x0 = -0.15 * scene.length + 0.9
@@ -311,7 +311,7 @@ def make_loop_keyframes(scene: synth.Scene | None = None, n_out: int = 12, n_bac
         T[:3, 3] = Rg @ synth.T_LI + sc.pos_gt
         if k >= n_out:  # the believed pose of a return keyframe: drifted
             j = k - n_out + 1
-            T = np.block([[synth.rotz(0.002 * j), np.array([[0.05 * j], [-0.03 * j], [0.01 * j]])],
+            T = np.block([[synth.rotz(0.004 * j), np.array([[0.15 * j], [-0.08 * j], [0.02 * j]])],
                           [np.zeros((1, 3)), np.ones((1, 1))]]) @ T
         rng = np.random.default_rng(seed + 1000 + k)
         pcd = np.concatenate([sc.body, rng.uniform(0, 100, (len(sc.body), 1)).astype(np.float32)], axis=1)
@@ -355,7 +355,8 @@ def run_loop_sequence(in_path: str, timeout: float = 600.0, exe: str = CPP_LOOP_
         v = ln.split()
         calls.append(dict(k=int(v[1]), ms=float(v[2]), closest=int(v[3]), n_src=int(v[4]), n_dst=int(v[5]),
                           iterations=int(v[6]), valid=bool(int(v[7])), score=float(v[8]),
-                          T=np.array([float(x) for x in v[9:25]], np.float32).reshape(4, 4), allocs=int(v[25])))
+                          T=np.array([float(x) for x in v[9:25]], np.float32).reshape(4, 4), allocs=int(v[25]),
+                          submaps_ms=float(v[26]), icp_ms=float(v[27])))
     out = json.loads(lines[-1])
     out["per_call"] = calls
     return out

@@ -39,7 +39,18 @@ for s in $STEPS; do
     icpx)  runs pytest_icpx 600 python -u -m pytest tests/test_gpu_icp.py -k "exchange or group" -x -v -s -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     spawn2) LIO_BENCH_REHEARSE=1 run spawn2 500 python bench.py --gpus 2 --steps 50 --warmup 5 --pipeline 0 --no-cpu --streams '' --icp-reps 2 ;;
     map)   runs pytest_map 900 python -u -m pytest tests/test_gpu_map.py tests/test_gpu_fullsize.py -x -v -p no:cacheprovider --timeout 600 --timeout-method thread ;;
+    lseqt) runs pytest_lseq 600 python -u -m pytest tests/test_cpp_stream.py tests/test_gpu_parity.py -k "loop_sequence or guard" -x -v -s -p no:cacheprovider --timeout 500 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    loopseqprof) run loopseqprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/loopseqprof" -o run --output-format csv -- fast-lio-sam_gps_amd/lio_gpu/_lib/loop_sequence /tmp/ls.bin &&
+                 run loopseqapi 300 rocprofv3 --hip-runtime-trace --stats -d "$OUT/loopseqapi" -o run --output-format csv -- fast-lio-sam_gps_amd/lio_gpu/_lib/loop_sequence /tmp/ls.bin ;;
+    loopseq) run loopseq 300 python -c "
+import sys, json, tempfile, os; sys.path.insert(0, 'fast-lio-sam_gps_amd')
+from lio_gpu import pipeline as PL
+kfs = PL.make_loop_keyframes(n_out=12, n_back=12)
+f = '/tmp/ls.bin'; PL.write_loop_sequence(f, kfs, range(12, 24))
+o = PL.run_loop_sequence(f); pc = o.pop('per_call'); print(json.dumps(o))
+for c in pc: print(c['k'], round(c['ms'], 3), round(c['submaps_ms'], 3), round(c['icp_ms'], 3), c['closest'], c['n_src'], c['n_dst'], c['iterations'], c['valid'], c['allocs'])
+" ;;
     bench) run bench 600 python bench.py --steps 200 --warmup 20 ;;
     knn)   run knn_timing 300 python scripts/knn_timing.py C2 &&
            run knn_prof 300 rocprofv3 --kernel-trace --stats -d "$OUT/knnprof" -o run --output-format csv -- python scripts/knn_timing.py C2 ;;

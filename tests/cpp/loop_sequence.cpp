@@ -84,21 +84,33 @@ int main(int argc, char** argv) {
             const std::vector<lio_gpu::PosePcd> keyframes(all.begin(), all.begin() + k + 1);
             const auto& latest = keyframes.back();
             const int64_t a0 = lio_alloc_count();
+            // loopTimerFunc's timed region; performLoopClosure's body (loop_closure.cpp:95-126) spelled out so
+            // its two stages are timed too: setSrcAndDstCloud (GPU submaps) and icpAlignment
             const auto t1 = clk::now();
             const int closest = lc.fetchClosestKeyframeIdx(latest, keyframes);
             lio_gpu::RegistrationOutput reg;
-            if (closest >= 0) reg = lc.performLoopClosure(latest, keyframes, closest);
+            size_t ns = 0, nd = 0;
+            auto ta = t1, tb = t1;
+            if (closest >= 0) {
+                ta = clk::now();
+                const auto sd = lc.setSrcAndDstCloud(keyframes, latest.idx_, closest, lc.config().num_submap_keyframes_,
+                                                     lc.config().voxel_res_);
+                tb = clk::now();
+                reg = lc.icpAlignment(sd.first, sd.second);
+                ns = sd.first.size();
+                nd = sd.second.size();
+            }
             const auto t2 = clk::now();
             const int64_t a1 = lio_alloc_count();
-            const double t = std::chrono::duration<double, std::milli>(t2 - t1).count();
+            auto msd = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+            const double t = msd(t1, t2);
             ms.push_back(t);
             allocs.push_back((long long)(a1 - a0));
             const lio_icp_result& last = lc.last_result();
-            std::printf("call %d %.4f %d %zu %zu %d %d %.9g", k, t, closest, lc.getSourceCloud().size(),
-                        lc.getTargetCloud().size(), closest >= 0 ? last.iterations : 0, reg.is_valid_ ? 1 : 0,
-                        closest >= 0 ? last.score : -1.0);
+            std::printf("call %d %.4f %d %zu %zu %d %d %.9g", k, t, closest, ns, nd, closest >= 0 ? last.iterations : 0,
+                        reg.is_valid_ ? 1 : 0, closest >= 0 ? last.score : -1.0);
             for (int j = 0; j < 16; ++j) std::printf(" %.9g", closest >= 0 ? (double)last.T[j] : 0.0);
-            std::printf(" %lld\n", (long long)(a1 - a0));
+            std::printf(" %lld %.4f %.4f\n", (long long)(a1 - a0), msd(ta, tb), msd(tb, t2));
         }
         std::vector<double> warm(ms.begin() + (ms.size() > 1 ? 1 : 0), ms.end());
         long long warm_allocs = 0;

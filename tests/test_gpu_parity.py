@@ -384,6 +384,7 @@ def test_seeded_second_knn_bit_exact(oracle, c1, shift):
     _check_sums(g, o)
 
 
+@pytest.mark.parametrize("scale", [0.05, 0.5])
 def test_seeded_guard_whole_box(oracle, scale):
     """The seeded pass's guard: a bound shrunk below the true 5th distance (lio_ctx_set_seed_scale)
     leaves lists that are not full; they are reset and the far pass searches the whole box, 3x3x3
