@@ -536,13 +536,6 @@ __global__ void __launch_bounds__(kIcpStatsThreads) icp_stats_kernel(IcpArgs a, 
         ids[k] = i < a.n ? a.nn_id[i] : -1;
         d2s[k] = i < a.n ? a.nn_d2[i] : 0.f;
     }
-    if (a.aid && !a.fitness) {  // sharded PCL float modes: the accepted ids ride the all-gather (coalesced)
-#pragma unroll
-        for (int k = 0; k < PER; ++k) {
-            const int i = base + k * kIcpStatsThreads, id = ids[k];
-            if (i < a.n) a.aid[i] = (id >= 0 && id != kNone && !((double)d2s[k] > a.max_d2)) ? id : -1;
-        }
-    }
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
         const int i = base + k * kIcpStatsThreads, id = ids[k];
@@ -741,8 +734,8 @@ int icp_build_tiles(const GridBuf& q, uint2* tiles, uint32_t* scratch, void*& tm
 //   sigma    = one_over_n * dst_demean * src_demean^T  (the depth sum sequential)
 // A float sum's value depends on its order, so each of the 6 + 9 chains runs on ONE
 // lane, in order; the block stages the correspondences through LDS around it.
-// The serial fallback of the parallel seqsum path (lio_seqsum.hip); sharded, it runs over the whole
-// source with the all-gathered ids.  icp_pcl_means_kernel also writes the compacted pairs (src xyz,
+// The serial fallback of the parallel seqsum path (lio_seqsum.hip); sharded, it runs on every rank over
+// the gathered pairs of all ranks.  icp_pcl_means_kernel also writes the compacted pairs (src xyz,
 // tgt xyz) for icp_pcl_sigma_kernel.
 // ----------------------------------------------------------------------------
 constexpr int kPclThreads = 1024;  // one block: a chunk of 1024 correspondences per round
@@ -875,6 +868,36 @@ void launch_icp_pcl_means_serial(const IcpArgs& a, float* pairs, int64_t cap, fl
     icp_pcl_means_kernel<<<1, kPclThreads, 0, st>>>(a, pairs, cap, out16);
 }
 
+// the serial means of pairs compacted already (the sharded fallback's gathered pairs): lanes 0 .. 5 each add
+// their column in order (staged through LDS a chunk at a time), out[6] = the count
+__global__ void __launch_bounds__(kPclThreads) icp_pcl_means_pairs_kernel(const float* __restrict__ pairs, int64_t cap,
+                                                                          const uint32_t* __restrict__ d_n,
+                                                                          float* __restrict__ out) {
+    __shared__ float s[6][kPclThreads];
+    const uint32_t n = *d_n;
+    float acc = 0.f;
+    bool first = true;
+    for (uint32_t base = 0; base < n; base += kPclThreads) {
+        const uint32_t cnt = min((uint32_t)kPclThreads, n - base);
+#pragma unroll
+        for (int d = 0; d < 6; ++d)
+            if (threadIdx.x < cnt) s[d][threadIdx.x] = pairs[d * cap + (int64_t)(base + threadIdx.x)];
+        __syncthreads();
+        if (threadIdx.x < 6) serial_add(s[threadIdx.x], cnt, acc, first);
+        __syncthreads();
+    }
+    if (threadIdx.x < 6) out[threadIdx.x] = acc;
+    if (threadIdx.x == 0) out[6] = __uint_as_float(n);
+}
+
+void launch_icp_pcl_means_pairs(const float* pairs, int64_t cap, const uint32_t* d_n, float* out16, hipStream_t st) {
+    icp_pcl_means_pairs_kernel<<<1, kPclThreads, 0, st>>>(pairs, cap, d_n, out16);
+}
+
+void launch_icp_pcl_sigma_serial(const float* pairs, int64_t cap, float* out16, hipStream_t st) {
+    icp_pcl_sigma_kernel<<<1, kPclThreads, 0, st>>>(pairs, cap, out16);
+}
+
 __global__ void __launch_bounds__(64) icp_combine_kernel(const double* __restrict__ recv, int64_t nsup, int world,
                                                         int64_t rank_stride, double* __restrict__ out17) {
     const int k = threadIdx.x;
@@ -889,48 +912,6 @@ __global__ void __launch_bounds__(64) icp_combine_kernel(const double* __restric
 
 void launch_icp_combine(const double* recv, int64_t nsup, int world, int64_t rank_stride, double* out17, hipStream_t st) {
     icp_combine_kernel<<<1, 64, 0, st>>>(recv, nsup, world, rank_stride, out17);
-}
-
-// the rest of the whole source through T (the shard's points are transformed by icp_tile_kernel)
-__global__ void __launch_bounds__(256) icp_xform_rest_kernel(float* __restrict__ cur, int64_t ns, int64_t b, int64_t n,
-                                                             IcpT T) {
-    const int64_t rest = ns - n;
-    for (int64_t j = blockIdx.x * 256 + threadIdx.x; j < rest; j += (int64_t)gridDim.x * 256) {
-        const int64_t i = j < b ? j : j + n;
-        float x, y, z;
-        xform_pcl(T.m, cur[3 * i], cur[3 * i + 1], cur[3 * i + 2], x, y, z);
-        cur[3 * i] = x;
-        cur[3 * i + 1] = y;
-        cur[3 * i + 2] = z;
-    }
-}
-
-void launch_icp_xform_rest(float* cur, int64_t ns, int64_t b, int64_t n, const float* T16, hipStream_t st) {
-    if (ns - n <= 0) return;
-    IcpT T;
-    for (int k = 0; k < 16; ++k) T.m[k] = T16[k];
-    const int64_t nb = std::min<int64_t>((ns - n + 255) / 256, 4096);
-    icp_xform_rest_kernel<<<(int)nb, 256, 0, st>>>(cur, ns, b, n, T);
-}
-
-// blockIdx.y = rank r: its shard [b_r, b_r + n_r) of the source, ids at recv + r * rank_stride + id_off
-__global__ void __launch_bounds__(256) icp_gather_ids_kernel(const double* __restrict__ recv, int world,
-                                                             int64_t rank_stride, int64_t id_off, int64_t ns,
-                                                             int* __restrict__ gid) {
-    const int r = blockIdx.y;
-    const int64_t nsup = (ns + kIcpSuper - 1) / kIcpSuper;
-    const int64_t b0 = nsup * r / world * kIcpSuper, e0 = nsup * (r + 1) / world * kIcpSuper;
-    const int64_t b = b0 < ns ? b0 : ns, e = e0 < ns ? e0 : ns;
-    const int* ids = reinterpret_cast<const int*>(recv + (size_t)r * rank_stride + id_off);
-    for (int64_t j = blockIdx.x * 256 + threadIdx.x; j < e - b; j += (int64_t)gridDim.x * 256) gid[b + j] = ids[j];
-}
-
-void launch_icp_gather_ids(const double* recv, int world, int64_t rank_stride, int64_t id_off, int64_t ns, int* gid,
-                           hipStream_t st) {
-    if (ns <= 0) return;
-    const int64_t per = (ns + world - 1) / world;
-    const int64_t nb = std::max<int64_t>(std::min<int64_t>((per + 255) / 256, 1024), 1);
-    icp_gather_ids_kernel<<<dim3((unsigned)nb, (unsigned)world), 256, 0, st>>>(recv, world, rank_stride, id_off, ns, gid);
 }
 
 void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st, uint32_t* order, int ntiles) {

@@ -20,6 +20,7 @@
 #include <algorithm>
 #include <cfloat>
 #include <cmath>
+#include <cstddef>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -335,13 +336,14 @@ struct lio_icp {
     float* h_pclout = nullptr; // pinned copy
     void* x_owner = nullptr;   // exchange state owned by the handle (lio_icp_mp.cpp: shm segment, RCCL comm)
     void (*x_owner_free)(void*) = nullptr;
-    // sharded PCL float modes (fid_sharded): the whole source on every rank — the original and the
-    // incrementally transformed cloud (this rank's shard is the slice [sh_begin, sh_begin + sh_n) of it,
-    // the tile kernel transforms that slice, icp_xform_rest the rest) — and the all-gathered accepted ids
-    float* d_srcf = nullptr;
-    float* d_curf = nullptr;
-    int* d_gid = nullptr;
-    int64_t full_cap = 0;
+    // sharded PCL float modes (fid_sharded): only this rank's shard on the device; the float chains split by
+    // window (lio_seqsum.hpp), the per-rank event-list slot of the exchange (grown from what the last pass
+    // needed, the same on every rank), pinned staging for a host exchange, the serial fallback's gathered pairs
+    int ev_slot = 2048, ev_slot_s = 2048;
+    double* h_xs = nullptr;
+    double* h_xr = nullptr;
+    int64_t hx_cap = 0;
+    lio::PclBuf pg;
     int64_t fid_stats[4] = {0, 0, 0, 0};  // re-passes, serial fallbacks, events of the last pass, passes
     int fid_flags = 0;
     int64_t fid_evcap = 0;
@@ -368,10 +370,8 @@ static void icp_join_src(lio_icp* h) {
     if (h->bg_src.joinable()) h->bg_src.join();
 }
 
-// the PCL float modes with more than one rank: the float chains need every rank's correspondences
+// the PCL float modes with more than one rank: the float chains run split over the ranks' windows
 static bool fid_sharded(const lio_icp* h) { return h->p.umeyama_float > 0 && h->world > 1; }
-// the incrementally transformed cloud of this rank's shard
-static float* shard_cur(const lio_icp* h) { return fid_sharded(h) ? h->d_curf + 3 * h->sh_begin : h->d_cur; }
 
 // Capacities grow geometrically from a floor sized for the reference's largest submaps (C4: 500 k points): a
 // loop-closure node whose submaps change size on every 2 Hz loopTimerFunc call (fast_lio_sam.cpp:682-730) then
@@ -456,11 +456,13 @@ int lio_icp_destroy(lio_icp* h) {
     lio_icp_set_exchange_owner(h, nullptr, nullptr);
     lio::grid_free(h->tgt);
     lio::grid_free(h->qgrid);
-    void* ptrs[] = {h->d_thist, h->d_tgt,  h->d_src,   h->d_cur,    h->d_fd2,   h->d_fid,  h->d_tiles, h->d_tscratch,
-                    h->d_ttmp, h->d_dbg,   h->d_tcost,  h->d_order, h->d_pcl16, h->d_srcf,  h->d_curf,
-                    h->d_gid};
+    void* ptrs[] = {h->d_thist, h->d_tgt, h->d_src,   h->d_cur,   h->d_fd2,  h->d_fid, h->d_tiles, h->d_tscratch,
+                    h->d_ttmp,  h->d_dbg, h->d_tcost, h->d_order, h->d_pcl16};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
+    lio::pcl_free(h->pg);
+    if (h->h_xs) (void)hipHostFree(h->h_xs);
+    if (h->h_xr) (void)hipHostFree(h->h_xr);
     if (h->h_super) (void)hipHostFree(h->h_super);
     if (h->h_pcl16) (void)hipHostFree(h->h_pcl16);
     lio::pcl_free(h->pcl);
@@ -615,20 +617,31 @@ int lio_icp_set_shard_device(lio_icp* h, int rank, int world, lio_allgather_dev_
     return LIO_OK;
 }
 
-// Exchange message of one rank, in doubles: its records (slot = ceil(records / world) of kIcpStride), then
-// in the PCL float modes its accepted 1-NN ids (int32, slot * kIcpSuper of them).  exchange_len is the
-// capacity; a pass sends exchange_count (records only unless `ids`).
+// Exchange messages of one rank, in doubles (all-gathered, rank r's at r * count of the receive buffer):
+//   records   every pass: its 4096-point records (slot = ceil(records / world) of kIcpStride); in the sharded
+//             PCL float modes followed by its windows' chain totals (lio_seqsum.hpp, kTotPad)
+//   events    sharded PCL float modes: the seqsum event message of its window (ev_slot events per chain),
+//             for the means followed by its first kPclMaxKc pairs (lio_pcl.hpp)
+//   blocks    sharded orders 2 / 3: its depth blocks of sigma and the verification statuses
+//   gather    the sharded serial fallback: its pairs in rounds
+// exchange_len is the capacity of every one of them (the event slot up to ev_slot_cap).
 static int64_t exchange_slot(int64_t ns, int world) {
     const int64_t nsup = (ns + lio::kIcpSuper - 1) / lio::kIcpSuper;
     return (nsup + world - 1) / world;
 }
-static int64_t exchange_len(int64_t ns, int world) {
-    return exchange_slot(ns, world) * (lio::kIcpStride + lio::kIcpSuper / 2);
+static int64_t shard_points_max(int64_t ns, int world) { return exchange_slot(ns, world) * lio::kIcpSuper; }
+static int64_t ev_slot_cap(int64_t ns, int world) { return std::max<int64_t>(4096, shard_points_max(ns, world) / 8); }
+static int64_t records_count(int64_t ns, int world) { return exchange_slot(ns, world) * lio::kIcpStride; }
+// blocks of a window in the block-sum message (seq_shard_totals)
+static int64_t tot_blocks(int64_t ns, int world) { return (shard_points_max(ns, world) + lio::kSeqBlock - 1) / lio::kSeqBlock + 1; }
+static int64_t tot_words(int64_t ns, int world, int nch) { return lio::seq_tot_words(nch, tot_blocks(ns, world)); }
+static int64_t exchange_len_fsh(int64_t ns, int world) {
+    const int64_t rec = records_count(ns, world) + tot_words(ns, world, lio::kSeqMaxChains);
+    const int64_t ev = lio::seqsum_msg_words(lio::kSeqMaxChains, (int)ev_slot_cap(ns, world)) + lio::pcl_heads_words();
+    const int64_t x3 = lio::pcl_x3_words(lio::pcl_blocks_slot(shard_points_max(ns, world)));
+    return std::max(std::max(rec, ev), std::max(x3, (int64_t)4096));
 }
-static int64_t exchange_count(int64_t ns, int world, bool ids) {
-    return exchange_slot(ns, world) * (ids ? lio::kIcpStride + lio::kIcpSuper / 2 : lio::kIcpStride);
-}
-static int64_t exchange_id_off(int64_t ns, int world) { return exchange_slot(ns, world) * lio::kIcpStride; }
+static int64_t exchange_len(int64_t ns, int world) { return exchange_len_fsh(ns, world); }
 
 // the records of every rank (rank r at recv + r * stride doubles) summed in global record order
 static void combine_records(const double* recv, int64_t ns, int world, int64_t stride, double out17[17]) {
@@ -664,9 +677,11 @@ int lio_icp_set_exchange_buffers(lio_icp* h, double* d_send, double* d_recv, int
     return LIO_OK;
 }
 
-// device exchange buffers for the current source (the handle's own unless the caller's are large enough)
+// device exchange buffers for the current source (the handle's own unless the caller's are large enough): the
+// sharded PCL float modes need exchange_len, the double statistics only the records
 static int exchange_reserve(lio_icp* h) {
-    const int64_t need = std::max<int64_t>(exchange_len(h->ns, h->world), lio::kIcpStride);
+    const int64_t need = std::max<int64_t>(fid_sharded(h) ? exchange_len(h->ns, h->world) : records_count(h->ns, h->world),
+                                           lio::kIcpStride);
     if (!h->h_out17) {  // the record-order sums land here whoever owns the exchange buffers
         IHIP(hipHostMalloc(&h->h_out17, 32 * sizeof(double), hipHostMallocMapped));
         IHIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->h_out17_dev), h->h_out17, 0));
@@ -674,7 +689,8 @@ static int exchange_reserve(lio_icp* h) {
     if (!h->h_out17_dev) return ifail(LIO_ERR_STATE, "lio_icp_align: no device view of the result block");
     if (h->x_ext) {
         if (h->x_len < need)
-            return ifail(LIO_ERR_ARG, "lio_icp_align: caller exchange buffers too small (lio_icp_exchange_len)");
+            return ifail(LIO_ERR_ARG, "lio_icp_align: caller exchange buffers too small (lio_icp_exchange_len: " +
+                                          std::to_string(need) + " doubles per rank)");
         return LIO_OK;
     }
     if (h->x_len < need || !h->d_xsend || !h->d_xrecv) {
@@ -727,22 +743,6 @@ static int icp_prepare(lio_icp* h) {
     }
     h->ntiles = 0;
     h->have_order = false;  // new tiles: cell order until a pass has measured them
-    if (fid_sharded(h)) {  // the whole source on every rank (the float chains run over all of it)
-        const int64_t nf = std::max<int64_t>(h->ns, 1);
-        if (nf > h->full_cap) {
-            for (void** q : {(void**)&h->d_srcf, (void**)&h->d_curf, (void**)&h->d_gid}) {
-                if (*q) (void)hipFree(*q);
-                *q = nullptr;
-            }
-            h->full_cap = 0;
-            IHIP(hipMalloc(&h->d_srcf, nf * 3 * sizeof(float)));
-            IHIP(hipMalloc(&h->d_curf, nf * 3 * sizeof(float)));
-            IHIP(hipMalloc(&h->d_gid, nf * sizeof(int)));
-            h->full_cap = nf;
-        }
-        if (h->ns > 0)
-            IHIP(hipMemcpyAsync(h->d_srcf, h->h_src, h->ns * 3 * sizeof(float), hipMemcpyHostToDevice, h->st));
-    }
     if (h->sh_n > 0) {
         IHIP(hipMemcpyAsync(h->d_src, h->h_src + 3 * h->sh_begin, h->sh_n * 3 * sizeof(float),
                             hipMemcpyHostToDevice, h->st));
@@ -844,13 +844,270 @@ static int enqueue_pcl(lio_icp* h, const lio::IcpArgs& pa) {
     return LIO_OK;
 }
 
+// ---------------------------------------------------------------- the sharded PCL float statistics
+// Per correspondence pass (world > 1, umeyama_float 1..3), three all-gathers on the handle's stream:
+//   records   the tile kernel, the records, the window's compaction, the means chains' block sums and the
+//             window's totals -> all-gather -> the records' sum (MSE, counts) and every window's place in the
+//             chains (seq_shard_offsets)
+//   events    the means chains counted and their events listed on the window -> all-gather (+ each window's
+//             first kPclMaxKc pairs) -> the global event lists, the walk over all of them (every rank: the serial
+//             floor), the window verified
+//   blocks    orders 2 / 3: the GEMM depth blocks starting in the window -> all-gather -> res += alpha * C_b over
+//             all blocks in order (order 1: the sigma chains take the means' three steps themselves)
+// so per-rank work and memory follow the window (source / world) except the walk and the order-of-blocks
+// sums, and every rank gets the one-rank transform bit for bit (the verification covers every element).
+
+// all-gather `cnt` doubles per rank from d_xsend into d_xrecv (rank r's at r * cnt) in the handle's stream order:
+// the device callback enqueues it (RCCL / torch on an external stream); a host callback goes through pinned
+// staging, one wait per call
+static int xchg(lio_icp* h, int64_t cnt) {
+    if (cnt > h->x_len) return ifail(LIO_ERR_STATE, "lio_icp_align: an exchange message is larger than the buffers");
+    if (h->fn_dev) {
+        if (h->fn_dev(h->d_xsend, cnt, h->d_xrecv, (void*)h->st, h->user_dev) != 0)
+            return ifail(LIO_ERR_STATE, "device all-gather callback failed");
+        return LIO_OK;
+    }
+    if (!h->fn) return ifail(LIO_ERR_STATE, "lio_icp_align: sharded without an exchange");
+    if (h->hx_cap < h->x_len) {
+        if (h->h_xs) (void)hipHostFree(h->h_xs);
+        if (h->h_xr) (void)hipHostFree(h->h_xr);
+        h->h_xs = h->h_xr = nullptr;
+        h->hx_cap = 0;
+        lio::count_alloc(2);
+        IHIP(hipHostMalloc(&h->h_xs, (size_t)h->x_len * sizeof(double), hipHostMallocDefault));
+        IHIP(hipHostMalloc(&h->h_xr, (size_t)h->x_len * h->world * sizeof(double), hipHostMallocDefault));
+        h->hx_cap = h->x_len;
+    }
+    IHIP(hipMemcpyAsync(h->h_xs, h->d_xsend, (size_t)cnt * sizeof(double), hipMemcpyDeviceToHost, h->st));
+    IHIP(hipStreamSynchronize(h->st));
+    if (h->fn(h->h_xs, cnt, h->h_xr, h->user) != 0) return ifail(LIO_ERR_STATE, "allgather callback failed");
+    IHIP(hipMemcpyAsync(h->d_xrecv, h->h_xr, (size_t)cnt * h->world * sizeof(double), hipMemcpyHostToDevice, h->st));
+    return LIO_OK;
+}
+
+static lio::SeqPairs fsh_means_src(const lio_icp* h) { return lio::SeqPairs{h->pcl.pairs, h->pcl.cap}; }
+static lio::SeqSigma fsh_sigma_src(const lio_icp* h) { return lio::SeqSigma{h->pcl.pairs, h->pcl.mean6, h->pcl.cap}; }
+
+// the means' event message is packed (seqsum_shard_mid / _repack): + the window's first pairs -> all-gather ->
+// the pairs after the window appended, the global lists, the walk, the window's verification
+static int fsh_means_events(lio_icp* h, int pass) {
+    lio::PclBuf& P = h->pcl;
+    const int order = h->p.umeyama_float;
+    const int64_t ev_words = lio::seqsum_msg_words(6, h->ev_slot);
+    const int64_t m2 = ev_words + (order != 1 ? lio::pcl_heads_words() : 0);
+    if (order != 1) lio::launch_pcl_shard_heads(P, h->d_xsend + ev_words, h->st);
+    int rc = xchg(h, m2);
+    if (rc) return rc;
+    if (order != 1) lio::launch_pcl_shard_heads_merge(P, h->d_xrecv, m2, ev_words, h->rank, h->world, h->st);
+    lio::seqsum_shard_tail(fsh_means_src(h), 6, P.small + lio::kPclN, P.means, pass, h->d_xrecv, m2, h->rank, h->world,
+                           h->ev_slot, h->st);
+    return LIO_OK;
+}
+
+// sigma and the result: order 1 the nine sigma chains sharded like the means (stage 0: from pass spass's block
+// sums; stage 1: the same lists exchanged again with a larger slot), orders 2 / 3 the depth blocks; then the
+// block exchange, the statuses combined, pcl_pack, and the pass's output on the host (one wait)
+static int fsh_sigma_pack(lio_icp* h, int spass, int stage = 0) {
+    lio::PclBuf& P = h->pcl;
+    const int order = h->p.umeyama_float;
+    const uint32_t* dn = P.small + lio::kPclN;
+    const int64_t nq_slot = lio::pcl_blocks_slot(shard_points_max(h->ns, h->world));
+    int rc = LIO_OK;
+    if (order == 1) {
+        const lio::SeqSigma ss = fsh_sigma_src(h);
+        if (stage == 0) {
+            lio::launch_pcl_mean6(P, P.means.result, h->st);
+            const int64_t nbs = tot_blocks(h->ns, h->world), tw = tot_words(h->ns, h->world, 9);
+            if (spass <= 1) {
+                lio::seqsum_shard_head(ss, 9, dn, P.sig, h->d_xsend, nbs, h->st);
+                if ((rc = xchg(h, tw))) return rc;
+            }
+            lio::seqsum_shard_mid(ss, 9, dn, P.sig, spass, h->d_xrecv, tw, nbs, h->rank, h->world, h->d_xsend,
+                                  h->ev_slot_s, h->st);
+        } else {
+            IHIP(hipMemsetAsync(P.sig.status + 1, 0, sizeof(uint32_t), h->st));
+            lio::seqsum_shard_repack(ss, 9, dn, P.sig, h->d_xsend, h->ev_slot_s, h->st);
+        }
+        const int64_t m = lio::seqsum_msg_words(9, h->ev_slot_s);
+        if ((rc = xchg(h, m))) return rc;
+        lio::seqsum_shard_tail(ss, 9, dn, P.sig, spass, h->d_xrecv, m, h->rank, h->world, h->ev_slot_s, h->st);
+    }
+    lio::launch_pcl_sigma_shard(P, order, h->d_xsend, nq_slot, h->st);
+    const int64_t m3 = order == 1 ? lio::kPclX3Hdr : lio::pcl_x3_words(nq_slot);
+    if ((rc = xchg(h, m3))) return rc;
+    lio::launch_pcl_x3_merge(P, order, h->d_xrecv, m3, h->world, nq_slot, h->d_pclout, h->st);
+    lio::launch_pcl_pack_shard(P, order, h->d_pclout, h->st);
+    IHIP(hipMemcpyAsync(h->h_pclout, h->d_pclout, lio::kPclOutWords * sizeof(float), hipMemcpyDeviceToHost, h->st));
+    IHIP(hipStreamSynchronize(h->st));
+    return LIO_OK;
+}
+
+// the serial fallback, sharded: every window's pairs gathered on every rank (in rounds that fit the exchange
+// buffers; O(source) memory for this path only), the serial chains over them
+static int fsh_serial(lio_icp* h, const lio::IcpArgs& a, bool lb_timeout) {
+    ++h->fid_stats[1];
+    lio::PclBuf& P = h->pcl;
+    lio::PclBuf& G = h->pg;
+    const int order = h->p.umeyama_float;
+    const uint32_t* dn = P.small + lio::kPclN;
+    if (lb_timeout) {  // the window's pairs re-compacted by the serial kernel (its count lands in d_pcl16[6])
+        lio::launch_icp_pcl_means_serial(a, P.pairs, P.cap, h->d_pcl16, h->st);
+        dn = reinterpret_cast<const uint32_t*>(h->d_pcl16 + 6);
+        IHIP(hipMemsetAsync(P.small + lio::kPclTicket + 1, 0, sizeof(uint32_t), h->st));
+    }
+    if (lio::pcl_reserve_plain(G, std::max<int64_t>(h->ns, 1), h->st)) return ifail(LIO_ERR_NOMEM, "lio_icp_align: fallback pairs");
+    const int64_t chunk = (exchange_len(h->ns, h->world) - 2) / 3;  // the capacity every exchange offers
+    const int64_t rounds = (shard_points_max(h->ns, h->world) + chunk - 1) / chunk;
+    for (int64_t t = 0; t < rounds; ++t) {
+        lio::launch_pcl_gather_pack(P, dn, t, chunk, h->d_xsend, h->st);
+        const int rc = xchg(h, lio::pcl_gather_words(chunk));
+        if (rc) return rc;
+        lio::launch_pcl_gather_unpack(G, h->d_xrecv, lio::pcl_gather_words(chunk), h->world, t, chunk, h->st);
+    }
+    const uint32_t* gn = G.small + lio::kPclN;
+    lio::launch_icp_pcl_means_pairs(G.pairs, G.cap, gn, h->d_pcl16, h->st);
+    if (order == lio::kPclSeq) {
+        lio::launch_icp_pcl_sigma_serial(G.pairs, G.cap, h->d_pcl16, h->st);
+        IHIP(hipMemcpyAsync(h->h_pclout, h->d_pcl16, 16 * sizeof(float), hipMemcpyDeviceToHost, h->st));
+    } else {
+        lio::launch_pcl_sigma(G, order, 1, h->st, h->d_pcl16);
+        lio::launch_pcl_pack(G, order, h->d_pclout, h->st, h->d_pcl16);
+        IHIP(hipMemcpyAsync(h->h_pclout, h->d_pclout, lio::kPclOutWords * sizeof(float), hipMemcpyDeviceToHost, h->st));
+    }
+    IHIP(hipStreamSynchronize(h->st));
+    h->h_pclout[16] = h->h_pclout[17] = 0.f;
+    IHIP(hipGetLastError());
+    return LIO_OK;
+}
+
+// the per-rank event slot for the next exchange: 1.5 x the longest list of this one (every rank saw the same
+// lists, so every rank picks the same slot), at least 1024, at most the capacity
+static int next_slot(const lio_icp* h, int longest) {
+    const int64_t want = ((int64_t)longest * 3 / 2 + 256 + 255) / 256 * 256;
+    return (int)std::min<int64_t>(std::max<int64_t>(want, 1024), ev_slot_cap(h->ns, h->world));
+}
+
+// pcl_finish for the sharded modes: the same re-pass policy (the statuses are every rank's, combined), plus a
+// re-exchange when a list only outgrew its slot; the serial fallback gathers the pairs
+static int pcl_finish_fsh(lio_icp* h, const lio::IcpArgs& a) {
+    const int order = h->p.umeyama_float;
+    lio::PclBuf& P = h->pcl;
+    const uint32_t* dn = P.small + lio::kPclN;
+    ++h->fid_stats[3];
+    {
+        int ev;
+        std::memcpy(&ev, h->h_pclout + 18, sizeof(ev));
+        h->fid_stats[2] = ev;
+    }
+    const bool lb_timeout = pcl_word(h, 3) != 0;
+    constexpr int kMaxPasses = 4;
+    int mpass = 1, spass = 1, reexchanges = 0;
+    while (!lb_timeout) {
+        const uint32_t bad = pcl_word(h, 0), over = pcl_word(h, 1), xf = pcl_word(h, 4);
+        const int mm = (int)pcl_word(h, 5), ms = (int)pcl_word(h, 6);
+        h->ev_slot = next_slot(h, mm);
+        if (order == 1 && ms > 0) h->ev_slot_s = next_slot(h, ms);
+        if ((bad | over) == 0) break;
+        if (bad) P.means.forced_dirty = P.sig.forced_dirty = true;
+        const bool hard = (xf & (2u | 4u | 0x200u)) != 0;
+        const int64_t cap = ev_slot_cap(h->ns, h->world);
+        if (!hard && (xf & (1u | 0x100u)) && mm <= cap && ms <= cap && reexchanges < 2) {
+            // a list longer than its slot, nothing else: the same lists again with the slot they need
+            ++reexchanges;
+            if (xf & 1u) {
+                IHIP(hipMemsetAsync(P.means.status + 1, 0, sizeof(uint32_t), h->st));
+                lio::seqsum_shard_repack(fsh_means_src(h), 6, dn, P.means, h->d_xsend, h->ev_slot, h->st);
+                int rc = fsh_means_events(h, mpass);
+                if (rc) return rc;
+                spass = 1;
+                rc = fsh_sigma_pack(h, 1);
+                if (rc) return rc;
+            } else {
+                const int rc = fsh_sigma_pack(h, spass, 1);
+                if (rc) return rc;
+            }
+            continue;
+        }
+        if (over) break;  // a list over its capacity: more passes only add events
+        if (bad & 0x3fu) {  // the means (sigma depends on them: its chains restart from pass 1)
+            if (mpass >= kMaxPasses) break;
+            ++mpass;
+            lio::seqsum_shard_mid(fsh_means_src(h), 6, dn, P.means, mpass, nullptr, 0, 0, h->rank, h->world,
+                                  h->d_xsend, h->ev_slot, h->st);
+            int rc = fsh_means_events(h, mpass);
+            if (rc) return rc;
+            spass = 1;
+            rc = fsh_sigma_pack(h, spass);
+            if (rc) return rc;
+        } else {
+            if (spass >= kMaxPasses) break;
+            const int rc = fsh_sigma_pack(h, ++spass);
+            if (rc) return rc;
+        }
+        ++h->fid_stats[0];
+        ++h->fid_stats[3];
+    }
+    if (lb_timeout || (pcl_word(h, 0) | pcl_word(h, 1)) != 0) {
+        const int rc = fsh_serial(h, a, lb_timeout);
+        if (rc) return rc;
+    }
+    IHIP(hipGetLastError());
+    return LIO_OK;
+}
+
+// one correspondence pass of the sharded PCL float modes (a: this rank's shard, as icp_pass built it)
+static int icp_pass_fsh(lio_icp* h, const lio::IcpArgs& a, bool apply_T, double out17[17], float* pcl16) {
+    if (h->world > 64) return ifail(LIO_ERR_ARG, "lio_icp_align: the sharded float statistics take at most 64 ranks");
+    int rc = exchange_reserve(h);
+    if (rc) return rc;
+    lio::PclBuf& P = h->pcl;
+    const uint32_t* dn = P.small + lio::kPclN;
+    const int64_t rec = records_count(h->ns, h->world), nbs = tot_blocks(h->ns, h->world);
+    const int64_t cnt1 = rec + tot_words(h->ns, h->world, 6);
+    const int64_t nsup = (h->ns + lio::kIcpSuper - 1) / lio::kIcpSuper;
+    if (h->timing) IHIP(hipEventRecord(h->ev.a, h->st));
+    if (h->sh_n > 0) lio::launch_icp_tiles(a, h->ntiles, h->st);
+    if (h->timing) IHIP(hipEventRecord(h->ev.m, h->st));
+    if (h->sh_n > 0) lio::launch_icp_stats(a, h->d_xsend, h->st, h->d_order, h->ntiles);
+    if (h->timing) IHIP(hipEventRecord(h->ev.b, h->st));
+    lio::launch_pcl_compact(a, P, h->st);
+    if (h->fid_flags & 4)  // test hook (lio_icp_set_fidelity_debug): report a look-back time-out for this pass
+        IHIP(hipMemsetAsync(P.small + lio::kPclTicket + 1, 1, sizeof(uint32_t), h->st));
+    lio::seqsum_shard_head(fsh_means_src(h), 6, dn, P.means, h->d_xsend + rec, nbs, h->st);
+    if ((rc = xchg(h, cnt1))) return rc;
+    lio::launch_icp_combine(h->d_xrecv, nsup, h->world, cnt1, h->h_out17_dev, h->st);
+    lio::seqsum_shard_mid(fsh_means_src(h), 6, dn, P.means, 1, h->d_xrecv + rec, cnt1, nbs, h->rank, h->world,
+                          h->d_xsend, h->ev_slot, h->st);
+    if ((rc = fsh_means_events(h, 1))) return rc;
+    if ((rc = fsh_sigma_pack(h, 1))) return rc;  // waits for the pass
+    IHIP(hipGetLastError());
+    h->have_prior = true;
+    if (h->sh_n > 0) h->have_order = true;
+    if (apply_T) ++h->nT;
+    if (h->timing && h->sh_n > 0) {
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, h->ev.a, h->ev.b) == hipSuccess) {
+            h->tm.icp_ms += ms;
+            ++h->tm.icp_launches;
+        }
+        if (hipEventElapsedTime(&ms, h->ev.a, h->ev.m) == hipSuccess) {
+            h->tm.icp_nn_ms += ms;
+            ++h->tm.icp_nn_launches;
+        }
+    }
+    std::memcpy(out17, h->h_out17, 17 * sizeof(double));
+    if ((rc = pcl_finish_fsh(h, a))) return rc;
+    std::memcpy(pcl16, h->h_pclout, 16 * sizeof(float));
+    return LIO_OK;
+}
+
 // One correspondence (or fitness) pass: GPU kernels + exchange + ordered sum.
 static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, double max_d2, double out17[17],
                     float* pcl16 = nullptr) {
     lio::IcpArgs a{};
     a.grid = lio::grid_view(h->tgt);
     a.tgt_by_id = h->tgt.by_id;
-    a.cur = shard_cur(h);
+    a.cur = h->d_cur;
     a.src = h->d_src;
     a.thist = h->d_thist;
     a.nT = h->nT;
@@ -890,26 +1147,14 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
 #endif
     const int nsup_loc = (int)((h->sh_n + lio::kIcpSuper - 1) / lio::kIcpSuper);
     const bool dev_x = h->world > 1 && h->fn_dev;  // device-side exchange: records stay on the device
-    // sharded PCL float modes: the accepted ids ride the exchange, the float chains run over the whole cloud
-    const bool fsh = pcl16 && fid_sharded(h) && !fitness;
-    const int64_t cnt = exchange_count(h->ns, h->world, fsh);  // doubles per rank this pass
-    const int64_t id_off = exchange_id_off(h->ns, h->world);
-    if (dev_x || fsh) {
+    // the sharded PCL float modes' correspondence passes: icp_pass_fsh (the chains split over the ranks' windows)
+    if (pcl16 && fid_sharded(h) && !fitness) return icp_pass_fsh(h, a, apply_T, out17, pcl16);
+    const int64_t cnt = records_count(h->ns, h->world);  // doubles per rank this pass
+    if (dev_x) {
         const int rc = exchange_reserve(h);
         if (rc) return rc;
-        if (h->x_len < cnt) return ifail(LIO_ERR_STATE, "lio_icp_align: exchange buffers smaller than a pass");
     }
-    if (fsh) a.aid = reinterpret_cast<int*>(h->d_xsend + id_off);
-    lio::IcpArgs pa = a;  // the float statistics' correspondences
-    if (fsh) {
-        pa.n = (int)h->ns;
-        pa.cur = h->d_curf;
-        pa.nn_id = h->d_gid;
-        pa.nn_d2 = nullptr;  // gated by icp_stats_kernel (-1 = rejected)
-        pa.aid = nullptr;
-    }
-    if (h->sh_n > 0 || dev_x || fsh) {
-        if (fsh && apply_T) lio::launch_icp_xform_rest(h->d_curf, h->ns, h->sh_begin, h->sh_n, T, h->st);
+    if (h->sh_n > 0 || dev_x) {
         if (h->timing) IHIP(hipEventRecord(h->ev.a, h->st));
         if (h->sh_n > 0) lio::launch_icp_tiles(a, h->ntiles, h->st);
         if (h->timing) IHIP(hipEventRecord(h->ev.m, h->st));
@@ -920,15 +1165,13 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
                 return ifail(LIO_ERR_STATE, "device all-gather callback failed");
             const int64_t nsup = (h->ns + lio::kIcpSuper - 1) / lio::kIcpSuper;
             lio::launch_icp_combine(h->d_xrecv, nsup, h->world, cnt, h->h_out17_dev, h->st);
-            if (fsh) lio::launch_icp_gather_ids(h->d_xrecv, h->world, cnt, id_off, h->ns, h->d_gid, h->st);
         } else if (h->sh_n > 0) {
             // records straight to host memory; the next pass's tile order in the same launch
             lio::launch_icp_stats(a, h->h_super_dev, h->st, fitness ? nullptr : h->d_order, h->ntiles);
         }
         if (h->timing) IHIP(hipEventRecord(h->ev.b, h->st));
-        // the float statistics now, unless the ids still have to cross the host exchange
-        if (pcl16 && (!fsh || dev_x)) {
-            const int rc = enqueue_pcl(h, pa);
+        if (pcl16) {  // one rank: the float statistics of its correspondences
+            const int rc = enqueue_pcl(h, a);
             if (rc) return rc;
         }
         IHIP(hipGetLastError());
@@ -1003,20 +1246,11 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
         }
     }
     if (!dev_x && h->world > 1) {
-        // host exchange: fixed-size slots (max records per rank, then the ids), summed in global record order
+        // host exchange: fixed-size slots (max records per rank), summed in global record order
         std::vector<double> send((size_t)cnt, 0.0), recv((size_t)cnt * h->world);
         std::memcpy(send.data(), h->h_super, (size_t)nsup_loc * lio::kIcpStride * sizeof(double));
-        if (fsh && h->sh_n > 0)
-            IHIP(hipMemcpy(send.data() + id_off, h->d_xsend + id_off, (size_t)h->sh_n * sizeof(int), hipMemcpyDeviceToHost));
         if (h->fn(send.data(), cnt, recv.data(), h->user) != 0) return ifail(LIO_ERR_STATE, "allgather callback failed");
         combine_records(recv.data(), h->ns, h->world, cnt, out17);
-        if (fsh) {  // every rank's ids back on the device, then the float statistics over the whole cloud
-            IHIP(hipMemcpyAsync(h->d_xrecv, recv.data(), recv.size() * sizeof(double), hipMemcpyHostToDevice, h->st));
-            lio::launch_icp_gather_ids(h->d_xrecv, h->world, cnt, id_off, h->ns, h->d_gid, h->st);
-            const int rc = enqueue_pcl(h, pa);
-            if (rc) return rc;
-            IHIP(hipStreamSynchronize(h->st));
-        }
     } else if (dev_x) {  // the record-order sums of every rank's records, computed on the device
         std::memcpy(out17, h->h_out17, 17 * sizeof(double));
     } else {
@@ -1025,7 +1259,7 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
             for (int k = 0; k < 17; ++k) out17[k] += h->h_super[(size_t)s * lio::kIcpStride + k];
     }
     if (pcl16) {
-        const int rc = pcl_finish(h, pa);
+        const int rc = pcl_finish(h, a);
         if (rc) return rc;
         std::memcpy(pcl16, h->h_pclout, 16 * sizeof(float));
     }
@@ -1110,30 +1344,54 @@ extern "C" int lio_seqsum6(int device, const float* x, int64_t n, int flags, flo
     return done(LIO_OK, "");
 }
 
-extern "C" int lio_icp_exchange_layout(int64_t ns, int world, int ids, int64_t* count, int64_t* id_off) {
-    if (ns < 0 || world < 1 || !count || !id_off) return ifail(LIO_ERR_ARG, "lio_icp_exchange_layout: bad arguments");
-    *count = exchange_count(ns, world, ids != 0);
-    *id_off = exchange_id_off(ns, world);
+// host mirrors of the sharded float chains' exchange logic (the device kernels run the same seq_shard_* helpers,
+// lio_seqsum.hpp): the gathered totals -> one window's offsets; the gathered event messages -> one chain's global
+// event lists.  tests/test_dist_gloo.py drives them with messages all-gathered over gloo.
+extern "C" int lio_seq_shard_offsets(const double* recv, int64_t stride, int64_t nb_slot, int rank, int world, int nch,
+                                     double* off0, double* var0, int32_t* floor_e, int64_t* gbase_nglobal) {
+    if (!recv || !off0 || !var0 || !floor_e || !gbase_nglobal || world < 1 || rank < 0 || rank >= world || nch < 1 ||
+        nch > lio::kSeqMaxChains || nb_slot < 1 || stride < lio::seq_tot_words(nch, nb_slot))
+        return ifail(LIO_ERR_ARG, "lio_seq_shard_offsets: bad arguments");
+    for (int c = 0; c < nch; ++c) {
+        int fl;
+        lio::seq_shard_offsets_chain(recv, stride, nb_slot, rank, world, c, off0[c], var0[c], fl, gbase_nglobal[0],
+                                     gbase_nglobal[1]);
+        floor_e[c] = fl;
+    }
     return LIO_OK;
 }
 
-// host mirror of icp_gather_ids_kernel (the sharded PCL float modes' id unpacking)
-extern "C" int lio_icp_gather_ids(const double* recv, int64_t ns, int world, int64_t count, int32_t* gid) {
-    if (!recv || !gid || ns < 0 || world < 1 || count < exchange_count(ns, world, true))
-        return ifail(LIO_ERR_ARG, "lio_icp_gather_ids: bad arguments");
-    const int64_t id_off = exchange_id_off(ns, world);
-    for (int r = 0; r < world; ++r) {
-        int64_t b = 0, n = 0;
-        shard_range(ns, r, world, b, n);
-        std::memcpy(gid + b, reinterpret_cast<const int32_t*>(recv + (size_t)r * (size_t)count + (size_t)id_off),
-                    (size_t)n * sizeof(int32_t));
+extern "C" int lio_seq_shard_merge(const double* recv, int64_t stride, int world, int slot, int chain, int64_t evs,
+                                   int32_t* pos, uint64_t* P, float* x, int32_t* nev_ptot_bad, uint64_t* ptot, float* x0) {
+    if (!recv || !pos || !P || !x || !nev_ptot_bad || !ptot || !x0 || world < 1 || world > 64 || slot < 0 || chain < 0 ||
+        chain >= lio::kSeqMaxChains || stride < lio::seqsum_msg_words(chain + 1, slot))
+        return ifail(LIO_ERR_ARG, "lio_seq_shard_merge: bad arguments");
+    int eoff[65];
+    uint64_t poff[65];
+    int64_t ppos[65];
+    int mx = 0;
+    const int bad = lio::seq_shard_merge_chain(recv, stride, world, slot, chain, evs, eoff, poff, ppos, *x0, mx);
+    nev_ptot_bad[0] = eoff[world];
+    nev_ptot_bad[1] = mx;
+    nev_ptot_bad[2] = bad;
+    *ptot = poff[world];
+    if (bad) return LIO_OK;
+    for (int r = 0; r < world; ++r) {  // seq_shard_merge's copy: every rank's events moved by the ranks before it
+        const double* ev = recv + (int64_t)r * stride + lio::kSeqHdrWords + (int64_t)chain * 2 * slot;
+        for (int j = 0; j < eoff[r + 1] - eoff[r]; ++j) {
+            const uint64_t w = (uint64_t)lio::seq_bits(ev[2 * j + 1]);
+            P[eoff[r] + j] = poff[r] + (uint64_t)lio::seq_bits(ev[2 * j]);
+            pos[eoff[r] + j] = (int32_t)(ppos[r] + (int64_t)(uint32_t)w);
+            uint32_t xb = (uint32_t)(w >> 32);
+            std::memcpy(&x[eoff[r] + j], &xb, sizeof(float));
+        }
     }
     return LIO_OK;
 }
 
 extern "C" int lio_icp_combine(const double* recv, int64_t ns, int world, double* out17) {
     if (!recv || !out17 || world < 1 || ns < 0) return ifail(LIO_ERR_ARG, "lio_icp_combine: bad arguments");
-    combine_records(recv, ns, world, exchange_count(ns, world, false), out17);
+    combine_records(recv, ns, world, records_count(ns, world), out17);
     return LIO_OK;
 }
 
@@ -1166,11 +1424,28 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
     h->bg_tgt_err.clear();
     h->bg_src_err.clear();
     if (pcl_float) {
-        if (lio::pcl_reserve(h->pcl, std::max<int64_t>(fid_sharded(h) ? h->ns : h->sh_n, kIcpCapFloor), h->p.umeyama_float, h->st))
+        // the window's pairs (sharded: + the kPclMaxKc pairs of the ranks after it, for the depth blocks that
+        // start in the window and end in the next)
+        const bool fsh = fid_sharded(h);
+        lio::PclBuf& P = h->pcl;
+        if (lio::pcl_reserve(P, std::max<int64_t>(h->sh_n + (fsh ? lio::kPclMaxKc : 0), kIcpCapFloor), h->p.umeyama_float, h->st))
             return ifail(LIO_ERR_NOMEM, "lio_icp_align: fidelity buffers");
-        h->pcl.means.dbg_noinc = h->pcl.sig.dbg_noinc = h->fid_flags & 1;
-        for (lio::SeqSumBuf* b : {&h->pcl.means, &h->pcl.sig})
+        P.means.dbg_noinc = P.sig.dbg_noinc = h->fid_flags & 1;
+        for (lio::SeqSumBuf* b : {&P.means, &P.sig})
             b->evcap = h->fid_evcap > 0 ? std::min(h->fid_evcap, b->evcap_alloc) : b->evcap_alloc;
+        P.mean6 = reinterpret_cast<float*>(P.small + lio::kPclMean6);
+        if (lio::seqsum_shard(P.means, fsh, h->st) ||
+            (h->p.umeyama_float == lio::kPclSeq && lio::seqsum_shard(P.sig, fsh, h->st)) ||
+            (fsh && lio::pcl_shard_reserve(P, h->ns / 340 + 4, h->st)))
+            return ifail(LIO_ERR_NOMEM, "lio_icp_align: sharded fidelity buffers");
+        P.n_all = fsh ? reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(P.means.sh) +
+                                                          offsetof(lio::SeqShard, n32))
+                      : nullptr;
+        if (fsh) {
+            const int cap = (int)ev_slot_cap(h->ns, h->world);
+            h->ev_slot = std::min(h->ev_slot, cap);
+            h->ev_slot_s = std::min(h->ev_slot_s, cap);
+        }
         if (!h->d_pcl16) IHIP(hipMalloc(&h->d_pcl16, 16 * sizeof(float)));
         if (!h->d_pclout) IHIP(hipMalloc(&h->d_pclout, 32 * sizeof(float)));
         if (!h->h_pclout) IHIP(hipHostMalloc(&h->h_pclout, 32 * sizeof(float), hipHostMallocDefault));
@@ -1182,12 +1457,8 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
         fin[i] = G[i];
         if (G[i] != ((i % 5 == 0) ? 1.f : 0.f)) ident = false;
     }
-    if (fid_sharded(h)) {  // the whole cloud restarts from the source on every rank
-        if (h->ns > 0)
-            IHIP(hipMemcpyAsync(h->d_curf, h->d_srcf, h->ns * 3 * sizeof(float), hipMemcpyDeviceToDevice, h->st));
-    } else if (h->sh_n > 0) {
+    if (h->sh_n > 0)
         IHIP(hipMemcpyAsync(h->d_cur, h->d_src, h->sh_n * 3 * sizeof(float), hipMemcpyDeviceToDevice, h->st));
-    }
     const int hist_need = std::max(h->p.max_iter, 1) + 4;  // one T per iteration plus the guess
     if (hist_need > h->thist_cap) {
         if (h->d_thist) IHIP(hipFree(h->d_thist));
@@ -1285,7 +1556,7 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
     out->score = fs[0] > 0 ? fs[16] / fs[0] : std::numeric_limits<double>::max();
     out->is_valid = (out->is_converged && out->score < h->p.score_threshold) ? 1 : 0;
     if (aligned && h->sh_n > 0) {
-        IHIP(hipMemcpyAsync(aligned, shard_cur(h), h->sh_n * 3 * sizeof(float), hipMemcpyDeviceToHost, h->st));
+        IHIP(hipMemcpyAsync(aligned, h->d_cur, h->sh_n * 3 * sizeof(float), hipMemcpyDeviceToHost, h->st));
         IHIP(hipStreamSynchronize(h->st));
     }
     return LIO_OK;

@@ -154,8 +154,6 @@ struct IcpArgs {
     const uint32_t* order;  // optional tile visit order (heaviest first, from the previous pass's costs)
     uint32_t* tile_cost;    // per tile: candidates scanned in this pass
     unsigned long long* dbg;  // optional counters (diagnostics): candidates, rings, tiles, lanes, tested
-    int* aid;               // optional (sharded PCL float modes): per shard point the accepted 1-NN id, or -1
-                            // (written by icp_stats_kernel beside the records; all-gathered with them)
 };
 
 constexpr int kIcpSuper = 4096;    // points per exchanged partial (shard granule)
@@ -174,18 +172,13 @@ void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st, uint32_t*
 // the all-gathered records (rank r's records from recv + r * rank_stride doubles) summed in global record
 // order, one thread per statistic (the order of lio_icp_combine: bit-identical) -> out17 (host-mapped)
 void launch_icp_combine(const double* recv, int64_t nsup, int world, int64_t rank_stride, double* out17, hipStream_t st);
-// sharded PCL float modes: cur[i] = T cur[i] (PCL's float order, as icp_tile_kernel applies it) for the
-// points of the whole source OUTSIDE this rank's shard [b, b + n), so every rank holds the full
-// incrementally transformed cloud bit for bit
-void launch_icp_xform_rest(float* cur, int64_t ns, int64_t b, int64_t n, const float* T16, hipStream_t st);
-// sharded PCL float modes: every rank's accepted ids (int32, from recv + r * rank_stride + id_off doubles)
-// into gid[0 .. ns) in global source order
-void launch_icp_gather_ids(const double* recv, int world, int64_t rank_stride, int64_t id_off, int64_t ns,
-                           int* gid, hipStream_t st);
 // PCL-order fidelity mode: out16[0..5] float sums (src, tgt), [6] count bits, [7..15] sigma accumulator
 // (row-major target x source) — serial float chains (one block); pairs: n * 6 floats scratch
 void launch_icp_pcl_stats(const IcpArgs& a, float* pairs, int64_t cap, float* out16, hipStream_t st);
 // the serial means alone (out16[0..6]; pairs compacted as a by-product): the fidelity orders' fallback
 void launch_icp_pcl_means_serial(const IcpArgs& a, float* pairs, int64_t cap, float* out16, hipStream_t st);
+// the same over pairs compacted already (*d_n of them), and order 1's serial sigma over them (out16[6] = n)
+void launch_icp_pcl_means_pairs(const float* pairs, int64_t cap, const uint32_t* d_n, float* out16, hipStream_t st);
+void launch_icp_pcl_sigma_serial(const float* pairs, int64_t cap, float* out16, hipStream_t st);
 
 }  // namespace lio

@@ -29,7 +29,7 @@ namespace {
 constexpr int kPT = 256;           // threads per compaction block
 constexpr int kPPer = 4;           // consecutive source points per thread
 constexpr int kPB = kPT * kPPer;   // source points per compaction block
-constexpr int kMaxKc = 1016;       // kc at a 48 KiB L1 (the largest modelled)
+constexpr int kMaxKc = kPclMaxKc;  // kc at a 48 KiB L1 (the largest modelled)
 constexpr int kPackWin = 1024;     // GEMM depth blocks staged per window in pcl_pack (36 KiB of LDS)
 
 // a.nn_d2 == nullptr (sharded): a.nn_id holds the all-gathered ids, the gate already applied (-1 = rejected)
@@ -258,7 +258,299 @@ __global__ void __launch_bounds__(kPackThreads) pcl_pack_kernel(const float* __r
     }
 }
 
+// ---------------------------------------------------------------- sharded statistics
+// this rank's first kMaxKc pairs, column-major (6 x kMaxKc floats) behind the means' event message
+__global__ void __launch_bounds__(256) pcl_heads_kernel(const float* __restrict__ pairs, int64_t cap,
+                                                        const uint32_t* __restrict__ d_n, float* __restrict__ out) {
+    const int64_t n = *d_n;
+    for (int e = threadIdx.x; e < 6 * kMaxKc; e += 256) {
+        const int d = e / kMaxKc, j = e % kMaxKc;
+        out[e] = j < n ? pairs[d * cap + j] : 0.f;
+    }
+}
+
+// The pairs after this window: the next ranks' heads (their first min(n_r, kMaxKc) pairs) in rank order, up to
+// kMaxKc of them, appended at pairs[n ..]; the first kPclTinyN pairs of the whole order -> ghead (column-major,
+// kPclTinyN per column: the lazy product's inputs when the whole count is below 14, every pair then a head).
+// One block; the message of rank r (its element count at word 0, the seqsum header) at recv + r * stride.
+__global__ void __launch_bounds__(256) pcl_heads_merge_kernel(float* __restrict__ pairs, int64_t cap,
+                                                              const uint32_t* __restrict__ d_n, const double* __restrict__ recv,
+                                                              int64_t stride, int64_t heads_off, int rank, int world,
+                                                              float* __restrict__ ghead) {
+    const int64_t n = *d_n;
+    int64_t got = 0;
+    for (int r = rank + 1; r < world && got < kMaxKc; ++r) {  // block-uniform
+        const double* m = recv + (size_t)r * (size_t)stride;
+        const int64_t nr = (int64_t)__double_as_longlong(m[0]);
+        const int64_t take = min(min(nr, (int64_t)kMaxKc), kMaxKc - got);
+        const float* h = reinterpret_cast<const float*>(m + heads_off);
+        for (int64_t e = threadIdx.x; e < 6 * take; e += 256) {
+            const int d = (int)(e / take);
+            const int64_t j = e % take;
+            pairs[d * cap + n + got + j] = h[d * kMaxKc + j];
+        }
+        got += take;
+    }
+    int64_t g = 0;
+    for (int r = 0; r < world && g < kPclTinyN; ++r) {
+        const double* m = recv + (size_t)r * (size_t)stride;
+        const int64_t nr = (int64_t)__double_as_longlong(m[0]);
+        const int64_t take = min(min(nr, (int64_t)kMaxKc), (int64_t)kPclTinyN - g);
+        const float* h = reinterpret_cast<const float*>(m + heads_off);
+        for (int64_t e = threadIdx.x; e < 6 * take; e += 256) {
+            const int d = (int)(e / take);
+            const int64_t j = e % take;
+            ghead[d * kPclTinyN + g + j] = h[d * kMaxKc + j];
+        }
+        g += take;
+    }
+}
+
+// depth blocks [q0, q1) of the whole chain (q0 = the first block starting in this window), each summed as in
+// pcl_sigma_blocks_kernel from the window's pairs and the ones appended after it; the results (9 floats per
+// block) and the header (the ranks' statuses, q0, the block count) into the message
+__global__ void __launch_bounds__(64) pcl_sigma_shard_kernel(const float* __restrict__ pairs, int64_t cap,
+                                                             const uint32_t* __restrict__ d_n, const SeqShard* __restrict__ sh,
+                                                             const float* __restrict__ sums6, int l1,
+                                                             const uint32_t* __restrict__ st_means,
+                                                             const uint32_t* __restrict__ lb_flag, double* __restrict__ msg,
+                                                             int64_t nq_slot) {
+    __shared__ float s[6][kMaxKc];
+    const int64_t nl = *d_n, gb = sh->gbase, n = sh->n_global;
+    const int lane = threadIdx.x;
+    const bool blocked = n + 6 >= 20;  // below: the lazy product (pcl_pack)
+    const int64_t kc = blocked ? eigen_gemm_kc(n, l1) : 1;
+    const int64_t q0 = blocked ? (gb + kc - 1) / kc : 0, q1 = blocked ? (gb + nl + kc - 1) / kc : 0;
+    if (blockIdx.x == 0 && lane == 0) {
+        msg[0] = (double)(st_means[0] & 0x3fu);  // this rank's verification failures
+        msg[1] = 0.0;
+        msg[2] = (double)(lb_flag ? *lb_flag : 0u);
+        msg[3] = (double)q0;
+        msg[4] = (double)min(q1 - q0, nq_slot);
+        msg[5] = (double)(q1 - q0 > nq_slot ? 1 : 0);  // more blocks than the slot (never with pcl_blocks_slot)
+    }
+    if (!blocked || nl == 0) return;
+    float* Cb = reinterpret_cast<float*>(msg + kPclX3Hdr);
+    const float oon = 1.f / (float)n;
+    const int r = lane / 3, c = lane % 3;
+    const float dm = lane < 9 ? sums6[3 + r] * oon : 0.f;
+    const float sm = lane < 9 ? sums6[c] * oon : 0.f;
+    for (int64_t q = q0 + blockIdx.x; q < min(q1, q0 + nq_slot); q += gridDim.x) {
+        const int64_t k0 = q * kc - gb;  // in the window's pairs (the tail of the last block: the appended ones)
+        const int cnt = (int)(n - q * kc < kc ? n - q * kc : kc);
+        {
+            constexpr int T = (kMaxKc + 63) / 64;
+            float v[6][T];
+#pragma unroll
+            for (int d = 0; d < 6; ++d)
+#pragma unroll
+                for (int t = 0; t < T; ++t) {
+                    const int j = t * 64 + lane;
+                    v[d][t] = j < cnt ? pairs[d * cap + k0 + j] : 0.f;
+                }
+#pragma unroll
+            for (int d = 0; d < 6; ++d)
+#pragma unroll
+                for (int t = 0; t < T; ++t)
+                    if (t * 64 + lane < cnt) s[d][t * 64 + lane] = v[d][t];
+        }
+        __syncthreads();
+        if (lane < 9) {
+            const float* dv = s[3 + r];
+            const float* sv = s[c];
+            float C0 = 0.f;
+            int j = 0;
+            for (; j + 8 <= cnt; j += 8) {
+                float pp[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) pp[u] = (dv[j + u] - dm) * (sv[j + u] - sm);
+#pragma unroll
+                for (int u = 0; u < 8; ++u) C0 += pp[u];
+            }
+            for (; j < cnt; ++j) C0 += (dv[j] - dm) * (sv[j] - sm);
+            Cb[(q - q0) * 9 + lane] = C0;
+        }
+        __syncthreads();
+    }
+}
+
+// order 1: the header only (no depth blocks), the sigma chains' statuses beside the means'
+__global__ void pcl_x3_header_kernel(const uint32_t* __restrict__ st_means, const uint32_t* __restrict__ st_sig,
+                                     const uint32_t* __restrict__ lb_flag, double* __restrict__ msg) {
+    msg[0] = (double)(st_means[0] & 0x3fu);
+    msg[1] = (double)(st_sig ? st_sig[0] & 0x1ffu : 0u);
+    msg[2] = (double)(lb_flag ? *lb_flag : 0u);
+    msg[3] = 0.0;
+    msg[4] = 0.0;
+    msg[5] = 0.0;
+}
+
+// every rank's depth blocks into Cbg (global order), the statuses OR-ed: merged = {means bad, means overflow,
+// sigma bad, sigma overflow, look-back}; the overflow words are the seqsum merges' (already global); out[20..22]
+__global__ void __launch_bounds__(256) pcl_x3_merge_kernel(const double* __restrict__ recv, int64_t stride, int world,
+                                                           float* __restrict__ Cbg, int64_t Cbg_cap,
+                                                           const uint32_t* __restrict__ over_means,
+                                                           const uint32_t* __restrict__ over_sig,
+                                                           const SeqShard* __restrict__ shm, const SeqShard* __restrict__ shs,
+                                                           uint32_t* __restrict__ merged, float* __restrict__ out) {
+    __shared__ uint32_t s_or[4];
+    if (threadIdx.x < 4) s_or[threadIdx.x] = 0u;
+    __syncthreads();
+    for (int r = 0; r < world; ++r) {
+        const double* m = recv + (size_t)r * (size_t)stride;
+        if (threadIdx.x == 0) {
+            s_or[0] |= (uint32_t)m[0];
+            s_or[1] |= (uint32_t)m[1];
+            s_or[2] |= (uint32_t)m[2];
+            s_or[3] |= (uint32_t)m[5];
+        }
+        const int64_t q0 = (int64_t)m[3], nq = (int64_t)m[4];
+        const float* cb = reinterpret_cast<const float*>(m + kPclX3Hdr);
+        for (int64_t e = threadIdx.x; e < 9 * nq; e += 256)
+            if (q0 * 9 + e < 9 * Cbg_cap) Cbg[q0 * 9 + e] = cb[e];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        merged[0] = s_or[0];
+        merged[1] = over_means[1] | (s_or[3] ? 0x3fu : 0u);
+        merged[2] = s_or[1];
+        merged[3] = over_sig ? over_sig[1] : 0u;
+        merged[4] = s_or[2];
+        const uint32_t xf = (shm ? shm->xflags : 0u) | (shs ? shs->xflags << 8 : 0u) | (s_or[3] ? 4u : 0u);
+        out[20] = __uint_as_float(xf);
+        out[21] = __int_as_float(shm ? shm->max_nev : 0);
+        out[22] = __int_as_float(shs ? shs->max_nev : 0);
+    }
+}
+
+__global__ void __launch_bounds__(256) pcl_gather_pack_kernel(const float* __restrict__ pairs, int64_t cap,
+                                                              const uint32_t* __restrict__ d_n, int64_t round, int64_t chunk,
+                                                              double* __restrict__ msg) {
+    const int64_t n = *d_n;
+    if (blockIdx.x == 0 && threadIdx.x == 0) msg[0] = (double)n;
+    float* out = reinterpret_cast<float*>(msg + 2);
+    const int64_t b = round * chunk;
+    for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < 6 * chunk; e += (int64_t)gridDim.x * 256) {
+        const int d = (int)(e / chunk);
+        const int64_t j = e % chunk;
+        out[e] = b + j < n ? pairs[d * cap + b + j] : 0.f;
+    }
+}
+
+__global__ void __launch_bounds__(256) pcl_gather_unpack_kernel(const double* __restrict__ recv, int64_t stride, int world,
+                                                                int64_t round, int64_t chunk, float* __restrict__ pairs,
+                                                                int64_t cap, uint32_t* __restrict__ n_all) {
+    int64_t base = 0;
+    for (int r = 0; r < world; ++r) {  // block-uniform
+        const double* m = recv + (size_t)r * (size_t)stride;
+        const int64_t nr = (int64_t)m[0];
+        const int64_t b = round * chunk, take = max((int64_t)0, min(chunk, nr - b));
+        const float* in = reinterpret_cast<const float*>(m + 2);
+        for (int64_t e = blockIdx.x * 256 + threadIdx.x; e < 6 * take; e += (int64_t)gridDim.x * 256) {
+            const int d = (int)(e / take);
+            const int64_t j = e % take;
+            if (base + b + j < cap) pairs[d * cap + base + b + j] = in[d * chunk + j];
+        }
+        base += nr;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) *n_all = (uint32_t)base;
+}
+
 }  // namespace
+
+int pcl_reserve_plain(PclBuf& p, int64_t n, hipStream_t st) {
+    n = n < 1 ? 1 : n;
+    if (n > p.cap) {
+        n = std::max<int64_t>(n + n / 2, 2 * p.cap);
+        count_alloc(2);
+        for (void* q : {(void*)p.pairs, (void*)p.Cb})
+            if (q) (void)hipFree(q);
+        p.pairs = nullptr;
+        p.Cb = nullptr;
+        p.cap = 0;
+        if (hipMalloc(&p.pairs, (size_t)n * 6 * sizeof(float)) != hipSuccess ||
+            hipMalloc(&p.Cb, (size_t)(n / 340 + 2) * 9 * sizeof(float)) != hipSuccess)
+            return -5;
+        p.cap = n;
+    }
+    if (!p.small) {
+        count_alloc();
+        if (hipMalloc(&p.small, 64 * sizeof(float)) != hipSuccess) return -5;
+        (void)hipMemsetAsync(p.small, 0, 64 * sizeof(float), st);
+    }
+    return 0;
+}
+
+int pcl_shard_reserve(PclBuf& p, int64_t n_blocks_global, hipStream_t st) {
+    if (!p.ghead || !p.merged) {
+        count_alloc(2);
+        if (hipMalloc(&p.ghead, 6 * kPclTinyN * sizeof(float)) != hipSuccess ||
+            hipMalloc(&p.merged, kPclMerged * sizeof(uint32_t)) != hipSuccess)
+            return -5;
+        (void)hipMemsetAsync(p.merged, 0, kPclMerged * sizeof(uint32_t), st);
+    }
+    if (n_blocks_global > p.Cbg_cap) {
+        const int64_t c = std::max<int64_t>(n_blocks_global + n_blocks_global / 2, 2 * p.Cbg_cap);
+        if (p.Cbg) (void)hipFree(p.Cbg);
+        p.Cbg = nullptr;
+        p.Cbg_cap = 0;
+        count_alloc();
+        if (hipMalloc(&p.Cbg, (size_t)c * 9 * sizeof(float)) != hipSuccess) return -5;
+        p.Cbg_cap = c;
+    }
+    return 0;
+}
+
+void launch_pcl_shard_heads(PclBuf& p, double* msg_heads, hipStream_t st) {
+    pcl_heads_kernel<<<1, 256, 0, st>>>(p.pairs, p.cap, p.small + kPclN, reinterpret_cast<float*>(msg_heads));
+}
+
+void launch_pcl_shard_heads_merge(PclBuf& p, const double* recv, int64_t stride, int64_t heads_off, int rank, int world,
+                                  hipStream_t st) {
+    pcl_heads_merge_kernel<<<1, 256, 0, st>>>(p.pairs, p.cap, p.small + kPclN, recv, stride, heads_off, rank, world,
+                                              p.ghead);
+}
+
+void launch_pcl_sigma_shard(PclBuf& p, int order, double* msg3, int64_t nq_slot, hipStream_t st) {
+    const uint32_t* lb = p.small + kPclTicket + 1;
+    if (order == 1) {
+        pcl_x3_header_kernel<<<1, 1, 0, st>>>(p.means.status, p.sig.status, lb, msg3);
+        return;
+    }
+    const int64_t grid = std::max<int64_t>(1, std::min<int64_t>(nq_slot, 4096));
+    pcl_sigma_shard_kernel<<<(int)grid, 64, 0, st>>>(p.pairs, p.cap, p.small + kPclN, p.means.sh, p.means.result,
+                                                     pcl_l1(order), p.means.status, lb, msg3, nq_slot);
+}
+
+void launch_pcl_x3_merge(PclBuf& p, int order, const double* recv, int64_t stride, int world, int64_t nq_slot,
+                         float* out, hipStream_t st) {
+    (void)nq_slot;
+    pcl_x3_merge_kernel<<<1, 256, 0, st>>>(recv, stride, world, p.Cbg, p.Cbg_cap, p.means.status,
+                                           order == 1 ? p.sig.status : nullptr, p.means.sh,
+                                           order == 1 ? p.sig.sh : nullptr, p.merged, out);
+}
+
+void launch_pcl_pack_shard(PclBuf& p, int order, float* out, hipStream_t st) {
+    pcl_pack_kernel<<<1, kPackThreads, 0, st>>>(p.ghead, kPclTinyN, p.n_all, p.means.result,
+                                                order == 1 ? p.sig.result : p.means.result, p.Cbg, order, pcl_l1(order),
+                                                p.merged, p.merged + 2, p.means.floor_e + p.means.nch, p.merged + 4, out);
+}
+
+void launch_pcl_mean6(PclBuf& p, const float* sums6, hipStream_t st) {
+    pcl_mean6_kernel<<<1, 64, 0, st>>>(sums6, p.n_all ? p.n_all : p.small + kPclN,
+                                       reinterpret_cast<float*>(p.small + kPclMean6));
+}
+
+void launch_pcl_gather_pack(const PclBuf& p, const uint32_t* d_n, int64_t round, int64_t chunk, double* msg, hipStream_t st) {
+    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((6 * chunk + 255) / 256, 1024));
+    pcl_gather_pack_kernel<<<(int)nb, 256, 0, st>>>(p.pairs, p.cap, d_n, round, chunk, msg);
+}
+
+void launch_pcl_gather_unpack(PclBuf& g, const double* recv, int64_t stride, int world, int64_t round, int64_t chunk,
+                              hipStream_t st) {
+    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>((6 * chunk + 255) / 256, 1024));
+    pcl_gather_unpack_kernel<<<(int)nb, 256, 0, st>>>(recv, stride, world, round, chunk, g.pairs, g.cap, g.small + kPclN);
+}
 
 int pcl_reserve(PclBuf& p, int64_t n, int order, hipStream_t st) {
     n = n < 1 ? 1 : n;
@@ -291,7 +583,7 @@ int pcl_reserve(PclBuf& p, int64_t n, int order, hipStream_t st) {
 }
 
 void pcl_free(PclBuf& p) {
-    void* ptrs[] = {p.pairs, p.bst, p.Cb, p.small};
+    void* ptrs[] = {p.pairs, p.bst, p.Cb, p.small, p.ghead, p.Cbg, p.merged};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     seqsum_free(p.means);

@@ -180,9 +180,11 @@ __device__ __forceinline__ void predict(const Src& src, const SeqSumBuf& b, int 
         const float* rc = b.recon + (size_t)c * b.nmax;
 #pragma unroll
         for (int i = 0; i < kSeqPer; ++i) in.e[i] = k0 + i < n ? binade_pred(rc[k0 + i], kPredSlack2) : kSpecial;
-        in.ep = k0 > 0 ? binade_pred(rc[k0 - 1], kPredSlack2) : kSpecial;
+        // a window's first element: its predecessor lives on the previous rank (the last verification's s)
+        in.ep = k0 > 0 ? binade_pred(rc[k0 - 1], kPredSlack2)
+                       : (b.sh && b.sh->gbase > 0 ? binade_pred(b.sh->prev_s[c], kPredSlack2) : kSpecial);
     }
-    if (k0 == 0) in.e[0] = binade_f(in.x[0]);  // s_0 = x_0 exactly
+    if (k0 == 0 && (!b.sh || b.sh->gbase == 0)) in.e[0] = binade_f(in.x[0]);  // s_0 = x_0 exactly
 }
 
 // per element: event flag and increment (element 0: the start, neither)
@@ -192,12 +194,13 @@ __device__ __forceinline__ void classify(const SeqSumBuf& b, int c, int64_t n, c
     const bool noinc = b.dbg_noinc && pass <= 1;
     const int64_t k0 = (int64_t)blockIdx.x * kSeqBlock + (int64_t)threadIdx.x * kSeqPer;
     const uint32_t* fb = b.forced ? b.forced + (size_t)c * (b.nmax / 32 + 1) : nullptr;
+    const int64_t gb = b.sh ? b.sh->gbase : 0;  // global index of local element 0 (sharded windows)
 #pragma unroll
     for (int i = 0; i < kSeqPer; ++i) {
         const int64_t k = k0 + i;
         ev[i] = false;
         inc[i] = 0;
-        if (k == 0 || k >= n) continue;
+        if (gb + k == 0 || k >= n) continue;  // the chain's start: neither event nor increment
         const int ep = i == 0 ? in.ep : in.e[i - 1];
         ev[i] = seq_event(in.x[i], in.e[i], ep, floor_e, forced_bit(fb, k), noinc, inc[i]);
     }
@@ -250,8 +253,10 @@ __global__ void __launch_bounds__(256) seq_scan1(SeqSumBuf b, const uint32_t* d_
     const int c = blockIdx.x;
     const int64_t n = *d_n;
     const int nb = (int)((n + kSeqBlock - 1) / kSeqBlock);
-    double off = 0.0, mb = 0.0;  // the offsets carried over windows (every thread's copy); this thread's max
-    double var = 0.0;            // every thread's copy of the allowance's running variance
+    // the offsets carried over windows (every thread's copy); this thread's max; every thread's copy of the
+    // allowance's running variance — a sharded window starts from the ranks before it (seq_shard_offsets)
+    double off = b.sh ? b.sh->off0[c] : 0.0, mb = 0.0;
+    double var = b.sh ? b.sh->var0[c] : 0.0;
     constexpr int kPerT = kScanWin / 256;
     for (int w0 = 0; w0 < nb; w0 += kScanWin) {
         const int m = min(kScanWin, nb - w0);
@@ -325,7 +330,8 @@ __global__ void __launch_bounds__(256) seq_scan1(SeqSumBuf b, const uint32_t* d_
     if (threadIdx.x == 0) {
         // |s_k| < 2^(ilogb(mb) + 2) with a binade of margin for the float chain's own drift; a run's sum
         // then has <= 53 significant bits when its binades stay >= floor
-        b.floor_e[c] = mb > 0.0 ? ilogb(mb) - 27 : -200;
+        // (sharded: the floor every rank computed from all ranks' totals, so the fixed-point unit is common)
+        b.floor_e[c] = b.sh ? b.sh->floor_e[c] : (mb > 0.0 ? ilogb(mb) - 27 : -200);
         if (c == 0 && pass <= 1) {
             b.status[0] = 0u;
             b.status[1] = 0u;
@@ -436,14 +442,19 @@ __global__ void __launch_bounds__(kSeqThreads) seq_events(Src src, SeqSumBuf b, 
     int Ein[kSeqPer];
     block_scan_elems(src, b, c, n, pass, in, ev, Pex, Ein);
     const int64_t k0 = (int64_t)blockIdx.x * kSeqBlock + (int64_t)threadIdx.x * kSeqPer;
+    // single rank: the walk's lists; sharded: this window's lists (local positions and prefixes, seq_shard_pack)
+    int* EPOS = b.sh ? b.lev_pos : b.ev_pos;
+    uint64_t* EPP = b.sh ? b.lev_P : b.ev_P;
+    float* EXX = b.sh ? b.lev_x : b.ev_x;
+    const int64_t es = b.sh ? b.evcap : b.evs;
 #pragma unroll
     for (int i = 0; i < kSeqPer; ++i)
         if (ev[i]) {
             const int idx = Ein[i] - 1;
             if (idx < b.evcap) {
-                b.ev_pos[(size_t)c * b.evcap + idx] = (int)(k0 + i);
-                b.ev_P[(size_t)c * b.evcap + idx] = Pex[i];
-                b.ev_x[(size_t)c * b.evcap + idx] = in.x[i];
+                EPOS[(size_t)c * es + idx] = (int)(k0 + i);
+                EPP[(size_t)c * es + idx] = Pex[i];
+                EXX[(size_t)c * es + idx] = in.x[i];
             }
         }
 }
@@ -501,7 +512,7 @@ __global__ void __launch_bounds__(kWalkThreads) seq_walk(Src src, SeqSumBuf b, c
     __shared__ WalkChunk wb[2];
     const int c = blockIdx.x;
     const int t = threadIdx.x, w = t >> 6;
-    const int64_t n = *d_n;
+    const int64_t n = b.sh ? b.sh->n_global : *d_n;  // sharded: every rank walks the whole chain's events
     if (n <= 0) {
         if (t == 0) b.result[c] = 0.f;
         return;
@@ -509,11 +520,11 @@ __global__ void __launch_bounds__(kWalkThreads) seq_walk(Src src, SeqSumBuf b, c
     if ((b.status[1] >> c) & 1u) return;  // event overflow: the caller falls back
     const int nev = b.floor_e[b.nch + c];
     const double unit = ldexp(1.0, b.floor_e[c] - 23);
-    const uint64_t* EP = b.ev_P + (size_t)c * b.evcap;
-    const float* EX = b.ev_x + (size_t)c * b.evcap;
-    float* ES = b.ev_s + (size_t)c * b.evcap;
+    const uint64_t* EP = b.ev_P + (size_t)c * b.evs;
+    const float* EX = b.ev_x + (size_t)c * b.evs;
+    float* ES = b.ev_s + (size_t)c * b.evs;
     const int nchunk = (nev + kWalkChunk - 1) / kWalkChunk;
-    float s = src(c, 0);  // the chain (lane 0 of wave 0)
+    float s = b.sh ? b.sh->x0[c] : src(c, 0);  // the chain (lane 0 of wave 0)
     if (nchunk > 0) walk_prepare(wb[0], 0, nev, unit, EP, EX, t, kWalkThreads);
     __syncthreads();
     for (int k = 0; k < nchunk; ++k) {
@@ -598,9 +609,10 @@ __global__ void __launch_bounds__(kSeqThreads) seq_verify(Src src, SeqSumBuf b, 
     int Ein[kSeqPer];
     block_scan_elems(src, b, c, n, pass, in, ev, Pex, Ein);
     const double unit = ldexp(1.0, b.floor_e[c] - 23);
-    const uint64_t* EP = b.ev_P + (size_t)c * b.evcap;
-    const float* ES = b.ev_s + (size_t)c * b.evcap;
-    const float x0 = src(c, 0);
+    const uint64_t* EP = b.ev_P + (size_t)c * b.evs;
+    const float* ES = b.ev_s + (size_t)c * b.evs;
+    const float x0 = b.sh ? b.sh->x0[c] : src(c, 0);
+    const int64_t gb = b.sh ? b.sh->gbase : 0;  // sharded: event positions are global, k0 local
     const int64_t k0 = (int64_t)blockIdx.x * kSeqBlock + (int64_t)threadIdx.x * kSeqPer;
     // s of element k from (inclusive event count E, inclusive increment prefix P, is-event)
     auto rebuild = [&](bool is_ev, int E, uint64_t Pin) -> float {
@@ -619,7 +631,7 @@ __global__ void __launch_bounds__(kSeqThreads) seq_verify(Src src, SeqSumBuf b, 
 #pragma unroll
         for (int i = 0; i < kSeqPer; ++i) {
             const int64_t k = k0 + i;
-            s[i] = k == 0 ? x0 : (k < n ? rebuild(ev[i], Ein[i], Pex[i] + inc2[i]) : 0.f);
+            s[i] = gb + k == 0 ? x0 : (k < n ? rebuild(ev[i], Ein[i], Pex[i] + inc2[i]) : 0.f);
         }
     }
     // predecessor of the thread's first element
@@ -630,13 +642,15 @@ __global__ void __launch_bounds__(kSeqThreads) seq_verify(Src src, SeqSumBuf b, 
     if (lane == 0) {
         if (w > 0) {
             prev = s_lastv[w - 1];
-        } else if (k0 > 0) {
-            // the previous block's last element: bEoff / bPoff of this block are its inclusive values; whether
-            // it is an event is read back from the event list (position)
+        } else if (gb + k0 > 0) {
+            // the previous block's last element (a window's first block: the previous rank's last): bEoff / bPoff
+            // of this block are its inclusive values (global once seq_shard_merge has added the ranks before);
+            // whether it is an event is read back from the event list (global position)
             const int E = b.bEoff[(size_t)c * b.nblk + blockIdx.x];
             const uint64_t Pin = b.bPoff[(size_t)c * b.nblk + blockIdx.x];
-            const bool is_ev = E > 0 && b.ev_pos[(size_t)c * b.evcap + (E - 1)] == (int)(k0 - 1);
+            const bool is_ev = E > 0 && b.ev_pos[(size_t)c * b.evs + (E - 1)] == (int)(gb + k0 - 1);
             prev = rebuild(is_ev, E, Pin);
+            if (k0 == 0) b.sh->prev_s[c] = prev;  // (k0 == 0 here only when sharded) the next pass's prediction
         }
     }
     bool bad = false;
@@ -645,7 +659,7 @@ __global__ void __launch_bounds__(kSeqThreads) seq_verify(Src src, SeqSumBuf b, 
         const int64_t k = k0 + i;
         if (k >= n) break;
         const float sp = i == 0 ? prev : s[i - 1];
-        if (k > 0) {
+        if (gb + k > 0) {
             const float want = sp + in.x[i];
             if (__float_as_uint(want) != __float_as_uint(s[i]) && !(want != want && s[i] != s[i])) {
                 bad = true;
@@ -660,8 +674,126 @@ __global__ void __launch_bounds__(kSeqThreads) seq_verify(Src src, SeqSumBuf b, 
     if (threadIdx.x == 0 && s_bad) atomicOr(&b.status[0], 1u << c);
 }
 
+// ---------------------------------------------------------------- sharded chains (lio_seqsum.hpp)
+// The window's block sums for the other ranks: [0] its element count, then per chain its blocks' (double sum,
+// sum |x|) (seq_bsum's, in block order; nb_slot per chain)
+__global__ void __launch_bounds__(256) seq_shard_totals(SeqSumBuf b, const uint32_t* d_n, double* __restrict__ out,
+                                                        int64_t nb_slot) {
+    const int c = blockIdx.x;
+    const int64_t n = *d_n;
+    const int nb = (int)((n + kSeqBlock - 1) / kSeqBlock);
+    double* o = out + kSeqTotHdr + (size_t)c * 2 * nb_slot;
+    for (int j = threadIdx.x; j < nb && j < nb_slot; j += 256) {
+        o[2 * j] = b.bsum[(size_t)c * b.nblk + j];
+        o[2 * j + 1] = b.babs[(size_t)c * b.nblk + j];
+    }
+    if (c == 0 && threadIdx.x == 0) out[0] = (double)n;
+}
+
+// every window's place in the chains (seq_shard_offsets_chain, lio_seqsum.hpp) for this rank's window
+__global__ void __launch_bounds__(64) seq_shard_offsets(SeqSumBuf b, int nch, const double* __restrict__ recv,
+                                                        int64_t stride, int64_t nb_slot, int rank, int world) {
+    const int c = threadIdx.x;
+    if (c >= nch) return;
+    SeqShard* sh = b.sh;
+    double off0, var0;
+    int fl;
+    int64_t gb, ng;
+    seq_shard_offsets_chain(recv, stride, nb_slot, rank, world, c, off0, var0, fl, gb, ng);
+    sh->off0[c] = off0;
+    sh->var0[c] = var0;
+    sh->floor_e[c] = fl;
+    if (c == 0) {
+        sh->gbase = gb;
+        sh->n_global = ng;
+        sh->n32 = (uint32_t)ng;
+    }
+}
+
+// The window's event lists for the other ranks (kSeqHdrWords + nch * 2 * slot doubles): n, the overflow bits of
+// its own lists, per chain the increment total, the event count and the first element, then per chain `slot`
+// events (the increment prefix; the position and the value packed in one word).  A list longer than the slot
+// travels cut: every rank sees its count and seq_shard_merge flags it.  One block per chain.
+template <class Src>
+__global__ void __launch_bounds__(256) seq_shard_pack(Src src, SeqSumBuf b, const uint32_t* d_n, double* __restrict__ msg,
+                                                      int slot) {
+    const int c = blockIdx.x;
+    const int64_t n = *d_n;
+    const int nev = b.floor_e[b.nch + c];  // this window's events (seq_scan2)
+    if (threadIdx.x == 0) {
+        if (c == 0) {
+            msg[0] = __longlong_as_double((long long)n);
+            msg[1] = __longlong_as_double((long long)b.status[1]);
+            b.sh->max_nev = 0;  // seq_shard_merge's outputs for this exchange
+            b.sh->xflags = 0u;
+        }
+        msg[2 + c] = __longlong_as_double((long long)b.ptot[c]);
+        msg[2 + kSeqMaxChains + c] = __longlong_as_double((long long)nev);
+        msg[2 + 2 * kSeqMaxChains + c] = n > 0 ? (double)src(c, 0) : 0.0;
+    }
+    const int m = min(min(nev, slot), (int)b.evcap);
+    double* ev = msg + kSeqHdrWords + (size_t)c * 2 * slot;
+    for (int j = threadIdx.x; j < m; j += 256) {
+        const size_t i = (size_t)c * b.evcap + j;
+        ev[2 * j] = __longlong_as_double((long long)b.lev_P[i]);
+        const uint64_t w = (uint64_t)(uint32_t)b.lev_pos[i] | ((uint64_t)__float_as_uint(b.lev_x[i]) << 32);
+        ev[2 * j + 1] = __longlong_as_double((long long)w);
+    }
+}
+
+// Every rank's event lists (rank r's message at recv + r * stride) -> the chain's global lists in element order:
+// rank r's events move by the elements and the increments of the ranks before it; this window's block offsets
+// become global the same way, the chain's total increment and event count and its first element are set.  A
+// rank's list longer than the slot, an overflow of its own list or more events than the global lists hold sets
+// the chain's overflow bit (the walk and the verification skip it; the caller re-exchanges or falls back).
+// One block per chain.
+__global__ void __launch_bounds__(256) seq_shard_merge(SeqSumBuf b, const uint32_t* d_n, const double* __restrict__ recv,
+                                                       int64_t stride, int rank, int world, int slot) {
+    __shared__ int s_eoff[65];
+    __shared__ uint64_t s_poff[65];
+    __shared__ int64_t s_pos[65];
+    __shared__ int s_bad;
+    const int c = blockIdx.x;
+    SeqShard* sh = b.sh;
+    if (threadIdx.x == 0) {
+        float x0;
+        int mx;
+        const int bad = seq_shard_merge_chain(recv, stride, world, slot, c, b.evs, s_eoff, s_poff, s_pos, x0, mx);
+        s_bad = bad;
+        b.floor_e[b.nch + c] = s_eoff[world];
+        b.ptot[c] = s_poff[world];
+        sh->x0[c] = x0;
+        atomicMax(&sh->max_nev, mx);
+        if (bad) {
+            atomicOr(&b.status[1], 1u << c);
+            atomicOr(&sh->xflags, (bad & 2 ? 1u : 0u) | (bad & 5 ? 2u : 0u));
+        }
+    }
+    __syncthreads();
+    if (s_bad) return;
+    for (int r = 0; r < world; ++r) {
+        const double* ev = recv + (size_t)r * (size_t)stride + kSeqHdrWords + (size_t)c * 2 * slot;
+        const int ner = s_eoff[r + 1] - s_eoff[r];
+        for (int j = threadIdx.x; j < ner; j += 256) {
+            const size_t d = (size_t)c * b.evs + s_eoff[r] + j;
+            const uint64_t w = (uint64_t)__double_as_longlong(ev[2 * j + 1]);
+            b.ev_P[d] = s_poff[r] + (uint64_t)__double_as_longlong(ev[2 * j]);
+            b.ev_pos[d] = (int)(s_pos[r] + (int64_t)(uint32_t)w);
+            b.ev_x[d] = __uint_as_float((uint32_t)(w >> 32));
+        }
+    }
+    // this window's block offsets: global (its rank's place in the lists)
+    const int64_t n = *d_n;
+    const int nb = (int)((n + kSeqBlock - 1) / kSeqBlock);
+    for (int j = threadIdx.x; j < nb; j += 256) {
+        b.bEoff[(size_t)c * b.nblk + j] += s_eoff[rank];
+        b.bPoff[(size_t)c * b.nblk + j] += s_poff[rank];
+    }
+}
+
 template <class Src>
 void seqsum_launch_impl(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, hipStream_t st) {
+    b.evs = b.evcap;  // single rank: the walk reads the lists seq_events writes
     const dim3 g(b.nblk, nch);
     if (pass <= 1) {
         // the forced-event bits of a previous alignment's failures are stale (none were set unless a re-pass ran)
@@ -691,6 +823,83 @@ void seqsum_launch(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, i
 template void seqsum_launch<SeqPairs>(const SeqPairs&, int, const uint32_t*, SeqSumBuf&, int, hipStream_t);
 template void seqsum_launch<SeqSigma>(const SeqSigma&, int, const uint32_t*, SeqSumBuf&, int, hipStream_t);
 
+// sharded pass 1, before the totals exchange: the stale forced bits cleared, the window's block sums, its totals
+template <class Src>
+void seqsum_shard_head(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, double* tot_out, int64_t nb_slot,
+                       hipStream_t st) {
+    const dim3 g(b.nblk, nch);
+    if (b.forced_dirty) {
+        (void)hipMemsetAsync(b.forced, 0, (size_t)nch * (b.nmax / 32 + 1) * sizeof(uint32_t), st);
+        b.forced_dirty = false;
+    }
+    seq_bsum<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n);
+    seq_shard_totals<<<nch, 256, 0, st>>>(b, d_n, tot_out, nb_slot);
+}
+
+// after the totals exchange (pass 1) or straight away (pass > 1): offsets, counts, local events, the message
+template <class Src>
+void seqsum_shard_mid(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, const double* tot_recv,
+                      int64_t tot_stride, int64_t nb_slot, int rank, int world, double* msg_out, int slot, hipStream_t st) {
+    const dim3 g(b.nblk, nch);
+    if (pass <= 1) {
+        seq_shard_offsets<<<1, 64, 0, st>>>(b, nch, tot_recv, tot_stride, nb_slot, rank, world);
+        seq_scan1<<<nch, 256, 0, st>>>(b, d_n, pass);
+    } else {
+        b.forced_dirty = true;  // the failures that led here set forced bits
+        (void)hipMemsetAsync(b.status, 0, 2 * sizeof(uint32_t), st);
+    }
+    seq_count<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
+    seq_scan2<<<nch, kSeqThreads, 0, st>>>(b, d_n);
+    seq_events<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
+    seq_shard_pack<Src><<<nch, 256, 0, st>>>(src, b, d_n, msg_out, slot);
+}
+
+// after the event exchange: the global lists, the walk over all of them, the window's verification
+template <class Src>
+void seqsum_shard_tail(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, const double* msg_recv,
+                       int64_t msg_stride, int rank, int world, int slot, hipStream_t st) {
+    const dim3 g(b.nblk, nch);
+    seq_shard_merge<<<nch, 256, 0, st>>>(b, d_n, msg_recv, msg_stride, rank, world, slot);
+    seq_walk<Src><<<nch, kWalkThreads, 0, st>>>(src, b, d_n);
+    seq_verify<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
+}
+
+template <class Src>
+void seqsum_shard_repack(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, double* msg_out, int slot,
+                         hipStream_t st) {
+    seq_shard_pack<Src><<<nch, 256, 0, st>>>(src, b, d_n, msg_out, slot);
+}
+
+#define LIO_SEQ_SHARD_INST(S)                                                                                      \
+    template void seqsum_shard_head<S>(const S&, int, const uint32_t*, SeqSumBuf&, double*, int64_t, hipStream_t); \
+    template void seqsum_shard_mid<S>(const S&, int, const uint32_t*, SeqSumBuf&, int, const double*, int64_t,     \
+                                      int64_t, int, int, double*, int, hipStream_t);                               \
+    template void seqsum_shard_tail<S>(const S&, int, const uint32_t*, SeqSumBuf&, int, const double*, int64_t, int, \
+                                       int, int, hipStream_t);                                                     \
+    template void seqsum_shard_repack<S>(const S&, int, const uint32_t*, SeqSumBuf&, double*, int, hipStream_t);
+LIO_SEQ_SHARD_INST(SeqPairs)
+LIO_SEQ_SHARD_INST(SeqSigma)
+#undef LIO_SEQ_SHARD_INST
+
+int seqsum_shard(SeqSumBuf& b, bool on, hipStream_t st) {
+    if (!on) {
+        b.sh = nullptr;
+        return 0;
+    }
+    if (b.nch < 1) return -1;
+    if (!b.lev_pos) {
+        count_alloc(4);
+        bool ok = hipMalloc(&b.sh, sizeof(SeqShard)) == hipSuccess &&
+                  hipMalloc(&b.lev_pos, (size_t)b.nch * b.evcap_alloc * sizeof(int)) == hipSuccess &&
+                  hipMalloc(&b.lev_P, (size_t)b.nch * b.evcap_alloc * sizeof(uint64_t)) == hipSuccess &&
+                  hipMalloc(&b.lev_x, (size_t)b.nch * b.evcap_alloc * sizeof(float)) == hipSuccess;
+        if (!ok) return -5;
+        (void)hipMemsetAsync(b.sh, 0, sizeof(SeqShard), st);
+    }
+    b.evs = b.evs_alloc;
+    return 0;
+}
+
 int seqsum_reserve(SeqSumBuf& b, int nch, int64_t nmax, hipStream_t st) {
     if (nch > kSeqMaxChains || nch < 1) return -1;
     nmax = nmax < 1 ? 1 : nmax;
@@ -703,6 +912,8 @@ int seqsum_reserve(SeqSumBuf& b, int nch, int64_t nmax, hipStream_t st) {
     b.nblk = (int)((nmax + kSeqBlock - 1) / kSeqBlock);
     count_alloc(18);
     b.evcap = b.evcap_alloc = nmax / 4 + 1024;  // events are ~0.3 % of a C4 chain; past a quarter the serial kernel is as fast
+    b.evs = b.evcap;
+    b.evs_alloc = 2 * b.evcap_alloc;  // the walk's lists: sharded, every rank's events (O(window): 2 x its own)
     const size_t nb = (size_t)nch * b.nblk;
     bool ok = hipMalloc(&b.bsum, nb * sizeof(double)) == hipSuccess && hipMalloc(&b.babs, nb * sizeof(double)) == hipSuccess &&
               hipMalloc(&b.boff, nb * sizeof(double)) == hipSuccess && hipMalloc(&b.bdelta, nb * sizeof(double)) == hipSuccess &&
@@ -710,10 +921,10 @@ int seqsum_reserve(SeqSumBuf& b, int nch, int64_t nmax, hipStream_t st) {
               hipMalloc(&b.bev, nb * sizeof(int)) == hipSuccess && hipMalloc(&b.bPoff, nb * sizeof(uint64_t)) == hipSuccess &&
               hipMalloc(&b.bEoff, nb * sizeof(int)) == hipSuccess && hipMalloc(&b.floor_e, 3 * nch * sizeof(int)) == hipSuccess &&
               hipMalloc(&b.ptot, nch * sizeof(uint64_t)) == hipSuccess &&
-              hipMalloc(&b.ev_pos, (size_t)nch * b.evcap * sizeof(int)) == hipSuccess &&
-              hipMalloc(&b.ev_P, (size_t)nch * b.evcap * sizeof(uint64_t)) == hipSuccess &&
-              hipMalloc(&b.ev_x, (size_t)nch * b.evcap * sizeof(float)) == hipSuccess &&
-              hipMalloc(&b.ev_s, (size_t)nch * b.evcap * sizeof(float)) == hipSuccess &&
+              hipMalloc(&b.ev_pos, (size_t)nch * b.evs_alloc * sizeof(int)) == hipSuccess &&
+              hipMalloc(&b.ev_P, (size_t)nch * b.evs_alloc * sizeof(uint64_t)) == hipSuccess &&
+              hipMalloc(&b.ev_x, (size_t)nch * b.evs_alloc * sizeof(float)) == hipSuccess &&
+              hipMalloc(&b.ev_s, (size_t)nch * b.evs_alloc * sizeof(float)) == hipSuccess &&
               hipMalloc(&b.recon, (size_t)nch * nmax * sizeof(float)) == hipSuccess &&
               hipMalloc(&b.forced, (size_t)nch * (nmax / 32 + 1) * sizeof(uint32_t)) == hipSuccess &&
               hipMalloc(&b.status, 4 * sizeof(uint32_t)) == hipSuccess && hipMalloc(&b.result, nch * sizeof(float)) == hipSuccess;
@@ -726,8 +937,9 @@ int seqsum_reserve(SeqSumBuf& b, int nch, int64_t nmax, hipStream_t st) {
 }
 
 void seqsum_free(SeqSumBuf& b) {
-    void* ptrs[] = {b.bsum, b.babs, b.boff, b.bdelta, b.btot, b.bev, b.bPoff, b.bEoff, b.floor_e, b.ptot, b.ev_pos,
-                    b.ev_P, b.ev_x, b.ev_s, b.recon, b.forced, b.status, b.result};
+    void* ptrs[] = {b.bsum, b.babs, b.boff,   b.bdelta, b.btot,   b.bev,   b.bPoff, b.bEoff, b.floor_e,
+                    b.ptot, b.ev_pos, b.ev_P, b.ev_x, b.ev_s, b.recon, b.forced, b.status, b.result,
+                    b.sh,   b.lev_pos, b.lev_P, b.lev_x};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);
     b = SeqSumBuf{};

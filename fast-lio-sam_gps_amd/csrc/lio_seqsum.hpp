@@ -18,6 +18,14 @@
 //     re-predicts from the reconstruction (pass 2, 3); the caller falls back to the serial kernel after.
 //
 // Chains are supplied by a source functor: value(c, k) of chain c at element k (k < n, n on the device).
+//
+// Sharded (SeqSumBuf::sh != nullptr): the chain's elements are split over ranks in order, this rank holding
+// the window [gbase, gbase + n) (lio_icp_host.cpp, the loop ICP over several GPUs).  Every rank predicts,
+// counts and lists the events of its own window — from the double prefix of the elements before it and a
+// binade floor common to all ranks (seq_shard_totals -> all-gather -> seq_shard_offsets) — the event lists
+// are all-gathered (seq_shard_pack -> all-gather -> seq_shard_merge: global positions and increment prefixes),
+// every rank walks ALL events (the serial floor, redundantly), and verifies its own window.  The result is the
+// sequential chain on every rank, whatever the window split, because the verification covers every element.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -28,6 +36,118 @@ constexpr int kSeqThreads = 256;                 // threads per block
 constexpr int kSeqPer = 4;                       // consecutive elements per thread (8: slower)
 constexpr int kSeqBlock = kSeqThreads * kSeqPer;  // elements per block
 constexpr int kSeqMaxChains = 9;
+
+// one rank's window of sharded chains (device memory; seq_shard_offsets / seq_shard_merge write it)
+struct SeqShard {
+    double off0[kSeqMaxChains];   // double prefix of the elements before the window (pass-1 prediction)
+    double var0[kSeqMaxChains];   // drift-allowance variance accumulated before it
+    int floor_e[kSeqMaxChains];   // the chain's binade floor: the same on every rank
+    float x0[kSeqMaxChains];      // the chain's first element (global element 0)
+    float prev_s[kSeqMaxChains];  // s at global element gbase - 1 (the last verification's; pass > 1 predictions)
+    int64_t gbase;                // global index of local element 0
+    int64_t n_global;             // elements over all ranks
+    uint32_t n32;                 // the same as a 32-bit count (the PCL kernels' d_n of the whole chain)
+    uint32_t xflags;              // exchange: bit 0 an event list longer than the slot, bit 1 global capacity
+    int max_nev;                  // largest per-rank per-chain event count of the last merge
+};
+
+// exchange message layout (doubles): block sums (seq_shard_totals: [0] the window's element count, then per chain
+// `nb_slot` pairs (block double sum, block sum |x|) of its kSeqBlock-element blocks), event lists (seq_shard_pack)
+constexpr int kSeqTotHdr = 8;
+constexpr int kSeqHdrWords = 32;                     // event message header: n, flags, ptot[9], nev[9], x0[9]
+__host__ __device__ inline int64_t seq_tot_words(int nch, int64_t nb_slot) { return kSeqTotHdr + (int64_t)nch * 2 * nb_slot; }
+
+__host__ __device__ inline int64_t seq_bits(double v) {
+    int64_t b;
+    __builtin_memcpy(&b, &v, sizeof(b));
+    return b;
+}
+__host__ __device__ inline double seq_from_bits(int64_t b) {
+    double v;
+    __builtin_memcpy(&v, &b, sizeof(v));
+    return v;
+}
+// half an ulp of a float of magnitude v >= 0 (2^(ilogb(v) - 24); 0 for 0), from the exponent bits
+__host__ __device__ inline double seq_half_ulp_f32(double v) {
+    if (!(v > 0.0)) return 0.0;
+    const int64_t e = ((seq_bits(v) >> 52) & 0x7ff) - 1023;
+    if (e < -990) return 0.0;
+    return seq_from_bits((int64_t)((uint64_t)(e - 24 + 1023) << 52));
+}
+
+// Chain c of the gathered block sums (rank r's message at recv + r * stride, nb_slot blocks per chain) -> this
+// window's starting prefix and drift variance, the chain's common floor, the window's first global index and the
+// chain's length: the formulas of seq_scan1 run over every window's blocks in chain order (offset, bound
+// |offset| + block sum |x|, variance + kSeqBlock (ulp / 2)^2 per block), so a window's predictions are as good as
+// one rank's.  The device (seq_shard_offsets) and the host mirror (lio_seq_shard_offsets) run this same code.
+__host__ __device__ inline void seq_shard_offsets_chain(const double* recv, int64_t stride, int64_t nb_slot, int rank,
+                                                        int world, int c, double& off0, double& var0, int& floor_e,
+                                                        int64_t& gbase, int64_t& n_global) {
+    double off = 0.0, var = 0.0, mb = 0.0;
+    int64_t pos = 0;
+    off0 = var0 = 0.0;
+    gbase = 0;
+    for (int r = 0; r < world; ++r) {
+        const double* m = recv + (int64_t)r * stride;
+        const int64_t nr = (int64_t)m[0];
+        if (r == rank) {
+            off0 = off;
+            var0 = var;
+            gbase = pos;
+        }
+        const int64_t nb = (nr + kSeqBlock - 1) / kSeqBlock;
+        const double* bl = m + kSeqTotHdr + (int64_t)c * 2 * nb_slot;
+        for (int64_t j = 0; j < nb && j < nb_slot; ++j) {
+            const double bound = (off < 0.0 ? -off : off) + bl[2 * j + 1];
+            mb = mb > bound ? mb : bound;
+            const double hu = seq_half_ulp_f32(bound);
+            var = var + (double)kSeqBlock * hu * hu;
+            off = off + bl[2 * j];
+        }
+        pos += nr;
+    }
+    floor_e = mb > 0.0 ? ilogb(mb) - 27 : -200;
+    n_global = pos;
+}
+
+// Chain c of the gathered event messages (rank r's at recv + r * stride): every rank's place in the chain's
+// global event lists (eoff, world + 1 entries), in its increments (poff) and in its elements (pos), the chain's
+// first element x0 and the longest list; returns the problems: 1 a rank's own list overflowed, 2 a list is
+// longer than the slot, 4 more events than evs (the device's seq_shard_merge and the host mirror share it).
+__host__ __device__ inline int seq_shard_merge_chain(const double* recv, int64_t stride, int world, int slot, int c,
+                                                     int64_t evs, int* eoff, uint64_t* poff, int64_t* pos, float& x0,
+                                                     int& max_nev) {
+    int e = 0, mx = 0, bad = 0;
+    uint64_t P = 0;
+    int64_t p = 0;
+    bool have_x0 = false;
+    x0 = 0.f;
+    for (int r = 0; r < world; ++r) {
+        const double* m = recv + (int64_t)r * stride;
+        const int64_t nr = seq_bits(m[0]);
+        const uint32_t of = (uint32_t)seq_bits(m[1]);
+        const int ner = (int)seq_bits(m[2 + kSeqMaxChains + c]);
+        eoff[r] = e;
+        poff[r] = P;
+        pos[r] = p;
+        if (!have_x0 && nr > 0) {
+            x0 = (float)m[2 + 2 * kSeqMaxChains + c];
+            have_x0 = true;
+        }
+        if ((of >> c) & 1u) bad |= 1;
+        if (ner > slot) bad |= 2;
+        mx = mx > ner ? mx : ner;
+        e += ner;
+        P += (uint64_t)seq_bits(m[2 + c]);
+        p += nr;
+    }
+    eoff[world] = e;
+    poff[world] = P;
+    pos[world] = p;
+    if (e > evs) bad |= 4;
+    max_nev = mx;
+    return bad;
+}
 
 struct SeqSumBuf {
     int nch = 0;
@@ -57,9 +177,20 @@ struct SeqSumBuf {
                                 // failure the caller acts on goes through a pass > 1)
     uint32_t* status = nullptr; // [0] chains failing verification (bits), [1] event overflow (bits)
     float* result = nullptr;    // [nch] final sums
+    // sharded: sh (device) set, evs the per-chain stride of the walk's (global) event lists ev_*, the local
+    // lists in lev_* (stride evcap); single rank: sh == nullptr, evs == evcap, events straight into ev_*
+    SeqShard* sh = nullptr;
+    int64_t evs = 0;
+    int64_t evs_alloc = 0;
+    int* lev_pos = nullptr;
+    uint64_t* lev_P = nullptr;
+    float* lev_x = nullptr;
 };
 
 int seqsum_reserve(SeqSumBuf& b, int nch, int64_t nmax, hipStream_t st);
+// sharded mode on / off (nmax already reserved): the SeqShard block and the global event lists (evs_global
+// events per chain; kept O(window): 2 x the local capacity)
+int seqsum_shard(SeqSumBuf& b, bool on, hipStream_t st);
 void seqsum_free(SeqSumBuf& b);
 
 // chain sources
@@ -101,5 +232,27 @@ __host__ __device__ inline int64_t eigen_gemm_kc(int64_t k, int64_t l1) {
 // the results are b.result[0 .. nch) and b.status (0 = verified) once the stream reaches them.
 template <class Src>
 void seqsum_launch(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, hipStream_t st);
+
+// Sharded pass, in three enqueued pieces around the caller's two all-gathers:
+//   seqsum_shard_head  pass 1: block sums -> tot_out (seq_tot_words(nch, nb_slot) doubles)
+//   seqsum_shard_mid   pass 1: seq_shard_offsets over the gathered block sums (rank `rank` of `world`, ranks'
+//                      messages tot_stride doubles apart); every pass: count, block offsets, local events,
+//                      the event message -> msg_out (kSeqHdrWords + nch * 2 * slot doubles)
+//   seqsum_shard_tail  seq_shard_merge over the gathered messages, the walk over all events, the verification
+//                      of the window
+template <class Src>
+void seqsum_shard_head(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, double* tot_out, int64_t nb_slot,
+                       hipStream_t st);
+template <class Src>
+void seqsum_shard_mid(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, const double* tot_recv,
+                      int64_t tot_stride, int64_t nb_slot, int rank, int world, double* msg_out, int slot, hipStream_t st);
+template <class Src>
+void seqsum_shard_tail(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, const double* msg_recv,
+                       int64_t msg_stride, int rank, int world, int slot, hipStream_t st);
+// the event message again with another slot (the local lists are unchanged; the caller clears status[1])
+template <class Src>
+void seqsum_shard_repack(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, double* msg_out, int slot,
+                         hipStream_t st);
+inline int64_t seqsum_msg_words(int nch, int slot) { return kSeqHdrWords + (int64_t)nch * 2 * slot; }
 
 }  // namespace lio

@@ -44,7 +44,7 @@ EXPORTS = [
     "lio_icp_umeyama_pcl_float_order", "lio_icp_get_fidelity_stats", "lio_icp_set_fidelity_debug", "lio_seqsum6",
     "lio_map_set_test_limits", "lio_rccl_unique_id", "lio_icp_set_shard_rccl", "lio_icp_set_shard_shm",
     "lio_shm_exchange_open", "lio_shm_exchange_allgather", "lio_shm_exchange_close", "lio_shm_exchange_set_timeout",
-    "lio_icp_exchange_layout", "lio_icp_gather_ids",
+    "lio_seq_shard_offsets", "lio_seq_shard_merge",
 ]
 
 
@@ -163,8 +163,11 @@ def _declare(L):
         "lio_shm_exchange_allgather": (C.c_int, [vp, dp, C.c_int64, dp]),
         "lio_shm_exchange_close": (C.c_int, [vp]),
         "lio_shm_exchange_set_timeout": (C.c_int, [vp, C.c_double]),
-        "lio_icp_exchange_layout": (C.c_int, [C.c_int64, C.c_int, C.c_int, C.POINTER(C.c_int64), C.POINTER(C.c_int64)]),
-        "lio_icp_gather_ids": (C.c_int, [dp, C.c_int64, C.c_int, C.c_int64, C.POINTER(C.c_int32)]),
+        "lio_seq_shard_offsets": (C.c_int, [dp, C.c_int64, C.c_int64, C.c_int, C.c_int, C.c_int, dp, dp, C.POINTER(C.c_int32),
+                                            C.POINTER(C.c_int64)]),
+        "lio_seq_shard_merge": (C.c_int, [dp, C.c_int64, C.c_int, C.c_int, C.c_int, C.c_int64, C.POINTER(C.c_int32),
+                                          C.POINTER(C.c_uint64), C.POINTER(C.c_float), C.POINTER(C.c_int32),
+                                          C.POINTER(C.c_uint64), C.POINTER(C.c_float)]),
         "lio_map_num_ids": (C.c_int64, [vp]),
         "lio_map_get_by_id": (C.c_int, [vp, fp, C.POINTER(C.c_uint8)]),
         "lio_map_nearest_search": (C.c_int, [vp, fp, C.c_int64, C.c_int, C.c_float, C.POINTER(C.c_int32), fp]),

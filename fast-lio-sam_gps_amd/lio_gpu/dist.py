@@ -80,21 +80,39 @@ def make_allgather(group=None, device=None):
     return _capi.ALLGATHER_FN(_cb)
 
 
-def exchange_layout(n_source: int, world: int, ids: bool):
-    """(doubles per rank of one pass, offset of the int32 ids in doubles) — records only, or records + the
-    rank's accepted 1-NN ids (the default PCL float mode's correspondence passes)"""
-    cnt, off = C.c_int64(), C.c_int64()
-    check(lib().lio_icp_exchange_layout(n_source, world, 1 if ids else 0, C.byref(cnt), C.byref(off)))
-    return cnt.value, off.value
+# the sharded float chains' messages (lio_seqsum.hpp): block sums ([0] the window's count; per chain at
+# SEQ_TOT_HDR + 2 c nb_slot its 1024-element blocks' (double sum, sum |x|)) and event lists (header: n, overflow bits,
+# increment totals, event counts, first elements; then per chain `slot` events of (increment prefix bits,
+# position | value bits << 32))
+SEQ_MAX_CHAINS, SEQ_TOT_HDR, SEQ_HDR_WORDS, SEQ_BLOCK = 9, 8, 32, 1024
 
 
-def gather_ids(recv: np.ndarray, n_source: int, world: int, count: int) -> np.ndarray:
-    """every rank's accepted ids (rank r's message at recv[r * count:]) in source order (lio_icp_gather_ids)"""
+def seq_shard_offsets(recv: np.ndarray, stride: int, nb_slot: int, rank: int, world: int, nch: int):
+    """rank `rank`'s window of chains 0..nch-1 from every rank's block sums (lio_seq_shard_offsets, the device's
+    seq_shard_offsets): (starting prefixes, drift variances, common floors, first global index, total)"""
     recv = np.ascontiguousarray(recv, dtype=np.float64)
-    gid = np.empty(n_source, np.int32)
-    check(lib().lio_icp_gather_ids(recv.ctypes.data_as(C.POINTER(C.c_double)), n_source, world, count,
-                                   gid.ctypes.data_as(C.POINTER(C.c_int32))))
-    return gid
+    off0, var0 = np.zeros(nch), np.zeros(nch)
+    fl = np.zeros(nch, np.int32)
+    gn = np.zeros(2, np.int64)
+    check(lib().lio_seq_shard_offsets(recv.ctypes.data_as(C.POINTER(C.c_double)), stride, nb_slot, rank, world, nch,
+                                      off0.ctypes.data_as(C.POINTER(C.c_double)), var0.ctypes.data_as(C.POINTER(C.c_double)),
+                                      fl.ctypes.data_as(C.POINTER(C.c_int32)), gn.ctypes.data_as(C.POINTER(C.c_int64))))
+    return off0, var0, fl, int(gn[0]), int(gn[1])
+
+
+def seq_shard_merge(recv: np.ndarray, stride: int, world: int, slot: int, chain: int, evs: int) -> dict:
+    """chain `chain`'s global event lists from every rank's event message (lio_seq_shard_merge, the device's
+    seq_shard_merge)"""
+    recv = np.ascontiguousarray(recv, dtype=np.float64)
+    pos, P, x = np.zeros(evs, np.int32), np.zeros(evs, np.uint64), np.zeros(evs, np.float32)
+    info, ptot, x0 = np.zeros(3, np.int32), np.zeros(1, np.uint64), np.zeros(1, np.float32)
+    check(lib().lio_seq_shard_merge(recv.ctypes.data_as(C.POINTER(C.c_double)), stride, world, slot, chain, evs,
+                                    pos.ctypes.data_as(C.POINTER(C.c_int32)), P.ctypes.data_as(C.POINTER(C.c_uint64)),
+                                    x.ctypes.data_as(C.POINTER(C.c_float)), info.ctypes.data_as(C.POINTER(C.c_int32)),
+                                    ptot.ctypes.data_as(C.POINTER(C.c_uint64)), x0.ctypes.data_as(C.POINTER(C.c_float))))
+    ne = int(info[0]) if info[2] == 0 else 0
+    return dict(pos=pos[:ne], P=P[:ne], x=x[:ne], nev=int(info[0]), longest=int(info[1]), bad=int(info[2]),
+                ptot=int(ptot[0]), x0=float(x0[0]))
 
 
 def exchange_len(n_source: int, world: int) -> int:

@@ -302,12 +302,18 @@ int lio_icp_set_shard(lio_icp* h, int rank, int world, lio_allgather_fn fn, void
  * ceil(records/world)*20 doubles, as lio_allgather_fn delivers them.       */
 int lio_icp_shard_range(int64_t n_source, int rank, int world, int64_t* begin, int64_t* count);
 int lio_icp_combine(const double* recv, int64_t n_source, int world, double* out17);
-/* The message of one rank per pass (host helpers, no device): *count doubles — the records, then with
- * ids != 0 (the PCL float modes, non-fitness passes) the rank's accepted 1-NN ids (int32, -1 = rejected)
- * from double *id_off on.  lio_icp_gather_ids unpacks every rank's ids of a recv (rank r at r * count)
- * into gid[0 .. n_source) in source order, as the device does before the float statistics.            */
-int lio_icp_exchange_layout(int64_t n_source, int world, int ids, int64_t* count, int64_t* id_off);
-int lio_icp_gather_ids(const double* recv, int64_t n_source, int world, int64_t count, int32_t* gid);
+/* Host mirrors of the sharded float chains' exchange (no device; the kernels run the same code):
+ * lio_seq_shard_offsets — every rank's block-sum message (rank r at recv + r * stride: [0] the window's
+ * element count, then per chain c at 8 + 2 c nb_slot its 1024-element blocks' (double sum, sum |x|)) -> rank
+ * `rank`'s starting prefix, drift variance and the common floor of chains 0 .. nch-1, its first global index
+ * and the total (gbase_nglobal[2]); lio_seq_shard_merge — every rank's event message (header: [0] n, [1] overflow bits,
+ * [2 + c] increment total, [11 + c] event count, [20 + c] first element; at 32 + 2 slot c the events:
+ * increment prefix bits, then position | value bits << 32) -> chain `chain`'s global lists (pos, P, x) and
+ * nev_ptot_bad = {events, longest list, problems (1 own overflow, 2 over the slot, 4 over evs)}.          */
+int lio_seq_shard_offsets(const double* recv, int64_t stride, int64_t nb_slot, int rank, int world, int nch,
+                          double* off0, double* var0, int32_t* floor_e, int64_t* gbase_nglobal);
+int lio_seq_shard_merge(const double* recv, int64_t stride, int world, int slot, int chain, int64_t evs,
+                        int32_t* pos, uint64_t* P, float* x, int32_t* nev_ptot_bad, uint64_t* ptot, float* x0);
 /* Host half of the float fidelity modes (no device needed): sums16 = the float sums the GPU
  * returns per pass [sum src xyz(3), sum tgt xyz(3), count (uint32 bits), sigma accumulator (9,
  * row-major target x source): unscaled for order 1] -> the incremental transform (row-major 4x4
@@ -334,9 +340,11 @@ int lio_seqsum6(int device, const float* x, int64_t n, int flags, float* sums6, 
  * torch.cuda.ExternalStream(stream)), the handle enqueues the record-order sum behind it and reads 17
  * doubles back: one host wait per pass, no host copies of the records.  Buffers: the handle's own,
  * or the caller's (lio_icp_set_exchange_buffers, e.g. tensors a collective library registered);
- * capacity lio_icp_exchange_len(n_source, world) doubles per rank.  The n of a pass may be less than
- * the capacity: records only (double statistics, fitness passes), or the records followed by the
- * rank's accepted correspondence ids as int32 (the PCL float modes); recv holds rank r at r * n.      */
+ * capacity lio_icp_exchange_len(n_source, world) doubles per rank.  The n of a call may be less than
+ * the capacity and differs between the calls of a pass, the same on every rank: the records (double
+ * statistics, fitness passes); in the PCL float modes (the default) three all-gathers per pass — the
+ * records followed by the window's chain totals, the window's float-chain event lists (and its first
+ * pairs), the window's GEMM depth blocks (lio_icp_host.cpp, lio_seqsum.hpp); recv holds rank r at r * n. */
 typedef int (*lio_allgather_dev_fn)(const double* d_send, int64_t n, double* d_recv, void* stream, void* user);
 int lio_icp_set_shard_device(lio_icp* h, int rank, int world, lio_allgather_dev_fn fn, void* user);
 int lio_icp_exchange_len(int64_t n_source, int world, int64_t* n_per_rank);

@@ -39,6 +39,7 @@ for s in $STEPS; do
     icpx)  runs pytest_icpx 600 python -u -m pytest tests/test_gpu_icp.py -k "exchange or group" -x -v -s -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     spawn2) LIO_BENCH_REHEARSE=1 run spawn2 500 python bench.py --gpus 2 --steps 50 --warmup 5 --pipeline 0 --no-cpu --streams '' --icp-reps 2 ;;
     map)   runs pytest_map 900 python -u -m pytest tests/test_gpu_map.py tests/test_gpu_fullsize.py -x -v -p no:cacheprovider --timeout 600 --timeout-method thread ;;
+    shardt) runs pytest_shard 900 python -u -m pytest tests/test_gpu_icp.py tests/test_gpu_fullsize.py tests/test_gpu_dist.py -k "group or exchange or emulated or multiprocess or recovery or timeout" -x -v -s -p no:cacheprovider --timeout 600 --timeout-method thread ;;
     lseqt) runs pytest_lseq 600 python -u -m pytest tests/test_cpp_stream.py tests/test_gpu_parity.py -k "loop_sequence or guard" -x -v -s -p no:cacheprovider --timeout 500 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     loopseqprof) run loopseqprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/loopseqprof" -o run --output-format csv -- fast-lio-sam_gps_amd/lio_gpu/_lib/loop_sequence /tmp/ls.bin &&

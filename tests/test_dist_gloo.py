@@ -144,11 +144,30 @@ def test_shm_exchange_cpp(world):
             np.testing.assert_array_equal(np.frombuffer(b), ld.combine((recs * (k + 1)).ravel(), NS, 1))
 
 
-def _ids_worker(rank, world, port, q):
-    """One rank of the default (PCL float) mode's exchange on CPU: the message is this rank's records followed
-    by its accepted 1-NN ids (int32, -1 = rejected) — lio_icp_exchange_layout — all-gathered through the same
-    ctypes callback the library calls; lio_icp_gather_ids then rebuilds the whole source's ids in source order
-    (what icp_gather_ids_kernel does on the device before the float chains) and the records combine as before."""
+def _windows(world):
+    """Synthetic windows of a chain split over `world` ranks (rank 1 empty when world > 2): per rank its elements
+    of 6 chains and its event lists (local positions, local increment prefixes, values)."""
+    rng = np.random.default_rng(7)
+    sizes = [int(v) for v in rng.integers(2000, 9000, world)]
+    if world > 2:
+        sizes[1] = 0
+    out = []
+    for r, n in enumerate(sizes):
+        x = (rng.normal(3.0, 40.0, (6, n))).astype(np.float32)
+        evs = []
+        for c in range(6):
+            ne = int(rng.integers(0, 60)) if n else 0
+            pos = np.sort(rng.choice(n, ne, replace=False)).astype(np.int64) if ne else np.zeros(0, np.int64)
+            P = np.sort(rng.integers(0, 1 << 40, ne)).astype(np.uint64)
+            evs.append((pos, P, x[c, pos] if ne else np.zeros(0, np.float32), int(rng.integers(1 << 40, 1 << 41))))
+        out.append((n, x, evs))
+    return out
+
+
+def _shard_msg_worker(rank, world, port, slot, q):
+    """One rank of the sharded float chains' exchange on CPU: its totals and its event
+    message in the documented layout (lio_gpu.dist.SEQ_*), all-gathered through the ctypes callback the library
+    calls (gloo), then the host mirrors of seq_shard_offsets / seq_shard_merge (the device kernels' own code)."""
     import sys
 
     here = os.path.dirname(os.path.abspath(__file__))
@@ -161,56 +180,91 @@ def _ids_worker(rank, world, port, q):
 
         from lio_gpu import dist as ld
 
-        recs = _records(NS)
-        ids = _ids(NS)
-        b, n = ld.shard_range(NS, rank, world)
-        cnt, off = ld.exchange_layout(NS, world, True)
-        cnt_rec, _ = ld.exchange_layout(NS, world, False)
-        r0 = b // 4096
-        mine = recs[r0: r0 + (n + 4095) // 4096]
-        send = np.zeros(cnt)
-        send[: mine.size] = mine.ravel()
-        send.view(np.int32)[2 * off: 2 * off + n] = ids[b: b + n]
+        n, x, evs = _windows(world)[rank]
         cb = ld.make_allgather()
-        recv = np.zeros(cnt * world)
-        assert cb(send.ctypes.data_as(C.POINTER(C.c_double)), cnt, recv.ctypes.data_as(C.POINTER(C.c_double)), None) == 0
-        gid = ld.gather_ids(recv, NS, world, cnt)
-        rec_only = np.concatenate([recv[r * cnt: r * cnt + cnt_rec] for r in range(world)])
-        q.put((rank, gid.tobytes(), ld.combine(rec_only, NS, world).tobytes()))
+        # block sums: [0] n, per chain nb_slot (block double sum, block sum |x|)
+        nbs = 10
+        tw = ld.SEQ_TOT_HDR + 6 * 2 * nbs
+        tot = np.zeros(tw)
+        tot[0] = n
+        for c in range(6):
+            for j, b0 in enumerate(range(0, n, ld.SEQ_BLOCK)):
+                blk = x[c, b0:b0 + ld.SEQ_BLOCK].astype(np.float64)
+                tot[ld.SEQ_TOT_HDR + c * 2 * nbs + 2 * j] = float(np.sum(blk))
+                tot[ld.SEQ_TOT_HDR + c * 2 * nbs + 2 * j + 1] = float(np.sum(np.abs(blk)))
+        rtot = np.zeros(tw * world)
+        assert cb(tot.ctypes.data_as(C.POINTER(C.c_double)), tw, rtot.ctypes.data_as(C.POINTER(C.c_double)), None) == 0
+        off = ld.seq_shard_offsets(rtot, tw, nbs, rank, world, 6)
+        # events
+        words = ld.SEQ_HDR_WORDS + 6 * 2 * slot
+        msg = np.zeros(words)
+        mi = msg.view(np.int64)
+        mi[0] = n
+        for c, (pos, P, xv, ptot) in enumerate(evs):
+            mi[2 + c] = np.int64(np.uint64(ptot).view(np.int64))
+            mi[2 + ld.SEQ_MAX_CHAINS + c] = len(pos)
+            msg[2 + 2 * ld.SEQ_MAX_CHAINS + c] = float(x[c, 0]) if n else 0.0
+            m = min(len(pos), slot)
+            b = ld.SEQ_HDR_WORDS + c * 2 * slot
+            mi[b:b + 2 * m:2] = P[:m].view(np.int64)
+            mi[b + 1:b + 2 * m:2] = (pos[:m].astype(np.uint64) | (xv[:m].view(np.uint32).astype(np.uint64) << np.uint64(32))).view(np.int64)
+        rmsg = np.zeros(words * world)
+        assert cb(msg.ctypes.data_as(C.POINTER(C.c_double)), words, rmsg.ctypes.data_as(C.POINTER(C.c_double)), None) == 0
+        merged = [ld.seq_shard_merge(rmsg, words, world, slot, c, 4096) for c in range(6)]
+        q.put((rank, off, merged))
     finally:
         dist.destroy_process_group()
 
 
-def _ids(ns):
-    rng = np.random.default_rng(99)
-    ids = rng.integers(0, 500_000, ns).astype(np.int32)
-    ids[rng.random(ns) < 0.1] = -1
-    return ids
-
-
-@pytest.mark.parametrize("world", [2, 3, 4])
-def test_sharded_icp_id_exchange_gloo(world):
-    """VERDICT r04 next #2 (the float mode sharded): every rank recovers every rank's accepted ids in source
-    order, bit for bit, and the record combine is unchanged by the ids riding behind the records."""
+@pytest.mark.parametrize("world,slot", [(2, 64), (3, 64), (4, 64), (3, 16)])
+def test_sharded_float_chain_messages_gloo(world, slot):
+    """The sharded PCL float statistics' messages over gloo: every rank gets the same common
+    floors and totals, its window's starting prefix is the double sum of the windows before it, and the merged
+    event lists are every rank's events in element order (positions and increment prefixes moved by the ranks
+    before); a list longer than the slot is flagged (bit 2) on every rank, so every rank takes the same re-exchange."""
     import sys
 
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                     "fast-lio-sam_gps_amd"))
-    from lio_gpu import dist as ld
-
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_ids_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_shard_msg_worker, args=(r, world, port, slot, q)) for r in range(world)]
     [p.start() for p in procs]
-    got = [q.get(timeout=120) for _ in range(world)]
+    got = sorted((q.get(timeout=120) for _ in range(world)), key=lambda t: t[0])
     [p.join(timeout=60) for p in procs]
     assert all(p.exitcode == 0 for p in procs)
-    ref_ids = _ids(NS)
-    ref = ld.combine(_records(NS).ravel(), NS, 1)
-    for rank, gid, comb in got:
-        np.testing.assert_array_equal(np.frombuffer(gid, np.int32), ref_ids)
-        np.testing.assert_array_equal(np.frombuffer(comb), ref)
+    win = _windows(world)
+    sizes = [w[0] for w in win]
+    for rank, off, merged in got:
+        off0, var0, fl, gbase, ng = off
+        assert gbase == sum(sizes[:rank]) and ng == sum(sizes)
+        for c in range(6):  # the prefix: the blocks of the windows before, block sums added in chain order
+            want = 0.0
+            for r in range(rank):
+                for b0 in range(0, sizes[r], 1024):
+                    want = want + float(np.sum(win[r][1][c, b0:b0 + 1024].astype(np.float64)))
+            assert off0[c] == want
+        np.testing.assert_array_equal(fl, got[0][1][2])  # the floors: identical on every rank
+        np.testing.assert_array_equal(var0 >= 0, True)
+        for c in range(6):
+            m = merged[c]
+            lens = [len(w[2][c][0]) for w in win]
+            if max(lens) > slot:
+                assert m["bad"] & 2 and m["longest"] == max(lens)
+                continue
+            assert m["bad"] == 0 and m["nev"] == sum(lens)
+            base = np.cumsum([0] + sizes[:-1])
+            pb = np.cumsum([0] + [w[2][c][3] for w in win[:-1]]).astype(np.uint64)
+            pos = np.concatenate([w[2][c][0] + base[r] for r, w in enumerate(win)])
+            P = np.concatenate([w[2][c][1] + pb[r] for r, w in enumerate(win)])
+            xs = np.concatenate([w[2][c][2] for w in win])
+            np.testing.assert_array_equal(m["pos"], pos)
+            np.testing.assert_array_equal(m["P"], P)
+            np.testing.assert_array_equal(m["x"], xs)
+            assert m["ptot"] == int(sum(w[2][c][3] for w in win)) % (1 << 64)
+            first = next(r for r in range(world) if sizes[r])
+            assert m["x0"] == float(win[first][1][c][0])
 
 
 def test_shm_exchange_reopen_same_name():

@@ -133,13 +133,13 @@ def test_c5_raw_scan_pipeline_three_scans(oracle):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("world,disp", [(4, (2.5, 4.0)), (2, (0.3, 1.5))])
+@pytest.mark.parametrize("world,disp", [(4, (2.5, 4.0)), (2, (0.3, 1.5)), (8, (2.5, 4.0))])
 def test_icp_c4_emulated_ranks_bit_identical(oracle, world, disp):
     """BASELINE.json configs[3]'s layout: the source sharded over `world` ranks (threads, one LoopClosure
-    each, in-process all-gather of the 4096-point records and the accepted correspondence ids), target
-    replicated, in the DEFAULT mode (PCL's float Umeyama, Eigen 3.3 order): every rank's transform equals the
-    one-rank transform bit for bit, and that transform is within 1e-5 of the oracle's float order 2 (VERDICT
-    r04 next #2: the multi-GPU loop ICP at the reference's arithmetic)."""
+    each, in-process host all-gathers), target replicated, in the DEFAULT mode (PCL's float Umeyama, Eigen 3.3
+    order) with the float chains split over the ranks' windows (round 6: block sums, event lists and depth blocks
+    exchanged; each rank holds only its shard): every rank's transform equals the one-rank transform bit for
+    bit, and that transform is within 1e-5 of the oracle's float order 2 (VERDICT r05 next #1)."""
     src, dst, _ = synth.make_icp_pair(n_points=500_000, seed=4321, disp=disp)
     bar = threading.Barrier(world)
     slots = [None] * world

@@ -263,13 +263,20 @@ def test_icp_double_statistics_opt_in_bound_at_c4(oracle, disp):
         assert gap < 1e-3
 
 
-@pytest.mark.parametrize("mode", [LC.FIDELITY_ORDER, LC.DOUBLE_STATS])
-@pytest.mark.parametrize("world", [2, 3])
-def test_icp_device_exchange_emulated_ranks(world, mode):
+@pytest.mark.parametrize("mode,world,debug", [(LC.FIDELITY_ORDER, 2, None), (LC.DOUBLE_STATS, 2, None),
+                                               (LC.FIDELITY_ORDER, 3, None), (LC.DOUBLE_STATS, 3, None),
+                                               (1, 2, None), (3, 3, None),
+                                               (LC.FIDELITY_ORDER, 2, ("repass", 1, 0)),
+                                               (LC.FIDELITY_ORDER, 3, ("serial", 0, 8)),
+                                               (LC.FIDELITY_ORDER, 2, ("timeout", 4, 0))])
+def test_icp_device_exchange_emulated_ranks(world, mode, debug):
     """The device-side exchange (lio_icp_set_shard_device + caller-owned exchange buffers, the form the
     RCCL paths use): `world` ranks as threads on the one GPU, the all-gather emulated with device copies
     between the ranks' torch buffers on each handle's own stream; the record-order sum runs on the
-    device.  Every rank's transform, score and iterations equal the one-rank alignment bit for bit."""
+    device.  Every rank's transform, score and iterations equal the one-rank alignment bit for bit — in the
+    sharded float orders 1-3 (the chains split over the ranks' windows) and through their
+    recovery paths on every rank: re-passes after a failed verification, the serial fallback over the gathered
+    pairs (event lists capped at 8), a compaction look-back time-out."""
     import threading
 
     import torch
@@ -312,6 +319,9 @@ def test_icp_device_exchange_emulated_ranks(world, mode):
     cbs = [make_cb(r) for r in range(world)]
     lcs = [LC.LoopClosure(LC.LoopClosureConfig(), umeyama_float=mode) for _ in range(world)]
     results = [None] * world
+    if debug:
+        for lc in lcs:
+            lc.set_fidelity_debug(debug[1], debug[2])
 
     def run(rank):
         h = lcs[rank]._h
@@ -333,3 +343,8 @@ def test_icp_device_exchange_emulated_ranks(world, mode):
         assert r is not None
         np.testing.assert_array_equal(np.array(list(r.T), np.float32), np.array(list(r1.T), np.float32))
         assert r.score == r1.score and r.iterations == r1.iterations and r.state == r1.state
+    if debug:
+        fs = [lc.fidelity_stats() for lc in lcs]
+        print(debug[0], fs)
+        key = "repasses" if debug[0] == "repass" else "serial"
+        assert all(f[key] > 0 for f in fs) and len({f[key] for f in fs}) == 1  # every rank took the same path
