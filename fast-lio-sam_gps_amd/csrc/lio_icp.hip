@@ -898,20 +898,35 @@ void launch_icp_pcl_sigma_serial(const float* pairs, int64_t cap, float* out16, 
     icp_pcl_sigma_kernel<<<1, kPclThreads, 0, st>>>(pairs, cap, out16);
 }
 
-__global__ void __launch_bounds__(64) icp_combine_kernel(const double* __restrict__ recv, int64_t nsup, int world,
-                                                        int64_t rank_stride, double* __restrict__ out17) {
+// the records of every rank summed in global record order, one lane per statistic (lio_icp_combine's order):
+// the records go through LDS in chunks, loaded by all lanes, so the 17 dependent chains read LDS, not HBM
+constexpr int kCombChunk = 256;
+__global__ void __launch_bounds__(256) icp_combine_kernel(const double* __restrict__ recv, int64_t nsup, int world,
+                                                         int64_t rank_stride, double* __restrict__ out17) {
+    __shared__ double s_rec[kCombChunk][17];
     const int k = threadIdx.x;
-    if (k >= 17) return;
     double acc = 0.0;
-    for (int r = 0; r < world; ++r) {
-        const int64_t s0 = nsup * r / world, s1 = nsup * (r + 1) / world;
-        for (int64_t s = s0; s < s1; ++s) acc += recv[(size_t)r * rank_stride + (size_t)(s - s0) * kIcpStride + k];
+    for (int64_t g0 = 0; g0 < nsup; g0 += kCombChunk) {
+        const int m = (int)min((int64_t)kCombChunk, nsup - g0);
+        for (int e = threadIdx.x; e < m * 17; e += 256) {
+            const int64_t s = g0 + e / 17;
+            // the rank holding record s (records split as nsup * r / world) and its slot in that rank's message
+            int r = (int)(s * world / nsup);
+            while (r + 1 < world && nsup * (r + 1) / world <= s) ++r;
+            while (r > 0 && nsup * r / world > s) --r;
+            const int64_t s0 = nsup * r / world;
+            s_rec[e / 17][e % 17] = recv[(size_t)r * rank_stride + (size_t)(s - s0) * kIcpStride + e % 17];
+        }
+        __syncthreads();
+        if (k < 17)
+            for (int j = 0; j < m; ++j) acc += s_rec[j][k];
+        __syncthreads();
     }
-    out17[k] = acc;
+    if (k < 17) out17[k] = acc;
 }
 
 void launch_icp_combine(const double* recv, int64_t nsup, int world, int64_t rank_stride, double* out17, hipStream_t st) {
-    icp_combine_kernel<<<1, 64, 0, st>>>(recv, nsup, world, rank_stride, out17);
+    icp_combine_kernel<<<1, 256, 0, st>>>(recv, nsup, world, rank_stride, out17);
 }
 
 void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st, uint32_t* order, int ntiles) {

@@ -621,7 +621,7 @@ int lio_icp_set_shard_device(lio_icp* h, int rank, int world, lio_allgather_dev_
 //   records   every pass: its 4096-point records (slot = ceil(records / world) of kIcpStride); in the sharded
 //             PCL float modes followed by its windows' chain totals (lio_seqsum.hpp, kTotPad)
 //   events    sharded PCL float modes: the seqsum event message of its window (ev_slot events per chain),
-//             for the means followed by its first kPclMaxKc pairs (lio_pcl.hpp)
+//             for the means with its first kPclMaxKc pairs (SeqHeads, lio_seqsum.hpp)
 //   blocks    sharded orders 2 / 3: its depth blocks of sigma and the verification statuses
 //   gather    the sharded serial fallback: its pairs in rounds
 // exchange_len is the capacity of every one of them (the event slot up to ev_slot_cap).
@@ -632,12 +632,12 @@ static int64_t exchange_slot(int64_t ns, int world) {
 static int64_t shard_points_max(int64_t ns, int world) { return exchange_slot(ns, world) * lio::kIcpSuper; }
 static int64_t ev_slot_cap(int64_t ns, int world) { return std::max<int64_t>(4096, shard_points_max(ns, world) / 8); }
 static int64_t records_count(int64_t ns, int world) { return exchange_slot(ns, world) * lio::kIcpStride; }
-// blocks of a window in the block-sum message (seq_shard_totals)
+// blocks of a window in the block-sum message (seq_bsum's tot_out)
 static int64_t tot_blocks(int64_t ns, int world) { return (shard_points_max(ns, world) + lio::kSeqBlock - 1) / lio::kSeqBlock + 1; }
 static int64_t tot_words(int64_t ns, int world, int nch) { return lio::seq_tot_words(nch, tot_blocks(ns, world)); }
 static int64_t exchange_len_fsh(int64_t ns, int world) {
     const int64_t rec = records_count(ns, world) + tot_words(ns, world, lio::kSeqMaxChains);
-    const int64_t ev = lio::seqsum_msg_words(lio::kSeqMaxChains, (int)ev_slot_cap(ns, world)) + lio::pcl_heads_words();
+    const int64_t ev = lio::seqsum_msg_words(lio::kSeqMaxChains, (int)ev_slot_cap(ns, world)) + lio::pcl_heads_words();  // >= 6 chains' heads
     const int64_t x3 = lio::pcl_x3_words(lio::pcl_blocks_slot(shard_points_max(ns, world)));
     return std::max(std::max(rec, ev), std::max(x3, (int64_t)4096));
 }
@@ -890,17 +890,16 @@ static lio::SeqSigma fsh_sigma_src(const lio_icp* h) { return lio::SeqSigma{h->p
 
 // the means' event message is packed (seqsum_shard_mid / _repack): + the window's first pairs -> all-gather ->
 // the pairs after the window appended, the global lists, the walk, the window's verification
+static int fsh_heads(const lio_icp* h) { return h->p.umeyama_float != 1 ? lio::kPclMaxKc : 0; }
 static int fsh_means_events(lio_icp* h, int pass) {
     lio::PclBuf& P = h->pcl;
-    const int order = h->p.umeyama_float;
-    const int64_t ev_words = lio::seqsum_msg_words(6, h->ev_slot);
-    const int64_t m2 = ev_words + (order != 1 ? lio::pcl_heads_words() : 0);
-    if (order != 1) lio::launch_pcl_shard_heads(P, h->d_xsend + ev_words, h->st);
+    const int64_t m2 = lio::seqsum_msg_words(6, h->ev_slot, fsh_heads(h));
     int rc = xchg(h, m2);
     if (rc) return rc;
-    if (order != 1) lio::launch_pcl_shard_heads_merge(P, h->d_xrecv, m2, ev_words, h->rank, h->world, h->st);
+    lio::SeqHeads hd;
+    if (fsh_heads(h)) hd = lio::SeqHeads{lio::kPclMaxKc, P.pairs, P.cap, P.ghead, lio::kPclTinyN};
     lio::seqsum_shard_tail(fsh_means_src(h), 6, P.small + lio::kPclN, P.means, pass, h->d_xrecv, m2, h->rank, h->world,
-                           h->ev_slot, h->st);
+                           h->ev_slot, hd, h->st);
     return LIO_OK;
 }
 
@@ -923,14 +922,15 @@ static int fsh_sigma_pack(lio_icp* h, int spass, int stage = 0) {
                 if ((rc = xchg(h, tw))) return rc;
             }
             lio::seqsum_shard_mid(ss, 9, dn, P.sig, spass, h->d_xrecv, tw, nbs, h->rank, h->world, h->d_xsend,
-                                  h->ev_slot_s, h->st);
+                                  h->ev_slot_s, 0, h->st);
         } else {
             IHIP(hipMemsetAsync(P.sig.status + 1, 0, sizeof(uint32_t), h->st));
-            lio::seqsum_shard_repack(ss, 9, dn, P.sig, h->d_xsend, h->ev_slot_s, h->st);
+            lio::seqsum_shard_repack(ss, 9, dn, P.sig, h->d_xsend, h->ev_slot_s, 0, h->st);
         }
         const int64_t m = lio::seqsum_msg_words(9, h->ev_slot_s);
         if ((rc = xchg(h, m))) return rc;
-        lio::seqsum_shard_tail(ss, 9, dn, P.sig, spass, h->d_xrecv, m, h->rank, h->world, h->ev_slot_s, h->st);
+        lio::seqsum_shard_tail(ss, 9, dn, P.sig, spass, h->d_xrecv, m, h->rank, h->world, h->ev_slot_s, lio::SeqHeads{},
+                               h->st);
     }
     lio::launch_pcl_sigma_shard(P, order, h->d_xsend, nq_slot, h->st);
     const int64_t m3 = order == 1 ? lio::kPclX3Hdr : lio::pcl_x3_words(nq_slot);
@@ -1002,9 +1002,13 @@ static int pcl_finish_fsh(lio_icp* h, const lio::IcpArgs& a) {
     const bool lb_timeout = pcl_word(h, 3) != 0;
     constexpr int kMaxPasses = 4;
     int mpass = 1, spass = 1, reexchanges = 0;
+    static const bool trace = std::getenv("LIO_FSH_TRACE") != nullptr;  // diagnostics: the re-pass decisions
     while (!lb_timeout) {
         const uint32_t bad = pcl_word(h, 0), over = pcl_word(h, 1), xf = pcl_word(h, 4);
         const int mm = (int)pcl_word(h, 5), ms = (int)pcl_word(h, 6);
+        if (trace)
+            std::fprintf(stderr, "fsh rank %d: bad %x over %x xflags %x longest %d/%d mpass %d spass %d slot %d\n", h->rank,
+                         bad, over, xf, mm, ms, mpass, spass, h->ev_slot);
         h->ev_slot = next_slot(h, mm);
         if (order == 1 && ms > 0) h->ev_slot_s = next_slot(h, ms);
         if ((bad | over) == 0) break;
@@ -1016,7 +1020,7 @@ static int pcl_finish_fsh(lio_icp* h, const lio::IcpArgs& a) {
             ++reexchanges;
             if (xf & 1u) {
                 IHIP(hipMemsetAsync(P.means.status + 1, 0, sizeof(uint32_t), h->st));
-                lio::seqsum_shard_repack(fsh_means_src(h), 6, dn, P.means, h->d_xsend, h->ev_slot, h->st);
+                lio::seqsum_shard_repack(fsh_means_src(h), 6, dn, P.means, h->d_xsend, h->ev_slot, fsh_heads(h), h->st);
                 int rc = fsh_means_events(h, mpass);
                 if (rc) return rc;
                 spass = 1;
@@ -1033,7 +1037,7 @@ static int pcl_finish_fsh(lio_icp* h, const lio::IcpArgs& a) {
             if (mpass >= kMaxPasses) break;
             ++mpass;
             lio::seqsum_shard_mid(fsh_means_src(h), 6, dn, P.means, mpass, nullptr, 0, 0, h->rank, h->world,
-                                  h->d_xsend, h->ev_slot, h->st);
+                                  h->d_xsend, h->ev_slot, fsh_heads(h), h->st);
             int rc = fsh_means_events(h, mpass);
             if (rc) return rc;
             spass = 1;
@@ -1048,6 +1052,7 @@ static int pcl_finish_fsh(lio_icp* h, const lio::IcpArgs& a) {
         ++h->fid_stats[3];
     }
     if (lb_timeout || (pcl_word(h, 0) | pcl_word(h, 1)) != 0) {
+        if (trace) std::fprintf(stderr, "fsh rank %d: serial fallback (look-back %d)\n", h->rank, (int)lb_timeout);
         const int rc = fsh_serial(h, a, lb_timeout);
         if (rc) return rc;
     }
@@ -1077,7 +1082,7 @@ static int icp_pass_fsh(lio_icp* h, const lio::IcpArgs& a, bool apply_T, double 
     if ((rc = xchg(h, cnt1))) return rc;
     lio::launch_icp_combine(h->d_xrecv, nsup, h->world, cnt1, h->h_out17_dev, h->st);
     lio::seqsum_shard_mid(fsh_means_src(h), 6, dn, P.means, 1, h->d_xrecv + rec, cnt1, nbs, h->rank, h->world,
-                          h->d_xsend, h->ev_slot, h->st);
+                          h->d_xsend, h->ev_slot, fsh_heads(h), h->st);
     if ((rc = fsh_means_events(h, 1))) return rc;
     if ((rc = fsh_sigma_pack(h, 1))) return rc;  // waits for the pass
     IHIP(hipGetLastError());

@@ -259,53 +259,6 @@ __global__ void __launch_bounds__(kPackThreads) pcl_pack_kernel(const float* __r
 }
 
 // ---------------------------------------------------------------- sharded statistics
-// this rank's first kMaxKc pairs, column-major (6 x kMaxKc floats) behind the means' event message
-__global__ void __launch_bounds__(256) pcl_heads_kernel(const float* __restrict__ pairs, int64_t cap,
-                                                        const uint32_t* __restrict__ d_n, float* __restrict__ out) {
-    const int64_t n = *d_n;
-    for (int e = threadIdx.x; e < 6 * kMaxKc; e += 256) {
-        const int d = e / kMaxKc, j = e % kMaxKc;
-        out[e] = j < n ? pairs[d * cap + j] : 0.f;
-    }
-}
-
-// The pairs after this window: the next ranks' heads (their first min(n_r, kMaxKc) pairs) in rank order, up to
-// kMaxKc of them, appended at pairs[n ..]; the first kPclTinyN pairs of the whole order -> ghead (column-major,
-// kPclTinyN per column: the lazy product's inputs when the whole count is below 14, every pair then a head).
-// One block; the message of rank r (its element count at word 0, the seqsum header) at recv + r * stride.
-__global__ void __launch_bounds__(256) pcl_heads_merge_kernel(float* __restrict__ pairs, int64_t cap,
-                                                              const uint32_t* __restrict__ d_n, const double* __restrict__ recv,
-                                                              int64_t stride, int64_t heads_off, int rank, int world,
-                                                              float* __restrict__ ghead) {
-    const int64_t n = *d_n;
-    int64_t got = 0;
-    for (int r = rank + 1; r < world && got < kMaxKc; ++r) {  // block-uniform
-        const double* m = recv + (size_t)r * (size_t)stride;
-        const int64_t nr = (int64_t)__double_as_longlong(m[0]);
-        const int64_t take = min(min(nr, (int64_t)kMaxKc), kMaxKc - got);
-        const float* h = reinterpret_cast<const float*>(m + heads_off);
-        for (int64_t e = threadIdx.x; e < 6 * take; e += 256) {
-            const int d = (int)(e / take);
-            const int64_t j = e % take;
-            pairs[d * cap + n + got + j] = h[d * kMaxKc + j];
-        }
-        got += take;
-    }
-    int64_t g = 0;
-    for (int r = 0; r < world && g < kPclTinyN; ++r) {
-        const double* m = recv + (size_t)r * (size_t)stride;
-        const int64_t nr = (int64_t)__double_as_longlong(m[0]);
-        const int64_t take = min(min(nr, (int64_t)kMaxKc), (int64_t)kPclTinyN - g);
-        const float* h = reinterpret_cast<const float*>(m + heads_off);
-        for (int64_t e = threadIdx.x; e < 6 * take; e += 256) {
-            const int d = (int)(e / take);
-            const int64_t j = e % take;
-            ghead[d * kPclTinyN + g + j] = h[d * kMaxKc + j];
-        }
-        g += take;
-    }
-}
-
 // depth blocks [q0, q1) of the whole chain (q0 = the first block starting in this window), each summed as in
 // pcl_sigma_blocks_kernel from the window's pairs and the ones appended after it; the results (9 floats per
 // block) and the header (the ranks' statuses, q0, the block count) into the message
@@ -499,16 +452,6 @@ int pcl_shard_reserve(PclBuf& p, int64_t n_blocks_global, hipStream_t st) {
         p.Cbg_cap = c;
     }
     return 0;
-}
-
-void launch_pcl_shard_heads(PclBuf& p, double* msg_heads, hipStream_t st) {
-    pcl_heads_kernel<<<1, 256, 0, st>>>(p.pairs, p.cap, p.small + kPclN, reinterpret_cast<float*>(msg_heads));
-}
-
-void launch_pcl_shard_heads_merge(PclBuf& p, const double* recv, int64_t stride, int64_t heads_off, int rank, int world,
-                                  hipStream_t st) {
-    pcl_heads_merge_kernel<<<1, 256, 0, st>>>(p.pairs, p.cap, p.small + kPclN, recv, stride, heads_off, rank, world,
-                                              p.ghead);
 }
 
 void launch_pcl_sigma_shard(PclBuf& p, int order, double* msg3, int64_t nq_slot, hipStream_t st) {

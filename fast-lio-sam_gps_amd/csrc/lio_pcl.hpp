@@ -51,14 +51,10 @@ struct PclBuf {
 int pcl_reserve_plain(PclBuf& p, int64_t n, hipStream_t st);
 int pcl_shard_reserve(PclBuf& p, int64_t n_blocks_global, hipStream_t st);
 
-// ---- sharded statistics (lio_icp_host.cpp fid_sharded): the means exchange carries, behind the seqsum event
-// message, this rank's first kPclMaxKc pairs (a depth block starting in one window may end in the next)
+// ---- sharded statistics (lio_icp_host.cpp fid_sharded): the means' seqsum event message carries this rank's
+// first kPclMaxKc pairs (SeqHeads: a depth block starting in one window may end in the next; seq_shard_merge
+// appends the next ranks' after the window and puts the first kPclTinyN of the whole order in ghead)
 inline int64_t pcl_heads_words() { return 3 * (int64_t)kPclMaxKc; }
-void launch_pcl_shard_heads(PclBuf& p, double* msg_heads, hipStream_t st);
-// the pairs after this window (the next ranks' heads, in order, up to kPclMaxKc) appended to it; the first
-// kPclTinyN pairs of the whole order -> ghead.  heads_off: the heads' offset in each rank's message
-void launch_pcl_shard_heads_merge(PclBuf& p, const double* recv, int64_t stride, int64_t heads_off, int rank, int world,
-                                  hipStream_t st);
 // depth blocks of the whole chain whose first element is in this window (orders 2 / 3), with the statuses, into
 // the message (kPclX3Hdr + nq_slot * 9 floats); nq_slot from pcl_blocks_slot
 inline int64_t pcl_blocks_slot(int64_t n_window_max) { return n_window_max / 340 + 3; }

@@ -207,11 +207,14 @@ __device__ __forceinline__ void classify(const SeqSumBuf& b, int c, int64_t n, c
 }
 
 template <class Src>
-__global__ void __launch_bounds__(kSeqThreads) seq_bsum(Src src, SeqSumBuf b, const uint32_t* d_n) {
+__global__ void __launch_bounds__(kSeqThreads) seq_bsum(Src src, SeqSumBuf b, const uint32_t* d_n,
+                                                          double* __restrict__ tot_out = nullptr, int64_t nb_slot = 0) {
     __shared__ double s_wd[kSeqThreads / 64];
     __shared__ double s_abs[kSeqThreads / 64];
     const int c = blockIdx.y;
     const int64_t n = *d_n;
+    // sharded: the block sums go straight into this window's message too (seq_shard_offsets on every rank)
+    if (tot_out && c == 0 && blockIdx.x == 0 && threadIdx.x == 0) tot_out[0] = (double)n;
     if ((int64_t)blockIdx.x * kSeqBlock >= n) return;  // block-uniform
     float x[kSeqPer];
     load_x(src, c, (int64_t)blockIdx.x * kSeqBlock + (int64_t)threadIdx.x * kSeqPer, n, x);
@@ -225,6 +228,10 @@ __global__ void __launch_bounds__(kSeqThreads) seq_bsum(Src src, SeqSumBuf b, co
     if (threadIdx.x == 0) {
         b.bsum[(size_t)c * b.nblk + blockIdx.x] = tot;
         b.babs[(size_t)c * b.nblk + blockIdx.x] = atot;
+        if (tot_out && blockIdx.x < nb_slot) {
+            tot_out[kSeqTotHdr + (size_t)c * 2 * nb_slot + 2 * blockIdx.x] = tot;
+            tot_out[kSeqTotHdr + (size_t)c * 2 * nb_slot + 2 * blockIdx.x + 1] = atot;
+        }
     }
 }
 
@@ -397,6 +404,12 @@ __global__ void __launch_bounds__(kSeqThreads) seq_scan2(SeqSumBuf b, const uint
         b.ptot[c] = P;
         b.floor_e[b.nch + c] = E;  // events of the chain
         if (E > b.evcap) atomicOr(&b.status[1], 1u << c);
+        if (b.sh) {
+            b.sh->nev_loc[c] = E;
+            b.sh->ptot_loc[c] = P;
+            b.sh->e_added[c] = 0;
+            b.sh->p_added[c] = 0;
+        }
     }
 }
 
@@ -675,38 +688,97 @@ __global__ void __launch_bounds__(kSeqThreads) seq_verify(Src src, SeqSumBuf b, 
 }
 
 // ---------------------------------------------------------------- sharded chains (lio_seqsum.hpp)
-// The window's block sums for the other ranks: [0] its element count, then per chain its blocks' (double sum,
-// sum |x|) (seq_bsum's, in block order; nb_slot per chain)
-__global__ void __launch_bounds__(256) seq_shard_totals(SeqSumBuf b, const uint32_t* d_n, double* __restrict__ out,
-                                                        int64_t nb_slot) {
+// Every window's place in the chains from the gathered block sums, for this rank's window: seq_scan1's
+// formulas run over all ranks' blocks in chain order — a block prefix in windows of kScanWin blocks (the same
+// structure as seq_scan1; every rank runs it over the same data with the same launch, so the floors agree bit
+// for bit).  One block per chain; lio_seqsum.hpp's seq_shard_offsets_chain states the same arithmetic
+// sequentially (the host mirror).  The blocks of rank r are blocks rb[r] .. rb[r + 1) of the chain.
+__global__ void __launch_bounds__(256) seq_shard_offsets(SeqSumBuf b, const double* __restrict__ recv, int64_t stride,
+                                                         int64_t nb_slot, int rank, int world) {
+    __shared__ double s_sum[kScanWin], s_abs[kScanWin];
+    __shared__ double s_vw[256 / 64];
+    __shared__ int64_t s_rb[65];
+    __shared__ double s_off0, s_var0;
     const int c = blockIdx.x;
-    const int64_t n = *d_n;
-    const int nb = (int)((n + kSeqBlock - 1) / kSeqBlock);
-    double* o = out + kSeqTotHdr + (size_t)c * 2 * nb_slot;
-    for (int j = threadIdx.x; j < nb && j < nb_slot; j += 256) {
-        o[2 * j] = b.bsum[(size_t)c * b.nblk + j];
-        o[2 * j + 1] = b.babs[(size_t)c * b.nblk + j];
-    }
-    if (c == 0 && threadIdx.x == 0) out[0] = (double)n;
-}
-
-// every window's place in the chains (seq_shard_offsets_chain, lio_seqsum.hpp) for this rank's window
-__global__ void __launch_bounds__(64) seq_shard_offsets(SeqSumBuf b, int nch, const double* __restrict__ recv,
-                                                        int64_t stride, int64_t nb_slot, int rank, int world) {
-    const int c = threadIdx.x;
-    if (c >= nch) return;
     SeqShard* sh = b.sh;
-    double off0, var0;
-    int fl;
-    int64_t gb, ng;
-    seq_shard_offsets_chain(recv, stride, nb_slot, rank, world, c, off0, var0, fl, gb, ng);
-    sh->off0[c] = off0;
-    sh->var0[c] = var0;
-    sh->floor_e[c] = fl;
-    if (c == 0) {
-        sh->gbase = gb;
-        sh->n_global = ng;
-        sh->n32 = (uint32_t)ng;
+    if (threadIdx.x == 0) {
+        int64_t g = 0, pos = 0;
+        for (int r = 0; r < world; ++r) {
+            const int64_t nr = (int64_t)recv[(size_t)r * (size_t)stride];
+            s_rb[r] = g;
+            if (r == rank && c == 0) sh->gbase = pos;
+            g += min((nr + kSeqBlock - 1) / kSeqBlock, nb_slot);
+            pos += nr;
+        }
+        s_rb[world] = g;
+        if (c == 0) {
+            sh->n_global = pos;
+            sh->n32 = (uint32_t)pos;
+        }
+        s_off0 = 0.0;
+        s_var0 = 0.0;
+    }
+    __syncthreads();
+    const int64_t G = s_rb[world], gmine = s_rb[rank];
+    double off = 0.0, mb = 0.0, var = 0.0;
+    constexpr int kPerT = kScanWin / 256;
+    for (int64_t w0 = 0; w0 < G; w0 += kScanWin) {
+        const int m = (int)min((int64_t)kScanWin, G - w0);
+        for (int j = threadIdx.x; j < m; j += blockDim.x) {
+            const int64_t g = w0 + j;
+            int r = 0;
+            while (s_rb[r + 1] <= g) ++r;
+            const double* bl = recv + (size_t)r * (size_t)stride + kSeqTotHdr + (size_t)c * 2 * nb_slot;
+            s_sum[j] = bl[2 * (g - s_rb[r])];
+            s_abs[j] = bl[2 * (g - s_rb[r]) + 1];
+        }
+        __syncthreads();
+        double o[kPerT], loc[kPerT], run = 0.0;
+#pragma unroll
+        for (int i = 0; i < kPerT; ++i) {
+            const int j = (int)threadIdx.x * kPerT + i;
+            loc[i] = run;
+            run = run + (j < m ? s_sum[j] : 0.0);
+        }
+        double tot;
+        const double ex = block_excl(run, s_vw, tot);
+        double vrun = 0.0, vloc[kPerT];
+#pragma unroll
+        for (int i = 0; i < kPerT; ++i) {
+            const int j = (int)threadIdx.x * kPerT + i;
+            o[i] = off + (ex + loc[i]);
+            const double big = j < m ? fabs(o[i]) + s_abs[j] : 0.0;
+            if (j < m) mb = fmax(mb, big);
+            const double hu = half_ulp_f32(big);
+            vloc[i] = vrun;
+            vrun = vrun + (j < m ? (double)kSeqBlock * hu * hu : 0.0);
+        }
+        double vtot;
+        const double vex = block_excl(vrun, s_vw, vtot);
+#pragma unroll
+        for (int i = 0; i < kPerT; ++i) {
+            const int64_t g = w0 + (int64_t)threadIdx.x * kPerT + i;
+            if (g == gmine && g < w0 + m) {  // this window's first block: its prefix and variance
+                s_off0 = o[i];
+                s_var0 = var + (vex + vloc[i]);
+            }
+        }
+        off = off + tot;
+        var = var + vtot;
+        __syncthreads();
+    }
+    {
+        __shared__ double s_mb[256 / 64];
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) mb = fmax(mb, __shfl_xor(mb, d, 64));
+        if ((threadIdx.x & 63) == 0) s_mb[threadIdx.x >> 6] = mb;
+        __syncthreads();
+        mb = fmax(fmax(s_mb[0], s_mb[1]), fmax(s_mb[2], s_mb[3]));
+    }
+    if (threadIdx.x == 0) {
+        sh->off0[c] = gmine >= G ? off : s_off0;  // a window without blocks: everything before it
+        sh->var0[c] = gmine >= G ? var : s_var0;
+        sh->floor_e[c] = mb > 0.0 ? ilogb(mb) - 27 : -200;
     }
 }
 
@@ -716,10 +788,16 @@ __global__ void __launch_bounds__(64) seq_shard_offsets(SeqSumBuf b, int nch, co
 // travels cut: every rank sees its count and seq_shard_merge flags it.  One block per chain.
 template <class Src>
 __global__ void __launch_bounds__(256) seq_shard_pack(Src src, SeqSumBuf b, const uint32_t* d_n, double* __restrict__ msg,
-                                                      int slot) {
+                                                      int slot, int nhead) {
     const int c = blockIdx.x;
     const int64_t n = *d_n;
-    const int nev = b.floor_e[b.nch + c];  // this window's events (seq_scan2)
+    // heads (nhead > 0): the first nhead elements of every chain after the events, float, chain-major (a depth block
+    // that starts in one window may end in the next: seq_shard_merge appends them after that window)
+    if (nhead > 0) {
+        float* h = reinterpret_cast<float*>(msg + kSeqHdrWords + (size_t)b.nch * 2 * slot) + (size_t)c * nhead;
+        for (int j = threadIdx.x; j < nhead; j += 256) h[j] = j < n ? src(c, j) : 0.f;
+    }
+    const int nev = b.sh->nev_loc[c];  // this window's events (seq_scan2)
     if (threadIdx.x == 0) {
         if (c == 0) {
             msg[0] = __longlong_as_double((long long)n);
@@ -727,7 +805,7 @@ __global__ void __launch_bounds__(256) seq_shard_pack(Src src, SeqSumBuf b, cons
             b.sh->max_nev = 0;  // seq_shard_merge's outputs for this exchange
             b.sh->xflags = 0u;
         }
-        msg[2 + c] = __longlong_as_double((long long)b.ptot[c]);
+        msg[2 + c] = __longlong_as_double((long long)b.sh->ptot_loc[c]);
         msg[2 + kSeqMaxChains + c] = __longlong_as_double((long long)nev);
         msg[2 + 2 * kSeqMaxChains + c] = n > 0 ? (double)src(c, 0) : 0.0;
     }
@@ -748,7 +826,9 @@ __global__ void __launch_bounds__(256) seq_shard_pack(Src src, SeqSumBuf b, cons
 // the chain's overflow bit (the walk and the verification skip it; the caller re-exchanges or falls back).
 // One block per chain.
 __global__ void __launch_bounds__(256) seq_shard_merge(SeqSumBuf b, const uint32_t* d_n, const double* __restrict__ recv,
-                                                       int64_t stride, int rank, int world, int slot) {
+                                                       int64_t stride, int rank, int world, int slot, int nhead,
+                                                       float* __restrict__ ext, int64_t ext_stride, float* __restrict__ ghead,
+                                                       int nghead) {
     __shared__ int s_eoff[65];
     __shared__ uint64_t s_poff[65];
     __shared__ int64_t s_pos[65];
@@ -770,6 +850,29 @@ __global__ void __launch_bounds__(256) seq_shard_merge(SeqSumBuf b, const uint32
         }
     }
     __syncthreads();
+    if (nhead > 0 && ext) {
+        // the elements after this window: the next ranks' heads in order, up to nhead, appended at ext[c][n ..];
+        // the chain's first nghead elements -> ghead[c][..]
+        const int64_t nw = *d_n;
+        int64_t got = 0;
+        for (int r = rank + 1; r < world && got < nhead; ++r) {  // block-uniform
+            const double* m = recv + (size_t)r * (size_t)stride;
+            const int64_t nr = seq_bits(m[0]);
+            const int64_t take = min(min(nr, (int64_t)nhead), (int64_t)nhead - got);
+            const float* h = reinterpret_cast<const float*>(m + kSeqHdrWords + (size_t)b.nch * 2 * slot) + (size_t)c * nhead;
+            for (int64_t j = threadIdx.x; j < take; j += 256) ext[(size_t)c * ext_stride + nw + got + j] = h[j];
+            got += take;
+        }
+        int64_t g = 0;
+        for (int r = 0; r < world && g < nghead; ++r) {
+            const double* m = recv + (size_t)r * (size_t)stride;
+            const int64_t nr = seq_bits(m[0]);
+            const int64_t take = min(min(nr, (int64_t)nhead), (int64_t)nghead - g);
+            const float* h = reinterpret_cast<const float*>(m + kSeqHdrWords + (size_t)b.nch * 2 * slot) + (size_t)c * nhead;
+            for (int64_t j = threadIdx.x; j < take; j += 256) ghead[(size_t)c * nghead + g + j] = h[j];
+            g += take;
+        }
+    }
     if (s_bad) return;
     for (int r = 0; r < world; ++r) {
         const double* ev = recv + (size_t)r * (size_t)stride + kSeqHdrWords + (size_t)c * 2 * slot;
@@ -782,12 +885,19 @@ __global__ void __launch_bounds__(256) seq_shard_merge(SeqSumBuf b, const uint32
             b.ev_x[d] = __uint_as_float((uint32_t)(w >> 32));
         }
     }
-    // this window's block offsets: global (its rank's place in the lists)
+    // this window's block offsets: global (its rank's place in the lists; after a re-exchange only the change)
     const int64_t n = *d_n;
     const int nb = (int)((n + kSeqBlock - 1) / kSeqBlock);
+    const int de = s_eoff[rank] - sh->e_added[c];
+    const uint64_t dp = s_poff[rank] - sh->p_added[c];
     for (int j = threadIdx.x; j < nb; j += 256) {
-        b.bEoff[(size_t)c * b.nblk + j] += s_eoff[rank];
-        b.bPoff[(size_t)c * b.nblk + j] += s_poff[rank];
+        b.bEoff[(size_t)c * b.nblk + j] += de;
+        b.bPoff[(size_t)c * b.nblk + j] += dp;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        sh->e_added[c] = s_eoff[rank];
+        sh->p_added[c] = s_poff[rank];
     }
 }
 
@@ -832,17 +942,17 @@ void seqsum_shard_head(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& 
         (void)hipMemsetAsync(b.forced, 0, (size_t)nch * (b.nmax / 32 + 1) * sizeof(uint32_t), st);
         b.forced_dirty = false;
     }
-    seq_bsum<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n);
-    seq_shard_totals<<<nch, 256, 0, st>>>(b, d_n, tot_out, nb_slot);
+    seq_bsum<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, tot_out, nb_slot);
 }
 
 // after the totals exchange (pass 1) or straight away (pass > 1): offsets, counts, local events, the message
 template <class Src>
 void seqsum_shard_mid(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, const double* tot_recv,
-                      int64_t tot_stride, int64_t nb_slot, int rank, int world, double* msg_out, int slot, hipStream_t st) {
+                      int64_t tot_stride, int64_t nb_slot, int rank, int world, double* msg_out, int slot, int nhead,
+                      hipStream_t st) {
     const dim3 g(b.nblk, nch);
     if (pass <= 1) {
-        seq_shard_offsets<<<1, 64, 0, st>>>(b, nch, tot_recv, tot_stride, nb_slot, rank, world);
+        seq_shard_offsets<<<nch, 256, 0, st>>>(b, tot_recv, tot_stride, nb_slot, rank, world);
         seq_scan1<<<nch, 256, 0, st>>>(b, d_n, pass);
     } else {
         b.forced_dirty = true;  // the failures that led here set forced bits
@@ -851,32 +961,33 @@ void seqsum_shard_mid(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b
     seq_count<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
     seq_scan2<<<nch, kSeqThreads, 0, st>>>(b, d_n);
     seq_events<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
-    seq_shard_pack<Src><<<nch, 256, 0, st>>>(src, b, d_n, msg_out, slot);
+    seq_shard_pack<Src><<<nch, 256, 0, st>>>(src, b, d_n, msg_out, slot, nhead);
 }
 
 // after the event exchange: the global lists, the walk over all of them, the window's verification
 template <class Src>
 void seqsum_shard_tail(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, const double* msg_recv,
-                       int64_t msg_stride, int rank, int world, int slot, hipStream_t st) {
+                       int64_t msg_stride, int rank, int world, int slot, const SeqHeads& hd, hipStream_t st) {
     const dim3 g(b.nblk, nch);
-    seq_shard_merge<<<nch, 256, 0, st>>>(b, d_n, msg_recv, msg_stride, rank, world, slot);
+    seq_shard_merge<<<nch, 256, 0, st>>>(b, d_n, msg_recv, msg_stride, rank, world, slot, hd.nhead, hd.ext,
+                                         hd.ext_stride, hd.ghead, hd.nghead);
     seq_walk<Src><<<nch, kWalkThreads, 0, st>>>(src, b, d_n);
     seq_verify<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
 }
 
 template <class Src>
 void seqsum_shard_repack(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, double* msg_out, int slot,
-                         hipStream_t st) {
-    seq_shard_pack<Src><<<nch, 256, 0, st>>>(src, b, d_n, msg_out, slot);
+                         int nhead, hipStream_t st) {
+    seq_shard_pack<Src><<<nch, 256, 0, st>>>(src, b, d_n, msg_out, slot, nhead);
 }
 
 #define LIO_SEQ_SHARD_INST(S)                                                                                      \
     template void seqsum_shard_head<S>(const S&, int, const uint32_t*, SeqSumBuf&, double*, int64_t, hipStream_t); \
     template void seqsum_shard_mid<S>(const S&, int, const uint32_t*, SeqSumBuf&, int, const double*, int64_t,     \
-                                      int64_t, int, int, double*, int, hipStream_t);                               \
+                                      int64_t, int, int, double*, int, int, hipStream_t);                          \
     template void seqsum_shard_tail<S>(const S&, int, const uint32_t*, SeqSumBuf&, int, const double*, int64_t, int, \
-                                       int, int, hipStream_t);                                                     \
-    template void seqsum_shard_repack<S>(const S&, int, const uint32_t*, SeqSumBuf&, double*, int, hipStream_t);
+                                       int, int, const SeqHeads&, hipStream_t);                                    \
+    template void seqsum_shard_repack<S>(const S&, int, const uint32_t*, SeqSumBuf&, double*, int, int, hipStream_t);
 LIO_SEQ_SHARD_INST(SeqPairs)
 LIO_SEQ_SHARD_INST(SeqSigma)
 #undef LIO_SEQ_SHARD_INST

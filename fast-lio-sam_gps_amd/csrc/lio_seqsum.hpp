@@ -22,7 +22,7 @@
 // Sharded (SeqSumBuf::sh != nullptr): the chain's elements are split over ranks in order, this rank holding
 // the window [gbase, gbase + n) (lio_icp_host.cpp, the loop ICP over several GPUs).  Every rank predicts,
 // counts and lists the events of its own window — from the double prefix of the elements before it and a
-// binade floor common to all ranks (seq_shard_totals -> all-gather -> seq_shard_offsets) — the event lists
+// binade floor common to all ranks (seq_bsum's block sums -> all-gather -> seq_shard_offsets) — the event lists
 // are all-gathered (seq_shard_pack -> all-gather -> seq_shard_merge: global positions and increment prefixes),
 // every rank walks ALL events (the serial floor, redundantly), and verifies its own window.  The result is the
 // sequential chain on every rank, whatever the window split, because the verification covers every element.
@@ -49,9 +49,16 @@ struct SeqShard {
     uint32_t n32;                 // the same as a 32-bit count (the PCL kernels' d_n of the whole chain)
     uint32_t xflags;              // exchange: bit 0 an event list longer than the slot, bit 1 global capacity
     int max_nev;                  // largest per-rank per-chain event count of the last merge
+    // the window's own lists (seq_scan2; the merge overwrites the SeqSumBuf copies with the chain's global ones, and
+    // a re-exchange packs the same lists again) and what the last merge added to its block offsets (a re-exchange
+    // merges again: the offsets move by the difference only)
+    int nev_loc[kSeqMaxChains];
+    uint64_t ptot_loc[kSeqMaxChains];
+    int e_added[kSeqMaxChains];
+    uint64_t p_added[kSeqMaxChains];
 };
 
-// exchange message layout (doubles): block sums (seq_shard_totals: [0] the window's element count, then per chain
+// exchange message layout (doubles): block sums (seq_bsum's tot_out: [0] the window's element count, then per chain
 // `nb_slot` pairs (block double sum, block sum |x|) of its kSeqBlock-element blocks), event lists (seq_shard_pack)
 constexpr int kSeqTotHdr = 8;
 constexpr int kSeqHdrWords = 32;                     // event message header: n, flags, ptot[9], nev[9], x0[9]
@@ -79,7 +86,11 @@ __host__ __device__ inline double seq_half_ulp_f32(double v) {
 // window's starting prefix and drift variance, the chain's common floor, the window's first global index and the
 // chain's length: the formulas of seq_scan1 run over every window's blocks in chain order (offset, bound
 // |offset| + block sum |x|, variance + kSeqBlock (ulp / 2)^2 per block), so a window's predictions are as good as
-// one rank's.  The device (seq_shard_offsets) and the host mirror (lio_seq_shard_offsets) run this same code.
+// one rank's.  This is the host mirror (lio_seq_shard_offsets); the device's seq_shard_offsets computes the same
+// quantities with the prefix re-associated (seq_scan1's block prefix over windows of 2048 blocks, one workgroup per
+// chain), so its off0 / var0 may differ from these in the last bits: every rank runs that kernel over the same
+// gathered bytes, so the floors and prefixes agree across ranks bit for bit, which is all the predictions need
+// (they are checked by the verification either way).
 __host__ __device__ inline void seq_shard_offsets_chain(const double* recv, int64_t stride, int64_t nb_slot, int rank,
                                                         int world, int c, double& off0, double& var0, int& floor_e,
                                                         int64_t& gbase, int64_t& n_global) {
@@ -234,25 +245,38 @@ template <class Src>
 void seqsum_launch(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, hipStream_t st);
 
 // Sharded pass, in three enqueued pieces around the caller's two all-gathers:
-//   seqsum_shard_head  pass 1: block sums -> tot_out (seq_tot_words(nch, nb_slot) doubles)
+//   seqsum_shard_head  pass 1: block sums (also -> tot_out, seq_tot_words(nch, nb_slot) doubles)
 //   seqsum_shard_mid   pass 1: seq_shard_offsets over the gathered block sums (rank `rank` of `world`, ranks'
 //                      messages tot_stride doubles apart); every pass: count, block offsets, local events,
 //                      the event message -> msg_out (kSeqHdrWords + nch * 2 * slot doubles)
 //   seqsum_shard_tail  seq_shard_merge over the gathered messages, the walk over all events, the verification
 //                      of the window
+// heads (nhead > 0): the event message also carries the first nhead elements of each chain (floats, after the
+// events); the merge appends the next ranks' heads after the window at ext[c * ext_stride + n ..] and the chain's
+// first nghead elements at ghead[c * nghead ..] (the PCL depth blocks that cross a window boundary)
+struct SeqHeads {
+    int nhead = 0;
+    float* ext = nullptr;
+    int64_t ext_stride = 0;
+    float* ghead = nullptr;
+    int nghead = 0;
+};
 template <class Src>
 void seqsum_shard_head(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, double* tot_out, int64_t nb_slot,
                        hipStream_t st);
 template <class Src>
 void seqsum_shard_mid(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, const double* tot_recv,
-                      int64_t tot_stride, int64_t nb_slot, int rank, int world, double* msg_out, int slot, hipStream_t st);
+                      int64_t tot_stride, int64_t nb_slot, int rank, int world, double* msg_out, int slot, int nhead,
+                      hipStream_t st);
 template <class Src>
 void seqsum_shard_tail(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, const double* msg_recv,
-                       int64_t msg_stride, int rank, int world, int slot, hipStream_t st);
+                       int64_t msg_stride, int rank, int world, int slot, const SeqHeads& hd, hipStream_t st);
 // the event message again with another slot (the local lists are unchanged; the caller clears status[1])
 template <class Src>
 void seqsum_shard_repack(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, double* msg_out, int slot,
-                         hipStream_t st);
-inline int64_t seqsum_msg_words(int nch, int slot) { return kSeqHdrWords + (int64_t)nch * 2 * slot; }
+                         int nhead, hipStream_t st);
+inline int64_t seqsum_msg_words(int nch, int slot, int nhead = 0) {
+    return kSeqHdrWords + (int64_t)nch * 2 * slot + ((int64_t)nch * nhead + 1) / 2;
+}
 
 }  // namespace lio

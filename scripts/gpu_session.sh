@@ -40,10 +40,17 @@ for s in $STEPS; do
     spawn2) LIO_BENCH_REHEARSE=1 run spawn2 500 python bench.py --gpus 2 --steps 50 --warmup 5 --pipeline 0 --no-cpu --streams '' --icp-reps 2 ;;
     map)   runs pytest_map 900 python -u -m pytest tests/test_gpu_map.py tests/test_gpu_fullsize.py -x -v -p no:cacheprovider --timeout 600 --timeout-method thread ;;
     shardt) runs pytest_shard 900 python -u -m pytest tests/test_gpu_icp.py tests/test_gpu_fullsize.py tests/test_gpu_dist.py -k "group or exchange or emulated or multiprocess or recovery or timeout" -x -v -s -p no:cacheprovider --timeout 600 --timeout-method thread ;;
-    shardprof) run shardprof4 300 python scripts/icp_shard_profile.py 4 3 B &&
+    shardprof) run shardprof4 300 env LIO_FSH_TRACE=1 python scripts/icp_shard_profile.py 4 3 B &&
                run shardprof8 300 python scripts/icp_shard_profile.py 8 2 B &&
                run shardtrace 300 rocprofv3 --kernel-trace --stats -d "$OUT/shardtrace" -o run --output-format csv -- python scripts/icp_shard_profile.py 4 2 B &&
                python scripts/icp_shard_kernels.py "$OUT/shardtrace/run_kernel_trace.csv" "$OUT/shard_kernels.txt" ;;
+    shardrep) for wr in "4 1" "8 7"; do
+                  set -- $wr
+                  run shardrec$1 300 python scripts/icp_shard_replay.py record $1 $2 /tmp/rec$1.npz B &&
+                  run shardrep$1 300 python scripts/icp_shard_replay.py replay $1 $2 /tmp/rec$1.npz 5 &&
+                  run shardreptrace$1 300 rocprofv3 --kernel-trace --stats -d "$OUT/shardrep$1" -o run --output-format csv -- python scripts/icp_shard_replay.py replay $1 $2 /tmp/rec$1.npz 3 &&
+                  python scripts/icp_shard_kernels.py "$OUT/shardrep$1/run_kernel_trace.csv" "$OUT/shardrep_kernels$1.txt"
+              done ;;
     lseqt) runs pytest_lseq 600 python -u -m pytest tests/test_cpp_stream.py tests/test_gpu_parity.py -k "loop_sequence or guard" -x -v -s -p no:cacheprovider --timeout 500 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     loopseqprof) run loopseqprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/loopseqprof" -o run --output-format csv -- fast-lio-sam_gps_amd/lio_gpu/_lib/loop_sequence /tmp/ls.bin &&

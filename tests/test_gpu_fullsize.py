@@ -178,6 +178,9 @@ def test_icp_c4_emulated_ranks_bit_identical(oracle, world, disp):
         assert r is not None
         np.testing.assert_array_equal(np.array(list(r.T), np.float32), T1)
         assert r.score == r1.score and r.iterations == r1.iterations
+    # the re-passes and re-exchanges recover on the sharded path as on one rank: no serial fallback
+    if single.fidelity_stats()["serial"] == 0:
+        assert all(lc.fidelity_stats()["serial"] == 0 for lc in lcs), [lc.fidelity_stats() for lc in lcs]
     o = oracle.icp_align(src, dst)  # float order 2 (oracle default)
     assert r1.iterations == o["iterations"] and r1.state == o["state"]
     np.testing.assert_allclose(T1.reshape(4, 4), o["T"], atol=1e-5)
