@@ -308,6 +308,8 @@ struct lio_icp {
     float* d_src = nullptr;
     float* d_cur = nullptr;
     float* d_thist = nullptr;  // transforms applied this alignment (the correspondence kernel's history)
+    uint8_t* d_edist = nullptr;  // the target's empty-space map (2 x edist_cap bytes: map + pass scratch)
+    int64_t edist_cap = 0;
     int thist_cap = 0, nT = 0;
     float* d_fd2 = nullptr;
     int* d_fid = nullptr;
@@ -456,8 +458,8 @@ int lio_icp_destroy(lio_icp* h) {
     lio_icp_set_exchange_owner(h, nullptr, nullptr);
     lio::grid_free(h->tgt);
     lio::grid_free(h->qgrid);
-    void* ptrs[] = {h->d_thist, h->d_tgt, h->d_src,   h->d_cur,   h->d_fd2,  h->d_fid, h->d_tiles, h->d_tscratch,
-                    h->d_ttmp,  h->d_dbg, h->d_tcost, h->d_order, h->d_pcl16};
+    void* ptrs[] = {h->d_edist, h->d_thist, h->d_tgt,   h->d_src,   h->d_cur,   h->d_fd2,  h->d_fid,
+                    h->d_tiles, h->d_tscratch, h->d_ttmp, h->d_dbg, h->d_tcost, h->d_order, h->d_pcl16};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     lio::pcl_free(h->pg);
@@ -555,6 +557,17 @@ static int target_build(lio_icp* h) {
     IHIP(hipMemcpyAsync(h->d_tgt, h->h_tgt, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice, h->st2));
     int rc = lio::grid_build(h->tgt, h->d_tgt, n, h->p.cell_size, h->st2);
     if (rc) return ifail(rc == -5 ? LIO_ERR_NOMEM : LIO_ERR_HIP, "target grid build failed");
+    const int64_t nc = h->tgt.geom.ncells;
+    if (nc > h->edist_cap) {
+        if (h->d_edist) IHIP(hipFree(h->d_edist));
+        h->d_edist = nullptr;
+        const int64_t c = std::max<int64_t>(std::max(nc + nc / 2, 2 * h->edist_cap), h->tgt.min_cells);
+        h->edist_cap = 0;
+        lio::count_alloc();
+        IHIP(hipMalloc(&h->d_edist, (size_t)c * 2));
+        h->edist_cap = c;
+    }
+    lio::launch_icp_empty_dist(h->tgt, h->d_edist + h->edist_cap, h->d_edist, h->st2);
     IHIP(hipStreamSynchronize(h->st2));
     // fixed accumulation centre: target bounding-box centre (float)
     const float* bb = h->tgt.aabb_host;
@@ -981,10 +994,12 @@ static int fsh_serial(lio_icp* h, const lio::IcpArgs& a, bool lb_timeout) {
 }
 
 // the per-rank event slot for the next exchange: 1.5 x the longest list of this one (every rank saw the same
-// lists, so every rank picks the same slot), at least 1024, at most the capacity
-static int next_slot(const lio_icp* h, int longest) {
+// lists, so every rank picks the same slot), at least 1024, at most the capacity, and never below the current
+// slot (a pass-1 list is longer than a later pass's: a slot that shrank in between would make every alignment's
+// first pass re-exchange)
+static int next_slot(const lio_icp* h, int longest, int cur) {
     const int64_t want = ((int64_t)longest * 3 / 2 + 256 + 255) / 256 * 256;
-    return (int)std::min<int64_t>(std::max<int64_t>(want, 1024), ev_slot_cap(h->ns, h->world));
+    return (int)std::min<int64_t>(std::max<int64_t>(std::max<int64_t>(want, 1024), cur), ev_slot_cap(h->ns, h->world));
 }
 
 // pcl_finish for the sharded modes: the same re-pass policy (the statuses are every rank's, combined), plus a
@@ -1009,8 +1024,8 @@ static int pcl_finish_fsh(lio_icp* h, const lio::IcpArgs& a) {
         if (trace)
             std::fprintf(stderr, "fsh rank %d: bad %x over %x xflags %x longest %d/%d mpass %d spass %d slot %d\n", h->rank,
                          bad, over, xf, mm, ms, mpass, spass, h->ev_slot);
-        h->ev_slot = next_slot(h, mm);
-        if (order == 1 && ms > 0) h->ev_slot_s = next_slot(h, ms);
+        h->ev_slot = next_slot(h, mm, h->ev_slot);
+        if (order == 1 && ms > 0) h->ev_slot_s = next_slot(h, ms, h->ev_slot_s);
         if ((bad | over) == 0) break;
         if (bad) P.means.forced_dirty = P.sig.forced_dirty = true;
         const bool hard = (xf & (2u | 4u | 0x200u)) != 0;
@@ -1127,6 +1142,7 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     // first bound box: the tile's own cells (r0 = 0; with the per-batch bound and the centre-out rows, pair A
     // 0.221 -> 0.212 ms per alignment against r0 = 1, pair B unchanged: profiles/r05_icp_r0_ab.txt)
     a.r0 = 0;
+    a.edist = h->d_edist;  // tiles without a candidate start at the nearest occupied cell's distance
     a.nn_d2 = h->d_fd2;
     a.nn_id = h->d_fid;
     a.qpts = h->qgrid.pts;

@@ -338,42 +338,40 @@ __global__ void pcl_x3_header_kernel(const uint32_t* __restrict__ st_means, cons
     msg[5] = 0.0;
 }
 
-// every rank's depth blocks into Cbg (global order), the statuses OR-ed: merged = {means bad, means overflow,
-// sigma bad, sigma overflow, look-back}; the overflow words are the seqsum merges' (already global); out[20..22]
+// every rank's depth blocks into Cbg (global order; block r copies rank r's), the statuses OR-ed (block 0):
+// merged = {means bad, means overflow, sigma bad, sigma overflow, look-back}; the overflow words are the seqsum
+// merges' (already global); out[20..22]
 __global__ void __launch_bounds__(256) pcl_x3_merge_kernel(const double* __restrict__ recv, int64_t stride, int world,
                                                            float* __restrict__ Cbg, int64_t Cbg_cap,
                                                            const uint32_t* __restrict__ over_means,
                                                            const uint32_t* __restrict__ over_sig,
                                                            const SeqShard* __restrict__ shm, const SeqShard* __restrict__ shs,
                                                            uint32_t* __restrict__ merged, float* __restrict__ out) {
-    __shared__ uint32_t s_or[4];
-    if (threadIdx.x < 4) s_or[threadIdx.x] = 0u;
-    __syncthreads();
-    for (int r = 0; r < world; ++r) {
-        const double* m = recv + (size_t)r * (size_t)stride;
-        if (threadIdx.x == 0) {
-            s_or[0] |= (uint32_t)m[0];
-            s_or[1] |= (uint32_t)m[1];
-            s_or[2] |= (uint32_t)m[2];
-            s_or[3] |= (uint32_t)m[5];
-        }
+    {
+        const double* m = recv + (size_t)blockIdx.x * (size_t)stride;
         const int64_t q0 = (int64_t)m[3], nq = (int64_t)m[4];
         const float* cb = reinterpret_cast<const float*>(m + kPclX3Hdr);
         for (int64_t e = threadIdx.x; e < 9 * nq; e += 256)
             if (q0 * 9 + e < 9 * Cbg_cap) Cbg[q0 * 9 + e] = cb[e];
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        merged[0] = s_or[0];
-        merged[1] = over_means[1] | (s_or[3] ? 0x3fu : 0u);
-        merged[2] = s_or[1];
-        merged[3] = over_sig ? over_sig[1] : 0u;
-        merged[4] = s_or[2];
-        const uint32_t xf = (shm ? shm->xflags : 0u) | (shs ? shs->xflags << 8 : 0u) | (s_or[3] ? 4u : 0u);
-        out[20] = __uint_as_float(xf);
-        out[21] = __int_as_float(shm ? shm->max_nev : 0);
-        out[22] = __int_as_float(shs ? shs->max_nev : 0);
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    uint32_t o0 = 0u, o1 = 0u, o2 = 0u, o3 = 0u;
+    for (int r = 0; r < world; ++r) {
+        const double* m = recv + (size_t)r * (size_t)stride;
+        o0 |= (uint32_t)m[0];
+        o1 |= (uint32_t)m[1];
+        o2 |= (uint32_t)m[2];
+        o3 |= (uint32_t)m[5];
     }
+    merged[0] = o0;
+    merged[1] = over_means[1] | (o3 ? 0x3fu : 0u);
+    merged[2] = o1;
+    merged[3] = over_sig ? over_sig[1] : 0u;
+    merged[4] = o2;
+    const uint32_t xf = (shm ? shm->xflags : 0u) | (shs ? shs->xflags << 8 : 0u) | (o3 ? 4u : 0u);
+    out[20] = __uint_as_float(xf);
+    out[21] = __int_as_float(shm ? shm->max_nev : 0);
+    out[22] = __int_as_float(shs ? shs->max_nev : 0);
 }
 
 __global__ void __launch_bounds__(256) pcl_gather_pack_kernel(const float* __restrict__ pairs, int64_t cap,
@@ -468,7 +466,7 @@ void launch_pcl_sigma_shard(PclBuf& p, int order, double* msg3, int64_t nq_slot,
 void launch_pcl_x3_merge(PclBuf& p, int order, const double* recv, int64_t stride, int world, int64_t nq_slot,
                          float* out, hipStream_t st) {
     (void)nq_slot;
-    pcl_x3_merge_kernel<<<1, 256, 0, st>>>(recv, stride, world, p.Cbg, p.Cbg_cap, p.means.status,
+    pcl_x3_merge_kernel<<<world, 256, 0, st>>>(recv, stride, world, p.Cbg, p.Cbg_cap, p.means.status,
                                            order == 1 ? p.sig.status : nullptr, p.means.sh,
                                            order == 1 ? p.sig.sh : nullptr, p.merged, out);
 }

@@ -495,25 +495,33 @@ struct WalkChunk {
     int fast[kWalkChunk / 64];
 };
 
-// chunk k's records into B by the threads [t0, t0 + nt) (nt a multiple of 64, t0 wave-aligned)
+// chunk k's records into B by the threads [t0, t0 + nt) (nt a multiple of 64, t0 wave-aligned, nt >= 192): every
+// load of the thread's share is issued before the first is used (the preparation runs beside the walk and must
+// stay shorter than it: one round trip to memory per chunk, not one per step)
+constexpr int kPrepMax = (kWalkChunk + 191) / 192;
 __device__ __forceinline__ void walk_prepare(WalkChunk& B, int k, int nev, double unit, const uint64_t* EP,
                                              const float* EX, int t, int nt) {
     const int e0 = k * kWalkChunk;
     const int m = min(kWalkChunk, nev - e0);
-    for (int j = t; j < kWalkChunk; j += nt) {  // wave-uniform trip count: one 64-event group per wave and step
-        const int i = e0 + j;
-        double R = 0.0;
-        float X = 0.f;
-        if (j < m) {
-            const uint64_t P = EP[i];
-            const uint64_t Pp = i > 0 ? EP[i - 1] : 0;
-            R = (double)(int64_t)(P - Pp) * unit;  // a run sum: exact (<= 53 significant bits)
-            X = EX[i];
-        }
+    uint64_t P[kPrepMax], Pp[kPrepMax];
+    float X[kPrepMax];
+#pragma unroll
+    for (int q = 0; q < kPrepMax; ++q) {
+        const int j = t + q * nt, i = e0 + j;
+        const bool in = j < m;
+        P[q] = in ? EP[i] : 0;
+        Pp[q] = in && i > 0 ? EP[i - 1] : 0;
+        X[q] = in ? EX[i] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < kPrepMax; ++q) {
+        const int j = t + q * nt;
+        if (j >= kWalkChunk) break;  // wave-uniform: one 64-event group per wave and step
+        const double R = j < m ? (double)(int64_t)(P[q] - Pp[q]) * unit : 0.0;  // a run sum: exact (<= 53 bits)
         const float Rf = (float)R;
         B.R[j] = R;
         B.Rf[j] = Rf;
-        B.x[j] = X;
+        B.x[j] = X[q];
         // a float exactly, and normal or zero (no denormal operand on the fast path)
         const uint64_t all = __ballot((double)Rf == R && (Rf == 0.f || fabsf(Rf) >= 1.17549435e-38f));
         if ((threadIdx.x & 63) == 0) B.fast[j >> 6] = all == ~0ull;
@@ -699,12 +707,15 @@ __global__ void __launch_bounds__(256) seq_shard_offsets(SeqSumBuf b, const doub
     __shared__ double s_vw[256 / 64];
     __shared__ int64_t s_rb[65];
     __shared__ double s_off0, s_var0;
+    __shared__ int64_t s_n[64];
     const int c = blockIdx.x;
     SeqShard* sh = b.sh;
+    if (threadIdx.x < world) s_n[threadIdx.x] = (int64_t)recv[(size_t)threadIdx.x * (size_t)stride];
+    __syncthreads();
     if (threadIdx.x == 0) {
         int64_t g = 0, pos = 0;
         for (int r = 0; r < world; ++r) {
-            const int64_t nr = (int64_t)recv[(size_t)r * (size_t)stride];
+            const int64_t nr = s_n[r];
             s_rb[r] = g;
             if (r == rank && c == 0) sh->gbase = pos;
             g += min((nr + kSeqBlock - 1) / kSeqBlock, nb_slot);
@@ -833,12 +844,16 @@ __global__ void __launch_bounds__(256) seq_shard_merge(SeqSumBuf b, const uint32
     __shared__ uint64_t s_poff[65];
     __shared__ int64_t s_pos[65];
     __shared__ int s_bad;
+    __shared__ double s_hdr[64 * kSeqHdrWords];  // every rank's header, loaded by all lanes at once
     const int c = blockIdx.x;
     SeqShard* sh = b.sh;
+    for (int e = threadIdx.x; e < world * kSeqHdrWords; e += 256)
+        s_hdr[e] = recv[(size_t)(e / kSeqHdrWords) * (size_t)stride + e % kSeqHdrWords];
+    __syncthreads();
     if (threadIdx.x == 0) {
         float x0;
         int mx;
-        const int bad = seq_shard_merge_chain(recv, stride, world, slot, c, b.evs, s_eoff, s_poff, s_pos, x0, mx);
+        const int bad = seq_shard_merge_chain(s_hdr, kSeqHdrWords, world, slot, c, b.evs, s_eoff, s_poff, s_pos, x0, mx);
         s_bad = bad;
         b.floor_e[b.nch + c] = s_eoff[world];
         b.ptot[c] = s_poff[world];
@@ -857,7 +872,7 @@ __global__ void __launch_bounds__(256) seq_shard_merge(SeqSumBuf b, const uint32
         int64_t got = 0;
         for (int r = rank + 1; r < world && got < nhead; ++r) {  // block-uniform
             const double* m = recv + (size_t)r * (size_t)stride;
-            const int64_t nr = seq_bits(m[0]);
+            const int64_t nr = seq_bits(s_hdr[r * kSeqHdrWords]);
             const int64_t take = min(min(nr, (int64_t)nhead), (int64_t)nhead - got);
             const float* h = reinterpret_cast<const float*>(m + kSeqHdrWords + (size_t)b.nch * 2 * slot) + (size_t)c * nhead;
             for (int64_t j = threadIdx.x; j < take; j += 256) ext[(size_t)c * ext_stride + nw + got + j] = h[j];
@@ -866,7 +881,7 @@ __global__ void __launch_bounds__(256) seq_shard_merge(SeqSumBuf b, const uint32
         int64_t g = 0;
         for (int r = 0; r < world && g < nghead; ++r) {
             const double* m = recv + (size_t)r * (size_t)stride;
-            const int64_t nr = seq_bits(m[0]);
+            const int64_t nr = seq_bits(s_hdr[r * kSeqHdrWords]);
             const int64_t take = min(min(nr, (int64_t)nhead), (int64_t)nghead - g);
             const float* h = reinterpret_cast<const float*>(m + kSeqHdrWords + (size_t)b.nch * 2 * slot) + (size_t)c * nhead;
             for (int64_t j = threadIdx.x; j < take; j += 256) ghead[(size_t)c * nghead + g + j] = h[j];
