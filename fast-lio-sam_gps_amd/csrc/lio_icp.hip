@@ -416,19 +416,6 @@ __device__ __forceinline__ void icp_tile_body(const IcpArgs& a, int tix, int nti
     // 2. final: everything within sqrt(B) of the tile box, minus what was scanned
     CellBox S{1, 0, 1, 0, 1, 0};  // scanned so far (empty)
     int r = a.r0;
-    if (a.edist && __any(act && (uint32_t)best == (uint32_t)kNone)) {
-        // a lane without a candidate: the first box that holds a target point is Q grown by the smallest
-        // empty-space distance over Q's cells (not one ring at a time through the empty cells around it)
-        const int qx = Q.x1 - Q.x0 + 1, qy = Q.y1 - Q.y0 + 1, nq = qx * qy * (Q.z1 - Q.z0 + 1);
-        int dmin = kIcpEdCap + 1;
-        for (int j = lane; j < nq; j += kIcpTileQ) {
-            const int cx = Q.x0 + j % qx, cy = Q.y0 + (j / qx) % qy, cz = Q.z0 + j / (qx * qy);
-            dmin = min(dmin, (int)a.edist[((size_t)cz * g.ny + cy) * g.nx + cx]);
-        }
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) dmin = min(dmin, __shfl_xor(dmin, d, 64));
-        r = max(r, dmin);
-    }
 #ifdef LIO_DIAG
     unsigned long long dg_cand = 0;  // candidates streamed before the final round, final rows
     int dg_rows = 0;
@@ -585,47 +572,6 @@ __global__ void __launch_bounds__(kIcpStatsThreads) icp_stats_kernel(IcpArgs a, 
             for (int w = 0; w < NW; ++w) s += red[w][threadIdx.x];
         super[(size_t)blockIdx.x * kIcpStride + threadIdx.x] = s;
     }
-}
-
-// ---- the target's empty-space map (launch_icp_empty_dist): L-inf distance transforms compose axis by axis,
-// d_xyz(c) = min_z' max(|dz|, min_y' max(|dy|, min_x' |dx|)) over occupied cells, capped at kIcpEdCap + 1
-__global__ void __launch_bounds__(256) icp_edist_x_kernel(const uint32_t* __restrict__ start, int nx, uint32_t ncells,
-                                                          uint8_t* __restrict__ out) {
-    const uint32_t c = blockIdx.x * 256u + threadIdx.x;
-    if (c >= ncells) return;
-    const int x = (int)(c % (uint32_t)nx);
-    const uint32_t row = c - (uint32_t)x;
-    auto occ = [&](int xx) { return start[row + (uint32_t)xx + 1] > start[row + (uint32_t)xx]; };
-    int d = kIcpEdCap + 1;
-    for (int k = 0; k <= kIcpEdCap; ++k)
-        if ((x - k >= 0 && occ(x - k)) || (x + k < nx && occ(x + k))) {
-            d = k;
-            break;
-        }
-    out[c] = (uint8_t)d;
-}
-
-// one axis of the composition: stride / len the axis's cell stride and extent
-__global__ void __launch_bounds__(256) icp_edist_axis_kernel(const uint8_t* __restrict__ in, uint32_t ncells,
-                                                             uint32_t stride, int len, uint8_t* __restrict__ out) {
-    const uint32_t c = blockIdx.x * 256u + threadIdx.x;
-    if (c >= ncells) return;
-    const int p = (int)((c / stride) % (uint32_t)len);
-    int d = in[c];
-    for (int k = 1; k < d; ++k) {  // max(k, .) >= k: nothing at k >= d can improve d
-        if (p - k >= 0) d = min(d, max(k, (int)in[c - (uint32_t)k * stride]));
-        if (p + k < len) d = min(d, max(k, (int)in[c + (uint32_t)k * stride]));
-    }
-    out[c] = (uint8_t)d;
-}
-
-void launch_icp_empty_dist(const GridBuf& g, uint8_t* tmp, uint8_t* out, hipStream_t st) {
-    const GridGeom& m = g.geom;
-    if (m.ncells == 0) return;
-    const int nb = (int)((m.ncells + 255) / 256);
-    icp_edist_x_kernel<<<nb, 256, 0, st>>>(g.start, m.nx, m.ncells, out);
-    icp_edist_axis_kernel<<<nb, 256, 0, st>>>(out, m.ncells, (uint32_t)m.nx, m.ny, tmp);
-    icp_edist_axis_kernel<<<nb, 256, 0, st>>>(tmp, m.ncells, (uint32_t)m.nx * (uint32_t)m.ny, m.nz, out);
 }
 
 // one wave per tile (several waves per tile, or several one-wave tiles per block, measured no faster:

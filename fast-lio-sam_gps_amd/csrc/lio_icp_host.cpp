@@ -308,8 +308,6 @@ struct lio_icp {
     float* d_src = nullptr;
     float* d_cur = nullptr;
     float* d_thist = nullptr;  // transforms applied this alignment (the correspondence kernel's history)
-    uint8_t* d_edist = nullptr;  // the target's empty-space map (2 x edist_cap bytes: map + pass scratch)
-    int64_t edist_cap = 0;
     int thist_cap = 0, nT = 0;
     float* d_fd2 = nullptr;
     int* d_fid = nullptr;
@@ -458,8 +456,8 @@ int lio_icp_destroy(lio_icp* h) {
     lio_icp_set_exchange_owner(h, nullptr, nullptr);
     lio::grid_free(h->tgt);
     lio::grid_free(h->qgrid);
-    void* ptrs[] = {h->d_edist, h->d_thist, h->d_tgt,   h->d_src,   h->d_cur,   h->d_fd2,  h->d_fid,
-                    h->d_tiles, h->d_tscratch, h->d_ttmp, h->d_dbg, h->d_tcost, h->d_order, h->d_pcl16};
+    void* ptrs[] = {h->d_thist, h->d_tgt,   h->d_src,   h->d_cur,   h->d_fd2,  h->d_fid, h->d_tiles,
+                    h->d_tscratch, h->d_ttmp, h->d_dbg, h->d_tcost, h->d_order, h->d_pcl16};
     for (void* q : ptrs)
         if (q) (void)hipFree(q);
     lio::pcl_free(h->pg);
@@ -557,17 +555,6 @@ static int target_build(lio_icp* h) {
     IHIP(hipMemcpyAsync(h->d_tgt, h->h_tgt, (size_t)n * 3 * sizeof(float), hipMemcpyHostToDevice, h->st2));
     int rc = lio::grid_build(h->tgt, h->d_tgt, n, h->p.cell_size, h->st2);
     if (rc) return ifail(rc == -5 ? LIO_ERR_NOMEM : LIO_ERR_HIP, "target grid build failed");
-    const int64_t nc = h->tgt.geom.ncells;
-    if (nc > h->edist_cap) {
-        if (h->d_edist) IHIP(hipFree(h->d_edist));
-        h->d_edist = nullptr;
-        const int64_t c = std::max<int64_t>(std::max(nc + nc / 2, 2 * h->edist_cap), h->tgt.min_cells);
-        h->edist_cap = 0;
-        lio::count_alloc();
-        IHIP(hipMalloc(&h->d_edist, (size_t)c * 2));
-        h->edist_cap = c;
-    }
-    lio::launch_icp_empty_dist(h->tgt, h->d_edist + h->edist_cap, h->d_edist, h->st2);
     IHIP(hipStreamSynchronize(h->st2));
     // fixed accumulation centre: target bounding-box centre (float)
     const float* bb = h->tgt.aabb_host;
@@ -1142,7 +1129,6 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
     // first bound box: the tile's own cells (r0 = 0; with the per-batch bound and the centre-out rows, pair A
     // 0.221 -> 0.212 ms per alignment against r0 = 1, pair B unchanged: profiles/r05_icp_r0_ab.txt)
     a.r0 = 0;
-    a.edist = h->d_edist;  // tiles without a candidate start at the nearest occupied cell's distance
     a.nn_d2 = h->d_fd2;
     a.nn_id = h->d_fid;
     a.qpts = h->qgrid.pts;

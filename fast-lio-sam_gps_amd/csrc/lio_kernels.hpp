@@ -154,14 +154,7 @@ struct IcpArgs {
     const uint32_t* order;  // optional tile visit order (heaviest first, from the previous pass's costs)
     uint32_t* tile_cost;    // per tile: candidates scanned in this pass
     unsigned long long* dbg;  // optional counters (diagnostics): candidates, rings, tiles, lanes, tested
-    const uint8_t* edist;     // per target cell: Chebyshev distance in cells to the nearest occupied one (capped,
-                              // launch_icp_empty_dist) — a tile without candidates starts its box that far out
 };
-
-// The target grid's empty-space map: per cell min(kIcpEdCap + 1, L-inf distance in cells to the nearest
-// non-empty cell), three separable passes (x, then y, then z) over the CSR offsets; tmp and out ncells bytes each
-constexpr int kIcpEdCap = 63;
-void launch_icp_empty_dist(const GridBuf& g, uint8_t* tmp, uint8_t* out, hipStream_t st);
 
 constexpr int kIcpSuper = 4096;    // points per exchanged partial (shard granule)
 constexpr int kIcpStride = 20;     // doubles per record (17 statistics, padded)
