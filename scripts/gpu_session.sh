@@ -51,13 +51,11 @@ for s in $STEPS; do
                   run shardreptrace$1 300 rocprofv3 --kernel-trace --stats -d "$OUT/shardrep$1" -o run --output-format csv -- python scripts/icp_shard_replay.py replay $1 $2 /tmp/rec$1.npz 3 &&
                   python scripts/icp_shard_kernels.py "$OUT/shardrep$1/run_kernel_trace.csv" "$OUT/shardrep_kernels$1.txt"
               done ;;
-    edab) run edab 600 bash -c 'for r in 1 2; do python scripts/icp_ab.py 1.0 5 && echo "^ new" && LIO_GPU_LIB=fast-lio-sam_gps_amd/build_ab/pre_edist/liblio_gpu.so python scripts/icp_ab.py 1.0 5 && echo "^ pre" || exit $?; done' &&
-          run edtrace 300 rocprofv3 --kernel-trace --stats -d "$OUT/edtrace" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
-          python scripts/icp_tile_passes.py "$OUT/edtrace/run_kernel_trace.csv" new > "$OUT/tile_passes_new.txt" &&
-          export LIO_GPU_LIB=fast-lio-sam_gps_amd/build_ab/pre_edist/liblio_gpu.so &&
-          run edtrace_pre 300 rocprofv3 --kernel-trace --stats -d "$OUT/edtrace_pre" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
-          unset LIO_GPU_LIB &&
-          python scripts/icp_tile_passes.py "$OUT/edtrace_pre/run_kernel_trace.csv" pre > "$OUT/tile_passes_pre.txt" ;;
+    icpab) AB=${AB:-pre_fuse}
+           run icpab 600 bash -c "for r in 1 2; do python scripts/icp_ab.py 1.0 5 && echo '^ new' && LIO_GPU_LIB=fast-lio-sam_gps_amd/build_ab/$AB/liblio_gpu.so python scripts/icp_ab.py 1.0 5 && echo '^ $AB' || exit \$?; done" &&
+           run icpabtrace 300 rocprofv3 --kernel-trace --stats -d "$OUT/icpabtrace" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
+           python scripts/icp_tile_passes.py "$OUT/icpabtrace/run_kernel_trace.csv" new > "$OUT/tile_passes_new.txt" &&
+           python scripts/kstats.py "$OUT/icpabtrace/run_kernel_stats.csv" > "$OUT/icpab_kstats.txt" ;;
     lseqt) runs pytest_lseq 600 python -u -m pytest tests/test_cpp_stream.py tests/test_gpu_parity.py -k "loop_sequence or guard" -x -v -s -p no:cacheprovider --timeout 500 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     loopseqprof) run loopseqprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/loopseqprof" -o run --output-format csv -- fast-lio-sam_gps_amd/lio_gpu/_lib/loop_sequence /tmp/ls.bin &&
