@@ -834,7 +834,6 @@ static int pcl_finish(lio_icp* h, const lio::IcpArgs& a) {
 // sharded all ranks' gathered ids over the whole cloud), enqueued; h_pclout once the stream gets there
 static int enqueue_pcl(lio_icp* h, const lio::IcpArgs& pa) {
     const int order = h->p.umeyama_float;
-    h->pcl.means.n_hint = h->pcl.sig.n_hint = std::max(pa.n, 1);  // the accepted pairs are at most the queries
     lio::launch_pcl_compact(pa, h->pcl, h->st);
     if (h->fid_flags & 4)  // test hook (lio_icp_set_fidelity_debug): report a look-back time-out for this pass
         IHIP(hipMemsetAsync(h->pcl.small + lio::kPclTicket + 1, 1, sizeof(uint32_t), h->st));
@@ -1069,7 +1068,6 @@ static int icp_pass_fsh(lio_icp* h, const lio::IcpArgs& a, bool apply_T, double 
     int rc = exchange_reserve(h);
     if (rc) return rc;
     lio::PclBuf& P = h->pcl;
-    P.means.n_hint = P.sig.n_hint = std::max(a.n, 1);  // the window's pairs are at most its queries
     const uint32_t* dn = P.small + lio::kPclN;
     const int64_t rec = records_count(h->ns, h->world), nbs = tot_blocks(h->ns, h->world);
     const int64_t cnt1 = rec + tot_words(h->ns, h->world, 6);

@@ -3,16 +3,15 @@
 // Per pass, for every chain (grid.y = chain):
 //   seq_bsum     block double prefix (prediction) totals, sum |x| (bound on |s|)
 //   seq_scan1    per chain, sequential over blocks: double block offsets, the binade floor
-//   seq_count_events  per element: predicted binade, event flag, fixed-point increment; the block offsets of
-//                increments and events by a decoupled look-back along the chain (integers: exact in any order);
-//                the events in element order: position, increment prefix, x (one launch)
+//   seq_count    per element: predicted binade, event flag, fixed-point increment -> block totals
+//   seq_scan2    per chain: exclusive block offsets of increments and events
+//   seq_events   the events in element order: position, increment prefix, x
 //   seq_walk     one block per chain replays the events (run sums exact in double) -> event results, sum
 //   seq_verify   every s_k rebuilt from the events; s_k == fl(s_{k-1} + x_k) checked for every k
 #include "lio_seqsum.hpp"
 
 #include <cmath>
 
-#include "lio_dev.hpp"
 #include "lio_error.hpp"
 
 namespace lio {
@@ -147,8 +146,9 @@ __device__ __forceinline__ bool forced_bit(const uint32_t* f, int64_t k) { retur
 
 // predictions for this thread's elements (pass 1: double prefix; later: the previous reconstruction)
 template <class Src>
-__device__ __forceinline__ void predict(const Src& src, const SeqSumBuf& b, int c, int blk, int64_t n, int pass,
-                                        ElemInfo& in, double* s_wd) {
+__device__ __forceinline__ void predict(const Src& src, const SeqSumBuf& b, int c, int64_t n, int pass, ElemInfo& in,
+                                        double* s_wd) {
+    const int blk = blockIdx.x;
     const int64_t k0 = (int64_t)blk * kSeqBlock + (int64_t)threadIdx.x * kSeqPer;
     load_x(src, c, k0, n, in.x);
     if (pass <= 1) {
@@ -189,10 +189,10 @@ __device__ __forceinline__ void predict(const Src& src, const SeqSumBuf& b, int 
 
 // per element: event flag and increment (element 0: the start, neither)
 template <class Src>
-__device__ __forceinline__ void classify(const SeqSumBuf& b, int c, int blk, int64_t n, const ElemInfo& in, int floor_e,
-                                         int pass, bool (&ev)[kSeqPer], uint64_t (&inc)[kSeqPer]) {
+__device__ __forceinline__ void classify(const SeqSumBuf& b, int c, int64_t n, const ElemInfo& in, int floor_e, int pass,
+                                         bool (&ev)[kSeqPer], uint64_t (&inc)[kSeqPer]) {
     const bool noinc = b.dbg_noinc && pass <= 1;
-    const int64_t k0 = (int64_t)blk * kSeqBlock + (int64_t)threadIdx.x * kSeqPer;
+    const int64_t k0 = (int64_t)blockIdx.x * kSeqBlock + (int64_t)threadIdx.x * kSeqPer;
     const uint32_t* fb = b.forced ? b.forced + (size_t)c * (b.nmax / 32 + 1) : nullptr;
     const int64_t gb = b.sh ? b.sh->gbase : 0;  // global index of local element 0 (sharded windows)
 #pragma unroll
@@ -346,18 +346,19 @@ __global__ void __launch_bounds__(256) seq_scan1(SeqSumBuf b, const uint32_t* d_
     }
 }
 
-// the block's elements with their exclusive increment prefix and inclusive event count, from the block offsets
-// seq_count_events stored (seq_verify: the same classification again, element by element)
 template <class Src>
-__device__ __forceinline__ void block_scan_elems(const Src& src, const SeqSumBuf& b, int c, int blk, int64_t n, int pass,
-                                                 ElemInfo& in, bool (&ev)[kSeqPer], uint64_t (&Pex)[kSeqPer],
-                                                 int (&Ein)[kSeqPer]) {
+__global__ void __launch_bounds__(kSeqThreads) seq_count(Src src, SeqSumBuf b, const uint32_t* d_n, int pass) {
     __shared__ double s_wd[kSeqThreads / 64];
     __shared__ uint64_t s_u[kSeqThreads / 64];
     __shared__ int s_i[kSeqThreads / 64];
-    predict(src, b, c, blk, n, pass, in, s_wd);
+    const int c = blockIdx.y;
+    const int64_t n = *d_n;
+    if ((int64_t)blockIdx.x * kSeqBlock >= n) return;
+    ElemInfo in;
+    predict(src, b, c, n, pass, in, s_wd);
+    bool ev[kSeqPer];
     uint64_t inc[kSeqPer];
-    classify<Src>(b, c, blk, n, in, b.floor_e[c], pass, ev, inc);
+    classify<Src>(b, c, n, in, b.floor_e[c], pass, ev, inc);
     uint64_t su = 0;
     int se = 0;
 #pragma unroll
@@ -367,8 +368,73 @@ __device__ __forceinline__ void block_scan_elems(const Src& src, const SeqSumBuf
     }
     uint64_t tu;
     int te;
-    uint64_t pu = block_excl(su, s_u, tu) + b.bPoff[(size_t)c * b.nblk + blk];
-    int pe = block_excl(se, s_i, te) + b.bEoff[(size_t)c * b.nblk + blk];
+    block_excl(su, s_u, tu);
+    block_excl(se, s_i, te);
+    if (threadIdx.x == 0) {
+        b.btot[(size_t)c * b.nblk + blockIdx.x] = tu;
+        b.bev[(size_t)c * b.nblk + blockIdx.x] = te;
+    }
+}
+
+// exclusive block offsets of the increments (wrapping) and event counts: integers, any order is exact
+__global__ void __launch_bounds__(kSeqThreads) seq_scan2(SeqSumBuf b, const uint32_t* d_n) {
+    __shared__ uint64_t s_u[kSeqThreads / 64];
+    __shared__ int s_i[kSeqThreads / 64];
+    const int c = blockIdx.x;
+    const int64_t n = *d_n;
+    const int nb = (int)((n + kSeqBlock - 1) / kSeqBlock);
+    uint64_t P = 0;
+    int E = 0;
+    for (int j0 = 0; j0 < nb; j0 += kSeqThreads) {  // block-uniform trip count
+        const int j = j0 + (int)threadIdx.x;
+        const uint64_t u = j < nb ? b.btot[(size_t)c * b.nblk + j] : 0;
+        const int e = j < nb ? b.bev[(size_t)c * b.nblk + j] : 0;
+        uint64_t tu;
+        int te;
+        const uint64_t pu = block_excl(u, s_u, tu);
+        const int pe = block_excl(e, s_i, te);
+        if (j < nb) {
+            b.bPoff[(size_t)c * b.nblk + j] = P + pu;
+            b.bEoff[(size_t)c * b.nblk + j] = E + pe;
+        }
+        P += tu;
+        E += te;
+    }
+    if (threadIdx.x == 0) {
+        b.ptot[c] = P;
+        b.floor_e[b.nch + c] = E;  // events of the chain
+        if (E > b.evcap) atomicOr(&b.status[1], 1u << c);
+        if (b.sh) {
+            b.sh->nev_loc[c] = E;
+            b.sh->ptot_loc[c] = P;
+            b.sh->e_added[c] = 0;
+            b.sh->p_added[c] = 0;
+        }
+    }
+}
+
+// the block's elements with their exclusive increment prefix and inclusive event count
+template <class Src>
+__device__ __forceinline__ void block_scan_elems(const Src& src, const SeqSumBuf& b, int c, int64_t n, int pass,
+                                                 ElemInfo& in, bool (&ev)[kSeqPer], uint64_t (&Pex)[kSeqPer],
+                                                 int (&Ein)[kSeqPer]) {
+    __shared__ double s_wd[kSeqThreads / 64];
+    __shared__ uint64_t s_u[kSeqThreads / 64];
+    __shared__ int s_i[kSeqThreads / 64];
+    predict(src, b, c, n, pass, in, s_wd);
+    uint64_t inc[kSeqPer];
+    classify<Src>(b, c, n, in, b.floor_e[c], pass, ev, inc);
+    uint64_t su = 0;
+    int se = 0;
+#pragma unroll
+    for (int i = 0; i < kSeqPer; ++i) {
+        su += inc[i];
+        se += ev[i] ? 1 : 0;
+    }
+    uint64_t tu;
+    int te;
+    uint64_t pu = block_excl(su, s_u, tu) + b.bPoff[(size_t)c * b.nblk + blockIdx.x];
+    int pe = block_excl(se, s_i, te) + b.bEoff[(size_t)c * b.nblk + blockIdx.x];
 #pragma unroll
     for (int i = 0; i < kSeqPer; ++i) {
         Pex[i] = pu;
@@ -378,138 +444,32 @@ __device__ __forceinline__ void block_scan_elems(const Src& src, const SeqSumBuf
     }
 }
 
-// Counts, block offsets and events in ONE launch (was count / scan / events: three launches, the
-// classification done twice).  Block x works on chain x % nch; each of the chain's nba active blocks takes its
-// block index by the chain's ticket (arrival order: a block only waits for blocks already running; one counter
-// per chain, so the tickets of the chains are taken in parallel), classifies its elements, publishes its event
-// count (an epoch-tagged word, lio_dev.hpp lb_word) and its increment total (a 64-bit word stored and drained
-// before the word that announces it; 8-byte agent-scope atomics on both sides) and sums every predecessor's
-// pair with the whole block.  Integers, so the offsets are exact in any order.  The chain's last block writes its
-// totals (and the overflow bit when the events exceed the lists); its last ticket resets the chain's counter.
 template <class Src>
-__global__ void __launch_bounds__(kSeqThreads) seq_count_events(Src src, SeqSumBuf b, const uint32_t* d_n, int pass,
-                                                                int nch, uint32_t epoch) {
-    __shared__ double s_wd[kSeqThreads / 64];
-    __shared__ uint64_t s_u[kSeqThreads / 64];
-    __shared__ int s_i[kSeqThreads / 64];
-    __shared__ uint32_t s_t;
-    __shared__ int s_eoff;
-    __shared__ uint64_t s_poff;
-    __shared__ uint32_t s_i32[kSeqThreads / 64];
+__global__ void __launch_bounds__(kSeqThreads) seq_events(Src src, SeqSumBuf b, const uint32_t* d_n, int pass) {
+    const int c = blockIdx.y;
     const int64_t n = *d_n;
-    const int nba = (int)((n + kSeqBlock - 1) / kSeqBlock);
-    const int c = (int)(blockIdx.x % (uint32_t)nch);
-    if (nba == 0) {  // empty chains: their totals are zero
-        if (blockIdx.x < (uint32_t)nch && threadIdx.x == 0) {
-            b.ptot[c] = 0;
-            b.floor_e[b.nch + c] = 0;
-            if (b.sh) {
-                b.sh->nev_loc[c] = 0;
-                b.sh->ptot_loc[c] = 0;
-                b.sh->e_added[c] = 0;
-                b.sh->p_added[c] = 0;
-            }
-        }
-        return;
-    }
-    if ((int64_t)nba * nch > (int64_t)gridDim.x) {  // the caller's bound (n_hint) was short: fall back
-        if (blockIdx.x < (uint32_t)nch && threadIdx.x == 0) atomicOr(&b.status[1], 1u << c);
-        return;
-    }
-    if ((int)(blockIdx.x / (uint32_t)nch) >= nba) return;  // block-uniform: past the chain's blocks
-    if (threadIdx.x == 0) {
-        s_t = atomicAdd(&b.lb_ticket[c], 1u);
-        if (s_t == (uint32_t)nba - 1) b.lb_ticket[c] = 0u;  // the chain's blocks all have their tickets
-    }
-    __syncthreads();
-    const int blk = (int)s_t;
+    if ((int64_t)blockIdx.x * kSeqBlock >= n) return;
     ElemInfo in;
-    predict(src, b, c, blk, n, pass, in, s_wd);
     bool ev[kSeqPer];
-    uint64_t inc[kSeqPer];
-    classify<Src>(b, c, blk, n, in, b.floor_e[c], pass, ev, inc);
-    uint64_t su = 0;
-    int se = 0;
-#pragma unroll
-    for (int i = 0; i < kSeqPer; ++i) {
-        su += inc[i];
-        se += ev[i] ? 1 : 0;
-    }
-    uint64_t tu;
-    int te;
-    const uint64_t pu0 = block_excl(su, s_u, tu);
-    const int pe0 = block_excl(se, s_i, te);
-    const size_t cb = (size_t)c * b.nblk;
-    if (threadIdx.x == 0) {  // publish the block's aggregate: the increments first, drained, then the word
-        lb_store(b.lb_agg + cb, blk, tu);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        lb_store(b.lb_word + cb, blk, lb_word(epoch, 1u, (uint32_t)te));
-    }
-    // the exclusive prefix: every predecessor's aggregate, read by the whole block at once (all blocks publish
-    // before they read, so no block waits on another's reading: one round trip instead of a look-back chain)
-    uint32_t accE = 0;
-    uint64_t accP = 0;
-    bool timeout = false;
-    for (int j = threadIdx.x; j < blk; j += kSeqThreads) {
-        unsigned long long w = lb_load(b.lb_word + cb, j);
-        for (uint32_t spins = 0; (uint32_t)(w >> 34) != epoch; w = lb_load(b.lb_word + cb, j))
-            if (++spins > (1u << 22)) {  // a safety valve only
-                timeout = true;
-                break;
-            }
-        accE += (uint32_t)w;
-        accP += lb_load(b.lb_agg + cb, j);
-    }
-    if (timeout) atomicOr(&b.status[1], 1u << c);  // never expected: the caller falls back
-    {
-        uint32_t t32;
-        uint64_t t64;
-        block_excl(accE, s_i32, t32);
-        block_excl(accP, s_u, t64);
-        accE = t32;
-        accP = t64;
-    }
-    if (threadIdx.x == 0) {
-        s_eoff = (int)accE;
-        s_poff = accP;
-        b.bEoff[cb + blk] = (int)accE;  // seq_verify's block offsets
-        b.bPoff[cb + blk] = accP;
-        if (blk == nba - 1) {  // the chain's totals
-            const int E = (int)accE + te;
-            const uint64_t P = accP + tu;
-            b.ptot[c] = P;
-            b.floor_e[b.nch + c] = E;
-            if (E > b.evcap) atomicOr(&b.status[1], 1u << c);
-            if (b.sh) {
-                b.sh->nev_loc[c] = E;
-                b.sh->ptot_loc[c] = P;
-                b.sh->e_added[c] = 0;
-                b.sh->p_added[c] = 0;
-            }
-        }
-    }
-    __syncthreads();
-    uint64_t pu = pu0 + s_poff;
-    int pe = pe0 + s_eoff;
-    const int64_t k0 = (int64_t)blk * kSeqBlock + (int64_t)threadIdx.x * kSeqPer;
+    uint64_t Pex[kSeqPer];
+    int Ein[kSeqPer];
+    block_scan_elems(src, b, c, n, pass, in, ev, Pex, Ein);
+    const int64_t k0 = (int64_t)blockIdx.x * kSeqBlock + (int64_t)threadIdx.x * kSeqPer;
     // single rank: the walk's lists; sharded: this window's lists (local positions and prefixes, seq_shard_pack)
     int* EPOS = b.sh ? b.lev_pos : b.ev_pos;
     uint64_t* EPP = b.sh ? b.lev_P : b.ev_P;
     float* EXX = b.sh ? b.lev_x : b.ev_x;
     const int64_t es = b.sh ? b.evcap : b.evs;
 #pragma unroll
-    for (int i = 0; i < kSeqPer; ++i) {
+    for (int i = 0; i < kSeqPer; ++i)
         if (ev[i]) {
-            const int idx = pe;  // exclusive count = this event's slot
+            const int idx = Ein[i] - 1;
             if (idx < b.evcap) {
                 EPOS[(size_t)c * es + idx] = (int)(k0 + i);
-                EPP[(size_t)c * es + idx] = pu;
+                EPP[(size_t)c * es + idx] = Pex[i];
                 EXX[(size_t)c * es + idx] = in.x[i];
             }
         }
-        pu += inc[i];
-        pe += ev[i] ? 1 : 0;
-    }
 }
 
 // The walk: s_{event-1} = s_{previous event} + run sum R (exact), s_event = fl(s_{event-1} + x_event), one chain
@@ -668,7 +628,7 @@ __global__ void __launch_bounds__(kSeqThreads) seq_verify(Src src, SeqSumBuf b, 
     bool ev[kSeqPer];
     uint64_t Pex[kSeqPer];
     int Ein[kSeqPer];
-    block_scan_elems(src, b, c, (int)blockIdx.x, n, pass, in, ev, Pex, Ein);
+    block_scan_elems(src, b, c, n, pass, in, ev, Pex, Ein);
     const double unit = ldexp(1.0, b.floor_e[c] - 23);
     const uint64_t* EP = b.ev_P + (size_t)c * b.evs;
     const float* ES = b.ev_s + (size_t)c * b.evs;
@@ -688,7 +648,7 @@ __global__ void __launch_bounds__(kSeqThreads) seq_verify(Src src, SeqSumBuf b, 
     {
         bool ev2[kSeqPer];
         uint64_t inc2[kSeqPer];
-        classify<Src>(b, c, (int)blockIdx.x, n, in, b.floor_e[c], pass, ev2, inc2);
+        classify<Src>(b, c, n, in, b.floor_e[c], pass, ev2, inc2);
 #pragma unroll
         for (int i = 0; i < kSeqPer; ++i) {
             const int64_t k = k0 + i;
@@ -956,23 +916,10 @@ __global__ void __launch_bounds__(256) seq_shard_merge(SeqSumBuf b, const uint32
     }
 }
 
-// blocks per chain of a launch: enough for the caller's bound on the count (the blocks past the device count
-// return at once)
-inline int seq_grid_blocks(const SeqSumBuf& b) {
-    const int64_t n = b.n_hint > 0 && b.n_hint < b.nmax ? b.n_hint : b.nmax;
-    return (int)std::max<int64_t>(1, (n + kSeqBlock - 1) / kSeqBlock);
-}
-
-template <class Src>
-void launch_count_events(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, hipStream_t st) {
-    b.lb_epoch = b.lb_epoch + 1u >= (1u << 30) ? 1u : b.lb_epoch + 1u;  // 30 bits, 0 reserved for "never written"
-    seq_count_events<Src><<<seq_grid_blocks(b) * nch, kSeqThreads, 0, st>>>(src, b, d_n, pass, nch, b.lb_epoch);
-}
-
 template <class Src>
 void seqsum_launch_impl(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, hipStream_t st) {
     b.evs = b.evcap;  // single rank: the walk reads the lists seq_events writes
-    const dim3 g(seq_grid_blocks(b), nch);
+    const dim3 g(b.nblk, nch);
     if (pass <= 1) {
         // the forced-event bits of a previous alignment's failures are stale (none were set unless a re-pass ran)
         if (b.forced_dirty) {
@@ -985,7 +932,9 @@ void seqsum_launch_impl(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf&
         b.forced_dirty = true;  // the failures that led here set forced bits
         (void)hipMemsetAsync(b.status, 0, 2 * sizeof(uint32_t), st);
     }
-    launch_count_events(src, nch, d_n, b, pass, st);
+    seq_count<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
+    seq_scan2<<<nch, kSeqThreads, 0, st>>>(b, d_n);
+    seq_events<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
     seq_walk<Src><<<nch, kWalkThreads, 0, st>>>(src, b, d_n);
     seq_verify<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
 }
@@ -1003,7 +952,7 @@ template void seqsum_launch<SeqSigma>(const SeqSigma&, int, const uint32_t*, Seq
 template <class Src>
 void seqsum_shard_head(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, double* tot_out, int64_t nb_slot,
                        hipStream_t st) {
-    const dim3 g(seq_grid_blocks(b), nch);
+    const dim3 g(b.nblk, nch);
     if (b.forced_dirty) {
         (void)hipMemsetAsync(b.forced, 0, (size_t)nch * (b.nmax / 32 + 1) * sizeof(uint32_t), st);
         b.forced_dirty = false;
@@ -1016,7 +965,7 @@ template <class Src>
 void seqsum_shard_mid(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, const double* tot_recv,
                       int64_t tot_stride, int64_t nb_slot, int rank, int world, double* msg_out, int slot, int nhead,
                       hipStream_t st) {
-    const dim3 g(seq_grid_blocks(b), nch);
+    const dim3 g(b.nblk, nch);
     if (pass <= 1) {
         seq_shard_offsets<<<nch, 256, 0, st>>>(b, tot_recv, tot_stride, nb_slot, rank, world);
         seq_scan1<<<nch, 256, 0, st>>>(b, d_n, pass);
@@ -1024,7 +973,9 @@ void seqsum_shard_mid(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b
         b.forced_dirty = true;  // the failures that led here set forced bits
         (void)hipMemsetAsync(b.status, 0, 2 * sizeof(uint32_t), st);
     }
-    launch_count_events(src, nch, d_n, b, pass, st);
+    seq_count<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
+    seq_scan2<<<nch, kSeqThreads, 0, st>>>(b, d_n);
+    seq_events<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
     seq_shard_pack<Src><<<nch, 256, 0, st>>>(src, b, d_n, msg_out, slot, nhead);
 }
 
@@ -1032,7 +983,7 @@ void seqsum_shard_mid(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b
 template <class Src>
 void seqsum_shard_tail(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, const double* msg_recv,
                        int64_t msg_stride, int rank, int world, int slot, const SeqHeads& hd, hipStream_t st) {
-    const dim3 g(seq_grid_blocks(b), nch);
+    const dim3 g(b.nblk, nch);
     seq_shard_merge<<<nch, 256, 0, st>>>(b, d_n, msg_recv, msg_stride, rank, world, slot, hd.nhead, hd.ext,
                                          hd.ext_stride, hd.ghead, hd.nghead);
     seq_walk<Src><<<nch, kWalkThreads, 0, st>>>(src, b, d_n);
@@ -1085,17 +1036,15 @@ int seqsum_reserve(SeqSumBuf& b, int nch, int64_t nmax, hipStream_t st) {
     b.nch = nch;
     b.nmax = nmax;
     b.nblk = (int)((nmax + kSeqBlock - 1) / kSeqBlock);
-    count_alloc(19);
+    count_alloc(18);
     b.evcap = b.evcap_alloc = nmax / 4 + 1024;  // events are ~0.3 % of a C4 chain; past a quarter the serial kernel is as fast
     b.evs = b.evcap;
     b.evs_alloc = 2 * b.evcap_alloc;  // the walk's lists: sharded, every rank's events (O(window): 2 x its own)
     const size_t nb = (size_t)nch * b.nblk;
     bool ok = hipMalloc(&b.bsum, nb * sizeof(double)) == hipSuccess && hipMalloc(&b.babs, nb * sizeof(double)) == hipSuccess &&
               hipMalloc(&b.boff, nb * sizeof(double)) == hipSuccess && hipMalloc(&b.bdelta, nb * sizeof(double)) == hipSuccess &&
-              hipMalloc(&b.lb_word, nb * sizeof(unsigned long long)) == hipSuccess &&
-              hipMalloc(&b.lb_agg, nb * sizeof(unsigned long long)) == hipSuccess &&
-              hipMalloc(&b.lb_ticket, kSeqMaxChains * sizeof(uint32_t)) == hipSuccess &&
-              hipMalloc(&b.bPoff, nb * sizeof(uint64_t)) == hipSuccess &&
+              hipMalloc(&b.btot, nb * sizeof(uint64_t)) == hipSuccess &&
+              hipMalloc(&b.bev, nb * sizeof(int)) == hipSuccess && hipMalloc(&b.bPoff, nb * sizeof(uint64_t)) == hipSuccess &&
               hipMalloc(&b.bEoff, nb * sizeof(int)) == hipSuccess && hipMalloc(&b.floor_e, 3 * nch * sizeof(int)) == hipSuccess &&
               hipMalloc(&b.ptot, nch * sizeof(uint64_t)) == hipSuccess &&
               hipMalloc(&b.ev_pos, (size_t)nch * b.evs_alloc * sizeof(int)) == hipSuccess &&
@@ -1110,13 +1059,11 @@ int seqsum_reserve(SeqSumBuf& b, int nch, int64_t nmax, hipStream_t st) {
         return -5;
     }
     (void)hipMemsetAsync(b.status, 0, 4 * sizeof(uint32_t), st);
-    (void)hipMemsetAsync(b.lb_word, 0, nb * sizeof(unsigned long long), st);  // epoch 0: never published
-    (void)hipMemsetAsync(b.lb_ticket, 0, kSeqMaxChains * sizeof(uint32_t), st);
     return 0;
 }
 
 void seqsum_free(SeqSumBuf& b) {
-    void* ptrs[] = {b.bsum, b.babs, b.boff,   b.bdelta, b.lb_word, b.lb_agg, b.lb_ticket, b.bPoff, b.bEoff, b.floor_e,
+    void* ptrs[] = {b.bsum, b.babs, b.boff,   b.bdelta, b.btot,   b.bev,   b.bPoff, b.bEoff, b.floor_e,
                     b.ptot, b.ev_pos, b.ev_P, b.ev_x, b.ev_s, b.recon, b.forced, b.status, b.result,
                     b.sh,   b.lev_pos, b.lev_P, b.lev_x};
     for (void* p : ptrs)

@@ -171,15 +171,10 @@ struct SeqSumBuf {
     double* babs = nullptr;     // [nch][nblk] sum |x| (bound on |s|)
     double* boff = nullptr;     // [nch][nblk] exclusive prefix of bsum
     double* bdelta = nullptr;   // [nch][nblk] drift allowance of the pass-1 prediction through the block's end
-    // seq_count_events' per-block aggregates along each chain: the word (epoch, flag, event count; lio_dev.hpp
-    // lb_word) and the 64-bit increment total of every block
-    unsigned long long* lb_word = nullptr;  // [nch][nblk]
-    unsigned long long* lb_agg = nullptr;   // [nch][nblk]
-    uint32_t lb_epoch = 0;                  // host: the launch's epoch (1 .. 2^30 - 1; 0: never written)
-    uint32_t* lb_ticket = nullptr;          // [kSeqMaxChains] per-chain block tickets (0 between launches)
-    int64_t n_hint = 0;     // host: an upper bound on the device count (grids sized for it; 0: nmax)
-    uint64_t* bPoff = nullptr;  // [nch][nblk] exclusive increment prefix of each block (fixed point, wrapping)
-    int* bEoff = nullptr;       // [nch][nblk] exclusive event count of each block
+    uint64_t* btot = nullptr;   // [nch][nblk] block increment totals (fixed point, wrapping)
+    int* bev = nullptr;         // [nch][nblk] block event counts
+    uint64_t* bPoff = nullptr;  // [nch][nblk] exclusive prefix of btot
+    int* bEoff = nullptr;       // [nch][nblk] exclusive prefix of bev
     int* floor_e = nullptr;     // [nch] binade floor (run exactness) ; [nch..2nch) nev ; [2nch..3nch) ok
     uint64_t* ptot = nullptr;   // [nch] total increments
     int* ev_pos = nullptr;      // [nch][evcap]
