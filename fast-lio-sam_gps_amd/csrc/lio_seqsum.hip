@@ -122,7 +122,7 @@ struct ElemInfo {
 // event / increment of element k >= 1 from its value, predicted binade e, the predecessor's ep, the floor
 __device__ __forceinline__ bool seq_event(float x, int e, int ep, int floor_e, bool forced, bool noinc, uint64_t& inc) {
     inc = 0;
-    if (forced || e == kSpecial || ep == kSpecial || (e > ep && !noinc) || e < floor_e || e - floor_e > 60) return true;
+    if (forced || e == kSpecial || ep == kSpecial || (e != ep && !noinc) || e < floor_e || e - floor_e > 60) return true;
     if (!(fabsf(x) <= 3.402823466e38f)) return true;  // non-finite
     const double t = ldexp((double)x, 23 - e);
     if (!(fabs(t) < 0x1p52)) return true;
@@ -487,7 +487,7 @@ __global__ void __launch_bounds__(kSeqThreads) seq_events(Src src, SeqSumBuf b, 
 constexpr int kWalkThreads = 256;
 constexpr int kWalkChunk = 1024;  // events per LDS chunk (x 2 buffers x 20 bytes)
 constexpr int kWalkU = 8;
-struct WalkChunk {
+struct alignas(16) WalkChunk {
     double R[kWalkChunk];  // run sums (exact)
     float Rf[kWalkChunk];  // the same as floats (fast groups)
     float x[kWalkChunk];
@@ -528,6 +528,53 @@ __device__ __forceinline__ void walk_prepare(WalkChunk& B, int k, int nev, doubl
     }
 }
 
+// the float form over one 64-event group from e0 (all fast), in four steps of 16: a step's operands are read from
+// LDS while the step before it adds (the LDS latency off the chain), results stored 4 at a time
+__device__ __forceinline__ float walk_fast(WalkChunk& B, int e0, float s) {
+    constexpr int nsteps = 4;
+    const float4* R4 = reinterpret_cast<const float4*>(B.Rf + e0);
+    const float4* X4 = reinterpret_cast<const float4*>(B.x + e0);
+    float4* F4 = reinterpret_cast<float4*>(B.f + e0);
+    float4 r0[4], x0[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        r0[q] = R4[q];
+        x0[q] = X4[q];
+    }
+#pragma unroll
+    for (int st = 0; st < nsteps; ++st) {
+        float4 r1[4], x1[4];
+        if (st + 1 < nsteps) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                r1[q] = R4[4 * (st + 1) + q];
+                x1[q] = X4[4 * (st + 1) + q];
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            float4 o;
+            s = (s + r0[q].x) + x0[q].x;
+            o.x = s;
+            s = (s + r0[q].y) + x0[q].y;
+            o.y = s;
+            s = (s + r0[q].z) + x0[q].z;
+            o.z = s;
+            s = (s + r0[q].w) + x0[q].w;
+            o.w = s;
+            F4[4 * st + q] = o;
+        }
+        if (st + 1 < nsteps) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                r0[q] = r1[q];
+                x0[q] = x1[q];
+            }
+        }
+    }
+    return s;
+}
+
 template <class Src>
 __global__ void __launch_bounds__(kWalkThreads) seq_walk(Src src, SeqSumBuf b, const uint32_t* d_n) {
     __shared__ WalkChunk wb[2];
@@ -546,29 +593,31 @@ __global__ void __launch_bounds__(kWalkThreads) seq_walk(Src src, SeqSumBuf b, c
     float* ES = b.ev_s + (size_t)c * b.evs;
     const int nchunk = (nev + kWalkChunk - 1) / kWalkChunk;
     float s = b.sh ? b.sh->x0[c] : src(c, 0);  // the chain (lane 0 of wave 0)
+#ifdef LIO_WALK_DIAG  // diagnostics build: the walk's time split and its general-form share, printed per chain
+    const uint64_t t0 = wall_clock64();
+    uint64_t t_walk = 0, t_sync = 0;
+    int n_fast = 0, n_slow = 0;
+#endif
     if (nchunk > 0) walk_prepare(wb[0], 0, nev, unit, EP, EX, t, kWalkThreads);
     __syncthreads();
+#ifdef LIO_WALK_DIAG
+    const uint64_t t1 = wall_clock64();
+#endif
     for (int k = 0; k < nchunk; ++k) {
+#ifdef LIO_WALK_DIAG
+        const uint64_t ta = wall_clock64();
+#endif
         if (w == 0) {
             if (t == 0) {
                 WalkChunk& B = wb[k & 1];
                 const int m = min(kWalkChunk, nev - k * kWalkChunk);
                 for (int g = 0; g < m; g += 64) {
                     const int cnt = min(64, m - g);
+#ifdef LIO_WALK_DIAG
+                    if (cnt == 64 && B.fast[g >> 6]) ++n_fast; else ++n_slow;
+#endif
                     if (cnt == 64 && B.fast[g >> 6]) {
-                        for (int l = g; l < g + 64; l += kWalkU) {
-                            float r[kWalkU], x[kWalkU];
-#pragma unroll
-                            for (int u = 0; u < kWalkU; ++u) {
-                                r[u] = B.Rf[l + u];
-                                x[u] = B.x[l + u];
-                            }
-#pragma unroll
-                            for (int u = 0; u < kWalkU; ++u) {
-                                s = (s + r[u]) + x[u];
-                                B.f[l + u] = s;
-                            }
-                        }
+                        s = walk_fast(B, g, s);
                     } else if (cnt == 64) {
                         for (int l = g; l < g + 64; l += kWalkU) {
                             double r[kWalkU];
@@ -600,8 +649,20 @@ __global__ void __launch_bounds__(kWalkThreads) seq_walk(Src src, SeqSumBuf b, c
                 for (int j = t - 64; j < kWalkChunk; j += kWalkThreads - 64) ES[e0 + j] = B.f[j];
             }
         }
+#ifdef LIO_WALK_DIAG
+        const uint64_t tb = wall_clock64();
+        t_walk += tb - ta;
+#endif
         __syncthreads();
+#ifdef LIO_WALK_DIAG
+        t_sync += wall_clock64() - tb;
+#endif
     }
+#ifdef LIO_WALK_DIAG
+    if (t == 0)
+        printf("walk chain %d: events %d groups fast %d general %d | ticks prologue %llu walk %llu sync %llu\n", c, nev,
+               n_fast, n_slow, (unsigned long long)(t1 - t0), (unsigned long long)t_walk, (unsigned long long)t_sync);
+#endif
     if (nchunk > 0) {
         const WalkChunk& B = wb[(nchunk - 1) & 1];
         const int e0 = (nchunk - 1) * kWalkChunk;
