@@ -148,7 +148,8 @@ def _loop_icp(args, LC, synth, local, world, rank, dist, rehearse, coll_dev, bar
     src, dst, Tgt = synth.make_icp_pair(n_points=500_000, seed=4321, disp=(2.5, 4.0))
     double = _time_double(args, LC, src, dst, local) if rank == 0 else None
     # the headline: the DEFAULT mode = PCL's float Umeyama in the Eigen 3.3 order (the reference's arithmetic,
-    # loop_closure.h:42), sharded over the ranks (records + accepted ids all-gathered)
+    # loop_closure.h:42), sharded over the ranks (each rank its window of the float chains: block sums, event
+    # lists and depth blocks all-gathered)
     lc = LC.LoopClosure(LC.LoopClosureConfig(), device=local)
     cb = None
     exchange = "none (1 rank)"
@@ -206,8 +207,8 @@ def _loop_icp(args, LC, synth, local, world, rank, dist, rehearse, coll_dev, bar
     nn_ms = itm["icp_nn_ms"] / max(itm["icp_nn_launches"], 1)
     loop_icp = {"config": "C4: 500k vs 500k, voxel 0.3 m, 2.5 m / 4 deg initial offset, PCL ICP semantics",
                 "mode": f"umeyama_float={LC.FIDELITY_ORDER} (default: PCL's float Umeyama, sequential float means, "
-                        "Eigen 3.3 GEMM sigma kc(32 KiB L1); seqsum: parallel, verified bit-exact; sharded: records "
-                        "+ accepted ids all-gathered, float chains over the whole cloud on every rank)",
+                        "Eigen 3.3 GEMM sigma kc(32 KiB L1); seqsum: parallel, verified bit-exact; sharded: each rank "
+                        "its source window; per pass records + block sums, event lists, depth blocks all-gathered)",
                 "seqsum": lc.fidelity_stats(),
                 # side figure: the opt-in double statistics (outside the 1e-5 bar), one rank
                 "double_stats": double,

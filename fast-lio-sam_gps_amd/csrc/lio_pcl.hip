@@ -9,13 +9,15 @@
 //              the end; orders 2 / 3: Eigen 3.3's GEMM, the depth blocked by kc(L1 32 / 48 KiB) and
 //              res += alpha * (block's sequential sum) per block (oracle/lio_oracle.cpp UmeyamaOrder)
 // Here:
-//   pcl_count / pcl_scan / pcl_scatter   the accepted pairs compacted in source order (n on the device)
+//   pcl_compact                          the accepted pairs compacted in source order (one launch, look-back)
 //   seqsum (lio_seqsum.hip)              the six mean chains (and order 1's nine sigma chains), bit-exact
 //                                        sequential float results computed in parallel
 //   pcl_sigma_blocks                     orders 2 / 3: one wave per kc block, nine sequential lanes from LDS
 //   pcl_pack                             res += alpha * C_b in block order; sums, count, sigma, status
-// Sharded (lio_icp_host.cpp fid_sharded): the correspondence order is global, so every rank runs these over
-// the whole source with the all-gathered accepted ids (IcpArgs::nn_d2 == nullptr: gated already).
+// Sharded (lio_icp_host.cpp fid_sharded): each rank compacts its window of the source (the windows in rank
+// order are the correspondence order); the chains are split over the windows (lio_seqsum.hpp seqsum_shard_*),
+// the depth blocks are summed by the rank holding their first pair (pcl_sigma_shard) and gathered in block
+// order (pcl_x3_merge) for pcl_pack.
 #include "lio_error.hpp"
 #include "lio_kernels.hpp"
 #include "lio_pcl.hpp"

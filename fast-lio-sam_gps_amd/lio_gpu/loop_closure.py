@@ -261,7 +261,8 @@ class LoopClosure:
 
 class LoopClosureGroup:
     """Single-process multi-GPU loop ICP (``lio_icp_group``): one handle per device, the source
-    sharded, the per-iteration records (and the accepted correspondence ids) all-gathered over RCCL (or through host memory with
+    sharded, the per-iteration messages (records; in the PCL float modes also the windows' chain block sums,
+    event lists and depth blocks) all-gathered over RCCL (or through host memory with
     ``LIO_ICP_EXCHANGE=host`` / a device listed twice).  Same results as :class:`LoopClosure`, bit
     for bit."""
 

@@ -113,7 +113,7 @@ def test_icp_nn_multi_iteration_prior():
 @pytest.mark.parametrize("n", [2, 4])
 def test_icp_group_bit_identical_to_one_handle(n, mode):
     """lio_icp_group (single-process multi-GPU): n ranks — all on device 0 on a one-GPU
-    box, so the records (and in the default PCL float mode the accepted ids) travel through host memory;
+    box, so the records (and in the default PCL float mode the float chains' messages) travel through host memory;
     distinct devices use RCCL — give the one-handle transform, score, iterations and aligned cloud bit for
     bit, in the default mode and in the opt-in double statistics."""
     src, dst, _ = synth.make_icp_pair(n_points=60_000, seed=12, disp=(1.0, 3.0))
@@ -294,7 +294,7 @@ def test_icp_device_exchange_emulated_ranks(world, mode, debug):
     def make_cb(rank):
         def cb(send_p, nn, recv_p, stream, user):
             try:
-                # a pass sends its records (+ the accepted ids in the PCL float modes): nn <= the capacity
+                # a pass's messages (records, block sums, event lists, depth blocks): nn <= the capacity
                 assert send_p == sends[rank].data_ptr() and recv_p == recvs[rank].data_ptr() and 0 < nn <= n
                 s = torch.cuda.ExternalStream(stream, device=dev)
                 e = torch.cuda.Event()
