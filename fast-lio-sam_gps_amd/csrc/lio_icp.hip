@@ -516,20 +516,57 @@ __device__ void icp_order_share(const uint32_t* __restrict__ cost, int n, uint32
 // Blocks [0, nsup) write the records; when `order` is given, blocks nsup .. nsup + 7 build the next
 // pass's tile order for the eight XCD shares in the same launch (they only read this pass's tile costs),
 // so the order runs beside the records instead of between them and the next pass.
+// exclusive prefix over the 1024 threads of the block (16 waves), total -> tot
+__device__ __forceinline__ uint32_t stats_block_excl(uint32_t v, uint32_t* s_w, uint32_t& tot) {
+    constexpr int NW = kIcpStatsThreads / 64;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t u = __shfl_up(inc, d, 64);
+        if (lane >= d) inc += u;
+    }
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    uint32_t off = 0, t = 0;
+#pragma unroll
+    for (int i = 0; i < NW; ++i) {
+        const uint32_t c = s_w[i];
+        if (i < w) off += c;
+        t += c;
+    }
+    __syncthreads();
+    tot = t;
+    return off + inc - v;
+}
+
 __global__ void __launch_bounds__(kIcpStatsThreads) icp_stats_kernel(IcpArgs a, double* __restrict__ super, int nsup,
-                                                                     uint32_t* __restrict__ order, int ntiles) {
+                                                                     uint32_t* __restrict__ order, int ntiles,
+                                                                     IcpCompact cp) {
     if ((int)blockIdx.x >= nsup) {  // block-uniform
         icp_order_share<kIcpStatsThreads>(a.tile_cost, ntiles, order, (int)blockIdx.x - nsup);
         return;
     }
     constexpr int NW = kIcpStatsThreads / 64, PER = kIcpSuper / kIcpStatsThreads;
     __shared__ double red[NW][kIcpStride];
+    __shared__ uint32_t s_rec, s_off, s_w[NW];
+    // the record: this block's, or with the compaction the arrival order's (a block only waits in the look-back
+    // for records whose blocks are already running)
+    int rec = blockIdx.x;
+    if (cp.pairs) {
+        if (threadIdx.x == 0) {
+            s_rec = atomicAdd(cp.ticket, 1u);
+            if (s_rec == (uint32_t)nsup - 1) *cp.ticket = 0u;  // every record block has its ticket
+        }
+        __syncthreads();
+        rec = (int)s_rec;
+    }
     double v[32];
 #pragma unroll
     for (int k = 0; k < 32; ++k) v[k] = 0.0;
     int ids[PER];
     float d2s[PER];
-    const int base = blockIdx.x * kIcpSuper + threadIdx.x;
+    const int base = rec * kIcpSuper + threadIdx.x;
 #pragma unroll
     for (int k = 0; k < PER; ++k) {  // all correspondence loads first: one round trip
         const int i = base + k * kIcpStatsThreads;
@@ -570,7 +607,50 @@ __global__ void __launch_bounds__(kIcpStatsThreads) icp_stats_kernel(IcpArgs a, 
         if (threadIdx.x < 17)
 #pragma unroll
             for (int w = 0; w < NW; ++w) s += red[w][threadIdx.x];
-        super[(size_t)blockIdx.x * kIcpStride + threadIdx.x] = s;
+        super[(size_t)rec * kIcpStride + threadIdx.x] = s;
+    }
+    if (!cp.pairs) return;  // block-uniform
+    // The accepted pairs of the record in source order (pcl_compact_kernel's result, one launch fewer): slab k
+    // = points rec * 4096 + 1024 k + t; the four slabs' flags packed two to a word (counts <= 1024) for the
+    // block prefix, the record's count chained over the records by the look-back.
+    bool ok[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) ok[k] = ids[k] >= 0 && ids[k] != kNone && !((double)d2s[k] > a.max_d2);
+    static_assert(PER == 4, "the packed slab counts assume four 1024-point slabs per record");
+    uint32_t t01, t23;
+    const uint32_t e01 = stats_block_excl((ok[0] ? 1u : 0u) | (ok[1] ? 1u << 16 : 0u), s_w, t01);
+    const uint32_t e23 = stats_block_excl((ok[2] ? 1u : 0u) | (ok[3] ? 1u << 16 : 0u), s_w, t23);
+    const uint32_t T[PER] = {t01 & 0xffffu, t01 >> 16, t23 & 0xffffu, t23 >> 16};
+    const uint32_t ex[PER] = {e01 & 0xffffu, e01 >> 16, e23 & 0xffffu, e23 >> 16};
+    const uint32_t R = T[0] + T[1] + T[2] + T[3];
+    if (threadIdx.x < 64) {  // wave 0: publish, look back, publish the prefix
+        uint32_t acc = 0;
+        if (rec > 0) {
+            if (threadIdx.x == 0) lb_store(cp.st, rec, lb_word(cp.epoch, 1u, R));
+            uint64_t unused;
+            bool timeout;
+            acc = lookback_excl<false>(cp.st, nullptr, nullptr, rec, cp.epoch, unused, timeout);
+            if (timeout && threadIdx.x == 0) atomicOr(cp.ticket + 1, 1u);  // flagged in pcl_pack's output
+        }
+        if (threadIdx.x == 0) {
+            lb_store(cp.st, rec, lb_word(cp.epoch, 2u, acc + R));
+            s_off = acc;
+            if (rec == nsup - 1) *cp.d_n = acc + R;
+        }
+    }
+    __syncthreads();
+    uint32_t before = s_off;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+        if (ok[k]) {
+            const int i = base + k * kIcpStatsThreads;
+            const uint32_t slot = before + ex[k];
+            const float4 q = a.tgt_by_id[ids[k]];
+            const float vv[6] = {a.cur[3 * i], a.cur[3 * i + 1], a.cur[3 * i + 2], q.x, q.y, q.z};
+#pragma unroll
+            for (int d = 0; d < 6; ++d) cp.pairs[d * cp.cap + slot] = vv[d];
+        }
+        before += T[k];
     }
 }
 
@@ -929,11 +1009,15 @@ void launch_icp_combine(const double* recv, int64_t nsup, int world, int64_t ran
     icp_combine_kernel<<<1, 256, 0, st>>>(recv, nsup, world, rank_stride, out17);
 }
 
-void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st, uint32_t* order, int ntiles) {
-    if (a.n == 0) return;
+void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st, uint32_t* order, int ntiles, const IcpCompact* cp) {
+    if (a.n == 0) {
+        if (cp && cp->d_n) (void)hipMemsetAsync(cp->d_n, 0, sizeof(uint32_t), st);  // no pairs
+        return;
+    }
     const int nsup = (a.n + kIcpSuper - 1) / kIcpSuper;
     const bool ord = order && ntiles > 0;
-    icp_stats_kernel<<<nsup + (ord ? 8 : 0), kIcpStatsThreads, 0, st>>>(a, super, nsup, ord ? order : nullptr, ntiles);
+    icp_stats_kernel<<<nsup + (ord ? 8 : 0), kIcpStatsThreads, 0, st>>>(a, super, nsup, ord ? order : nullptr, ntiles,
+                                                                         cp ? *cp : IcpCompact{});
 }
 
 }  // namespace lio

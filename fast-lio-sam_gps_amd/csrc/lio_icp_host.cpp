@@ -834,7 +834,7 @@ static int pcl_finish(lio_icp* h, const lio::IcpArgs& a) {
 // sharded all ranks' gathered ids over the whole cloud), enqueued; h_pclout once the stream gets there
 static int enqueue_pcl(lio_icp* h, const lio::IcpArgs& pa) {
     const int order = h->p.umeyama_float;
-    lio::launch_pcl_compact(pa, h->pcl, h->st);
+    (void)pa;  // the pairs were compacted by the statistics launch (icp_pass: launch_icp_stats with IcpCompact)
     if (h->fid_flags & 4)  // test hook (lio_icp_set_fidelity_debug): report a look-back time-out for this pass
         IHIP(hipMemsetAsync(h->pcl.small + lio::kPclTicket + 1, 1, sizeof(uint32_t), h->st));
     lio::launch_pcl_means(h->pcl, 1, h->st);
@@ -1075,9 +1075,10 @@ static int icp_pass_fsh(lio_icp* h, const lio::IcpArgs& a, bool apply_T, double 
     if (h->timing) IHIP(hipEventRecord(h->ev.a, h->st));
     if (h->sh_n > 0) lio::launch_icp_tiles(a, h->ntiles, h->st);
     if (h->timing) IHIP(hipEventRecord(h->ev.m, h->st));
-    if (h->sh_n > 0) lio::launch_icp_stats(a, h->d_xsend, h->st, h->d_order, h->ntiles);
+    const lio::IcpCompact cpa = lio::pcl_compact_args(P);  // the window's pairs compacted by the same launch
+    if (h->sh_n > 0) lio::launch_icp_stats(a, h->d_xsend, h->st, h->d_order, h->ntiles, &cpa);
+    else IHIP(hipMemsetAsync(cpa.d_n, 0, sizeof(uint32_t), h->st));  // an empty window: no pairs
     if (h->timing) IHIP(hipEventRecord(h->ev.b, h->st));
-    lio::launch_pcl_compact(a, P, h->st);
     if (h->fid_flags & 4)  // test hook (lio_icp_set_fidelity_debug): report a look-back time-out for this pass
         IHIP(hipMemsetAsync(P.small + lio::kPclTicket + 1, 1, sizeof(uint32_t), h->st));
     lio::seqsum_shard_head(fsh_means_src(h), 6, dn, P.means, h->d_xsend + rec, nbs, h->st);
@@ -1165,8 +1166,12 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
         if (h->timing) IHIP(hipEventRecord(h->ev.a, h->st));
         if (h->sh_n > 0) lio::launch_icp_tiles(a, h->ntiles, h->st);
         if (h->timing) IHIP(hipEventRecord(h->ev.m, h->st));
+        // the PCL float modes: the accepted pairs compacted by the same launch (one rank: the whole source)
+        lio::IcpCompact cpa;
+        if (pcl16 && !fitness) cpa = lio::pcl_compact_args(h->pcl);
+        const lio::IcpCompact* cp = pcl16 && !fitness ? &cpa : nullptr;
         if (dev_x) {  // records -> device send buffer -> in-stream all-gather -> record-order sum
-            if (h->sh_n > 0) lio::launch_icp_stats(a, h->d_xsend, h->st, fitness ? nullptr : h->d_order, h->ntiles);
+            if (h->sh_n > 0) lio::launch_icp_stats(a, h->d_xsend, h->st, fitness ? nullptr : h->d_order, h->ntiles, cp);
             IHIP(hipGetLastError());
             if (h->fn_dev(h->d_xsend, cnt, h->d_xrecv, (void*)h->st, h->user_dev) != 0)
                 return ifail(LIO_ERR_STATE, "device all-gather callback failed");
@@ -1174,8 +1179,9 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
             lio::launch_icp_combine(h->d_xrecv, nsup, h->world, cnt, h->h_out17_dev, h->st);
         } else if (h->sh_n > 0) {
             // records straight to host memory; the next pass's tile order in the same launch
-            lio::launch_icp_stats(a, h->h_super_dev, h->st, fitness ? nullptr : h->d_order, h->ntiles);
+            lio::launch_icp_stats(a, h->h_super_dev, h->st, fitness ? nullptr : h->d_order, h->ntiles, cp);
         }
+        if (cp && h->sh_n == 0) IHIP(hipMemsetAsync(cp->d_n, 0, sizeof(uint32_t), h->st));  // no pairs
         if (h->timing) IHIP(hipEventRecord(h->ev.b, h->st));
         if (pcl16) {  // one rank: the float statistics of its correspondences
             const int rc = enqueue_pcl(h, a);

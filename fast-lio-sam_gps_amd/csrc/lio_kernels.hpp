@@ -168,7 +168,20 @@ int icp_build_tiles(const GridBuf& q, uint2* tiles, uint32_t* scratch, void*& tm
 void launch_icp_tiles(const IcpArgs& a, int ntiles, hipStream_t st);
 // tile order for the next pass: descending log2(cost) buckets (one block)
 // one record per 4096 points; with `order`, the next pass's tile order from a.tile_cost in the same launch
-void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st, uint32_t* order = nullptr, int ntiles = 0);
+// With cp.pairs set (the PCL float modes' correspondence passes), the same launch compacts the accepted pairs
+// in source order into cp.pairs (column-major, cp.cap per column: cur xyz, target xyz) — one record block per
+// 4096 points, the records' counts chained by a look-back (cp.st / cp.ticket / cp.epoch as pcl_compact_kernel's),
+// the total into *cp.d_n; a look-back time-out sets cp.ticket[1].
+struct IcpCompact {
+    float* pairs = nullptr;
+    int64_t cap = 0;
+    unsigned long long* st = nullptr;
+    uint32_t* ticket = nullptr;
+    uint32_t epoch = 0;
+    uint32_t* d_n = nullptr;
+};
+void launch_icp_stats(const IcpArgs& a, double* super, hipStream_t st, uint32_t* order = nullptr, int ntiles = 0,
+                      const IcpCompact* cp = nullptr);
 // the all-gathered records (rank r's records from recv + r * rank_stride doubles) summed in global record
 // order, one thread per statistic (the order of lio_icp_combine: bit-identical) -> out17 (host-mapped)
 void launch_icp_combine(const double* recv, int64_t nsup, int world, int64_t rank_stride, double* out17, hipStream_t st);

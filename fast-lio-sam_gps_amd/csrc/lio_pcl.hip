@@ -9,7 +9,8 @@
 //              the end; orders 2 / 3: Eigen 3.3's GEMM, the depth blocked by kc(L1 32 / 48 KiB) and
 //              res += alpha * (block's sequential sum) per block (oracle/lio_oracle.cpp UmeyamaOrder)
 // Here:
-//   pcl_compact                          the accepted pairs compacted in source order (one launch, look-back)
+//   (icp_stats_kernel, IcpCompact)       the accepted pairs compacted in source order by the statistics launch
+//                                        (one look-back over the 4096-point records)
 //   seqsum (lio_seqsum.hip)              the six mean chains (and order 1's nine sigma chains), bit-exact
 //                                        sequential float results computed in parallel
 //   pcl_sigma_blocks                     orders 2 / 3: one wave per kc block, nine sequential lanes from LDS
@@ -28,95 +29,8 @@ namespace lio {
 
 namespace {
 
-constexpr int kPT = 256;           // threads per compaction block
-constexpr int kPPer = 4;           // consecutive source points per thread
-constexpr int kPB = kPT * kPPer;   // source points per compaction block
 constexpr int kMaxKc = kPclMaxKc;  // kc at a 48 KiB L1 (the largest modelled)
 constexpr int kPackWin = 1024;     // GEMM depth blocks staged per window in pcl_pack (36 KiB of LDS)
-
-// a.nn_d2 == nullptr (sharded): a.nn_id holds the all-gathered ids, the gate already applied (-1 = rejected)
-__device__ __forceinline__ bool pcl_accept(const IcpArgs& a, int i) {
-    const int id = a.nn_id[i];
-    const float d2 = a.nn_d2 ? a.nn_d2[i] : 0.f;
-    return id >= 0 && id != kNone && !((double)d2 > a.max_d2);
-}
-
-__device__ __forceinline__ uint32_t block_excl_u32(uint32_t v, uint32_t* s_w, uint32_t& tot) {
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    uint32_t inc = v;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t u = __shfl_up(inc, d, 64);
-        if (lane >= d) inc += u;
-    }
-    if (lane == 63) s_w[w] = inc;
-    __syncthreads();
-    uint32_t off = 0, t = 0;
-    for (int i = 0; i < (int)(blockDim.x >> 6); ++i) {
-        if (i < w) off += s_w[i];
-        t += s_w[i];
-    }
-    __syncthreads();
-    tot = t;
-    return off + inc - v;
-}
-
-// The accepted pairs compacted in source order in ONE launch (was count / scan / scatter, 3 launches): every
-// block takes a logical index by ticket (arrival order, so a block only ever waits for blocks already running),
-// publishes its count, and looks back over its predecessors' status words — (epoch, flag, value): flag 1 the
-// block's count, flag 2 its inclusive prefix — until an inclusive one; integers, so any look-back order is
-// exact.  The epoch (a per-launch counter) makes the previous pass's words stale without a memset; the last
-// logical block writes the total and resets the ticket.
-__global__ void __launch_bounds__(kPT) pcl_compact_kernel(IcpArgs a, unsigned long long* __restrict__ st,
-                                                          uint32_t* __restrict__ ticket, uint32_t epoch,
-                                                          float* __restrict__ pairs, int64_t cap,
-                                                          uint32_t* __restrict__ d_n, int nb) {
-    __shared__ uint32_t s_w[kPT / 64];
-    __shared__ uint32_t s_b, s_off;
-    if (threadIdx.x == 0) s_b = atomicAdd(ticket, 1u);
-    __syncthreads();
-    const int b = (int)s_b;
-    const int i0 = b * kPB + threadIdx.x * kPPer;
-    bool ok[kPPer];
-    uint32_t c = 0;
-#pragma unroll
-    for (int i = 0; i < kPPer; ++i) {
-        ok[i] = i0 + i < a.n && pcl_accept(a, i0 + i);
-        c += ok[i] ? 1u : 0u;
-    }
-    uint32_t tot;
-    const uint32_t ex = block_excl_u32(c, s_w, tot);
-    if (threadIdx.x < 64) {  // wave 0: publish, look back (64 predecessors per read), publish the prefix
-        uint32_t acc = 0;
-        if (b > 0) {
-            if (threadIdx.x == 0) lb_store(st, b, lb_word(epoch, 1u, tot));
-            uint64_t unused;
-            bool timeout;
-            acc = lookback_excl<false>(st, nullptr, nullptr, b, epoch, unused, timeout);
-            if (timeout && threadIdx.x == 0) atomicOr(ticket + 1, 1u);  // flagged in pcl_pack's output
-        }
-        if (threadIdx.x == 0) {
-            lb_store(st, b, lb_word(epoch, 2u, acc + tot));
-            s_off = acc;
-            if (b == nb - 1) {
-                *d_n = acc + tot;
-                *ticket = 0u;  // every block has taken its ticket (this one came last)
-            }
-        }
-    }
-    __syncthreads();
-    uint32_t slot = s_off + ex;
-#pragma unroll
-    for (int i = 0; i < kPPer; ++i)
-        if (ok[i]) {
-            const int p = i0 + i;
-            const float4 q = a.tgt_by_id[a.nn_id[p]];
-            const float v[6] = {a.cur[3 * p], a.cur[3 * p + 1], a.cur[3 * p + 2], q.x, q.y, q.z};
-#pragma unroll
-            for (int d = 0; d < 6; ++d) pairs[d * cap + slot] = v[d];
-            ++slot;
-        }
-}
 
 // float means of the sequential sums (order 1's sigma chains read them)
 __global__ void pcl_mean6_kernel(const float* __restrict__ sums6, const uint32_t* __restrict__ d_n,
@@ -507,7 +421,7 @@ int pcl_reserve(PclBuf& p, int64_t n, int order, hipStream_t st) {
         p.bst = nullptr;
         p.Cb = nullptr;
         p.cap = 0;
-        const int64_t nb = (n + kPB - 1) / kPB;
+        const int64_t nb = (n + kIcpSuper - 1) / kIcpSuper + 1;  // one look-back word per 4096-point record
         const int64_t nkc = n / 340 + 2;  // kc >= max_kc / 2 >= 340 once the depth is blocked
         if (hipMalloc(&p.pairs, (size_t)n * 6 * sizeof(float)) != hipSuccess ||
             hipMalloc(&p.bst, (size_t)nb * sizeof(unsigned long long)) != hipSuccess ||
@@ -534,15 +448,16 @@ void pcl_free(PclBuf& p) {
     p = PclBuf{};
 }
 
-void launch_pcl_compact(const IcpArgs& a, PclBuf& p, hipStream_t st) {
-    const int nb = (a.n + kPB - 1) / kPB;
-    uint32_t* d_n = p.small + kPclN;
-    if (nb == 0) {
-        (void)hipMemsetAsync(d_n, 0, sizeof(uint32_t), st);
-        return;
-    }
+IcpCompact pcl_compact_args(PclBuf& p) {
     p.epoch = p.epoch + 1u >= (1u << 30) ? 1u : p.epoch + 1u;  // 30 bits, 0 reserved for "never written"
-    pcl_compact_kernel<<<nb, kPT, 0, st>>>(a, p.bst, p.small + kPclTicket, p.epoch, p.pairs, p.cap, d_n, nb);
+    IcpCompact c;
+    c.pairs = p.pairs;
+    c.cap = p.cap;
+    c.st = p.bst;
+    c.ticket = p.small + kPclTicket;
+    c.epoch = p.epoch;
+    c.d_n = p.small + kPclN;
+    return c;
 }
 
 void launch_pcl_means(PclBuf& p, int pass, hipStream_t st) {

@@ -29,7 +29,7 @@ struct PclBuf {
     float* pairs = nullptr;   // accepted (src xyz, tgt xyz) in source order, column-major: pairs[d * cap + k]
                               // (the chains' per-thread loads are then contiguous, not 24 bytes apart);
                               // sharded: this rank's window, then the next kPclMaxKc pairs of the ranks after it
-    unsigned long long* bst = nullptr;  // per compaction block: look-back status word (epoch, flag, value)
+    unsigned long long* bst = nullptr;  // per 4096-point record of the statistics launch: look-back status word (epoch, flag, value)
     uint32_t epoch = 0;                 // compaction launches so far (mod 2^30, 0 skipped)
     float* Cb = nullptr;      // orders 2 / 3: per depth block, 9 sequential block sums
     uint32_t* small = nullptr;
@@ -76,7 +76,8 @@ void launch_pcl_gather_unpack(PclBuf& g, const double* recv, int64_t stride, int
 int pcl_reserve(PclBuf& p, int64_t n, int order, hipStream_t st);
 void pcl_free(PclBuf& p);
 // the accepted correspondences of the pass (a.nn_id / a.nn_d2 / a.cur after the correspondence kernel)
-void launch_pcl_compact(const IcpArgs& a, PclBuf& p, hipStream_t st);
+// the compaction's arguments for the statistics launch (launch_icp_stats' IcpCompact; a new look-back epoch)
+IcpCompact pcl_compact_args(PclBuf& p);
 void launch_pcl_means(PclBuf& p, int pass, hipStream_t st);
 // sums6: the six float sums the sigma / pack use (nullptr: the seqsum result of launch_pcl_means; the serial
 // fallback passes its own, which need no verification)
