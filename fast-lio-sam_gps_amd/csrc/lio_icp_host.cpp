@@ -1083,9 +1083,17 @@ static int icp_pass_fsh(lio_icp* h, const lio::IcpArgs& a, bool apply_T, double 
         IHIP(hipMemsetAsync(P.small + lio::kPclTicket + 1, 1, sizeof(uint32_t), h->st));
     lio::seqsum_shard_head(fsh_means_src(h), 6, dn, P.means, h->d_xsend + rec, nbs, h->st);
     if ((rc = xchg(h, cnt1))) return rc;
-    lio::launch_icp_combine(h->d_xrecv, nsup, h->world, cnt1, h->h_out17_dev, h->st);
+    // the records' sum in record order rides the offsets launch (lio_icp_combine's order)
+    lio::SeqRecordSum rs;
+    rs.recv = h->d_xrecv;
+    rs.nrec = nsup;
+    rs.world = h->world;
+    rs.stride = cnt1;
+    rs.width = lio::kIcpStride;
+    rs.nval = 17;
+    rs.out = h->h_out17_dev;
     lio::seqsum_shard_mid(fsh_means_src(h), 6, dn, P.means, 1, h->d_xrecv + rec, cnt1, nbs, h->rank, h->world,
-                          h->d_xsend, h->ev_slot, fsh_heads(h), h->st);
+                          h->d_xsend, h->ev_slot, fsh_heads(h), h->st, &rs);
     if ((rc = fsh_means_events(h, 1))) return rc;
     if ((rc = fsh_sigma_pack(h, 1))) return rc;  // waits for the pass
     IHIP(hipGetLastError());

@@ -762,9 +762,36 @@ __global__ void __launch_bounds__(kSeqThreads) seq_verify(Src src, SeqSumBuf b, 
 // structure as seq_scan1; every rank runs it over the same data with the same launch, so the floors agree bit
 // for bit).  One block per chain; lio_seqsum.hpp's seq_shard_offsets_chain states the same arithmetic
 // sequentially (the host mirror).  The blocks of rank r are blocks rb[r] .. rb[r + 1) of the chain.
+// SeqRecordSum's job (the offsets launch's last workgroup): the records through LDS in chunks, loaded by all lanes,
+// then summed by nval lanes in record order
+__device__ void seq_record_sum(const SeqRecordSum& rs, double* s_buf, int cap_rec) {
+    const int k = threadIdx.x;
+    double acc = 0.0;
+    for (int64_t g0 = 0; g0 < rs.nrec; g0 += cap_rec) {
+        const int m = (int)min((int64_t)cap_rec, rs.nrec - g0);
+        for (int e = threadIdx.x; e < m * rs.nval; e += blockDim.x) {
+            const int64_t sidx = g0 + e / rs.nval;
+            int r = (int)(sidx * rs.world / rs.nrec);  // the rank holding record sidx
+            while (r + 1 < rs.world && rs.nrec * (r + 1) / rs.world <= sidx) ++r;
+            while (r > 0 && rs.nrec * r / rs.world > sidx) --r;
+            const int64_t s0 = rs.nrec * r / rs.world;
+            s_buf[e] = rs.recv[(size_t)r * rs.stride + (size_t)(sidx - s0) * rs.width + e % rs.nval];
+        }
+        __syncthreads();
+        if (k < rs.nval)
+            for (int j = 0; j < m; ++j) acc += s_buf[j * rs.nval + k];
+        __syncthreads();
+    }
+    if (k < rs.nval) rs.out[k] = acc;
+}
+
 __global__ void __launch_bounds__(256) seq_shard_offsets(SeqSumBuf b, const double* __restrict__ recv, int64_t stride,
-                                                         int64_t nb_slot, int rank, int world) {
+                                                         int64_t nb_slot, int rank, int world, SeqRecordSum rs) {
     __shared__ double s_sum[kScanWin], s_abs[kScanWin];
+    if (rs.out && (int)blockIdx.x == b.nch) {  // block-uniform: the extra job
+        seq_record_sum(rs, s_sum, kScanWin / max(rs.nval, 1));
+        return;
+    }
     __shared__ double s_vw[256 / 64];
     __shared__ int64_t s_rb[65];
     __shared__ double s_off0, s_var0;
@@ -1025,10 +1052,11 @@ void seqsum_shard_head(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& 
 template <class Src>
 void seqsum_shard_mid(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, const double* tot_recv,
                       int64_t tot_stride, int64_t nb_slot, int rank, int world, double* msg_out, int slot, int nhead,
-                      hipStream_t st) {
+                      hipStream_t st, const SeqRecordSum* rs) {
     const dim3 g(b.nblk, nch);
     if (pass <= 1) {
-        seq_shard_offsets<<<nch, 256, 0, st>>>(b, tot_recv, tot_stride, nb_slot, rank, world);
+        const SeqRecordSum job = rs && rs->out ? *rs : SeqRecordSum{};
+        seq_shard_offsets<<<nch + (job.out ? 1 : 0), 256, 0, st>>>(b, tot_recv, tot_stride, nb_slot, rank, world, job);
         seq_scan1<<<nch, 256, 0, st>>>(b, d_n, pass);
     } else {
         b.forced_dirty = true;  // the failures that led here set forced bits
@@ -1060,7 +1088,7 @@ void seqsum_shard_repack(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf
 #define LIO_SEQ_SHARD_INST(S)                                                                                      \
     template void seqsum_shard_head<S>(const S&, int, const uint32_t*, SeqSumBuf&, double*, int64_t, hipStream_t); \
     template void seqsum_shard_mid<S>(const S&, int, const uint32_t*, SeqSumBuf&, int, const double*, int64_t,     \
-                                      int64_t, int, int, double*, int, int, hipStream_t);                          \
+                                      int64_t, int, int, double*, int, int, hipStream_t, const SeqRecordSum*);     \
     template void seqsum_shard_tail<S>(const S&, int, const uint32_t*, SeqSumBuf&, int, const double*, int64_t, int, \
                                        int, int, const SeqHeads&, hipStream_t);                                    \
     template void seqsum_shard_repack<S>(const S&, int, const uint32_t*, SeqSumBuf&, double*, int, int, hipStream_t);

@@ -261,13 +261,25 @@ struct SeqHeads {
     float* ghead = nullptr;
     int nghead = 0;
 };
+// An extra job for seqsum_shard_mid's offsets launch (one more workgroup): nrec records of `width` doubles, rank r
+// holding records [nrec r / world, nrec (r + 1) / world) at recv + r * stride, their first nval values summed in
+// record order into out (the ICP's per-pass statistics: lio_icp_combine's order, bit for bit)
+struct SeqRecordSum {
+    const double* recv = nullptr;
+    int64_t nrec = 0;
+    int world = 1;
+    int64_t stride = 0;
+    int width = 0;
+    int nval = 0;
+    double* out = nullptr;
+};
 template <class Src>
 void seqsum_shard_head(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, double* tot_out, int64_t nb_slot,
                        hipStream_t st);
 template <class Src>
 void seqsum_shard_mid(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, const double* tot_recv,
                       int64_t tot_stride, int64_t nb_slot, int rank, int world, double* msg_out, int slot, int nhead,
-                      hipStream_t st);
+                      hipStream_t st, const SeqRecordSum* rs = nullptr);
 template <class Src>
 void seqsum_shard_tail(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& b, int pass, const double* msg_recv,
                        int64_t msg_stride, int rank, int world, int slot, const SeqHeads& hd, hipStream_t st);
