@@ -21,6 +21,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdint>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 #include <utility>
@@ -346,10 +347,20 @@ public:
     FilterGPU(const FilterGPU&) = delete;
     FilterGPU& operator=(const FilterGPU&) = delete;
     lio_filter* handle() { return f_; }
+    // host scratch kept across calls (submap_voxelize: the concatenated keyframes and the filter's output), so a
+    // loop timer's calls touch no fresh pages once the largest submap has been seen
+    std::vector<float>& scratch(int i) { return scratch_[i]; }
 
 private:
     lio_filter* f_ = nullptr;
+    std::vector<float> scratch_[2];
 };
+
+// grow a scratch vector to at least n elements, never shrinking it (no zero-fill of reused capacity)
+inline float* scratch_at_least(std::vector<float>& v, size_t n) {
+    if (v.size() < n) v.resize(std::max(n, v.size() + v.size() / 2));
+    return v.data();
+}
 
 // pcl::VoxelGrid<PointT>: setLeafSize / setInputCloud / filter (FAST-LIO downSizeFilterSurf,
 // utilities.hpp voxelizePcd)
@@ -381,20 +392,26 @@ template <typename PointT>
 std::vector<PointT> submap_voxelize(FilterGPU& f, const std::vector<const std::vector<PointT>*>& clouds,
                                     const std::vector<const double*>& poses16, float voxel_res) {
     if (clouds.size() != poses16.size()) throw Error(LIO_ERR_ARG, "submap_voxelize: clouds / poses mismatch");
-    std::vector<PointT> all;
+    constexpr int S = float_stride<PointT>();
     std::vector<int64_t> off{0};
     std::vector<double> T;
     for (size_t k = 0; k < clouds.size(); ++k) {
-        all.insert(all.end(), clouds[k]->begin(), clouds[k]->end());
-        off.push_back((int64_t)all.size());
+        off.push_back(off.back() + (int64_t)clouds[k]->size());
         T.insert(T.end(), poses16[k], poses16[k] + 16);
     }
-    std::vector<PointT> out(all.size());
+    const size_t n_all = (size_t)off.back();
+    // concatenated into reused host memory, sized at least for a C4-sized submap (2^19 points) from the first call
+    const size_t n_cap = std::max(n_all, (size_t)1 << 19) * S + 1;
+    float* all = scratch_at_least(f.scratch(0), n_cap);
+    for (size_t k = 0; k < clouds.size(); ++k)
+        if (!clouds[k]->empty())
+            std::memcpy(all + (size_t)off[k] * S, clouds[k]->data(), clouds[k]->size() * sizeof(PointT));
+    float* res = scratch_at_least(f.scratch(1), n_cap);
     int64_t n = 0;
-    check(lio_submap_voxelize(f.handle(), reinterpret_cast<const float*>(all.data()), off.data(), (int)clouds.size(),
-                              float_stride<PointT>(), T.data(), voxel_res, reinterpret_cast<float*>(out.data()), &n),
+    check(lio_submap_voxelize(f.handle(), all, off.data(), (int)clouds.size(), S, T.data(), voxel_res, res, &n),
           "submap_voxelize");
-    out.resize((size_t)n);
+    std::vector<PointT> out((size_t)n);
+    if (n) std::memcpy(out.data(), res, (size_t)n * sizeof(PointT));
     return out;
 }
 

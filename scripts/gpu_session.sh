@@ -56,6 +56,14 @@ for s in $STEPS; do
            run icpabtrace 300 rocprofv3 --kernel-trace --stats -d "$OUT/icpabtrace" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 &&
            python scripts/icp_tile_passes.py "$OUT/icpabtrace/run_kernel_trace.csv" new > "$OUT/tile_passes_new.txt" &&
            python scripts/kstats.py "$OUT/icpabtrace/run_kernel_stats.csv" > "$OUT/icpab_kstats.txt" ;;
+    lseqab) run lseqgen 300 python -c "
+import sys; sys.path.insert(0, 'fast-lio-sam_gps_amd')
+from lio_gpu import pipeline as PL
+kfs = PL.make_loop_keyframes(n_out=12, n_back=12); PL.write_loop_sequence('/tmp/ls.bin', kfs, range(12, 24))" &&
+            for r in 1 2 3; do
+                run lseq_new_$r 120 fast-lio-sam_gps_amd/lio_gpu/_lib/loop_sequence /tmp/ls.bin &&
+                run lseq_pre_$r 120 fast-lio-sam_gps_amd/build_ab/lseq_pre/loop_sequence /tmp/ls.bin || exit $?
+            done ;;
     lseqt) runs pytest_lseq 600 python -u -m pytest tests/test_cpp_stream.py tests/test_gpu_parity.py -k "loop_sequence or guard" -x -v -s -p no:cacheprovider --timeout 500 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     loopseqprof) run loopseqprof 300 rocprofv3 --kernel-trace --stats -d "$OUT/loopseqprof" -o run --output-format csv -- fast-lio-sam_gps_amd/lio_gpu/_lib/loop_sequence /tmp/ls.bin &&
