@@ -98,7 +98,7 @@ def parse():
     ap.add_argument("--watchdog-s", type=float, default=240.0,
                     help="N > 1: seconds after the headline measurement before rank 0 prints what it has and every "
                          "rank exits (a collective of the secondary sections that never returns)")
-    ap.add_argument("--pmc-sq", default=os.path.join(ROOT, "profiles", "r05_pmc_sq_c3.json"),
+    ap.add_argument("--pmc-sq", default=os.path.join(ROOT, "profiles", "r06_pmc_sq_c3.json"),
                     help="SQ issue / wait breakdown per kernel (scripts/pmc_sq_summary.py of a rocprofv3 --pmc pass)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_summary.json"),
                     help="per-launch HBM traffic measured with rocprofv3 --pmc (profiles/)")
@@ -239,7 +239,7 @@ def _profile_meta(path):
 def _icp_traffic():
     """the ICP tile kernel's HBM traffic per pass from the committed FETCH_SIZE / WRITE_SIZE passes
     (scripts/icp_pmc_traffic.py over scripts/icp_ab.py 1.0 1)"""
-    path = os.path.join(ROOT, "profiles", "r05_pmc_icp_traffic.json")
+    path = os.path.join(ROOT, "profiles", "r06_pmc_icp_traffic.json")
     try:
         pm = json.load(open(path))
     except Exception:
@@ -252,7 +252,7 @@ def _icp_traffic():
 def _icp_sq(args):
     """the ICP correspondence kernels' issue / wait breakdown from the committed SQ counter pass (C4 pairs A
     and B, scripts/icp_ab.py under rocprofv3 --pmc; scripts/pmc_sq_summary.py)"""
-    path = os.path.join(ROOT, "profiles", "r05_pmc_sq_icp.json")
+    path = os.path.join(ROOT, "profiles", "r06_pmc_sq_icp.json")
     try:
         pm = json.load(open(path))
     except Exception:
