@@ -135,7 +135,8 @@ for c in pc: print(c['k'], round(c['ms'], 3), round(c['submaps_ms'], 3), round(c
              run icp_pmc_valu 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU --kernel-trace -d "$OUT/icppmc" -o run --output-format csv -- python scripts/icp_ab.py 1.0 1 ;;
     mapt)  run map_timing 400 python scripts/map_incr_timing.py 20 ;;
     mapprof) run map_prof 400 rocprofv3 --kernel-trace --stats -d "$OUT/mapprof" -o run --output-format csv -- python scripts/map_incr_timing.py 20 ;;
-    nearab) run near_ab 600 bash -c 'for r in 1 2; do python scripts/near_ab.py C3 && LIO_GPU_LIB=build_ab/pre_chunk/liblio_gpu.so python scripts/near_ab.py C3 && LIO_GPU_LIB=build_ab/chunk_u4/liblio_gpu.so python scripts/near_ab.py C3 || exit $?; done' ;;
+    nearab) AB=${AB:-pre_near}
+            run near_ab 600 bash -c "for r in 1 2 3; do python scripts/near_ab.py C3 && LIO_GPU_LIB=fast-lio-sam_gps_amd/build_ab/$AB/liblio_gpu.so python scripts/near_ab.py C3 || exit \$?; done" ;;
     parity) runs pytest_parity 600 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_fullsize.py -x -v -p no:cacheprovider --timeout 500 --timeout-method thread ;;
     icpseed) run icpseed_ab 600 bash -c 'for r in 1 2; do python scripts/icp_ab.py 1.0 5 && LIO_GPU_LIB=fast-lio-sam_gps_amd/build_ab/noseed/liblio_gpu.so python scripts/icp_ab.py 1.0 5 || exit $?; done' ;;
     icppre) run icppre_ab 900 bash -c 'for r in 1 2; do for v in default pre0 pre4 pre025; do if [ $v = default ]; then python scripts/icp_ab.py 1.0 5; else LIO_GPU_LIB=fast-lio-sam_gps_amd/build_ab/$v/liblio_gpu.so python scripts/icp_ab.py 1.0 5; fi || exit $?; echo "^ $v"; done; done' ;;
