@@ -639,8 +639,9 @@ def main():
 
     # ------------------------------------------------- the loop leg as the node runs it (secondary)
     # tests/cpp/loop_sequence.cpp: one lio_gpu::LoopClosure, keyframes_ growing by one per call, each call timed
-    # like loopTimerFunc's "loop: %.1f" (fetchClosestKeyframeIdx + performLoopClosure); the first call is the
-    # cold one (buffers sized), the rest must not allocate (lio_alloc_count)
+    # like loopTimerFunc's "loop: %.1f" (fetchClosestKeyframeIdx + performLoopClosure); the LoopClosure is
+    # prewarmed when the node starts (prewarm_ms: buffers at their floors, code objects loaded), so no call is
+    # cold, and no call after the first may allocate (lio_alloc_count)
     loop_seq = None
     if args.loop_seq > 0 and rank == 0:
         try:

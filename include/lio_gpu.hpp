@@ -704,6 +704,27 @@ public:
         return icp_.icpAlignment(src, dst, &aligned_);
     }
 
+    // Node start-up (no counterpart in the reference): one small submap and alignment through every stage, so
+    // the device buffers (their C4-sized floors), the kernels' code objects and the sort scratch exist before
+    // the first loopTimerFunc call — which otherwise pays ~65 ms for them.  Results are discarded.
+    void prewarm() {
+        std::vector<PointXYZI> a, b;
+        for (int i = 0; i < 100; ++i)  // past the voxel filter's one-block size: the large-input path warmed too
+            for (int j = 0; j < 100; ++j)
+                for (int k = 0; k < 4; ++k) {  // a 100 m x 100 m x 18 m lattice (a submap's extent), b shifted 5 cm
+                    const float x = 1.0f * (float)i, y = 1.0f * (float)j, z = 6.0f * (float)k;
+                    a.push_back({x, y, z, 0.f});
+                    b.push_back({x + 0.05f, y - 0.03f, z + 0.02f, 0.f});
+                }
+        const double I[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+        std::vector<const double*> poses{I};
+        std::vector<const std::vector<PointXYZI>*> ca{&a}, cb{&b};
+        const auto sa = submap_voxelize(f_, ca, poses, (float)config_.voxel_res_);
+        const auto sb = submap_voxelize(f_, cb, poses, (float)config_.voxel_res_);
+        icpAlignment(sa, sb);
+        aligned_.clear();
+    }
+
     // loop_closure.cpp:95-126 (submap_range < 0: num_submap_keyframes_)
     RegistrationOutput performLoopClosure(const PosePcd& query_keyframe, const std::vector<PosePcd>& keyframes,
                                           int closest_keyframe_idx, int submap_range = -1) {
@@ -755,7 +776,9 @@ public:
                      int max_iteration = 3, int point_filter_num = 4, float blind = 2.0f, float filter_size_surf = 0.5f,
                      int device = 0)
         : sm_(tree), lc_(config, device), fs_map_(filter_size_map), max_iter_(max_iteration),
-          prep_{point_filter_num, blind, filter_size_surf, 4} {}
+          prep_{point_filter_num, blind, filter_size_surf, 4} {
+        lc_.prewarm();  // node start-up: the loop leg's first loopTimerFunc call is not the one to size its buffers
+    }
 
     // one raw sweep (n float records of `stride`, the time offset [ms] at field 4), its IMU poses and the
     // scan-end pose; init / P0 the propagated state and covariance
