@@ -8,6 +8,8 @@
 //   seq_events   the events in element order: position, increment prefix, x
 //   seq_walk     one block per chain replays the events (run sums exact in double) -> event results, sum
 //   seq_verify   every s_k rebuilt from the events; s_k == fl(s_{k-1} + x_k) checked for every k
+// A single rank runs the last three as ONE launch, seq_tail (the walk follows the event blocks as they publish,
+// the verification follows the walk); the sharded path keeps them apart (the event exchange sits between).
 #include "lio_seqsum.hpp"
 
 #include <cmath>
@@ -146,9 +148,8 @@ __device__ __forceinline__ bool forced_bit(const uint32_t* f, int64_t k) { retur
 
 // predictions for this thread's elements (pass 1: double prefix; later: the previous reconstruction)
 template <class Src>
-__device__ __forceinline__ void predict(const Src& src, const SeqSumBuf& b, int c, int64_t n, int pass, ElemInfo& in,
-                                        double* s_wd) {
-    const int blk = blockIdx.x;
+__device__ __forceinline__ void predict(const Src& src, const SeqSumBuf& b, int c, int blk, int64_t n, int pass,
+                                        ElemInfo& in, double* s_wd) {
     const int64_t k0 = (int64_t)blk * kSeqBlock + (int64_t)threadIdx.x * kSeqPer;
     load_x(src, c, k0, n, in.x);
     if (pass <= 1) {
@@ -189,10 +190,10 @@ __device__ __forceinline__ void predict(const Src& src, const SeqSumBuf& b, int 
 
 // per element: event flag and increment (element 0: the start, neither)
 template <class Src>
-__device__ __forceinline__ void classify(const SeqSumBuf& b, int c, int64_t n, const ElemInfo& in, int floor_e, int pass,
-                                         bool (&ev)[kSeqPer], uint64_t (&inc)[kSeqPer]) {
+__device__ __forceinline__ void classify(const SeqSumBuf& b, int c, int blk, int64_t n, const ElemInfo& in, int floor_e,
+                                         int pass, bool (&ev)[kSeqPer], uint64_t (&inc)[kSeqPer]) {
     const bool noinc = b.dbg_noinc && pass <= 1;
-    const int64_t k0 = (int64_t)blockIdx.x * kSeqBlock + (int64_t)threadIdx.x * kSeqPer;
+    const int64_t k0 = (int64_t)blk * kSeqBlock + (int64_t)threadIdx.x * kSeqPer;
     const uint32_t* fb = b.forced ? b.forced + (size_t)c * (b.nmax / 32 + 1) : nullptr;
     const int64_t gb = b.sh ? b.sh->gbase : 0;  // global index of local element 0 (sharded windows)
 #pragma unroll
@@ -355,10 +356,10 @@ __global__ void __launch_bounds__(kSeqThreads) seq_count(Src src, SeqSumBuf b, c
     const int64_t n = *d_n;
     if ((int64_t)blockIdx.x * kSeqBlock >= n) return;
     ElemInfo in;
-    predict(src, b, c, n, pass, in, s_wd);
+    predict(src, b, c, (int)blockIdx.x, n, pass, in, s_wd);
     bool ev[kSeqPer];
     uint64_t inc[kSeqPer];
-    classify<Src>(b, c, n, in, b.floor_e[c], pass, ev, inc);
+    classify<Src>(b, c, (int)blockIdx.x, n, in, b.floor_e[c], pass, ev, inc);
     uint64_t su = 0;
     int se = 0;
 #pragma unroll
@@ -415,15 +416,15 @@ __global__ void __launch_bounds__(kSeqThreads) seq_scan2(SeqSumBuf b, const uint
 
 // the block's elements with their exclusive increment prefix and inclusive event count
 template <class Src>
-__device__ __forceinline__ void block_scan_elems(const Src& src, const SeqSumBuf& b, int c, int64_t n, int pass,
+__device__ __forceinline__ void block_scan_elems(const Src& src, const SeqSumBuf& b, int c, int blk, int64_t n, int pass,
                                                  ElemInfo& in, bool (&ev)[kSeqPer], uint64_t (&Pex)[kSeqPer],
                                                  int (&Ein)[kSeqPer]) {
     __shared__ double s_wd[kSeqThreads / 64];
     __shared__ uint64_t s_u[kSeqThreads / 64];
     __shared__ int s_i[kSeqThreads / 64];
-    predict(src, b, c, n, pass, in, s_wd);
+    predict(src, b, c, blk, n, pass, in, s_wd);
     uint64_t inc[kSeqPer];
-    classify<Src>(b, c, n, in, b.floor_e[c], pass, ev, inc);
+    classify<Src>(b, c, blk, n, in, b.floor_e[c], pass, ev, inc);
     uint64_t su = 0;
     int se = 0;
 #pragma unroll
@@ -433,8 +434,8 @@ __device__ __forceinline__ void block_scan_elems(const Src& src, const SeqSumBuf
     }
     uint64_t tu;
     int te;
-    uint64_t pu = block_excl(su, s_u, tu) + b.bPoff[(size_t)c * b.nblk + blockIdx.x];
-    int pe = block_excl(se, s_i, te) + b.bEoff[(size_t)c * b.nblk + blockIdx.x];
+    uint64_t pu = block_excl(su, s_u, tu) + b.bPoff[(size_t)c * b.nblk + blk];
+    int pe = block_excl(se, s_i, te) + b.bEoff[(size_t)c * b.nblk + blk];
 #pragma unroll
     for (int i = 0; i < kSeqPer; ++i) {
         Pex[i] = pu;
@@ -444,17 +445,46 @@ __device__ __forceinline__ void block_scan_elems(const Src& src, const SeqSumBuf
     }
 }
 
-template <class Src>
-__global__ void __launch_bounds__(kSeqThreads) seq_events(Src src, SeqSumBuf b, const uint32_t* d_n, int pass) {
-    const int c = blockIdx.y;
-    const int64_t n = *d_n;
-    if ((int64_t)blockIdx.x * kSeqBlock >= n) return;
+// The fused tail's in-launch hand-offs (seq_tail) use agent-scope (sc1) accesses on both sides, MI355X_MICROARCH.md's
+// hand-off table row 1: every storing wave stores its payload sc1 and waits (s_waitcnt vmcnt(0)), a workgroup barrier,
+// then one lane stores the flag sc1; the consumer polls the flag sc1 and loads the payload sc1.  F = false: the
+// separate launches (kernel boundaries order everything), plain accesses.
+typedef __attribute__((address_space(1))) uint32_t sq_gu32;
+typedef __attribute__((address_space(1))) unsigned long long sq_gu64;
+template <bool F>
+__device__ __forceinline__ uint32_t ld32(const void* p) {
+    if constexpr (F) return __hip_atomic_load((const sq_gu32*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *(const uint32_t*)p;
+}
+template <bool F>
+__device__ __forceinline__ uint64_t ld64(const void* p) {
+    if constexpr (F) return __hip_atomic_load((const sq_gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *(const unsigned long long*)p;
+}
+template <bool F>
+__device__ __forceinline__ void st32(void* p, uint32_t v) {
+    if constexpr (F) __hip_atomic_store((sq_gu32*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *(uint32_t*)p = v;
+}
+template <bool F>
+__device__ __forceinline__ void st64(void* p, uint64_t v) {
+    if constexpr (F) __hip_atomic_store((sq_gu64*)p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else *(unsigned long long*)p = v;
+}
+// a spin's safety valve (wall_clock64 counts at 100 MHz): 20 ms, far beyond any pass; a time-out is a verification
+// failure (re-pass) or an event overflow (the serial kernel), never a wrong result
+constexpr uint64_t kSpinTicks = 2000000;
+
+// block blk's events in element order: position, increment prefix, x (F: published by the block's flag)
+template <class Src, bool F>
+__device__ __forceinline__ void events_block(const Src& src, const SeqSumBuf& b, int c, int blk, int64_t n, int pass,
+                                             uint32_t epoch) {
     ElemInfo in;
     bool ev[kSeqPer];
     uint64_t Pex[kSeqPer];
     int Ein[kSeqPer];
-    block_scan_elems(src, b, c, n, pass, in, ev, Pex, Ein);
-    const int64_t k0 = (int64_t)blockIdx.x * kSeqBlock + (int64_t)threadIdx.x * kSeqPer;
+    block_scan_elems(src, b, c, blk, n, pass, in, ev, Pex, Ein);
+    const int64_t k0 = (int64_t)blk * kSeqBlock + (int64_t)threadIdx.x * kSeqPer;
     // single rank: the walk's lists; sharded: this window's lists (local positions and prefixes, seq_shard_pack)
     int* EPOS = b.sh ? b.lev_pos : b.ev_pos;
     uint64_t* EPP = b.sh ? b.lev_P : b.ev_P;
@@ -465,16 +495,28 @@ __global__ void __launch_bounds__(kSeqThreads) seq_events(Src src, SeqSumBuf b, 
         if (ev[i]) {
             const int idx = Ein[i] - 1;
             if (idx < b.evcap) {
-                EPOS[(size_t)c * es + idx] = (int)(k0 + i);
-                EPP[(size_t)c * es + idx] = Pex[i];
-                EXX[(size_t)c * es + idx] = in.x[i];
+                st32<F>(EPOS + (size_t)c * es + idx, (uint32_t)(k0 + i));
+                st64<F>(EPP + (size_t)c * es + idx, Pex[i]);
+                st32<F>(EXX + (size_t)c * es + idx, __float_as_uint(in.x[i]));
             }
         }
+    if constexpr (F) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) st32<true>(b.evflag + (size_t)c * b.nblk + blk, epoch);
+    }
+}
+
+template <class Src>
+__global__ void __launch_bounds__(kSeqThreads) seq_events(Src src, SeqSumBuf b, const uint32_t* d_n, int pass) {
+    const int64_t n = *d_n;
+    if ((int64_t)blockIdx.x * kSeqBlock >= n) return;
+    events_block<Src, false>(src, b, (int)blockIdx.y, (int)blockIdx.x, n, pass, 0u);
 }
 
 // The walk: s_{event-1} = s_{previous event} + run sum R (exact), s_event = fl(s_{event-1} + x_event), one chain
 // per block.  The chain of dependent operations is the serial floor; everything else is kept off it:
-//   * the event records stream through LDS in chunks of kWalkChunk, double-buffered: while wave 0 walks chunk k,
+//   * the event records stream through LDS in chunks of C events, double-buffered: while wave 0 walks chunk k,
 //     waves 1-3 prepare chunk k+1 (run sums from the increment prefixes, the fast-path test) and store chunk
 //     k-1's results, so the walk never waits on a global load;
 //   * fast groups: when every run sum R of a 64-event group is a float exactly (tested while preparing), the
@@ -485,38 +527,69 @@ __global__ void __launch_bounds__(kSeqThreads) seq_events(Src src, SeqSumBuf b, 
 //   * other groups (a run spanning more than 24 bits of the chain's fixed-point unit) take the general form,
 //     fl32(fl32(fl64(s + R)) + x).  seq_verify checks every element either way.
 constexpr int kWalkThreads = 256;
-constexpr int kWalkChunk = 1024;  // events per LDS chunk (x 2 buffers x 20 bytes)
+constexpr int kWalkChunk = 1024;  // events per LDS chunk, separate launches (x 2 buffers x 20 bytes)
+constexpr int kTailChunk = 512;   // the fused tail's: 20 KB of LDS, so its event / verification roles keep 7 blocks per CU
 constexpr int kWalkU = 8;
+template <int C>
 struct alignas(16) WalkChunk {
-    double R[kWalkChunk];  // run sums (exact)
-    float Rf[kWalkChunk];  // the same as floats (fast groups)
-    float x[kWalkChunk];
-    float f[kWalkChunk];   // the walk's results
-    int fast[kWalkChunk / 64];
+    double R[C];  // run sums (exact)
+    float Rf[C];  // the same as floats (fast groups)
+    float x[C];
+    float f[C];   // the walk's results
+    int fast[C / 64];
 };
+
+// F: every element block whose events start before e_end has published them (its flag holds this launch's epoch).
+// Wave-uniform; jdone (the wave's own) = blocks already seen published, in element order.  false: time-out.
+__device__ __forceinline__ bool wait_events(const SeqSumBuf& b, int c, int nb, int e_end, int& jdone, uint32_t epoch) {
+    const int lane = threadIdx.x & 63;
+    const int* EO = b.bEoff + (size_t)c * b.nblk;
+    const uint32_t* FL = b.evflag + (size_t)c * b.nblk;
+    const uint64_t t0 = wall_clock64();
+    while (jdone < nb) {
+        const int j = jdone + lane;
+        const bool need = j < nb && EO[j] < e_end;  // bEoff is non-decreasing: the needed blocks are a prefix
+        const bool ok = !need || ld32<true>(FL + j) == epoch;
+        const uint64_t bad = __ballot(!ok);
+        if (bad) {
+            jdone += __builtin_ctzll(bad);
+            if (wall_clock64() - t0 > kSpinTicks) return false;
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        const uint64_t done = __ballot(!need);
+        if (done) {
+            jdone += __builtin_ctzll(done);
+            return true;
+        }
+        jdone += 64;
+    }
+    return true;
+}
 
 // chunk k's records into B by the threads [t0, t0 + nt) (nt a multiple of 64, t0 wave-aligned, nt >= 192): every
 // load of the thread's share is issued before the first is used (the preparation runs beside the walk and must
 // stay shorter than it: one round trip to memory per chunk, not one per step)
-constexpr int kPrepMax = (kWalkChunk + 191) / 192;
-__device__ __forceinline__ void walk_prepare(WalkChunk& B, int k, int nev, double unit, const uint64_t* EP,
+template <int C, bool F>
+__device__ __forceinline__ void walk_prepare(WalkChunk<C>& B, int k, int nev, double unit, const uint64_t* EP,
                                              const float* EX, int t, int nt) {
-    const int e0 = k * kWalkChunk;
-    const int m = min(kWalkChunk, nev - e0);
+    constexpr int kPrepMax = (C + 191) / 192;
+    const int e0 = k * C;
+    const int m = min(C, nev - e0);
     uint64_t P[kPrepMax], Pp[kPrepMax];
     float X[kPrepMax];
 #pragma unroll
     for (int q = 0; q < kPrepMax; ++q) {
         const int j = t + q * nt, i = e0 + j;
         const bool in = j < m;
-        P[q] = in ? EP[i] : 0;
-        Pp[q] = in && i > 0 ? EP[i - 1] : 0;
-        X[q] = in ? EX[i] : 0.f;
+        P[q] = in ? ld64<F>(EP + i) : 0;
+        Pp[q] = in && i > 0 ? ld64<F>(EP + i - 1) : 0;
+        X[q] = in ? __uint_as_float(ld32<F>(EX + i)) : 0.f;
     }
 #pragma unroll
     for (int q = 0; q < kPrepMax; ++q) {
         const int j = t + q * nt;
-        if (j >= kWalkChunk) break;  // wave-uniform: one 64-event group per wave and step
+        if (j >= C) break;  // wave-uniform: one 64-event group per wave and step
         const double R = j < m ? (double)(int64_t)(P[q] - Pp[q]) * unit : 0.0;  // a run sum: exact (<= 53 bits)
         const float Rf = (float)R;
         B.R[j] = R;
@@ -528,13 +601,13 @@ __device__ __forceinline__ void walk_prepare(WalkChunk& B, int k, int nev, doubl
     }
 }
 
-// the float form over one 64-event group from e0 (all fast), in four steps of 16: a step's operands are read from
-// LDS while the step before it adds (the LDS latency off the chain), results stored 4 at a time
-__device__ __forceinline__ float walk_fast(WalkChunk& B, int e0, float s) {
+// the float form over one 64-event group (all fast), in four steps of 16: a step's operands are read from LDS while
+// the step before it adds (the LDS latency off the chain), results stored 4 at a time
+__device__ __forceinline__ float walk_fast(const float* Rf, const float* Xs, float* Fo, float s) {
     constexpr int nsteps = 4;
-    const float4* R4 = reinterpret_cast<const float4*>(B.Rf + e0);
-    const float4* X4 = reinterpret_cast<const float4*>(B.x + e0);
-    float4* F4 = reinterpret_cast<float4*>(B.f + e0);
+    const float4* R4 = reinterpret_cast<const float4*>(Rf);
+    const float4* X4 = reinterpret_cast<const float4*>(Xs);
+    float4* F4 = reinterpret_cast<float4*>(Fo);
     float4 r0[4], x0[4];
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
@@ -575,133 +648,199 @@ __device__ __forceinline__ float walk_fast(WalkChunk& B, int e0, float s) {
     return s;
 }
 
-template <class Src>
-__global__ void __launch_bounds__(kWalkThreads) seq_walk(Src src, SeqSumBuf b, const uint32_t* d_n) {
-    __shared__ WalkChunk wb[2];
-    const int c = blockIdx.x;
+// wave 0, lane 0: chunk B's m events from s
+template <int C>
+__device__ __forceinline__ float walk_chunk(WalkChunk<C>& B, int m, float s) {
+    for (int g = 0; g < m; g += 64) {
+        const int cnt = min(64, m - g);
+        if (cnt == 64 && B.fast[g >> 6]) {
+            s = walk_fast(B.Rf + g, B.x + g, B.f + g, s);
+        } else if (cnt == 64) {
+            for (int l = g; l < g + 64; l += kWalkU) {
+                double r[kWalkU];
+                float x[kWalkU];
+#pragma unroll
+                for (int u = 0; u < kWalkU; ++u) {
+                    r[u] = B.R[l + u];
+                    x[u] = B.x[l + u];
+                }
+#pragma unroll
+                for (int u = 0; u < kWalkU; ++u) {
+                    s = (float)((double)s + r[u]) + x[u];
+                    B.f[l + u] = s;
+                }
+            }
+        } else {
+            for (int l = g; l < g + cnt; ++l) {
+                s = (float)((double)s + B.R[l]) + B.x[l];
+                B.f[l] = s;
+            }
+        }
+    }
+    return s;
+}
+
+// F: the walk's progress word of chain c, epoch << 32 | events whose results are stored (sc1)
+__device__ __forceinline__ void walk_publish(const SeqSumBuf& b, int c, uint32_t epoch, uint32_t done) {
+    st64<true>(b.wprog + c, ((uint64_t)epoch << 32) | done);
+}
+
+// the walker of chain c (kWalkThreads threads).  F: the events arrive in this launch (wait_events before a chunk
+// is prepared), the results are stored sc1 and published chunk by chunk for the verification roles
+template <class Src, int C, bool F>
+__device__ __forceinline__ void walk_chain(const Src& src, const SeqSumBuf& b, int c, int64_t n, uint32_t epoch) {
+    __shared__ WalkChunk<C> wb[2];
+    __shared__ int s_abort;
     const int t = threadIdx.x, w = t >> 6;
-    const int64_t n = b.sh ? b.sh->n_global : *d_n;  // sharded: every rank walks the whole chain's events
     if (n <= 0) {
         if (t == 0) b.result[c] = 0.f;
         return;
     }
-    if ((b.status[1] >> c) & 1u) return;  // event overflow: the caller falls back
+    if ((b.status[1] >> c) & 1u) return;  // event overflow: the caller falls back (the verification roles skip too)
     const int nev = b.floor_e[b.nch + c];
     const double unit = ldexp(1.0, b.floor_e[c] - 23);
     const uint64_t* EP = b.ev_P + (size_t)c * b.evs;
     const float* EX = b.ev_x + (size_t)c * b.evs;
     float* ES = b.ev_s + (size_t)c * b.evs;
-    const int nchunk = (nev + kWalkChunk - 1) / kWalkChunk;
+    const int nchunk = (nev + C - 1) / C;
+    const int nb = (int)((n + kSeqBlock - 1) / kSeqBlock);
+    int jdone = 0;  // F: this wave's published-blocks prefix
     float s = b.sh ? b.sh->x0[c] : src(c, 0);  // the chain (lane 0 of wave 0)
-#ifdef LIO_WALK_DIAG  // diagnostics build: the walk's time split and its general-form share, printed per chain
-    const uint64_t t0 = wall_clock64();
-    uint64_t t_walk = 0, t_sync = 0;
-    int n_fast = 0, n_slow = 0;
+#ifdef LIO_TAIL_DIAG  // diagnostics build: the walker's time split (wall_clock64 ticks, 10 ns)
+    const uint64_t d_t0 = wall_clock64();
+    uint64_t d_walk = 0, d_wait = 0, d_ready = 0;
 #endif
-    if (nchunk > 0) walk_prepare(wb[0], 0, nev, unit, EP, EX, t, kWalkThreads);
+    if (t == 0) s_abort = 0;
     __syncthreads();
-#ifdef LIO_WALK_DIAG
-    const uint64_t t1 = wall_clock64();
+    if (nchunk > 0) {
+        if (F && !wait_events(b, c, nb, min(nev, C), jdone, epoch)) s_abort = 1;
+        walk_prepare<C, F>(wb[0], 0, nev, unit, EP, EX, t, kWalkThreads);
+    }
+    __syncthreads();
+#ifdef LIO_TAIL_DIAG
+    d_ready = wall_clock64() - d_t0;
 #endif
-    for (int k = 0; k < nchunk; ++k) {
-#ifdef LIO_WALK_DIAG
-        const uint64_t ta = wall_clock64();
-#endif
+    for (int k = 0; k < nchunk && !s_abort; ++k) {
         if (w == 0) {
-            if (t == 0) {
-                WalkChunk& B = wb[k & 1];
-                const int m = min(kWalkChunk, nev - k * kWalkChunk);
-                for (int g = 0; g < m; g += 64) {
-                    const int cnt = min(64, m - g);
-#ifdef LIO_WALK_DIAG
-                    if (cnt == 64 && B.fast[g >> 6]) ++n_fast; else ++n_slow;
+#ifdef LIO_TAIL_DIAG
+            const uint64_t ta = wall_clock64();
 #endif
-                    if (cnt == 64 && B.fast[g >> 6]) {
-                        s = walk_fast(B, g, s);
-                    } else if (cnt == 64) {
-                        for (int l = g; l < g + 64; l += kWalkU) {
-                            double r[kWalkU];
-                            float x[kWalkU];
-#pragma unroll
-                            for (int u = 0; u < kWalkU; ++u) {
-                                r[u] = B.R[l + u];
-                                x[u] = B.x[l + u];
-                            }
-#pragma unroll
-                            for (int u = 0; u < kWalkU; ++u) {
-                                s = (float)((double)s + r[u]) + x[u];
-                                B.f[l + u] = s;
-                            }
-                        }
-                    } else {
-                        for (int l = g; l < g + cnt; ++l) {
-                            s = (float)((double)s + B.R[l]) + B.x[l];
-                            B.f[l] = s;
-                        }
-                    }
-                }
-            }
+            if (t == 0) s = walk_chunk(wb[k & 1], min(C, nev - k * C), s);
+#ifdef LIO_TAIL_DIAG
+            d_walk += wall_clock64() - ta;
+#endif
         } else {
-            if (k + 1 < nchunk) walk_prepare(wb[(k + 1) & 1], k + 1, nev, unit, EP, EX, t - 64, kWalkThreads - 64);
+            if (F && t == 64 && k > 1) walk_publish(b, c, epoch, (uint32_t)((k - 1) * C));  // chunks < k-1: stored
+            if (k + 1 < nchunk) {
+#ifdef LIO_TAIL_DIAG
+                const uint64_t ta = wall_clock64();
+#endif
+                if (F && !wait_events(b, c, nb, min(nev, (k + 2) * C), jdone, epoch)) s_abort = 1;
+#ifdef LIO_TAIL_DIAG
+                d_wait += wall_clock64() - ta;
+#endif
+                walk_prepare<C, F>(wb[(k + 1) & 1], k + 1, nev, unit, EP, EX, t - 64, kWalkThreads - 64);
+            }
             if (k > 0) {  // chunk k-1's results (its buffer's f: the preparation above writes only R, Rf, x)
-                const WalkChunk& B = wb[(k - 1) & 1];
-                const int e0 = (k - 1) * kWalkChunk;
-                for (int j = t - 64; j < kWalkChunk; j += kWalkThreads - 64) ES[e0 + j] = B.f[j];
+                const WalkChunk<C>& B = wb[(k - 1) & 1];
+                const int e0 = (k - 1) * C;
+                for (int j = t - 64; j < C; j += kWalkThreads - 64) st32<F>(ES + e0 + j, __float_as_uint(B.f[j]));
+                if (F) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
         }
-#ifdef LIO_WALK_DIAG
-        const uint64_t tb = wall_clock64();
-        t_walk += tb - ta;
-#endif
         __syncthreads();
-#ifdef LIO_WALK_DIAG
-        t_sync += wall_clock64() - tb;
-#endif
     }
-#ifdef LIO_WALK_DIAG
-    if (t == 0)
-        printf("walk chain %d: events %d groups fast %d general %d | ticks prologue %llu walk %llu sync %llu\n", c, nev,
-               n_fast, n_slow, (unsigned long long)(t1 - t0), (unsigned long long)t_walk, (unsigned long long)t_sync);
-#endif
+    if (s_abort) {  // F only: a time-out waiting for events; the chain goes to the serial kernel
+        if (t == 0) {
+            atomicOr(&b.status[1], 1u << c);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            walk_publish(b, c, epoch, 0xffffffffu);
+        }
+        return;
+    }
     if (nchunk > 0) {
-        const WalkChunk& B = wb[(nchunk - 1) & 1];
-        const int e0 = (nchunk - 1) * kWalkChunk;
+        const WalkChunk<C>& B = wb[(nchunk - 1) & 1];
+        const int e0 = (nchunk - 1) * C;
         const int m = nev - e0;
-        for (int j = t; j < m; j += kWalkThreads) ES[e0 + j] = B.f[j];
+        for (int j = t; j < m; j += kWalkThreads) st32<F>(ES + e0 + j, __float_as_uint(B.f[j]));
     }
+    if constexpr (F) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) walk_publish(b, c, epoch, (uint32_t)nev);
+    }
+#ifdef LIO_TAIL_DIAG
+    __shared__ uint64_t s_wait;
+    if (t == 64) s_wait = d_wait;
+    __syncthreads();
+    if (t == 0)
+        printf("tail walker %d F%d: events %d ready %llu walk %llu wait(w1) %llu total %llu start %llu\n", c, (int)F, nev,
+               (unsigned long long)d_ready, (unsigned long long)d_walk, (unsigned long long)s_wait,
+               (unsigned long long)(wall_clock64() - d_t0), (unsigned long long)(d_t0 % 100000000ull));
+#endif
     if (t == 0) {
-        const uint64_t Plast = nev > 0 ? EP[nev - 1] : 0;
+        const uint64_t Plast = nev > 0 ? ld64<F>(EP + nev - 1) : 0;
         b.result[c] = (float)((double)s + (double)(int64_t)(b.ptot[c] - Plast) * unit);
     }
 }
 
-// s_k for every element from the events; checks s_k == fl(s_{k-1} + x_k); stores the reconstruction
 template <class Src>
-__global__ void __launch_bounds__(kSeqThreads) seq_verify(Src src, SeqSumBuf b, const uint32_t* d_n, int pass) {
+__global__ void __launch_bounds__(kWalkThreads) seq_walk(Src src, SeqSumBuf b, const uint32_t* d_n) {
+    const int64_t n = b.sh ? b.sh->n_global : *d_n;  // sharded: every rank walks the whole chain's events
+    walk_chain<Src, kWalkChunk, false>(src, b, (int)blockIdx.x, n, 0u);
+}
+
+// s_k for every element of block blk from the events; checks s_k == fl(s_{k-1} + x_k); stores the reconstruction.
+// F: the events and their results arrive in this launch: the walk's progress word is polled first
+template <class Src, bool F>
+__device__ __forceinline__ void verify_block(const Src& src, const SeqSumBuf& b, int c, int blk, int64_t n, int pass,
+                                             uint32_t epoch) {
     __shared__ float s_lastv[kSeqThreads / 64];
-    __shared__ uint32_t s_bad;
-    const int c = blockIdx.y;
-    const int64_t n = *d_n;
-    if ((int64_t)blockIdx.x * kSeqBlock >= n) return;
-    if ((b.status[1] >> c) & 1u) return;
+    __shared__ uint32_t s_bad, s_skip;
     if (threadIdx.x == 0) s_bad = 0;
+    // the block's predictions, events and prefixes need no walk result (F: done while the walk runs; measured 2 %
+    // faster per alignment than waiting first, profiles/r06_seq_tail_ab.txt)
     ElemInfo in;
     bool ev[kSeqPer];
     uint64_t Pex[kSeqPer];
     int Ein[kSeqPer];
-    block_scan_elems(src, b, c, n, pass, in, ev, Pex, Ein);
+    block_scan_elems(src, b, c, blk, n, pass, in, ev, Pex, Ein);
+    if constexpr (F) {
+        if (threadIdx.x == 0) {
+            // every event up to this block's last one walked and stored
+            const uint32_t need = (uint32_t)(b.bEoff[(size_t)c * b.nblk + blk] + b.bev[(size_t)c * b.nblk + blk]);
+            const uint64_t t0 = wall_clock64();
+            uint32_t skip = 0;
+            for (;;) {
+                const uint64_t wv = ld64<true>(b.wprog + c);
+                if ((uint32_t)(wv >> 32) == epoch && (uint32_t)wv >= need) break;
+                if (wall_clock64() - t0 > kSpinTicks) {
+                    skip = 2;
+                    break;
+                }
+                __builtin_amdgcn_s_sleep(2);
+            }
+            if (!skip && ((ld32<true>(b.status + 1) >> c) & 1u)) skip = 1;  // the walker gave up: serial kernel
+            s_skip = skip;
+        }
+        __syncthreads();
+        if (s_skip) {
+            if (threadIdx.x == 0 && s_skip == 2) atomicOr(&b.status[0], 1u << c);  // time-out: a re-pass
+            return;
+        }
+    }
     const double unit = ldexp(1.0, b.floor_e[c] - 23);
     const uint64_t* EP = b.ev_P + (size_t)c * b.evs;
     const float* ES = b.ev_s + (size_t)c * b.evs;
     const float x0 = b.sh ? b.sh->x0[c] : src(c, 0);
     const int64_t gb = b.sh ? b.sh->gbase : 0;  // sharded: event positions are global, k0 local
-    const int64_t k0 = (int64_t)blockIdx.x * kSeqBlock + (int64_t)threadIdx.x * kSeqPer;
+    const int64_t k0 = (int64_t)blk * kSeqBlock + (int64_t)threadIdx.x * kSeqPer;
     // s of element k from (inclusive event count E, inclusive increment prefix P, is-event)
     auto rebuild = [&](bool is_ev, int E, uint64_t Pin) -> float {
         const int idx = E - 1;
-        if (is_ev) return ES[idx];
-        const float bs = idx >= 0 ? ES[idx] : x0;
-        const uint64_t bp = idx >= 0 ? EP[idx] : 0;
+        if (is_ev) return __uint_as_float(ld32<F>(ES + idx));
+        const float bs = idx >= 0 ? __uint_as_float(ld32<F>(ES + idx)) : x0;
+        const uint64_t bp = idx >= 0 ? ld64<F>(EP + idx) : 0;
         return (float)((double)bs + (double)(int64_t)(Pin - bp) * unit);
     };
     // inclusive increment prefix = exclusive + the element's own increment (classify is deterministic)
@@ -709,7 +848,7 @@ __global__ void __launch_bounds__(kSeqThreads) seq_verify(Src src, SeqSumBuf b, 
     {
         bool ev2[kSeqPer];
         uint64_t inc2[kSeqPer];
-        classify<Src>(b, c, n, in, b.floor_e[c], pass, ev2, inc2);
+        classify<Src>(b, c, blk, n, in, b.floor_e[c], pass, ev2, inc2);
 #pragma unroll
         for (int i = 0; i < kSeqPer; ++i) {
             const int64_t k = k0 + i;
@@ -728,9 +867,9 @@ __global__ void __launch_bounds__(kSeqThreads) seq_verify(Src src, SeqSumBuf b, 
             // the previous block's last element (a window's first block: the previous rank's last): bEoff / bPoff
             // of this block are its inclusive values (global once seq_shard_merge has added the ranks before);
             // whether it is an event is read back from the event list (global position)
-            const int E = b.bEoff[(size_t)c * b.nblk + blockIdx.x];
-            const uint64_t Pin = b.bPoff[(size_t)c * b.nblk + blockIdx.x];
-            const bool is_ev = E > 0 && b.ev_pos[(size_t)c * b.evs + (E - 1)] == (int)(gb + k0 - 1);
+            const int E = b.bEoff[(size_t)c * b.nblk + blk];
+            const uint64_t Pin = b.bPoff[(size_t)c * b.nblk + blk];
+            const bool is_ev = E > 0 && (int)ld32<F>(b.ev_pos + (size_t)c * b.evs + (E - 1)) == (int)(gb + k0 - 1);
             prev = rebuild(is_ev, E, Pin);
             if (k0 == 0) b.sh->prev_s[c] = prev;  // (k0 == 0 here only when sharded) the next pass's prediction
         }
@@ -754,6 +893,45 @@ __global__ void __launch_bounds__(kSeqThreads) seq_verify(Src src, SeqSumBuf b, 
     if (bad) s_bad = 1;
     __syncthreads();
     if (threadIdx.x == 0 && s_bad) atomicOr(&b.status[0], 1u << c);
+}
+
+template <class Src>
+__global__ void __launch_bounds__(kSeqThreads) seq_verify(Src src, SeqSumBuf b, const uint32_t* d_n, int pass) {
+    const int c = blockIdx.y;
+    const int64_t n = *d_n;
+    if ((int64_t)blockIdx.x * kSeqBlock >= n) return;
+    if ((b.status[1] >> c) & 1u) return;
+    verify_block<Src, false>(src, b, c, (int)blockIdx.x, n, pass, 0u);
+}
+
+// The fused tail (single rank): events, walk and verification in ONE launch, so the walk starts on the first
+// blocks' events while later blocks still list theirs, and the verification runs behind the walk on the CUs the
+// walkers leave idle.  Roles by workgroup index: [0, nch) the walkers, then the event blocks, then the verification
+// blocks, both element-major.  Walkers wait on event blocks (which wait on nothing), verification blocks on
+// walkers.  Workgroups are dispatched in index order (observed, not promised): every walker and event block is then
+// resident before a verification block; were it not, the waits' time-outs (kSpinTicks) end them as a failed
+// verification (a re-pass) or an event overflow (the serial kernel) — slower, never wrong, never hung.
+template <class Src>
+__global__ void __launch_bounds__(kSeqThreads) seq_tail(Src src, SeqSumBuf b, const uint32_t* d_n, int pass, int nch,
+                                                        uint32_t epoch) {
+    static_assert(kSeqThreads == kWalkThreads, "one block size for every role");
+    const uint32_t r = blockIdx.x;
+    const int64_t n = *d_n;
+    if (r < (uint32_t)nch) {
+        walk_chain<Src, kTailChunk, true>(src, b, (int)r, n, epoch);
+        return;
+    }
+    uint32_t i = r - (uint32_t)nch;
+    const uint32_t nrole = (uint32_t)b.nblk * (uint32_t)nch;
+    const bool verify = i >= nrole;
+    if (verify) i -= nrole;
+    const int c = (int)(i % (uint32_t)nch), blk = (int)(i / (uint32_t)nch);
+    if ((int64_t)blk * kSeqBlock >= n) return;
+    if ((b.status[1] >> c) & 1u) return;  // event overflow (seq_scan2): the serial kernel
+    if (verify)
+        verify_block<Src, true>(src, b, c, blk, n, pass, epoch);
+    else
+        events_block<Src, true>(src, b, c, blk, n, pass, epoch);
 }
 
 // ---------------------------------------------------------------- sharded chains (lio_seqsum.hpp)
@@ -1022,9 +1200,11 @@ void seqsum_launch_impl(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf&
     }
     seq_count<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
     seq_scan2<<<nch, kSeqThreads, 0, st>>>(b, d_n);
-    seq_events<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
-    seq_walk<Src><<<nch, kWalkThreads, 0, st>>>(src, b, d_n);
-    seq_verify<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
+    // events, walk and verification: one launch (seq_tail); its grid is sized for the capacity, the blocks past n
+    // leave at once
+    const uint32_t total = (uint32_t)nch * (1u + 2u * (uint32_t)b.nblk);
+    if (++b.tail_epoch == 0) b.tail_epoch = 1;  // flags and progress words of earlier launches never match
+    seq_tail<Src><<<total, kSeqThreads, 0, st>>>(src, b, d_n, pass, nch, b.tail_epoch);
 }
 
 }  // namespace
@@ -1125,7 +1305,7 @@ int seqsum_reserve(SeqSumBuf& b, int nch, int64_t nmax, hipStream_t st) {
     b.nch = nch;
     b.nmax = nmax;
     b.nblk = (int)((nmax + kSeqBlock - 1) / kSeqBlock);
-    count_alloc(18);
+    count_alloc(20);
     b.evcap = b.evcap_alloc = nmax / 4 + 1024;  // events are ~0.3 % of a C4 chain; past a quarter the serial kernel is as fast
     b.evs = b.evcap;
     b.evs_alloc = 2 * b.evcap_alloc;  // the walk's lists: sharded, every rank's events (O(window): 2 x its own)
@@ -1142,18 +1322,24 @@ int seqsum_reserve(SeqSumBuf& b, int nch, int64_t nmax, hipStream_t st) {
               hipMalloc(&b.ev_s, (size_t)nch * b.evs_alloc * sizeof(float)) == hipSuccess &&
               hipMalloc(&b.recon, (size_t)nch * nmax * sizeof(float)) == hipSuccess &&
               hipMalloc(&b.forced, (size_t)nch * (nmax / 32 + 1) * sizeof(uint32_t)) == hipSuccess &&
-              hipMalloc(&b.status, 4 * sizeof(uint32_t)) == hipSuccess && hipMalloc(&b.result, nch * sizeof(float)) == hipSuccess;
+              hipMalloc(&b.status, 4 * sizeof(uint32_t)) == hipSuccess && hipMalloc(&b.result, nch * sizeof(float)) == hipSuccess &&
+              hipMalloc(&b.evflag, nb * sizeof(uint32_t)) == hipSuccess &&
+              hipMalloc(&b.wprog, nch * sizeof(uint64_t)) == hipSuccess;
     if (!ok) {
         seqsum_free(b);
         return -5;
     }
     (void)hipMemsetAsync(b.status, 0, 4 * sizeof(uint32_t), st);
+    (void)hipMemsetAsync(b.evflag, 0, nb * sizeof(uint32_t), st);
+    (void)hipMemsetAsync(b.wprog, 0, nch * sizeof(uint64_t), st);
+    b.tail_epoch = 0;
     return 0;
 }
 
 void seqsum_free(SeqSumBuf& b) {
     void* ptrs[] = {b.bsum, b.babs, b.boff,   b.bdelta, b.btot,   b.bev,   b.bPoff, b.bEoff, b.floor_e,
                     b.ptot, b.ev_pos, b.ev_P, b.ev_x, b.ev_s, b.recon, b.forced, b.status, b.result,
+                    b.evflag, b.wprog,
                     b.sh,   b.lev_pos, b.lev_P, b.lev_x};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);

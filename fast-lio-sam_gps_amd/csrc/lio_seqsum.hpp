@@ -188,6 +188,11 @@ struct SeqSumBuf {
                                 // failure the caller acts on goes through a pass > 1)
     uint32_t* status = nullptr; // [0] chains failing verification (bits), [1] event overflow (bits)
     float* result = nullptr;    // [nch] final sums
+    // the fused tail (seq_tail, single rank): event blocks' published flags, the walkers' progress words, the
+    // launch's epoch (host; tags the flags and words, never 0)
+    uint32_t* evflag = nullptr; // [nch][nblk]
+    uint64_t* wprog = nullptr;  // [nch] epoch << 32 | events walked and stored
+    uint32_t tail_epoch = 0;
     // sharded: sh (device) set, evs the per-chain stride of the walk's (global) event lists ev_*, the local
     // lists in lev_* (stride evcap); single rank: sh == nullptr, evs == evcap, events straight into ev_*
     SeqShard* sh = nullptr;
