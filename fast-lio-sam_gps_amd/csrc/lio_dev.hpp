@@ -1167,7 +1167,8 @@ __device__ __forceinline__ unsigned long long lb_load(const unsigned long long* 
 // The exclusive prefix of block b (all 64 lanes of the calling wave; b > 0, its aggregate already published).
 // 64-bit second values ride along: aggregate / inclusive in agg64[j] / inc64[j], stored before the word that
 // announces them (store, s_waitcnt vmcnt(0), word) and loaded after it (the load's address depends on the flag).
-// spin bound: a safety valve only (sets *timeout), every predecessor publishes before it looks back itself.
+// time bound: a safety valve only (sets *timeout after 20 ms of wall_clock64's 100 MHz), every predecessor publishes
+// before it looks back itself.
 template <bool WITH64>
 __device__ inline uint32_t lookback_excl(const unsigned long long* st, const unsigned long long* agg64,
                                          const unsigned long long* inc64, int b, uint32_t epoch, uint64_t& ex64,
@@ -1176,7 +1177,7 @@ __device__ inline uint32_t lookback_excl(const unsigned long long* st, const uns
     uint32_t acc = 0;
     uint64_t acc64 = 0;
     timeout = false;
-    uint32_t spins = 0;
+    const uint64_t t0 = wall_clock64();
     for (int j = b - 1; j >= 0;) {
         const int idx = j - lane;
         unsigned long long w = idx >= 0 ? lb_load(st, idx) : lb_word(epoch, 2u, 0u);
@@ -1187,7 +1188,7 @@ __device__ inline uint32_t lookback_excl(const unsigned long long* st, const uns
         const int fi = incl ? __builtin_ctzll(incl) : 64;   // nearest inclusive word
         const int fv = inval ? __builtin_ctzll(inval) : 64; // nearest unpublished word
         if (fv < fi) {  // a word before the nearest inclusive one is not published yet: read the window again
-            if (++spins > (1u << 24)) {
+            if (wall_clock64() - t0 > 2000000ull) {
                 timeout = true;
                 break;
             }

@@ -8,12 +8,14 @@
 //   seq_events   the events in element order: position, increment prefix, x
 //   seq_walk     one block per chain replays the events (run sums exact in double) -> event results, sum
 //   seq_verify   every s_k rebuilt from the events; s_k == fl(s_{k-1} + x_k) checked for every k
-// A single rank runs the last three as ONE launch, seq_tail (the walk follows the event blocks as they publish,
-// the verification follows the walk); the sharded path keeps them apart (the event exchange sits between).
+// A single rank runs seq_count .. seq_verify as ONE launch, seq_tail (the block offsets by a look-back, the walk
+// following the event blocks as they publish, the verification following the walk); the sharded path keeps them
+// apart (the event exchange sits between).
 #include "lio_seqsum.hpp"
 
 #include <cmath>
 
+#include "lio_dev.hpp"
 #include "lio_error.hpp"
 
 namespace lio {
@@ -414,11 +416,12 @@ __global__ void __launch_bounds__(kSeqThreads) seq_scan2(SeqSumBuf b, const uint
     }
 }
 
-// the block's elements with their exclusive increment prefix and inclusive event count
+// the block's elements with their exclusive increment prefix and inclusive event count within the block, and the
+// block's totals
 template <class Src>
-__device__ __forceinline__ void block_scan_elems(const Src& src, const SeqSumBuf& b, int c, int blk, int64_t n, int pass,
+__device__ __forceinline__ void block_scan_local(const Src& src, const SeqSumBuf& b, int c, int blk, int64_t n, int pass,
                                                  ElemInfo& in, bool (&ev)[kSeqPer], uint64_t (&Pex)[kSeqPer],
-                                                 int (&Ein)[kSeqPer]) {
+                                                 int (&Ein)[kSeqPer], uint64_t& tu, int& te) {
     __shared__ double s_wd[kSeqThreads / 64];
     __shared__ uint64_t s_u[kSeqThreads / 64];
     __shared__ int s_i[kSeqThreads / 64];
@@ -432,16 +435,31 @@ __device__ __forceinline__ void block_scan_elems(const Src& src, const SeqSumBuf
         su += inc[i];
         se += ev[i] ? 1 : 0;
     }
-    uint64_t tu;
-    int te;
-    uint64_t pu = block_excl(su, s_u, tu) + b.bPoff[(size_t)c * b.nblk + blk];
-    int pe = block_excl(se, s_i, te) + b.bEoff[(size_t)c * b.nblk + blk];
+    uint64_t pu = block_excl(su, s_u, tu);
+    int pe = block_excl(se, s_i, te);
 #pragma unroll
     for (int i = 0; i < kSeqPer; ++i) {
         Pex[i] = pu;
         pu += inc[i];
         pe += ev[i] ? 1 : 0;
         Ein[i] = pe;
+    }
+}
+
+// ... and with the block's offsets in the chain (seq_scan2's)
+template <class Src>
+__device__ __forceinline__ void block_scan_elems(const Src& src, const SeqSumBuf& b, int c, int blk, int64_t n, int pass,
+                                                 ElemInfo& in, bool (&ev)[kSeqPer], uint64_t (&Pex)[kSeqPer],
+                                                 int (&Ein)[kSeqPer]) {
+    uint64_t tu;
+    int te;
+    block_scan_local(src, b, c, blk, n, pass, in, ev, Pex, Ein, tu, te);
+    const uint64_t P0 = b.bPoff[(size_t)c * b.nblk + blk];
+    const int E0 = b.bEoff[(size_t)c * b.nblk + blk];
+#pragma unroll
+    for (int i = 0; i < kSeqPer; ++i) {
+        Pex[i] += P0;
+        Ein[i] += E0;
     }
 }
 
@@ -475,15 +493,11 @@ __device__ __forceinline__ void st64(void* p, uint64_t v) {
 // failure (re-pass) or an event overflow (the serial kernel), never a wrong result
 constexpr uint64_t kSpinTicks = 2000000;
 
-// block blk's events in element order: position, increment prefix, x (F: published by the block's flag)
-template <class Src, bool F>
-__device__ __forceinline__ void events_block(const Src& src, const SeqSumBuf& b, int c, int blk, int64_t n, int pass,
-                                             uint32_t epoch) {
-    ElemInfo in;
-    bool ev[kSeqPer];
-    uint64_t Pex[kSeqPer];
-    int Ein[kSeqPer];
-    block_scan_elems(src, b, c, blk, n, pass, in, ev, Pex, Ein);
+// the events of block blk in element order (position, increment prefix, x) from its prefixes Pex / Ein
+template <bool F>
+__device__ __forceinline__ void store_events(const SeqSumBuf& b, int c, int blk, const ElemInfo& in,
+                                             const bool (&ev)[kSeqPer], const uint64_t (&Pex)[kSeqPer],
+                                             const int (&Ein)[kSeqPer]) {
     const int64_t k0 = (int64_t)blk * kSeqBlock + (int64_t)threadIdx.x * kSeqPer;
     // single rank: the walk's lists; sharded: this window's lists (local positions and prefixes, seq_shard_pack)
     int* EPOS = b.sh ? b.lev_pos : b.ev_pos;
@@ -500,18 +514,19 @@ __device__ __forceinline__ void events_block(const Src& src, const SeqSumBuf& b,
                 st32<F>(EXX + (size_t)c * es + idx, __float_as_uint(in.x[i]));
             }
         }
-    if constexpr (F) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (threadIdx.x == 0) st32<true>(b.evflag + (size_t)c * b.nblk + blk, epoch);
-    }
 }
 
 template <class Src>
 __global__ void __launch_bounds__(kSeqThreads) seq_events(Src src, SeqSumBuf b, const uint32_t* d_n, int pass) {
+    const int c = blockIdx.y, blk = blockIdx.x;
     const int64_t n = *d_n;
-    if ((int64_t)blockIdx.x * kSeqBlock >= n) return;
-    events_block<Src, false>(src, b, (int)blockIdx.y, (int)blockIdx.x, n, pass, 0u);
+    if ((int64_t)blk * kSeqBlock >= n) return;
+    ElemInfo in;
+    bool ev[kSeqPer];
+    uint64_t Pex[kSeqPer];
+    int Ein[kSeqPer];
+    block_scan_elems(src, b, c, blk, n, pass, in, ev, Pex, Ein);
+    store_events<false>(b, c, blk, in, ev, Pex, Ein);
 }
 
 // The walk: s_{event-1} = s_{previous event} + run sum R (exact), s_event = fl(s_{event-1} + x_event), one chain
@@ -528,7 +543,7 @@ __global__ void __launch_bounds__(kSeqThreads) seq_events(Src src, SeqSumBuf b, 
 //     fl32(fl32(fl64(s + R)) + x).  seq_verify checks every element either way.
 constexpr int kWalkThreads = 256;
 constexpr int kWalkChunk = 1024;  // events per LDS chunk, separate launches (x 2 buffers x 20 bytes)
-constexpr int kTailChunk = 512;   // the fused tail's: 20 KB of LDS, so its event / verification roles keep 7 blocks per CU
+constexpr int kTailChunk = 512;   // the fused tail's: 20 KB of LDS, so its other roles keep their occupancy
 constexpr int kWalkU = 8;
 template <int C>
 struct alignas(16) WalkChunk {
@@ -537,45 +552,17 @@ struct alignas(16) WalkChunk {
     float x[C];
     float f[C];   // the walk's results
     int fast[C / 64];
+    int m;        // events in the chunk (the fused tail: known once its events are published)
 };
 
-// F: every element block whose events start before e_end has published them (its flag holds this launch's epoch).
-// Wave-uniform; jdone (the wave's own) = blocks already seen published, in element order.  false: time-out.
-__device__ __forceinline__ bool wait_events(const SeqSumBuf& b, int c, int nb, int e_end, int& jdone, uint32_t epoch) {
-    const int lane = threadIdx.x & 63;
-    const int* EO = b.bEoff + (size_t)c * b.nblk;
-    const uint32_t* FL = b.evflag + (size_t)c * b.nblk;
-    const uint64_t t0 = wall_clock64();
-    while (jdone < nb) {
-        const int j = jdone + lane;
-        const bool need = j < nb && EO[j] < e_end;  // bEoff is non-decreasing: the needed blocks are a prefix
-        const bool ok = !need || ld32<true>(FL + j) == epoch;
-        const uint64_t bad = __ballot(!ok);
-        if (bad) {
-            jdone += __builtin_ctzll(bad);
-            if (wall_clock64() - t0 > kSpinTicks) return false;
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        const uint64_t done = __ballot(!need);
-        if (done) {
-            jdone += __builtin_ctzll(done);
-            return true;
-        }
-        jdone += 64;
-    }
-    return true;
-}
-
-// chunk k's records into B by the threads [t0, t0 + nt) (nt a multiple of 64, t0 wave-aligned, nt >= 192): every
+// chunk k's m records into B by the threads [t0, t0 + nt) (nt a multiple of 64, t0 wave-aligned, nt >= 192): every
 // load of the thread's share is issued before the first is used (the preparation runs beside the walk and must
 // stay shorter than it: one round trip to memory per chunk, not one per step)
 template <int C, bool F>
-__device__ __forceinline__ void walk_prepare(WalkChunk<C>& B, int k, int nev, double unit, const uint64_t* EP,
+__device__ __forceinline__ void walk_prepare(WalkChunk<C>& B, int k, int m, double unit, const uint64_t* EP,
                                              const float* EX, int t, int nt) {
     constexpr int kPrepMax = (C + 191) / 192;
     const int e0 = k * C;
-    const int m = min(C, nev - e0);
     uint64_t P[kPrepMax], Pp[kPrepMax];
     float X[kPrepMax];
 #pragma unroll
@@ -680,155 +667,65 @@ __device__ __forceinline__ float walk_chunk(WalkChunk<C>& B, int m, float s) {
     return s;
 }
 
-// F: the walk's progress word of chain c, epoch << 32 | events whose results are stored (sc1)
-__device__ __forceinline__ void walk_publish(const SeqSumBuf& b, int c, uint32_t epoch, uint32_t done) {
-    st64<true>(b.wprog + c, ((uint64_t)epoch << 32) | done);
-}
-
-// the walker of chain c (kWalkThreads threads).  F: the events arrive in this launch (wait_events before a chunk
-// is prepared), the results are stored sc1 and published chunk by chunk for the verification roles
-template <class Src, int C, bool F>
-__device__ __forceinline__ void walk_chain(const Src& src, const SeqSumBuf& b, int c, int64_t n, uint32_t epoch) {
+// the walker of chain c, separate launches: every event listed before it starts
+template <class Src>
+__global__ void __launch_bounds__(kWalkThreads) seq_walk(Src src, SeqSumBuf b, const uint32_t* d_n) {
+    constexpr int C = kWalkChunk;
     __shared__ WalkChunk<C> wb[2];
-    __shared__ int s_abort;
+    const int c = blockIdx.x;
     const int t = threadIdx.x, w = t >> 6;
+    const int64_t n = b.sh ? b.sh->n_global : *d_n;  // sharded: every rank walks the whole chain's events
     if (n <= 0) {
         if (t == 0) b.result[c] = 0.f;
         return;
     }
-    if ((b.status[1] >> c) & 1u) return;  // event overflow: the caller falls back (the verification roles skip too)
+    if ((b.status[1] >> c) & 1u) return;  // event overflow: the caller falls back
     const int nev = b.floor_e[b.nch + c];
     const double unit = ldexp(1.0, b.floor_e[c] - 23);
     const uint64_t* EP = b.ev_P + (size_t)c * b.evs;
     const float* EX = b.ev_x + (size_t)c * b.evs;
     float* ES = b.ev_s + (size_t)c * b.evs;
     const int nchunk = (nev + C - 1) / C;
-    const int nb = (int)((n + kSeqBlock - 1) / kSeqBlock);
-    int jdone = 0;  // F: this wave's published-blocks prefix
     float s = b.sh ? b.sh->x0[c] : src(c, 0);  // the chain (lane 0 of wave 0)
-#ifdef LIO_TAIL_DIAG  // diagnostics build: the walker's time split (wall_clock64 ticks, 10 ns)
-    const uint64_t d_t0 = wall_clock64();
-    uint64_t d_walk = 0, d_wait = 0, d_ready = 0;
-#endif
-    if (t == 0) s_abort = 0;
+    if (nchunk > 0) walk_prepare<C, false>(wb[0], 0, min(C, nev), unit, EP, EX, t, kWalkThreads);
     __syncthreads();
-    if (nchunk > 0) {
-        if (F && !wait_events(b, c, nb, min(nev, C), jdone, epoch)) s_abort = 1;
-        walk_prepare<C, F>(wb[0], 0, nev, unit, EP, EX, t, kWalkThreads);
-    }
-    __syncthreads();
-#ifdef LIO_TAIL_DIAG
-    d_ready = wall_clock64() - d_t0;
-#endif
-    for (int k = 0; k < nchunk && !s_abort; ++k) {
+    for (int k = 0; k < nchunk; ++k) {
         if (w == 0) {
-#ifdef LIO_TAIL_DIAG
-            const uint64_t ta = wall_clock64();
-#endif
             if (t == 0) s = walk_chunk(wb[k & 1], min(C, nev - k * C), s);
-#ifdef LIO_TAIL_DIAG
-            d_walk += wall_clock64() - ta;
-#endif
         } else {
-            if (F && t == 64 && k > 1) walk_publish(b, c, epoch, (uint32_t)((k - 1) * C));  // chunks < k-1: stored
-            if (k + 1 < nchunk) {
-#ifdef LIO_TAIL_DIAG
-                const uint64_t ta = wall_clock64();
-#endif
-                if (F && !wait_events(b, c, nb, min(nev, (k + 2) * C), jdone, epoch)) s_abort = 1;
-#ifdef LIO_TAIL_DIAG
-                d_wait += wall_clock64() - ta;
-#endif
-                walk_prepare<C, F>(wb[(k + 1) & 1], k + 1, nev, unit, EP, EX, t - 64, kWalkThreads - 64);
-            }
+            if (k + 1 < nchunk)
+                walk_prepare<C, false>(wb[(k + 1) & 1], k + 1, min(C, nev - (k + 1) * C), unit, EP, EX, t - 64,
+                                       kWalkThreads - 64);
             if (k > 0) {  // chunk k-1's results (its buffer's f: the preparation above writes only R, Rf, x)
                 const WalkChunk<C>& B = wb[(k - 1) & 1];
                 const int e0 = (k - 1) * C;
-                for (int j = t - 64; j < C; j += kWalkThreads - 64) st32<F>(ES + e0 + j, __float_as_uint(B.f[j]));
-                if (F) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                for (int j = t - 64; j < C; j += kWalkThreads - 64) ES[e0 + j] = B.f[j];
             }
         }
         __syncthreads();
-    }
-    if (s_abort) {  // F only: a time-out waiting for events; the chain goes to the serial kernel
-        if (t == 0) {
-            atomicOr(&b.status[1], 1u << c);
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            walk_publish(b, c, epoch, 0xffffffffu);
-        }
-        return;
     }
     if (nchunk > 0) {
         const WalkChunk<C>& B = wb[(nchunk - 1) & 1];
         const int e0 = (nchunk - 1) * C;
-        const int m = nev - e0;
-        for (int j = t; j < m; j += kWalkThreads) st32<F>(ES + e0 + j, __float_as_uint(B.f[j]));
+        for (int j = t; j < nev - e0; j += kWalkThreads) ES[e0 + j] = B.f[j];
     }
-    if constexpr (F) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (t == 0) walk_publish(b, c, epoch, (uint32_t)nev);
-    }
-#ifdef LIO_TAIL_DIAG
-    __shared__ uint64_t s_wait;
-    if (t == 64) s_wait = d_wait;
-    __syncthreads();
-    if (t == 0)
-        printf("tail walker %d F%d: events %d ready %llu walk %llu wait(w1) %llu total %llu start %llu\n", c, (int)F, nev,
-               (unsigned long long)d_ready, (unsigned long long)d_walk, (unsigned long long)s_wait,
-               (unsigned long long)(wall_clock64() - d_t0), (unsigned long long)(d_t0 % 100000000ull));
-#endif
     if (t == 0) {
-        const uint64_t Plast = nev > 0 ? ld64<F>(EP + nev - 1) : 0;
+        const uint64_t Plast = nev > 0 ? EP[nev - 1] : 0;
         b.result[c] = (float)((double)s + (double)(int64_t)(b.ptot[c] - Plast) * unit);
     }
 }
 
-template <class Src>
-__global__ void __launch_bounds__(kWalkThreads) seq_walk(Src src, SeqSumBuf b, const uint32_t* d_n) {
-    const int64_t n = b.sh ? b.sh->n_global : *d_n;  // sharded: every rank walks the whole chain's events
-    walk_chain<Src, kWalkChunk, false>(src, b, (int)blockIdx.x, n, 0u);
-}
-
-// s_k for every element of block blk from the events; checks s_k == fl(s_{k-1} + x_k); stores the reconstruction.
-// F: the events and their results arrive in this launch: the walk's progress word is polled first
+// s_k for every element of block blk (its offsets E0 / P0 in the chain, its prefixes already including them) rebuilt
+// from the events; checks s_k == fl(s_{k-1} + x_k); stores the reconstruction.  F: the event lists and results
+// were written in this launch (sc1 loads)
 template <class Src, bool F>
-__device__ __forceinline__ void verify_block(const Src& src, const SeqSumBuf& b, int c, int blk, int64_t n, int pass,
-                                             uint32_t epoch) {
+__device__ __forceinline__ void verify_check(const Src& src, const SeqSumBuf& b, int c, int blk, int64_t n, int pass,
+                                             const ElemInfo& in, const bool (&ev)[kSeqPer],
+                                             const uint64_t (&Pex)[kSeqPer], const int (&Ein)[kSeqPer], int E0,
+                                             uint64_t P0) {
     __shared__ float s_lastv[kSeqThreads / 64];
-    __shared__ uint32_t s_bad, s_skip;
+    __shared__ uint32_t s_bad;
     if (threadIdx.x == 0) s_bad = 0;
-    // the block's predictions, events and prefixes need no walk result (F: done while the walk runs; measured 2 %
-    // faster per alignment than waiting first, profiles/r06_seq_tail_ab.txt)
-    ElemInfo in;
-    bool ev[kSeqPer];
-    uint64_t Pex[kSeqPer];
-    int Ein[kSeqPer];
-    block_scan_elems(src, b, c, blk, n, pass, in, ev, Pex, Ein);
-    if constexpr (F) {
-        if (threadIdx.x == 0) {
-            // every event up to this block's last one walked and stored
-            const uint32_t need = (uint32_t)(b.bEoff[(size_t)c * b.nblk + blk] + b.bev[(size_t)c * b.nblk + blk]);
-            const uint64_t t0 = wall_clock64();
-            uint32_t skip = 0;
-            for (;;) {
-                const uint64_t wv = ld64<true>(b.wprog + c);
-                if ((uint32_t)(wv >> 32) == epoch && (uint32_t)wv >= need) break;
-                if (wall_clock64() - t0 > kSpinTicks) {
-                    skip = 2;
-                    break;
-                }
-                __builtin_amdgcn_s_sleep(2);
-            }
-            if (!skip && ((ld32<true>(b.status + 1) >> c) & 1u)) skip = 1;  // the walker gave up: serial kernel
-            s_skip = skip;
-        }
-        __syncthreads();
-        if (s_skip) {
-            if (threadIdx.x == 0 && s_skip == 2) atomicOr(&b.status[0], 1u << c);  // time-out: a re-pass
-            return;
-        }
-    }
     const double unit = ldexp(1.0, b.floor_e[c] - 23);
     const uint64_t* EP = b.ev_P + (size_t)c * b.evs;
     const float* ES = b.ev_s + (size_t)c * b.evs;
@@ -864,13 +761,11 @@ __device__ __forceinline__ void verify_block(const Src& src, const SeqSumBuf& b,
         if (w > 0) {
             prev = s_lastv[w - 1];
         } else if (gb + k0 > 0) {
-            // the previous block's last element (a window's first block: the previous rank's last): bEoff / bPoff
-            // of this block are its inclusive values (global once seq_shard_merge has added the ranks before);
-            // whether it is an event is read back from the event list (global position)
-            const int E = b.bEoff[(size_t)c * b.nblk + blk];
-            const uint64_t Pin = b.bPoff[(size_t)c * b.nblk + blk];
-            const bool is_ev = E > 0 && (int)ld32<F>(b.ev_pos + (size_t)c * b.evs + (E - 1)) == (int)(gb + k0 - 1);
-            prev = rebuild(is_ev, E, Pin);
+            // the previous block's last element (a window's first block: the previous rank's last): the block's
+            // offsets are its inclusive values (global once seq_shard_merge has added the ranks before); whether
+            // it is an event is read back from the event list (global position)
+            const bool is_ev = E0 > 0 && (int)ld32<F>(b.ev_pos + (size_t)c * b.evs + (E0 - 1)) == (int)(gb + k0 - 1);
+            prev = rebuild(is_ev, E0, P0);
             if (k0 == 0) b.sh->prev_s[c] = prev;  // (k0 == 0 here only when sharded) the next pass's prediction
         }
     }
@@ -897,28 +792,273 @@ __device__ __forceinline__ void verify_block(const Src& src, const SeqSumBuf& b,
 
 template <class Src>
 __global__ void __launch_bounds__(kSeqThreads) seq_verify(Src src, SeqSumBuf b, const uint32_t* d_n, int pass) {
-    const int c = blockIdx.y;
+    const int c = blockIdx.y, blk = blockIdx.x;
     const int64_t n = *d_n;
-    if ((int64_t)blockIdx.x * kSeqBlock >= n) return;
+    if ((int64_t)blk * kSeqBlock >= n) return;
     if ((b.status[1] >> c) & 1u) return;
-    verify_block<Src, false>(src, b, c, (int)blockIdx.x, n, pass, 0u);
+    ElemInfo in;
+    bool ev[kSeqPer];
+    uint64_t Pex[kSeqPer];
+    int Ein[kSeqPer];
+    block_scan_elems(src, b, c, blk, n, pass, in, ev, Pex, Ein);
+    verify_check<Src, false>(src, b, c, blk, n, pass, in, ev, Pex, Ein, b.bEoff[(size_t)c * b.nblk + blk],
+                             b.bPoff[(size_t)c * b.nblk + blk]);
 }
 
-// The fused tail (single rank): events, walk and verification in ONE launch, so the walk starts on the first
-// blocks' events while later blocks still list theirs, and the verification runs behind the walk on the CUs the
-// walkers leave idle.  Roles by workgroup index: [0, nch) the walkers, then the event blocks, then the verification
-// blocks, both element-major.  Walkers wait on event blocks (which wait on nothing), verification blocks on
-// walkers.  Workgroups are dispatched in index order (observed, not promised): every walker and event block is then
-// resident before a verification block; were it not, the waits' time-outs (kSpinTicks) end them as a failed
-// verification (a re-pass) or an event overflow (the serial kernel) — slower, never wrong, never hung.
+// ---------------------------------------------------------------- the fused tail (single rank)
+// seq_count + seq_scan2 + seq_events + seq_walk + seq_verify as ONE launch, seq_tail.  Roles by workgroup index:
+// [0, nch) the walkers, then the event blocks, then the verification blocks, both element-major.
+//   * an event block classifies its elements (seq_count's work), takes its place in the chain by a decoupled
+//     look-back over its predecessors (event counts in the status words, increment sums beside them; lio_dev.hpp
+//     lookback_excl), lists its events and publishes its flag word, epoch << 32 | inclusive event count;
+//   * a walker follows the flag words in block order and walks each chunk once all its events are listed; every
+//     stored chunk of results is published by its progress word, epoch << 32 | events walked;
+//   * a verification block does its own classification first, then waits for its event block's offsets and for
+//     the walk to pass its last event, then checks.
+// Event blocks wait only on lower event blocks, walkers on event blocks, verification blocks on both.  Workgroups
+// are dispatched in index order (observed, not promised): every walker and event block is then resident before a
+// verification block.  Were it not, the waits' time-outs (kSpinTicks) end them as a failed verification (a
+// re-pass) or an event overflow (the serial kernel) — slower, never wrong, never hung.
+
+// the event block (c, blk)
+template <class Src>
+__device__ __forceinline__ void tail_events(const Src& src, const SeqSumBuf& b, int c, int blk, int64_t n, int pass,
+                                            uint32_t epoch, int nb) {
+    __shared__ uint64_t s_P;
+    __shared__ int s_E;
+    ElemInfo in;
+    bool ev[kSeqPer];
+    uint64_t Pex[kSeqPer];
+    int Ein[kSeqPer];
+    uint64_t tu;
+    int te;
+    block_scan_local(src, b, c, blk, n, pass, in, ev, Pex, Ein, tu, te);
+    const size_t bi = (size_t)c * b.nblk + blk;
+    const uint32_t ep30 = epoch & 0x3fffffffu;  // the status words' epoch field (never 0: seqsum_launch_impl)
+    if (threadIdx.x < 64) {  // wave 0: publish the aggregate, look back, publish the inclusive prefix
+        unsigned long long* lst = b.lbst + (size_t)c * b.nblk;
+        unsigned long long* lag = b.lbagg + (size_t)c * b.nblk;
+        unsigned long long* lin = b.lbinc + (size_t)c * b.nblk;
+        uint32_t E = 0;
+        uint64_t P = 0;
+        if (blk > 0) {
+            if (threadIdx.x == 0) {
+                st64<true>(lag + blk, tu);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                lb_store(lst, blk, lb_word(ep30, 1u, (uint32_t)te));
+            }
+            bool timeout;
+            E = lookback_excl<true>(lst, lag, lin, blk, ep30, P, timeout);
+            if (timeout && threadIdx.x == 0) atomicOr(&b.status[1], 1u << c);  // never expected: the serial kernel
+        }
+        if (threadIdx.x == 0) {
+            st64<true>(lin + blk, P + tu);
+            // the block's offsets for its verification block, the chain's totals from the last block (sc1: read in
+            // this launch)
+            st32<true>(b.bEoff + bi, E);
+            st64<true>(b.bPoff + bi, P);
+            if (blk == nb - 1) {
+                st32<true>(b.floor_e + b.nch + c, E + (uint32_t)te);
+                st64<true>(b.ptot + c, P + tu);
+            }
+            if ((int64_t)E + te > b.evcap) atomicOr(&b.status[1], 1u << c);  // the lists overflow: the serial kernel
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            lb_store(lst, blk, lb_word(ep30, 2u, E + (uint32_t)te));
+            s_E = (int)E;
+            s_P = P;
+        }
+    }
+    __syncthreads();
+    const int E0 = s_E;
+    const uint64_t P0 = s_P;
+#pragma unroll
+    for (int i = 0; i < kSeqPer; ++i) {
+        Pex[i] += P0;
+        Ein[i] += E0;
+    }
+    store_events<true>(b, c, blk, in, ev, Pex, Ein);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) st64<true>(b.evflag + (size_t)c * b.nblk + blk, ((uint64_t)epoch << 32) | (uint32_t)(E0 + te));
+}
+
+// the walker's view of the event blocks (one per wave, wave-uniform): blocks [0, jdone) seen published, their
+// events [0, eknown) listed.  Advances until eknown >= e_end or every block is seen (then eknown = the total).
+// false: time-out
+__device__ __forceinline__ bool tail_wait(const SeqSumBuf& b, int c, int nb, int e_end, int& jdone, int& eknown,
+                                          uint32_t epoch) {
+    const int lane = threadIdx.x & 63;
+    const unsigned long long* FL = b.evflag + (size_t)c * b.nblk;
+    const uint64_t t0 = wall_clock64();
+    while (eknown < e_end && jdone < nb) {
+        const int j = jdone + lane;
+        const uint64_t wv = j < nb ? ld64<true>(FL + j) : 0ull;
+        const bool valid = j < nb && (uint32_t)(wv >> 32) == epoch;
+        const uint64_t inval = __ballot(j < nb && !valid);
+        const int lim = min(64, nb - jdone);
+        const int f = inval ? (int)__builtin_ctzll(inval) : lim;  // published prefix of the window
+        if (f > 0) {
+            eknown = __shfl((int)(uint32_t)wv, f - 1, 64);
+            jdone += f;
+        }
+        if (f < lim && eknown < e_end) {
+            if (wall_clock64() - t0 > kSpinTicks) return false;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+    return true;
+}
+
+__device__ __forceinline__ void walk_publish(const SeqSumBuf& b, int c, uint32_t epoch, uint32_t done) {
+    st64<true>(b.wprog + c, ((uint64_t)epoch << 32) | done);
+}
+
+// the walker of chain c
+template <class Src>
+__device__ __forceinline__ void tail_walk(const Src& src, const SeqSumBuf& b, int c, int64_t n, uint32_t epoch, int nb) {
+    constexpr int C = kTailChunk;
+    __shared__ WalkChunk<C> wb[2];
+    __shared__ int s_abort;
+    const int t = threadIdx.x, w = t >> 6;
+    if (n <= 0) {
+        if (t == 0) b.result[c] = 0.f;
+        return;
+    }
+    const double unit = ldexp(1.0, b.floor_e[c] - 23);
+    const uint64_t* EP = b.ev_P + (size_t)c * b.evs;
+    const float* EX = b.ev_x + (size_t)c * b.evs;
+    float* ES = b.ev_s + (size_t)c * b.evs;
+    int jdone = 0, eknown = 0;  // this wave's view of the event blocks
+    float s = src(c, 0);        // the chain (lane 0 of wave 0)
+    // the events of chunk k (every wave of the caller agrees): m = 0 past the last chunk; false: give up
+    auto chunk_events = [&](int k, int& m) -> bool {
+        if (!tail_wait(b, c, nb, (k + 1) * C, jdone, eknown, epoch)) return false;
+        if (eknown > b.evcap) return false;  // the lists overflowed (the event block flagged it)
+        m = max(0, min(C, eknown - k * C));
+        return true;
+    };
+    if (t == 0) s_abort = 0;
+    __syncthreads();
+    {
+        int m0 = 0;
+        if (!chunk_events(0, m0)) s_abort = 1;
+        walk_prepare<C, true>(wb[0], 0, m0, unit, EP, EX, t, kWalkThreads);
+        if (t == 0) wb[0].m = m0;
+    }
+    __syncthreads();
+    int k = 0;
+    for (; !s_abort && wb[k & 1].m > 0; ++k) {
+        if (w == 0) {
+            if (t == 0) s = walk_chunk(wb[k & 1], wb[k & 1].m, s);
+        } else {
+            if (t == 64 && k > 1) walk_publish(b, c, epoch, (uint32_t)((k - 1) * C));  // chunks < k-1: stored
+            int m1 = 0;
+            if (wb[k & 1].m == C && !chunk_events(k + 1, m1)) s_abort = 1;
+            walk_prepare<C, true>(wb[(k + 1) & 1], k + 1, m1, unit, EP, EX, t - 64, kWalkThreads - 64);
+            if (t == 64) wb[(k + 1) & 1].m = m1;
+            if (k > 0) {  // chunk k-1's results (its buffer's f: the preparation above writes only R, Rf, x, m)
+                const WalkChunk<C>& B = wb[(k - 1) & 1];
+                const int e0 = (k - 1) * C;
+                for (int j = t - 64; j < C; j += kWalkThreads - 64) st32<true>(ES + e0 + j, __float_as_uint(B.f[j]));
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+        }
+        __syncthreads();
+    }
+    if (s_abort) {  // a time-out or an overflow: the chain goes to the serial kernel
+        if (t == 0) {
+            atomicOr(&b.status[1], 1u << c);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            walk_publish(b, c, epoch, 0xffffffffu);
+        }
+        return;
+    }
+    // k = the chunks walked, every one full but the last; its results are in wb[(k - 1) & 1]
+    const int nev = k > 0 ? (k - 1) * C + wb[(k - 1) & 1].m : 0;
+    if (k > 0) {
+        const WalkChunk<C>& B = wb[(k - 1) & 1];
+        const int e0 = (k - 1) * C;
+        for (int j = t; j < nev - e0; j += kWalkThreads) st32<true>(ES + e0 + j, __float_as_uint(B.f[j]));
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+        walk_publish(b, c, epoch, (uint32_t)nev);
+        const uint64_t Plast = nev > 0 ? ld64<true>(EP + nev - 1) : 0;
+        b.result[c] = (float)((double)s + (double)(int64_t)(ld64<true>(b.ptot + c) - Plast) * unit);
+    }
+}
+
+// the verification block (c, blk)
+template <class Src>
+__device__ __forceinline__ void tail_verify(const Src& src, const SeqSumBuf& b, int c, int blk, int64_t n, int pass,
+                                            uint32_t epoch) {
+    __shared__ uint32_t s_skip;
+    __shared__ int s_E;
+    __shared__ uint64_t s_P;
+    ElemInfo in;
+    bool ev[kSeqPer];
+    uint64_t Pex[kSeqPer];
+    int Ein[kSeqPer];
+    uint64_t tu;
+    int te;
+    block_scan_local(src, b, c, blk, n, pass, in, ev, Pex, Ein, tu, te);  // needs no other block
+    if (threadIdx.x == 0) {
+        const size_t bi = (size_t)c * b.nblk + blk;
+        const uint64_t t0 = wall_clock64();
+        uint32_t skip = 0, need = 0;
+        for (;;) {  // the event block: its offsets
+            const uint64_t wv = ld64<true>(b.evflag + bi);
+            if ((uint32_t)(wv >> 32) == epoch) {
+                need = (uint32_t)wv;
+                break;
+            }
+            if (wall_clock64() - t0 > kSpinTicks) {
+                skip = 2;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!skip) {
+            s_E = (int)ld32<true>(b.bEoff + bi);
+            s_P = ld64<true>(b.bPoff + bi);
+        }
+        while (!skip) {  // the walk past this block's last event
+            const uint64_t wv = ld64<true>(b.wprog + c);
+            if ((uint32_t)(wv >> 32) == epoch && (uint32_t)wv >= need) break;
+            if (wall_clock64() - t0 > kSpinTicks) {
+                skip = 2;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!skip && ((ld32<true>(b.status + 1) >> c) & 1u)) skip = 1;  // the serial kernel takes the chain
+        s_skip = skip;
+    }
+    __syncthreads();
+    if (s_skip) {
+        if (threadIdx.x == 0 && s_skip == 2) atomicOr(&b.status[0], 1u << c);  // time-out: a re-pass
+        return;
+    }
+    const int E0 = s_E;
+    const uint64_t P0 = s_P;
+#pragma unroll
+    for (int i = 0; i < kSeqPer; ++i) {
+        Pex[i] += P0;
+        Ein[i] += E0;
+    }
+    verify_check<Src, true>(src, b, c, blk, n, pass, in, ev, Pex, Ein, E0, P0);
+}
+
 template <class Src>
 __global__ void __launch_bounds__(kSeqThreads) seq_tail(Src src, SeqSumBuf b, const uint32_t* d_n, int pass, int nch,
                                                         uint32_t epoch) {
     static_assert(kSeqThreads == kWalkThreads, "one block size for every role");
     const uint32_t r = blockIdx.x;
     const int64_t n = *d_n;
+    const int nb = (int)((n + kSeqBlock - 1) / kSeqBlock);
     if (r < (uint32_t)nch) {
-        walk_chain<Src, kTailChunk, true>(src, b, (int)r, n, epoch);
+        tail_walk<Src>(src, b, (int)r, n, epoch, nb);
         return;
     }
     uint32_t i = r - (uint32_t)nch;
@@ -926,12 +1066,11 @@ __global__ void __launch_bounds__(kSeqThreads) seq_tail(Src src, SeqSumBuf b, co
     const bool verify = i >= nrole;
     if (verify) i -= nrole;
     const int c = (int)(i % (uint32_t)nch), blk = (int)(i / (uint32_t)nch);
-    if ((int64_t)blk * kSeqBlock >= n) return;
-    if ((b.status[1] >> c) & 1u) return;  // event overflow (seq_scan2): the serial kernel
+    if (blk >= nb) return;
     if (verify)
-        verify_block<Src, true>(src, b, c, blk, n, pass, epoch);
+        tail_verify<Src>(src, b, c, blk, n, pass, epoch);
     else
-        events_block<Src, true>(src, b, c, blk, n, pass, epoch);
+        tail_events<Src>(src, b, c, blk, n, pass, epoch, nb);
 }
 
 // ---------------------------------------------------------------- sharded chains (lio_seqsum.hpp)
@@ -1198,12 +1337,13 @@ void seqsum_launch_impl(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf&
         b.forced_dirty = true;  // the failures that led here set forced bits
         (void)hipMemsetAsync(b.status, 0, 2 * sizeof(uint32_t), st);
     }
-    seq_count<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
-    seq_scan2<<<nch, kSeqThreads, 0, st>>>(b, d_n);
-    // events, walk and verification: one launch (seq_tail); its grid is sized for the capacity, the blocks past n
-    // leave at once
+    // count, offsets, events, walk and verification: one launch (seq_tail); its grid is sized for the capacity, the
+    // blocks past n leave at once
     const uint32_t total = (uint32_t)nch * (1u + 2u * (uint32_t)b.nblk);
-    if (++b.tail_epoch == 0) b.tail_epoch = 1;  // flags and progress words of earlier launches never match
+    // flags and progress words of earlier launches never match (the look-back's status words keep 30 bits of it)
+    do {
+        ++b.tail_epoch;
+    } while ((b.tail_epoch & 0x3fffffffu) == 0);
     seq_tail<Src><<<total, kSeqThreads, 0, st>>>(src, b, d_n, pass, nch, b.tail_epoch);
 }
 
@@ -1305,7 +1445,7 @@ int seqsum_reserve(SeqSumBuf& b, int nch, int64_t nmax, hipStream_t st) {
     b.nch = nch;
     b.nmax = nmax;
     b.nblk = (int)((nmax + kSeqBlock - 1) / kSeqBlock);
-    count_alloc(20);
+    count_alloc(23);
     b.evcap = b.evcap_alloc = nmax / 4 + 1024;  // events are ~0.3 % of a C4 chain; past a quarter the serial kernel is as fast
     b.evs = b.evcap;
     b.evs_alloc = 2 * b.evcap_alloc;  // the walk's lists: sharded, every rank's events (O(window): 2 x its own)
@@ -1323,14 +1463,17 @@ int seqsum_reserve(SeqSumBuf& b, int nch, int64_t nmax, hipStream_t st) {
               hipMalloc(&b.recon, (size_t)nch * nmax * sizeof(float)) == hipSuccess &&
               hipMalloc(&b.forced, (size_t)nch * (nmax / 32 + 1) * sizeof(uint32_t)) == hipSuccess &&
               hipMalloc(&b.status, 4 * sizeof(uint32_t)) == hipSuccess && hipMalloc(&b.result, nch * sizeof(float)) == hipSuccess &&
-              hipMalloc(&b.evflag, nb * sizeof(uint32_t)) == hipSuccess &&
+              hipMalloc(&b.evflag, nb * sizeof(uint64_t)) == hipSuccess &&
+              hipMalloc(&b.lbst, nb * sizeof(uint64_t)) == hipSuccess && hipMalloc(&b.lbagg, nb * sizeof(uint64_t)) == hipSuccess &&
+              hipMalloc(&b.lbinc, nb * sizeof(uint64_t)) == hipSuccess &&
               hipMalloc(&b.wprog, nch * sizeof(uint64_t)) == hipSuccess;
     if (!ok) {
         seqsum_free(b);
         return -5;
     }
     (void)hipMemsetAsync(b.status, 0, 4 * sizeof(uint32_t), st);
-    (void)hipMemsetAsync(b.evflag, 0, nb * sizeof(uint32_t), st);
+    (void)hipMemsetAsync(b.evflag, 0, nb * sizeof(uint64_t), st);
+    (void)hipMemsetAsync(b.lbst, 0, nb * sizeof(uint64_t), st);
     (void)hipMemsetAsync(b.wprog, 0, nch * sizeof(uint64_t), st);
     b.tail_epoch = 0;
     return 0;
@@ -1339,7 +1482,7 @@ int seqsum_reserve(SeqSumBuf& b, int nch, int64_t nmax, hipStream_t st) {
 void seqsum_free(SeqSumBuf& b) {
     void* ptrs[] = {b.bsum, b.babs, b.boff,   b.bdelta, b.btot,   b.bev,   b.bPoff, b.bEoff, b.floor_e,
                     b.ptot, b.ev_pos, b.ev_P, b.ev_x, b.ev_s, b.recon, b.forced, b.status, b.result,
-                    b.evflag, b.wprog,
+                    b.evflag, b.wprog, b.lbst, b.lbagg, b.lbinc,
                     b.sh,   b.lev_pos, b.lev_P, b.lev_x};
     for (void* p : ptrs)
         if (p) (void)hipFree(p);

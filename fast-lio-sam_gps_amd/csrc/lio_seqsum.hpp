@@ -188,10 +188,13 @@ struct SeqSumBuf {
                                 // failure the caller acts on goes through a pass > 1)
     uint32_t* status = nullptr; // [0] chains failing verification (bits), [1] event overflow (bits)
     float* result = nullptr;    // [nch] final sums
-    // the fused tail (seq_tail, single rank): event blocks' published flags, the walkers' progress words, the
-    // launch's epoch (host; tags the flags and words, never 0)
-    uint32_t* evflag = nullptr; // [nch][nblk]
-    uint64_t* wprog = nullptr;  // [nch] epoch << 32 | events walked and stored
+    // the fused tail (seq_tail, single rank): event blocks' flag words, the walkers' progress words, the look-back's
+    // status words and 64-bit sums, the launch's epoch (host; tags the words, its low 30 bits never 0)
+    unsigned long long* evflag = nullptr; // [nch][nblk] epoch << 32 | inclusive event count
+    uint64_t* wprog = nullptr;            // [nch] epoch << 32 | events walked and stored
+    unsigned long long* lbst = nullptr;   // [nch][nblk] lio_dev.hpp lb_word
+    unsigned long long* lbagg = nullptr;  // [nch][nblk] the block's increment sum
+    unsigned long long* lbinc = nullptr;  // [nch][nblk] its inclusive prefix
     uint32_t tail_epoch = 0;
     // sharded: sh (device) set, evs the per-chain stride of the walk's (global) event lists ev_*, the local
     // lists in lev_* (stride evcap); single rank: sh == nullptr, evs == evcap, events straight into ev_*
