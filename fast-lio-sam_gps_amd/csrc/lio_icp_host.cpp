@@ -18,6 +18,8 @@
 #include "lio_pool.hpp"
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cfloat>
 #include <cmath>
 #include <cstddef>
@@ -333,7 +335,9 @@ struct lio_icp {
     float* h_pcl16 = nullptr;  // pinned copy
     lio::PclBuf pcl;           // umeyama_float: compacted pairs + seqsum chains
     float* d_pclout = nullptr; // pcl_pack output (kPclOutWords)
-    float* h_pclout = nullptr; // pinned copy
+    float* h_pclout = nullptr; // pinned, host-mapped: a copy, or the pack's own stores (pcl_wait polls [23])
+    float* h_pclout_dev = nullptr;
+    uint32_t pcl_seq = 0;      // the last sequence number handed to the pack
     void* x_owner = nullptr;   // exchange state owned by the handle (lio_icp_mp.cpp: shm segment, RCCL comm)
     void (*x_owner_free)(void*) = nullptr;
     // sharded PCL float modes (fid_sharded): only this rank's shard on the device; the float chains split by
@@ -777,6 +781,26 @@ static uint32_t pcl_word(const lio_icp* h, int w) {
     return u;
 }
 
+// one rank: the pack stores its words straight into h_pclout (host-mapped) and its sequence number last; the host
+// polls that word instead of a copy launch and an event wait (the pass's last launch is the pack)
+static uint32_t pcl_next_seq(lio_icp* h) {
+    if (++h->pcl_seq == 0) h->pcl_seq = 1;
+    return h->pcl_seq;
+}
+static int pcl_wait(lio_icp* h, uint32_t seq) {
+    const volatile uint32_t* w = reinterpret_cast<const volatile uint32_t*>(h->h_pclout + 23);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t spin = 0; *w != seq; ++spin) {
+        if ((spin & 1023u) == 1023u && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+            IHIP(hipStreamSynchronize(h->st));  // a failed launch reports here
+            if (*w != seq) return ifail(LIO_ERR_STATE, "lio_icp_align: the statistics never arrived");
+            break;
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return LIO_OK;
+}
+
 static int pcl_finish(lio_icp* h, const lio::IcpArgs& a) {
     const int order = h->p.umeyama_float;
     // the compaction's look-back timed out (h_pclout[19]; never expected): its pairs cannot be trusted, so the
@@ -808,9 +832,10 @@ static int pcl_finish(lio_icp* h, const lio::IcpArgs& a) {
         }
         ++h->fid_stats[0];
         ++h->fid_stats[3];
-        lio::launch_pcl_pack(h->pcl, order, h->d_pclout, h->st);
-        IHIP(hipMemcpyAsync(h->h_pclout, h->d_pclout, lio::kPclOutWords * sizeof(float), hipMemcpyDeviceToHost, h->st));
-        IHIP(hipStreamSynchronize(h->st));
+        const uint32_t seq = pcl_next_seq(h);
+        lio::launch_pcl_pack(h->pcl, order, h->h_pclout_dev, h->st, nullptr, seq);
+        const int rc = pcl_wait(h, seq);
+        if (rc) return rc;
     }
     if (lb_timeout || (pcl_word(h, 0) | pcl_word(h, 1)) != 0) {  // the serial kernels: one lane per chain
         ++h->fid_stats[1];
@@ -839,8 +864,7 @@ static int enqueue_pcl(lio_icp* h, const lio::IcpArgs& pa) {
         IHIP(hipMemsetAsync(h->pcl.small + lio::kPclTicket + 1, 1, sizeof(uint32_t), h->st));
     lio::launch_pcl_means(h->pcl, 1, h->st);
     lio::launch_pcl_sigma(h->pcl, order, 1, h->st);
-    lio::launch_pcl_pack(h->pcl, order, h->d_pclout, h->st);
-    IHIP(hipMemcpyAsync(h->h_pclout, h->d_pclout, lio::kPclOutWords * sizeof(float), hipMemcpyDeviceToHost, h->st));
+    lio::launch_pcl_pack(h->pcl, order, h->h_pclout_dev, h->st, nullptr, pcl_next_seq(h));
     return LIO_OK;
 }
 
@@ -1196,8 +1220,13 @@ static int icp_pass(lio_icp* h, bool fitness, bool apply_T, const float* T, doub
             if (rc) return rc;
         }
         IHIP(hipGetLastError());
-        IHIP(hipEventRecord(h->ev.done, h->st));
-        IHIP(hipEventSynchronize(h->ev.done));
+        if (pcl16 && !h->timing) {  // the pack's sequence number (it is the pass's last launch)
+            const int rc = pcl_wait(h, h->pcl_seq);
+            if (rc) return rc;
+        } else {
+            IHIP(hipEventRecord(h->ev.done, h->st));
+            IHIP(hipEventSynchronize(h->ev.done));
+        }
     } else {
         IHIP(hipStreamSynchronize(h->st));
     }
@@ -1469,7 +1498,10 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
         }
         if (!h->d_pcl16) IHIP(hipMalloc(&h->d_pcl16, 16 * sizeof(float)));
         if (!h->d_pclout) IHIP(hipMalloc(&h->d_pclout, 32 * sizeof(float)));
-        if (!h->h_pclout) IHIP(hipHostMalloc(&h->h_pclout, 32 * sizeof(float), hipHostMallocDefault));
+        if (!h->h_pclout) {
+            IHIP(hipHostMalloc(&h->h_pclout, 32 * sizeof(float), hipHostMallocMapped));
+            IHIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->h_pclout_dev), h->h_pclout, 0));
+        }
     }
     float fin[16], G[16];
     bool ident = true;

@@ -106,7 +106,7 @@ __global__ void __launch_bounds__(kPackThreads) pcl_pack_kernel(const float* __r
                                                       const uint32_t* __restrict__ st_means,
                                                       const uint32_t* __restrict__ st_sig,
                                                       const int* __restrict__ nev6, const uint32_t* __restrict__ flags,
-                                                      float* __restrict__ out) {
+                                                      float* __restrict__ out, uint32_t seq) {
     __shared__ float s_c[9][kPackWin + 1];  // +1: the nine lanes' rows in different banks
     const uint32_t n = *d_n;
     const int lane = threadIdx.x;
@@ -171,6 +171,17 @@ __global__ void __launch_bounds__(kPackThreads) pcl_pack_kernel(const float* __r
             for (int k = 0; k < 6; ++k) ev = max(ev, nev6[k]);
         out[18] = __int_as_float(ev);
         out[19] = __uint_as_float(flags ? *flags : 0u);  // compaction look-back timed out (never expected)
+    }
+    if (seq) {
+        // out host-mapped, the host polling out[23]: every word above stored and drained, then the sequence
+        // number behind a system-scope release
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (lane == 0) {
+            __threadfence_system();
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __hip_atomic_store(reinterpret_cast<uint32_t*>(out + 23), seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
     }
 }
 
@@ -390,7 +401,7 @@ void launch_pcl_x3_merge(PclBuf& p, int order, const double* recv, int64_t strid
 void launch_pcl_pack_shard(PclBuf& p, int order, float* out, hipStream_t st) {
     pcl_pack_kernel<<<1, kPackThreads, 0, st>>>(p.ghead, kPclTinyN, p.n_all, p.means.result,
                                                 order == 1 ? p.sig.result : p.means.result, p.Cbg, order, pcl_l1(order),
-                                                p.merged, p.merged + 2, p.means.floor_e + p.means.nch, p.merged + 4, out);
+                                                p.merged, p.merged + 2, p.means.floor_e + p.means.nch, p.merged + 4, out, 0u);
 }
 
 void launch_pcl_mean6(PclBuf& p, const float* sums6, hipStream_t st) {
@@ -477,7 +488,7 @@ void launch_pcl_sigma(PclBuf& p, int order, int pass, hipStream_t st, const floa
     }
 }
 
-void launch_pcl_pack(PclBuf& p, int order, float* out, hipStream_t st, const float* sums6) {
+void launch_pcl_pack(PclBuf& p, int order, float* out, hipStream_t st, const float* sums6, uint32_t seq) {
     const uint32_t* d_n = p.small + kPclN;
     const uint32_t* zero = p.small + kPclZero;  // the serial fallback's sums need no verification
     const bool serial = sums6 != nullptr;
@@ -485,7 +496,7 @@ void launch_pcl_pack(PclBuf& p, int order, float* out, hipStream_t st, const flo
     pcl_pack_kernel<<<1, kPackThreads, 0, st>>>(p.pairs, p.cap, d_n, sums6, order == 1 ? p.sig.result : sums6, p.Cb, order,
                                       pcl_l1(order), serial ? zero : p.means.status,
                                       order == 1 && !serial ? p.sig.status : zero,
-                                      serial ? nullptr : p.means.floor_e + p.means.nch, p.small + kPclTicket + 1, out);
+                                      serial ? nullptr : p.means.floor_e + p.means.nch, p.small + kPclTicket + 1, out, seq);
 }
 
 }  // namespace lio

@@ -18,7 +18,8 @@ constexpr int kPclZero = 16;   // two zero words (status of sums that need no ve
 constexpr int kPclTicket = 20; // compaction block ticket (reset by the last block); [21] look-back time-out flag
 constexpr int kPclOutWords = 24;  // pcl_pack output: 16 statistics, 2 status words, events (max over the means),
                                   // the compaction's time-out flag; sharded: [20] exchange flags (means | sigma << 8),
-                                  // [21] / [22] the largest per-rank event list of the means / sigma chains
+                                  // [21] / [22] the largest per-rank event list of the means / sigma chains; [23] the
+                                  // sequence number a polling host waits for (one rank, lio_icp_host.cpp pcl_wait)
 
 constexpr int kPclMaxKc = 1016;   // the largest GEMM depth block modelled (kc at a 48 KiB L1)
 constexpr int kPclTinyN = 16;     // n + 6 < 20: Eigen's lazy coefficient-based product (pcl_pack)
@@ -83,6 +84,7 @@ void launch_pcl_means(PclBuf& p, int pass, hipStream_t st);
 // fallback passes its own, which need no verification)
 void launch_pcl_sigma(PclBuf& p, int order, int pass, hipStream_t st, const float* sums6 = nullptr);
 // kPclOutWords floats -> out (device)
-void launch_pcl_pack(PclBuf& p, int order, float* out, hipStream_t st, const float* sums6 = nullptr);
+// seq != 0: out is host-mapped and out[23] = seq is stored last (system scope) for a host that polls it
+void launch_pcl_pack(PclBuf& p, int order, float* out, hipStream_t st, const float* sums6 = nullptr, uint32_t seq = 0);
 
 }  // namespace lio
