@@ -1481,6 +1481,7 @@ int lio_icp_align(lio_icp* h, const float* guess16, lio_icp_result* out, float* 
         if (lio::pcl_reserve(P, std::max<int64_t>(h->sh_n + (fsh ? lio::kPclMaxKc : 0), kIcpCapFloor), h->p.umeyama_float, h->st))
             return ifail(LIO_ERR_NOMEM, "lio_icp_align: fidelity buffers");
         P.means.dbg_noinc = P.sig.dbg_noinc = h->fid_flags & 1;
+        P.n_hint = fsh ? 0 : h->sh_n;  // one rank: the accepted pairs are a subset of the source
         for (lio::SeqSumBuf* b : {&P.means, &P.sig})
             b->evcap = h->fid_evcap > 0 ? std::min(h->fid_evcap, b->evcap_alloc) : b->evcap_alloc;
         P.mean6 = reinterpret_cast<float*>(P.small + lio::kPclMean6);

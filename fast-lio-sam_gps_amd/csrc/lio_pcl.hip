@@ -41,11 +41,13 @@ __global__ void pcl_mean6_kernel(const float* __restrict__ sums6, const uint32_t
 }
 
 // orders 2 / 3: block q of the depth = pairs [q kc, (q + 1) kc): lane e < 9 (r = e / 3, c = e % 3) adds
-// (tgt_r - dm_r) * (src_c - sm_c) in order from 0 (gebp's 1 x 1 remainder path: C0 += A0 * B0, no FMA)
-__global__ void __launch_bounds__(64) pcl_sigma_blocks_kernel(const float* __restrict__ pairs, int64_t cap,
-                                                              const uint32_t* __restrict__ d_n,
-                                                              const float* __restrict__ sums6, int l1,
-                                                              float* __restrict__ Cb) {
+// (tgt_r - dm_r) * (src_c - sm_c) in order from 0 (gebp's 1 x 1 remainder path: C0 += A0 * B0, no FMA).  256
+// threads stage the block (4 loads per column each; 64 threads: 14.4 us per launch at C4 pair B, 256: 12.0), nine add.
+constexpr int kSigThreads = 256;
+__global__ void __launch_bounds__(kSigThreads) pcl_sigma_blocks_kernel(const float* __restrict__ pairs, int64_t cap,
+                                                                       const uint32_t* __restrict__ d_n,
+                                                                       const float* __restrict__ sums6, int l1,
+                                                                       float* __restrict__ Cb) {
     __shared__ float s[6][kMaxKc];
     const uint32_t n = *d_n;
     if (n + 6 < 20) return;  // the lazy coefficient-based product: pcl_pack
@@ -60,20 +62,20 @@ __global__ void __launch_bounds__(64) pcl_sigma_blocks_kernel(const float* __res
         const int64_t k0 = q * kc;
         const int cnt = (int)((int64_t)n - k0 < kc ? (int64_t)n - k0 : kc);
         {  // coalesced per column; all six columns' loads in flight together (one round trip)
-            constexpr int T = (kMaxKc + 63) / 64;
+            constexpr int T = (kMaxKc + kSigThreads - 1) / kSigThreads;
             float v[6][T];
 #pragma unroll
             for (int d = 0; d < 6; ++d)
 #pragma unroll
                 for (int t = 0; t < T; ++t) {
-                    const int j = t * 64 + lane;
+                    const int j = t * kSigThreads + lane;
                     v[d][t] = j < cnt ? pairs[d * cap + k0 + j] : 0.f;
                 }
 #pragma unroll
             for (int d = 0; d < 6; ++d)
 #pragma unroll
                 for (int t = 0; t < T; ++t)
-                    if (t * 64 + lane < cnt) s[d][t * 64 + lane] = v[d][t];
+                    if (t * kSigThreads + lane < cnt) s[d][t * kSigThreads + lane] = v[d][t];
         }
         __syncthreads();
         if (lane < 9) {
@@ -483,8 +485,10 @@ void launch_pcl_sigma(PclBuf& p, int order, int pass, hipStream_t st, const floa
         pcl_mean6_kernel<<<1, 64, 0, st>>>(sums6, d_n, mean6);
         seqsum_launch(SeqSigma{p.pairs, mean6, p.cap}, 9, d_n, p.sig, pass, st);
     } else {
-        const int64_t grid = std::min<int64_t>(p.cap / 340 + 2, 4096);
-        pcl_sigma_blocks_kernel<<<(int)grid, 64, 0, st>>>(p.pairs, p.cap, d_n, sums6, pcl_l1(order), p.Cb);
+        // one workgroup per depth block of the largest n possible (n_hint: the source points, else the capacity)
+        const int64_t nmax = p.n_hint > 0 ? std::min(p.n_hint, p.cap) : p.cap;
+        const int64_t grid = std::min<int64_t>(nmax / 340 + 2, 4096);
+        pcl_sigma_blocks_kernel<<<(int)grid, kSigThreads, 0, st>>>(p.pairs, p.cap, d_n, sums6, pcl_l1(order), p.Cb);
     }
 }
 

@@ -35,6 +35,7 @@ struct PclBuf {
     float* Cb = nullptr;      // orders 2 / 3: per depth block, 9 sequential block sums
     uint32_t* small = nullptr;
     int64_t cap = 0;
+    int64_t n_hint = 0;       // > 0: no more accepted pairs than this in the next passes (the source's points)
     SeqSumBuf means;          // 6 chains
     SeqSumBuf sig;            // 9 chains (order 1)
     // sharded (world > 1, lio_icp_host.cpp): the whole chain's count (means.sh->n32), the first kPclTinyN pairs
