@@ -1,16 +1,16 @@
 // lio_seqsum.hip — sequential float summation chains evaluated in parallel, bit-exact (lio_seqsum.hpp).
 //
-// Per pass, for every chain (grid.y = chain):
+// Per pass, for every chain:
 //   seq_bsum     block double prefix (prediction) totals, sum |x| (bound on |s|)
 //   seq_scan1    per chain, sequential over blocks: double block offsets, the binade floor
-//   seq_count    per element: predicted binade, event flag, fixed-point increment -> block totals
-//   seq_scan2    per chain: exclusive block offsets of increments and events
-//   seq_events   the events in element order: position, increment prefix, x
-//   seq_walk     one block per chain replays the events (run sums exact in double) -> event results, sum
-//   seq_verify   every s_k rebuilt from the events; s_k == fl(s_{k-1} + x_k) checked for every k
-// A single rank runs seq_count .. seq_verify as ONE launch, seq_tail (the block offsets by a look-back, the walk
-// following the event blocks as they publish, the verification following the walk); the sharded path keeps them
-// apart (the event exchange sits between).
+//   count        per element: predicted binade, event flag, fixed-point increment -> block totals
+//   offsets      exclusive block offsets of increments and events
+//   events       the events in element order: position, increment prefix, x
+//   walk         one workgroup per chain replays the events (run sums exact in double) -> event results, sum
+//   verify       every s_k rebuilt from the events; s_k == fl(s_{k-1} + x_k) checked for every k
+// One rank: count .. verify are ONE launch, seq_tail (the offsets by a look-back, the walk following the event
+// blocks as they publish, the verification following the walk).  Sharded: seq_count, seq_scan2 and seq_events on
+// the window, the event exchange, seq_shard_merge, then walk and verify as one launch (seq_shard_walkverify).
 #include "lio_seqsum.hpp"
 
 #include <cmath>
@@ -277,7 +277,7 @@ __global__ void __launch_bounds__(256) seq_scan1(SeqSumBuf b, const uint32_t* d_
         __syncthreads();
         // block offsets by a block prefix (thread t: blocks t kPerT .. +kPerT-1 in order, then the threads' runs
         // in a fixed order): deterministic, and every kernel reads these stored offsets, so the predictions agree
-        // between seq_count / seq_events / seq_verify (predict() takes a block's first predecessor from
+        // between the count, events and verification roles (predict() takes a block's first predecessor from
         // boff[b-1] + bsum[b-1], the previous block's own last prediction)
         {
             double loc[kPerT], run = 0.0;
@@ -540,10 +540,10 @@ __global__ void __launch_bounds__(kSeqThreads) seq_events(Src src, SeqSumBuf b, 
 //     operands (53 >= 2 * 24 + 2: double rounding is innocuous for a sum), and when the increments are right
 //     s + R is the float s_{event-1} itself;
 //   * other groups (a run spanning more than 24 bits of the chain's fixed-point unit) take the general form,
-//     fl32(fl32(fl64(s + R)) + x).  seq_verify checks every element either way.
+//     fl32(fl32(fl64(s + R)) + x).  The verification checks every element either way.
 constexpr int kWalkThreads = 256;
-constexpr int kWalkChunk = 1024;  // events per LDS chunk, separate launches (x 2 buffers x 20 bytes)
-constexpr int kTailChunk = 512;   // the fused tail's: 20 KB of LDS, so its other roles keep their occupancy
+constexpr int kTailChunk = 512;  // events per LDS chunk (x 2 buffers x 20 bytes: 20 KB, so the other roles of the
+                                 // launch keep their occupancy)
 constexpr int kWalkU = 8;
 template <int C>
 struct alignas(16) WalkChunk {
@@ -667,19 +667,23 @@ __device__ __forceinline__ float walk_chunk(WalkChunk<C>& B, int m, float s) {
     return s;
 }
 
-// the walker of chain c, separate launches: every event listed before it starts
-template <class Src>
-__global__ void __launch_bounds__(kWalkThreads) seq_walk(Src src, SeqSumBuf b, const uint32_t* d_n) {
-    constexpr int C = kWalkChunk;
-    __shared__ WalkChunk<C> wb[2];
-    const int c = blockIdx.x;
+// F: the walk's progress word of chain c, epoch << 32 | events whose results are stored (sc1)
+__device__ __forceinline__ void walk_publish(const SeqSumBuf& b, int c, uint32_t epoch, uint32_t done) {
+    st64<true>(b.wprog + c, ((uint64_t)epoch << 32) | done);
+}
+
+// the walker of chain c when every event is listed before it starts (sharded, after seq_shard_merge).  F: the
+// results stored sc1 and published chunk by chunk for the verification blocks of the same launch
+// (seq_shard_walkverify)
+template <class Src, int C, bool F>
+__device__ __forceinline__ void walk_known(const Src& src, const SeqSumBuf& b, int c, int64_t n, uint32_t epoch,
+                                           WalkChunk<C>* wb) {
     const int t = threadIdx.x, w = t >> 6;
-    const int64_t n = b.sh ? b.sh->n_global : *d_n;  // sharded: every rank walks the whole chain's events
     if (n <= 0) {
         if (t == 0) b.result[c] = 0.f;
         return;
     }
-    if ((b.status[1] >> c) & 1u) return;  // event overflow: the caller falls back
+    if ((b.status[1] >> c) & 1u) return;  // event overflow: the caller falls back (verification blocks skip too)
     const int nev = b.floor_e[b.nch + c];
     const double unit = ldexp(1.0, b.floor_e[c] - 23);
     const uint64_t* EP = b.ev_P + (size_t)c * b.evs;
@@ -693,13 +697,15 @@ __global__ void __launch_bounds__(kWalkThreads) seq_walk(Src src, SeqSumBuf b, c
         if (w == 0) {
             if (t == 0) s = walk_chunk(wb[k & 1], min(C, nev - k * C), s);
         } else {
+            if (F && t == 64 && k > 1) walk_publish(b, c, epoch, (uint32_t)((k - 1) * C));  // chunks < k-1: stored
             if (k + 1 < nchunk)
                 walk_prepare<C, false>(wb[(k + 1) & 1], k + 1, min(C, nev - (k + 1) * C), unit, EP, EX, t - 64,
                                        kWalkThreads - 64);
             if (k > 0) {  // chunk k-1's results (its buffer's f: the preparation above writes only R, Rf, x)
                 const WalkChunk<C>& B = wb[(k - 1) & 1];
                 const int e0 = (k - 1) * C;
-                for (int j = t - 64; j < C; j += kWalkThreads - 64) ES[e0 + j] = B.f[j];
+                for (int j = t - 64; j < C; j += kWalkThreads - 64) st32<F>(ES + e0 + j, __float_as_uint(B.f[j]));
+                if (F) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             }
         }
         __syncthreads();
@@ -707,7 +713,12 @@ __global__ void __launch_bounds__(kWalkThreads) seq_walk(Src src, SeqSumBuf b, c
     if (nchunk > 0) {
         const WalkChunk<C>& B = wb[(nchunk - 1) & 1];
         const int e0 = (nchunk - 1) * C;
-        for (int j = t; j < nev - e0; j += kWalkThreads) ES[e0 + j] = B.f[j];
+        for (int j = t; j < nev - e0; j += kWalkThreads) st32<F>(ES + e0 + j, __float_as_uint(B.f[j]));
+    }
+    if constexpr (F) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (t == 0) walk_publish(b, c, epoch, (uint32_t)nev);
     }
     if (t == 0) {
         const uint64_t Plast = nev > 0 ? EP[nev - 1] : 0;
@@ -788,21 +799,6 @@ __device__ __forceinline__ void verify_check(const Src& src, const SeqSumBuf& b,
     if (bad) s_bad = 1;
     __syncthreads();
     if (threadIdx.x == 0 && s_bad) atomicOr(&b.status[0], 1u << c);
-}
-
-template <class Src>
-__global__ void __launch_bounds__(kSeqThreads) seq_verify(Src src, SeqSumBuf b, const uint32_t* d_n, int pass) {
-    const int c = blockIdx.y, blk = blockIdx.x;
-    const int64_t n = *d_n;
-    if ((int64_t)blk * kSeqBlock >= n) return;
-    if ((b.status[1] >> c) & 1u) return;
-    ElemInfo in;
-    bool ev[kSeqPer];
-    uint64_t Pex[kSeqPer];
-    int Ein[kSeqPer];
-    block_scan_elems(src, b, c, blk, n, pass, in, ev, Pex, Ein);
-    verify_check<Src, false>(src, b, c, blk, n, pass, in, ev, Pex, Ein, b.bEoff[(size_t)c * b.nblk + blk],
-                             b.bPoff[(size_t)c * b.nblk + blk]);
 }
 
 // ---------------------------------------------------------------- the fused tail (single rank)
@@ -907,10 +903,6 @@ __device__ __forceinline__ bool tail_wait(const SeqSumBuf& b, int c, int nb, int
         }
     }
     return true;
-}
-
-__device__ __forceinline__ void walk_publish(const SeqSumBuf& b, int c, uint32_t epoch, uint32_t done) {
-    st64<true>(b.wprog + c, ((uint64_t)epoch << 32) | done);
 }
 
 // the walker of chain c
@@ -1071,6 +1063,55 @@ __global__ void __launch_bounds__(kSeqThreads) seq_tail(Src src, SeqSumBuf b, co
         tail_verify<Src>(src, b, c, blk, n, pass, epoch);
     else
         tail_events<Src>(src, b, c, blk, n, pass, epoch, nb);
+}
+
+// sharded, after seq_shard_merge: the walk over every rank's events and this window's verification in ONE launch.
+// Workgroups [0, nch) walk (every event already listed), the rest verify the window's blocks, element-major, each
+// after its own classification waiting for the walk to pass its last event (the walkers' progress words; the same
+// hand-off as seq_tail's, and its time-out: a failed verification, so a re-pass)
+template <class Src>
+__global__ void __launch_bounds__(kSeqThreads) seq_shard_walkverify(Src src, SeqSumBuf b, const uint32_t* d_n, int pass,
+                                                                    int nch, uint32_t epoch) {
+    static_assert(kSeqThreads == kWalkThreads, "one block size for every role");
+    __shared__ WalkChunk<kTailChunk> wb[2];
+    __shared__ uint32_t s_skip;
+    const uint32_t r = blockIdx.x;
+    if (r < (uint32_t)nch) {
+        walk_known<Src, kTailChunk, true>(src, b, (int)r, b.sh->n_global, epoch, wb);
+        return;
+    }
+    const uint32_t i = r - (uint32_t)nch;
+    const int c = (int)(i % (uint32_t)nch), blk = (int)(i / (uint32_t)nch);
+    const int64_t n = *d_n;
+    if ((int64_t)blk * kSeqBlock >= n) return;
+    if ((b.status[1] >> c) & 1u) return;
+    ElemInfo in;
+    bool ev[kSeqPer];
+    uint64_t Pex[kSeqPer];
+    int Ein[kSeqPer];
+    block_scan_elems(src, b, c, blk, n, pass, in, ev, Pex, Ein);
+    const size_t bi = (size_t)c * b.nblk + blk;
+    if (threadIdx.x == 0) {
+        const uint32_t need = (uint32_t)(b.bEoff[bi] + b.bev[bi]);  // global (merged) offsets: the block's last event
+        const uint64_t t0 = wall_clock64();
+        uint32_t skip = 0;
+        for (;;) {
+            const uint64_t wv = ld64<true>(b.wprog + c);
+            if ((uint32_t)(wv >> 32) == epoch && (uint32_t)wv >= need) break;
+            if (wall_clock64() - t0 > kSpinTicks) {
+                skip = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        s_skip = skip;
+    }
+    __syncthreads();
+    if (s_skip) {
+        if (threadIdx.x == 0) atomicOr(&b.status[0], 1u << c);  // time-out: a re-pass
+        return;
+    }
+    verify_check<Src, true>(src, b, c, blk, n, pass, in, ev, Pex, Ein, b.bEoff[bi], b.bPoff[bi]);
 }
 
 // ---------------------------------------------------------------- sharded chains (lio_seqsum.hpp)
@@ -1395,8 +1436,12 @@ void seqsum_shard_tail(const Src& src, int nch, const uint32_t* d_n, SeqSumBuf& 
     const dim3 g(b.nblk, nch);
     seq_shard_merge<<<nch, 256, 0, st>>>(b, d_n, msg_recv, msg_stride, rank, world, slot, hd.nhead, hd.ext,
                                          hd.ext_stride, hd.ghead, hd.nghead);
-    seq_walk<Src><<<nch, kWalkThreads, 0, st>>>(src, b, d_n);
-    seq_verify<Src><<<g, kSeqThreads, 0, st>>>(src, b, d_n, pass);
+    (void)g;
+    do {
+        ++b.tail_epoch;
+    } while ((b.tail_epoch & 0x3fffffffu) == 0);
+    seq_shard_walkverify<Src><<<(uint32_t)nch * (1u + (uint32_t)b.nblk), kSeqThreads, 0, st>>>(src, b, d_n, pass, nch,
+                                                                                                 b.tail_epoch);
 }
 
 template <class Src>
