@@ -247,7 +247,12 @@ constexpr int kScanWin = 2048;
 // walk, bounded per block by the block's largest |s| (|offset| + sum |x|): V += kSeqBlock (ulp / 2)^2,
 // delta = kDriftSigmas sqrt(V) through the block's end (non-decreasing, so conservative for every element of
 // the block).  Only a performance model: a drift past it fails verification and the chain takes a second pass.
-constexpr double kDriftSigmas = 2.0;
+// 3 sigmas (round 6; 2 before): C4 pair B's re-passes 11 -> 0 in 110 passes for ~1 % more events, 2.35 -> 2.25 ms per
+// alignment, pair A +7 us; 4 sigmas: more events, no fewer re-passes (profiles/r06_drift_sigmas_ab.txt)
+#ifndef LIO_DRIFT_SIGMAS
+#define LIO_DRIFT_SIGMAS 3.0
+#endif
+constexpr double kDriftSigmas = LIO_DRIFT_SIGMAS;
 
 // half an ulp of a float of magnitude v >= 0 (2^(ilogb(v) - 24); 0 for 0), from the exponent bits
 __device__ __forceinline__ double half_ulp_f32(double v) {
