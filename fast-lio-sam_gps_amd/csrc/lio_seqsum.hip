@@ -26,7 +26,13 @@ constexpr int kSpecial = -1000;  // zero, subnormal or non-finite: no binade
 // prediction slack near binade edges (mantissa bits): pass 1 predicts from a double prefix sum that drifts
 // from the float chain by its accumulated rounding (measured: a few units on C4 chains of |s| ~ 1e4-1e5,
 // ~2^-12 relative), later passes from a reconstruction within a few ulps of it
-constexpr int kPredSlack1 = 13;  // 2^-10 relative
+// 10 bits: 2^-13 relative (round 6, with the 3-sigma drift band below; 13 before): C4 pair B's longest event list
+// 4 634 -> 4 100, 2.24 -> 2.20 ms per alignment, still no re-pass; 7 bits: re-passes return
+// (profiles/r06_drift_sigmas_ab.txt)
+#ifndef LIO_PRED_SLACK1
+#define LIO_PRED_SLACK1 10
+#endif
+constexpr int kPredSlack1 = LIO_PRED_SLACK1;
 constexpr int kPredSlack2 = 4;   // 16 ulps
 
 __device__ __forceinline__ int binade_f(float f) {
