@@ -553,8 +553,12 @@ __global__ void __launch_bounds__(kSeqThreads) seq_events(Src src, SeqSumBuf b, 
 //   * other groups (a run spanning more than 24 bits of the chain's fixed-point unit) take the general form,
 //     fl32(fl32(fl64(s + R)) + x).  The verification checks every element either way.
 constexpr int kWalkThreads = 256;
-constexpr int kTailChunk = 512;  // events per LDS chunk (x 2 buffers x 20 bytes: 20 KB, so the other roles of the
-                                 // launch keep their occupancy)
+// events per LDS chunk (x 2 buffers x 20 bytes: 20 KB, so the other roles of the launch keep their occupancy); C4 pair
+// B per alignment: 256 2.20-2.22 ms, 512 2.18-2.21, 1024 2.29-2.31 (profiles/r06_seq_tail_ab.txt)
+#ifndef LIO_TAIL_CHUNK
+#define LIO_TAIL_CHUNK 512
+#endif
+constexpr int kTailChunk = LIO_TAIL_CHUNK;
 constexpr int kWalkU = 8;
 template <int C>
 struct alignas(16) WalkChunk {
